@@ -1,0 +1,196 @@
+// C ABI entry points (include/zkm_hip.h): context, PCS commit, kernel-level helpers.
+// Shard prover entry points (setup/commit/open) live in prover.cpp.
+#include <cstring>
+#include <string>
+
+#include "../../include/zkm_hip.h"
+#include "internal.hpp"
+
+namespace zkm {
+
+thread_local std::string g_last_error;
+
+hipStream_t Ctx::acquire_stream() {
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!free_streams.empty()) {
+            hipStream_t s = free_streams.back();
+            free_streams.pop_back();
+            return s;
+        }
+    }
+    HIP_CHECK(hipSetDevice(device));
+    hipStream_t s;
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+}
+void Ctx::release_stream(hipStream_t s) {
+    std::lock_guard<std::mutex> g(mu);
+    free_streams.push_back(s);
+}
+
+int guard_status(const std::exception &e) {
+    g_last_error = e.what();
+    if (dynamic_cast<const ArgError *>(&e)) return ZKM_ERR_ARG;
+    return ZKM_ERR_HIP;
+}
+
+// host row-major matrix -> device column-major Montgomery
+DBuf upload_matrix(const zkm_matrix_t &m, hipStream_t s) {
+    ARG_CHECK(m.data || m.height * m.width == 0, "matrix data is NULL");
+    const uint64_t n = m.height * m.width;
+    DBuf col(n ? n : 1, s);
+    if (n) {
+        DBuf raw(n, s);
+        HIP_CHECK(hipMemcpyAsync(raw.p, m.data, n * 4, hipMemcpyHostToDevice, s));
+        launch_to_col_major(raw.p, m.height, m.width, m.repr == ZKM_REPR_MONTGOMERY, col.p, s);
+        HIP_CHECK(hipStreamSynchronize(s));  // raw freed on scope exit (stream-ordered anyway)
+    }
+    return col;
+}
+
+}  // namespace zkm
+
+using namespace zkm;
+
+#define GUARD_BEGIN try {
+#define GUARD_END                                  \
+    }                                              \
+    catch (const std::exception &e) {              \
+        return guard_status(e);                    \
+    }
+
+extern "C" {
+
+const char *zkm_last_error(void) { return g_last_error.c_str(); }
+
+int zkm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int zkm_init(int device, zkm_ctx **out) {
+    GUARD_BEGIN
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        g_last_error = "no HIP device " + std::to_string(device);
+        return ZKM_ERR_NO_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0) {
+        g_last_error = std::string("device is ") + prop.gcnArchName + ", this library is built for gfx950";
+        return ZKM_ERR_NO_DEVICE;
+    }
+    HIP_CHECK(hipSetDevice(device));
+    auto *c = new Ctx();
+    c->device = device;
+    build_twiddles(*c, 24);  // transforms up to 2^24 (two-adicity)
+    *out = reinterpret_cast<zkm_ctx *>(c);
+    return ZKM_OK;
+    GUARD_END
+}
+
+void zkm_destroy(zkm_ctx *ctx) {
+    if (!ctx) return;
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    for (auto s : c->free_streams) (void)hipStreamDestroy(s);
+    (void)hipFree(c->tw_fwd);
+    (void)hipFree(c->tw_inv);
+    delete c;
+}
+
+void zkm_free_bytes(uint8_t *p) { free(p); }
+
+int zkm_coset_lde(zkm_ctx *ctx, const zkm_matrix_t *m, uint32_t shift, uint32_t *out) {
+    GUARD_BEGIN
+    ARG_CHECK(ctx && m && out, "null argument");
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    HIP_CHECK(hipSetDevice(c->device));
+    StreamLease L(c);
+    DBuf col = upload_matrix(*m, L.s);
+    DMat src{col.p, m->height, m->width};
+    DBuf ld(2 * m->height * m->width, L.s);
+    DMat dst{ld.p, 2 * m->height, m->width};
+    lde_batch(*c, src, kb::to_mont(shift), dst, L.s);
+    DBuf rm(2 * m->height * m->width, L.s);
+    launch_from_col_major(ld.p, 2 * m->height, m->width, rm.p, L.s);
+    HIP_CHECK(hipMemcpyAsync(out, rm.p, 2 * m->height * m->width * 4, hipMemcpyDeviceToHost, L.s));
+    HIP_CHECK(hipStreamSynchronize(L.s));
+    return ZKM_OK;
+    GUARD_END
+}
+
+int zkm_poseidon2_permute(zkm_ctx *ctx, uint32_t *states, uint64_t n) {
+    GUARD_BEGIN
+    ARG_CHECK(ctx && (states || !n), "null argument");
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    HIP_CHECK(hipSetDevice(c->device));
+    StreamLease L(c);
+    std::vector<uint32_t> h(states, states + n * 16);
+    for (auto &x : h) x = kb::to_mont(x);
+    DBuf d(n * 16, L.s);
+    HIP_CHECK(hipMemcpyAsync(d.p, h.data(), n * 64, hipMemcpyHostToDevice, L.s));
+    launch_poseidon2_batch(d.p, n, L.s);
+    HIP_CHECK(hipMemcpyAsync(h.data(), d.p, n * 64, hipMemcpyDeviceToHost, L.s));
+    HIP_CHECK(hipStreamSynchronize(L.s));
+    for (uint64_t i = 0; i < n * 16; i++) states[i] = kb::from_mont(h[i]);
+    return ZKM_OK;
+    GUARD_END
+}
+
+int zkm_pcs_commit_root(zkm_ctx *ctx, const zkm_matrix_t *mats, uint32_t n, uint32_t root_out[8]) {
+    GUARD_BEGIN
+    ARG_CHECK(ctx && mats && n && root_out, "null argument");
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    HIP_CHECK(hipSetDevice(c->device));
+    StreamLease L(c);
+    DTree t;
+    for (uint32_t i = 0; i < n; i++) {
+        DBuf col = upload_matrix(mats[i], L.s);
+        DMat src{col.p, mats[i].height, mats[i].width};
+        t.owned.emplace_back(2 * mats[i].height * (mats[i].width ? mats[i].width : 1), L.s);
+        DMat dst{t.owned.back().p, 2 * mats[i].height, mats[i].width};
+        lde_batch(*c, src, kb::to_mont(kb::GENERATOR), dst, L.s);
+        t.mats.push_back(dst);
+    }
+    tree_build(t, L.s);
+    for (int k = 0; k < 8; k++) root_out[k] = kb::from_mont(t.root[k]);
+    return ZKM_OK;
+    GUARD_END
+}
+
+int zkm_bench_lde(zkm_ctx *ctx, uint64_t h, uint64_t w, int iters, double *ms_out) {
+    GUARD_BEGIN
+    ARG_CHECK(ctx && ms_out && iters > 0, "null argument");
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    HIP_CHECK(hipSetDevice(c->device));
+    StreamLease L(c);
+    DBuf src(h * w, L.s), dst(2 * h * w, L.s);
+    // deterministic fill: Montgomery of index hash (values in [0,p))
+    std::vector<uint32_t> host(h * w);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (auto &v : host) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = (uint32_t)(x % kb::P); }
+    HIP_CHECK(hipMemcpyAsync(src.p, host.data(), h * w * 4, hipMemcpyHostToDevice, L.s));
+    DMat s{src.p, h, w}, d{dst.p, 2 * h, w};
+    lde_batch(*c, s, kb::to_mont(3), d, L.s);  // warm-up
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    HIP_CHECK(hipEventRecord(e0, L.s));
+    for (int i = 0; i < iters; i++) lde_batch(*c, s, kb::to_mont(3), d, L.s);
+    HIP_CHECK(hipEventRecord(e1, L.s));
+    HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    *ms_out = ms / iters;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return ZKM_OK;
+    GUARD_END
+}
+
+}  // extern "C"

@@ -1,0 +1,116 @@
+// Internal declarations of the MI355X shard prover (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kb31.cuh"
+
+namespace zkm {
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct ArgError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define HIP_CHECK(expr)                                                                       \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            throw ::zkm::HipError(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" + \
+                                  __FILE__ + ":" + std::to_string(__LINE__));                 \
+    } while (0)
+#define ARG_CHECK(cond, msg)                        \
+    do {                                            \
+        if (!(cond)) throw ::zkm::ArgError(msg);    \
+    } while (0)
+
+inline int ilog2(uint64_t n) {
+    int l = 0;
+    while ((1ull << l) < n) l++;
+    return l;
+}
+
+// Stream-ordered device buffer.
+struct DBuf {
+    uint32_t *p = nullptr;
+    size_t words = 0;
+    hipStream_t s = nullptr;
+    DBuf() = default;
+    DBuf(size_t n, hipStream_t st) : words(n), s(st) {
+        if (n) HIP_CHECK(hipMallocAsync((void **)&p, n * sizeof(uint32_t), st));
+    }
+    DBuf(const DBuf &) = delete;
+    DBuf &operator=(const DBuf &) = delete;
+    DBuf(DBuf &&o) noexcept { *this = std::move(o); }
+    DBuf &operator=(DBuf &&o) noexcept {
+        reset();
+        p = o.p; words = o.words; s = o.s;
+        o.p = nullptr; o.words = 0;
+        return *this;
+    }
+    void reset() {
+        if (p) (void)hipFreeAsync(p, s);
+        p = nullptr;
+        words = 0;
+    }
+    ~DBuf() { reset(); }
+};
+
+// Column-major device matrix (Montgomery values), column stride = height.
+struct DMat {
+    uint32_t *d = nullptr;
+    uint64_t height = 0, width = 0;
+};
+
+// Device Merkle tree over several column-major matrices (MerkleTreeMmcs semantics,
+// pinned by crates/recursion/circuit/src/fri.rs:363-405).
+struct DTree {
+    std::vector<DMat> mats;        // commit order
+    std::vector<DBuf> owned;       // storage of mats (if owned)
+    int log_max = 0;
+    std::vector<DBuf> layers;      // layers[i]: (max_h >> i) digests x 8 words, digest-major
+    uint32_t root[8];              // Montgomery
+};
+
+struct Ctx {
+    int device = 0;
+    int tw_log = 0;                 // twiddle tables cover transforms up to 2^tw_log
+    uint32_t *tw_fwd = nullptr;     // tw[h + j] = w_{2h}^j  (Montgomery), size 2^tw_log
+    uint32_t *tw_inv = nullptr;
+    std::mutex mu;
+    std::vector<hipStream_t> free_streams;
+    hipStream_t acquire_stream();
+    void release_stream(hipStream_t s);
+};
+
+struct StreamLease {
+    Ctx *c;
+    hipStream_t s;
+    explicit StreamLease(Ctx *ctx) : c(ctx), s(ctx->acquire_stream()) {}
+    ~StreamLease() { c->release_stream(s); }
+};
+
+// ---------------------------------------------------------------- kernels (launchers)
+// host row-major (canonical or Montgomery) -> device column-major Montgomery
+void launch_to_col_major(const uint32_t *d_rowmajor, uint64_t h, uint64_t w, bool montgomery_in,
+                         uint32_t *d_col, hipStream_t s);
+void launch_from_col_major(const uint32_t *d_col, uint64_t h, uint64_t w, uint32_t *d_rowmajor_canon,
+                           hipStream_t s);
+void build_twiddles(Ctx &c, int log_max);
+// Bit-reversed coset LDE of `src` (h x w col-major) into `dst` (2h x w col-major):
+// dst column c row i = p_c(shift * w_{2h}^{rev(i)}), p_c interpolating src column c on H_h.
+void lde_batch(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst, hipStream_t s);
+
+// Merkle
+void tree_build(DTree &t, hipStream_t s);
+void launch_poseidon2_batch(uint32_t *d_states, uint64_t n, hipStream_t s);
+
+}  // namespace zkm

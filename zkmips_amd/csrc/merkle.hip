@@ -1,0 +1,134 @@
+// Poseidon2 Merkle commitment (MerkleTreeMmcs over PaddingFreeSponge<P,16,8,8> leaves and
+// TruncatedPermutation<P,2,8,16> nodes, crates/stark/src/kb31_poseidon2.rs:173-177) on gfx950.
+//
+// Tree semantics pinned by crates/recursion/circuit/src/fri.rs:363-405:
+//   leaf i   = sponge(row i of every tallest matrix, concatenated in commit order)
+//   node     = compress(left, right), then, if matrices of that height exist,
+//              compress(node, sponge(their rows)).
+// One thread hashes one row: matrices are column-major, so a wavefront reads 64 consecutive
+// rows of a column (256 B) per absorbed element.  Digests are stored digest-major (32 B each).
+#include <algorithm>
+#include <numeric>
+
+#include "internal.hpp"
+#include "p2.cuh"
+
+namespace zkm {
+
+static constexpr int NT = 256;
+
+// Absorb `ncols` columns (device pointer table) of row i into the sponge; overwrite mode.
+__device__ __forceinline__ void sponge_row(const uint64_t *__restrict__ cols, int ncols, uint64_t i, uint32_t s[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) s[k] = 0;
+    for (int base = 0; base < ncols; base += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (base + k < ncols) s[k] = ((const uint32_t *)cols[base + k])[i];
+        p2::permute(s);
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_hash_leaves(const uint64_t *__restrict__ cols, int ncols, uint64_t nrows,
+                                                    uint32_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= nrows) return;
+    uint32_t s[16];
+    sponge_row(cols, ncols, i, s);
+    uint4 *o = (uint4 *)(out + i * 8);
+    o[0] = make_uint4(s[0], s[1], s[2], s[3]);
+    o[1] = make_uint4(s[4], s[5], s[6], s[7]);
+}
+
+__global__ __launch_bounds__(NT) void k_compress_level(const uint32_t *__restrict__ prev, uint32_t *__restrict__ out,
+                                                       uint64_t h, const uint64_t *__restrict__ inj, int ninj) {
+    uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= h) return;
+    uint32_t s[16];
+    const uint4 *p = (const uint4 *)(prev + i * 16);
+    uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+    s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+    s[8] = c.x; s[9] = c.y; s[10] = c.z; s[11] = c.w; s[12] = d.x; s[13] = d.y; s[14] = d.z; s[15] = d.w;
+    p2::permute(s);
+    if (ninj) {
+        uint32_t r[16];
+        sponge_row(inj, ninj, i, r);
+#pragma unroll
+        for (int k = 0; k < 8; k++) s[8 + k] = r[k];
+        p2::permute(s);
+    }
+    uint4 *o = (uint4 *)(out + i * 8);
+    o[0] = make_uint4(s[0], s[1], s[2], s[3]);
+    o[1] = make_uint4(s[4], s[5], s[6], s[7]);
+}
+
+__global__ void k_p2_batch(uint32_t *st, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    uint32_t s[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) s[k] = st[i * 16 + k];
+    p2::permute(s);
+#pragma unroll
+    for (int k = 0; k < 16; k++) st[i * 16 + k] = s[k];
+}
+
+void launch_poseidon2_batch(uint32_t *d, uint64_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_p2_batch, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, d, n);
+    HIP_CHECK(hipGetLastError());
+}
+
+static DBuf upload_cols(const std::vector<const DMat *> &group, std::vector<uint64_t> &host, hipStream_t s) {
+    host.clear();
+    for (const DMat *m : group)
+        for (uint64_t c = 0; c < m->width; c++) host.push_back((uint64_t)(uintptr_t)(m->d + c * m->height));
+    DBuf d(host.size() * 2 + 2, s);
+    if (!host.empty()) HIP_CHECK(hipMemcpyAsync(d.p, host.data(), host.size() * 8, hipMemcpyHostToDevice, s));
+    return d;
+}
+
+void tree_build(DTree &t, hipStream_t s) {
+    const int n = (int)t.mats.size();
+    ARG_CHECK(n > 0, "empty MMCS batch");
+    std::vector<int> order(n);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return t.mats[a].height > t.mats[b].height; });
+    const uint64_t maxh = t.mats[order[0]].height;
+    ARG_CHECK((maxh & (maxh - 1)) == 0, "matrix heights must be powers of two");
+    t.log_max = ilog2(maxh);
+    t.layers.clear();
+    t.layers.resize(t.log_max + 1);
+    std::vector<std::vector<uint64_t>> keep(t.log_max + 2);
+    std::vector<DBuf> colbufs;
+    size_t pos = 0;
+    std::vector<const DMat *> grp;
+    while (pos < order.size() && t.mats[order[pos]].height == maxh) grp.push_back(&t.mats[order[pos++]]);
+    colbufs.push_back(upload_cols(grp, keep[0], s));
+    int ncols = (int)keep[0].size();
+    t.layers[0] = DBuf(maxh * 8, s);
+    hipLaunchKernelGGL(k_hash_leaves, dim3((unsigned)((maxh + NT - 1) / NT)), dim3(NT), 0, s,
+                       (const uint64_t *)colbufs.back().p, ncols, maxh, t.layers[0].p);
+    HIP_CHECK(hipGetLastError());
+    uint64_t h = maxh;
+    for (int L = 1; L <= t.log_max; L++) {
+        h >>= 1;
+        grp.clear();
+        while (pos < order.size() && t.mats[order[pos]].height == h) grp.push_back(&t.mats[order[pos++]]);
+        ARG_CHECK(grp.empty() || true, "");
+        colbufs.push_back(upload_cols(grp, keep[L], s));
+        int ninj = grp.empty() ? 0 : (int)keep[L].size();
+        // a group of zero-width matrices still injects hash(empty) = 0-digest: keep semantics
+        bool inject = !grp.empty();
+        t.layers[L] = DBuf(h * 8, s);
+        hipLaunchKernelGGL(k_compress_level, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
+                           (const uint32_t *)t.layers[L - 1].p, t.layers[L].p, h,
+                           (const uint64_t *)colbufs.back().p, inject ? (ninj ? ninj : -1) : 0);
+        HIP_CHECK(hipGetLastError());
+    }
+    ARG_CHECK(pos == order.size(), "matrix heights must be distinct powers of two <= max");
+    HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max].p, 32, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace zkm
