@@ -97,7 +97,8 @@ void zkm_destroy(zkm_ctx *ctx) {
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
-    for (auto s : c->free_streams) (void)hipStreamDestroy(s);
+    // Streams are intentionally not destroyed: proving keys and shard data may outlive the
+    // context handle, and their stream-ordered buffers are released on the stream that made them.
     (void)hipFree(c->tw_fwd);
     (void)hipFree(c->tw_inv);
     delete c;

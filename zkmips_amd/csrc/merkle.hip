@@ -11,6 +11,7 @@
 #include <numeric>
 
 #include "internal.hpp"
+#include "open_kernels.hpp"
 #include "p2.cuh"
 
 namespace zkm {
@@ -115,7 +116,6 @@ void tree_build(DTree &t, hipStream_t s) {
         h >>= 1;
         grp.clear();
         while (pos < order.size() && t.mats[order[pos]].height == h) grp.push_back(&t.mats[order[pos++]]);
-        ARG_CHECK(grp.empty() || true, "");
         colbufs.push_back(upload_cols(grp, keep[L], s));
         int ninj = grp.empty() ? 0 : (int)keep[L].size();
         // a group of zero-width matrices still injects hash(empty) = 0-digest: keep semantics
@@ -127,6 +127,24 @@ void tree_build(DTree &t, hipStream_t s) {
         HIP_CHECK(hipGetLastError());
     }
     ARG_CHECK(pos == order.size(), "matrix heights must be distinct powers of two <= max");
+    HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max].p, 32, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s) {
+    ARG_CHECK(nleaves && (nleaves & (nleaves - 1)) == 0, "leaf count must be a power of two");
+    t.log_max = ilog2(nleaves);
+    t.layers.clear();
+    t.layers.resize(t.log_max + 1);
+    t.layers[0] = std::move(leaves);
+    uint64_t h = nleaves;
+    for (int L = 1; L <= t.log_max; L++) {
+        h >>= 1;
+        t.layers[L] = DBuf(h * 8, s);
+        hipLaunchKernelGGL(k_compress_level, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
+                           (const uint32_t *)t.layers[L - 1].p, t.layers[L].p, h, (const uint64_t *)nullptr, 0);
+        HIP_CHECK(hipGetLastError());
+    }
     HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max].p, 32, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
 }

@@ -150,9 +150,17 @@ struct ColMap {
 };
 
 // Strided pass: rows r at stride S within outer blocks of R*S; 64-column tiles.
+struct Twist {
+    const uint32_t *lo0, *hi0, *lo1, *hi1;
+    __device__ __forceinline__ uint32_t f(int e, uint32_t k) const {
+        return e ? mul(hi1[k >> 12], lo1[k & 4095]) : mul(hi0[k >> 12], lo0[k & 4095]);
+    }
+};
+
 template <int LOGR, bool DIT>
 __global__ __launch_bounds__(NT) void k_ntt_strided(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
-                                                    int L, int logS, const uint32_t *__restrict__ tw, int bitrev_out) {
+                                                    int L, int logS, const uint32_t *__restrict__ tw, int bitrev_out,
+                                                    Twist tws, int twist_out, uint64_t dst_half) {
     constexpr int R = 1 << LOGR;
     constexpr int T = TS;
     __shared__ uint32_t x[R * T];
@@ -170,7 +178,15 @@ __global__ __launch_bounds__(NT) void k_ntt_strided(const uint32_t *src, uint32_
     }
     __syncthreads();
     tile_stages<LOGR, T, DIT>(x, tw, S, c0);
-    if (!bitrev_out) {
+    if (twist_out) {
+        // natural coefficient index n -> two twisted outputs (E0, E1 halves)
+        for (int i = threadIdx.x; i < R * T; i += NT) {
+            const int r = i / T, t = i & (T - 1);
+            const uint64_t n = base + (uint64_t)r * S + c0 + t;
+            dp[n] = mul(x[i], tws.f(0, (uint32_t)n));
+            dp[dst_half + n] = mul(x[i], tws.f(1, (uint32_t)n));
+        }
+    } else if (!bitrev_out) {
         for (int i = threadIdx.x; i < R * T; i += NT) {
             const int r = i / T, t = i & (T - 1);
             dp[base + (uint64_t)r * S + c0 + t] = x[i];
@@ -191,9 +207,6 @@ __global__ __launch_bounds__(NT) void k_ntt_strided(const uint32_t *src, uint32_
 //   multiplied by f_e(k) = hi_e[k >> 12] * lo_e[k & 4095] (k = rev_L(n)) and transformed into
 //   dst + md.off(v) + e * dst_half.
 //   bitrev_out: single-pass transform (R == N): write natural n to row rev_L(n).
-struct Twist {
-    const uint32_t *lo0, *hi0, *lo1, *hi1;
-};
 template <int LOGR, bool DIT>
 __global__ __launch_bounds__(NT) void k_ntt_contig(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                    int L, const uint32_t *__restrict__ tw, int bitrev_out,
@@ -205,16 +218,24 @@ __global__ __launch_bounds__(NT) void k_ntt_contig(const uint32_t *src, uint32_t
     const uint32_t *sp = src + ms.off(blockIdx.y) + base;
     for (int i = threadIdx.x; i < R; i += NT) a[i] = sp[i];
     __syncthreads();
+    if (use_twist == 2) {
+        // twist on output: natural coefficient n -> E0 / E1 halves (DIT iNTT of bit-reversed input)
+        for (int i = threadIdx.x; i < R; i += NT) x[i] = a[i];
+        __syncthreads();
+        tile_stages<LOGR, 1, DIT>(x, tw, 1, 0);
+        uint32_t *dp = dst + md.off(blockIdx.y);
+        for (int i = threadIdx.x; i < R; i += NT) {
+            const uint32_t n = (uint32_t)(base + i);
+            dp[n] = mul(x[i], tws.f(0, n));
+            dp[dst_half + n] = mul(x[i], tws.f(1, n));
+        }
+        return;
+    }
     const int ne = use_twist ? 2 : 1;
     for (int e = 0; e < ne; e++) {
         for (int i = threadIdx.x; i < R; i += NT) {
             uint32_t v = a[i];
-            if (use_twist) {
-                const uint32_t k = rev_bits((uint32_t)(base + i), L);
-                const uint32_t *lo = e ? tws.lo1 : tws.lo0;
-                const uint32_t *hi = e ? tws.hi1 : tws.hi0;
-                v = mul(v, mul(hi[k >> 12], lo[k & 4095]));
-            }
+            if (use_twist) v = mul(v, tws.f(e, rev_bits((uint32_t)(base + i), L)));
             x[i] = v;
         }
         __syncthreads();
@@ -232,11 +253,12 @@ __global__ __launch_bounds__(NT) void k_ntt_contig(const uint32_t *src, uint32_t
 // ------------------------------------------------------------------ dispatch
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
-                        int logS, const uint32_t *tw, int bitrev_out, hipStream_t s) {
+                        int logS, const uint32_t *tw, int bitrev_out, hipStream_t s, Twist tws = Twist{},
+                        int twist_out = 0, uint64_t dst_half = 0) {
     uint64_t tiles = (1ull << L) >> (logR + 6);
     dim3 g((unsigned)tiles, nv);
 #define SCASE(k) \
-    case k: hipLaunchKernelGGL((k_ntt_strided<k, DIT>), g, dim3(NT), 0, s, src, dst, ms, md, L, logS, tw, bitrev_out); break;
+    case k: hipLaunchKernelGGL((k_ntt_strided<k, DIT>), g, dim3(NT), 0, s, src, dst, ms, md, L, logS, tw, bitrev_out, tws, twist_out, dst_half); break;
     switch (logR) { SCASE(1) SCASE(2) SCASE(3) SCASE(4) SCASE(5) SCASE(6) default: throw ArgError("bad strided radix"); }
 #undef SCASE
     HIP_CHECK(hipGetLastError());
@@ -274,17 +296,8 @@ static std::vector<int> strided_plan(int L, int &logC) {
     return p;
 }
 
-void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s) {
-    const uint64_t N = src.height, W = src.width;
-    if (!W) return;
-    const int L = ilog2(N);
-    ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
-    ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
-    ARG_CHECK(dst.height == 2 * N && dst.width == W, "LDE destination shape");
-    int logC;
-    std::vector<int> sp = strided_plan(L, logC);
-
-    // twist tables: f0(k) = shift^k / N, f1(k) = (shift w_2N)^k / N, k = hi*4096 + lo
+static DBuf make_twist(uint64_t N, int L, uint32_t shift, Twist &tws, hipStream_t s) {
+    // f0(k) = shift^k / N, f1(k) = (shift w_2N)^k / N, k = hi*4096 + lo
     const int nhi = (int)((N + 4095) / 4096);
     std::vector<uint32_t> tt(2 * (4096 + nhi));
     const uint32_t ninv = inv(to_mont((uint32_t)(N % P)));
@@ -299,7 +312,61 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
     }
     DBuf dtt(tt.size(), s);
     HIP_CHECK(hipMemcpyAsync(dtt.p, tt.data(), tt.size() * 4, hipMemcpyHostToDevice, s));
-    Twist tws{dtt.p, dtt.p + 4096, dtt.p + 4096 + nhi, dtt.p + 2 * 4096 + nhi};
+    HIP_CHECK(hipStreamSynchronize(s));  // tt is pageable host memory
+    tws = Twist{dtt.p, dtt.p + 4096, dtt.p + 4096 + nhi, dtt.p + 2 * 4096 + nhi};
+    return dtt;
+}
+
+// Bit-reversed input evaluations (quotient chunks, produced bit-reversed by k_quotient):
+//   DIT iNTT (bit-reversed in -> natural coefficients), twist on the last pass's write into both
+//   LDE halves, then DIF in place (natural -> bit-reversed): no permutation pass at all.
+void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s) {
+    const uint64_t N = src.height, W = src.width;
+    if (!W) return;
+    const int L = ilog2(N);
+    ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
+    ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
+    ARG_CHECK(dst.height == 2 * N && dst.width == W, "LDE destination shape");
+    int logC;
+    std::vector<int> sp = strided_plan(L, logC);
+    Twist tws;
+    DBuf dtt = make_twist(N, L, shift, tws, s);
+    const uint32_t nv = (uint32_t)W;
+    ColMap m_src{N, 0, 1}, m_dst1{2 * N, 0, 1}, m_dst2{2 * N, N, 2};
+    if (sp.empty()) {
+        run_contig<true>(logC, src.d, dst.d, m_src, m_dst1, nv, L, c.tw_inv, 0, tws, 2, N, s);
+    } else {
+        DBuf work(N * W, s);
+        run_contig<true>(logC, src.d, work.p, m_src, m_src, nv, L, c.tw_inv, 0, tws, 0, 0, s);
+        int logS = logC;
+        for (int i = (int)sp.size() - 1; i >= 0; i--) {
+            const bool last = (i == 0);
+            run_strided<true>(sp[i], work.p, last ? dst.d : work.p, m_src, last ? m_dst1 : m_src, nv, L, logS,
+                              c.tw_inv, 0, s, tws, last ? 1 : 0, N);
+            logS += sp[i];
+        }
+    }
+    // forward DIF in place on both halves
+    int logS = L;
+    for (size_t i = 0; i < sp.size(); i++) {
+        logS -= sp[i];
+        run_strided<false>(sp[i], dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, logS, c.tw_fwd, 0, s);
+    }
+    run_contig<false>(logC, dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, c.tw_fwd, 0, Twist{}, 0, 0, s);
+}
+
+void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s) {
+    const uint64_t N = src.height, W = src.width;
+    if (!W) return;
+    const int L = ilog2(N);
+    ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
+    ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
+    ARG_CHECK(dst.height == 2 * N && dst.width == W, "LDE destination shape");
+    int logC;
+    std::vector<int> sp = strided_plan(L, logC);
+
+    Twist tws;
+    DBuf dtt = make_twist(N, L, shift, tws, s);
 
     // work buffer: per column 2N ([E0 | E1]); the iNTT runs in its first half
     DBuf work(2 * N * W, s);

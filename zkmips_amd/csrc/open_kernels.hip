@@ -1,0 +1,499 @@
+// Device kernels of MachineProver::open (crates/stark/src/prover.rs:298-653) on gfx950.
+//
+//  k_perm_rows / scan : generate_permutation_trace (crates/stark/src/permutation.rs:102-196)
+//  k_quotient         : quotient_values + Chip::eval (crates/stark/src/quotient.rs:19-171,
+//                       chip.rs:259-271, permutation.rs:205-347, folder.rs:79-102)
+//  k_inv_points       : batch inverses of (z - s w^i) (barycentric weights, FRI denominators)
+//  k_open_dot         : opened values p(z) = (z'^N - 1)/N sum_j y_j w_j  (TwoAdicFriPcs::open)
+//  k_fri_reduce       : reduced openings per LDE height (semantics: recursion/circuit/src/fri.rs:97-209)
+//  k_fri_fold / leaves: commit phase (fri.rs:247-361 semantics; Plonky3 fold_even_odd)
+//  k_pow              : proof-of-work grind (challenger.rs:209-221 check_witness)
+//  k_gather           : query openings (rows + Merkle paths)
+// All data is column-major Montgomery; EF values are 4 consecutive words.
+#include "internal.hpp"
+#include "open_kernels.hpp"
+#include "p2.cuh"
+
+namespace zkm {
+
+using namespace kb;
+static constexpr int NT = 256;
+
+__device__ __forceinline__ ef ld_ef(const uint32_t *p) {
+    uint4 v = *(const uint4 *)p;
+    return ef{{v.x, v.y, v.z, v.w}};
+}
+__device__ __forceinline__ void st_ef(uint32_t *p, const ef &e) { *(uint4 *)p = make_uint4(e.c[0], e.c[1], e.c[2], e.c[3]); }
+
+// w_M^j for j in [0, M): tw[M/2 + j] for j < M/2, negated above.
+__device__ __forceinline__ uint32_t root_pow(const uint32_t *__restrict__ tw, uint64_t M, uint64_t j) {
+    if (M == 1) return ONE;
+    const uint64_t h = M >> 1;
+    return j < h ? tw[h + j] : neg(tw[h + (j - h)]);
+}
+
+// value of a VirtualPairCol at one row; advances vp past it
+__device__ __forceinline__ uint32_t apply_vpc(const uint32_t *__restrict__ &vp, const uint32_t *__restrict__ main,
+                                              const uint32_t *__restrict__ prep, uint64_t ldm, uint64_t row) {
+    uint32_t nt = vp[0];
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < nt; i++) {
+        uint32_t col = vp[1 + 2 * i], w = vp[2 + 2 * i];
+        uint32_t v = (col & 0x80000000u) ? main[(uint64_t)(col & 0x7fffffffu) * ldm + row] : prep[(uint64_t)col * ldm + row];
+        acc = add(acc, mul(v, w));
+    }
+    acc = add(acc, vp[1 + 2 * nt]);
+    vp += 2 + 2 * nt;
+    return acc;
+}
+
+// ------------------------------------------------------------------ permutation trace
+__global__ __launch_bounds__(NT) void k_perm_rows(PermArgs a) {
+    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r >= a.n) return;
+    const uint32_t *prog = a.prog;
+    const uint32_t nloc = prog[2];
+    const uint32_t *table = prog + prog[3];
+    ef total = ef_zero();
+    for (int b = 0; b < a.nb; b++) {
+        ef num = ef_zero(), den = ef_one();
+        for (uint32_t i = b * a.batch; i < nloc && i < (uint32_t)(b + 1) * a.batch; i++) {
+            const uint32_t *lk = table + 4 * i;
+            ef d = ef_add_base(a.alpha, lk[0]);
+            ef bp = a.beta;
+            const uint32_t *vp = prog + lk[3];
+            for (uint32_t v = 0; v < lk[2]; v++) {
+                uint32_t x = apply_vpc(vp, a.main, a.prep, a.n, r);
+                d = ef_add(d, ef_mul_base(bp, x));
+                bp = ef_mul(bp, a.beta);
+            }
+            uint32_t m = apply_vpc(vp, a.main, a.prep, a.n, r);
+            if (!lk[1]) m = neg(m);
+            // num/den += m/d
+            num = ef_add(ef_mul(num, d), ef_mul_base(den, m));
+            den = ef_mul(den, d);
+        }
+        ef s = ef_mul(num, ef_inv(den));
+#pragma unroll
+        for (int e = 0; e < 4; e++) a.out[(uint64_t)(4 * b + e) * a.n + r] = s.c[e];
+        total = ef_add(total, s);
+    }
+    st_ef(a.rowsum + 4 * r, total);
+}
+
+// inclusive scan of EF values: block scan (1024 per block) + block totals + fix-up
+__device__ __forceinline__ ef warp_scan_incl(ef v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        ef t;
+#pragma unroll
+        for (int e = 0; e < 4; e++) t.c[e] = __shfl_up(v.c[e], o, 64);
+        if (lane >= o) v = ef_add(v, t);
+    }
+    return v;
+}
+
+// scans 4 consecutive elements per thread; writes inclusive scan to out_cols (4 columns, stride n)
+// (or back into `data` when out_cols == nullptr) and the block total to totals[blockIdx]
+__global__ __launch_bounds__(NT) void k_scan_block(uint32_t *data, uint64_t n, uint32_t *totals) {
+    __shared__ uint32_t wsum[NT / 64][4];
+    const uint64_t base = (uint64_t)blockIdx.x * NT * 4 + threadIdx.x * 4;
+    ef v[4];
+    ef run = ef_zero();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        v[k] = (base + k < n) ? ld_ef(data + 4 * (base + k)) : ef_zero();
+        run = ef_add(run, v[k]);
+        v[k] = run;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    ef incl = warp_scan_incl(run, lane);
+    if (lane == 63)
+        for (int e = 0; e < 4; e++) wsum[wid][e] = incl.c[e];
+    __syncthreads();
+    ef off = ef_sub(incl, run);  // exclusive within wave
+    for (int w = 0; w < wid; w++) off = ef_add(off, ef{{wsum[w][0], wsum[w][1], wsum[w][2], wsum[w][3]}});
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (base + k < n) st_ef(data + 4 * (base + k), ef_add(v[k], off));
+    if (threadIdx.x == NT - 1) st_ef(totals + 4 * blockIdx.x, ef_add(off, run));
+}
+
+__global__ void k_scan_totals(uint32_t *totals, uint64_t nblocks) {
+    // single thread sequential exclusive scan (nblocks <= 2^13)
+    if (threadIdx.x || blockIdx.x) return;
+    ef run = ef_zero();
+    for (uint64_t i = 0; i < nblocks; i++) {
+        ef t = ld_ef(totals + 4 * i);
+        st_ef(totals + 4 * i, run);
+        run = ef_add(run, t);
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_scan_fix(const uint32_t *data, uint64_t n, const uint32_t *totals,
+                                                 uint32_t *out_cols) {
+    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    ef v = ef_add(ld_ef(data + 4 * i), ld_ef(totals + 4 * (i / (NT * 4))));
+#pragma unroll
+    for (int e = 0; e < 4; e++) out_cols[(uint64_t)e * n + i] = v.c[e];
+}
+
+void launch_perm_trace(const PermArgs &a, hipStream_t s) {
+    if (a.nb < 0) return;
+    hipLaunchKernelGGL(k_perm_rows, dim3((unsigned)((a.n + NT - 1) / NT)), dim3(NT), 0, s, a);
+    HIP_CHECK(hipGetLastError());
+    const uint64_t nblk = (a.n + NT * 4 - 1) / (NT * 4);
+    DBuf totals(4 * nblk, s);
+    hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nblk), dim3(NT), 0, s, a.rowsum, a.n, totals.p);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(64), 0, s, totals.p, nblk);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_scan_fix, dim3((unsigned)((a.n + NT - 1) / NT)), dim3(NT), 0, s, a.rowsum, a.n, totals.p,
+                       a.out + (uint64_t)4 * a.nb * a.n);
+    HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ quotient
+static constexpr int QSTACK = 24;
+
+__global__ __launch_bounds__(NT) void k_quotient(QuotArgs a) {
+    extern __shared__ uint32_t lds_stack[];  // [wave][depth][64]
+    const uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    uint32_t *stk = lds_stack + (threadIdx.x >> 6) * QSTACK * 64 + lane;
+    if (t >= a.q) return;  // q is a multiple of 64 (>= 16 rows * 2 ... checked on host)
+    const uint64_t ldm = a.ld;  // LDE height (column stride)
+    const uint64_t rl = t;
+    const uint64_t k = rev_bits((uint32_t)t, a.log_q);
+    const uint64_t kn = (k + a.step) & (a.q - 1);
+    const uint64_t rn = rev_bits((uint32_t)kn, a.log_q);
+    // selectors at x = 3 w_Q^k over trace domain H_N (quotient.rs:42; Plonky3 selectors_on_coset)
+    const uint32_t x = mul(a.gen, root_pow(a.tw, a.q, k));
+    const uint32_t zh = (a.q == 2 * a.n) ? ((k & 1) ? sub(neg(a.gen_pow_n), ONE) : sub(a.gen_pow_n, ONE))
+                                         : sub(a.gen_pow_n, ONE);
+    const uint32_t d_first = sub(x, ONE), d_last = sub(x, a.wn_inv);
+    const uint32_t inv_fl = inv(mul(mul(d_first, d_last), zh));  // one inversion for three
+    const uint32_t is_first = mul(mul(inv_fl, d_last), mul(zh, zh));
+    const uint32_t is_last = mul(mul(inv_fl, d_first), mul(zh, zh));
+    const uint32_t is_trans = d_last;
+    const uint32_t inv_z = mul(inv_fl, mul(d_first, d_last));
+
+    const uint32_t *main = a.main, *prep = a.prep, *perm = a.perm;
+    const uint32_t *prog = a.prog;
+    const uint32_t *code = prog + prog[1];
+    const uint32_t code_len = prog[0];
+    ef acc = ef_zero();
+    uint32_t k_c = 0;  // constraint index
+    // ---- AIR program (postfix; stack top in a register, the rest in LDS) ----
+    int sp = 0;
+    uint32_t top = 0;
+    bool has = false;
+#define PUSH(v)                                   \
+    do {                                          \
+        if (has) { stk[sp * 64] = top; sp++; }    \
+        top = (v);                                \
+        has = true;                               \
+    } while (0)
+    for (uint32_t pc = 0; pc < code_len;) {
+        const uint32_t op = code[pc++];
+        switch (op) {
+        case 1: { uint32_t c = code[pc++]; PUSH(main[(uint64_t)c * ldm + rl]); break; }
+        case 2: { uint32_t c = code[pc++]; PUSH(main[(uint64_t)c * ldm + rn]); break; }
+        case 3: { uint32_t c = code[pc++]; PUSH(prep[(uint64_t)c * ldm + rl]); break; }
+        case 4: { uint32_t c = code[pc++]; PUSH(prep[(uint64_t)c * ldm + rn]); break; }
+        case 5: { uint32_t v = code[pc++]; PUSH(v); break; }
+        case 6: { uint32_t i = code[pc++]; PUSH(a.pv[i]); break; }
+        case 7: PUSH(is_first); break;
+        case 8: PUSH(is_last); break;
+        case 9: PUSH(is_trans); break;
+        case 10: { sp--; top = add(stk[sp * 64], top); break; }
+        case 11: { sp--; top = sub(stk[sp * 64], top); break; }
+        case 12: { sp--; top = mul(stk[sp * 64], top); break; }
+        case 13: top = neg(top); break;
+        case 14: {
+            acc = ef_add(acc, ef_mul_base(ld_ef(a.pows + 4 * k_c), top));
+            k_c++;
+            if (sp) { sp--; top = stk[sp * 64]; } else has = false;
+            break;
+        }
+        default: break;
+        }
+    }
+#undef PUSH
+    // ---- LogUp constraints (permutation.rs:256-333) ----
+    const uint32_t nloc = prog[2];
+    if (nloc) {
+        const uint32_t *table = prog + prog[3];
+        const int nb = a.perm_w - 1;
+        ef sum_l = ef_zero(), sum_n = ef_zero();
+        for (int b = 0; b < nb; b++) {
+            ef prod = ef_one(), num = ef_zero();
+            for (uint32_t i = b * a.batch; i < nloc && i < (uint32_t)(b + 1) * a.batch; i++) {
+                const uint32_t *lk = table + 4 * i;
+                ef rlc = ef_add_base(a.alpha_p, lk[0]);
+                ef bp = a.beta_p;
+                const uint32_t *vp = prog + lk[3];
+                for (uint32_t v = 0; v < lk[2]; v++) {
+                    uint32_t xv = apply_vpc(vp, main, prep, ldm, rl);
+                    rlc = ef_add(rlc, ef_mul_base(bp, xv));
+                    bp = ef_mul(bp, a.beta_p);
+                }
+                uint32_t m = apply_vpc(vp, main, prep, ldm, rl);
+                if (!lk[1]) m = neg(m);
+                // numerator = sum_i m_i prod_{j != i} rlc_j, built incrementally
+                num = ef_add(ef_mul(num, rlc), ef_mul_base(prod, m));
+                prod = ef_mul(prod, rlc);
+            }
+            ef entry, entry_n;
+            for (int e = 0; e < 4; e++) {
+                entry.c[e] = perm[(uint64_t)(4 * b + e) * ldm + rl];
+                entry_n.c[e] = perm[(uint64_t)(4 * b + e) * ldm + rn];
+            }
+            sum_l = ef_add(sum_l, entry);
+            sum_n = ef_add(sum_n, entry_n);
+            ef c = ef_sub(ef_mul(prod, entry), num);
+            acc = ef_add(acc, ef_mul(ld_ef(a.pows + 4 * k_c), c));
+            k_c++;
+        }
+        ef phi_l, phi_n;
+        for (int e = 0; e < 4; e++) {
+            phi_l.c[e] = perm[(uint64_t)(4 * nb + e) * ldm + rl];
+            phi_n.c[e] = perm[(uint64_t)(4 * nb + e) * ldm + rn];
+        }
+        ef c0 = ef_mul_base(ef_sub(phi_l, sum_l), is_first);
+        acc = ef_add(acc, ef_mul(ld_ef(a.pows + 4 * k_c), c0)); k_c++;
+        ef c1 = ef_mul_base(ef_sub(ef_sub(phi_n, phi_l), sum_n), is_trans);
+        acc = ef_add(acc, ef_mul(ld_ef(a.pows + 4 * k_c), c1)); k_c++;
+        ef c2 = ef_mul_base(ef_sub(phi_l, a.lcs), is_last);
+        acc = ef_add(acc, ef_mul(ld_ef(a.pows + 4 * k_c), c2)); k_c++;
+    }
+    if (a.global) {
+        const uint32_t W = a.main_w;
+        for (int i = 0; i < 7; i++) {
+            uint32_t cx = mul(sub(main[(uint64_t)(W - 14 + i) * ldm + rl], a.gcs[i]), is_last);
+            acc = ef_add(acc, ef_mul_base(ld_ef(a.pows + 4 * k_c), cx)); k_c++;
+            uint32_t cy = mul(sub(main[(uint64_t)(W - 7 + i) * ldm + rl], a.gcs[7 + i]), is_last);
+            acc = ef_add(acc, ef_mul_base(ld_ef(a.pows + 4 * k_c), cy)); k_c++;
+        }
+    }
+    const ef q = ef_mul_base(acc, inv_z);
+    // chunk c = k mod 2^lqd (= top bit of t when lqd = 1), stored bit-reversed within the chunk
+    const uint64_t c = t >> a.log_n;
+    const uint64_t pos = t & (a.n - 1);
+#pragma unroll
+    for (int e = 0; e < 4; e++) a.chunks[(c * 4 + e) * a.n + pos] = q.c[e];
+}
+
+void launch_quotient(const QuotArgs &a, hipStream_t s) {
+    const size_t lds = (size_t)(NT / 64) * QSTACK * 64 * 4;
+    hipLaunchKernelGGL(k_quotient, dim3((unsigned)((a.q + NT - 1) / NT)), dim3(NT), lds, s, a);
+    HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ batch inverses at points
+// out[i] = (mul_omega ? w^idx : 1) / (z - s * w_M^idx), idx = bitrev ? rev(i) : i
+static constexpr int INV_CHUNK = 32;
+__global__ __launch_bounds__(NT) void k_inv_points(ef z, uint32_t s, const uint32_t *__restrict__ tw, uint64_t M,
+                                                   int log_m, int bitrev, int mul_omega, uint32_t *out) {
+    const uint64_t c = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    const uint64_t i0 = c * INV_CHUNK;
+    if (i0 >= M) return;
+    const uint64_t i1 = i0 + INV_CHUNK < M ? i0 + INV_CHUNK : M;
+    ef run = ef_one();
+    for (uint64_t i = i0; i < i1; i++) {
+        const uint64_t idx = bitrev ? rev_bits((uint32_t)i, log_m) : i;
+        ef d = ef_sub(z, ef_base(mul(s, root_pow(tw, M, idx))));
+        run = ef_mul(run, d);
+        st_ef(out + 4 * i, run);  // prefix products
+    }
+    ef inv_all = ef_inv(run);
+    for (uint64_t i = i1; i-- > i0;) {
+        const uint64_t idx = bitrev ? rev_bits((uint32_t)i, log_m) : i;
+        const uint32_t om = root_pow(tw, M, idx);
+        ef d = ef_sub(z, ef_base(mul(s, om)));
+        ef prev = (i > i0) ? ld_ef(out + 4 * (i - 1)) : ef_one();
+        ef v = ef_mul(inv_all, prev);
+        inv_all = ef_mul(inv_all, d);
+        st_ef(out + 4 * i, mul_omega ? ef_mul_base(v, om) : v);
+    }
+}
+
+void launch_inv_points(const ef &z, uint32_t s, const uint32_t *tw, uint64_t M, bool bitrev, bool mul_omega,
+                       uint32_t *out, hipStream_t st) {
+    const uint64_t chunks = (M + INV_CHUNK - 1) / INV_CHUNK;
+    hipLaunchKernelGGL(k_inv_points, dim3((unsigned)((chunks + NT - 1) / NT)), dim3(NT), 0, st, z, s, tw, M,
+                       ilog2(M), (int)bitrev, (int)mul_omega, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ opening dot products
+// partial[(col * nseg + seg) * 2 + p] = sum_{j in seg} y_{j + p} w_j   (p = 1 only if with_next)
+__global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint64_t n,
+                                                 const uint32_t *__restrict__ w, int with_next, int nseg,
+                                                 uint32_t *partial) {
+    __shared__ uint32_t red[2][NT / 64][4];
+    const uint32_t *y = (const uint32_t *)cols[blockIdx.y];
+    const uint64_t seg_len = (n + nseg - 1) / nseg;
+    const uint64_t j0 = (uint64_t)blockIdx.x * seg_len;
+    const uint64_t j1 = j0 + seg_len < n ? j0 + seg_len : n;
+    ef a0 = ef_zero(), a1 = ef_zero();
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += NT) {
+        ef wj = ld_ef(w + 4 * j);
+        a0 = ef_add(a0, ef_mul_base(wj, y[j]));
+        if (with_next) a1 = ef_add(a1, ef_mul_base(wj, y[(j + 1) & (n - 1)]));
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            a0.c[e] = add(a0.c[e], __shfl_xor(a0.c[e], o, 64));
+            a1.c[e] = add(a1.c[e], __shfl_xor(a1.c[e], o, 64));
+        }
+    if (lane == 0)
+        for (int e = 0; e < 4; e++) { red[0][wid][e] = a0.c[e]; red[1][wid][e] = a1.c[e]; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ef s0 = ef_zero(), s1 = ef_zero();
+        for (int k = 0; k < NT / 64; k++) {
+            s0 = ef_add(s0, ef{{red[0][k][0], red[0][k][1], red[0][k][2], red[0][k][3]}});
+            s1 = ef_add(s1, ef{{red[1][k][0], red[1][k][1], red[1][k][2], red[1][k][3]}});
+        }
+        uint32_t *o = partial + ((uint64_t)blockIdx.y * nseg + blockIdx.x) * 8;
+        st_ef(o, s0);
+        st_ef(o + 4, s1);
+    }
+}
+
+void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next, int nseg,
+                     uint32_t *partial, hipStream_t s) {
+    if (!ncols) return;
+    hipLaunchKernelGGL(k_open_dot, dim3(nseg, ncols), dim3(NT), 0, s, d_cols, n, w, (int)with_next, nseg, partial);
+    HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ FRI reduced openings
+// ro[i] += sum_m sum_p (B_{m,p} - A_{m,p} S_m(i)) * inv_p[i],  S_m(i) = sum_c alpha^c y_{m,c}[i]
+// terms: per matrix: [ncols, col table offset, npts, (pt, A(4), B(4)) x npts] (words)
+__global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= a.h) return;
+    ef t0 = ef_zero(), t1 = ef_zero();
+    const uint32_t *d = a.desc;
+    for (uint32_t m = 0; m < a.nmats; m++) {
+        const uint32_t ncols = d[0], coff = d[1], npts = d[2];
+        ef s = ef_zero();
+        for (uint32_t c = 0; c < ncols; c++) {
+            const uint32_t *col = (const uint32_t *)a.cols[coff + c];
+            s = ef_add(s, ef_mul_base(ld_ef(a.alpha_pows + 4 * c), col[i]));
+        }
+        const uint32_t *pp = d + 3;
+        for (uint32_t p = 0; p < npts; p++, pp += 9) {
+            ef A{{pp[1], pp[2], pp[3], pp[4]}}, B{{pp[5], pp[6], pp[7], pp[8]}};
+            ef v = ef_sub(B, ef_mul(A, s));
+            if (pp[0]) t1 = ef_add(t1, v); else t0 = ef_add(t0, v);
+        }
+        d = pp;
+    }
+    ef r = ld_ef(a.ro + 4 * i);
+    r = ef_add(r, ef_mul(t0, ld_ef(a.inv0 + 4 * i)));
+    if (a.inv1) r = ef_add(r, ef_mul(t1, ld_ef(a.inv1 + 4 * i)));
+    st_ef(a.ro + 4 * i, r);
+}
+
+void launch_fri_reduce(const ReduceArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_fri_reduce, dim3((unsigned)((a.h + NT - 1) / NT)), dim3(NT), 0, s, a);
+    HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ FRI commit phase
+// next[i] = (1/2 + b/2 g^-rev(i)) lo + (1/2 - b/2 g^-rev(i)) hi + b^2 ro[i]; g = w_{2h}
+__global__ __launch_bounds__(NT) void k_fri_fold(const uint32_t *cur, uint64_t h, int log_h, ef half_beta, ef beta2,
+                                                 const uint32_t *__restrict__ tw_inv, const uint32_t *ro, uint32_t *next) {
+    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= h) return;
+    const uint32_t half = halve(ONE);
+    const uint32_t g = tw_inv[h + rev_bits((uint32_t)i, log_h)];
+    const ef pw = ef_mul_base(half_beta, g);
+    const ef lo = ld_ef(cur + 8 * i), hi = ld_ef(cur + 8 * i + 4);
+    ef r = ef_add(ef_mul(ef_add_base(pw, half), lo), ef_mul(ef_sub(ef_base(half), pw), hi));
+    if (ro) r = ef_add(r, ef_mul(beta2, ld_ef(ro + 4 * i)));
+    st_ef(next + 4 * i, r);
+}
+
+__global__ __launch_bounds__(NT) void k_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= h) return;
+    uint32_t s[16];
+    const uint4 a = *(const uint4 *)(cur + 8 * i), b = *(const uint4 *)(cur + 8 * i + 4);
+    s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+#pragma unroll
+    for (int k = 8; k < 16; k++) s[k] = 0;
+    p2::permute(s);
+    uint4 *o = (uint4 *)(out + 8 * i);
+    o[0] = make_uint4(s[0], s[1], s[2], s[3]);
+    o[1] = make_uint4(s[4], s[5], s[6], s[7]);
+}
+
+void launch_fri_fold(const uint32_t *cur, uint64_t h, const ef &half_beta, const ef &beta2, const uint32_t *tw_inv,
+                     const uint32_t *ro, uint32_t *next, hipStream_t s) {
+    hipLaunchKernelGGL(k_fri_fold, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s, cur, h, ilog2(h), half_beta,
+                       beta2, tw_inv, ro, next);
+    HIP_CHECK(hipGetLastError());
+}
+void launch_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_fri_leaves, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s, cur, h, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ proof of work
+__global__ __launch_bounds__(NT) void k_pow(PowArgs a, uint32_t base, uint32_t *result) {
+    const uint32_t w = base + blockIdx.x * NT + threadIdx.x;
+    if (w >= P) return;
+    uint32_t s[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) s[k] = a.state[k];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (k < (int)a.nin) s[k] = a.in[k];
+    const uint32_t wm = to_mont(w);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (k == (int)a.nin) s[k] = wm;
+    p2::permute(s);
+    if ((from_mont(s[7]) & a.mask) == 0) atomicMin(result, w);
+}
+
+uint32_t run_pow(const PowArgs &a, hipStream_t s) {
+    DBuf res(1, s);
+    const uint32_t batch = 1u << 20;
+    for (uint64_t base = 0; base < P; base += batch) {
+        uint32_t init = 0xffffffffu, got = 0;
+        HIP_CHECK(hipMemcpyAsync(res.p, &init, 4, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_pow, dim3(batch / NT), dim3(NT), 0, s, a, (uint32_t)base, res.p);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(&got, res.p, 4, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (got != 0xffffffffu) return got;
+    }
+    throw HipError("no proof-of-work witness found");
+}
+
+// ------------------------------------------------------------------ gathers
+// item: src (u64 ptr), stride (elements), count, dst offset
+__global__ __launch_bounds__(64) void k_gather(const uint64_t *__restrict__ items, uint32_t *dst) {
+    const uint64_t *it = items + 3 * blockIdx.x;
+    const uint32_t *src = (const uint32_t *)it[0];
+    const uint64_t stride = it[1] & 0xffffffffull, count = it[1] >> 32;
+    const uint64_t off = it[2];
+    for (uint64_t k = threadIdx.x; k < count; k += 64) dst[off + k] = src[k * stride];
+}
+
+void launch_gather(const uint64_t *d_items, uint32_t nitems, uint32_t *dst, hipStream_t s) {
+    if (!nitems) return;
+    hipLaunchKernelGGL(k_gather, dim3(nitems), dim3(64), 0, s, d_items, dst);
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace zkm

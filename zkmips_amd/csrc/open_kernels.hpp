@@ -1,0 +1,70 @@
+// Kernel argument blocks and launchers of open_kernels.hip.
+#pragma once
+#include "internal.hpp"
+
+namespace zkm {
+
+struct PermArgs {
+    const uint32_t *prog;     // flattened chip program (device)
+    const uint32_t *main;     // trace, column-major natural, n rows
+    const uint32_t *prep;     // preprocessed trace or nullptr
+    uint64_t n;
+    kb::ef alpha, beta;       // local permutation challenges
+    int batch, nb;            // lookups per batch, number of batch columns
+    uint32_t *out;            // flattened perm trace, column-major (4 * (nb + 1) columns)
+    uint32_t *rowsum;         // scratch: n EF
+};
+void launch_perm_trace(const PermArgs &a, hipStream_t s);
+
+struct QuotArgs {
+    const uint32_t *prog;
+    const uint32_t *main, *prep, *perm;  // LDEs (column stride ld, bit-reversed rows)
+    uint64_t ld;                         // LDE height (2n)
+    uint64_t n, q;                       // trace height, quotient domain size
+    int log_n, log_q, step;
+    const uint32_t *tw;                  // forward twiddles
+    uint32_t gen, gen_pow_n, wn_inv;     // 3, 3^n, w_n^-1 (Montgomery)
+    const uint32_t *pv;                  // public values (Montgomery)
+    const uint32_t *pows;                // alpha^(nc-1-k), EF
+    kb::ef alpha_p, beta_p, lcs;
+    uint32_t gcs[14];
+    int batch, perm_w, global, main_w;
+    uint32_t *chunks;                    // 2^lqd chunks x 4 columns x n rows (bit-reversed rows)
+};
+void launch_quotient(const QuotArgs &a, hipStream_t s);
+
+void launch_inv_points(const kb::ef &z, uint32_t s, const uint32_t *tw, uint64_t M, bool bitrev, bool mul_omega,
+                       uint32_t *out, hipStream_t st);
+void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next, int nseg,
+                     uint32_t *partial, hipStream_t s);
+
+struct ReduceArgs {
+    const uint64_t *cols;      // column pointer table
+    const uint32_t *desc;      // per-matrix descriptors
+    uint32_t nmats;
+    const uint32_t *alpha_pows;// alpha^c, EF
+    const uint32_t *inv0, *inv1;  // 1/(z_p - x_i), EF (inv1 may be null)
+    uint32_t *ro;              // EF accumulator, h entries
+    uint64_t h;
+};
+void launch_fri_reduce(const ReduceArgs &a, hipStream_t s);
+void launch_fri_fold(const uint32_t *cur, uint64_t h, const kb::ef &half_beta, const kb::ef &beta2,
+                     const uint32_t *tw_inv, const uint32_t *ro, uint32_t *next, hipStream_t s);
+void launch_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out, hipStream_t s);
+
+struct PowArgs {
+    uint32_t state[16];
+    uint32_t in[8];
+    uint32_t nin;
+    uint32_t mask;
+};
+uint32_t run_pow(const PowArgs &a, hipStream_t s);
+
+void launch_gather(const uint64_t *d_items, uint32_t nitems, uint32_t *dst, hipStream_t s);
+
+// LDE variant for bit-reversed input evaluations (quotient chunks)
+void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst, hipStream_t s);
+// tree from a precomputed leaf digest layer (FRI commit-phase trees)
+void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s);
+
+}  // namespace zkm

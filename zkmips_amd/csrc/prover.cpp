@@ -1,0 +1,807 @@
+// MI355X shard prover: MachineProver::{setup, commit, open} behind the C ABI.
+//
+// Host-side orchestration follows the reference step by step:
+//   StarkMachine::setup            crates/stark/src/machine.rs:332-439
+//   CpuProver::commit              crates/stark/src/prover.rs:258-292
+//   CpuProver::open                crates/stark/src/prover.rs:298-653
+//   TwoAdicFriPcs::open + FRI      Plonky3 fork @faa24ca (not vendored); semantics pinned by the
+//                                  verifier restatement crates/recursion/circuit/src/fri.rs:34-405
+// Every O(N) step runs on the GPU (open_kernels.hip, ntt.hip, merkle.hip); the host keeps the
+// Fiat-Shamir transcript (a few hundred Poseidon2 permutations) and assembles the proof.
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <numeric>
+
+#include "../../include/zkm_hip.h"
+#include "chip.hpp"
+#include "internal.hpp"
+#include "open_kernels.hpp"
+#include "p2.cuh"
+
+namespace zkm {
+
+using namespace kb;
+using Digest = std::array<uint32_t, 8>;
+
+int guard_status(const std::exception &e);
+DBuf upload_matrix(const zkm_matrix_t &m, hipStream_t s);
+extern thread_local std::string g_last_error;
+
+static const uint32_t CURVE_START[14] = {637514027u, 1595065213u, 1998064738u, 72333738u,  1211544370u,
+                                         822986770u, 1518535784u, 1604177449u, 90440090u, 259343427u,
+                                         140470264u, 1162099742u, 941559812u,  1064053343u};
+
+// ------------------------------------------------------------------ host challenger (Montgomery)
+struct Challenger {
+    uint32_t st[16] = {0};
+    uint32_t in[8] = {0};
+    int nin = 0;
+    uint32_t out[8] = {0};
+    int nout = 0;
+    void duplex() {
+        for (int i = 0; i < nin; i++) st[i] = in[i];
+        nin = 0;
+        p2::permute(st);
+        memcpy(out, st, 32);
+        nout = 8;
+    }
+    void observe(uint32_t v) {
+        nout = 0;
+        in[nin++] = v;
+        if (nin == 8) duplex();
+    }
+    void observe(const uint32_t *v, size_t n) { for (size_t i = 0; i < n; i++) observe(v[i]); }
+    void observe_ef(const ef &e) { observe(e.c, 4); }
+    uint32_t sample() {
+        if (nin || !nout) duplex();
+        return out[--nout];
+    }
+    ef sample_ef() {
+        ef e;
+        for (int i = 0; i < 4; i++) e.c[i] = sample();
+        return e;
+    }
+    uint32_t sample_bits(int bits) { return from_mont(sample()) & ((1u << bits) - 1u); }
+    void load(const zkm_challenger_t &c) {
+        for (int i = 0; i < 16; i++) st[i] = to_mont(c.sponge_state[i]);
+        nin = (int)c.num_inputs;
+        nout = (int)c.num_outputs;
+        ARG_CHECK(nin <= 8 && nout <= 8, "challenger buffers");
+        for (int i = 0; i < 8; i++) { in[i] = to_mont(c.input_buffer[i]); out[i] = to_mont(c.output_buffer[i]); }
+    }
+    void store(zkm_challenger_t &c) const {
+        for (int i = 0; i < 16; i++) c.sponge_state[i] = from_mont(st[i]);
+        c.num_inputs = (uint32_t)nin;
+        c.num_outputs = (uint32_t)nout;
+        for (int i = 0; i < 8; i++) {
+            c.input_buffer[i] = i < nin ? from_mont(in[i]) : 0u;
+            c.output_buffer[i] = i < nout ? from_mont(out[i]) : 0u;
+        }
+    }
+};
+
+// ------------------------------------------------------------------ keys and shard data
+struct Pk {
+    int device = 0;
+    Machine m;
+    zkm_config_t cfg{};
+    uint32_t commit[8];        // Montgomery
+    uint32_t pc_start;         // Montgomery
+    uint32_t gcs[14];          // Montgomery
+    std::vector<int> trace_chip;
+    std::vector<uint64_t> heights;
+    std::vector<DBuf> traces;  // column-major natural (Montgomery)
+    DTree tree;                // LDEs owned by tree.owned
+    std::vector<DBuf> progs;   // flattened chip programs (device)
+    int pk_index(int chip) const {
+        for (size_t i = 0; i < trace_chip.size(); i++)
+            if (trace_chip[i] == chip) return (int)i;
+        return -1;
+    }
+};
+
+struct MainData {
+    std::vector<int> chip;         // machine chip index, in commit order (height desc, name)
+    std::vector<uint64_t> heights;
+    std::vector<DBuf> traces;      // column-major natural
+    DTree tree;
+    std::vector<uint32_t> pv;      // canonical
+};
+
+static std::vector<int> sort_order(const std::vector<uint64_t> &h, const std::vector<std::string> &names) {
+    std::vector<int> o(h.size());
+    std::iota(o.begin(), o.end(), 0);
+    std::stable_sort(o.begin(), o.end(), [&](int a, int b) {
+        if (h[a] != h[b]) return h[a] > h[b];
+        return names[a] < names[b];
+    });
+    return o;
+}
+
+static void add_lde(Ctx &c, DTree &t, const DMat &src, uint32_t shift, bool bitrev_in, hipStream_t s) {
+    t.owned.emplace_back(2 * src.height * (src.width ? src.width : 1), s);
+    DMat dst{t.owned.back().p, 2 * src.height, src.width};
+    if (bitrev_in) lde_batch_bitrev_in(c, src, shift, dst, s);
+    else lde_batch(c, src, shift, dst, s);
+    t.mats.push_back(dst);
+}
+
+// ------------------------------------------------------------------ proof object + bincode
+struct ChipOpen {
+    std::vector<ef> prep_l, prep_n, main_l, main_n, perm_l, perm_n;
+    std::vector<ef> quot;  // nq * 4
+    uint32_t gcs[14];
+    ef lcs;
+    uint64_t log_degree;
+};
+struct BatchOpen {
+    std::vector<std::vector<uint32_t>> vals;
+    std::vector<Digest> path;
+};
+struct Step {
+    ef sib;
+    std::vector<Digest> path;
+};
+struct Query {
+    std::vector<BatchOpen> input;
+    std::vector<Step> steps;
+};
+struct Proof {
+    Digest main_c, perm_c, quot_c;
+    std::vector<ChipOpen> chips;
+    std::vector<Digest> fri_commits;
+    std::vector<Query> queries;
+    ef final_poly;
+    uint32_t pow;
+    std::vector<std::string> names;
+    std::vector<uint32_t> pv;  // canonical
+};
+
+struct Writer {
+    std::vector<uint8_t> b;
+    bool mont;
+    void put(const void *p, size_t n) { b.insert(b.end(), (const uint8_t *)p, (const uint8_t *)p + n); }
+    void u64(uint64_t v) { put(&v, 8); }
+    void f(uint32_t mont_val) { uint32_t v = mont ? mont_val : from_mont(mont_val); put(&v, 4); }
+    void fc(uint32_t canon) { uint32_t v = mont ? to_mont(canon) : canon; put(&v, 4); }
+    void e(const ef &x) { for (int i = 0; i < 4; i++) f(x.c[i]); }
+    void d(const Digest &x) { for (int i = 0; i < 8; i++) f(x[i]); }
+    void ev(const std::vector<ef> &v) { u64(v.size()); for (auto &x : v) e(x); }
+    void dv(const std::vector<Digest> &v) { u64(v.size()); for (auto &x : v) d(x); }
+};
+
+// bincode-1 (fixint, LE) layout of ShardProof (crates/stark/src/types.rs:77-83); chip_ordering
+// sorted by index; field elements canonical unless cfg.proof_montgomery.
+static std::vector<uint8_t> serialize(const Proof &p, bool mont) {
+    Writer w{{}, mont};
+    w.d(p.main_c); w.d(p.perm_c); w.d(p.quot_c);
+    w.u64(p.chips.size());
+    for (auto &c : p.chips) {
+        w.ev(c.prep_l); w.ev(c.prep_n); w.ev(c.main_l); w.ev(c.main_n); w.ev(c.perm_l); w.ev(c.perm_n);
+        w.u64(c.quot.size() / 4);
+        for (size_t j = 0; j < c.quot.size() / 4; j++) {
+            w.u64(4);
+            for (int e = 0; e < 4; e++) w.e(c.quot[4 * j + e]);
+        }
+        for (int j = 0; j < 14; j++) w.f(c.gcs[j]);
+        w.e(c.lcs);
+        w.u64(c.log_degree);
+    }
+    w.dv(p.fri_commits);
+    w.u64(p.queries.size());
+    for (auto &q : p.queries) {
+        w.u64(q.input.size());
+        for (auto &bo : q.input) {
+            w.u64(bo.vals.size());
+            for (auto &row : bo.vals) { w.u64(row.size()); for (uint32_t x : row) w.f(x); }
+            w.dv(bo.path);
+        }
+        w.u64(q.steps.size());
+        for (auto &st : q.steps) { w.e(st.sib); w.dv(st.path); }
+    }
+    w.e(p.final_poly);
+    w.f(p.pow);
+    w.u64(p.names.size());
+    for (size_t i = 0; i < p.names.size(); i++) {
+        w.u64(p.names[i].size());
+        w.put(p.names[i].data(), p.names[i].size());
+        w.u64(i);
+    }
+    w.u64(p.pv.size());
+    for (uint32_t x : p.pv) w.fc(x);
+    return std::move(w.b);
+}
+
+static Digest dig(const uint32_t *r) { Digest d; memcpy(d.data(), r, 32); return d; }
+
+// ------------------------------------------------------------------ open
+struct OpenReq {
+    int round, mat;
+    int npts;
+    ef pts[2];
+    std::vector<ef> vals[2];
+};
+
+static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Challenger &ch, hipStream_t s) {
+    const Machine &m = pk.m;
+    const int lb = (int)pk.cfg.log_blowup;
+    const int n = (int)md.chip.size();
+    Proof proof;
+    proof.main_c = dig(md.tree.root);
+    for (int i = 0; i < n; i++) proof.names.push_back(m.chips[md.chip[i]].name);
+    proof.pv = md.pv;
+
+    // observe public values then the main commitment (prover.rs:322-323)
+    ARG_CHECK((int)md.pv.size() >= m.num_pv, "fewer public values than num_pv_elts");
+    for (int i = 0; i < m.num_pv; i++) ch.observe(to_mont(md.pv[i]));
+    ch.observe(md.tree.root, 8);
+    const ef perm_alpha = ch.sample_ef(), perm_beta = ch.sample_ef();
+
+    // ---- permutation traces (prover.rs:337-365) ----
+    proof.chips.resize(n);
+    std::vector<DBuf> perm_traces(n);
+    DTree perm_tree;
+    for (int i = 0; i < n; i++) {
+        const ChipDesc &cd = m.chips[md.chip[i]];
+        const uint64_t N = md.heights[i];
+        const int pki = pk.pk_index(md.chip[i]);
+        ARG_CHECK(pki < 0 || pk.heights[pki] == N, "preprocessed and main heights differ");
+        ChipOpen &co = proof.chips[i];
+        co.log_degree = (uint64_t)ilog2(N);
+        co.lcs = ef_zero();
+        const int pw = cd.perm_w;
+        perm_traces[i] = DBuf(N * 4 * (pw ? pw : 1), s);
+        if (pw) {
+            DBuf rowsum(4 * N, s);
+            PermArgs a{pk.progs[md.chip[i]].p, md.traces[i].p, pki >= 0 ? pk.traces[pki].p : nullptr, N, perm_alpha,
+                       perm_beta, 1 << cd.log_qd, pw - 1, perm_traces[i].p, rowsum.p};
+            launch_perm_trace(a, s);
+            uint32_t l[4];
+            for (int e = 0; e < 4; e++)
+                HIP_CHECK(hipMemcpyAsync(&l[e], perm_traces[i].p + (uint64_t)(4 * (pw - 1) + e) * N + N - 1, 4,
+                                         hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            co.lcs = ef{{l[0], l[1], l[2], l[3]}};
+        }
+        if (cd.scope == 1) {
+            for (int k = 0; k < 14; k++)
+                HIP_CHECK(hipMemcpyAsync(&co.gcs[k], md.traces[i].p + (uint64_t)(cd.main_w - 14 + k) * N + N - 1, 4,
+                                         hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+        } else {
+            for (int k = 0; k < 14; k++) co.gcs[k] = to_mont(CURVE_START[k]);
+        }
+        DMat src{perm_traces[i].p, N, (uint64_t)4 * pw};
+        add_lde(c, perm_tree, src, to_mont(GENERATOR), false, s);
+    }
+    tree_build(perm_tree, s);
+    proof.perm_c = dig(perm_tree.root);
+    ch.observe(perm_tree.root, 8);
+    for (int i = 0; i < n; i++) {
+        ch.observe_ef(proof.chips[i].lcs);
+        ch.observe(proof.chips[i].gcs, 14);
+    }
+    const ef alpha = ch.sample_ef();
+
+    // ---- quotient values, split, commit (prover.rs:415-498) ----
+    std::vector<uint32_t> pv_mont(md.pv.size() + 1, 0);
+    for (size_t k = 0; k < md.pv.size(); k++) pv_mont[k] = to_mont(md.pv[k]);
+    DBuf d_pv(pv_mont.size(), s);
+    HIP_CHECK(hipMemcpyAsync(d_pv.p, pv_mont.data(), pv_mont.size() * 4, hipMemcpyHostToDevice, s));
+    DTree q_tree;
+    std::vector<DBuf> q_chunks(n);
+    std::vector<int> chunk_chip;  // chip of each quotient chunk
+    for (int i = 0; i < n; i++) {
+        const ChipDesc &cd = m.chips[md.chip[i]];
+        const uint64_t N = md.heights[i];
+        const int logN = ilog2(N), lqd = cd.log_qd;
+        ARG_CHECK(lqd <= lb, "log_quotient_degree > log_blowup is not supported (Plonky3 asserts too)");
+        const uint64_t Q = N << lqd;
+        std::vector<uint32_t> pows(4 * (cd.n_constraints + 1));
+        ef a = ef_one();
+        for (int k = cd.n_constraints - 1; k >= 0; k--) {
+            memcpy(&pows[4 * k], a.c, 16);
+            a = ef_mul(a, alpha);
+        }
+        DBuf d_pows(pows.size(), s);
+        HIP_CHECK(hipMemcpyAsync(d_pows.p, pows.data(), pows.size() * 4, hipMemcpyHostToDevice, s));
+        const int pki = pk.pk_index(md.chip[i]);
+        q_chunks[i] = DBuf(((uint64_t)4 << lqd) * N, s);
+        QuotArgs qa{};
+        qa.prog = pk.progs[md.chip[i]].p;
+        qa.main = md.tree.mats[i].d;
+        qa.prep = pki >= 0 ? pk.tree.mats[pki].d : nullptr;
+        qa.perm = perm_tree.mats[i].d;
+        qa.ld = 2 * N;
+        qa.n = N; qa.q = Q; qa.log_n = logN; qa.log_q = logN + lqd; qa.step = 1 << lqd;
+        qa.tw = c.tw_fwd;
+        qa.gen = to_mont(GENERATOR);
+        qa.gen_pow_n = pow(qa.gen, N);
+        qa.wn_inv = inv(two_adic_gen(logN));
+        qa.pv = d_pv.p;
+        qa.pows = d_pows.p;
+        qa.alpha_p = perm_alpha; qa.beta_p = perm_beta; qa.lcs = proof.chips[i].lcs;
+        memcpy(qa.gcs, proof.chips[i].gcs, sizeof qa.gcs);
+        qa.batch = 1 << lqd; qa.perm_w = cd.perm_w; qa.global = cd.scope == 1; qa.main_w = cd.main_w;
+        qa.chunks = q_chunks[i].p;
+        launch_quotient(qa, s);
+        HIP_CHECK(hipStreamSynchronize(s));  // d_pows lifetime
+        const uint32_t wq = two_adic_gen(logN + lqd);
+        for (int j = 0; j < (1 << lqd); j++) {
+            DMat src{q_chunks[i].p + (uint64_t)j * 4 * N, N, 4};
+            add_lde(c, q_tree, src, inv(pow(wq, (uint64_t)j)), true, s);
+            chunk_chip.push_back(i);
+        }
+    }
+    tree_build(q_tree, s);
+    proof.quot_c = dig(q_tree.root);
+    ch.observe(q_tree.root, 8);
+    const ef zeta = ch.sample_ef();
+
+    // ---- opening points (prover.rs:503-544) ----
+    const DTree *trees[4] = {&pk.tree, &md.tree, &perm_tree, &q_tree};
+    std::vector<OpenReq> req;
+    for (size_t t = 0; t < pk.trace_chip.size(); t++) {
+        OpenReq r{0, (int)t, 1, {zeta, zeta}, {}};
+        if (!m.chips[pk.trace_chip[t]].local_only) { r.pts[1] = ef_mul_base(zeta, two_adic_gen(ilog2(pk.heights[t]))); r.npts = 2; }
+        req.push_back(r);
+    }
+    for (int i = 0; i < n; i++) {
+        OpenReq r{1, i, 1, {zeta, zeta}, {}};
+        if (!m.chips[md.chip[i]].local_only) { r.pts[1] = ef_mul_base(zeta, two_adic_gen(ilog2(md.heights[i]))); r.npts = 2; }
+        req.push_back(r);
+    }
+    for (int i = 0; i < n; i++) req.push_back(OpenReq{2, i, 2, {zeta, ef_mul_base(zeta, two_adic_gen(ilog2(md.heights[i])))}, {}});
+    for (size_t j = 0; j < chunk_chip.size(); j++) req.push_back(OpenReq{3, (int)j, 1, {zeta, zeta}, {}});
+
+    // ---- opened values by barycentric evaluation over the trace domain ----
+    //   p(z) = ((z/s)^N - 1)/N * sum_j y_j w^j / (z/s - w^j); next point g z uses y_{j+1}.
+    {
+        const int nseg = 32;
+        std::vector<uint64_t> heights_done;
+        std::vector<std::pair<uint64_t, DBuf>> wtab;  // natural-order weights per trace height (s = 1)
+        auto weights_for = [&](uint64_t N) -> const uint32_t * {
+            for (auto &pr : wtab) if (pr.first == N) return pr.second.p;
+            wtab.emplace_back(N, DBuf(4 * N, s));
+            launch_inv_points(zeta, ONE, c.tw_fwd, N, false, true, wtab.back().second.p, s);
+            return wtab.back().second.p;
+        };
+        for (auto &r : req) {
+            const uint32_t *ybase;
+            uint64_t N, W;
+            bool bitrev = false;
+            uint32_t shift = ONE;
+            if (r.round == 0) { ybase = pk.traces[r.mat].p; N = pk.heights[r.mat]; W = m.chips[pk.trace_chip[r.mat]].prep_w; }
+            else if (r.round == 1) { ybase = md.traces[r.mat].p; N = md.heights[r.mat]; W = m.chips[md.chip[r.mat]].main_w; }
+            else if (r.round == 2) { ybase = perm_traces[r.mat].p; N = md.heights[r.mat]; W = 4 * m.chips[md.chip[r.mat]].perm_w; }
+            else {
+                int ci = chunk_chip[r.mat];
+                int j = 0;
+                for (int k = 0; k < r.mat; k++) if (chunk_chip[k] == ci) j++;
+                N = md.heights[ci];
+                const int lqd = m.chips[md.chip[ci]].log_qd;
+                ybase = q_chunks[ci].p + (uint64_t)j * 4 * N;
+                W = 4;
+                bitrev = true;
+                shift = mul(to_mont(GENERATOR), pow(two_adic_gen(ilog2(N) + lqd), (uint64_t)j));
+            }
+            r.vals[0].assign(W, ef_zero());
+            r.vals[1].assign(W, ef_zero());
+            if (!W) continue;
+            const uint32_t *w;
+            DBuf wq;
+            const ef zs = ef_mul_base(zeta, inv(shift));
+            if (!bitrev) w = weights_for(N);
+            else {
+                wq = DBuf(4 * N, s);
+                launch_inv_points(zs, ONE, c.tw_fwd, N, true, true, wq.p, s);
+                w = wq.p;
+            }
+            std::vector<uint64_t> cols(W);
+            for (uint64_t k = 0; k < W; k++) cols[k] = (uint64_t)(uintptr_t)(ybase + k * N);
+            DBuf dcols(2 * W, s);
+            HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), W * 8, hipMemcpyHostToDevice, s));
+            DBuf part(W * nseg * 8, s);
+            const bool with_next = r.npts == 2;
+            launch_open_dot((const uint64_t *)dcols.p, (uint32_t)W, N, w, with_next, nseg, part.p, s);
+            std::vector<uint32_t> hp(W * nseg * 8);
+            HIP_CHECK(hipMemcpyAsync(hp.data(), part.p, hp.size() * 4, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            // prefactor (z'^N - 1) / N
+            const ef zn = ef_pow(zs, N);
+            const ef pre = ef_mul_base(ef_sub(zn, ef_one()), inv(to_mont((uint32_t)(N % P))));
+            for (uint64_t k = 0; k < W; k++) {
+                ef a0 = ef_zero(), a1 = ef_zero();
+                for (int sg = 0; sg < nseg; sg++) {
+                    const uint32_t *q = &hp[(k * nseg + sg) * 8];
+                    a0 = ef_add(a0, ef{{q[0], q[1], q[2], q[3]}});
+                    a1 = ef_add(a1, ef{{q[4], q[5], q[6], q[7]}});
+                }
+                r.vals[0][k] = ef_mul(pre, a0);
+                r.vals[1][k] = ef_mul(pre, a1);  // (g z)^N = z^N for the trace-domain generator g
+            }
+        }
+    }
+
+    // ---- PCS open: FRI alpha, reduced openings (fri.rs:71-215 semantics) ----
+    const ef fri_alpha = ch.sample_ef();
+    int log_max = 0;
+    for (auto *t : trees) log_max = std::max(log_max, t->log_max);
+    std::vector<DBuf> ro(32);
+    std::vector<int> pow_cnt(32, 0);
+    {
+        // group (round, mat) by LDE height, in global order
+        struct Item { const DMat *mat; const OpenReq *r; };
+        std::vector<std::vector<Item>> by_h(32);
+        for (auto &r : req) {
+            const DMat *mm = &trees[r.round]->mats[r.mat];
+            by_h[ilog2(mm->height)].push_back(Item{mm, &r});
+        }
+        uint64_t max_w = 1;
+        for (auto &r : req) max_w = std::max<uint64_t>(max_w, trees[r.round]->mats[r.mat].width);
+        std::vector<uint32_t> apow(4 * max_w);
+        {
+            ef a = ef_one();
+            for (uint64_t k = 0; k < max_w; k++) { memcpy(&apow[4 * k], a.c, 16); a = ef_mul(a, fri_alpha); }
+        }
+        DBuf d_apow(apow.size(), s);
+        HIP_CHECK(hipMemcpyAsync(d_apow.p, apow.data(), apow.size() * 4, hipMemcpyHostToDevice, s));
+        auto alpha_pow = [&](uint64_t e) { return ef_pow(fri_alpha, e); };
+        for (int lh = 0; lh < 32; lh++) {
+            if (by_h[lh].empty()) continue;
+            const uint64_t H = 1ull << lh;
+            const uint64_t N = H >> lb;
+            ro[lh] = DBuf(4 * H, s);
+            HIP_CHECK(hipMemsetAsync(ro[lh].p, 0, 16 * H, s));
+            // denominators 1/(z - 3 w_H^rev(i)) for z = zeta and zeta * w_N
+            DBuf inv0(4 * H, s), inv1(4 * H, s);
+            launch_inv_points(zeta, to_mont(GENERATOR), c.tw_fwd, H, true, false, inv0.p, s);
+            const ef znext = ef_mul_base(zeta, two_adic_gen(ilog2(N)));
+            bool need1 = false;
+            std::vector<uint64_t> cols;
+            std::vector<uint32_t> desc;
+            for (auto &it : by_h[lh]) {
+                const uint64_t W = it.mat->width;
+                desc.push_back((uint32_t)W);
+                desc.push_back((uint32_t)cols.size());
+                desc.push_back((uint32_t)it.r->npts);
+                for (uint64_t k = 0; k < W; k++) cols.push_back((uint64_t)(uintptr_t)(it.mat->d + k * it.mat->height));
+                for (int p = 0; p < it.r->npts; p++) {
+                    // offset alpha^pow; A = alpha^pow, B = alpha^pow * sum_c alpha^c p_c(z)
+                    const ef ao = alpha_pow((uint64_t)pow_cnt[lh]);
+                    ef sz = ef_zero();
+                    ef ac = ef_one();
+                    for (uint64_t k = 0; k < W; k++) { sz = ef_add(sz, ef_mul(ac, it.r->vals[p][k])); ac = ef_mul(ac, fri_alpha); }
+                    const ef B = ef_mul(ao, sz);
+                    const bool is_next = p == 1;
+                    ARG_CHECK(!is_next || ef_eq(it.r->pts[1], znext), "unexpected opening point");
+                    if (is_next) need1 = true;
+                    desc.push_back(is_next ? 1u : 0u);
+                    for (int e = 0; e < 4; e++) desc.push_back(ao.c[e]);
+                    for (int e = 0; e < 4; e++) desc.push_back(B.c[e]);
+                    pow_cnt[lh] += (int)W;
+                }
+            }
+            if (need1) launch_inv_points(znext, to_mont(GENERATOR), c.tw_fwd, H, true, false, inv1.p, s);
+            DBuf dcols(2 * cols.size() + 2, s), ddesc(desc.size() + 1, s);
+            if (!cols.empty()) HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipMemcpyAsync(ddesc.p, desc.data(), desc.size() * 4, hipMemcpyHostToDevice, s));
+            ReduceArgs ra{(const uint64_t *)dcols.p, ddesc.p, (uint32_t)by_h[lh].size(), d_apow.p, inv0.p,
+                          need1 ? inv1.p : nullptr, ro[lh].p, H};
+            launch_fri_reduce(ra, s);
+            HIP_CHECK(hipStreamSynchronize(s));  // host vectors / temporaries
+        }
+    }
+
+    // ---- FRI commit phase ----
+    const int nrounds = log_max - lb;
+    std::vector<DTree> ftrees(std::max(nrounds, 0));
+    DBuf cur;
+    uint64_t cur_n = 1ull << log_max;
+    {
+        cur = DBuf(4 * cur_n, s);
+        HIP_CHECK(hipMemcpyAsync(cur.p, ro[log_max].p, 16 * cur_n, hipMemcpyDeviceToDevice, s));
+    }
+    const uint32_t half = halve(ONE);
+    for (int rd = 0; rd < nrounds; rd++) {
+        const int lf = log_max - 1 - rd;
+        const uint64_t h = cur_n >> 1;
+        DBuf leaves(8 * h, s);
+        launch_fri_leaves(cur.p, h, leaves.p, s);
+        // keep the folded-from vector: queries open (lo, hi) pairs of it
+        ftrees[rd].owned.push_back(std::move(cur));
+        tree_from_leaves(ftrees[rd], std::move(leaves), h, s);
+        proof.fri_commits.push_back(dig(ftrees[rd].root));
+        ch.observe(ftrees[rd].root, 8);
+        const ef beta = ch.sample_ef();
+        DBuf next(4 * h, s);
+        launch_fri_fold(ftrees[rd].owned.back().p, h, ef_mul_base(beta, half), ef_mul(beta, beta), c.tw_inv,
+                        ro[lf].p ? ro[lf].p : nullptr, next.p, s);
+        cur = std::move(next);
+        cur_n = h;
+        (void)lf;
+    }
+    std::vector<uint32_t> fin(4 * cur_n);
+    HIP_CHECK(hipMemcpyAsync(fin.data(), cur.p, fin.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    proof.final_poly = ef{{fin[0], fin[1], fin[2], fin[3]}};
+    bool final_ok = true;
+    for (uint64_t i = 1; i < cur_n; i++)
+        final_ok &= memcmp(&fin[4 * i], &fin[0], 16) == 0;
+    ch.observe_ef(proof.final_poly);
+
+    // ---- proof of work (canonical: smallest witness) ----
+    {
+        PowArgs pa{};
+        memcpy(pa.state, ch.st, 64);
+        memcpy(pa.in, ch.in, 32);
+        pa.nin = (uint32_t)ch.nin;
+        pa.mask = (1u << pk.cfg.pow_bits) - 1u;
+        const uint32_t w = pk.cfg.pow_bits ? run_pow(pa, s) : 0u;
+        proof.pow = to_mont(w);
+        ch.observe(to_mont(w));
+        const uint32_t bits = ch.sample_bits((int)pk.cfg.pow_bits);
+        ARG_CHECK(bits == 0, "proof-of-work witness check failed");
+    }
+
+    // ---- queries: gather rows and Merkle paths ----
+    const uint32_t nq = pk.cfg.num_queries;
+    std::vector<uint64_t> idx(nq);
+    for (uint32_t q = 0; q < nq; q++) idx[q] = ch.sample_bits(log_max);
+    std::vector<uint64_t> items;  // (src, stride | count << 32, dst)
+    uint64_t total = 0;
+    auto item = [&](const uint32_t *src, uint64_t stride, uint64_t count) {
+        items.push_back((uint64_t)(uintptr_t)src);
+        items.push_back(stride | (count << 32));
+        items.push_back(total);
+        total += count;
+    };
+    for (uint32_t q = 0; q < nq; q++) {
+        for (int t = 0; t < 4; t++) {
+            const DTree *tt = trees[t];
+            const uint64_t ri = idx[q] >> (log_max - tt->log_max);
+            for (auto &mm : tt->mats) {
+                const uint64_t row = ri >> (tt->log_max - ilog2(mm.height));
+                if (mm.width) item(mm.d + row, mm.height, mm.width);
+            }
+            for (int l = 0; l < tt->log_max; l++) item(tt->layers[l].p + ((ri >> l) ^ 1) * 8, 1, 8);
+        }
+        for (int rd = 0; rd < nrounds; rd++) {
+            const uint64_t ii = idx[q] >> rd, pair = ii >> 1;
+            item(ftrees[rd].owned.back().p + 8 * pair + 4 * ((ii ^ 1) & 1), 1, 4);
+            for (int l = 0; l < ftrees[rd].log_max; l++) item(ftrees[rd].layers[l].p + ((pair >> l) ^ 1) * 8, 1, 8);
+        }
+    }
+    DBuf ditems(items.size() * 2 + 2, s), dout(total + 1, s);
+    HIP_CHECK(hipMemcpyAsync(ditems.p, items.data(), items.size() * 8, hipMemcpyHostToDevice, s));
+    launch_gather((const uint64_t *)ditems.p, (uint32_t)(items.size() / 3), dout.p, s);
+    std::vector<uint32_t> g(total + 1);
+    HIP_CHECK(hipMemcpyAsync(g.data(), dout.p, total * 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    uint64_t off = 0;
+    proof.queries.resize(nq);
+    for (uint32_t q = 0; q < nq; q++) {
+        Query &Q = proof.queries[q];
+        for (int t = 0; t < 4; t++) {
+            const DTree *tt = trees[t];
+            BatchOpen bo;
+            for (auto &mm : tt->mats) {
+                bo.vals.emplace_back(g.begin() + off, g.begin() + off + mm.width);
+                off += mm.width;
+            }
+            for (int l = 0; l < tt->log_max; l++) { bo.path.push_back(dig(&g[off])); off += 8; }
+            Q.input.push_back(std::move(bo));
+        }
+        for (int rd = 0; rd < nrounds; rd++) {
+            Step st;
+            st.sib = ef{{g[off], g[off + 1], g[off + 2], g[off + 3]}};
+            off += 4;
+            for (int l = 0; l < ftrees[rd].log_max; l++) { st.path.push_back(dig(&g[off])); off += 8; }
+            Q.steps.push_back(std::move(st));
+        }
+    }
+
+    // ---- opened values into the proof (prover.rs:558-640) ----
+    for (int i = 0; i < n; i++) {
+        ChipOpen &co = proof.chips[i];
+        const int pki = pk.pk_index(md.chip[i]);
+        const int pw_ = m.chips[md.chip[i]].prep_w;
+        if (pki >= 0) {
+            const OpenReq &r = req[pki];
+            co.prep_l = r.vals[0];
+            co.prep_n = r.npts == 2 ? r.vals[1] : std::vector<ef>(pw_, ef_zero());
+        }
+        const OpenReq &mr = req[pk.trace_chip.size() + i];
+        co.main_l = mr.vals[0];
+        co.main_n = mr.npts == 2 ? mr.vals[1] : std::vector<ef>(mr.vals[0].size(), ef_zero());
+        const OpenReq &pr = req[pk.trace_chip.size() + n + i];
+        co.perm_l = pr.vals[0];
+        co.perm_n = pr.vals[1];
+    }
+    {
+        size_t qi = pk.trace_chip.size() + 2 * n;
+        for (int i = 0; i < n; i++) {
+            const int nq_ = 1 << m.chips[md.chip[i]].log_qd;
+            for (int j = 0; j < nq_; j++, qi++)
+                for (int e = 0; e < 4; e++) proof.chips[i].quot.push_back(req[qi].vals[0][e]);
+        }
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (!final_ok) throw std::runtime_error("UNSATISFIED: FRI final polynomial is not constant");
+    return serialize(proof, pk.cfg.proof_montgomery != 0);
+}
+
+}  // namespace zkm
+
+using namespace zkm;
+
+static int status_of(const std::exception &e) {
+    (void)hipDeviceSynchronize();  // no buffer is released while kernels that use it are in flight
+    std::string w = e.what();
+    if (w.rfind("UNSATISFIED", 0) == 0) { g_last_error = w; return ZKM_ERR_UNSATISFIED; }
+    if (w.find("not supported") != std::string::npos) { g_last_error = w; return ZKM_ERR_UNSUPPORTED; }
+    return guard_status(e);
+}
+#define GUARD_BEGIN try {
+#define GUARD_END                         \
+    }                                     \
+    catch (const std::exception &e) {     \
+        return status_of(e);              \
+    }
+
+extern "C" {
+
+int zkm_setup(zkm_ctx *ctx, const uint32_t *blob, size_t nwords, const zkm_config_t *cfg, const zkm_matrix_t *prep,
+              uint32_t nprep, uint32_t pc_start, const uint32_t gcs[14], zkm_pk **pk_out, uint32_t commit_out[8]) {
+    GUARD_BEGIN
+    ARG_CHECK(ctx && blob && cfg && pk_out && commit_out && gcs, "null argument");
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    HIP_CHECK(hipSetDevice(c->device));
+    ARG_CHECK(cfg->log_blowup == 1, "only log_blowup = 1 is supported");
+    ARG_CHECK(cfg->pow_bits < 31, "pow_bits");
+    auto pk = std::make_unique<Pk>();
+    pk->device = c->device;
+    pk->m = parse_machine(blob, nwords);
+    pk->cfg = *cfg;
+    pk->pc_start = to_mont(pc_start);
+    for (int k = 0; k < 14; k++) pk->gcs[k] = to_mont(gcs[k]);
+    ARG_CHECK(nprep == pk->m.chips.size(), "one preprocessed matrix slot per machine chip");
+    StreamLease L(c);
+    for (auto &cd : pk->m.chips) {
+        std::vector<uint32_t> f = flatten_chip(cd);
+        pk->progs.emplace_back(f.size(), L.s);
+        HIP_CHECK(hipMemcpyAsync(pk->progs.back().p, f.data(), f.size() * 4, hipMemcpyHostToDevice, L.s));
+        HIP_CHECK(hipStreamSynchronize(L.s));
+    }
+    // preprocessed traces sorted by (height desc, name) (machine.rs:383-384)
+    std::vector<int> chips;
+    std::vector<uint64_t> hs;
+    std::vector<std::string> names;
+    for (size_t i = 0; i < pk->m.chips.size(); i++) {
+        if (pk->m.chips[i].prep_w == 0) continue;
+        ARG_CHECK(prep[i].data && prep[i].width == (uint64_t)pk->m.chips[i].prep_w, "preprocessed trace shape");
+        chips.push_back((int)i);
+        hs.push_back(prep[i].height);
+        names.push_back(pk->m.chips[i].name);
+    }
+    ARG_CHECK(!chips.empty(), "machine has no preprocessed trace (MerkleTree of an empty batch)");
+    for (int o : sort_order(hs, names)) {
+        const int ci = chips[o];
+        ARG_CHECK((prep[ci].height & (prep[ci].height - 1)) == 0, "heights must be powers of two");
+        pk->trace_chip.push_back(ci);
+        pk->heights.push_back(prep[ci].height);
+        pk->traces.push_back(upload_matrix(prep[ci], L.s));
+        DMat src{pk->traces.back().p, prep[ci].height, prep[ci].width};
+        add_lde(*c, pk->tree, src, to_mont(GENERATOR), false, L.s);
+    }
+    tree_build(pk->tree, L.s);
+    memcpy(pk->commit, pk->tree.root, 32);
+    for (int k = 0; k < 8; k++) commit_out[k] = from_mont(pk->commit[k]);
+    *pk_out = reinterpret_cast<zkm_pk *>(pk.release());
+    return ZKM_OK;
+    GUARD_END
+}
+
+void zkm_pk_free(zkm_pk *p) {
+    if (!p) return;
+    Pk *pk = reinterpret_cast<Pk *>(p);
+    (void)hipSetDevice(pk->device);
+    (void)hipDeviceSynchronize();
+    delete pk;
+}
+
+int zkm_pk_observe(const zkm_pk *p, zkm_challenger_t *c) {
+    GUARD_BEGIN
+    ARG_CHECK(p && c, "null argument");
+    const Pk *pk = reinterpret_cast<const Pk *>(p);
+    Challenger ch;
+    ch.load(*c);
+    ch.observe(pk->commit, 8);
+    ch.observe(pk->pc_start);
+    ch.observe(pk->gcs, 14);
+    ch.observe(0u);
+    ch.store(*c);
+    return ZKM_OK;
+    GUARD_END
+}
+
+int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32_t ntraces, const uint32_t *pv,
+               uint32_t npv, zkm_main **out, uint32_t commit_out[8]) {
+    GUARD_BEGIN
+    ARG_CHECK(ctx && p && traces && ntraces && out && commit_out && (pv || !npv), "null argument");
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    const Pk *pk = reinterpret_cast<const Pk *>(p);
+    HIP_CHECK(hipSetDevice(c->device));
+    StreamLease L(c);
+    auto md = std::make_unique<MainData>();
+    std::vector<uint64_t> hs;
+    std::vector<std::string> names;
+    std::vector<int> chip;
+    for (uint32_t i = 0; i < ntraces; i++) {
+        ARG_CHECK(traces[i].name, "trace without a chip name");
+        const int ci = pk->m.index_of(traces[i].name);
+        ARG_CHECK(ci >= 0, std::string("unknown chip ") + traces[i].name);
+        ARG_CHECK(traces[i].width == (uint64_t)pk->m.chips[ci].main_w, "main trace width mismatch");
+        ARG_CHECK(traces[i].height >= 16 && (traces[i].height & (traces[i].height - 1)) == 0,
+                  "trace heights must be powers of two >= 16");
+        hs.push_back(traces[i].height);
+        names.push_back(traces[i].name);
+        chip.push_back(ci);
+    }
+    for (int o : sort_order(hs, names)) {  // prover.rs:264
+        md->chip.push_back(chip[o]);
+        md->heights.push_back(hs[o]);
+        md->traces.push_back(upload_matrix(traces[o], L.s));
+        DMat src{md->traces.back().p, traces[o].height, traces[o].width};
+        add_lde(*c, md->tree, src, to_mont(GENERATOR), false, L.s);
+    }
+    tree_build(md->tree, L.s);
+    md->pv.assign(pv, pv + npv);
+    for (int k = 0; k < 8; k++) commit_out[k] = from_mont(md->tree.root[k]);
+    *out = reinterpret_cast<zkm_main *>(md.release());
+    return ZKM_OK;
+    GUARD_END
+}
+
+void zkm_main_free(zkm_main *m) {
+    if (!m) return;
+    delete reinterpret_cast<MainData *>(m);
+}
+
+int zkm_open(zkm_ctx *ctx, const zkm_pk *p, zkm_main *mainp, zkm_challenger_t *chs, uint8_t **proof_out,
+             uint64_t *proof_len) {
+    std::unique_ptr<MainData> md(reinterpret_cast<MainData *>(mainp));
+    GUARD_BEGIN
+    ARG_CHECK(ctx && p && mainp && chs && proof_out && proof_len, "null argument");
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    const Pk *pk = reinterpret_cast<const Pk *>(p);
+    HIP_CHECK(hipSetDevice(c->device));
+    StreamLease L(c);
+    Challenger ch;
+    ch.load(*chs);
+    std::vector<uint8_t> bytes = open_shard(*c, *pk, *md, ch, L.s);
+    HIP_CHECK(hipStreamSynchronize(L.s));
+    ch.store(*chs);
+    uint8_t *buf = (uint8_t *)malloc(bytes.size());
+    ARG_CHECK(buf, "out of host memory");
+    memcpy(buf, bytes.data(), bytes.size());
+    *proof_out = buf;
+    *proof_len = bytes.size();
+    md.reset();
+    return ZKM_OK;
+    GUARD_END
+}
+
+int zkm_prove_shard(zkm_ctx *ctx, const zkm_pk *pk, const zkm_matrix_t *traces, uint32_t ntraces, const uint32_t *pv,
+                    uint32_t npv, const zkm_challenger_t *base, uint8_t **proof_out, uint64_t *proof_len) {
+    if (!base) { g_last_error = "null challenger"; return ZKM_ERR_ARG; }
+    zkm_main *md = nullptr;
+    uint32_t root[8];
+    int rc = zkm_commit(ctx, pk, traces, ntraces, pv, npv, &md, root);
+    if (rc) return rc;
+    zkm_challenger_t ch = *base;
+    return zkm_open(ctx, pk, md, &ch, proof_out, proof_len);
+}
+
+}  // extern "C"
