@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark: shard trace rows proved per second (BASELINE.json `metric`).
+
+Workload (N = 1 unless --gpus): the S-SHARD synthetic shard of SURVEY.md §8d at 2^22 rows —
+FibCpu (main 67 columns, 20 local lookups -> 11 EF LogUp columns, quotient degree 2, shaped like
+the reference's Cpu chip) plus the preprocessed FibTable chip — proven end to end exactly as the
+reference's CpuProver::commit + CpuProver::open would (LDE, Poseidon2 MMCS, LogUp trace, quotient,
+openings, FRI with 84 queries and 16 PoW bits).  One step = one shard proof with the traces
+already resident in HBM; for N > 1 every rank proves its own shard (shards are independent,
+prove.rs:208-209) and the proof bytes are gathered over RCCL inside the timed region.
+
+Also reported: the roofline of the dominant stage (HIP events on the launching stream over the
+timed region), the PCIe-inclusive rate (host traces), and the CPU oracle on a bounded sample.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse_profile(text):
+    out = {}
+    for line in text.strip().splitlines():
+        name, cnt, ms, units = line.split()
+        out[name] = (int(cnt), float(ms), float(units))
+    return out
+
+
+def device_matrix(tensor, name, keep):
+    from zkmips_amd._lib import Matrix, ZKM_REPR_CANONICAL
+    nm = name.encode()
+    keep.append(nm)
+    return Matrix(nm, tensor.data_ptr(), tensor.shape[0], tensor.shape[1], ZKM_REPR_CANONICAL | 0x100)
+
+
+def prove_resident(prover, dev_traces, pvs):
+    """zkm_prove_shard over device-resident row-major traces (ZKM_MEM_DEVICE)."""
+    from zkmips_amd._lib import Matrix, check, lib
+    keep = []
+    arr = (Matrix * len(dev_traces))(*[device_matrix(t, n, keep) for n, t in dev_traces.items()])
+    base = prover.base_challenger()
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_uint64()
+    check(lib().zkm_prove_shard(prover.dev.h, prover.pk, arr, len(dev_traces), pvs.ctypes.data, pvs.size,
+                                C.byref(base), C.byref(out), C.byref(n)), "zkm_prove_shard")
+    b = C.string_at(out, n.value)
+    lib().zkm_free_bytes(out)
+    return b
+
+
+STAGE_KERNEL = {"merkle_leaves": "k_hash_leaves", "merkle_nodes": "k_compress_level", "quotient": "k_quotient",
+                "fri_reduce": "k_fri_reduce", "perm_trace": "k_perm_rows", "open_eval": "k_open_dot"}
+
+
+def pmc_traffic(stage):
+    """HBM bytes per launch of the stage's kernel from the newest committed rocprofv3 PMC summary
+    (profiles/rNN_pmc_summary.json: 2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction, tools/pmc_summary.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    k = STAGE_KERNEL.get(stage)
+    if not files or not k:
+        return None, None
+    d = json.load(open(files[-1]))["kernels"].get(k, {})
+    if "hbm_bytes_per_launch" not in d:
+        return None, None
+    return round(d["hbm_bytes_per_launch"]), os.path.basename(files[-1])
+
+
+def cpu_baseline(log_n, queries):
+    """The CPU oracle (a C/OpenMP restatement, not the reference binary) on one bounded shard."""
+    from tests import _oracle as O
+    from zkmips_amd import workloads as W
+    n = 1 << log_n
+    m, prep, traces, pvs = W.fib_shard(n, seed=1)
+    pr = O.OracleProver(m, prep, num_queries=queries)
+    t0 = time.time()
+    rc, proof = pr.prove(traces, pvs)
+    dt = time.time() - t0
+    assert rc == 0
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": n / dt, "unit": "rows/s", "cores": cores, "kind": "port",
+            "sample": f"one S-SHARD FibCpu 2^{log_n}-row shard (+FibTable), full commit+open, {queries} queries, "
+                      f"{dt:.2f} s wall on {cores} OpenMP threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--log-n", type=int, default=22)
+    ap.add_argument("--queries", type=int, default=84)
+    ap.add_argument("--cpu-log-n", type=int, default=18)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-out", default="")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from zkmips_amd import workloads as W
+    from zkmips_amd._lib import Device, lib
+    from zkmips_amd.prover import HipProver
+
+    n = 1 << args.log_n
+    m, prep, traces, pvs = W.fib_shard(n, seed=1000 + rank)
+    dev = Device(local_rank)
+    prover = HipProver(dev, m, prep, num_queries=args.queries)
+    dev_traces = {k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in traces.items()}
+    torch.cuda.synchronize()
+    rows_per_shard = max(v.shape[0] for v in traces.values())
+
+    def gather(proof):
+        """MachineProof aggregation: all ranks' shard proofs over RCCL (zkmips_amd/dist.py)."""
+        if world == 1:
+            return {0: proof}
+        from zkmips_amd.dist import gather_proofs
+        return gather_proofs({rank: proof}, device="cuda")
+
+    for _ in range(args.warmup):
+        gather(prove_resident(prover, dev_traces, pvs))
+
+    lib().zkm_profile_reset()
+    lib().zkm_profile_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    proof = b""
+    for _ in range(args.steps):
+        proof = prove_resident(prover, dev_traces, pvs)
+        gather(proof)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    lib().zkm_profile_enable(0)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    need = lib().zkm_profile_dump(None, 0)
+    buf = C.create_string_buffer(need)
+    lib().zkm_profile_dump(buf, need)
+    prof = parse_profile(buf.value.decode())
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # PCIe-inclusive rate (host traces, same prover): one extra untimed-by-value pass
+    tp = time.perf_counter()
+    prover.prove_shard(traces, pvs)
+    pcie_s = time.perf_counter() - tp
+
+    kernel_stages = ["lde", "merkle_leaves", "merkle_nodes", "quotient", "perm_trace", "open_eval", "fri_reduce"]
+    dom = max((s for s in kernel_stages if s in prof), key=lambda s: prof[s][1])
+    cnt, ms, units = prof[dom]
+    achieved = units / (ms / 1e3) / 1e9  # GB/s, algorithmic bytes / measured stage time
+    traffic, tsrc = pmc_traffic(dom)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
+                "launches": cnt, "avg_ms": round(ms / cnt, 4),
+                "algorithmic_bytes_per_launch": round(units / cnt), "traffic_source": tsrc}
+    stages = {k: {"count": v[0], "ms_per_step": round(v[1] / args.steps, 3)} for k, v in sorted(prof.items())}
+
+    value = world * rows_per_shard * args.steps / elapsed
+    line = {
+        "metric": "shard trace rows proved/sec at 2^22 rows",
+        "value": round(value, 1),
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
+        "data": "synthetic (seeded S-SHARD traces, SURVEY.md §8d)",
+        "config": {"workload": f"S-SHARD FibCpu 2^{args.log_n} rows (main 67, LogUp 11 EF, quotient 2) + FibTable "
+                               f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard",
+                   "rows_per_shard": rows_per_shard, "fri_queries": args.queries, "pow_bits": 16, "log_blowup": 1,
+                   "shards_per_gpu_per_step": 1, "parallelism": f"shard-parallel x{world}",
+                   "proof_bytes": len(proof)},
+        "pcie_inclusive_rows_per_s": round(rows_per_shard / pcie_s, 1),
+        "roofline": roofline,
+        "stages_ms_per_step": stages,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_log_n, args.queries)
+    if args.profile_out:
+        with open(args.profile_out, "w") as f:
+            f.write(buf.value.decode())
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

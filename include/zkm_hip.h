@@ -37,6 +37,8 @@ extern "C" {
 
 #define ZKM_REPR_CANONICAL 0u
 #define ZKM_REPR_MONTGOMERY 1u
+#define ZKM_MEM_DEVICE 0x100u  /* OR into zkm_matrix_t.repr: `data` is a row-major buffer already
+                                  resident in the context GPU's memory (e.g. a torch tensor) */
 
 typedef struct zkm_ctx zkm_ctx;   /* one per GPU: device, stream pool, twiddle tables */
 typedef struct zkm_pk zkm_pk;     /* DeviceProvingKey   (prover.rs:40, machine.rs:55-75)   */
@@ -66,7 +68,7 @@ typedef struct {
     const uint32_t *data;   /* height * width values, row-major */
     uint64_t height;        /* power of two, >= 16 for traces */
     uint64_t width;
-    uint32_t repr;          /* ZKM_REPR_CANONICAL or ZKM_REPR_MONTGOMERY */
+    uint32_t repr;          /* ZKM_REPR_CANONICAL or ZKM_REPR_MONTGOMERY, | ZKM_MEM_DEVICE */
 } zkm_matrix_t;
 
 /* ---- context ---- */
@@ -120,6 +122,12 @@ int zkm_poseidon2_permute(zkm_ctx *ctx, uint32_t *states, uint64_t n);
 /* Timing helper: runs `iters` LDEs of a resident random h x w matrix, returns average ms of the
  * whole LDE and of each kernel stage via HIP events (see bench.py). */
 int zkm_bench_lde(zkm_ctx *ctx, uint64_t h, uint64_t w, int iters, double *ms_out);
+
+/* ---- stage profiling (HIP events on the launching stream; see bench.py) ----
+ * zkm_profile_dump writes lines "stage count total_ms units" and returns the bytes needed. */
+void zkm_profile_enable(int on);
+void zkm_profile_reset(void);
+size_t zkm_profile_dump(char *buf, size_t len);
 
 /*
  * Machine blob (u32 words), produced by zkmips_amd/machine.py:

@@ -40,11 +40,14 @@ DBuf upload_matrix(const zkm_matrix_t &m, hipStream_t s) {
     ARG_CHECK(m.data || m.height * m.width == 0, "matrix data is NULL");
     const uint64_t n = m.height * m.width;
     DBuf col(n ? n : 1, s);
-    if (n) {
+    const bool mont = (m.repr & 0xffu) == ZKM_REPR_MONTGOMERY;
+    if (n && (m.repr & ZKM_MEM_DEVICE)) {
+        launch_to_col_major(m.data, m.height, m.width, mont, col.p, s);
+    } else if (n) {
         DBuf raw(n, s);
         HIP_CHECK(hipMemcpyAsync(raw.p, m.data, n * 4, hipMemcpyHostToDevice, s));
-        launch_to_col_major(raw.p, m.height, m.width, m.repr == ZKM_REPR_MONTGOMERY, col.p, s);
-        HIP_CHECK(hipStreamSynchronize(s));  // raw freed on scope exit (stream-ordered anyway)
+        launch_to_col_major(raw.p, m.height, m.width, mont, col.p, s);
+        HIP_CHECK(hipStreamSynchronize(s));  // pageable source must stay valid until copied
     }
     return col;
 }

@@ -13,6 +13,7 @@
 #include "internal.hpp"
 #include "open_kernels.hpp"
 #include "p2.cuh"
+#include "prof.hpp"
 
 namespace zkm {
 
@@ -108,9 +109,13 @@ void tree_build(DTree &t, hipStream_t s) {
     colbufs.push_back(upload_cols(grp, keep[0], s));
     int ncols = (int)keep[0].size();
     t.layers[0] = DBuf(maxh * 8, s);
+    {
+    PROF("merkle_leaves", s, 4.0 * maxh * ncols + 32.0 * maxh);  // algorithmic bytes
     hipLaunchKernelGGL(k_hash_leaves, dim3((unsigned)((maxh + NT - 1) / NT)), dim3(NT), 0, s,
                        (const uint64_t *)colbufs.back().p, ncols, maxh, t.layers[0].p);
     HIP_CHECK(hipGetLastError());
+    }
+    PROF("merkle_nodes", s, 96.0 * maxh);
     uint64_t h = maxh;
     for (int L = 1; L <= t.log_max; L++) {
         h >>= 1;

@@ -14,6 +14,7 @@
 // Passes: the lowest <= 12 bits in one contiguous LDS tile (4096 elements), the remaining bits
 // in strided passes of <= 6 bits over 64-column-wide tiles (256 B coalesced rows).
 #include "internal.hpp"
+#include "prof.hpp"
 
 namespace zkm {
 
@@ -323,6 +324,7 @@ static DBuf make_twist(uint64_t N, int L, uint32_t shift, Twist &tws, hipStream_
 void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s) {
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
+    PROF("lde", s, 12.0 * N * W);
     const int L = ilog2(N);
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
@@ -358,6 +360,7 @@ void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hip
 void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s) {
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
+    PROF("lde", s, 12.0 * N * W);
     const int L = ilog2(N);
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");

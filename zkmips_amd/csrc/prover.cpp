@@ -18,6 +18,7 @@
 #include "internal.hpp"
 #include "open_kernels.hpp"
 #include "p2.cuh"
+#include "prof.hpp"
 
 namespace zkm {
 
@@ -238,6 +239,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     ch.observe(md.tree.root, 8);
     const ef perm_alpha = ch.sample_ef(), perm_beta = ch.sample_ef();
 
+    PROF("open_total", s, 0);
     // ---- permutation traces (prover.rs:337-365) ----
     proof.chips.resize(n);
     std::vector<DBuf> perm_traces(n);
@@ -256,7 +258,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             DBuf rowsum(4 * N, s);
             PermArgs a{pk.progs[md.chip[i]].p, md.traces[i].p, pki >= 0 ? pk.traces[pki].p : nullptr, N, perm_alpha,
                        perm_beta, 1 << cd.log_qd, pw - 1, perm_traces[i].p, rowsum.p};
-            launch_perm_trace(a, s);
+            { PROF("perm_trace", s, 4.0 * N * (cd.main_w + cd.prep_w) + 16.0 * N * (pw + 2)); launch_perm_trace(a, s); }
             uint32_t l[4];
             for (int e = 0; e < 4; e++)
                 HIP_CHECK(hipMemcpyAsync(&l[e], perm_traces[i].p + (uint64_t)(4 * (pw - 1) + e) * N + N - 1, 4,
@@ -325,7 +327,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         memcpy(qa.gcs, proof.chips[i].gcs, sizeof qa.gcs);
         qa.batch = 1 << lqd; qa.perm_w = cd.perm_w; qa.global = cd.scope == 1; qa.main_w = cd.main_w;
         qa.chunks = q_chunks[i].p;
-        launch_quotient(qa, s);
+        { PROF("quotient", s, 8.0 * Q * (cd.main_w + cd.prep_w + 4 * cd.perm_w) + 16.0 * Q); launch_quotient(qa, s); }
         HIP_CHECK(hipStreamSynchronize(s));  // d_pows lifetime
         const uint32_t wq = two_adic_gen(logN + lqd);
         for (int j = 0; j < (1 << lqd); j++) {
@@ -404,6 +406,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), W * 8, hipMemcpyHostToDevice, s));
             DBuf part(W * nseg * 8, s);
             const bool with_next = r.npts == 2;
+            PROF("open_eval", s, 4.0 * N * W + 16.0 * N);
             launch_open_dot((const uint64_t *)dcols.p, (uint32_t)W, N, w, with_next, nseg, part.p, s);
             std::vector<uint32_t> hp(W * nseg * 8);
             HIP_CHECK(hipMemcpyAsync(hp.data(), part.p, hp.size() * 4, hipMemcpyDeviceToHost, s));
@@ -489,7 +492,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             HIP_CHECK(hipMemcpyAsync(ddesc.p, desc.data(), desc.size() * 4, hipMemcpyHostToDevice, s));
             ReduceArgs ra{(const uint64_t *)dcols.p, ddesc.p, (uint32_t)by_h[lh].size(), d_apow.p, inv0.p,
                           need1 ? inv1.p : nullptr, ro[lh].p, H};
-            launch_fri_reduce(ra, s);
+            { PROF("fri_reduce", s, 4.0 * H * cols.size() + 16.0 * H * (need1 ? 4 : 3)); launch_fri_reduce(ra, s); }
             HIP_CHECK(hipStreamSynchronize(s));  // host vectors / temporaries
         }
     }
@@ -504,6 +507,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         HIP_CHECK(hipMemcpyAsync(cur.p, ro[log_max].p, 16 * cur_n, hipMemcpyDeviceToDevice, s));
     }
     const uint32_t half = halve(ONE);
+    PROF("fri_commit_phase", s, 0);
     for (int rd = 0; rd < nrounds; rd++) {
         const int lf = log_max - 1 - rd;
         const uint64_t h = cur_n >> 1;
@@ -538,6 +542,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         memcpy(pa.in, ch.in, 32);
         pa.nin = (uint32_t)ch.nin;
         pa.mask = (1u << pk.cfg.pow_bits) - 1u;
+        PROF("pow", s, 0);
         const uint32_t w = pk.cfg.pow_bits ? run_pow(pa, s) : 0u;
         proof.pow = to_mont(w);
         ch.observe(to_mont(w));
@@ -749,6 +754,7 @@ int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32
         names.push_back(traces[i].name);
         chip.push_back(ci);
     }
+    PROF("commit_total", L.s, 0);
     for (int o : sort_order(hs, names)) {  // prover.rs:264
         md->chip.push_back(chip[o]);
         md->heights.push_back(hs[o]);

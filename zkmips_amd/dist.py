@@ -1,0 +1,69 @@
+"""Multi-GPU shard proving: one process per GPU, shards partitioned across ranks.
+
+The reference proves all shards of a batch in parallel and independently: each shard opens on a
+clone of a challenger that has only observed the proving key (crates/core/machine/src/utils/
+prove.rs:208-209, :487-521; verifier mirrors it, crates/stark/src/machine.rs:620-624).  So the data
+path needs no collective: shards are dealt round-robin to ranks and proved locally.  The only
+exchange is the aggregation of finished proofs (KB-MB each) to build the MachineProof in shard
+order — done with one all_gather over the process group (RCCL over xGMI with backend "nccl",
+gloo on CPU for tests).
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Sequence
+
+
+def assign_shards(num_shards: int, world: int, rank: int) -> List[int]:
+    """Round-robin shard indices for `rank` (shard i -> rank i % world)."""
+    return [i for i in range(num_shards) if i % world == rank]
+
+
+def _encode(local: Dict[int, bytes]) -> bytes:
+    out = bytearray(len(local).to_bytes(8, "little"))
+    for idx in sorted(local):
+        b = local[idx]
+        out += idx.to_bytes(8, "little") + len(b).to_bytes(8, "little") + b
+    return bytes(out)
+
+
+def _decode(buf: bytes) -> Dict[int, bytes]:
+    n = int.from_bytes(buf[:8], "little")
+    pos, res = 8, {}
+    for _ in range(n):
+        idx = int.from_bytes(buf[pos:pos + 8], "little")
+        ln = int.from_bytes(buf[pos + 8:pos + 16], "little")
+        res[idx] = bytes(buf[pos + 16:pos + 16 + ln])
+        pos += 16 + ln
+    return res
+
+
+def gather_proofs(local: Dict[int, bytes], device="cpu") -> Dict[int, bytes]:
+    """All-gather every rank's {shard index: proof bytes}; returns the union on every rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    payload = _encode(local)
+    ln = torch.tensor([len(payload)], dtype=torch.int64, device=device)
+    dist.all_reduce(ln, op=dist.ReduceOp.MAX)
+    size = int(ln.item())
+    buf = torch.zeros(size + 8, dtype=torch.uint8, device=device)
+    buf[:8] = torch.tensor(list(len(payload).to_bytes(8, "little")), dtype=torch.uint8, device=device)
+    if payload:
+        buf[8:8 + len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    out: Dict[int, bytes] = {}
+    for p in parts:
+        raw = p.cpu().numpy().tobytes()
+        n = int.from_bytes(raw[:8], "little")
+        out.update(_decode(raw[8:8 + n]))
+    return out
+
+
+def prove_shards_distributed(prove_one: Callable[[int], bytes], num_shards: int, device="cpu") -> List[bytes]:
+    """MachineProver::prove across ranks: each rank proves its shards, proofs come back in shard order."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    local = {i: prove_one(i) for i in assign_shards(num_shards, world, rank)}
+    allp = gather_proofs(local, device)
+    return [allp[i] for i in range(num_shards)]
