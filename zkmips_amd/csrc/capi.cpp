@@ -87,6 +87,12 @@ int zkm_init(int device, zkm_ctx **out) {
         return ZKM_ERR_NO_DEVICE;
     }
     HIP_CHECK(hipSetDevice(device));
+    // Keep freed stream-ordered memory in the pool: the default release threshold (0) hands
+    // gigabytes back to the driver at every synchronisation and re-maps them for the next shard.
+    hipMemPool_t pool;
+    HIP_CHECK(hipDeviceGetDefaultMemPool(&pool, device));
+    uint64_t thr = ~0ull;
+    HIP_CHECK(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr));
     auto *c = new Ctx();
     c->device = device;
     build_twiddles(*c, 24);  // transforms up to 2^24 (two-adicity)

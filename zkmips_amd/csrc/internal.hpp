@@ -76,12 +76,15 @@ struct DTree {
     std::vector<DMat> mats;        // commit order
     std::vector<DBuf> owned;       // storage of mats (if owned)
     int log_max = 0;
-    std::vector<DBuf> layers;      // layers[i]: (max_h >> i) digests x 8 words, digest-major
+    std::vector<uint32_t *> layers;  // layers[i]: (max_h >> i) digests x 8 words, digest-major
+    std::vector<DBuf> layer_store;   // storage behind `layers`
     uint32_t root[8];              // Montgomery
 };
 
 struct Ctx {
     int device = 0;
+    // cached per (log n, shift): LDE twist tables (lo[4096] | hi[n/4096]) x 2 cosets
+    std::vector<std::pair<std::pair<int, uint32_t>, DBuf>> twists;
     int tw_log = 0;                 // twiddle tables cover transforms up to 2^tw_log
     uint32_t *tw_fwd = nullptr;     // tw[h + j] = w_{2h}^j  (Montgomery), size 2^tw_log
     uint32_t *tw_inv = nullptr;

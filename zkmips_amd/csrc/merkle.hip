@@ -81,6 +81,35 @@ void launch_poseidon2_batch(uint32_t *d, uint64_t n, hipStream_t s) {
     HIP_CHECK(hipGetLastError());
 }
 
+static constexpr int NT_TOP = 256;
+static constexpr uint64_t TOP_MAX = 256;  // levels with <= TOP_MAX nodes are built by one workgroup
+static_assert(TOP_MAX <= NT_TOP, "one node per thread per level");
+
+// Builds `nlev` levels above `prev` (2*h1 digests) in one workgroup: level k has h1 >> k nodes and
+// is written contiguously to out (level 0 first).  Intermediate levels also live in LDS.
+__global__ __launch_bounds__(NT_TOP) void k_tree_top(const uint32_t *__restrict__ prev, uint64_t h1, int nlev,
+                                                     uint32_t *__restrict__ out) {
+    __shared__ uint32_t cur[TOP_MAX * 8];
+    uint64_t h = h1, off = 0;
+    for (int lev = 0; lev < nlev; lev++, h >>= 1) {
+        uint32_t res[8];
+        for (uint64_t i = threadIdx.x; i < h; i += NT_TOP) {
+            uint32_t s[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) s[k] = lev == 0 ? prev[i * 16 + k] : cur[i * 16 + k];
+            p2::permute(s);
+#pragma unroll
+            for (int k = 0; k < 8; k++) { res[k] = s[k]; out[(off + i) * 8 + k] = s[k]; }
+        }
+        __syncthreads();
+        for (uint64_t i = threadIdx.x; i < h; i += NT_TOP)
+#pragma unroll
+            for (int k = 0; k < 8; k++) cur[i * 8 + k] = res[k];
+        __syncthreads();
+        off += h;
+    }
+}
+
 static DBuf upload_cols(const std::vector<const DMat *> &group, std::vector<uint64_t> &host, hipStream_t s) {
     host.clear();
     for (const DMat *m : group)
@@ -88,6 +117,34 @@ static DBuf upload_cols(const std::vector<const DMat *> &group, std::vector<uint
     DBuf d(host.size() * 2 + 2, s);
     if (!host.empty()) HIP_CHECK(hipMemcpyAsync(d.p, host.data(), host.size() * 8, hipMemcpyHostToDevice, s));
     return d;
+}
+
+// Levels 1..log_max above layers[0]; inj[L] = column table of matrices injected at level L.
+static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<const DBuf *, int>> &inj, hipStream_t s) {
+    uint64_t h = maxh;
+    for (int L = 1; L <= t.log_max; L++) {
+        h >>= 1;
+        bool later_inj = false;
+        for (int k = L; k <= t.log_max; k++) later_inj |= inj[k].second != 0;
+        if (h <= TOP_MAX && !later_inj) {
+            // remaining levels L..log_max in one workgroup, one contiguous allocation
+            const int nlev = t.log_max - L + 1;
+            t.layer_store.emplace_back(2 * h * 8, s);
+            uint32_t *base = t.layer_store.back().p;
+            uint64_t off = 0, hh = h;
+            for (int k = L; k <= t.log_max; k++, hh >>= 1) { t.layers[k] = base + off * 8; off += hh; }
+            hipLaunchKernelGGL(k_tree_top, dim3(1), dim3(NT_TOP), 0, s, (const uint32_t *)t.layers[L - 1], h, nlev, base);
+            HIP_CHECK(hipGetLastError());
+            break;
+        }
+        t.layer_store.emplace_back(h * 8, s);
+        t.layers[L] = t.layer_store.back().p;
+        const int ninj = inj[L].second;
+        hipLaunchKernelGGL(k_compress_level, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
+                           (const uint32_t *)t.layers[L - 1], t.layers[L], h,
+                           inj[L].first ? (const uint64_t *)inj[L].first->p : (const uint64_t *)nullptr, ninj);
+        HIP_CHECK(hipGetLastError());
+    }
 }
 
 void tree_build(DTree &t, hipStream_t s) {
@@ -99,58 +156,54 @@ void tree_build(DTree &t, hipStream_t s) {
     const uint64_t maxh = t.mats[order[0]].height;
     ARG_CHECK((maxh & (maxh - 1)) == 0, "matrix heights must be powers of two");
     t.log_max = ilog2(maxh);
-    t.layers.clear();
-    t.layers.resize(t.log_max + 1);
+    t.layers.assign(t.log_max + 1, nullptr);
+    t.layer_store.clear();
     std::vector<std::vector<uint64_t>> keep(t.log_max + 2);
     std::vector<DBuf> colbufs;
+    colbufs.reserve(t.log_max + 2);
+    std::vector<std::pair<const DBuf *, int>> inj(t.log_max + 1, {nullptr, 0});
     size_t pos = 0;
     std::vector<const DMat *> grp;
     while (pos < order.size() && t.mats[order[pos]].height == maxh) grp.push_back(&t.mats[order[pos++]]);
     colbufs.push_back(upload_cols(grp, keep[0], s));
-    int ncols = (int)keep[0].size();
-    t.layers[0] = DBuf(maxh * 8, s);
-    {
-    PROF("merkle_leaves", s, 4.0 * maxh * ncols + 32.0 * maxh);  // algorithmic bytes
-    hipLaunchKernelGGL(k_hash_leaves, dim3((unsigned)((maxh + NT - 1) / NT)), dim3(NT), 0, s,
-                       (const uint64_t *)colbufs.back().p, ncols, maxh, t.layers[0].p);
-    HIP_CHECK(hipGetLastError());
-    }
-    PROF("merkle_nodes", s, 96.0 * maxh);
+    const int ncols = (int)keep[0].size();
     uint64_t h = maxh;
     for (int L = 1; L <= t.log_max; L++) {
         h >>= 1;
         grp.clear();
         while (pos < order.size() && t.mats[order[pos]].height == h) grp.push_back(&t.mats[order[pos++]]);
+        if (grp.empty()) continue;
         colbufs.push_back(upload_cols(grp, keep[L], s));
-        int ninj = grp.empty() ? 0 : (int)keep[L].size();
-        // a group of zero-width matrices still injects hash(empty) = 0-digest: keep semantics
-        bool inject = !grp.empty();
-        t.layers[L] = DBuf(h * 8, s);
-        hipLaunchKernelGGL(k_compress_level, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
-                           (const uint32_t *)t.layers[L - 1].p, t.layers[L].p, h,
-                           (const uint64_t *)colbufs.back().p, inject ? (ninj ? ninj : -1) : 0);
+        // a group of zero-width matrices still injects hash(empty) = the zero digest
+        inj[L] = {&colbufs.back(), keep[L].empty() ? -1 : (int)keep[L].size()};
+    }
+    ARG_CHECK(pos == order.size(), "matrix heights must be powers of two <= max");
+    t.layer_store.emplace_back(maxh * 8, s);
+    t.layers[0] = t.layer_store.back().p;
+    {
+        PROF("merkle_leaves", s, 4.0 * maxh * ncols + 32.0 * maxh);  // algorithmic bytes
+        hipLaunchKernelGGL(k_hash_leaves, dim3((unsigned)((maxh + NT - 1) / NT)), dim3(NT), 0, s,
+                           (const uint64_t *)colbufs[0].p, ncols, maxh, t.layers[0]);
         HIP_CHECK(hipGetLastError());
     }
-    ARG_CHECK(pos == order.size(), "matrix heights must be distinct powers of two <= max");
-    HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max].p, 32, hipMemcpyDeviceToHost, s));
+    {
+        PROF("merkle_nodes", s, 96.0 * maxh);
+        build_levels(t, maxh, inj, s);
+    }
+    HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max], 32, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
 }
 
 void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s) {
     ARG_CHECK(nleaves && (nleaves & (nleaves - 1)) == 0, "leaf count must be a power of two");
     t.log_max = ilog2(nleaves);
-    t.layers.clear();
-    t.layers.resize(t.log_max + 1);
-    t.layers[0] = std::move(leaves);
-    uint64_t h = nleaves;
-    for (int L = 1; L <= t.log_max; L++) {
-        h >>= 1;
-        t.layers[L] = DBuf(h * 8, s);
-        hipLaunchKernelGGL(k_compress_level, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
-                           (const uint32_t *)t.layers[L - 1].p, t.layers[L].p, h, (const uint64_t *)nullptr, 0);
-        HIP_CHECK(hipGetLastError());
-    }
-    HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max].p, 32, hipMemcpyDeviceToHost, s));
+    t.layers.assign(t.log_max + 1, nullptr);
+    t.layer_store.clear();
+    t.layer_store.push_back(std::move(leaves));
+    t.layers[0] = t.layer_store.back().p;
+    std::vector<std::pair<const DBuf *, int>> inj(t.log_max + 1, {nullptr, 0});
+    build_levels(t, nleaves, inj, s);
+    HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max], 32, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
 }
 

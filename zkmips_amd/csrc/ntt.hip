@@ -297,9 +297,16 @@ static std::vector<int> strided_plan(int L, int &logC) {
     return p;
 }
 
-static DBuf make_twist(uint64_t N, int L, uint32_t shift, Twist &tws, hipStream_t s) {
-    // f0(k) = shift^k / N, f1(k) = (shift w_2N)^k / N, k = hi*4096 + lo
+// Twist tables f0(k) = shift^k / N, f1(k) = (shift w_2N)^k / N, k = hi*4096 + lo; cached per
+// (N, shift) in the context (a handful of distinct pairs per machine), built once on the host.
+static Twist get_twist(Ctx &c, uint64_t N, int L, uint32_t shift, hipStream_t s) {
     const int nhi = (int)((N + 4095) / 4096);
+    std::lock_guard<std::mutex> g(c.mu);
+    for (auto &kv : c.twists)
+        if (kv.first.first == L && kv.first.second == shift) {
+            const uint32_t *p = kv.second.p;
+            return Twist{p, p + 4096, p + 4096 + nhi, p + 2 * 4096 + nhi};
+        }
     std::vector<uint32_t> tt(2 * (4096 + nhi));
     const uint32_t ninv = inv(to_mont((uint32_t)(N % P)));
     uint32_t sh[2] = {shift, mul(shift, two_adic_gen(L + 1))};
@@ -311,11 +318,11 @@ static DBuf make_twist(uint64_t N, int L, uint32_t shift, Twist &tws, hipStream_
         uint32_t y = ninv;
         for (int i = 0; i < nhi; i++) { hi[i] = y; y = mul(y, step); }
     }
-    DBuf dtt(tt.size(), s);
-    HIP_CHECK(hipMemcpyAsync(dtt.p, tt.data(), tt.size() * 4, hipMemcpyHostToDevice, s));
-    HIP_CHECK(hipStreamSynchronize(s));  // tt is pageable host memory
-    tws = Twist{dtt.p, dtt.p + 4096, dtt.p + 4096 + nhi, dtt.p + 2 * 4096 + nhi};
-    return dtt;
+    c.twists.emplace_back(std::make_pair(L, shift), DBuf(tt.size(), s));
+    const uint32_t *p = c.twists.back().second.p;
+    HIP_CHECK(hipMemcpyAsync((void *)p, tt.data(), tt.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    return Twist{p, p + 4096, p + 4096 + nhi, p + 2 * 4096 + nhi};
 }
 
 // Bit-reversed input evaluations (quotient chunks, produced bit-reversed by k_quotient):
@@ -331,8 +338,7 @@ void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hip
     ARG_CHECK(dst.height == 2 * N && dst.width == W, "LDE destination shape");
     int logC;
     std::vector<int> sp = strided_plan(L, logC);
-    Twist tws;
-    DBuf dtt = make_twist(N, L, shift, tws, s);
+    const Twist tws = get_twist(c, N, L, shift, s);
     const uint32_t nv = (uint32_t)W;
     ColMap m_src{N, 0, 1}, m_dst1{2 * N, 0, 1}, m_dst2{2 * N, N, 2};
     if (sp.empty()) {
@@ -368,8 +374,7 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
     int logC;
     std::vector<int> sp = strided_plan(L, logC);
 
-    Twist tws;
-    DBuf dtt = make_twist(N, L, shift, tws, s);
+    const Twist tws = get_twist(c, N, L, shift, s);
 
     // work buffer: per column 2N ([E0 | E1]); the iNTT runs in its first half
     DBuf work(2 * N * W, s);

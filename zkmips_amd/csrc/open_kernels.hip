@@ -60,12 +60,10 @@ __global__ __launch_bounds__(NT) void k_perm_rows(PermArgs a) {
         for (uint32_t i = b * a.batch; i < nloc && i < (uint32_t)(b + 1) * a.batch; i++) {
             const uint32_t *lk = table + 4 * i;
             ef d = ef_add_base(a.alpha, lk[0]);
-            ef bp = a.beta;
             const uint32_t *vp = prog + lk[3];
             for (uint32_t v = 0; v < lk[2]; v++) {
                 uint32_t x = apply_vpc(vp, a.main, a.prep, a.n, r);
-                d = ef_add(d, ef_mul_base(bp, x));
-                bp = ef_mul(bp, a.beta);
+                d = ef_add(d, ef_mul_base(ld_ef(a.beta_pows + 4 * v), x));
             }
             uint32_t m = apply_vpc(vp, a.main, a.prep, a.n, r);
             if (!lk[1]) m = neg(m);
@@ -119,14 +117,29 @@ __global__ __launch_bounds__(NT) void k_scan_block(uint32_t *data, uint64_t n, u
     if (threadIdx.x == NT - 1) st_ef(totals + 4 * blockIdx.x, ef_add(off, run));
 }
 
-__global__ void k_scan_totals(uint32_t *totals, uint64_t nblocks) {
-    // single thread sequential exclusive scan (nblocks <= 2^13)
-    if (threadIdx.x || blockIdx.x) return;
+// exclusive scan of the block totals by one workgroup: contiguous chunk per thread + LDS scan
+__global__ __launch_bounds__(NT) void k_scan_totals(uint32_t *totals, uint64_t nblocks) {
+    __shared__ uint32_t sums[NT][4];
+    const uint64_t per = (nblocks + NT - 1) / NT;
+    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nblocks ? b0 + per : nblocks;
     ef run = ef_zero();
-    for (uint64_t i = 0; i < nblocks; i++) {
+    for (uint64_t i = b0; i < b1; i++) run = ef_add(run, ld_ef(totals + 4 * i));
+    for (int e = 0; e < 4; e++) sums[threadIdx.x][e] = run.c[e];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ef acc = ef_zero();
+        for (int t = 0; t < NT; t++) {
+            ef v{{sums[t][0], sums[t][1], sums[t][2], sums[t][3]}};
+            for (int e = 0; e < 4; e++) sums[t][e] = acc.c[e];
+            acc = ef_add(acc, v);
+        }
+    }
+    __syncthreads();
+    ef off{{sums[threadIdx.x][0], sums[threadIdx.x][1], sums[threadIdx.x][2], sums[threadIdx.x][3]}};
+    for (uint64_t i = b0; i < b1; i++) {
         ef t = ld_ef(totals + 4 * i);
-        st_ef(totals + 4 * i, run);
-        run = ef_add(run, t);
+        st_ef(totals + 4 * i, off);
+        off = ef_add(off, t);
     }
 }
 
@@ -147,7 +160,7 @@ void launch_perm_trace(const PermArgs &a, hipStream_t s) {
     DBuf totals(4 * nblk, s);
     hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nblk), dim3(NT), 0, s, a.rowsum, a.n, totals.p);
     HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(64), 0, s, totals.p, nblk);
+    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(NT), 0, s, totals.p, nblk);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_scan_fix, dim3((unsigned)((a.n + NT - 1) / NT)), dim3(NT), 0, s, a.rowsum, a.n, totals.p,
                        a.out + (uint64_t)4 * a.nb * a.n);
@@ -232,12 +245,10 @@ __global__ __launch_bounds__(NT) void k_quotient(QuotArgs a) {
             for (uint32_t i = b * a.batch; i < nloc && i < (uint32_t)(b + 1) * a.batch; i++) {
                 const uint32_t *lk = table + 4 * i;
                 ef rlc = ef_add_base(a.alpha_p, lk[0]);
-                ef bp = a.beta_p;
                 const uint32_t *vp = prog + lk[3];
                 for (uint32_t v = 0; v < lk[2]; v++) {
                     uint32_t xv = apply_vpc(vp, main, prep, ldm, rl);
-                    rlc = ef_add(rlc, ef_mul_base(bp, xv));
-                    bp = ef_mul(bp, a.beta_p);
+                    rlc = ef_add(rlc, ef_mul_base(ld_ef(a.beta_pows + 4 * v), xv));
                 }
                 uint32_t m = apply_vpc(vp, main, prep, ldm, rl);
                 if (!lk[1]) m = neg(m);

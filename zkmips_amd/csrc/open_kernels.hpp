@@ -9,7 +9,8 @@ struct PermArgs {
     const uint32_t *main;     // trace, column-major natural, n rows
     const uint32_t *prep;     // preprocessed trace or nullptr
     uint64_t n;
-    kb::ef alpha, beta;       // local permutation challenges
+    kb::ef alpha;             // local permutation challenge alpha
+    const uint32_t *beta_pows;// beta^(j+1), EF, j < max lookup arity (device)
     int batch, nb;            // lookups per batch, number of batch columns
     uint32_t *out;            // flattened perm trace, column-major (4 * (nb + 1) columns)
     uint32_t *rowsum;         // scratch: n EF
@@ -26,7 +27,8 @@ struct QuotArgs {
     uint32_t gen, gen_pow_n, wn_inv;     // 3, 3^n, w_n^-1 (Montgomery)
     const uint32_t *pv;                  // public values (Montgomery)
     const uint32_t *pows;                // alpha^(nc-1-k), EF
-    kb::ef alpha_p, beta_p, lcs;
+    kb::ef alpha_p, lcs;
+    const uint32_t *beta_pows;           // beta^(j+1), EF (device)
     uint32_t gcs[14];
     int batch, perm_w, global, main_w;
     uint32_t *chunks;                    // 2^lqd chunks x 4 columns x n rows (bit-reversed rows)

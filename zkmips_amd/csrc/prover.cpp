@@ -238,6 +238,17 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     for (int i = 0; i < m.num_pv; i++) ch.observe(to_mont(md.pv[i]));
     ch.observe(md.tree.root, 8);
     const ef perm_alpha = ch.sample_ef(), perm_beta = ch.sample_ef();
+    // beta^(j+1) for every lookup arity (rlc = alpha + kind + sum_j beta^(j+1) v_j, permutation.rs:48-57)
+    size_t max_arity = 1;
+    for (auto &cd : m.chips)
+        for (auto &l : cd.local) max_arity = std::max(max_arity, l.values.size());
+    std::vector<uint32_t> bpow(4 * max_arity);
+    {
+        ef b = perm_beta;
+        for (size_t j = 0; j < max_arity; j++) { memcpy(&bpow[4 * j], b.c, 16); b = ef_mul(b, perm_beta); }
+    }
+    DBuf d_bpow(bpow.size(), s);
+    HIP_CHECK(hipMemcpyAsync(d_bpow.p, bpow.data(), bpow.size() * 4, hipMemcpyHostToDevice, s));
 
     PROF("open_total", s, 0);
     // ---- permutation traces (prover.rs:337-365) ----
@@ -257,7 +268,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         if (pw) {
             DBuf rowsum(4 * N, s);
             PermArgs a{pk.progs[md.chip[i]].p, md.traces[i].p, pki >= 0 ? pk.traces[pki].p : nullptr, N, perm_alpha,
-                       perm_beta, 1 << cd.log_qd, pw - 1, perm_traces[i].p, rowsum.p};
+                       d_bpow.p, 1 << cd.log_qd, pw - 1, perm_traces[i].p, rowsum.p};
             { PROF("perm_trace", s, 4.0 * N * (cd.main_w + cd.prep_w) + 16.0 * N * (pw + 2)); launch_perm_trace(a, s); }
             uint32_t l[4];
             for (int e = 0; e < 4; e++)
@@ -323,7 +334,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         qa.wn_inv = inv(two_adic_gen(logN));
         qa.pv = d_pv.p;
         qa.pows = d_pows.p;
-        qa.alpha_p = perm_alpha; qa.beta_p = perm_beta; qa.lcs = proof.chips[i].lcs;
+        qa.alpha_p = perm_alpha; qa.beta_pows = d_bpow.p; qa.lcs = proof.chips[i].lcs;
         memcpy(qa.gcs, proof.chips[i].gcs, sizeof qa.gcs);
         qa.batch = 1 << lqd; qa.perm_w = cd.perm_w; qa.global = cd.scope == 1; qa.main_w = cd.main_w;
         qa.chunks = q_chunks[i].p;
@@ -359,72 +370,78 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
 
     // ---- opened values by barycentric evaluation over the trace domain ----
     //   p(z) = ((z/s)^N - 1)/N * sum_j y_j w^j / (z/s - w^j); next point g z uses y_{j+1}.
+    // All dot products are launched back to back and read back with one copy.
     {
         const int nseg = 32;
-        std::vector<uint64_t> heights_done;
-        std::vector<std::pair<uint64_t, DBuf>> wtab;  // natural-order weights per trace height (s = 1)
-        auto weights_for = [&](uint64_t N) -> const uint32_t * {
-            for (auto &pr : wtab) if (pr.first == N) return pr.second.p;
-            wtab.emplace_back(N, DBuf(4 * N, s));
-            launch_inv_points(zeta, ONE, c.tw_fwd, N, false, true, wtab.back().second.p, s);
-            return wtab.back().second.p;
-        };
+        struct Pend { OpenReq *r; const uint32_t *ybase; uint64_t N, W; bool bitrev; uint32_t shift; uint64_t coff, poff; ef pre; };
+        std::vector<Pend> pend;
+        uint64_t ncols_all = 0, nparts = 0;
         for (auto &r : req) {
-            const uint32_t *ybase;
-            uint64_t N, W;
-            bool bitrev = false;
-            uint32_t shift = ONE;
-            if (r.round == 0) { ybase = pk.traces[r.mat].p; N = pk.heights[r.mat]; W = m.chips[pk.trace_chip[r.mat]].prep_w; }
-            else if (r.round == 1) { ybase = md.traces[r.mat].p; N = md.heights[r.mat]; W = m.chips[md.chip[r.mat]].main_w; }
-            else if (r.round == 2) { ybase = perm_traces[r.mat].p; N = md.heights[r.mat]; W = 4 * m.chips[md.chip[r.mat]].perm_w; }
+            Pend q{&r, nullptr, 0, 0, false, ONE, 0, 0, ef_zero()};
+            if (r.round == 0) { q.ybase = pk.traces[r.mat].p; q.N = pk.heights[r.mat]; q.W = m.chips[pk.trace_chip[r.mat]].prep_w; }
+            else if (r.round == 1) { q.ybase = md.traces[r.mat].p; q.N = md.heights[r.mat]; q.W = m.chips[md.chip[r.mat]].main_w; }
+            else if (r.round == 2) { q.ybase = perm_traces[r.mat].p; q.N = md.heights[r.mat]; q.W = 4 * m.chips[md.chip[r.mat]].perm_w; }
             else {
-                int ci = chunk_chip[r.mat];
+                const int ci = chunk_chip[r.mat];
                 int j = 0;
                 for (int k = 0; k < r.mat; k++) if (chunk_chip[k] == ci) j++;
-                N = md.heights[ci];
+                q.N = md.heights[ci];
                 const int lqd = m.chips[md.chip[ci]].log_qd;
-                ybase = q_chunks[ci].p + (uint64_t)j * 4 * N;
-                W = 4;
-                bitrev = true;
-                shift = mul(to_mont(GENERATOR), pow(two_adic_gen(ilog2(N) + lqd), (uint64_t)j));
+                q.ybase = q_chunks[ci].p + (uint64_t)j * 4 * q.N;
+                q.W = 4;
+                q.bitrev = true;
+                q.shift = mul(to_mont(GENERATOR), pow(two_adic_gen(ilog2(q.N) + lqd), (uint64_t)j));
             }
-            r.vals[0].assign(W, ef_zero());
-            r.vals[1].assign(W, ef_zero());
-            if (!W) continue;
-            const uint32_t *w;
-            DBuf wq;
-            const ef zs = ef_mul_base(zeta, inv(shift));
-            if (!bitrev) w = weights_for(N);
-            else {
-                wq = DBuf(4 * N, s);
-                launch_inv_points(zs, ONE, c.tw_fwd, N, true, true, wq.p, s);
-                w = wq.p;
+            r.vals[0].assign(q.W, ef_zero());
+            r.vals[1].assign(q.W, ef_zero());
+            q.coff = ncols_all;
+            q.poff = nparts;
+            ncols_all += q.W;
+            nparts += q.W * nseg * 8;
+            const ef zs = ef_mul_base(zeta, inv(q.shift));
+            q.pre = ef_mul_base(ef_sub(ef_pow(zs, q.N), ef_one()), inv(to_mont((uint32_t)(q.N % P))));
+            pend.push_back(q);
+        }
+        std::vector<uint64_t> cols(ncols_all + 1);
+        for (auto &q : pend)
+            for (uint64_t k = 0; k < q.W; k++) cols[q.coff + k] = (uint64_t)(uintptr_t)(q.ybase + k * q.N);
+        DBuf dcols(2 * cols.size(), s), part(nparts + 1, s);
+        HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s));
+        std::vector<std::pair<uint64_t, DBuf>> wtab;  // natural-order weights per trace height (shift 1)
+        std::vector<DBuf> wchunk;
+        for (auto &q : pend) {
+            if (!q.W) continue;
+            const uint32_t *w = nullptr;
+            if (!q.bitrev) {
+                for (auto &pr : wtab) if (pr.first == q.N) w = pr.second.p;
+                if (!w) {
+                    wtab.emplace_back(q.N, DBuf(4 * q.N, s));
+                    w = wtab.back().second.p;
+                    launch_inv_points(zeta, ONE, c.tw_fwd, q.N, false, true, (uint32_t *)w, s);
+                }
+            } else {
+                wchunk.emplace_back(4 * q.N, s);
+                w = wchunk.back().p;
+                launch_inv_points(ef_mul_base(zeta, inv(q.shift)), ONE, c.tw_fwd, q.N, true, true, (uint32_t *)w, s);
             }
-            std::vector<uint64_t> cols(W);
-            for (uint64_t k = 0; k < W; k++) cols[k] = (uint64_t)(uintptr_t)(ybase + k * N);
-            DBuf dcols(2 * W, s);
-            HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), W * 8, hipMemcpyHostToDevice, s));
-            DBuf part(W * nseg * 8, s);
-            const bool with_next = r.npts == 2;
-            PROF("open_eval", s, 4.0 * N * W + 16.0 * N);
-            launch_open_dot((const uint64_t *)dcols.p, (uint32_t)W, N, w, with_next, nseg, part.p, s);
-            std::vector<uint32_t> hp(W * nseg * 8);
-            HIP_CHECK(hipMemcpyAsync(hp.data(), part.p, hp.size() * 4, hipMemcpyDeviceToHost, s));
-            HIP_CHECK(hipStreamSynchronize(s));
-            // prefactor (z'^N - 1) / N
-            const ef zn = ef_pow(zs, N);
-            const ef pre = ef_mul_base(ef_sub(zn, ef_one()), inv(to_mont((uint32_t)(N % P))));
-            for (uint64_t k = 0; k < W; k++) {
+            PROF("open_eval", s, 4.0 * q.N * q.W + 16.0 * q.N);
+            launch_open_dot((const uint64_t *)dcols.p + q.coff, (uint32_t)q.W, q.N, w, q.r->npts == 2, nseg,
+                            part.p + q.poff, s);
+        }
+        std::vector<uint32_t> hp(nparts + 1);
+        HIP_CHECK(hipMemcpyAsync(hp.data(), part.p, nparts * 4, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (auto &q : pend)
+            for (uint64_t k = 0; k < q.W; k++) {
                 ef a0 = ef_zero(), a1 = ef_zero();
                 for (int sg = 0; sg < nseg; sg++) {
-                    const uint32_t *q = &hp[(k * nseg + sg) * 8];
-                    a0 = ef_add(a0, ef{{q[0], q[1], q[2], q[3]}});
-                    a1 = ef_add(a1, ef{{q[4], q[5], q[6], q[7]}});
+                    const uint32_t *x = &hp[q.poff + (k * nseg + sg) * 8];
+                    a0 = ef_add(a0, ef{{x[0], x[1], x[2], x[3]}});
+                    a1 = ef_add(a1, ef{{x[4], x[5], x[6], x[7]}});
                 }
-                r.vals[0][k] = ef_mul(pre, a0);
-                r.vals[1][k] = ef_mul(pre, a1);  // (g z)^N = z^N for the trace-domain generator g
+                q.r->vals[0][k] = ef_mul(q.pre, a0);
+                q.r->vals[1][k] = ef_mul(q.pre, a1);  // (g z)^N = z^N for the trace-domain generator g
             }
-        }
     }
 
     // ---- PCS open: FRI alpha, reduced openings (fri.rs:71-215 semantics) ----
@@ -570,12 +587,12 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 const uint64_t row = ri >> (tt->log_max - ilog2(mm.height));
                 if (mm.width) item(mm.d + row, mm.height, mm.width);
             }
-            for (int l = 0; l < tt->log_max; l++) item(tt->layers[l].p + ((ri >> l) ^ 1) * 8, 1, 8);
+            for (int l = 0; l < tt->log_max; l++) item(tt->layers[l] + ((ri >> l) ^ 1) * 8, 1, 8);
         }
         for (int rd = 0; rd < nrounds; rd++) {
             const uint64_t ii = idx[q] >> rd, pair = ii >> 1;
             item(ftrees[rd].owned.back().p + 8 * pair + 4 * ((ii ^ 1) & 1), 1, 4);
-            for (int l = 0; l < ftrees[rd].log_max; l++) item(ftrees[rd].layers[l].p + ((pair >> l) ^ 1) * 8, 1, 8);
+            for (int l = 0; l < ftrees[rd].log_max; l++) item(ftrees[rd].layers[l] + ((pair >> l) ^ 1) * 8, 1, 8);
         }
     }
     DBuf ditems(items.size() * 2 + 2, s), dout(total + 1, s);
