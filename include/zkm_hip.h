@@ -117,6 +117,8 @@ int zkm_pcs_commit_root(zkm_ctx *ctx, const zkm_matrix_t *mats, uint32_t n, uint
 /* ---- kernel-level entry points (parity tests, microbenchmarks) ---- */
 /* out (host, row-major (h << 1) x w, canonical): bit-reversed coset LDE with the given shift */
 int zkm_coset_lde(zkm_ctx *ctx, const zkm_matrix_t *m, uint32_t shift_canonical, uint32_t *out);
+/* same; bitrev_in != 0: the input rows are the evaluations in bit-reversed order (quotient chunks) */
+int zkm_coset_lde_ex(zkm_ctx *ctx, const zkm_matrix_t *m, uint32_t shift_canonical, int bitrev_in, uint32_t *out);
 /* n independent Poseidon2-16 permutations of canonical states (in place, host memory) */
 int zkm_poseidon2_permute(zkm_ctx *ctx, uint32_t *states, uint64_t n);
 /* Timing helper: runs `iters` LDEs of a resident random h x w matrix, returns average ms of the

@@ -51,6 +51,28 @@ def test_coset_lde_vs_oracle(dev, logn):
     assert np.array_equal(got, exp)
 
 
+@pytest.mark.parametrize("logn,w", [(20, 2), (22, 1)])
+def test_coset_lde_large_vs_oracle(dev, logn, w):
+    m = W.random_matrix(1 << logn, w, seed=logn)
+    assert np.array_equal(dev.coset_lde(m, 3), O.lde(m, 1, 3))
+
+
+@pytest.mark.parametrize("logn", [3, 12, 13, 14, 17, 20])
+def test_coset_lde_bitrev_input(dev, logn):
+    """The quotient-chunk pipeline: evaluations handed over in bit-reversed row order."""
+    n = 1 << logn
+    m = W.random_matrix(n, 3, seed=100 + logn)
+    idx = np.asarray([int(format(i, f"0{logn}b")[::-1], 2) for i in range(n)]) if logn <= 14 else None
+    if idx is None:
+        r = np.arange(n, dtype=np.uint64)
+        idx = np.zeros(n, np.uint64)
+        for b in range(logn):
+            idx |= ((r >> np.uint64(b)) & np.uint64(1)) << np.uint64(logn - 1 - b)
+    shift = pow(3, (P - 1) >> (logn + 1), P)
+    got = dev.coset_lde(m[idx], shift, bitrev_in=True)
+    assert np.array_equal(got, O.lde(m, 1, shift))
+
+
 def test_coset_lde_other_shift(dev):
     m = W.random_matrix(1 << 13, 4, seed=5)
     shift = pow(3, (P - 1) >> 14, P)  # quotient-chunk style shift w_2N^-1 analogue

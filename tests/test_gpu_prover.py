@@ -40,7 +40,7 @@ def test_setup_commitment_matches(dev):
     assert np.array_equal(gpu.vk_commit, cpu.commit)
 
 
-@pytest.mark.parametrize("n", [16, 64, 1024, 1 << 13])
+@pytest.mark.parametrize("n", [16, 64, 1024, 1 << 13, 1 << 16])
 def test_shard_proof_bytes_identical(dev, n):
     gpu, cpu, traces, pvs = provers(dev, n)
     ch = gpu.base_challenger()

@@ -59,6 +59,7 @@ def lib():
     L.zkm_destroy.argtypes = [vp]
     L.zkm_device_count.restype = C.c_int
     L.zkm_coset_lde.argtypes = [vp, C.POINTER(Matrix), C.c_uint32, vp]
+    L.zkm_coset_lde_ex.argtypes = [vp, C.POINTER(Matrix), C.c_uint32, C.c_int, vp]
     L.zkm_poseidon2_permute.argtypes = [vp, vp, C.c_uint64]
     L.zkm_pcs_commit_root.argtypes = [vp, C.POINTER(Matrix), C.c_uint32, vp]
     L.zkm_bench_lde.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
@@ -122,11 +123,11 @@ class Device:
             pass
 
     # ---- kernel-level helpers ----
-    def coset_lde(self, m: np.ndarray, shift: int = 3) -> np.ndarray:
+    def coset_lde(self, m: np.ndarray, shift: int = 3, bitrev_in: bool = False) -> np.ndarray:
         keep = []
         mm = matrix(m, keep=keep)
         out = np.zeros((2 * mm.height, mm.width), np.uint32)
-        check(lib().zkm_coset_lde(self.h, C.byref(mm), shift, out.ctypes.data), "zkm_coset_lde")
+        check(lib().zkm_coset_lde_ex(self.h, C.byref(mm), shift, int(bitrev_in), out.ctypes.data), "zkm_coset_lde")
         return out
 
     def poseidon2_permute(self, states: np.ndarray) -> np.ndarray:

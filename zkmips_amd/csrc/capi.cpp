@@ -115,7 +115,11 @@ void zkm_destroy(zkm_ctx *ctx) {
 
 void zkm_free_bytes(uint8_t *p) { free(p); }
 
+int zkm_coset_lde_ex(zkm_ctx *ctx, const zkm_matrix_t *m, uint32_t shift, int bitrev_in, uint32_t *out);
 int zkm_coset_lde(zkm_ctx *ctx, const zkm_matrix_t *m, uint32_t shift, uint32_t *out) {
+    return zkm_coset_lde_ex(ctx, m, shift, 0, out);
+}
+int zkm_coset_lde_ex(zkm_ctx *ctx, const zkm_matrix_t *m, uint32_t shift, int bitrev_in, uint32_t *out) {
     GUARD_BEGIN
     ARG_CHECK(ctx && m && out, "null argument");
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
@@ -125,7 +129,8 @@ int zkm_coset_lde(zkm_ctx *ctx, const zkm_matrix_t *m, uint32_t shift, uint32_t 
     DMat src{col.p, m->height, m->width};
     DBuf ld(2 * m->height * m->width, L.s);
     DMat dst{ld.p, 2 * m->height, m->width};
-    lde_batch(*c, src, kb::to_mont(shift), dst, L.s);
+    if (bitrev_in) lde_batch_bitrev_in(*c, src, kb::to_mont(shift), dst, L.s);
+    else lde_batch(*c, src, kb::to_mont(shift), dst, L.s);
     DBuf rm(2 * m->height * m->width, L.s);
     launch_from_col_major(ld.p, 2 * m->height, m->width, rm.p, L.s);
     HIP_CHECK(hipMemcpyAsync(out, rm.p, 2 * m->height * m->width * 4, hipMemcpyDeviceToHost, L.s));

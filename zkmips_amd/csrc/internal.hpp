@@ -111,6 +111,8 @@ void build_twiddles(Ctx &c, int log_max);
 // Bit-reversed coset LDE of `src` (h x w col-major) into `dst` (2h x w col-major):
 // dst column c row i = p_c(shift * w_{2h}^{rev(i)}), p_c interpolating src column c on H_h.
 void lde_batch(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst, hipStream_t s);
+// same, for evaluations given in bit-reversed row order
+void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst, hipStream_t s);
 
 // Merkle
 void tree_build(DTree &t, hipStream_t s);

@@ -21,23 +21,35 @@ constexpr uint32_t ONE = 0x01fffffeu;      // 2^32 mod P  (Montgomery 1)
 constexpr uint32_t GENERATOR = 3u;
 constexpr int TWO_ADICITY = 24;
 
+KB_HD uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// a + b < 2P < 2^32: s - P wraps above s exactly when s < P
 KB_HD uint32_t add(uint32_t a, uint32_t b) {
     uint32_t s = a + b;
-    return s >= P ? s - P : s;
+    return umin(s, s - P);
 }
+// a - b wraps exactly when a < b; adding P then lands in [0, P) below the wrapped value
 KB_HD uint32_t sub(uint32_t a, uint32_t b) {
     uint32_t d = a - b;
-    return a < b ? d + P : d;
+    return umin(d, d + P);
 }
 KB_HD uint32_t neg(uint32_t a) { return a ? P - a : 0u; }
 KB_HD uint32_t dbl(uint32_t a) { return add(a, a); }
 
-// Montgomery reduction of t < P * 2^32
+KB_HD uint32_t umulhi(uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __umulhi(a, b);
+#else
+    return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+
+// Montgomery reduction of t < P * 2^32.  m = t_lo * P^-1 makes the low words of t and m*P equal,
+// so (t - m*P) / 2^32 = t_hi - mulhi(m, P) exactly, in (-P, P); the wrapped negative case is
+// repaired by min(r, r + P) (no 64-bit subtract, no compare/select through VCC).
 KB_HD uint32_t redc(uint64_t t) {
-    uint32_t m = (uint32_t)t * MU;
-    uint64_t u = (uint64_t)m * P;
-    uint32_t r = (uint32_t)((t - u) >> 32);
-    return t < u ? r + P : r;
+    const uint32_t m = (uint32_t)t * MU;
+    const uint32_t r = (uint32_t)(t >> 32) - umulhi(m, P);
+    return umin(r, r + P);
 }
 KB_HD uint32_t mul(uint32_t a, uint32_t b) { return redc((uint64_t)a * b); }
 KB_HD uint32_t sqr(uint32_t a) { return mul(a, a); }

@@ -11,8 +11,10 @@
 //      applies both twists to the bit-reversed coefficients and starts both transforms.
 //   3. DIT passes (bit-reversed in -> natural out); the last pass writes every output element
 //      to its bit-reversed row, so the LDE is produced without a separate permutation pass.
-// Passes: the lowest <= 12 bits in one contiguous LDS tile (4096 elements), the remaining bits
-// in strided passes of <= 6 bits over 64-column-wide tiles (256 B coalesced rows).
+// Passes: the lowest <= 13 bits in one contiguous LDS tile (8192 elements), the remaining bits
+// in strided passes of <= 9 bits over 32/64-column-wide tiles (128/256 B coalesced rows); the
+// inverse's last pass, the twists and the forward's first pass are one fused kernel, so a 2^22
+// column costs 3 HBM passes.  Butterflies run in radix-8 register groups (stage_group).
 #include "internal.hpp"
 #include "prof.hpp"
 
@@ -21,9 +23,6 @@ namespace zkm {
 using namespace kb;
 
 static constexpr int NT = 256;          // threads per workgroup
-static constexpr int LOGC_MAX = 12;     // contiguous tile: 4096 elements
-static constexpr int LOGS_MAX = 6;      // strided tile radix
-static constexpr int TS = 64;           // strided tile width (columns of 4 B)
 
 // ------------------------------------------------------------------ layout conversion
 __global__ void k_to_col_major(const uint32_t *__restrict__ in, uint64_t h, uint64_t w, int mont_in,
@@ -107,37 +106,75 @@ void build_twiddles(Ctx &c, int log_max) {
     c.tw_log = log_max;
 }
 
-// ------------------------------------------------------------------ tile stages
-// LDS tile x[r * T + t], R = 2^LOGR rows, T columns.  Global lower index of a butterfly at
-// (row r_lo, column t) is n = base + r_lo * S + c0 + t, stage half-size h = hr * S.
-template <int LOGR, int T, bool DIT>
-__device__ __forceinline__ void tile_stages(uint32_t *x, const uint32_t *__restrict__ tw, uint64_t S, uint64_t c0) {
-    constexpr int R = 1 << LOGR;
-    constexpr int NB = R * T / 2;
-#pragma unroll 1
-    for (int st = 0; st < LOGR; st++) {
-        const int lhr = DIT ? st : (LOGR - 1 - st);
-        const int hr = 1 << lhr;
-        const uint64_t h = (uint64_t)hr * S;
-        for (int b = threadIdx.x; b < NB; b += NT) {
-            const int t = b & (T - 1);
-            const int p = b / T;
-            const int rlo = ((p >> lhr) << (lhr + 1)) | (p & (hr - 1));
-            const uint64_t j = (uint64_t)(p & (hr - 1)) * S + c0 + t;
-            const uint32_t w = tw[h + j];
-            uint32_t *lo = x + rlo * T + t;
-            uint32_t *hi = lo + hr * T;
-            uint32_t u = *lo, v = *hi;
-            if (DIT) {
-                v = mul(v, w);
-                *lo = add(u, v);
-                *hi = sub(u, v);
-            } else {
-                *lo = add(u, v);
-                *hi = mul(sub(u, v), w);
+// ------------------------------------------------------------------ tile stage engine
+// A tile lives in LDS as x[r * LD + t] (R rows, T columns, row pitch LD).  Row r, column t holds
+// global index base + r*S + c0 + t, so the butterfly of a stage with half-size h = hr*S at lower
+// row r uses w_{2h}^{(r mod hr)*S + c0 + t} = tw[h + (r mod hr)*S + c0 + t] (all indices < 2^24).
+// Stages are processed G <= 3 at a time: each thread holds the 2^G elements a group of G stages
+// touches in registers, so a tile makes one LDS round trip per 3 stages instead of per stage.
+template <int G, int T, int LD, bool DIT>
+__device__ __forceinline__ void stage_group(uint32_t *x, int R, int lc, const uint32_t *__restrict__ tw, uint32_t S,
+                                            uint32_t c0) {
+    constexpr int E = 1 << G;
+    const int hrc = 1 << lc;
+    const int ngroups = (R * T) >> G;
+    for (int g = threadIdx.x; g < ngroups; g += NT) {
+        const int t = g & (T - 1);
+        const int q = g / T;
+        const int rlow = q & (hrc - 1);
+        const int r0 = ((q >> lc) << (lc + G)) | rlow;
+        uint32_t v[E];
+#pragma unroll
+        for (int k = 0; k < E; k++) v[k] = x[(r0 + k * hrc) * LD + t];
+        const uint32_t jb = (uint32_t)rlow * S + c0 + (uint32_t)t;
+        const uint32_t step = (uint32_t)hrc * S;
+        if (DIT) {
+#pragma unroll
+            for (int b = 0; b < G; b++) {
+                const uint32_t h = step << b;
+#pragma unroll
+                for (int k = 0; k < E; k++) {
+                    if (k & (1 << b)) continue;
+                    const uint32_t w = tw[h + jb + (uint32_t)(k & ((1 << b) - 1)) * step];
+                    const uint32_t u = v[k], y = mul(v[k + (1 << b)], w);
+                    v[k] = add(u, y);
+                    v[k + (1 << b)] = sub(u, y);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int b = G - 1; b >= 0; b--) {
+                const uint32_t h = step << b;
+#pragma unroll
+                for (int k = 0; k < E; k++) {
+                    if (k & (1 << b)) continue;
+                    const uint32_t w = tw[h + jb + (uint32_t)(k & ((1 << b) - 1)) * step];
+                    const uint32_t u = v[k], y = v[k + (1 << b)];
+                    v[k] = add(u, y);
+                    v[k + (1 << b)] = mul(sub(u, y), w);
+                }
             }
         }
-        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < E; k++) x[(r0 + k * hrc) * LD + t] = v[k];
+    }
+    __syncthreads();
+}
+
+// All LOGR stages of a tile: DIT bottom-up (half-sizes 1,2,4,...), DIF top-down.
+template <int LOGR, int T, int LD, bool DIT>
+__device__ __forceinline__ void tile_stages(uint32_t *x, const uint32_t *__restrict__ tw, uint32_t S, uint32_t c0) {
+    constexpr int R = 1 << LOGR;
+    if (DIT) {
+        int lc = 0;
+        for (; lc + 3 <= LOGR; lc += 3) stage_group<3, T, LD, true>(x, R, lc, tw, S, c0);
+        if (LOGR - lc == 2) stage_group<2, T, LD, true>(x, R, lc, tw, S, c0);
+        else if (LOGR - lc == 1) stage_group<1, T, LD, true>(x, R, lc, tw, S, c0);
+    } else {
+        int rem = LOGR;
+        for (; rem >= 3; rem -= 3) stage_group<3, T, LD, false>(x, R, rem - 3, tw, S, c0);
+        if (rem == 2) stage_group<2, T, LD, false>(x, R, 0, tw, S, c0);
+        else if (rem == 1) stage_group<1, T, LD, false>(x, R, 0, tw, S, c0);
     }
 }
 
@@ -150,7 +187,6 @@ struct ColMap {
     }
 };
 
-// Strided pass: rows r at stride S within outer blocks of R*S; 64-column tiles.
 struct Twist {
     const uint32_t *lo0, *hi0, *lo1, *hi1;
     __device__ __forceinline__ uint32_t f(int e, uint32_t k) const {
@@ -158,90 +194,102 @@ struct Twist {
     }
 };
 
-template <int LOGR, bool DIT>
+enum PassMode { MODE_PLAIN = 0, MODE_BITREV_OUT = 1, MODE_TWIST_OUT = 2 };
+
+// Strided pass: rows at stride S = 2^logS inside outer blocks of R*S, tiles of T columns.
+//   MODE_BITREV_OUT (last DIT pass, R*S == N): natural n = r*S + c goes to row rev_L(n).
+//   MODE_TWIST_OUT  (last DIT pass of an inverse transform): natural coefficient n goes to both
+//                   LDE halves multiplied by the coset twists f_0(n), f_1(n).
+template <int LOGR, int T, bool DIT>
 __global__ __launch_bounds__(NT) void k_ntt_strided(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
-                                                    int L, int logS, const uint32_t *__restrict__ tw, int bitrev_out,
-                                                    Twist tws, int twist_out, uint64_t dst_half) {
+                                                    int logS, const uint32_t *__restrict__ tw, int mode, Twist tws,
+                                                    uint64_t dst_half) {
     constexpr int R = 1 << LOGR;
-    constexpr int T = TS;
-    __shared__ uint32_t x[R * T];
-    const uint64_t S = 1ull << logS;
-    const uint64_t groups = S / T;
-    const uint64_t tile = blockIdx.x;
-    const uint64_t outer = tile / groups;
-    const uint64_t c0 = (tile % groups) * T;
-    const uint64_t base = outer * (uint64_t)R * S;
+    constexpr int LD = T + 1;  // padded rows: conflict-free column walks (bit-reversed write)
+    __shared__ uint32_t x[R * LD];
+    const uint32_t S = 1u << logS;
+    const uint32_t groups = S / T;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t outer = tile / groups;
+    const uint32_t c0 = (tile % groups) * T;
+    const uint32_t base = outer * (uint32_t)R * S;
     const uint32_t *sp = src + ms.off(blockIdx.y);
     uint32_t *dp = dst + md.off(blockIdx.y);
     for (int i = threadIdx.x; i < R * T; i += NT) {
         const int r = i / T, t = i & (T - 1);
-        x[i] = sp[base + (uint64_t)r * S + c0 + t];
+        x[r * LD + t] = sp[base + (uint32_t)r * S + c0 + t];
     }
     __syncthreads();
-    tile_stages<LOGR, T, DIT>(x, tw, S, c0);
-    if (twist_out) {
-        // natural coefficient index n -> two twisted outputs (E0, E1 halves)
+    tile_stages<LOGR, T, LD, DIT>(x, tw, S, c0);
+    if (mode == MODE_PLAIN) {
         for (int i = threadIdx.x; i < R * T; i += NT) {
             const int r = i / T, t = i & (T - 1);
-            const uint64_t n = base + (uint64_t)r * S + c0 + t;
-            dp[n] = mul(x[i], tws.f(0, (uint32_t)n));
-            dp[dst_half + n] = mul(x[i], tws.f(1, (uint32_t)n));
+            dp[base + (uint32_t)r * S + c0 + t] = x[r * LD + t];
         }
-    } else if (!bitrev_out) {
+    } else if (mode == MODE_TWIST_OUT) {
         for (int i = threadIdx.x; i < R * T; i += NT) {
             const int r = i / T, t = i & (T - 1);
-            dp[base + (uint64_t)r * S + c0 + t] = x[i];
+            const uint32_t n = base + (uint32_t)r * S + c0 + t;
+            const uint32_t v = x[r * LD + t];
+            dp[n] = mul(v, tws.f(0, n));
+            dp[dst_half + n] = mul(v, tws.f(1, n));
         }
     } else {
-        // last pass (outer == 0, R*S == N): natural n = r*S + c -> row rev_L(n) = rev_S(c)*R + rev_R(r)
         for (int i = threadIdx.x; i < R * T; i += NT) {
             const int t = i / R, q = i & (R - 1);
-            const uint64_t c = c0 + t;
-            const uint32_t r = rev_bits((uint32_t)q, LOGR);
-            dp[(uint64_t)rev_bits((uint32_t)c, logS) * R + q] = x[r * T + t];
+            dp[(uint64_t)rev_bits(c0 + t, logS) * R + q] = x[(int)rev_bits((uint32_t)q, LOGR) * LD + t];
         }
     }
 }
 
-// Contiguous pass over blocks of R consecutive elements.
-//   twist != nullptr (DIT only): input = bit-reversed coefficients; for e in {0,1} the tile is
-//   multiplied by f_e(k) = hi_e[k >> 12] * lo_e[k & 4095] (k = rev_L(n)) and transformed into
-//   dst + md.off(v) + e * dst_half.
-//   bitrev_out: single-pass transform (R == N): write natural n to row rev_L(n).
+// Contiguous pass over blocks of R consecutive elements (bit-reversed-input pipeline):
+//   MODE_PLAIN: stages only; MODE_TWIST_OUT: DIT (inverse) then twisted writes to both halves.
 template <int LOGR, bool DIT>
 __global__ __launch_bounds__(NT) void k_ntt_contig(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
-                                                   int L, const uint32_t *__restrict__ tw, int bitrev_out,
-                                                   Twist tws, int use_twist, uint64_t dst_half) {
+                                                   const uint32_t *__restrict__ tw, int mode, Twist tws,
+                                                   uint64_t dst_half) {
     constexpr int R = 1 << LOGR;
-    __shared__ uint32_t a[R];
     __shared__ uint32_t x[R];
-    const uint64_t base = (uint64_t)blockIdx.x * R;
+    const uint32_t base = blockIdx.x * (uint32_t)R;
     const uint32_t *sp = src + ms.off(blockIdx.y) + base;
-    for (int i = threadIdx.x; i < R; i += NT) a[i] = sp[i];
+    for (int i = threadIdx.x; i < R; i += NT) x[i] = sp[i];
     __syncthreads();
-    if (use_twist == 2) {
-        // twist on output: natural coefficient n -> E0 / E1 halves (DIT iNTT of bit-reversed input)
-        for (int i = threadIdx.x; i < R; i += NT) x[i] = a[i];
-        __syncthreads();
-        tile_stages<LOGR, 1, DIT>(x, tw, 1, 0);
-        uint32_t *dp = dst + md.off(blockIdx.y);
+    tile_stages<LOGR, 1, 1, DIT>(x, tw, 1, 0);
+    uint32_t *dp = dst + md.off(blockIdx.y);
+    if (mode == MODE_TWIST_OUT) {
         for (int i = threadIdx.x; i < R; i += NT) {
-            const uint32_t n = (uint32_t)(base + i);
+            const uint32_t n = base + i;
             dp[n] = mul(x[i], tws.f(0, n));
             dp[dst_half + n] = mul(x[i], tws.f(1, n));
         }
-        return;
+    } else {
+        for (int i = threadIdx.x; i < R; i += NT) dp[base + i] = x[i];
     }
-    const int ne = use_twist ? 2 : 1;
-    for (int e = 0; e < ne; e++) {
-        for (int i = threadIdx.x; i < R; i += NT) {
-            uint32_t v = a[i];
-            if (use_twist) v = mul(v, tws.f(e, rev_bits((uint32_t)(base + i), L)));
-            x[i] = v;
-        }
+}
+
+// Fused middle of the natural-input LDE: the inverse NTT's last (contiguous, DIF) pass, the two
+// coset twists, and the first (contiguous, DIT) pass of both forward transforms, on one tile.
+// The DIF output tile (bit-reversed coefficients) is exactly the DIT input tile, so the
+// coefficients never round-trip through HBM.  bitrev_out: the whole transform fits the tile.
+template <int LOGR>
+__global__ __launch_bounds__(NT) void k_lde_fused(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, int L,
+                                                  const uint32_t *__restrict__ tw_inv,
+                                                  const uint32_t *__restrict__ tw_fwd, Twist tws, uint64_t dst_half,
+                                                  int bitrev_out) {
+    constexpr int R = 1 << LOGR;
+    __shared__ uint32_t a[R];
+    __shared__ uint32_t x[R];
+    const uint32_t base = blockIdx.x * (uint32_t)R;
+    const uint32_t *sp = src + ms.off(blockIdx.y) + base;
+    for (int i = threadIdx.x; i < R; i += NT) a[i] = sp[i];
+    __syncthreads();
+    tile_stages<LOGR, 1, 1, false>(a, tw_inv, 1, 0);
+    uint32_t *dcol = dst + md.off(blockIdx.y);
+    for (int e = 0; e < 2; e++) {
+        for (int i = threadIdx.x; i < R; i += NT) x[i] = mul(a[i], tws.f(e, rev_bits(base + i, L)));
         __syncthreads();
-        tile_stages<LOGR, 1, DIT>(x, tw, 1, 0);
-        uint32_t *dp = dst + md.off(blockIdx.y) + (uint64_t)e * dst_half;
+        tile_stages<LOGR, 1, 1, true>(x, tw_fwd, 1, 0);
+        uint32_t *dp = dcol + (uint64_t)e * dst_half;
         if (!bitrev_out) {
             for (int i = threadIdx.x; i < R; i += NT) dp[base + i] = x[i];
         } else {
@@ -252,43 +300,73 @@ __global__ __launch_bounds__(NT) void k_ntt_contig(const uint32_t *src, uint32_t
 }
 
 // ------------------------------------------------------------------ dispatch
+static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
+static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
+
+static int strided_T(int logR) { return logR >= 9 ? 32 : 64; }
+
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
-                        int logS, const uint32_t *tw, int bitrev_out, hipStream_t s, Twist tws = Twist{},
-                        int twist_out = 0, uint64_t dst_half = 0) {
-    uint64_t tiles = (1ull << L) >> (logR + 6);
-    dim3 g((unsigned)tiles, nv);
-#define SCASE(k) \
-    case k: hipLaunchKernelGGL((k_ntt_strided<k, DIT>), g, dim3(NT), 0, s, src, dst, ms, md, L, logS, tw, bitrev_out, tws, twist_out, dst_half); break;
-    switch (logR) { SCASE(1) SCASE(2) SCASE(3) SCASE(4) SCASE(5) SCASE(6) default: throw ArgError("bad strided radix"); }
+                        int logS, const uint32_t *tw, int mode, hipStream_t s, Twist tws = Twist{},
+                        uint64_t dst_half = 0) {
+    const int T = strided_T(logR);
+    ARG_CHECK((1 << logS) >= T, "strided pass narrower than its tile");
+    dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
+#define SCASE(k, t)                                                                                             \
+    case k:                                                                                                     \
+        hipLaunchKernelGGL((k_ntt_strided<k, t, DIT>), g, dim3(NT), 0, s, src, dst, ms, md, logS, tw, mode, tws, \
+                           dst_half);                                                                           \
+        break;
+    switch (logR) {
+        SCASE(1, 64) SCASE(2, 64) SCASE(3, 64) SCASE(4, 64) SCASE(5, 64) SCASE(6, 64) SCASE(7, 64) SCASE(8, 64)
+        SCASE(9, 32)
+        default: throw ArgError("bad strided radix");
+    }
 #undef SCASE
     HIP_CHECK(hipGetLastError());
 }
 
 template <bool DIT>
 static void run_contig(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
-                       const uint32_t *tw, int bitrev_out, Twist tws, int use_twist, uint64_t dst_half, hipStream_t s) {
-    uint64_t tiles = (1ull << L) >> logR;
-    dim3 g((unsigned)tiles, nv);
-#define CCASE(k)                                                                                             \
-    case k:                                                                                                  \
-        hipLaunchKernelGGL((k_ntt_contig<k, DIT>), g, dim3(NT), 0, s, src, dst, ms, md, L, tw, bitrev_out, tws, \
-                           use_twist, dst_half);                                                             \
+                       const uint32_t *tw, int mode, Twist tws, uint64_t dst_half, hipStream_t s) {
+    dim3 g((unsigned)((1ull << L) >> logR), nv);
+#define CCASE(k)                                                                                                 \
+    case k:                                                                                                      \
+        hipLaunchKernelGGL((k_ntt_contig<k, DIT>), g, dim3(NT), 0, s, src, dst, ms, md, tw, mode, tws, dst_half); \
         break;
     switch (logR) {
         CCASE(1) CCASE(2) CCASE(3) CCASE(4) CCASE(5) CCASE(6) CCASE(7) CCASE(8) CCASE(9) CCASE(10) CCASE(11) CCASE(12)
+        CCASE(13)
         default: throw ArgError("bad contiguous radix");
     }
 #undef CCASE
     HIP_CHECK(hipGetLastError());
 }
 
+static void run_fused(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
+                      const uint32_t *tw_inv, const uint32_t *tw_fwd, Twist tws, uint64_t dst_half, int bitrev_out,
+                      hipStream_t s) {
+    dim3 g((unsigned)((1ull << L) >> logR), nv);
+#define FCASE(k)                                                                                                    \
+    case k:                                                                                                         \
+        hipLaunchKernelGGL((k_lde_fused<k>), g, dim3(NT), 0, s, src, dst, ms, md, L, tw_inv, tw_fwd, tws, dst_half, \
+                           bitrev_out);                                                                             \
+        break;
+    switch (logR) {
+        FCASE(1) FCASE(2) FCASE(3) FCASE(4) FCASE(5) FCASE(6) FCASE(7) FCASE(8) FCASE(9) FCASE(10) FCASE(11) FCASE(12)
+        FCASE(13)
+        default: throw ArgError("bad fused radix");
+    }
+#undef FCASE
+    HIP_CHECK(hipGetLastError());
+}
+
 // strided pass radices for the bits above the contiguous tile (top to bottom, i.e. DIF order)
 static std::vector<int> strided_plan(int L, int &logC) {
-    logC = L < LOGC_MAX ? L : LOGC_MAX;
+    logC = L < LOGC ? L : LOGC;
     int rem = L - logC;
     std::vector<int> p;
-    int np = (rem + LOGS_MAX - 1) / LOGS_MAX;
+    int np = (rem + LOGS - 1) / LOGS;
     for (int i = 0; i < np; i++) {
         int b = rem / (np - i);
         p.push_back(b);
@@ -342,27 +420,28 @@ void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hip
     const uint32_t nv = (uint32_t)W;
     ColMap m_src{N, 0, 1}, m_dst1{2 * N, 0, 1}, m_dst2{2 * N, N, 2};
     if (sp.empty()) {
-        run_contig<true>(logC, src.d, dst.d, m_src, m_dst1, nv, L, c.tw_inv, 0, tws, 2, N, s);
+        run_contig<true>(logC, src.d, dst.d, m_src, m_dst1, nv, L, c.tw_inv, MODE_TWIST_OUT, tws, N, s);
     } else {
         DBuf work(N * W, s);
-        run_contig<true>(logC, src.d, work.p, m_src, m_src, nv, L, c.tw_inv, 0, tws, 0, 0, s);
+        run_contig<true>(logC, src.d, work.p, m_src, m_src, nv, L, c.tw_inv, MODE_PLAIN, tws, 0, s);
         int logS = logC;
         for (int i = (int)sp.size() - 1; i >= 0; i--) {
             const bool last = (i == 0);
             run_strided<true>(sp[i], work.p, last ? dst.d : work.p, m_src, last ? m_dst1 : m_src, nv, L, logS,
-                              c.tw_inv, 0, s, tws, last ? 1 : 0, N);
+                              c.tw_inv, last ? MODE_TWIST_OUT : MODE_PLAIN, s, tws, N);
             logS += sp[i];
         }
     }
-    // forward DIF in place on both halves
     int logS = L;
     for (size_t i = 0; i < sp.size(); i++) {
         logS -= sp[i];
-        run_strided<false>(sp[i], dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, logS, c.tw_fwd, 0, s);
+        run_strided<false>(sp[i], dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, logS, c.tw_fwd, MODE_PLAIN, s);
     }
-    run_contig<false>(logC, dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, c.tw_fwd, 0, Twist{}, 0, 0, s);
+    run_contig<false>(logC, dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, c.tw_fwd, MODE_PLAIN, Twist{}, 0, s);
 }
 
+// Natural-input LDE (traces):  [strided DIF iNTT passes] -> fused {contiguous DIF iNTT, twists,
+// contiguous DIT forward x2} -> [strided DIT forward passes, the last writing bit-reversed rows].
 void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s) {
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
@@ -373,42 +452,30 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
     ARG_CHECK(dst.height == 2 * N && dst.width == W, "LDE destination shape");
     int logC;
     std::vector<int> sp = strided_plan(L, logC);
-
     const Twist tws = get_twist(c, N, L, shift, s);
-
+    const uint32_t nv = (uint32_t)W;
+    ColMap m_src{N, 0, 1}, m_w1{2 * N, 0, 1}, m_w2{2 * N, N, 2};
+    if (sp.empty()) {
+        run_fused(logC, src.d, dst.d, m_src, m_w1, nv, L, c.tw_inv, c.tw_fwd, tws, N, 1, s);
+        return;
+    }
     // work buffer: per column 2N ([E0 | E1]); the iNTT runs in its first half
     DBuf work(2 * N * W, s);
-    ColMap m_src{N, 0, 1};
-    ColMap m_w1{2 * N, 0, 1};       // one virtual column per column, first half
-    ColMap m_w2{2 * N, N, 2};       // two virtual columns per column (E0, E1)
-    ColMap m_dst2{2 * N, N, 2};     // LDE halves
-    const uint32_t nv = (uint32_t)W;
-
-    // 1. iNTT (DIF, inverse twiddles): strided passes top-down, then contiguous
     const uint32_t *in = src.d;
     ColMap min = m_src;
     int logS = L;
     for (size_t i = 0; i < sp.size(); i++) {
         logS -= sp[i];
-        run_strided<false>(sp[i], in, work.p, min, m_w1, nv, L, logS, c.tw_inv, 0, s);
+        run_strided<false>(sp[i], in, work.p, min, m_w1, nv, L, logS, c.tw_inv, MODE_PLAIN, s);
         in = work.p;
         min = m_w1;
     }
-    run_contig<false>(logC, in, work.p, min, m_w1, nv, L, c.tw_inv, 0, tws, 0, 0, s);
-
-    // 2./3. forward DIT for E0 and E1
-    const bool single = sp.empty();
-    if (single) {
-        // twist + full transform + bit-reversed write straight into the LDE
-        run_contig<true>(logC, work.p, dst.d, m_w1, m_w1, nv, L, c.tw_fwd, 1, tws, 1, N, s);
-        return;
-    }
-    run_contig<true>(logC, work.p, work.p, m_w1, m_w1, nv, L, c.tw_fwd, 0, tws, 1, N, s);
+    run_fused(logC, work.p, work.p, m_w1, m_w1, nv, L, c.tw_inv, c.tw_fwd, tws, N, 0, s);
     logS = logC;
     for (int i = (int)sp.size() - 1; i >= 0; i--) {
         const bool last = (i == 0);
-        run_strided<true>(sp[i], work.p, last ? dst.d : work.p, m_w2, last ? m_dst2 : m_w2, 2 * nv, L, logS, c.tw_fwd,
-                          last ? 1 : 0, s);
+        run_strided<true>(sp[i], work.p, last ? dst.d : work.p, m_w2, last ? m_w2 : m_w2, 2 * nv, L, logS, c.tw_fwd,
+                          last ? MODE_BITREV_OUT : MODE_PLAIN, s);
         logS += sp[i];
     }
 }

@@ -70,25 +70,26 @@ KB_HD void internal_layer(uint32_t s[16]) {
     uint32_t sum = 0;
 #pragma unroll
     for (int i = 0; i < 16; i++) sum = add(sum, s[i]);
-    uint32_t d[16];
-    d[0] = neg(dbl(s[0]));
-    d[1] = s[1];
-    d[2] = dbl(s[2]);
-    d[3] = div_pow2(s[3], 1);
-    d[4] = add(dbl(s[4]), s[4]);
-    d[5] = dbl(dbl(s[5]));
-    d[6] = neg(div_pow2(s[6], 1));
-    d[7] = neg(add(dbl(s[7]), s[7]));
-    d[8] = neg(dbl(dbl(s[8])));
-    d[9] = div_pow2(s[9], 8);
-    d[10] = div_pow2(s[10], 3);
-    d[11] = div_pow2(s[11], 24);
-    d[12] = neg(div_pow2(s[12], 8));
-    d[13] = neg(div_pow2(s[13], 3));
-    d[14] = neg(div_pow2(s[14], 4));
-    d[15] = neg(div_pow2(s[15], 24));
-#pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = add(d[i], sum);
+    // s_i <- V_i s_i + sum; negative V_i as sum - |V_i| s_i
+    const uint32_t x0 = dbl(s[0]), x6 = div_pow2(s[6], 1), x7 = add(dbl(s[7]), s[7]), x8 = dbl(dbl(s[8]));
+    const uint32_t x12 = div_pow2(s[12], 8), x13 = div_pow2(s[13], 3), x14 = div_pow2(s[14], 4);
+    const uint32_t x15 = div_pow2(s[15], 24);
+    s[0] = sub(sum, x0);
+    s[1] = add(s[1], sum);
+    s[2] = add(dbl(s[2]), sum);
+    s[3] = add(div_pow2(s[3], 1), sum);
+    s[4] = add(add(dbl(s[4]), s[4]), sum);
+    s[5] = add(dbl(dbl(s[5])), sum);
+    s[6] = sub(sum, x6);
+    s[7] = sub(sum, x7);
+    s[8] = sub(sum, x8);
+    s[9] = add(div_pow2(s[9], 8), sum);
+    s[10] = add(div_pow2(s[10], 3), sum);
+    s[11] = add(div_pow2(s[11], 24), sum);
+    s[12] = sub(sum, x12);
+    s[13] = sub(sum, x13);
+    s[14] = sub(sum, x14);
+    s[15] = sub(sum, x15);
 }
 
 KB_HD void permute(uint32_t s[16]) {
