@@ -124,6 +124,11 @@ int zkm_poseidon2_permute(zkm_ctx *ctx, uint32_t *states, uint64_t n);
 /* Timing helper: runs `iters` LDEs of a resident random h x w matrix, returns average ms of the
  * whole LDE and of each kernel stage via HIP events (see bench.py). */
 int zkm_bench_lde(zkm_ctx *ctx, uint64_t h, uint64_t w, int iters, double *ms_out);
+/* Generates and compiles (hiprtc, gfx950, no device needed) the per-chip specialised quotient
+ * kernels zkm_setup builds for this machine blob; returns the total code-object size.  Build /
+ * codegen check only.  zkm_setup compiles the same kernels (set ZKM_NO_JIT=1 to use the generic
+ * interpreter kernel instead; ZKM_JIT_DUMP=<dir> writes the generated sources). */
+int zkm_quotient_jit_compile(const uint32_t *blob, size_t nwords, uint64_t *code_bytes);
 
 /* ---- stage profiling (HIP events on the launching stream; see bench.py) ----
  * zkm_profile_dump writes lines "stage count total_ms units" and returns the bytes needed. */

@@ -1,0 +1,284 @@
+// JIT-specialised quotient kernels (hiprtc, gfx950).
+//
+// At setup (MachineProver::setup / pk_to_device) every chip's constraint program and lookup
+// descriptors are lowered to straight-line HIP: column reads are hoisted to the top of the kernel
+// (so their HBM latency overlaps), constants and VirtualPairCol weights become literals, LogUp
+// batches are unrolled, and the folding sum(alpha^(n-1-k) C_k) keeps the reference's constraint
+// order (crates/stark/src/folder.rs:79-102, permutation.rs:256-346).  The generic interpreter
+// kernel (open_kernels.hip k_quotient) remains as the GPU path when JIT compilation is disabled
+// (ZKM_NO_JIT=1) or fails.
+#include "jit.hpp"
+
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <sstream>
+
+#include "jit_prelude.inc"
+
+namespace zkm {
+
+int guard_status(const std::exception &e);  // capi.cpp
+
+namespace {
+
+std::string hex(uint32_t v) {
+    char b[16];
+    snprintf(b, sizeof b, "0x%08xu", v);
+    return b;
+}
+
+struct Gen {
+    std::ostringstream body;
+    int tmp = 0;
+    std::map<std::string, std::string> loads;  // load expr -> variable
+    std::ostringstream head;
+    std::string var(const std::string &prefix) { return prefix + std::to_string(tmp++); }
+    // hoisted column read
+    std::string col(const char *arr, uint32_t c, const char *row) {
+        std::string key = std::string(arr) + "_" + std::to_string(c) + "_" + row;
+        auto it = loads.find(key);
+        if (it != loads.end()) return it->second;
+        std::string v = "c_" + key;
+        head << "    const uint32_t " << v << " = A." << arr << "[(uint64_t)" << c << " * A.ld + " << row << "];\n";
+        loads[key] = v;
+        return v;
+    }
+};
+
+// value of a VirtualPairCol at the local row
+std::string vpc_expr(Gen &g, const VPC &v) {
+    std::string acc = kb::to_mont(v.constant) ? hex(kb::to_mont(v.constant)) : "";
+    for (size_t i = 0; i < v.cols.size(); i++) {
+        const uint32_t col = v.cols[i];
+        const std::string x = (col & 0x80000000u) ? g.col("main", col & 0x7fffffffu, "rl") : g.col("prep", col, "rl");
+        const uint32_t w = kb::to_mont(v.weights[i]);
+        std::string term = (w == kb::ONE) ? x : "mul(" + x + ", " + hex(w) + ")";
+        acc = acc.empty() ? term : "add(" + acc + ", " + term + ")";
+    }
+    if (acc.empty()) acc = "0u";
+    std::string t = g.var("v");
+    g.body << "    const uint32_t " << t << " = " << acc << ";\n";
+    return t;
+}
+
+std::string gen_source(const ChipDesc &c, const std::string &fname) {
+    Gen g;
+    std::ostringstream o;
+    int k = 0;  // constraint index
+    auto emit_base = [&](const std::string &x) {
+        g.body << "    acc = ef_add(acc, ef_mul_base(POW(" << k << "), " << x << "));\n";
+        k++;
+    };
+    auto emit_ext = [&](const std::string &x) {
+        g.body << "    acc = ef_add(acc, ef_mul(POW(" << k << "), " << x << "));\n";
+        k++;
+    };
+    // ---- AIR program -> straight-line code ----
+    std::vector<std::string> st;
+    for (size_t pc = 0; pc < c.code.size();) {
+        const uint32_t op = c.code[pc++];
+        switch (op) {
+        case OP_MAIN_L: st.push_back(g.col("main", c.code[pc++], "rl")); break;
+        case OP_MAIN_N: st.push_back(g.col("main", c.code[pc++], "rn")); break;
+        case OP_PREP_L: st.push_back(g.col("prep", c.code[pc++], "rl")); break;
+        case OP_PREP_N: st.push_back(g.col("prep", c.code[pc++], "rn")); break;
+        case OP_CONST: st.push_back(hex(kb::to_mont(c.code[pc++]))); break;
+        case OP_PV: st.push_back("A.pv[" + std::to_string(c.code[pc++]) + "]"); break;
+        case OP_IS_FIRST: st.push_back("is_first"); break;
+        case OP_IS_LAST: st.push_back("is_last"); break;
+        case OP_IS_TRANS: st.push_back("is_trans"); break;
+        case OP_ADD: case OP_SUB: case OP_MUL: {
+            std::string b = st.back(); st.pop_back();
+            std::string a = st.back(); st.pop_back();
+            std::string t = g.var("t");
+            const char *f = op == OP_ADD ? "add" : op == OP_SUB ? "sub" : "mul";
+            g.body << "    const uint32_t " << t << " = " << f << "(" << a << ", " << b << ");\n";
+            st.push_back(t);
+            break;
+        }
+        case OP_NEG: {
+            std::string a = st.back(); st.pop_back();
+            std::string t = g.var("t");
+            g.body << "    const uint32_t " << t << " = neg(" << a << ");\n";
+            st.push_back(t);
+            break;
+        }
+        case OP_EMIT: {
+            std::string a = st.back(); st.pop_back();
+            emit_base(a);
+            break;
+        }
+        default: throw ArgError("bad opcode in JIT");
+        }
+    }
+    // ---- LogUp constraints (permutation.rs:256-333) ----
+    const int nloc = (int)c.local.size();
+    if (nloc) {
+        const int batch = 1 << c.log_qd, nb = c.perm_w - 1;
+        std::vector<std::string> el, en;
+        for (int b = 0; b <= nb; b++) {
+            std::string l = g.var("pl"), n_ = g.var("pn");
+            std::string le = "ef{{", ne = "ef{{";
+            for (int e = 0; e < 4; e++) {
+                le += (e ? ", " : "") + g.col("perm", 4 * b + e, "rl");
+                ne += (e ? ", " : "") + g.col("perm", 4 * b + e, "rn");
+            }
+            g.body << "    const ef " << l << " = " << le << "}};\n";
+            g.body << "    const ef " << n_ << " = " << ne << "}};\n";
+            el.push_back(l);
+            en.push_back(n_);
+        }
+        for (int b = 0; b < nb; b++) {
+            std::string prod = g.var("pr"), num = g.var("nu");
+            g.body << "    ef " << prod << " = ef_one(), " << num << " = ef_zero();\n";
+            for (int i = b * batch; i < nloc && i < (b + 1) * batch; i++) {
+                const LookupDesc &lk = c.local[i];
+                std::string rlc = g.var("r");
+                g.body << "    ef " << rlc << " = ef_add_base(alpha_p, " << hex(kb::to_mont(lk.kind)) << ");\n";
+                for (size_t v = 0; v < lk.values.size(); v++) {
+                    std::string x = vpc_expr(g, lk.values[v]);
+                    g.body << "    " << rlc << " = ef_add(" << rlc << ", ef_mul_base(BPOW(" << v << "), " << x << "));\n";
+                }
+                std::string m = vpc_expr(g, lk.mult);
+                if (!lk.is_send) {
+                    std::string t = g.var("t");
+                    g.body << "    const uint32_t " << t << " = neg(" << m << ");\n";
+                    m = t;
+                }
+                g.body << "    " << num << " = ef_add(ef_mul(" << num << ", " << rlc << "), ef_mul_base(" << prod << ", " << m << "));\n";
+                g.body << "    " << prod << " = ef_mul(" << prod << ", " << rlc << ");\n";
+            }
+            std::string cc = g.var("cc");
+            g.body << "    const ef " << cc << " = ef_sub(ef_mul(" << prod << ", " << el[b] << "), " << num << ");\n";
+            emit_ext(cc);
+        }
+        std::string sl = g.var("sl"), sn = g.var("sn");
+        g.body << "    ef " << sl << " = ef_zero(), " << sn << " = ef_zero();\n";
+        for (int b = 0; b < nb; b++)
+            g.body << "    " << sl << " = ef_add(" << sl << ", " << el[b] << "); " << sn << " = ef_add(" << sn << ", " << en[b] << ");\n";
+        emit_ext("ef_mul_base(ef_sub(" + el[nb] + ", " + sl + "), is_first)");
+        emit_ext("ef_mul_base(ef_sub(ef_sub(" + en[nb] + ", " + el[nb] + "), " + sn + "), is_trans)");
+        emit_ext("ef_mul_base(ef_sub(" + el[nb] + ", lcs), is_last)");
+    }
+    if (c.scope == 1) {
+        for (int i = 0; i < 7; i++) {
+            emit_base("mul(sub(" + g.col("main", c.main_w - 14 + i, "rl") + ", A.gcs[" + std::to_string(i) + "]), is_last)");
+            emit_base("mul(sub(" + g.col("main", c.main_w - 7 + i, "rl") + ", A.gcs[" + std::to_string(7 + i) + "]), is_last)");
+        }
+    }
+    ARG_CHECK(k == c.n_constraints, "JIT constraint count mismatch");
+
+    o << "typedef unsigned int uint32_t;\ntypedef unsigned long long uint64_t;\n"
+      << kJitPrelude << "\nusing namespace kb;\n"
+      << "#define POW(k) ef{{A.pows[4*(k)], A.pows[4*(k)+1], A.pows[4*(k)+2], A.pows[4*(k)+3]}}\n"
+      << "#define BPOW(v) ef{{A.beta_pows[4*(v)], A.beta_pows[4*(v)+1], A.beta_pows[4*(v)+2], A.beta_pows[4*(v)+3]}}\n"
+      << "extern \"C\" __global__ void __launch_bounds__(256) " << fname << "(const ZkmQuotJitArgs A) {\n"
+      << "    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n"
+      << "    if (t >= A.q) return;\n"
+      << "    const uint64_t rl = t;\n"
+      << "    const uint64_t k = rev_bits((uint32_t)t, A.log_q);\n"
+      << "    const uint64_t kn = (k + A.step) & (A.q - 1);\n"
+      << "    const uint64_t rn = rev_bits((uint32_t)kn, A.log_q);\n"
+      << "    const uint64_t hq = A.q >> 1;\n"
+      << "    const uint32_t om = k < hq ? A.tw[hq + k] : neg(A.tw[hq + (k - hq)]);\n"
+      << "    const uint32_t x = mul(A.gen, om);\n"
+      << "    const uint32_t zh = (A.q == 2 * A.n) ? ((k & 1) ? sub(neg(A.gen_pow_n), ONE) : sub(A.gen_pow_n, ONE)) : sub(A.gen_pow_n, ONE);\n"
+      << "    const uint32_t d_first = sub(x, ONE), d_last = sub(x, A.wn_inv);\n"
+      << "    const uint32_t inv_fl = inv(mul(mul(d_first, d_last), zh));\n"
+      << "    const uint32_t zh2 = mul(zh, zh);\n"
+      << "    const uint32_t is_first = mul(mul(inv_fl, d_last), zh2);\n"
+      << "    const uint32_t is_last = mul(mul(inv_fl, d_first), zh2);\n"
+      << "    const uint32_t is_trans = d_last;\n"
+      << "    const uint32_t inv_z = mul(inv_fl, mul(d_first, d_last));\n"
+      << "    const ef alpha_p = ef{{A.alpha_p[0], A.alpha_p[1], A.alpha_p[2], A.alpha_p[3]}};\n"
+      << "    const ef lcs = ef{{A.lcs[0], A.lcs[1], A.lcs[2], A.lcs[3]}};\n"
+      << "    (void)is_first; (void)is_last; (void)is_trans; (void)alpha_p; (void)lcs;\n"
+      << g.head.str()
+      << "    ef acc = ef_zero();\n"
+      << g.body.str()
+      << "    const ef qv = ef_mul_base(acc, inv_z);\n"
+      << "    const uint64_t c = t >> A.log_n, pos = t & (A.n - 1);\n"
+      << "    A.chunks[(c * 4 + 0) * A.n + pos] = qv.c[0];\n"
+      << "    A.chunks[(c * 4 + 1) * A.n + pos] = qv.c[1];\n"
+      << "    A.chunks[(c * 4 + 2) * A.n + pos] = qv.c[2];\n"
+      << "    A.chunks[(c * 4 + 3) * A.n + pos] = qv.c[3];\n"
+      << "}\n";
+    return o.str();
+}
+
+}  // namespace
+
+bool jit_enabled() {
+    const char *e = getenv("ZKM_NO_JIT");
+    return !(e && *e && *e != '0');
+}
+
+static const char *kJitName = "zkm_quot_jit";
+
+std::vector<char> jit_quotient_code(const ChipDesc &c, const std::string &arch_name) {
+    const std::string src = gen_source(c, kJitName);
+    if (const char *d = getenv("ZKM_JIT_DUMP")) {
+        if (FILE *f = fopen((std::string(d) + "/" + c.name + ".hip").c_str(), "w")) {
+            fputs(src.c_str(), f);
+            fclose(f);
+        }
+    }
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "quotient_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+        throw HipError("hiprtcCreateProgram failed");
+    std::string arch = "--offload-arch=" + arch_name;
+    const char *opts[] = {arch.c_str(), "-O3", "-std=c++17"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        hiprtcGetProgramLogSize(prog, &ls);
+        std::string log(ls + 1, '\0');
+        hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        throw HipError("hiprtc compile failed for chip " + c.name + ": " + log.substr(0, 2000));
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    std::vector<char> code(cs);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    return code;
+}
+
+JitKernel jit_quotient(const ChipDesc &c, int device) {
+    JitKernel k;
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    std::string arch = prop.gcnArchName;
+    arch = arch.substr(0, arch.find(':'));  // "gfx950:sramecc+:xnack-" -> "gfx950"
+    k.code = jit_quotient_code(c, arch);
+    HIP_CHECK(hipModuleLoadData(&k.mod, k.code.data()));
+    HIP_CHECK(hipModuleGetFunction(&k.fn, k.mod, kJitName));
+    k.ok = true;
+    return k;
+}
+
+void launch_quotient_jit(const JitKernel &k, const ZkmQuotJitArgs &a, hipStream_t s) {
+    ZkmQuotJitArgs args = a;
+    void *params[] = {&args};
+    const unsigned grid = (unsigned)((a.q + 255) / 256);
+    HIP_CHECK(hipModuleLaunchKernel(k.fn, grid, 1, 1, 256, 1, 1, 0, s, params, nullptr));
+}
+
+}  // namespace zkm
+
+extern "C" int zkm_quotient_jit_compile(const uint32_t *blob, size_t nwords, uint64_t *code_bytes) {
+    try {
+        ARG_CHECK(blob && code_bytes, "null argument");
+        const zkm::Machine m = zkm::parse_machine(blob, nwords);
+        uint64_t total = 0;
+        for (const auto &c : m.chips) total += zkm::jit_quotient_code(c, "gfx950").size();
+        *code_bytes = total;
+        return 0;
+    } catch (const std::exception &e) {
+        return zkm::guard_status(e);
+    }
+}

@@ -11,10 +11,12 @@
 #include <algorithm>
 #include <array>
 #include <cstring>
+#include <future>
 #include <numeric>
 
 #include "../../include/zkm_hip.h"
 #include "chip.hpp"
+#include "jit.hpp"
 #include "internal.hpp"
 #include "open_kernels.hpp"
 #include "p2.cuh"
@@ -95,6 +97,11 @@ struct Pk {
     std::vector<DBuf> traces;  // column-major natural (Montgomery)
     DTree tree;                // LDEs owned by tree.owned
     std::vector<DBuf> progs;   // flattened chip programs (device)
+    std::vector<JitKernel> jit;  // per-chip specialised quotient kernels (jit.cpp); !ok -> interpreter
+    ~Pk() {
+        for (auto &k : jit)
+            if (k.mod) (void)hipModuleUnload(k.mod);
+    }
     int pk_index(int chip) const {
         for (size_t i = 0; i < trace_chip.size(); i++)
             if (trace_chip[i] == chip) return (int)i;
@@ -338,7 +345,21 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         memcpy(qa.gcs, proof.chips[i].gcs, sizeof qa.gcs);
         qa.batch = 1 << lqd; qa.perm_w = cd.perm_w; qa.global = cd.scope == 1; qa.main_w = cd.main_w;
         qa.chunks = q_chunks[i].p;
-        { PROF("quotient", s, 8.0 * Q * (cd.main_w + cd.prep_w + 4 * cd.perm_w) + 16.0 * Q); launch_quotient(qa, s); }
+        {
+            PROF("quotient", s, 8.0 * Q * (cd.main_w + cd.prep_w + 4 * cd.perm_w) + 16.0 * Q);
+            const JitKernel &jk = pk.jit[md.chip[i]];
+            if (jk.ok) {
+                ZkmQuotJitArgs ja{};
+                ja.main = qa.main; ja.prep = qa.prep; ja.perm = qa.perm; ja.pv = qa.pv; ja.pows = qa.pows;
+                ja.beta_pows = qa.beta_pows; ja.tw = qa.tw; ja.chunks = qa.chunks;
+                ja.ld = qa.ld; ja.n = qa.n; ja.q = qa.q; ja.log_n = qa.log_n; ja.log_q = qa.log_q; ja.step = qa.step;
+                ja.gen = qa.gen; ja.gen_pow_n = qa.gen_pow_n; ja.wn_inv = qa.wn_inv;
+                memcpy(ja.alpha_p, qa.alpha_p.c, 16); memcpy(ja.lcs, qa.lcs.c, 16); memcpy(ja.gcs, qa.gcs, sizeof ja.gcs);
+                launch_quotient_jit(jk, ja, s);
+            } else {
+                launch_quotient(qa, s);
+            }
+        }
         HIP_CHECK(hipStreamSynchronize(s));  // d_pows lifetime
         const uint32_t wq = two_adic_gen(logN + lqd);
         for (int j = 0; j < (1 << lqd); j++) {
@@ -695,6 +716,23 @@ int zkm_setup(zkm_ctx *ctx, const uint32_t *blob, size_t nwords, const zkm_confi
         pk->progs.emplace_back(f.size(), L.s);
         HIP_CHECK(hipMemcpyAsync(pk->progs.back().p, f.data(), f.size() * 4, hipMemcpyHostToDevice, L.s));
         HIP_CHECK(hipStreamSynchronize(L.s));
+    }
+    pk->jit.resize(pk->m.chips.size());
+    if (jit_enabled()) {
+        // hiprtc compiles are independent per chip: run them concurrently
+        std::vector<std::future<JitKernel>> fut;
+        for (auto &cd : pk->m.chips)
+            fut.push_back(std::async(std::launch::async, [&cd, dev = c->device] {
+                (void)hipSetDevice(dev);
+                try {
+                    return jit_quotient(cd, dev);
+                } catch (const std::exception &e) {
+                    fprintf(stderr, "zkm: quotient JIT failed for chip %s, using the interpreter kernel: %s\n",
+                            cd.name.c_str(), e.what());
+                    return JitKernel{};
+                }
+            }));
+        for (size_t i = 0; i < fut.size(); i++) pk->jit[i] = fut[i].get();
     }
     // preprocessed traces sorted by (height desc, name) (machine.rs:383-384)
     std::vector<int> chips;
