@@ -57,7 +57,7 @@ def prove_resident(prover, dev_traces, pvs):
     return b
 
 
-STAGE_KERNEL = {"merkle_leaves": "k_hash_leaves", "merkle_nodes": "k_compress_level", "quotient": "k_quotient",
+STAGE_KERNEL = {"merkle_leaves": "k_hash_leaves", "merkle_nodes": "k_compress_level", "quotient": "zkm_quot_jit",
                 "fri_reduce": "k_fri_reduce", "perm_trace": "k_perm_rows", "open_eval": "k_open_dot"}
 
 

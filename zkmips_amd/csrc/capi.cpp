@@ -87,12 +87,6 @@ int zkm_init(int device, zkm_ctx **out) {
         return ZKM_ERR_NO_DEVICE;
     }
     HIP_CHECK(hipSetDevice(device));
-    // Keep freed stream-ordered memory in the pool: the default release threshold (0) hands
-    // gigabytes back to the driver at every synchronisation and re-maps them for the next shard.
-    hipMemPool_t pool;
-    HIP_CHECK(hipDeviceGetDefaultMemPool(&pool, device));
-    uint64_t thr = ~0ull;
-    HIP_CHECK(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr));
     auto *c = new Ctx();
     c->device = device;
     build_twiddles(*c, 24);  // transforms up to 2^24 (two-adicity)
@@ -110,7 +104,8 @@ void zkm_destroy(zkm_ctx *ctx) {
     // context handle, and their stream-ordered buffers are released on the stream that made them.
     (void)hipFree(c->tw_fwd);
     (void)hipFree(c->tw_inv);
-    delete c;
+    delete c;       // cached twist tables go back to the pool
+    pool_trim();    // blocks still owned by live keys / shard data stay allocated
 }
 
 void zkm_free_bytes(uint8_t *p) { free(p); }

@@ -1,5 +1,6 @@
 // Internal declarations of the MI355X shard prover (not part of the C ABI).
 #pragma once
+#include "prof.hpp"
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -38,6 +39,12 @@ inline int ilog2(uint64_t n) {
     return l;
 }
 
+// Caching device allocator (pool.cpp): stream-tagged reuse of hipMalloc'd blocks.
+void *pool_alloc(size_t bytes, hipStream_t s);
+void pool_free(void *p, hipStream_t s);
+void pool_trim();  // synchronises the device, returns cached blocks to the driver
+void pool_stats(size_t *in_use, size_t *cached);
+
 // Stream-ordered device buffer.
 struct DBuf {
     uint32_t *p = nullptr;
@@ -45,7 +52,7 @@ struct DBuf {
     hipStream_t s = nullptr;
     DBuf() = default;
     DBuf(size_t n, hipStream_t st) : words(n), s(st) {
-        if (n) HIP_CHECK(hipMallocAsync((void **)&p, n * sizeof(uint32_t), st));
+        if (n) p = (uint32_t *)pool_alloc(n * sizeof(uint32_t), st);
     }
     DBuf(const DBuf &) = delete;
     DBuf &operator=(const DBuf &) = delete;
@@ -57,7 +64,7 @@ struct DBuf {
         return *this;
     }
     void reset() {
-        if (p) (void)hipFreeAsync(p, s);
+        if (p) pool_free(p, s);
         p = nullptr;
         words = 0;
     }

@@ -49,6 +49,21 @@ ProfScope::~ProfScope() {
     g_pending.push_back(Rec{name, e0, e1, units});
 }
 
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+HostScope::HostScope(const char *n) : name(n) {
+    if (g_prof_on.load(std::memory_order_relaxed)) t0 = now_ms();
+}
+HostScope::~HostScope() {
+    if (t0 < 0) return;
+    const double ms = now_ms() - t0;
+    std::lock_guard<std::mutex> g(g_mu);
+    Tot &t = g_tot[std::string("host:") + name];
+    t.count++;
+    t.ms += ms;
+}
+
 }  // namespace zkm
 
 extern "C" {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 
 namespace zkm {
 
@@ -18,8 +19,17 @@ struct ProfScope {
     ~ProfScope();
 };
 
+// host wall-clock of a scope (recorded as stage "host:<name>")
+struct HostScope {
+    const char *name;
+    double t0 = -1;
+    explicit HostScope(const char *n);
+    ~HostScope();
+};
+
 #define ZKM_PROF_CAT2(a, b) a##b
 #define ZKM_PROF_CAT(a, b) ZKM_PROF_CAT2(a, b)
+#define HPROF(name) ::zkm::HostScope ZKM_PROF_CAT(_hprof_, __LINE__)(name)
 #define PROF(name, stream, units) ::zkm::ProfScope ZKM_PROF_CAT(_prof_, __LINE__)(name, stream, units)
 
 }  // namespace zkm

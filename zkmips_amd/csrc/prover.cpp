@@ -616,6 +616,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             for (int l = 0; l < ftrees[rd].log_max; l++) item(ftrees[rd].layers[l] + ((pair >> l) ^ 1) * 8, 1, 8);
         }
     }
+    HPROF("gather_wait");
     DBuf ditems(items.size() * 2 + 2, s), dout(total + 1, s);
     HIP_CHECK(hipMemcpyAsync(ditems.p, items.data(), items.size() * 8, hipMemcpyHostToDevice, s));
     launch_gather((const uint64_t *)ditems.p, (uint32_t)(items.size() / 3), dout.p, s);
@@ -672,6 +673,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     }
     HIP_CHECK(hipStreamSynchronize(s));
     if (!final_ok) throw std::runtime_error("UNSATISFIED: FRI final polynomial is not constant");
+    HPROF("serialize");
     return serialize(proof, pk.cfg.proof_montgomery != 0);
 }
 
@@ -810,6 +812,7 @@ int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32
         chip.push_back(ci);
     }
     PROF("commit_total", L.s, 0);
+    HPROF("commit");
     for (int o : sort_order(hs, names)) {  // prover.rs:264
         md->chip.push_back(chip[o]);
         md->heights.push_back(hs[o]);
@@ -841,6 +844,7 @@ int zkm_open(zkm_ctx *ctx, const zkm_pk *p, zkm_main *mainp, zkm_challenger_t *c
     StreamLease L(c);
     Challenger ch;
     ch.load(*chs);
+    HPROF("open");
     std::vector<uint8_t> bytes = open_shard(*c, *pk, *md, ch, L.s);
     HIP_CHECK(hipStreamSynchronize(L.s));
     ch.store(*chs);
@@ -849,6 +853,7 @@ int zkm_open(zkm_ctx *ctx, const zkm_pk *p, zkm_main *mainp, zkm_challenger_t *c
     memcpy(buf, bytes.data(), bytes.size());
     *proof_out = buf;
     *proof_len = bytes.size();
+    HPROF("free_main");
     md.reset();
     return ZKM_OK;
     GUARD_END
