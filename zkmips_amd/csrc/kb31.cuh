@@ -52,10 +52,18 @@ KB_HD uint32_t redc(uint64_t t) {
     return umin(r, r + P);
 }
 KB_HD uint32_t mul(uint32_t a, uint32_t b) { return redc((uint64_t)a * b); }
+// a * b / R in (0, 2P), unreduced, for a * b < P * 2^32: adding P * 2^32 to the product lifts the
+// Montgomery quotient by P (same low word, so the same m) and no correction step is needed.
+KB_HD uint32_t mul_lazy(uint32_t a, uint32_t b) {
+    const uint64_t t = (uint64_t)a * b + ((uint64_t)P << 32);
+    const uint32_t m = (uint32_t)t * MU;
+    return (uint32_t)(t >> 32) - umulhi(m, P);
+}
 KB_HD uint32_t sqr(uint32_t a) { return mul(a, a); }
 KB_HD uint32_t to_mont(uint32_t x) { return mul(x % P, R2); }
 KB_HD uint32_t from_mont(uint32_t x) { return redc((uint64_t)x); }
-KB_HD uint32_t cube(uint32_t a) { return mul(sqr(a), a); }
+// a^2 stays lazy in (0, 2P): (2P) * a < P * 2^32 keeps the second reduction exact
+KB_HD uint32_t cube(uint32_t a) { return mul(mul_lazy(a, a), a); }
 
 KB_HD uint32_t pow(uint32_t a, uint64_t e) {
     uint32_t r = ONE;

@@ -75,36 +75,56 @@ __global__ void k_p2_batch(uint32_t *st, uint64_t n) {
     for (int k = 0; k < 16; k++) st[i * 16 + k] = s[k];
 }
 
+__global__ __launch_bounds__(NT) void k_p2_batch16(uint32_t *st, uint64_t n);
+
+// small batches are latency-bound: they take the 16-lane form
 void launch_poseidon2_batch(uint32_t *d, uint64_t n, hipStream_t s) {
     if (!n) return;
-    hipLaunchKernelGGL(k_p2_batch, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, d, n);
+    if (n <= 1024)
+        hipLaunchKernelGGL(k_p2_batch16, dim3((unsigned)((n * 16 + NT - 1) / NT)), dim3(NT), 0, s, d, n);
+    else
+        hipLaunchKernelGGL(k_p2_batch, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, d, n);
     HIP_CHECK(hipGetLastError());
 }
 
-static constexpr int NT_TOP = 256;
-static constexpr uint64_t TOP_MAX = 256;  // levels with <= TOP_MAX nodes are built by one workgroup
-static_assert(TOP_MAX <= NT_TOP, "one node per thread per level");
+// ---- latency-bound levels: one node per 16-lane row (p2x16) ----
+static constexpr uint64_t SMALL16 = 8192;  // levels with <= SMALL16 nodes use the 16-lane form
+static constexpr int NT_TOP = 1024;
+static constexpr uint64_t TOP_MAX = NT_TOP / 16;  // levels with <= TOP_MAX nodes: one workgroup
 
-// Builds `nlev` levels above `prev` (2*h1 digests) in one workgroup: level k has h1 >> k nodes and
-// is written contiguously to out (level 0 first).  Intermediate levels also live in LDS.
+__global__ __launch_bounds__(NT) void k_compress16(const uint32_t *__restrict__ prev, uint32_t *__restrict__ out,
+                                                   uint64_t h) {
+    const uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    const uint64_t i = t >> 4;
+    const int l = (int)(t & 15);
+    const p2x16::Lane c = p2x16::lane_consts(l);
+    const uint32_t x = p2x16::permute(i < h ? prev[i * 16 + l] : 0u, c);  // all lanes take part
+    if (i < h && l < 8) out[i * 8 + l] = x;
+}
+
+__global__ __launch_bounds__(NT) void k_p2_batch16(uint32_t *st, uint64_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    const uint64_t i = t >> 4;
+    const int l = (int)(t & 15);
+    const uint32_t x = p2x16::permute(i < n ? st[i * 16 + l] : 0u, p2x16::lane_consts(l));
+    if (i < n) st[i * 16 + l] = x;
+}
+
+// Builds `nlev` levels above `prev` (2*h1 digests, h1 <= TOP_MAX) in one workgroup: level k has
+// h1 >> k nodes and is written contiguously to out (level 0 first); levels also live in LDS.
 __global__ __launch_bounds__(NT_TOP) void k_tree_top(const uint32_t *__restrict__ prev, uint64_t h1, int nlev,
                                                      uint32_t *__restrict__ out) {
-    __shared__ uint32_t cur[TOP_MAX * 8];
+    __shared__ uint32_t buf[2][TOP_MAX * 8];
+    const int i = threadIdx.x >> 4, l = threadIdx.x & 15;
+    const p2x16::Lane c = p2x16::lane_consts(l);
     uint64_t h = h1, off = 0;
     for (int lev = 0; lev < nlev; lev++, h >>= 1) {
-        uint32_t res[8];
-        for (uint64_t i = threadIdx.x; i < h; i += NT_TOP) {
-            uint32_t s[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) s[k] = lev == 0 ? prev[i * 16 + k] : cur[i * 16 + k];
-            p2::permute(s);
-#pragma unroll
-            for (int k = 0; k < 8; k++) { res[k] = s[k]; out[(off + i) * 8 + k] = s[k]; }
+        const uint32_t *src = lev == 0 ? prev : buf[(lev - 1) & 1];
+        const uint32_t x = p2x16::permute((uint64_t)i < h ? src[i * 16 + l] : 0u, c);
+        if ((uint64_t)i < h && l < 8) {
+            buf[lev & 1][i * 8 + l] = x;
+            out[(off + i) * 8 + l] = x;
         }
-        __syncthreads();
-        for (uint64_t i = threadIdx.x; i < h; i += NT_TOP)
-#pragma unroll
-            for (int k = 0; k < 8; k++) cur[i * 8 + k] = res[k];
         __syncthreads();
         off += h;
     }
@@ -126,6 +146,7 @@ static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
         h >>= 1;
         bool later_inj = false;
         for (int k = L; k <= t.log_max; k++) later_inj |= inj[k].second != 0;
+        const int ninj = inj[L].second;
         if (h <= TOP_MAX && !later_inj) {
             // remaining levels L..log_max in one workgroup, one contiguous allocation
             const int nlev = t.log_max - L + 1;
@@ -139,7 +160,12 @@ static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
         }
         t.layer_store.emplace_back(h * 8, s);
         t.layers[L] = t.layer_store.back().p;
-        const int ninj = inj[L].second;
+        if (h <= SMALL16 && ninj == 0) {
+            hipLaunchKernelGGL(k_compress16, dim3((unsigned)((h * 16 + NT - 1) / NT)), dim3(NT), 0, s,
+                               (const uint32_t *)t.layers[L - 1], t.layers[L], h);
+            HIP_CHECK(hipGetLastError());
+            continue;
+        }
         hipLaunchKernelGGL(k_compress_level, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
                            (const uint32_t *)t.layers[L - 1], t.layers[L], h,
                            inj[L].first ? (const uint64_t *)inj[L].first->p : (const uint64_t *)nullptr, ninj);

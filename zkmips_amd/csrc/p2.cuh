@@ -114,6 +114,26 @@ KB_HD void permute(uint32_t s[16]) {
     }
 }
 
+// Internal-layer diagonal V (canonical), as field elements: air.rs:12-29
+constexpr uint32_t cx_inv2k(int k) {  // 2^-k mod p
+    uint64_t r = 1, h = (kb::P + 1) / 2;
+    for (int i = 0; i < k; i++) r = r * h % kb::P;
+    return (uint32_t)r;
+}
+constexpr uint32_t cx_neg(uint32_t x) { return x ? kb::P - x : 0; }
+struct DiagTable {
+    uint32_t v[16];
+};
+constexpr DiagTable make_diag() {
+    DiagTable d{};
+    const uint32_t canon[16] = {cx_neg(2), 1, 2, cx_inv2k(1), 3, 4, cx_neg(cx_inv2k(1)), cx_neg(3), cx_neg(4),
+                                cx_inv2k(8), cx_inv2k(3), cx_inv2k(24), cx_neg(cx_inv2k(8)), cx_neg(cx_inv2k(3)),
+                                cx_neg(cx_inv2k(4)), cx_neg(cx_inv2k(24))};
+    for (int i = 0; i < 16; i++) d.v[i] = cx_to_mont(canon[i]);
+    return d;
+}
+constexpr DiagTable DIAG = make_diag();
+
 // TruncatedPermutation<_,2,8,16>: perm(l || r)[0..8]
 KB_HD void compress(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
     uint32_t s[16];
@@ -125,3 +145,67 @@ KB_HD void compress(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
 }
 
 }  // namespace p2
+
+// Latency-optimised permutation: one state spread over a 16-lane row of the wavefront (lane l
+// holds s_l, 4 states per wave).  The linear layers become cross-lane DPP adds, so one
+// permutation is a ~5x shorter dependent chain than the one-thread form; it costs ~3x more lane
+// work, so it is used only where few permutations are in flight (tree tops, small levels,
+// transcript).  Every lane of the wave must execute it (DPP reads neighbour lanes).
+namespace p2x16 {
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int QP(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }
+constexpr int ROR(int k) { return 0x120 + k; }
+
+// external layer: M4 = circ(2,3,1,1) per 4-lane block (n_j = quad_sum + x_j + 2 x_{j+1}),
+// then the column sums over the four blocks (lanes j, j+4, j+8, j+12)
+__device__ __forceinline__ uint32_t external(uint32_t x) {
+    using namespace kb;
+    const uint32_t q = add(x, dpp<QP(1, 0, 3, 2)>(x));
+    const uint32_t S = add(q, dpp<QP(2, 3, 0, 1)>(q));
+    const uint32_t n = add(add(S, x), dbl(dpp<QP(1, 2, 3, 0)>(x)));
+    uint32_t c = add(n, dpp<ROR(4)>(n));
+    c = add(c, dpp<ROR(8)>(c));
+    return add(n, c);
+}
+
+__device__ __constant__ inline p2::RcTable kRc = p2::RC;
+__device__ __constant__ inline p2::DiagTable kDiag = p2::DIAG;
+
+// per-lane round constants (full rounds) and internal diagonal entry; l = lane within the row
+struct Lane {
+    uint32_t rc[8];
+    uint32_t dg;
+    int l;
+};
+__device__ __forceinline__ Lane lane_consts(int l) {
+    Lane c;
+#pragma unroll
+    for (int r = 0; r < 8; r++) c.rc[r] = kRc.ext[r][l];
+    c.dg = kDiag.v[l];
+    c.l = l;
+    return c;
+}
+
+__device__ __forceinline__ uint32_t permute(uint32_t x, const Lane &c) {
+    using namespace kb;
+    x = external(x);
+#pragma unroll
+    for (int r = 0; r < 4; r++) x = external(cube(add(x, c.rc[r])));
+#pragma unroll
+    for (int r = 0; r < 13; r++) {
+        const uint32_t y = cube(add(x, p2::RC.inr[r]));
+        x = (c.l == 0) ? y : x;
+        uint32_t s = add(x, dpp<ROR(1)>(x));
+        s = add(s, dpp<ROR(2)>(s));
+        s = add(s, dpp<ROR(4)>(s));
+        s = add(s, dpp<ROR(8)>(s));
+        x = add(mul(x, c.dg), s);
+    }
+#pragma unroll
+    for (int r = 4; r < 8; r++) x = external(cube(add(x, c.rc[r])));
+    return x;
+}
+}  // namespace p2x16
