@@ -220,7 +220,7 @@ void tree_build(DTree &t, hipStream_t s) {
     HIP_CHECK(hipStreamSynchronize(s));
 }
 
-void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s) {
+void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s, bool read_root) {
     ARG_CHECK(nleaves && (nleaves & (nleaves - 1)) == 0, "leaf count must be a power of two");
     t.log_max = ilog2(nleaves);
     t.layers.assign(t.log_max + 1, nullptr);
@@ -229,6 +229,7 @@ void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s) 
     t.layers[0] = t.layer_store.back().p;
     std::vector<std::pair<const DBuf *, int>> inj(t.log_max + 1, {nullptr, 0});
     build_levels(t, nleaves, inj, s);
+    if (!read_root) return;
     HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max], 32, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
 }

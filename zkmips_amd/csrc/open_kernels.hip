@@ -420,10 +420,12 @@ void launch_fri_reduce(const ReduceArgs &a, hipStream_t s) {
 
 // ------------------------------------------------------------------ FRI commit phase
 // next[i] = (1/2 + b/2 g^-rev(i)) lo + (1/2 - b/2 g^-rev(i)) hi + b^2 ro[i]; g = w_{2h}
-__global__ __launch_bounds__(NT) void k_fri_fold(const uint32_t *cur, uint64_t h, int log_h, ef half_beta, ef beta2,
+// fargs = (b/2, b^2) as two EF values, written on the device by k_fri_chal
+__global__ __launch_bounds__(NT) void k_fri_fold(const uint32_t *cur, uint64_t h, int log_h, const uint32_t *fargs,
                                                  const uint32_t *__restrict__ tw_inv, const uint32_t *ro, uint32_t *next) {
     const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (i >= h) return;
+    const ef half_beta = ld_ef(fargs), beta2 = ld_ef(fargs + 4);
     const uint32_t half = halve(ONE);
     const uint32_t g = tw_inv[h + rev_bits((uint32_t)i, log_h)];
     const ef pw = ef_mul_base(half_beta, g);
@@ -433,6 +435,7 @@ __global__ __launch_bounds__(NT) void k_fri_fold(const uint32_t *cur, uint64_t h
     st_ef(next + 4 * i, r);
 }
 
+// leaf i = sponge(cur[2i] || cur[2i+1]) (8 elements: one permutation)
 __global__ __launch_bounds__(NT) void k_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out) {
     const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (i >= h) return;
@@ -446,15 +449,74 @@ __global__ __launch_bounds__(NT) void k_fri_leaves(const uint32_t *cur, uint64_t
     o[0] = make_uint4(s[0], s[1], s[2], s[3]);
     o[1] = make_uint4(s[4], s[5], s[6], s[7]);
 }
+__global__ __launch_bounds__(NT) void k_fri_leaves16(const uint32_t *cur, uint64_t h, uint32_t *out) {
+    const uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    const uint64_t i = t >> 4;
+    const int l = (int)(t & 15);
+    const uint32_t x = p2x16::permute(i < h && l < 8 ? cur[8 * i + l] : 0u, p2x16::lane_consts(l));
+    if (i < h && l < 8) out[8 * i + l] = x;
+}
 
-void launch_fri_fold(const uint32_t *cur, uint64_t h, const ef &half_beta, const ef &beta2, const uint32_t *tw_inv,
+// One FRI round of the Fiat-Shamir transcript on the device (DuplexChallenger semantics of the
+// host Challenger: observe the 8 root words, sample beta as 4 words): keeps the commit phase free
+// of host round trips.  One wavefront; the permutation runs in the 16-lane form (all four rows
+// compute the same state).  Also records the root for the proof and the fold arguments.
+__global__ __launch_bounds__(64) void k_fri_chal(DevChallenger *c, const uint32_t *root, uint32_t *root_out,
+                                                 uint32_t *fargs) {
+    __shared__ uint32_t st[16], in[8], out[8];
+    __shared__ int nin, nout;
+    const int tid = threadIdx.x, l = tid & 15;
+    if (tid < 16) st[tid] = c->st[tid];
+    if (tid < 8) { in[tid] = c->in[tid]; out[tid] = c->out[tid]; root_out[tid] = root[tid]; }
+    if (tid == 0) { nin = (int)c->nin; nout = (int)c->nout; }
+    __syncthreads();
+    const p2x16::Lane lc = p2x16::lane_consts(l);
+    auto duplex = [&]() {
+        const uint32_t x = p2x16::permute(l < nin ? in[l] : st[l], lc);
+        __syncthreads();
+        if (tid < 16) st[tid] = x;
+        if (tid < 8) out[tid] = x;
+        if (tid == 0) { nin = 0; nout = 8; }
+        __syncthreads();
+    };
+    for (int k = 0; k < 8; k++) {  // observe(root[k])
+        if (tid == 0) { nout = 0; in[nin] = root[k]; nin++; }
+        __syncthreads();
+        if (nin == 8) duplex();
+    }
+    uint32_t beta[4];
+    for (int k = 0; k < 4; k++) {  // sample()
+        if (nin || !nout) duplex();
+        beta[k] = out[nout - 1];
+        __syncthreads();
+        if (tid == 0) nout--;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const ef b{{beta[0], beta[1], beta[2], beta[3]}};
+        st_ef(fargs, ef_mul_base(b, halve(ONE)));
+        st_ef(fargs + 4, ef_mul(b, b));
+    }
+    if (tid < 16) c->st[tid] = st[tid];
+    if (tid < 8) { c->in[tid] = in[tid]; c->out[tid] = out[tid]; }
+    if (tid == 0) { c->nin = (uint32_t)nin; c->nout = (uint32_t)nout; }
+}
+
+void launch_fri_fold(const uint32_t *cur, uint64_t h, const uint32_t *fargs, const uint32_t *tw_inv,
                      const uint32_t *ro, uint32_t *next, hipStream_t s) {
-    hipLaunchKernelGGL(k_fri_fold, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s, cur, h, ilog2(h), half_beta,
-                       beta2, tw_inv, ro, next);
+    hipLaunchKernelGGL(k_fri_fold, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s, cur, h, ilog2(h), fargs,
+                       tw_inv, ro, next);
     HIP_CHECK(hipGetLastError());
 }
 void launch_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_fri_leaves, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s, cur, h, out);
+    if (h <= 8192)
+        hipLaunchKernelGGL(k_fri_leaves16, dim3((unsigned)((h * 16 + NT - 1) / NT)), dim3(NT), 0, s, cur, h, out);
+    else
+        hipLaunchKernelGGL(k_fri_leaves, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s, cur, h, out);
+    HIP_CHECK(hipGetLastError());
+}
+void launch_fri_chal(DevChallenger *c, const uint32_t *root, uint32_t *root_out, uint32_t *fargs, hipStream_t s) {
+    hipLaunchKernelGGL(k_fri_chal, dim3(1), dim3(64), 0, s, c, root, root_out, fargs);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -50,8 +50,17 @@ struct ReduceArgs {
     uint64_t h;
 };
 void launch_fri_reduce(const ReduceArgs &a, hipStream_t s);
-void launch_fri_fold(const uint32_t *cur, uint64_t h, const kb::ef &half_beta, const kb::ef &beta2,
-                     const uint32_t *tw_inv, const uint32_t *ro, uint32_t *next, hipStream_t s);
+// duplex-challenger state in device memory (Montgomery), same fields as the host Challenger
+struct DevChallenger {
+    uint32_t st[16];
+    uint32_t in[8];
+    uint32_t nin;
+    uint32_t out[8];
+    uint32_t nout;
+};
+void launch_fri_chal(DevChallenger *c, const uint32_t *root, uint32_t *root_out, uint32_t *fargs, hipStream_t s);
+void launch_fri_fold(const uint32_t *cur, uint64_t h, const uint32_t *fargs, const uint32_t *tw_inv,
+                     const uint32_t *ro, uint32_t *next, hipStream_t s);
 void launch_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out, hipStream_t s);
 
 struct PowArgs {
@@ -67,6 +76,7 @@ void launch_gather(const uint64_t *d_items, uint32_t nitems, uint32_t *dst, hipS
 // LDE variant for bit-reversed input evaluations (quotient chunks)
 void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst, hipStream_t s);
 // tree from a precomputed leaf digest layer (FRI commit-phase trees)
-void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s);
+// read_root = false: the root stays on the device (t.layers[t.log_max]); t.root is not set
+void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s, bool read_root = true);
 
 }  // namespace zkm

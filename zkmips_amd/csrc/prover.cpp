@@ -544,8 +544,18 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         cur = DBuf(4 * cur_n, s);
         HIP_CHECK(hipMemcpyAsync(cur.p, ro[log_max].p, 16 * cur_n, hipMemcpyDeviceToDevice, s));
     }
-    const uint32_t half = halve(ONE);
     PROF("fri_commit_phase", s, 0);
+    // transcript on the device for the whole phase: no host round trip per round
+    DBuf dchal_buf((sizeof(DevChallenger) + 3) / 4, s), droots(8 * std::max(nrounds, 1), s),
+        dfargs(8 * std::max(nrounds, 1), s);
+    DevChallenger hc{};
+    memcpy(hc.st, ch.st, 64);
+    memcpy(hc.in, ch.in, 32);
+    memcpy(hc.out, ch.out, 32);
+    hc.nin = (uint32_t)ch.nin;
+    hc.nout = (uint32_t)ch.nout;
+    DevChallenger *dchal = reinterpret_cast<DevChallenger *>(dchal_buf.p);
+    HIP_CHECK(hipMemcpyAsync(dchal, &hc, sizeof hc, hipMemcpyHostToDevice, s));
     for (int rd = 0; rd < nrounds; rd++) {
         const int lf = log_max - 1 - rd;
         const uint64_t h = cur_n >> 1;
@@ -553,20 +563,28 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         launch_fri_leaves(cur.p, h, leaves.p, s);
         // keep the folded-from vector: queries open (lo, hi) pairs of it
         ftrees[rd].owned.push_back(std::move(cur));
-        tree_from_leaves(ftrees[rd], std::move(leaves), h, s);
-        proof.fri_commits.push_back(dig(ftrees[rd].root));
-        ch.observe(ftrees[rd].root, 8);
-        const ef beta = ch.sample_ef();
+        tree_from_leaves(ftrees[rd], std::move(leaves), h, s, false);
+        launch_fri_chal(dchal, ftrees[rd].layers[ftrees[rd].log_max], droots.p + 8 * rd, dfargs.p + 8 * rd, s);
         DBuf next(4 * h, s);
-        launch_fri_fold(ftrees[rd].owned.back().p, h, ef_mul_base(beta, half), ef_mul(beta, beta), c.tw_inv,
-                        ro[lf].p ? ro[lf].p : nullptr, next.p, s);
+        launch_fri_fold(ftrees[rd].owned.back().p, h, dfargs.p + 8 * rd, c.tw_inv, ro[lf].p ? ro[lf].p : nullptr,
+                        next.p, s);
         cur = std::move(next);
         cur_n = h;
-        (void)lf;
     }
-    std::vector<uint32_t> fin(4 * cur_n);
+    std::vector<uint32_t> fin(4 * cur_n), hroots(8 * std::max(nrounds, 1));
     HIP_CHECK(hipMemcpyAsync(fin.data(), cur.p, fin.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(hroots.data(), droots.p, hroots.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(&hc, dchal, sizeof hc, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    for (int rd = 0; rd < nrounds; rd++) {
+        memcpy(ftrees[rd].root, &hroots[8 * rd], 32);
+        proof.fri_commits.push_back(dig(ftrees[rd].root));
+    }
+    memcpy(ch.st, hc.st, 64);
+    memcpy(ch.in, hc.in, 32);
+    memcpy(ch.out, hc.out, 32);
+    ch.nin = (int)hc.nin;
+    ch.nout = (int)hc.nout;
     proof.final_poly = ef{{fin[0], fin[1], fin[2], fin[3]}};
     bool final_ok = true;
     for (uint64_t i = 1; i < cur_n; i++)
