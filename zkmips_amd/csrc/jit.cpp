@@ -1,4 +1,4 @@
-// JIT-specialised quotient kernels (hiprtc, gfx950).
+// JIT-specialised quotient and permutation-trace kernels (hiprtc, gfx950).
 //
 // At setup (MachineProver::setup / pk_to_device) every chip's constraint program and lookup
 // descriptors are lowered to straight-line HIP: column reads are hoisted to the top of the kernel
@@ -171,11 +171,7 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
     }
     ARG_CHECK(k == c.n_constraints, "JIT constraint count mismatch");
 
-    o << "typedef unsigned int uint32_t;\ntypedef unsigned long long uint64_t;\n"
-      << kJitPrelude << "\nusing namespace kb;\n"
-      << "#define POW(k) ef{{A.pows[4*(k)], A.pows[4*(k)+1], A.pows[4*(k)+2], A.pows[4*(k)+3]}}\n"
-      << "#define BPOW(v) ef{{A.beta_pows[4*(v)], A.beta_pows[4*(v)+1], A.beta_pows[4*(v)+2], A.beta_pows[4*(v)+3]}}\n"
-      << "extern \"C\" __global__ void __launch_bounds__(256) " << fname << "(const ZkmQuotJitArgs A) {\n"
+    o << "extern \"C\" __global__ void __launch_bounds__(256) " << fname << "(const ZkmQuotJitArgs A) {\n"
       << "    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n"
       << "    if (t >= A.q) return;\n"
       << "    const uint64_t rl = t;\n"
@@ -209,6 +205,75 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
     return o.str();
 }
 
+// Permutation (LogUp) trace rows, generate_permutation_trace (crates/stark/src/permutation.rs:
+// 156-203): per batch b, s_b = sum_i m_i / rlc_i as num_b / den_b, built incrementally exactly as
+// the interpreter kernel; the nb denominators share ONE extension-field inversion (prefix
+// products, Montgomery's trick), then the row total goes to rowsum for the running-sum scan.
+std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
+    const int nloc = (int)c.local.size();
+    if (!nloc) return "";
+    Gen g;
+    const int batch = 1 << c.log_qd, nb = c.perm_w - 1;
+    g.body << "    const ef alpha = ef{{A.alpha[0], A.alpha[1], A.alpha[2], A.alpha[3]}};\n";
+    for (int b = 0; b < nb; b++) {
+        g.body << "    ef num" << b << " = ef_zero(), den" << b << " = ef_one();\n";
+        for (int i = b * batch; i < nloc && i < (b + 1) * batch; i++) {
+            const LookupDesc &lk = c.local[i];
+            std::string d = g.var("d");
+            g.body << "    ef " << d << " = ef_add_base(alpha, " << hex(kb::to_mont(lk.kind)) << ");\n";
+            for (size_t v = 0; v < lk.values.size(); v++) {
+                std::string x = vpc_expr(g, lk.values[v]);
+                g.body << "    " << d << " = ef_add(" << d << ", ef_mul_base(BPOW(" << v << "), " << x << "));\n";
+            }
+            std::string m = vpc_expr(g, lk.mult);
+            if (!lk.is_send) {
+                std::string t = g.var("t");
+                g.body << "    const uint32_t " << t << " = neg(" << m << ");\n";
+                m = t;
+            }
+            g.body << "    num" << b << " = ef_add(ef_mul(num" << b << ", " << d << "), ef_mul_base(den" << b << ", " << m
+                   << "));\n";
+            g.body << "    den" << b << " = ef_mul(den" << b << ", " << d << ");\n";
+        }
+    }
+    // one inversion for all batches
+    g.body << "    ef pre0 = den0;\n";
+    for (int b = 1; b < nb; b++) g.body << "    const ef pre" << b << " = ef_mul(pre" << b - 1 << ", den" << b << ");\n";
+    g.body << "    ef iv = ef_inv(pre" << nb - 1 << ");\n";
+    for (int b = nb - 1; b >= 1; b--) {
+        g.body << "    const ef s" << b << " = ef_mul(num" << b << ", ef_mul(iv, pre" << b - 1 << "));\n";
+        g.body << "    iv = ef_mul(iv, den" << b << ");\n";
+    }
+    g.body << "    const ef s0 = ef_mul(num0, iv);\n";
+    g.body << "    ef total = ef_zero();\n";
+    for (int b = 0; b < nb; b++) {
+        for (int e = 0; e < 4; e++)
+            g.body << "    A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = s" << b << ".c[" << e << "];\n";
+        g.body << "    total = ef_add(total, s" << b << ");\n";
+    }
+    std::ostringstream o;
+    o << "extern \"C\" __global__ void __launch_bounds__(256) " << fname << "(const ZkmPermJitArgs A) {\n"
+      << "    const uint64_t rl = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n"
+      << "    if (rl >= A.ld) return;\n"
+      << g.head.str() << g.body.str()
+      << "    A.rowsum[4 * rl + 0] = total.c[0];\n"
+      << "    A.rowsum[4 * rl + 1] = total.c[1];\n"
+      << "    A.rowsum[4 * rl + 2] = total.c[2];\n"
+      << "    A.rowsum[4 * rl + 3] = total.c[3];\n"
+      << "}\n";
+    return o.str();
+}
+
+std::string chip_source(const ChipDesc &c) {
+    std::ostringstream o;
+    o << "typedef unsigned int uint32_t;\ntypedef unsigned long long uint64_t;\n"
+      << kJitPrelude << "\nusing namespace kb;\n"
+      << "#define POW(k) ef{{A.pows[4*(k)], A.pows[4*(k)+1], A.pows[4*(k)+2], A.pows[4*(k)+3]}}\n"
+      << "#define BPOW(v) ef{{A.beta_pows[4*(v)], A.beta_pows[4*(v)+1], A.beta_pows[4*(v)+2], A.beta_pows[4*(v)+3]}}\n"
+      << gen_source(c, "zkm_quot_jit") << gen_perm_source(c, "zkm_perm_jit");
+    return o.str();
+}
+
 }  // namespace
 
 bool jit_enabled() {
@@ -216,10 +281,8 @@ bool jit_enabled() {
     return !(e && *e && *e != '0');
 }
 
-static const char *kJitName = "zkm_quot_jit";
-
-std::vector<char> jit_quotient_code(const ChipDesc &c, const std::string &arch_name) {
-    const std::string src = gen_source(c, kJitName);
+std::vector<char> jit_chip_code(const ChipDesc &c, const std::string &arch_name) {
+    const std::string src = chip_source(c);
     if (const char *d = getenv("ZKM_JIT_DUMP")) {
         if (FILE *f = fopen((std::string(d) + "/" + c.name + ".hip").c_str(), "w")) {
             fputs(src.c_str(), f);
@@ -248,15 +311,16 @@ std::vector<char> jit_quotient_code(const ChipDesc &c, const std::string &arch_n
     return code;
 }
 
-JitKernel jit_quotient(const ChipDesc &c, int device) {
+JitKernel jit_chip(const ChipDesc &c, int device) {
     JitKernel k;
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     std::string arch = prop.gcnArchName;
     arch = arch.substr(0, arch.find(':'));  // "gfx950:sramecc+:xnack-" -> "gfx950"
-    k.code = jit_quotient_code(c, arch);
+    k.code = jit_chip_code(c, arch);
     HIP_CHECK(hipModuleLoadData(&k.mod, k.code.data()));
-    HIP_CHECK(hipModuleGetFunction(&k.fn, k.mod, kJitName));
+    HIP_CHECK(hipModuleGetFunction(&k.fn, k.mod, "zkm_quot_jit"));
+    if (!c.local.empty()) HIP_CHECK(hipModuleGetFunction(&k.fn_perm, k.mod, "zkm_perm_jit"));
     k.ok = true;
     return k;
 }
@@ -268,6 +332,13 @@ void launch_quotient_jit(const JitKernel &k, const ZkmQuotJitArgs &a, hipStream_
     HIP_CHECK(hipModuleLaunchKernel(k.fn, grid, 1, 1, 256, 1, 1, 0, s, params, nullptr));
 }
 
+void launch_perm_jit(const JitKernel &k, const ZkmPermJitArgs &a, hipStream_t s) {
+    ZkmPermJitArgs args = a;
+    void *params[] = {&args};
+    const unsigned grid = (unsigned)((a.ld + 255) / 256);
+    HIP_CHECK(hipModuleLaunchKernel(k.fn_perm, grid, 1, 1, 256, 1, 1, 0, s, params, nullptr));
+}
+
 }  // namespace zkm
 
 extern "C" int zkm_quotient_jit_compile(const uint32_t *blob, size_t nwords, uint64_t *code_bytes) {
@@ -275,7 +346,7 @@ extern "C" int zkm_quotient_jit_compile(const uint32_t *blob, size_t nwords, uin
         ARG_CHECK(blob && code_bytes, "null argument");
         const zkm::Machine m = zkm::parse_machine(blob, nwords);
         uint64_t total = 0;
-        for (const auto &c : m.chips) total += zkm::jit_quotient_code(c, "gfx950").size();
+        for (const auto &c : m.chips) total += zkm::jit_chip_code(c, "gfx950").size();
         *code_bytes = total;
         return 0;
     } catch (const std::exception &e) {

@@ -15,4 +15,12 @@ struct ZkmQuotJitArgs {
     unsigned alpha_p[4], lcs[4];
     unsigned gcs[14];
 };
+struct ZkmPermJitArgs {
+    const unsigned *main, *prep;  // traces, column-major natural, column stride ld
+    const unsigned *beta_pows;    // beta^(j+1), EF
+    unsigned *out;                // perm trace batch columns (4 per batch), column stride ld
+    unsigned *rowsum;             // per-row EF total (scan input)
+    unsigned long long ld;        // rows
+    unsigned alpha[4];
+};
 #endif

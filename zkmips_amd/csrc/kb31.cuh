@@ -55,7 +55,14 @@ KB_HD uint32_t mul(uint32_t a, uint32_t b) { return redc((uint64_t)a * b); }
 // a * b / R in (0, 2P), unreduced, for a * b < P * 2^32: adding P * 2^32 to the product lifts the
 // Montgomery quotient by P (same low word, so the same m) and no correction step is needed.
 KB_HD uint32_t mul_lazy(uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    // one v_mad_u64_u32 yields both words (left to itself the compiler recomputes the low word
+    // with a separate v_mul_lo_u32, a half-rate instruction per call)
+    uint64_t t;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(t) : "v"(a), "v"(b), "s"((uint64_t)P << 32) : "vcc");
+#else
     const uint64_t t = (uint64_t)a * b + ((uint64_t)P << 32);
+#endif
     const uint32_t m = (uint32_t)t * MU;
     return (uint32_t)(t >> 32) - umulhi(m, P);
 }

@@ -152,10 +152,12 @@ __global__ __launch_bounds__(NT) void k_scan_fix(const uint32_t *data, uint64_t 
     for (int e = 0; e < 4; e++) out_cols[(uint64_t)e * n + i] = v.c[e];
 }
 
-void launch_perm_trace(const PermArgs &a, hipStream_t s) {
+void launch_perm_trace(const PermArgs &a, hipStream_t s, bool rows_done) {
     if (a.nb < 0) return;
-    hipLaunchKernelGGL(k_perm_rows, dim3((unsigned)((a.n + NT - 1) / NT)), dim3(NT), 0, s, a);
-    HIP_CHECK(hipGetLastError());
+    if (!rows_done) {
+        hipLaunchKernelGGL(k_perm_rows, dim3((unsigned)((a.n + NT - 1) / NT)), dim3(NT), 0, s, a);
+        HIP_CHECK(hipGetLastError());
+    }
     const uint64_t nblk = (a.n + NT * 4 - 1) / (NT * 4);
     DBuf totals(4 * nblk, s);
     hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nblk), dim3(NT), 0, s, a.rowsum, a.n, totals.p);

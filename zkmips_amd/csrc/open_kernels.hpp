@@ -15,7 +15,8 @@ struct PermArgs {
     uint32_t *out;            // flattened perm trace, column-major (4 * (nb + 1) columns)
     uint32_t *rowsum;         // scratch: n EF
 };
-void launch_perm_trace(const PermArgs &a, hipStream_t s);
+// rows_done: the per-row batch columns and rowsum were already written (JIT kernel); only scan
+void launch_perm_trace(const PermArgs &a, hipStream_t s, bool rows_done = false);
 
 struct QuotArgs {
     const uint32_t *prog;

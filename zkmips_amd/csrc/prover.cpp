@@ -276,7 +276,18 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             DBuf rowsum(4 * N, s);
             PermArgs a{pk.progs[md.chip[i]].p, md.traces[i].p, pki >= 0 ? pk.traces[pki].p : nullptr, N, perm_alpha,
                        d_bpow.p, 1 << cd.log_qd, pw - 1, perm_traces[i].p, rowsum.p};
-            { PROF("perm_trace", s, 4.0 * N * (cd.main_w + cd.prep_w) + 16.0 * N * (pw + 2)); launch_perm_trace(a, s); }
+            {
+                PROF("perm_trace", s, 4.0 * N * (cd.main_w + cd.prep_w) + 16.0 * N * (pw + 2));
+                const JitKernel &jk = pk.jit[md.chip[i]];
+                if (jk.fn_perm) {
+                    ZkmPermJitArgs ja{};
+                    ja.main = a.main; ja.prep = a.prep; ja.beta_pows = a.beta_pows; ja.out = a.out;
+                    ja.rowsum = a.rowsum; ja.ld = N;
+                    memcpy(ja.alpha, a.alpha.c, 16);
+                    launch_perm_jit(jk, ja, s);
+                }
+                launch_perm_trace(a, s, jk.fn_perm != nullptr);
+            }
             uint32_t l[4];
             for (int e = 0; e < 4; e++)
                 HIP_CHECK(hipMemcpyAsync(&l[e], perm_traces[i].p + (uint64_t)(4 * (pw - 1) + e) * N + N - 1, 4,
@@ -745,7 +756,7 @@ int zkm_setup(zkm_ctx *ctx, const uint32_t *blob, size_t nwords, const zkm_confi
             fut.push_back(std::async(std::launch::async, [&cd, dev = c->device] {
                 (void)hipSetDevice(dev);
                 try {
-                    return jit_quotient(cd, dev);
+                    return jit_chip(cd, dev);
                 } catch (const std::exception &e) {
                     fprintf(stderr, "zkm: quotient JIT failed for chip %s, using the interpreter kernel: %s\n",
                             cd.name.c_str(), e.what());
