@@ -104,6 +104,7 @@ void zkm_destroy(zkm_ctx *ctx) {
     // context handle, and their stream-ordered buffers are released on the stream that made them.
     (void)hipFree(c->tw_fwd);
     (void)hipFree(c->tw_inv);
+    (void)hipFree(c->tt_fwd);  // tt_inv shares the allocation
     delete c;       // cached twist tables go back to the pool
     pool_trim();    // blocks still owned by live keys / shard data stay allocated
 }

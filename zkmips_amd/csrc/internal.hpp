@@ -95,6 +95,8 @@ struct Ctx {
     int tw_log = 0;                 // twiddle tables cover transforms up to 2^tw_log
     uint32_t *tw_fwd = nullptr;     // tw[h + j] = w_{2h}^j  (Montgomery), size 2^tw_log
     uint32_t *tw_inv = nullptr;
+    uint32_t *tt_fwd = nullptr;     // per-thread twiddle rows of the 8192-point tiles (ntt.hip)
+    uint32_t *tt_inv = nullptr;
     std::mutex mu;
     std::vector<hipStream_t> free_streams;
     hipStream_t acquire_stream();

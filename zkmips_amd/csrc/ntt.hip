@@ -88,6 +88,24 @@ __global__ void k_build_twiddles(uint32_t *tw, uint32_t *twi, int log_max, const
     twi[i] = pow(iroots[k + 1], j);
 }
 
+// rows for layouts SE = 2, 32, 512 (offsets 0, 2, 34 rows), one row per (SE, off < SE):
+// k = 0: w_{2SE}^off; k = 1,2: w_{4SE}^{off + SE m}; k = 3..6: w_{8SE}^..; k = 7..14: w_{16SE}^..
+static constexpr uint32_t TT_WORDS = (2 + 32 + 512) * 16;
+__device__ __forceinline__ uint32_t tt_row(int SE) { return SE == 2 ? 0u : SE == 32 ? 2u : 34u; }
+__global__ void k_build_tile_tw(const uint32_t *tw, const uint32_t *twi, uint32_t *tt, uint32_t *tti) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= TT_WORDS) return;
+    const uint32_t row = i >> 4, k = i & 15;
+    const uint32_t SE = row < 2 ? 2 : row < 34 ? 32 : 512;
+    const uint32_t off = row - (SE == 2 ? 0 : SE == 32 ? 2 : 34);
+    if (k == 15) { tt[i] = 0; tti[i] = 0; return; }
+    const uint32_t st = k == 0 ? 0 : k < 3 ? 1 : k < 7 ? 2 : 3;
+    const uint32_t m = k - ((1u << st) - 1);
+    const uint32_t idx = (SE << st) + off + SE * m;
+    tt[i] = tw[idx];
+    tti[i] = twi[idx];
+}
+
 void build_twiddles(Ctx &c, int log_max) {
     size_t n = 1ull << log_max;
     HIP_CHECK(hipMalloc((void **)&c.tw_fwd, n * 4));
@@ -104,6 +122,13 @@ void build_twiddles(Ctx &c, int log_max) {
     HIP_CHECK(hipDeviceSynchronize());
     HIP_CHECK(hipFree(d_r));
     c.tw_log = log_max;
+    // per-thread twiddle rows of the 8192-point register tiles (t13::net16)
+    HIP_CHECK(hipMalloc((void **)&c.tt_fwd, 2 * TT_WORDS * 4));
+    c.tt_inv = c.tt_fwd + TT_WORDS;
+    hipLaunchKernelGGL(k_build_tile_tw, dim3((TT_WORDS + NT - 1) / NT), dim3(NT), 0, 0, c.tw_fwd, c.tw_inv, c.tt_fwd,
+                       c.tt_inv);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipDeviceSynchronize());
 }
 
 // ------------------------------------------------------------------ tile stage engine
@@ -112,20 +137,29 @@ void build_twiddles(Ctx &c, int log_max) {
 // row r uses w_{2h}^{(r mod hr)*S + c0 + t} = tw[h + (r mod hr)*S + c0 + t] (all indices < 2^24).
 // Stages are processed G <= 3 at a time: each thread holds the 2^G elements a group of G stages
 // touches in registers, so a tile makes one LDS round trip per 3 stages instead of per stage.
-template <int G, int T, int LD, bool DIT>
+// LDS address of tile element (row r, column t).  Strided tiles (SWS >= 0) XOR-swizzle the
+// column with row bits SWS..SWS+4, so that the bit-reversed row walk of MODE_BITREV_OUT (32 lanes
+// on rows 2^SWS apart) hits 32 distinct banks; row-major walks stay conflict-free.
+template <int LD, int SWS>
+__device__ __forceinline__ int tile_at(int r, int t) {
+    if constexpr (SWS < 0) return r * LD + t;
+    else return r * LD + (t ^ ((r >> SWS) & 31));
+}
+
+template <int G, int T, int LD, bool DIT, int SWS, int NTH>
 __device__ __forceinline__ void stage_group(uint32_t *x, int R, int lc, const uint32_t *__restrict__ tw, uint32_t S,
                                             uint32_t c0) {
     constexpr int E = 1 << G;
     const int hrc = 1 << lc;
     const int ngroups = (R * T) >> G;
-    for (int g = threadIdx.x; g < ngroups; g += NT) {
+    for (int g = threadIdx.x; g < ngroups; g += NTH) {
         const int t = g & (T - 1);
         const int q = g / T;
         const int rlow = q & (hrc - 1);
         const int r0 = ((q >> lc) << (lc + G)) | rlow;
         uint32_t v[E];
 #pragma unroll
-        for (int k = 0; k < E; k++) v[k] = x[(r0 + k * hrc) * LD + t];
+        for (int k = 0; k < E; k++) v[k] = x[tile_at<LD, SWS>(r0 + k * hrc, t)];
         const uint32_t jb = (uint32_t)rlow * S + c0 + (uint32_t)t;
         const uint32_t step = (uint32_t)hrc * S;
         if (DIT) {
@@ -156,25 +190,25 @@ __device__ __forceinline__ void stage_group(uint32_t *x, int R, int lc, const ui
             }
         }
 #pragma unroll
-        for (int k = 0; k < E; k++) x[(r0 + k * hrc) * LD + t] = v[k];
+        for (int k = 0; k < E; k++) x[tile_at<LD, SWS>(r0 + k * hrc, t)] = v[k];
     }
     __syncthreads();
 }
 
 // All LOGR stages of a tile: DIT bottom-up (half-sizes 1,2,4,...), DIF top-down.
-template <int LOGR, int T, int LD, bool DIT>
+template <int LOGR, int T, int LD, bool DIT, int SWS, int NTH>
 __device__ __forceinline__ void tile_stages(uint32_t *x, const uint32_t *__restrict__ tw, uint32_t S, uint32_t c0) {
     constexpr int R = 1 << LOGR;
     if (DIT) {
         int lc = 0;
-        for (; lc + 3 <= LOGR; lc += 3) stage_group<3, T, LD, true>(x, R, lc, tw, S, c0);
-        if (LOGR - lc == 2) stage_group<2, T, LD, true>(x, R, lc, tw, S, c0);
-        else if (LOGR - lc == 1) stage_group<1, T, LD, true>(x, R, lc, tw, S, c0);
+        for (; lc + 3 <= LOGR; lc += 3) stage_group<3, T, LD, true, SWS, NTH>(x, R, lc, tw, S, c0);
+        if (LOGR - lc == 2) stage_group<2, T, LD, true, SWS, NTH>(x, R, lc, tw, S, c0);
+        else if (LOGR - lc == 1) stage_group<1, T, LD, true, SWS, NTH>(x, R, lc, tw, S, c0);
     } else {
         int rem = LOGR;
-        for (; rem >= 3; rem -= 3) stage_group<3, T, LD, false>(x, R, rem - 3, tw, S, c0);
-        if (rem == 2) stage_group<2, T, LD, false>(x, R, 0, tw, S, c0);
-        else if (rem == 1) stage_group<1, T, LD, false>(x, R, 0, tw, S, c0);
+        for (; rem >= 3; rem -= 3) stage_group<3, T, LD, false, SWS, NTH>(x, R, rem - 3, tw, S, c0);
+        if (rem == 2) stage_group<2, T, LD, false, SWS, NTH>(x, R, 0, tw, S, c0);
+        else if (rem == 1) stage_group<1, T, LD, false, SWS, NTH>(x, R, 0, tw, S, c0);
     }
 }
 
@@ -189,6 +223,9 @@ struct ColMap {
 
 struct Twist {
     const uint32_t *lo0, *hi0, *lo1, *hi1;
+    // 8192-tile form (k_lde_fused13): f_e(rev_L(b 2^13 + i)) = g_e[b] * u_e[t][j] for element j of
+    // thread t in layout L2 (i = lay_idx<2>(t, j)); u_e: 512 x 16, g_e: 2^(L-13) entries
+    const uint32_t *u0, *g0, *u1, *g1;
     __device__ __forceinline__ uint32_t f(int e, uint32_t k) const {
         return e ? mul(hi1[k >> 12], lo1[k & 4095]) : mul(hi0[k >> 12], lo0[k & 4095]);
     }
@@ -200,12 +237,13 @@ enum PassMode { MODE_PLAIN = 0, MODE_BITREV_OUT = 1, MODE_TWIST_OUT = 2 };
 //   MODE_BITREV_OUT (last DIT pass, R*S == N): natural n = r*S + c goes to row rev_L(n).
 //   MODE_TWIST_OUT  (last DIT pass of an inverse transform): natural coefficient n goes to both
 //                   LDE halves multiplied by the coset twists f_0(n), f_1(n).
-template <int LOGR, int T, bool DIT>
-__global__ __launch_bounds__(NT) void k_ntt_strided(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+template <int LOGR, int T, bool DIT, int NTH>
+__global__ __launch_bounds__(NTH) void k_ntt_strided(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                     int logS, const uint32_t *__restrict__ tw, int mode, Twist tws,
                                                     uint64_t dst_half) {
     constexpr int R = 1 << LOGR;
-    constexpr int LD = T + 1;  // padded rows: conflict-free column walks (bit-reversed write)
+    constexpr int LD = T;                             // rows unpadded, columns XOR-swizzled
+    constexpr int SWS = LOGR >= 5 ? LOGR - 5 : 0;    // see tile_at
     __shared__ uint32_t x[R * LD];
     const uint32_t S = 1u << logS;
     const uint32_t groups = S / T;
@@ -215,55 +253,55 @@ __global__ __launch_bounds__(NT) void k_ntt_strided(const uint32_t *src, uint32_
     const uint32_t base = outer * (uint32_t)R * S;
     const uint32_t *sp = src + ms.off(blockIdx.y);
     uint32_t *dp = dst + md.off(blockIdx.y);
-    for (int i = threadIdx.x; i < R * T; i += NT) {
+    for (int i = threadIdx.x; i < R * T; i += NTH) {
         const int r = i / T, t = i & (T - 1);
-        x[r * LD + t] = sp[base + (uint32_t)r * S + c0 + t];
+        x[tile_at<LD, SWS>(r, t)] = sp[base + (uint32_t)r * S + c0 + t];
     }
     __syncthreads();
-    tile_stages<LOGR, T, LD, DIT>(x, tw, S, c0);
+    tile_stages<LOGR, T, LD, DIT, SWS, NTH>(x, tw, S, c0);
     if (mode == MODE_PLAIN) {
-        for (int i = threadIdx.x; i < R * T; i += NT) {
+        for (int i = threadIdx.x; i < R * T; i += NTH) {
             const int r = i / T, t = i & (T - 1);
-            dp[base + (uint32_t)r * S + c0 + t] = x[r * LD + t];
+            dp[base + (uint32_t)r * S + c0 + t] = x[tile_at<LD, SWS>(r, t)];
         }
     } else if (mode == MODE_TWIST_OUT) {
-        for (int i = threadIdx.x; i < R * T; i += NT) {
+        for (int i = threadIdx.x; i < R * T; i += NTH) {
             const int r = i / T, t = i & (T - 1);
             const uint32_t n = base + (uint32_t)r * S + c0 + t;
-            const uint32_t v = x[r * LD + t];
+            const uint32_t v = x[tile_at<LD, SWS>(r, t)];
             dp[n] = mul(v, tws.f(0, n));
             dp[dst_half + n] = mul(v, tws.f(1, n));
         }
     } else {
-        for (int i = threadIdx.x; i < R * T; i += NT) {
+        for (int i = threadIdx.x; i < R * T; i += NTH) {
             const int t = i / R, q = i & (R - 1);
-            dp[(uint64_t)rev_bits(c0 + t, logS) * R + q] = x[(int)rev_bits((uint32_t)q, LOGR) * LD + t];
+            dp[(uint64_t)rev_bits(c0 + t, logS) * R + q] = x[tile_at<LD, SWS>((int)rev_bits((uint32_t)q, LOGR), t)];
         }
     }
 }
 
 // Contiguous pass over blocks of R consecutive elements (bit-reversed-input pipeline):
 //   MODE_PLAIN: stages only; MODE_TWIST_OUT: DIT (inverse) then twisted writes to both halves.
-template <int LOGR, bool DIT>
-__global__ __launch_bounds__(NT) void k_ntt_contig(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+template <int LOGR, bool DIT, int NTH>
+__global__ __launch_bounds__(NTH) void k_ntt_contig(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                    const uint32_t *__restrict__ tw, int mode, Twist tws,
                                                    uint64_t dst_half) {
     constexpr int R = 1 << LOGR;
     __shared__ uint32_t x[R];
     const uint32_t base = blockIdx.x * (uint32_t)R;
     const uint32_t *sp = src + ms.off(blockIdx.y) + base;
-    for (int i = threadIdx.x; i < R; i += NT) x[i] = sp[i];
+    for (int i = threadIdx.x; i < R; i += NTH) x[i] = sp[i];
     __syncthreads();
-    tile_stages<LOGR, 1, 1, DIT>(x, tw, 1, 0);
+    tile_stages<LOGR, 1, 1, DIT, -1, NTH>(x, tw, 1, 0);
     uint32_t *dp = dst + md.off(blockIdx.y);
     if (mode == MODE_TWIST_OUT) {
-        for (int i = threadIdx.x; i < R; i += NT) {
+        for (int i = threadIdx.x; i < R; i += NTH) {
             const uint32_t n = base + i;
             dp[n] = mul(x[i], tws.f(0, n));
             dp[dst_half + n] = mul(x[i], tws.f(1, n));
         }
     } else {
-        for (int i = threadIdx.x; i < R; i += NT) dp[base + i] = x[i];
+        for (int i = threadIdx.x; i < R; i += NTH) dp[base + i] = x[i];
     }
 }
 
@@ -271,8 +309,8 @@ __global__ __launch_bounds__(NT) void k_ntt_contig(const uint32_t *src, uint32_t
 // coset twists, and the first (contiguous, DIT) pass of both forward transforms, on one tile.
 // The DIF output tile (bit-reversed coefficients) is exactly the DIT input tile, so the
 // coefficients never round-trip through HBM.  bitrev_out: the whole transform fits the tile.
-template <int LOGR>
-__global__ __launch_bounds__(NT) void k_lde_fused(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, int L,
+template <int LOGR, int NTH>
+__global__ __launch_bounds__(NTH) void k_lde_fused(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, int L,
                                                   const uint32_t *__restrict__ tw_inv,
                                                   const uint32_t *__restrict__ tw_fwd, Twist tws, uint64_t dst_half,
                                                   int bitrev_out) {
@@ -281,21 +319,340 @@ __global__ __launch_bounds__(NT) void k_lde_fused(const uint32_t *src, uint32_t 
     __shared__ uint32_t x[R];
     const uint32_t base = blockIdx.x * (uint32_t)R;
     const uint32_t *sp = src + ms.off(blockIdx.y) + base;
-    for (int i = threadIdx.x; i < R; i += NT) a[i] = sp[i];
+    for (int i = threadIdx.x; i < R; i += NTH) a[i] = sp[i];
     __syncthreads();
-    tile_stages<LOGR, 1, 1, false>(a, tw_inv, 1, 0);
+    tile_stages<LOGR, 1, 1, false, -1, NTH>(a, tw_inv, 1, 0);
     uint32_t *dcol = dst + md.off(blockIdx.y);
     for (int e = 0; e < 2; e++) {
-        for (int i = threadIdx.x; i < R; i += NT) x[i] = mul(a[i], tws.f(e, rev_bits(base + i, L)));
+        for (int i = threadIdx.x; i < R; i += NTH) x[i] = mul(a[i], tws.f(e, rev_bits(base + i, L)));
         __syncthreads();
-        tile_stages<LOGR, 1, 1, true>(x, tw_fwd, 1, 0);
+        tile_stages<LOGR, 1, 1, true, -1, NTH>(x, tw_fwd, 1, 0);
         uint32_t *dp = dcol + (uint64_t)e * dst_half;
         if (!bitrev_out) {
-            for (int i = threadIdx.x; i < R; i += NT) dp[base + i] = x[i];
+            for (int i = threadIdx.x; i < R; i += NTH) dp[base + i] = x[i];
         } else {
-            for (int i = threadIdx.x; i < R; i += NT) dp[i] = x[rev_bits((uint32_t)i, LOGR)];
+            for (int i = threadIdx.x; i < R; i += NTH) dp[i] = x[rev_bits((uint32_t)i, LOGR)];
         }
         __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ 8192-point register tiles
+// One workgroup of 512 threads holds an 8192-element tile in registers, 16 elements per thread,
+// in one of three layouts (index of element j of thread t):
+//   L512: t + 512 j                       stages h = 512..4096 in registers
+//   L32 : (t >> 5) * 512 + (t & 31) + 32 j  stages h = 32..256
+//   L2  : (t >> 1) * 32  + (t & 1)  + 2 j   stages h = 2..16; h = 1 pairs lanes t, t^1 (DPP)
+// Layout changes go through a 34 KB LDS tile whose rows are padded (sw13) so that every layout's
+// ds_read_b32 / ds_write_b32 is conflict-free within each 32-lane half.
+// Butterflies: DIF x' = x + y, y' = (x - y) w;  DIT t = y w, x' = x + t, y' = x - t;
+// w = w_{2h}^{i mod h} from tw[h + (i mod h)].
+namespace t13 {
+constexpr int NTH = 512;
+
+// padded LDS word address: row pitch 34 per 32 words.  For every layout, element j's address is a
+// per-thread base plus a constant (foldable into the ds_* immediate offset), and each 32-lane
+// half of a wave hits 32 distinct banks: L512 and L32 walk consecutive words; L2 lanes 2m + b
+// land on bank b + 2m + 2j.
+__device__ __forceinline__ uint32_t sw13(uint32_t idx) { return idx + 2 * (idx >> 5); }
+constexpr uint32_t LDS13 = 8192 + 2 * 256;
+
+template <int SE>
+__device__ __forceinline__ uint32_t lay_idx(uint32_t t, uint32_t j) {
+    if constexpr (SE == 512) return t + 512 * j;
+    else if constexpr (SE == 32) return (t >> 5) * 512 + (t & 31) + 32 * j;
+    else return (t >> 1) * 32 + (t & 1) + 2 * j;
+}
+template <int SE>
+__device__ __forceinline__ uint32_t lay_off(uint32_t t) {  // (index of element 0) mod SE
+    if constexpr (SE == 512) return (uint32_t)t;
+    else if constexpr (SE == 32) return (uint32_t)(t & 31);
+    else return (uint32_t)(t & 1);
+}
+
+// the four in-register stages of a layout with element stride SE
+template <bool DIT, int SE>
+__device__ __forceinline__ void net16(uint32_t v[16], uint32_t off, const uint32_t *__restrict__ tt) {
+    // this thread's 15 twiddles, contiguous (k_build_tile_tw)
+    uint32_t w16[16];
+    const uint4 *row = (const uint4 *)(tt + (tt_row(SE) + off) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint4 r = row[q];
+        w16[4 * q] = r.x; w16[4 * q + 1] = r.y; w16[4 * q + 2] = r.z; w16[4 * q + 3] = r.w;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int st = DIT ? q : 3 - q;  // DIT: h = SE, 2SE, 4SE, 8SE; DIF: reverse
+        const int span = 1 << st;
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+            const uint32_t w = w16[span - 1 + m];
+#pragma unroll
+            for (int j = m; j < 16; j += 2 * span) {
+                const uint32_t x = v[j], y = v[j + span];
+                if (DIT) {
+                    const uint32_t tt = mul(y, w);
+                    v[j] = add(x, tt);
+                    v[j + span] = sub(x, tt);
+                } else {
+                    v[j] = add(x, y);
+                    v[j + span] = mul(sub(x, y), w);
+                }
+            }
+        }
+    }
+}
+
+// h = 1 stage (w = 1 for both DIF and DIT): lanes t (even) and t^1 (odd) exchange by DPP
+__device__ __forceinline__ void stage_h1(uint32_t v[16], bool odd) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0xB1 /*quad_perm [1,0,3,2]*/, 0xF,
+                                                                  0xF, false);
+        const uint32_t neg_or_v = odd ? P - v[j] : v[j];  // odd lane: nb - v = nb + (P - v)
+        v[j] = add(nb, neg_or_v);
+    }
+}
+
+template <int SE>
+__device__ __forceinline__ void to_lds(uint32_t *x, const uint32_t v[16], uint32_t t) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) x[sw13(lay_idx<SE>(t, j))] = v[j];
+}
+template <int SE>
+__device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint32_t t) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = x[sw13(lay_idx<SE>(t, j))];
+}
+
+// DIF over all 13 stages: v in L512 (natural) -> v in L2 (bit-reversed within the tile)
+__device__ __forceinline__ void dif13(uint32_t v[16], uint32_t *x, uint32_t t, const uint32_t *__restrict__ tw) {
+    net16<false, 512>(v, lay_off<512>(t), tw);
+    to_lds<512>(x, v, t);
+    __syncthreads();
+    from_lds<32>(x, v, t);
+    net16<false, 32>(v, lay_off<32>(t), tw);
+    __syncthreads();
+    to_lds<32>(x, v, t);
+    __syncthreads();
+    from_lds<2>(x, v, t);
+    net16<false, 2>(v, lay_off<2>(t), tw);
+    stage_h1(v, t & 1);
+    __syncthreads();  // LDS free for the next user
+}
+
+// DIT over all 13 stages: v in L2 (bit-reversed input) -> v in L512 (natural)
+__device__ __forceinline__ void dit13(uint32_t v[16], uint32_t *x, uint32_t t, const uint32_t *__restrict__ tw) {
+    stage_h1(v, t & 1);
+    net16<true, 2>(v, lay_off<2>(t), tw);
+    to_lds<2>(x, v, t);
+    __syncthreads();
+    from_lds<32>(x, v, t);
+    net16<true, 32>(v, lay_off<32>(t), tw);
+    __syncthreads();
+    to_lds<32>(x, v, t);
+    __syncthreads();
+    from_lds<512>(x, v, t);
+    net16<true, 512>(v, lay_off<512>(t), tw);
+    __syncthreads();
+}
+}  // namespace t13
+
+// Fused middle of the natural-input LDE for transforms larger than one tile: the iNTT's last 13
+// (DIF) stages, both coset twists and the forward transforms' first 13 (DIT) stages, with the
+// coefficients kept in registers between the two cosets.
+__global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+                                                          int L, const uint32_t *__restrict__ tt_inv,
+                                                          const uint32_t *__restrict__ tt_fwd, Twist tws,
+                                                          uint64_t dst_half) {
+    using namespace t13;
+    __shared__ uint32_t x[LDS13];
+    __shared__ uint32_t cs[8192];  // the coefficients, private per thread (cs[j * 512 + t]): frees 16 VGPRs
+    const uint32_t t = threadIdx.x;
+    const uint32_t base = blockIdx.x * 8192u;
+    const uint32_t *sp = src + ms.off(blockIdx.y) + base;
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = sp[lay_idx<512>(t, j)];
+    dif13(v, x, t, tt_inv);
+#pragma unroll
+    for (int j = 0; j < 16; j++) cs[j * 512 + t] = v[j];
+    uint32_t *dcol = dst + md.off(blockIdx.y);
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        {
+            const uint32_t ge = e ? tws.g1[blockIdx.x] : tws.g0[blockIdx.x];
+            const uint4 *ur = (const uint4 *)((e ? tws.u1 : tws.u0) + t * 16);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint4 u = ur[q];
+                v[4 * q] = mul(mul(cs[(4 * q) * 512 + t], ge), u.x);
+                v[4 * q + 1] = mul(mul(cs[(4 * q + 1) * 512 + t], ge), u.y);
+                v[4 * q + 2] = mul(mul(cs[(4 * q + 2) * 512 + t], ge), u.z);
+                v[4 * q + 3] = mul(mul(cs[(4 * q + 3) * 512 + t], ge), u.w);
+            }
+        }
+        dit13(v, x, t, tt_fwd);
+        uint32_t *dp = dcol + (uint64_t)e * dst_half + base;
+#pragma unroll
+        for (int j = 0; j < 16; j++) dp[lay_idx<512>(t, j)] = v[j];
+    }
+}
+
+// ------------------------------------------------------------------ 512-row strided register tiles
+// One workgroup of 1024 threads: 512 rows (stride S) x 32 consecutive columns, 16 elements per
+// thread as two radix-8 networks.  Lane -> column (t = tid & 31), so every global access moves
+// whole 128-B row segments and every row-major LDS access is conflict-free; the columns are
+// XOR-swizzled by row bits 4..8 so that the bit-reversed column walk of the BITREV output is too.
+// Layouts (u = tid >> 5, network n in {0,1}, element k < 8, g = 2u + n):
+//   LH: row (u + 32n) + 64k          stages h_r = 64, 128, 256 rows
+//   LM: row (g >> 3) * 64 + (g & 7) + 8k   h_r = 8, 16, 32
+//   LL: row 8g + k                   h_r = 1, 2, 4
+// The butterfly at rows (r, r + h_r) of the transform uses w_{2h}^{(r mod h_r) S + c0 + t}, h = h_r S.
+namespace s9 {
+constexpr int NTH = 1024;
+enum { LH = 0, LM = 1, LL = 2 };
+
+__device__ __forceinline__ uint32_t at(uint32_t r, uint32_t t) { return r * 32 + (t ^ ((r >> 4) & 31)); }
+
+template <int LAY>
+__device__ __forceinline__ uint32_t row0(uint32_t u, int n) {
+    const uint32_t g = 2 * u + n;
+    if constexpr (LAY == LH) return u + 32 * n;
+    else if constexpr (LAY == LM) return (g >> 3) * 64 + (g & 7);
+    else return 8 * g;
+}
+template <int LAY> constexpr uint32_t RS = LAY == LH ? 64 : LAY == LM ? 8 : 1;
+
+// three stages of one network; off = row0 mod RS
+template <bool DIT, int LAY>
+__device__ __forceinline__ void net8(uint32_t *v, uint32_t off, uint32_t S, uint32_t ct,
+                                     const uint32_t *__restrict__ tw) {
+    constexpr uint32_t rs = RS<LAY>;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const int st = DIT ? q : 2 - q;
+        const int span = 1 << st;
+        const uint32_t h = (rs << st) * S;
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+            const uint32_t w = tw[h + (off + rs * m) * S + ct];
+#pragma unroll
+            for (int k = m; k < 8; k += 2 * span) {
+                const uint32_t a = v[k], b = v[k + span];
+                if (DIT) {
+                    const uint32_t tt = mul(b, w);
+                    v[k] = add(a, tt);
+                    v[k + span] = sub(a, tt);
+                } else {
+                    v[k] = add(a, b);
+                    v[k + span] = mul(sub(a, b), w);
+                }
+            }
+        }
+    }
+}
+
+template <bool DIT, int LAY>
+__device__ __forceinline__ void nets(uint32_t v[16], uint32_t u, uint32_t S, uint32_t ct,
+                                     const uint32_t *__restrict__ tw) {
+#pragma unroll
+    for (int n = 0; n < 2; n++) net8<DIT, LAY>(v + 8 * n, row0<LAY>(u, n) % RS<LAY>, S, ct, tw);
+}
+template <int LAY>
+__device__ __forceinline__ void to_lds(uint32_t *x, const uint32_t v[16], uint32_t u, uint32_t t) {
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[at(row0<LAY>(u, n) + RS<LAY> * k, t)] = v[8 * n + k];
+}
+template <int LAY>
+__device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint32_t u, uint32_t t) {
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[8 * n + k] = x[at(row0<LAY>(u, n) + RS<LAY> * k, t)];
+}
+}  // namespace s9
+
+// 9 strided stages (rows at stride S = 2^logS) of a transform, natural order in and out, or (DIT)
+// with the MODE_BITREV_OUT / MODE_TWIST_OUT writes of k_ntt_strided.
+template <bool DIT, int MODE>
+__global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+                                                       int logS, const uint32_t *__restrict__ tw, Twist tws,
+                                                       uint64_t dst_half) {
+    using namespace s9;
+    __shared__ uint32_t x[512 * 32];
+    const uint32_t S = 1u << logS;
+    const uint32_t groups = S >> 5;
+    const uint32_t outer = blockIdx.x / groups;
+    const uint32_t c0 = (blockIdx.x % groups) * 32;
+    const uint32_t base = outer * 512u * S;
+    const uint32_t t = threadIdx.x & 31, u = threadIdx.x >> 5;
+    const uint32_t ct = c0 + t;
+    const uint32_t *sp = src + ms.off(blockIdx.y) + base + ct;
+    uint32_t *dp = dst + md.off(blockIdx.y);
+    uint32_t v[16];
+    if (DIT) {
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[8 * n + k] = sp[(row0<LL>(u, n) + k) * S];
+        nets<true, LL>(v, u, S, ct, tw);
+        to_lds<LL>(x, v, u, t);
+        __syncthreads();
+        from_lds<LM>(x, v, u, t);
+        nets<true, LM>(v, u, S, ct, tw);
+        __syncthreads();
+        to_lds<LM>(x, v, u, t);
+        __syncthreads();
+        from_lds<LH>(x, v, u, t);
+        nets<true, LH>(v, u, S, ct, tw);
+        if (MODE == MODE_PLAIN) {
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) dp[base + (row0<LH>(u, n) + 64 * k) * S + ct] = v[8 * n + k];
+        } else if (MODE == MODE_TWIST_OUT) {
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t i = base + (row0<LH>(u, n) + 64 * k) * S + ct;
+                    dp[i] = mul(v[8 * n + k], tws.f(0, i));
+                    dp[dst_half + i] = mul(v[8 * n + k], tws.f(1, i));
+                }
+        } else {  // BITREV_OUT: natural n = r S + c -> row rev_L(n) = rev_logS(c) * 512 + rev_9(r)
+            __syncthreads();
+            to_lds<LH>(x, v, u, t);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t idx = (uint32_t)i * NTH + threadIdx.x;
+                const uint32_t tc = idx >> 9, q = idx & 511;
+                dp[(uint64_t)rev_bits(c0 + tc, logS) * 512 + q] = x[at(rev_bits(q, 9), tc)];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[8 * n + k] = sp[(row0<LH>(u, n) + 64 * k) * S];
+        nets<false, LH>(v, u, S, ct, tw);
+        to_lds<LH>(x, v, u, t);
+        __syncthreads();
+        from_lds<LM>(x, v, u, t);
+        nets<false, LM>(v, u, S, ct, tw);
+        __syncthreads();
+        to_lds<LM>(x, v, u, t);
+        __syncthreads();
+        from_lds<LL>(x, v, u, t);
+        nets<false, LL>(v, u, S, ct, tw);
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) dp[base + (row0<LL>(u, n) + k) * S + ct] = v[8 * n + k];
     }
 }
 
@@ -303,7 +660,7 @@ __global__ __launch_bounds__(NT) void k_lde_fused(const uint32_t *src, uint32_t 
 static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
 static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
 
-static int strided_T(int logR) { return logR >= 9 ? 32 : 64; }
+static int strided_T(int logR) { return logR >= 9 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
 
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
@@ -312,9 +669,25 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     const int T = strided_T(logR);
     ARG_CHECK((1 << logS) >= T, "strided pass narrower than its tile");
     dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
+    if (logR == 9) {  // register-tile kernel (T = 32)
+        if (!DIT)
+            hipLaunchKernelGGL((k_ntt_s9<false, MODE_PLAIN>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw, tws,
+                               dst_half);
+        else if (mode == MODE_PLAIN)
+            hipLaunchKernelGGL((k_ntt_s9<true, MODE_PLAIN>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw, tws,
+                               dst_half);
+        else if (mode == MODE_TWIST_OUT)
+            hipLaunchKernelGGL((k_ntt_s9<true, MODE_TWIST_OUT>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tws, dst_half);
+        else
+            hipLaunchKernelGGL((k_ntt_s9<true, MODE_BITREV_OUT>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tws, dst_half);
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
 #define SCASE(k, t)                                                                                             \
     case k:                                                                                                     \
-        hipLaunchKernelGGL((k_ntt_strided<k, t, DIT>), g, dim3(NT), 0, s, src, dst, ms, md, logS, tw, mode, tws, \
+        hipLaunchKernelGGL((k_ntt_strided<k, t, DIT, NT>), g, dim3(NT), 0, s, src, dst, ms, md, logS, tw, mode, tws, \
                            dst_half);                                                                           \
         break;
     switch (logR) {
@@ -332,7 +705,7 @@ static void run_contig(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, 
     dim3 g((unsigned)((1ull << L) >> logR), nv);
 #define CCASE(k)                                                                                                 \
     case k:                                                                                                      \
-        hipLaunchKernelGGL((k_ntt_contig<k, DIT>), g, dim3(NT), 0, s, src, dst, ms, md, tw, mode, tws, dst_half); \
+        hipLaunchKernelGGL((k_ntt_contig<k, DIT, NT>), g, dim3(NT), 0, s, src, dst, ms, md, tw, mode, tws, dst_half); \
         break;
     switch (logR) {
         CCASE(1) CCASE(2) CCASE(3) CCASE(4) CCASE(5) CCASE(6) CCASE(7) CCASE(8) CCASE(9) CCASE(10) CCASE(11) CCASE(12)
@@ -349,8 +722,8 @@ static void run_fused(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, C
     dim3 g((unsigned)((1ull << L) >> logR), nv);
 #define FCASE(k)                                                                                                    \
     case k:                                                                                                         \
-        hipLaunchKernelGGL((k_lde_fused<k>), g, dim3(NT), 0, s, src, dst, ms, md, L, tw_inv, tw_fwd, tws, dst_half, \
-                           bitrev_out);                                                                             \
+        hipLaunchKernelGGL((k_lde_fused<k, NT>), g, dim3(NT), 0, s, src, dst, ms, md, L, tw_inv, tw_fwd, tws,    \
+                               dst_half, bitrev_out);                                                               \
         break;
     switch (logR) {
         FCASE(1) FCASE(2) FCASE(3) FCASE(4) FCASE(5) FCASE(6) FCASE(7) FCASE(8) FCASE(9) FCASE(10) FCASE(11) FCASE(12)
@@ -377,30 +750,59 @@ static std::vector<int> strided_plan(int L, int &logC) {
 
 // Twist tables f0(k) = shift^k / N, f1(k) = (shift w_2N)^k / N, k = hi*4096 + lo; cached per
 // (N, shift) in the context (a handful of distinct pairs per machine), built once on the host.
+static uint32_t host_rev(uint32_t x, int bits) {
+    uint32_t r = 0;
+    for (int i = 0; i < bits; i++) { r = (r << 1) | (x & 1u); x >>= 1; }
+    return r;
+}
+
 static Twist get_twist(Ctx &c, uint64_t N, int L, uint32_t shift, hipStream_t s) {
     const int nhi = (int)((N + 4095) / 4096);
+    const int ng = L > 13 ? 1 << (L - 13) : 0;
+    const size_t per = 4096 + nhi + (ng ? 8192 + ng : 0);  // per coset
+    auto make = [&](const uint32_t *p) {
+        Twist t{p, p + 4096, p + per, p + per + 4096, nullptr, nullptr, nullptr, nullptr};
+        if (ng) {
+            t.u0 = p + 4096 + nhi;
+            t.g0 = t.u0 + 8192;
+            t.u1 = p + per + 4096 + nhi;
+            t.g1 = t.u1 + 8192;
+        }
+        return t;
+    };
     std::lock_guard<std::mutex> g(c.mu);
     for (auto &kv : c.twists)
-        if (kv.first.first == L && kv.first.second == shift) {
-            const uint32_t *p = kv.second.p;
-            return Twist{p, p + 4096, p + 4096 + nhi, p + 2 * 4096 + nhi};
-        }
-    std::vector<uint32_t> tt(2 * (4096 + nhi));
+        if (kv.first.first == L && kv.first.second == shift) return make(kv.second.p);
+    std::vector<uint32_t> tt(2 * per);
     const uint32_t ninv = inv(to_mont((uint32_t)(N % P)));
     uint32_t sh[2] = {shift, mul(shift, two_adic_gen(L + 1))};
     for (int e = 0; e < 2; e++) {
-        uint32_t *lo = tt.data() + e * (4096 + nhi), *hi = lo + 4096;
+        uint32_t *lo = tt.data() + e * per, *hi = lo + 4096;
         uint32_t x = ONE;
         for (int i = 0; i < 4096; i++) { lo[i] = x; x = mul(x, sh[e]); }
         uint32_t step = x;  // shift^4096
         uint32_t y = ninv;
         for (int i = 0; i < nhi; i++) { hi[i] = y; y = mul(y, step); }
+        if (ng) {
+            // u_e = s^(2^(L-13)); tile factor u_e^rev13(i), block factor s^rev_{L-13}(b) / N
+            uint32_t *u = hi + nhi, *gg = u + 8192;
+            const uint32_t ue = pow(sh[e], 1ull << (L - 13));
+            std::vector<uint32_t> upow(8192);
+            uint32_t z = ONE;
+            for (int i = 0; i < 8192; i++) { upow[i] = z; z = mul(z, ue); }
+            for (uint32_t t = 0; t < 512; t++)
+                for (uint32_t j = 0; j < 16; j++) {
+                    const uint32_t i = (t >> 1) * 32 + (t & 1) + 2 * j;
+                    u[t * 16 + j] = upow[host_rev(i, 13)];
+                }
+            for (int b = 0; b < ng; b++) gg[b] = mul(pow(sh[e], host_rev((uint32_t)b, L - 13)), ninv);
+        }
     }
     c.twists.emplace_back(std::make_pair(L, shift), DBuf(tt.size(), s));
     const uint32_t *p = c.twists.back().second.p;
     HIP_CHECK(hipMemcpyAsync((void *)p, tt.data(), tt.size() * 4, hipMemcpyHostToDevice, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    return Twist{p, p + 4096, p + 4096 + nhi, p + 2 * 4096 + nhi};
+    return make(p);
 }
 
 // Bit-reversed input evaluations (quotient chunks, produced bit-reversed by k_quotient):
@@ -470,7 +872,13 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
         in = work.p;
         min = m_w1;
     }
-    run_fused(logC, work.p, work.p, m_w1, m_w1, nv, L, c.tw_inv, c.tw_fwd, tws, N, 0, s);
+    if (logC == 13) {
+        hipLaunchKernelGGL(k_lde_fused13, dim3((unsigned)(N >> 13), nv), dim3(t13::NTH), 0, s, work.p, work.p, m_w1, m_w1,
+                           L, c.tt_inv, c.tt_fwd, tws, N);
+        HIP_CHECK(hipGetLastError());
+    } else {
+        run_fused(logC, work.p, work.p, m_w1, m_w1, nv, L, c.tw_inv, c.tw_fwd, tws, N, 0, s);
+    }
     logS = logC;
     for (int i = (int)sp.size() - 1; i >= 0; i--) {
         const bool last = (i == 0);
