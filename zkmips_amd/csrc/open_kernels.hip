@@ -306,29 +306,40 @@ void launch_quotient(const QuotArgs &a, hipStream_t s) {
 
 // ------------------------------------------------------------------ batch inverses at points
 // out[i] = (mul_omega ? w^idx : 1) / (z - s * w_M^idx), idx = bitrev ? rev(i) : i
-static constexpr int INV_CHUNK = 32;
+static constexpr int INV_CHUNK = 8;  // prefix products stay in registers
+
+// out[i] = (optionally w^idx *) 1 / (z - s w_M^idx), idx = i or rev(i): Montgomery's trick over
+// INV_CHUNK consecutive i per thread, one extension-field inversion per chunk
 __global__ __launch_bounds__(NT) void k_inv_points(ef z, uint32_t s, const uint32_t *__restrict__ tw, uint64_t M,
                                                    int log_m, int bitrev, int mul_omega, uint32_t *out) {
     const uint64_t c = (uint64_t)blockIdx.x * NT + threadIdx.x;
     const uint64_t i0 = c * INV_CHUNK;
-    if (i0 >= M) return;
-    const uint64_t i1 = i0 + INV_CHUNK < M ? i0 + INV_CHUNK : M;
-    ef run = ef_one();
-    for (uint64_t i = i0; i < i1; i++) {
-        const uint64_t idx = bitrev ? rev_bits((uint32_t)i, log_m) : i;
-        ef d = ef_sub(z, ef_base(mul(s, root_pow(tw, M, idx))));
-        run = ef_mul(run, d);
-        st_ef(out + 4 * i, run);  // prefix products
+    if (i0 >= M) return;  // M is a power of two >= INV_CHUNK or a single partial chunk
+    const int cnt = (int)(M - i0 < (uint64_t)INV_CHUNK ? M - i0 : INV_CHUNK);
+    uint32_t om[INV_CHUNK];
+    ef d[INV_CHUNK], pre[INV_CHUNK];
+#pragma unroll
+    for (int k = 0; k < INV_CHUNK; k++) {
+        if (k < cnt) {
+            const uint64_t i = i0 + k;
+            om[k] = root_pow(tw, M, bitrev ? rev_bits((uint32_t)i, log_m) : i);
+        } else {
+            om[k] = ONE;
+        }
     }
-    ef inv_all = ef_inv(run);
-    for (uint64_t i = i1; i-- > i0;) {
-        const uint64_t idx = bitrev ? rev_bits((uint32_t)i, log_m) : i;
-        const uint32_t om = root_pow(tw, M, idx);
-        ef d = ef_sub(z, ef_base(mul(s, om)));
-        ef prev = (i > i0) ? ld_ef(out + 4 * (i - 1)) : ef_one();
-        ef v = ef_mul(inv_all, prev);
-        inv_all = ef_mul(inv_all, d);
-        st_ef(out + 4 * i, mul_omega ? ef_mul_base(v, om) : v);
+    ef run = ef_one();
+#pragma unroll
+    for (int k = 0; k < INV_CHUNK; k++) {
+        d[k] = k < cnt ? ef_sub(z, ef_base(mul(s, om[k]))) : ef_one();
+        pre[k] = run;
+        run = ef_mul(run, d[k]);
+    }
+    ef iv = ef_inv(run);
+#pragma unroll
+    for (int k = INV_CHUNK - 1; k >= 0; k--) {
+        const ef v = ef_mul(iv, pre[k]);
+        iv = ef_mul(iv, d[k]);
+        if (k < cnt) st_ef(out + 4 * (i0 + k), mul_omega ? ef_mul_base(v, om[k]) : v);
     }
 }
 
@@ -341,48 +352,67 @@ void launch_inv_points(const ef &z, uint32_t s, const uint32_t *tw, uint64_t M, 
 }
 
 // ------------------------------------------------------------------ opening dot products
-// partial[(col * nseg + seg) * 2 + p] = sum_{j in seg} y_{j + p} w_j   (p = 1 only if with_next)
-__global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint64_t n,
+// partial[(col * nseg + seg) * 8 + 4p .. +4] = sum_{j in seg} y_{j + p} w_j   (p = 1 only if with_next)
+// Columns are processed OPEN_CB at a time so each weight (16 B) is read once per chunk instead of
+// once per column; the row loop is unrolled so several loads are in flight per thread.
+static constexpr int OPEN_CB = 8;
+__global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                  const uint32_t *__restrict__ w, int with_next, int nseg,
                                                  uint32_t *partial) {
-    __shared__ uint32_t red[2][NT / 64][4];
-    const uint32_t *y = (const uint32_t *)cols[blockIdx.y];
+    __shared__ uint32_t red[NT / 64][OPEN_CB][8];
     const uint64_t seg_len = (n + nseg - 1) / nseg;
     const uint64_t j0 = (uint64_t)blockIdx.x * seg_len;
     const uint64_t j1 = j0 + seg_len < n ? j0 + seg_len : n;
-    ef a0 = ef_zero(), a1 = ef_zero();
+    const uint32_t cb0 = blockIdx.y * OPEN_CB;
+    const int nc = (int)(ncols - cb0 < (uint32_t)OPEN_CB ? ncols - cb0 : OPEN_CB);
+    const uint32_t *y[OPEN_CB];
+#pragma unroll
+    for (int k = 0; k < OPEN_CB; k++) y[k] = (const uint32_t *)cols[cb0 + (k < nc ? k : 0)];
+    ef a0[OPEN_CB], a1[OPEN_CB];
+#pragma unroll
+    for (int k = 0; k < OPEN_CB; k++) { a0[k] = ef_zero(); a1[k] = ef_zero(); }
     for (uint64_t j = j0 + threadIdx.x; j < j1; j += NT) {
-        ef wj = ld_ef(w + 4 * j);
-        a0 = ef_add(a0, ef_mul_base(wj, y[j]));
-        if (with_next) a1 = ef_add(a1, ef_mul_base(wj, y[(j + 1) & (n - 1)]));
+        const ef wj = ld_ef(w + 4 * j);
+        const uint64_t jn = (j + 1) & (n - 1);
+        uint32_t v0[OPEN_CB], v1[OPEN_CB];
+#pragma unroll
+        for (int k = 0; k < OPEN_CB; k++) {
+            v0[k] = y[k][j];
+            v1[k] = with_next ? y[k][jn] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < OPEN_CB; k++) {
+            a0[k] = ef_add(a0[k], ef_mul_base(wj, v0[k]));
+            if (with_next) a1[k] = ef_add(a1[k], ef_mul_base(wj, v1[k]));
+        }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
+    for (int k = 0; k < OPEN_CB; k++) {
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            a0.c[e] = add(a0.c[e], __shfl_xor(a0.c[e], o, 64));
-            a1.c[e] = add(a1.c[e], __shfl_xor(a1.c[e], o, 64));
-        }
-    if (lane == 0)
-        for (int e = 0; e < 4; e++) { red[0][wid][e] = a0.c[e]; red[1][wid][e] = a1.c[e]; }
+        for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                a0[k].c[e] = add(a0[k].c[e], __shfl_xor(a0[k].c[e], o, 64));
+                a1[k].c[e] = add(a1[k].c[e], __shfl_xor(a1[k].c[e], o, 64));
+            }
+        if (lane == 0)
+            for (int e = 0; e < 4; e++) { red[wid][k][e] = a0[k].c[e]; red[wid][k][4 + e] = a1[k].c[e]; }
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        ef s0 = ef_zero(), s1 = ef_zero();
-        for (int k = 0; k < NT / 64; k++) {
-            s0 = ef_add(s0, ef{{red[0][k][0], red[0][k][1], red[0][k][2], red[0][k][3]}});
-            s1 = ef_add(s1, ef{{red[1][k][0], red[1][k][1], red[1][k][2], red[1][k][3]}});
-        }
-        uint32_t *o = partial + ((uint64_t)blockIdx.y * nseg + blockIdx.x) * 8;
-        st_ef(o, s0);
-        st_ef(o + 4, s1);
+    if (threadIdx.x < (unsigned)nc * 8) {
+        const int k = threadIdx.x >> 3, e = threadIdx.x & 7;
+        uint32_t acc = 0;
+        for (int q = 0; q < NT / 64; q++) acc = add(acc, red[q][k][e]);
+        partial[((uint64_t)(cb0 + k) * nseg + blockIdx.x) * 8 + e] = acc;
     }
 }
 
 void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next, int nseg,
                      uint32_t *partial, hipStream_t s) {
     if (!ncols) return;
-    hipLaunchKernelGGL(k_open_dot, dim3(nseg, ncols), dim3(NT), 0, s, d_cols, n, w, (int)with_next, nseg, partial);
+    hipLaunchKernelGGL(k_open_dot, dim3(nseg, (ncols + OPEN_CB - 1) / OPEN_CB), dim3(NT), 0, s, d_cols, ncols, n, w,
+                       (int)with_next, nseg, partial);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -397,10 +427,15 @@ __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
     for (uint32_t m = 0; m < a.nmats; m++) {
         const uint32_t ncols = d[0], coff = d[1], npts = d[2];
         ef s = ef_zero();
-        for (uint32_t c = 0; c < ncols; c++) {
-            const uint32_t *col = (const uint32_t *)a.cols[coff + c];
-            s = ef_add(s, ef_mul_base(ld_ef(a.alpha_pows + 4 * c), col[i]));
+        uint32_t c = 0;
+        for (; c + 8 <= ncols; c += 8) {  // 8 loads in flight
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = ((const uint32_t *)a.cols[coff + c + k])[i];
+#pragma unroll
+            for (int k = 0; k < 8; k++) s = ef_add(s, ef_mul_base(ld_ef(a.alpha_pows + 4 * (c + k)), v[k]));
         }
+        for (; c < ncols; c++) s = ef_add(s, ef_mul_base(ld_ef(a.alpha_pows + 4 * c), ((const uint32_t *)a.cols[coff + c])[i]));
         const uint32_t *pp = d + 3;
         for (uint32_t p = 0; p < npts; p++, pp += 9) {
             ef A{{pp[1], pp[2], pp[3], pp[4]}}, B{{pp[5], pp[6], pp[7], pp[8]}};

@@ -404,7 +404,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     //   p(z) = ((z/s)^N - 1)/N * sum_j y_j w^j / (z/s - w^j); next point g z uses y_{j+1}.
     // All dot products are launched back to back and read back with one copy.
     {
-        const int nseg = 32;
+        const int nseg = 128;  // row segments per column chunk (k_open_dot grid: nseg x ceil(W / 8))
         struct Pend { OpenReq *r; const uint32_t *ybase; uint64_t N, W; bool bitrev; uint32_t shift; uint64_t coff, poff; ef pre; };
         std::vector<Pend> pend;
         uint64_t ncols_all = 0, nparts = 0;
