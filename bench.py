@@ -75,6 +75,27 @@ def pmc_traffic(stage):
     return round(d["hbm_bytes_per_launch"]), os.path.basename(files[-1])
 
 
+VALU_PEAK_TSLOTS = 256 * 4 * 32 * 2.4e9 / 1e12  # CUs x SIMDs x SIMD-32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
+
+
+def valu_roofline(perms, ms):
+    """Poseidon2 leaf hashing is integer-VALU bound: issue slots per permutation (static ISA count of
+    the permutation weighted by the measured issue cost of each instruction class,
+    profiles/rNN_isa_p2.json from tools/isa_slots.py) x permutations / measured stage time, against
+    the architectural VALU issue rate."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_isa_p2.json")))
+    if not files:
+        return None
+    slots = json.load(open(files[-1]))["issue_slots"]
+    pps = perms / (ms / 1e3)
+    achieved = pps * slots / 1e12
+    return {"bound": "valu", "achieved": round(achieved, 2), "peak": round(VALU_PEAK_TSLOTS, 2),
+            "unit": "T VALU issue slots/s", "frac": round(achieved / VALU_PEAK_TSLOTS, 4),
+            "permutations_per_s": round(pps), "slots_per_permutation": slots,
+            "source": os.path.basename(files[-1])}
+
+
 def cpu_baseline(log_n, queries):
     """The CPU oracle (a C/OpenMP restatement, not the reference binary) on one bounded shard."""
     from tests import _oracle as O
@@ -180,7 +201,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
                 "launches": cnt, "avg_ms": round(ms / cnt, 4),
                 "algorithmic_bytes_per_launch": round(units / cnt), "traffic_source": tsrc}
-    stages = {k: {"count": v[0], "ms_per_step": round(v[1] / args.steps, 3)} for k, v in sorted(prof.items())}
+    if dom == "merkle_leaves" and "merkle_leaves_perms" in prof:
+        roofline["valu"] = valu_roofline(prof["merkle_leaves_perms"][2], ms)
+    stages = {k: {"count": v[0], "ms_per_step": round(v[1] / args.steps, 3)}
+              for k, v in sorted(prof.items()) if not k.endswith("_perms")}
 
     value = world * rows_per_shard * args.steps / elapsed
     line = {

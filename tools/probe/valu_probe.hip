@@ -29,6 +29,18 @@ KERNEL32(k_mul_u24, "v_mul_u32_u24 %0, %0, %1")
 KERNEL32(k_mad_u24, "v_mad_u32_u24 %0, %0, %1, %0")
 KERNEL32(k_add3, "v_add3_u32 %0, %0, %1, %0")
 KERNEL32(k_lshl_add, "v_lshl_add_u32 %0, %0, 3, %1")
+KERNEL32(k_sub, "v_sub_u32 %0, %0, %1")
+KERNEL32(k_add_lit, "v_add_u32 %0, 0x80ffffff, %0")
+KERNEL32(k_add_e64, "v_add_u32_e64 %0, %0, %1")
+KERNEL32(k_and, "v_and_b32 %0, %0, %1")
+KERNEL32(k_xor, "v_xor_b32 %0, %0, %1")
+KERNEL32(k_lshl, "v_lshlrev_b32 %0, 3, %0")
+KERNEL32(k_max, "v_max_u32 %0, %0, %1")
+KERNEL32(k_min3, "v_min3_u32 %0, %0, %1, %0")
+KERNEL32(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+KERNEL32(k_addmin, "v_add_u32 %0, %0, %1\n v_min_u32 %0, %0, %1")
+KERNEL32(k_mov, "v_mov_b32 %0, %1")
+KERNEL32(k_pk_add_u16, "v_pk_add_u16 %0, %0, %1")
 
 #define CHAIN8_64(INS)                                                                      \
     asm volatile(INS : "+v"(a0) : "v"(b)); asm volatile(INS : "+v"(a1) : "v"(b));             \
@@ -68,6 +80,10 @@ int main() {
         {"v_add_u32", k_add}, {"v_min_u32", k_min}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi},
         {"v_mul_u32_u24", k_mul_u24}, {"v_mad_u32_u24", k_mad_u24}, {"v_add3_u32", k_add3},
         {"v_lshl_add_u32", k_lshl_add}, {"v_lshl_add_u64", k_lshl_add_u64}, {"v_mad_u64_u32", k_mad_u64},
+        {"v_sub_u32", k_sub}, {"v_add_u32 literal", k_add_lit}, {"v_add_u32_e64", k_add_e64}, {"v_and_b32", k_and},
+        {"v_xor_b32", k_xor}, {"v_lshlrev_b32", k_lshl}, {"v_max_u32", k_max}, {"v_min3_u32", k_min3},
+        {"v_cndmask_b32", k_cndmask}, {"add+min (x2 ops)", k_addmin}, {"v_mov_b32", k_mov},
+        {"v_pk_add_u16", k_pk_add_u16},
     };
     hipEvent_t e0, e1;
     hipEventCreate(&e0);

@@ -208,6 +208,7 @@ void tree_build(DTree &t, hipStream_t s) {
     t.layers[0] = t.layer_store.back().p;
     {
         PROF("merkle_leaves", s, 4.0 * maxh * ncols + 32.0 * maxh);  // algorithmic bytes
+        prof_add("merkle_leaves_perms", (double)maxh * ((ncols + 7) / 8));
         hipLaunchKernelGGL(k_hash_leaves, dim3((unsigned)((maxh + NT - 1) / NT)), dim3(NT), 0, s,
                            (const uint64_t *)colbufs[0].p, ncols, maxh, t.layers[0]);
         HIP_CHECK(hipGetLastError());

@@ -64,6 +64,14 @@ HostScope::~HostScope() {
     t.ms += ms;
 }
 
+void prof_add(const char *name, double units) {
+    if (!g_prof_on.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> g(g_mu);
+    Tot &t = g_tot[name];
+    t.count++;
+    t.units += units;
+}
+
 }  // namespace zkm
 
 extern "C" {

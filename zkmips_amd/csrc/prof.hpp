@@ -27,6 +27,9 @@ struct HostScope {
     ~HostScope();
 };
 
+// adds work units to a stage without timing it (e.g. permutations behind a timed stage)
+void prof_add(const char *name, double units);
+
 #define ZKM_PROF_CAT2(a, b) a##b
 #define ZKM_PROF_CAT(a, b) ZKM_PROF_CAT2(a, b)
 #define HPROF(name) ::zkm::HostScope ZKM_PROF_CAT(_hprof_, __LINE__)(name)
