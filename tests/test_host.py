@@ -89,3 +89,18 @@ def test_quotient_jit_codegen_compiles_for_gfx950():
     bad[1] = 99
     assert lib.zkm_quotient_jit_compile(bad.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(bad.size),
                                         ctypes.byref(n)) == -1
+
+
+def test_product_poseidon2_host_matches_oracle(tmp_path):
+    """The product permutation (p2.cuh: scaled state, 64-bit linear layers, lazy reductions) compiled
+    for the host agrees with the oracle's on KAT-style edge states and random states."""
+    exe = tmp_path / "p2chk"
+    orc = tmp_path / "orc_p2.o"
+    import subprocess
+    subprocess.check_call(["gcc", "-O2", "-c", os.path.join(ROOT, "oracle", "poseidon2.c"), "-o", str(orc)])
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "--offload-arch=gfx950", "-x", "hip",
+                           os.path.join(ROOT, "tools", "check", "p2_host_check.cpp"), "-x", "none", str(orc),
+                           "-o", str(exe)])
+    out = subprocess.run([str(exe), "40000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 mismatches" in out.stdout

@@ -4,7 +4,8 @@ Compiles zkmips_amd/csrc/merkle.hip for gfx950 (device only), disassembles k_p2_
 permutation per thread, straight-line) and weights each VALU instruction by its measured issue cost
 on MI355X (tools/probe/valu_probe.hip, profiles/r01_valu_probe.txt): v_add/v_sub/bitwise/v_mov run
 at the full SIMD-32 rate (1 slot per wave64 instruction pair of cycles), everything else we use
-(min/max, shifts, 32-bit multiplies, v_mad_u64_u32, 3-operand forms, DPP/SDWA forms) at half rate
+(min/max, shifts, 32-bit multiplies, v_mad_u64_u32, v_lshl_add_u64, carry-out adds v_add_co/v_addc_co,
+3-operand forms, DPP/SDWA forms) at half rate
 (2 slots).  Writes profiles/<tag>_isa_p2.json.   python tools/isa_slots.py r01
 """
 import collections

@@ -66,6 +66,21 @@ __global__ void k_mad_u64(unsigned *out, unsigned seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7);
 }
 
+
+// 64-bit add as a carry pair: v_add_co_u32 (carry out to an SGPR pair) + v_addc_co_u32
+#define ADDC(lo, hi, S) asm volatile("v_add_co_u32_e64 %0, " S ", %0, %2\n v_addc_co_u32_e64 %1, " S ", %1, 0, " S \
+                                     : "+v"(lo), "+v"(hi) : "v"(b) : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55");
+__global__ void k_add64_pair(unsigned *out, unsigned seed) {
+    unsigned l0 = threadIdx.x ^ seed, l1 = l0 + 1, l2 = l0 + 2, l3 = l0 + 3, h0 = 0, h1 = 0, h2 = 0, h3 = 0, b = seed * 3 + 1;
+    for (int i = 0; i < ITERS; i++) {
+        ADDC(l0, h0, "s[40:41]") ADDC(l1, h1, "s[42:43]") ADDC(l2, h2, "s[44:45]") ADDC(l3, h3, "s[46:47]")
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = l0 ^ l1 ^ l2 ^ l3 ^ h0 ^ h1 ^ h2 ^ h3;
+}
+KERNEL32(k_add_co, "v_add_co_u32 %0, vcc, %0, %1")
+KERNEL32(k_sub_co, "v_sub_co_u32 %0, vcc, %0, %1")
+
+
 typedef void (*kfn)(unsigned *, unsigned);
 
 int main() {
@@ -83,7 +98,8 @@ int main() {
         {"v_sub_u32", k_sub}, {"v_add_u32 literal", k_add_lit}, {"v_add_u32_e64", k_add_e64}, {"v_and_b32", k_and},
         {"v_xor_b32", k_xor}, {"v_lshlrev_b32", k_lshl}, {"v_max_u32", k_max}, {"v_min3_u32", k_min3},
         {"v_cndmask_b32", k_cndmask}, {"add+min (x2 ops)", k_addmin}, {"v_mov_b32", k_mov},
-        {"v_pk_add_u16", k_pk_add_u16},
+        {"v_pk_add_u16", k_pk_add_u16}, {"v_add_co_u32 (vcc)", k_add_co}, {"v_sub_co_u32 (vcc)", k_sub_co},
+        {"add_co+addc pair (x2 ops)", k_add64_pair},
     };
     hipEvent_t e0, e1;
     hipEventCreate(&e0);

@@ -6,9 +6,6 @@
 //   External layer: M4 blocks + column sums (crates/core/machine/src/operations/poseidon2/air.rs:31-56).
 //   Internal layer: s_i <- V_i s_i + sum(s), V = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,
 //                   -1/2^8,-1/8,-1/16,-1/2^24] (air.rs:12-29).
-//
-// The internal diagonal is applied without multiplications: every V_i is +-2^a, +-3 or
-// +-2^-k, and x * 2^-k mod p is computed with shifts because p = 127 * 2^24 + 1.
 #pragma once
 #include "kb31.cuh"
 
@@ -17,6 +14,33 @@ namespace p2 {
 #include "p2_rc.inc"
 
 constexpr uint32_t cx_to_mont(uint32_t x) { return (uint32_t)((((uint64_t)(x % kb::P)) << 32) % kb::P); }
+constexpr uint32_t cx_mulmod(uint32_t a, uint32_t b) { return (uint32_t)((uint64_t)a * b % kb::P); }
+constexpr uint32_t cx_pow(uint32_t a, uint64_t e) {
+    uint64_t r = 1, b = a % kb::P;
+    for (; e; e >>= 1, b = b * b % kb::P)
+        if (e & 1) r = r * b % kb::P;
+    return (uint32_t)r;
+}
+constexpr uint32_t cx_inv(uint32_t a) { return cx_pow(a, kb::P - 2); }
+constexpr uint32_t cx_neg(uint32_t x) { return x ? kb::P - x : 0; }
+constexpr uint32_t cx_inv2k(int k) { return cx_inv(cx_pow(2, (uint64_t)k)); }  // 2^-k mod p
+
+// Internal-layer diagonal V (canonical), air.rs:12-29
+struct DiagTable {
+    uint32_t v[16];
+};
+constexpr DiagTable make_diag_canon() {
+    return DiagTable{{cx_neg(2), 1, 2, cx_inv2k(1), 3, 4, cx_neg(cx_inv2k(1)), cx_neg(3), cx_neg(4), cx_inv2k(8),
+                      cx_inv2k(3), cx_inv2k(24), cx_neg(cx_inv2k(8)), cx_neg(cx_inv2k(3)), cx_neg(cx_inv2k(4)),
+                      cx_neg(cx_inv2k(24))}};
+}
+constexpr DiagTable make_diag() {  // Montgomery form (R V_i)
+    DiagTable d = make_diag_canon();
+    for (int i = 0; i < 16; i++) d.v[i] = cx_to_mont(d.v[i]);
+    return d;
+}
+constexpr DiagTable DIAG_C = make_diag_canon();
+constexpr DiagTable DIAG = make_diag();
 
 struct RcTable {
     uint32_t ext[8][16];  // full rounds 0..7 (Montgomery)
@@ -33,106 +57,174 @@ constexpr RcTable make_rc() {
 }
 constexpr RcTable RC = make_rc();
 
-// x * 2^-k mod p for 1 <= k <= 24 (x in [0,p)): (x + m p) / 2^k with m = -x mod 2^k,
-// and m p = m + (127 m) 2^24, so the quotient is (127 m) 2^(24-k) + (x + m) >> k  (< p).
-KB_HD uint32_t div_pow2(uint32_t x, int k) {
-    uint32_t m = (0u - x) & ((1u << k) - 1u);
-    return ((m * 127u) << (24 - k)) + ((x + m) >> k);
+// ---------------------------------------------------------------------------------------------
+// One-thread permutation: scaled state, 64-bit linear layers, lazy Montgomery reductions.
+//
+// The state is carried at the scale LAMBDA = 2^80 mod p (a stored value v stands for v / LAMBDA)
+// instead of the Montgomery scale R = 2^32.  Because LAMBDA^2 = R^5 a full round closes on itself:
+//   r  = redc(v + LAMBDA rc)   scale LAMBDA / R   (one Montgomery reduction of a 64-bit sum)
+//   y  = r^3 / R^2             scale LAMBDA       (two Montgomery products)
+//   v' = M_E y                 scale LAMBDA       (64-bit integer adds, no reductions at all)
+// The internal layer s_i <- V_i s_i + sum is one v_mad_u64_u32 + one lazy reduction per element,
+// redc(s_i (R V_i) + X) with X = R sum (mod p), and element 0's next S-box input is taken straight
+// from the partial sum.  Every 32-bit intermediate stays in (0, 2P) (bounds in the comments);
+// input and output are canonical Montgomery values in [0, P).
+//
+// Device code pins the instruction selection with inline asm: one v_mad_u64_u32 per product-sum
+// (left alone the compiler splits a*b + (P << 32) into v_mul_lo + v_mul_hi + add) and an opaque
+// 32-bit subtract in the reduction (otherwise it widens it to a 64-bit v_sub_co/v_subb pair).
+constexpr uint64_t LIFT = (uint64_t)kb::P << 32;  // = 0 mod p, keeps t >= P 2^32
+#ifdef __HIP_DEVICE_COMPILE__
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {  // c in VGPRs
+    uint64_t t, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "v"(c));
+    return t;
+}
+__device__ __forceinline__ uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) {  // k uniform (SGPR)
+    uint64_t t, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "s"(k), "v"(c));
+    return t;
+}
+__device__ __forceinline__ uint64_t mad64_lift(uint32_t a, uint32_t b) {  // a b + LIFT, LIFT in SGPRs
+    uint64_t t, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "s"(LIFT));
+    return t;
+}
+__device__ __forceinline__ uint32_t sub32(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+#else
+inline uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
+inline uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) { return (uint64_t)a * k + c; }
+inline uint64_t mad64_lift(uint32_t a, uint32_t b) { return (uint64_t)a * b + LIFT; }
+inline uint32_t sub32(uint32_t a, uint32_t b) { return a - b; }
+#endif
+// t in [P 2^32, 2P 2^32) -> t / 2^32 mod p in (t / 2^32 - P, t / 2^32): low words of t and m P
+// agree, so the quotient is exact without a 64-bit subtract
+KB_HD uint32_t redc_hi(uint64_t t) {
+    const uint32_t m = (uint32_t)t * kb::MU;
+    return sub32((uint32_t)(t >> 32), kb::umulhi(m, kb::P));
+}
+KB_HD uint32_t mul_l(uint32_t a, uint32_t b) { return redc_hi(mad64_lift(a, b)); }  // a b < P 2^32
+// r < P + 2^10: r^2 < P 2^32 -> sq < 2P; sq r < 2P (P + 2^10) < P 2^32 -> result in (0, 2P)
+KB_HD uint32_t cube_l(uint32_t r) { return mul_l(mul_l(r, r), r); }
+// 32-bit representative of v < 2^38 (2^31 = 2^24 - 1 mod p): lo + hi (2^24 - 1) < 2^31 + hi 2^24
+KB_HD uint32_t fold31(uint64_t v) {
+    const uint32_t hi = (uint32_t)(v >> 31), lo = (uint32_t)v & 0x7fffffffu;
+    return lo + (hi << 24) - hi;
 }
 
-KB_HD void m4(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t &x3) {
-    using namespace kb;
-    uint32_t t01 = add(x0, x1);
-    uint32_t t23 = add(x2, x3);
-    uint32_t t0123 = add(t01, t23);
-    uint32_t t01123 = add(t0123, x1);
-    uint32_t t01233 = add(t0123, x3);
-    uint32_t n3 = add(t01233, dbl(x0));
-    uint32_t n1 = add(t01123, dbl(x2));
-    uint32_t n0 = add(t01123, t01);
-    uint32_t n2 = add(t01233, t23);
-    x0 = n0; x1 = n1; x2 = n2; x3 = n3;
+constexpr uint32_t LAMBDA = cx_pow(2, 80);  // LAMBDA^2 = 2^160 = R^5
+constexpr uint32_t K_IN = LAMBDA;           // mont(x R, K_IN) = x LAMBDA
+constexpr uint32_t K_OUT = cx_inv2k(16);    // mont(x LAMBDA, R^2 / LAMBDA) = x R
+constexpr uint32_t R_MOD = cx_pow(2, 32);   // X = R lo + (R 2^30) hi for sum = hi 2^30 + lo
+constexpr uint32_t R_2_30 = cx_pow(2, 62);
+
+struct FastTable {
+    uint64_t ext[8][16];  // LIFT + LAMBDA rc (full rounds)
+    uint64_t inr[13];     // LIFT + LAMBDA rc (partial rounds, element 0)
+};
+constexpr FastTable make_fast() {
+    FastTable t{};
+    for (int r = 0; r < 4; r++)
+        for (int i = 0; i < 16; i++) t.ext[r][i] = LIFT + cx_mulmod(LAMBDA, kP2RoundConstCanon[r][i] % kb::P);
+    for (int r = 0; r < 13; r++) t.inr[r] = LIFT + cx_mulmod(LAMBDA, kP2RoundConstCanon[4 + r][0] % kb::P);
+    for (int r = 4; r < 8; r++)
+        for (int i = 0; i < 16; i++) t.ext[r][i] = LIFT + cx_mulmod(LAMBDA, kP2RoundConstCanon[r + 13][i] % kb::P);
+    return t;
+}
+constexpr FastTable FT = make_fast();
+
+// External layer on y < 2P: circ(2 M4, M4, M4, M4) y, outputs < 35 * 2P < 2^37.
+KB_HD void external64(const uint32_t y[16], uint64_t v[16]) {
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+        const uint64_t t01 = (uint64_t)y[j] + y[j + 1], t23 = (uint64_t)y[j + 2] + y[j + 3];
+        const uint64_t t0123 = t01 + t23;
+        const uint64_t t01123 = t0123 + y[j + 1], t01233 = t0123 + y[j + 3];
+        v[j] = t01123 + t01;
+        v[j + 1] = t01123 + 2 * (uint64_t)y[j + 2];
+        v[j + 2] = t01233 + t23;
+        v[j + 3] = t01233 + 2 * (uint64_t)y[j];
+    }
+    uint64_t sums[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) sums[k] = (v[k] + v[4 + k]) + (v[8 + k] + v[12 + k]);
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] += sums[j & 3];
 }
 
-KB_HD void external_layer(uint32_t s[16]) {
-    using namespace kb;
+// full round from prepared S-box inputs r (scale LAMBDA / R, r < P + 2^10) to v (scale LAMBDA)
+KB_HD void full_round(const uint32_t r[16], uint64_t v[16]) {
+    uint32_t y[16];
 #pragma unroll
-    for (int j = 0; j < 16; j += 4) m4(s[j], s[j + 1], s[j + 2], s[j + 3]);
-    uint32_t sums[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) sums[k] = add(add(s[k], s[4 + k]), add(s[8 + k], s[12 + k]));
-#pragma unroll
-    for (int j = 0; j < 16; j++) s[j] = add(s[j], sums[j & 3]);
+    for (int j = 0; j < 16; j++) y[j] = cube_l(r[j]);
+    external64(y, v);
 }
-
-KB_HD void internal_layer(uint32_t s[16]) {
-    using namespace kb;
-    uint32_t sum = 0;
+// S-box inputs of full round `rd` from v < 2^38: t - LIFT < 2^38 + P, so r < P + 2^7
+KB_HD void prep_full(const uint64_t v[16], int rd, uint32_t r[16]) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) sum = add(sum, s[i]);
-    // s_i <- V_i s_i + sum; negative V_i as sum - |V_i| s_i
-    const uint32_t x0 = dbl(s[0]), x6 = div_pow2(s[6], 1), x7 = add(dbl(s[7]), s[7]), x8 = dbl(dbl(s[8]));
-    const uint32_t x12 = div_pow2(s[12], 8), x13 = div_pow2(s[13], 3), x14 = div_pow2(s[14], 4);
-    const uint32_t x15 = div_pow2(s[15], 24);
-    s[0] = sub(sum, x0);
-    s[1] = add(s[1], sum);
-    s[2] = add(dbl(s[2]), sum);
-    s[3] = add(div_pow2(s[3], 1), sum);
-    s[4] = add(add(dbl(s[4]), s[4]), sum);
-    s[5] = add(dbl(dbl(s[5])), sum);
-    s[6] = sub(sum, x6);
-    s[7] = sub(sum, x7);
-    s[8] = sub(sum, x8);
-    s[9] = add(div_pow2(s[9], 8), sum);
-    s[10] = add(div_pow2(s[10], 3), sum);
-    s[11] = add(div_pow2(s[11], 24), sum);
-    s[12] = sub(sum, x12);
-    s[13] = sub(sum, x13);
-    s[14] = sub(sum, x14);
-    s[15] = sub(sum, x15);
+    for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j] + FT.ext[rd][j]);
 }
 
 KB_HD void permute(uint32_t s[16]) {
-    using namespace kb;
-    external_layer(s);
+    uint32_t r[16], y[16];
+    uint64_t v[16];
+    // Montgomery input (< P) -> scale LAMBDA, initial external layer
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
+    for (int j = 0; j < 16; j++) y[j] = mul_l(s[j], K_IN);
+    external64(y, v);
 #pragma unroll
-        for (int i = 0; i < 16; i++) s[i] = cube(add(s[i], RC.ext[r][i]));
-        external_layer(s);
+    for (int rd = 0; rd < 4; rd++) {
+        prep_full(v, rd, r);
+        full_round(r, v);
     }
+    // partial rounds.  s_j (j >= 1) < 2P at scale LAMBDA; r0 = element 0's S-box input.
+    uint32_t sj[16];
 #pragma unroll
-    for (int r = 0; r < 13; r++) {
-        s[0] = cube(add(s[0], RC.inr[r]));
-        internal_layer(s);
+    for (int j = 1; j < 16; j++) sj[j] = fold31(v[j]);  // v < 70P -> < 2^31 + 70 * 2^24 < 2P
+    uint32_t r0 = redc_hi(v[0] + FT.inr[0]);
+#pragma unroll
+    for (int k = 0; k < 13; k++) {
+        const uint32_t y0 = cube_l(r0);  // (0, 2P)
+        uint64_t rest = 0;
+#pragma unroll
+        for (int j = 1; j < 16; j++) rest += sj[j];  // < 30P
+        const uint64_t acc = rest + y0;              // < 32P < 2^36
+        // element 0: V_0 = -2, so x0' = sum_{j>=1} x_j - x0; next S-box input directly
+        // (t - LIFT < 33P, so r0 < P + 17)
+        const uint64_t e0 = rest + (2 * kb::P - y0);
+        if (k < 12) {
+            r0 = redc_hi(e0 + FT.inr[k + 1]);
+            // X = R acc (mod p), X - LIFT < 2^30 R_MOD + 64 P < P (2^32 - 2P); with s_j < 2P and
+            // DIAG < P the sum below stays under 2P 2^32, so the outputs are in (0, 2P)
+            const uint32_t lo = (uint32_t)acc & 0x3fffffffu, hi = (uint32_t)(acc >> 30);
+            const uint64_t X = mad64(lo, R_MOD, mad64(hi, R_2_30, LIFT));
+#pragma unroll
+            for (int j = 1; j < 16; j++) sj[j] = redc_hi(mad64_ks(sj[j], DIAG.v[j], X));
+        } else {
+            // last partial round: produce the S-box inputs of full round 4 (scale LAMBDA / R):
+            // redc(V_j s_j + acc + LAMBDA rc) with canonical V_j, < 2P -> one conditional subtract
+            r[0] = redc_hi(e0 + FT.ext[4][0]);
+#pragma unroll
+            for (int j = 1; j < 16; j++) {
+                const uint32_t t = redc_hi(mad64_ks(sj[j], DIAG_C.v[j], acc + FT.ext[4][j]));
+                r[j] = kb::umin(t, t - kb::P);
+            }
+        }
     }
+    full_round(r, v);
 #pragma unroll
-    for (int r = 4; r < 8; r++) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) s[i] = cube(add(s[i], RC.ext[r][i]));
-        external_layer(s);
+    for (int rd = 5; rd < 8; rd++) {
+        prep_full(v, rd, r);
+        full_round(r, v);
     }
+    // scale LAMBDA -> Montgomery, reduced: fold31(v) < 2^32, fold31 * K_OUT < P 2^32
+#pragma unroll
+    for (int j = 0; j < 16; j++) s[j] = kb::mul(fold31(v[j]), K_OUT);
 }
-
-// Internal-layer diagonal V (canonical), as field elements: air.rs:12-29
-constexpr uint32_t cx_inv2k(int k) {  // 2^-k mod p
-    uint64_t r = 1, h = (kb::P + 1) / 2;
-    for (int i = 0; i < k; i++) r = r * h % kb::P;
-    return (uint32_t)r;
-}
-constexpr uint32_t cx_neg(uint32_t x) { return x ? kb::P - x : 0; }
-struct DiagTable {
-    uint32_t v[16];
-};
-constexpr DiagTable make_diag() {
-    DiagTable d{};
-    const uint32_t canon[16] = {cx_neg(2), 1, 2, cx_inv2k(1), 3, 4, cx_neg(cx_inv2k(1)), cx_neg(3), cx_neg(4),
-                                cx_inv2k(8), cx_inv2k(3), cx_inv2k(24), cx_neg(cx_inv2k(8)), cx_neg(cx_inv2k(3)),
-                                cx_neg(cx_inv2k(4)), cx_neg(cx_inv2k(24))};
-    for (int i = 0; i < 16; i++) d.v[i] = cx_to_mont(canon[i]);
-    return d;
-}
-constexpr DiagTable DIAG = make_diag();
 
 // TruncatedPermutation<_,2,8,16>: perm(l || r)[0..8]
 KB_HD void compress(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
