@@ -19,23 +19,17 @@ namespace zkm {
 
 static constexpr int NT = 256;
 
-// Absorb `ncols` columns (device pointer table) of row i into the sponge; overwrite mode.
-__device__ __forceinline__ void sponge_row(const uint64_t *__restrict__ cols, int ncols, uint64_t i, uint32_t s[16]) {
-#pragma unroll
-    for (int k = 0; k < 16; k++) s[k] = 0;
-    for (int base = 0; base < ncols; base += 8) {
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (base + k < ncols) s[k] = ((const uint32_t *)cols[base + k])[i];
-        p2::permute(s);
-    }
+// Sponge digest of row i of `ncols` columns (device pointer table); the state stays in the
+// permutation's internal representation between chunks (p2::Sponge).
+__device__ __forceinline__ void sponge_row(const uint64_t *__restrict__ cols, int ncols, uint64_t i, uint32_t d[8]) {
+    p2::sponge_hash(ncols, [&](int k) { return ((const uint32_t *)cols[k])[i]; }, d);
 }
 
 __global__ __launch_bounds__(NT) void k_hash_leaves(const uint64_t *__restrict__ cols, int ncols, uint64_t nrows,
                                                     uint32_t *__restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (i >= nrows) return;
-    uint32_t s[16];
+    uint32_t s[8];
     sponge_row(cols, ncols, i, s);
     uint4 *o = (uint4 *)(out + i * 8);
     o[0] = make_uint4(s[0], s[1], s[2], s[3]);
@@ -53,7 +47,7 @@ __global__ __launch_bounds__(NT) void k_compress_level(const uint32_t *__restric
     s[8] = c.x; s[9] = c.y; s[10] = c.z; s[11] = c.w; s[12] = d.x; s[13] = d.y; s[14] = d.z; s[15] = d.w;
     p2::permute(s);
     if (ninj) {
-        uint32_t r[16];
+        uint32_t r[8];
         sponge_row(inj, ninj, i, r);
 #pragma unroll
         for (int k = 0; k < 8; k++) s[8 + k] = r[k];

@@ -90,6 +90,18 @@ __device__ __forceinline__ uint64_t mad64_lift(uint32_t a, uint32_t b) {  // a b
     asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "s"(LIFT));
     return t;
 }
+// c + a and c + 2a for 64-bit c: a v_mad_u64_u32 with an inline-constant multiplier takes the
+// 32-bit operand as is (v_lshl_add_u64 would first need a zeroed high word, one more v_mov)
+__device__ __forceinline__ uint64_t add_w(uint64_t c, uint32_t a) {
+    uint64_t t, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(t), "=s"(cc) : "v"(a), "v"(c));
+    return t;
+}
+__device__ __forceinline__ uint64_t add_w2(uint64_t c, uint32_t a) {
+    uint64_t t, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, 2, %3" : "=v"(t), "=s"(cc) : "v"(a), "v"(c));
+    return t;
+}
 __device__ __forceinline__ uint32_t sub32(uint32_t a, uint32_t b) {
     uint32_t r;
     asm("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -99,6 +111,8 @@ __device__ __forceinline__ uint32_t sub32(uint32_t a, uint32_t b) {
 inline uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 inline uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) { return (uint64_t)a * k + c; }
 inline uint64_t mad64_lift(uint32_t a, uint32_t b) { return (uint64_t)a * b + LIFT; }
+inline uint64_t add_w(uint64_t c, uint32_t a) { return c + a; }
+inline uint64_t add_w2(uint64_t c, uint32_t a) { return c + 2 * (uint64_t)a; }
 inline uint32_t sub32(uint32_t a, uint32_t b) { return a - b; }
 #endif
 // t in [P 2^32, 2P 2^32) -> t / 2^32 mod p in (t / 2^32 - P, t / 2^32): low words of t and m P
@@ -137,65 +151,136 @@ constexpr FastTable make_fast() {
 }
 constexpr FastTable FT = make_fast();
 
-// External layer on y < 2P: circ(2 M4, M4, M4, M4) y, outputs < 35 * 2P < 2^37.
-KB_HD void external64(const uint32_t y[16], uint64_t v[16]) {
+// Round-constant injection.  The S-box output y_j = redc(sq r + A_j) takes an arbitrary addend
+// A_j = LIFT + K_j (K_j < P keeps t < 2P 2^32), which adds K_j / R to y_j for free.  Choosing
+// K = R M_E^{-1} (LAMBDA rc') makes the next external layer emit v + LAMBDA rc' directly, so the
+// next round's S-box input is just redc(v) (LIFT enters once per column sum, not per element).
+// M_E = (I_4 + J_4) (x) M4, M_E^{-1} = (I_4 - J_4 / 5) (x) M4^{-1}; M4 as in external64 below.
+struct Inj {
+    uint64_t a[16];
+};
+constexpr uint32_t cx_sub(uint32_t a, uint32_t b) { return a >= b ? a - b : a + kb::P - b; }
+constexpr uint32_t cx_add(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + b) % kb::P); }
+constexpr Inj make_inj(const uint32_t c_canon[16]) {  // c = rc' (canonical) per element
+    // M4^{-1} by Gauss-Jordan mod p
+    uint32_t m[4][8] = {{2, 3, 1, 1, 1, 0, 0, 0}, {1, 2, 3, 1, 0, 1, 0, 0}, {1, 1, 2, 3, 0, 0, 1, 0},
+                        {3, 1, 1, 2, 0, 0, 0, 1}};
+    for (int col = 0; col < 4; col++) {
+        int piv = col;
+        while (m[piv][col] == 0) piv++;
+        for (int k = 0; k < 8; k++) { const uint32_t t = m[col][k]; m[col][k] = m[piv][k]; m[piv][k] = t; }
+        const uint32_t iv = cx_inv(m[col][col]);
+        for (int k = 0; k < 8; k++) m[col][k] = cx_mulmod(m[col][k], iv);
+        for (int r = 0; r < 4; r++)
+            if (r != col && m[r][col]) {
+                const uint32_t f = m[r][col];
+                for (int k = 0; k < 8; k++) m[r][k] = cx_sub(m[r][k], cx_mulmod(f, m[col][k]));
+            }
+    }
+    uint32_t u[16] = {}, tot[4] = {};
+    for (int b = 0; b < 4; b++)
+        for (int i = 0; i < 4; i++) {
+            uint32_t acc = 0;
+            for (int k = 0; k < 4; k++) acc = cx_add(acc, cx_mulmod(m[i][4 + k], cx_mulmod(LAMBDA, c_canon[4 * b + k] % kb::P)));
+            u[4 * b + i] = acc;
+            tot[i] = cx_add(tot[i], acc);
+        }
+    const uint32_t inv5 = cx_inv(5);
+    Inj r{};
+    for (int j = 0; j < 16; j++) {
+        const uint32_t d = cx_sub(u[j], cx_mulmod(inv5, tot[j & 3]));
+        r.a[j] = LIFT + cx_mulmod(d, R_MOD);
+    }
+    return r;
+}
+struct InjTable {
+    Inj full[8];  // full[i]: injects full round i's constants (i = 1..3, 5..7; 0 and 4 unused)
+    Inj part0;    // injects partial round 0's constant (element 0 only)
+};
+constexpr InjTable make_inj_table() {
+    InjTable t{};
+    for (int i = 1; i < 8; i++) {
+        if (i == 4) continue;
+        const int row = i < 4 ? i : i + 13;
+        t.full[i] = make_inj(kP2RoundConstCanon[row]);
+    }
+    uint32_t c[16] = {};
+    c[0] = kP2RoundConstCanon[4][0];
+    t.part0 = make_inj(c);
+    return t;
+}
+constexpr InjTable INJ = make_inj_table();
+
+#ifdef __HIP_DEVICE_COMPILE__
+__device__ __forceinline__ uint64_t mad64_add(uint32_t a, uint32_t b, uint64_t k) {  // a b + k, k uniform
+    uint64_t t, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "s"(k));
+    return t;
+}
+#else
+inline uint64_t mad64_add(uint32_t a, uint32_t b, uint64_t k) { return (uint64_t)a * b + k; }
+#endif
+// cube with injected addend (see Inj); r < P + 2^10 -> (0, 2P)
+KB_HD uint32_t cube_inj(uint32_t r, uint64_t addend) { return redc_hi(mad64_add(mul_l(r, r), r, addend)); }
+
+// External layer on y < 2P: circ(2 M4, M4, M4, M4) y, outputs < 35 * 2P < 2^37, plus `lift`
+// (LIFT or 0) on every output via the four column sums.
+KB_HD void external64(const uint32_t y[16], uint64_t v[16], uint64_t lift = 0) {
 #pragma unroll
     for (int j = 0; j < 16; j += 4) {
         const uint64_t t01 = (uint64_t)y[j] + y[j + 1], t23 = (uint64_t)y[j + 2] + y[j + 3];
         const uint64_t t0123 = t01 + t23;
-        const uint64_t t01123 = t0123 + y[j + 1], t01233 = t0123 + y[j + 3];
+        const uint64_t t01123 = add_w(t0123, y[j + 1]), t01233 = add_w(t0123, y[j + 3]);
         v[j] = t01123 + t01;
-        v[j + 1] = t01123 + 2 * (uint64_t)y[j + 2];
+        v[j + 1] = add_w2(t01123, y[j + 2]);
         v[j + 2] = t01233 + t23;
-        v[j + 3] = t01233 + 2 * (uint64_t)y[j];
+        v[j + 3] = add_w2(t01233, y[j]);
     }
     uint64_t sums[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) sums[k] = (v[k] + v[4 + k]) + (v[8 + k] + v[12 + k]);
+    for (int k = 0; k < 4; k++) {
+        sums[k] = (v[k] + v[4 + k]) + (v[8 + k] + v[12 + k]);
+        if (lift) sums[k] += lift;
+    }
 #pragma unroll
     for (int j = 0; j < 16; j++) v[j] += sums[j & 3];
 }
 
-// full round from prepared S-box inputs r (scale LAMBDA / R, r < P + 2^10) to v (scale LAMBDA)
-KB_HD void full_round(const uint32_t r[16], uint64_t v[16]) {
-    uint32_t y[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) y[j] = cube_l(r[j]);
-    external64(y, v);
-}
-// S-box inputs of full round `rd` from v < 2^38: t - LIFT < 2^38 + P, so r < P + 2^7
-KB_HD void prep_full(const uint64_t v[16], int rd, uint32_t r[16]) {
-#pragma unroll
-    for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j] + FT.ext[rd][j]);
-}
-
-KB_HD void permute(uint32_t s[16]) {
+// Core permutation on the internal representation: y (scale LAMBDA, each < 2P) -> v, the last
+// external layer's 64-bit outputs (scale LAMBDA, < 70P); fold31(v) is again a valid y.
+KB_HD void permute_lam(const uint32_t y_in[16], uint64_t v[16]) {
     uint32_t r[16], y[16];
-    uint64_t v[16];
-    // Montgomery input (< P) -> scale LAMBDA, initial external layer
+    external64(y_in, v);
 #pragma unroll
-    for (int j = 0; j < 16; j++) y[j] = mul_l(s[j], K_IN);
-    external64(y, v);
+    for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j] + FT.ext[0][j]);  // round 0: explicit constants
+    // full rounds 0..2: constants of rounds 1..3 injected by the S-box, LIFT by the column sums
 #pragma unroll
-    for (int rd = 0; rd < 4; rd++) {
-        prep_full(v, rd, r);
-        full_round(r, v);
+    for (int rd = 0; rd < 3; rd++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], INJ.full[rd + 1].a[j]);
+        external64(y, v, LIFT);
+#pragma unroll
+        for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j]);  // v in [LIFT, LIFT + 70P): r < P + 35
     }
+    // full round 3 injects partial round 0's constant (element 0 only); no LIFT: v feeds fold31
+#pragma unroll
+    for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], INJ.part0.a[j]);
+    external64(y, v);
     // partial rounds.  s_j (j >= 1) < 2P at scale LAMBDA; r0 = element 0's S-box input.
     uint32_t sj[16];
 #pragma unroll
     for (int j = 1; j < 16; j++) sj[j] = fold31(v[j]);  // v < 70P -> < 2^31 + 70 * 2^24 < 2P
-    uint32_t r0 = redc_hi(v[0] + FT.inr[0]);
+    uint32_t r0 = redc_hi(v[0] + LIFT);
 #pragma unroll
     for (int k = 0; k < 13; k++) {
         const uint32_t y0 = cube_l(r0);  // (0, 2P)
-        uint64_t rest = 0;
+        uint64_t rest = sj[1];
 #pragma unroll
-        for (int j = 1; j < 16; j++) rest += sj[j];  // < 30P
-        const uint64_t acc = rest + y0;              // < 32P < 2^36
+        for (int j = 2; j < 16; j++) rest = add_w(rest, sj[j]);  // < 30P
+        const uint64_t acc = add_w(rest, y0);                     // < 32P < 2^36
         // element 0: V_0 = -2, so x0' = sum_{j>=1} x_j - x0; next S-box input directly
         // (t - LIFT < 33P, so r0 < P + 17)
-        const uint64_t e0 = rest + (2 * kb::P - y0);
+        const uint64_t e0 = add_w(rest, 2 * kb::P - y0);
         if (k < 12) {
             r0 = redc_hi(e0 + FT.inr[k + 1]);
             // X = R acc (mod p), X - LIFT < 2^30 R_MOD + 64 P < P (2^32 - 2P); with s_j < 2P and
@@ -215,15 +300,86 @@ KB_HD void permute(uint32_t s[16]) {
             }
         }
     }
-    full_round(r, v);
+    // full rounds 4..6 inject rounds 5..7; round 7 plain
 #pragma unroll
-    for (int rd = 5; rd < 8; rd++) {
-        prep_full(v, rd, r);
-        full_round(r, v);
+    for (int rd = 4; rd < 7; rd++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], INJ.full[rd + 1].a[j]);
+        external64(y, v, LIFT);
+#pragma unroll
+        for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j]);
     }
-    // scale LAMBDA -> Montgomery, reduced: fold31(v) < 2^32, fold31 * K_OUT < P 2^32
 #pragma unroll
-    for (int j = 0; j < 16; j++) s[j] = kb::mul(fold31(v[j]), K_OUT);
+    for (int j = 0; j < 16; j++) y[j] = cube_l(r[j]);
+    external64(y, v);
+}
+
+// Montgomery (< P) <-> internal representation
+KB_HD uint32_t to_lam(uint32_t x) { return mul_l(x, K_IN); }                 // (0, 2P), scale LAMBDA
+KB_HD uint32_t from_lam(uint64_t v) { return kb::mul(fold31(v), K_OUT); }  // fold31 * K_OUT < P 2^32
+
+KB_HD void permute(uint32_t s[16]) {
+    uint32_t y[16];
+    uint64_t v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) y[j] = to_lam(s[j]);
+    permute_lam(y, v);
+#pragma unroll
+    for (int j = 0; j < 16; j++) s[j] = from_lam(v[j]);
+}
+
+// PaddingFreeSponge<_,16,8,8> (overwrite mode) with the state kept in the internal
+// representation between permutations: absorbing a chunk converts only the 8 new inputs, and the
+// carried elements are folded (fold31) instead of converted out and back in.
+struct Sponge {
+    uint32_t y[16];  // scale LAMBDA, < 2P
+    uint64_t v[16];  // last permutation's output layer
+    KB_HD void init() {
+#pragma unroll
+        for (int j = 0; j < 16; j++) y[j] = 0;
+    }
+    // absorb a full chunk of 8 Montgomery inputs and permute
+    KB_HD void absorb8(const uint32_t in[8]) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) y[j] = to_lam(in[j]);
+        permute_lam(y, v);
+#pragma unroll
+        for (int j = 0; j < 16; j++) y[j] = fold31(v[j]);
+    }
+    // absorb rate inputs already in the internal representation
+    KB_HD void absorb_y(const uint32_t yin[8]) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) y[j] = yin[j];
+        permute_lam(y, v);
+#pragma unroll
+        for (int j = 0; j < 16; j++) y[j] = fold31(v[j]);
+    }
+    KB_HD void digest(uint32_t out[8]) const {
+#pragma unroll
+        for (int j = 0; j < 8; j++) out[j] = kb::mul(y[j], K_OUT);  // y = fold31(v) < 2^32
+    }
+};
+
+// Sponge hash of n Montgomery elements ld(0..n-1) (PaddingFreeSponge, overwrite mode: a partial
+// last chunk leaves the rest of the rate as the previous permutation wrote it; n = 0 -> zeros).
+template <class Load>
+KB_HD void sponge_hash(int n, const Load &ld, uint32_t out[8]) {
+    Sponge sp;
+    sp.init();
+    int base = 0;
+    for (; base + 8 <= n; base += 8) {
+        uint32_t in[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) in[k] = ld(base + k);
+        sp.absorb8(in);
+    }
+    if (base < n) {
+        uint32_t yin[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) yin[k] = base + k < n ? to_lam(ld(base + k)) : sp.y[k];
+        sp.absorb_y(yin);
+    }
+    sp.digest(out);
 }
 
 // TruncatedPermutation<_,2,8,16>: perm(l || r)[0..8]
