@@ -22,7 +22,10 @@ static constexpr int NT = 256;
 // Sponge digest of row i of `ncols` columns (device pointer table); the state stays in the
 // permutation's internal representation between chunks (p2::Sponge).
 __device__ __forceinline__ void sponge_row(const uint64_t *__restrict__ cols, int ncols, uint64_t i, uint32_t d[8]) {
-    p2::sponge_hash(ncols, [&](int k) { return ((const uint32_t *)cols[k])[i]; }, d);
+    // global (not flat) loads: flat loads also count on lgkmcnt, so every scalar-load wait inside
+    // the permutation would drain the prefetched chunk
+    typedef const __attribute__((address_space(1))) uint32_t *gptr;
+    p2::sponge_hash(ncols, [&](int k) { return ((gptr)cols[k])[i]; }, d);
 }
 
 __global__ __launch_bounds__(NT) void k_hash_leaves(const uint64_t *__restrict__ cols, int ncols, uint64_t nrows,

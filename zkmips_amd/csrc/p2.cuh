@@ -107,7 +107,22 @@ __device__ __forceinline__ uint32_t sub32(uint32_t a, uint32_t b) {
     asm("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+// Per-use scalar constants.  In a loop around the permutation (sponge, PoW) the compiler hoists
+// the ~300 distinct round/injection constants into SGPRs, runs out, and spills them to VGPR lanes
+// (a v_readlane per use).  A volatile s_mov at the point of use keeps them as immediates.
+__device__ __forceinline__ uint32_t kc32(uint32_t k) {
+    uint32_t r;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(k));
+    return r;
+}
+__device__ __forceinline__ uint64_t kc64(uint64_t k) {
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3" : "=s"(lo), "=s"(hi) : "i"((uint32_t)k), "i"((uint32_t)(k >> 32)));
+    return ((uint64_t)hi << 32) | lo;
+}
 #else
+inline uint32_t kc32(uint32_t k) { return k; }
+inline uint64_t kc64(uint64_t k) { return k; }
 inline uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 inline uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) { return (uint64_t)a * k + c; }
 inline uint64_t mad64_lift(uint32_t a, uint32_t b) { return (uint64_t)a * b + LIFT; }
@@ -252,19 +267,19 @@ KB_HD void permute_lam(const uint32_t y_in[16], uint64_t v[16]) {
     uint32_t r[16], y[16];
     external64(y_in, v);
 #pragma unroll
-    for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j] + FT.ext[0][j]);  // round 0: explicit constants
+    for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j] + kc64(FT.ext[0][j]));  // round 0: explicit constants
     // full rounds 0..2: constants of rounds 1..3 injected by the S-box, LIFT by the column sums
 #pragma unroll
     for (int rd = 0; rd < 3; rd++) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], INJ.full[rd + 1].a[j]);
+        for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], kc64(INJ.full[rd + 1].a[j]));
         external64(y, v, LIFT);
 #pragma unroll
         for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j]);  // v in [LIFT, LIFT + 70P): r < P + 35
     }
     // full round 3 injects partial round 0's constant (element 0 only); no LIFT: v feeds fold31
 #pragma unroll
-    for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], INJ.part0.a[j]);
+    for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], kc64(INJ.part0.a[j]));
     external64(y, v);
     // partial rounds.  s_j (j >= 1) < 2P at scale LAMBDA; r0 = element 0's S-box input.
     uint32_t sj[16];
@@ -282,20 +297,20 @@ KB_HD void permute_lam(const uint32_t y_in[16], uint64_t v[16]) {
         // (t - LIFT < 33P, so r0 < P + 17)
         const uint64_t e0 = add_w(rest, 2 * kb::P - y0);
         if (k < 12) {
-            r0 = redc_hi(e0 + FT.inr[k + 1]);
+            r0 = redc_hi(e0 + kc64(FT.inr[k + 1]));
             // X = R acc (mod p), X - LIFT < 2^30 R_MOD + 64 P < P (2^32 - 2P); with s_j < 2P and
             // DIAG < P the sum below stays under 2P 2^32, so the outputs are in (0, 2P)
             const uint32_t lo = (uint32_t)acc & 0x3fffffffu, hi = (uint32_t)(acc >> 30);
             const uint64_t X = mad64(lo, R_MOD, mad64(hi, R_2_30, LIFT));
 #pragma unroll
-            for (int j = 1; j < 16; j++) sj[j] = redc_hi(mad64_ks(sj[j], DIAG.v[j], X));
+            for (int j = 1; j < 16; j++) sj[j] = redc_hi(mad64_ks(sj[j], kc32(DIAG.v[j]), X));
         } else {
             // last partial round: produce the S-box inputs of full round 4 (scale LAMBDA / R):
             // redc(V_j s_j + acc + LAMBDA rc) with canonical V_j, < 2P -> one conditional subtract
-            r[0] = redc_hi(e0 + FT.ext[4][0]);
+            r[0] = redc_hi(e0 + kc64(FT.ext[4][0]));
 #pragma unroll
             for (int j = 1; j < 16; j++) {
-                const uint32_t t = redc_hi(mad64_ks(sj[j], DIAG_C.v[j], acc + FT.ext[4][j]));
+                const uint32_t t = redc_hi(mad64_ks(sj[j], kc32(DIAG_C.v[j]), acc + kc64(FT.ext[4][j])));
                 r[j] = kb::umin(t, t - kb::P);
             }
         }
@@ -304,7 +319,7 @@ KB_HD void permute_lam(const uint32_t y_in[16], uint64_t v[16]) {
 #pragma unroll
     for (int rd = 4; rd < 7; rd++) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], INJ.full[rd + 1].a[j]);
+        for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], kc64(INJ.full[rd + 1].a[j]));
         external64(y, v, LIFT);
 #pragma unroll
         for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j]);
@@ -362,21 +377,38 @@ struct Sponge {
 
 // Sponge hash of n Montgomery elements ld(0..n-1) (PaddingFreeSponge, overwrite mode: a partial
 // last chunk leaves the rest of the rate as the previous permutation wrote it; n = 0 -> zeros).
+// The next chunk is loaded before the current one is permuted, so global-load latency overlaps
+// the permutation.
 template <class Load>
 KB_HD void sponge_hash(int n, const Load &ld, uint32_t out[8]) {
     Sponge sp;
     sp.init();
+    if (n <= 0) {
+        sp.digest(out);
+        return;
+    }
+    // loads are unconditional (index clamped to n - 1): a conditional load is a branch, and the
+    // copy at its join point would force the wait before the permutation
+    auto ldc = [&](int k) { return ld(k < n ? k : n - 1); };
+    uint32_t nxt[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) nxt[k] = ldc(k);
     int base = 0;
     for (; base + 8 <= n; base += 8) {
         uint32_t in[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) in[k] = ld(base + k);
+        for (int k = 0; k < 8; k++) in[k] = nxt[k];
+#pragma unroll
+        for (int k = 0; k < 8; k++) nxt[k] = ldc(base + 8 + k);
+#ifdef __HIP_DEVICE_COMPILE__
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the permutation
+#endif
         sp.absorb8(in);
     }
     if (base < n) {
         uint32_t yin[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) yin[k] = base + k < n ? to_lam(ld(base + k)) : sp.y[k];
+        for (int k = 0; k < 8; k++) yin[k] = base + k < n ? to_lam(nxt[k]) : sp.y[k];
         sp.absorb_y(yin);
     }
     sp.digest(out);
