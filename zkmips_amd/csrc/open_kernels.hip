@@ -352,10 +352,19 @@ void launch_inv_points(const ef &z, uint32_t s, const uint32_t *tw, uint64_t M, 
 }
 
 // ------------------------------------------------------------------ opening dot products
-// partial[(col * nseg + seg) * 8 + 4p .. +4] = sum_{j in seg} y_{j + p} w_j   (p = 1 only if with_next)
-// Columns are processed OPEN_CB at a time so each weight (16 B) is read once per chunk instead of
-// once per column; the row loop is unrolled so several loads are in flight per thread.
-static constexpr int OPEN_CB = 8;
+// partial[(col * nseg + seg) * 8 + 4p .. +4] = sum_{j in seg} y_{j + p} w_j / R  (p = 1 only if with_next)
+// Each thread takes rows in pairs (j, j + NT): per EF component the two products go into one
+// v_mad_u64_u32 chain and one lazy Montgomery reduction, accumulated unreduced in 64 bits
+// (11 issue slots per pair instead of 2 x 14 for reduced multiply-adds).  OPEN_CB columns share
+// each weight load.
+static constexpr int OPEN_CB = 4;
+__device__ __forceinline__ uint64_t pair_acc(uint64_t acc, uint32_t ya, uint32_t wa, uint32_t yb, uint32_t wb) {
+    // ya wa + yb wb + LIFT < 2P^2 + LIFT < 2P 2^32 -> (0, 2P)
+    return p2::add_w(acc, p2::redc_hi(p2::mad64(ya, wa, p2::mad64_lift(yb, wb))));
+}
+// sum of lazy terms (< 2^62) -> canonical Montgomery value: redc(acc) R^2 / R = acc mod p
+__device__ __forceinline__ uint32_t acc_mod(uint64_t acc) { return mul(redc(acc), R2); }
+
 __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                  const uint32_t *__restrict__ w, int with_next, int nseg,
                                                  uint32_t *partial) {
@@ -368,36 +377,55 @@ __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ co
     const uint32_t *y[OPEN_CB];
 #pragma unroll
     for (int k = 0; k < OPEN_CB; k++) y[k] = (const uint32_t *)cols[cb0 + (k < nc ? k : 0)];
-    ef a0[OPEN_CB], a1[OPEN_CB];
+    uint64_t a0[OPEN_CB][4], a1[OPEN_CB][4];
 #pragma unroll
-    for (int k = 0; k < OPEN_CB; k++) { a0[k] = ef_zero(); a1[k] = ef_zero(); }
-    for (uint64_t j = j0 + threadIdx.x; j < j1; j += NT) {
-        const ef wj = ld_ef(w + 4 * j);
-        const uint64_t jn = (j + 1) & (n - 1);
-        uint32_t v0[OPEN_CB], v1[OPEN_CB];
+    for (int k = 0; k < OPEN_CB; k++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) { a0[k][e] = 0; a1[k][e] = 0; }
+    for (uint64_t ja = j0 + threadIdx.x; ja < j1; ja += 2 * NT) {
+        const uint64_t jb0 = ja + NT;
+        const bool hb = jb0 < j1;
+        const uint64_t jb = hb ? jb0 : ja;  // a missing second row pairs with weight 0
+        const uint4 wa = *(const uint4 *)(w + 4 * ja);
+        uint4 wb = *(const uint4 *)(w + 4 * jb);
+        if (!hb) wb = make_uint4(0, 0, 0, 0);
+        const uint32_t wav[4] = {wa.x, wa.y, wa.z, wa.w}, wbv[4] = {wb.x, wb.y, wb.z, wb.w};
+        uint32_t va[OPEN_CB], vb[OPEN_CB], na[OPEN_CB], nb[OPEN_CB];
 #pragma unroll
         for (int k = 0; k < OPEN_CB; k++) {
-            v0[k] = y[k][j];
-            v1[k] = with_next ? y[k][jn] : 0u;
+            va[k] = y[k][ja];
+            vb[k] = y[k][jb];
+            if (with_next) {
+                na[k] = y[k][(ja + 1) & (n - 1)];
+                nb[k] = y[k][(jb + 1) & (n - 1)];
+            }
         }
 #pragma unroll
-        for (int k = 0; k < OPEN_CB; k++) {
-            a0[k] = ef_add(a0[k], ef_mul_base(wj, v0[k]));
-            if (with_next) a1[k] = ef_add(a1[k], ef_mul_base(wj, v1[k]));
-        }
+        for (int k = 0; k < OPEN_CB; k++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                a0[k][e] = pair_acc(a0[k][e], va[k], wav[e], vb[k], wbv[e]);
+                if (with_next) a1[k][e] = pair_acc(a1[k][e], na[k], wav[e], nb[k], wbv[e]);
+            }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < OPEN_CB; k++) {
+        uint32_t r0[4], r1[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            r0[e] = acc_mod(a0[k][e]);
+            r1[e] = with_next ? acc_mod(a1[k][e]) : 0u;
+        }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1)
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                a0[k].c[e] = add(a0[k].c[e], __shfl_xor(a0[k].c[e], o, 64));
-                a1[k].c[e] = add(a1[k].c[e], __shfl_xor(a1[k].c[e], o, 64));
+                r0[e] = add(r0[e], __shfl_xor(r0[e], o, 64));
+                r1[e] = add(r1[e], __shfl_xor(r1[e], o, 64));
             }
         if (lane == 0)
-            for (int e = 0; e < 4; e++) { red[wid][k][e] = a0[k].c[e]; red[wid][k][4 + e] = a1[k].c[e]; }
+            for (int e = 0; e < 4; e++) { red[wid][k][e] = r0[e]; red[wid][k][4 + e] = r1[e]; }
     }
     __syncthreads();
     if (threadIdx.x < (unsigned)nc * 8) {
@@ -406,6 +434,14 @@ __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ co
         for (int q = 0; q < NT / 64; q++) acc = add(acc, red[q][k][e]);
         partial[((uint64_t)(cb0 + k) * nseg + blockIdx.x) * 8 + e] = acc;
     }
+}
+
+int open_dot_nseg(uint64_t ncols, uint64_t n) {
+    const uint64_t chunks = (ncols + OPEN_CB - 1) / OPEN_CB;
+    uint64_t nseg = chunks ? (2048 + chunks - 1) / chunks : 1;
+    const uint64_t max_seg = std::max<uint64_t>(1, n / (2 * NT));  // at least one row pair per thread
+    nseg = std::min<uint64_t>(std::max<uint64_t>(nseg, 1), std::min<uint64_t>(max_seg, 4096));
+    return (int)nseg;
 }
 
 void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next, int nseg,
@@ -417,6 +453,7 @@ void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const u
 }
 
 // ------------------------------------------------------------------ FRI reduced openings
+static constexpr uint32_t MONT_2_16 = p2::cx_to_mont(1u << 16);
 // ro[i] += sum_m sum_p (B_{m,p} - A_{m,p} S_m(i)) * inv_p[i],  S_m(i) = sum_c alpha^c y_{m,c}[i]
 // terms: per matrix: [ncols, col table offset, npts, (pt, A(4), B(4)) x npts] (words)
 __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
@@ -426,16 +463,31 @@ __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
     const uint32_t *d = a.desc;
     for (uint32_t m = 0; m < a.nmats; m++) {
         const uint32_t ncols = d[0], coff = d[1], npts = d[2];
-        ef s = ef_zero();
+        // S = sum_c alpha^c y_c / R with the (uniform) alpha^c split into 16-bit halves: eight
+        // v_mad_u64_u32 per element (SGPR multipliers, products < 2^47) accumulate without any
+        // reduction; S = redc(lo) + mont(redc(hi), 2^16) at the end of the matrix
+        uint64_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+        auto term = [&](uint32_t c, uint32_t v) {
+            const uint32_t *ap = a.alpha_pows + 4 * c;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const uint32_t al = ap[e] & 0xffffu, ah = ap[e] >> 16;
+                lo[e] = p2::mad64_ks(v, al, lo[e]);
+                hi[e] = p2::mad64_ks(v, ah, hi[e]);
+            }
+        };
         uint32_t c = 0;
         for (; c + 8 <= ncols; c += 8) {  // 8 loads in flight
             uint32_t v[8];
 #pragma unroll
             for (int k = 0; k < 8; k++) v[k] = ((const uint32_t *)a.cols[coff + c + k])[i];
 #pragma unroll
-            for (int k = 0; k < 8; k++) s = ef_add(s, ef_mul_base(ld_ef(a.alpha_pows + 4 * (c + k)), v[k]));
+            for (int k = 0; k < 8; k++) term(c + k, v[k]);
         }
-        for (; c < ncols; c++) s = ef_add(s, ef_mul_base(ld_ef(a.alpha_pows + 4 * c), ((const uint32_t *)a.cols[coff + c])[i]));
+        for (; c < ncols; c++) term(c, ((const uint32_t *)a.cols[coff + c])[i]);
+        ef s;
+#pragma unroll
+        for (int e = 0; e < 4; e++) s.c[e] = add(redc(lo[e]), mul(redc(hi[e]), MONT_2_16));
         const uint32_t *pp = d + 3;
         for (uint32_t p = 0; p < npts; p++, pp += 9) {
             ef A{{pp[1], pp[2], pp[3], pp[4]}}, B{{pp[5], pp[6], pp[7], pp[8]}};

@@ -404,12 +404,12 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     //   p(z) = ((z/s)^N - 1)/N * sum_j y_j w^j / (z/s - w^j); next point g z uses y_{j+1}.
     // All dot products are launched back to back and read back with one copy.
     {
-        const int nseg = 128;  // row segments per column chunk (k_open_dot grid: nseg x ceil(W / 8))
-        struct Pend { OpenReq *r; const uint32_t *ybase; uint64_t N, W; bool bitrev; uint32_t shift; uint64_t coff, poff; ef pre; };
+        // row segments per column chunk (k_open_dot grid: nseg x ceil(W / OPEN_CB)), sized per request
+        struct Pend { OpenReq *r; const uint32_t *ybase; uint64_t N, W; bool bitrev; uint32_t shift; uint64_t coff, poff; ef pre; int nseg; };
         std::vector<Pend> pend;
         uint64_t ncols_all = 0, nparts = 0;
         for (auto &r : req) {
-            Pend q{&r, nullptr, 0, 0, false, ONE, 0, 0, ef_zero()};
+            Pend q{&r, nullptr, 0, 0, false, ONE, 0, 0, ef_zero(), 1};
             if (r.round == 0) { q.ybase = pk.traces[r.mat].p; q.N = pk.heights[r.mat]; q.W = m.chips[pk.trace_chip[r.mat]].prep_w; }
             else if (r.round == 1) { q.ybase = md.traces[r.mat].p; q.N = md.heights[r.mat]; q.W = m.chips[md.chip[r.mat]].main_w; }
             else if (r.round == 2) { q.ybase = perm_traces[r.mat].p; q.N = md.heights[r.mat]; q.W = 4 * m.chips[md.chip[r.mat]].perm_w; }
@@ -428,8 +428,9 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             r.vals[1].assign(q.W, ef_zero());
             q.coff = ncols_all;
             q.poff = nparts;
+            q.nseg = open_dot_nseg(q.W, q.N);
             ncols_all += q.W;
-            nparts += q.W * nseg * 8;
+            nparts += q.W * q.nseg * 8;
             const ef zs = ef_mul_base(zeta, inv(q.shift));
             q.pre = ef_mul_base(ef_sub(ef_pow(zs, q.N), ef_one()), inv(to_mont((uint32_t)(q.N % P))));
             pend.push_back(q);
@@ -457,7 +458,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 launch_inv_points(ef_mul_base(zeta, inv(q.shift)), ONE, c.tw_fwd, q.N, true, true, (uint32_t *)w, s);
             }
             PROF("open_eval", s, 4.0 * q.N * q.W + 16.0 * q.N);
-            launch_open_dot((const uint64_t *)dcols.p + q.coff, (uint32_t)q.W, q.N, w, q.r->npts == 2, nseg,
+            launch_open_dot((const uint64_t *)dcols.p + q.coff, (uint32_t)q.W, q.N, w, q.r->npts == 2, q.nseg,
                             part.p + q.poff, s);
         }
         std::vector<uint32_t> hp(nparts + 1);
@@ -466,8 +467,8 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         for (auto &q : pend)
             for (uint64_t k = 0; k < q.W; k++) {
                 ef a0 = ef_zero(), a1 = ef_zero();
-                for (int sg = 0; sg < nseg; sg++) {
-                    const uint32_t *x = &hp[q.poff + (k * nseg + sg) * 8];
+                for (int sg = 0; sg < q.nseg; sg++) {
+                    const uint32_t *x = &hp[q.poff + (k * q.nseg + sg) * 8];
                     a0 = ef_add(a0, ef{{x[0], x[1], x[2], x[3]}});
                     a1 = ef_add(a1, ef{{x[4], x[5], x[6], x[7]}});
                 }
