@@ -362,8 +362,6 @@ __device__ __forceinline__ uint64_t pair_acc(uint64_t acc, uint32_t ya, uint32_t
     // ya wa + yb wb + LIFT < 2P^2 + LIFT < 2P 2^32 -> (0, 2P)
     return p2::add_w(acc, p2::redc_hi(p2::mad64(ya, wa, p2::mad64_lift(yb, wb))));
 }
-// sum of lazy terms (< 2^62) -> canonical Montgomery value: redc(acc) R^2 / R = acc mod p
-__device__ __forceinline__ uint32_t acc_mod(uint64_t acc) { return mul(redc(acc), R2); }
 
 __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                  const uint32_t *__restrict__ w, int with_next, int nseg,
@@ -453,7 +451,6 @@ void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const u
 }
 
 // ------------------------------------------------------------------ FRI reduced openings
-static constexpr uint32_t MONT_2_16 = p2::cx_to_mont(1u << 16);
 // ro[i] += sum_m sum_p (B_{m,p} - A_{m,p} S_m(i)) * inv_p[i],  S_m(i) = sum_c alpha^c y_{m,c}[i]
 // terms: per matrix: [ncols, col table offset, npts, (pt, A(4), B(4)) x npts] (words)
 __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
@@ -463,31 +460,20 @@ __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
     const uint32_t *d = a.desc;
     for (uint32_t m = 0; m < a.nmats; m++) {
         const uint32_t ncols = d[0], coff = d[1], npts = d[2];
-        // S = sum_c alpha^c y_c / R with the (uniform) alpha^c split into 16-bit halves: eight
-        // v_mad_u64_u32 per element (SGPR multipliers, products < 2^47) accumulate without any
-        // reduction; S = redc(lo) + mont(redc(hi), 2^16) at the end of the matrix
-        uint64_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
-        auto term = [&](uint32_t c, uint32_t v) {
-            const uint32_t *ap = a.alpha_pows + 4 * c;
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const uint32_t al = ap[e] & 0xffffu, ah = ap[e] >> 16;
-                lo[e] = p2::mad64_ks(v, al, lo[e]);
-                hi[e] = p2::mad64_ks(v, ah, hi[e]);
-            }
-        };
+        // S = sum_c alpha^c y_c / R: the (uniform) alpha^c split into 16-bit halves, eight
+        // v_mad_u64_u32 per element (SGPR multipliers) and no reduction until the matrix ends
+        EfAcc acc;
+        acc.zero();
         uint32_t c = 0;
         for (; c + 8 <= ncols; c += 8) {  // 8 loads in flight
             uint32_t v[8];
 #pragma unroll
             for (int k = 0; k < 8; k++) v[k] = ((const uint32_t *)a.cols[coff + c + k])[i];
 #pragma unroll
-            for (int k = 0; k < 8; k++) term(c + k, v[k]);
+            for (int k = 0; k < 8; k++) acc.base(v[k], a.alpha_pows + 4 * (c + k));
         }
-        for (; c < ncols; c++) term(c, ((const uint32_t *)a.cols[coff + c])[i]);
-        ef s;
-#pragma unroll
-        for (int e = 0; e < 4; e++) s.c[e] = add(redc(lo[e]), mul(redc(hi[e]), MONT_2_16));
+        for (; c < ncols; c++) acc.base(((const uint32_t *)a.cols[coff + c])[i], a.alpha_pows + 4 * c);
+        const ef s = acc.value();
         const uint32_t *pp = d + 3;
         for (uint32_t p = 0; p < npts; p++, pp += 9) {
             ef A{{pp[1], pp[2], pp[3], pp[4]}}, B{{pp[5], pp[6], pp[7], pp[8]}};

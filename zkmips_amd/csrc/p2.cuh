@@ -7,7 +7,7 @@
 //   Internal layer: s_i <- V_i s_i + sum(s), V = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,
 //                   -1/2^8,-1/8,-1/16,-1/2^24] (air.rs:12-29).
 #pragma once
-#include "kb31.cuh"
+#include "kb_lazy.cuh"
 
 namespace p2 {
 
@@ -69,73 +69,18 @@ constexpr RcTable RC = make_rc();
 // redc(s_i (R V_i) + X) with X = R sum (mod p), and element 0's next S-box input is taken straight
 // from the partial sum.  Every 32-bit intermediate stays in (0, 2P) (bounds in the comments);
 // input and output are canonical Montgomery values in [0, P).
-//
-// Device code pins the instruction selection with inline asm: one v_mad_u64_u32 per product-sum
-// (left alone the compiler splits a*b + (P << 32) into v_mul_lo + v_mul_hi + add) and an opaque
-// 32-bit subtract in the reduction (otherwise it widens it to a 64-bit v_sub_co/v_subb pair).
-constexpr uint64_t LIFT = (uint64_t)kb::P << 32;  // = 0 mod p, keeps t >= P 2^32
-#ifdef __HIP_DEVICE_COMPILE__
-__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {  // c in VGPRs
-    uint64_t t, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "v"(c));
-    return t;
-}
-__device__ __forceinline__ uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) {  // k uniform (SGPR)
-    uint64_t t, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "s"(k), "v"(c));
-    return t;
-}
-__device__ __forceinline__ uint64_t mad64_lift(uint32_t a, uint32_t b) {  // a b + LIFT, LIFT in SGPRs
-    uint64_t t, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "s"(LIFT));
-    return t;
-}
-// c + a and c + 2a for 64-bit c: a v_mad_u64_u32 with an inline-constant multiplier takes the
-// 32-bit operand as is (v_lshl_add_u64 would first need a zeroed high word, one more v_mov)
-__device__ __forceinline__ uint64_t add_w(uint64_t c, uint32_t a) {
-    uint64_t t, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(t), "=s"(cc) : "v"(a), "v"(c));
-    return t;
-}
-__device__ __forceinline__ uint64_t add_w2(uint64_t c, uint32_t a) {
-    uint64_t t, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, 2, %3" : "=v"(t), "=s"(cc) : "v"(a), "v"(c));
-    return t;
-}
-__device__ __forceinline__ uint32_t sub32(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-// Per-use scalar constants.  In a loop around the permutation (sponge, PoW) the compiler hoists
-// the ~300 distinct round/injection constants into SGPRs, runs out, and spills them to VGPR lanes
-// (a v_readlane per use).  A volatile s_mov at the point of use keeps them as immediates.
-__device__ __forceinline__ uint32_t kc32(uint32_t k) {
-    uint32_t r;
-    asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(k));
-    return r;
-}
-__device__ __forceinline__ uint64_t kc64(uint64_t k) {
-    uint32_t lo, hi;
-    asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3" : "=s"(lo), "=s"(hi) : "i"((uint32_t)k), "i"((uint32_t)(k >> 32)));
-    return ((uint64_t)hi << 32) | lo;
-}
-#else
-inline uint32_t kc32(uint32_t k) { return k; }
-inline uint64_t kc64(uint64_t k) { return k; }
-inline uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
-inline uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) { return (uint64_t)a * k + c; }
-inline uint64_t mad64_lift(uint32_t a, uint32_t b) { return (uint64_t)a * b + LIFT; }
-inline uint64_t add_w(uint64_t c, uint32_t a) { return c + a; }
-inline uint64_t add_w2(uint64_t c, uint32_t a) { return c + 2 * (uint64_t)a; }
-inline uint32_t sub32(uint32_t a, uint32_t b) { return a - b; }
-#endif
-// t in [P 2^32, 2P 2^32) -> t / 2^32 mod p in (t / 2^32 - P, t / 2^32): low words of t and m P
-// agree, so the quotient is exact without a 64-bit subtract
-KB_HD uint32_t redc_hi(uint64_t t) {
-    const uint32_t m = (uint32_t)t * kb::MU;
-    return sub32((uint32_t)(t >> 32), kb::umulhi(m, kb::P));
-}
+using kb::add_w;
+using kb::add_w2;
+using kb::kc32;
+using kb::kc64;
+using kb::LIFT;
+using kb::mad64;
+using kb::mad64_add;
+using kb::mad64_ks;
+using kb::mad64_lift;
+using kb::redc_hi;
+using kb::sub32;
+
 KB_HD uint32_t mul_l(uint32_t a, uint32_t b) { return redc_hi(mad64_lift(a, b)); }  // a b < P 2^32
 // r < P + 2^10: r^2 < P 2^32 -> sq < 2P; sq r < 2P (P + 2^10) < P 2^32 -> result in (0, 2P)
 KB_HD uint32_t cube_l(uint32_t r) { return mul_l(mul_l(r, r), r); }
@@ -226,15 +171,6 @@ constexpr InjTable make_inj_table() {
 }
 constexpr InjTable INJ = make_inj_table();
 
-#ifdef __HIP_DEVICE_COMPILE__
-__device__ __forceinline__ uint64_t mad64_add(uint32_t a, uint32_t b, uint64_t k) {  // a b + k, k uniform
-    uint64_t t, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "s"(k));
-    return t;
-}
-#else
-inline uint64_t mad64_add(uint32_t a, uint32_t b, uint64_t k) { return (uint64_t)a * b + k; }
-#endif
 // cube with injected addend (see Inj); r < P + 2^10 -> (0, 2P)
 KB_HD uint32_t cube_inj(uint32_t r, uint64_t addend) { return redc_hi(mad64_add(mul_l(r, r), r, addend)); }
 
