@@ -100,3 +100,27 @@ def test_multi_shard_prove(dev):
     for tr, pv, pf in zip(shards, pvss, proofs):
         rc, ref = cpu.prove(tr, pv)
         assert rc == 0 and pf == ref
+
+
+def test_concurrent_shards_from_threads(dev):
+    """prove_with_context calls commit/open for all shards of a batch from rayon workers at once
+    (crates/core/machine/src/utils/prove.rs:487-521): concurrent calls (one stream each) must give
+    exactly the proofs of sequential calls."""
+    import threading
+    gpu, cpu, _, _ = provers(dev, 1 << 12, nq=8)
+    work = [W.fib_shard(1 << 12, seed)[2:] for seed in (11, 12, 13, 14)]
+    seq = [gpu.prove_shard(tr, pv) for tr, pv in work]
+    out = [None] * len(work)
+
+    def run(i):
+        for _ in range(2):
+            out[i] = gpu.prove_shard(*work[i])
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(len(work))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert out == seq
+    rc, ref = cpu.prove(*work[0])
+    assert rc == 0 and seq[0] == ref

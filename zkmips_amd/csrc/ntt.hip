@@ -62,8 +62,52 @@ __global__ void k_from_col_major(const uint32_t *__restrict__ in, uint64_t h, ui
     }
 }
 
+// Narrow matrices (w <= 128): a block takes 64 whole rows, so its read is one contiguous span of
+// 64 w words (the 64x64-tile kernel reads 4 w-byte rows in 256-byte pieces and, for w = 67, spends
+// a second tile column on 3 words per row); each column then leaves as one 256-byte segment.
+static constexpr int TW_ROWS = 64, TW_MAXW = 128;
+__global__ __launch_bounds__(NT) void k_to_col_major_rows(const uint32_t *__restrict__ in, uint64_t h, uint32_t w,
+                                                          int mont_in, uint32_t *__restrict__ out) {
+    __shared__ uint32_t tile[TW_MAXW * (TW_ROWS + 1)];  // [c][r], pitch 65: conflict-free both ways
+    const uint64_t r0 = (uint64_t)blockIdx.x * TW_ROWS;
+    const uint32_t nr = (uint32_t)(h - r0 < TW_ROWS ? h - r0 : TW_ROWS);
+    const uint32_t n = nr * w;
+    const uint32_t *src = in + r0 * w;
+    constexpr int PER = TW_MAXW * TW_ROWS / NT;  // 32 elements per thread at most
+    uint32_t v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {  // all loads issued before the first LDS store
+        const uint32_t i = threadIdx.x + k * NT;
+        v[k] = i < n ? src[i] : 0u;
+    }
+    const float rw = 1.0f / (float)w;  // i / w by a float reciprocal, corrected (i < 2^13)
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t i = threadIdx.x + k * NT;
+        if (i < n) {
+            uint32_t r = (uint32_t)((float)i * rw);
+            if (r * w > i) r--;
+            else if ((r + 1) * w <= i) r++;
+            const uint32_t c = i - r * w;
+            tile[c * (TW_ROWS + 1) + r] = mont_in ? v[k] : to_mont(v[k]);
+        }
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (uint32_t i = threadIdx.x; i < w * TW_ROWS; i += NT) {
+        const uint32_t c = i / TW_ROWS, r = i % TW_ROWS;
+        if (r < nr) out[(uint64_t)c * h + r0 + r] = tile[c * (TW_ROWS + 1) + r];
+    }
+}
+
 void launch_to_col_major(const uint32_t *d_in, uint64_t h, uint64_t w, bool mont_in, uint32_t *d_out, hipStream_t s) {
     if (!h || !w) return;
+    if (w <= TW_MAXW) {
+        hipLaunchKernelGGL(k_to_col_major_rows, dim3((unsigned)((h + TW_ROWS - 1) / TW_ROWS)), dim3(NT), 0, s, d_in, h,
+                           (uint32_t)w, (int)mont_in, d_out);
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
     dim3 g((unsigned)((h + 63) / 64), (unsigned)((w + 63) / 64));
     hipLaunchKernelGGL(k_to_col_major, g, dim3(NT), 0, s, d_in, h, w, (int)mont_in, d_out);
     HIP_CHECK(hipGetLastError());
@@ -392,12 +436,19 @@ __device__ __forceinline__ void net16(uint32_t v[16], uint32_t off, const uint32
             for (int j = m; j < 16; j += 2 * span) {
                 const uint32_t x = v[j], y = v[j + span];
                 if (DIT) {
-                    const uint32_t tt = mul(y, w);
-                    v[j] = add(x, tt);
-                    v[j + span] = sub(x, tt);
+                    const uint32_t tt = mul(y, w);  // y may be lazy (< 2P): y w < P 2^32
+                    if (q < 3 && ((j >> (st + 1)) & 1)) {
+                        // both outputs are the multiplied operand of the next stage: leave them
+                        // unreduced in [0, 2P)
+                        v[j] = x + tt;
+                        v[j + span] = x + (P - tt);
+                    } else {
+                        v[j] = add(x, tt);
+                        v[j + span] = sub(x, tt);
+                    }
                 } else {
                     v[j] = add(x, y);
-                    v[j + span] = mul(sub(x, y), w);
+                    v[j + span] = mul(x + (P - y), w);  // (0, 2P) operand: no reduction before the product
                 }
             }
         }
@@ -487,10 +538,11 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const uint4 u = ur[q];
-                v[4 * q] = mul(mul(cs[(4 * q) * 512 + t], ge), u.x);
-                v[4 * q + 1] = mul(mul(cs[(4 * q + 1) * 512 + t], ge), u.y);
-                v[4 * q + 2] = mul(mul(cs[(4 * q + 2) * 512 + t], ge), u.z);
-                v[4 * q + 3] = mul(mul(cs[(4 * q + 3) * 512 + t], ge), u.w);
+                // inner product lazy (0, 2P): the outer one reduces
+                v[4 * q] = mul(mul_lazy(cs[(4 * q) * 512 + t], ge), u.x);
+                v[4 * q + 1] = mul(mul_lazy(cs[(4 * q + 1) * 512 + t], ge), u.y);
+                v[4 * q + 2] = mul(mul_lazy(cs[(4 * q + 2) * 512 + t], ge), u.z);
+                v[4 * q + 3] = mul(mul_lazy(cs[(4 * q + 3) * 512 + t], ge), u.w);
             }
         }
         dit13(v, x, t, tt_fwd);
@@ -543,11 +595,16 @@ __device__ __forceinline__ void net8(uint32_t *v, uint32_t off, uint32_t S, uint
                 const uint32_t a = v[k], b = v[k + span];
                 if (DIT) {
                     const uint32_t tt = mul(b, w);
-                    v[k] = add(a, tt);
-                    v[k + span] = sub(a, tt);
+                    if (q < 2 && ((k >> (st + 1)) & 1)) {  // next stage multiplies both: lazy [0, 2P)
+                        v[k] = a + tt;
+                        v[k + span] = a + (P - tt);
+                    } else {
+                        v[k] = add(a, tt);
+                        v[k + span] = sub(a, tt);
+                    }
                 } else {
                     v[k] = add(a, b);
-                    v[k + span] = mul(sub(a, b), w);
+                    v[k + span] = mul(a + (P - b), w);
                 }
             }
         }
