@@ -235,8 +235,19 @@ def main():
                 "algorithmic_bytes_per_launch": round(units / cnt), "traffic_source": tsrc}
     if dom == "merkle_leaves" and "merkle_leaves_perms" in prof:
         roofline["valu"] = valu_roofline(prof["merkle_leaves_perms"][2], ms)
+    ntt = None
+    if "lde" in prof and "lde_gfops" in prof:
+        # NTT GF-ops/s (BASELINE metric) against the HBM roofline of the same work: 12 B of HBM
+        # traffic per input element (4 B read, 8 B written) at 8 TB/s, i.e. (8e12 / 12) x ops/elem
+        lcnt, lms, lbytes = prof["lde"]
+        gfops = prof["lde_gfops"][2]
+        rate = gfops / (lms / 1e3)
+        roof = HBM_PEAK_GBS * 1e9 / lbytes * gfops
+        ntt = {"gf_ops_per_s": float(f"{rate:.4g}"), "hbm_roofline_gf_ops_per_s": float(f"{roof:.4g}"),
+               "frac": round(rate / roof, 4), "algorithmic_GBps": round(lbytes / (lms / 1e3) / 1e9, 1),
+               "launches": lcnt, "stage_ms_per_shard": round(lms / (args.steps * K), 3)}
     stages = {k: {"count": v[0], "ms_per_shard": round(v[1] / (args.steps * K), 3)}
-              for k, v in sorted(prof.items()) if not k.endswith("_perms")}
+              for k, v in sorted(prof.items()) if not k.endswith("_perms") and not k.endswith("_gfops")}
 
     value = world * K * rows_per_shard * args.steps / elapsed
     line = {
@@ -261,6 +272,7 @@ def main():
                    "proof_bytes": len(proof)},
         "pcie_inclusive_rows_per_s": round(rows_per_shard / pcie_s, 1),
         "roofline": roofline,
+        "ntt": ntt,
         "stages_ms_per_shard": stages,
     }
     if not args.no_cpu_baseline and world == 1:

@@ -43,29 +43,37 @@ KB_HD uint32_t umulhi(uint32_t a, uint32_t b) {
 #endif
 }
 
-// Montgomery reduction of t < P * 2^32.  m = t_lo * P^-1 makes the low words of t and m*P equal,
-// so (t - m*P) / 2^32 = t_hi - mulhi(m, P) exactly, in (-P, P); the wrapped negative case is
-// repaired by min(r, r + P) (no 64-bit subtract, no compare/select through VCC).
-KB_HD uint32_t redc(uint64_t t) {
-    const uint32_t m = (uint32_t)t * MU;
-    const uint32_t r = (uint32_t)(t >> 32) - umulhi(m, P);
-    return umin(r, r + P);
-}
-KB_HD uint32_t mul(uint32_t a, uint32_t b) { return redc((uint64_t)a * b); }
-// a * b / R in (0, 2P), unreduced, for a * b < P * 2^32: adding P * 2^32 to the product lifts the
-// Montgomery quotient by P (same low word, so the same m) and no correction step is needed.
-KB_HD uint32_t mul_lazy(uint32_t a, uint32_t b) {
+// Montgomery reduction with m = -t_lo P^-1: t + m P is a multiple of 2^32 and, for t < P 2^32,
+// (t + m P) / 2^32 lies in [0, 2P).  On gfx950 that is one v_mul_lo_u32 and one v_mad_u64_u32
+// (the quotient is the high word of the mad), so a reduction costs 4 issue slots, and the lazy
+// result needs no offset to stay non-negative.
+constexpr uint32_t MUN = 0x7effffffu;  // -P^{-1} mod 2^32
 #ifdef __HIP_DEVICE_COMPILE__
-    // one v_mad_u64_u32 yields both words (left to itself the compiler recomputes the low word
-    // with a separate v_mul_lo_u32, a half-rate instruction per call)
-    uint64_t t;
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(t) : "v"(a), "v"(b), "s"((uint64_t)P << 32) : "vcc");
-#else
-    const uint64_t t = (uint64_t)a * b + ((uint64_t)P << 32);
-#endif
-    const uint32_t m = (uint32_t)t * MU;
-    return (uint32_t)(t >> 32) - umulhi(m, P);
+__device__ __forceinline__ uint32_t redc2(uint64_t t) {  // t < P 2^32 -> [0, 2P)
+    const uint32_t m = (uint32_t)t * MUN;
+    uint64_t u, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(u), "=s"(cc) : "v"(m), "s"(P), "v"(t));
+    return (uint32_t)(u >> 32);
 }
+__device__ __forceinline__ uint64_t prod64(uint32_t a, uint32_t b) {  // one v_mad_u64_u32 (addend 0)
+    uint64_t u, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(u), "=s"(cc) : "v"(a), "v"(b));
+    return u;
+}
+#else
+KB_HD uint32_t redc2(uint64_t t) {
+    const uint32_t m = (uint32_t)t * MUN;
+    return (uint32_t)((t + (uint64_t)m * P) >> 32);
+}
+KB_HD uint64_t prod64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+#endif
+KB_HD uint32_t redc(uint64_t t) {  // t < P 2^32 -> [0, P)
+    const uint32_t r = redc2(t);
+    return umin(r, r - P);
+}
+KB_HD uint32_t mul(uint32_t a, uint32_t b) { return redc(prod64(a, b)); }
+// a * b / R in [0, 2P), unreduced, for a * b < P * 2^32
+KB_HD uint32_t mul_lazy(uint32_t a, uint32_t b) { return redc2(prod64(a, b)); }
 KB_HD uint32_t sqr(uint32_t a) { return mul(a, a); }
 KB_HD uint32_t to_mont(uint32_t x) { return mul(x % P, R2); }
 KB_HD uint32_t from_mont(uint32_t x) { return redc((uint64_t)x); }

@@ -4,28 +4,27 @@
 // file is embedded in the hiprtc prelude).
 //
 // Device code pins the instruction selection with inline asm: one v_mad_u64_u32 per product-sum
-// (left alone the compiler splits a*b + (P << 32) into v_mul_lo + v_mul_hi + add) and an opaque
-// 32-bit subtract in the reduction (otherwise it widens it to a 64-bit v_sub_co/v_subb pair).
+// (left alone the compiler splits a*b + c into v_mul_lo + v_mul_hi + adds).  Reductions are
+// kb::redc2 (kb31.cuh): t < P 2^32 -> [0, 2P) in 4 issue slots.
 #pragma once
 #include "kb31.cuh"
 
 namespace kb {
 
-constexpr uint64_t LIFT = (uint64_t)kb::P << 32;  // = 0 mod p, keeps t >= P 2^32
 #ifdef __HIP_DEVICE_COMPILE__
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {  // c in VGPRs
     uint64_t t, cc;
     asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "v"(c));
     return t;
 }
+__device__ __forceinline__ uint64_t prod64_ks(uint32_t a, uint32_t k) {  // a k, k uniform (SGPR)
+    uint64_t t, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(t), "=s"(cc) : "v"(a), "s"(k));
+    return t;
+}
 __device__ __forceinline__ uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) {  // k uniform (SGPR)
     uint64_t t, cc;
     asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "s"(k), "v"(c));
-    return t;
-}
-__device__ __forceinline__ uint64_t mad64_lift(uint32_t a, uint32_t b) {  // a b + LIFT, LIFT in SGPRs
-    uint64_t t, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(t), "=s"(cc) : "v"(a), "v"(b), "s"(LIFT));
     return t;
 }
 // c + a and c + 2a for 64-bit c: a v_mad_u64_u32 with an inline-constant multiplier takes the
@@ -39,11 +38,6 @@ __device__ __forceinline__ uint64_t add_w2(uint64_t c, uint32_t a) {
     uint64_t t, cc;
     asm("v_mad_u64_u32 %0, %1, %2, 2, %3" : "=v"(t), "=s"(cc) : "v"(a), "v"(c));
     return t;
-}
-__device__ __forceinline__ uint32_t sub32(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
 }
 // Per-use scalar constants.  In a loop around the permutation (sponge, PoW) the compiler hoists
 // the ~300 distinct round/injection constants into SGPRs, runs out, and spills them to VGPR lanes
@@ -59,21 +53,14 @@ __device__ __forceinline__ uint64_t kc64(uint64_t k) {
     return ((uint64_t)hi << 32) | lo;
 }
 #else
-inline uint32_t kc32(uint32_t k) { return k; }
-inline uint64_t kc64(uint64_t k) { return k; }
-inline uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
-inline uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) { return (uint64_t)a * k + c; }
-inline uint64_t mad64_lift(uint32_t a, uint32_t b) { return (uint64_t)a * b + LIFT; }
-inline uint64_t add_w(uint64_t c, uint32_t a) { return c + a; }
-inline uint64_t add_w2(uint64_t c, uint32_t a) { return c + 2 * (uint64_t)a; }
-inline uint32_t sub32(uint32_t a, uint32_t b) { return a - b; }
+KB_HD uint32_t kc32(uint32_t k) { return k; }
+KB_HD uint64_t kc64(uint64_t k) { return k; }
+KB_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
+KB_HD uint64_t mad64_ks(uint32_t a, uint32_t k, uint64_t c) { return (uint64_t)a * k + c; }
+KB_HD uint64_t prod64_ks(uint32_t a, uint32_t k) { return (uint64_t)a * k; }
+KB_HD uint64_t add_w(uint64_t c, uint32_t a) { return c + a; }
+KB_HD uint64_t add_w2(uint64_t c, uint32_t a) { return c + 2 * (uint64_t)a; }
 #endif
-// t in [P 2^32, 2P 2^32) -> t / 2^32 mod p in (t / 2^32 - P, t / 2^32): low words of t and m P
-// agree, so the quotient is exact without a 64-bit subtract
-KB_HD uint32_t redc_hi(uint64_t t) {
-    const uint32_t m = (uint32_t)t * kb::MU;
-    return sub32((uint32_t)(t >> 32), kb::umulhi(m, kb::P));
-}
 #ifdef __HIP_DEVICE_COMPILE__
 __device__ __forceinline__ uint64_t mad64_add(uint32_t a, uint32_t b, uint64_t k) {  // a b + k, k uniform
     uint64_t t, cc;
@@ -81,7 +68,7 @@ __device__ __forceinline__ uint64_t mad64_add(uint32_t a, uint32_t b, uint64_t k
     return t;
 }
 #else
-inline uint64_t mad64_add(uint32_t a, uint32_t b, uint64_t k) { return (uint64_t)a * b + k; }
+KB_HD uint64_t mad64_add(uint32_t a, uint32_t b, uint64_t k) { return (uint64_t)a * b + k; }
 #endif
 constexpr uint32_t MONT_2_16 = (uint32_t)(((uint64_t)1 << 48) % P);  // 2^16 in Montgomery form
 
@@ -126,7 +113,7 @@ struct EfAcc {
 KB_HD ef ef_dot2(const ef &base, uint32_t x0, const uint32_t *u0, uint32_t x1, const uint32_t *u1) {
     ef r;
     for (int e = 0; e < 4; e++) {
-        const uint32_t t = redc_hi(mad64_ks(x0, u0[e], mad64_ks(x1, u1[e], LIFT)));  // (0, 2P)
+        const uint32_t t = redc2(mad64_ks(x0, u0[e], prod64_ks(x1, u1[e])));  // x0 u0 + x1 u1 < 2P^2 -> [0, 2P)
         r.c[e] = add(base.c[e], umin(t, t - P));
     }
     return r;

@@ -862,6 +862,13 @@ static Twist get_twist(Ctx &c, uint64_t N, int L, uint32_t shift, hipStream_t s)
     return make(p);
 }
 
+// Algorithmic GF operations of one column's blowup-2 coset LDE: iNTT over N,
+// N twists, forward NTT over 2N = 3 (N/2) log N + N + 3 N log 2N (mul + add + sub per butterfly).
+static double lde_gf_ops(uint64_t N) {
+    const double L = (double)ilog2(N);
+    return 3.0 * (N / 2.0) * L + (double)N + 3.0 * (double)N * (L + 1.0);
+}
+
 // Bit-reversed input evaluations (quotient chunks, produced bit-reversed by k_quotient):
 //   DIT iNTT (bit-reversed in -> natural coefficients), twist on the last pass's write into both
 //   LDE halves, then DIF in place (natural -> bit-reversed): no permutation pass at all.
@@ -869,6 +876,7 @@ void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hip
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
     PROF("lde", s, 12.0 * N * W);
+    prof_add("lde_gfops", lde_gf_ops(N) * W);
     const int L = ilog2(N);
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
@@ -918,6 +926,7 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
     PROF("lde", s, 12.0 * N * W);
+    prof_add("lde_gfops", lde_gf_ops(N) * W);
     const int L = ilog2(N);
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");

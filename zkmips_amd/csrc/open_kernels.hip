@@ -359,8 +359,8 @@ void launch_inv_points(const ef &z, uint32_t s, const uint32_t *tw, uint64_t M, 
 // each weight load.
 static constexpr int OPEN_CB = 4;
 __device__ __forceinline__ uint64_t pair_acc(uint64_t acc, uint32_t ya, uint32_t wa, uint32_t yb, uint32_t wb) {
-    // ya wa + yb wb + LIFT < 2P^2 + LIFT < 2P 2^32 -> (0, 2P)
-    return p2::add_w(acc, p2::redc_hi(p2::mad64(ya, wa, p2::mad64_lift(yb, wb))));
+    // ya wa + yb wb < 2P^2 < P 2^32 -> [0, 2P)
+    return add_w(acc, redc2(mad64(ya, wa, prod64(yb, wb))));
 }
 
 __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,

@@ -62,7 +62,7 @@ constexpr RcTable RC = make_rc();
 //
 // The state is carried at the scale LAMBDA = 2^80 mod p (a stored value v stands for v / LAMBDA)
 // instead of the Montgomery scale R = 2^32.  Because LAMBDA^2 = R^5 a full round closes on itself:
-//   r  = redc(v + LAMBDA rc)   scale LAMBDA / R   (one Montgomery reduction of a 64-bit sum)
+//   r  = redc(v + LAMBDA rc)   scale LAMBDA / R   (one 4-slot Montgomery reduction, kb::redc2)
 //   y  = r^3 / R^2             scale LAMBDA       (two Montgomery products)
 //   v' = M_E y                 scale LAMBDA       (64-bit integer adds, no reductions at all)
 // The internal layer s_i <- V_i s_i + sum is one v_mad_u64_u32 + one lazy reduction per element,
@@ -73,16 +73,15 @@ using kb::add_w;
 using kb::add_w2;
 using kb::kc32;
 using kb::kc64;
-using kb::LIFT;
 using kb::mad64;
 using kb::mad64_add;
 using kb::mad64_ks;
-using kb::mad64_lift;
-using kb::redc_hi;
-using kb::sub32;
+using kb::prod64;
+using kb::prod64_ks;
+using kb::redc2;
 
-KB_HD uint32_t mul_l(uint32_t a, uint32_t b) { return redc_hi(mad64_lift(a, b)); }  // a b < P 2^32
-// r < P + 2^10: r^2 < P 2^32 -> sq < 2P; sq r < 2P (P + 2^10) < P 2^32 -> result in (0, 2P)
+KB_HD uint32_t mul_l(uint32_t a, uint32_t b) { return redc2(prod64(a, b)); }  // a b < P 2^32 -> [0, 2P)
+// r < P + 2^10: r^2 < P 2^32 -> sq < 2P; sq r < 2P (P + 2^10) < P 2^32 -> result in [0, 2P)
 KB_HD uint32_t cube_l(uint32_t r) { return mul_l(mul_l(r, r), r); }
 // 32-bit representative of v < 2^38 (2^31 = 2^24 - 1 mod p): lo + hi (2^24 - 1) < 2^31 + hi 2^24
 KB_HD uint32_t fold31(uint64_t v) {
@@ -97,24 +96,24 @@ constexpr uint32_t R_MOD = cx_pow(2, 32);   // X = R lo + (R 2^30) hi for sum = 
 constexpr uint32_t R_2_30 = cx_pow(2, 62);
 
 struct FastTable {
-    uint64_t ext[8][16];  // LIFT + LAMBDA rc (full rounds)
-    uint64_t inr[13];     // LIFT + LAMBDA rc (partial rounds, element 0)
+    uint64_t ext[8][16];  // LAMBDA rc (full rounds)
+    uint64_t inr[13];     // LAMBDA rc (partial rounds, element 0)
 };
 constexpr FastTable make_fast() {
     FastTable t{};
     for (int r = 0; r < 4; r++)
-        for (int i = 0; i < 16; i++) t.ext[r][i] = LIFT + cx_mulmod(LAMBDA, kP2RoundConstCanon[r][i] % kb::P);
-    for (int r = 0; r < 13; r++) t.inr[r] = LIFT + cx_mulmod(LAMBDA, kP2RoundConstCanon[4 + r][0] % kb::P);
+        for (int i = 0; i < 16; i++) t.ext[r][i] = cx_mulmod(LAMBDA, kP2RoundConstCanon[r][i] % kb::P);
+    for (int r = 0; r < 13; r++) t.inr[r] = cx_mulmod(LAMBDA, kP2RoundConstCanon[4 + r][0] % kb::P);
     for (int r = 4; r < 8; r++)
-        for (int i = 0; i < 16; i++) t.ext[r][i] = LIFT + cx_mulmod(LAMBDA, kP2RoundConstCanon[r + 13][i] % kb::P);
+        for (int i = 0; i < 16; i++) t.ext[r][i] = cx_mulmod(LAMBDA, kP2RoundConstCanon[r + 13][i] % kb::P);
     return t;
 }
 constexpr FastTable FT = make_fast();
 
 // Round-constant injection.  The S-box output y_j = redc(sq r + A_j) takes an arbitrary addend
-// A_j = LIFT + K_j (K_j < P keeps t < 2P 2^32), which adds K_j / R to y_j for free.  Choosing
+// A_j = K_j (K_j < P keeps t < P 2^32), which adds K_j / R to y_j for free.  Choosing
 // K = R M_E^{-1} (LAMBDA rc') makes the next external layer emit v + LAMBDA rc' directly, so the
-// next round's S-box input is just redc(v) (LIFT enters once per column sum, not per element).
+// next round's S-box input is just redc(v).
 // M_E = (I_4 + J_4) (x) M4, M_E^{-1} = (I_4 - J_4 / 5) (x) M4^{-1}; M4 as in external64 below.
 struct Inj {
     uint64_t a[16];
@@ -149,7 +148,7 @@ constexpr Inj make_inj(const uint32_t c_canon[16]) {  // c = rc' (canonical) per
     Inj r{};
     for (int j = 0; j < 16; j++) {
         const uint32_t d = cx_sub(u[j], cx_mulmod(inv5, tot[j & 3]));
-        r.a[j] = LIFT + cx_mulmod(d, R_MOD);
+        r.a[j] = cx_mulmod(d, R_MOD);
     }
     return r;
 }
@@ -172,11 +171,10 @@ constexpr InjTable make_inj_table() {
 constexpr InjTable INJ = make_inj_table();
 
 // cube with injected addend (see Inj); r < P + 2^10 -> (0, 2P)
-KB_HD uint32_t cube_inj(uint32_t r, uint64_t addend) { return redc_hi(mad64_add(mul_l(r, r), r, addend)); }
+KB_HD uint32_t cube_inj(uint32_t r, uint64_t addend) { return redc2(mad64_add(mul_l(r, r), r, addend)); }
 
-// External layer on y < 2P: circ(2 M4, M4, M4, M4) y, outputs < 35 * 2P < 2^37, plus `lift`
-// (LIFT or 0) on every output via the four column sums.
-KB_HD void external64(const uint32_t y[16], uint64_t v[16], uint64_t lift = 0) {
+// External layer on y < 2P: circ(2 M4, M4, M4, M4) y, outputs < 35 * 2P < 2^37.
+KB_HD void external64(const uint32_t y[16], uint64_t v[16]) {
 #pragma unroll
     for (int j = 0; j < 16; j += 4) {
         const uint64_t t01 = (uint64_t)y[j] + y[j + 1], t23 = (uint64_t)y[j + 2] + y[j + 3];
@@ -191,7 +189,6 @@ KB_HD void external64(const uint32_t y[16], uint64_t v[16], uint64_t lift = 0) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         sums[k] = (v[k] + v[4 + k]) + (v[8 + k] + v[12 + k]);
-        if (lift) sums[k] += lift;
     }
 #pragma unroll
     for (int j = 0; j < 16; j++) v[j] += sums[j & 3];
@@ -203,17 +200,17 @@ KB_HD void permute_lam(const uint32_t y_in[16], uint64_t v[16]) {
     uint32_t r[16], y[16];
     external64(y_in, v);
 #pragma unroll
-    for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j] + kc64(FT.ext[0][j]));  // round 0: explicit constants
-    // full rounds 0..2: constants of rounds 1..3 injected by the S-box, LIFT by the column sums
+    for (int j = 0; j < 16; j++) r[j] = redc2(v[j] + kc64(FT.ext[0][j]));  // round 0: explicit constants
+    // full rounds 0..2: constants of rounds 1..3 injected by the S-box
 #pragma unroll
     for (int rd = 0; rd < 3; rd++) {
 #pragma unroll
         for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], kc64(INJ.full[rd + 1].a[j]));
-        external64(y, v, LIFT);
+        external64(y, v);
 #pragma unroll
-        for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j]);  // v in [LIFT, LIFT + 70P): r < P + 35
+        for (int j = 0; j < 16; j++) r[j] = redc2(v[j]);  // v < 70P: r < P + 35
     }
-    // full round 3 injects partial round 0's constant (element 0 only); no LIFT: v feeds fold31
+    // full round 3 injects partial round 0's constant (element 0 only)
 #pragma unroll
     for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], kc64(INJ.part0.a[j]));
     external64(y, v);
@@ -221,7 +218,7 @@ KB_HD void permute_lam(const uint32_t y_in[16], uint64_t v[16]) {
     uint32_t sj[16];
 #pragma unroll
     for (int j = 1; j < 16; j++) sj[j] = fold31(v[j]);  // v < 70P -> < 2^31 + 70 * 2^24 < 2P
-    uint32_t r0 = redc_hi(v[0] + LIFT);
+    uint32_t r0 = redc2(v[0]);
 #pragma unroll
     for (int k = 0; k < 13; k++) {
         const uint32_t y0 = cube_l(r0);  // (0, 2P)
@@ -230,23 +227,23 @@ KB_HD void permute_lam(const uint32_t y_in[16], uint64_t v[16]) {
         for (int j = 2; j < 16; j++) rest = add_w(rest, sj[j]);  // < 30P
         const uint64_t acc = add_w(rest, y0);                     // < 32P < 2^36
         // element 0: V_0 = -2, so x0' = sum_{j>=1} x_j - x0; next S-box input directly
-        // (t - LIFT < 33P, so r0 < P + 17)
+        // (t < 33P, so r0 < P + 17)
         const uint64_t e0 = add_w(rest, 2 * kb::P - y0);
         if (k < 12) {
-            r0 = redc_hi(e0 + kc64(FT.inr[k + 1]));
-            // X = R acc (mod p), X - LIFT < 2^30 R_MOD + 64 P < P (2^32 - 2P); with s_j < 2P and
+            r0 = redc2(e0 + kc64(FT.inr[k + 1]));
+            // X = R acc (mod p), X < 2^30 R_MOD + 64 P < P (2^32 - 2P); with s_j < 2P and
             // DIAG < P the sum below stays under 2P 2^32, so the outputs are in (0, 2P)
             const uint32_t lo = (uint32_t)acc & 0x3fffffffu, hi = (uint32_t)(acc >> 30);
-            const uint64_t X = mad64(lo, R_MOD, mad64(hi, R_2_30, LIFT));
+            const uint64_t X = mad64_ks(lo, kc32(R_MOD), prod64_ks(hi, kc32(R_2_30)));
 #pragma unroll
-            for (int j = 1; j < 16; j++) sj[j] = redc_hi(mad64_ks(sj[j], kc32(DIAG.v[j]), X));
+            for (int j = 1; j < 16; j++) sj[j] = redc2(mad64_ks(sj[j], kc32(DIAG.v[j]), X));
         } else {
             // last partial round: produce the S-box inputs of full round 4 (scale LAMBDA / R):
             // redc(V_j s_j + acc + LAMBDA rc) with canonical V_j, < 2P -> one conditional subtract
-            r[0] = redc_hi(e0 + kc64(FT.ext[4][0]));
+            r[0] = redc2(e0 + kc64(FT.ext[4][0]));
 #pragma unroll
             for (int j = 1; j < 16; j++) {
-                const uint32_t t = redc_hi(mad64_ks(sj[j], kc32(DIAG_C.v[j]), acc + kc64(FT.ext[4][j])));
+                const uint32_t t = redc2(mad64_ks(sj[j], kc32(DIAG_C.v[j]), acc + kc64(FT.ext[4][j])));
                 r[j] = kb::umin(t, t - kb::P);
             }
         }
@@ -256,9 +253,9 @@ KB_HD void permute_lam(const uint32_t y_in[16], uint64_t v[16]) {
     for (int rd = 4; rd < 7; rd++) {
 #pragma unroll
         for (int j = 0; j < 16; j++) y[j] = cube_inj(r[j], kc64(INJ.full[rd + 1].a[j]));
-        external64(y, v, LIFT);
+        external64(y, v);
 #pragma unroll
-        for (int j = 0; j < 16; j++) r[j] = redc_hi(v[j]);
+        for (int j = 0; j < 16; j++) r[j] = redc2(v[j]);
     }
 #pragma unroll
     for (int j = 0; j < 16; j++) y[j] = cube_l(r[j]);
