@@ -134,9 +134,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # ZKM_BENCH_REHEARSE=1: rehearse the N-rank flow on a box with fewer GPUs (ranks share the
+    # cards, gloo instead of RCCL); never set by the driver, so the N-GPU bench is always RCCL
+    rehearse = os.environ.get("ZKM_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
+    coll_dev = "cpu" if rehearse else "cuda"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from zkmips_amd import workloads as W
     from zkmips_amd._lib import Device, lib
@@ -180,7 +189,7 @@ def main():
         if world == 1:
             return {0: proof}
         from zkmips_amd.dist import gather_proofs
-        return gather_proofs({rank: proof}, device="cuda")
+        return gather_proofs({rank: proof}, device=coll_dev)
 
     if args.warmup:
         run_steps(args.warmup)
@@ -197,7 +206,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

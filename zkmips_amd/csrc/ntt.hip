@@ -493,63 +493,107 @@ __device__ __forceinline__ void dif13(uint32_t v[16], uint32_t *x, uint32_t t, c
     __syncthreads();  // LDS free for the next user
 }
 
-// DIT over all 13 stages: v in L2 (bit-reversed input) -> v in L512 (natural)
-__device__ __forceinline__ void dit13(uint32_t v[16], uint32_t *x, uint32_t t, const uint32_t *__restrict__ tw) {
-    stage_h1(v, t & 1);
-    net16<true, 2>(v, lay_off<2>(t), tw);
-    to_lds<2>(x, v, t);
-    __syncthreads();
-    from_lds<32>(x, v, t);
-    net16<true, 32>(v, lay_off<32>(t), tw);
-    __syncthreads();
-    to_lds<32>(x, v, t);
-    __syncthreads();
-    from_lds<512>(x, v, t);
-    net16<true, 512>(v, lay_off<512>(t), tw);
-    __syncthreads();
-}
 }  // namespace t13
 
 // Fused middle of the natural-input LDE for transforms larger than one tile: the iNTT's last 13
-// (DIF) stages, both coset twists and the forward transforms' first 13 (DIT) stages, with the
-// coefficients kept in registers between the two cosets.
-__global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
-                                                          int L, const uint32_t *__restrict__ tt_inv,
-                                                          const uint32_t *__restrict__ tt_fwd, Twist tws,
-                                                          uint64_t dst_half) {
+// (DIF) stages, both coset twists and the forward transforms' first 13 (DIT) stages.  Both cosets
+// run at once: the coefficients never leave registers, the two forward transforms share their
+// twiddle loads and barriers.  VALU-bound: 343 issue slots per input element (19.5 butterflies
+// + 4 twist products), measured at 0.86 of the VALU issue rate.
+namespace t13 {
+template <bool DIT, int SE>
+__device__ __forceinline__ void net16x2(uint32_t v0[16], uint32_t v1[16], uint32_t off,
+                                        const uint32_t *__restrict__ tt) {
+    uint32_t w16[16];
+    const uint4 *row = (const uint4 *)(tt + (tt_row(SE) + off) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint4 r = row[q];
+        w16[4 * q] = r.x; w16[4 * q + 1] = r.y; w16[4 * q + 2] = r.z; w16[4 * q + 3] = r.w;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int st = DIT ? q : 3 - q;
+        const int span = 1 << st;
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+            const uint32_t w = w16[span - 1 + m];
+#pragma unroll
+            for (int j = m; j < 16; j += 2 * span) {
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    uint32_t *v = e ? v1 : v0;
+                    const uint32_t x = v[j], y = v[j + span];
+                    const uint32_t tt = mul(y, w);
+                    if (q < 3 && ((j >> (st + 1)) & 1)) {
+                        v[j] = x + tt;
+                        v[j + span] = x + (P - tt);
+                    } else {
+                        v[j] = add(x, tt);
+                        v[j + span] = sub(x, tt);
+                    }
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void dit13x2(uint32_t v0[16], uint32_t v1[16], uint32_t *x, uint32_t t,
+                                        const uint32_t *__restrict__ tw) {
+    uint32_t *x1 = x + LDS13;
+    stage_h1(v0, t & 1);
+    stage_h1(v1, t & 1);
+    net16x2<true, 2>(v0, v1, lay_off<2>(t), tw);
+    to_lds<2>(x, v0, t);
+    to_lds<2>(x1, v1, t);
+    __syncthreads();
+    from_lds<32>(x, v0, t);
+    from_lds<32>(x1, v1, t);
+    net16x2<true, 32>(v0, v1, lay_off<32>(t), tw);
+    __syncthreads();
+    to_lds<32>(x, v0, t);
+    to_lds<32>(x1, v1, t);
+    __syncthreads();
+    from_lds<512>(x, v0, t);
+    from_lds<512>(x1, v1, t);
+    net16x2<true, 512>(v0, v1, lay_off<512>(t), tw);
+}
+}  // namespace t13
+
+__global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src, uint32_t *dst, ColMap ms,
+                                                            ColMap md, int L, const uint32_t *__restrict__ tt_inv,
+                                                            const uint32_t *__restrict__ tt_fwd, Twist tws,
+                                                            uint64_t dst_half) {
     using namespace t13;
-    __shared__ uint32_t x[LDS13];
-    __shared__ uint32_t cs[8192];  // the coefficients, private per thread (cs[j * 512 + t]): frees 16 VGPRs
+    __shared__ uint32_t x[2 * LDS13];
     const uint32_t t = threadIdx.x;
     const uint32_t base = blockIdx.x * 8192u;
     const uint32_t *sp = src + ms.off(blockIdx.y) + base;
-    uint32_t v[16];
+    uint32_t v0[16], v1[16];
 #pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = sp[lay_idx<512>(t, j)];
-    dif13(v, x, t, tt_inv);
+    for (int j = 0; j < 16; j++) v0[j] = sp[lay_idx<512>(t, j)];
+    dif13(v0, x, t, tt_inv);
+    {
+        const uint32_t g0 = tws.g0[blockIdx.x], g1 = tws.g1[blockIdx.x];
+        const uint4 *u0 = (const uint4 *)(tws.u0 + t * 16), *u1 = (const uint4 *)(tws.u1 + t * 16);
 #pragma unroll
-    for (int j = 0; j < 16; j++) cs[j * 512 + t] = v[j];
-    uint32_t *dcol = dst + md.off(blockIdx.y);
+        for (int q = 0; q < 4; q++) {
+            const uint4 a = u0[q], b = u1[q];
+            const uint32_t au[4] = {a.x, a.y, a.z, a.w}, bu[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int e = 0; e < 2; e++) {
-        {
-            const uint32_t ge = e ? tws.g1[blockIdx.x] : tws.g0[blockIdx.x];
-            const uint4 *ur = (const uint4 *)((e ? tws.u1 : tws.u0) + t * 16);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint4 u = ur[q];
-                // inner product lazy (0, 2P): the outer one reduces
-                v[4 * q] = mul(mul_lazy(cs[(4 * q) * 512 + t], ge), u.x);
-                v[4 * q + 1] = mul(mul_lazy(cs[(4 * q + 1) * 512 + t], ge), u.y);
-                v[4 * q + 2] = mul(mul_lazy(cs[(4 * q + 2) * 512 + t], ge), u.z);
-                v[4 * q + 3] = mul(mul_lazy(cs[(4 * q + 3) * 512 + t], ge), u.w);
+            for (int r = 0; r < 4; r++) {
+                const uint32_t c = v0[4 * q + r];
+                v1[4 * q + r] = mul(mul_lazy(c, g1), bu[r]);
+                v0[4 * q + r] = mul(mul_lazy(c, g0), au[r]);
             }
         }
-        dit13(v, x, t, tt_fwd);
-        uint32_t *dp = dcol + (uint64_t)e * dst_half + base;
-#pragma unroll
-        for (int j = 0; j < 16; j++) dp[lay_idx<512>(t, j)] = v[j];
     }
+    dit13x2(v0, v1, x, t, tt_fwd);
+    uint32_t *dp = dst + md.off(blockIdx.y) + base;
+#pragma unroll
+    for (int j = 0; j < 16; j++) dp[lay_idx<512>(t, j)] = v0[j];
+#pragma unroll
+    for (int j = 0; j < 16; j++) dp[dst_half + lay_idx<512>(t, j)] = v1[j];
 }
 
 // ------------------------------------------------------------------ 512-row strided register tiles
@@ -713,6 +757,161 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9(const uint32_t *src, uint
     }
 }
 
+// Same tiles and networks as k_ntt_s9, addressed through buffer descriptors: every global access
+// (data, twiddles, stores) is one per-thread 32-bit voffset fixed for the kernel plus a
+// wave-uniform soffset (k S words, twiddle stage bases) computed on the scalar unit, so the
+// address arithmetic leaves the VALU (k_ntt_s9 spent ~40 % of its VALU issue on 64-bit address
+// math).  LDS tiles are XOR-swizzled only where the bit-reversed output walk needs it, so the
+// other layouts' LDS addresses are a base plus immediate offsets.
+namespace s9 {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t bld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+__device__ __forceinline__ void bst(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, 0);
+}
+template <bool SWZ>
+__device__ __forceinline__ uint32_t atb(uint32_t r, uint32_t t) {
+    if constexpr (SWZ) return r * 32 + (t ^ ((r >> 4) & 31));
+    else return r * 32 + t;
+}
+
+// three stages of one network; twiddle w_{2h}^{(off + rs m) S + ct} read at voff = (off S + ct) * 4
+// plus the uniform soff0 + (h + rs m S) * 4
+template <bool DIT, int LAY>
+__device__ __forceinline__ void net8b(uint32_t *v, __amdgpu_buffer_rsrc_t rtw, uint32_t voff, uint32_t soff0,
+                                      uint32_t S4) {
+    constexpr uint32_t rs = RS<LAY>;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const int st = DIT ? q : 2 - q;
+        const int span = 1 << st;
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+            const uint32_t w = bld(rtw, voff, soff0 + (rs * (uint32_t)(span + m)) * S4);
+#pragma unroll
+            for (int k = m; k < 8; k += 2 * span) {
+                const uint32_t a = v[k], b = v[k + span];
+                if (DIT) {
+                    const uint32_t tt = mul(b, w);
+                    if (q < 2 && ((k >> (st + 1)) & 1)) {
+                        v[k] = a + tt;
+                        v[k + span] = a + (P - tt);
+                    } else {
+                        v[k] = add(a, tt);
+                        v[k + span] = sub(a, tt);
+                    }
+                } else {
+                    v[k] = add(a, b);
+                    v[k + span] = mul(a + (P - b), w);
+                }
+            }
+        }
+    }
+}
+template <int LAY, bool SWZ>
+__device__ __forceinline__ void to_ldsb(uint32_t *x, const uint32_t v[16], uint32_t u, uint32_t t) {
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[atb<SWZ>(row0<LAY>(u, n) + RS<LAY> * k, t)] = v[8 * n + k];
+}
+template <int LAY, bool SWZ>
+__device__ __forceinline__ void from_ldsb(const uint32_t *x, uint32_t v[16], uint32_t u, uint32_t t) {
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[8 * n + k] = x[atb<SWZ>(row0<LAY>(u, n) + RS<LAY> * k, t)];
+}
+}  // namespace s9
+
+template <bool DIT, int MODE>
+__global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+                                                        int logS, const uint32_t *__restrict__ tw,
+                                                        uint32_t tw_words) {
+    using namespace s9;
+    constexpr bool SWZ = DIT && MODE == MODE_BITREV_OUT;
+    __shared__ uint32_t x[512 * 32];
+    const uint32_t S = 1u << logS, S4 = S * 4;
+    const uint32_t outer = blockIdx.x >> (logS - 5);
+    const uint32_t c0 = (blockIdx.x & ((S >> 5) - 1)) * 32;
+    const uint32_t base = outer * 512u * S;
+    const uint32_t t = threadIdx.x & 31, u = threadIdx.x >> 5;
+    const uint32_t ct = c0 + t;
+    const auto rsrc = mkrs(src + ms.off(blockIdx.y) + base, 512u * S4);
+    const auto rtw = mkrs(tw, tw_words * 4);
+    const uint32_t vLL = ct * 4;                    // twiddle offsets per layout / network
+    const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4, vLM1 = (((2 * u + 1) & 7) * S + ct) * 4;
+    const uint32_t vLH = (u * S + ct) * 4;          // also rows u + 32 n + 64 k of the tile
+    const uint32_t vL16 = (16 * u * S + ct) * 4;    // rows 16 u + 8 n + k of the tile
+    uint32_t v[16];
+    if (DIT) {
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, vL16, (uint32_t)(8 * n + k) * S4);
+        net8b<true, LL>(v, rtw, vLL, 0, S4);
+        net8b<true, LL>(v + 8, rtw, vLL, 0, S4);
+        to_ldsb<LL, false>(x, v, u, t);
+        __syncthreads();
+        from_ldsb<LM, false>(x, v, u, t);
+        net8b<true, LM>(v, rtw, vLM0, 0, S4);
+        net8b<true, LM>(v + 8, rtw, vLM1, 0, S4);
+        __syncthreads();
+        to_ldsb<LM, false>(x, v, u, t);
+        __syncthreads();
+        from_ldsb<LH, false>(x, v, u, t);
+        net8b<true, LH>(v, rtw, vLH, 0, S4);
+        net8b<true, LH>(v + 8, rtw, vLH, 32 * S4, S4);
+        if (MODE == MODE_PLAIN) {
+            const auto rdst = mkrs(dst + md.off(blockIdx.y) + base, 512u * S4);
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, vLH, (uint32_t)(32 * n + 64 * k) * S4);
+        } else {  // BITREV_OUT: natural n = r S + c -> row rev_L(n) = rev_logS(c) * 512 + rev_9(r)
+            __syncthreads();
+            to_ldsb<LH, SWZ>(x, v, u, t);
+            __syncthreads();
+            const auto rdst = mkrs(dst + md.off(blockIdx.y), 512u * S4);
+            const uint32_t q = threadIdx.x & 511, hb = threadIdx.x >> 9, rq = rev_bits(q, 9);
+            const uint32_t vo = (((rev_bits(c0, logS) + (hb << (logS - 1))) << 9) + q) * 4;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t tc = 2 * i + hb;
+                const uint32_t so = (rev_bits((uint32_t)(2 * i), 5) << (logS - 5)) << 11;  // rows x 512 words x 4 B
+                bst(x[atb<SWZ>(rq, tc)], rdst, vo, so);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, vLH, (uint32_t)(32 * n + 64 * k) * S4);
+        net8b<false, LH>(v, rtw, vLH, 0, S4);
+        net8b<false, LH>(v + 8, rtw, vLH, 32 * S4, S4);
+        to_ldsb<LH, false>(x, v, u, t);
+        __syncthreads();
+        from_ldsb<LM, false>(x, v, u, t);
+        net8b<false, LM>(v, rtw, vLM0, 0, S4);
+        net8b<false, LM>(v + 8, rtw, vLM1, 0, S4);
+        __syncthreads();
+        to_ldsb<LM, false>(x, v, u, t);
+        __syncthreads();
+        from_ldsb<LL, false>(x, v, u, t);
+        net8b<false, LL>(v, rtw, vLL, 0, S4);
+        net8b<false, LL>(v + 8, rtw, vLL, 0, S4);
+        const auto rdst = mkrs(dst + md.off(blockIdx.y) + base, 512u * S4);
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, vL16, (uint32_t)(8 * n + k) * S4);
+    }
+}
+
 // ------------------------------------------------------------------ dispatch
 static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
 static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
@@ -722,11 +921,24 @@ static int strided_T(int logR) { return logR >= 9 ? 32 : 64; }  // >= 32: the sw
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
                         int logS, const uint32_t *tw, int mode, hipStream_t s, Twist tws = Twist{},
-                        uint64_t dst_half = 0) {
+                        uint64_t dst_half = 0, uint32_t tw_words = 0) {
     const int T = strided_T(logR);
     ARG_CHECK((1 << logS) >= T, "strided pass narrower than its tile");
     dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
-    if (logR == 9) {  // register-tile kernel (T = 32)
+    if (logR == 9 && tw_words && mode != MODE_TWIST_OUT) {  // buffer-addressed register tiles
+        if (!DIT)
+            hipLaunchKernelGGL((k_ntt_s9b<false, MODE_PLAIN>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tw_words);
+        else if (mode == MODE_PLAIN)
+            hipLaunchKernelGGL((k_ntt_s9b<true, MODE_PLAIN>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tw_words);
+        else
+            hipLaunchKernelGGL((k_ntt_s9b<true, MODE_BITREV_OUT>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
+                               tw, tw_words);
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
+    if (logR == 9) {  // register-tile kernel (T = 32), flat addressing: the twisted-output pass
         if (!DIT)
             hipLaunchKernelGGL((k_ntt_s9<false, MODE_PLAIN>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw, tws,
                                dst_half);
@@ -895,14 +1107,15 @@ void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hip
         for (int i = (int)sp.size() - 1; i >= 0; i--) {
             const bool last = (i == 0);
             run_strided<true>(sp[i], work.p, last ? dst.d : work.p, m_src, last ? m_dst1 : m_src, nv, L, logS,
-                              c.tw_inv, last ? MODE_TWIST_OUT : MODE_PLAIN, s, tws, N);
+                              c.tw_inv, last ? MODE_TWIST_OUT : MODE_PLAIN, s, tws, N, 1u << c.tw_log);
             logS += sp[i];
         }
     }
     int logS = L;
     for (size_t i = 0; i < sp.size(); i++) {
         logS -= sp[i];
-        run_strided<false>(sp[i], dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, logS, c.tw_fwd, MODE_PLAIN, s);
+        run_strided<false>(sp[i], dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, logS, c.tw_fwd, MODE_PLAIN, s, Twist{}, 0,
+                           1u << c.tw_log);
     }
     run_contig<false>(logC, dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, c.tw_fwd, MODE_PLAIN, Twist{}, 0, s);
 }
@@ -953,13 +1166,14 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
         int logS = L;
         for (size_t i = 0; i < sp.size(); i++) {
             logS -= sp[i];
-            run_strided<false>(sp[i], in, work.p, min, m_w1, nb, L, logS, c.tw_inv, MODE_PLAIN, s);
+            run_strided<false>(sp[i], in, work.p, min, m_w1, nb, L, logS, c.tw_inv, MODE_PLAIN, s, Twist{}, 0,
+                               1u << c.tw_log);
             in = work.p;
             min = m_w1;
         }
         if (logC == 13) {
-            hipLaunchKernelGGL(k_lde_fused13, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, work.p, work.p, m_w1,
-                               m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
+            hipLaunchKernelGGL(k_lde_fused13, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, work.p, work.p,
+                               m_w1, m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
             HIP_CHECK(hipGetLastError());
         } else {
             run_fused(logC, work.p, work.p, m_w1, m_w1, nb, L, c.tw_inv, c.tw_fwd, tws, N, 0, s);
@@ -968,7 +1182,7 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
         for (int i = (int)sp.size() - 1; i >= 0; i--) {
             const bool last = (i == 0);
             run_strided<true>(sp[i], work.p, last ? out : work.p, m_w2, m_w2, 2 * nb, L, logS, c.tw_fwd,
-                              last ? MODE_BITREV_OUT : MODE_PLAIN, s);
+                              last ? MODE_BITREV_OUT : MODE_PLAIN, s, Twist{}, 0, 1u << c.tw_log);
             logS += sp[i];
         }
     }
