@@ -124,3 +124,34 @@ def test_concurrent_shards_from_threads(dev):
     assert out == seq
     rc, ref = cpu.prove(*work[0])
     assert rc == 0 and seq[0] == ref
+
+
+def test_shard_proof_bytes_identical_2e18(dev):
+    """Byte parity at the largest size the oracle proves in seconds (84 queries, as the bench)."""
+    gpu, cpu, traces, pvs = provers(dev, 1 << 18, nq=84)
+    proof = gpu.prove_shard(traces, pvs)
+    rc, ref = cpu.prove(traces, pvs)
+    assert rc == 0 and proof == ref
+
+
+@pytest.mark.parametrize("logn", [20, 22, 23])
+def test_full_size_proof_verifies(dev, logn):
+    """BASELINE sizes (2^20 .. 2^23 rows; 2^23 is the largest the two-adicity allows at blowup 2):
+    size-independent properties where the oracle prover would take minutes -- the oracle's
+    restated verifier accepts the GPU proof, proving twice is deterministic, and a flipped
+    proof byte is rejected."""
+    gpu, cpu, traces, pvs = provers(dev, 1 << logn, nq=84)
+    proof = gpu.prove_shard(traces, pvs)
+    assert cpu.verify(proof) == 0
+    assert gpu.prove_shard(traces, pvs) == proof
+    bad = bytearray(proof)
+    bad[len(bad) // 2] ^= 1
+    assert cpu.verify(bytes(bad)) != 0
+
+
+def test_two_adicity_limit_is_an_error(dev):
+    """A 2^24-row trace would need a 2^25-point LDE, beyond KoalaBear's two-adicity (24): the C ABI
+    returns an error status instead of faulting."""
+    from zkmips_amd._lib import ZkmError
+    with pytest.raises(ZkmError):
+        dev.bench_lde(1 << 24, 1, 1)
