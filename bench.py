@@ -119,6 +119,10 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--log-n", type=int, default=22)
+    ap.add_argument("--workload", choices=["fib", "alu"], default="fib",
+                    help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Byte "
+                         "restated from the reference AIRs + CPU stand-in, zkmips_amd/mips_alu.py), 2^(log-n) "
+                         "instructions per shard")
     ap.add_argument("--queries", type=int, default=84)
     ap.add_argument("--cpu-log-n", type=int, default=18)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -155,7 +159,11 @@ def main():
     K = max(1, args.inflight)
     shards = []
     for k in range(K):
-        m, prep, traces_k, pvs_k = W.fib_shard(n, seed=1000 + rank * K + k)
+        if args.workload == "alu":
+            from zkmips_amd import mips_alu as A
+            m, prep, traces_k, pvs_k = A.alu_shard(n // 2, n // 2, seed=1000 + rank * K + k)
+        else:
+            m, prep, traces_k, pvs_k = W.fib_shard(n, seed=1000 + rank * K + k)
         shards.append(({kk: torch.from_numpy(v.view(np.int32)).cuda() for kk, v in traces_k.items()}, pvs_k, traces_k))
     dev = Device(local_rank)
     prover = HipProver(dev, m, prep, num_queries=args.queries)
@@ -279,8 +287,11 @@ def main():
         "vs_baseline": None,
         "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
         "data": "synthetic (seeded S-SHARD traces, SURVEY.md §8d)",
-        "config": {"workload": f"S-SHARD FibCpu 2^{args.log_n} rows (main 67, LogUp 11 EF, quotient 2) + FibTable "
-                               f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard",
+        "config": {"workload": (f"S-SHARD FibCpu 2^{args.log_n} rows (main 67, LogUp 11 EF, quotient 2) + FibTable "
+                                f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard")
+                   if args.workload == "fib" else
+                   (f"MIPS ALU slice: InstrSource 2^{args.log_n} + AddSub 2^{args.log_n - 1} + Bitwise "
+                    f"2^{args.log_n - 1} + Byte 2^16 (prep 12): full commit+open per shard"),
                    "rows_per_shard": rows_per_shard, "fri_queries": args.queries, "pow_bits": 16, "log_blowup": 1,
                    "shards_per_gpu_per_step": K, "parallelism": f"shard-parallel x{world}, {K} in flight per GPU",
                    "proof_bytes": len(proof)},
