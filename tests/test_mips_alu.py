@@ -1,4 +1,4 @@
-"""MIPS ALU slice (AddSub, Bitwise, Byte restated from the reference AIRs; zkmips_amd/mips_alu.py).
+"""MIPS ALU slice (AddSub, Bitwise, Lt, ShiftLeft, Byte restated from the reference AIRs; zkmips_amd/mips_alu.py).
 
 CPU part: the trace generators reproduce the reference's own fixtures and table semantics, the
 oracle proves and its verifier accepts a multi-chip shard whose Byte / Instruction lookups balance
@@ -48,7 +48,7 @@ def test_reference_fixture_events():
 
 @pytest.fixture(scope="module")
 def shard():
-    return A.alu_shard(300, 200, seed=5)
+    return A.alu_shard(300, 200, seed=5, n_lt=250, n_sll=100)
 
 
 @pytest.fixture(scope="module")
@@ -60,13 +60,42 @@ def oracle(shard):
 def test_alu_shard_proves_and_verifies(shard, oracle):
     m, _, tr, pv = shard
     heights = {k: v.shape[0] for k, v in tr.items()}
-    assert heights == {"InstrSource": 512, "AddSub": 512, "Bitwise": 256, "Byte": 65536}
-    assert [c.perm_width_ef for c in m.chips] == [2, 5, 4, 6]
+    assert heights == {"InstrSource": 1024, "AddSub": 512, "Bitwise": 256, "Lt": 256, "ShiftLeft": 128,
+                       "Byte": 65536}
+    assert [c.name for c in m.chips] == ["InstrSource", "AddSub", "Bitwise", "Lt", "ShiftLeft", "Byte"]
+    assert [c.perm_width_ef for c in m.chips] == [2, 5, 4, 3, 4, 6]
     rc, proof = oracle.prove(tr, pv)
     assert rc == 0 and oracle.verify(proof) == 0
 
 
-@pytest.mark.parametrize("what", ["carry", "bitwise_result", "byte_mult", "dropped_instruction"])
+def test_shard_without_some_chips(oracle):
+    """A shard includes only the chips that have events (MachineAir::included)."""
+    m, prep, tr, pv = A.alu_shard(64, 32, seed=8)
+    assert sorted(tr) == ["AddSub", "Bitwise", "Byte", "InstrSource"]
+    rc, proof = oracle.prove(tr, pv)
+    assert rc == 0 and oracle.verify(proof) == 0
+
+
+def test_lt_sll_semantics():
+    """SLT/SLTU over equal, sign-differing and shared-prefix operands; SLL by every shift amount."""
+    ev = A.events_from_list([], [], [(0, A.OP_SLT, 1, 0xFFFFFFFF, 0), (4, A.OP_SLTU, 0, 0xFFFFFFFF, 0),
+                                     (8, A.OP_SLT, 0, 7, 7), (12, A.OP_SLTU, 1, 0x12345600, 0x12345700),
+                                     (16, A.OP_SLT, 0, 0x7FFFFFFF, 0x80000000)],
+                            [(4 * i, A.OP_SLL, (0x81234567 << (i & 31)) & 0xFFFFFFFF, 0x81234567, i) for i in range(40)])
+    m, prep, tr, pv = A.alu_shard_from(ev)
+    lt = tr["Lt"]
+    assert list(lt[:5, A.LT_COMP_EQ]) == [0, 0, 1, 0, 0]
+    assert list(lt[3, A.LT_FLAGS:A.LT_FLAGS + 4]) == [0, 1, 0, 0]  # first differing byte from the top
+    sl = tr["ShiftLeft"]
+    assert all(sl[i, A.SL_NBYTES + ((i & 31) // 8)] == 1 for i in range(40))
+    assert list(sl[50, A.SL_NBITS:A.SL_NBITS + 2]) == [1, 0] and sl[50, A.SL_MULT] == 1  # padding row
+    cpu = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = cpu.prove(tr, pv)
+    assert rc == 0 and cpu.verify(proof) == 0
+
+
+@pytest.mark.parametrize("what", ["carry", "bitwise_result", "byte_mult", "dropped_instruction", "lt_result",
+                                  "sll_carry"])
 def test_alu_tamper_rejected(shard, oracle, what):
     _, _, tr, pv = shard
     bad = {k: v.copy() for k, v in tr.items()}
@@ -76,8 +105,13 @@ def test_alu_tamper_rejected(shard, oracle, what):
         bad["Bitwise"][3, A.BW_A] = (int(bad["Bitwise"][3, A.BW_A]) + 1) % 256
     elif what == "byte_mult":
         bad["Byte"][1234, A.B_U8RANGE] += 1
+    elif what == "lt_result":  # SLT result flipped together with the intermediate sltu
+        bad["Lt"][9, A.LT_A] ^= 1
+        bad["Lt"][9, A.LT_SLTU_R] ^= 1
+    elif what == "sll_carry":
+        bad["ShiftLeft"][4, A.SL_CARRY] += 1
     else:  # the CPU stand-in claims an instruction no ALU chip executes
-        bad["InstrSource"][510, A.IS_REAL] = 1  # a padding row (500 events)
+        bad["InstrSource"][1000, A.IS_REAL] = 1  # a padding row (850 events)
     rc, proof = oracle.prove(bad, pv)
     assert rc == 0
     assert oracle.verify(proof) != 0
@@ -93,10 +127,11 @@ def dev():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_add,n_bit", [(300, 200), (1 << 13, 5000), (1 << 15, 1 << 15)])
-def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit):
+@pytest.mark.parametrize("n_add,n_bit,n_lt,n_sll", [(300, 200, 0, 0), (300, 200, 250, 100),
+                                                   (1 << 13, 5000, 3000, 1 << 12), (1 << 15, 1 << 15, 1 << 15, 1 << 15)])
+def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit, n_lt, n_sll):
     from zkmips_amd.prover import HipProver
-    m, prep, tr, pv = A.alu_shard(n_add, n_bit, seed=n_add)
+    m, prep, tr, pv = A.alu_shard(n_add, n_bit, seed=n_add, n_lt=n_lt, n_sll=n_sll)
     gpu = HipProver(dev, m, prep, num_queries=16)
     cpu = O.OracleProver(m, prep, num_queries=16)
     assert np.array_equal(gpu.vk_commit, cpu.commit)
@@ -109,7 +144,7 @@ def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit):
 @pytest.mark.gpu
 def test_alu_gpu_full_size_verifies(dev):
     from zkmips_amd.prover import HipProver
-    m, prep, tr, pv = A.alu_shard(1 << 21, 1 << 21, seed=9)
+    m, prep, tr, pv = A.alu_shard(1 << 20, 1 << 20, seed=9, n_lt=1 << 20, n_sll=1 << 20)
     assert tr["InstrSource"].shape[0] == 1 << 22
     gpu = HipProver(dev, m, prep, num_queries=84)
     cpu = O.OracleProver(m, prep, num_queries=84)

@@ -8,6 +8,8 @@ alpha powers of the quotient fold and the LogUp column layout):
 * ``AddSub``  crates/core/machine/src/alu/add_sub/mod.rs:180-226 (+ AddOperation,
   crates/core/machine/src/operations/add.rs:55-99); trace: event_to_row :149-163.
 * ``Bitwise`` crates/core/machine/src/alu/bitwise/mod.rs:184-234; columns :33-59.
+* ``Lt``      crates/core/machine/src/alu/lt/mod.rs:277-466 (SLT/SLTU); trace: event_to_row :179-263.
+* ``ShiftLeft`` crates/core/machine/src/alu/sll/mod.rs:273-406 (SLL); trace :200-260, padding :142-155.
 * ``Byte``    crates/core/machine/src/bytes/{air.rs:24-74, columns.rs, mod.rs:50-120, trace.rs:40-70}:
   the preprocessed 2^16-row table of all byte operations and its 10 multiplicity columns.
 
@@ -170,9 +172,120 @@ def instr_source_chip() -> ChipDesc:
     return ch
 
 
+# ---------------------------------------------------------------- Lt
+# LtCols (alu/lt/mod.rs:37-86)
+(LT_PC, LT_NPC, LT_SLT, LT_SLTU, LT_A, LT_B, LT_C, LT_FLAGS, LT_BM, LT_CM, LT_INV, LT_MSB_B, LT_MSB_C, LT_BIT_B,
+ LT_BIT_C, LT_SLTU_R, LT_COMP_EQ, LT_SIGN_EQ, LT_CMP, LT_BEQ) = (0, 1, 2, 3, 4, 8, 12, 16, 20, 21, 22, 23, 24, 25,
+                                                                 26, 27, 28, 29, 30, 32)
+LT_WIDTH = 36
+OP_SLT, OP_SLTU, OP_SLL = 13, 14, 9
+INV_128 = pow(128, P - 2, P)
+
+
+def lt_chip() -> ChipDesc:
+    """LtChip::eval, alu/lt/mod.rs:277-466."""
+    ch = ChipDesc("Lt", prep_width=0, main_width=LT_WIDTH, local_only=True)
+    M = main
+    is_slt, is_sltu = M(LT_SLT), M(LT_SLTU)
+    is_real = is_slt + is_sltu
+    mult = V([("main", LT_SLT, 1), ("main", LT_SLTU, 1)])
+    b = [M(LT_B + i) for i in range(4)]
+    c = [M(LT_C + i) for i in range(4)]
+    b_comp, c_comp = list(b), list(c)
+    b_comp[3] = b[3] * is_sltu + M(LT_BM) * is_slt
+    c_comp[3] = c[3] * is_sltu + M(LT_CM) * is_slt
+    ch.sends.append(Lookup([V.const(B_AND), _m(LT_BM), ZERO, _m(LT_B + 3), V.const(0x7F)], mult, KIND_BYTE))
+    ch.sends.append(Lookup([V.const(B_AND), _m(LT_CM), ZERO, _m(LT_C + 3), V.const(0x7F)], mult, KIND_BYTE))
+    ch.assert_zero(M(LT_BIT_B) - M(LT_MSB_B) * is_slt)
+    ch.assert_zero(M(LT_BIT_C) - M(LT_MSB_C) * is_slt)
+    ch.assert_zero(M(LT_MSB_B) - (b[3] - M(LT_BM)) * INV_128)
+    ch.assert_zero(M(LT_MSB_C) - (c[3] - M(LT_CM)) * INV_128)
+    _assert_bool(ch, M(LT_SIGN_EQ))
+    ch.assert_zero(M(LT_SIGN_EQ) * (M(LT_BIT_B) - M(LT_BIT_C)))
+    ch.assert_zero(is_real * (1 - M(LT_SIGN_EQ)) * (M(LT_BIT_B) + M(LT_BIT_C) - 1))
+    ch.assert_zero(M(LT_A) - (M(LT_BIT_B) * (1 - M(LT_BIT_C)) + M(LT_SIGN_EQ) * M(LT_SLTU_R)))
+    for i in (1, 2, 3):
+        ch.assert_zero(M(LT_A + i))
+    flags = [M(LT_FLAGS + i) for i in range(4)]
+    sum_flags = flags[0] + flags[1] + flags[2] + flags[3]
+    for f in flags:
+        _assert_bool(ch, f)
+    _assert_bool(ch, sum_flags)
+    ch.assert_zero(is_real * ((1 - M(LT_COMP_EQ)) - sum_flags))
+    _assert_bool(ch, M(LT_COMP_EQ))
+    visited, bcb, ccb = Expr.lift(0), Expr.lift(0), Expr.lift(0)
+    for i in (3, 2, 1, 0):
+        visited = visited + flags[i]
+        bcb = bcb + b_comp[i] * flags[i]
+        ccb = ccb + c_comp[i] * flags[i]
+        ch.assert_zero((1 - visited) * (b_comp[i] - c_comp[i]))
+        ch.assert_zero(M(LT_COMP_EQ) * visited)
+    ch.assert_zero(M(LT_CMP) - bcb)
+    ch.assert_zero(M(LT_CMP + 1) - ccb)
+    ch.assert_zero((1 - M(LT_COMP_EQ)) * (M(LT_INV) * (M(LT_CMP) - M(LT_CMP + 1)) - is_real))
+    ch.sends.append(Lookup([V.const(B_LTU), _m(LT_SLTU_R), ZERO, _m(LT_CMP), _m(LT_CMP + 1)], mult, KIND_BYTE))
+    _assert_bool(ch, is_slt)
+    _assert_bool(ch, is_sltu)
+    _assert_bool(ch, is_real)
+    w = lambda base: [_m(base + i) for i in range(4)]
+    op = V([("main", LT_SLT, OP_SLT), ("main", LT_SLTU, OP_SLTU)])
+    ch.receives.append(Lookup(_instruction(LT_PC, LT_NPC, op, w(LT_A), w(LT_B), w(LT_C)), mult, KIND_INSTRUCTION))
+    return ch
+
+
+# ---------------------------------------------------------------- ShiftLeft
+# ShiftLeftCols (alu/sll/mod.rs:64-98)
+SL_PC, SL_NPC, SL_A, SL_B, SL_C, SL_CBITS, SL_NBITS, SL_MULT, SL_RES, SL_CARRY, SL_NBYTES, SL_REAL = (
+    0, 1, 2, 6, 10, 14, 22, 30, 31, 35, 39, 43)
+SL_WIDTH = 44
+
+
+def shift_left_chip() -> ChipDesc:
+    """ShiftLeft::eval, alu/sll/mod.rs:273-406."""
+    ch = ChipDesc("ShiftLeft", prep_width=0, main_width=SL_WIDTH, local_only=True)
+    M = main
+    cb = [M(SL_CBITS + i) for i in range(8)]
+    ch.assert_zero(sum((cb[i] * (1 << i) for i in range(1, 8)), cb[0]) - M(SL_C))
+    nbits = cb[0] + cb[1] * 2 + cb[2] * 4
+    for i in range(8):
+        ch.assert_zero(M(SL_NBITS + i) * (nbits - i))
+    for i in range(8):
+        ch.assert_zero(M(SL_NBITS + i) * (M(SL_MULT) - (1 << i)))
+    for i in range(4):
+        v = M(SL_B + i) * M(SL_MULT) - M(SL_CARRY + i) * 256
+        if i > 0:
+            v = v + M(SL_CARRY + i - 1)
+        ch.assert_zero(M(SL_RES + i) - v)
+    nbytes = cb[3] + cb[4] * 2
+    for i in range(4):
+        ch.assert_zero(M(SL_NBYTES + i) * (nbytes - i))
+    for nb in range(4):
+        for i in range(4):
+            rhs = Expr.lift(0) if i < nb else M(SL_RES + i - nb)
+            ch.assert_zero(M(SL_NBYTES + nb) * (M(SL_A + i) - rhs))
+    for i in range(8):
+        _assert_bool(ch, cb[i])
+    for i in range(8):
+        _assert_bool(ch, M(SL_NBITS + i))
+    ch.assert_zero(sum((M(SL_NBITS + i) for i in range(1, 8)), M(SL_NBITS)) - 1)
+    for base in (SL_RES, SL_CARRY):
+        for k in (0, 2):
+            ch.sends.append(Lookup([V.const(B_U8RANGE), ZERO, ZERO, _m(base + k), _m(base + k + 1)], _m(SL_REAL),
+                                   KIND_BYTE))
+    for i in range(4):
+        _assert_bool(ch, M(SL_NBYTES + i))
+    ch.assert_zero(sum((M(SL_NBYTES + i) for i in range(1, 4)), M(SL_NBYTES)) - 1)
+    _assert_bool(ch, M(SL_REAL))
+    w = lambda base: [_m(base + i) for i in range(4)]
+    ch.receives.append(Lookup(_instruction(SL_PC, SL_NPC, V.const(OP_SLL), w(SL_A), w(SL_B), w(SL_C)), _m(SL_REAL),
+                              KIND_INSTRUCTION))
+    return ch
+
+
 def alu_machine() -> MachineDesc:
     # chip order as in MipsAir::chips (crates/core/machine/src/mips/mod.rs): Cpu first, ALUs, Byte
-    return MachineDesc([instr_source_chip(), add_sub_chip(), bitwise_chip(), byte_chip()], NUM_PV_ELTS)
+    return MachineDesc([instr_source_chip(), add_sub_chip(), bitwise_chip(), lt_chip(), shift_left_chip(),
+                        byte_chip()], NUM_PV_ELTS)
 
 
 # ---------------------------------------------------------------- trace generation
@@ -184,100 +297,216 @@ def _pow2(n: int) -> int:
     return max(16, 1 << max(0, (n - 1).bit_length()))
 
 
-def alu_events(n_add: int, n_bit: int, seed: int = 3):
-    """Synthetic ALU events: (opcode, a, b, c, pc) with a = op(b, c), half ADD/SUB, the four bitwise
-    ops in turn; operands uniform u32 (SplitMix64)."""
-    r = splitmix64(0xA1B0000 + seed, 2 * (n_add + n_bit) + 2)
-    b = (r[0::2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-    c = (r[1::2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-    i = np.arange(n_add + n_bit, dtype=np.uint32)
-    pc = (0x00400000 + 4 * i).astype(np.uint32)
-    ba, ca = b[:n_add].astype(np.uint64), c[:n_add].astype(np.uint64)
+def alu_events(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0):
+    """Synthetic ALU events per chip: (opcode, a, b, c, pc) with a = op(b, c) as the executor computes
+    it; ADD/SUB, the four bitwise ops and SLT/SLTU alternate; operands uniform u32 (SplitMix64),
+    Lt operands share their top bytes half of the time so every comparison-byte position occurs."""
+    n = n_add + n_bit + n_lt + n_sll
+    r = splitmix64(0xA1B0000 + seed, 2 * n + 2)
+    b = (r[0::2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)[:n]
+    c = (r[1::2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)[:n]
+    pc = (0x00400000 + 4 * np.arange(n, dtype=np.uint64)).astype(np.uint32)
+    out, o = {}, 0
+    ba, ca = b[o:o + n_add].astype(np.uint64), c[o:o + n_add].astype(np.uint64)
     is_sub = (np.arange(n_add) % 2 == 1)
     a_add = np.where(is_sub, (ba - ca) & np.uint64(0xFFFFFFFF), (ba + ca) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-    op_add = np.where(is_sub, OP_SUB, OP_ADD).astype(np.uint32)
-    bb, cb = b[n_add:n_add + n_bit], c[n_add:n_add + n_bit]
+    out["add"] = (np.where(is_sub, OP_SUB, OP_ADD).astype(np.uint32), a_add, b[o:o + n_add], c[o:o + n_add],
+                  pc[o:o + n_add])
+    o += n_add
+    bb, cb = b[o:o + n_bit], c[o:o + n_bit]
     kind = np.arange(n_bit) % 4
     ops = np.asarray([OP_AND, OP_OR, OP_XOR, OP_NOR], np.uint32)[kind]
     a_bit = np.select([kind == 0, kind == 1, kind == 2], [bb & cb, bb | cb, bb ^ cb], ~(bb | cb)).astype(np.uint32)
-    return {"add": (op_add, a_add, b[:n_add], c[:n_add], pc[:n_add]),
-            "bit": (ops, a_bit, bb, cb, pc[n_add:n_add + n_bit])}
+    out["bit"] = (ops, a_bit, bb, cb, pc[o:o + n_bit])
+    o += n_bit
+    bl, cl = b[o:o + n_lt].copy(), c[o:o + n_lt].copy()
+    k = np.arange(n_lt)
+    keep = (k % 8).astype(np.uint32)  # 0..3 top bytes shared (0 = independent), 4 = equal, 5..7 independent
+    for nb in (1, 2, 3):
+        m = np.uint32(((1 << (8 * nb)) - 1) << (8 * (4 - nb)))
+        sel = keep == nb
+        cl[sel] = (cl[sel] & ~m) | (bl[sel] & m)
+    cl[keep == 4] = bl[keep == 4]
+    slt = k % 2 == 0
+    lt_s = bl.view(np.int32) < cl.view(np.int32)
+    out["lt"] = (np.where(slt, OP_SLT, OP_SLTU).astype(np.uint32), np.where(slt, lt_s, bl < cl).astype(np.uint32),
+                 bl, cl, pc[o:o + n_lt])
+    o += n_lt
+    bs, cs = b[o:o + n_sll], c[o:o + n_sll]
+    out["sll"] = (np.full(n_sll, OP_SLL, np.uint32), (bs << (cs & np.uint32(31))).astype(np.uint32), bs, cs,
+                  pc[o:o + n_sll])
+    return out
 
 
-def events_from_list(add_events, bit_events):
+def events_from_list(add_events, bit_events, lt_events=(), sll_events=()):
     """Events given as the reference's AluEvent::new(pc, opcode, a, b, c) tuples (next_pc = pc + 4,
     crates/core/executor/src/events/instr.rs:31-33)."""
     def cols(evs):
         arr = np.asarray([(op, a, b, c, pc) for pc, op, a, b, c in evs], np.uint64).reshape(-1, 5)
         return tuple(arr[:, i].astype(np.uint32) for i in range(5))
-    return {"add": cols(add_events), "bit": cols(bit_events)}
+    return {"add": cols(add_events), "bit": cols(bit_events), "lt": cols(lt_events), "sll": cols(sll_events)}
 
 
-def alu_shard(n_add: int, n_bit: int, seed: int = 3):
+def alu_shard(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0):
     """(machine, prep_traces, traces, public_values) of one ALU-slice shard of random events."""
-    return alu_shard_from(alu_events(n_add, n_bit, seed), seed)
+    return alu_shard_from(alu_events(n_add, n_bit, seed, n_lt, n_sll), seed)
+
+
+def _inv_table():
+    """(x mod p)^-1 for x = b - c, b, c bytes (index x + 255)."""
+    return np.asarray([pow(x % P, P - 2, P) if x else 0 for x in range(-255, 256)], np.uint64)
 
 
 def alu_shard_from(ev, seed: int = 3):
-    n_add, n_bit = len(ev["add"][0]), len(ev["bit"][0])
     mult = np.zeros((BYTE_ROWS, BYTE_MULT_WIDTH), np.uint64)
 
     def byte_lookup(op, b, c, m=1):
-        np.add.at(mult[:, op], (b.astype(np.int64) << 8) + c.astype(np.int64), m)
+        np.add.at(mult[:, op], (np.asarray(b).astype(np.int64) << 8) + np.asarray(c).astype(np.int64), m)
 
+    traces = {}
     # AddSub (event_to_row, add_sub/mod.rs:149-163; AddOperation::populate, add.rs:21-52)
     op, a, b, c, pc = ev["add"]
-    sub = op == OP_SUB
-    op1 = np.where(sub, a, b)
-    val = (op1.astype(np.uint64) + c) & np.uint64(0xFFFFFFFF)
-    t_as = np.zeros((_pow2(n_add), AS_WIDTH), np.uint32)
-    t_as[:n_add, AS_PC] = pc
-    t_as[:n_add, AS_NPC] = pc + 4
-    t_as[:n_add, AS_VAL:AS_VAL + 4] = _bytes(val.astype(np.uint32))
-    x, y = _bytes(op1), _bytes(c)
-    cy = np.zeros((n_add, 3), np.uint32)
-    prev = np.zeros(n_add, np.uint32)
-    for k in range(3):
-        prev = ((x[:, k] + y[:, k] + prev) > 255).astype(np.uint32)
-        cy[:, k] = prev
-    t_as[:n_add, AS_CARRY:AS_CARRY + 3] = cy
-    t_as[:n_add, AS_OP1:AS_OP1 + 4] = x
-    t_as[:n_add, AS_OP2:AS_OP2 + 4] = y
-    t_as[:n_add, AS_ADD] = ~sub
-    t_as[:n_add, AS_SUB] = sub
-    for word in (x, y, _bytes(val.astype(np.uint32))):
-        byte_lookup(B_U8RANGE, word[:, 0], word[:, 1])
-        byte_lookup(B_U8RANGE, word[:, 2], word[:, 3])
+    n_add = len(op)
+    if n_add:
+        sub = op == OP_SUB
+        op1 = np.where(sub, a, b)
+        val = ((op1.astype(np.uint64) + c) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        t = np.zeros((_pow2(n_add), AS_WIDTH), np.uint32)
+        t[:n_add, AS_PC] = pc
+        t[:n_add, AS_NPC] = pc + 4
+        t[:n_add, AS_VAL:AS_VAL + 4] = _bytes(val)
+        x, y = _bytes(op1), _bytes(c)
+        prev = np.zeros(n_add, np.uint32)
+        for k in range(3):
+            prev = ((x[:, k] + y[:, k] + prev) > 255).astype(np.uint32)
+            t[:n_add, AS_CARRY + k] = prev
+        t[:n_add, AS_OP1:AS_OP1 + 4] = x
+        t[:n_add, AS_OP2:AS_OP2 + 4] = y
+        t[:n_add, AS_ADD] = ~sub
+        t[:n_add, AS_SUB] = sub
+        for word in (x, y, _bytes(val)):
+            byte_lookup(B_U8RANGE, word[:, 0], word[:, 1])
+            byte_lookup(B_U8RANGE, word[:, 2], word[:, 3])
+        traces["AddSub"] = t
 
-    # Bitwise (bitwise/mod.rs event_to_row): one byte lookup per limb
-    op, a, b, c, pc2 = ev["bit"]
-    t_bw = np.zeros((_pow2(n_bit), BW_WIDTH), np.uint32)
-    t_bw[:n_bit, BW_PC] = pc2
-    t_bw[:n_bit, BW_NPC] = pc2 + 4
-    ab, bb, cb = _bytes(a), _bytes(b), _bytes(c)
-    t_bw[:n_bit, BW_A:BW_A + 4] = ab
-    t_bw[:n_bit, BW_B:BW_B + 4] = bb
-    t_bw[:n_bit, BW_C:BW_C + 4] = cb
-    for col, o in ((BW_NOR, OP_NOR), (BW_XOR, OP_XOR), (BW_OR, OP_OR), (BW_AND, OP_AND)):
-        t_bw[:n_bit, col] = op == o
-    bop = np.select([op == OP_AND, op == OP_OR, op == OP_XOR], [B_AND, B_OR, B_XOR], B_NOR)
-    for k in range(4):
-        for o in (B_AND, B_OR, B_XOR, B_NOR):
-            s = bop == o
-            byte_lookup(o, bb[s, k], cb[s, k])
+    # Bitwise (bitwise/mod.rs:140-171): one byte lookup per limb
+    op, a, b, c, pc = ev["bit"]
+    n_bit = len(op)
+    if n_bit:
+        t = np.zeros((_pow2(n_bit), BW_WIDTH), np.uint32)
+        t[:n_bit, BW_PC] = pc
+        t[:n_bit, BW_NPC] = pc + 4
+        ab, bb, cb = _bytes(a), _bytes(b), _bytes(c)
+        t[:n_bit, BW_A:BW_A + 4] = ab
+        t[:n_bit, BW_B:BW_B + 4] = bb
+        t[:n_bit, BW_C:BW_C + 4] = cb
+        for col, o in ((BW_NOR, OP_NOR), (BW_XOR, OP_XOR), (BW_OR, OP_OR), (BW_AND, OP_AND)):
+            t[:n_bit, col] = op == o
+        bop = np.select([op == OP_AND, op == OP_OR, op == OP_XOR], [B_AND, B_OR, B_XOR], B_NOR)
+        for k in range(4):
+            for o in (B_AND, B_OR, B_XOR, B_NOR):
+                s_ = bop == o
+                byte_lookup(o, bb[s_, k], cb[s_, k])
+        traces["Bitwise"] = t
+
+    # Lt (alu/lt/mod.rs:179-263)
+    op, a, b, c, pc = ev["lt"]
+    n_lt = len(op)
+    if n_lt:
+        t = np.zeros((_pow2(n_lt), LT_WIDTH), np.uint32)
+        ab, bb, cb = _bytes(a), _bytes(b), _bytes(c)
+        slt = op == OP_SLT
+        t[:n_lt, LT_PC] = pc
+        t[:n_lt, LT_NPC] = pc + 4
+        t[:n_lt, LT_A:LT_A + 4] = ab
+        t[:n_lt, LT_B:LT_B + 4] = bb
+        t[:n_lt, LT_C:LT_C + 4] = cb
+        bm, cm = bb[:, 3] & 0x7F, cb[:, 3] & 0x7F
+        t[:n_lt, LT_BM], t[:n_lt, LT_CM] = bm, cm
+        byte_lookup(B_AND, bb[:, 3], np.full(n_lt, 0x7F))
+        byte_lookup(B_AND, cb[:, 3], np.full(n_lt, 0x7F))
+        bc, cc = bb.copy(), cb.copy()
+        bc[slt, 3], cc[slt, 3] = bm[slt], cm[slt]
+        diff = bc != cc
+        first = np.full(n_lt, -1)
+        for i in (0, 1, 2, 3):  # the most significant differing byte wins
+            first = np.where(diff[:, i], i, first)
+        has = first >= 0
+        fi = np.where(has, first, 0)
+        rows = np.arange(n_lt)
+        bcb = np.where(has, bc[rows, fi], 0).astype(np.int64)
+        ccb = np.where(has, cc[rows, fi], 0).astype(np.int64)
+        sltu = (bcb < ccb).astype(np.uint32)
+        for i in range(4):
+            t[:n_lt, LT_FLAGS + i] = has & (first == i)
+        t[:n_lt, LT_INV] = _inv_table()[bcb - ccb + 255].astype(np.uint32)
+        t[:n_lt, LT_CMP], t[:n_lt, LT_CMP + 1] = bcb, ccb
+        t[:n_lt, LT_SLTU_R] = sltu
+        t[:n_lt, LT_COMP_EQ] = ~has
+        msb_b, msb_c = bb[:, 3] >> 7, cb[:, 3] >> 7
+        t[:n_lt, LT_MSB_B], t[:n_lt, LT_MSB_C] = msb_b, msb_c
+        t[:n_lt, LT_SIGN_EQ] = np.where(slt, msb_b == msb_c, True)
+        t[:n_lt, LT_SLT], t[:n_lt, LT_SLTU] = slt, ~slt
+        t[:n_lt, LT_BIT_B], t[:n_lt, LT_BIT_C] = msb_b * slt, msb_c * slt
+        assert np.array_equal(ab[:, 0], (msb_b * slt) * (1 - msb_c * slt) + t[:n_lt, LT_SIGN_EQ] * sltu)
+        byte_lookup(B_LTU, bcb, ccb)
+        traces["Lt"] = t
+
+    # ShiftLeft (alu/sll/mod.rs:200-260); padded rows: shift_by_n_bits[0] = shift_by_n_bytes[0] =
+    # bit_shift_multiplier = 1 (:142-155)
+    op, a, b, c, pc = ev["sll"]
+    n_sll = len(op)
+    if n_sll:
+        t = np.zeros((_pow2(n_sll), SL_WIDTH), np.uint32)
+        t[:, SL_NBITS] = 1
+        t[:, SL_NBYTES] = 1
+        t[:, SL_MULT] = 1
+        bb = _bytes(b)
+        t[:n_sll, SL_PC] = pc
+        t[:n_sll, SL_NPC] = pc + 4
+        t[:n_sll, SL_A:SL_A + 4] = _bytes(a)
+        t[:n_sll, SL_B:SL_B + 4] = bb
+        t[:n_sll, SL_C:SL_C + 4] = _bytes(c)
+        for i in range(8):
+            t[:n_sll, SL_CBITS + i] = (c >> i) & 1
+        nb = c % 8
+        t[:n_sll, SL_NBITS] = 0
+        for i in range(8):
+            t[:n_sll, SL_NBITS + i] = nb == i
+        mul = (np.uint32(1) << nb).astype(np.uint32)
+        t[:n_sll, SL_MULT] = mul
+        carry = np.zeros(n_sll, np.uint32)
+        res = np.zeros((n_sll, 4), np.uint32)
+        cry = np.zeros((n_sll, 4), np.uint32)
+        for i in range(4):
+            v = bb[:, i] * mul + carry
+            carry = v >> 8
+            res[:, i], cry[:, i] = v & 0xFF, carry
+        t[:n_sll, SL_RES:SL_RES + 4] = res
+        t[:n_sll, SL_CARRY:SL_CARRY + 4] = cry
+        nbyte = (c & 31) // 8
+        t[:n_sll, SL_NBYTES] = 0
+        for i in range(4):
+            t[:n_sll, SL_NBYTES + i] = nbyte == i
+        t[:n_sll, SL_REAL] = 1
+        for word in (res, cry):
+            byte_lookup(B_U8RANGE, word[:, 0], word[:, 1])
+            byte_lookup(B_U8RANGE, word[:, 2], word[:, 3])
+        traces["ShiftLeft"] = t
 
     # instruction source: the CPU's send_instruction tuple of every ALU event
-    n = n_add + n_bit
-    t_is = np.zeros((_pow2(n), IS_WIDTH), np.uint32)
-    ops = np.concatenate([ev["add"][0], ev["bit"][0]])
-    t_is[:n, IS_PC] = np.concatenate([ev["add"][4], ev["bit"][4]])
-    t_is[:n, IS_NPC] = t_is[:n, IS_PC] + 4
-    t_is[:n, IS_OP] = ops
+    kinds = [ev[k] for k in ("add", "bit", "lt", "sll")]
+    n = sum(len(e[0]) for e in kinds)
+    t = np.zeros((_pow2(n), IS_WIDTH), np.uint32)
+    t[:n, IS_PC] = np.concatenate([e[4] for e in kinds])
+    t[:n, IS_NPC] = t[:n, IS_PC] + 4
+    t[:n, IS_OP] = np.concatenate([e[0] for e in kinds])
     for base, j in ((IS_A, 1), (IS_B, 2), (IS_C, 3)):
-        t_is[:n, base:base + 4] = _bytes(np.concatenate([ev["add"][j], ev["bit"][j]]))
-    t_is[:n, IS_REAL] = 1
+        t[:n, base:base + 4] = _bytes(np.concatenate([e[j] for e in kinds]))
+    t[:n, IS_REAL] = 1
+    traces = {"InstrSource": t, **traces}
 
     assert mult.max() < P
-    traces = {"InstrSource": t_is, "AddSub": t_as, "Bitwise": t_bw, "Byte": mult.astype(np.uint32)}
+    traces["Byte"] = mult.astype(np.uint32)
     pvs = (splitmix64(0xA1B1000 + seed, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
     return alu_machine(), {"Byte": byte_prep_trace()}, traces, pvs
