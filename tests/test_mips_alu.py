@@ -1,4 +1,4 @@
-"""MIPS ALU slice (AddSub, Bitwise, Lt, ShiftLeft, Byte restated from the reference AIRs; zkmips_amd/mips_alu.py).
+"""MIPS ALU slice (AddSub, Bitwise, Lt, ShiftLeft, ShiftRight, Byte restated from the reference AIRs; zkmips_amd/mips_alu.py).
 
 CPU part: the trace generators reproduce the reference's own fixtures and table semantics, the
 oracle proves and its verifier accepts a multi-chip shard whose Byte / Instruction lookups balance
@@ -48,7 +48,7 @@ def test_reference_fixture_events():
 
 @pytest.fixture(scope="module")
 def shard():
-    return A.alu_shard(300, 200, seed=5, n_lt=250, n_sll=100)
+    return A.alu_shard(300, 200, seed=5, n_lt=250, n_sll=100, n_sr=120)
 
 
 @pytest.fixture(scope="module")
@@ -61,9 +61,9 @@ def test_alu_shard_proves_and_verifies(shard, oracle):
     m, _, tr, pv = shard
     heights = {k: v.shape[0] for k, v in tr.items()}
     assert heights == {"InstrSource": 1024, "AddSub": 512, "Bitwise": 256, "Lt": 256, "ShiftLeft": 128,
-                       "Byte": 65536}
-    assert [c.name for c in m.chips] == ["InstrSource", "AddSub", "Bitwise", "Lt", "ShiftLeft", "Byte"]
-    assert [c.perm_width_ef for c in m.chips] == [2, 5, 4, 3, 4, 6]
+                       "ShiftRight": 128, "Byte": 65536}
+    assert [c.name for c in m.chips] == ["InstrSource", "AddSub", "Bitwise", "Lt", "ShiftLeft", "ShiftRight", "Byte"]
+    assert [c.perm_width_ef for c in m.chips] == [2, 5, 4, 3, 4, 14, 6]
     rc, proof = oracle.prove(tr, pv)
     assert rc == 0 and oracle.verify(proof) == 0
 
@@ -74,6 +74,22 @@ def test_shard_without_some_chips(oracle):
     assert sorted(tr) == ["AddSub", "Bitwise", "Byte", "InstrSource"]
     rc, proof = oracle.prove(tr, pv)
     assert rc == 0 and oracle.verify(proof) == 0
+
+
+def test_shift_right_semantics():
+    """SRL/SRA/ROR by every shift amount, including negative operands for SRA."""
+    b = 0x8123F567
+    evs = []
+    for i in range(40):
+        s = i & 31
+        evs += [(12 * i, A.OP_SRL, b >> s, b, i), (12 * i + 4, A.OP_SRA, ((b - (1 << 32)) >> s) & 0xFFFFFFFF, b, i),
+                (12 * i + 8, A.OP_ROR, ((b >> s) | (b << (32 - s))) & 0xFFFFFFFF, b, i)]
+    m, prep, tr, pv = A.alu_shard_from(A.events_from_list([], [], sr_events=evs))
+    sr = tr["ShiftRight"]
+    assert sr.shape[0] == 128 and sr[127, A.SR_NBITS] == 1 and sr[127, A.SR_NBYTES] == 1  # padding rows
+    cpu = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = cpu.prove(tr, pv)
+    assert rc == 0 and cpu.verify(proof) == 0
 
 
 def test_lt_sll_semantics():
@@ -95,7 +111,7 @@ def test_lt_sll_semantics():
 
 
 @pytest.mark.parametrize("what", ["carry", "bitwise_result", "byte_mult", "dropped_instruction", "lt_result",
-                                  "sll_carry"])
+                                  "sll_carry", "sr_sign"])
 def test_alu_tamper_rejected(shard, oracle, what):
     _, _, tr, pv = shard
     bad = {k: v.copy() for k, v in tr.items()}
@@ -110,8 +126,10 @@ def test_alu_tamper_rejected(shard, oracle, what):
         bad["Lt"][9, A.LT_SLTU_R] ^= 1
     elif what == "sll_carry":
         bad["ShiftLeft"][4, A.SL_CARRY] += 1
+    elif what == "sr_sign":  # an SRA/ROR row whose sign bit disagrees with b's top byte
+        bad["ShiftRight"][5, A.SR_MSB] ^= 1
     else:  # the CPU stand-in claims an instruction no ALU chip executes
-        bad["InstrSource"][1000, A.IS_REAL] = 1  # a padding row (850 events)
+        bad["InstrSource"][1000, A.IS_REAL] = 1  # a padding row (970 events)
     rc, proof = oracle.prove(bad, pv)
     assert rc == 0
     assert oracle.verify(proof) != 0
@@ -127,11 +145,12 @@ def dev():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_add,n_bit,n_lt,n_sll", [(300, 200, 0, 0), (300, 200, 250, 100),
-                                                   (1 << 13, 5000, 3000, 1 << 12), (1 << 15, 1 << 15, 1 << 15, 1 << 15)])
-def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit, n_lt, n_sll):
+@pytest.mark.parametrize("n_add,n_bit,n_lt,n_sll,n_sr", [(300, 200, 0, 0, 0), (300, 200, 250, 100, 120),
+                                                        (1 << 13, 5000, 3000, 1 << 12, 7000),
+                                                        (1 << 15, 1 << 15, 1 << 15, 1 << 14, 1 << 14)])
+def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit, n_lt, n_sll, n_sr):
     from zkmips_amd.prover import HipProver
-    m, prep, tr, pv = A.alu_shard(n_add, n_bit, seed=n_add, n_lt=n_lt, n_sll=n_sll)
+    m, prep, tr, pv = A.alu_shard(n_add, n_bit, seed=n_add, n_lt=n_lt, n_sll=n_sll, n_sr=n_sr)
     gpu = HipProver(dev, m, prep, num_queries=16)
     cpu = O.OracleProver(m, prep, num_queries=16)
     assert np.array_equal(gpu.vk_commit, cpu.commit)
@@ -144,7 +163,7 @@ def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit, n_lt, n_sll):
 @pytest.mark.gpu
 def test_alu_gpu_full_size_verifies(dev):
     from zkmips_amd.prover import HipProver
-    m, prep, tr, pv = A.alu_shard(1 << 20, 1 << 20, seed=9, n_lt=1 << 20, n_sll=1 << 20)
+    m, prep, tr, pv = A.alu_shard(1 << 20, 1 << 20, seed=9, n_lt=1 << 20, n_sll=1 << 19, n_sr=1 << 19)
     assert tr["InstrSource"].shape[0] == 1 << 22
     gpu = HipProver(dev, m, prep, num_queries=84)
     cpu = O.OracleProver(m, prep, num_queries=84)

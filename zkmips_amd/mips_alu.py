@@ -10,6 +10,7 @@ alpha powers of the quotient fold and the LogUp column layout):
 * ``Bitwise`` crates/core/machine/src/alu/bitwise/mod.rs:184-234; columns :33-59.
 * ``Lt``      crates/core/machine/src/alu/lt/mod.rs:277-466 (SLT/SLTU); trace: event_to_row :179-263.
 * ``ShiftLeft`` crates/core/machine/src/alu/sll/mod.rs:273-406 (SLL); trace :200-260, padding :142-155.
+* ``ShiftRight`` crates/core/machine/src/alu/sr/mod.rs:338-536 (SRL, SRA, ROR); trace :220-325.
 * ``Byte``    crates/core/machine/src/bytes/{air.rs:24-74, columns.rs, mod.rs:50-120, trace.rs:40-70}:
   the preprocessed 2^16-row table of all byte operations and its 10 multiplicity columns.
 
@@ -282,10 +283,71 @@ def shift_left_chip() -> ChipDesc:
     return ch
 
 
+# ---------------------------------------------------------------- ShiftRight
+# ShiftRightCols (alu/sr/mod.rs:88-137)
+(SR_PC, SR_NPC, SR_A, SR_B, SR_C, SR_NBITS, SR_NBYTES, SR_BYTE_RES, SR_BIT_RES, SR_CARRY, SR_SHIFTED, SR_MSB,
+ SR_CBITS, SR_SRL, SR_ROR, SR_SRA, SR_REAL) = (0, 1, 2, 6, 10, 14, 22, 26, 34, 42, 50, 58, 59, 67, 68, 69, 70)
+SR_WIDTH = 71
+OP_SRL, OP_SRA, OP_ROR = 10, 11, 12
+
+
+def shift_right_chip() -> ChipDesc:
+    """ShiftRightChip::eval, alu/sr/mod.rs:338-536 (SRL, SRA, ROR)."""
+    ch = ChipDesc("ShiftRight", prep_width=0, main_width=SR_WIDTH, local_only=True)
+    M = main
+    real = _m(SR_REAL)
+    ch.sends.append(Lookup([V.const(B_MSB), _m(SR_MSB), ZERO, _m(SR_B + 3), ZERO], real, KIND_BYTE))
+    cb = [M(SR_CBITS + i) for i in range(8)]
+    ch.assert_zero(sum((cb[i] * (1 << i) for i in range(1, 8)), cb[0]) - M(SR_C))
+    nbits = cb[0] + cb[1] * 2 + cb[2] * 4
+    for i in range(8):
+        ch.assert_zero(M(SR_NBITS + i) * (nbits - i))
+    ch.assert_zero(sum((M(SR_NBITS + i) for i in range(1, 8)), M(SR_NBITS)) - 1)
+    nbytes = cb[3] + cb[4] * 2
+    for i in range(4):
+        ch.assert_zero(M(SR_NBYTES + i) * (nbytes - i))
+    ch.assert_zero(sum((M(SR_NBYTES + i) for i in range(1, 4)), M(SR_NBYTES)) - 1)
+    sext = [M(SR_B + i) for i in range(4)]
+    sext += [M(SR_SRA) * M(SR_MSB) * 0xFF + M(SR_ROR) * M(SR_B + i) for i in range(4)]
+    for nb in range(4):
+        for i in range(8 - nb):
+            ch.assert_zero(M(SR_NBYTES + nb) * (M(SR_BYTE_RES + i) - sext[i + nb]))
+    carry_mult = sum((M(SR_NBITS + i) * (1 << (8 - i)) for i in range(1, 8)), M(SR_NBITS) * 256)
+    nbits_vpc = V([("main", SR_CBITS, 1), ("main", SR_CBITS + 1, 2), ("main", SR_CBITS + 2, 4)])
+    for i in range(7, -1, -1):
+        ch.sends.append(Lookup([V.const(B_SHRCARRY), _m(SR_SHIFTED + i), _m(SR_CARRY + i), _m(SR_BYTE_RES + i),
+                                nbits_vpc], real, KIND_BYTE))
+    for i in range(7, -1, -1):
+        v = M(SR_SHIFTED + i)
+        if i + 1 < 8:
+            v = v + M(SR_CARRY + i + 1) * carry_mult
+        ch.assert_zero(v - M(SR_BIT_RES + i))
+    for i in range(4):
+        ch.assert_zero(M(SR_A + i) - M(SR_BIT_RES + i))
+    for col in (SR_SRL, SR_SRA, SR_ROR, SR_REAL, SR_MSB):
+        _assert_bool(ch, M(col))
+    for i in range(4):
+        _assert_bool(ch, M(SR_NBYTES + i))
+    for i in range(8):
+        _assert_bool(ch, M(SR_NBITS + i))
+    for i in range(8):
+        _assert_bool(ch, cb[i])
+    for base in (SR_BYTE_RES, SR_BIT_RES, SR_CARRY, SR_SHIFTED):
+        for k in (0, 2, 4, 6):
+            ch.sends.append(Lookup([V.const(B_U8RANGE), ZERO, ZERO, _m(base + k), _m(base + k + 1)], real, KIND_BYTE))
+    for col in (SR_SRL, SR_SRA, SR_ROR, SR_REAL):
+        _assert_bool(ch, M(col))
+    ch.assert_zero(M(SR_SRL) + M(SR_SRA) + M(SR_ROR) - M(SR_REAL))
+    w = lambda base: [_m(base + i) for i in range(4)]
+    op = V([("main", SR_SRL, OP_SRL), ("main", SR_SRA, OP_SRA), ("main", SR_ROR, OP_ROR)])
+    ch.receives.append(Lookup(_instruction(SR_PC, SR_NPC, op, w(SR_A), w(SR_B), w(SR_C)), real, KIND_INSTRUCTION))
+    return ch
+
+
 def alu_machine() -> MachineDesc:
     # chip order as in MipsAir::chips (crates/core/machine/src/mips/mod.rs): Cpu first, ALUs, Byte
     return MachineDesc([instr_source_chip(), add_sub_chip(), bitwise_chip(), lt_chip(), shift_left_chip(),
-                        byte_chip()], NUM_PV_ELTS)
+                        shift_right_chip(), byte_chip()], NUM_PV_ELTS)
 
 
 # ---------------------------------------------------------------- trace generation
@@ -297,11 +359,11 @@ def _pow2(n: int) -> int:
     return max(16, 1 << max(0, (n - 1).bit_length()))
 
 
-def alu_events(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0):
+def alu_events(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0, n_sr: int = 0):
     """Synthetic ALU events per chip: (opcode, a, b, c, pc) with a = op(b, c) as the executor computes
     it; ADD/SUB, the four bitwise ops and SLT/SLTU alternate; operands uniform u32 (SplitMix64),
     Lt operands share their top bytes half of the time so every comparison-byte position occurs."""
-    n = n_add + n_bit + n_lt + n_sll
+    n = n_add + n_bit + n_lt + n_sll + n_sr
     r = splitmix64(0xA1B0000 + seed, 2 * n + 2)
     b = (r[0::2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)[:n]
     c = (r[1::2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)[:n]
@@ -335,21 +397,32 @@ def alu_events(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int 
     bs, cs = b[o:o + n_sll], c[o:o + n_sll]
     out["sll"] = (np.full(n_sll, OP_SLL, np.uint32), (bs << (cs & np.uint32(31))).astype(np.uint32), bs, cs,
                   pc[o:o + n_sll])
+    o += n_sll
+    br, cr = b[o:o + n_sr], c[o:o + n_sr]
+    kind = np.arange(n_sr) % 3
+    sh = (cr & np.uint32(31)).astype(np.uint64)
+    b64 = br.astype(np.uint64)
+    srl = b64 >> sh
+    sra = (br.view(np.int32).astype(np.int64) >> sh.astype(np.int64)).astype(np.uint64)
+    ror = ((b64 | (b64 << np.uint64(32))) >> sh)
+    a_sr = (np.select([kind == 0, kind == 1], [srl, sra], ror) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    out["sr"] = (np.asarray([OP_SRL, OP_SRA, OP_ROR], np.uint32)[kind], a_sr, br, cr, pc[o:o + n_sr])
     return out
 
 
-def events_from_list(add_events, bit_events, lt_events=(), sll_events=()):
+def events_from_list(add_events, bit_events, lt_events=(), sll_events=(), sr_events=()):
     """Events given as the reference's AluEvent::new(pc, opcode, a, b, c) tuples (next_pc = pc + 4,
     crates/core/executor/src/events/instr.rs:31-33)."""
     def cols(evs):
         arr = np.asarray([(op, a, b, c, pc) for pc, op, a, b, c in evs], np.uint64).reshape(-1, 5)
         return tuple(arr[:, i].astype(np.uint32) for i in range(5))
-    return {"add": cols(add_events), "bit": cols(bit_events), "lt": cols(lt_events), "sll": cols(sll_events)}
+    return {"add": cols(add_events), "bit": cols(bit_events), "lt": cols(lt_events), "sll": cols(sll_events),
+            "sr": cols(sr_events)}
 
 
-def alu_shard(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0):
+def alu_shard(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0, n_sr: int = 0):
     """(machine, prep_traces, traces, public_values) of one ALU-slice shard of random events."""
-    return alu_shard_from(alu_events(n_add, n_bit, seed, n_lt, n_sll), seed)
+    return alu_shard_from(alu_events(n_add, n_bit, seed, n_lt, n_sll, n_sr), seed)
 
 
 def _inv_table():
@@ -494,8 +567,57 @@ def alu_shard_from(ev, seed: int = 3):
             byte_lookup(B_U8RANGE, word[:, 2], word[:, 3])
         traces["ShiftLeft"] = t
 
+    # ShiftRight (alu/sr/mod.rs:220-325); padded rows: shift_by_n_bits[0] = shift_by_n_bytes[0] = 1
+    op, a, b, c, pc = ev.get("sr", (np.zeros(0, np.uint32),) * 5)
+    n_sr = len(op)
+    if n_sr:
+        t = np.zeros((_pow2(n_sr), SR_WIDTH), np.uint32)
+        t[:, SR_NBITS] = 1
+        t[:, SR_NBYTES] = 1
+        t[:n_sr, SR_PC] = pc
+        t[:n_sr, SR_NPC] = pc + 4
+        t[:n_sr, SR_A:SR_A + 4] = _bytes(a)
+        bb = _bytes(b)
+        t[:n_sr, SR_B:SR_B + 4] = bb
+        t[:n_sr, SR_C:SR_C + 4] = _bytes(c)
+        msb = (b >> 31) & 1
+        t[:n_sr, SR_MSB] = msb
+        byte_lookup(B_MSB, bb[:, 3], np.zeros(n_sr, np.uint32))
+        for i in range(8):
+            t[:n_sr, SR_CBITS + i] = (c >> i) & 1
+        t[:n_sr, SR_SRL], t[:n_sr, SR_SRA], t[:n_sr, SR_ROR] = op == OP_SRL, op == OP_SRA, op == OP_ROR
+        t[:n_sr, SR_REAL] = 1
+        nbyte = ((c & 31) // 8).astype(np.uint64)
+        nbit = ((c & 31) % 8).astype(np.uint32)
+        b64 = b.astype(np.uint64)
+        sext = np.where(op == OP_SRA, (b.view(np.int32).astype(np.int64)).astype(np.uint64),
+                        np.where(op == OP_ROR, b64 | (b64 << np.uint64(32)), b64))
+        bsr = sext >> (np.uint64(8) * nbyte)
+        byte_res = np.stack([((bsr >> np.uint64(8 * i)) & np.uint64(0xFF)).astype(np.uint32) for i in range(8)], 1)
+        t[:n_sr, SR_NBYTES] = 0
+        for i in range(4):
+            t[:n_sr, SR_NBYTES + i] = nbyte == i
+        t[:n_sr, SR_NBITS] = 0
+        for i in range(8):
+            t[:n_sr, SR_NBITS + i] = nbit == i
+        shifted = byte_res >> nbit[:, None]
+        carry = byte_res & ((np.uint32(1) << nbit) - 1)[:, None]
+        bit_res = shifted.copy()
+        bit_res[:, :7] = (shifted[:, :7] + (carry[:, 1:] << (8 - nbit)[:, None])) & 0xFF
+        t[:n_sr, SR_BYTE_RES:SR_BYTE_RES + 8] = byte_res
+        t[:n_sr, SR_BIT_RES:SR_BIT_RES + 8] = bit_res
+        t[:n_sr, SR_CARRY:SR_CARRY + 8] = carry
+        t[:n_sr, SR_SHIFTED:SR_SHIFTED + 8] = shifted
+        assert np.array_equal(bit_res[:, :4], t[:n_sr, SR_A:SR_A + 4])
+        for i in range(8):
+            byte_lookup(B_SHRCARRY, byte_res[:, i], nbit)
+        for word in (byte_res, bit_res, carry, shifted):
+            for k in (0, 2, 4, 6):
+                byte_lookup(B_U8RANGE, word[:, k], word[:, k + 1])
+        traces["ShiftRight"] = t
+
     # instruction source: the CPU's send_instruction tuple of every ALU event
-    kinds = [ev[k] for k in ("add", "bit", "lt", "sll")]
+    kinds = [ev[k] for k in ("add", "bit", "lt", "sll", "sr") if k in ev]
     n = sum(len(e[0]) for e in kinds)
     t = np.zeros((_pow2(n), IS_WIDTH), np.uint32)
     t[:n, IS_PC] = np.concatenate([e[4] for e in kinds])
