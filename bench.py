@@ -128,7 +128,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-out", default="")
     ap.add_argument("--profile-steps", type=int, default=3, help="single-shard proofs in the profiled region")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="shards proven concurrently per GPU (one host thread + HIP stream each), as the "
                          "reference's prove_with_context runs commit/open for all shards of a batch at once")
     args = ap.parse_args()
