@@ -162,7 +162,7 @@ def main():
         if args.workload == "alu":
             from zkmips_amd import mips_alu as A
             m, prep, traces_k, pvs_k = A.alu_shard(n // 4, n // 4, seed=1000 + rank * K + k, n_lt=n // 4,
-                                                   n_sll=n // 8, n_sr=n // 8)
+                                                   n_sll=n // 8, n_sr=n // 16, n_clz=n // 16)
         else:
             m, prep, traces_k, pvs_k = W.fib_shard(n, seed=1000 + rank * K + k)
         shards.append(({kk: torch.from_numpy(v.view(np.int32)).cuda() for kk, v in traces_k.items()}, pvs_k, traces_k))
@@ -292,7 +292,8 @@ def main():
                                 f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard")
                    if args.workload == "fib" else
                    (f"MIPS ALU slice: InstrSource 2^{args.log_n} + AddSub, Bitwise, Lt 2^{args.log_n - 2} + ShiftLeft, "
-                    f"ShiftRight 2^{args.log_n - 3} + Byte 2^16 (prep 12): full commit+open per shard"),
+                    f"ShiftRight (CPU + CloClz SRLs) 2^{args.log_n - 3} + CloClz 2^{args.log_n - 4} + Byte 2^16 "
+                    f"(prep 12): full commit+open per shard"),
                    "rows_per_shard": rows_per_shard, "fri_queries": args.queries, "pow_bits": 16, "log_blowup": 1,
                    "shards_per_gpu_per_step": K, "parallelism": f"shard-parallel x{world}, {K} in flight per GPU",
                    "proof_bytes": len(proof)},

@@ -1,4 +1,4 @@
-"""MIPS ALU slice (AddSub, Bitwise, Lt, ShiftLeft, ShiftRight, Byte restated from the reference AIRs; zkmips_amd/mips_alu.py).
+"""MIPS ALU slice (AddSub, Bitwise, Lt, ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs; zkmips_amd/mips_alu.py).
 
 CPU part: the trace generators reproduce the reference's own fixtures and table semantics, the
 oracle proves and its verifier accepts a multi-chip shard whose Byte / Instruction lookups balance
@@ -48,7 +48,7 @@ def test_reference_fixture_events():
 
 @pytest.fixture(scope="module")
 def shard():
-    return A.alu_shard(300, 200, seed=5, n_lt=250, n_sll=100, n_sr=120)
+    return A.alu_shard(300, 200, seed=5, n_lt=250, n_sll=100, n_sr=120, n_clz=40)
 
 
 @pytest.fixture(scope="module")
@@ -61,9 +61,10 @@ def test_alu_shard_proves_and_verifies(shard, oracle):
     m, _, tr, pv = shard
     heights = {k: v.shape[0] for k, v in tr.items()}
     assert heights == {"InstrSource": 1024, "AddSub": 512, "Bitwise": 256, "Lt": 256, "ShiftLeft": 128,
-                       "ShiftRight": 128, "Byte": 65536}
-    assert [c.name for c in m.chips] == ["InstrSource", "AddSub", "Bitwise", "Lt", "ShiftLeft", "ShiftRight", "Byte"]
-    assert [c.perm_width_ef for c in m.chips] == [2, 5, 4, 3, 4, 14, 6]
+                       "ShiftRight": 256, "CloClz": 64, "Byte": 65536}
+    assert [c.name for c in m.chips] == ["InstrSource", "AddSub", "Bitwise", "Lt", "ShiftLeft", "ShiftRight",
+                                         "CloClz", "Byte"]
+    assert [c.perm_width_ef for c in m.chips] == [2, 5, 4, 3, 4, 14, 4, 6]
     rc, proof = oracle.prove(tr, pv)
     assert rc == 0 and oracle.verify(proof) == 0
 
@@ -74,6 +75,22 @@ def test_shard_without_some_chips(oracle):
     assert sorted(tr) == ["AddSub", "Bitwise", "Byte", "InstrSource"]
     rc, proof = oracle.prove(tr, pv)
     assert rc == 0 and oracle.verify(proof) == 0
+
+
+def test_cloclz_reference_fixture():
+    """The events of the reference's CloClz generate_trace test (alu/clo_clz/mod.rs:289-296); every
+    non-zero operand makes the chip send an SRL that the ShiftRight chip receives."""
+    ev = A.events_from_list([], [], clz_events=[(0, A.OP_CLZ, 32, 0, 0), (0, A.OP_CLZ, 8, 0x00800000, 0),
+                                                (0, A.OP_CLZ, 0, 0xFFFFFFFF, 0), (0, A.OP_CLO, 32, 0xFFFFFFFF, 0),
+                                                (0, A.OP_CLO, 8, 0xFF7FFFFF, 0), (0, A.OP_CLO, 0, 0, 0)])
+    m, prep, tr, pv = A.alu_shard_from(ev)
+    cz, sr = tr["CloClz"], tr["ShiftRight"]
+    assert list(cz[:6, A.CZ_BB_ZERO]) == [1, 0, 0, 1, 0, 0]
+    assert list(sr[:4, A.SR_PC]) == [A.UNUSED_PC] * 4 and sr[:4, A.SR_SRL].all()
+    assert list(cz[10, [A.CZ_A, A.CZ_CLZ, A.CZ_BB_ZERO, A.CZ_REAL]]) == [32, 1, 1, 0]  # padding row
+    cpu = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = cpu.prove(tr, pv)
+    assert rc == 0 and cpu.verify(proof) == 0
 
 
 def test_shift_right_semantics():
@@ -111,7 +128,7 @@ def test_lt_sll_semantics():
 
 
 @pytest.mark.parametrize("what", ["carry", "bitwise_result", "byte_mult", "dropped_instruction", "lt_result",
-                                  "sll_carry", "sr_sign"])
+                                  "sll_carry", "sr_sign", "clz_count"])
 def test_alu_tamper_rejected(shard, oracle, what):
     _, _, tr, pv = shard
     bad = {k: v.copy() for k, v in tr.items()}
@@ -126,10 +143,12 @@ def test_alu_tamper_rejected(shard, oracle, what):
         bad["Lt"][9, A.LT_SLTU_R] ^= 1
     elif what == "sll_carry":
         bad["ShiftLeft"][4, A.SL_CARRY] += 1
+    elif what == "clz_count":  # a wrong leading-zero count: the SRL it sends has no receiver
+        bad["CloClz"][3, A.CZ_A] += 1
     elif what == "sr_sign":  # an SRA/ROR row whose sign bit disagrees with b's top byte
         bad["ShiftRight"][5, A.SR_MSB] ^= 1
     else:  # the CPU stand-in claims an instruction no ALU chip executes
-        bad["InstrSource"][1000, A.IS_REAL] = 1  # a padding row (970 events)
+        bad["InstrSource"][1020, A.IS_REAL] = 1  # a padding row (1010 events)
     rc, proof = oracle.prove(bad, pv)
     assert rc == 0
     assert oracle.verify(proof) != 0
@@ -145,12 +164,12 @@ def dev():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_add,n_bit,n_lt,n_sll,n_sr", [(300, 200, 0, 0, 0), (300, 200, 250, 100, 120),
-                                                        (1 << 13, 5000, 3000, 1 << 12, 7000),
-                                                        (1 << 15, 1 << 15, 1 << 15, 1 << 14, 1 << 14)])
-def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit, n_lt, n_sll, n_sr):
+@pytest.mark.parametrize("n_add,n_bit,n_lt,n_sll,n_sr,n_clz", [(300, 200, 0, 0, 0, 0), (300, 200, 250, 100, 120, 40),
+                                                              (1 << 13, 5000, 3000, 1 << 12, 7000, 3000),
+                                                              (1 << 15, 1 << 15, 1 << 15, 1 << 14, 1 << 13, 1 << 13)])
+def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit, n_lt, n_sll, n_sr, n_clz):
     from zkmips_amd.prover import HipProver
-    m, prep, tr, pv = A.alu_shard(n_add, n_bit, seed=n_add, n_lt=n_lt, n_sll=n_sll, n_sr=n_sr)
+    m, prep, tr, pv = A.alu_shard(n_add, n_bit, seed=n_add, n_lt=n_lt, n_sll=n_sll, n_sr=n_sr, n_clz=n_clz)
     gpu = HipProver(dev, m, prep, num_queries=16)
     cpu = O.OracleProver(m, prep, num_queries=16)
     assert np.array_equal(gpu.vk_commit, cpu.commit)
@@ -163,7 +182,8 @@ def test_alu_gpu_proof_bytes_identical(dev, n_add, n_bit, n_lt, n_sll, n_sr):
 @pytest.mark.gpu
 def test_alu_gpu_full_size_verifies(dev):
     from zkmips_amd.prover import HipProver
-    m, prep, tr, pv = A.alu_shard(1 << 20, 1 << 20, seed=9, n_lt=1 << 20, n_sll=1 << 19, n_sr=1 << 19)
+    m, prep, tr, pv = A.alu_shard(1 << 20, 1 << 20, seed=9, n_lt=1 << 20, n_sll=1 << 19, n_sr=1 << 18,
+                                  n_clz=1 << 18)
     assert tr["InstrSource"].shape[0] == 1 << 22
     gpu = HipProver(dev, m, prep, num_queries=84)
     cpu = O.OracleProver(m, prep, num_queries=84)

@@ -11,6 +11,8 @@ alpha powers of the quotient fold and the LogUp column layout):
 * ``Lt``      crates/core/machine/src/alu/lt/mod.rs:277-466 (SLT/SLTU); trace: event_to_row :179-263.
 * ``ShiftLeft`` crates/core/machine/src/alu/sll/mod.rs:273-406 (SLL); trace :200-260, padding :142-155.
 * ``ShiftRight`` crates/core/machine/src/alu/sr/mod.rs:338-536 (SRL, SRA, ROR); trace :220-325.
+* ``CloClz``  crates/core/machine/src/alu/clo_clz/mod.rs:181-271 (CLZ/CLO); it sends an SRL to
+  ShiftRight like the executor's dependency event (executor/src/dependencies.rs:107-122).
 * ``Byte``    crates/core/machine/src/bytes/{air.rs:24-74, columns.rs, mod.rs:50-120, trace.rs:40-70}:
   the preprocessed 2^16-row table of all byte operations and its 10 multiplicity columns.
 
@@ -344,10 +346,53 @@ def shift_right_chip() -> ChipDesc:
     return ch
 
 
+# ---------------------------------------------------------------- CloClz
+# CloClzCols (alu/clo_clz/mod.rs:44-73)
+CZ_PC, CZ_NPC, CZ_A, CZ_B, CZ_BB, CZ_BB_ZERO, CZ_SR1, CZ_CLZ, CZ_CLO, CZ_REAL = 0, 1, 2, 6, 10, 14, 15, 19, 20, 21
+CZ_WIDTH = 22
+OP_CLZ, OP_CLO = 19, 20
+UNUSED_PC, DEFAULT_PC_INC = 1, 4  # crates/stark/src/air/builder.rs:19-22
+
+
+def clo_clz_chip() -> ChipDesc:
+    """CloClzChip::eval, alu/clo_clz/mod.rs:181-271.  It sends an SRL to the ShiftRight chip
+    (send_alu, builder.rs:283-322) to prove that bit 31 - a of bb is its leading one."""
+    ch = ChipDesc("CloClz", prep_width=0, main_width=CZ_WIDTH, local_only=True)
+    M = main
+    for i in range(4):
+        ch.assert_zero(M(CZ_CLO) * (M(CZ_B + i) + M(CZ_BB + i) - 255))
+        ch.assert_zero(M(CZ_CLZ) * (M(CZ_B + i) - M(CZ_BB + i)))
+    real = _m(CZ_REAL)
+    for k in (0, 2):
+        ch.sends.append(Lookup([V.const(B_U8RANGE), ZERO, ZERO, _m(CZ_BB + k), _m(CZ_BB + k + 1)], real, KIND_BYTE))
+    ch.sends.append(Lookup([V.const(B_LTU), V.const(1), ZERO, _m(CZ_A), V.const(33)], real, KIND_BYTE))
+    for i in (1, 2, 3):
+        ch.assert_zero(M(CZ_REAL) * M(CZ_A + i))
+    w = lambda base: [_m(base + i) for i in range(4)]
+    op = V([("main", CZ_CLO, OP_CLO), ("main", CZ_CLZ, OP_CLZ)])
+    ch.receives.append(Lookup(_instruction(CZ_PC, CZ_NPC, op, w(CZ_A), w(CZ_B), [ZERO] * 4), real, KIND_INSTRUCTION))
+    zero_bb = M(CZ_BB_ZERO)
+    _assert_bool(ch, zero_bb)
+    ch.assert_zero(zero_bb * sum((M(CZ_BB + i) * (1 << (8 * i)) for i in range(1, 4)), M(CZ_BB)))
+    ch.assert_zero(zero_bb * M(CZ_BB + 3))
+    ch.assert_zero(zero_bb * (M(CZ_A) - 32))
+    srl = [ZERO, ZERO, V.const(UNUSED_PC), V.const(UNUSED_PC + DEFAULT_PC_INC),
+           V.const(UNUSED_PC + 2 * DEFAULT_PC_INC), ZERO, V.const(OP_SRL)]
+    srl += w(CZ_SR1) + w(CZ_BB) + [V([("main", CZ_A, P - 1)], 31), ZERO, ZERO, ZERO] + [ZERO] * 4
+    srl += [ZERO, ZERO, ZERO, ZERO, V.const(1)]
+    ch.sends.append(Lookup(srl, V([("main", CZ_BB_ZERO, P - 1)], 1), KIND_INSTRUCTION))
+    ch.assert_zero((1 - zero_bb) * (sum((M(CZ_SR1 + i) * (1 << (8 * i)) for i in range(1, 4)), M(CZ_SR1)) - 1))
+    ch.assert_zero((1 - zero_bb) * M(CZ_SR1 + 3))
+    _assert_bool(ch, M(CZ_CLO))
+    _assert_bool(ch, M(CZ_CLZ))
+    ch.assert_zero(M(CZ_CLO) + M(CZ_CLZ) - 1)
+    return ch
+
+
 def alu_machine() -> MachineDesc:
     # chip order as in MipsAir::chips (crates/core/machine/src/mips/mod.rs): Cpu first, ALUs, Byte
     return MachineDesc([instr_source_chip(), add_sub_chip(), bitwise_chip(), lt_chip(), shift_left_chip(),
-                        shift_right_chip(), byte_chip()], NUM_PV_ELTS)
+                        shift_right_chip(), clo_clz_chip(), byte_chip()], NUM_PV_ELTS)
 
 
 # ---------------------------------------------------------------- trace generation
@@ -359,11 +404,12 @@ def _pow2(n: int) -> int:
     return max(16, 1 << max(0, (n - 1).bit_length()))
 
 
-def alu_events(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0, n_sr: int = 0):
+def alu_events(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0, n_sr: int = 0,
+               n_clz: int = 0):
     """Synthetic ALU events per chip: (opcode, a, b, c, pc) with a = op(b, c) as the executor computes
     it; ADD/SUB, the four bitwise ops and SLT/SLTU alternate; operands uniform u32 (SplitMix64),
     Lt operands share their top bytes half of the time so every comparison-byte position occurs."""
-    n = n_add + n_bit + n_lt + n_sll + n_sr
+    n = n_add + n_bit + n_lt + n_sll + n_sr + n_clz
     r = splitmix64(0xA1B0000 + seed, 2 * n + 2)
     b = (r[0::2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)[:n]
     c = (r[1::2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)[:n]
@@ -407,22 +453,40 @@ def alu_events(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int 
     ror = ((b64 | (b64 << np.uint64(32))) >> sh)
     a_sr = (np.select([kind == 0, kind == 1], [srl, sra], ror) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     out["sr"] = (np.asarray([OP_SRL, OP_SRA, OP_ROR], np.uint32)[kind], a_sr, br, cr, pc[o:o + n_sr])
+    o += n_sr
+    bz = b[o:o + n_clz] >> (c[o:o + n_clz] & np.uint32(31))  # every leading-zero count occurs
+    k = np.arange(n_clz)
+    clo = k % 2 == 1
+    bz = np.where(clo, ~bz, bz).astype(np.uint32)
+    bz[k % 16 == 14] = 0
+    bz[k % 16 == 15] = 0xFFFFFFFF
+    out["clz"] = (np.where(clo, OP_CLO, OP_CLZ).astype(np.uint32), _count_leading(bz, clo), bz,
+                  np.zeros(n_clz, np.uint32), pc[o:o + n_clz])
     return out
 
 
-def events_from_list(add_events, bit_events, lt_events=(), sll_events=(), sr_events=()):
+def _count_leading(b: np.ndarray, ones: np.ndarray) -> np.ndarray:
+    x = np.where(ones, ~b, b).astype(np.uint32)
+    n = np.full(len(x), 32, np.uint32)
+    for s_ in range(31, -1, -1):
+        n = np.where((x >> s_) & 1, np.minimum(n, 31 - s_), n)
+    return n.astype(np.uint32)
+
+
+def events_from_list(add_events, bit_events, lt_events=(), sll_events=(), sr_events=(), clz_events=()):
     """Events given as the reference's AluEvent::new(pc, opcode, a, b, c) tuples (next_pc = pc + 4,
     crates/core/executor/src/events/instr.rs:31-33)."""
     def cols(evs):
         arr = np.asarray([(op, a, b, c, pc) for pc, op, a, b, c in evs], np.uint64).reshape(-1, 5)
         return tuple(arr[:, i].astype(np.uint32) for i in range(5))
     return {"add": cols(add_events), "bit": cols(bit_events), "lt": cols(lt_events), "sll": cols(sll_events),
-            "sr": cols(sr_events)}
+            "sr": cols(sr_events), "clz": cols(clz_events)}
 
 
-def alu_shard(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0, n_sr: int = 0):
+def alu_shard(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int = 0, n_sr: int = 0,
+              n_clz: int = 0):
     """(machine, prep_traces, traces, public_values) of one ALU-slice shard of random events."""
-    return alu_shard_from(alu_events(n_add, n_bit, seed, n_lt, n_sll, n_sr), seed)
+    return alu_shard_from(alu_events(n_add, n_bit, seed, n_lt, n_sll, n_sr, n_clz), seed)
 
 
 def _inv_table():
@@ -567,8 +631,42 @@ def alu_shard_from(ev, seed: int = 3):
             byte_lookup(B_U8RANGE, word[:, 2], word[:, 3])
         traces["ShiftLeft"] = t
 
+    # CloClz (alu/clo_clz/mod.rs:85-160); its SRL dependencies (executor/src/dependencies.rs:107-122)
+    # join the ShiftRight events with pc = UNUSED_PC
+    none = (np.zeros(0, np.uint32),) * 5
+    op, a, b, c, pc = ev.get("clz", none)
+    n_cz = len(op)
+    dep = none
+    if n_cz:
+        t = np.zeros((_pow2(n_cz), CZ_WIDTH), np.uint32)
+        t[:, CZ_A] = 32  # padding rows: clz(0) = 32
+        t[:, CZ_CLZ] = 1
+        t[:, CZ_BB_ZERO] = 1
+        clo = op == OP_CLO
+        bbv = np.where(clo, ~b, b).astype(np.uint32)
+        t[:n_cz, CZ_PC] = pc
+        t[:n_cz, CZ_NPC] = pc + 4
+        t[:n_cz, CZ_A:CZ_A + 4] = _bytes(a)
+        t[:n_cz, CZ_B:CZ_B + 4] = _bytes(b)
+        t[:n_cz, CZ_BB:CZ_BB + 4] = _bytes(bbv)
+        nz = bbv != 0
+        t[:n_cz, CZ_BB_ZERO] = ~nz
+        sh = np.where(nz, 31 - a.astype(np.int64), 0).astype(np.uint32)
+        sr1 = np.where(nz, bbv >> sh, 0).astype(np.uint32)
+        t[:n_cz, CZ_SR1:CZ_SR1 + 4] = _bytes(sr1)
+        t[:n_cz, CZ_CLZ], t[:n_cz, CZ_CLO] = ~clo, clo
+        t[:n_cz, CZ_REAL] = 1
+        bbb = _bytes(bbv)
+        byte_lookup(B_U8RANGE, bbb[:, 0], bbb[:, 1])
+        byte_lookup(B_U8RANGE, bbb[:, 2], bbb[:, 3])
+        byte_lookup(B_LTU, a, np.full(n_cz, 33))
+        traces["CloClz"] = t
+        nd = int(nz.sum())
+        dep = (np.full(nd, OP_SRL, np.uint32), sr1[nz], bbv[nz], sh[nz], np.full(nd, UNUSED_PC, np.uint32))
+
     # ShiftRight (alu/sr/mod.rs:220-325); padded rows: shift_by_n_bits[0] = shift_by_n_bytes[0] = 1
-    op, a, b, c, pc = ev.get("sr", (np.zeros(0, np.uint32),) * 5)
+    cpu_sr = ev.get("sr", none)
+    op, a, b, c, pc = (np.concatenate([cpu_sr[j], dep[j]]).astype(np.uint32) for j in range(5))
     n_sr = len(op)
     if n_sr:
         t = np.zeros((_pow2(n_sr), SR_WIDTH), np.uint32)
@@ -617,7 +715,7 @@ def alu_shard_from(ev, seed: int = 3):
         traces["ShiftRight"] = t
 
     # instruction source: the CPU's send_instruction tuple of every ALU event
-    kinds = [ev[k] for k in ("add", "bit", "lt", "sll", "sr") if k in ev]
+    kinds = [ev[k] for k in ("add", "bit", "lt", "sll", "sr", "clz") if k in ev]
     n = sum(len(e[0]) for e in kinds)
     t = np.zeros((_pow2(n), IS_WIDTH), np.uint32)
     t[:n, IS_PC] = np.concatenate([e[4] for e in kinds])
