@@ -58,7 +58,7 @@ def prove_resident(prover, dev_traces, pvs):
 
 
 STAGE_KERNEL = {"merkle_leaves": "k_hash_leaves", "merkle_nodes": "k_compress_level", "quotient": "zkm_quot_jit",
-                "fri_reduce": "k_fri_reduce", "perm_trace": "k_perm_rows", "open_eval": "k_open_dot"}
+                "fri_reduce": "k_fri_reduce", "perm_trace": "zkm_perm_jit", "open_eval": "k_open_dot"}
 
 
 def pmc_traffic(stage):
@@ -73,6 +73,25 @@ def pmc_traffic(stage):
     if "hbm_bytes_per_launch" not in d:
         return None, None
     return round(d["hbm_bytes_per_launch"]), os.path.basename(files[-1])
+
+
+def lde_measured_hbm():
+    """HBM-bandwidth utilisation of the LDE/NTT kernels (BASELINE north star: >= 40 %): PMC bytes
+    (2 x FETCH_SIZE + WRITE_SIZE per launch, the gfx950 correction of tools/pmc_summary.py) over the
+    kernels' measured durations, summed over every LDE kernel of the committed rocprofv3 profile."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None
+    byts = ms = 0.0
+    for k, v in json.load(open(files[-1]))["kernels"].items():
+        if ("ntt" in k or "lde" in k) and "hbm_bytes_per_launch" in v and "avg_ms" in v:
+            byts += v["hbm_bytes_per_launch"] * v["calls"]
+            ms += v["avg_ms"] * v["calls"]
+    if not ms:
+        return None
+    gbps = byts / (ms / 1e3) / 1e9
+    return {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBS, 4), "source": os.path.basename(files[-1])}
 
 
 VALU_PEAK_TSLOTS = 256 * 4 * 32 * 2.4e9 / 1e12  # CUs x SIMDs x SIMD-32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
@@ -120,8 +139,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--log-n", type=int, default=22)
     ap.add_argument("--workload", choices=["fib", "alu"], default="fib",
-                    help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Byte "
-                         "restated from the reference AIRs + CPU stand-in, zkmips_amd/mips_alu.py), 2^(log-n) "
+                    help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
+                         "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
+                         "zkmips_amd/mips_alu.py), 2^(log-n) "
                          "instructions per shard")
     ap.add_argument("--queries", type=int, default=84)
     ap.add_argument("--cpu-log-n", type=int, default=18)
@@ -269,6 +289,9 @@ def main():
         ntt = {"gf_ops_per_s": float(f"{rate:.4g}"), "hbm_roofline_gf_ops_per_s": float(f"{roof:.4g}"),
                "frac": round(rate / roof, 4), "algorithmic_GBps": round(lbytes / (lms / 1e3) / 1e9, 1),
                "launches": lcnt, "stage_ms_per_shard": round(lms / nprof, 3)}
+        meas = lde_measured_hbm()
+        if meas:
+            ntt["hbm_measured"] = meas
     stages = {k: {"count": v[0], "ms_per_shard": round(v[1] / nprof, 3)}
               for k, v in sorted(prof.items()) if not k.endswith("_perms") and not k.endswith("_gfops")}
 
