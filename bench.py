@@ -75,23 +75,28 @@ def pmc_traffic(stage):
     return round(d["hbm_bytes_per_launch"]), os.path.basename(files[-1])
 
 
-def lde_measured_hbm():
-    """HBM-bandwidth utilisation of the LDE/NTT kernels (BASELINE north star: >= 40 %): PMC bytes
-    (2 x FETCH_SIZE + WRITE_SIZE per launch, the gfx950 correction of tools/pmc_summary.py) over the
-    kernels' measured durations, summed over every LDE kernel of the committed rocprofv3 profile."""
+def measured_hbm(match):
+    """HBM-bandwidth utilisation of a kernel family (BASELINE north star: NTT and quotient achieved
+    HBM GB/s): PMC bytes (2 x FETCH_SIZE + WRITE_SIZE per launch, the gfx950 correction of
+    tools/pmc_summary.py) over the kernels' measured durations, summed over every kernel whose name
+    satisfies `match` in the committed rocprofv3 profile."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not files:
         return None
     byts = ms = 0.0
     for k, v in json.load(open(files[-1]))["kernels"].items():
-        if ("ntt" in k or "lde" in k) and "hbm_bytes_per_launch" in v and "avg_ms" in v:
+        if match(k) and "hbm_bytes_per_launch" in v and "avg_ms" in v:
             byts += v["hbm_bytes_per_launch"] * v["calls"]
             ms += v["avg_ms"] * v["calls"]
     if not ms:
         return None
     gbps = byts / (ms / 1e3) / 1e9
     return {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBS, 4), "source": os.path.basename(files[-1])}
+
+
+def lde_measured_hbm():
+    return measured_hbm(lambda k: "ntt" in k or "lde" in k)
 
 
 VALU_PEAK_TSLOTS = 256 * 4 * 32 * 2.4e9 / 1e12  # CUs x SIMDs x SIMD-32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
@@ -292,6 +297,9 @@ def main():
         meas = lde_measured_hbm()
         if meas:
             ntt["hbm_measured"] = meas
+    hbm_kernels = {name: measured_hbm(lambda k, p=pat: k == p)
+                   for name, pat in (("quotient", "zkm_quot_jit"), ("logup_trace", "zkm_perm_jit"),
+                                     ("fri_reduce", "k_fri_reduce"), ("openings", "k_open_dot"))}
     stages = {k: {"count": v[0], "ms_per_shard": round(v[1] / nprof, 3)}
               for k, v in sorted(prof.items()) if not k.endswith("_perms") and not k.endswith("_gfops")}
 
@@ -323,6 +331,7 @@ def main():
         "pcie_inclusive_rows_per_s": round(rows_per_shard / pcie_s, 1),
         "roofline": roofline,
         "ntt": ntt,
+        "hbm_measured": {k: v for k, v in hbm_kernels.items() if v},
         "stages_ms_per_shard": stages,
         "profiled_region": f"{nprof} single-shard proofs after the timed region (stages, roofline, ntt, serial_ms_per_shard)",
     }
