@@ -143,11 +143,12 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--log-n", type=int, default=22)
-    ap.add_argument("--workload", choices=["fib", "alu"], default="fib",
+    ap.add_argument("--workload", choices=["fib", "alu", "core"], default="fib",
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
                          "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
                          "zkmips_amd/mips_alu.py), 2^(log-n) "
-                         "instructions per shard")
+                         "instructions per shard; core: Cpu + Program chips over the ALU slice "
+                         "(zkmips_amd/mips_core.py), 3/4 * 2^(log-n) straight-line instructions, Cpu 2^(log-n) rows")
     ap.add_argument("--queries", type=int, default=84)
     ap.add_argument("--cpu-log-n", type=int, default=18)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -183,8 +184,14 @@ def main():
     n = 1 << args.log_n
     K = max(1, args.inflight)
     shards = []
+    core = None
+    if args.workload == "core":  # one program (one proving key); its trace is generated once and proven K times
+        from zkmips_amd import mips_core as MC
+        core = MC.core_shard(3 * n // 4, seed=1)
     for k in range(K):
-        if args.workload == "alu":
+        if core is not None:
+            m, prep, traces_k, pvs_k = core
+        elif args.workload == "alu":
             from zkmips_amd import mips_alu as A
             m, prep, traces_k, pvs_k = A.alu_shard(n // 4, n // 4, seed=1000 + rank * K + k, n_lt=n // 4,
                                                    n_sll=n // 8, n_sr=n // 16, n_clz=n // 16)
@@ -322,6 +329,10 @@ def main():
         "config": {"workload": (f"S-SHARD FibCpu 2^{args.log_n} rows (main 67, LogUp 11 EF, quotient 2) + FibTable "
                                 f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard")
                    if args.workload == "fib" else
+                   (f"MIPS core shard: Cpu 2^{args.log_n} (main 67, LogUp 11 EF) + Program 2^{args.log_n} (prep 14) "
+                    f"+ AddSub, Bitwise, Lt, ShiftLeft, ShiftRight, CloClz + Byte 2^16 + RegisterState: "
+                    f"{3 * n // 4} instructions, full commit+open per shard")
+                   if args.workload == "core" else
                    (f"MIPS ALU slice: InstrSource 2^{args.log_n} + AddSub, Bitwise, Lt 2^{args.log_n - 2} + ShiftLeft, "
                     f"ShiftRight (CPU + CloClz SRLs) 2^{args.log_n - 3} + CloClz 2^{args.log_n - 4} + Byte 2^16 "
                     f"(prep 12): full commit+open per shard"),

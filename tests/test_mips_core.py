@@ -1,0 +1,124 @@
+"""MIPS core shard: the reference's Cpu and Program chips (zkmips_amd/mips_core.py) on top of the ALU
+slice, with the register-memory argument closed by the RegisterState stand-in.
+
+CPU part: the trace satisfies every constraint and every lookup balances (direct evaluation,
+tests/_air_check.py); the oracle proves it and its verifier accepts; forged ALU results, register
+values, timestamps, pcs and program rows are rejected.  GPU part: the HIP prover's proofs are
+byte-identical to the oracle's, and a shard whose Cpu chip has 2^22 rows (the §8 "Cpu-shaped chip"
+at the bench height) verifies."""
+import numpy as np
+import pytest
+
+from tests import _air_check
+from tests import _oracle as O
+from zkmips_amd import mips_alu as A
+from zkmips_amd import mips_core as C
+
+
+@pytest.fixture(scope="module")
+def shard():
+    return C.core_shard(700, seed=4)
+
+
+@pytest.fixture(scope="module")
+def oracle(shard):
+    m, prep, _, _ = shard
+    return O.OracleProver(m, prep, num_queries=16)
+
+
+def test_core_chip_shapes(shard):
+    m, prep, tr, pv = shard
+    cpu = m.chips[m.chip_index("Cpu")]
+    # cpu/columns/mod.rs: 67 main columns; 21 local lookups -> 11 EF permutation columns (§8 "Cpu-shaped")
+    assert cpu.main_width == 67 and cpu.perm_width_ef == 11 and cpu.log_quotient_degree == 1
+    assert tr["Cpu"].shape == (1024, 67) and prep["Program"].shape == (1024, 14)
+    assert tr["Program"][:700].all() and not tr["Program"][700:].any()
+    assert tr["Cpu"][699, C.C_REAL] == 1 and tr["Cpu"][700, C.C_REAL] == 0
+
+
+@pytest.mark.parametrize("n,seed", [(1, 2), (17, 3), (700, 4), (5000, 5)])
+def test_core_trace_satisfies_air(n, seed):
+    bad, unbalanced = _air_check.check(*C.core_shard(n, seed=seed))
+    assert bad == [] and unbalanced == []
+
+
+def test_core_shard_proves_and_verifies(shard, oracle):
+    _, _, tr, pv = shard
+    rc, proof = oracle.prove(tr, pv)
+    assert rc == 0 and oracle.verify(proof) == 0
+
+
+def _tamper(tr, what):
+    bad = {k: v.copy() for k, v in tr.items()}
+    t = bad["Cpu"]
+    if what == "alu_result":  # the CPU claims a result the ALU chips never produced
+        t[10, C.C_A_VAL] = (int(t[10, C.C_A_VAL]) + 1) % 256
+    elif what == "register_read":  # a forged register value read by op_b
+        t[20, C.C_B_ACC + C.ACC_VALUE] ^= 1
+    elif what == "timestamp":  # an access whose previous timestamp is after the current one
+        t[30, C.C_B_ACC + C.ACC_PREV_CLK] += 7
+    elif what == "pc":
+        t[40, C.C_NPC] += 4
+    elif what == "program":  # the executed instruction is not the committed program's
+        t[50, C.C_OPC] = (int(t[50, C.C_OPC]) + 1) % 256
+    elif what == "register_final":
+        bad["RegisterState"][5, C.RS_FIN_VAL] ^= 1
+    elif what == "clk":
+        t[60, C.C_CLK16] += 1
+    return bad
+
+
+@pytest.mark.parametrize("what", ["alu_result", "register_read", "timestamp", "pc", "program", "register_final",
+                                  "clk"])
+def test_core_tamper_rejected(shard, oracle, what):
+    m, prep, tr, pv = shard
+    bad = _tamper(tr, what)
+    assert _air_check.check(m, prep, bad, pv) != ([], [])
+    rc, proof = oracle.prove(bad, pv)
+    assert rc == 0
+    assert oracle.verify(proof) != 0
+
+
+def test_core_register_chain(shard):
+    """Every register's first access reads the initial value the RegisterState row receives and its
+    last access is what that row sends (the memory argument closes inside the shard)."""
+    _, _, tr, _ = shard
+    rs = tr["RegisterState"]
+    assert list(rs[:, C.RS_ADDR]) == list(range(32))
+    assert (rs[:, C.RS_FIN_CLK] <= 5 * 699 + C.POS_A).all() and rs[0, C.RS_INIT_VAL:C.RS_INIT_VAL + 4].sum() == 0
+
+
+# ---------------------------------------------------------------- GPU parity
+@pytest.fixture(scope="module")
+def dev():
+    from zkmips_amd._lib import Device
+    d = Device(0)
+    yield d
+    d.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed", [(17, 3), (700, 4), (20000, 6), (1 << 17, 7)])
+def test_core_gpu_proof_bytes_identical(dev, n, seed):
+    from zkmips_amd.prover import HipProver
+    m, prep, tr, pv = C.core_shard(n, seed=seed)
+    gpu = HipProver(dev, m, prep, num_queries=16)
+    cpu = O.OracleProver(m, prep, num_queries=16)
+    assert np.array_equal(gpu.vk_commit, cpu.commit)
+    proof = gpu.prove_shard(tr, pv)
+    rc, ref = cpu.prove(tr, pv)
+    assert rc == 0 and proof == ref
+    assert cpu.verify(proof) == 0
+
+
+@pytest.mark.gpu
+def test_core_gpu_full_size_verifies(dev):
+    from zkmips_amd.prover import HipProver
+    n = (1 << 21) + 12345
+    m, prep, tr, pv = C.core_shard(n, seed=11)
+    assert tr["Cpu"].shape == (1 << 22, 67)
+    gpu = HipProver(dev, m, prep, num_queries=84)
+    cpu = O.OracleProver(m, prep, num_queries=84)
+    proof = gpu.prove_shard(tr, pv)
+    assert cpu.verify(proof) == 0
+    assert cpu.verify(gpu.prove_shard(_tamper(tr, "register_read"), pv)) != 0

@@ -93,7 +93,10 @@ def pv(i: int) -> Expr:
 
 IS_FIRST = Expr([OP_IS_FIRST], 1)
 IS_LAST = Expr([OP_IS_LAST], 1)
-IS_TRANSITION = Expr([OP_IS_TRANS], 1)
+# Plonky3 SymbolicExpression::degree_multiple: IsFirstRow / IsLastRow count 1, IsTransition 0 (the
+# reference's CpuChip has when_transition().when(next).when_not(next) constraints of degree 3 under
+# its blowup-2 config, which only holds with a degree-0 transition selector)
+IS_TRANSITION = Expr([OP_IS_TRANS], 0)
 
 
 @dataclass

@@ -494,12 +494,44 @@ def _inv_table():
     return np.asarray([pow(x % P, P - 2, P) if x else 0 for x in range(-255, 256)], np.uint64)
 
 
+def byte_lookup_into(mult: np.ndarray):
+    """Accumulator of Byte-chip multiplicities (bytes/trace.rs:40-70: row b * 256 + c, U16Range at a1)."""
+    def byte_lookup(op, b, c, m=1):
+        idx = ((np.asarray(b).astype(np.int64) << 8) + np.asarray(c).astype(np.int64)).ravel()
+        if np.ndim(m) == 0:
+            mult[:, op] += np.bincount(idx, minlength=BYTE_ROWS).astype(np.uint64) * np.uint64(m)
+        else:
+            w = np.broadcast_to(np.asarray(m, np.int64), np.shape(idx))
+            mult[:, op] += np.bincount(idx, weights=w, minlength=BYTE_ROWS).astype(np.uint64)
+    return byte_lookup
+
+
 def alu_shard_from(ev, seed: int = 3):
     mult = np.zeros((BYTE_ROWS, BYTE_MULT_WIDTH), np.uint64)
+    traces = alu_traces(ev, mult)
 
-    def byte_lookup(op, b, c, m=1):
-        np.add.at(mult[:, op], (np.asarray(b).astype(np.int64) << 8) + np.asarray(c).astype(np.int64), m)
+    # instruction source: the CPU's send_instruction tuple of every ALU event
+    kinds = [ev[k] for k in ("add", "bit", "lt", "sll", "sr", "clz") if k in ev]
+    n = sum(len(e[0]) for e in kinds)
+    t = np.zeros((_pow2(n), IS_WIDTH), np.uint32)
+    t[:n, IS_PC] = np.concatenate([e[4] for e in kinds])
+    t[:n, IS_NPC] = t[:n, IS_PC] + 4
+    t[:n, IS_OP] = np.concatenate([e[0] for e in kinds])
+    for base, j in ((IS_A, 1), (IS_B, 2), (IS_C, 3)):
+        t[:n, base:base + 4] = _bytes(np.concatenate([e[j] for e in kinds]))
+    t[:n, IS_REAL] = 1
+    traces = {"InstrSource": t, **traces}
 
+    assert mult.max() < P
+    traces["Byte"] = mult.astype(np.uint32)
+    pvs = (splitmix64(0xA1B1000 + seed, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
+    return alu_machine(), {"Byte": byte_prep_trace()}, traces, pvs
+
+
+def alu_traces(ev, mult: np.ndarray) -> dict:
+    """Traces of the ALU chips that have events in `ev` ({kind: (opcode, a, b, c, pc)}); their Byte
+    lookups are added to `mult`."""
+    byte_lookup = byte_lookup_into(mult)
     traces = {}
     # AddSub (event_to_row, add_sub/mod.rs:149-163; AddOperation::populate, add.rs:21-52)
     op, a, b, c, pc = ev["add"]
@@ -714,19 +746,4 @@ def alu_shard_from(ev, seed: int = 3):
                 byte_lookup(B_U8RANGE, word[:, k], word[:, k + 1])
         traces["ShiftRight"] = t
 
-    # instruction source: the CPU's send_instruction tuple of every ALU event
-    kinds = [ev[k] for k in ("add", "bit", "lt", "sll", "sr", "clz") if k in ev]
-    n = sum(len(e[0]) for e in kinds)
-    t = np.zeros((_pow2(n), IS_WIDTH), np.uint32)
-    t[:n, IS_PC] = np.concatenate([e[4] for e in kinds])
-    t[:n, IS_NPC] = t[:n, IS_PC] + 4
-    t[:n, IS_OP] = np.concatenate([e[0] for e in kinds])
-    for base, j in ((IS_A, 1), (IS_B, 2), (IS_C, 3)):
-        t[:n, base:base + 4] = _bytes(np.concatenate([e[j] for e in kinds]))
-    t[:n, IS_REAL] = 1
-    traces = {"InstrSource": t, **traces}
-
-    assert mult.max() < P
-    traces["Byte"] = mult.astype(np.uint32)
-    pvs = (splitmix64(0xA1B1000 + seed, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
-    return alu_machine(), {"Byte": byte_prep_trace()}, traces, pvs
+    return traces
