@@ -1,11 +1,12 @@
-"""MIPS core shard: the reference's Cpu and Program chips (zkmips_amd/mips_core.py) on top of the ALU
-slice, with the register-memory argument closed by the RegisterState stand-in.
+"""MIPS core shard: the reference's Cpu, Program and Branch chips (zkmips_amd/mips_core.py) on top of
+the ALU slice, with the register-memory argument closed by the RegisterState stand-in.
 
 CPU part: the trace satisfies every constraint and every lookup balances (direct evaluation,
 tests/_air_check.py); the oracle proves it and its verifier accepts; forged ALU results, register
-values, timestamps, pcs and program rows are rejected.  GPU part: the HIP prover's proofs are
-byte-identical to the oracle's, and a shard whose Cpu chip has 2^22 rows (the §8 "Cpu-shaped chip"
-at the bench height) verifies."""
+values, timestamps, pcs, program rows and branch decisions are rejected.  Programs are straight-line
+code and counted loops with forward branches of all six kinds (delay slots as the executor runs them).
+GPU part: the HIP prover's proofs are byte-identical to the oracle's, and shards whose Cpu chip has
+2^22 rows (the §8 "Cpu-shaped chip" at the bench height) verify."""
 import numpy as np
 import pytest
 
@@ -79,6 +80,83 @@ def test_core_tamper_rejected(shard, oracle, what):
     assert oracle.verify(proof) != 0
 
 
+def _branch_kinds_program():
+    """Every branch kind on a positive, a negative and a zero operand (BEQ/BNE on equal and unequal
+    registers), each followed by its delay slot and one instruction it skips when taken."""
+    prog = [(A.OP_ADD, 1, 0, 5, 0, 1), (A.OP_ADD, 2, 0, C.M32 - 4, 0, 1), (A.OP_ADD, 6, 0, 5, 0, 1)]
+    for op in C.BRANCH_OPS:
+        for rs, rt in ((1, 6), (2, 1), (0, 0)):
+            if op in (C.OP_BEQ, C.OP_BNE):
+                prog.append((op, rs, rt, 8, 0, 1))  # target = next_pc + 8
+            else:
+                prog.append((op, rs, 0, 8, 1, 1))
+            prog.append((A.OP_ADD, 4, 4, 1, 0, 1))  # delay slot: always runs
+            prog.append((A.OP_ADD, 5, 5, 1, 0, 1))  # skipped when taken
+    # offset 0 targets the delay slot itself: it runs twice, the first time with next_pc == pc
+    prog += [(C.OP_BEQ, 0, 0, 0, 0, 1), (A.OP_ADD, 7, 7, 3, 0, 1)]
+    return prog
+
+
+def test_branch_kinds():
+    prog = _branch_kinds_program()
+    m, prep, tr, pv = C.program_shard(prog, seed=2)
+    br = tr["Branch"]
+    assert br.shape == (32, C.BR_WIDTH)
+    taken = list(br[:18, C.BR_BRANCHING])
+    # (5, 5), (-5, 5), (0, 0) per kind in BRANCH_OPS order: BEQ, BGEZ, BGTZ, BLEZ, BLTZ, BNE
+    assert taken == [1, 0, 1,  1, 0, 1,  1, 0, 0,  0, 1, 1,  0, 1, 0,  0, 1, 0]
+    assert list(br[:18, C.BR_LT]) == [0, 1, 0] * 6 and list(br[:18, C.BR_GT]) == [0, 0, 0] + [1, 0, 0] * 4 + [0, 0, 0]
+    cpu = tr["Cpu"]
+    n = int(cpu[:, C.C_REAL].sum())
+    assert n == 3 + 18 * 3 - sum(taken) + 3
+    assert br[18, C.BR_BRANCHING] == 1 and list(cpu[n - 2:n, C.C_PC]) == [cpu[n - 3, C.C_PC] + 4] * 2
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+@pytest.mark.parametrize("body,iters,seed", [(4, 3, 1), (12, 7, 1), (40, 25, 2), (60, 40, 3)])
+def test_loop_trace_satisfies_air(body, iters, seed):
+    m, prep, tr, pv = C.loop_shard(body, iters, seed)
+    assert int(tr["Program"][C.loop_program(body, iters, seed).__len__() - 2, 0]) == iters  # the bne ran iters times
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+
+
+@pytest.fixture(scope="module")
+def loop():
+    return C.loop_shard(40, 25, seed=2)
+
+
+def test_loop_shard_proves_and_verifies(loop):
+    m, prep, tr, pv = loop
+    o = O.OracleProver(m, prep, num_queries=16)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+@pytest.mark.parametrize("what", ["flip_taken", "target", "lt_flag", "delay_slot_npc"])
+def test_branch_tamper_rejected(loop, what):
+    m, prep, tr, pv = loop
+    bad = {k: v.copy() for k, v in tr.items()}
+    br = bad["Branch"]
+    if what == "flip_taken":  # claims the branch was not taken (next_next_pc unchanged)
+        i = int(np.nonzero(br[:, C.BR_BRANCHING])[0][0])
+        br[i, C.BR_BRANCHING] = 0
+    elif what == "target":
+        br[3, C.BR_TGT] ^= 4
+    elif what == "lt_flag":
+        br[5, C.BR_LT] ^= 1
+    else:  # the CPU continues somewhere else after a taken branch's delay slot
+        cpu = bad["Cpu"]
+        i = int(np.nonzero(cpu[:, C.C_SEQ] == 0)[0][0]) + 1
+        cpu[i, C.C_NPC] += 4
+    assert _air_check.check(m, prep, bad, pv) != ([], [])
+    o = O.OracleProver(m, prep, num_queries=16)
+    rc, proof = o.prove(bad, pv)
+    assert rc == 0 and o.verify(proof) != 0
+
+
 def test_core_register_chain(shard):
     """Every register's first access reads the initial value the RegisterState row receives and its
     last access is what that row sends (the memory argument closes inside the shard)."""
@@ -109,6 +187,33 @@ def test_core_gpu_proof_bytes_identical(dev, n, seed):
     rc, ref = cpu.prove(tr, pv)
     assert rc == 0 and proof == ref
     assert cpu.verify(proof) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("body,iters,seed", [(12, 7, 1), (40, 300, 2), (60, 4000, 3)])
+def test_loop_gpu_proof_bytes_identical(dev, body, iters, seed):
+    from zkmips_amd.prover import HipProver
+    m, prep, tr, pv = C.loop_shard(body, iters, seed)
+    gpu = HipProver(dev, m, prep, num_queries=16)
+    cpu = O.OracleProver(m, prep, num_queries=16)
+    assert np.array_equal(gpu.vk_commit, cpu.commit)
+    proof = gpu.prove_shard(tr, pv)
+    rc, ref = cpu.prove(tr, pv)
+    assert rc == 0 and proof == ref
+    assert cpu.verify(proof) == 0
+
+
+@pytest.mark.gpu
+def test_loop_gpu_full_size_verifies(dev):
+    from zkmips_amd.prover import HipProver
+    m, prep, tr, pv = C.loop_shard(60, 40000, seed=5)
+    assert tr["Cpu"].shape == (1 << 22, 67)
+    gpu = HipProver(dev, m, prep, num_queries=84)
+    cpu = O.OracleProver(m, prep, num_queries=84)
+    assert cpu.verify(gpu.prove_shard(tr, pv)) == 0
+    bad = {k: v.copy() for k, v in tr.items()}
+    bad["Branch"][777, C.BR_LT] ^= 1
+    assert cpu.verify(gpu.prove_shard(bad, pv)) != 0
 
 
 @pytest.mark.gpu

@@ -529,12 +529,16 @@ def alu_shard_from(ev, seed: int = 3):
 
 
 def alu_traces(ev, mult: np.ndarray) -> dict:
-    """Traces of the ALU chips that have events in `ev` ({kind: (opcode, a, b, c, pc)}); their Byte
+    """Traces of the ALU chips that have events in `ev` ({kind: (opcode, a, b, c, pc[, next_pc])}); their Byte
     lookups are added to `mult`."""
     byte_lookup = byte_lookup_into(mult)
+    # events may carry their next_pc (AluEvent::next_pc: a delay-slot instruction after a taken branch
+    # continues at the target); without it next_pc = pc + 4
+    ev = {k: tuple(e[:5]) + ((e[5] if len(e) > 5 else (np.asarray(e[4]) + 4).astype(np.uint32)),)
+          for k, e in ev.items()}
     traces = {}
     # AddSub (event_to_row, add_sub/mod.rs:149-163; AddOperation::populate, add.rs:21-52)
-    op, a, b, c, pc = ev["add"]
+    op, a, b, c, pc, npc = ev["add"]
     n_add = len(op)
     if n_add:
         sub = op == OP_SUB
@@ -542,7 +546,7 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
         val = ((op1.astype(np.uint64) + c) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
         t = np.zeros((_pow2(n_add), AS_WIDTH), np.uint32)
         t[:n_add, AS_PC] = pc
-        t[:n_add, AS_NPC] = pc + 4
+        t[:n_add, AS_NPC] = npc
         t[:n_add, AS_VAL:AS_VAL + 4] = _bytes(val)
         x, y = _bytes(op1), _bytes(c)
         prev = np.zeros(n_add, np.uint32)
@@ -559,12 +563,12 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
         traces["AddSub"] = t
 
     # Bitwise (bitwise/mod.rs:140-171): one byte lookup per limb
-    op, a, b, c, pc = ev["bit"]
+    op, a, b, c, pc, npc = ev["bit"]
     n_bit = len(op)
     if n_bit:
         t = np.zeros((_pow2(n_bit), BW_WIDTH), np.uint32)
         t[:n_bit, BW_PC] = pc
-        t[:n_bit, BW_NPC] = pc + 4
+        t[:n_bit, BW_NPC] = npc
         ab, bb, cb = _bytes(a), _bytes(b), _bytes(c)
         t[:n_bit, BW_A:BW_A + 4] = ab
         t[:n_bit, BW_B:BW_B + 4] = bb
@@ -579,14 +583,14 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
         traces["Bitwise"] = t
 
     # Lt (alu/lt/mod.rs:179-263)
-    op, a, b, c, pc = ev["lt"]
+    op, a, b, c, pc, npc = ev["lt"]
     n_lt = len(op)
     if n_lt:
         t = np.zeros((_pow2(n_lt), LT_WIDTH), np.uint32)
         ab, bb, cb = _bytes(a), _bytes(b), _bytes(c)
         slt = op == OP_SLT
         t[:n_lt, LT_PC] = pc
-        t[:n_lt, LT_NPC] = pc + 4
+        t[:n_lt, LT_NPC] = npc
         t[:n_lt, LT_A:LT_A + 4] = ab
         t[:n_lt, LT_B:LT_B + 4] = bb
         t[:n_lt, LT_C:LT_C + 4] = cb
@@ -623,7 +627,7 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
 
     # ShiftLeft (alu/sll/mod.rs:200-260); padded rows: shift_by_n_bits[0] = shift_by_n_bytes[0] =
     # bit_shift_multiplier = 1 (:142-155)
-    op, a, b, c, pc = ev["sll"]
+    op, a, b, c, pc, npc = ev["sll"]
     n_sll = len(op)
     if n_sll:
         t = np.zeros((_pow2(n_sll), SL_WIDTH), np.uint32)
@@ -632,7 +636,7 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
         t[:, SL_MULT] = 1
         bb = _bytes(b)
         t[:n_sll, SL_PC] = pc
-        t[:n_sll, SL_NPC] = pc + 4
+        t[:n_sll, SL_NPC] = npc
         t[:n_sll, SL_A:SL_A + 4] = _bytes(a)
         t[:n_sll, SL_B:SL_B + 4] = bb
         t[:n_sll, SL_C:SL_C + 4] = _bytes(c)
@@ -665,8 +669,8 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
 
     # CloClz (alu/clo_clz/mod.rs:85-160); its SRL dependencies (executor/src/dependencies.rs:107-122)
     # join the ShiftRight events with pc = UNUSED_PC
-    none = (np.zeros(0, np.uint32),) * 5
-    op, a, b, c, pc = ev.get("clz", none)
+    none = (np.zeros(0, np.uint32),) * 6
+    op, a, b, c, pc, npc = ev.get("clz", none)
     n_cz = len(op)
     dep = none
     if n_cz:
@@ -677,7 +681,7 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
         clo = op == OP_CLO
         bbv = np.where(clo, ~b, b).astype(np.uint32)
         t[:n_cz, CZ_PC] = pc
-        t[:n_cz, CZ_NPC] = pc + 4
+        t[:n_cz, CZ_NPC] = npc
         t[:n_cz, CZ_A:CZ_A + 4] = _bytes(a)
         t[:n_cz, CZ_B:CZ_B + 4] = _bytes(b)
         t[:n_cz, CZ_BB:CZ_BB + 4] = _bytes(bbv)
@@ -694,18 +698,19 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
         byte_lookup(B_LTU, a, np.full(n_cz, 33))
         traces["CloClz"] = t
         nd = int(nz.sum())
-        dep = (np.full(nd, OP_SRL, np.uint32), sr1[nz], bbv[nz], sh[nz], np.full(nd, UNUSED_PC, np.uint32))
+        dep = (np.full(nd, OP_SRL, np.uint32), sr1[nz], bbv[nz], sh[nz], np.full(nd, UNUSED_PC, np.uint32),
+               np.full(nd, UNUSED_PC + DEFAULT_PC_INC, np.uint32))
 
     # ShiftRight (alu/sr/mod.rs:220-325); padded rows: shift_by_n_bits[0] = shift_by_n_bytes[0] = 1
     cpu_sr = ev.get("sr", none)
-    op, a, b, c, pc = (np.concatenate([cpu_sr[j], dep[j]]).astype(np.uint32) for j in range(5))
+    op, a, b, c, pc, npc = (np.concatenate([cpu_sr[j], dep[j]]).astype(np.uint32) for j in range(6))
     n_sr = len(op)
     if n_sr:
         t = np.zeros((_pow2(n_sr), SR_WIDTH), np.uint32)
         t[:, SR_NBITS] = 1
         t[:, SR_NBYTES] = 1
         t[:n_sr, SR_PC] = pc
-        t[:n_sr, SR_NPC] = pc + 4
+        t[:n_sr, SR_NPC] = npc
         t[:n_sr, SR_A:SR_A + 4] = _bytes(a)
         bb = _bytes(b)
         t[:n_sr, SR_B:SR_B + 4] = bb

@@ -20,7 +20,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import mips_alu as A
-from .machine import (ChipDesc, IS_FIRST, IS_LAST, IS_TRANSITION, KIND_BYTE, KIND_INSTRUCTION, KIND_MEMORY,
+from .machine import (ChipDesc, Expr, IS_FIRST, IS_LAST, IS_TRANSITION, KIND_BYTE, KIND_INSTRUCTION, KIND_MEMORY,
                       KIND_PROGRAM, Lookup, MachineDesc, P, VirtualPairCol as V, main, main_next, pv)
 from .workloads import NUM_PV_ELTS, PROOF_MAX_NUM_PVS, splitmix64
 
@@ -169,15 +169,119 @@ def register_state_chip() -> ChipDesc:
     return ch
 
 
+# ---------------------------------------------------------------- Branch (control_flow/branch)
+OP_BEQ, OP_BGEZ, OP_BGTZ, OP_BLEZ, OP_BLTZ, OP_BNE = 21, 22, 23, 24, 25, 26  # executor/src/opcode.rs:39-44
+BRANCH_OPS = (OP_BEQ, OP_BGEZ, OP_BGTZ, OP_BLEZ, OP_BLTZ, OP_BNE)
+# BranchColumns (control_flow/branch/columns.rs:11-61); a KoalaBearWordRangeChecker is 8 bits of the
+# top byte + 6 running products (operations/koala_bear_word.rs:11-31)
+RC_WIDTH = 14
+BR_PC, BR_NPC, BR_NPC_RC, BR_TGT, BR_NNPC, BR_NNPC_RC = 0, 1, 5, 19, 23, 27
+BR_A, BR_B, BR_C = 41, 45, 49
+BR_BEQ, BR_BNE, BR_BLTZ, BR_BLEZ, BR_BGTZ, BR_BGEZ = range(53, 59)
+BR_BRANCHING, BR_GT, BR_LT = 59, 60, 61
+BR_WIDTH = 62
+
+
+def _word_range_check(ch, value, rc, is_real):
+    """KoalaBearWordRangeChecker::range_check (operations/koala_bear_word.rs:54-115): the word is a
+    canonical field element (top byte < 0x7F, or == 0x7F with zero lower bytes)."""
+    M = main
+    bits = [M(rc + i) for i in range(8)]
+    rec = Expr.lift(0)
+    for i, b in enumerate(bits):
+        _assert_bool(ch, b, is_real)
+        rec = rec + (1 << i) * b
+    ch.assert_zero(is_real * (rec - M(value + 3)))
+    ch.assert_zero(is_real * bits[7])
+    ch.assert_zero(is_real * (M(rc + 8) - bits[0] * bits[1]))
+    for k in range(1, 6):
+        ch.assert_zero(is_real * (M(rc + 8 + k) - M(rc + 7 + k) * bits[k + 1]))
+    ch.assert_zero(is_real * M(rc + 13) * (M(value) + M(value + 1) + M(value + 2)))
+
+
+def _send_alu(ch, opcode, a, b, c, mult):
+    """send_alu (stark/src/air/builder.rs:282-323): an Instruction lookup at UNUSED_PC."""
+    vals = [ZERO, ZERO, V.const(A.UNUSED_PC), V.const(A.UNUSED_PC + A.DEFAULT_PC_INC),
+            V.const(A.UNUSED_PC + 2 * A.DEFAULT_PC_INC), ZERO, V.const(opcode)]
+    vals += list(a) + list(b) + list(c) + [ZERO] * 4 + [ZERO, ZERO, ZERO, ZERO, V.const(1)]
+    ch.sends.append(Lookup(vals, mult, KIND_INSTRUCTION))
+
+
+def branch_chip() -> ChipDesc:
+    """BranchChip::eval (control_flow/branch/air.rs:27-210), constraints and lookups in its order."""
+    ch = ChipDesc("Branch", prep_width=0, main_width=BR_WIDTH, local_only=True)
+    M = main
+    order = (BR_BEQ, BR_BNE, BR_BLTZ, BR_BGEZ, BR_BLEZ, BR_BGTZ)
+    for col in order:
+        _assert_bool(ch, M(col))
+    is_real = M(BR_BEQ) + M(BR_BNE) + M(BR_BLTZ) + M(BR_BGEZ) + M(BR_BLEZ) + M(BR_BGTZ)
+    _assert_bool(ch, is_real)
+    real_v = V([("main", col, 1) for col in order])
+    opcode = V([("main", BR_BEQ, OP_BEQ), ("main", BR_BNE, OP_BNE), ("main", BR_BLTZ, OP_BLTZ),
+                ("main", BR_BGEZ, OP_BGEZ), ("main", BR_BLEZ, OP_BLEZ), ("main", BR_BGTZ, OP_BGTZ)])
+    red_v = lambda base: V([("main", base + i, 1 << (8 * i)) for i in range(4)])
+    red = lambda base: sum((M(base + i) * (1 << (8 * i)) for i in range(1, 4)), M(base))
+    ins = [ZERO, ZERO, _m(BR_PC), red_v(BR_NPC), red_v(BR_NNPC), ZERO, opcode]
+    ins += _vword(BR_A) + _vword(BR_B) + _vword(BR_C) + [ZERO] * 4 + [V.const(1), ZERO, ZERO, ZERO, ZERO]
+    ch.receives.append(Lookup(ins, real_v, KIND_INSTRUCTION))
+    _word_range_check(ch, BR_NPC, BR_NPC_RC, is_real)
+    _word_range_check(ch, BR_NNPC, BR_NNPC_RC, is_real)
+    br = M(BR_BRANCHING)
+    _send_alu(ch, A.OP_ADD, _vword(BR_TGT), _vword(BR_NPC), _vword(BR_C), _m(BR_BRANCHING))
+    ch.assert_zero(is_real * (1 - br) * (red(BR_NPC) + 4 - red(BR_NNPC)))
+    not_br = V([("main", col, 1) for col in order] + [("main", BR_BRANCHING, P - 1)])
+    for base in (BR_NPC, BR_NNPC):
+        for k in (0, 2):
+            ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, _m(base + k), _m(base + k + 1)], not_br,
+                                   KIND_BYTE))
+    for i in range(4):
+        ch.assert_zero(is_real * br * (M(BR_TGT + i) - M(BR_NNPC + i)))
+    ch.assert_zero((1 - is_real) * br)
+    _assert_bool(ch, br, is_real)
+    gt, lt = M(BR_GT), M(BR_LT)
+    beq, bne, bltz, blez, bgtz, bgez = (M(c) for c in (BR_BEQ, BR_BNE, BR_BLTZ, BR_BLEZ, BR_BGTZ, BR_BGEZ))
+    ch.assert_zero(beq * br * (gt + lt))
+    ch.assert_zero(beq * (1 - br) * (gt + lt - 1))
+    ch.assert_zero(bne * br * (gt + lt - 1))
+    ch.assert_zero(bne * (1 - br) * (gt + lt))
+    ch.assert_zero(bltz * br * (lt - 1))
+    ch.assert_zero(bltz * (1 - br) * lt)
+    ch.assert_zero(blez * br * gt)
+    ch.assert_zero(blez * (1 - br) * (gt - 1))
+    ch.assert_zero(bgtz * br * (gt - 1))
+    ch.assert_zero(bgtz * (1 - br) * gt)
+    ch.assert_zero(bgez * br * lt)
+    ch.assert_zero(bgez * (1 - br) * (lt - 1))
+    _send_alu(ch, A.OP_SLT, [_m(BR_LT), ZERO, ZERO, ZERO], _vword(BR_A), _vword(BR_B), real_v)
+    _send_alu(ch, A.OP_SLT, [_m(BR_GT), ZERO, ZERO, ZERO], _vword(BR_B), _vword(BR_A), real_v)
+    return ch
+
+
+def _range_checker_cols(v: np.ndarray) -> np.ndarray:
+    """KoalaBearWordRangeChecker::populate (operations/koala_bear_word.rs:34-52)."""
+    bits = ((v[:, None].astype(np.uint64) >> (24 + np.arange(8, dtype=np.uint64))) & 1).astype(np.uint32)
+    out = np.zeros((len(v), RC_WIDTH), np.uint32)
+    out[:, :8] = bits
+    acc = bits[:, 0] * bits[:, 1]
+    out[:, 8] = acc
+    for k in range(1, 6):
+        acc = acc * bits[:, k + 1]
+        out[:, 8 + k] = acc
+    return out
+
+
 def core_machine() -> MachineDesc:
-    # MipsAir::chips order (crates/core/machine/src/mips/mod.rs): Program, Cpu, ALUs, ..., Byte, memory
-    return MachineDesc([program_chip(), cpu_chip(), A.add_sub_chip(), A.bitwise_chip(), A.lt_chip(),
-                        A.shift_left_chip(), A.shift_right_chip(), A.clo_clz_chip(), A.byte_chip(),
+    # MipsAir::chips order (crates/core/machine/src/mips/mod.rs:207-431): Cpu, Program, ALUs, Branch, ...,
+    # Byte; the memory stand-in last
+    return MachineDesc([cpu_chip(), program_chip(), A.add_sub_chip(), A.bitwise_chip(), A.shift_right_chip(),
+                        A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), A.byte_chip(),
                         register_state_chip()], NUM_PV_ELTS)
 
 
 # ---------------------------------------------------------------- program + execution
-# (opcode, uses immediate c) mix of straight-line ALU code
+# An instruction is (opcode, op_a, op_b, op_c, imm_b, imm_c) at pc = PC_BASE + 4 * index
+# (Instruction::new, executor/src/instruction.rs; branches: op_a = rs, op_b = rt or immediate 0,
+# op_c = sign-extended offset << 2, instruction.rs:405-475).
 _MIX = [(A.OP_ADD, 0), (A.OP_ADD, 1), (A.OP_SUB, 0), (A.OP_AND, 0), (A.OP_AND, 1), (A.OP_OR, 0), (A.OP_OR, 1),
         (A.OP_XOR, 0), (A.OP_XOR, 1), (A.OP_NOR, 0), (A.OP_SLT, 0), (A.OP_SLT, 1), (A.OP_SLTU, 0),
         (A.OP_SLL, 1), (A.OP_SRL, 1), (A.OP_SRA, 1), (A.OP_ROR, 1), (A.OP_SRL, 0), (A.OP_CLZ, 1), (A.OP_CLO, 1)]
@@ -185,6 +289,10 @@ _KIND = {A.OP_ADD: "add", A.OP_SUB: "add", A.OP_AND: "bit", A.OP_OR: "bit", A.OP
          A.OP_SLT: "lt", A.OP_SLTU: "lt", A.OP_SLL: "sll", A.OP_SRL: "sr", A.OP_SRA: "sr", A.OP_ROR: "sr",
          A.OP_CLZ: "clz", A.OP_CLO: "clz"}
 M32 = 0xFFFFFFFF
+
+
+def _s32(x):
+    return x - (1 << 32) if x >> 31 else x
 
 
 def _alu(op, b, c):
@@ -201,7 +309,7 @@ def _alu(op, b, c):
     if op == A.OP_NOR:
         return ~(b | c) & M32
     if op == A.OP_SLT:
-        return int((b - (1 << 32) if b >> 31 else b) < (c - (1 << 32) if c >> 31 else c))
+        return int(_s32(b) < _s32(c))
     if op == A.OP_SLTU:
         return int(b < c)
     s = c & 31
@@ -210,117 +318,210 @@ def _alu(op, b, c):
     if op == A.OP_SRL:
         return b >> s
     if op == A.OP_SRA:
-        return ((b - (1 << 32) if b >> 31 else b) >> s) & M32
+        return (_s32(b) >> s) & M32
     if op == A.OP_ROR:
         return ((b >> s) | (b << (32 - s))) & M32 if s else b
     x = b if op == A.OP_CLZ else ~b & M32
     return 32 - x.bit_length()
 
 
+def _taken(op, a, b):
+    """Executor::execute_branch (executor/src/executor.rs:2098-2120)."""
+    if op == OP_BEQ:
+        return a == b
+    if op == OP_BNE:
+        return a != b
+    sa = _s32(a)
+    return {OP_BGEZ: sa >= 0, OP_BLEZ: sa <= 0, OP_BGTZ: sa > 0, OP_BLTZ: sa < 0}[op]
+
+
+def _random_alu(r, avoid=()):
+    """One random ALU instruction from 5 random words (destination never in `avoid`)."""
+    op, imm = _MIX[int(r[0] % len(_MIX))]
+    regs = [x for x in range(32) if x not in avoid]
+    ra = 0 if (r[4] % 16 == 0 and 0 not in avoid) else regs[1 + int(r[1] % (len(regs) - 1))]
+    rb = int(r[2] % 32)
+    if op in (A.OP_CLZ, A.OP_CLO):
+        c = 0
+    elif imm and op in (A.OP_SLL, A.OP_SRL, A.OP_SRA, A.OP_ROR):
+        c = int(r[3] % 32)
+    elif imm:
+        c = int(r[3] & np.uint64(M32))
+    else:
+        c = int(r[3] % 32)
+    return (op, ra, rb, c, 0, imm)
+
+
 def random_program(n: int, seed: int = 1):
-    """n straight-line ALU instructions: (opcode, op_a, op_b, op_c, imm_c); register 0 is written now and
-    then (the write is dropped, op_a_0)."""
+    """n straight-line ALU instructions; register 0 is written now and then (the write is dropped,
+    op_a_0)."""
     r = splitmix64(0xC0DE000 + seed, 5 * n + 5)
-    prog = []
-    for i in range(n):
-        op, imm = _MIX[int(r[5 * i] % len(_MIX))]
-        ra = int(r[5 * i + 1] % 32) if r[5 * i + 4] % 16 == 0 else 1 + int(r[5 * i + 1] % 31)
-        rb = int(r[5 * i + 2] % 32)
-        if op in (A.OP_CLZ, A.OP_CLO):
-            c = 0
-        elif imm and op in (A.OP_SLL, A.OP_SRL, A.OP_SRA, A.OP_ROR):
-            c = int(r[5 * i + 3] % 32)
-        elif imm:
-            c = int(r[5 * i + 3] & np.uint64(M32))
-        else:
-            c = int(r[5 * i + 3] % 32)
-        prog.append((op, ra, rb, c, imm))
+    return [_random_alu(r[5 * i:5 * i + 5]) for i in range(n)]
+
+
+COUNTER = 3  # loop counter register of loop_program
+
+
+def loop_program(body: int, iters: int, seed: int = 1):
+    """A counted loop (the shape of examples/fibonacci's guest loop):
+
+        r3 = r0 + iters
+      L: <body: random ALU instructions and forward branches of all six kinds>
+        r3 = r3 + (-1)
+        bne r3, r0, L
+        <delay slot: one ALU instruction>
+
+    Forward branches skip 0..2 instructions past their delay slot and never leave the body; no
+    branch sits in a delay slot."""
+    assert body >= 4 and 0 < iters < (1 << 31)
+    r = splitmix64(0xB0D1000 + seed, 6 * body + 12)
+    prog = [(A.OP_ADD, COUNTER, 0, iters, 0, 1)]
+    k = 0
+    while k < body:
+        w = r[6 * k:6 * k + 6]
+        j = len(prog)  # index of this instruction; the body ends at 1 + body
+        room = (1 + body) - (j + 2)  # instructions after the delay slot left in the body
+        if w[5] % 5 == 0 and room >= 0 and k + 1 < body:
+            op = BRANCH_OPS[int(w[0] % 6)]
+            skip = int(w[3] % 3) if room >= 2 else int(w[3] % (room + 1))
+            rs = int(w[1] % 32)
+            off = 4 * (skip + 1)  # target = next_pc + off: `skip` instructions past the delay slot
+            if op in (OP_BEQ, OP_BNE):
+                prog.append((op, rs, int(w[2] % 8), off, 0, 1))  # low registers: equal now and then
+            else:
+                prog.append((op, rs, 0, off, 1, 1))
+            k += 1
+            prog.append(_random_alu(r[6 * k:6 * k + 5], avoid=(COUNTER,)))  # delay slot
+            k += 1
+            continue
+        prog.append(_random_alu(w[:5], avoid=(COUNTER,)))
+        k += 1
+    prog.append((A.OP_ADD, COUNTER, COUNTER, M32, 0, 1))
+    back = (1 - (len(prog) + 1)) * 4  # target = pc(L) = next_pc + c, next_pc = pc of the delay slot
+    prog.append((OP_BNE, COUNTER, 0, back & M32, 0, 1))
+    prog.append(_random_alu(r[6 * body + 6:6 * body + 11], avoid=(COUNTER,)))
     return prog
 
 
-def core_shard(n: int, seed: int = 1, shard: int = 1):
-    """(machine, prep_traces, traces, public_values) of one shard executing an n-instruction
-    straight-line program once (n < 2^24 / 5: the CPU clk is range-checked to 24 bits)."""
-    assert 0 < n and 5 * n + 5 < (1 << 24)
-    prog = random_program(n, seed)
+def _execute(prog, regs, shard, max_steps):
+    """Runs `prog` from PC_BASE until pc leaves it (delay slots: pc <- next_pc, next_pc <- next_next_pc).
+    Returns the per-step records, the ALU/Branch events in execution order (the instruction's own
+    event, then the dependencies emit_branch_dependencies adds, executor/src/dependencies.rs:175-224),
+    and each register's last (shard, timestamp)."""
+    end = PC_BASE + 4 * len(prog)
+    last = [(0, 0)] * 32
+    pc, npc = PC_BASE, PC_BASE + 4
+    steps = []
+    ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
+    branches = []
+    U = A.UNUSED_PC
+    while pc != end:
+        assert PC_BASE <= pc < end and len(steps) < max_steps
+        k = (pc - PC_BASE) >> 2
+        op, ra, rb, c, immb, immc = prog[k]
+        clk = 5 * len(steps)
+        acc = []
+        if immc:
+            cv = c
+            acc.append(None)
+        else:
+            acc.append(last[c])
+            last[c] = (shard, clk + POS_C)
+            cv = regs[c]
+        if immb:
+            bv = rb
+            acc.append(None)
+        else:
+            acc.append(last[rb])
+            last[rb] = (shard, clk + POS_B)
+            bv = regs[rb]
+        prev_a = regs[ra]
+        if op in BRANCH_OPS:
+            av = written = prev_a
+            taken = _taken(op, prev_a, bv)
+            nnpc = (npc + cv) & M32 if taken else npc + 4
+            branches.append((pc, op, av, bv, cv, npc, nnpc, taken))
+            ev["lt"].append((A.OP_SLT, int(_s32(av) < _s32(bv)), av, bv, U, U + 4))
+            ev["lt"].append((A.OP_SLT, int(_s32(av) > _s32(bv)), bv, av, U, U + 4))
+            if taken:
+                ev["add"].append((A.OP_ADD, nnpc, npc, cv, U, U + 4))
+        else:
+            av = _alu(op, bv, cv)
+            written = av if ra else 0
+            if ra:
+                regs[ra] = av
+            nnpc = npc + 4
+            ev[_KIND[op]].append((op, av, bv, cv, pc, npc))
+        acc.append(last[ra])
+        last[ra] = (shard, clk + POS_A)
+        steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc))
+        pc, npc = npc, nnpc
+    return steps, ev, branches, last
+
+
+def _ev_arrays(lst):
+    arr = np.asarray(lst, np.uint64).reshape(-1, 6)
+    return tuple(arr[:, i].astype(np.uint32) for i in range(6))
+
+
+def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24) // 5 - 1):
+    """(machine, prep_traces, traces, public_values) of one shard executing `prog` from PC_BASE to its end
+    (at most max_steps instructions: the CPU clk is range-checked to 24 bits)."""
     init = splitmix64(0x5EED000 + seed, 32) & np.uint64(M32)
     regs = [0] + [int(x) for x in init[1:]]
     init_vals = list(regs)
-    last = [(0, 0)] * 32  # (shard, timestamp) of each register's previous access
+    steps, ev, branches, last = _execute(prog, regs, shard, max_steps)
+    n = len(steps)
+    assert n > 0
     height = max(16, 1 << (n - 1).bit_length())
     t = np.zeros((height, CPU_WIDTH), np.uint32)
     t[n:, C_IMMB] = 1
     t[n:, C_IMMC] = 1
     t[n:, C_RW_A] = 1
-    rows = {k: [] for k in ("op", "a", "b", "c", "pc")}
-    acc = np.zeros((n, 3, 4), np.int64)  # per access (C, B, A): prev_shard, prev_clk, compare, diff
-    vals = np.zeros((n, 6), np.int64)  # a, b, c, prev_a, written a, executed? (unused)
-    for i, (op, ra, rb, c, imm) in enumerate(prog):
-        clk = 5 * i
-        if not imm:
-            ps, pc_ = last[c]
-            acc[i, 0] = (ps, pc_, ps == shard, 0)
-            last[c] = (shard, clk + POS_C)
-            cv = regs[c]
-        else:
-            cv = c
-        ps, pc_ = last[rb]
-        acc[i, 1] = (ps, pc_, ps == shard, 0)
-        last[rb] = (shard, clk + POS_B)
-        bv = regs[rb]
-        av = _alu(op, bv, cv)
-        ps, pc_ = last[ra]
-        acc[i, 2] = (ps, pc_, ps == shard, 0)
-        last[ra] = (shard, clk + POS_A)
-        prev_a = regs[ra]
-        written = av if ra else 0
-        if ra:
-            regs[ra] = av
-        vals[i] = (av, bv, cv, prev_a, written, 0)
-        rows["op"].append(op)
-        rows["pc"].append(PC_BASE + 4 * i)
-    ops = np.asarray(rows["op"], np.uint32)
-    pcs = np.asarray(rows["pc"], np.uint32)
-    av, bv, cv, prev_a, written = (vals[:, j].astype(np.uint32) for j in range(5))
+    S = np.asarray([s_[:11] for s_ in steps], np.int64)
+    ks, ops = S[:, 0], S[:, 1].astype(np.uint32)
+    av, bv, cv, prev_a, written = (S[:, j].astype(np.uint32) for j in range(2, 7))
+    npc, nnpc, immb, immc = S[:, 7], S[:, 8], S[:, 9].astype(bool), S[:, 10].astype(bool)
+    P_ = np.asarray(prog, np.int64).reshape(-1, 6)
+    pcs = (PC_BASE + 4 * ks).astype(np.uint32)
     clk = 5 * np.arange(n, dtype=np.int64)
-    immc = np.asarray([p[4] for p in prog], np.uint32)
-    opa = np.asarray([p[1] for p in prog], np.uint32)
-    opb = np.asarray([p[2] for p in prog], np.uint32)
-    opc = np.asarray([p[3] for p in prog], np.uint32)
+    is_branch = np.isin(ops, BRANCH_OPS)
 
     mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
     byte_lookup = A.byte_lookup_into(mult)
+    instr_cols = np.zeros((len(prog), C_IMMC + 1 - C_OPCODE), np.uint32)  # InstructionCols
+    instr_cols[:, 0] = P_[:, 0]
+    instr_cols[:, C_OPA - C_OPCODE] = P_[:, 1]
+    instr_cols[:, C_OPB - C_OPCODE:C_OPB - C_OPCODE + 4] = A._bytes(P_[:, 2].astype(np.uint32))
+    instr_cols[:, C_OPC - C_OPCODE:C_OPC - C_OPCODE + 4] = A._bytes(P_[:, 3].astype(np.uint32))
+    instr_cols[:, C_OPA0 - C_OPCODE] = P_[:, 1] == 0
+    instr_cols[:, C_IMMB - C_OPCODE] = P_[:, 4]
+    instr_cols[:, C_IMMC - C_OPCODE] = P_[:, 5]
     t[:n, C_SHARD] = shard
     t[:n, C_CLK16] = clk & 0xFFFF
     t[:n, C_CLK8] = (clk >> 16) & 0xFF
     t[:n, C_PC] = pcs
-    t[:n, C_NPC] = pcs + 4
-    t[:n, C_NNPC] = pcs + 8
-    t[:n, C_OPCODE] = ops
-    t[:n, C_OPA] = opa
-    t[:n, C_OPB:C_OPB + 4] = A._bytes(opb)
-    t[:n, C_OPC:C_OPC + 4] = A._bytes(opc)
-    t[:n, C_OPA0] = opa == 0
-    t[:n, C_IMMB] = 0
-    t[:n, C_IMMC] = immc
+    t[:n, C_NPC] = npc
+    t[:n, C_NNPC] = nnpc
+    t[:n, C_OPCODE:C_IMMC + 1] = instr_cols[ks]
     t[:n, C_RW_A] = 0
-    t[:n, C_SEQ] = 1
+    t[:n, C_SEQ] = ~is_branch
+    t[:n, C_A_IMM] = is_branch
     t[:n, C_A_VAL:C_A_VAL + 4] = A._bytes(av)
     t[:n, C_REAL] = 1
     byte_lookup(A.B_U16RANGE, np.full(n, shard >> 8), np.full(n, shard & 0xFF))  # U16Range(shard): row a1
     byte_lookup(A.B_U16RANGE, (clk & 0xFFFF) >> 8, clk & 0xFF)
     byte_lookup(A.B_U8RANGE, np.zeros(n, np.int64), (clk >> 16) & 0xFF)
-    for j, (base, value, pos, mask) in enumerate(((C_C_ACC, cv, POS_C, immc == 0), (C_B_ACC, bv, POS_B, None),
-                                                   (C_A_ACC + 4, written, POS_A, None))):
-        sel = np.ones(n, bool) if mask is None else mask
+    for j, (base, value, pos, sel) in enumerate(((C_C_ACC, cv, POS_C, ~immc), (C_B_ACC, bv, POS_B, ~immb),
+                                                 (C_A_ACC + 4, written, POS_A, np.ones(n, bool)))):
+        prev = np.asarray([a_[11][j] if a_[11][j] is not None else (0, 0) for a_ in steps], np.int64).reshape(-1, 2)
         t[:n, base + ACC_VALUE:base + ACC_VALUE + 4] = A._bytes(value)  # value always (cpu/trace.rs:151-152)
-        t[:n, base + ACC_PREV_SHARD] = np.where(sel, acc[:, j, 0], 0)
-        t[:n, base + ACC_PREV_CLK] = np.where(sel, acc[:, j, 1], 0)
-        comp = acc[:, j, 2].astype(bool)
+        t[:n, base + ACC_PREV_SHARD] = np.where(sel, prev[:, 0], 0)
+        t[:n, base + ACC_PREV_CLK] = np.where(sel, prev[:, 1], 0)
+        comp = prev[:, 0] == shard
         t[:n, base + ACC_COMPARE] = sel & comp
         cur = np.where(comp, clk + pos, shard)
-        prev = np.where(comp, acc[:, j, 1], acc[:, j, 0])
-        d = (cur - prev - 1).astype(np.int64)
+        d = cur - np.where(comp, prev[:, 1], prev[:, 0]) - 1
         assert (d[sel] >= 0).all() and (d[sel] < (1 << 24)).all()
         d = np.where(sel, d, 0)
         t[:n, base + ACC_D16] = d & 0xFFFF
@@ -332,22 +533,18 @@ def core_shard(n: int, seed: int = 1, shard: int = 1):
     byte_lookup(A.B_U8RANGE, wb[:, 0], wb[:, 1])
     byte_lookup(A.B_U8RANGE, wb[:, 2], wb[:, 3])
 
-    # ALU chips from the executed instructions (the CPU sends them, the ALU chips receive them)
-    ev = {}
-    kind_of = np.asarray([_KIND.get(o, "") for o in range(max(_KIND) + 1)])[ops]
-    for kind in ("add", "bit", "lt", "sll", "sr", "clz"):
-        s = kind_of == kind
-        ev[kind] = (ops[s], av[s], bv[s], cv[s], pcs[s])
     traces = {"Cpu": t}
-    traces.update(A.alu_traces(ev, mult))
+    traces.update(A.alu_traces({k: _ev_arrays(v) for k, v in ev.items()}, mult))
+    if branches:
+        traces["Branch"] = _branch_trace(branches, byte_lookup)
 
-    # Program: one row per instruction, executed once
-    ph = max(16, 1 << (n - 1).bit_length())
+    # Program: one row per instruction, multiplicity = executions
+    ph = max(16, 1 << (len(prog) - 1).bit_length())
     prep = np.zeros((ph, PROG_PREP_WIDTH), np.uint32)
-    prep[:n, 0] = pcs
-    prep[:n, 1:PROG_PREP_WIDTH] = t[:n, C_OPCODE:C_IMMC + 1]
+    prep[:len(prog), 0] = PC_BASE + 4 * np.arange(len(prog))
+    prep[:len(prog), 1:PROG_PREP_WIDTH] = instr_cols
     pm = np.zeros((ph, 1), np.uint32)
-    pm[:n, 0] = 1
+    pm[:len(prog), 0] = np.bincount(ks, minlength=len(prog))
     traces["Program"] = pm
 
     rs = np.zeros((32, RS_WIDTH), np.uint32)
@@ -363,7 +560,49 @@ def core_shard(n: int, seed: int = 1, shard: int = 1):
     traces["Byte"] = mult.astype(np.uint32)
     pvs = (splitmix64(0xC0DE100 + seed, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
     pvs[PV_START_PC] = PC_BASE
-    pvs[PV_NEXT_PC] = PC_BASE + 4 * n
+    pvs[PV_NEXT_PC] = PC_BASE + 4 * len(prog)
     pvs[PV_EXECUTION_SHARD] = shard
     prep_traces = {"Program": prep, "Byte": A.byte_prep_trace()}
     return core_machine(), prep_traces, traces, pvs
+
+
+def _branch_trace(branches, byte_lookup):
+    """BranchChip::event_to_row (control_flow/branch/trace.rs:85-130)."""
+    B = np.asarray(branches, np.int64).reshape(-1, 8)
+    nb = len(B)
+    t = np.zeros((A._pow2(nb), BR_WIDTH), np.uint32)
+    op, a, b, c, npc, nnpc, taken = (B[:, j] for j in range(1, 8))
+    t[:nb, BR_PC] = B[:, 0]
+    for col, code in ((BR_BEQ, OP_BEQ), (BR_BNE, OP_BNE), (BR_BLTZ, OP_BLTZ), (BR_BGTZ, OP_BGTZ),
+                      (BR_BLEZ, OP_BLEZ), (BR_BGEZ, OP_BGEZ)):
+        t[:nb, col] = op == code
+    t[:nb, BR_A:BR_A + 4] = A._bytes(a.astype(np.uint32))
+    t[:nb, BR_B:BR_B + 4] = A._bytes(b.astype(np.uint32))
+    t[:nb, BR_C:BR_C + 4] = A._bytes(c.astype(np.uint32))
+    sa, sb = a.astype(np.uint32).view(np.int32), b.astype(np.uint32).view(np.int32)
+    t[:nb, BR_LT] = sa < sb
+    t[:nb, BR_GT] = sa > sb
+    t[:nb, BR_NPC:BR_NPC + 4] = A._bytes(npc.astype(np.uint32))
+    t[:nb, BR_TGT:BR_TGT + 4] = A._bytes(((npc + c) & M32).astype(np.uint32))
+    t[:nb, BR_NNPC:BR_NNPC + 4] = A._bytes(nnpc.astype(np.uint32))
+    t[:nb, BR_NPC_RC:BR_NPC_RC + RC_WIDTH] = _range_checker_cols(npc.astype(np.uint32))
+    t[:nb, BR_NNPC_RC:BR_NNPC_RC + RC_WIDTH] = _range_checker_cols(nnpc.astype(np.uint32))
+    t[:nb, BR_BRANCHING] = taken
+    nt = taken == 0
+    for v in (npc[nt], nnpc[nt]):
+        w = A._bytes(v.astype(np.uint32))
+        byte_lookup(A.B_U8RANGE, w[:, 0], w[:, 1])
+        byte_lookup(A.B_U8RANGE, w[:, 2], w[:, 3])
+    return t
+
+
+def core_shard(n: int, seed: int = 1, shard: int = 1):
+    """One shard executing an n-instruction straight-line program once (n < 2^24 / 5)."""
+    assert 0 < n and 5 * n + 5 < (1 << 24)
+    return program_shard(random_program(n, seed), seed, shard)
+
+
+def loop_shard(body: int, iters: int, seed: int = 1, shard: int = 1):
+    """One shard executing loop_program(body, iters): iters * (body + 3) + 1 instructions plus the
+    forward branches' skips."""
+    return program_shard(loop_program(body, iters, seed), seed, shard)
