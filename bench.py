@@ -147,7 +147,7 @@ def main():
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
                          "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
                          "zkmips_amd/mips_alu.py), 2^(log-n) "
-                         "instructions per shard; core: Cpu + Program + Branch chips over the ALU slice "
+                         "instructions per shard; core: Cpu + Program + Branch + Jump chips over the ALU slice "
                          "(zkmips_amd/mips_core.py) running a counted loop, Cpu 2^(log-n) rows")
     ap.add_argument("--queries", type=int, default=84)
     ap.add_argument("--cpu-log-n", type=int, default=18)
@@ -187,7 +187,7 @@ def main():
     core = None
     if args.workload == "core":  # one program (one proving key); its trace is generated once and proven K times
         from zkmips_amd import mips_core as MC
-        core = MC.loop_shard(60, (3 * n // 4) // 63, seed=1)
+        core = MC.loop_shard(60, (3 * n // 4) // 104, seed=1)  # ~98 instructions per iteration
     for k in range(K):
         if core is not None:
             m, prep, traces_k, pvs_k = core
@@ -329,10 +329,11 @@ def main():
         "config": {"workload": (f"S-SHARD FibCpu 2^{args.log_n} rows (main 67, LogUp 11 EF, quotient 2) + FibTable "
                                 f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard")
                    if args.workload == "fib" else
-                   (f"MIPS core shard: a counted loop (60-instruction body of ALU ops and forward branches) "
+                   (f"MIPS core shard: a counted loop (60-instruction body of ALU ops, forward branches, jal/jalr calls "
+                    f"of a subroutine, bal) "
                     f"executed to {int(traces['Cpu'][:, 65].sum())} instructions: Cpu 2^{args.log_n} (main 67, "
                     f"LogUp 11 EF) + Program (prep 14) + AddSub, Bitwise, Lt, ShiftLeft, ShiftRight, CloClz, "
-                    f"Branch + Byte 2^16 (prep 12) + RegisterState: full commit+open per shard")
+                    f"Branch, Jump + Byte 2^16 (prep 12) + RegisterState: full commit+open per shard")
                    if args.workload == "core" else
                    (f"MIPS ALU slice: InstrSource 2^{args.log_n} + AddSub, Bitwise, Lt 2^{args.log_n - 2} + ShiftLeft, "
                     f"ShiftRight (CPU + CloClz SRLs) 2^{args.log_n - 3} + CloClz 2^{args.log_n - 4} + Byte 2^16 "

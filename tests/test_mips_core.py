@@ -116,10 +116,40 @@ def test_branch_kinds():
     assert rc == 0 and o.verify(proof) == 0
 
 
+def test_jump_kinds():
+    """j, jal, jr, jalr and bal (the executor's Jumpi / Jump / JumpDirect), each with its delay slot."""
+    S = C.PC_BASE + 4 * 12
+    prog = [(A.OP_ADD, 30, 0, S, 0, 1),                    # 0: r30 = S
+            (C.OP_JUMPI, 31, S, 0, 1, 1),                  # 1: jal S
+            (A.OP_ADD, 4, 4, 1, 0, 1),                     # 2: delay slot
+            (C.OP_JUMP, 31, 30, 0, 0, 1),                  # 3: jalr r31, r30
+            (A.OP_ADD, 4, 4, 1, 0, 1),                     # 4: delay slot
+            (C.OP_JUMPDIRECT, 31, 8, 0, 1, 1),             # 5: bal +8 (skips 7)
+            (A.OP_ADD, 4, 4, 1, 0, 1),                     # 6: delay slot
+            (A.OP_ADD, 5, 5, 1, 0, 1),                     # 7: skipped
+            (C.OP_JUMPI, 0, C.PC_BASE + 4 * 16, 0, 1, 1),  # 8: j END
+            (A.OP_ADD, 4, 4, 1, 0, 1),                     # 9: delay slot
+            (A.OP_ADD, 5, 5, 1, 0, 1),                     # 10: skipped
+            (A.OP_ADD, 5, 5, 1, 0, 1),                     # 11: skipped
+            (A.OP_ADD, 6, 6, 7, 0, 1),                     # 12: S
+            (C.OP_JUMP, 0, 31, 0, 0, 1),                   # 13: jr r31
+            (A.OP_ADD, 6, 6, 1, 0, 1),                     # 14: delay slot
+            (A.OP_ADD, 5, 5, 1, 0, 1)]                     # 15: skipped
+    m, prep, tr, pv = C.program_shard(prog, seed=2)
+    j = tr["Jump"]
+    pcs = [int(x) for x in tr["Cpu"][tr["Cpu"][:, C.C_REAL] == 1, C.C_PC]]
+    assert [(p - C.PC_BASE) // 4 for p in pcs] == [0, 1, 2, 12, 13, 14, 3, 4, 12, 13, 14, 5, 6, 8, 9]
+    assert int(j[:, C.J_JUMP].sum()) == 3 and int(j[:, C.J_JUMPI].sum()) == 2 and int(j[:, C.J_JDIRECT].sum()) == 1
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
 @pytest.mark.parametrize("body,iters,seed", [(4, 3, 1), (12, 7, 1), (40, 25, 2), (60, 40, 3)])
 def test_loop_trace_satisfies_air(body, iters, seed):
     m, prep, tr, pv = C.loop_shard(body, iters, seed)
-    assert int(tr["Program"][C.loop_program(body, iters, seed).__len__() - 2, 0]) == iters  # the bne ran iters times
+    assert int(tr["Program"][body + 3, 0]) == iters  # the loop-closing bne ran iters times
     assert _air_check.check(m, prep, tr, pv) == ([], [])
 
 
@@ -135,7 +165,7 @@ def test_loop_shard_proves_and_verifies(loop):
     assert rc == 0 and o.verify(proof) == 0
 
 
-@pytest.mark.parametrize("what", ["flip_taken", "target", "lt_flag", "delay_slot_npc"])
+@pytest.mark.parametrize("what", ["flip_taken", "target", "lt_flag", "delay_slot_npc", "link", "jump_target"])
 def test_branch_tamper_rejected(loop, what):
     m, prep, tr, pv = loop
     bad = {k: v.copy() for k, v in tr.items()}
@@ -143,10 +173,17 @@ def test_branch_tamper_rejected(loop, what):
     if what == "flip_taken":  # claims the branch was not taken (next_next_pc unchanged)
         i = int(np.nonzero(br[:, C.BR_BRANCHING])[0][0])
         br[i, C.BR_BRANCHING] = 0
-    elif what == "target":
-        br[3, C.BR_TGT] ^= 4
+    elif what == "target":  # only constrained when the branch is taken (the ADD lookup's multiplicity)
+        i = int(np.nonzero(br[:, C.BR_BRANCHING])[0][1])
+        br[i, C.BR_TGT] ^= 4
     elif what == "lt_flag":
         br[5, C.BR_LT] ^= 1
+    elif what == "link":  # a jump-and-link that stores a wrong return address
+        bad["Jump"][2, C.J_A] += 4
+    elif what == "jump_target":  # j / jal / jr whose next_next_pc is not its target
+        j = bad["Jump"]
+        i = int(np.nonzero(j[:, C.J_JUMPI] + j[:, C.J_JUMP])[0][0])
+        j[i, C.J_NNPC] += 4
     else:  # the CPU continues somewhere else after a taken branch's delay slot
         cpu = bad["Cpu"]
         i = int(np.nonzero(cpu[:, C.C_SEQ] == 0)[0][0]) + 1
@@ -206,7 +243,7 @@ def test_loop_gpu_proof_bytes_identical(dev, body, iters, seed):
 @pytest.mark.gpu
 def test_loop_gpu_full_size_verifies(dev):
     from zkmips_amd.prover import HipProver
-    m, prep, tr, pv = C.loop_shard(60, 40000, seed=5)
+    m, prep, tr, pv = C.loop_shard(60, 30000, seed=5)
     assert tr["Cpu"].shape == (1 << 22, 67)
     gpu = HipProver(dev, m, prep, num_queries=84)
     cpu = O.OracleProver(m, prep, num_queries=84)

@@ -270,11 +270,64 @@ def _range_checker_cols(v: np.ndarray) -> np.ndarray:
     return out
 
 
+# ---------------------------------------------------------------- Jump (control_flow/jump)
+OP_JUMP, OP_JUMPI, OP_JUMPDIRECT = 27, 28, 29  # JR/JALR, J/JAL, BAL (executor/src/opcode.rs:45-47)
+JUMP_OPS = (OP_JUMP, OP_JUMPI, OP_JUMPDIRECT)
+# JumpColumns (control_flow/jump/columns.rs:9-37)
+J_PC, J_NPC, J_NPC_RC, J_NNPC, J_NNPC_RC, J_A, J_B, J_C = 0, 1, 5, 19, 23, 37, 41, 45
+J_JUMP, J_JUMPI, J_JDIRECT, J_A_RC = 49, 50, 51, 52
+J_WIDTH = 66
+
+
+def jump_chip() -> ChipDesc:
+    """JumpChip::eval (control_flow/jump/air.rs:19-115), constraints and lookups in its order."""
+    ch = ChipDesc("Jump", prep_width=0, main_width=J_WIDTH, local_only=True)
+    M = main
+    for col in (J_JUMP, J_JUMPI, J_JDIRECT):
+        _assert_bool(ch, M(col))
+    is_real = M(J_JUMP) + M(J_JUMPI) + M(J_JDIRECT)
+    _assert_bool(ch, is_real)
+    real_v = V([("main", J_JUMP, 1), ("main", J_JUMPI, 1), ("main", J_JDIRECT, 1)])
+    opcode = V([("main", J_JUMP, OP_JUMP), ("main", J_JUMPI, OP_JUMPI), ("main", J_JDIRECT, OP_JUMPDIRECT)])
+    red_v = lambda base: V([("main", base + i, 1 << (8 * i)) for i in range(4)])
+    red = lambda base: sum((M(base + i) * (1 << (8 * i)) for i in range(1, 4)), M(base))
+    ins = [ZERO, ZERO, _m(J_PC), red_v(J_NPC), red_v(J_NNPC), ZERO, opcode]
+    ins += _vword(J_A) + _vword(J_B) + _vword(J_C) + [ZERO] * 4 + [ZERO, ZERO, ZERO, ZERO, ZERO]
+    ch.receives.append(Lookup(ins, real_v, KIND_INSTRUCTION))
+    ch.assert_zero(is_real * (red(J_A) - (red(J_NPC) + 4)))
+    _word_range_check(ch, J_A, J_A_RC, is_real)
+    _word_range_check(ch, J_NPC, J_NPC_RC, is_real)
+    _word_range_check(ch, J_NNPC, J_NNPC_RC, is_real)
+    for i in range(4):
+        ch.assert_zero((M(J_JUMP) + M(J_JUMPI)) * (M(J_NNPC + i) - M(J_B + i)))
+    _send_alu(ch, A.OP_ADD, _vword(J_NNPC), _vword(J_NPC), _vword(J_B), _m(J_JDIRECT))
+    return ch
+
+
+def _jump_trace(jumps):
+    """JumpChip::event_to_row (control_flow/jump/trace.rs:83-102); no byte lookups."""
+    J = np.asarray(jumps, np.int64).reshape(-1, 7)
+    nj = len(J)
+    t = np.zeros((A._pow2(nj), J_WIDTH), np.uint32)
+    op = J[:, 1]
+    t[:nj, J_PC] = J[:, 0]
+    t[:nj, J_JUMP] = op == OP_JUMP
+    t[:nj, J_JUMPI] = op == OP_JUMPI
+    t[:nj, J_JDIRECT] = op == OP_JUMPDIRECT
+    for base, j in ((J_A, 2), (J_B, 3), (J_C, 4), (J_NPC, 5), (J_NNPC, 6)):
+        t[:nj, base:base + 4] = A._bytes(J[:, j].astype(np.uint32))
+    t[:nj, J_A_RC:J_A_RC + RC_WIDTH] = _range_checker_cols(J[:, 2].astype(np.uint32))
+    t[:nj, J_NPC_RC:J_NPC_RC + RC_WIDTH] = _range_checker_cols(J[:, 5].astype(np.uint32))
+    t[:nj, J_NNPC_RC:J_NNPC_RC + RC_WIDTH] = _range_checker_cols(J[:, 6].astype(np.uint32))
+    return t
+
+
 def core_machine() -> MachineDesc:
     # MipsAir::chips order (crates/core/machine/src/mips/mod.rs:207-431): Cpu, Program, ALUs, Branch, ...,
     # Byte; the memory stand-in last
     return MachineDesc([cpu_chip(), program_chip(), A.add_sub_chip(), A.bitwise_chip(), A.shift_right_chip(),
-                        A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), A.byte_chip(),
+                        A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(),
+                        A.byte_chip(),
                         register_state_chip()], NUM_PV_ELTS)
 
 
@@ -359,29 +412,43 @@ def random_program(n: int, seed: int = 1):
     return [_random_alu(r[5 * i:5 * i + 5]) for i in range(n)]
 
 
-COUNTER = 3  # loop counter register of loop_program
+COUNTER, TARGET, LINK = 3, 30, 31  # loop counter, call-target and link registers of loop_program
+_AVOID = (COUNTER, TARGET, LINK)
+SUB_LEN = 5  # subroutine: 3 ALU instructions, jr r31, delay slot
 
 
 def loop_program(body: int, iters: int, seed: int = 1):
-    """A counted loop (the shape of examples/fibonacci's guest loop):
+    """A counted loop (the shape of examples/fibonacci's guest loop) calling a subroutine:
 
         r3 = r0 + iters
-      L: <body: random ALU instructions and forward branches of all six kinds>
+        r30 = r0 + S
+      L: <body: random ALU instructions, forward branches of all six kinds (BEQ/BNE/BLTZ/BLEZ/BGTZ/BGEZ),
+          calls `jal S` / `jalr r31, r30`, and forward `bal` (link in r31)>
         r3 = r3 + (-1)
         bne r3, r0, L
-        <delay slot: one ALU instruction>
+        <delay slot>
+        j END
+        <delay slot>
+      S: <3 ALU instructions>
+        jr r31
+        <delay slot>
+      END:
 
     Forward branches skip 0..2 instructions past their delay slot and never leave the body; no
-    branch sits in a delay slot."""
+    branch or jump sits in a delay slot; ALU instructions never write r3, r30, r31."""
     assert body >= 4 and 0 < iters < (1 << 31)
-    r = splitmix64(0xB0D1000 + seed, 6 * body + 12)
-    prog = [(A.OP_ADD, COUNTER, 0, iters, 0, 1)]
+    r = splitmix64(0xB0D1000 + seed, 6 * body + 64)
+    n_total = 2 + body + 5 + SUB_LEN
+    sub_pc = PC_BASE + 4 * (2 + body + 5)
+    prog = [(A.OP_ADD, COUNTER, 0, iters, 0, 1), (A.OP_ADD, TARGET, 0, sub_pc, 0, 1)]
     k = 0
+    alu = lambda w: _random_alu(w, avoid=_AVOID)
     while k < body:
         w = r[6 * k:6 * k + 6]
-        j = len(prog)  # index of this instruction; the body ends at 1 + body
-        room = (1 + body) - (j + 2)  # instructions after the delay slot left in the body
-        if w[5] % 5 == 0 and room >= 0 and k + 1 < body:
+        j = len(prog)  # index of this instruction; the body ends at 2 + body
+        room = (2 + body) - (j + 2)  # instructions after the delay slot left in the body
+        kind = int(w[5] % 10)
+        if kind < 2 and room >= 0 and k + 1 < body:  # forward branch
             op = BRANCH_OPS[int(w[0] % 6)]
             skip = int(w[3] % 3) if room >= 2 else int(w[3] % (room + 1))
             rs = int(w[1] % 32)
@@ -391,15 +458,32 @@ def loop_program(body: int, iters: int, seed: int = 1):
             else:
                 prog.append((op, rs, 0, off, 1, 1))
             k += 1
-            prog.append(_random_alu(r[6 * k:6 * k + 5], avoid=(COUNTER,)))  # delay slot
+        elif kind == 2 and room >= 0 and k + 1 < body:  # bal: forward jump-and-link
+            skip = int(w[3] % 3) if room >= 2 else int(w[3] % (room + 1))
+            prog.append((OP_JUMPDIRECT, LINK, 4 * (skip + 1), 0, 1, 1))
+            k += 1
+        elif kind == 3 and k + 1 < body:  # jal S
+            prog.append((OP_JUMPI, LINK, sub_pc, 0, 1, 1))
+            k += 1
+        elif kind == 4 and k + 1 < body:  # jalr r31, r30
+            prog.append((OP_JUMP, LINK, TARGET, 0, 0, 1))
+            k += 1
+        else:
+            prog.append(alu(w[:5]))
             k += 1
             continue
-        prog.append(_random_alu(w[:5], avoid=(COUNTER,)))
+        prog.append(alu(r[6 * k:6 * k + 5]))  # delay slot
         k += 1
+    assert len(prog) == 2 + body
     prog.append((A.OP_ADD, COUNTER, COUNTER, M32, 0, 1))
-    back = (1 - (len(prog) + 1)) * 4  # target = pc(L) = next_pc + c, next_pc = pc of the delay slot
+    back = (2 - (len(prog) + 1)) * 4  # target = pc(L) = next_pc + c, next_pc = pc of the delay slot
     prog.append((OP_BNE, COUNTER, 0, back & M32, 0, 1))
-    prog.append(_random_alu(r[6 * body + 6:6 * body + 11], avoid=(COUNTER,)))
+    w = r[6 * body:]
+    prog.append(alu(w[0:5]))
+    prog.append((OP_JUMPI, 0, PC_BASE + 4 * n_total, 0, 1, 1))  # j END
+    prog.append(alu(w[5:10]))
+    prog += [alu(w[10:15]), alu(w[15:20]), alu(w[20:25]), (OP_JUMP, 0, LINK, 0, 0, 1), alu(w[25:30])]
+    assert len(prog) == n_total
     return prog
 
 
@@ -413,7 +497,7 @@ def _execute(prog, regs, shard, max_steps):
     pc, npc = PC_BASE, PC_BASE + 4
     steps = []
     ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
-    branches = []
+    branches, jumps = [], []
     U = A.UNUSED_PC
     while pc != end:
         assert PC_BASE <= pc < end and len(steps) < max_steps
@@ -445,6 +529,16 @@ def _execute(prog, regs, shard, max_steps):
             ev["lt"].append((A.OP_SLT, int(_s32(av) > _s32(bv)), bv, av, U, U + 4))
             if taken:
                 ev["add"].append((A.OP_ADD, nnpc, npc, cv, U, U + 4))
+        elif op in JUMP_OPS:
+            # execute_jump / execute_jumpi / execute_jump_direct (executor.rs:2122-2154): link = next_pc + 4
+            av = (npc + 4) & M32
+            written = av if ra else 0
+            if ra:
+                regs[ra] = av
+            nnpc = (npc + bv) & M32 if op == OP_JUMPDIRECT else bv
+            jumps.append((pc, op, av, bv, cv, npc, nnpc))
+            if op == OP_JUMPDIRECT:  # emit_jump_dependencies (dependencies.rs:230-248)
+                ev["add"].append((A.OP_ADD, nnpc, npc, bv, U, U + 4))
         else:
             av = _alu(op, bv, cv)
             written = av if ra else 0
@@ -456,7 +550,7 @@ def _execute(prog, regs, shard, max_steps):
         last[ra] = (shard, clk + POS_A)
         steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc))
         pc, npc = npc, nnpc
-    return steps, ev, branches, last
+    return steps, ev, branches, jumps, last
 
 
 def _ev_arrays(lst):
@@ -470,7 +564,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     init = splitmix64(0x5EED000 + seed, 32) & np.uint64(M32)
     regs = [0] + [int(x) for x in init[1:]]
     init_vals = list(regs)
-    steps, ev, branches, last = _execute(prog, regs, shard, max_steps)
+    steps, ev, branches, jumps, last = _execute(prog, regs, shard, max_steps)
     n = len(steps)
     assert n > 0
     height = max(16, 1 << (n - 1).bit_length())
@@ -486,6 +580,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     pcs = (PC_BASE + 4 * ks).astype(np.uint32)
     clk = 5 * np.arange(n, dtype=np.int64)
     is_branch = np.isin(ops, BRANCH_OPS)
+    is_seq = ~(is_branch | np.isin(ops, JUMP_OPS))
 
     mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
     byte_lookup = A.byte_lookup_into(mult)
@@ -505,7 +600,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     t[:n, C_NNPC] = nnpc
     t[:n, C_OPCODE:C_IMMC + 1] = instr_cols[ks]
     t[:n, C_RW_A] = 0
-    t[:n, C_SEQ] = ~is_branch
+    t[:n, C_SEQ] = is_seq
     t[:n, C_A_IMM] = is_branch
     t[:n, C_A_VAL:C_A_VAL + 4] = A._bytes(av)
     t[:n, C_REAL] = 1
@@ -537,6 +632,8 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     traces.update(A.alu_traces({k: _ev_arrays(v) for k, v in ev.items()}, mult))
     if branches:
         traces["Branch"] = _branch_trace(branches, byte_lookup)
+    if jumps:
+        traces["Jump"] = _jump_trace(jumps)
 
     # Program: one row per instruction, multiplicity = executions
     ph = max(16, 1 << (len(prog) - 1).bit_length())
