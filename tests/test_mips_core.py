@@ -1,4 +1,4 @@
-"""MIPS core shard: the reference's Cpu, Program and Branch chips (zkmips_amd/mips_core.py) on top of
+"""MIPS core shard: the reference's Cpu, Program, Branch, Jump and Mul chips (zkmips_amd/mips_core.py) on top of
 the ALU slice, with the register-memory argument closed by the RegisterState stand-in.
 
 CPU part: the trace satisfies every constraint and every lookup balances (direct evaluation,
@@ -199,8 +199,61 @@ def test_core_register_chain(shard):
     last access is what that row sends (the memory argument closes inside the shard)."""
     _, _, tr, _ = shard
     rs = tr["RegisterState"]
-    assert list(rs[:, C.RS_ADDR]) == list(range(32))
-    assert (rs[:, C.RS_FIN_CLK] <= 5 * 699 + C.POS_A).all() and rs[0, C.RS_INIT_VAL:C.RS_INIT_VAL + 4].sum() == 0
+    assert rs.shape[0] == 64 and list(rs[:C.NUM_REGS, C.RS_ADDR]) == list(range(C.NUM_REGS))  # + LO, HI
+    assert rs[:C.NUM_REGS, C.RS_REAL].all() and not rs[C.NUM_REGS:].any()
+    assert (rs[:, C.RS_FIN_CLK] <= 5 * 699 + C.POS_HI).all() and rs[0, C.RS_INIT_VAL:C.RS_INIT_VAL + 4].sum() == 0
+
+
+def _word(row, base):
+    return int(sum(int(row[base + i]) << (8 * i) for i in range(4)))
+
+
+def test_mul_kinds():
+    """MUL / MULT / MULTU on sign and carry edge cases; LO and HI end up in registers 32 and 33."""
+    vals = [(7, 6), (C.M32, C.M32), (C.M32 - 2, 5), (0x80000000, 0x80000000), (0x12345678, 0x9ABCDEF0), (0, C.M32)]
+    prog = []
+    for b, c in vals:
+        prog += [(A.OP_ADD, 1, 0, b, 0, 1), (A.OP_ADD, 2, 0, c, 0, 1)]
+        prog += [(C.OP_MUL, 3, 1, 2, 0, 0), (C.OP_MULT, C.REG_LO, 1, 2, 0, 0), (C.OP_MULTU, C.REG_LO, 1, 2, 0, 0)]
+    m, prep, tr, pv = C.program_shard(prog, seed=3)
+    mu = tr["Mul"]
+    assert mu.shape == (32, C.MU_WIDTH)
+    for k, (b, c) in enumerate(vals):
+        sb = b - (1 << 32) if b >> 31 else b
+        sc = c - (1 << 32) if c >> 31 else c
+        r_mul, r_mult, r_multu = mu[3 * k], mu[3 * k + 1], mu[3 * k + 2]
+        assert _word(r_mul, C.MU_A) == (b * c) & C.M32 and r_mul[C.MU_HRR] == 0
+        p = (sb * sc) & ((1 << 64) - 1)
+        assert (_word(r_mult, C.MU_A), _word(r_mult, C.MU_HI)) == (p & C.M32, p >> 32) and r_mult[C.MU_HRR] == 1
+        assert (_word(r_multu, C.MU_A), _word(r_multu, C.MU_HI)) == ((b * c) & C.M32, (b * c) >> 32)
+    rs = tr["RegisterState"]
+    b, c = vals[-1]
+    assert _word(rs[C.REG_LO], C.RS_FIN_VAL) == (b * c) & C.M32 and _word(rs[C.REG_HI], C.RS_FIN_VAL) == (b * c) >> 32
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+@pytest.mark.parametrize("what", ["carry", "hi", "sign_extend", "hi_register"])
+def test_mul_tamper_rejected(shard, oracle, what):
+    m, prep, tr, pv = shard
+    bad = {k: v.copy() for k, v in tr.items()}
+    mu = bad["Mul"]
+    i = int(np.nonzero(mu[:, C.MU_MULT])[0][0])
+    if what == "carry":
+        mu[i, C.MU_CARRY + 2] += 1
+    elif what == "hi":  # a forged HI in both the chip and its register write
+        mu[i, C.MU_HI] ^= 1
+        mu[i, C.MU_HI_ACC + 4] ^= 1
+    elif what == "sign_extend":  # MULT treated as unsigned
+        j = int(np.nonzero(mu[:, C.MU_BSE])[0][0])
+        mu[j, C.MU_BSE] = 0
+    else:  # the HI write is dropped from the memory argument
+        mu[i, C.MU_HRR] = 0
+    assert _air_check.check(m, prep, bad, pv) != ([], [])
+    rc, proof = oracle.prove(bad, pv)
+    assert rc == 0 and oracle.verify(proof) != 0
 
 
 # ---------------------------------------------------------------- GPU parity

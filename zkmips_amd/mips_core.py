@@ -53,12 +53,17 @@ def _vword(base):
     return [_m(base + i) for i in range(4)]
 
 
-def _eval_memory_access(ch, acc, prev_value_base, clk_pos, addr_col, do_check_expr, do_check_vpc):
+CPU_CLK = ((C_CLK8, 65536), (C_CLK16, 1))  # clk = clk_8bit_limb * 2^16 + clk_16bit_limb
+
+
+def _eval_memory_access(ch, acc, prev_value_base, clk_pos, addr, do_check_expr, do_check_vpc, shard_col=C_SHARD,
+                        clk_terms=CPU_CLK):
     """MemoryAirBuilder::eval_memory_access + eval_memory_access_timestamp + eval_range_check_24bits
-    (air/memory.rs:18-62, :90-173) for one register access of the CPU row."""
+    (air/memory.rs:18-62, :90-173) for one register access at timestamp clk + clk_pos; `addr` is the
+    register-number column or a constant (VirtualPairCol)."""
     M = main
-    shard = M(C_SHARD)
-    clk = M(C_CLK8) * 65536 + M(C_CLK16) + clk_pos
+    shard = M(shard_col)
+    clk = sum((M(c) * w for c, w in clk_terms[1:]), M(clk_terms[0][0]) * clk_terms[0][1]) + clk_pos
     compare = M(acc + ACC_COMPARE)
     _assert_bool(ch, do_check_expr)
     _assert_bool(ch, compare, do_check_expr)
@@ -69,8 +74,9 @@ def _eval_memory_access(ch, acc, prev_value_base, clk_pos, addr_col, do_check_ex
     ch.assert_zero(do_check_expr * (diff_minus_one - (M(acc + ACC_D16) + M(acc + ACC_D8) * 65536)))
     ch.sends.append(Lookup([V.const(A.B_U16RANGE), _m(acc + ACC_D16), ZERO, ZERO, ZERO], do_check_vpc, KIND_BYTE))
     ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, ZERO, _m(acc + ACC_D8)], do_check_vpc, KIND_BYTE))
-    prev_vals = [_m(acc + ACC_PREV_SHARD), _m(acc + ACC_PREV_CLK), _m(addr_col)] + _vword(prev_value_base)
-    cur_vals = [_m(C_SHARD), V([("main", C_CLK8, 65536), ("main", C_CLK16, 1)], clk_pos), _m(addr_col)]
+    addr_v = addr if isinstance(addr, V) else _m(addr)
+    prev_vals = [_m(acc + ACC_PREV_SHARD), _m(acc + ACC_PREV_CLK), addr_v] + _vword(prev_value_base)
+    cur_vals = [_m(shard_col), V([("main", c, w) for c, w in clk_terms], clk_pos), addr_v]
     cur_vals += _vword(acc + ACC_VALUE)
     ch.sends.append(Lookup(prev_vals, do_check_vpc, KIND_MEMORY))
     ch.receives.append(Lookup(cur_vals, do_check_vpc, KIND_MEMORY))
@@ -270,6 +276,134 @@ def _range_checker_cols(v: np.ndarray) -> np.ndarray:
     return out
 
 
+# ---------------------------------------------------------------- Mul (alu/mul)
+OP_MUL, OP_MULT, OP_MULTU = 2, 3, 4  # executor/src/opcode.rs:18-20
+MUL_OPS = (OP_MUL, OP_MULT, OP_MULTU)
+REG_LO, REG_HI, NUM_REGS = 32, 33, 34  # Register::LO / HI; MULT/MULTU write LO via op_a, HI at position HI
+POS_HI = 4
+# MulCols (alu/mul/mod.rs:35-105); op_hi_access is MemoryReadWriteCols (prev_value + access)
+MU_PC, MU_NPC, MU_HI, MU_A, MU_B, MU_C, MU_CARRY, MU_PROD = 0, 1, 2, 6, 10, 14, 18, 26
+MU_BMSB, MU_CMSB, MU_BSE, MU_CSE, MU_MUL, MU_MULT, MU_MULTU, MU_REAL = range(34, 42)
+MU_HI_ACC, MU_HRR, MU_SHARD, MU_CLK = 42, 55, 56, 57
+MU_WIDTH = 58
+
+
+def mul_chip() -> ChipDesc:
+    """MulChip::eval (alu/mul/mod.rs:335-506), constraints and lookups in its order."""
+    ch = ChipDesc("Mul", prep_width=0, main_width=MU_WIDTH, local_only=True)
+    M = main
+    real = _m(MU_REAL)
+    for msb, byte in ((MU_BMSB, MU_B + 3), (MU_CMSB, MU_C + 3)):
+        ch.sends.append(Lookup([V.const(A.B_MSB), _m(msb), ZERO, _m(byte), ZERO], real, KIND_BYTE))
+    ch.assert_zero(M(MU_BSE) - M(MU_MULT) * M(MU_BMSB))
+    ch.assert_zero(M(MU_CSE) - M(MU_MULT) * M(MU_CMSB))
+    b = [M(MU_B + i) for i in range(4)] + [M(MU_BSE) * 255] * 4
+    c = [M(MU_C + i) for i in range(4)] + [M(MU_CSE) * 255] * 4
+    m = [None] * 8
+    for i in range(8):
+        for j in range(8):
+            if i + j < 8:
+                t = b[i] * c[j]
+                m[i + j] = t if m[i + j] is None else m[i + j] + t
+    carry = [M(MU_CARRY + i) for i in range(8)]
+    prod = [M(MU_PROD + i) for i in range(8)]
+    for i in range(8):
+        rhs = m[i] - carry[i] * 256 if i == 0 else m[i] + carry[i - 1] - carry[i] * 256
+        ch.assert_zero(prod[i] - rhs)
+    has_hi = M(MU_MULT) + M(MU_MULTU)
+    for i in range(4):
+        ch.assert_zero(prod[i] - M(MU_A + i))
+        ch.assert_zero(has_hi * (prod[i + 4] - M(MU_HI + i)))
+    for col in (MU_BMSB, MU_CMSB, MU_BSE, MU_CSE, MU_MUL, MU_MULT, MU_MULTU, MU_REAL, MU_HRR):
+        _assert_bool(ch, M(col))
+    ch.assert_zero(M(MU_BSE) * (M(MU_BMSB) - 1))
+    ch.assert_zero(M(MU_CSE) * (M(MU_CMSB) - 1))
+    ch.assert_zero(M(MU_REAL) * (M(MU_MUL) + M(MU_MULT) + M(MU_MULTU) - 1))
+    for i in range(8):  # slice_range_check_u16(carry)
+        ch.sends.append(Lookup([V.const(A.B_U16RANGE), _m(MU_CARRY + i), ZERO, ZERO, ZERO], real, KIND_BYTE))
+    for k in range(0, 8, 2):  # slice_range_check_u8(product)
+        ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, _m(MU_PROD + k), _m(MU_PROD + k + 1)], real,
+                               KIND_BYTE))
+    opcode = V([("main", MU_MUL, OP_MUL), ("main", MU_MULT, OP_MULT), ("main", MU_MULTU, OP_MULTU)])
+    ins = [_m(MU_SHARD), _m(MU_CLK), _m(MU_PC), _m(MU_NPC), V([("main", MU_NPC, 1)], 4), ZERO, opcode]
+    ins += _vword(MU_A) + _vword(MU_B) + _vword(MU_C) + _vword(MU_HI) + [ZERO, ZERO, _m(MU_HRR), ZERO, V.const(1)]
+    ch.receives.append(Lookup(ins, real, KIND_INSTRUCTION))
+    _eval_memory_access(ch, MU_HI_ACC + 4, MU_HI_ACC, POS_HI, V.const(REG_HI), M(MU_HRR), _m(MU_HRR),
+                        shard_col=MU_SHARD, clk_terms=((MU_CLK, 1),))
+    ch.assert_zero(M(MU_HRR) * (M(MU_MULT) + M(MU_MULTU) - 1))
+    for i in range(4):
+        ch.assert_zero(M(MU_HRR) * (M(MU_HI + i) - M(MU_HI_ACC + 4 + ACC_VALUE + i)))
+    ch.assert_zero((1 - M(MU_HRR)) * M(MU_CLK))
+    ch.assert_zero((1 - M(MU_HRR)) * M(MU_SHARD))
+    return ch
+
+
+def _access_cols(t, rows, base, value, prev, shard, clk, sel, byte_lookup):
+    """MemoryAccessCols::populate_access (memory/consistency/trace.rs:36-100) for rows `rows` (value,
+    previous (shard, timestamp), compare flag, 16+8-bit limbs of the timestamp difference - 1) and the
+    Byte lookups of its range checks; `sel` masks the accesses that happened."""
+    t[rows, base + ACC_VALUE:base + ACC_VALUE + 4] = A._bytes(value)
+    t[rows, base + ACC_PREV_SHARD] = np.where(sel, prev[:, 0], 0)
+    t[rows, base + ACC_PREV_CLK] = np.where(sel, prev[:, 1], 0)
+    comp = prev[:, 0] == shard
+    t[rows, base + ACC_COMPARE] = sel & comp
+    cur = np.where(comp, clk, shard)
+    d = cur - np.where(comp, prev[:, 1], prev[:, 0]) - 1
+    assert (d[sel] >= 0).all() and (d[sel] < (1 << 24)).all()
+    d = np.where(sel, d, 0)
+    t[rows, base + ACC_D16] = d & 0xFFFF
+    t[rows, base + ACC_D8] = d >> 16
+    byte_lookup(A.B_U16RANGE, (d[sel] & 0xFFFF) >> 8, d[sel] & 0xFF)
+    byte_lookup(A.B_U8RANGE, np.zeros(int(sel.sum()), np.int64), d[sel] >> 16)
+
+
+def _mul_trace(muls, shard, byte_lookup):
+    """MulChip::event_to_row (alu/mul/mod.rs:218-318).  muls: (op, a, b, c, pc, npc, hi, clk, prev_hi,
+    prev_shard, prev_clk) in execution order; clk < 0 for MUL (no HI record)."""
+    E = np.asarray(muls, np.int64).reshape(-1, 11)
+    n = len(E)
+    t = np.zeros((A._pow2(n), MU_WIDTH), np.uint32)
+    op, a, b, c, pc, npc, hi, clk = (E[:, j] for j in range(8))
+    t[:n, MU_PC], t[:n, MU_NPC] = pc, npc
+    for base, v in ((MU_HI, hi), (MU_A, a), (MU_B, b), (MU_C, c)):
+        t[:n, base:base + 4] = A._bytes(v.astype(np.uint32))
+    bw, cw = A._bytes(b.astype(np.uint32)).astype(np.int64), A._bytes(c.astype(np.uint32)).astype(np.int64)
+    bmsb, cmsb = bw[:, 3] >> 7, cw[:, 3] >> 7
+    bse, cse = (op == OP_MULT) & (bmsb == 1), (op == OP_MULT) & (cmsb == 1)
+    t[:n, MU_BMSB], t[:n, MU_CMSB], t[:n, MU_BSE], t[:n, MU_CSE] = bmsb, cmsb, bse, cse
+    b8 = np.concatenate([bw, np.where(bse, 255, 0)[:, None].repeat(4, 1)], axis=1)
+    c8 = np.concatenate([cw, np.where(cse, 255, 0)[:, None].repeat(4, 1)], axis=1)
+    prod = np.zeros((n, 8), np.int64)
+    for i in range(8):
+        for j in range(8 - i):
+            prod[:, i + j] += b8[:, i] * c8[:, j]
+    carry = np.zeros((n, 8), np.int64)
+    for i in range(8):
+        carry[:, i] = prod[:, i] >> 8
+        prod[:, i] &= 0xFF
+        if i + 1 < 8:
+            prod[:, i + 1] += carry[:, i]
+    t[:n, MU_CARRY:MU_CARRY + 8] = carry
+    t[:n, MU_PROD:MU_PROD + 8] = prod
+    t[:n, MU_MUL], t[:n, MU_MULT], t[:n, MU_MULTU] = op == OP_MUL, op == OP_MULT, op == OP_MULTU
+    t[:n, MU_REAL] = 1
+    byte_lookup(A.B_MSB, bw[:, 3], np.zeros(n, np.int64))
+    byte_lookup(A.B_MSB, cw[:, 3], np.zeros(n, np.int64))
+    for i in range(8):
+        byte_lookup(A.B_U16RANGE, carry[:, i] >> 8, carry[:, i] & 0xFF)
+    for k in range(0, 8, 2):
+        byte_lookup(A.B_U8RANGE, prod[:, k], prod[:, k + 1])
+    hrr = clk >= 0
+    rows = np.arange(n)
+    t[:n, MU_HRR] = hrr
+    t[:n, MU_SHARD] = np.where(hrr, shard, 0)
+    t[:n, MU_CLK] = np.where(hrr, clk, 0)
+    t[:n, MU_HI_ACC:MU_HI_ACC + 4] = np.where(hrr[:, None], A._bytes(E[:, 8].astype(np.uint32)), 0)
+    _access_cols(t, rows, MU_HI_ACC + 4, np.where(hrr, hi, 0).astype(np.uint32), E[:, 9:11], shard,
+                 np.where(hrr, clk + POS_HI, 0), hrr, byte_lookup)
+    return t
+
+
 # ---------------------------------------------------------------- Jump (control_flow/jump)
 OP_JUMP, OP_JUMPI, OP_JUMPDIRECT = 27, 28, 29  # JR/JALR, J/JAL, BAL (executor/src/opcode.rs:45-47)
 JUMP_OPS = (OP_JUMP, OP_JUMPI, OP_JUMPDIRECT)
@@ -325,7 +459,8 @@ def _jump_trace(jumps):
 def core_machine() -> MachineDesc:
     # MipsAir::chips order (crates/core/machine/src/mips/mod.rs:207-431): Cpu, Program, ALUs, Branch, ...,
     # Byte; the memory stand-in last
-    return MachineDesc([cpu_chip(), program_chip(), A.add_sub_chip(), A.bitwise_chip(), A.shift_right_chip(),
+    return MachineDesc([cpu_chip(), program_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
+                        A.shift_right_chip(),
                         A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(),
                         A.byte_chip(),
                         register_state_chip()], NUM_PV_ELTS)
@@ -337,7 +472,8 @@ def core_machine() -> MachineDesc:
 # op_c = sign-extended offset << 2, instruction.rs:405-475).
 _MIX = [(A.OP_ADD, 0), (A.OP_ADD, 1), (A.OP_SUB, 0), (A.OP_AND, 0), (A.OP_AND, 1), (A.OP_OR, 0), (A.OP_OR, 1),
         (A.OP_XOR, 0), (A.OP_XOR, 1), (A.OP_NOR, 0), (A.OP_SLT, 0), (A.OP_SLT, 1), (A.OP_SLTU, 0),
-        (A.OP_SLL, 1), (A.OP_SRL, 1), (A.OP_SRA, 1), (A.OP_ROR, 1), (A.OP_SRL, 0), (A.OP_CLZ, 1), (A.OP_CLO, 1)]
+        (A.OP_SLL, 1), (A.OP_SRL, 1), (A.OP_SRA, 1), (A.OP_ROR, 1), (A.OP_SRL, 0), (A.OP_CLZ, 1), (A.OP_CLO, 1),
+        (OP_MUL, 0), (OP_MULT, 0), (OP_MULTU, 0)]
 _KIND = {A.OP_ADD: "add", A.OP_SUB: "add", A.OP_AND: "bit", A.OP_OR: "bit", A.OP_XOR: "bit", A.OP_NOR: "bit",
          A.OP_SLT: "lt", A.OP_SLTU: "lt", A.OP_SLL: "sll", A.OP_SRL: "sr", A.OP_SRA: "sr", A.OP_ROR: "sr",
          A.OP_CLZ: "clz", A.OP_CLO: "clz"}
@@ -374,6 +510,11 @@ def _alu(op, b, c):
         return (_s32(b) >> s) & M32
     if op == A.OP_ROR:
         return ((b >> s) | (b << (32 - s))) & M32 if s else b
+    if op == OP_MUL:
+        return (b * c) & M32
+    if op in (OP_MULT, OP_MULTU):  # (lo, hi), executor.rs:1900-1907
+        prod = (_s32(b) * _s32(c)) & ((1 << 64) - 1) if op == OP_MULT else b * c
+        return prod & M32, prod >> 32
     x = b if op == A.OP_CLZ else ~b & M32
     return 32 - x.bit_length()
 
@@ -394,6 +535,8 @@ def _random_alu(r, avoid=()):
     regs = [x for x in range(32) if x not in avoid]
     ra = 0 if (r[4] % 16 == 0 and 0 not in avoid) else regs[1 + int(r[1] % (len(regs) - 1))]
     rb = int(r[2] % 32)
+    if op in (OP_MULT, OP_MULTU):  # MULT rs, rt: op_a = LO (instruction.rs:368-370)
+        ra = REG_LO
     if op in (A.OP_CLZ, A.OP_CLO):
         c = 0
     elif imm and op in (A.OP_SLL, A.OP_SRL, A.OP_SRA, A.OP_ROR):
@@ -493,11 +636,11 @@ def _execute(prog, regs, shard, max_steps):
     event, then the dependencies emit_branch_dependencies adds, executor/src/dependencies.rs:175-224),
     and each register's last (shard, timestamp)."""
     end = PC_BASE + 4 * len(prog)
-    last = [(0, 0)] * 32
+    last = [(0, 0)] * NUM_REGS
     pc, npc = PC_BASE, PC_BASE + 4
     steps = []
     ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
-    branches, jumps = [], []
+    branches, jumps, muls = [], [], []
     U = A.UNUSED_PC
     while pc != end:
         assert PC_BASE <= pc < end and len(steps) < max_steps
@@ -539,6 +682,19 @@ def _execute(prog, regs, shard, max_steps):
             jumps.append((pc, op, av, bv, cv, npc, nnpc))
             if op == OP_JUMPDIRECT:  # emit_jump_dependencies (dependencies.rs:230-248)
                 ev["add"].append((A.OP_ADD, nnpc, npc, bv, U, U + 4))
+        elif op in MUL_OPS:  # the Mul chip; MULT/MULTU also write HI at position HI (alu_rw, executor.rs:1430-1449)
+            hi = 0
+            if op == OP_MUL:
+                av = _alu(op, bv, cv)
+                muls.append((op, av, bv, cv, pc, npc, 0, -1, 0, 0, 0))
+            else:
+                av, hi = _alu(op, bv, cv)
+                ps, pcl = last[REG_HI]
+                muls.append((op, av, bv, cv, pc, npc, hi, clk, regs[REG_HI], ps, pcl))
+            written = av if ra else 0
+            if ra:
+                regs[ra] = av
+            nnpc = npc + 4
         else:
             av = _alu(op, bv, cv)
             written = av if ra else 0
@@ -548,9 +704,12 @@ def _execute(prog, regs, shard, max_steps):
             ev[_KIND[op]].append((op, av, bv, cv, pc, npc))
         acc.append(last[ra])
         last[ra] = (shard, clk + POS_A)
-        steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc))
+        if op in (OP_MULT, OP_MULTU):
+            last[REG_HI] = (shard, clk + POS_HI)
+            regs[REG_HI] = hi
+        steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc, hi if op in MUL_OPS else 0))
         pc, npc = npc, nnpc
-    return steps, ev, branches, jumps, last
+    return steps, ev, branches, jumps, muls, last
 
 
 def _ev_arrays(lst):
@@ -561,10 +720,10 @@ def _ev_arrays(lst):
 def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24) // 5 - 1):
     """(machine, prep_traces, traces, public_values) of one shard executing `prog` from PC_BASE to its end
     (at most max_steps instructions: the CPU clk is range-checked to 24 bits)."""
-    init = splitmix64(0x5EED000 + seed, 32) & np.uint64(M32)
+    init = splitmix64(0x5EED000 + seed, NUM_REGS) & np.uint64(M32)
     regs = [0] + [int(x) for x in init[1:]]
     init_vals = list(regs)
-    steps, ev, branches, jumps, last = _execute(prog, regs, shard, max_steps)
+    steps, ev, branches, jumps, muls, last = _execute(prog, regs, shard, max_steps)
     n = len(steps)
     assert n > 0
     height = max(16, 1 << (n - 1).bit_length())
@@ -601,6 +760,12 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     t[:n, C_OPCODE:C_IMMC + 1] = instr_cols[ks]
     t[:n, C_RW_A] = 0
     t[:n, C_SEQ] = is_seq
+    his = np.asarray([s_[12] for s_ in steps], np.int64)
+    mult_div = np.isin(ops, (OP_MULT, OP_MULTU))  # is_mult_div_instruction: check memory, send shard/clk
+    t[:n, C_HI_PREV_A:C_HI_PREV_A + 4] = A._bytes(his.astype(np.uint32))
+    t[:n, C_CHECK_MEM] = mult_div
+    t[:n, C_SHARD_SEND] = np.where(mult_div, shard, 0)
+    t[:n, C_CLK_SEND] = np.where(mult_div, clk, 0)
     t[:n, C_A_IMM] = is_branch
     t[:n, C_A_VAL:C_A_VAL + 4] = A._bytes(av)
     t[:n, C_REAL] = 1
@@ -634,6 +799,8 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
         traces["Branch"] = _branch_trace(branches, byte_lookup)
     if jumps:
         traces["Jump"] = _jump_trace(jumps)
+    if muls:
+        traces["Mul"] = _mul_trace(muls, shard, byte_lookup)
 
     # Program: one row per instruction, multiplicity = executions
     ph = max(16, 1 << (len(prog) - 1).bit_length())
@@ -644,13 +811,14 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     pm[:len(prog), 0] = np.bincount(ks, minlength=len(prog))
     traces["Program"] = pm
 
-    rs = np.zeros((32, RS_WIDTH), np.uint32)
-    rs[:, RS_ADDR] = np.arange(32)
-    rs[:, RS_INIT_VAL:RS_INIT_VAL + 4] = A._bytes(np.asarray(init_vals, np.uint32))
-    rs[:, RS_FIN_SHARD] = [s_ for s_, _ in last]
-    rs[:, RS_FIN_CLK] = [c_ for _, c_ in last]
-    rs[:, RS_FIN_VAL:RS_FIN_VAL + 4] = A._bytes(np.asarray(regs, np.uint32))
-    rs[:, RS_REAL] = 1
+    rs = np.zeros((A._pow2(NUM_REGS), RS_WIDTH), np.uint32)
+    R = NUM_REGS
+    rs[:R, RS_ADDR] = np.arange(R)
+    rs[:R, RS_INIT_VAL:RS_INIT_VAL + 4] = A._bytes(np.asarray(init_vals, np.uint32))
+    rs[:R, RS_FIN_SHARD] = [s_ for s_, _ in last]
+    rs[:R, RS_FIN_CLK] = [c_ for _, c_ in last]
+    rs[:R, RS_FIN_VAL:RS_FIN_VAL + 4] = A._bytes(np.asarray(regs, np.uint32))
+    rs[:R, RS_REAL] = 1
     traces["RegisterState"] = rs
 
     assert mult.max() < P
