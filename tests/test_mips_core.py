@@ -1,4 +1,4 @@
-"""MIPS core shard: the reference's Cpu, Program, Branch, Jump and Mul chips (zkmips_amd/mips_core.py) on top of
+"""MIPS core shard: the reference's Cpu, Program, Branch, Jump, Mul and DivRem chips (zkmips_amd/mips_core.py) on top of
 the ALU slice, with the register-memory argument closed by the RegisterState stand-in.
 
 CPU part: the trace satisfies every constraint and every lookup balances (direct evaluation,
@@ -235,6 +235,61 @@ def test_mul_kinds():
     assert rc == 0 and o.verify(proof) == 0
 
 
+_DIV_VALUES = [(7, 2), (C.M32 - 6, 2), (7, C.M32 - 1), (C.M32 - 6, C.M32 - 1), (0x80000000, C.M32), (5, 0), (0, 5),
+               (C.M32, C.M32), (0x80000000, 1), (123456789, 1000)]
+
+
+def test_divrem_kinds():
+    """DIV / DIVU / MOD / MODU on signs, i32::MIN / -1 overflow and division by zero (the AIR's c = 0
+    branch: quotient 2^32 - 1, remainder b); DIV/DIVU leave (quotient, remainder) in (LO, HI)."""
+    prog = []
+    for b, c in _DIV_VALUES:
+        prog += [(A.OP_ADD, 1, 0, b, 0, 1), (A.OP_ADD, 2, 0, c, 0, 1)]
+        prog += [(C.OP_DIV, C.REG_LO, 1, 2, 0, 0), (C.OP_DIVU, C.REG_LO, 1, 2, 0, 0), (C.OP_MOD, 3, 1, 2, 0, 0),
+                 (C.OP_MODU, 4, 1, 2, 0, 0)]
+    m, prep, tr, pv = C.program_shard(prog, seed=3)
+    d = tr["DivRem"]
+    s32 = lambda x: x - (1 << 32) if x >> 31 else x
+    for k, (b, c) in enumerate(_DIV_VALUES):
+        rows = d[4 * k:4 * k + 4]
+        if c == 0:
+            want_s = want_u = (C.M32, b)
+        elif s32(b) == -(1 << 31) and s32(c) == -1:
+            want_s, want_u = (b, 0), (b // c, b % c)
+        else:
+            q = int(abs(s32(b)) // abs(s32(c))) * (1 if (s32(b) < 0) == (s32(c) < 0) else -1)
+            want_s, want_u = (q & C.M32, (s32(b) - q * s32(c)) & C.M32), (b // c, b % c)
+        assert (_word(rows[0], C.DV_Q), _word(rows[0], C.DV_R)) == want_s
+        assert (_word(rows[1], C.DV_Q), _word(rows[1], C.DV_R)) == want_u
+        assert _word(rows[2], C.DV_R) == want_s[1] and _word(rows[3], C.DV_R) == want_u[1]
+        assert rows[0, C.DV_OVF] == (b == 0x80000000 and c == C.M32) and rows[0, C.DV_IS_C0 + 10] == (c == 0)
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+@pytest.mark.parametrize("what", ["quotient", "remainder_sign", "div_carry", "c_is_zero"])
+def test_divrem_tamper_rejected(shard, oracle, what):
+    m, prep, tr, pv = shard
+    bad = {k: v.copy() for k, v in tr.items()}
+    d = bad["DivRem"]
+    nz = np.nonzero(d[:, C.DV_IS_C0 + 10] == 0)[0]
+    i = int(nz[0])
+    if what == "quotient":  # q + 1 with the remainder unchanged
+        d[i, C.DV_Q] = (int(d[i, C.DV_Q]) + 1) % 256
+    elif what == "remainder_sign":
+        j = int(np.nonzero(d[:, C.DV_DIV] + d[:, C.DV_MOD])[0][0])
+        d[j, C.DV_RNEG] ^= 1
+    elif what == "div_carry":
+        d[i, C.DV_CARRY] ^= 1
+    else:  # claims division by zero for a nonzero divisor
+        d[i, C.DV_IS_C0 + 10] = 1
+    assert _air_check.check(m, prep, bad, pv) != ([], [])
+    rc, proof = oracle.prove(bad, pv)
+    assert rc == 0 and oracle.verify(proof) != 0
+
+
 @pytest.mark.parametrize("what", ["carry", "hi", "sign_extend", "hi_register"])
 def test_mul_tamper_rejected(shard, oracle, what):
     m, prep, tr, pv = shard
@@ -254,6 +309,33 @@ def test_mul_tamper_rejected(shard, oracle, what):
     assert _air_check.check(m, prep, bad, pv) != ([], [])
     rc, proof = oracle.prove(bad, pv)
     assert rc == 0 and oracle.verify(proof) != 0
+
+
+def _with_global_chip(shard, seed=9):
+    """The core shard plus a Global-scope chip (commit_scope Global, crates/core/machine/src/global/mod.rs:202):
+    its last row's last 14 main columns are the shard's septic global cumulative sum, which the prover
+    captures (prover.rs:352-361), observes, and the quotient ties to the trace with 14 last-row
+    constraints (permutation.rs:331-343).  The septic-curve accumulation itself is not restated; the
+    digest here is 14 synthetic field elements."""
+    from zkmips_amd.machine import ChipDesc, MachineDesc, main
+    from zkmips_amd.workloads import splitmix64
+    m, prep, tr, pv = shard
+    ch = ChipDesc("GlobalStandIn", prep_width=0, main_width=15, commit_scope=1)
+    ch.assert_zero(main(0) * (main(0) - 1))
+    mg = MachineDesc(m.chips + [ch], m.num_pv)
+    g = np.zeros((64, 15), np.uint32)
+    g[:40, 0] = 1
+    g[:, 1:] = (splitmix64(0x61B0000 + seed, 64 * 14) % np.uint64(A.P)).astype(np.uint32).reshape(64, 14)
+    return mg, prep, {**tr, "GlobalStandIn": g}, pv
+
+
+def test_global_scope_chip(shard):
+    mg, prep, tr, pv = _with_global_chip(shard)
+    assert mg.chips[-1].num_constraints == 1 + 14
+    o = O.OracleProver(mg, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+    assert tr["GlobalStandIn"][-1, 1:].astype("<u4").tobytes() in proof  # the captured digest
 
 
 # ---------------------------------------------------------------- GPU parity
@@ -277,6 +359,18 @@ def test_core_gpu_proof_bytes_identical(dev, n, seed):
     rc, ref = cpu.prove(tr, pv)
     assert rc == 0 and proof == ref
     assert cpu.verify(proof) == 0
+
+
+@pytest.mark.gpu
+def test_global_scope_gpu_proof_bytes_identical(dev, shard):
+    from zkmips_amd.prover import HipProver
+    mg, prep, tr, pv = _with_global_chip(shard)
+    gpu = HipProver(dev, mg, prep, num_queries=16)
+    cpu = O.OracleProver(mg, prep, num_queries=16)
+    proof = gpu.prove_shard(tr, pv)
+    rc, ref = cpu.prove(tr, pv)
+    assert rc == 0 and proof == ref and cpu.verify(proof) == 0
+    assert tr["GlobalStandIn"][-1, 1:].astype("<u4").tobytes() in proof
 
 
 @pytest.mark.gpu

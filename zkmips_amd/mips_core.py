@@ -404,6 +404,214 @@ def _mul_trace(muls, shard, byte_lookup):
     return t
 
 
+# ---------------------------------------------------------------- DivRem (alu/divrem)
+OP_DIV, OP_DIVU, OP_MOD, OP_MODU = 5, 6, 7, 8  # executor/src/opcode.rs:21-24
+DIV_OPS = (OP_DIV, OP_DIVU, OP_MOD, OP_MODU)
+MULT_DIV = (OP_MULT, OP_MULTU, OP_DIV, OP_DIVU)  # Instruction::is_mult_div_instruction (instruction.rs:302)
+# DivRemCols (alu/divrem/mod.rs); IsZeroWordOperation = 4 x (inverse, result) + lower, upper, result
+DV_PC, DV_NPC, DV_B, DV_C, DV_Q, DV_R, DV_ABS_R, DV_ABS_C, DV_MAXC = 0, 1, 2, 6, 10, 14, 18, 22, 26
+DV_CTQ, DV_CARRY, DV_IS_C0 = 30, 38, 46
+DV_DIV, DV_DIVU, DV_MOD, DV_MODU, DV_OVF, DV_OVF_B, DV_OVF_C = 57, 58, 59, 60, 61, 62, 73
+DV_BMSB, DV_RMSB, DV_CMSB, DV_BNEG, DV_RNEG, DV_CNEG, DV_RCM = range(84, 91)
+DV_HI_ACC, DV_SHARD, DV_CLK = 91, 104, 105
+DV_WIDTH = 106
+IZW_WIDTH = 11
+
+
+def _is_zero_word(ch, a, base, is_real):
+    """IsZeroWordOperation::eval (operations/is_zero_word.rs:49-92) with IsZeroOperation per byte
+    (operations/is_zero.rs:47-66)."""
+    M = main
+    for i in range(4):
+        inv, res = M(base + 2 * i), M(base + 2 * i + 1)
+        ch.assert_zero(is_real * ((1 - inv * a[i]) - res))
+        _assert_bool(ch, res, is_real)
+        ch.assert_zero(is_real * res * a[i])
+    _assert_bool(ch, is_real)
+    lower, upper, result = M(base + 8), M(base + 9), M(base + 10)
+    for x in (lower, upper, result):
+        _assert_bool(ch, x, is_real)
+    ch.assert_zero(is_real * (lower - M(base + 1) * M(base + 3)))
+    ch.assert_zero(is_real * (upper - M(base + 5) * M(base + 7)))
+    ch.assert_zero(is_real * (result - lower * upper))
+
+
+def _is_equal_word(ch, a, b, base, is_real):
+    """IsEqualWordOperation::eval (operations/is_equal_word.rs:38-58)."""
+    _assert_bool(ch, is_real)
+    _is_zero_word(ch, [a[i] - b[i] for i in range(4)], base, is_real)
+
+
+def divrem_chip() -> ChipDesc:
+    """DivRemChip::eval (alu/divrem/mod.rs), constraints and lookups in its order."""
+    ch = ChipDesc("DivRem", prep_width=0, main_width=DV_WIDTH, local_only=True)
+    M = main
+    w = lambda base: [M(base + i) for i in range(4)]
+    div, divu, mod_, modu = M(DV_DIV), M(DV_DIVU), M(DV_MOD), M(DV_MODU)
+    is_real = div + divu + mod_ + modu
+    real_v = V([("main", c, 1) for c in (DV_DIV, DV_DIVU, DV_MOD, DV_MODU)])
+    for msb, neg in ((DV_BMSB, DV_BNEG), (DV_RMSB, DV_RNEG), (DV_CMSB, DV_CNEG)):
+        ch.assert_zero(M(msb) * (div + mod_) - M(neg))
+    mul_op = V([("main", DV_DIV, OP_MULT), ("main", DV_MOD, OP_MULT), ("main", DV_DIVU, OP_MULTU),
+                ("main", DV_MODU, OP_MULTU)])
+    ctq = [_m(DV_CTQ + i) for i in range(8)]
+    vals = [ZERO, ZERO, V.const(A.UNUSED_PC), V.const(A.UNUSED_PC + 4), V.const(A.UNUSED_PC + 8), ZERO, mul_op]
+    vals += ctq[:4] + _vword(DV_Q) + _vword(DV_C) + ctq[4:] + [ZERO, ZERO, ZERO, ZERO, V.const(1)]
+    ch.sends.append(Lookup(vals, real_v, KIND_INSTRUCTION))  # send_alu_with_hi(MULT/MULTU, ...)
+    _is_equal_word(ch, w(DV_B), [0, 0, 0, 0x80], DV_OVF_B, is_real)
+    _is_equal_word(ch, w(DV_C), [0xFF] * 4, DV_OVF_C, is_real)
+    ch.assert_zero(M(DV_OVF) - M(DV_OVF_B + 10) * M(DV_OVF_C + 10) * (div + mod_))
+    carry = [M(DV_CARRY + i) for i in range(8)]
+    e = []
+    for i in range(8):
+        x = M(DV_CTQ + i) + (M(DV_R + i) if i < 4 else M(DV_RNEG) * 255) - carry[i] * 256
+        e.append(x + carry[i - 1] if i > 0 else x)
+    ovf, bneg = M(DV_OVF), M(DV_BNEG)
+    for i in range(8):
+        if i < 4:
+            ch.assert_zero(M(DV_B + i) - e[i])
+        else:
+            ch.assert_zero((1 - ovf) * bneg * (e[i] - 255))
+            ch.assert_zero((1 - ovf) * (1 - bneg) * e[i])
+            ch.assert_zero(ovf * e[i])
+    rneg, cneg = M(DV_RNEG), M(DV_CNEG)
+    rem_sum = M(DV_R) + M(DV_R + 1) + M(DV_R + 2) + M(DV_R + 3)
+    ch.assert_zero(rneg * (bneg - 1))
+    ch.assert_zero(rem_sum * (1 - rneg) * bneg)
+    _is_zero_word(ch, w(DV_C), DV_IS_C0, is_real)
+    c0 = M(DV_IS_C0 + 10)
+    for i in range(4):
+        ch.assert_zero(c0 * (M(DV_Q + i) - 255))
+    for i in range(4):
+        ch.assert_zero((1 - cneg) * (M(DV_C + i) - M(DV_ABS_C + i)))
+        ch.assert_zero((1 - rneg) * (M(DV_R + i) - M(DV_ABS_R + i)))
+    _send_alu(ch, A.OP_ADD, [ZERO] * 4, _vword(DV_C), _vword(DV_ABS_C), _m(DV_CNEG))
+    _send_alu(ch, A.OP_ADD, [ZERO] * 4, _vword(DV_R), _vword(DV_ABS_R), _m(DV_RNEG))
+    mx = [c0 * 1 + (1 - c0) * M(DV_ABS_C)] + [(1 - c0) * M(DV_ABS_C + i) for i in (1, 2, 3)]
+    for i in range(4):
+        ch.assert_zero(is_real * (M(DV_MAXC + i) - mx[i]))
+    ch.assert_zero((1 - c0) * is_real - M(DV_RCM))
+    _send_alu(ch, A.OP_SLTU, [V.const(1), ZERO, ZERO, ZERO], _vword(DV_ABS_R), _vword(DV_MAXC), _m(DV_RCM))
+    for msb, byte in ((DV_BMSB, DV_B + 3), (DV_CMSB, DV_C + 3), (DV_RMSB, DV_R + 3)):
+        ch.sends.append(Lookup([V.const(A.B_MSB), _m(msb), ZERO, _m(byte), ZERO], real_v, KIND_BYTE))
+    for base in (DV_Q, DV_R):
+        for k in (0, 2):
+            ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, _m(base + k), _m(base + k + 1)], real_v,
+                                   KIND_BYTE))
+    for i in range(8):
+        _assert_bool(ch, carry[i])
+    for k in range(0, 8, 2):
+        ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, _m(DV_CTQ + k), _m(DV_CTQ + k + 1)], real_v,
+                               KIND_BYTE))
+    for col in (DV_DIV, DV_DIVU, DV_MOD, DV_MODU, DV_OVF, DV_BMSB, DV_RMSB, DV_CMSB, DV_BNEG, DV_RNEG, DV_CNEG):
+        _assert_bool(ch, M(col))
+    ch.assert_zero(is_real * (1 - (divu + div + mod_ + modu)))
+    opcode = V([("main", DV_DIVU, OP_DIVU), ("main", DV_DIV, OP_DIV), ("main", DV_MOD, OP_MOD),
+                ("main", DV_MODU, OP_MODU)])
+    npc4 = V([("main", DV_NPC, 1)], 4)
+    ins = [_m(DV_SHARD), _m(DV_CLK), _m(DV_PC), _m(DV_NPC), npc4, ZERO, opcode] + _vword(DV_Q) + _vword(DV_B)
+    ins += _vword(DV_C) + _vword(DV_R) + [ZERO, ZERO, V.const(1), ZERO, V.const(1)]
+    ch.receives.append(Lookup(ins, V([("main", DV_DIV, 1), ("main", DV_DIVU, 1)]), KIND_INSTRUCTION))
+    ins = [ZERO, ZERO, _m(DV_PC), _m(DV_NPC), npc4, ZERO, opcode] + _vword(DV_R) + _vword(DV_B) + _vword(DV_C)
+    ins += [ZERO] * 4 + [ZERO, ZERO, ZERO, ZERO, V.const(1)]
+    ch.receives.append(Lookup(ins, V([("main", DV_MOD, 1), ("main", DV_MODU, 1)]), KIND_INSTRUCTION))
+    _eval_memory_access(ch, DV_HI_ACC + 4, DV_HI_ACC, POS_HI, V.const(REG_HI), div + divu,
+                        V([("main", DV_DIV, 1), ("main", DV_DIVU, 1)]), shard_col=DV_SHARD,
+                        clk_terms=((DV_CLK, 1),))
+    for i in range(4):
+        ch.assert_zero((div + divu) * (M(DV_R + i) - M(DV_HI_ACC + 4 + ACC_VALUE + i)))
+    return ch
+
+
+def _izw_cols(words: np.ndarray) -> np.ndarray:
+    """IsZeroWordOperation::populate_from_field_element over rows of 4 field elements."""
+    n = len(words)
+    out = np.zeros((n, IZW_WIDTH), np.uint32)
+    x = words.astype(np.int64) % P
+    inv = np.asarray([[pow(int(v), P - 2, P) if v else 0 for v in row] for row in x], np.int64).reshape(n, 4)
+    z = (x == 0).astype(np.uint32)
+    out[:, 0:8:2] = inv
+    out[:, 1:8:2] = z
+    out[:, 8] = z[:, 0] * z[:, 1]
+    out[:, 9] = z[:, 2] * z[:, 3]
+    out[:, 10] = out[:, 8] * out[:, 9]
+    return out
+
+
+def _qr(op, b, c):
+    """get_quotient_and_remainder (executor/src/utils.rs:33-43)."""
+    if c == 0:
+        return M32, b
+    if op in (OP_DIV, OP_MOD):
+        sb, sc = _s32(b), _s32(c)
+        if sb == -(1 << 31) and sc == -1:
+            return b, 0  # wrapping_div / wrapping_rem
+        q = abs(sb) // abs(sc) * (1 if (sb < 0) == (sc < 0) else -1)
+        return q & M32, (sb - q * sc) & M32
+    return b // c, b % c
+
+
+def _divrem_trace(divs, shard, byte_lookup):
+    """DivRemChip::generate_trace (alu/divrem/mod.rs).  divs: (op, b, c, pc, npc, clk, prev_hi, prev_shard,
+    prev_clk) in execution order; clk < 0 for MOD/MODU (no HI record)."""
+    E = np.asarray(divs, np.int64).reshape(-1, 9)
+    n = len(E)
+    t = np.zeros((A._pow2(n), DV_WIDTH), np.uint32)
+    op, b, c, pc, npc, clk = (E[:, j] for j in range(6))
+    qr = np.asarray([_qr(int(o), int(x), int(y)) for o, x, y in zip(op, b, c)], np.int64).reshape(n, 2)
+    q, r = qr[:, 0], qr[:, 1]
+    signed = np.isin(op, (OP_DIV, OP_MOD))
+    u = lambda v: v.astype(np.uint32)
+    t[:n, DV_PC], t[:n, DV_NPC] = pc, npc
+    for base, v in ((DV_B, b), (DV_C, c), (DV_Q, q), (DV_R, r)):
+        t[:n, base:base + 4] = A._bytes(u(v))
+    for col, code in ((DV_DIV, OP_DIV), (DV_DIVU, OP_DIVU), (DV_MOD, OP_MOD), (DV_MODU, OP_MODU)):
+        t[:n, col] = op == code
+    t[:n, DV_IS_C0:DV_IS_C0 + IZW_WIDTH] = _izw_cols(A._bytes(u(c)))
+    diff = lambda x, k: A._bytes(u(x)).astype(np.int64) - np.asarray(list(k), np.int64)[None, :]
+    t[:n, DV_OVF_B:DV_OVF_B + IZW_WIDTH] = _izw_cols(diff(b, (0, 0, 0, 0x80)))
+    t[:n, DV_OVF_C:DV_OVF_C + IZW_WIDTH] = _izw_cols(diff(c, (255, 255, 255, 255)))
+    bmsb, cmsb, rmsb = b >> 31, c >> 31, r >> 31
+    t[:n, DV_BMSB], t[:n, DV_CMSB], t[:n, DV_RMSB] = bmsb, cmsb, rmsb
+    t[:n, DV_BNEG], t[:n, DV_CNEG], t[:n, DV_RNEG] = bmsb & signed, cmsb & signed, rmsb & signed
+    t[:n, DV_OVF] = signed & (b == 0x80000000) & (c == M32)
+    sabs = lambda v: np.abs(u(v).view(np.int32).astype(np.int64))
+    abs_r = np.where(signed, sabs(r), r)
+    abs_c = np.where(signed, sabs(c), c)
+    t[:n, DV_ABS_R:DV_ABS_R + 4] = A._bytes(u(abs_r))
+    t[:n, DV_ABS_C:DV_ABS_C + 4] = A._bytes(u(abs_c))
+    t[:n, DV_MAXC:DV_MAXC + 4] = A._bytes(u(np.maximum(1, abs_c)))
+    t[:n, DV_RCM] = c != 0
+    s32 = lambda v: u(v).view(np.int32).astype(object)
+    ctq = np.asarray([(int(qq) * int(cc)) & ((1 << 64) - 1) for qq, cc in
+                      zip(np.where(signed, s32(q), q.astype(object)), np.where(signed, s32(c), c.astype(object)))],
+                     np.uint64)
+    ctq_b = np.stack([(ctq >> np.uint64(8 * i)) & np.uint64(0xFF) for i in range(8)], axis=1).astype(np.int64)
+    r64 = np.where(signed, r | np.where(rmsb == 1, 0xFFFFFFFF00000000, 0), r).astype(np.uint64)
+    r_b = np.stack([(r64 >> np.uint64(8 * i)) & np.uint64(0xFF) for i in range(8)], axis=1).astype(np.int64)
+    carry = np.zeros((n, 8), np.int64)
+    for i in range(8):
+        x = ctq_b[:, i] + r_b[:, i] + (carry[:, i - 1] if i else 0)
+        carry[:, i] = x >> 8
+    t[:n, DV_CTQ:DV_CTQ + 8] = ctq_b
+    t[:n, DV_CARRY:DV_CARRY + 8] = carry
+    hrr = clk >= 0
+    t[:n, DV_SHARD] = np.where(hrr, shard, 0)
+    t[:n, DV_CLK] = np.where(hrr, clk, 0)
+    t[:n, DV_HI_ACC:DV_HI_ACC + 4] = np.where(hrr[:, None], A._bytes(u(E[:, 6])), 0)
+    _access_cols(t, np.arange(n), DV_HI_ACC + 4, u(np.where(hrr, r, 0)), E[:, 7:9], shard,
+                 np.where(hrr, clk + POS_HI, 0), hrr, byte_lookup)
+    for v in (b, c, r):
+        byte_lookup(A.B_MSB, A._bytes(u(v))[:, 3], np.zeros(n, np.int64))
+    for v in (q, r):
+        wb = A._bytes(u(v))
+        byte_lookup(A.B_U8RANGE, wb[:, 0], wb[:, 1])
+        byte_lookup(A.B_U8RANGE, wb[:, 2], wb[:, 3])
+    for k in range(0, 8, 2):
+        byte_lookup(A.B_U8RANGE, ctq_b[:, k], ctq_b[:, k + 1])
+    return t, q, r, abs_c, abs_r, ctq
+
+
 # ---------------------------------------------------------------- Jump (control_flow/jump)
 OP_JUMP, OP_JUMPI, OP_JUMPDIRECT = 27, 28, 29  # JR/JALR, J/JAL, BAL (executor/src/opcode.rs:45-47)
 JUMP_OPS = (OP_JUMP, OP_JUMPI, OP_JUMPDIRECT)
@@ -459,7 +667,7 @@ def _jump_trace(jumps):
 def core_machine() -> MachineDesc:
     # MipsAir::chips order (crates/core/machine/src/mips/mod.rs:207-431): Cpu, Program, ALUs, Branch, ...,
     # Byte; the memory stand-in last
-    return MachineDesc([cpu_chip(), program_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
+    return MachineDesc([cpu_chip(), program_chip(), divrem_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
                         A.shift_right_chip(),
                         A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(),
                         A.byte_chip(),
@@ -473,7 +681,7 @@ def core_machine() -> MachineDesc:
 _MIX = [(A.OP_ADD, 0), (A.OP_ADD, 1), (A.OP_SUB, 0), (A.OP_AND, 0), (A.OP_AND, 1), (A.OP_OR, 0), (A.OP_OR, 1),
         (A.OP_XOR, 0), (A.OP_XOR, 1), (A.OP_NOR, 0), (A.OP_SLT, 0), (A.OP_SLT, 1), (A.OP_SLTU, 0),
         (A.OP_SLL, 1), (A.OP_SRL, 1), (A.OP_SRA, 1), (A.OP_ROR, 1), (A.OP_SRL, 0), (A.OP_CLZ, 1), (A.OP_CLO, 1),
-        (OP_MUL, 0), (OP_MULT, 0), (OP_MULTU, 0)]
+        (OP_MUL, 0), (OP_MULT, 0), (OP_MULTU, 0), (OP_DIV, 0), (OP_DIVU, 0), (OP_MOD, 0), (OP_MODU, 0)]
 _KIND = {A.OP_ADD: "add", A.OP_SUB: "add", A.OP_AND: "bit", A.OP_OR: "bit", A.OP_XOR: "bit", A.OP_NOR: "bit",
          A.OP_SLT: "lt", A.OP_SLTU: "lt", A.OP_SLL: "sll", A.OP_SRL: "sr", A.OP_SRA: "sr", A.OP_ROR: "sr",
          A.OP_CLZ: "clz", A.OP_CLO: "clz"}
@@ -535,7 +743,7 @@ def _random_alu(r, avoid=()):
     regs = [x for x in range(32) if x not in avoid]
     ra = 0 if (r[4] % 16 == 0 and 0 not in avoid) else regs[1 + int(r[1] % (len(regs) - 1))]
     rb = int(r[2] % 32)
-    if op in (OP_MULT, OP_MULTU):  # MULT rs, rt: op_a = LO (instruction.rs:368-370)
+    if op in (OP_MULT, OP_MULTU, OP_DIV, OP_DIVU):  # MULT/DIV rs, rt: op_a = LO (instruction.rs:368-384)
         ra = REG_LO
     if op in (A.OP_CLZ, A.OP_CLO):
         c = 0
@@ -640,7 +848,7 @@ def _execute(prog, regs, shard, max_steps):
     pc, npc = PC_BASE, PC_BASE + 4
     steps = []
     ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
-    branches, jumps, muls = [], [], []
+    branches, jumps, muls, divs = [], [], [], []
     U = A.UNUSED_PC
     while pc != end:
         assert PC_BASE <= pc < end and len(steps) < max_steps
@@ -695,6 +903,31 @@ def _execute(prog, regs, shard, max_steps):
             if ra:
                 regs[ra] = av
             nnpc = npc + 4
+        elif op in DIV_OPS:  # the DivRem chip; the reference executor traps on c = 0, the AIR covers it
+            q, r = _qr(op, bv, cv)
+            if op in (OP_DIV, OP_DIVU):  # (LO, HI) = (quotient, remainder)
+                av, hi = q, r
+                ps, pcl = last[REG_HI]
+                divs.append((op, bv, cv, pc, npc, clk, regs[REG_HI], ps, pcl))
+            else:
+                av, hi = r, 0
+                divs.append((op, bv, cv, pc, npc, -1, 0, 0, 0))
+            # emit_divrem_dependencies (dependencies.rs:12-102)
+            signed = op in (OP_DIV, OP_MOD)
+            abs_c = abs(_s32(cv)) if signed else cv
+            abs_r = abs(_s32(r)) if signed else r
+            if signed and cv >> 31:
+                ev["add"].append((A.OP_ADD, 0, cv, abs_c & M32, U, U + 4))
+            if signed and r >> 31:
+                ev["add"].append((A.OP_ADD, 0, r, abs_r & M32, U, U + 4))
+            ctq = ((_s32(q) * _s32(cv)) if signed else q * cv) & ((1 << 64) - 1)
+            muls.append((OP_MULT if signed else OP_MULTU, ctq & M32, q, cv, U, U + 4, ctq >> 32, -1, 0, 0, 0))
+            if cv:
+                ev["lt"].append((A.OP_SLTU, 1, abs_r & M32, max(1, abs_c) & M32, U, U + 4))
+            written = av if ra else 0
+            if ra:
+                regs[ra] = av
+            nnpc = npc + 4
         else:
             av = _alu(op, bv, cv)
             written = av if ra else 0
@@ -704,12 +937,13 @@ def _execute(prog, regs, shard, max_steps):
             ev[_KIND[op]].append((op, av, bv, cv, pc, npc))
         acc.append(last[ra])
         last[ra] = (shard, clk + POS_A)
-        if op in (OP_MULT, OP_MULTU):
+        if op in MULT_DIV:
             last[REG_HI] = (shard, clk + POS_HI)
             regs[REG_HI] = hi
-        steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc, hi if op in MUL_OPS else 0))
+        steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc,
+                      hi if op in MUL_OPS + DIV_OPS else 0))
         pc, npc = npc, nnpc
-    return steps, ev, branches, jumps, muls, last
+    return steps, ev, branches, jumps, muls, divs, last
 
 
 def _ev_arrays(lst):
@@ -723,7 +957,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     init = splitmix64(0x5EED000 + seed, NUM_REGS) & np.uint64(M32)
     regs = [0] + [int(x) for x in init[1:]]
     init_vals = list(regs)
-    steps, ev, branches, jumps, muls, last = _execute(prog, regs, shard, max_steps)
+    steps, ev, branches, jumps, muls, divs, last = _execute(prog, regs, shard, max_steps)
     n = len(steps)
     assert n > 0
     height = max(16, 1 << (n - 1).bit_length())
@@ -761,7 +995,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     t[:n, C_RW_A] = 0
     t[:n, C_SEQ] = is_seq
     his = np.asarray([s_[12] for s_ in steps], np.int64)
-    mult_div = np.isin(ops, (OP_MULT, OP_MULTU))  # is_mult_div_instruction: check memory, send shard/clk
+    mult_div = np.isin(ops, MULT_DIV)  # is_mult_div_instruction: check memory, send shard/clk
     t[:n, C_HI_PREV_A:C_HI_PREV_A + 4] = A._bytes(his.astype(np.uint32))
     t[:n, C_CHECK_MEM] = mult_div
     t[:n, C_SHARD_SEND] = np.where(mult_div, shard, 0)
@@ -799,6 +1033,8 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
         traces["Branch"] = _branch_trace(branches, byte_lookup)
     if jumps:
         traces["Jump"] = _jump_trace(jumps)
+    if divs:
+        traces["DivRem"] = _divrem_trace(divs, shard, byte_lookup)[0]
     if muls:
         traces["Mul"] = _mul_trace(muls, shard, byte_lookup)
 
