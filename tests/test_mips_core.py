@@ -269,6 +269,45 @@ def test_divrem_kinds():
     assert rc == 0 and o.verify(proof) == 0
 
 
+def test_movcond_reference_fixture():
+    """The program of the reference's test_mov_cond_prove (misc/mov_cond/mod.rs tests): MOVZ/MOVN (MEQ/MNE)
+    with zero and nonzero conditions, to r0 and r30, and WSBH into LO and r0."""
+    prog = [(A.OP_ADD, 29, 0, 0xF, 0, 1), (A.OP_ADD, 28, 0, 0x8F8F, 0, 1),
+            (C.OP_MEQ, 30, 29, 0, 0, 0), (C.OP_MEQ, 30, 29, 28, 0, 0), (C.OP_MEQ, 0, 29, 0, 0, 0),
+            (C.OP_MEQ, 0, 29, 29, 0, 0), (C.OP_MNE, 30, 29, 28, 0, 0), (C.OP_MNE, 0, 29, 0, 0, 0),
+            (C.OP_WSBH, 32, 29, 0, 0, 1), (C.OP_WSBH, 32, 31, 0, 0, 1), (C.OP_WSBH, 0, 29, 0, 0, 1)]
+    m, prep, tr, pv = C.program_shard(prog, seed=4)
+    mc = tr["MovCond"]
+    assert int(mc[:, C.MC_MEQ].sum()) == 4 and int(mc[:, C.MC_MNE].sum()) == 2 and int(mc[:, C.MC_WSBH].sum()) == 3
+    assert _word(mc[0], C.MC_A) == 0xF and _word(mc[4], C.MC_A) == 0xF  # MOVZ with rt = r0, MOVN with rt = r28
+    assert _word(mc[6], C.MC_A) == 0x0F00  # WSBH swaps the bytes of each halfword
+    rs = tr["RegisterState"]
+    r31 = _word(rs[31], C.RS_INIT_VAL)
+    want = ((r31 >> 16 & 0xFF) << 24) | ((r31 >> 24 & 0xFF) << 16) | ((r31 & 0xFF) << 8) | (r31 >> 8 & 0xFF)
+    assert _word(rs[C.REG_LO], C.RS_FIN_VAL) == want
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+@pytest.mark.parametrize("what", ["moved", "kept", "wsbh"])
+def test_movcond_tamper_rejected(shard, oracle, what):
+    m, prep, tr, pv = shard
+    bad = {k: v.copy() for k, v in tr.items()}
+    mc = bad["MovCond"]
+    if what == "moved":  # a MOVZ/MOVN that moved, with a different value in both the chip and the CPU
+        i = int(np.nonzero((mc[:, C.MC_MEQ] == 1) & (mc[:, C.MC_C0 + 10] == 1))[0][0])
+    elif what == "kept":
+        i = int(np.nonzero((mc[:, C.MC_MEQ] == 1) & (mc[:, C.MC_C0 + 10] == 0))[0][0])
+    else:
+        i = int(np.nonzero(mc[:, C.MC_WSBH])[0][0])
+    mc[i, C.MC_A] = (int(mc[i, C.MC_A]) + 1) % 256
+    assert _air_check.check(m, prep, bad, pv) != ([], [])
+    rc, proof = oracle.prove(bad, pv)
+    assert rc == 0 and oracle.verify(proof) != 0
+
+
 @pytest.mark.parametrize("what", ["quotient", "remainder_sign", "div_carry", "c_is_zero"])
 def test_divrem_tamper_rejected(shard, oracle, what):
     m, prep, tr, pv = shard
@@ -295,7 +334,7 @@ def test_mul_tamper_rejected(shard, oracle, what):
     m, prep, tr, pv = shard
     bad = {k: v.copy() for k, v in tr.items()}
     mu = bad["Mul"]
-    i = int(np.nonzero(mu[:, C.MU_MULT])[0][0])
+    i = int(np.nonzero(mu[:, C.MU_MULT] * mu[:, C.MU_HRR])[0][0])  # a CPU MULT (DivRem's have no HI record)
     if what == "carry":
         mu[i, C.MU_CARRY + 2] += 1
     elif what == "hi":  # a forged HI in both the chip and its register write

@@ -612,6 +612,50 @@ def _divrem_trace(divs, shard, byte_lookup):
     return t, q, r, abs_c, abs_r, ctq
 
 
+# ---------------------------------------------------------------- MovCond (misc/mov_cond)
+OP_MEQ, OP_MNE, OP_WSBH = 50, 51, 52  # MOVZ, MOVN, WSBH (executor/src/opcode.rs:70-72)
+MOVCOND_OPS = (OP_MEQ, OP_MNE, OP_WSBH)
+# MovCondCols (misc/mov_cond/mod.rs)
+MC_PC, MC_NPC, MC_A, MC_PREV_A, MC_B, MC_C, MC_C0, MC_MNE, MC_MEQ, MC_WSBH = 0, 1, 2, 6, 10, 14, 18, 29, 30, 31
+MC_WIDTH = 32
+
+
+def movcond_chip() -> ChipDesc:
+    """MovCondChip::eval + eval_wsbh (misc/mov_cond/mod.rs), constraints and lookups in its order."""
+    ch = ChipDesc("MovCond", prep_width=0, main_width=MC_WIDTH, local_only=True)
+    M = main
+    mne, meq, wsbh = M(MC_MNE), M(MC_MEQ), M(MC_WSBH)
+    is_real = mne + meq + wsbh
+    opcode = V([("main", MC_WSBH, OP_WSBH), ("main", MC_MEQ, OP_MEQ), ("main", MC_MNE, OP_MNE)])
+    ins = [ZERO, ZERO, _m(MC_PC), _m(MC_NPC), V([("main", MC_NPC, 1)], 4), ZERO, opcode]
+    ins += _vword(MC_A) + _vword(MC_B) + _vword(MC_C) + _vword(MC_PREV_A)
+    ins += [ZERO, V([("main", MC_MNE, 1), ("main", MC_MEQ, 1)]), ZERO, ZERO, V.const(1)]
+    ch.receives.append(Lookup(ins, V([("main", c, 1) for c in (MC_MNE, MC_MEQ, MC_WSBH)]), KIND_INSTRUCTION))
+    _is_zero_word(ch, [M(MC_C + i) for i in range(4)], MC_C0, is_real)
+    r = M(MC_C0 + 10)
+    for cond, src in ((meq * r, MC_B), (meq * (1 - r), MC_PREV_A), (mne * (1 - r), MC_B), (mne * r, MC_PREV_A)):
+        for i in range(4):
+            ch.assert_zero(cond * (M(MC_A + i) - M(src + i)))
+    for i, j in ((0, 1), (1, 0), (2, 3), (3, 2)):
+        ch.assert_zero(wsbh * (M(MC_A + i) - M(MC_B + j)))
+    for x in (mne, meq, wsbh, is_real):
+        _assert_bool(ch, x)
+    return ch
+
+
+def _movcond_trace(movs):
+    """MovCondChip::event_to_row (misc/mov_cond/mod.rs): (pc, npc, op, a, b, c, prev_a)."""
+    E = np.asarray(movs, np.int64).reshape(-1, 7)
+    n = len(E)
+    t = np.zeros((A._pow2(n), MC_WIDTH), np.uint32)
+    t[:n, MC_PC], t[:n, MC_NPC] = E[:, 0], E[:, 1]
+    for base, j in ((MC_A, 3), (MC_B, 4), (MC_C, 5), (MC_PREV_A, 6)):
+        t[:n, base:base + 4] = A._bytes(E[:, j].astype(np.uint32))
+    t[:n, MC_C0:MC_C0 + IZW_WIDTH] = _izw_cols(A._bytes(E[:, 5].astype(np.uint32)))
+    t[:n, MC_MEQ], t[:n, MC_MNE], t[:n, MC_WSBH] = E[:, 2] == OP_MEQ, E[:, 2] == OP_MNE, E[:, 2] == OP_WSBH
+    return t
+
+
 # ---------------------------------------------------------------- Jump (control_flow/jump)
 OP_JUMP, OP_JUMPI, OP_JUMPDIRECT = 27, 28, 29  # JR/JALR, J/JAL, BAL (executor/src/opcode.rs:45-47)
 JUMP_OPS = (OP_JUMP, OP_JUMPI, OP_JUMPDIRECT)
@@ -669,7 +713,7 @@ def core_machine() -> MachineDesc:
     # Byte; the memory stand-in last
     return MachineDesc([cpu_chip(), program_chip(), divrem_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
                         A.shift_right_chip(),
-                        A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(),
+                        A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(), movcond_chip(),
                         A.byte_chip(),
                         register_state_chip()], NUM_PV_ELTS)
 
@@ -681,7 +725,8 @@ def core_machine() -> MachineDesc:
 _MIX = [(A.OP_ADD, 0), (A.OP_ADD, 1), (A.OP_SUB, 0), (A.OP_AND, 0), (A.OP_AND, 1), (A.OP_OR, 0), (A.OP_OR, 1),
         (A.OP_XOR, 0), (A.OP_XOR, 1), (A.OP_NOR, 0), (A.OP_SLT, 0), (A.OP_SLT, 1), (A.OP_SLTU, 0),
         (A.OP_SLL, 1), (A.OP_SRL, 1), (A.OP_SRA, 1), (A.OP_ROR, 1), (A.OP_SRL, 0), (A.OP_CLZ, 1), (A.OP_CLO, 1),
-        (OP_MUL, 0), (OP_MULT, 0), (OP_MULTU, 0), (OP_DIV, 0), (OP_DIVU, 0), (OP_MOD, 0), (OP_MODU, 0)]
+        (OP_MUL, 0), (OP_MULT, 0), (OP_MULTU, 0), (OP_DIV, 0), (OP_DIVU, 0), (OP_MOD, 0), (OP_MODU, 0),
+        ("MFLO", 0), ("MFHI", 0), ("MTLO", 0), ("MTHI", 0), (OP_MEQ, 0), (OP_MNE, 0), (OP_WSBH, 1)]
 _KIND = {A.OP_ADD: "add", A.OP_SUB: "add", A.OP_AND: "bit", A.OP_OR: "bit", A.OP_XOR: "bit", A.OP_NOR: "bit",
          A.OP_SLT: "lt", A.OP_SLTU: "lt", A.OP_SLL: "sll", A.OP_SRL: "sr", A.OP_SRA: "sr", A.OP_ROR: "sr",
          A.OP_CLZ: "clz", A.OP_CLO: "clz"}
@@ -743,9 +788,12 @@ def _random_alu(r, avoid=()):
     regs = [x for x in range(32) if x not in avoid]
     ra = 0 if (r[4] % 16 == 0 and 0 not in avoid) else regs[1 + int(r[1] % (len(regs) - 1))]
     rb = int(r[2] % 32)
+    if isinstance(op, str):  # MFLO/MFHI rd = lo/hi; MTLO/MTHI lo/hi = rs: ADDs with register 32/33 (instruction.rs:387-394)
+        reg = REG_LO if op.endswith("LO") else REG_HI
+        return (A.OP_ADD, ra, reg, 0, 0, 1) if op.startswith("MF") else (A.OP_ADD, reg, rb, 0, 0, 1)
     if op in (OP_MULT, OP_MULTU, OP_DIV, OP_DIVU):  # MULT/DIV rs, rt: op_a = LO (instruction.rs:368-384)
         ra = REG_LO
-    if op in (A.OP_CLZ, A.OP_CLO):
+    if op in (A.OP_CLZ, A.OP_CLO, OP_WSBH):
         c = 0
     elif imm and op in (A.OP_SLL, A.OP_SRL, A.OP_SRA, A.OP_ROR):
         c = int(r[3] % 32)
@@ -848,7 +896,7 @@ def _execute(prog, regs, shard, max_steps):
     pc, npc = PC_BASE, PC_BASE + 4
     steps = []
     ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
-    branches, jumps, muls, divs = [], [], [], []
+    branches, jumps, muls, divs, movs = [], [], [], [], []
     U = A.UNUSED_PC
     while pc != end:
         assert PC_BASE <= pc < end and len(steps) < max_steps
@@ -903,6 +951,18 @@ def _execute(prog, regs, shard, max_steps):
             if ra:
                 regs[ra] = av
             nnpc = npc + 4
+        elif op in MOVCOND_OPS:  # execute_condmov / execute_wsbh (executor.rs:1782-1857)
+            if op == OP_WSBH:
+                av = (((bv >> 16) & 0xFF) << 24) | (((bv >> 24) & 0xFF) << 16) | ((bv & 0xFF) << 8) | ((bv >> 8) & 0xFF)
+                hi = 0
+            else:
+                av = bv if (cv == 0) == (op == OP_MEQ) else prev_a
+                hi = prev_a  # hi_or_prev_a
+            movs.append((pc, npc, op, av, bv, cv, hi))
+            written = av if ra else 0
+            if ra:
+                regs[ra] = av
+            nnpc = npc + 4
         elif op in DIV_OPS:  # the DivRem chip; the reference executor traps on c = 0, the AIR covers it
             q, r = _qr(op, bv, cv)
             if op in (OP_DIV, OP_DIVU):  # (LO, HI) = (quotient, remainder)
@@ -941,9 +1001,9 @@ def _execute(prog, regs, shard, max_steps):
             last[REG_HI] = (shard, clk + POS_HI)
             regs[REG_HI] = hi
         steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc,
-                      hi if op in MUL_OPS + DIV_OPS else 0))
+                      hi if op in MUL_OPS + DIV_OPS + MOVCOND_OPS else 0))
         pc, npc = npc, nnpc
-    return steps, ev, branches, jumps, muls, divs, last
+    return steps, ev, branches, jumps, muls, divs, movs, last
 
 
 def _ev_arrays(lst):
@@ -957,7 +1017,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     init = splitmix64(0x5EED000 + seed, NUM_REGS) & np.uint64(M32)
     regs = [0] + [int(x) for x in init[1:]]
     init_vals = list(regs)
-    steps, ev, branches, jumps, muls, divs, last = _execute(prog, regs, shard, max_steps)
+    steps, ev, branches, jumps, muls, divs, movs, last = _execute(prog, regs, shard, max_steps)
     n = len(steps)
     assert n > 0
     height = max(16, 1 << (n - 1).bit_length())
@@ -992,7 +1052,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     t[:n, C_NPC] = npc
     t[:n, C_NNPC] = nnpc
     t[:n, C_OPCODE:C_IMMC + 1] = instr_cols[ks]
-    t[:n, C_RW_A] = 0
+    t[:n, C_RW_A] = np.isin(ops, (OP_MEQ, OP_MNE))  # is_rw_a_instruction (instruction.rs:180-200)
     t[:n, C_SEQ] = is_seq
     his = np.asarray([s_[12] for s_ in steps], np.int64)
     mult_div = np.isin(ops, MULT_DIV)  # is_mult_div_instruction: check memory, send shard/clk
@@ -1033,6 +1093,8 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
         traces["Branch"] = _branch_trace(branches, byte_lookup)
     if jumps:
         traces["Jump"] = _jump_trace(jumps)
+    if movs:
+        traces["MovCond"] = _movcond_trace(movs)
     if divs:
         traces["DivRem"] = _divrem_trace(divs, shard, byte_lookup)[0]
     if muls:
