@@ -147,7 +147,7 @@ def main():
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
                          "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
                          "zkmips_amd/mips_alu.py), 2^(log-n) "
-                         "instructions per shard; core: Cpu + Program + Mul + DivRem + Branch + Jump + MovCond chips over the ALU slice "
+                         "instructions per shard; core: Cpu + Program + Mul + DivRem + Branch + Jump + MovCond + MemoryInstrs chips over the ALU slice "
                          "(zkmips_amd/mips_core.py) running a counted loop, Cpu 2^(log-n) rows")
     ap.add_argument("--queries", type=int, default=84)
     ap.add_argument("--cpu-log-n", type=int, default=18)
@@ -329,10 +329,10 @@ def main():
         "config": {"workload": (f"S-SHARD FibCpu 2^{args.log_n} rows (main 67, LogUp 11 EF, quotient 2) + FibTable "
                                 f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard")
                    if args.workload == "fib" else
-                   (f"MIPS core shard: a counted loop (60-instruction body of ALU ops, forward branches, jal/jalr calls "
+                   (f"MIPS core shard: a counted loop (60-instruction body of ALU and load/store ops, forward branches, jal/jalr calls "
                     f"of a subroutine, bal) "
                     f"executed to {int(traces['Cpu'][:, 65].sum())} instructions: Cpu 2^{args.log_n} (main 67, "
-                    f"LogUp 11 EF) + Program (prep 14) + DivRem, AddSub, Bitwise, Mul, Lt, ShiftLeft, ShiftRight, CloClz, MovCond, "
+                    f"LogUp 11 EF) + Program (prep 14) + DivRem, AddSub, Bitwise, Mul, Lt, ShiftLeft, ShiftRight, CloClz, MovCond, MemoryInstrs, "
                     f"Branch, Jump + Byte 2^16 (prep 12) + RegisterState: full commit+open per shard")
                    if args.workload == "core" else
                    (f"MIPS ALU slice: InstrSource 2^{args.log_n} + AddSub, Bitwise, Lt 2^{args.log_n - 2} + ShiftLeft, "

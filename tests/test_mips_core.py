@@ -199,8 +199,10 @@ def test_core_register_chain(shard):
     last access is what that row sends (the memory argument closes inside the shard)."""
     _, _, tr, _ = shard
     rs = tr["RegisterState"]
-    assert rs.shape[0] == 64 and list(rs[:C.NUM_REGS, C.RS_ADDR]) == list(range(C.NUM_REGS))  # + LO, HI
-    assert rs[:C.NUM_REGS, C.RS_REAL].all() and not rs[C.NUM_REGS:].any()
+    assert list(rs[:C.NUM_REGS, C.RS_ADDR]) == list(range(C.NUM_REGS))  # 32 GPRs + LO, HI
+    words = rs[C.NUM_REGS:][rs[C.NUM_REGS:, C.RS_REAL] == 1, C.RS_ADDR]  # then the data words touched
+    assert len(words) and (words >= C.DATA_BASE).all() and (np.diff(words.astype(np.int64)) > 0).all()
+    assert rs[:C.NUM_REGS, C.RS_REAL].all() and not rs[C.NUM_REGS + len(words):].any()
     assert (rs[:, C.RS_FIN_CLK] <= 5 * 699 + C.POS_HI).all() and rs[0, C.RS_INIT_VAL:C.RS_INIT_VAL + 4].sum() == 0
 
 
@@ -289,6 +291,141 @@ def test_movcond_reference_fixture():
     o = O.OracleProver(m, prep, num_queries=8)
     rc, proof = o.prove(tr, pv)
     assert rc == 0 and o.verify(proof) == 0
+
+
+_ADD = A.OP_ADD
+# crates/core/machine/src/programs.rs:126-196 and mips/mod.rs:1042-1054 (Instruction::new(op, a, b, c, imm_b, imm_c))
+SIMPLE_MEMORY_PROGRAM = [
+    (_ADD, 29, 0, 0x12348765, 0, 1), (C.OP_SW, 29, 0, 0x27654320, 0, 1), (C.OP_LW, 28, 0, 0x27654320, 0, 1),
+    (C.OP_LBU, 27, 0, 0x27654320, 0, 1), (C.OP_LBU, 26, 0, 0x27654321, 0, 1), (C.OP_LBU, 25, 0, 0x27654322, 0, 1),
+    (C.OP_LBU, 24, 0, 0x27654323, 0, 1), (C.OP_LB, 23, 0, 0x27654320, 0, 1), (C.OP_LB, 22, 0, 0x27654321, 0, 1),
+    (C.OP_LHU, 21, 0, 0x27654320, 0, 1), (C.OP_LHU, 20, 0, 0x27654322, 0, 1), (C.OP_LH, 19, 0, 0x27654320, 0, 1),
+    (C.OP_LH, 18, 0, 0x27654322, 0, 1), (_ADD, 17, 0, 0x38276525, 0, 1), (C.OP_SW, 29, 0, 0x43627530, 0, 1),
+    (C.OP_SB, 17, 0, 0x43627530, 0, 1), (C.OP_LW, 16, 0, 0x43627530, 0, 1), (C.OP_SB, 17, 0, 0x43627531, 0, 1),
+    (C.OP_LW, 15, 0, 0x43627530, 0, 1), (C.OP_SB, 17, 0, 0x43627532, 0, 1), (C.OP_LW, 14, 0, 0x43627530, 0, 1),
+    (C.OP_SB, 17, 0, 0x43627533, 0, 1), (C.OP_LW, 13, 0, 0x43627530, 0, 1), (C.OP_SW, 29, 0, 0x43627530, 0, 1),
+    (C.OP_SH, 17, 0, 0x43627530, 0, 1), (C.OP_LW, 12, 0, 0x43627530, 0, 1), (C.OP_SH, 17, 0, 0x43627532, 0, 1),
+    (C.OP_LW, 11, 0, 0x43627530, 0, 1)]
+OTHER_MEMORY_PROGRAM = [
+    (_ADD, 29, 0, (1 << 20) + (1 << 15) + (1 << 6) - 1, 0, 1), (_ADD, 27, 0, 3325, 0, 1),
+    (_ADD, 25, 0, (1 << 28) + (1 << 12) + (1 << 18) - 1, 0, 1), (_ADD, 17, 0, 0x43627530, 0, 1),
+    (_ADD, 22, 0, 80, 0, 1), (_ADD, 10, 0, 100, 0, 1), (C.OP_LWR, 29, 27, 1, 0, 1), (C.OP_LWL, 29, 27, 1, 0, 1),
+    (C.OP_LL, 29, 27, 3, 0, 1), (_ADD, 15, 0, (1 << 20) + (1 << 15) + (1 << 6) - 1, 0, 1),
+    (C.OP_SWL, 15, 22, 2, 0, 1), (C.OP_SWR, 15, 22, 2, 0, 1), (C.OP_SWL, 26, 10, 2, 0, 1),
+    (C.OP_SWR, 26, 10, 2, 0, 1), (C.OP_LWR, 29, 27, 0, 0, 1), (C.OP_LWL, 29, 27, 0, 0, 1)]
+SC_PROGRAM = [(_ADD, 29, 0, 0x12348765, 0, 1), (C.OP_SW, 29, 0, 0x27654320, 0, 1), (C.OP_LL, 28, 0, 0x27654320, 0, 1),
+              (_ADD, 28, 28, 1, 0, 1), (C.OP_SC, 28, 0, 0x27654320, 0, 1), (C.OP_LW, 29, 0, 0x27654320, 0, 1)]
+
+
+def _reference_alu_fixtures():
+    """The straight-line programs of the reference's per-instruction tests (core/machine/src/mips/mod.rs:
+    test_simple_prove, test_shift_prove, test_sub/add/add_overflow_prove, test_mul_mod_prove,
+    test_mult_div_prove, test_lt_prove, test_bitwise_prove, test_divrem_prove, test_cloclz_prove)."""
+    M32 = C.M32
+    progs = [[(_ADD, 29, 0, 5, 0, 1), (_ADD, 30, 0, 37, 0, 1), (_ADD, 31, 30, 29, 0, 0)]]
+    pairs = [(1, 1), (1234, 5678), (0xFFFF, 0xFFFF - 1), (M32 - 1, M32), (M32, 0)]
+    for op in (A.OP_SRL, A.OP_ROR, A.OP_SRA, A.OP_SLL):
+        progs += [[(_ADD, 29, 0, b, 0, 1), (_ADD, 30, 0, c, 0, 1), (op, 31, 29, 3, 0, 0)] for b, c in pairs]
+    for op, b in ((A.OP_SUB, 5), (_ADD, 5), (_ADD, 0xEFFFFFFF)):
+        progs.append([(_ADD, 29, 0, b, 0, 1), (_ADD, 30, 0, 8 if b == 5 else 2, 0, 1), (op, 31, 30, 29, 0, 0)])
+    pairs = [(1, 1), (1234, 5678), (8765, 4321), (0xFFFF, 0xFFFF - 1), (M32 - 1, M32)]
+    for op in (C.OP_MUL, C.OP_MOD, C.OP_MODU):
+        progs += [[(_ADD, 29, 0, b, 0, 1), (_ADD, 30, 0, c, 0, 1), (op, 31, 30, 29, 0, 0)] for b, c in pairs]
+    for op in (C.OP_MULT, C.OP_MULTU, C.OP_DIV, C.OP_DIVU):
+        progs += [[(_ADD, 29, 0, b, 0, 1), (_ADD, 30, 0, c, 0, 1), (op, 32, 30, 29, 0, 0)] for b, c in pairs]
+    for op in (A.OP_SLT, A.OP_SLTU, A.OP_XOR, A.OP_OR, A.OP_AND):
+        progs.append([(_ADD, 29, 0, 5, 0, 1), (_ADD, 30, 0, 8, 0, 1), (op, 31, 30, 29, 0, 0)])
+    pairs = [(1, 1), (123, 456 * 789), (123 * 456, 789), (0xFFFF * (0xFFFF - 1), 0xFFFF), (M32 - 5, M32 - 7)]
+    for op in (C.OP_DIV, C.OP_DIVU):
+        progs += [[(_ADD, 29, 0, b, 0, 1), (_ADD, 30, 0, c, 0, 1), (op, 32, 29, 30, 0, 0)] for b, c in pairs]
+    for op in (A.OP_CLZ, A.OP_CLO):
+        progs += [[(_ADD, 29, 0, v, 0, 1), (op, 30, 29, 0, 0, 1)]
+                  for v in (0, 0x0A0B0C0D, 0x1000, 0xFF7FFFFF, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFF)]
+    return progs
+
+
+def _reference_control_fixtures():
+    """test_beq/bne_(not_)branching_prove, test_rest_branch_prove, test_j/jr/jal/jalr_prove
+    (core/machine/src/mips/mod.rs:751-1039): each leaves the program through its branch or jump."""
+    progs = [[(_ADD, 29, 0, x, 0, 1), (_ADD, 30, 0, y, 0, 1), (op, 29, 30, 100, 0, 1)]
+             for op, x, y in ((C.OP_BEQ, 1, 1), (C.OP_BEQ, 1, 2), (C.OP_BNE, 1, 2), (C.OP_BNE, 0, 0))]
+    for op in (C.OP_BLTZ, C.OP_BGEZ, C.OP_BLEZ, C.OP_BGTZ):
+        progs += [[(_ADD, 29, 0, v, 0, 1), (op, 29, 0, 100, 1, 1)] for v in (0, 1, C.M32)]
+    progs += [[(_ADD, 11, 0, 100, 0, 1), (C.OP_JUMPI, 0, 100, 0, 1, 1)],
+              [(_ADD, 11, 0, 100, 0, 1), (C.OP_JUMP, 0, 11, 0, 0, 1)],
+              [(_ADD, 31, 0, 0, 0, 1), (C.OP_JUMPI, 31, 100, 0, 1, 1)],
+              [(_ADD, 5, 0, 0, 0, 1), (_ADD, 11, 11, 100, 0, 1), (C.OP_JUMP, 5, 11, 0, 0, 1)]]
+    return progs
+
+
+def test_reference_instruction_programs():
+    """All straight-line programs of the reference's per-instruction tests, run back to back in one shard."""
+    prog = [ins for p in _reference_alu_fixtures() for ins in p]
+    m, prep, tr, pv = C.program_shard(prog, seed=6)
+    assert int(tr["Cpu"][:, C.C_REAL].sum()) == len(prog)
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+@pytest.mark.parametrize("k", range(20))
+def test_reference_control_programs(k):
+    prog = _reference_control_fixtures()[k]
+    m, prep, tr, pv = C.program_shard(prog, seed=k)
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+def _final(tr, addr):
+    rs = tr["RegisterState"]
+    i = int(np.nonzero((rs[:, C.RS_ADDR] == addr) & (rs[:, C.RS_REAL] == 1))[0][0])
+    return _word(rs[i], C.RS_FIN_VAL)
+
+
+@pytest.mark.parametrize("name", ["simple_memory", "other_memory", "sc"])
+def test_memory_reference_programs(name):
+    """The reference's own memory-instruction programs (programs.rs simple_memory_program /
+    other_memory_program, mips/mod.rs test_sc_prove) prove and verify through the MemoryInstrs chip."""
+    prog = {"simple_memory": SIMPLE_MEMORY_PROGRAM, "other_memory": OTHER_MEMORY_PROGRAM, "sc": SC_PROGRAM}[name]
+    m, prep, tr, pv = C.program_shard(prog, seed=1)
+    if name == "simple_memory":
+        assert [_final(tr, r) for r in (28, 27, 26, 25, 24)] == [0x12348765, 0x65, 0x87, 0x34, 0x12]
+        assert [_final(tr, r) for r in (23, 22, 21, 20, 19, 18)] == [0x65, 0xFFFFFF87, 0x8765, 0x1234, 0xFFFF8765,
+                                                                      0x1234]
+        assert [_final(tr, r) for r in (16, 15, 14, 13)] == [0x12348725, 0x12342525, 0x12252525, 0x25252525]
+        assert [_final(tr, r) for r in (12, 11)] == [0x12346525, 0x65256525]
+    elif name == "sc":
+        assert _final(tr, 28) == 1 and _final(tr, 29) == 0x12348766 and _final(tr, 0x27654320) == 0x12348766
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+@pytest.mark.parametrize("what", ["load_value", "store_merge", "memory_final", "address"])
+def test_memory_tamper_rejected(shard, oracle, what):
+    m, prep, tr, pv = shard
+    bad = {k: v.copy() for k, v in tr.items()}
+    mi = bad["MemoryInstrs"]
+    if what == "load_value":  # an LW that returns something else than the word in memory
+        i = int(np.nonzero(mi[:, C.MI_SEL + 4])[0][0])
+        mi[i, C.MI_UMV] = (int(mi[i, C.MI_UMV]) + 1) % 256
+        mi[i, C.MI_A] = mi[i, C.MI_UMV]
+    elif what == "store_merge":  # an SB that also changes a neighbouring byte
+        i = int(np.nonzero(mi[:, C.MI_SEL + 8])[0][0])
+        j = (int(mi[i, C.MI_LS2]) + 1) % 4
+        mi[i, C.MI_ACC + 4 + j] = (int(mi[i, C.MI_ACC + 4 + j]) + 1) % 256
+    elif what == "memory_final":  # the memory argument's closing value of a data word
+        rs = bad["RegisterState"]
+        rs[C.NUM_REGS + 1, C.RS_FIN_VAL] ^= 1
+    else:  # the access goes to another word than b + c
+        mi[3, C.MI_ALIGNED] += 4
+    assert _air_check.check(m, prep, bad, pv) != ([], [])
+    rc, proof = oracle.prove(bad, pv)
+    assert rc == 0 and oracle.verify(proof) != 0
 
 
 @pytest.mark.parametrize("what", ["moved", "kept", "wsbh"])
@@ -398,6 +535,22 @@ def test_core_gpu_proof_bytes_identical(dev, n, seed):
     rc, ref = cpu.prove(tr, pv)
     assert rc == 0 and proof == ref
     assert cpu.verify(proof) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["alu_fixtures", "simple_memory", "other_memory", "sc", "jalr"])
+def test_reference_programs_gpu_proof_bytes_identical(dev, name):
+    """The reference's own instruction-test programs: GPU proof bytes == oracle proof bytes."""
+    from zkmips_amd.prover import HipProver
+    prog = {"alu_fixtures": [ins for p in _reference_alu_fixtures() for ins in p],
+            "simple_memory": SIMPLE_MEMORY_PROGRAM, "other_memory": OTHER_MEMORY_PROGRAM, "sc": SC_PROGRAM,
+            "jalr": _reference_control_fixtures()[-1]}[name]
+    m, prep, tr, pv = C.program_shard(prog, seed=6)
+    gpu = HipProver(dev, m, prep, num_queries=16)
+    cpu = O.OracleProver(m, prep, num_queries=16)
+    proof = gpu.prove_shard(tr, pv)
+    rc, ref = cpu.prove(tr, pv)
+    assert rc == 0 and proof == ref and cpu.verify(proof) == 0
 
 
 @pytest.mark.gpu

@@ -656,6 +656,219 @@ def _movcond_trace(movs):
     return t
 
 
+# ---------------------------------------------------------------- MemoryInstrs (memory/instructions)
+OP_LB, OP_LBU, OP_LH, OP_LHU, OP_LW, OP_LWL, OP_LWR, OP_LL = range(31, 39)  # executor/src/opcode.rs:50-63
+OP_SB, OP_SH, OP_SW, OP_SWL, OP_SWR, OP_SC = range(39, 45)
+LOAD_OPS, STORE_OPS = tuple(range(31, 39)), tuple(range(39, 45))
+MEM_OPS = LOAD_OPS + STORE_OPS
+REF_NUM_REGISTERS = 36  # executor/src/register.rs:3: data addresses start above the register file
+DATA_BASE = 0x00010000
+# MemoryInstructionsColumns (memory/instructions/columns.rs:15-103); selectors in opcode order
+MI_PC, MI_NPC, MI_SHARD, MI_CLK, MI_A, MI_B, MI_C, MI_SEL = 0, 1, 2, 3, 4, 8, 12, 16
+MI_ADDR, MI_ALIGNED, MI_LS2, MI_L1, MI_L2, MI_L3, MI_ADDR_RC, MI_ACC = 30, 34, 35, 36, 37, 38, 39, 53
+MI_PREV_A, MI_UMV, MI_MSBIT, MI_MSBYTE, MI_NEG, MI_MSBZ = 66, 70, 74, 75, 76, 77
+MI_WIDTH = 79
+
+
+def memory_instructions_chip() -> ChipDesc:
+    """MemoryInstructionsChip::eval (memory/instructions/air.rs:23-519): address = b + c through the ADD
+    table, word range and register-file checks, offset flags, the memory access at the aligned address,
+    load extraction (LB/LBU/LH/LHU/LW/LWL/LWR/LL with the SUB that sign-extends) and store merging
+    (SB/SH/SW/SWL/SWR/SC), constraints and lookups in the reference's order."""
+    ch = ChipDesc("MemoryInstrs", prep_width=0, main_width=MI_WIDTH, local_only=True)
+    M = main
+    sel = [M(MI_SEL + k) for k in range(14)]
+    lb, lbu, lh, lhu, lw, lwl, lwr, ll, sb, sh, sw, swl, swr, sc = sel
+    is_real = sum(sel[1:], sel[0])
+    real_v = V([("main", MI_SEL + k, 1) for k in range(14)])
+    for x in sel:
+        _assert_bool(ch, x)
+    _assert_bool(ch, is_real)
+    # eval_memory_address_and_access (:129-225)
+    _send_alu(ch, A.OP_ADD, _vword(MI_ADDR), _vword(MI_B), _vword(MI_C), real_v)
+    _word_range_check(ch, MI_ADDR, MI_ADDR_RC, is_real)
+    ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, _m(MI_ADDR + 1), _m(MI_ADDR + 2)], real_v, KIND_BYTE))
+    ch.sends.append(Lookup([V.const(A.B_LTU), V.const(1), ZERO, V.const(REF_NUM_REGISTERS - 1), _m(MI_ADDR)],
+                           _m(MI_MSBZ + 1), KIND_BYTE))
+    res = M(MI_MSBZ + 1)
+    ch.assert_zero(res * (is_real - 1))
+    x = M(MI_ADDR + 1) + M(MI_ADDR + 2) + M(MI_ADDR + 3)
+    ch.assert_zero(is_real * ((1 - M(MI_MSBZ) * x) - res))  # IsZeroOperation (operations/is_zero.rs:47-66)
+    _assert_bool(ch, res, is_real)
+    ch.assert_zero(is_real * res * x)
+    l1, l2, l3, two = M(MI_L1), M(MI_L2), M(MI_L3), M(MI_LS2)
+    oz = 1 - l1 - l2 - l3
+    for f in (l1, l2, l3, oz):  # eval_offset_value_flags (:496-519)
+        _assert_bool(ch, f)
+    ch.assert_zero(oz * two)
+    ch.assert_zero(l1 * (two - 1))
+    ch.assert_zero(l2 * (two - 2))
+    ch.assert_zero(l3 * (two - 3))
+    red = sum((M(MI_ADDR + i) * (1 << (8 * i)) for i in range(1, 4)), M(MI_ADDR))
+    ch.assert_zero(is_real * ((M(MI_ALIGNED) + two) - red))
+    ch.sends.append(Lookup([V.const(A.B_AND), _m(MI_LS2), ZERO, _m(MI_ADDR), V.const(3)], real_v, KIND_BYTE))
+    _eval_memory_access(ch, MI_ACC + 4, MI_ACC, 0, _m(MI_ALIGNED), is_real, real_v, shard_col=MI_SHARD,
+                        clk_terms=((MI_CLK, 1),))
+    mem = [M(MI_ACC + 4 + i) for i in range(4)]
+    pm = [M(MI_ACC + i) for i in range(4)]
+    loads = lb + lbu + lh + lhu + lw + lwl + lwr + ll
+    for i in range(4):
+        ch.assert_zero(loads * (mem[i] - pm[i]))
+    # eval_memory_load / eval_unsigned_mem_value (:228-284, :402-493)
+    umv = [M(MI_UMV + i) for i in range(4)]
+    pa = [M(MI_PREV_A + i) for i in range(4)]
+    a = [M(MI_A + i) for i in range(4)]
+    byte_value = [mem[0] * oz + mem[1] * l1 + mem[2] * l2 + mem[3] * l3, 0, 0, 0]
+    for i in range(4):
+        ch.assert_zero((lb + lbu) * (byte_value[i] - umv[i]))
+    ch.assert_zero((lh + lhu) * (l1 + l3))
+    ch.assert_zero(lw * (oz - 1))
+    half = [oz * mem[0] + l2 * mem[2], oz * mem[1] + l2 * mem[3], 0, 0]
+    for i in range(4):
+        ch.assert_zero((lh + lhu) * (half[i] - umv[i]))
+    for i in range(4):
+        ch.assert_zero(lw * (mem[i] - umv[i]))
+    lwr_v = [mem[0] * oz + mem[1] * l1 + mem[2] * l2 + mem[3] * l3,
+             mem[1] * oz + mem[2] * l1 + mem[3] * l2 + pa[1] * l3,
+             mem[2] * oz + mem[3] * l1 + pa[2] * (1 - l1 - oz),
+             mem[3] * oz + pa[3] * (1 - oz)]
+    for i in range(4):
+        ch.assert_zero(lwr * (umv[i] - lwr_v[i]))
+    lwl_v = [mem[0] * l3 + pa[0] * (1 - l3),
+             mem[1] * l3 + mem[0] * l2 + pa[1] * l1 + pa[1] * oz,
+             mem[2] * l3 + mem[1] * l2 + mem[0] * l1 + pa[2] * oz,
+             mem[3] * l3 + mem[2] * l2 + mem[1] * l1 + mem[0] * oz]
+    for i in range(4):
+        ch.assert_zero(lwl * (umv[i] - lwl_v[i]))
+    for i in range(4):
+        ch.assert_zero(ll * (umv[i] - mem[i]))
+    ch.assert_zero(ll * (oz - 1))
+    neg = M(MI_NEG)
+    ch.assert_zero(neg - (lb + lh) * M(MI_MSBIT))
+    ch.sends.append(Lookup([V.const(A.B_MSB), _m(MI_MSBIT), ZERO, _m(MI_MSBYTE), ZERO],
+                           V([("main", MI_SEL + 0, 1), ("main", MI_SEL + 2, 1)]), KIND_BYTE))
+    ch.assert_zero(M(MI_MSBYTE) - (lb * umv[0] + lh * umv[1]))
+    _send_alu(ch, A.OP_SUB, _vword(MI_A), _vword(MI_UMV), [ZERO, _m(MI_SEL + 0), _m(MI_SEL + 2), ZERO], _m(MI_NEG))
+    pos = (lb + lh - neg) + lbu + lhu + lw + ll + lwl + lwr
+    for i in range(4):
+        ch.assert_zero(pos * (umv[i] - a[i]))
+    # eval_memory_store (:287-398)
+    sb_v = [a[0] * oz + (1 - oz) * pm[0], a[0] * l1 + (1 - l1) * pm[1], a[0] * l2 + (1 - l2) * pm[2],
+            a[0] * l3 + (1 - l3) * pm[3]]
+    for i in range(4):
+        ch.assert_zero(sb * (mem[i] - sb_v[i]))
+    ch.assert_zero(sh * (l1 + l3))
+    ch.assert_zero(sw * (oz - 1))
+    sh_v = [a[0] * oz + (1 - oz) * pm[0], a[1] * oz + (1 - oz) * pm[1], a[0] * l2 + (1 - l2) * pm[2],
+            a[1] * l2 + (1 - l2) * pm[3]]
+    for i in range(4):
+        ch.assert_zero(sh * (mem[i] - sh_v[i]))
+    for i in range(4):
+        ch.assert_zero(sw * (mem[i] - a[i]))
+    swl_v = [a[3] * oz + a[2] * l1 + a[1] * l2 + a[0] * l3,
+             pm[1] * oz + a[3] * l1 + a[2] * l2 + a[1] * l3,
+             pm[2] * (oz + l1) + a[3] * l2 + a[2] * l3,
+             pm[3] * (1 - l3) + a[3] * l3]
+    for i in range(4):
+        ch.assert_zero(swl * (mem[i] - swl_v[i]))
+    swr_v = [a[0] * oz + pm[0] * (1 - oz),
+             a[1] * oz + a[0] * l1 + pm[1] * (l2 + l3),
+             a[2] * oz + a[1] * l1 + a[0] * l2 + pm[2] * l3,
+             a[3] * oz + a[2] * l1 + a[1] * l2 + a[0] * l3]
+    for i in range(4):
+        ch.assert_zero(swr * (mem[i] - swr_v[i]))
+    ch.assert_zero(sc * (oz - 1))
+    for i in range(4):
+        ch.assert_zero(sc * (pa[i] - mem[i]))
+    ch.assert_zero(sc * (a[0] - 1))
+    for i in (1, 2, 3):
+        ch.assert_zero(sc * a[i])
+    opcode = V([("main", MI_SEL + k, 31 + k) for k in range(14)])
+    ins = [_m(MI_SHARD), _m(MI_CLK), _m(MI_PC), _m(MI_NPC), V([("main", MI_NPC, 1)], 4), ZERO, opcode]
+    ins += _vword(MI_A) + _vword(MI_B) + _vword(MI_C) + _vword(MI_PREV_A)
+    ins += [V([("main", MI_SEL + k, 1) for k in range(8, 13)]), V.const(1), V.const(1), ZERO, V.const(1)]
+    ch.receives.append(Lookup(ins, real_v, KIND_INSTRUCTION))
+    return ch
+
+
+def _load_value(op, mem, two, rt):
+    """execute_load's value (executor/src/executor.rs:1953-2005); `two` = addr & 3."""
+    if op in (OP_LB, OP_LBU):
+        v = (mem >> (8 * two)) & 0xFF
+        return (v - 256) & M32 if op == OP_LB and v >> 7 else v
+    if op in (OP_LH, OP_LHU):
+        v = (mem >> (8 * (two & 2))) & 0xFFFF
+        return (v - 65536) & M32 if op == OP_LH and v >> 15 else v
+    if op == OP_LWL:
+        sh = 24 - 8 * two
+        return (rt & ~((M32 << sh) & M32) & M32) | ((mem << sh) & M32)
+    if op == OP_LWR:
+        sh = 8 * two
+        return (rt & ~(M32 >> sh) & M32) | (mem >> sh)
+    return mem  # LW, LL
+
+
+def _store_value(op, mem, two, rt):
+    """execute_store's merged word (executor/src/executor.rs:2029-2079)."""
+    if op == OP_SB:
+        return (mem & (M32 ^ (0xFF << (8 * two)))) | ((rt & 0xFF) << (8 * two))
+    if op == OP_SH:
+        s = 8 * (two & 2)
+        return (mem & (M32 ^ (0xFFFF << s))) | ((rt & 0xFFFF) << s)
+    if op == OP_SWL:
+        sh = 24 - 8 * two
+        return (mem & ~(M32 >> sh) & M32) | (rt >> sh)
+    if op == OP_SWR:
+        sh = 8 * two
+        return (mem & ~((M32 << sh) & M32) & M32) | ((rt << sh) & M32)
+    return rt  # SW, SC
+
+
+def _mem_instr_trace(mevs, shard, byte_lookup):
+    """MemoryInstructionsChip::event_to_row (memory/instructions/trace.rs:88-251).  mevs: (pc, npc, op, a,
+    b, c, prev_a, clk, addr, prev_mem, mem, mem_prev_shard, mem_prev_clk)."""
+    E = np.asarray(mevs, np.int64).reshape(-1, 13)
+    n = len(E)
+    t = np.zeros((A._pow2(n), MI_WIDTH), np.uint32)
+    u = lambda v: v.astype(np.uint32)
+    pc, npc, op, a, b, c, prev_a, clk, addr, pmem, nmem = (E[:, j] for j in range(11))
+    t[:n, MI_PC], t[:n, MI_NPC], t[:n, MI_SHARD], t[:n, MI_CLK] = pc, npc, shard, clk
+    for base, v in ((MI_A, a), (MI_B, b), (MI_C, c), (MI_PREV_A, prev_a), (MI_ADDR, addr), (MI_ACC, pmem)):
+        t[:n, base:base + 4] = A._bytes(u(v))
+    for k in range(14):
+        t[:n, MI_SEL + k] = op == 31 + k
+    two = addr & 3
+    t[:n, MI_ALIGNED] = addr - two
+    t[:n, MI_LS2] = two
+    t[:n, MI_L1], t[:n, MI_L2], t[:n, MI_L3] = two == 1, two == 2, two == 3
+    t[:n, MI_ADDR_RC:MI_ADDR_RC + RC_WIDTH] = _range_checker_cols(u(addr))
+    _access_cols(t, np.arange(n), MI_ACC + 4, u(nmem), E[:, 11:13], shard, clk, np.ones(n, bool), byte_lookup)
+    ab = A._bytes(u(addr)).astype(np.int64)
+    byte_lookup(A.B_AND, ab[:, 0], np.full(n, 3))
+    ld = np.isin(op, LOAD_OPS)
+    mb = A._bytes(u(pmem)).astype(np.int64)
+    byte_ = mb[np.arange(n), two]
+    half = np.where((two >> 1) & 1, pmem >> 16, pmem & 0xFFFF)
+    umv = np.select([np.isin(op, (OP_LB, OP_LBU)), np.isin(op, (OP_LH, OP_LHU)), np.isin(op, (OP_LWL, OP_LWR))],
+                    [byte_, half, a], pmem)
+    umv = np.where(ld, umv, 0)
+    t[:n, MI_UMV:MI_UMV + 4] = A._bytes(u(umv))
+    signed = np.isin(op, (OP_LB, OP_LH))
+    msbyte = np.where(op == OP_LB, umv & 0xFF, (umv >> 8) & 0xFF)
+    msbit = msbyte >> 7
+    t[:n, MI_MSBYTE] = np.where(signed, msbyte, 0)
+    t[:n, MI_MSBIT] = np.where(signed, msbit, 0)
+    t[:n, MI_NEG] = signed & (msbit == 1)
+    byte_lookup(A.B_MSB, msbyte[signed], np.zeros(int(signed.sum()), np.int64))
+    byte_lookup(A.B_U8RANGE, ab[:, 1], ab[:, 2])
+    s = ab[:, 1] + ab[:, 2] + ab[:, 3]
+    t[:n, MI_MSBZ] = np.asarray([pow(int(x), P - 2, P) if x else 0 for x in s], np.int64)
+    t[:n, MI_MSBZ + 1] = s == 0
+    z = s == 0
+    byte_lookup(A.B_LTU, np.full(int(z.sum()), REF_NUM_REGISTERS - 1), ab[z, 0])
+    return t
+
+
 # ---------------------------------------------------------------- Jump (control_flow/jump)
 OP_JUMP, OP_JUMPI, OP_JUMPDIRECT = 27, 28, 29  # JR/JALR, J/JAL, BAL (executor/src/opcode.rs:45-47)
 JUMP_OPS = (OP_JUMP, OP_JUMPI, OP_JUMPDIRECT)
@@ -713,7 +926,8 @@ def core_machine() -> MachineDesc:
     # Byte; the memory stand-in last
     return MachineDesc([cpu_chip(), program_chip(), divrem_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
                         A.shift_right_chip(),
-                        A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(), movcond_chip(),
+                        A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(), memory_instructions_chip(),
+                        movcond_chip(),
                         A.byte_chip(),
                         register_state_chip()], NUM_PV_ELTS)
 
@@ -727,6 +941,7 @@ _MIX = [(A.OP_ADD, 0), (A.OP_ADD, 1), (A.OP_SUB, 0), (A.OP_AND, 0), (A.OP_AND, 1
         (A.OP_SLL, 1), (A.OP_SRL, 1), (A.OP_SRA, 1), (A.OP_ROR, 1), (A.OP_SRL, 0), (A.OP_CLZ, 1), (A.OP_CLO, 1),
         (OP_MUL, 0), (OP_MULT, 0), (OP_MULTU, 0), (OP_DIV, 0), (OP_DIVU, 0), (OP_MOD, 0), (OP_MODU, 0),
         ("MFLO", 0), ("MFHI", 0), ("MTLO", 0), ("MTHI", 0), (OP_MEQ, 0), (OP_MNE, 0), (OP_WSBH, 1)]
+_MIX += [(op, 1) for op in MEM_OPS]
 _KIND = {A.OP_ADD: "add", A.OP_SUB: "add", A.OP_AND: "bit", A.OP_OR: "bit", A.OP_XOR: "bit", A.OP_NOR: "bit",
          A.OP_SLT: "lt", A.OP_SLTU: "lt", A.OP_SLL: "sll", A.OP_SRL: "sr", A.OP_SRA: "sr", A.OP_ROR: "sr",
          A.OP_CLZ: "clz", A.OP_CLO: "clz"}
@@ -791,6 +1006,15 @@ def _random_alu(r, avoid=()):
     if isinstance(op, str):  # MFLO/MFHI rd = lo/hi; MTLO/MTHI lo/hi = rs: ADDs with register 32/33 (instruction.rs:387-394)
         reg = REG_LO if op.endswith("LO") else REG_HI
         return (A.OP_ADD, ra, reg, 0, 0, 1) if op.startswith("MF") else (A.OP_ADD, reg, rb, 0, 0, 1)
+    if op in MEM_OPS:  # base r0 + offset into a 256-byte data window, so words are re-read and re-written
+        sub = int((r[3] >> np.uint64(8)) % 4)
+        if op in (OP_LW, OP_LL, OP_SW, OP_SC):
+            sub = 0
+        elif op in (OP_LH, OP_LHU, OP_SH):
+            sub &= 2
+        if op in STORE_OPS and op != OP_SC:
+            ra = int(r[1] % 32)  # the stored register is only read
+        return (op, ra, 0, DATA_BASE + 4 * int(r[3] % 64) + sub, 0, 1)
     if op in (OP_MULT, OP_MULTU, OP_DIV, OP_DIVU):  # MULT/DIV rs, rt: op_a = LO (instruction.rs:368-384)
         ra = REG_LO
     if op in (A.OP_CLZ, A.OP_CLO, OP_WSBH):
@@ -896,10 +1120,11 @@ def _execute(prog, regs, shard, max_steps):
     pc, npc = PC_BASE, PC_BASE + 4
     steps = []
     ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
-    branches, jumps, muls, divs, movs = [], [], [], [], []
+    branches, jumps, muls, divs, movs, mevs = [], [], [], [], [], []
+    mem, mem_init, mem_last = {}, {}, {}
     U = A.UNUSED_PC
-    while pc != end:
-        assert PC_BASE <= pc < end and len(steps) < max_steps
+    while PC_BASE <= pc < end:  # the program halts when pc leaves it
+        assert len(steps) < max_steps
         k = (pc - PC_BASE) >> 2
         op, ra, rb, c, immb, immc = prog[k]
         clk = 5 * len(steps)
@@ -951,6 +1176,41 @@ def _execute(prog, regs, shard, max_steps):
             if ra:
                 regs[ra] = av
             nnpc = npc + 4
+        elif op in MEM_OPS:  # execute_load / execute_store (executor.rs:1932-2096)
+            addr = (bv + cv) & M32
+            two = addr & 3
+            aligned = addr - two
+            if aligned not in mem:
+                mem[aligned] = mem_init[aligned] = _mem_word(aligned)
+            pmem = mem[aligned]
+            mps, mpc = mem_last.get(aligned, (0, 0))
+            hi = prev_a  # hi_or_prev_a = the register's previous value
+            if op in LOAD_OPS:
+                av = nmem = None
+                av = _load_value(op, pmem, two, prev_a)
+                nmem = pmem
+                written = av if ra else 0
+                if ra:
+                    regs[ra] = av
+            else:
+                nmem = _store_value(op, pmem, two, prev_a)
+                mem[aligned] = nmem
+                if op == OP_SC:  # SC writes 1 to rt
+                    av = 1
+                    written = 1 if ra else 0
+                    if ra:
+                        regs[ra] = 1
+                else:  # op_a is read, not written
+                    av = written = prev_a
+            mem_last[aligned] = (shard, clk)
+            mevs.append((pc, npc, op, av, bv, cv, prev_a, clk, addr, pmem, nmem, mps, mpc))
+            # emit_memory_dependencies (dependencies.rs:125-180): the address ADD, the sign-extending SUB
+            ev["add"].append((A.OP_ADD, addr, bv, cv, U, U + 4))
+            if op in (OP_LB, OP_LH):
+                um = (pmem >> (8 * two)) & 0xFF if op == OP_LB else (pmem >> (8 * (two & 2))) & 0xFFFF
+                if um >> (7 if op == OP_LB else 15):
+                    ev["add"].append((A.OP_SUB, av, um, 256 if op == OP_LB else 65536, U, U + 4))
+            nnpc = npc + 4
         elif op in MOVCOND_OPS:  # execute_condmov / execute_wsbh (executor.rs:1782-1857)
             if op == OP_WSBH:
                 av = (((bv >> 16) & 0xFF) << 24) | (((bv >> 24) & 0xFF) << 16) | ((bv & 0xFF) << 8) | ((bv >> 8) & 0xFF)
@@ -1001,9 +1261,14 @@ def _execute(prog, regs, shard, max_steps):
             last[REG_HI] = (shard, clk + POS_HI)
             regs[REG_HI] = hi
         steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc,
-                      hi if op in MUL_OPS + DIV_OPS + MOVCOND_OPS else 0))
+                      hi if op in MUL_OPS + DIV_OPS + MOVCOND_OPS + MEM_OPS else 0))
         pc, npc = npc, nnpc
-    return steps, ev, branches, jumps, muls, divs, movs, last
+    return steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last)
+
+
+def _mem_word(addr):
+    """Initial content of a data word (synthetic, deterministic in the address)."""
+    return (addr * 0x9E3779B1 + 0x7F4A7C15) & M32
 
 
 def _ev_arrays(lst):
@@ -1017,7 +1282,8 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     init = splitmix64(0x5EED000 + seed, NUM_REGS) & np.uint64(M32)
     regs = [0] + [int(x) for x in init[1:]]
     init_vals = list(regs)
-    steps, ev, branches, jumps, muls, divs, movs, last = _execute(prog, regs, shard, max_steps)
+    steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last) = \
+        _execute(prog, regs, shard, max_steps)
     n = len(steps)
     assert n > 0
     height = max(16, 1 << (n - 1).bit_length())
@@ -1052,15 +1318,16 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     t[:n, C_NPC] = npc
     t[:n, C_NNPC] = nnpc
     t[:n, C_OPCODE:C_IMMC + 1] = instr_cols[ks]
-    t[:n, C_RW_A] = np.isin(ops, (OP_MEQ, OP_MNE))  # is_rw_a_instruction (instruction.rs:180-200)
+    t[:n, C_RW_A] = np.isin(ops, (OP_MEQ, OP_MNE) + MEM_OPS)  # is_rw_a_instruction (instruction.rs:180-205)
     t[:n, C_SEQ] = is_seq
     his = np.asarray([s_[12] for s_ in steps], np.int64)
-    mult_div = np.isin(ops, MULT_DIV)  # is_mult_div_instruction: check memory, send shard/clk
+    # is_mult_div_instruction || is_check_memory_instruction: the row sends its shard and clk
+    mult_div = np.isin(ops, MULT_DIV + MEM_OPS)
     t[:n, C_HI_PREV_A:C_HI_PREV_A + 4] = A._bytes(his.astype(np.uint32))
     t[:n, C_CHECK_MEM] = mult_div
     t[:n, C_SHARD_SEND] = np.where(mult_div, shard, 0)
     t[:n, C_CLK_SEND] = np.where(mult_div, clk, 0)
-    t[:n, C_A_IMM] = is_branch
+    t[:n, C_A_IMM] = is_branch | np.isin(ops, (OP_SB, OP_SH, OP_SW, OP_SWL, OP_SWR))  # cpu/trace.rs:135-138
     t[:n, C_A_VAL:C_A_VAL + 4] = A._bytes(av)
     t[:n, C_REAL] = 1
     byte_lookup(A.B_U16RANGE, np.full(n, shard >> 8), np.full(n, shard & 0xFF))  # U16Range(shard): row a1
@@ -1099,6 +1366,8 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
         traces["DivRem"] = _divrem_trace(divs, shard, byte_lookup)[0]
     if muls:
         traces["Mul"] = _mul_trace(muls, shard, byte_lookup)
+    if mevs:
+        traces["MemoryInstrs"] = _mem_instr_trace(mevs, shard, byte_lookup)
 
     # Program: one row per instruction, multiplicity = executions
     ph = max(16, 1 << (len(prog) - 1).bit_length())
@@ -1109,13 +1378,17 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     pm[:len(prog), 0] = np.bincount(ks, minlength=len(prog))
     traces["Program"] = pm
 
-    rs = np.zeros((A._pow2(NUM_REGS), RS_WIDTH), np.uint32)
-    R = NUM_REGS
-    rs[:R, RS_ADDR] = np.arange(R)
-    rs[:R, RS_INIT_VAL:RS_INIT_VAL + 4] = A._bytes(np.asarray(init_vals, np.uint32))
-    rs[:R, RS_FIN_SHARD] = [s_ for s_, _ in last]
-    rs[:R, RS_FIN_CLK] = [c_ for _, c_ in last]
-    rs[:R, RS_FIN_VAL:RS_FIN_VAL + 4] = A._bytes(np.asarray(regs, np.uint32))
+    # registers, then every data word the shard touched (MemoryLocal's entries: addr, initial and final
+    # (shard, clk, value), memory/local.rs:204-270)
+    addrs = sorted(mem)
+    R = NUM_REGS + len(addrs)
+    rs = np.zeros((A._pow2(R), RS_WIDTH), np.uint32)
+    rs[:R, RS_ADDR] = list(range(NUM_REGS)) + addrs
+    rs[:R, RS_INIT_VAL:RS_INIT_VAL + 4] = A._bytes(np.asarray(init_vals + [mem_init[x] for x in addrs], np.uint32))
+    fin = last + [mem_last[x] for x in addrs]
+    rs[:R, RS_FIN_SHARD] = [s_ for s_, _ in fin]
+    rs[:R, RS_FIN_CLK] = [c_ for _, c_ in fin]
+    rs[:R, RS_FIN_VAL:RS_FIN_VAL + 4] = A._bytes(np.asarray(regs + [mem[x] for x in addrs], np.uint32))
     rs[:R, RS_REAL] = 1
     traces["RegisterState"] = rs
 
@@ -1123,7 +1396,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     traces["Byte"] = mult.astype(np.uint32)
     pvs = (splitmix64(0xC0DE100 + seed, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
     pvs[PV_START_PC] = PC_BASE
-    pvs[PV_NEXT_PC] = PC_BASE + 4 * len(prog)
+    pvs[PV_NEXT_PC] = int(npc[-1])  # where the program left off (its end, or a jump out of it)
     pvs[PV_EXECUTION_SHARD] = shard
     prep_traces = {"Program": prep, "Byte": A.byte_prep_trace()}
     return core_machine(), prep_traces, traces, pvs
