@@ -147,7 +147,7 @@ def main():
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
                          "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
                          "zkmips_amd/mips_alu.py), 2^(log-n) "
-                         "instructions per shard; core: Cpu + Program + Mul + DivRem + Branch + Jump + MovCond + MemoryInstrs chips over the ALU slice "
+                         "instructions per shard; core: Cpu + Program + Mul + DivRem + Branch + Jump + MovCond + MemoryInstrs + MiscInstrs chips over the ALU slice "
                          "(zkmips_amd/mips_core.py) running a counted loop, Cpu 2^(log-n) rows")
     ap.add_argument("--queries", type=int, default=84)
     ap.add_argument("--cpu-log-n", type=int, default=18)
@@ -332,7 +332,7 @@ def main():
                    (f"MIPS core shard: a counted loop (60-instruction body of ALU and load/store ops, forward branches, jal/jalr calls "
                     f"of a subroutine, bal) "
                     f"executed to {int(traces['Cpu'][:, 65].sum())} instructions: Cpu 2^{args.log_n} (main 67, "
-                    f"LogUp 11 EF) + Program (prep 14) + DivRem, AddSub, Bitwise, Mul, Lt, ShiftLeft, ShiftRight, CloClz, MovCond, MemoryInstrs, "
+                    f"LogUp 11 EF) + Program (prep 14) + DivRem, AddSub, Bitwise, Mul, Lt, ShiftLeft, ShiftRight, CloClz, MovCond, MemoryInstrs, MiscInstrs, "
                     f"Branch, Jump + Byte 2^16 (prep 12) + RegisterState: full commit+open per shard")
                    if args.workload == "core" else
                    (f"MIPS ALU slice: InstrSource 2^{args.log_n} + AddSub, Bitwise, Lt 2^{args.log_n - 2} + ShiftLeft, "

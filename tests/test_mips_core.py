@@ -1,5 +1,6 @@
-"""MIPS core shard: the reference's Cpu, Program, Branch, Jump, Mul and DivRem chips (zkmips_amd/mips_core.py) on top of
-the ALU slice, with the register-memory argument closed by the RegisterState stand-in.
+"""MIPS core shard: the reference's Cpu, Program, Branch, Jump, Mul, DivRem, MovCond, MemoryInstrs and
+MiscInstrs chips (zkmips_amd/mips_core.py) on top of the ALU slice, with the memory argument closed by the
+MemoryLocal-shaped RegisterState stand-in.  The reference's own instruction-test programs are fixtures.
 
 CPU part: the trace satisfies every constraint and every lookup balances (direct evaluation,
 tests/_air_check.py); the oracle proves it and its verifier accepts; forged ALU results, register
@@ -379,6 +380,60 @@ def test_reference_control_programs(k):
     assert rc == 0 and o.verify(proof) == 0
 
 
+# misc/others/mod.rs test_misc_prove
+MISC_PROGRAM = [
+    (_ADD, 29, 0, 0xF, 0, 1), (_ADD, 28, 0, 0x8F8F, 0, 1),
+    (C.OP_SEXT, 30, 29, 0, 0, 1), (C.OP_SEXT, 31, 28, 0, 0, 1), (C.OP_SEXT, 0, 28, 0, 0, 1),
+    (C.OP_SEXT, 30, 29, 1, 0, 1), (C.OP_SEXT, 31, 28, 1, 0, 1), (C.OP_SEXT, 0, 28, 1, 0, 1),
+    (C.OP_EXT, 30, 28, 0x21, 0, 1), (C.OP_EXT, 30, 31, 0x1EF, 0, 1), (C.OP_EXT, 0, 28, 0x21, 0, 1),
+    (C.OP_INS, 30, 29, 0x21, 0, 1), (C.OP_INS, 30, 31, 0x3EF, 0, 1), (C.OP_INS, 0, 29, 0x21, 0, 1),
+    (C.OP_MADDU, 32, 31, 31, 0, 0), (C.OP_MADDU, 32, 29, 31, 0, 0), (C.OP_MADDU, 32, 29, 0, 0, 0),
+    (C.OP_MSUBU, 32, 31, 31, 0, 0), (C.OP_MSUBU, 32, 29, 31, 0, 0), (C.OP_MSUBU, 32, 29, 0, 0, 0),
+    (C.OP_MADD, 32, 31, 31, 0, 0), (C.OP_MADD, 32, 29, 31, 0, 0), (C.OP_MADD, 32, 29, 0, 0, 0),
+    (C.OP_MSUB, 32, 31, 31, 0, 0), (C.OP_MSUB, 32, 29, 31, 0, 0), (C.OP_MSUB, 32, 29, 0, 0, 0),
+    (C.OP_TEQ, 28, 29, 0, 0, 1), (C.OP_TEQ, 28, 0, 0, 0, 1), (C.OP_TEQ, 0, 28, 0, 0, 1)]
+
+
+def test_misc_reference_fixture():
+    """The reference's test_misc_prove program: SEB/SEH, EXT, INS, MADDU/MSUBU/MADD/MSUB (HI:LO
+    accumulate and its 64-bit AddDouble), TEQ (non-trapping)."""
+    m, prep, tr, pv = C.program_shard(MISC_PROGRAM, seed=1)
+    ms = tr["MiscInstrs"]
+    assert [int(ms[:, C.MS_SEL + k].sum()) for k in range(8)] == [6, 3, 3, 3, 3, 3, 3, 3]
+    assert _final(tr, 31) == 0xFFFF8F8F  # SEH of 0x8F8F
+    # MADDU, MSUBU, MADD and MSUB of the same operands cancel pairwise: HI:LO returns to its start
+    rs = tr["RegisterState"]
+    assert _word(rs[C.REG_LO], C.RS_FIN_VAL) == _word(rs[C.REG_LO], C.RS_INIT_VAL)
+    assert _word(rs[C.REG_HI], C.RS_FIN_VAL) == _word(rs[C.REG_HI], C.RS_INIT_VAL)
+    assert _air_check.check(m, prep, tr, pv) == ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+@pytest.mark.parametrize("what", ["ins_result", "maddsub_carry", "sext_sign", "teq_equal"])
+def test_misc_tamper_rejected(what):
+    m, prep, tr, pv = C.program_shard(MISC_PROGRAM, seed=1)
+    bad = {k: v.copy() for k, v in tr.items()}
+    ms = bad["MiscInstrs"]
+    if what == "ins_result":
+        i = int(np.nonzero(ms[:, C.MS_SEL + 1])[0][0])
+        ms[i, C.MS_A] ^= 4
+    elif what == "maddsub_carry":
+        i = int(np.nonzero(ms[:, C.MS_SEL + 3])[0][0])
+        ms[i, C.MS_SPEC + 16] ^= 1
+    elif what == "sext_sign":
+        i = int(np.nonzero(ms[:, C.MS_SEL])[0][1])
+        ms[i, C.MS_SPEC] ^= 1
+    else:  # a TEQ that claims its operands are equal (it would have trapped)
+        i = int(np.nonzero(ms[:, C.MS_SEL + 7])[0][0])
+        ms[i, C.MS_SPEC + 2] = 1
+    assert _air_check.check(m, prep, bad, pv) != ([], [])
+    o = O.OracleProver(m, prep, num_queries=8)
+    rc, proof = o.prove(bad, pv)
+    assert rc == 0 and o.verify(proof) != 0
+
+
 def _final(tr, addr):
     rs = tr["RegisterState"]
     i = int(np.nonzero((rs[:, C.RS_ADDR] == addr) & (rs[:, C.RS_REAL] == 1))[0][0])
@@ -538,13 +593,13 @@ def test_core_gpu_proof_bytes_identical(dev, n, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["alu_fixtures", "simple_memory", "other_memory", "sc", "jalr"])
+@pytest.mark.parametrize("name", ["alu_fixtures", "simple_memory", "other_memory", "sc", "jalr", "misc"])
 def test_reference_programs_gpu_proof_bytes_identical(dev, name):
     """The reference's own instruction-test programs: GPU proof bytes == oracle proof bytes."""
     from zkmips_amd.prover import HipProver
     prog = {"alu_fixtures": [ins for p in _reference_alu_fixtures() for ins in p],
             "simple_memory": SIMPLE_MEMORY_PROGRAM, "other_memory": OTHER_MEMORY_PROGRAM, "sc": SC_PROGRAM,
-            "jalr": _reference_control_fixtures()[-1]}[name]
+            "jalr": _reference_control_fixtures()[-1], "misc": MISC_PROGRAM}[name]
     m, prep, tr, pv = C.program_shard(prog, seed=6)
     gpu = HipProver(dev, m, prep, num_queries=16)
     cpu = O.OracleProver(m, prep, num_queries=16)

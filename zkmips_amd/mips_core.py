@@ -869,6 +869,212 @@ def _mem_instr_trace(mevs, shard, byte_lookup):
     return t
 
 
+# ---------------------------------------------------------------- MiscInstrs (misc/others)
+OP_INS, OP_MADDU, OP_MSUBU, OP_MADD, OP_MSUB = 45, 46, 47, 48, 49  # executor/src/opcode.rs:65-75
+OP_EXT, OP_TEQ, OP_SEXT = 53, 54, 55
+MISC_OPS = (OP_SEXT, OP_INS, OP_EXT, OP_MADDU, OP_MSUBU, OP_MADD, OP_MSUB, OP_TEQ)  # column order
+MADDSUB_OPS = (OP_MADDU, OP_MSUBU, OP_MADD, OP_MSUB)
+# MiscInstrColumns (misc/others/columns/mod.rs); misc_specific_columns is a union whose widest view is
+# MaddsubCols: mul_lo, mul_hi, AddDoubleOperation (value, value_hi, carry[7]), src2_hi, src2_lo, op_hi_access
+MS_SHARD, MS_CLK, MS_PC, MS_NPC, MS_A, MS_PREV_A, MS_B, MS_C, MS_SPEC = 0, 1, 2, 3, 4, 8, 12, 16, 20
+MS_SEL = 64  # is_sext, is_ins, is_ext, is_maddu, is_msubu, is_madd, is_msub, is_teq
+MS_WIDTH = 72
+_MD_LO, _MD_HI, _MD_VAL, _MD_VALHI, _MD_CARRY, _MD_S2HI, _MD_S2LO, _MD_HIACC = 0, 4, 8, 12, 16, 23, 27, 31
+
+
+def _add_double(ch, a, a_hi, b, b_hi, val, val_hi, carry, is_real, real_v, byte_words):
+    """AddDoubleOperation::eval (operations/add_double.rs): 64-bit byte-wise add with 7 carries."""
+    M = main
+    ov = [a[0] + b[0] - val[0]] + [a[j] + b[j] - val[j] + carry[j - 1] for j in (1, 2, 3)]
+    for j in range(4):
+        ch.assert_zero(is_real * (ov[j] * (ov[j] - 256)))
+    for j in range(4):
+        ch.assert_zero(is_real * (carry[j] * (ov[j] - 256)))
+    for j in range(4):
+        ch.assert_zero(is_real * ((carry[j] - 1) * ov[j]))
+    ovh = [a_hi[j] + b_hi[j] - val_hi[j] + carry[3 + j] for j in range(4)]
+    for j in range(4):
+        ch.assert_zero(is_real * (ovh[j] * (ovh[j] - 256)))
+    for j in range(3):
+        ch.assert_zero(is_real * (carry[4 + j] * (ovh[j] - 256)))
+    for j in range(3):
+        ch.assert_zero(is_real * ((carry[4 + j] - 1) * ovh[j]))
+    for j in range(7):
+        _assert_bool(ch, carry[j], is_real)
+    _assert_bool(ch, is_real, is_real)
+    for base in byte_words:  # slice_range_check_u8 of a, a_hi, b, b_hi, value, value_hi
+        for k in (0, 2):
+            ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, _m(base + k), _m(base + k + 1)], real_v,
+                                   KIND_BYTE))
+
+
+def _shift_word(*terms):
+    """Word([const + sum(weight * col), 0, 0, 0]) as VirtualPairCols: terms = (const, [(col, weight)])."""
+    const, cols = terms
+    return [V([("main", c, w % P) for c, w in cols], const), ZERO, ZERO, ZERO]
+
+
+def misc_instructions_chip() -> ChipDesc:
+    """MiscInstrsChip::eval with eval_ext / eval_ins / eval_maddsub / eval_sext (misc/others/air.rs:24-418):
+    SEXT (SEB/SEH), EXT, INS, MADDU/MSUBU/MADD/MSUB and TEQ, constraints and lookups in its order."""
+    ch = ChipDesc("MiscInstrs", prep_width=0, main_width=MS_WIDTH, local_only=True)
+    M = main
+    sext, ins, ext, maddu, msubu, madd, msub, teq = (M(MS_SEL + k) for k in range(8))
+    is_real = sext + ins + ext + maddu + msubu + madd + msub + teq
+    for k in range(8):
+        _assert_bool(ch, M(MS_SEL + k))
+    _assert_bool(ch, is_real)
+    sel = lambda *ks, const=0: V([("main", MS_SEL + k, 1) for k in ks], const)
+    opcode = V([("main", MS_SEL + k, op) for k, op in enumerate(MISC_OPS)])
+    npc4 = V([("main", MS_NPC, 1)], 4)
+    body = [opcode] + _vword(MS_A) + _vword(MS_B) + _vword(MS_C) + _vword(MS_PREV_A)
+    ch.receives.append(Lookup([_m(MS_SHARD), _m(MS_CLK), _m(MS_PC), _m(MS_NPC), npc4, ZERO] + body +
+                              [ZERO, sel(3, 4, 5, 6, 1), sel(3, 4, 5, 6), ZERO, V.const(1)], sel(3, 4, 5, 6),
+                              KIND_INSTRUCTION))
+    ch.receives.append(Lookup([ZERO, ZERO, _m(MS_PC), _m(MS_NPC), npc4, ZERO] + body +
+                              [ZERO, sel(3, 4, 5, 6, 1), ZERO, ZERO, V.const(1)], sel(0, 7, 2, 1), KIND_INSTRUCTION))
+    S = MS_SPEC
+    red = lambda base: sum((M(base + i) * (1 << (8 * i)) for i in range(1, 4)), M(base))
+    # eval_ext: ext view = lsb, msbd, sll_val
+    lsb, msbd = S, S + 1
+    _send_alu(ch, A.OP_SLL, _vword(S + 2), _vword(MS_B), _shift_word(31, [(lsb, -1), (msbd, -1)]), _m(MS_SEL + 2))
+    _send_alu(ch, A.OP_SRL, _vword(MS_A), _vword(S + 2), _shift_word(31, [(msbd, -1)]), _m(MS_SEL + 2))
+    ch.assert_zero(ext * (red(MS_C) - (M(lsb) + M(msbd) * 32)))
+    ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, _m(lsb), _m(msbd)], _m(MS_SEL + 2), KIND_BYTE))
+    ch.sends.append(Lookup([V.const(A.B_LTU), V.const(1), ZERO, V([("main", lsb, 1), ("main", msbd, 1)]),
+                            V.const(32)], _m(MS_SEL + 2), KIND_BYTE))
+    # eval_ins: ins view = lsb, msb, ror_val, srl_val, sll_val, add_val
+    lsb, msb, ror, srl, sll, add = S, S + 1, S + 2, S + 6, S + 10, S + 14
+    isv = _m(MS_SEL + 1)
+    _send_alu(ch, A.OP_ROR, _vword(ror), _vword(MS_PREV_A), _shift_word(0, [(lsb, 1)]), isv)
+    _send_alu(ch, A.OP_SRL, _vword(srl), _vword(ror), _shift_word(1, [(msb, 1), (lsb, -1)]), isv)
+    _send_alu(ch, A.OP_SLL, _vword(sll), _vword(MS_B), _shift_word(31, [(msb, -1), (lsb, 1)]), isv)
+    _send_alu(ch, A.OP_ADD, _vword(add), _vword(srl), _vword(sll), isv)
+    _send_alu(ch, A.OP_ROR, _vword(MS_A), _vword(add), _shift_word(31, [(msb, -1)]), isv)
+    ch.assert_zero(ins * (red(MS_C) - (M(lsb) + M(msb) * 32)))
+    ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, _m(lsb), _m(msb)], isv, KIND_BYTE))
+    ch.sends.append(Lookup([V.const(A.B_LTU), V.const(1), ZERO, _m(lsb), V([("main", msb, 1)], 1)], isv, KIND_BYTE))
+    ch.sends.append(Lookup([V.const(A.B_LTU), V.const(1), ZERO, _m(msb), V.const(32)], isv, KIND_BYTE))
+    # eval_maddsub
+    md_real = maddu + msubu + madd + msub
+    md_v = sel(3, 4, 5, 6)
+    is_add, is_sub = maddu + madd, msubu + msub
+    mul_op = V([("main", MS_SEL + 5, OP_MULT), ("main", MS_SEL + 6, OP_MULT), ("main", MS_SEL + 3, OP_MULTU),
+                ("main", MS_SEL + 4, OP_MULTU)])
+    vals = [ZERO, ZERO, V.const(A.UNUSED_PC), V.const(A.UNUSED_PC + 4), V.const(A.UNUSED_PC + 8), ZERO, mul_op]
+    vals += _vword(S + _MD_LO) + _vword(MS_B) + _vword(MS_C) + _vword(S + _MD_HI) + [ZERO, ZERO, ZERO, ZERO,
+                                                                                       V.const(1)]
+    ch.sends.append(Lookup(vals, md_v, KIND_INSTRUCTION))  # send_alu_with_hi(MULT/MULTU, ...)
+    hacc = S + _MD_HIACC
+    for i in range(4):
+        ch.assert_zero(md_real * (M(S + _MD_S2HI + i) - (M(hacc + i) * is_add + M(hacc + 4 + ACC_VALUE + i) * is_sub)))
+        ch.assert_zero(md_real * (M(S + _MD_S2LO + i) - (M(MS_PREV_A + i) * is_add + M(MS_A + i) * is_sub)))
+    w = lambda base: [M(base + i) for i in range(4)]
+    _add_double(ch, w(S + _MD_LO), w(S + _MD_HI), w(S + _MD_S2LO), w(S + _MD_S2HI), w(S + _MD_VAL), w(S + _MD_VALHI),
+                [M(S + _MD_CARRY + j) for j in range(7)], md_real, md_v,
+                (S + _MD_LO, S + _MD_HI, S + _MD_S2LO, S + _MD_S2HI, S + _MD_VAL, S + _MD_VALHI))
+    for i in range(4):
+        ch.assert_zero(is_add * (M(MS_A + i) - M(S + _MD_VAL + i)))
+    for i in range(4):
+        ch.assert_zero(is_add * (M(hacc + 4 + ACC_VALUE + i) - M(S + _MD_VALHI + i)))
+    for i in range(4):
+        ch.assert_zero(is_sub * (M(MS_PREV_A + i) - M(S + _MD_VAL + i)))
+    for i in range(4):
+        ch.assert_zero(is_sub * (M(hacc + i) - M(S + _MD_VALHI + i)))
+    _eval_memory_access(ch, hacc + 4, hacc, POS_HI, V.const(REG_HI), md_real, md_v, shard_col=MS_SHARD,
+                        clk_terms=((MS_CLK, 1),))
+    # eval_sext: sext view = most_sig_bit, sig_byte, a_eq_b, is_seb, is_seh
+    msbit, sbyte, aeqb, seb, seh = (M(S + k) for k in range(5))
+    for i in range(4):
+        ch.assert_zero(teq * aeqb * (M(MS_A + i) - M(MS_B + i)))
+    ch.assert_zero(teq * aeqb)
+    ch.sends.append(Lookup([V.const(A.B_MSB), _m(S), ZERO, _m(S + 1), ZERO], _m(MS_SEL + 0), KIND_BYTE))
+    c0 = M(MS_C)
+    ch.assert_zero(sext * (c0 * (c0 - 1)))
+    ch.assert_zero(sext * seb * c0)
+    ch.assert_zero(sext * seh * (c0 - 1))
+    ch.assert_zero(sext * seb * (M(MS_B) - sbyte))
+    ch.assert_zero(sext * seh * (M(MS_B + 1) - sbyte))
+    sign = msbit * 255
+    ch.assert_zero(sext * (M(MS_A) - M(MS_B)))
+    ch.assert_zero(sext * seb * (M(MS_A + 1) - sign))
+    ch.assert_zero(sext * seh * (M(MS_A + 1) - M(MS_B + 1)))
+    ch.assert_zero(sext * (M(MS_A + 2) - sign))
+    ch.assert_zero(sext * (M(MS_A + 3) - sign))
+    ch.assert_zero((ins + ext) * M(MS_C + 2))
+    ch.assert_zero((ins + ext) * M(MS_C + 3))
+    return ch
+
+
+def _misc_trace(misc, shard, byte_lookup):
+    """MiscInstrsChip::event_to_row + populate_* (misc/others/trace.rs:81-262).  misc: (op, a, b, c, prev_a,
+    pc, npc, clk, hi_prev, hi_new, hi_prev_shard, hi_prev_clk)."""
+    E = np.asarray(misc, np.int64).reshape(-1, 12)
+    n = len(E)
+    t = np.zeros((A._pow2(n), MS_WIDTH), np.uint32)
+    u = lambda v: np.asarray(v, np.int64).astype(np.uint32)
+    S = MS_SPEC
+    for r, (op, a, b, c, pa, pc, npc, clk, hp, hn, hps, hpc) in enumerate(E.tolist()):
+        row = t[r]
+        row[MS_PC], row[MS_NPC] = pc, npc
+        for base, v in ((MS_A, a), (MS_B, b), (MS_C, c), (MS_PREV_A, pa)):
+            row[base:base + 4] = A._bytes(u([v]))[0]
+        row[MS_SEL + MISC_OPS.index(op)] = 1
+        if op in (OP_SEXT, OP_TEQ):
+            if c > 0:
+                bit, byte = (b & 0xFFFF) >> 15, (b >> 8) & 0xFF
+                row[S + 4] = 1
+            else:
+                bit, byte = (b & 0xFF) >> 7, b & 0xFF
+                row[S + 3] = 1
+            row[S], row[S + 1], row[S + 2] = bit, byte, int(a == b)
+            if op == OP_SEXT:
+                byte_lookup(A.B_MSB, np.asarray([byte]), np.zeros(1, np.int64))
+        elif op == OP_EXT:
+            lsb, msbd = c & 31, c >> 5
+            row[S], row[S + 1] = lsb, msbd
+            row[S + 2:S + 6] = A._bytes(u([(b << (31 - lsb - msbd)) & M32]))[0]
+            byte_lookup(A.B_U8RANGE, np.asarray([lsb]), np.asarray([msbd]))
+            byte_lookup(A.B_LTU, np.asarray([lsb + msbd]), np.asarray([32]))
+        elif op == OP_INS:
+            lsb, msb = c & 31, c >> 5
+            ror = ((pa >> lsb) | (pa << (32 - lsb))) & M32 if lsb else pa
+            srl = ror >> (msb - lsb + 1)
+            sll = (b << (31 - msb + lsb)) & M32
+            row[S], row[S + 1] = lsb, msb
+            for off, v in ((2, ror), (6, srl), (10, sll), (14, (srl + sll) & M32)):
+                row[S + off:S + off + 4] = A._bytes(u([v]))[0]
+            byte_lookup(A.B_U8RANGE, np.asarray([lsb]), np.asarray([msb]))
+            byte_lookup(A.B_LTU, np.asarray([lsb]), np.asarray([msb + 1]))
+            byte_lookup(A.B_LTU, np.asarray([msb]), np.asarray([32]))
+        else:  # MADDU / MSUBU / MADD / MSUB
+            row[MS_SHARD], row[MS_CLK] = shard, clk
+            signed = op in (OP_MADD, OP_MSUB)
+            prod = ((_s32(b) * _s32(c)) if signed else b * c) & ((1 << 64) - 1)
+            is_add = op in (OP_MADDU, OP_MADD)
+            s2lo, s2hi = (pa, hp) if is_add else (a, hn)
+            tot = (prod + ((s2hi << 32) | s2lo)) & ((1 << 64) - 1)
+            ab = list(prod.to_bytes(8, "little")), list(((s2hi << 32) | s2lo).to_bytes(8, "little"))
+            carry, cy = [], 0
+            for j in range(7):
+                cy = 1 if ab[0][j] + ab[1][j] + cy > 255 else 0
+                carry.append(cy)
+            for off, v in ((_MD_LO, prod & M32), (_MD_HI, prod >> 32), (_MD_VAL, tot & M32), (_MD_VALHI, tot >> 32),
+                           (_MD_S2HI, s2hi), (_MD_S2LO, s2lo), (_MD_HIACC, hp)):
+                row[S + off:S + off + 4] = A._bytes(u([v]))[0]
+            row[S + _MD_CARRY:S + _MD_CARRY + 7] = carry
+            for v in (prod & M32, prod >> 32, s2lo, s2hi, tot & M32, tot >> 32):
+                wb = A._bytes(u([v]))
+                byte_lookup(A.B_U8RANGE, wb[:, 0], wb[:, 1])
+                byte_lookup(A.B_U8RANGE, wb[:, 2], wb[:, 3])
+    md = np.isin(E[:, 0], MADDSUB_OPS)
+    if md.any():
+        rows = np.nonzero(md)[0]
+        _access_cols(t, rows, S + _MD_HIACC + 4, u(E[rows, 9]), E[rows][:, 10:12], shard, E[rows, 7] + POS_HI,
+                     np.ones(len(rows), bool), byte_lookup)
+    return t
+
+
 # ---------------------------------------------------------------- Jump (control_flow/jump)
 OP_JUMP, OP_JUMPI, OP_JUMPDIRECT = 27, 28, 29  # JR/JALR, J/JAL, BAL (executor/src/opcode.rs:45-47)
 JUMP_OPS = (OP_JUMP, OP_JUMPI, OP_JUMPDIRECT)
@@ -927,7 +1133,7 @@ def core_machine() -> MachineDesc:
     return MachineDesc([cpu_chip(), program_chip(), divrem_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
                         A.shift_right_chip(),
                         A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(), memory_instructions_chip(),
-                        movcond_chip(),
+                        movcond_chip(), misc_instructions_chip(),
                         A.byte_chip(),
                         register_state_chip()], NUM_PV_ELTS)
 
@@ -942,6 +1148,7 @@ _MIX = [(A.OP_ADD, 0), (A.OP_ADD, 1), (A.OP_SUB, 0), (A.OP_AND, 0), (A.OP_AND, 1
         (OP_MUL, 0), (OP_MULT, 0), (OP_MULTU, 0), (OP_DIV, 0), (OP_DIVU, 0), (OP_MOD, 0), (OP_MODU, 0),
         ("MFLO", 0), ("MFHI", 0), ("MTLO", 0), ("MTHI", 0), (OP_MEQ, 0), (OP_MNE, 0), (OP_WSBH, 1)]
 _MIX += [(op, 1) for op in MEM_OPS]
+_MIX += [(OP_SEXT, 1), (OP_EXT, 1), (OP_INS, 1), (OP_MADDU, 0), (OP_MSUBU, 0), (OP_MADD, 0), (OP_MSUB, 0)]
 _KIND = {A.OP_ADD: "add", A.OP_SUB: "add", A.OP_AND: "bit", A.OP_OR: "bit", A.OP_XOR: "bit", A.OP_NOR: "bit",
          A.OP_SLT: "lt", A.OP_SLTU: "lt", A.OP_SLL: "sll", A.OP_SRL: "sr", A.OP_SRA: "sr", A.OP_ROR: "sr",
          A.OP_CLZ: "clz", A.OP_CLO: "clz"}
@@ -1006,6 +1213,15 @@ def _random_alu(r, avoid=()):
     if isinstance(op, str):  # MFLO/MFHI rd = lo/hi; MTLO/MTHI lo/hi = rs: ADDs with register 32/33 (instruction.rs:387-394)
         reg = REG_LO if op.endswith("LO") else REG_HI
         return (A.OP_ADD, ra, reg, 0, 0, 1) if op.startswith("MF") else (A.OP_ADD, reg, rb, 0, 0, 1)
+    if op in (OP_SEXT, OP_EXT, OP_INS):  # SEB/SEH; EXT/INS fields (msbd/msb << 5 | lsb), INS narrower than 32
+        lsb = int(r[3] % 32)
+        hi5 = int((r[3] >> np.uint64(8)) % (32 - lsb))
+        if op == OP_INS and lsb == 0 and hi5 == 31:
+            hi5 = 30
+        c = int(r[3] % 2) if op == OP_SEXT else ((hi5 + (lsb if op == OP_INS else 0)) << 5) | lsb
+        return (op, ra, rb, c, 0, 1)
+    if op in MADDSUB_OPS:
+        return (op, REG_LO, rb, int(r[3] % 32), 0, 0)
     if op in MEM_OPS:  # base r0 + offset into a 256-byte data window, so words are re-read and re-written
         sub = int((r[3] >> np.uint64(8)) % 4)
         if op in (OP_LW, OP_LL, OP_SW, OP_SC):
@@ -1120,7 +1336,7 @@ def _execute(prog, regs, shard, max_steps):
     pc, npc = PC_BASE, PC_BASE + 4
     steps = []
     ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
-    branches, jumps, muls, divs, movs, mevs = [], [], [], [], [], []
+    branches, jumps, muls, divs, movs, mevs, misc = [], [], [], [], [], [], []
     mem, mem_init, mem_last = {}, {}, {}
     U = A.UNUSED_PC
     while PC_BASE <= pc < end:  # the program halts when pc leaves it
@@ -1211,6 +1427,53 @@ def _execute(prog, regs, shard, max_steps):
                 if um >> (7 if op == OP_LB else 15):
                     ev["add"].append((A.OP_SUB, av, um, 256 if op == OP_LB else 65536, U, U + 4))
             nnpc = npc + 4
+        elif op in MISC_OPS:  # executor.rs:1692-1834; dependencies: emit_misc_dependencies (dependencies.rs:251-376)
+            hi = ev_prev = 0
+            if op == OP_SEXT:
+                v, bits = (bv & 0xFFFF, 16) if cv else (bv & 0xFF, 8)
+                av = (v - (1 << bits) if v >> (bits - 1) else v) & M32
+            elif op == OP_EXT:
+                lsb, msbd = cv & 31, cv >> 5
+                av = (bv & (M32 if msbd + lsb == 31 else (1 << (msbd + lsb + 1)) - 1)) >> lsb
+                sll = (bv << (31 - lsb - msbd)) & M32
+                ev["sll"].append((A.OP_SLL, sll, bv, 31 - lsb - msbd, U, U + 4))
+                ev["sr"].append((A.OP_SRL, av, sll, 31 - msbd, U, U + 4))
+            elif op == OP_INS:
+                lsb, msb = cv & 31, cv >> 5
+                width = msb - lsb + 1
+                field = (((1 << width) - 1) << lsb) & M32
+                av = (prev_a & ~field & M32) | ((bv << lsb) & field)
+                hi = ev_prev = prev_a
+                ror = ((prev_a >> lsb) | (prev_a << (32 - lsb))) & M32 if lsb else prev_a
+                srl = ror >> width
+                sll = (bv << (31 - msb + lsb)) & M32
+                add = (srl + sll) & M32
+                ev["sr"].append((A.OP_ROR, ror, prev_a, lsb, U, U + 4))
+                ev["sr"].append((A.OP_SRL, srl, ror, width, U, U + 4))
+                ev["sll"].append((A.OP_SLL, sll, bv, 31 - msb + lsb, U, U + 4))
+                ev["add"].append((A.OP_ADD, add, srl, sll, U, U + 4))
+                ev["sr"].append((A.OP_ROR, av, add, 31 - msb, U, U + 4))
+            elif op == OP_TEQ:  # traps when equal (execute_teq); only non-trapping TEQs reach a trace
+                av = prev_a
+                assert av != bv, "TEQ trap"
+            if op in MADDSUB_OPS:  # (HI, LO) +/-= b * c; LO through op_a, HI at position HI
+                signed = op in (OP_MADD, OP_MSUB)
+                prod = ((_s32(bv) * _s32(cv)) if signed else bv * cv) & ((1 << 64) - 1)
+                addend = (regs[REG_HI] << 32) | prev_a
+                out = (addend + prod if op in (OP_MADDU, OP_MADD) else addend - prod) & ((1 << 64) - 1)
+                av, hn = out & M32, out >> 32
+                hi = ev_prev = prev_a
+                hps, hpc = last[REG_HI]
+                misc.append((op, av, bv, cv, ev_prev, pc, npc, clk, regs[REG_HI], hn, hps, hpc))
+                last[REG_HI] = (shard, clk + POS_HI)
+                regs[REG_HI] = hn
+                muls.append((OP_MULT if signed else OP_MULTU, prod & M32, bv, cv, U, U + 4, prod >> 32, -1, 0, 0, 0))
+            else:
+                misc.append((op, av, bv, cv, ev_prev, pc, npc, 0, 0, 0, 0, 0))
+            written = av if ra else 0
+            if ra:
+                regs[ra] = av
+            nnpc = npc + 4
         elif op in MOVCOND_OPS:  # execute_condmov / execute_wsbh (executor.rs:1782-1857)
             if op == OP_WSBH:
                 av = (((bv >> 16) & 0xFF) << 24) | (((bv >> 24) & 0xFF) << 16) | ((bv & 0xFF) << 8) | ((bv >> 8) & 0xFF)
@@ -1261,9 +1524,9 @@ def _execute(prog, regs, shard, max_steps):
             last[REG_HI] = (shard, clk + POS_HI)
             regs[REG_HI] = hi
         steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc,
-                      hi if op in MUL_OPS + DIV_OPS + MOVCOND_OPS + MEM_OPS else 0))
+                      hi if op in MUL_OPS + DIV_OPS + MOVCOND_OPS + MEM_OPS + MISC_OPS else 0))
         pc, npc = npc, nnpc
-    return steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last)
+    return steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc
 
 
 def _mem_word(addr):
@@ -1282,7 +1545,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     init = splitmix64(0x5EED000 + seed, NUM_REGS) & np.uint64(M32)
     regs = [0] + [int(x) for x in init[1:]]
     init_vals = list(regs)
-    steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last) = \
+    steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc = \
         _execute(prog, regs, shard, max_steps)
     n = len(steps)
     assert n > 0
@@ -1318,11 +1581,11 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     t[:n, C_NPC] = npc
     t[:n, C_NNPC] = nnpc
     t[:n, C_OPCODE:C_IMMC + 1] = instr_cols[ks]
-    t[:n, C_RW_A] = np.isin(ops, (OP_MEQ, OP_MNE) + MEM_OPS)  # is_rw_a_instruction (instruction.rs:180-205)
+    t[:n, C_RW_A] = np.isin(ops, (OP_MEQ, OP_MNE, OP_INS) + MEM_OPS + MADDSUB_OPS)  # is_rw_a (instruction.rs:180-205)
     t[:n, C_SEQ] = is_seq
     his = np.asarray([s_[12] for s_ in steps], np.int64)
     # is_mult_div_instruction || is_check_memory_instruction: the row sends its shard and clk
-    mult_div = np.isin(ops, MULT_DIV + MEM_OPS)
+    mult_div = np.isin(ops, MULT_DIV + MEM_OPS + MADDSUB_OPS)
     t[:n, C_HI_PREV_A:C_HI_PREV_A + 4] = A._bytes(his.astype(np.uint32))
     t[:n, C_CHECK_MEM] = mult_div
     t[:n, C_SHARD_SEND] = np.where(mult_div, shard, 0)
@@ -1368,6 +1631,8 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
         traces["Mul"] = _mul_trace(muls, shard, byte_lookup)
     if mevs:
         traces["MemoryInstrs"] = _mem_instr_trace(mevs, shard, byte_lookup)
+    if misc:
+        traces["MiscInstrs"] = _misc_trace(misc, shard, byte_lookup)
 
     # Program: one row per instruction, multiplicity = executions
     ph = max(16, 1 << (len(prog) - 1).bit_length())
