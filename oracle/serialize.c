@@ -169,3 +169,18 @@ int orc_proof_deserialize(orc_proof_t *p, const orc_config_t *cfg, const uint8_t
     if (r.p != r.n) r.err = 1;
     return r.err ? -1 : 0;
 }
+
+/* bincode-1 of a BTreeMap<[F; 8], usize> (the prover's vk map, crates/prover/src/shapes.rs:370-379,
+ * loaded at crates/prover/src/lib.rs:232): u64 length, then per entry the digest with no length
+ * prefix and the usize as u64 — the same field/length conventions as the proof serializer above. */
+size_t orc_serialize_digest_map(const uint32_t *keys, const uint64_t *vals, uint64_t n, int montgomery, uint8_t **out) {
+    wbuf_t w = {0, 0, 0};
+    g_mont = montgomery;
+    wu64(&w, n);
+    for (uint64_t i = 0; i < n; i++) {
+        digest_t d; memcpy(d.v, keys + 8 * i, 32);
+        wdig(&w, d); wu64(&w, vals[i]);
+    }
+    *out = w.b;
+    return w.n;
+}

@@ -59,4 +59,5 @@ int orc_verify_shard(const orc_pk_t *vk, const orc_proof_t *p, orc_chal_t *ch);
 void orc_proof_free(orc_proof_t *p);
 
 size_t orc_proof_serialize(const orc_proof_t *p, const orc_config_t *cfg, uint8_t **out);
+size_t orc_serialize_digest_map(const uint32_t *keys, const uint64_t *vals, uint64_t n, int montgomery, uint8_t **out);
 int orc_proof_deserialize(orc_proof_t *p, const orc_config_t *cfg, const uint8_t *b, size_t n);

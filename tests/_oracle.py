@@ -49,6 +49,9 @@ def lib():
                                     C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_uint64)]
         L.orc_api_verify.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, u32p]
         L.orc_api_free_bytes.argtypes = [C.POINTER(C.c_uint8)]
+        L.orc_serialize_digest_map.argtypes = [u32p, np.ctypeslib.ndpointer(np.uint64), C.c_uint64, C.c_int,
+                                               C.POINTER(C.POINTER(C.c_uint8))]
+        L.orc_serialize_digest_map.restype = C.c_size_t
         _lib = L
     return _lib
 
@@ -112,6 +115,18 @@ def commit_root(mats):
     out = np.zeros(8, np.uint32)
     lib().orc_api_commit_root(len(mats), _ptrs(mats), hs, ws, out)
     return out
+
+
+def serialize_digest_map(keys, vals, montgomery=False) -> bytes:
+    """bincode of BTreeMap<[F;8], usize> with the proof serializer's conventions (oracle/serialize.c)."""
+    k = _u32(keys).reshape(-1, 8)
+    v = np.ascontiguousarray(vals, dtype=np.uint64)
+    out = C.POINTER(C.c_uint8)()
+    n = lib().orc_serialize_digest_map(k if k.size else np.zeros(8, np.uint32), v if v.size else np.zeros(1, np.uint64),
+                                       k.shape[0], int(montgomery), C.byref(out))
+    data = bytes(C.string_at(out, n))
+    lib().orc_api_free_bytes(out)
+    return data
 
 
 class Challenger:

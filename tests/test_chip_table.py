@@ -1,0 +1,112 @@
+"""Every restated MIPS chip pinned to reference-held data (CPU only).
+
+For each chip: its shape (prep, main, perm EF columns, log quotient degree, local_only) as the machine
+blob describes it, the reference `MachineAir` impl it restates, and its per-row cost
+prep + main + 4*perm_EF + 4*2^log_qd (crates/stark/src/chip.rs:154-163) against the reference's own
+`crates/core/executor/src/artifacts/mips_costs.json` (copied to tests/golden/ by make_ref_fixtures.py;
+the reference checks the same file in mips/mod.rs:720-727).
+
+`local_only` decides whether a chip's main trace is opened at zeta only or at zeta and g*zeta
+(crates/stark/src/prover.rs:519-532, 577-590).  The default is false (crates/stark/src/air/machine.rs:77-79);
+the chips marked True override it in the reference (file:line below).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests import _oracle as O
+from zkmips_amd import mips_alu as A
+from zkmips_amd import mips_core as MC
+from zkmips_amd.machine import MachineDesc
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+COSTS = json.load(open(os.path.join(GOLDEN, "mips_costs.json")))
+
+# name: (builder, prep, main, perm_ef, log_qd, local_only, reference MachineAir impl, local_only override)
+CHIPS = {
+    "Cpu": (MC.cpu_chip, 0, 67, 11, 1, False, "cpu/trace.rs:20", None),
+    "Program": (MC.program_chip, 14, 1, 2, 1, False, "program/mod.rs:53", None),
+    "Byte": (A.byte_chip, 12, 10, 6, 1, False, "bytes/trace.rs:17", None),
+    "AddSub": (A.add_sub_chip, 0, 19, 5, 1, True, "alu/add_sub/mod.rs:65", "alu/add_sub/mod.rs:145"),
+    "Bitwise": (A.bitwise_chip, 0, 18, 4, 1, True, "alu/bitwise/mod.rs:61", "alu/bitwise/mod.rs:133"),
+    "Lt": (A.lt_chip, 0, 36, 3, 1, True, "alu/lt/mod.rs:96", "alu/lt/mod.rs:172"),
+    "ShiftLeft": (A.shift_left_chip, 0, 44, 4, 1, True, "alu/sll/mod.rs:102", "alu/sll/mod.rs:193"),
+    "ShiftRight": (A.shift_right_chip, 0, 71, 14, 1, False, "alu/sr/mod.rs:139", None),
+    "CloClz": (A.clo_clz_chip, 0, 22, 4, 1, False, "alu/clo_clz/mod.rs:75", None),
+    "Mul": (MC.mul_chip, 0, 58, 11, 1, True, "alu/mul/mod.rs:138", "alu/mul/mod.rs:214"),
+    "DivRem": (MC.divrem_chip, 0, 106, 12, 1, True, "alu/divrem/mod.rs:199", "alu/divrem/mod.rs:360"),
+    "Branch": (MC.branch_chip, 0, 62, 5, 1, True, "control_flow/branch/trace.rs:21", "control_flow/branch/trace.rs:76"),
+    "Jump": (MC.jump_chip, 0, 66, 2, 1, True, "control_flow/jump/trace.rs:21", "control_flow/jump/trace.rs:76"),
+    "MovCond": (MC.movcond_chip, 0, 32, 2, 1, True, "misc/mov_cond/mod.rs:64", "misc/mov_cond/mod.rs:119"),
+    "MemoryInstrs": (MC.memory_instructions_chip, 0, 79, 7, 1, True, "memory/instructions/trace.rs:25",
+                     "memory/instructions/trace.rs:82"),
+    "MiscInstrs": (MC.misc_instructions_chip, 0, 72, 17, 1, False, "misc/others/trace.rs:24", None),
+}
+
+
+def _cost(ch):
+    return ch.prep_width + ch.main_width + 4 * ch.perm_width_ef + 4 * (1 << ch.log_quotient_degree)
+
+
+@pytest.mark.parametrize("name", sorted(CHIPS))
+def test_chip_shape_and_cost(name):
+    build, prep, main, perm, lqd, local_only, _impl, _override = CHIPS[name]
+    ch = build()
+    assert ch.name == name
+    assert (ch.prep_width, ch.main_width, ch.perm_width_ef, ch.log_quotient_degree) == (prep, main, perm, lqd)
+    assert ch.local_only is local_only
+    assert _cost(ch) == COSTS[name], f"{name}: cost {_cost(ch)} != mips_costs.json {COSTS[name]}"
+
+
+def test_local_only_reaches_the_blob():
+    """The machine blob carries each chip's local_only to the prover (and the oracle)."""
+    chips = [CHIPS[n][0]() for n in sorted(CHIPS)]
+    m = MachineDesc(chips, 8)
+    mh = O.lib().orc_api_machine_new(m.blob(), m.blob().size)
+    try:
+        for i, n in enumerate(sorted(CHIPS)):
+            info = np.zeros(7, np.int32)
+            assert O.lib().orc_api_machine_info(mh, i, info) == 0
+            assert (info[0], info[1], info[2], info[3]) == CHIPS[n][1:5]
+            assert bool(info[5]) is CHIPS[n][5]
+    finally:
+        O.lib().orc_api_machine_free(mh)
+
+
+def test_every_restated_chip_is_a_reference_chip():
+    """Chips the shard builders put in a machine are reference chips (plus the documented stand-ins)."""
+    stand_ins = {"RegisterState", "InstrSource"}
+    names = {c.name for c in MC.core_machine().chips}
+    assert names - stand_ins <= set(COSTS)
+    assert names - stand_ins <= set(CHIPS)
+
+
+def test_dummy_vk_map_bytes_reproduced():
+    """crates/prover/dummy_vk_map.bin, regenerated from its decoded entries with the proof serializer's
+    conventions (u64 fixint lengths, [F;8] with no length, canonical u32 field elements, usize as u64),
+    hashes to the reference file's sha256.  Montgomery encoding does not."""
+    import hashlib
+    d = json.load(open(os.path.join(GOLDEN, "dummy_vk_map.json")))
+    assert d["rule_holds"]
+    n = d["entries"]
+    keys = np.repeat(np.arange(n, dtype=np.uint32)[:, None], 8, axis=1)
+    vals = np.arange(n, dtype=np.uint64)
+    b = O.serialize_digest_map(keys, vals)
+    assert len(b) == d["bytes"]
+    assert hashlib.sha256(b).hexdigest() == d["sha256"]
+    bm = O.serialize_digest_map(keys, vals, montgomery=True)
+    assert hashlib.sha256(bm).hexdigest() != d["sha256"]
+    rec = np.frombuffer(b[8:], np.uint8).reshape(n, 40)
+    assert [int(x) for x in rec[1, :32].copy().view("<u4")] + [int(rec[1, 32:].copy().view("<u8")[0])] == d["first"][1]
+
+
+def test_maximal_shapes_fixture():
+    """The reference's 2^22 shard compositions name only chips of mips_costs.json; each holds a
+    Cpu of at most 2^22 rows and no chip taller than 2^22."""
+    shapes = json.load(open(os.path.join(GOLDEN, "maximal_shapes_22.json")))
+    assert len(shapes) == 175
+    for s in shapes:
+        assert set(s) <= set(COSTS)
+        assert s["Cpu"] <= 22 and max(s.values()) <= 22

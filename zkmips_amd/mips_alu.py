@@ -295,7 +295,7 @@ OP_SRL, OP_SRA, OP_ROR = 10, 11, 12
 
 def shift_right_chip() -> ChipDesc:
     """ShiftRightChip::eval, alu/sr/mod.rs:338-536 (SRL, SRA, ROR)."""
-    ch = ChipDesc("ShiftRight", prep_width=0, main_width=SR_WIDTH, local_only=True)
+    ch = ChipDesc("ShiftRight", prep_width=0, main_width=SR_WIDTH)
     M = main
     real = _m(SR_REAL)
     ch.sends.append(Lookup([V.const(B_MSB), _m(SR_MSB), ZERO, _m(SR_B + 3), ZERO], real, KIND_BYTE))
@@ -357,7 +357,7 @@ UNUSED_PC, DEFAULT_PC_INC = 1, 4  # crates/stark/src/air/builder.rs:19-22
 def clo_clz_chip() -> ChipDesc:
     """CloClzChip::eval, alu/clo_clz/mod.rs:181-271.  It sends an SRL to the ShiftRight chip
     (send_alu, builder.rs:283-322) to prove that bit 31 - a of bb is its leading one."""
-    ch = ChipDesc("CloClz", prep_width=0, main_width=CZ_WIDTH, local_only=True)
+    ch = ChipDesc("CloClz", prep_width=0, main_width=CZ_WIDTH)
     M = main
     for i in range(4):
         ch.assert_zero(M(CZ_CLO) * (M(CZ_B + i) + M(CZ_BB + i) - 255))

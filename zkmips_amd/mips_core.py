@@ -917,7 +917,7 @@ def _shift_word(*terms):
 def misc_instructions_chip() -> ChipDesc:
     """MiscInstrsChip::eval with eval_ext / eval_ins / eval_maddsub / eval_sext (misc/others/air.rs:24-418):
     SEXT (SEB/SEH), EXT, INS, MADDU/MSUBU/MADD/MSUB and TEQ, constraints and lookups in its order."""
-    ch = ChipDesc("MiscInstrs", prep_width=0, main_width=MS_WIDTH, local_only=True)
+    ch = ChipDesc("MiscInstrs", prep_width=0, main_width=MS_WIDTH)
     M = main
     sext, ins, ext, maddu, msubu, madd, msub, teq = (M(MS_SEL + k) for k in range(8))
     is_real = sext + ins + ext + maddu + msubu + madd + msub + teq
