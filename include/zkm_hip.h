@@ -77,6 +77,14 @@ void zkm_destroy(zkm_ctx *ctx);
 const char *zkm_last_error(void);  /* thread-local message of the last failing call */
 int zkm_device_count(void);
 
+/* ---- page-locked host memory for traces ----
+ * A trace generator that writes its RowMajorMatrix storage here hands the prover host buffers
+ * the DMA engines read directly: the H2D copy runs asynchronously, overlapped with this and other
+ * shards' kernels, at the PCIe rate.  Any other host pointer is also accepted (the runtime stages
+ * it, and the call waits for the copy).  Backs the Rust shim's trace allocator. */
+int zkm_host_alloc(size_t bytes, void **out);
+void zkm_host_free(void *p);
+
 /* ---- MachineProver::setup (prover.rs:52 -> machine.rs:332-439) ----
  * machine_blob: machine description (format below); prep[i] is the preprocessed trace of
  * machine chip i (data == NULL / width 0 for chips without one).  Writes the preprocessed

@@ -63,30 +63,66 @@ static kb_t *lde_of(const kb_t *evals, size_t h, size_t w, kb_t shift, int log_b
     return out;
 }
 
-/* opened value of every column of a committed LDE (bit-reversed, 2^lb * n rows) at z:
- * interpolate the low coset (first n rows = GENERATOR * H_n, bit-reversed) and evaluate. */
-static void open_matrix_at(const orc_mat_t *lde, int log_blowup, ef_t z, ef_t *out) {
-    size_t H = lde->height, n = H >> log_blowup, w = lde->width;
-    int logn = log2_exact(n);
-    ef_t zs = ef_mul_base(z, kb_inv(KB_GENERATOR));
-#pragma omp parallel for schedule(dynamic, 1)
-    for (size_t c = 0; c < w; c++) {
-        kb_t *buf = (kb_t *)malloc(sizeof(kb_t) * n);
-        for (size_t j = 0; j < n; j++) buf[j] = lde->data[(size_t)rev_bits((uint32_t)j, logn) * w + c];
-        orc_dft_natural(buf, logn, 1);
-        out[c] = orc_eval_coeffs_ef(buf, n, zs);
-        free(buf);
+/* Montgomery's batch inversion, in independent chunks (one field inversion per chunk) so the
+ * chunks run in parallel; every element must be non-zero. */
+#define BI_CHUNK 4096
+static void batch_inverse(ef_t *v, size_t n) {
+#pragma omp parallel for schedule(static)
+    for (size_t c0 = 0; c0 < n; c0 += BI_CHUNK) {
+        size_t m = n - c0 < BI_CHUNK ? n - c0 : BI_CHUNK;
+        ef_t pre[BI_CHUNK], acc = ef_one();
+        for (size_t i = 0; i < m; i++) { pre[i] = acc; acc = ef_mul(acc, v[c0 + i]); }
+        ef_t inv = ef_inv(acc);
+        for (size_t i = m; i-- > 0;) { ef_t t = ef_mul(inv, pre[i]); inv = ef_mul(inv, v[c0 + i]); v[c0 + i] = t; }
+    }
+}
+static void batch_inverse_kb(kb_t *v, size_t n) {
+#pragma omp parallel for schedule(static)
+    for (size_t c0 = 0; c0 < n; c0 += BI_CHUNK) {
+        size_t m = n - c0 < BI_CHUNK ? n - c0 : BI_CHUNK;
+        kb_t pre[BI_CHUNK], acc = 1;
+        for (size_t i = 0; i < m; i++) { pre[i] = acc; acc = kb_mul(acc, v[c0 + i]); }
+        kb_t inv = kb_inv(acc);
+        for (size_t i = m; i-- > 0;) { kb_t t = kb_mul(inv, pre[i]); inv = kb_mul(inv, v[c0 + i]); v[c0 + i] = t; }
     }
 }
 
-static void batch_inverse(ef_t *v, size_t n) {
-    if (!n) return;
-    ef_t *pre = (ef_t *)malloc(sizeof(ef_t) * n);
-    ef_t acc = ef_one();
-    for (size_t i = 0; i < n; i++) { pre[i] = acc; acc = ef_mul(acc, v[i]); }
-    ef_t inv = ef_inv(acc);
-    for (size_t i = n; i-- > 0;) { ef_t t = ef_mul(inv, pre[i]); inv = ef_mul(inv, v[i]); v[i] = t; }
-    free(pre);
+/* pw[k] = g^k for k < n (parallel: each chunk starts from its own power) */
+static kb_t *powers(kb_t g, size_t n) {
+    kb_t *pw = (kb_t *)malloc(sizeof(kb_t) * (n ? n : 1));
+#pragma omp parallel for schedule(static)
+    for (size_t c0 = 0; c0 < n; c0 += BI_CHUNK) {
+        kb_t x = kb_pow(g, c0);
+        for (size_t i = c0; i < n && i < c0 + BI_CHUNK; i++) { pw[i] = x; x = kb_mul(x, g); }
+    }
+    return pw;
+}
+
+/* opened value of every column of a committed LDE (bit-reversed, 2^lb * n rows) at z, by
+ * barycentric interpolation over the low coset D = GENERATOR * H_n: its first n rows, where row r
+ * holds p(3 w_n^{rev_n(r)}).  With x = z / 3:
+ *     p(z) = (x^n - 1) / n * sum_j p(3 w^j) * w^j / (x - w^j). */
+static void open_matrix_at(const orc_mat_t *lde, int log_blowup, ef_t z, ef_t *out) {
+    size_t H = lde->height, n = H >> log_blowup, w = lde->width;
+    int logn = log2_exact(n);
+    ef_t x = ef_mul_base(z, kb_inv(KB_GENERATOR));
+    kb_t *om = powers(kb_two_adic_gen(logn), n);
+    ef_t *wt = (ef_t *)malloc(sizeof(ef_t) * n);
+#pragma omp parallel for schedule(static)
+    for (size_t j = 0; j < n; j++) wt[j] = ef_sub(x, ef_from_base(om[j]));
+    batch_inverse(wt, n);
+#pragma omp parallel for schedule(static)
+    for (size_t j = 0; j < n; j++) wt[j] = ef_mul_base(wt[j], om[j]);
+    ef_t pre = ef_mul_base(ef_sub(ef_pow(x, n), ef_one()), kb_inv((kb_t)(n % KB_P)));
+#pragma omp parallel for schedule(dynamic, 1)
+    for (size_t c = 0; c < w; c++) {
+        ef_t acc = ef_zero();
+        for (size_t j = 0; j < n; j++)
+            acc = ef_add(acc, ef_mul_base(wt[j], lde->data[(size_t)rev_bits((uint32_t)j, logn) * w + c]));
+        out[c] = ef_mul(pre, acc);
+    }
+    free(wt);
+    free(om);
 }
 
 /* ------------------------------------------------------------------- setup */
@@ -285,15 +321,29 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
         ef_t *q = (ef_t *)malloc(sizeof(ef_t) * Q);
         size_t step = (size_t)1 << lqd;
         int pw = c->perm_width_ef;
+        /* selectors on the quotient coset 3 * H_Q (zerofier_coset.rs:22-71, quotient.rs:42): the
+         * three denominators of every point inverted in batches */
+        kb_t *xs = powers(wQ, Q), *d1 = (kb_t *)malloc(sizeof(kb_t) * Q), *d2 = (kb_t *)malloc(sizeof(kb_t) * Q),
+             *d3 = (kb_t *)malloc(sizeof(kb_t) * Q);
+#pragma omp parallel for schedule(static)
+        for (size_t k = 0; k < Q; k++) {
+            xs[k] = kb_mul(KB_GENERATOR, xs[k]);
+            d1[k] = kb_sub(xs[k], 1);
+            d2[k] = kb_sub(xs[k], wN_inv);
+            d3[k] = kb_sub(kb_pow(xs[k], N), 1);
+        }
+        batch_inverse_kb(d1, Q);
+        batch_inverse_kb(d2, Q);
+        batch_inverse_kb(d3, Q);
 #pragma omp parallel for schedule(static)
         for (size_t k = 0; k < Q; k++) {
             size_t rl = rev_bits((uint32_t)k, logQ), rn = rev_bits((uint32_t)((k + step) % Q), logQ);
-            kb_t x = kb_mul(KB_GENERATOR, kb_pow(wQ, k));
+            kb_t x = xs[k];
             kb_t zh = kb_sub(kb_pow(x, N), 1);
-            kb_t is_first = kb_mul(zh, kb_inv(kb_sub(x, 1)));
-            kb_t is_last = kb_mul(zh, kb_inv(kb_sub(x, wN_inv)));
+            kb_t is_first = kb_mul(zh, d1[k]);
+            kb_t is_last = kb_mul(zh, d2[k]);
             kb_t is_trans = kb_sub(x, wN_inv);
-            kb_t invz = kb_inv(zh);
+            kb_t invz = d3[k];
             const kb_t *pl = prep_lde ? prep_lde->data + rl * prep_lde->width : NULL;
             const kb_t *pn = prep_lde ? prep_lde->data + rn * prep_lde->width : NULL;
             const kb_t *ml = main_lde->data + rl * main_lde->width, *mn = main_lde->data + rn * main_lde->width;
@@ -307,7 +357,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
                                       perm_ch[0], perm_ch[1], out->chips[i].lcs, out->chips[i].gcs, pows);
             q[k] = ef_mul_base(acc, invz);
         }
-        free(pows);
+        free(pows); free(xs); free(d1); free(d2); free(d3);
         /* split_evals: chunk j takes rows k = j (mod 2^lqd); domain shift 3 * wQ^j, commit shift wQ^-j */
         for (int j = 0; j < (1 << lqd); j++) {
             kb_t *chunk = (kb_t *)malloc(sizeof(kb_t) * N * 4);
@@ -377,11 +427,13 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
             }
             ef_t z = req[r].pts[p];
             ef_t *den = (ef_t *)malloc(sizeof(ef_t) * H);
+            kb_t *xp = powers(wH, H);
 #pragma omp parallel for schedule(static)
             for (size_t i = 0; i < H; i++) {
-                kb_t x = kb_mul(KB_GENERATOR, kb_pow(wH, rev_bits((uint32_t)i, lh)));
+                kb_t x = kb_mul(KB_GENERATOR, xp[rev_bits((uint32_t)i, lh)]);
                 den[i] = ef_sub(z, ef_from_base(x));
             }
+            free(xp);
             batch_inverse(den, H);
 #pragma omp parallel for schedule(static)
             for (size_t i = 0; i < H; i++) {

@@ -6,7 +6,7 @@ on MI355X (tools/probe/valu_probe.hip, profiles/r01_valu_probe.txt): v_add/v_sub
 at the full SIMD-32 rate (1 slot per wave64 instruction pair of cycles), everything else we use
 (min/max, shifts, 32-bit multiplies, v_mad_u64_u32, v_lshl_add_u64, carry-out adds v_add_co/v_addc_co,
 3-operand forms, DPP/SDWA forms) at half rate
-(2 slots).  Writes profiles/<tag>_isa_p2.json.   python tools/isa_slots.py r01
+(2 slots).  Writes profiles/<tag>_isa_p2.json and zkmips_amd/isa_p2.json.   python tools/isa_slots.py r01
 """
 import collections
 import json
@@ -43,6 +43,8 @@ def main(tag):
            "full_rate_pattern": FULL.pattern, "by_op": dict(ops.most_common())}
     path = os.path.join(ROOT, "profiles", f"{tag}_isa_p2.json")
     json.dump(out, open(path, "w"), indent=1)
+    # the copy bench.py reads on the GPU box (profiles/ does not travel there)
+    json.dump(out, open(os.path.join(ROOT, "zkmips_amd", "isa_p2.json"), "w"), indent=1)
     print(path, out["valu_instructions"], slots)
 
 

@@ -63,6 +63,8 @@ def lib():
     L.zkm_poseidon2_permute.argtypes = [vp, vp, C.c_uint64]
     L.zkm_pcs_commit_root.argtypes = [vp, C.POINTER(Matrix), C.c_uint32, vp]
     L.zkm_bench_lde.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+    L.zkm_host_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
+    L.zkm_host_free.argtypes = [vp]
     if hasattr(L, "zkm_setup"):
         L.zkm_setup.argtypes = [vp, vp, C.c_size_t, C.POINTER(Config), C.POINTER(Matrix), C.c_uint32, C.c_uint32,
                                 vp, C.POINTER(vp), vp]
@@ -101,6 +103,29 @@ def matrix(arr: np.ndarray, name: str = "", montgomery: bool = False, keep: list
         keep.append(nm)
     return Matrix(nm, a.ctypes.data if a.size else None, a.shape[0], a.shape[1],
                   ZKM_REPR_MONTGOMERY if montgomery else ZKM_REPR_CANONICAL)
+
+
+class PinnedArray:
+    """A numpy u32 array in page-locked host memory (zkm_host_alloc): traces written here cross PCIe
+    by asynchronous DMA, overlapped with kernels.  Keep the object alive while the array is used."""
+
+    def __init__(self, shape):
+        n = int(np.prod(shape))
+        self.p = C.c_void_p()
+        check(lib().zkm_host_alloc(max(4, n * 4), C.byref(self.p)), "zkm_host_alloc")
+        self.array = np.ctypeslib.as_array(C.cast(self.p, C.POINTER(C.c_uint32)), shape=(max(1, n),))[:n].reshape(shape)
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            self.array = None
+            lib().zkm_host_free(self.p)
+            self.p = None
+
+
+def pinned_copy(a: np.ndarray) -> PinnedArray:
+    b = PinnedArray(a.shape)
+    np.copyto(b.array, as_u32(a))
+    return b
 
 
 class Device:

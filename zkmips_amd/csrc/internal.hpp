@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -103,12 +104,26 @@ struct Ctx {
     void release_stream(hipStream_t s);
 };
 
+// One HIP stream per entry-point call.  When the call unwinds with an exception, only this
+// stream is drained (device buffers are stream-ordered in the pool; host temporaries that async
+// copies may still touch are gone once the stream is idle) — other shards' streams keep running.
 struct StreamLease {
     Ctx *c;
     hipStream_t s;
-    explicit StreamLease(Ctx *ctx) : c(ctx), s(ctx->acquire_stream()) {}
-    ~StreamLease() { c->release_stream(s); }
+    int exc0;
+    explicit StreamLease(Ctx *ctx) : c(ctx), s(ctx->acquire_stream()), exc0(std::uncaught_exceptions()) {}
+    ~StreamLease() {
+        if (std::uncaught_exceptions() > exc0) (void)hipStreamSynchronize(s);
+        c->release_stream(s);
+    }
 };
+
+// host/device row-major zkm_matrix_t -> device column-major Montgomery (capi.cpp)
+}  // namespace zkm
+#include "../../include/zkm_hip.h"
+namespace zkm {
+void upload_matrix_into(Ctx &c, const zkm_matrix_t &m, uint32_t *col, hipStream_t s);
+DBuf upload_matrix(Ctx &c, const zkm_matrix_t &m, hipStream_t s);
 
 // ---------------------------------------------------------------- kernels (launchers)
 // host row-major (canonical or Montgomery) -> device column-major Montgomery

@@ -247,10 +247,10 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
       << g.pipelined(8, "ZKM_JIT_LOOKAHEAD_Q")  // measured: 8 -> 2.27 ms, 24 -> 2.44, unpipelined 2.78
       << "    const ef qv = ef_mul_base(facc.value(), inv_z);\n"
       << "    const uint64_t c = t >> A.log_n, pos = t & (A.n - 1);\n"
-      << "    A.chunks[(c * 4 + 0) * A.n + pos] = qv.c[0];\n"
-      << "    A.chunks[(c * 4 + 1) * A.n + pos] = qv.c[1];\n"
-      << "    A.chunks[(c * 4 + 2) * A.n + pos] = qv.c[2];\n"
-      << "    A.chunks[(c * 4 + 3) * A.n + pos] = qv.c[3];\n"
+      << "    A.chunks[c * A.cstride + 0 * A.n + pos] = qv.c[0];\n"
+      << "    A.chunks[c * A.cstride + 1 * A.n + pos] = qv.c[1];\n"
+      << "    A.chunks[c * A.cstride + 2 * A.n + pos] = qv.c[2];\n"
+      << "    A.chunks[c * A.cstride + 3 * A.n + pos] = qv.c[3];\n"
       << "}\n";
     return o.str();
 }

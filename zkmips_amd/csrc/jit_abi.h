@@ -10,6 +10,7 @@ struct ZkmQuotJitArgs {
     const unsigned *tw;                  // forward twiddles
     unsigned *chunks;                    // 2^lqd chunks x 4 columns x n rows (bit-reversed rows)
     unsigned long long ld, n, q;
+    unsigned long long cstride;          // words between chunk j and chunk j+1 (column stride is n)
     int log_n, log_q, step, pad0;
     unsigned gen, gen_pow_n, wn_inv, pad1;
     unsigned alpha_p[4], lcs[4];

@@ -295,7 +295,7 @@ __global__ __launch_bounds__(NT) void k_quotient(QuotArgs a) {
     const uint64_t c = t >> a.log_n;
     const uint64_t pos = t & (a.n - 1);
 #pragma unroll
-    for (int e = 0; e < 4; e++) a.chunks[(c * 4 + e) * a.n + pos] = q.c[e];
+    for (int e = 0; e < 4; e++) a.chunks[c * a.cstride + e * a.n + pos] = q.c[e];
 }
 
 void launch_quotient(const QuotArgs &a, hipStream_t s) {

@@ -33,6 +33,7 @@ struct QuotArgs {
     uint32_t gcs[14];
     int batch, perm_w, global, main_w;
     uint32_t *chunks;                    // 2^lqd chunks x 4 columns x n rows (bit-reversed rows)
+    uint64_t cstride;                    // words from chunk j to chunk j+1
 };
 void launch_quotient(const QuotArgs &a, hipStream_t s);
 

@@ -28,7 +28,6 @@ using namespace kb;
 using Digest = std::array<uint32_t, 8>;
 
 int guard_status(const std::exception &e);
-DBuf upload_matrix(const zkm_matrix_t &m, hipStream_t s);
 extern thread_local std::string g_last_error;
 
 static const uint32_t CURVE_START[14] = {637514027u, 1595065213u, 1998064738u, 72333738u,  1211544370u,
@@ -112,7 +111,8 @@ struct Pk {
 struct MainData {
     std::vector<int> chip;         // machine chip index, in commit order (height desc, name)
     std::vector<uint64_t> heights;
-    std::vector<DBuf> traces;      // column-major natural
+    std::vector<DBuf> store;       // one column-major natural buffer per height group
+    std::vector<const uint32_t *> trace;  // chip i's columns inside its group's buffer
     DTree tree;
     std::vector<uint32_t> pv;      // canonical
 };
@@ -133,6 +133,29 @@ static void add_lde(Ctx &c, DTree &t, const DMat &src, uint32_t shift, bool bitr
     if (bitrev_in) lde_batch_bitrev_in(c, src, shift, dst, s);
     else lde_batch(c, src, shift, dst, s);
     t.mats.push_back(dst);
+}
+
+// One LDE launch sequence for several same-height matrices whose columns sit side by side in `src`
+// (column stride N): the evaluations go to one buffer owned by the tree, and each matrix gets its
+// sub-view (returned in order; the caller places them in the tree's commit order).  Same-height
+// chips of a shard thus share launches instead of taking a handful each.
+static std::vector<DMat> lde_group(Ctx &c, DTree &t, const uint32_t *src, uint64_t N, const std::vector<uint64_t> &widths,
+                                   uint32_t shift, bool bitrev_in, hipStream_t s) {
+    const uint64_t W = std::accumulate(widths.begin(), widths.end(), (uint64_t)0);
+    t.owned.emplace_back(2 * N * (W ? W : 1), s);
+    uint32_t *dst = t.owned.back().p;
+    if (W) {
+        DMat sm{const_cast<uint32_t *>(src), N, W}, dm{dst, 2 * N, W};
+        if (bitrev_in) lde_batch_bitrev_in(c, sm, shift, dm, s);
+        else lde_batch(c, sm, shift, dm, s);
+    }
+    std::vector<DMat> v;
+    uint64_t off = 0;
+    for (uint64_t w : widths) {
+        v.push_back(DMat{dst + off * 2 * N, 2 * N, w});
+        off += w;
+    }
+    return v;
 }
 
 // ------------------------------------------------------------------ proof object + bincode
@@ -260,7 +283,22 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     PROF("open_total", s, 0);
     // ---- permutation traces (prover.rs:337-365) ----
     proof.chips.resize(n);
-    std::vector<DBuf> perm_traces(n);
+    // chips come in commit order (height desc), so same-height chips are adjacent: one perm-trace
+    // buffer per height group, LDE'd together once every chip of the group has its trace
+    std::vector<const uint32_t *> perm_traces(n);
+    std::vector<DBuf> perm_store;
+    std::vector<int> grp_end(n);
+    for (int a = 0, b; a < n; a = b) {
+        uint64_t W = 0;
+        for (b = a; b < n && md.heights[b] == md.heights[a]; b++) W += 4 * (uint64_t)m.chips[md.chip[b]].perm_w;
+        perm_store.emplace_back(md.heights[a] * (W ? W : 1), s);
+        uint64_t off = 0;
+        for (int k = a; k < b; k++) {
+            perm_traces[k] = perm_store.back().p + off * md.heights[a];
+            off += 4 * (uint64_t)m.chips[md.chip[k]].perm_w;
+            grp_end[k] = b;
+        }
+    }
     DTree perm_tree;
     for (int i = 0; i < n; i++) {
         const ChipDesc &cd = m.chips[md.chip[i]];
@@ -271,11 +309,10 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         co.log_degree = (uint64_t)ilog2(N);
         co.lcs = ef_zero();
         const int pw = cd.perm_w;
-        perm_traces[i] = DBuf(N * 4 * (pw ? pw : 1), s);
         if (pw) {
             DBuf rowsum(4 * N, s);
-            PermArgs a{pk.progs[md.chip[i]].p, md.traces[i].p, pki >= 0 ? pk.traces[pki].p : nullptr, N, perm_alpha,
-                       d_bpow.p, 1 << cd.log_qd, pw - 1, perm_traces[i].p, rowsum.p};
+            PermArgs a{pk.progs[md.chip[i]].p, md.trace[i], pki >= 0 ? pk.traces[pki].p : nullptr, N, perm_alpha,
+                       d_bpow.p, 1 << cd.log_qd, pw - 1, const_cast<uint32_t *>(perm_traces[i]), rowsum.p};
             {
                 PROF("perm_trace", s, 4.0 * N * (cd.main_w + cd.prep_w) + 16.0 * N * (pw + 2));
                 const JitKernel &jk = pk.jit[md.chip[i]];
@@ -290,21 +327,27 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             }
             uint32_t l[4];
             for (int e = 0; e < 4; e++)
-                HIP_CHECK(hipMemcpyAsync(&l[e], perm_traces[i].p + (uint64_t)(4 * (pw - 1) + e) * N + N - 1, 4,
+                HIP_CHECK(hipMemcpyAsync(&l[e], perm_traces[i] + (uint64_t)(4 * (pw - 1) + e) * N + N - 1, 4,
                                          hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
             co.lcs = ef{{l[0], l[1], l[2], l[3]}};
         }
         if (cd.scope == 1) {
             for (int k = 0; k < 14; k++)
-                HIP_CHECK(hipMemcpyAsync(&co.gcs[k], md.traces[i].p + (uint64_t)(cd.main_w - 14 + k) * N + N - 1, 4,
+                HIP_CHECK(hipMemcpyAsync(&co.gcs[k], md.trace[i] + (uint64_t)(cd.main_w - 14 + k) * N + N - 1, 4,
                                          hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
         } else {
             for (int k = 0; k < 14; k++) co.gcs[k] = to_mont(CURVE_START[k]);
         }
-        DMat src{perm_traces[i].p, N, (uint64_t)4 * pw};
-        add_lde(c, perm_tree, src, to_mont(GENERATOR), false, s);
+        if (grp_end[i] == i + 1) {  // last chip of its height group: LDE the group
+            int a = i;
+            while (a > 0 && md.heights[a - 1] == N) a--;
+            std::vector<uint64_t> ws;
+            for (int k = a; k <= i; k++) ws.push_back(4 * (uint64_t)m.chips[md.chip[k]].perm_w);
+            for (const DMat &v : lde_group(c, perm_tree, perm_traces[a], N, ws, to_mont(GENERATOR), false, s))
+                perm_tree.mats.push_back(v);
+        }
     }
     tree_build(perm_tree, s);
     proof.perm_c = dig(perm_tree.root);
@@ -321,7 +364,25 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     DBuf d_pv(pv_mont.size(), s);
     HIP_CHECK(hipMemcpyAsync(d_pv.p, pv_mont.data(), pv_mont.size() * 4, hipMemcpyHostToDevice, s));
     DTree q_tree;
-    std::vector<DBuf> q_chunks(n);
+    // Quotient chunks grouped like the perm traces, by (height, log_qd): in a group of g chips, chunk
+    // j of the group's k-th chip is columns 4k..4k+3 of block j (block stride 4gN), so every chunk j
+    // of the group is one bit-reversed-input LDE with the shared shift (3 w^j)^-1.
+    std::vector<DBuf> q_store;
+    std::vector<std::vector<const uint32_t *>> q_ptr(n);
+    std::vector<std::vector<DMat>> q_view(n);
+    std::vector<uint64_t> q_cstride(n);
+    std::vector<int> q_first(n);
+    for (int a = 0, b; a < n; a = b) {
+        const int lqd = m.chips[md.chip[a]].log_qd;
+        for (b = a; b < n && md.heights[b] == md.heights[a] && m.chips[md.chip[b]].log_qd == lqd; b++) {}
+        const uint64_t N = md.heights[a], T = 4 * (uint64_t)(b - a);
+        q_store.emplace_back(((uint64_t)1 << lqd) * T * N, s);
+        for (int k = a; k < b; k++) {
+            q_first[k] = a;
+            q_cstride[k] = T * N;
+            for (int j = 0; j < (1 << lqd); j++) q_ptr[k].push_back(q_store.back().p + j * T * N + 4 * (uint64_t)(k - a) * N);
+        }
+    }
     std::vector<int> chunk_chip;  // chip of each quotient chunk
     for (int i = 0; i < n; i++) {
         const ChipDesc &cd = m.chips[md.chip[i]];
@@ -338,7 +399,6 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         DBuf d_pows(pows.size(), s);
         HIP_CHECK(hipMemcpyAsync(d_pows.p, pows.data(), pows.size() * 4, hipMemcpyHostToDevice, s));
         const int pki = pk.pk_index(md.chip[i]);
-        q_chunks[i] = DBuf(((uint64_t)4 << lqd) * N, s);
         QuotArgs qa{};
         qa.prog = pk.progs[md.chip[i]].p;
         qa.main = md.tree.mats[i].d;
@@ -355,14 +415,15 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         qa.alpha_p = perm_alpha; qa.beta_pows = d_bpow.p; qa.lcs = proof.chips[i].lcs;
         memcpy(qa.gcs, proof.chips[i].gcs, sizeof qa.gcs);
         qa.batch = 1 << lqd; qa.perm_w = cd.perm_w; qa.global = cd.scope == 1; qa.main_w = cd.main_w;
-        qa.chunks = q_chunks[i].p;
+        qa.chunks = const_cast<uint32_t *>(q_ptr[i][0]);
+        qa.cstride = q_cstride[i];
         {
             PROF("quotient", s, 8.0 * Q * (cd.main_w + cd.prep_w + 4 * cd.perm_w) + 16.0 * Q);
             const JitKernel &jk = pk.jit[md.chip[i]];
             if (jk.ok) {
                 ZkmQuotJitArgs ja{};
                 ja.main = qa.main; ja.prep = qa.prep; ja.perm = qa.perm; ja.pv = qa.pv; ja.pows = qa.pows;
-                ja.beta_pows = qa.beta_pows; ja.tw = qa.tw; ja.chunks = qa.chunks;
+                ja.beta_pows = qa.beta_pows; ja.tw = qa.tw; ja.chunks = qa.chunks; ja.cstride = qa.cstride;
                 ja.ld = qa.ld; ja.n = qa.n; ja.q = qa.q; ja.log_n = qa.log_n; ja.log_q = qa.log_q; ja.step = qa.step;
                 ja.gen = qa.gen; ja.gen_pow_n = qa.gen_pow_n; ja.wn_inv = qa.wn_inv;
                 memcpy(ja.alpha_p, qa.alpha_p.c, 16); memcpy(ja.lcs, qa.lcs.c, 16); memcpy(ja.gcs, qa.gcs, sizeof ja.gcs);
@@ -372,13 +433,21 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             }
         }
         HIP_CHECK(hipStreamSynchronize(s));  // d_pows lifetime
-        const uint32_t wq = two_adic_gen(logN + lqd);
-        for (int j = 0; j < (1 << lqd); j++) {
-            DMat src{q_chunks[i].p + (uint64_t)j * 4 * N, N, 4};
-            add_lde(c, q_tree, src, inv(pow(wq, (uint64_t)j)), true, s);
-            chunk_chip.push_back(i);
+        if (i + 1 == n || q_first[i + 1] != q_first[i]) {  // last chip of its group: LDE the group's chunks
+            const int a = q_first[i];
+            const uint32_t wq = two_adic_gen(logN + lqd);
+            const std::vector<uint64_t> ws(i - a + 1, 4);
+            for (int j = 0; j < (1 << lqd); j++) {
+                std::vector<DMat> v = lde_group(c, q_tree, q_ptr[a][j], N, ws, inv(pow(wq, (uint64_t)j)), true, s);
+                for (int k = a; k <= i; k++) q_view[k].push_back(v[k - a]);
+            }
         }
     }
+    for (int i = 0; i < n; i++)
+        for (const DMat &v : q_view[i]) {
+            q_tree.mats.push_back(v);
+            chunk_chip.push_back(i);
+        }
     tree_build(q_tree, s);
     proof.quot_c = dig(q_tree.root);
     ch.observe(q_tree.root, 8);
@@ -411,15 +480,15 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         for (auto &r : req) {
             Pend q{&r, nullptr, 0, 0, false, ONE, 0, 0, ef_zero(), 1};
             if (r.round == 0) { q.ybase = pk.traces[r.mat].p; q.N = pk.heights[r.mat]; q.W = m.chips[pk.trace_chip[r.mat]].prep_w; }
-            else if (r.round == 1) { q.ybase = md.traces[r.mat].p; q.N = md.heights[r.mat]; q.W = m.chips[md.chip[r.mat]].main_w; }
-            else if (r.round == 2) { q.ybase = perm_traces[r.mat].p; q.N = md.heights[r.mat]; q.W = 4 * m.chips[md.chip[r.mat]].perm_w; }
+            else if (r.round == 1) { q.ybase = md.trace[r.mat]; q.N = md.heights[r.mat]; q.W = m.chips[md.chip[r.mat]].main_w; }
+            else if (r.round == 2) { q.ybase = perm_traces[r.mat]; q.N = md.heights[r.mat]; q.W = 4 * m.chips[md.chip[r.mat]].perm_w; }
             else {
                 const int ci = chunk_chip[r.mat];
                 int j = 0;
                 for (int k = 0; k < r.mat; k++) if (chunk_chip[k] == ci) j++;
                 q.N = md.heights[ci];
                 const int lqd = m.chips[md.chip[ci]].log_qd;
-                q.ybase = q_chunks[ci].p + (uint64_t)j * 4 * q.N;
+                q.ybase = q_ptr[ci][j];
                 q.W = 4;
                 q.bitrev = true;
                 q.shift = mul(to_mont(GENERATOR), pow(two_adic_gen(ilog2(q.N) + lqd), (uint64_t)j));
@@ -712,7 +781,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
 using namespace zkm;
 
 static int status_of(const std::exception &e) {
-    (void)hipDeviceSynchronize();  // no buffer is released while kernels that use it are in flight
+    // the failing call's stream was drained by its StreamLease; other streams are not touched
     std::string w = e.what();
     if (w.rfind("UNSATISFIED", 0) == 0) { g_last_error = w; return ZKM_ERR_UNSATISFIED; }
     if (w.find("not supported") != std::string::npos) { g_last_error = w; return ZKM_ERR_UNSUPPORTED; }
@@ -783,7 +852,7 @@ int zkm_setup(zkm_ctx *ctx, const uint32_t *blob, size_t nwords, const zkm_confi
         ARG_CHECK((prep[ci].height & (prep[ci].height - 1)) == 0, "heights must be powers of two");
         pk->trace_chip.push_back(ci);
         pk->heights.push_back(prep[ci].height);
-        pk->traces.push_back(upload_matrix(prep[ci], L.s));
+        pk->traces.push_back(upload_matrix(*c, prep[ci], L.s));
         DMat src{pk->traces.back().p, prep[ci].height, prep[ci].width};
         add_lde(*c, pk->tree, src, to_mont(GENERATOR), false, L.s);
     }
@@ -843,12 +912,27 @@ int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32
     }
     PROF("commit_total", L.s, 0);
     HPROF("commit");
-    for (int o : sort_order(hs, names)) {  // prover.rs:264
-        md->chip.push_back(chip[o]);
-        md->heights.push_back(hs[o]);
-        md->traces.push_back(upload_matrix(traces[o], L.s));
-        DMat src{md->traces.back().p, traces[o].height, traces[o].width};
-        add_lde(*c, md->tree, src, to_mont(GENERATOR), false, L.s);
+    // sorted by (height desc, name) (prover.rs:264); each run of equal heights is uploaded side by
+    // side into one column-major buffer and LDE'd in one batch
+    const std::vector<int> ord = sort_order(hs, names);
+    for (size_t a = 0, b; a < ord.size(); a = b) {
+        const uint64_t N = hs[ord[a]];
+        uint64_t W = 0;
+        for (b = a; b < ord.size() && hs[ord[b]] == N; b++) W += traces[ord[b]].width;
+        md->store.emplace_back(N * (W ? W : 1), L.s);
+        uint32_t *base = md->store.back().p;
+        std::vector<uint64_t> ws;
+        uint64_t off = 0;
+        for (size_t k = a; k < b; k++) {
+            const int o = ord[k];
+            md->chip.push_back(chip[o]);
+            md->heights.push_back(N);
+            md->trace.push_back(base + off * N);
+            upload_matrix_into(*c, traces[o], base + off * N, L.s);
+            ws.push_back(traces[o].width);
+            off += traces[o].width;
+        }
+        for (const DMat &v : lde_group(*c, md->tree, base, N, ws, to_mont(GENERATOR), false, L.s)) md->tree.mats.push_back(v);
     }
     tree_build(md->tree, L.s);
     md->pv.assign(pv, pv + npv);

@@ -489,6 +489,21 @@ def alu_shard(n_add: int, n_bit: int, seed: int = 3, n_lt: int = 0, n_sll: int =
     return alu_shard_from(alu_events(n_add, n_bit, seed, n_lt, n_sll, n_sr, n_clz), seed)
 
 
+def inv_mod_p(x) -> np.ndarray:
+    """Element-wise x^-1 mod p (0 for x = 0), by square-and-multiply over the whole array."""
+    x = np.asarray(x, np.int64) % P
+    b = x.astype(np.uint64)
+    r = np.ones_like(b)
+    e = P - 2
+    while e:
+        if e & 1:
+            r = r * b % np.uint64(P)
+        b = b * b % np.uint64(P)
+        e >>= 1
+    r[x == 0] = 0
+    return r.astype(np.int64)
+
+
 def _inv_table():
     """(x mod p)^-1 for x = b - c, b, c bytes (index x + 255)."""
     return np.asarray([pow(x % P, P - 2, P) if x else 0 for x in range(-255, 256)], np.uint64)

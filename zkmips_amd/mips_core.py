@@ -528,7 +528,7 @@ def _izw_cols(words: np.ndarray) -> np.ndarray:
     n = len(words)
     out = np.zeros((n, IZW_WIDTH), np.uint32)
     x = words.astype(np.int64) % P
-    inv = np.asarray([[pow(int(v), P - 2, P) if v else 0 for v in row] for row in x], np.int64).reshape(n, 4)
+    inv = A.inv_mod_p(x).reshape(n, 4)
     z = (x == 0).astype(np.uint32)
     out[:, 0:8:2] = inv
     out[:, 1:8:2] = z
@@ -862,7 +862,7 @@ def _mem_instr_trace(mevs, shard, byte_lookup):
     byte_lookup(A.B_MSB, msbyte[signed], np.zeros(int(signed.sum()), np.int64))
     byte_lookup(A.B_U8RANGE, ab[:, 1], ab[:, 2])
     s = ab[:, 1] + ab[:, 2] + ab[:, 3]
-    t[:n, MI_MSBZ] = np.asarray([pow(int(x), P - 2, P) if x else 0 for x in s], np.int64)
+    t[:n, MI_MSBZ] = A.inv_mod_p(s)
     t[:n, MI_MSBZ + 1] = s == 0
     z = s == 0
     byte_lookup(A.B_LTU, np.full(int(z.sum()), REF_NUM_REGISTERS - 1), ab[z, 0])
@@ -1007,70 +1007,87 @@ def misc_instructions_chip() -> ChipDesc:
 
 
 def _misc_trace(misc, shard, byte_lookup):
-    """MiscInstrsChip::event_to_row + populate_* (misc/others/trace.rs:81-262).  misc: (op, a, b, c, prev_a,
-    pc, npc, clk, hi_prev, hi_new, hi_prev_shard, hi_prev_clk)."""
+    """MiscInstrsChip::event_to_row + populate_* (misc/others/trace.rs:81-262), vectorised over the rows of
+    each opcode group.  misc: (op, a, b, c, prev_a, pc, npc, clk, hi_prev, hi_new, hi_prev_shard, hi_prev_clk)."""
     E = np.asarray(misc, np.int64).reshape(-1, 12)
     n = len(E)
     t = np.zeros((A._pow2(n), MS_WIDTH), np.uint32)
-    u = lambda v: np.asarray(v, np.int64).astype(np.uint32)
+    u64 = lambda v: np.asarray(v, np.int64).astype(np.uint64)
+    wb = lambda v: A._bytes(u64(v) & np.uint64(M32))
     S = MS_SPEC
-    for r, (op, a, b, c, pa, pc, npc, clk, hp, hn, hps, hpc) in enumerate(E.tolist()):
-        row = t[r]
-        row[MS_PC], row[MS_NPC] = pc, npc
-        for base, v in ((MS_A, a), (MS_B, b), (MS_C, c), (MS_PREV_A, pa)):
-            row[base:base + 4] = A._bytes(u([v]))[0]
-        row[MS_SEL + MISC_OPS.index(op)] = 1
-        if op in (OP_SEXT, OP_TEQ):
-            if c > 0:
-                bit, byte = (b & 0xFFFF) >> 15, (b >> 8) & 0xFF
-                row[S + 4] = 1
-            else:
-                bit, byte = (b & 0xFF) >> 7, b & 0xFF
-                row[S + 3] = 1
-            row[S], row[S + 1], row[S + 2] = bit, byte, int(a == b)
-            if op == OP_SEXT:
-                byte_lookup(A.B_MSB, np.asarray([byte]), np.zeros(1, np.int64))
-        elif op == OP_EXT:
-            lsb, msbd = c & 31, c >> 5
-            row[S], row[S + 1] = lsb, msbd
-            row[S + 2:S + 6] = A._bytes(u([(b << (31 - lsb - msbd)) & M32]))[0]
-            byte_lookup(A.B_U8RANGE, np.asarray([lsb]), np.asarray([msbd]))
-            byte_lookup(A.B_LTU, np.asarray([lsb + msbd]), np.asarray([32]))
-        elif op == OP_INS:
-            lsb, msb = c & 31, c >> 5
-            ror = ((pa >> lsb) | (pa << (32 - lsb))) & M32 if lsb else pa
-            srl = ror >> (msb - lsb + 1)
-            sll = (b << (31 - msb + lsb)) & M32
-            row[S], row[S + 1] = lsb, msb
-            for off, v in ((2, ror), (6, srl), (10, sll), (14, (srl + sll) & M32)):
-                row[S + off:S + off + 4] = A._bytes(u([v]))[0]
-            byte_lookup(A.B_U8RANGE, np.asarray([lsb]), np.asarray([msb]))
-            byte_lookup(A.B_LTU, np.asarray([lsb]), np.asarray([msb + 1]))
-            byte_lookup(A.B_LTU, np.asarray([msb]), np.asarray([32]))
-        else:  # MADDU / MSUBU / MADD / MSUB
-            row[MS_SHARD], row[MS_CLK] = shard, clk
-            signed = op in (OP_MADD, OP_MSUB)
-            prod = ((_s32(b) * _s32(c)) if signed else b * c) & ((1 << 64) - 1)
-            is_add = op in (OP_MADDU, OP_MADD)
-            s2lo, s2hi = (pa, hp) if is_add else (a, hn)
-            tot = (prod + ((s2hi << 32) | s2lo)) & ((1 << 64) - 1)
-            ab = list(prod.to_bytes(8, "little")), list(((s2hi << 32) | s2lo).to_bytes(8, "little"))
-            carry, cy = [], 0
-            for j in range(7):
-                cy = 1 if ab[0][j] + ab[1][j] + cy > 255 else 0
-                carry.append(cy)
-            for off, v in ((_MD_LO, prod & M32), (_MD_HI, prod >> 32), (_MD_VAL, tot & M32), (_MD_VALHI, tot >> 32),
-                           (_MD_S2HI, s2hi), (_MD_S2LO, s2lo), (_MD_HIACC, hp)):
-                row[S + off:S + off + 4] = A._bytes(u([v]))[0]
-            row[S + _MD_CARRY:S + _MD_CARRY + 7] = carry
-            for v in (prod & M32, prod >> 32, s2lo, s2hi, tot & M32, tot >> 32):
-                wb = A._bytes(u([v]))
-                byte_lookup(A.B_U8RANGE, wb[:, 0], wb[:, 1])
-                byte_lookup(A.B_U8RANGE, wb[:, 2], wb[:, 3])
+    op, a, b, c, pa = (E[:, j] for j in range(5))
+    t[:n, MS_PC], t[:n, MS_NPC] = E[:, 5], E[:, 6]
+    for base, v in ((MS_A, a), (MS_B, b), (MS_C, c), (MS_PREV_A, pa)):
+        t[:n, base:base + 4] = wb(v)
+    col = np.full(64, -1, np.int64)
+    col[list(MISC_OPS)] = np.arange(len(MISC_OPS))
+    t[np.arange(n), MS_SEL + col[op]] = 1
+    # SEXT / TEQ: sext view (most_sig_bit, sig_byte, a_eq_b, is_seb, is_seh)
+    r = np.nonzero((op == OP_SEXT) | (op == OP_TEQ))[0]
+    if len(r):
+        bb, half = b[r], c[r] > 0
+        bit = np.where(half, (bb & 0xFFFF) >> 15, (bb & 0xFF) >> 7)
+        byte = np.where(half, (bb >> 8) & 0xFF, bb & 0xFF)
+        t[r, S], t[r, S + 1], t[r, S + 2] = bit, byte, a[r] == bb
+        t[r, S + 3], t[r, S + 4] = ~half, half
+        sx = op[r] == OP_SEXT
+        byte_lookup(A.B_MSB, byte[sx], np.zeros(int(sx.sum()), np.int64))
+    # EXT: ext view (lsb, msbd, sll_val)
+    r = np.nonzero(op == OP_EXT)[0]
+    if len(r):
+        lsb, msbd = c[r] & 31, c[r] >> 5
+        t[r, S], t[r, S + 1] = lsb, msbd
+        t[r, S + 2:S + 6] = wb(u64(b[r]) << u64(31 - lsb - msbd))
+        byte_lookup(A.B_U8RANGE, lsb, msbd)
+        byte_lookup(A.B_LTU, lsb + msbd, np.full(len(r), 32))
+    # INS: ins view (lsb, msb, ror_val, srl_val, sll_val, add_val); the SRL shift is the field width, which
+    # the generator keeps below 32 (a full-width INS cannot satisfy eval_ins: see _execute)
+    r = np.nonzero(op == OP_INS)[0]
+    if len(r):
+        lsb, msb = c[r] & 31, c[r] >> 5
+        p = u64(pa[r])
+        ror = ((p >> u64(lsb)) | (p << u64(32 - lsb))) & np.uint64(M32)
+        srl = ror >> u64(msb - lsb + 1)
+        sll = (u64(b[r]) << u64(31 - msb + lsb)) & np.uint64(M32)
+        t[r, S], t[r, S + 1] = lsb, msb
+        for off, v in ((2, ror), (6, srl), (10, sll), (14, srl + sll)):
+            t[r, S + off:S + off + 4] = wb(v)
+        byte_lookup(A.B_U8RANGE, lsb, msb)
+        byte_lookup(A.B_LTU, lsb, msb + 1)
+        byte_lookup(A.B_LTU, msb, np.full(len(r), 32))
+    # MADDU / MSUBU / MADD / MSUB: maddsub view (product, 64-bit AddDouble with its 7 carries, HI access)
+    r = np.nonzero(np.isin(op, MADDSUB_OPS))[0]
+    if len(r):
+        o = op[r]
+        t[r, MS_SHARD], t[r, MS_CLK] = shard, E[r, 7]
+        signed = (o == OP_MADD) | (o == OP_MSUB)
+        sb = np.where(b[r] >> 31, b[r] - (1 << 32), b[r])
+        sc = np.where(c[r] >> 31, c[r] - (1 << 32), c[r])
+        prod = np.where(signed, (sb * sc).astype(np.uint64), u64(b[r]) * u64(c[r]))
+        is_add = (o == OP_MADDU) | (o == OP_MADD)
+        s2lo = np.where(is_add, pa[r], a[r])
+        s2hi = np.where(is_add, E[r, 8], E[r, 9])
+        addend = (u64(s2hi) << np.uint64(32)) | u64(s2lo)
+        tot = prod + addend  # wraps mod 2^64
+        pb = prod[:, None] >> (np.uint64(8) * np.arange(8, dtype=np.uint64))[None, :] & np.uint64(0xFF)
+        qb = addend[:, None] >> (np.uint64(8) * np.arange(8, dtype=np.uint64))[None, :] & np.uint64(0xFF)
+        cy = np.zeros(len(r), np.uint64)
+        for j in range(7):
+            cy = ((pb[:, j] + qb[:, j] + cy) > 255).astype(np.uint64)
+            t[r, S + _MD_CARRY + j] = cy
+        lo32 = lambda v: v & np.uint64(M32)
+        hi32 = lambda v: v >> np.uint64(32)
+        for off, v in ((_MD_LO, lo32(prod)), (_MD_HI, hi32(prod)), (_MD_VAL, lo32(tot)), (_MD_VALHI, hi32(tot)),
+                       (_MD_S2HI, u64(s2hi)), (_MD_S2LO, u64(s2lo)), (_MD_HIACC, u64(E[r, 8]))):
+            t[r, S + off:S + off + 4] = wb(v)
+        for v in (lo32(prod), hi32(prod), u64(s2lo), u64(s2hi), lo32(tot), hi32(tot)):
+            w = wb(v)
+            byte_lookup(A.B_U8RANGE, w[:, 0], w[:, 1])
+            byte_lookup(A.B_U8RANGE, w[:, 2], w[:, 3])
     md = np.isin(E[:, 0], MADDSUB_OPS)
     if md.any():
         rows = np.nonzero(md)[0]
-        _access_cols(t, rows, S + _MD_HIACC + 4, u(E[rows, 9]), E[rows][:, 10:12], shard, E[rows, 7] + POS_HI,
+        _access_cols(t, rows, S + _MD_HIACC + 4, E[rows, 9].astype(np.uint32), E[rows][:, 10:12], shard, E[rows, 7] + POS_HI,
                      np.ones(len(rows), bool), byte_lookup)
     return t
 
@@ -1204,10 +1221,15 @@ def _taken(op, a, b):
     return {OP_BGEZ: sa >= 0, OP_BLEZ: sa <= 0, OP_BGTZ: sa > 0, OP_BLTZ: sa < 0}[op]
 
 
+_REGS_AVOID = {}
+
+
 def _random_alu(r, avoid=()):
     """One random ALU instruction from 5 random words (destination never in `avoid`)."""
     op, imm = _MIX[int(r[0] % len(_MIX))]
-    regs = [x for x in range(32) if x not in avoid]
+    regs = _REGS_AVOID.get(avoid)
+    if regs is None:
+        regs = _REGS_AVOID[avoid] = [x for x in range(32) if x not in avoid]
     ra = 0 if (r[4] % 16 == 0 and 0 not in avoid) else regs[1 + int(r[1] % (len(regs) - 1))]
     rb = int(r[2] % 32)
     if isinstance(op, str):  # MFLO/MFHI rd = lo/hi; MTLO/MTHI lo/hi = rs: ADDs with register 32/33 (instruction.rs:387-394)
@@ -1441,6 +1463,12 @@ def _execute(prog, regs, shard, max_steps):
             elif op == OP_INS:
                 lsb, msb = cv & 31, cv >> 5
                 width = msb - lsb + 1
+                # A full-width INS (width 32) has no satisfying MiscInstrs row: eval_ins proves
+                # a = ror(srl + sll, 31 - msb) with srl looked up as SRL(ror, 32), which the ShiftRight chip
+                # evaluates with the shift masked to 0 (srl = ror, so a = prev_a + b), while the reference's
+                # dependency event says srl = 0 (dependencies.rs:328-329).  The reference cannot prove it
+                # either; such programs are rejected here rather than producing an unprovable shard.
+                assert width < 32, "full-width INS is not provable by the MiscInstrs AIR"
                 field = (((1 << width) - 1) << lsb) & M32
                 av = (prev_a & ~field & M32) | ((bv << lsb) & field)
                 hi = ev_prev = prev_a
