@@ -223,7 +223,7 @@ def pmc_child(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--log-n", type=int, default=22)
     ap.add_argument("--workload", choices=["fib", "alu", "core"], default="fib",

@@ -96,9 +96,12 @@ static inline ef_t ef_inv(ef_t a) {
 }
 static inline ef_t ef_div(ef_t a, ef_t b) { return ef_mul(a, ef_inv(b)); }
 
+/* reverse the low `bits` bits of x (x < 2^bits) */
 static inline uint32_t rev_bits(uint32_t x, int bits) {
-    uint32_t r = 0;
-    for (int i = 0; i < bits; i++) { r = (r << 1) | (x & 1); x >>= 1; }
-    return r;
+    x = ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+    x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+    x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+    x = __builtin_bswap32(x);
+    return bits ? x >> (32 - bits) : 0;
 }
 static inline int log2_exact(uint64_t n) { int l = 0; while ((1ull << l) < n) l++; return l; }

@@ -12,47 +12,52 @@ static const kb_t DIAG[16] = {
     (KB_P - 1) >> 8, (KB_P - 1) >> 3, (KB_P - 1) >> 4, 127,
 };
 
-static void m4(kb_t *x) {
-    /* apply_m_4 (air.rs:31-42): matrix [[2,3,1,1],[1,2,3,1],[1,1,2,3],[3,1,1,2]] */
-    kb_t t01 = kb_add(x[0], x[1]);
-    kb_t t23 = kb_add(x[2], x[3]);
-    kb_t t0123 = kb_add(t01, t23);
-    kb_t t01123 = kb_add(t0123, x[1]);
-    kb_t t01233 = kb_add(t0123, x[3]);
-    kb_t n3 = kb_add(t01233, kb_add(x[0], x[0]));
-    kb_t n1 = kb_add(t01123, kb_add(x[2], x[2]));
-    kb_t n0 = kb_add(t01123, t01);
-    kb_t n2 = kb_add(t01233, t23);
-    x[0] = n0; x[1] = n1; x[2] = n2; x[3] = n3;
-}
+/* Linear layers accumulate in 64 bits and reduce once per output element (every intermediate is a
+ * small multiple of p, far below 2^64); S-box inputs x + rc stay below 2^32. */
+static inline kb_t red(uint64_t x) { return (kb_t)(x % KB_P); }
 
 static void external_layer(kb_t *s) {
-    for (int j = 0; j < 16; j += 4) m4(s + j);
-    kb_t sums[4];
-    for (int k = 0; k < 4; k++) sums[k] = kb_add(kb_add(s[k], s[4 + k]), kb_add(s[8 + k], s[12 + k]));
-    for (int j = 0; j < 16; j++) s[j] = kb_add(s[j], sums[j & 3]);
+    /* apply_m_4 (air.rs:31-42): matrix [[2,3,1,1],[1,2,3,1],[1,1,2,3],[3,1,1,2]] per 4-block,
+     * then add the column sums over the four blocks (air.rs:44-56) */
+    uint64_t t[16];
+    for (int j = 0; j < 16; j += 4) {
+        uint64_t x0 = s[j], x1 = s[j + 1], x2 = s[j + 2], x3 = s[j + 3];
+        uint64_t t01 = x0 + x1, t23 = x2 + x3, t0123 = t01 + t23;
+        uint64_t t01123 = t0123 + x1, t01233 = t0123 + x3;
+        t[j] = t01123 + t01;
+        t[j + 1] = t01123 + 2 * x2;
+        t[j + 2] = t01233 + t23;
+        t[j + 3] = t01233 + 2 * x0;
+    }
+    uint64_t sums[4];
+    for (int k = 0; k < 4; k++) sums[k] = t[k] + t[4 + k] + t[8 + k] + t[12 + k];
+    for (int j = 0; j < 16; j++) s[j] = red(t[j] + sums[j & 3]);
 }
 
 static void internal_layer(kb_t *s) {
-    kb_t sum = 0;
-    for (int i = 0; i < 16; i++) sum = kb_add(sum, s[i]);
-    for (int i = 0; i < 16; i++) s[i] = kb_add(kb_mul(s[i], DIAG[i]), sum);
+    uint64_t sum = 0;
+    for (int i = 0; i < 16; i++) sum += s[i];
+    for (int i = 0; i < 16; i++) s[i] = red((uint64_t)s[i] * DIAG[i] + sum);
 }
 
-static inline kb_t cube(kb_t x) { return kb_mul(kb_mul(x, x), x); }
+/* (x + rc)^3 with x, rc < p */
+static inline kb_t sbox(kb_t x, kb_t rc) {
+    uint64_t y = (uint64_t)x + rc;
+    return red((uint64_t)red(y * y) * y);
+}
 
 void orc_p2_permute(kb_t st[16]) {
     external_layer(st);
     for (int r = 0; r < RF / 2; r++) {
-        for (int i = 0; i < 16; i++) st[i] = cube(kb_add(st[i], ORC_P2_RC[r][i]));
+        for (int i = 0; i < 16; i++) st[i] = sbox(st[i], ORC_P2_RC[r][i]);
         external_layer(st);
     }
     for (int r = 0; r < RP; r++) {
-        st[0] = cube(kb_add(st[0], ORC_P2_RC[RF / 2 + r][0]));
+        st[0] = sbox(st[0], ORC_P2_RC[RF / 2 + r][0]);
         internal_layer(st);
     }
     for (int r = RF / 2; r < RF; r++) {
-        for (int i = 0; i < 16; i++) st[i] = cube(kb_add(st[i], ORC_P2_RC[r + RP][i]));
+        for (int i = 0; i < 16; i++) st[i] = sbox(st[i], ORC_P2_RC[r + RP][i]);
         external_layer(st);
     }
 }

@@ -91,8 +91,9 @@ def test_coset_lde_linearity_large(dev):
     assert np.all(dev.coset_lde(c) == 12345)
 
 
-@pytest.mark.parametrize("logn,w", [(4, 67), (10, 67), (14, 9)])
+@pytest.mark.parametrize("logn,w", [(4, 67), (10, 67), (14, 9), (20, 67)])
 def test_pcs_commit_root_vs_oracle(dev, logn, w):
+    """(20, 67) is BASELINE configuration 2 (S-COMMIT: a 2^20 x 67 trace, LDE + Poseidon2 MMCS root)."""
     m = W.random_matrix(1 << logn, w, seed=logn + w)
     assert np.array_equal(dev.pcs_commit_root([m]), O.commit_root([m]))
 

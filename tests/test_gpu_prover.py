@@ -134,6 +134,18 @@ def test_shard_proof_bytes_identical_2e18(dev):
     assert rc == 0 and proof == ref
 
 
+def test_shard_proof_bytes_identical_2e22(dev):
+    """Byte parity at the headline configuration itself: a 2^22-row FibCpu shard, 84 queries, the
+    proof the bench times (the oracle needs ~1 min of its OpenMP threads for it)."""
+    gpu, cpu, traces, pvs = provers(dev, 1 << 22, nq=84, seed=1000)
+    ch = gpu.base_challenger()
+    proof = gpu.open(gpu.commit(traces, pvs), ch)
+    och = cpu.base_challenger()
+    rc, ref = cpu.prove(traces, pvs, och)
+    assert rc == 0 and proof == ref
+    assert same_challenger(ch.to_words(), och.s)
+
+
 @pytest.mark.parametrize("logn", [20, 22, 23])
 def test_full_size_proof_verifies(dev, logn):
     """BASELINE sizes (2^20 .. 2^23 rows; 2^23 is the largest the two-adicity allows at blowup 2):
