@@ -475,7 +475,7 @@ def main():
                     f"of a subroutine, bal) "
                     f"executed to {int(traces['Cpu'][:, 65].sum())} instructions: Cpu 2^{args.log_n} (main 67, "
                     f"LogUp 11 EF) + Program (prep 14) + DivRem, AddSub, Bitwise, Mul, Lt, ShiftLeft, ShiftRight, CloClz, MovCond, MemoryInstrs, MiscInstrs, "
-                    f"Branch, Jump + Byte 2^16 (prep 12) + RegisterState: full commit+open per shard")
+                    f"Branch, Jump, MemoryLocal, Global (septic-curve digest) + Byte 2^16 (prep 12): full commit+open per shard")
                    if args.workload == "core" else
                    (f"MIPS ALU slice: InstrSource 2^{args.log_n} + AddSub, Bitwise, Lt 2^{args.log_n - 2} + ShiftLeft, "
                     f"ShiftRight (CPU + CloClz SRLs) 2^{args.log_n - 3} + CloClz 2^{args.log_n - 4} + Byte 2^16 "

@@ -19,6 +19,7 @@ import pytest
 from tests import _oracle as O
 from zkmips_amd import mips_alu as A
 from zkmips_amd import mips_core as MC
+from zkmips_amd import mips_memory as MM
 from zkmips_amd.machine import MachineDesc
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -43,6 +44,8 @@ CHIPS = {
     "MemoryInstrs": (MC.memory_instructions_chip, 0, 79, 7, 1, True, "memory/instructions/trace.rs:25",
                      "memory/instructions/trace.rs:82"),
     "MiscInstrs": (MC.misc_instructions_chip, 0, 72, 17, 1, False, "misc/others/trace.rs:24", None),
+    "MemoryLocal": (MM.memory_local_chip, 0, 56, 9, 1, False, "memory/local.rs:86", None),
+    "Global": (MM.global_chip, 0, 99, 2, 1, False, "global/mod.rs:65", None),
 }
 
 
@@ -77,7 +80,7 @@ def test_local_only_reaches_the_blob():
 
 def test_every_restated_chip_is_a_reference_chip():
     """Chips the shard builders put in a machine are reference chips (plus the documented stand-ins)."""
-    stand_ins = {"RegisterState", "InstrSource"}
+    stand_ins = {"InstrSource"}
     names = {c.name for c in MC.core_machine().chips}
     assert names - stand_ins <= set(COSTS)
     assert names - stand_ins <= set(CHIPS)

@@ -1,6 +1,6 @@
 """MIPS core shard: the reference's Cpu, Program, Branch, Jump, Mul, DivRem, MovCond, MemoryInstrs and
 MiscInstrs chips (zkmips_amd/mips_core.py) on top of the ALU slice, with the memory argument closed by the
-MemoryLocal-shaped RegisterState stand-in.  The reference's own instruction-test programs are fixtures.
+MemoryLocal and Global chips (zkmips_amd/mips_memory.py).  The reference's own instruction-test programs are fixtures.
 
 CPU part: the trace satisfies every constraint and every lookup balances (direct evaluation,
 tests/_air_check.py); the oracle proves it and its verifier accepts; forged ALU results, register
@@ -15,6 +15,7 @@ from tests import _air_check
 from tests import _oracle as O
 from zkmips_amd import mips_alu as A
 from zkmips_amd import mips_core as C
+from zkmips_amd import mips_memory as MM
 
 
 @pytest.fixture(scope="module")
@@ -63,8 +64,8 @@ def _tamper(tr, what):
         t[40, C.C_NPC] += 4
     elif what == "program":  # the executed instruction is not the committed program's
         t[50, C.C_OPC] = (int(t[50, C.C_OPC]) + 1) % 256
-    elif what == "register_final":
-        bad["RegisterState"][5, C.RS_FIN_VAL] ^= 1
+    elif what == "register_final":  # the value MemoryLocal says a register holds at the shard's end
+        bad["MemoryLocal"][0, MM.ML_ENTRY_WIDTH + MM.ML_FVAL] ^= 1
     elif what == "clk":
         t[60, C.C_CLK16] += 1
     return bad
@@ -196,15 +197,18 @@ def test_branch_tamper_rejected(loop, what):
 
 
 def test_core_register_chain(shard):
-    """Every register's first access reads the initial value the RegisterState row receives and its
-    last access is what that row sends (the memory argument closes inside the shard)."""
+    """MemoryLocal holds every register the shard accessed, then every data word it touched, each once
+    with its value at the shard's start and end; the Global chip receives two messages per entry."""
     _, _, tr, _ = shard
-    rs = tr["RegisterState"]
-    assert list(rs[:C.NUM_REGS, C.RS_ADDR]) == list(range(C.NUM_REGS))  # 32 GPRs + LO, HI
-    words = rs[C.NUM_REGS:][rs[C.NUM_REGS:, C.RS_REAL] == 1, C.RS_ADDR]  # then the data words touched
-    assert len(words) and (words >= C.DATA_BASE).all() and (np.diff(words.astype(np.int64)) > 0).all()
-    assert rs[:C.NUM_REGS, C.RS_REAL].all() and not rs[C.NUM_REGS + len(words):].any()
-    assert (rs[:, C.RS_FIN_CLK] <= 5 * 699 + C.POS_HI).all() and rs[0, C.RS_INIT_VAL:C.RS_INIT_VAL + 4].sum() == 0
+    e = MM.local_entries(tr["MemoryLocal"])
+    regs = e[e[:, 0] < C.NUM_REGS, 0]
+    words = e[e[:, 0] >= C.NUM_REGS, 0]
+    assert len(regs) and (np.diff(regs) > 0).all() and len(words) and (words >= C.DATA_BASE).all()
+    assert (np.diff(words) > 0).all() and len(regs) + len(words) == len(e)
+    assert (e[:, 5] <= 5 * 699 + C.POS_HI).all() and (e[:, 4] == 1).all() and (e[:, 1:3] == 0).all()
+    assert int(tr["Global"][:, MM.G_REAL].sum()) == 2 * len(e)
+    if 0 in regs:
+        assert e[e[:, 0] == 0, 3][0] == 0 and e[e[:, 0] == 0, 6][0] == 0  # r0 stays 0
 
 
 def _word(row, base):
@@ -229,9 +233,8 @@ def test_mul_kinds():
         p = (sb * sc) & ((1 << 64) - 1)
         assert (_word(r_mult, C.MU_A), _word(r_mult, C.MU_HI)) == (p & C.M32, p >> 32) and r_mult[C.MU_HRR] == 1
         assert (_word(r_multu, C.MU_A), _word(r_multu, C.MU_HI)) == ((b * c) & C.M32, (b * c) >> 32)
-    rs = tr["RegisterState"]
     b, c = vals[-1]
-    assert _word(rs[C.REG_LO], C.RS_FIN_VAL) == (b * c) & C.M32 and _word(rs[C.REG_HI], C.RS_FIN_VAL) == (b * c) >> 32
+    assert _final(tr, C.REG_LO) == (b * c) & C.M32 and _final(tr, C.REG_HI) == (b * c) >> 32
     assert _air_check.check(m, prep, tr, pv) == ([], [])
     o = O.OracleProver(m, prep, num_queries=8)
     rc, proof = o.prove(tr, pv)
@@ -284,10 +287,9 @@ def test_movcond_reference_fixture():
     assert int(mc[:, C.MC_MEQ].sum()) == 4 and int(mc[:, C.MC_MNE].sum()) == 2 and int(mc[:, C.MC_WSBH].sum()) == 3
     assert _word(mc[0], C.MC_A) == 0xF and _word(mc[4], C.MC_A) == 0xF  # MOVZ with rt = r0, MOVN with rt = r28
     assert _word(mc[6], C.MC_A) == 0x0F00  # WSBH swaps the bytes of each halfword
-    rs = tr["RegisterState"]
-    r31 = _word(rs[31], C.RS_INIT_VAL)
+    r31 = _initial(tr, 31)
     want = ((r31 >> 16 & 0xFF) << 24) | ((r31 >> 24 & 0xFF) << 16) | ((r31 & 0xFF) << 8) | (r31 >> 8 & 0xFF)
-    assert _word(rs[C.REG_LO], C.RS_FIN_VAL) == want
+    assert _final(tr, C.REG_LO) == want
     assert _air_check.check(m, prep, tr, pv) == ([], [])
     o = O.OracleProver(m, prep, num_queries=8)
     rc, proof = o.prove(tr, pv)
@@ -402,9 +404,8 @@ def test_misc_reference_fixture():
     assert [int(ms[:, C.MS_SEL + k].sum()) for k in range(8)] == [6, 3, 3, 3, 3, 3, 3, 3]
     assert _final(tr, 31) == 0xFFFF8F8F  # SEH of 0x8F8F
     # MADDU, MSUBU, MADD and MSUB of the same operands cancel pairwise: HI:LO returns to its start
-    rs = tr["RegisterState"]
-    assert _word(rs[C.REG_LO], C.RS_FIN_VAL) == _word(rs[C.REG_LO], C.RS_INIT_VAL)
-    assert _word(rs[C.REG_HI], C.RS_FIN_VAL) == _word(rs[C.REG_HI], C.RS_INIT_VAL)
+    assert _final(tr, C.REG_LO) == _initial(tr, C.REG_LO)
+    assert _final(tr, C.REG_HI) == _initial(tr, C.REG_HI)
     assert _air_check.check(m, prep, tr, pv) == ([], [])
     o = O.OracleProver(m, prep, num_queries=8)
     rc, proof = o.prove(tr, pv)
@@ -435,9 +436,13 @@ def test_misc_tamper_rejected(what):
 
 
 def _final(tr, addr):
-    rs = tr["RegisterState"]
-    i = int(np.nonzero((rs[:, C.RS_ADDR] == addr) & (rs[:, C.RS_REAL] == 1))[0][0])
-    return _word(rs[i], C.RS_FIN_VAL)
+    e = MM.local_entries(tr["MemoryLocal"])
+    return int(e[e[:, 0] == addr, 6][0])
+
+
+def _initial(tr, addr):
+    e = MM.local_entries(tr["MemoryLocal"])
+    return int(e[e[:, 0] == addr, 3][0])
 
 
 @pytest.mark.parametrize("name", ["simple_memory", "other_memory", "sc"])
@@ -474,8 +479,9 @@ def test_memory_tamper_rejected(shard, oracle, what):
         j = (int(mi[i, C.MI_LS2]) + 1) % 4
         mi[i, C.MI_ACC + 4 + j] = (int(mi[i, C.MI_ACC + 4 + j]) + 1) % 256
     elif what == "memory_final":  # the memory argument's closing value of a data word
-        rs = bad["RegisterState"]
-        rs[C.NUM_REGS + 1, C.RS_FIN_VAL] ^= 1
+        ml = bad["MemoryLocal"].reshape(-1, MM.ML_ENTRY_WIDTH)
+        k = int(np.nonzero(ml[:, MM.ML_ADDR] >= C.DATA_BASE)[0][0])
+        ml[k, MM.ML_FVAL] ^= 1
     else:  # the access goes to another word than b + c
         mi[3, C.MI_ALIGNED] += 4
     assert _air_check.check(m, prep, bad, pv) != ([], [])

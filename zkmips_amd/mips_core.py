@@ -9,17 +9,17 @@ ALU slice.
   timestamp range checks), shard/clk/pc/is_real constraints against the public values.
 * the ALU chips and the Byte table of `mips_alu` receive the CPU's instructions and byte lookups.
 
-Stand-in: in a real shard the register accesses' memory lookups are closed by MemoryLocal (and its
-global interactions with the Global chip's septic-curve digest).  ``RegisterState`` stands in for
-that: one row per register receiving its value at the shard's start and sending its value at the
-end, so the memory argument balances inside the shard.  The program is straight-line MIPS ALU code
-(no branches: the Branch/Jump chips are not restated), executed once per shard.
+The memory argument of a shard closes through MemoryLocal (every register and data word the shard
+touched: its value at the shard's start received, its value at the end sent) and the Global chip,
+which lifts MemoryLocal's global messages onto the septic curve and accumulates them into the shard's
+global cumulative sum (zkmips_amd/mips_memory.py).
 """
 from __future__ import annotations
 
 import numpy as np
 
 from . import mips_alu as A
+from . import mips_memory as MM
 from .machine import (ChipDesc, Expr, IS_FIRST, IS_LAST, IS_TRANSITION, KIND_BYTE, KIND_INSTRUCTION, KIND_MEMORY,
                       KIND_PROGRAM, Lookup, MachineDesc, P, VirtualPairCol as V, main, main_next, pv)
 from .workloads import NUM_PV_ELTS, PROOF_MAX_NUM_PVS, splitmix64
@@ -156,22 +156,6 @@ PROG_PREP_WIDTH, PROG_MAIN_WIDTH = 14, 1
 def program_chip() -> ChipDesc:
     ch = ChipDesc("Program", prep_width=PROG_PREP_WIDTH, main_width=PROG_MAIN_WIDTH)
     ch.receives.append(Lookup([V.single_prep(i) for i in range(PROG_PREP_WIDTH)], _m(0), KIND_PROGRAM))
-    return ch
-
-
-# ---------------------------------------------------------------- register-state stand-in
-RS_ADDR, RS_INIT_SHARD, RS_INIT_CLK, RS_INIT_VAL, RS_FIN_SHARD, RS_FIN_CLK, RS_FIN_VAL, RS_REAL = 0, 1, 2, 3, 7, 8, 9, 13
-RS_WIDTH = 14
-
-
-def register_state_chip() -> ChipDesc:
-    """Closes the register chain of the memory argument inside the shard (stand-in for MemoryLocal)."""
-    ch = ChipDesc("RegisterState", prep_width=0, main_width=RS_WIDTH, local_only=True)
-    ch.receives.append(Lookup([_m(RS_INIT_SHARD), _m(RS_INIT_CLK), _m(RS_ADDR)] + _vword(RS_INIT_VAL),
-                              _m(RS_REAL), KIND_MEMORY))
-    ch.sends.append(Lookup([_m(RS_FIN_SHARD), _m(RS_FIN_CLK), _m(RS_ADDR)] + _vword(RS_FIN_VAL), _m(RS_REAL),
-                           KIND_MEMORY))
-    _assert_bool(ch, main(RS_REAL))
     return ch
 
 
@@ -1151,8 +1135,7 @@ def core_machine() -> MachineDesc:
                         A.shift_right_chip(),
                         A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(), memory_instructions_chip(),
                         movcond_chip(), misc_instructions_chip(),
-                        A.byte_chip(),
-                        register_state_chip()], NUM_PV_ELTS)
+                        MM.memory_local_chip(), MM.global_chip(), A.byte_chip()], NUM_PV_ELTS)
 
 
 # ---------------------------------------------------------------- program + execution
@@ -1671,19 +1654,14 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     pm[:len(prog), 0] = np.bincount(ks, minlength=len(prog))
     traces["Program"] = pm
 
-    # registers, then every data word the shard touched (MemoryLocal's entries: addr, initial and final
-    # (shard, clk, value), memory/local.rs:204-270)
-    addrs = sorted(mem)
-    R = NUM_REGS + len(addrs)
-    rs = np.zeros((A._pow2(R), RS_WIDTH), np.uint32)
-    rs[:R, RS_ADDR] = list(range(NUM_REGS)) + addrs
-    rs[:R, RS_INIT_VAL:RS_INIT_VAL + 4] = A._bytes(np.asarray(init_vals + [mem_init[x] for x in addrs], np.uint32))
-    fin = last + [mem_last[x] for x in addrs]
-    rs[:R, RS_FIN_SHARD] = [s_ for s_, _ in fin]
-    rs[:R, RS_FIN_CLK] = [c_ for _, c_ in fin]
-    rs[:R, RS_FIN_VAL:RS_FIN_VAL + 4] = A._bytes(np.asarray(regs + [mem[x] for x in addrs], np.uint32))
-    rs[:R, RS_REAL] = 1
-    traces["RegisterState"] = rs
+    # MemoryLocal: every register the shard accessed, then every data word it touched, by address (the
+    # reference collects them from a hash map; the order is free); initial (shard, clk) = (0, 0)
+    ent = [(r, 0, 0, init_vals[r], last[r][0], last[r][1], regs[r]) for r in range(NUM_REGS) if last[r] != (0, 0)]
+    ent += [(x, 0, 0, mem_init[x], mem_last[x][0], mem_last[x][1], mem[x]) for x in sorted(mem)]
+    ent = np.asarray(ent, np.int64).reshape(-1, 7)
+    traces["MemoryLocal"] = MM.memory_local_trace(ent)
+    gmsg, grec = MM.memory_local_global_events(ent)
+    traces["Global"], _ = MM.global_trace(gmsg, grec, np.full(len(gmsg), KIND_MEMORY, np.uint32), byte_lookup)
 
     assert mult.max() < P
     traces["Byte"] = mult.astype(np.uint32)
