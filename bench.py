@@ -320,7 +320,9 @@ def main():
         for j in range(nsteps):
             ev.synchronize()
             nxt = issue(j + 1) if j + 1 < nsteps else None
-            pr = prove_resident(prover, bufs[j % 2], pv)
+            # ZKM_BENCH_DMA_PROBE=1 (experiment only): the same copies, proofs from the resident traces
+            src = dev_t if os.environ.get("ZKM_BENCH_DMA_PROBE") == "1" else bufs[j % 2]
+            pr = prove_resident(prover, src, pv)
             ev = nxt
         return pr
 
@@ -346,8 +348,8 @@ def main():
         """MachineProof aggregation: all ranks' shard proofs over RCCL (zkmips_amd/dist.py)."""
         if world == 1:
             return {0: proof}
-        from zkmips_amd.dist import gather_proofs
-        return gather_proofs({rank: proof}, device=coll_dev)
+        from zkmips_amd.dist import gather_proofs_to_root
+        return gather_proofs_to_root({rank: proof}, device=coll_dev)
 
     if args.warmup:
         run_steps(args.warmup, "pipelined")

@@ -4,9 +4,10 @@ The reference proves all shards of a batch in parallel and independently: each s
 clone of a challenger that has only observed the proving key (crates/core/machine/src/utils/
 prove.rs:208-209, :487-521; verifier mirrors it, crates/stark/src/machine.rs:620-624).  So the data
 path needs no collective: shards are dealt round-robin to ranks and proved locally.  The only
-exchange is the aggregation of finished proofs (KB-MB each) to build the MachineProof in shard
-order — done with one all_gather over the process group (RCCL over xGMI with backend "nccl",
-gloo on CPU for tests).
+exchange is the aggregation of finished proofs (KB-MB each) to rank 0, which assembles the
+MachineProof in shard order and runs the machine-level check the reference's verifier ends with: the
+shards' global cumulative sums add up to the zero digest (crates/stark/src/machine.rs:639-654) — one
+gather over the process group (RCCL over xGMI with backend "nccl", gloo on CPU for tests).
 """
 from __future__ import annotations
 
@@ -60,10 +61,45 @@ def gather_proofs(local: Dict[int, bytes], device="cpu") -> Dict[int, bytes]:
     return out
 
 
-def prove_shards_distributed(prove_one: Callable[[int], bytes], num_shards: int, device="cpu") -> List[bytes]:
-    """MachineProver::prove across ranks: each rank proves its shards, proofs come back in shard order."""
+def gather_proofs_to_root(local: Dict[int, bytes], device="cpu", root: int = 0) -> Dict[int, bytes]:
+    """Gather every rank's {shard index: proof bytes} to `root` only (one padded gather; the padding is
+    the largest rank payload, agreed by an 8-byte all_reduce).  Returns the union on root, {} elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    payload = _encode(local)
+    ln = torch.tensor([len(payload)], dtype=torch.int64, device=device)
+    dist.all_reduce(ln, op=dist.ReduceOp.MAX)
+    size = int(ln.item())
+    buf = torch.zeros(size + 8, dtype=torch.uint8, device=device)
+    buf[:8] = torch.tensor(list(len(payload).to_bytes(8, "little")), dtype=torch.uint8, device=device)
+    if payload:
+        buf[8:8 + len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == root else None
+    dist.gather(buf, parts, dst=root)
+    out: Dict[int, bytes] = {}
+    if rank == root:
+        for p in parts:
+            raw = p.cpu().numpy().tobytes()
+            n = int.from_bytes(raw[:8], "little")
+            out.update(_decode(raw[8:8 + n]))
+    return out
+
+
+def prove_shards_distributed(prove_one: Callable[[int], bytes], num_shards: int, device="cpu",
+                             check_global_sum: bool = False) -> List[bytes]:
+    """MachineProver::prove across ranks: each rank proves its shards; rank 0 receives every proof in
+    shard order (other ranks get []), and with check_global_sum verifies that the shards' global
+    cumulative sums add up to the zero digest (machine.rs:639-654)."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
     local = {i: prove_one(i) for i in assign_shards(num_shards, world, rank)}
-    allp = gather_proofs(local, device)
-    return [allp[i] for i in range(num_shards)]
+    allp = gather_proofs_to_root(local, device)
+    if rank != 0:
+        return []
+    proofs = [allp[i] for i in range(num_shards)]
+    if check_global_sum:
+        from .proof import machine_global_sum_is_zero
+        if not machine_global_sum_is_zero(proofs):
+            raise ValueError("the shards' global cumulative sums do not add up to zero")
+    return proofs

@@ -1135,7 +1135,8 @@ def core_machine() -> MachineDesc:
                         A.shift_right_chip(),
                         A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(), memory_instructions_chip(),
                         movcond_chip(), misc_instructions_chip(),
-                        MM.memory_local_chip(), MM.global_chip(), A.byte_chip()], NUM_PV_ELTS)
+                        MM.memory_global_chip(True), MM.memory_global_chip(False), MM.memory_local_chip(),
+                        MM.global_chip(), A.byte_chip()], NUM_PV_ELTS)
 
 
 # ---------------------------------------------------------------- program + execution
@@ -1331,21 +1332,36 @@ def loop_program(body: int, iters: int, seed: int = 1):
     return prog
 
 
-def _execute(prog, regs, shard, max_steps):
-    """Runs `prog` from PC_BASE until pc leaves it (delay slots: pc <- next_pc, next_pc <- next_next_pc).
-    Returns the per-step records, the ALU/Branch events in execution order (the instruction's own
-    event, then the dependencies emit_branch_dependencies adds, executor/src/dependencies.rs:175-224),
-    and each register's last (shard, timestamp)."""
+def fresh_state():
+    """Machine state before the first instruction: each register's / data word's last access
+    (shard, timestamp), the data words' values, and (pc, next_pc)."""
+    return {"last": [(0, 0)] * NUM_REGS, "pc": PC_BASE, "npc": PC_BASE + 4, "mem": {}, "mem_init": {},
+            "mem_last": {}}
+
+
+def _execute(prog, regs, shard, max_steps, state=None):
+    """Runs `prog` from the state's pc until pc leaves it (delay slots: pc <- next_pc, next_pc <-
+    next_next_pc).  Returns the per-step records, the ALU/Branch events in execution order (the
+    instruction's own event, then the dependencies emit_branch_dependencies adds,
+    executor/src/dependencies.rs:175-224), and each register's last (shard, timestamp).
+    With a `state` (continuation), the shard ends after max_steps instructions at the first point
+    where the next instruction is not a delay slot (a shard's first row has next_pc = pc + 4,
+    cpu/air/mod.rs eval_pc), and `state`/`regs` carry over to the next shard."""
+    split = state is not None
+    if state is None:
+        state = fresh_state()
     end = PC_BASE + 4 * len(prog)
-    last = [(0, 0)] * NUM_REGS
-    pc, npc = PC_BASE, PC_BASE + 4
+    last = state["last"]
+    pc, npc = state["pc"], state["npc"]
     steps = []
     ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
     branches, jumps, muls, divs, movs, mevs, misc = [], [], [], [], [], [], []
-    mem, mem_init, mem_last = {}, {}, {}
+    mem, mem_init, mem_last = state["mem"], state["mem_init"], state["mem_last"]
     U = A.UNUSED_PC
     while PC_BASE <= pc < end:  # the program halts when pc leaves it
-        assert len(steps) < max_steps
+        if split and len(steps) >= max_steps and npc == pc + 4:
+            break
+        assert len(steps) < max_steps or (split and len(steps) < max_steps + 2)
         k = (pc - PC_BASE) >> 2
         op, ra, rb, c, immb, immc = prog[k]
         clk = 5 * len(steps)
@@ -1537,6 +1553,7 @@ def _execute(prog, regs, shard, max_steps):
         steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc,
                       hi if op in MUL_OPS + DIV_OPS + MOVCOND_OPS + MEM_OPS + MISC_OPS else 0))
         pc, npc = npc, nnpc
+    state["pc"], state["npc"] = pc, npc
     return steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc
 
 
@@ -1550,14 +1567,23 @@ def _ev_arrays(lst):
     return tuple(arr[:, i].astype(np.uint32) for i in range(6))
 
 
-def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24) // 5 - 1):
-    """(machine, prep_traces, traces, public_values) of one shard executing `prog` from PC_BASE to its end
-    (at most max_steps instructions: the CPU clk is range-checked to 24 bits)."""
+def initial_registers(seed: int):
     init = splitmix64(0x5EED000 + seed, NUM_REGS) & np.uint64(M32)
-    regs = [0] + [int(x) for x in init[1:]]
-    init_vals = list(regs)
+    return [0] + [int(x) for x in init[1:]]
+
+
+def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24) // 5 - 1, state=None, regs=None):
+    """(machine, prep_traces, traces, public_values) of one shard executing `prog` from PC_BASE to its end
+    (at most max_steps instructions: the CPU clk is range-checked to 24 bits).  With `state` and `regs`
+    (program_shards), the shard continues a longer execution and stops after about max_steps."""
+    if state is None:
+        regs = initial_registers(seed)
+    start_regs, start_last = list(regs), list(state["last"]) if state else [(0, 0)] * NUM_REGS
+    start_mem = dict(state["mem"]) if state else {}
+    start_mem_last = dict(state["mem_last"]) if state else {}
+    start_pc = state["pc"] if state else PC_BASE
     steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc = \
-        _execute(prog, regs, shard, max_steps)
+        _execute(prog, regs, shard, max_steps, state)
     n = len(steps)
     assert n > 0
     height = max(16, 1 << (n - 1).bit_length())
@@ -1655,9 +1681,11 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     traces["Program"] = pm
 
     # MemoryLocal: every register the shard accessed, then every data word it touched, by address (the
-    # reference collects them from a hash map; the order is free); initial (shard, clk) = (0, 0)
-    ent = [(r, 0, 0, init_vals[r], last[r][0], last[r][1], regs[r]) for r in range(NUM_REGS) if last[r] != (0, 0)]
-    ent += [(x, 0, 0, mem_init[x], mem_last[x][0], mem_last[x][1], mem[x]) for x in sorted(mem)]
+    # reference collects them from a hash map; the order is free), with the access record before the
+    # shard (shard, clk, value) and after it
+    ent = [(r, *start_last[r], start_regs[r], *last[r], regs[r]) for r in range(NUM_REGS) if last[r] != start_last[r]]
+    ent += [(x, *start_mem_last.get(x, (0, 0)), start_mem.get(x, mem_init[x]), *mem_last[x], mem[x])
+            for x in sorted(mem) if mem_last[x] != start_mem_last.get(x)]
     ent = np.asarray(ent, np.int64).reshape(-1, 7)
     traces["MemoryLocal"] = MM.memory_local_trace(ent)
     gmsg, grec = MM.memory_local_global_events(ent)
@@ -1666,7 +1694,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     assert mult.max() < P
     traces["Byte"] = mult.astype(np.uint32)
     pvs = (splitmix64(0xC0DE100 + seed, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
-    pvs[PV_START_PC] = PC_BASE
+    pvs[PV_START_PC] = start_pc
     pvs[PV_NEXT_PC] = int(npc[-1])  # where the program left off (its end, or a jump out of it)
     pvs[PV_EXECUTION_SHARD] = shard
     prep_traces = {"Program": prep, "Byte": A.byte_prep_trace()}
@@ -1701,6 +1729,68 @@ def _branch_trace(branches, byte_lookup):
         byte_lookup(A.B_U8RANGE, w[:, 0], w[:, 1])
         byte_lookup(A.B_U8RANGE, w[:, 2], w[:, 3])
     return t
+
+
+def memory_shard(state, regs, init_regs, shard: int, seed: int = 1):
+    """The shard that initialises and finalises the memory image of a whole execution (the executor's
+    postprocess, executor.rs:2538-2596): address 0 first, then every accessed register, then every touched
+    data word; MemoryGlobalInit sends each address's initial value, MemoryGlobalFinalize receives its
+    final access record, the Global chip accumulates both.  Public values chain the address ranges
+    (previous_*_addr_bits = 0: this is the only memory shard)."""
+    last, mem, mem_init, mem_last = state["last"], state["mem"], state["mem_init"], state["mem_last"]
+    rec0 = last[0] if last[0] != (0, 0) else (0, 1)
+    init = [(0, 0, 1, 1)]
+    fin = [(0, regs[0], rec0[0], rec0[1])]
+    for r in range(1, NUM_REGS):
+        if last[r] != (0, 0):
+            init.append((r, init_regs[r], 1, 1))
+            fin.append((r, regs[r], last[r][0], last[r][1]))
+    for x in sorted(mem):
+        init.append((x, mem_init[x], 1, 1))
+        fin.append((x, mem[x], mem_last[x][0], mem_last[x][1]))
+    mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
+    byte_lookup = A.byte_lookup_into(mult)
+    ti, mi, ri = MM.memory_global_trace(np.asarray(init, np.int64), True)
+    tf, mf, rf = MM.memory_global_trace(np.asarray(fin, np.int64), False)
+    msg, rec = np.concatenate([mi, mf]), np.concatenate([ri, rf])
+    tg, _ = MM.global_trace(msg, rec, np.full(len(msg), KIND_MEMORY, np.uint32), byte_lookup)
+    traces = {"MemoryGlobalInit": ti, "MemoryGlobalFinalize": tf, "Global": tg, "Byte": mult.astype(np.uint32)}
+    pvs = (splitmix64(0xC0DE100 + seed + shard, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
+    last_addr = max(a for a, *_ in init)
+    pvs[MM.PV_PREV_INIT_BITS:MM.PV_PREV_INIT_BITS + 32] = 0
+    pvs[MM.PV_PREV_FIN_BITS:MM.PV_PREV_FIN_BITS + 32] = 0
+    pvs[MM.PV_LAST_INIT_BITS:MM.PV_LAST_INIT_BITS + 32] = MM._bits32(last_addr)
+    pvs[MM.PV_LAST_FIN_BITS:MM.PV_LAST_FIN_BITS + 32] = MM._bits32(last_addr)
+    pvs[PV_SHARD] = shard
+    prep_traces = {"Program": None, "Byte": A.byte_prep_trace()}
+    return core_machine(), prep_traces, traces, pvs
+
+
+def program_shards(prog, seed: int = 1, shard_size: int = 1 << 12):
+    """A whole execution of `prog` as the reference's continuation shards (prove_with_context): CPU shards of
+    about shard_size instructions (the register/memory state carries over, each shard's MemoryLocal
+    closes its accesses through the Global chip), then the memory shard.  Returns the list of
+    (machine, prep_traces, traces, public_values)."""
+    regs = initial_registers(seed)
+    init_regs = list(regs)
+    state = fresh_state()
+    end = PC_BASE + 4 * len(prog)
+    out, shard = [], 1
+    while PC_BASE <= state["pc"] < end:
+        out.append(program_shard(prog, seed, shard, shard_size, state=state, regs=regs))
+        shard += 1
+    m, prep, traces, pvs = memory_shard(state, regs, init_regs, shard, seed)
+    # every shard holds the preprocessed chips (the verifier opens each vk chip in every shard,
+    # verifier.rs:123-138): the Program chip with zero multiplicities here
+    prep["Program"] = out[0][1]["Program"]
+    traces["Program"] = np.zeros((prep["Program"].shape[0], PROG_MAIN_WIDTH), np.uint32)
+    out.append((m, prep, traces, pvs))
+    return out
+
+
+def shard_global_digest(traces) -> np.ndarray:
+    """ShardProof::global_cumulative_sum of a shard: the Global chip's last-row cumulative sum."""
+    return traces["Global"][-1, MM.G_CUM_X:MM.G_CUM_X + 14].copy()
 
 
 def core_shard(n: int, seed: int = 1, shard: int = 1):

@@ -281,3 +281,159 @@ def global_trace(messages: np.ndarray, is_receive: np.ndarray, kinds: np.ndarray
         t[n:, G_SUMCHK:G_SUMCHK + 7] = final_chk
         t[n:, G_CUM_X:G_CUM_X + 14] = final
     return t, np.asarray(final, np.uint32)
+
+
+# ---------------------------------------------------------------- MemoryGlobalInit / Finalize (memory/global.rs)
+# MemoryInitCols (memory/global.rs:206-241)
+MG_SHARD, MG_TS, MG_ADDR, MG_LT = 0, 1, 2, 3                     # lt_cols: AssertLtColsBits<_, 32>
+MG_BITS = 35                                                     # addr_bits: KoalaBearBitDecomposition
+MG_AND = 67                                                      #   and_most_sig_byte_decomp_0_to_{2..7}
+MG_VALUE, MG_REAL, MG_NEXT_COMP = 73, 105, 106
+MG_IZ_INV, MG_IZ_RES, MG_FIRST_COMP, MG_LAST_ADDR = 107, 108, 109, 110
+MG_WIDTH = 111
+# PublicValues (crates/stark/src/air/public_values.rs:22-60)
+PV_PREV_INIT_BITS, PV_LAST_INIT_BITS, PV_PREV_FIN_BITS, PV_LAST_FIN_BITS = 45, 77, 109, 141
+
+
+def _koala_bear_range_check(ch, value, bits_base, and_base, is_real):
+    """KoalaBearBitDecomposition::range_check (operations/koala_bear_range.rs:51-120)."""
+    M = main
+    bits = [M(bits_base + i) for i in range(32)]
+    rec = Expr.lift(0)
+    for i, b in enumerate(bits):
+        _assert_bool(ch, b, is_real)
+        rec = rec + ((1 << i) % P) * b
+    ch.assert_zero(is_real * (rec - M(value)))
+    msb = bits[24:32]
+    ch.assert_zero(is_real * msb[7])
+    ch.assert_zero(is_real * (M(and_base) - msb[0] * msb[1]))
+    for k in range(1, 6):
+        ch.assert_zero(is_real * (M(and_base + k) - M(and_base + k - 1) * msb[k + 1]))
+    lower = Expr.lift(0)
+    for b in bits[:24]:
+        lower = lower + b
+    ch.assert_zero(is_real * M(and_base + 5) * lower)
+
+
+def _assert_lt_bits(ch, flags_base, a, b, is_real, flags_next=False):
+    """AssertLtColsBits<_, 32>::eval (operations/cmp.rs:289-354): a < b as 32-bit little-endian bit
+    vectors; the flag marks the most significant differing bit."""
+    col = main_next if flags_next else main
+    flags = [col(flags_base + i) for i in range(32)]
+    s = Expr.lift(0)
+    for f in flags:
+        _assert_bool(ch, f)
+        s = s + f
+    ch.assert_zero(is_real * (s - 1))
+    visited, acmp, bcmp = Expr.lift(0), Expr.lift(0), Expr.lift(0)
+    for i in range(31, -1, -1):
+        visited = visited + flags[i]
+        acmp = acmp + a[i] * flags[i]
+        bcmp = bcmp + b[i] * flags[i]
+        ch.assert_zero(is_real * (1 - visited) * (a[i] - b[i]))
+    ch.assert_zero(is_real * acmp)
+    ch.assert_zero(is_real * (bcmp - 1))
+
+
+def memory_global_chip(initialize: bool) -> ChipDesc:
+    """MemoryGlobalChip::eval (memory/global.rs:245-442) for MemoryGlobalInit / MemoryGlobalFinalize."""
+    from .machine import IS_LAST, pv
+    ch = ChipDesc("MemoryGlobalInit" if initialize else "MemoryGlobalFinalize", prep_width=0, main_width=MG_WIDTH)
+    M, N = main, main_next
+    real = M(MG_REAL)
+    _assert_bool(ch, real)
+    for i in range(32):
+        _assert_bool(ch, M(MG_VALUE + i))
+    byte = [V([("main", MG_VALUE + 8 * k + i, 1 << i) for i in range(8)]) for k in range(4)]
+    if initialize:
+        vals = [ZERO, ZERO, _m(MG_ADDR)] + byte + [_m(MG_REAL), ZERO, V.const(KIND_MEMORY)]
+    else:
+        vals = [_m(MG_SHARD), _m(MG_TS), _m(MG_ADDR)] + byte + [ZERO, _m(MG_REAL), V.const(KIND_MEMORY)]
+    ch.sends.append(Lookup(vals, _m(MG_REAL), KIND_GLOBAL))
+    _koala_bear_range_check(ch, MG_ADDR, MG_BITS, MG_AND, real)
+    ch.assert_zero(IS_TRANSITION * (N(MG_NEXT_COMP) - N(MG_REAL)))
+    _assert_lt_bits(ch, MG_LT, [M(MG_BITS + i) for i in range(32)], [N(MG_BITS + i) for i in range(32)],
+                    N(MG_NEXT_COMP), flags_next=True)
+    ch.assert_zero(IS_TRANSITION * (1 - real) * N(MG_REAL))
+    prev_base = PV_PREV_INIT_BITS if initialize else PV_PREV_FIN_BITS
+    last_base = PV_LAST_INIT_BITS if initialize else PV_LAST_FIN_BITS
+    prev_bits = [pv(prev_base + i) for i in range(32)]
+    prev_addr = Expr.lift(0)
+    for i in range(32):
+        prev_addr = prev_addr + prev_bits[i] * ((1 << i) % P)
+    # IsZeroOperation::eval(prev_addr, is_prev_addr_zero, is_first_row) (operations/is_zero.rs:42-66)
+    res = M(MG_IZ_RES)
+    ch.assert_zero(IS_FIRST * ((1 - M(MG_IZ_INV) * prev_addr) - res))
+    ch.assert_zero(IS_FIRST * (res * (res - 1)))
+    ch.assert_zero(IS_FIRST * res * prev_addr)
+    _assert_bool(ch, M(MG_FIRST_COMP))
+    ch.assert_zero(IS_FIRST * (M(MG_FIRST_COMP) - (1 - res)))
+    ch.assert_zero(IS_FIRST * (real - 1))
+    _assert_lt_bits(ch, MG_LT, prev_bits, [M(MG_BITS + i) for i in range(32)], M(MG_FIRST_COMP))
+    ch.assert_zero(IS_FIRST * res * M(MG_ADDR))
+    ch.assert_zero(IS_FIRST * res * (N(MG_REAL) - 1))
+    ch.assert_zero(IS_FIRST * res * (N(MG_NEXT_COMP) - 1))
+    if initialize:
+        ch.assert_zero(real * (M(MG_TS) - 1))
+    for i in range(32):
+        ch.assert_zero(IS_FIRST * (1 - M(MG_FIRST_COMP)) * M(MG_VALUE + i))
+    ch.assert_zero(IS_TRANSITION * (M(MG_LAST_ADDR) - real * (1 - N(MG_REAL))))
+    for i in range(32):
+        bit = M(MG_BITS + i) - pv(last_base + i)
+        ch.assert_zero(IS_LAST * real * bit)
+        ch.assert_zero(IS_TRANSITION * M(MG_LAST_ADDR) * bit)
+    return ch
+
+
+def _bits32(x: int):
+    return [(int(x) >> i) & 1 for i in range(32)]
+
+
+def memory_global_trace(events: np.ndarray, initialize: bool, prev_addr: int = 0):
+    """MemoryGlobalChip::generate_dependencies + generate_trace (memory/global.rs:62-188).  events: n x 4
+    (addr, value, shard, timestamp).  Returns (trace, global messages n x 7, is_receive n)."""
+    ev = np.asarray(events, np.int64).reshape(-1, 4)
+    ev = ev[np.argsort(ev[:, 0], kind="stable")]
+    n = len(ev)
+    t = np.zeros((A._pow2(n), MG_WIDTH), np.uint32)
+    addr = ev[:, 0]
+    t[:n, MG_ADDR], t[:n, MG_SHARD], t[:n, MG_TS] = addr, ev[:, 2], ev[:, 3]
+    bits = (addr[:, None] >> np.arange(32, dtype=np.int64)) & 1
+    t[:n, MG_BITS:MG_BITS + 32] = bits
+    msb = bits[:, 24:32]
+    acc = msb[:, 0] * msb[:, 1]
+    t[:n, MG_AND] = acc
+    for k in range(1, 6):
+        acc = acc * msb[:, k + 1]
+        t[:n, MG_AND + k] = acc
+    t[:n, MG_VALUE:MG_VALUE + 32] = (ev[:, 1:2] >> np.arange(32, dtype=np.int64)) & 1
+    t[:n, MG_REAL] = 1
+
+    def lt_flags(a: int, b: int):
+        x = a ^ b
+        f = [0] * 32
+        if x:
+            f[x.bit_length() - 1] = 1
+        return f
+
+    if n:
+        t[0, MG_IZ_INV] = _inv(prev_addr) if prev_addr else 0
+        t[0, MG_IZ_RES] = 1 if prev_addr == 0 else 0
+        t[0, MG_FIRST_COMP] = 1 if prev_addr != 0 else 0
+        if prev_addr != 0:
+            assert prev_addr < addr[0]
+            t[0, MG_LT:MG_LT + 32] = lt_flags(prev_addr, int(addr[0]))
+        for i in range(1, n):
+            assert addr[i - 1] < addr[i]
+            t[i, MG_NEXT_COMP] = 1
+            t[i, MG_LT:MG_LT + 32] = lt_flags(int(addr[i - 1]), int(addr[i]))
+        t[n - 1, MG_LAST_ADDR] = 1
+    else:
+        t[0, MG_IZ_RES] = 1 if prev_addr == 0 else 0
+    msg = np.zeros((n, 7), np.uint32)
+    if not initialize:
+        msg[:, 0], msg[:, 1] = ev[:, 2], ev[:, 3]
+    msg[:, 2] = addr
+    msg[:, 3:7] = A._bytes(ev[:, 1].astype(np.uint32))
+    rec = np.full(n, 0 if initialize else 1, np.uint8)
+    return t, msg, rec
