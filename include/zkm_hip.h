@@ -48,7 +48,7 @@ typedef struct zkm_main zkm_main; /* ShardMainData<SC, DeviceMatrix, DeviceProve
 typedef struct {
     uint32_t num_queries;      /* FRI_QUERIES, default 84 */
     uint32_t pow_bits;         /* proof_of_work_bits, 16 */
-    uint32_t log_blowup;       /* 1 (only value supported) */
+    uint32_t log_blowup;       /* 1 (core config) or 2 (compressed_fri_config, kb31_poseidon2.rs:217-227) */
     uint32_t proof_montgomery; /* 0: field elements in proof bytes are canonical; 1: Montgomery */
 } zkm_config_t;
 

@@ -74,10 +74,11 @@ int orc_api_machine_info(void *mh, int chip, int32_t *info /* prep,main,perm_ef,
 }
 
 void *orc_api_setup(void *mh, int num_queries, int pow_bits, int montgomery, const uint32_t *const *prep,
-                    const uint64_t *prep_heights, uint32_t pc_start, const uint32_t *gcs, uint32_t *commit_out) {
+                    const uint64_t *prep_heights, uint32_t pc_start, const uint32_t *gcs, uint32_t *commit_out,
+                    int log_blowup) {
     orc_machine_t *m = (orc_machine_t *)mh;
     orc_pk_t *pk = (orc_pk_t *)calloc(1, sizeof *pk);
-    orc_config_t cfg = {num_queries, pow_bits, 1, montgomery};
+    orc_config_t cfg = {num_queries, pow_bits, log_blowup, montgomery};
     size_t *h = (size_t *)calloc(m->nchips + 1, sizeof(size_t));
     for (int i = 0; i < m->nchips; i++) h[i] = prep_heights[i];
     int rc = orc_setup(pk, m, cfg, (const kb_t *const *)prep, h, pc_start, gcs);

@@ -230,7 +230,11 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
       << "    const uint64_t hq = A.q >> 1;\n"
       << "    const uint32_t om = k < hq ? A.tw[hq + k] : neg(A.tw[hq + (k - hq)]);\n"
       << "    const uint32_t x = mul(A.gen, om);\n"
-      << "    const uint32_t zh = (A.q == 2 * A.n) ? ((k & 1) ? sub(neg(A.gen_pow_n), ONE) : sub(A.gen_pow_n, ONE)) : sub(A.gen_pow_n, ONE);\n"
+      // Z_H(x) = x^n - 1 = 3^n w_{Q/n}^(k mod Q/n) - 1 (Q/n = 2^log_qd: 1, 2 or 4 values)
+      << "    const uint64_t qn = A.q / A.n;\n"
+      << "    uint32_t zp = ONE;\n"
+      << "    if (qn > 1) { const uint64_t zm = k & (qn - 1), zhh = qn >> 1; zp = zm < zhh ? A.tw[zhh + zm] : neg(A.tw[zhh + (zm - zhh)]); }\n"
+      << "    const uint32_t zh = sub(mul(A.gen_pow_n, zp), ONE);\n"
       << "    const uint32_t d_first = sub(x, ONE), d_last = sub(x, A.wn_inv);\n"
       << "    const uint32_t inv_fl = inv(mul(mul(d_first, d_last), zh));\n"
       << "    const uint32_t zh2 = mul(zh, zh);\n"

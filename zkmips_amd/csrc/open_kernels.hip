@@ -185,8 +185,14 @@ __global__ __launch_bounds__(NT) void k_quotient(QuotArgs a) {
     const uint64_t rn = rev_bits((uint32_t)kn, a.log_q);
     // selectors at x = 3 w_Q^k over trace domain H_N (quotient.rs:42; Plonky3 selectors_on_coset)
     const uint32_t x = mul(a.gen, root_pow(a.tw, a.q, k));
-    const uint32_t zh = (a.q == 2 * a.n) ? ((k & 1) ? sub(neg(a.gen_pow_n), ONE) : sub(a.gen_pow_n, ONE))
-                                         : sub(a.gen_pow_n, ONE);
+    // Z_H(x) = x^n - 1 = 3^n w_{Q/n}^(k mod Q/n) - 1 (Q/n = 2^log_qd: 1, 2 or 4 values)
+    const uint64_t qn = a.q / a.n;
+    uint32_t zp = ONE;
+    if (qn > 1) {
+        const uint64_t zm = k & (qn - 1), zhh = qn >> 1;
+        zp = zm < zhh ? a.tw[zhh + zm] : neg(a.tw[zhh + (zm - zhh)]);
+    }
+    const uint32_t zh = sub(mul(a.gen_pow_n, zp), ONE);
     const uint32_t d_first = sub(x, ONE), d_last = sub(x, a.wn_inv);
     const uint32_t inv_fl = inv(mul(mul(d_first, d_last), zh));  // one inversion for three
     const uint32_t is_first = mul(mul(inv_fl, d_last), mul(zh, zh));

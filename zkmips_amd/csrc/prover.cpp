@@ -127,12 +127,36 @@ static std::vector<int> sort_order(const std::vector<uint64_t> &h, const std::ve
     return o;
 }
 
-static void add_lde(Ctx &c, DTree &t, const DMat &src, uint32_t shift, bool bitrev_in, hipStream_t s) {
-    t.owned.emplace_back(2 * src.height * (src.width ? src.width : 1), s);
-    DMat dst{t.owned.back().p, 2 * src.height, src.width};
-    if (bitrev_in) lde_batch_bitrev_in(c, src, shift, dst, s);
-    else lde_batch(c, src, shift, dst, s);
-    t.mats.push_back(dst);
+// Bit-reversed coset LDE with blowup 2^lb of src (N x W) into dst (column stride N << lb): row i holds
+// p(shift * w_{2^lb N}^{rev(i)}).  The blowup-2 kernels give rows [0, 2N) directly; for blowup 4, rows
+// [2N, 4N) are the blowup-2 LDE with shift * w_{4N} (rev_{4N}(2N + j) = 2 rev_{2N}(j) + 1), so two
+// passes through a 2N-row buffer fill the two halves of every column.
+static void lde_into(Ctx &c, const DMat &src, uint32_t shift, bool bitrev_in, int lb, uint32_t *dst, hipStream_t s) {
+    const uint64_t N = src.height, W = src.width;
+    if (!W) return;
+    ARG_CHECK(lb == 1 || lb == 2, "log_blowup must be 1 or 2");
+    if (lb == 1) {
+        DMat d{dst, 2 * N, W};
+        if (bitrev_in) lde_batch_bitrev_in(c, src, shift, d, s);
+        else lde_batch(c, src, shift, d, s);
+        return;
+    }
+    DBuf tmp(2 * N * W, s);
+    DMat d{tmp.p, 2 * N, W};
+    for (int half = 0; half < 2; half++) {
+        const uint32_t sh = half ? mul(shift, two_adic_gen(ilog2(N) + 2)) : shift;
+        if (bitrev_in) lde_batch_bitrev_in(c, src, sh, d, s);
+        else lde_batch(c, src, sh, d, s);
+        HIP_CHECK(hipMemcpy2DAsync(dst + half * 2 * N, 4 * N * 4, tmp.p, 2 * N * 4, 2 * N * 4, W,
+                                   hipMemcpyDeviceToDevice, s));
+    }
+}
+
+static void add_lde(Ctx &c, DTree &t, const DMat &src, uint32_t shift, bool bitrev_in, int lb, hipStream_t s) {
+    const uint64_t H = src.height << lb;
+    t.owned.emplace_back(H * (src.width ? src.width : 1), s);
+    lde_into(c, src, shift, bitrev_in, lb, t.owned.back().p, s);
+    t.mats.push_back(DMat{t.owned.back().p, H, src.width});
 }
 
 // One LDE launch sequence for several same-height matrices whose columns sit side by side in `src`
@@ -140,19 +164,15 @@ static void add_lde(Ctx &c, DTree &t, const DMat &src, uint32_t shift, bool bitr
 // sub-view (returned in order; the caller places them in the tree's commit order).  Same-height
 // chips of a shard thus share launches instead of taking a handful each.
 static std::vector<DMat> lde_group(Ctx &c, DTree &t, const uint32_t *src, uint64_t N, const std::vector<uint64_t> &widths,
-                                   uint32_t shift, bool bitrev_in, hipStream_t s) {
-    const uint64_t W = std::accumulate(widths.begin(), widths.end(), (uint64_t)0);
-    t.owned.emplace_back(2 * N * (W ? W : 1), s);
+                                   uint32_t shift, bool bitrev_in, int lb, hipStream_t s) {
+    const uint64_t W = std::accumulate(widths.begin(), widths.end(), (uint64_t)0), H = N << lb;
+    t.owned.emplace_back(H * (W ? W : 1), s);
     uint32_t *dst = t.owned.back().p;
-    if (W) {
-        DMat sm{const_cast<uint32_t *>(src), N, W}, dm{dst, 2 * N, W};
-        if (bitrev_in) lde_batch_bitrev_in(c, sm, shift, dm, s);
-        else lde_batch(c, sm, shift, dm, s);
-    }
+    lde_into(c, DMat{const_cast<uint32_t *>(src), N, W}, shift, bitrev_in, lb, dst, s);
     std::vector<DMat> v;
     uint64_t off = 0;
     for (uint64_t w : widths) {
-        v.push_back(DMat{dst + off * 2 * N, 2 * N, w});
+        v.push_back(DMat{dst + off * H, H, w});
         off += w;
     }
     return v;
@@ -345,7 +365,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             while (a > 0 && md.heights[a - 1] == N) a--;
             std::vector<uint64_t> ws;
             for (int k = a; k <= i; k++) ws.push_back(4 * (uint64_t)m.chips[md.chip[k]].perm_w);
-            for (const DMat &v : lde_group(c, perm_tree, perm_traces[a], N, ws, to_mont(GENERATOR), false, s))
+            for (const DMat &v : lde_group(c, perm_tree, perm_traces[a], N, ws, to_mont(GENERATOR), false, lb, s))
                 perm_tree.mats.push_back(v);
         }
     }
@@ -404,7 +424,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         qa.main = md.tree.mats[i].d;
         qa.prep = pki >= 0 ? pk.tree.mats[pki].d : nullptr;
         qa.perm = perm_tree.mats[i].d;
-        qa.ld = 2 * N;
+        qa.ld = N << lb;  // the quotient domain's Q = N 2^lqd points are the first Q bit-reversed LDE rows
         qa.n = N; qa.q = Q; qa.log_n = logN; qa.log_q = logN + lqd; qa.step = 1 << lqd;
         qa.tw = c.tw_fwd;
         qa.gen = to_mont(GENERATOR);
@@ -438,7 +458,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             const uint32_t wq = two_adic_gen(logN + lqd);
             const std::vector<uint64_t> ws(i - a + 1, 4);
             for (int j = 0; j < (1 << lqd); j++) {
-                std::vector<DMat> v = lde_group(c, q_tree, q_ptr[a][j], N, ws, inv(pow(wq, (uint64_t)j)), true, s);
+                std::vector<DMat> v = lde_group(c, q_tree, q_ptr[a][j], N, ws, inv(pow(wq, (uint64_t)j)), true, lb, s);
                 for (int k = a; k <= i; k++) q_view[k].push_back(v[k - a]);
             }
         }
@@ -802,7 +822,7 @@ int zkm_setup(zkm_ctx *ctx, const uint32_t *blob, size_t nwords, const zkm_confi
     ARG_CHECK(ctx && blob && cfg && pk_out && commit_out && gcs, "null argument");
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
     HIP_CHECK(hipSetDevice(c->device));
-    ARG_CHECK(cfg->log_blowup == 1, "only log_blowup = 1 is supported");
+    ARG_CHECK(cfg->log_blowup == 1 || cfg->log_blowup == 2, "log_blowup must be 1 or 2");
     ARG_CHECK(cfg->pow_bits < 31, "pow_bits");
     auto pk = std::make_unique<Pk>();
     pk->device = c->device;
@@ -854,7 +874,7 @@ int zkm_setup(zkm_ctx *ctx, const uint32_t *blob, size_t nwords, const zkm_confi
         pk->heights.push_back(prep[ci].height);
         pk->traces.push_back(upload_matrix(*c, prep[ci], L.s));
         DMat src{pk->traces.back().p, prep[ci].height, prep[ci].width};
-        add_lde(*c, pk->tree, src, to_mont(GENERATOR), false, L.s);
+        add_lde(*c, pk->tree, src, to_mont(GENERATOR), false, (int)cfg->log_blowup, L.s);
     }
     tree_build(pk->tree, L.s);
     memcpy(pk->commit, pk->tree.root, 32);
@@ -932,7 +952,8 @@ int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32
             ws.push_back(traces[o].width);
             off += traces[o].width;
         }
-        for (const DMat &v : lde_group(*c, md->tree, base, N, ws, to_mont(GENERATOR), false, L.s)) md->tree.mats.push_back(v);
+        for (const DMat &v : lde_group(*c, md->tree, base, N, ws, to_mont(GENERATOR), false, (int)pk->cfg.log_blowup, L.s))
+            md->tree.mats.push_back(v);
     }
     tree_build(md->tree, L.s);
     md->pv.assign(pv, pv + npv);

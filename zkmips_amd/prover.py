@@ -42,11 +42,12 @@ class HipProver:
 
     def __init__(self, device: Device, machine: MachineDesc, prep_traces: Dict[str, np.ndarray],
                  num_queries: int = 84, pow_bits: int = 16, proof_montgomery: bool = False,
-                 pc_start: int = 0x00400000, initial_global_cumulative_sum: Optional[np.ndarray] = None):
+                 pc_start: int = 0x00400000, initial_global_cumulative_sum: Optional[np.ndarray] = None,
+                 log_blowup: int = 1):
         self.dev = device
         self.machine = machine
         self.blob = machine.blob()
-        self.cfg = Config(num_queries, pow_bits, 1, int(proof_montgomery))
+        self.cfg = Config(num_queries, pow_bits, log_blowup, int(proof_montgomery))
         keep: list = []
         mats = (Matrix * len(machine.chips))()
         for i, c in enumerate(machine.chips):

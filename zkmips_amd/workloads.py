@@ -147,3 +147,29 @@ def fib_shard(n: int, seed: int = 7):
     prep_traces = {"FibTable": fib_table_prep(th)}
     traces = {"FibCpu": fib_cpu_trace(n, pvs), "FibTable": fib_table_trace(th)}
     return m, prep_traces, traces, pvs
+
+
+def deg5_shard(n: int, seed: int = 7):
+    """fib_shard plus a degree-5 chip (log_quotient_degree 2, which needs blowup 4): ``Pow5`` proves
+    y = x^5 on every row and sends/receives (x, y) as a balanced local lookup; its height is n / 2, so
+    the shard mixes quotient degrees 2 and 4 and three trace heights (compressed_fri_config's
+    shape of problem, crates/stark/src/kb31_poseidon2.rs:217-227; COMPRESS_DEGREE, prover/src/lib.rs:106)."""
+    from .machine import ChipDesc, Lookup, VirtualPairCol, main
+    m, prep, traces, pvs = fib_shard(n, seed)
+    ch = ChipDesc("Pow5", prep_width=0, main_width=3)
+    x, y, real = main(0), main(1), main(2)
+    ch.assert_zero(y - x * x * x * x * x)
+    ch.assert_zero(real * (real - 1))
+    vals = [VirtualPairCol.single_main(0), VirtualPairCol.single_main(1)]
+    ch.sends.append(Lookup(vals, VirtualPairCol.single_main(2), 5))
+    ch.receives.append(Lookup(list(vals), VirtualPairCol.single_main(2), 5))
+    m.chips.append(ch)
+    h = max(16, n // 2)
+    xs = splitmix64(0xDE65000 + seed, h) % np.uint64(P)
+    t = np.zeros((h, 3), np.uint32)
+    t[:, 0] = xs
+    x2 = xs * xs % np.uint64(P)
+    t[:, 1] = x2 * x2 % np.uint64(P) * xs % np.uint64(P)
+    t[:, 2] = (np.arange(h) % 4 != 3)
+    traces["Pow5"] = t
+    return m, prep, traces, pvs
