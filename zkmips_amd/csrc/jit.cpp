@@ -250,7 +250,9 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
       << "    facc.zero();\n"
       << g.pipelined(8, "ZKM_JIT_LOOKAHEAD_Q")  // measured: 8 -> 2.27 ms, 24 -> 2.44, unpipelined 2.78
       << "    const ef qv = ef_mul_base(facc.value(), inv_z);\n"
-      << "    const uint64_t c = t >> A.log_n, pos = t & (A.n - 1);\n"
+      // chunk j = k mod 2^lqd (split_evals); t = rev_Q(k) = rev_lqd(j) * n + rev_n(k >> lqd), so the
+      // chunk's position t mod n is its bit-reversed row
+      << "    const uint64_t c = k & (uint64_t)(A.step - 1), pos = t & (A.n - 1);\n"
       << "    A.chunks[c * A.cstride + 0 * A.n + pos] = qv.c[0];\n"
       << "    A.chunks[c * A.cstride + 1 * A.n + pos] = qv.c[1];\n"
       << "    A.chunks[c * A.cstride + 2 * A.n + pos] = qv.c[2];\n"

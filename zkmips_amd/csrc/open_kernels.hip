@@ -297,8 +297,9 @@ __global__ __launch_bounds__(NT) void k_quotient(QuotArgs a) {
         }
     }
     const ef q = ef_mul_base(acc, inv_z);
-    // chunk c = k mod 2^lqd (= top bit of t when lqd = 1), stored bit-reversed within the chunk
-    const uint64_t c = t >> a.log_n;
+    // chunk c = k mod 2^lqd (t = rev_Q(k) = rev_lqd(c) n + rev_n(k >> lqd)), stored bit-reversed within
+    // the chunk
+    const uint64_t c = k & (uint64_t)(a.step - 1);
     const uint64_t pos = t & (a.n - 1);
 #pragma unroll
     for (int e = 0; e < 4; e++) a.chunks[c * a.cstride + e * a.n + pos] = q.c[e];
