@@ -656,11 +656,11 @@ def test_loop_gpu_full_size_verifies(dev):
 @pytest.mark.gpu
 def test_core_gpu_full_size_verifies(dev):
     from zkmips_amd.prover import HipProver
-    # random-instruction shard, Cpu 2^17 rows: core_shard's Python executor costs ~0.4 ms per instruction
-    # with MiscInstrs in the mix, so the 2^22-row Cpu case is test_loop_gpu_full_size_verifies
-    n = (1 << 16) + 12345
+    # random-instruction shard at the headline height: Cpu 2^22 rows (2.1M instructions, every
+    # restated chip incl. MiscInstrs, MemoryLocal and Global; ~30 s of trace generation)
+    n = (1 << 21) + 12345
     m, prep, tr, pv = C.core_shard(n, seed=11)
-    assert tr["Cpu"].shape == (1 << 17, 67)
+    assert tr["Cpu"].shape == (1 << 22, 67)
     gpu = HipProver(dev, m, prep, num_queries=84)
     cpu = O.OracleProver(m, prep, num_queries=84)
     proof = gpu.prove_shard(tr, pv)
