@@ -61,6 +61,27 @@ __global__ __launch_bounds__(NT) void k_compress_level(const uint32_t *__restric
     o[1] = make_uint4(s[4], s[5], s[6], s[7]);
 }
 
+// Level with injected matrices whose rows were hashed beforehand (by k_hash_leaves, the prefetching
+// one-thread-per-row sponge): node = compress(compress(left, right), digest of the injected row).
+__global__ __launch_bounds__(NT) void k_compress_inject(const uint32_t *__restrict__ prev, uint32_t *__restrict__ out,
+                                                        uint64_t h, const uint32_t *__restrict__ inj_digest) {
+    uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= h) return;
+    uint32_t s[16];
+    const uint4 *p = (const uint4 *)(prev + i * 16);
+    uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+    s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+    s[8] = c.x; s[9] = c.y; s[10] = c.z; s[11] = c.w; s[12] = d.x; s[13] = d.y; s[14] = d.z; s[15] = d.w;
+    p2::permute(s);
+    const uint4 *q = (const uint4 *)(inj_digest + i * 8);
+    uint4 e = q[0], f = q[1];
+    s[8] = e.x; s[9] = e.y; s[10] = e.z; s[11] = e.w; s[12] = f.x; s[13] = f.y; s[14] = f.z; s[15] = f.w;
+    p2::permute(s);
+    uint4 *o = (uint4 *)(out + i * 8);
+    o[0] = make_uint4(s[0], s[1], s[2], s[3]);
+    o[1] = make_uint4(s[4], s[5], s[6], s[7]);
+}
+
 __global__ void k_p2_batch(uint32_t *st, uint64_t n) {
     uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
@@ -160,6 +181,18 @@ static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
         if (h <= SMALL16 && ninj == 0) {
             hipLaunchKernelGGL(k_compress16, dim3((unsigned)((h * 16 + NT - 1) / NT)), dim3(NT), 0, s,
                                (const uint32_t *)t.layers[L - 1], t.layers[L], h);
+            HIP_CHECK(hipGetLastError());
+            continue;
+        }
+        if (ninj > 0) {
+            // the injected rows go through the leaf kernel first (its prefetching sponge runs at the
+            // VALU-issue bound; one thread doing compress + sponge + compress ran at ~0.75 of it)
+            DBuf dig(8 * h, s);
+            hipLaunchKernelGGL(k_hash_leaves, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
+                               (const uint64_t *)inj[L].first->p, ninj, h, dig.p);
+            HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(k_compress_inject, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
+                               (const uint32_t *)t.layers[L - 1], t.layers[L], h, (const uint32_t *)dig.p);
             HIP_CHECK(hipGetLastError());
             continue;
         }
