@@ -20,6 +20,7 @@ from tests import _oracle as O
 from zkmips_amd import mips_alu as A
 from zkmips_amd import mips_core as MC
 from zkmips_amd import mips_memory as MM
+from zkmips_amd import mips_syscall as SY
 from zkmips_amd.machine import MachineDesc
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -46,7 +47,17 @@ CHIPS = {
     "MiscInstrs": (MC.misc_instructions_chip, 0, 72, 17, 1, False, "misc/others/trace.rs:24", None),
     "MemoryLocal": (MM.memory_local_chip, 0, 56, 9, 1, False, "memory/local.rs:86", None),
     "Global": (MM.global_chip, 0, 99, 2, 1, False, "global/mod.rs:65", None),
+    "MemoryGlobalInit": (lambda: MM.memory_global_chip(True), 0, 111, 2, 1, False, "memory/global.rs:48", None),
+    "MemoryGlobalFinalize": (lambda: MM.memory_global_chip(False), 0, 111, 2, 1, False, "memory/global.rs:48",
+                             None),
+    "SyscallInstrs": (SY.syscall_instrs_chip, 0, 64, 2, 1, False, "syscall/instructions/trace.rs:25", None),
+    "SyscallCore": (lambda: SY.syscall_chip(True), 0, 6, 2, 1, False, "syscall/chip.rs:78", None),
+    "SyscallPrecompile": (lambda: SY.syscall_chip(False), 0, 6, 2, 1, False, "syscall/chip.rs:78", None),
+    "ShaExtend": (SY.sha_extend_chip, 0, 176, 37, 1, False, "sha256/extend/trace.rs:18", None),
+    "ShaCompress": (SY.sha_compress_chip, 0, 262, 59, 1, False, "sha256/compress/trace.rs:21", None),
 }
+# precompile chips are costed per call: rows per event x per-row cost (mips/mod.rs:216-222)
+ROWS_PER_EVENT = {"ShaExtend": 48, "ShaCompress": 80}
 
 
 def _cost(ch):
@@ -60,7 +71,8 @@ def test_chip_shape_and_cost(name):
     assert ch.name == name
     assert (ch.prep_width, ch.main_width, ch.perm_width_ef, ch.log_quotient_degree) == (prep, main, perm, lqd)
     assert ch.local_only is local_only
-    assert _cost(ch) == COSTS[name], f"{name}: cost {_cost(ch)} != mips_costs.json {COSTS[name]}"
+    cost = ROWS_PER_EVENT.get(name, 1) * _cost(ch)
+    assert cost == COSTS[name], f"{name}: cost {cost} != mips_costs.json {COSTS[name]}"
 
 
 def test_local_only_reaches_the_blob():

@@ -171,3 +171,18 @@ class Device:
         ms = C.c_double()
         check(lib().zkm_bench_lde(self.h, h, w, iters, C.byref(ms)), "zkm_bench_lde")
         return ms.value
+
+
+def prefill_jit_cache(machines) -> int:
+    """Compile every chip's quotient/permutation kernels of `machines` for gfx950 into the JIT's on-disk
+    code-object cache (zkmips_amd/jit_cache, see csrc/jit.cpp); no device needed.  Returns code bytes."""
+    total = 0
+    for m in machines:
+        blob = np.ascontiguousarray(m.blob(), np.uint32)
+        n = C.c_uint64(0)
+        rc = lib().zkm_quotient_jit_compile(blob.ctypes.data_as(C.c_void_p), C.c_size_t(blob.size), C.byref(n))
+        if rc != 0:
+            raise ZkmError(f"quotient JIT compile failed ({rc}): {lib().zkm_last_error().decode()}")
+        total += n.value
+    return total
+

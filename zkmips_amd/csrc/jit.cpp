@@ -7,14 +7,26 @@
 // order (crates/stark/src/folder.rs:79-102, permutation.rs:256-346).  The generic interpreter
 // kernel (open_kernels.hip k_quotient) remains as the GPU path when JIT compilation is disabled
 // (ZKM_NO_JIT=1) or fails.
+//
+// Compiled code objects are cached by a hash of (source, arch, options): in memory for the process,
+// and on disk in ZKM_JIT_CACHE (default: jit_cache/ next to this library; "off" disables it), so a
+// large chip (ShaExtend: ~1 min of hiprtc) compiles once per tree.  __graft_entry__.build() fills
+// the cache for the shipped machines on the build host (hiprtc needs no device).
 #include "jit.hpp"
 
+#include <dlfcn.h>
 #include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <fstream>
+#include <future>
 #include <map>
+#include <mutex>
 #include <sstream>
+#include <unordered_map>
 
 #include "jit_prelude.inc"
 
@@ -332,10 +344,74 @@ bool jit_enabled() {
     return !(e && *e && *e != '0');
 }
 
+namespace {
+
+uint64_t fnv1a(const std::string &s, uint64_t h = 1469598103934665603ull) {
+    for (unsigned char ch : s) h = (h ^ ch) * 1099511628211ull;
+    return h;
+}
+
+std::string cache_dir() {
+    if (const char *e = getenv("ZKM_JIT_CACHE")) return std::string(e) == "off" ? std::string() : std::string(e);
+    Dl_info info;
+    if (!dladdr((void *)&fnv1a, &info) || !info.dli_fname) return std::string();
+    std::string lib = info.dli_fname;
+    const size_t slash = lib.rfind('/');
+    return (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/jit_cache";
+}
+
+std::mutex g_cache_mu;
+std::unordered_map<uint64_t, std::vector<char>> g_cache;
+
+bool read_file(const std::string &path, std::vector<char> &out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return !out.empty();
+}
+
+void write_file_atomic(const std::string &dir, const std::string &name, const std::vector<char> &code) {
+    mkdir(dir.c_str(), 0755);  // may already exist
+    const std::string tmp = dir + "/." + name + "." + std::to_string(getpid()) + ".tmp";
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) return;  // read-only tree: the in-memory cache still holds it
+        f.write(code.data(), (std::streamsize)code.size());
+        if (!f) { unlink(tmp.c_str()); return; }
+    }
+    if (rename(tmp.c_str(), (dir + "/" + name).c_str()) != 0) unlink(tmp.c_str());
+}
+
+std::vector<char> compile_source(const std::string &src, const std::string &name, const std::string &arch_name);
+
+}  // namespace
+
 std::vector<char> jit_chip_code(const ChipDesc &c, const std::string &arch_name) {
     const std::string src = chip_source(c);
+    const uint64_t key = fnv1a(src, fnv1a(arch_name + "|-O3|-std=c++17|"));
+    {
+        std::lock_guard<std::mutex> g(g_cache_mu);
+        auto it = g_cache.find(key);
+        if (it != g_cache.end()) return it->second;
+    }
+    char kname[32];
+    snprintf(kname, sizeof kname, "%016llx", (unsigned long long)key);
+    const std::string dir = cache_dir(), fname = c.name + "-" + arch_name + "-" + kname + ".co";
+    std::vector<char> code;
+    if (dir.empty() || !read_file(dir + "/" + fname, code)) {
+        code = compile_source(src, c.name, arch_name);
+        if (!dir.empty()) write_file_atomic(dir, fname, code);
+    }
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    g_cache[key] = code;
+    return code;
+}
+
+namespace {
+
+std::vector<char> compile_source(const std::string &src, const std::string &name, const std::string &arch_name) {
     if (const char *d = getenv("ZKM_JIT_DUMP")) {
-        if (FILE *f = fopen((std::string(d) + "/" + c.name + ".hip").c_str(), "w")) {
+        if (FILE *f = fopen((std::string(d) + "/" + name + ".hip").c_str(), "w")) {
             fputs(src.c_str(), f);
             fclose(f);
         }
@@ -352,7 +428,7 @@ std::vector<char> jit_chip_code(const ChipDesc &c, const std::string &arch_name)
         std::string log(ls + 1, '\0');
         hiprtcGetProgramLog(prog, &log[0]);
         hiprtcDestroyProgram(&prog);
-        throw HipError("hiprtc compile failed for chip " + c.name + ": " + log.substr(0, 2000));
+        throw HipError("hiprtc compile failed for chip " + name + ": " + log.substr(0, 2000));
     }
     size_t cs = 0;
     hiprtcGetCodeSize(prog, &cs);
@@ -361,6 +437,8 @@ std::vector<char> jit_chip_code(const ChipDesc &c, const std::string &arch_name)
     hiprtcDestroyProgram(&prog);
     return code;
 }
+
+}  // namespace
 
 JitKernel jit_chip(const ChipDesc &c, int device) {
     JitKernel k;
@@ -396,8 +474,11 @@ extern "C" int zkm_quotient_jit_compile(const uint32_t *blob, size_t nwords, uin
     try {
         ARG_CHECK(blob && code_bytes, "null argument");
         const zkm::Machine m = zkm::parse_machine(blob, nwords);
+        std::vector<std::future<size_t>> fut;  // chips compile concurrently (and fill the cache)
+        for (const auto &c : m.chips)
+            fut.push_back(std::async(std::launch::async, [&c] { return zkm::jit_chip_code(c, "gfx950").size(); }));
         uint64_t total = 0;
-        for (const auto &c : m.chips) total += zkm::jit_chip_code(c, "gfx950").size();
+        for (auto &f : fut) total += f.get();
         *code_bytes = total;
         return 0;
     } catch (const std::exception &e) {

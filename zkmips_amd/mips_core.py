@@ -20,6 +20,7 @@ import numpy as np
 
 from . import mips_alu as A
 from . import mips_memory as MM
+from . import mips_syscall as SY
 from .machine import (ChipDesc, Expr, IS_FIRST, IS_LAST, IS_TRANSITION, KIND_BYTE, KIND_INSTRUCTION, KIND_MEMORY,
                       KIND_PROGRAM, Lookup, MachineDesc, P, VirtualPairCol as V, main, main_next, pv)
 from .workloads import NUM_PV_ELTS, PROOF_MAX_NUM_PVS, splitmix64
@@ -1129,14 +1130,15 @@ def _jump_trace(jumps):
 
 
 def core_machine() -> MachineDesc:
-    # MipsAir::chips order (crates/core/machine/src/mips/mod.rs:207-431): Cpu, Program, ALUs, Branch, ...,
-    # Byte; the memory stand-in last
-    return MachineDesc([cpu_chip(), program_chip(), divrem_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
-                        A.shift_right_chip(),
-                        A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(), jump_chip(), memory_instructions_chip(),
-                        movcond_chip(), misc_instructions_chip(),
+    # MipsAir::get_airs_and_costs order (crates/core/machine/src/mips/mod.rs:207-437): Cpu, Program, the
+    # precompiles, SyscallCore/Precompile, the ALUs, Branch, Jump, SyscallInstrs, MemoryInstrs, MiscInstrs,
+    # the memory chips, Global, Byte, (SysLinux,) MovCond
+    return MachineDesc([cpu_chip(), program_chip(), SY.sha_extend_chip(), SY.sha_compress_chip(), SY.syscall_chip(True),
+                        SY.syscall_chip(False), divrem_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
+                        A.shift_right_chip(), A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(),
+                        jump_chip(), SY.syscall_instrs_chip(), memory_instructions_chip(), misc_instructions_chip(),
                         MM.memory_global_chip(True), MM.memory_global_chip(False), MM.memory_local_chip(),
-                        MM.global_chip(), A.byte_chip()], NUM_PV_ELTS)
+                        MM.global_chip(), A.byte_chip(), movcond_chip()], NUM_PV_ELTS)
 
 
 # ---------------------------------------------------------------- program + execution
@@ -1336,7 +1338,7 @@ def fresh_state():
     """Machine state before the first instruction: each register's / data word's last access
     (shard, timestamp), the data words' values, and (pc, next_pc)."""
     return {"last": [(0, 0)] * NUM_REGS, "pc": PC_BASE, "npc": PC_BASE + 4, "mem": {}, "mem_init": {},
-            "mem_last": {}}
+            "mem_last": {}, "precompile": [], "exit_code": None}
 
 
 def _execute(prog, regs, shard, max_steps, state=None):
@@ -1357,14 +1359,19 @@ def _execute(prog, regs, shard, max_steps, state=None):
     ev = {k: [] for k in ("add", "bit", "lt", "sll", "sr", "clz")}
     branches, jumps, muls, divs, movs, mevs, misc = [], [], [], [], [], [], []
     mem, mem_init, mem_last = state["mem"], state["mem_init"], state["mem_last"]
+    # the CPU's own MemoryLocal entries for data words: (shard, clk, value) before its first access in the
+    # shard; entries a syscall closed early (SyscallContext::postprocess) go to cpu_done
+    cpu_first, cpu_done = {}, []
+    syscalls, commits = [], {}
     U = A.UNUSED_PC
-    while PC_BASE <= pc < end:  # the program halts when pc leaves it
+    clk = 0
+    while PC_BASE <= pc < end and state.get("exit_code") is None:  # the program halts when pc leaves it
         if split and len(steps) >= max_steps and npc == pc + 4:
             break
         assert len(steps) < max_steps or (split and len(steps) < max_steps + 2)
         k = (pc - PC_BASE) >> 2
         op, ra, rb, c, immb, immc = prog[k]
-        clk = 5 * len(steps)
+        extra = 0
         acc = []
         if immc:
             cv = c
@@ -1421,6 +1428,8 @@ def _execute(prog, regs, shard, max_steps, state=None):
                 mem[aligned] = mem_init[aligned] = _mem_word(aligned)
             pmem = mem[aligned]
             mps, mpc = mem_last.get(aligned, (0, 0))
+            if aligned not in cpu_first:
+                cpu_first[aligned] = (mps, mpc, pmem)
             hi = prev_a  # hi_or_prev_a = the register's previous value
             if op in LOAD_OPS:
                 av = nmem = None
@@ -1538,6 +1547,27 @@ def _execute(prog, regs, shard, max_steps, state=None):
             if ra:
                 regs[ra] = av
             nnpc = npc + 4
+        elif op == SY.OP_SYSCALL:  # executor.rs:1570-1652: V0 holds the code, A0/A1 the arguments
+            code = prev_a
+            sid = SY.syscall_id(code)
+            extra = code >> 24
+            av = hi = code  # the syscalls here return None: V0 keeps the code
+            npc = pc + 4  # SyscallContext::new: next_pc = pc + 4 (HALT sets 0)
+            if sid == SY.syscall_id(SY.HALT):
+                npc = 0
+                state["exit_code"] = bv
+            elif sid == SY.COMMIT:
+                commits[bv] = cv
+            elif code in SY.PRECOMPILES:
+                pm = SY.PrecompileMemory(mem, mem_init, mem_last, cpu_first, cpu_done, shard, _mem_word)
+                pev = SY.PRECOMPILES[code](pm, shard, clk, bv, cv)
+                state["precompile"].append((code, (shard, clk, sid, bv, cv), pev))
+            else:
+                raise NotImplementedError(f"syscall {code:#x}")
+            syscalls.append((pc, npc, shard, clk, av, bv, cv, prev_a, sid))
+            written = av
+            regs[ra] = av
+            nnpc = npc + 4
         else:
             av = _alu(op, bv, cv)
             written = av if ra else 0
@@ -1551,10 +1581,15 @@ def _execute(prog, regs, shard, max_steps, state=None):
             last[REG_HI] = (shard, clk + POS_HI)
             regs[REG_HI] = hi
         steps.append((k, op, av, bv, cv, prev_a, written, npc, nnpc, immb, immc, acc,
-                      hi if op in MUL_OPS + DIV_OPS + MOVCOND_OPS + MEM_OPS + MISC_OPS else 0))
+                      hi if op in MUL_OPS + DIV_OPS + MOVCOND_OPS + MEM_OPS + MISC_OPS + (SY.OP_SYSCALL,) else 0,
+                      clk, extra))
+        clk += 5 + extra
+        assert clk < (1 << 24), "the shard's clk must stay within 24 bits"
         pc, npc = npc, nnpc
     state["pc"], state["npc"] = pc, npc
-    return steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc
+    mem_entries = cpu_done + [(x, *cpu_first[x], *mem_last[x], mem[x]) for x in sorted(cpu_first)]
+    sysinfo = {"syscalls": syscalls, "commits": commits, "mem_entries": mem_entries}
+    return steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc, sysinfo
 
 
 def _mem_word(addr):
@@ -1579,10 +1614,8 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     if state is None:
         regs = initial_registers(seed)
     start_regs, start_last = list(regs), list(state["last"]) if state else [(0, 0)] * NUM_REGS
-    start_mem = dict(state["mem"]) if state else {}
-    start_mem_last = dict(state["mem_last"]) if state else {}
     start_pc = state["pc"] if state else PC_BASE
-    steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc = \
+    steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc, sysinfo = \
         _execute(prog, regs, shard, max_steps, state)
     n = len(steps)
     assert n > 0
@@ -1597,9 +1630,13 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     npc, nnpc, immb, immc = S[:, 7], S[:, 8], S[:, 9].astype(bool), S[:, 10].astype(bool)
     P_ = np.asarray(prog, np.int64).reshape(-1, 6)
     pcs = (PC_BASE + 4 * ks).astype(np.uint32)
-    clk = 5 * np.arange(n, dtype=np.int64)
+    clk = np.asarray([s_[13] for s_ in steps], np.int64)
+    extra = np.asarray([s_[14] for s_ in steps], np.int64)
     is_branch = np.isin(ops, BRANCH_OPS)
-    is_seq = ~(is_branch | np.isin(ops, JUMP_OPS))
+    is_syscall = ops == SY.OP_SYSCALL
+    # cpu/trace.rs:179-195: HALT / SYS_EXT_GROUP syscalls halt
+    halt = is_syscall & np.isin(prev_a & 0xFFFF, (SY.syscall_id(SY.HALT), SY.SYS_EXT_GROUP))
+    is_seq = ~(is_branch | np.isin(ops, JUMP_OPS) | halt)
 
     mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
     byte_lookup = A.byte_lookup_into(mult)
@@ -1618,11 +1655,13 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     t[:n, C_NPC] = npc
     t[:n, C_NNPC] = nnpc
     t[:n, C_OPCODE:C_IMMC + 1] = instr_cols[ks]
-    t[:n, C_RW_A] = np.isin(ops, (OP_MEQ, OP_MNE, OP_INS) + MEM_OPS + MADDSUB_OPS)  # is_rw_a (instruction.rs:180-205)
+    t[:n, C_RW_A] = np.isin(ops, (OP_MEQ, OP_MNE, OP_INS, SY.OP_SYSCALL) + MEM_OPS + MADDSUB_OPS)  # instruction.rs:180-205
     t[:n, C_SEQ] = is_seq
+    t[:n, C_HALT] = halt
+    t[:n, C_EXTRA] = extra
     his = np.asarray([s_[12] for s_ in steps], np.int64)
     # is_mult_div_instruction || is_check_memory_instruction: the row sends its shard and clk
-    mult_div = np.isin(ops, MULT_DIV + MEM_OPS + MADDSUB_OPS)
+    mult_div = np.isin(ops, MULT_DIV + MEM_OPS + MADDSUB_OPS + (SY.OP_SYSCALL,))
     t[:n, C_HI_PREV_A:C_HI_PREV_A + 4] = A._bytes(his.astype(np.uint32))
     t[:n, C_CHECK_MEM] = mult_div
     t[:n, C_SHARD_SEND] = np.where(mult_div, shard, 0)
@@ -1670,6 +1709,14 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
         traces["MemoryInstrs"] = _mem_instr_trace(mevs, shard, byte_lookup)
     if misc:
         traces["MiscInstrs"] = _misc_trace(misc, shard, byte_lookup)
+    sc = np.asarray(sysinfo["syscalls"], np.int64).reshape(-1, 9)
+    core_sc = np.zeros((0, 5), np.int64)
+    if len(sc):
+        traces["SyscallInstrs"] = SY.syscall_instrs_trace(sc)
+        # SyscallChip(Core) rows: codes with a table (byte 2) or Linux syscalls (chip.rs:157-166)
+        tab = ((sc[:, 7] >> 16) & 0xFF == 1) | ((sc[:, 7] >> 8) & 0xFF != 0)
+        core_sc = sc[tab][:, [2, 3, 8, 5, 6]]
+        traces["SyscallCore"] = SY.syscall_trace(core_sc)
 
     # Program: one row per instruction, multiplicity = executions
     ph = max(16, 1 << (len(prog) - 1).bit_length())
@@ -1684,19 +1731,27 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     # reference collects them from a hash map; the order is free), with the access record before the
     # shard (shard, clk, value) and after it
     ent = [(r, *start_last[r], start_regs[r], *last[r], regs[r]) for r in range(NUM_REGS) if last[r] != start_last[r]]
-    ent += [(x, *start_mem_last.get(x, (0, 0)), start_mem.get(x, mem_init[x]), *mem_last[x], mem[x])
-            for x in sorted(mem) if mem_last[x] != start_mem_last.get(x)]
+    ent += sysinfo["mem_entries"]
     ent = np.asarray(ent, np.int64).reshape(-1, 7)
     traces["MemoryLocal"] = MM.memory_local_trace(ent)
     gmsg, grec = MM.memory_local_global_events(ent)
-    traces["Global"], _ = MM.global_trace(gmsg, grec, np.full(len(gmsg), KIND_MEMORY, np.uint32), byte_lookup)
+    # Global messages in chip order: SyscallCore's sends, then MemoryLocal's
+    smsg = SY.syscall_global_messages(core_sc)
+    msg = np.concatenate([smsg, gmsg])
+    rec = np.concatenate([np.zeros(len(smsg), np.uint8), grec])
+    kinds = np.concatenate([np.full(len(smsg), SY.KIND_SYSCALL, np.uint32), np.full(len(gmsg), KIND_MEMORY, np.uint32)])
+    traces["Global"], _ = MM.global_trace(msg, rec, kinds, byte_lookup)
 
     assert mult.max() < P
     traces["Byte"] = mult.astype(np.uint32)
     pvs = (splitmix64(0xC0DE100 + seed, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
     pvs[PV_START_PC] = start_pc
-    pvs[PV_NEXT_PC] = int(npc[-1])  # where the program left off (its end, or a jump out of it)
+    pvs[PV_NEXT_PC] = int(npc[-1])  # where the program left off (its end, a jump out of it, or 0 on HALT)
     pvs[PV_EXECUTION_SHARD] = shard
+    for idx, word in sysinfo["commits"].items():  # COMMIT: committed_value_digest[idx] (syscalls/commit.rs)
+        pvs[4 * idx:4 * idx + 4] = A._bytes(np.asarray([word], np.uint32))[0]
+    if halt.any():
+        pvs[PV_EXIT_CODE] = int(bv[halt][0])
     prep_traces = {"Program": prep, "Byte": A.byte_prep_trace()}
     return core_machine(), prep_traces, traces, pvs
 
@@ -1766,26 +1821,110 @@ def memory_shard(state, regs, init_regs, shard: int, seed: int = 1):
     return core_machine(), prep_traces, traces, pvs
 
 
-def program_shards(prog, seed: int = 1, shard_size: int = 1 << 12):
+PRECOMPILE_CHIP = {SY.SHA_EXTEND: "ShaExtend", SY.SHA_COMPRESS: "ShaCompress"}
+
+
+def precompile_shard(code: int, events, shard: int, seed: int = 1):
+    """A precompile shard (ExecutionRecord::split, executor/src/record.rs:130-193): the syscall events of one
+    precompile, its chip's rows, SyscallPrecompile (one row per call), the calls' local memory accesses in
+    MemoryLocal and the Global chip accumulating the syscall receives and the memory messages."""
+    mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
+    byte_lookup = A.byte_lookup_into(mult)
+    pevs = [e for _, _, e in events]
+    sev = np.asarray([s_ for _, s_, _ in events], np.int64).reshape(-1, 5)
+    traces = {}
+    if code == SY.SHA_EXTEND:
+        traces["ShaExtend"] = SY.sha_extend_trace(pevs, byte_lookup)
+    elif code == SY.SHA_COMPRESS:
+        traces["ShaCompress"] = SY.sha_compress_trace(pevs, byte_lookup)
+    else:
+        raise NotImplementedError(hex(code))
+    traces["SyscallPrecompile"] = SY.syscall_trace(sev)
+    ent = np.asarray([x for e in pevs for x in e["local"]], np.int64).reshape(-1, 7)
+    traces["MemoryLocal"] = MM.memory_local_trace(ent)
+    gmsg, grec = MM.memory_local_global_events(ent)
+    smsg = SY.syscall_global_messages(sev)
+    msg = np.concatenate([smsg, gmsg])
+    rec = np.concatenate([np.ones(len(smsg), np.uint8), grec])
+    kinds = np.concatenate([np.full(len(smsg), SY.KIND_SYSCALL, np.uint32), np.full(len(gmsg), KIND_MEMORY, np.uint32)])
+    traces["Global"], _ = MM.global_trace(msg, rec, kinds, byte_lookup)
+    assert mult.max() < P
+    traces["Byte"] = mult.astype(np.uint32)
+    pvs = (splitmix64(0xC0DE100 + seed + shard, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
+    pvs[PV_SHARD] = shard
+    return core_machine(), {"Program": None, "Byte": A.byte_prep_trace()}, traces, pvs
+
+
+def program_shards(prog, seed: int = 1, shard_size: int = 1 << 12, precompile_events_per_shard: int = 1 << 10):
     """A whole execution of `prog` as the reference's continuation shards (prove_with_context): CPU shards of
     about shard_size instructions (the register/memory state carries over, each shard's MemoryLocal
-    closes its accesses through the Global chip), then the memory shard.  Returns the list of
+    closes its accesses through the Global chip), then the precompile shards (each precompile's calls in
+    chunks, ExecutionRecord::split), then the memory shard.  Returns the list of
     (machine, prep_traces, traces, public_values)."""
     regs = initial_registers(seed)
     init_regs = list(regs)
     state = fresh_state()
     end = PC_BASE + 4 * len(prog)
     out, shard = [], 1
-    while PC_BASE <= state["pc"] < end:
+    while PC_BASE <= state["pc"] < end and state["exit_code"] is None:
         out.append(program_shard(prog, seed, shard, shard_size, state=state, regs=regs))
         shard += 1
-    m, prep, traces, pvs = memory_shard(state, regs, init_regs, shard, seed)
+    by_code = {}
+    for ev in state["precompile"]:
+        by_code.setdefault(ev[0], []).append(ev)
+    for code in sorted(by_code, key=lambda c: list(PRECOMPILE_CHIP).index(c)):
+        evs = by_code[code]
+        for k in range(0, len(evs), precompile_events_per_shard):
+            out.append(precompile_shard(code, evs[k:k + precompile_events_per_shard], shard, seed))
+            shard += 1
+    out.append(memory_shard(state, regs, init_regs, shard, seed))
     # every shard holds the preprocessed chips (the verifier opens each vk chip in every shard,
-    # verifier.rs:123-138): the Program chip with zero multiplicities here
-    prep["Program"] = out[0][1]["Program"]
-    traces["Program"] = np.zeros((prep["Program"].shape[0], PROG_MAIN_WIDTH), np.uint32)
-    out.append((m, prep, traces, pvs))
+    # verifier.rs:123-138): the Program chip with zero multiplicities in the non-CPU shards
+    prog_prep = out[0][1]["Program"]
+    for m, prep, traces, pvs in out:
+        if "Program" not in traces:
+            prep["Program"] = prog_prep
+            traces["Program"] = np.zeros((prog_prep.shape[0], PROG_MAIN_WIDTH), np.uint32)
     return out
+
+
+SHA_H_PTR = DATA_BASE + 0x300
+SHA_H0 = [0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19]
+
+
+def sha_program(calls: int, seed: int = 1, loads: int = 4, commit: bool = True, halt: bool = True,
+                compress: bool = True):
+    """A guest hashing `calls` random 64-byte blocks the way the reference's sha2 guests do: per block it
+    stores 16 words, calls SHA_EXTEND on them (two buffers used in turn, so a word's CPU MemoryLocal
+    entry is split by the syscall), then SHA_COMPRESS into the state at SHA_H_PTR (initialised to the
+    SHA-256 IV), reads some words back and sums them; then COMMITs the sum and HALTs."""
+    r = splitmix64(0x5A5A000 + seed, 16 * calls + 8)
+    prog = []
+    acc, tmp = 10, 9
+    if compress:
+        for i, hv in enumerate(SHA_H0):
+            prog += [(A.OP_ADD, 8, 0, hv, 0, 1), (OP_SW, 8, 0, SHA_H_PTR + 4 * i, 0, 1)]
+    for k in range(calls):
+        w_ptr = DATA_BASE + 0x400 + 0x100 * (k % 2)
+        for i in range(16):
+            prog.append((A.OP_ADD, 8, 0, int(r[16 * k + i] & np.uint64(M32)), 0, 1))
+            prog.append((OP_SW, 8, 0, w_ptr + 4 * i, 0, 1))
+        prog += [(A.OP_ADD, SY.REG_V0, 0, SY.SHA_EXTEND, 0, 1), (A.OP_ADD, SY.REG_A0, 0, w_ptr, 0, 1),
+                 (A.OP_ADD, SY.REG_A1, 0, 0, 0, 1), (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
+        if compress:
+            prog += [(A.OP_ADD, SY.REG_V0, 0, SY.SHA_COMPRESS, 0, 1), (A.OP_ADD, SY.REG_A1, 0, SHA_H_PTR, 0, 1),
+                     (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0),
+                     (OP_LW, tmp, 0, SHA_H_PTR + 4 * (k % 8), 0, 1), (A.OP_ADD, acc, acc, tmp, 0, 0)]
+        for j in range(loads):
+            prog.append((OP_LW, tmp, 0, w_ptr + 4 * (16 + (7 * j + k) % 48), 0, 1))
+            prog.append((A.OP_ADD, acc, acc, tmp, 0, 0))
+    if commit:
+        prog += [(A.OP_ADD, SY.REG_V0, 0, SY.COMMIT, 0, 1), (A.OP_ADD, SY.REG_A0, 0, 3, 0, 1),
+                 (A.OP_ADD, SY.REG_A1, acc, 0, 0, 1), (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
+    if halt:
+        prog += [(A.OP_ADD, SY.REG_V0, 0, SY.HALT, 0, 1), (A.OP_ADD, SY.REG_A0, 0, 0, 0, 1),
+                 (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
+    return prog
 
 
 def shard_global_digest(traces) -> np.ndarray:
