@@ -55,6 +55,7 @@ CHIPS = {
     "SyscallPrecompile": (lambda: SY.syscall_chip(False), 0, 6, 2, 1, False, "syscall/chip.rs:78", None),
     "ShaExtend": (SY.sha_extend_chip, 0, 176, 37, 1, False, "sha256/extend/trace.rs:18", None),
     "ShaCompress": (SY.sha_compress_chip, 0, 262, 59, 1, False, "sha256/compress/trace.rs:21", None),
+    "SysLinux": (SY.sys_linux_chip, 0, 69, 12, 1, False, "sys_linux/trace.rs:21", None),
 }
 # precompile chips are costed per call: rows per event x per-row cost (mips/mod.rs:216-222)
 ROWS_PER_EVENT = {"ShaExtend": 48, "ShaCompress": 80}

@@ -205,3 +205,102 @@ def test_syscall_gpu_proofs_identical(run):
         assert rc == 0 and p == ref
         proofs.append(p)
     assert machine_global_sum_is_zero(proofs)
+
+
+# sys_linux_tests::sys_linux_program (crates/core/machine/src/syscall/precompiles/sys_linux/mod.rs:22-179),
+# as (opcode, op_a, op_b, op_c, imm_b, imm_c) rows: 64 stores, then every Linux syscall the SysLinux
+# table covers (mmap/mmap2 with and without a hint, brk, clone, fcntl over its fd/cmd cases, the
+# no-op syscalls, read, write), then exit_group
+def _sys_linux_program():
+    ADD, SW = 0, C.OP_SW
+    w_ptr, h_ptr = 100, 1000
+    prog = [(ADD, 29, 0, 5, 0, 1)]
+    for i in range(64):
+        prog += [(ADD, 30, 0, w_ptr + 4 * i, 0, 1), (SW, 29, 30, 0, 0, 1)]
+    calls = [(SY.SYS_MMAP, w_ptr, h_ptr), (SY.SYS_MMAP, 0, h_ptr), (SY.SYS_MMAP2, w_ptr, h_ptr),
+             (SY.SYS_MMAP2, 0, h_ptr), (SY.SYS_BRK, 0, h_ptr), (SY.SYS_CLONE, 0, h_ptr)]
+    calls += [(SY.SYS_FCNTL, a0, a1) for a1 in (3, 1) for a0 in (0, 1, 2, 0xff)] + [(SY.SYS_FCNTL, 1, 0x33)]
+    calls += [(code, 1, 1) for code in (4263, 4005, 4288, 4006, 4194, 4195, 4206, 4215, 4218, 4222, 4240, 4338)]
+    calls += [(SY.SYS_READ, 0, 0x33), (SY.SYS_READ, 1, 0x33)]
+    for code, a0, a1 in calls:
+        prog += [(ADD, 2, 0, code, 0, 1), (ADD, 4, 0, a0, 0, 1), (ADD, 5, 0, a1, 0, 1), (SY.OP_SYSCALL, 2, 4, 5, 0, 0)]
+    for a1 in (0x33, 0x11):
+        prog += [(ADD, 2, 0, SY.SYS_WRITE, 0, 1), (ADD, 4, 0, 0, 0, 1), (ADD, 5, 0, a1, 0, 1), (ADD, 6, 0, 0x100, 0, 1),
+                 (SY.OP_SYSCALL, 2, 4, 5, 0, 0)]
+    prog += [(ADD, 2, 0, SY.SYS_EXT_GROUP, 0, 1), (ADD, 4, 0, 0, 0, 1), (SY.OP_SYSCALL, 2, 4, 5, 0, 0)]
+    return prog
+
+
+@pytest.fixture(scope="module")
+def linux_run():
+    return C.program_shards(_sys_linux_program(), seed=5, shard_size=100)
+
+
+def test_sys_linux_program_results():
+    state, regs = _execute(_sys_linux_program(), seed=5)
+    assert state["exit_code"] == 0 and state["pc"] == 0
+    evs = [e for k, _, e in state["precompile"]]
+    assert all(k == SY.SYS_LINUX for k, _, _ in state["precompile"]) and len(evs) == 32
+    heap0 = C.initial_registers(5)[C.REG_HEAP]
+    mm = [e for e in evs if e["code"] in (SY.SYS_MMAP, SY.SYS_MMAP2)]
+    assert [e["v0"] for e in mm] == [100, heap0, 100, (heap0 + 0x1000) & 0xFFFFFFFF]  # 1000 rounds up to a page
+    fc = [(e["a0"], e["a1"], e["v0"], e["writes"][0][1]) for e in evs if e["code"] == SY.SYS_FCNTL]
+    assert fc[:4] == [(0, 3, 0, 0), (1, 3, 1, 0), (2, 3, 1, 0), (0xff, 3, 0xFFFFFFFF, 9)]
+    assert fc[4:] == [(0, 1, 0, 0), (1, 1, 1, 0), (2, 1, 2, 0), (0xff, 1, 0xFFFFFFFF, 9), (1, 0x33, 0xFFFFFFFF, 9)]
+    wr = [e for e in evs if e["code"] == SY.SYS_WRITE]
+    assert [e["v0"] for e in wr] == [0x100, 0x100]
+    assert regs[SY.REG_A3] == 0
+
+
+def test_sys_linux_shards_satisfy_air(linux_run):
+    assert "SysLinux" in linux_run[-2][2] and int(linux_run[-2][2]["SysLinux"][:, SY.SL_REAL].sum()) == 32
+    for m, prep, tr, pv in linux_run:
+        assert _air_check.check(m, {k: v for k, v in prep.items() if v is not None}, tr, pv) == ([], [])
+    digs = np.asarray([C.shard_global_digest(tr) for _, _, tr, _ in linux_run])
+    assert np.array_equal(S.digest_sum(digs), S.CURVE_CUMULATIVE_SUM_START)
+    last_cpu = [pv for _, _, tr, pv in linux_run if "Cpu" in tr][-1]
+    assert last_cpu[C.PV_NEXT_PC] == 0 and last_cpu[SY.PV_EXIT_CODE] == 0
+
+
+@pytest.mark.parametrize("what", ["brk_result", "fcntl_errno", "mmap_heap"])
+def test_sys_linux_tamper_rejected(linux_run, what):
+    m, prep, tr, pv = linux_run[-2]
+    t = tr["SysLinux"]
+    codes = t[:, SY.SL_ID]
+    bad = {n: v.copy() for n, v in tr.items()}
+    if what == "brk_result":
+        k = int(np.nonzero(codes == SY.SYS_BRK)[0][0])
+        bad["SysLinux"][k, SY.SL_RES] ^= 1
+    elif what == "fcntl_errno":
+        k = int(np.nonzero((codes == SY.SYS_FCNTL) & (t[:, SY.SL_A0] == 0xff))[0][0])
+        bad["SysLinux"][k, SY.SL_OUT + 4] = 0
+    else:
+        k = int(np.nonzero((codes == SY.SYS_MMAP) & (t[:, SY.SL_MMAP_A0_0] == 1))[0][0])
+        bad["SysLinux"][k, SY.SL_IO + 4] ^= 4
+    prep = {n: v for n, v in prep.items() if v is not None}
+    assert _air_check.check(m, prep, bad, pv) != ([], [])
+
+
+def test_sys_linux_oracle_proofs_verify(linux_run):
+    m, prep, _, _ = linux_run[0]
+    pr = O.OracleProver(m, {k: v for k, v in prep.items() if v is not None}, num_queries=4)
+    proofs = []
+    for _, _, tr, pv in linux_run:
+        rc, p = pr.prove(tr, pv)
+        assert rc == 0 and pr.verify(p) == 0
+        proofs.append(p)
+    assert machine_global_sum_is_zero(proofs)
+
+
+@pytest.mark.gpu
+def test_sys_linux_gpu_proofs_identical(linux_run):
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    m, prep, _, _ = linux_run[0]
+    prep = {k: v for k, v in prep.items() if v is not None}
+    gpu = HipProver(Device(0), m, prep, num_queries=16)
+    cpu = O.OracleProver(m, prep, num_queries=16)
+    for _, _, tr, pv in linux_run:
+        p = gpu.prove_shard(tr, pv)
+        rc, ref = cpu.prove(tr, pv)
+        assert rc == 0 and p == ref

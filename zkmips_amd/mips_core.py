@@ -264,7 +264,8 @@ def _range_checker_cols(v: np.ndarray) -> np.ndarray:
 # ---------------------------------------------------------------- Mul (alu/mul)
 OP_MUL, OP_MULT, OP_MULTU = 2, 3, 4  # executor/src/opcode.rs:18-20
 MUL_OPS = (OP_MUL, OP_MULT, OP_MULTU)
-REG_LO, REG_HI, NUM_REGS = 32, 33, 34  # Register::LO / HI; MULT/MULTU write LO via op_a, HI at position HI
+REG_LO, REG_HI = 32, 33  # Register::LO / HI; MULT/MULTU write LO via op_a, HI at position HI
+REG_BRK, REG_HEAP, NUM_REGS = 34, 35, 36  # executor/src/register.rs:3-42
 POS_HI = 4
 # MulCols (alu/mul/mod.rs:35-105); op_hi_access is MemoryReadWriteCols (prev_value + access)
 MU_PC, MU_NPC, MU_HI, MU_A, MU_B, MU_C, MU_CARRY, MU_PROD = 0, 1, 2, 6, 10, 14, 18, 26
@@ -1138,7 +1139,7 @@ def core_machine() -> MachineDesc:
                         A.shift_right_chip(), A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(),
                         jump_chip(), SY.syscall_instrs_chip(), memory_instructions_chip(), misc_instructions_chip(),
                         MM.memory_global_chip(True), MM.memory_global_chip(False), MM.memory_local_chip(),
-                        MM.global_chip(), A.byte_chip(), movcond_chip()], NUM_PV_ELTS)
+                        MM.global_chip(), A.byte_chip(), SY.sys_linux_chip(), movcond_chip()], NUM_PV_ELTS)
 
 
 # ---------------------------------------------------------------- program + execution
@@ -1362,6 +1363,8 @@ def _execute(prog, regs, shard, max_steps, state=None):
     # the CPU's own MemoryLocal entries for data words: (shard, clk, value) before its first access in the
     # shard; entries a syscall closed early (SyscallContext::postprocess) go to cpu_done
     cpu_first, cpu_done = {}, []
+    # the CPU's register entries likewise: the record each register's open entry starts from
+    reg_start, reg_done = [(last[r], regs[r]) for r in range(NUM_REGS)], []
     syscalls, commits = [], {}
     U = A.UNUSED_PC
     clk = 0
@@ -1558,10 +1561,21 @@ def _execute(prog, regs, shard, max_steps, state=None):
                 state["exit_code"] = bv
             elif sid == SY.COMMIT:
                 commits[bv] = cv
-            elif code in SY.PRECOMPILES:
-                pm = SY.PrecompileMemory(mem, mem_init, mem_last, cpu_first, cpu_done, shard, _mem_word)
-                pev = SY.PRECOMPILES[code](pm, shard, clk, bv, cv)
-                state["precompile"].append((code, (shard, clk, sid, bv, cv), pev))
+            elif code in SY.PRECOMPILES or SY.is_linux(code):
+                pm = SY.PrecompileMemory(mem, mem_init, mem_last, cpu_first, cpu_done, shard, _mem_word,
+                                         regs, last, reg_start, reg_done)
+                if SY.is_linux(code):  # syscalls/precompiles/sys_linux/*.rs: V0 <- v0 unless None
+                    ret, pev = SY.exec_sys_linux(pm, shard, clk, code, bv, cv)
+                    if sid == SY.SYS_EXT_GROUP:
+                        npc = 0
+                        state["exit_code"] = bv
+                    if ret is not None:
+                        av = ret
+                    key = SY.SYS_LINUX
+                else:
+                    pev = SY.PRECOMPILES[code](pm, shard, clk, bv, cv)
+                    key = code
+                state["precompile"].append((key, (shard, clk, sid, bv, cv), pev))
             else:
                 raise NotImplementedError(f"syscall {code:#x}")
             syscalls.append((pc, npc, shard, clk, av, bv, cv, prev_a, sid))
@@ -1588,7 +1602,9 @@ def _execute(prog, regs, shard, max_steps, state=None):
         pc, npc = npc, nnpc
     state["pc"], state["npc"] = pc, npc
     mem_entries = cpu_done + [(x, *cpu_first[x], *mem_last[x], mem[x]) for x in sorted(cpu_first)]
-    sysinfo = {"syscalls": syscalls, "commits": commits, "mem_entries": mem_entries}
+    reg_entries = reg_done + [(r, *reg_start[r][0], reg_start[r][1], *last[r], regs[r]) for r in range(NUM_REGS)
+                              if last[r] != reg_start[r][0]]
+    sysinfo = {"syscalls": syscalls, "commits": commits, "mem_entries": mem_entries, "reg_entries": reg_entries}
     return steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc, sysinfo
 
 
@@ -1613,7 +1629,6 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     (program_shards), the shard continues a longer execution and stops after about max_steps."""
     if state is None:
         regs = initial_registers(seed)
-    start_regs, start_last = list(regs), list(state["last"]) if state else [(0, 0)] * NUM_REGS
     start_pc = state["pc"] if state else PC_BASE
     steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc, sysinfo = \
         _execute(prog, regs, shard, max_steps, state)
@@ -1730,8 +1745,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     # MemoryLocal: every register the shard accessed, then every data word it touched, by address (the
     # reference collects them from a hash map; the order is free), with the access record before the
     # shard (shard, clk, value) and after it
-    ent = [(r, *start_last[r], start_regs[r], *last[r], regs[r]) for r in range(NUM_REGS) if last[r] != start_last[r]]
-    ent += sysinfo["mem_entries"]
+    ent = sysinfo["reg_entries"] + sysinfo["mem_entries"]
     ent = np.asarray(ent, np.int64).reshape(-1, 7)
     traces["MemoryLocal"] = MM.memory_local_trace(ent)
     gmsg, grec = MM.memory_local_global_events(ent)
@@ -1821,7 +1835,7 @@ def memory_shard(state, regs, init_regs, shard: int, seed: int = 1):
     return core_machine(), prep_traces, traces, pvs
 
 
-PRECOMPILE_CHIP = {SY.SHA_EXTEND: "ShaExtend", SY.SHA_COMPRESS: "ShaCompress"}
+PRECOMPILE_CHIP = {SY.SHA_EXTEND: "ShaExtend", SY.SHA_COMPRESS: "ShaCompress", SY.SYS_LINUX: "SysLinux"}
 
 
 def precompile_shard(code: int, events, shard: int, seed: int = 1):
@@ -1837,6 +1851,8 @@ def precompile_shard(code: int, events, shard: int, seed: int = 1):
         traces["ShaExtend"] = SY.sha_extend_trace(pevs, byte_lookup)
     elif code == SY.SHA_COMPRESS:
         traces["ShaCompress"] = SY.sha_compress_trace(pevs, byte_lookup)
+    elif code == SY.SYS_LINUX:
+        traces["SysLinux"] = SY.sys_linux_trace(pevs, byte_lookup)
     else:
         raise NotImplementedError(hex(code))
     traces["SyscallPrecompile"] = SY.syscall_trace(sev)

@@ -39,6 +39,11 @@ HALT, COMMIT, COMMIT_DEFERRED_PROOFS = 0x00_00_00_00, 0x00_00_00_10, 0x00_00_00_
 ENTER_UNCONSTRAINED, EXIT_UNCONSTRAINED, HINT_LEN = 0x03, 0x04, 0xF0
 SHA_EXTEND, SHA_COMPRESS = 0x30_01_00_05, 0x01_01_00_06
 SYS_EXT_GROUP = 4246
+# Linux syscalls (code.rs:143-183), handled by the SysLinux precompile table (byte 1 != 0)
+SYS_LINUX, SYS_READ, SYS_WRITE, SYS_BRK, SYS_FCNTL, SYS_MMAP2, SYS_CLONE, SYS_MMAP = 4000, 4003, 4004, 4045, 4055, 4090, 4120, 4210
+SYS_NOPS = (4005, 4006, 4091, 4194, 4195, 4206, 4215, 4218, 4222, 4240, 4263, 4288, 4338)  # open .. prlimit64
+REG_A2, REG_A3, REG_BRK, REG_HEAP = 6, 7, 34, 35
+MIPS_EBADF, PAGE_SIZE = 9, 0x1000
 PV_DIGEST_WORDS = 8
 PV_DEFERRED = 32  # deferred_proofs_digest follows the 8 committed-value digest words
 PV_EXIT_CODE = 42
@@ -46,6 +51,10 @@ PV_EXIT_CODE = 42
 
 def syscall_id(code: int) -> int:
     return code & 0xFFFF
+
+
+def is_linux(code: int) -> bool:
+    return code in (SYS_READ, SYS_WRITE, SYS_BRK, SYS_FCNTL, SYS_MMAP2, SYS_CLONE, SYS_MMAP, SYS_EXT_GROUP) + SYS_NOPS
 
 
 def _w(base):
@@ -829,17 +838,233 @@ def _rotr_np(x, s):
     return ((x >> s) | (x << (32 - s))) & M32
 
 
+# ---------------------------------------------------------------- SysLinux
+# SysLinuxCols (sys_linux/columns.rs:12-62)
+SL_SHARD, SL_CLK, SL_ID, SL_A0, SL_A1, SL_RES, SL_IO, SL_OUT = 0, 1, 2, 3, 7, 11, 15, 28
+SL_A0_0, SL_A0_1, SL_A0_2, SL_MMAP, SL_MMAP2, SL_MMAP_A0_0, SL_PAGE_OFF, SL_OFF_0, SL_UPPER = range(41, 50)
+SL_CLONE, SL_EXIT, SL_BRK, SL_GT = 50, 51, 52, 53  # GtColsBytes: byte_flags[4], a_cmp, b_cmp, result
+SL_FCNTL, SL_A1_1, SL_A1_3, SL_F_A1_1, SL_F_A1_3, SL_READ, SL_WRITE, SL_NOP, SL_REAL = range(60, 69)
+SL_WIDTH = 69
+
+
+def _eval_gt_bytes(ch, a_base, b_base, base, is_real, is_real_v):
+    """GtColsBytes::eval (operations/cmp.rs:74-137): a > b over little-endian bytes."""
+    M = main
+    _u8_pairs(ch, _vw(a_base), is_real_v)
+    _u8_pairs(ch, _vw(b_base), is_real_v)
+    flags = [M(base + i) for i in range(4)]
+    for f in flags:
+        _assert_bool(ch, f, is_real)
+    _assert_bool(ch, sum(flags[1:], flags[0]), is_real)
+    visited = Expr.lift(0)
+    first_gt = Expr.lift(0)
+    b_cmp = Expr.lift(0)
+    for i in range(3, -1, -1):
+        visited = visited + flags[i]
+        first_gt = first_gt + M(a_base + i) * flags[i]
+        b_cmp = b_cmp + M(b_base + i) * flags[i]
+        ch.assert_zero((1 - visited) * is_real * (M(a_base + i) - M(b_base + i)))
+    ch.assert_zero(is_real * (M(base + 4) - first_gt))
+    ch.assert_zero(is_real * (M(base + 5) - b_cmp))
+    ch.sends.append(Lookup([V.const(A.B_LTU), _m(base + 6), ZERO, _m(base + 5), _m(base + 4)], is_real_v, KIND_BYTE))
+
+
+def sys_linux_chip() -> ChipDesc:
+    """SysLinuxChip::eval (sys_linux/air.rs:33-323): eval_brk, eval_clone, eval_exit_group, eval_fnctl,
+    eval_read, eval_write, eval_mmap, eval_nop, the A3 write, flag checks, the syscall receive."""
+    from .mips_core import ACC_VALUE, _eval_memory_access
+    ch = ChipDesc("SysLinux", prep_width=0, main_width=SL_WIDTH)
+    M = main
+    f = lambda c: M(c)
+    a0, a1, res = _w(SL_A0), _w(SL_A1), _w(SL_RES)
+    io_prev, io_val = _w(SL_IO), _w(SL_IO + 4 + ACC_VALUE)
+    out = _w(SL_OUT + 4 + ACC_VALUE)
+    mem = lambda acc, reg, chk, chk_v: _eval_memory_access(ch, acc + 4, acc, 0, V.const(reg), chk, chk_v,
+                                                           shard_col=SL_SHARD, clk_terms=((SL_CLK, 1),))
+    word_is = lambda when, w, k: [ch.assert_zero(when * (w[j] - ((k >> (8 * j)) & 0xFF))) for j in range(4)]
+    a0s = f(SL_A0_0) + f(SL_A0_1) + f(SL_A0_2)
+    # eval_brk
+    mem(SL_IO, REG_BRK, f(SL_BRK), _m(SL_BRK))
+    _eval_gt_bytes(ch, SL_A0, SL_IO + 4 + ACC_VALUE, SL_GT, f(SL_BRK), _m(SL_BRK))
+    gt = f(SL_GT + 6)
+    for j in range(4):
+        ch.assert_zero(f(SL_BRK) * gt * (res[j] - a0[j]))
+    for j in range(4):
+        ch.assert_zero(f(SL_BRK) * (1 - gt) * (res[j] - io_prev[j]))
+    word_is(f(SL_BRK), out, 0)
+    # eval_clone
+    word_is(f(SL_CLONE), out, 0)
+    word_is(f(SL_CLONE), res, 1)
+    # eval_exit_group
+    word_is(f(SL_EXIT), out, 0)
+    # eval_fnctl
+    fc = f(SL_FCNTL)
+    ch.assert_zero(fc * f(SL_A1_1) * (a1[0] - 1))
+    ch.assert_zero(fc * f(SL_A1_3) * (a1[0] - 3))
+    for j in (1, 2, 3):
+        ch.assert_zero(fc * (f(SL_A1_1) + f(SL_A1_3)) * a1[j])
+    ch.assert_zero(f(SL_F_A1_3) * (f(SL_A1_3) * fc - 1))
+    ch.assert_zero(f(SL_F_A1_1) * (f(SL_A1_1) * fc - 1))
+    word_is(f(SL_F_A1_3) * f(SL_A0_0), res, 0)
+    word_is(f(SL_F_A1_3) * (f(SL_A0_1) + f(SL_A0_2)), res, 1)
+    word_is(f(SL_F_A1_3) * (1 - a0s), res, M32)
+    word_is(fc * (1 - (f(SL_A1_3) + f(SL_A1_1))), res, M32)
+    word_is((f(SL_F_A1_3) + f(SL_F_A1_1)) * a0s, out, 0)
+    word_is((f(SL_F_A1_3) + f(SL_F_A1_1)) * (1 - a0s), out, MIPS_EBADF)
+    word_is(fc * (1 - (f(SL_A1_3) + f(SL_A1_1))), out, MIPS_EBADF)
+    # eval_read
+    word_is(f(SL_READ) * f(SL_A0_0), res, 0)
+    word_is(f(SL_READ) * f(SL_A0_0), out, 0)
+    word_is(f(SL_READ) * (1 - f(SL_A0_0)), res, M32)
+    word_is(f(SL_READ) * (1 - f(SL_A0_0)), out, MIPS_EBADF)
+    # eval_write
+    mem(SL_IO, REG_A2, f(SL_WRITE), _m(SL_WRITE))
+    for j in range(4):
+        ch.assert_zero(f(SL_WRITE) * (res[j] - io_val[j]))
+    word_is(f(SL_WRITE), out, 0)
+    # eval_mmap
+    mm = f(SL_MMAP)
+    ch.assert_zero(mm * f(SL_OFF_0) * f(SL_PAGE_OFF))
+    ch.assert_zero(mm * (f(SL_PAGE_OFF) + f(SL_UPPER) - _reduce(SL_A1)))
+    size = f(SL_UPPER) + PAGE_SIZE * (1 - f(SL_OFF_0))
+    ch.assert_zero(mm * f(SL_A0_0) * (_reduce(SL_IO + 4 + ACC_VALUE) - (size + _reduce(SL_IO))))
+    ch.assert_zero(f(SL_MMAP_A0_0) * (mm * f(SL_A0_0) - 1))
+    for j in range(4):
+        ch.assert_zero(f(SL_MMAP_A0_0) * f(SL_A0_0) * (io_prev[j] - res[j]))
+    mem(SL_IO, REG_HEAP, f(SL_MMAP_A0_0), _m(SL_MMAP_A0_0))
+    for j in range(4):
+        ch.assert_zero(mm * (1 - f(SL_A0_0)) * (a0[j] - res[j]))
+    # eval_nop
+    word_is(f(SL_NOP), out, 0)
+    word_is(f(SL_NOP), res, 0)
+    # the A3 write
+    mem(SL_OUT, REG_A3, f(SL_REAL), _m(SL_REAL))
+    for c in (SL_A0_0, SL_A0_1, SL_A0_2, SL_MMAP, SL_MMAP2, SL_MMAP_A0_0, SL_OFF_0, SL_CLONE, SL_EXIT, SL_BRK,
+              SL_FCNTL, SL_A1_1, SL_A1_3, SL_F_A1_1, SL_F_A1_3, SL_READ, SL_WRITE, SL_NOP, SL_REAL):
+        _assert_bool(ch, f(c))
+    real = f(SL_REAL)
+    ch.assert_zero(real * f(SL_A0_0) * a0[0])
+    ch.assert_zero(real * f(SL_A0_1) * (a0[0] - 1))
+    ch.assert_zero(real * f(SL_A0_2) * (a0[0] - 2))
+    for j in (1, 2, 3):
+        ch.assert_zero(real * a0s * a0[j])
+    sid = f(SL_ID)
+    ch.assert_zero(mm * (1 - f(SL_MMAP2)) * (sid - SYS_MMAP))
+    ch.assert_zero(f(SL_MMAP2) * (sid - SYS_MMAP2))
+    ch.assert_zero(f(SL_MMAP2) * (mm - 1))
+    for col, code in ((SL_CLONE, SYS_CLONE), (SL_EXIT, SYS_EXT_GROUP), (SL_BRK, SYS_BRK), (SL_FCNTL, SYS_FCNTL),
+                      (SL_READ, SYS_READ), (SL_WRITE, SYS_WRITE)):
+        ch.assert_zero(f(col) * (sid - code))
+    kinds = [f(c) for c in (SL_CLONE, SL_EXIT, SL_BRK, SL_FCNTL, SL_READ, SL_WRITE, SL_NOP)]
+    ch.assert_zero(real * (sum(kinds, mm) - 1))
+    ch.receives.append(Lookup([_m(SL_SHARD), _m(SL_CLK), _m(SL_ID), _reduce_v(SL_A0), _reduce_v(SL_A1)],
+                              _m(SL_REAL), KIND_SYSCALL))
+    return ch
+
+
+def sys_linux_trace(events, byte_lookup) -> np.ndarray:
+    """SysLinuxChip::event_to_row (sys_linux/trace.rs:106-167), one row per Linux syscall."""
+    from .mips_core import ACC_VALUE, _access_cols
+    n = len(events)
+    t = np.zeros((max(16, 1 << max(0, (n - 1).bit_length())), SL_WIDTH), np.uint32)
+    for k, e in enumerate(events):
+        code, a0, a1 = e["code"], e["a0"], e["a1"]
+        r = np.asarray([k])
+        row = t[k]
+        row[SL_SHARD], row[SL_CLK], row[SL_ID], row[SL_REAL] = e["shard"], e["clk"], code, 1
+        row[SL_A0:SL_A0 + 4] = A._bytes(np.asarray([a0], np.uint32))[0]
+        row[SL_A1:SL_A1 + 4] = A._bytes(np.asarray([a1], np.uint32))[0]
+        row[SL_RES:SL_RES + 4] = A._bytes(np.asarray([e["v0"]], np.uint32))[0]
+        row[SL_A0_0], row[SL_A0_1], row[SL_A0_2] = a0 == 0, a0 == 1, a0 == 2
+        shard, clk = np.asarray([e["shard"]]), np.asarray([e["clk"]])
+        one = np.ones(1, bool)
+
+        def write(acc, rec):
+            prev, val, ps, pc_ = rec
+            t[k, acc:acc + 4] = A._bytes(np.asarray([prev], np.uint32))[0]
+            _access_cols(t, r, acc + 4 + ACC_VALUE, np.asarray([val], np.uint32), np.asarray([[ps, pc_]]), shard, clk,
+                         one, byte_lookup)
+
+        def read(acc, rec):
+            write(acc, (rec[0], rec[0], rec[1], rec[2]))
+
+        write(SL_OUT, e["writes"][0])
+        if code == SYS_BRK:
+            row[SL_BRK] = 1
+            brk = e["reads"][0][0]
+            ab, bb = [(a0 >> (8 * j)) & 0xFF for j in range(4)], [(brk >> (8 * j)) & 0xFF for j in range(4)]
+            res, ac, bc = 0, 0, 0
+            for j in range(3, -1, -1):  # GtColsBytes::populate: the most significant differing byte
+                if ab[j] != bb[j]:
+                    row[SL_GT + j] = 1
+                    ac, bc, res = ab[j], bb[j], int(ab[j] > bb[j])
+                    break
+            row[SL_GT + 4], row[SL_GT + 5], row[SL_GT + 6] = ac, bc, res
+            byte_lookup(A.B_LTU, np.asarray([bc]), np.asarray([ac]))
+            _u8_pairs_lookup([np.asarray([ab]), np.asarray([bb])], byte_lookup)
+            read(SL_IO, e["reads"][0])
+        elif code == SYS_CLONE:
+            row[SL_CLONE] = 1
+        elif code == SYS_EXT_GROUP:
+            row[SL_EXIT] = 1
+        elif code == SYS_FCNTL:
+            row[SL_FCNTL] = 1
+            row[SL_A1_1], row[SL_A1_3] = a1 == 1, a1 == 3
+            row[SL_F_A1_1], row[SL_F_A1_3] = a1 == 1, a1 == 3
+        elif code in (SYS_MMAP, SYS_MMAP2):
+            row[SL_MMAP], row[SL_MMAP2], row[SL_MMAP_A0_0] = 1, code == SYS_MMAP2, a0 == 0
+            row[SL_PAGE_OFF], row[SL_OFF_0], row[SL_UPPER] = a1 & 0xFFF, (a1 & 0xFFF) == 0, (a1 >> 12) << 12
+            if a0 == 0:
+                write(SL_IO, e["writes"][1])
+        elif code == SYS_READ:
+            row[SL_READ] = 1
+        elif code == SYS_WRITE:
+            read(SL_IO, e["reads"][0])
+            row[SL_WRITE] = 1
+        else:
+            row[SL_NOP] = 1
+    return t
+
+
 # ---------------------------------------------------------------- execution of the precompiles
 class PrecompileMemory:
     """The memory view of one syscall (SyscallContext::mr / mw, context.rs:63-100): every access at
     (shard, clk) updates the shared memory image; the first access to a word closes the CPU's open
     MemoryLocal entry for it and opens the syscall's own (initial = the previous record, final = the last)."""
 
-    def __init__(self, mem, mem_init, mem_last, cpu_first, cpu_done, shard, init_word):
+    def __init__(self, mem, mem_init, mem_last, cpu_first, cpu_done, shard, init_word, regs=None, last=None,
+                 reg_start=None, reg_done=None):
         self.mem, self.mem_init, self.mem_last = mem, mem_init, mem_last
         self.cpu_first, self.cpu_done = cpu_first, cpu_done
         self.shard, self.init_word = shard, init_word
+        self.regs, self.last, self.reg_start, self.reg_done = regs, last, reg_start, reg_done
         self.local = {}
+        self.reg_local = {}
+
+    def _touch_reg(self, r):
+        if self.last[r] != self.reg_start[r][0]:  # the CPU's open entry for r ends here
+            s0, v0 = self.reg_start[r]
+            self.reg_done.append((r, *s0, v0, *self.last[r], self.regs[r]))
+        if r not in self.reg_local:
+            self.reg_local[r] = (*self.last[r], self.regs[r])
+
+    def reg_read(self, r, clk):
+        """rr_traced (context.rs:102-111) -> (value, prev_shard, prev_clk)"""
+        self._touch_reg(r)
+        ps, pc_ = self.last[r]
+        self.last[r] = (self.shard, clk)
+        self.reg_start[r] = (self.last[r], self.regs[r])
+        return self.regs[r], ps, pc_
+
+    def reg_write(self, r, value, clk):
+        """rw_traced (context.rs:113-123) -> (prev_value, value, prev_shard, prev_clk)"""
+        self._touch_reg(r)
+        ps, pc_ = self.last[r]
+        prev = self.regs[r]
+        self.regs[r] = value & M32
+        self.last[r] = (self.shard, clk)
+        self.reg_start[r] = (self.last[r], self.regs[r])
+        return prev, value & M32, ps, pc_
 
     def _touch(self, addr):
         if addr not in self.mem:
@@ -872,7 +1097,8 @@ class PrecompileMemory:
 
     def local_entries(self):
         """The syscall's MemoryLocal entries (addr, initial shard/clk/value, final shard/clk/value)."""
-        return [(a, s, c, v, *self.mem_last[a], self.mem[a]) for a, (s, c, v) in self.local.items()]
+        ent = [(r, s, c, v, *self.last[r], self.regs[r]) for r, (s, c, v) in self.reg_local.items()]
+        return ent + [(a, s, c, v, *self.mem_last[a], self.mem[a]) for a, (s, c, v) in self.local.items()]
 
 
 def _rotr(x, s):
@@ -922,6 +1148,56 @@ def exec_sha_compress(pm: PrecompileMemory, shard: int, clk: int, w_ptr: int, h_
     ev["hw"] = [pm.write(h_ptr + 4 * i, hx[i] + v[i], clk + 1) for i in range(8)]
     ev["local"] = pm.local_entries()
     return ev
+
+
+def exec_sys_linux(pm: PrecompileMemory, shard: int, clk: int, code: int, a0: int, a1: int):
+    """The Linux syscalls (executor/src/syscalls/precompiles/sys_linux/*.rs): returns (value for V0 or None,
+    LinuxEvent as a dict: read records (value, prev_shard, prev_clk), write records (prev, value, prev_shard,
+    prev_clk))."""
+    reads, writes, ret = [], [], 0
+    if code == SYS_BRK:  # sysbrk.rs
+        rec = pm.reg_read(REG_BRK, clk)
+        reads.append(rec)
+        ret = a0 if a0 > rec[0] else rec[0]
+        writes.append(pm.reg_write(REG_A3, 0, clk))
+    elif code in (SYS_MMAP, SYS_MMAP2):  # sysmmap.rs
+        size = a1
+        if size & (PAGE_SIZE - 1):
+            size = (size + PAGE_SIZE - (size & (PAGE_SIZE - 1))) & M32
+        writes.append(pm.reg_write(REG_A3, 0, clk))
+        if a0 == 0:
+            ret = pm.regs[REG_HEAP]
+            writes.append(pm.reg_write(REG_HEAP, ret + size, clk))
+        else:
+            ret = a0
+    elif code == SYS_CLONE:
+        ret = 1
+        writes.append(pm.reg_write(REG_A3, 0, clk))
+    elif code == SYS_EXT_GROUP:
+        ret = None
+        writes.append(pm.reg_write(REG_A3, 0, clk))
+    elif code == SYS_FCNTL:  # sysfcntl.rs
+        if a1 == 3 and a0 in (0, 1, 2):
+            ret, err = (0 if a0 == 0 else 1), 0
+        elif a1 == 1 and a0 in (0, 1, 2):
+            ret, err = a0, 0
+        else:
+            ret, err = M32, MIPS_EBADF
+        writes.append(pm.reg_write(REG_A3, err, clk))
+    elif code == SYS_READ:  # sysread.rs: only stdin
+        ret, err = (0, 0) if a0 == 0 else (M32, MIPS_EBADF)
+        writes.append(pm.reg_write(REG_A3, err, clk))
+    elif code == SYS_WRITE:  # syswrite.rs: returns A2 (the byte count); the bytes go to the host fd
+        rec = pm.reg_read(REG_A2, clk)
+        reads.append(rec)
+        ret = rec[0]
+        writes.append(pm.reg_write(REG_A3, 0, clk))
+    else:  # sysnop.rs
+        ret = 0
+        writes.append(pm.reg_write(REG_A3, 0, clk))
+    ev = {"shard": shard, "clk": clk, "a0": a0, "a1": a1, "v0": 0 if ret is None else ret, "code": code,
+          "reads": reads, "writes": writes, "local": pm.local_entries()}
+    return ret, ev
 
 
 def sha256_extend_ref(w16):
