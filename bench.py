@@ -203,6 +203,9 @@ def make_shard(workload, n, seed):
     if workload == "core":
         from zkmips_amd import mips_core as MC
         return MC.loop_shard(60, (3 * n // 4) // 104, seed=1)  # ~98 instructions per iteration
+    if workload == "maxshape":  # the reference's 2^22 maximal shape, scaled to 2^log_n Cpu rows
+        from zkmips_amd import shapes as SH
+        return SH.shape_shard(SH.MAXIMAL_22, seed=1, down=22 - (n.bit_length() - 1))
     if workload == "alu":
         from zkmips_amd import mips_alu as A
         return A.alu_shard(n // 4, n // 4, seed=seed, n_lt=n // 4, n_sll=n // 8, n_sr=n // 16, n_clz=n // 16)
@@ -226,12 +229,13 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--log-n", type=int, default=22)
-    ap.add_argument("--workload", choices=["fib", "alu", "core"], default="fib",
+    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape"], default="fib",
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
                          "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
                          "zkmips_amd/mips_alu.py), 2^(log-n) "
                          "instructions per shard; core: Cpu + Program + Mul + DivRem + Branch + Jump + MovCond + MemoryInstrs + MiscInstrs chips over the ALU slice "
-                         "(zkmips_amd/mips_core.py) running a counted loop, Cpu 2^(log-n) rows")
+                         "(zkmips_amd/mips_core.py) running a counted loop, Cpu 2^(log-n) rows; maxshape: a MIPS shard "
+                         "padded to the reference's maximal_shapes.json[\"22\"][2] (zkmips_amd/shapes.py)")
     ap.add_argument("--queries", type=int, default=84)
     ap.add_argument("--cpu-log-n", type=int, default=18)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -272,8 +276,8 @@ def main():
     K = max(1, args.inflight)
     shards = []
     core = None
-    if args.workload == "core":  # one program (one proving key); its trace is generated once and proven K times
-        core = make_shard("core", n, 1)
+    if args.workload in ("core", "maxshape"):  # one program (one proving key), generated once, proven K times
+        core = make_shard(args.workload, n, 1)
     for k in range(K):
         m, prep, traces_k, pvs_k = core if core is not None else make_shard(args.workload, n, 1000 + rank * K + k)
         pinned = {}
@@ -408,7 +412,7 @@ def main():
     pageable_s = time.perf_counter() - tp
 
     # HBM bytes per kernel of one shard proof, measured on this box now (rank 0, N = 1 only)
-    pmc = None if (args.no_pmc or world > 1) else pmc_in_run(args)
+    pmc = None if (args.no_pmc or world > 1 or args.workload == "maxshape") else pmc_in_run(args)
     kernel_stages = ["lde", "merkle_leaves", "merkle_nodes", "quotient", "perm_trace", "open_eval", "fri_reduce"]
     dom = max((s for s in kernel_stages if s in prof), key=lambda s: prof[s][1])
     cnt, ms, units = prof[dom]
@@ -479,6 +483,11 @@ def main():
                     f"LogUp 11 EF) + Program (prep 14) + DivRem, AddSub, Bitwise, Mul, Lt, ShiftLeft, ShiftRight, CloClz, MovCond, MemoryInstrs, MiscInstrs, "
                     f"Branch, Jump, MemoryLocal, Global (septic-curve digest) + Byte 2^16 (prep 12): full commit+open per shard")
                    if args.workload == "core" else
+                   (f"MIPS shard in the reference maximal shape maximal_shapes.json[\"22\"][2] scaled to Cpu 2^{args.log_n}: "
+                    + ", ".join(f"{k} 2^{int(np.log2(len(traces[k])))}" for k in sorted(traces, key=lambda c: -len(traces[c])))
+                    + f"; {int(traces['Cpu'][:, 65].sum())} instructions (loop of ALU, load/store, branch, conditional-move "
+                      f"ops, HALT): full commit+open per shard")
+                   if args.workload == "maxshape" else
                    (f"MIPS ALU slice: InstrSource 2^{args.log_n} + AddSub, Bitwise, Lt 2^{args.log_n - 2} + ShiftLeft, "
                     f"ShiftRight (CPU + CloClz SRLs) 2^{args.log_n - 3} + CloClz 2^{args.log_n - 4} + Byte 2^16 "
                     f"(prep 12): full commit+open per shard"),
