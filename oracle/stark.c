@@ -11,9 +11,20 @@
  * verifier restatement crates/recursion/circuit/src/fri.rs:34-405 (not vendored: Plonky3 fork
  * ProjectZKM/Plonky3@faa24ca4597eebeecbf71b194b71c7d1a99b3f01).
  */
+#include <omp.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include "stark.h"
+
+/* ORC_TIMING=1: per-phase wall times of orc_prove_shard on stderr (profiling the CPU baseline) */
+static double t_last;
+static void phase(const char *name) {
+    static int on = -1;
+    if (on < 0) on = getenv("ORC_TIMING") != NULL;
+    const double t = omp_get_wtime();
+    if (on && name) fprintf(stderr, "orc %-14s %8.3f s\n", name, t - t_last);
+    t_last = t;
+}
 
 /* ---------------- constraint evaluators (base = prover, ext = verifier) ---------------- */
 static inline ef_t ef_mul_kb(ef_t a, kb_t b) { return ef_mul_base(a, b); }
@@ -226,6 +237,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
     const orc_machine_t *m = pk->m;
     const int lb = pk->cfg.log_blowup;
     memset(out, 0, sizeof *out);
+    phase(NULL);
     /* ---- commit (prover.rs:258-292): sort by (height desc, name) ---- */
     ord_t *o = (ord_t *)malloc(sizeof(ord_t) * n);
     for (int i = 0; i < n; i++) { o[i].idx = i; o[i].h = heights[i]; o[i].name = m->chips[chip_idx[i]].name; }
@@ -245,6 +257,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
         main_mats[i].height = hs[i] << lb;
         main_mats[i].width = chips[i]->main_width;
     }
+    phase("main_lde");
     orc_tree_t main_tree;
     orc_tree_build(&main_tree, main_mats, n, 1);
     out->main_commit = orc_tree_root(&main_tree);
@@ -255,6 +268,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
     out->pv = (kb_t *)malloc(sizeof(kb_t) * (npv + 1));
     memcpy(out->pv, pv, sizeof(kb_t) * npv);
 
+    phase("main_commit");
     /* ---- open (prover.rs:298-653) ---- */
     orc_chal_observe_slice(ch, pv, m->num_pv);
     orc_chal_observe_digest(ch, out->main_commit);
@@ -288,6 +302,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
         perm_mats[i].width = 4 * pw;
         out->chips[i].log_degree = log2_exact(hs[i]);
     }
+    phase("perm_trace_lde");
     orc_tree_t perm_tree;
     orc_tree_build(&perm_tree, perm_mats, n, 1);
     out->perm_commit = orc_tree_root(&perm_tree);
@@ -298,6 +313,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
     }
     ef_t alpha = orc_chal_sample_ef(ch);
 
+    phase("perm");
     /* ---- quotient values (quotient.rs) + split/commit (prover.rs:476-498) ---- */
     int nchunks = 0;
     for (int i = 0; i < n; i++) nchunks += 1 << chips[i]->log_qd;
@@ -378,6 +394,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
     orc_chal_observe_digest(ch, out->quot_commit);
     ef_t zeta = orc_chal_sample_ef(ch);
 
+    phase("quotient");
     /* ---- opening points (prover.rs:503-544) and values ---- */
     orc_tree_t *trees[4] = {(orc_tree_t *)&pk->tree, &main_tree, &perm_tree, &q_tree};
     int nreq = pk->ntraces + 2 * n + nchunks;
@@ -405,6 +422,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
         }
     }
 
+    phase("open_values");
     /* ---- TwoAdicFriPcs::open: alpha, reduced openings (fri.rs:71-215 semantics) ---- */
     ef_t fri_alpha = orc_chal_sample_ef(ch);
     int log_max = 0;
@@ -448,6 +466,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
     }
     free(apow);
 
+    phase("fri_reduce");
     /* ---- FRI commit phase (fri.rs:34-69, 247-361 semantics) ---- */
     orc_fri_t *fri = &out->fri;
     int nrounds = log_max - lb;
@@ -492,6 +511,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
     orc_chal_observe_ef(ch, fri->final_poly);
     fri->pow_witness = orc_chal_grind(ch, pk->cfg.pow_bits);
 
+    phase("fri_commit");
     /* ---- queries ---- */
     fri->nqueries = pk->cfg.num_queries;
     fri->queries = (orc_query_t *)calloc(fri->nqueries, sizeof(orc_query_t));
@@ -531,6 +551,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
         }
     }
 
+    phase("queries");
     /* ---- opened values (prover.rs:558-640) ---- */
     r = 0;
     for (int i = 0; i < n; i++) {
