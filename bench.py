@@ -182,7 +182,8 @@ def host_info():
 
 
 def cpu_baseline(log_n, queries):
-    """The CPU oracle (a C/OpenMP restatement, not the reference binary) on one bounded shard."""
+    """The CPU oracle (a C/OpenMP restatement, not the reference binary; AVX-512 Poseidon2 and LDE, batch
+    inversions, oracle/p2x16.c, oracle/lde_x16.c) on one shard of the headline size."""
     from tests import _oracle as O
     from zkmips_amd import workloads as W
     n = 1 << log_n
@@ -195,7 +196,7 @@ def cpu_baseline(log_n, queries):
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": n / dt, "unit": "rows/s", "cores": cores, "kind": "port", "host": host_info(),
             "sample": f"one S-SHARD FibCpu 2^{log_n}-row shard (+FibTable), full commit+open, {queries} queries, "
-                      f"{dt:.2f} s wall on {cores} OpenMP threads"}
+                      f"{dt:.2f} s wall on {cores} OpenMP threads (AVX-512 Poseidon2/LDE)"}
 
 
 def make_shard(workload, n, seed):
@@ -210,6 +211,80 @@ def make_shard(workload, n, seed):
         from zkmips_amd import mips_alu as A
         return A.alu_shard(n // 4, n // 4, seed=seed, n_lt=n // 4, n_sll=n // 8, n_sr=n // 16, n_clz=n // 16)
     return W.fib_shard(n, seed=seed)
+
+
+def execution_bench(args):
+    """BASELINE config 3: a whole sha2-precompile-shaped execution proven shard by shard on one GPU.
+    The guest (mips_core.sha_program) hashes `--sha-blocks` 64-byte blocks with SHA_EXTEND + SHA_COMPRESS,
+    COMMITs and HALTs; the execution splits into CPU shards of 2^log_n-ish rows, SHA_EXTEND and
+    SHA_COMPRESS precompile shards and the memory shard.  Every step proves all of them (traces resident
+    in HBM, `--inflight` shards concurrently); the machine-level global sum of the proofs is checked."""
+    import threading
+    import torch
+    from zkmips_amd import mips_core as MC
+    from zkmips_amd._lib import Device
+    from zkmips_amd.proof import machine_global_sum_is_zero
+    from zkmips_amd.prover import HipProver
+    t0 = time.time()
+    max_steps = min((1 << args.log_n) * 4 // 5, (1 << 24) // 5 - 1)
+    run = MC.program_shards(MC.sha_program(args.sha_blocks, seed=1), seed=1, shard_size=max_steps,
+                            precompile_events_per_shard=args.sha_events_per_shard)
+    gen_s = time.time() - t0
+    print(f"sha2: {len(run)} shards generated in {gen_s:.1f} s", file=sys.stderr, flush=True)
+    torch.cuda.set_device(0)
+    m, prep, _, _ = run[0]
+    prep = {k: v for k, v in prep.items() if v is not None}
+    prover = HipProver(Device(0), m, prep, num_queries=args.queries)
+    dev = [({k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in tr.items()}, pv) for _, _, tr, pv in run]
+    rows = [max(v.shape[0] for v in tr.values()) for _, _, tr, _ in run]
+    kinds = ["cpu" if "Cpu" in tr else "memory" if "MemoryGlobalInit" in tr else
+             "sha_extend" if "ShaExtend" in tr else "sha_compress" for _, _, tr, _ in run]
+    torch.cuda.synchronize()
+
+    def prove_all():
+        out = [None] * len(run)
+        nxt = [0]
+        lock = threading.Lock()
+
+        def worker():
+            while True:
+                with lock:
+                    i = nxt[0]
+                    nxt[0] += 1
+                if i >= len(run):
+                    return
+                out[i] = prove_resident(prover, dev[i][0], dev[i][1])
+        th = [threading.Thread(target=worker) for _ in range(max(1, args.inflight))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return out
+
+    for _ in range(max(1, args.warmup)):
+        proofs = prove_all()
+        print("sha2: warmup execution proven", file=sys.stderr, flush=True)
+    assert machine_global_sum_is_zero(proofs), "the execution's global cumulative sums do not add to zero"
+    torch.cuda.synchronize()
+    t1 = time.time()
+    for _ in range(args.steps):
+        prove_all()
+    torch.cuda.synchronize()
+    el = time.time() - t1
+    line = {
+        "metric": "shard trace rows proved/sec (whole sha2-precompile execution, BASELINE config 3)",
+        "value": round(sum(rows) * args.steps / el, 1), "unit": "rows/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
+        "data": "synthetic sha2 guest (mips_core.sha_program), traces resident in HBM",
+        "config": {"workload": f"sha2-precompile execution: {args.sha_blocks} blocks, {len(run)} shards "
+                               f"({', '.join(f'{k} 2^{r.bit_length() - 1}' for k, r in zip(kinds, rows))}), "
+                               f"all MIPS + syscall + SHA-256 + memory chips, full commit+open per shard",
+                   "shards": len(run), "rows_per_execution": sum(rows), "fri_queries": args.queries,
+                   "proof_bytes": sum(len(p) for p in proofs), "parallelism": f"{args.inflight} shards in flight",
+                   "trace_generation_s": round(gen_s, 1), "global_sum_checked": True},
+    }
+    print(json.dumps(line), flush=True)
 
 
 def pmc_child(args):
@@ -229,7 +304,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--log-n", type=int, default=22)
-    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape"], default="fib",
+    ap.add_argument("--sha-blocks", type=int, default=16384, help="sha2 workload: 64-byte blocks hashed")
+    ap.add_argument("--sha-events-per-shard", type=int, default=16384,
+                    help="sha2 workload: precompile calls per precompile shard")
+    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2"], default="fib",
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
                          "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
                          "zkmips_amd/mips_alu.py), 2^(log-n) "
@@ -237,7 +315,7 @@ def main():
                          "(zkmips_amd/mips_core.py) running a counted loop, Cpu 2^(log-n) rows; maxshape: a MIPS shard "
                          "padded to the reference's maximal_shapes.json[\"22\"][2] (zkmips_amd/shapes.py)")
     ap.add_argument("--queries", type=int, default=84)
-    ap.add_argument("--cpu-log-n", type=int, default=18)
+    ap.add_argument("--cpu-log-n", type=int, default=22)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 HBM counter passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -249,6 +327,8 @@ def main():
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
+    if args.workload == "sha2":
+        return execution_bench(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

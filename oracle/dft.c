@@ -11,6 +11,7 @@
  * textbook iterative radix-2 (bit-reverse + DIT), one column at a time.
  */
 #include <stdlib.h>
+#include <string.h>
 #include "oracle_internal.h"
 
 void orc_dft_natural(kb_t *a, int logn, int inverse) {
@@ -47,22 +48,73 @@ void orc_interpolate_col(const kb_t *m, size_t h, size_t w, size_t col, kb_t *co
     orc_dft_natural(coeffs, log2_exact(h), 1);
 }
 
+/* w_n^j (or w_n^-j), j < n/2, for n = 2^logn: built once per (logn, direction) and kept */
+static kb_t *tw_cache[2][32];
+static const kb_t *twiddles(int logn, int inverse) {
+    kb_t *t = __atomic_load_n(&tw_cache[inverse][logn], __ATOMIC_ACQUIRE);
+    if (t) return t;
+    size_t h = ((size_t)1 << logn) >> 1;
+    t = (kb_t *)malloc(sizeof(kb_t) * (h ? h : 1));
+    kb_t w = kb_two_adic_gen(logn);
+    if (inverse) w = kb_inv(w);
+    kb_t x = 1;
+    for (size_t j = 0; j < h; j++) { t[j] = x; x = kb_mul(x, w); }
+    kb_t *expect = NULL;
+    if (!__atomic_compare_exchange_n(&tw_cache[inverse][logn], &expect, t, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+        free(t);
+        t = expect;
+    }
+    return t;
+}
+
+/* decimation-in-frequency radix-2 transform: natural-order input, bit-reversed output */
+static void dif(kb_t *a, int logn, const kb_t *tw) {
+    size_t n = (size_t)1 << logn;
+    for (int s = logn; s >= 1; s--) {
+        size_t m = (size_t)1 << s, h = m >> 1, stride = n >> s;
+        for (size_t k = 0; k < n; k += m)
+            for (size_t j = 0; j < h; j++) {
+                kb_t u = a[k + j], v = a[k + j + h];
+                a[k + j] = kb_add(u, v);
+                a[k + j + h] = kb_mul(kb_sub(u, v), tw[j * stride]);
+            }
+    }
+}
+
 /* evals: h x w row-major, treated as evaluations over H_h (natural order).
- * out: (h << log_blowup) x w row-major, bit-reversed rows, row i = p(shift * w^{rev(i)}). */
+ * out: (h << log_blowup) x w row-major, bit-reversed rows, row i = p(shift * w^{rev(i)}).
+ * Per column: inverse DIF (coefficients, bit-reversed), reorder and scale by shift^i / h, zero-extend,
+ * forward DIF, whose bit-reversed output is already the committed row order.  Columns go in groups
+ * of 8 so the row-major gather and scatter touch whole cache lines. */
+#define LDE_G 8
 void orc_coset_lde_bitrev(const kb_t *evals, size_t h, size_t w, int log_blowup, kb_t shift, kb_t *out) {
     int logh = log2_exact(h);
     int logH = logh + log_blowup;
     size_t H = (size_t)1 << logH;
+    if (h >= 16 && orc_p2x16_available()) {  /* 16 columns per AVX-512 block (lde_x16.c) */
+        orc_coset_lde_bitrev_x16(evals, h, w, log_blowup, shift, out);
+        return;
+    }
+    const kb_t *twi = twiddles(logh, 1), *twf = twiddles(logH, 0);
+    const kb_t hinv = kb_inv((kb_t)(h % KB_P));
 #pragma omp parallel for schedule(dynamic, 1)
-    for (size_t c = 0; c < w; c++) {
-        kb_t *buf = (kb_t *)calloc(H, sizeof(kb_t));
-        for (size_t i = 0; i < h; i++) buf[i] = evals[i * w + c];
-        orc_dft_natural(buf, logh, 1);
-        kb_t s = 1;
-        for (size_t i = 0; i < h; i++) { buf[i] = kb_mul(buf[i], s); s = kb_mul(s, shift); }
-        orc_dft_natural(buf, logH, 0);
-        for (size_t i = 0; i < H; i++) out[i * w + c] = buf[rev_bits((uint32_t)i, logH)];
+    for (size_t c0 = 0; c0 < w; c0 += LDE_G) {
+        const size_t g = w - c0 < LDE_G ? w - c0 : LDE_G;
+        kb_t *buf = (kb_t *)malloc(sizeof(kb_t) * h * g), *ext = (kb_t *)malloc(sizeof(kb_t) * H * g);
+        for (size_t i = 0; i < h; i++)
+            for (size_t k = 0; k < g; k++) buf[k * h + i] = evals[i * w + c0 + k];
+        for (size_t k = 0; k < g; k++) {
+            kb_t *b = buf + k * h, *e = ext + k * H;
+            dif(b, logh, twi);
+            kb_t s = hinv;
+            for (size_t i = 0; i < h; i++) { e[i] = kb_mul(b[rev_bits((uint32_t)i, logh)], s); s = kb_mul(s, shift); }
+            memset(e + h, 0, sizeof(kb_t) * (H - h));
+            dif(e, logH, twf);
+        }
+        for (size_t i = 0; i < H; i++)
+            for (size_t k = 0; k < g; k++) out[i * w + c0 + k] = ext[k * H + i];
         free(buf);
+        free(ext);
     }
 }
 

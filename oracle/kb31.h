@@ -55,17 +55,15 @@ static inline ef_t ef_add_base(ef_t a, kb_t b) { a.c[0] = kb_add(a.c[0], b); ret
 static inline ef_t ef_mul_base(ef_t a, kb_t b) { for (int i = 0; i < 4; i++) a.c[i] = kb_mul(a.c[i], b); return a; }
 
 static inline ef_t ef_mul(ef_t a, ef_t b) {
-    /* schoolbook product, then fold X^4 = W */
-    uint64_t t[7] = {0};
-    for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++)
-            t[i + j] = (t[i + j] + (uint64_t)a.c[i] * b.c[j]) % KB_P;
+    /* schoolbook product folded with X^4 = W; products < 2^62, so up to four share one reduction */
+    const uint64_t a0 = a.c[0], a1 = a.c[1], a2 = a.c[2], a3 = a.c[3];
+    const uint64_t b0 = b.c[0], b1 = b.c[1], b2 = b.c[2], b3 = b.c[3];
+    const uint64_t h0 = (a1 * b3 + a2 * b2 + a3 * b1) % KB_P, h1 = (a2 * b3 + a3 * b2) % KB_P, h2 = (a3 * b3) % KB_P;
     ef_t r;
-    for (int i = 0; i < 4; i++) {
-        uint64_t v = t[i];
-        if (i + 4 < 7) v += (uint64_t)KB_W * t[i + 4];
-        r.c[i] = (kb_t)(v % KB_P);
-    }
+    r.c[0] = (kb_t)((a0 * b0 + KB_W * h0) % KB_P);
+    r.c[1] = (kb_t)((a0 * b1 + a1 * b0 + KB_W * h1) % KB_P);
+    r.c[2] = (kb_t)((a0 * b2 + a1 * b1 + a2 * b0 + KB_W * h2) % KB_P);
+    r.c[3] = (kb_t)((a0 * b3 + a1 * b2 + a2 * b1 + a3 * b0) % KB_P);
     return r;
 }
 static inline ef_t ef_square(ef_t a) { return ef_mul(a, a); }
@@ -79,7 +77,8 @@ static inline ef_t ef_pow(ef_t a, uint64_t e) {
  * r = 1 + p + p^2 + p^3.  Frobenius on F[X]/(X^4-W): X^p = W^((p-1)/4) X. */
 static inline ef_t ef_frobenius(ef_t a) {
     /* X^{p} = z X with z = W^((p-1)/4) */
-    kb_t z = kb_pow(KB_W, (KB_P - 1) / 4);
+    static kb_t z;
+    if (!z) z = kb_pow(KB_W, (KB_P - 1) / 4);
     ef_t r;
     kb_t zi = 1;
     for (int i = 0; i < 4; i++) { r.c[i] = kb_mul(a.c[i], zi); zi = kb_mul(zi, z); }

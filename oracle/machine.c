@@ -55,6 +55,7 @@ int orc_machine_parse(orc_machine_t *m, const uint32_t *w, size_t n) {
             all[i].kind = rd(&r);
             all[i].scope = rd(&r);
             all[i].nvalues = (int)rd(&r);
+            if (all[i].nvalues > 255) return -4; /* the LogUp evaluators keep beta^1..beta^256 */
             all[i].values = (orc_vpc_t *)calloc(all[i].nvalues + 1, sizeof(orc_vpc_t));
             for (int v = 0; v < all[i].nvalues; v++) parse_vpc(&r, &all[i].values[v]);
             parse_vpc(&r, &all[i].mult);

@@ -45,8 +45,14 @@ void orc_tree_build(orc_tree_t *t, orc_mat_t *mats, int nmats, int owns) {
     while (pos < nmats && mats[order[pos]].height == maxh) pos++;
     g0 = pos;
     t->layers[0] = (digest_t *)malloc(sizeof(digest_t) * maxh);
+    const int x16 = orc_p2x16_available();
+    if (x16 && maxh >= 16) {
 #pragma omp parallel for schedule(static)
-    for (size_t r = 0; r < maxh; r++) hash_rows(mats, order, g0, r, &t->layers[0][r]);
+        for (size_t r = 0; r < maxh; r += 16) orc_p2x16_hash_rows(mats, order, g0, r, &t->layers[0][r]);
+    } else {
+#pragma omp parallel for schedule(static)
+        for (size_t r = 0; r < maxh; r++) hash_rows(mats, order, g0, r, &t->layers[0][r]);
+    }
     size_t h = maxh;
     for (int L = 1; L < t->nlayers; L++) {
         h >>= 1;
@@ -55,6 +61,19 @@ void orc_tree_build(orc_tree_t *t, orc_mat_t *mats, int nmats, int owns) {
         int ng = pos - gstart;
         digest_t *prev = t->layers[L - 1];
         digest_t *cur = (digest_t *)malloc(sizeof(digest_t) * h);
+        if (x16 && h >= 16) {  /* 16 nodes per AVX-512 batch (p2x16.c) */
+#pragma omp parallel for schedule(static)
+            for (size_t i = 0; i < h; i += 16) {
+                orc_p2x16_compress_pairs(prev + 2 * i, cur + i);
+                if (ng) {
+                    digest_t rd[16];
+                    orc_p2x16_hash_rows(mats, order + gstart, ng, i, rd);
+                    orc_p2x16_compress2(cur + i, rd, cur + i);
+                }
+            }
+            t->layers[L] = cur;
+            continue;
+        }
 #pragma omp parallel for schedule(static)
         for (size_t i = 0; i < h; i++) {
             digest_t d = orc_p2_compress(prev[2 * i], prev[2 * i + 1]);

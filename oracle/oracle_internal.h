@@ -14,6 +14,7 @@
 void orc_dft_natural(kb_t *a, int logn, int inverse);
 void orc_interpolate_col(const kb_t *m, size_t h, size_t w, size_t col, kb_t *coeffs);
 void orc_coset_lde_bitrev(const kb_t *evals, size_t h, size_t w, int log_blowup, kb_t shift, kb_t *out);
+void orc_coset_lde_bitrev_x16(const kb_t *evals, size_t h, size_t w, int log_blowup, kb_t shift, kb_t *out);
 ef_t orc_eval_coeffs_ef(const kb_t *coeffs, size_t n, ef_t z);
 
 /* ----------------------------------------------------------------- mmcs.c */
@@ -32,6 +33,11 @@ typedef struct {
 } orc_tree_t;
 
 void orc_tree_build(orc_tree_t *t, orc_mat_t *mats, int nmats, int owns);
+/* p2x16.c: 16 Poseidon2 states per AVX-512 batch (same digests as poseidon2.c) */
+int orc_p2x16_available(void);
+void orc_p2x16_hash_rows(const orc_mat_t *mats, const int *group, int ng, size_t row0, digest_t *out);
+void orc_p2x16_compress_pairs(const digest_t *in, digest_t *out);
+void orc_p2x16_compress2(const digest_t *a, const digest_t *b, digest_t *out);
 void orc_tree_free(orc_tree_t *t);
 digest_t orc_tree_root(const orc_tree_t *t);
 /* rows: per matrix, pointer into the matrix (no copy); path: log_max_height digests */

@@ -125,13 +125,26 @@ static void open_matrix_at(const orc_mat_t *lde, int log_blowup, ef_t z, ef_t *o
 #pragma omp parallel for schedule(static)
     for (size_t j = 0; j < n; j++) wt[j] = ef_mul_base(wt[j], om[j]);
     ef_t pre = ef_mul_base(ef_sub(ef_pow(x, n), ef_one()), kb_inv((kb_t)(n % KB_P)));
-#pragma omp parallel for schedule(dynamic, 1)
+    /* rows in storage order (row r holds point j = rev(r)), every column accumulated per row: the
+     * matrix streams once; per-thread partial sums are added in thread order */
+    int nt = omp_get_max_threads();
+    ef_t *part = (ef_t *)calloc((size_t)nt * (w ? w : 1), sizeof(ef_t));
+#pragma omp parallel
+    {
+        ef_t *acc = part + (size_t)omp_get_thread_num() * w;
+#pragma omp for schedule(static)
+        for (size_t r = 0; r < n; r++) {
+            const ef_t wr = wt[rev_bits((uint32_t)r, logn)];
+            const kb_t *row = lde->data + r * w;
+            for (size_t c = 0; c < w; c++) acc[c] = ef_add(acc[c], ef_mul_base(wr, row[c]));
+        }
+    }
     for (size_t c = 0; c < w; c++) {
         ef_t acc = ef_zero();
-        for (size_t j = 0; j < n; j++)
-            acc = ef_add(acc, ef_mul_base(wt[j], lde->data[(size_t)rev_bits((uint32_t)j, logn) * w + c]));
+        for (int t = 0; t < nt; t++) acc = ef_add(acc, part[(size_t)t * w + c]);
         out[c] = ef_mul(pre, acc);
     }
+    free(part);
     free(wt);
     free(om);
 }
@@ -199,27 +212,44 @@ static void gen_perm_trace(const orc_chip_t *ch, const kb_t *prep, const kb_t *m
     *lcs = ef_zero();
     if (!pw) return;
     int batch = 1 << ch->log_qd, nb = pw - 1;
+    const int nl = ch->nlocal;
     size_t W = ch->main_width, PWd = ch->prep_width;
+    /* rows in chunks: every lookup denominator of the chunk inverted with one field inversion */
+    const size_t RB = 256;
+    ef_t bpw[256];
+    bpw[0] = beta;
+    for (int v = 1; v < 256; v++) bpw[v] = ef_mul(bpw[v - 1], beta);
 #pragma omp parallel for schedule(static)
-    for (size_t r = 0; r < h; r++) {
-        const kb_t *ml = main + r * W;
-        const kb_t *pl = prep ? prep + r * PWd : NULL;
-        for (int b = 0; b < nb; b++) {
-            ef_t s = ef_zero();
-            for (int i = b * batch; i < ch->nlocal && i < (b + 1) * batch; i++) {
+    for (size_t r0 = 0; r0 < h; r0 += RB) {
+        const size_t rn = h - r0 < RB ? h - r0 : RB;
+        ef_t *d = (ef_t *)malloc(sizeof(ef_t) * rn * nl), *pre = (ef_t *)malloc(sizeof(ef_t) * rn * nl);
+        kb_t *mu = (kb_t *)malloc(sizeof(kb_t) * rn * nl);
+        for (size_t r = 0; r < rn; r++) {
+            const kb_t *ml = main + (r0 + r) * W;
+            const kb_t *pl = prep ? prep + (r0 + r) * PWd : NULL;
+            for (int i = 0; i < nl; i++) {
                 const orc_lookup_t *lk = &ch->local[i];
-                ef_t d = ef_add(alpha, ef_from_base(lk->kind));
-                ef_t bp = beta;
-                for (int v = 0; v < lk->nvalues; v++) {
-                    d = ef_add(d, ef_mul_base(bp, orc_vpc_apply(&lk->values[v], pl, ml)));
-                    bp = ef_mul(bp, beta);
-                }
-                kb_t mu = orc_vpc_apply(&lk->mult, pl, ml);
-                if (!lk->is_send) mu = kb_neg(mu);
-                s = ef_add(s, ef_mul_base(ef_inv(d), mu));
+                ef_t x = ef_add(alpha, ef_from_base(lk->kind));
+                for (int v = 0; v < lk->nvalues && v < 256; v++)
+                    x = ef_add(x, ef_mul_base(bpw[v], orc_vpc_apply(&lk->values[v], pl, ml)));
+                kb_t m = orc_vpc_apply(&lk->mult, pl, ml);
+                d[r * nl + i] = x;
+                mu[r * nl + i] = lk->is_send ? m : kb_neg(m);
             }
-            perm[r * pw + b] = s;
         }
+        const size_t k = rn * nl;
+        ef_t acc = ef_one();
+        for (size_t j = 0; j < k; j++) { pre[j] = acc; acc = ef_mul(acc, d[j]); }
+        ef_t inv = ef_inv(acc);
+        for (size_t j = k; j-- > 0;) { ef_t t = ef_mul(inv, pre[j]); inv = ef_mul(inv, d[j]); d[j] = t; }
+        for (size_t r = 0; r < rn; r++)
+            for (int b = 0; b < nb; b++) {
+                ef_t sum = ef_zero();
+                for (int i = b * batch; i < nl && i < (b + 1) * batch; i++)
+                    sum = ef_add(sum, ef_mul_base(d[r * nl + i], mu[r * nl + i]));
+                perm[(r0 + r) * pw + b] = sum;
+            }
+        free(d); free(pre); free(mu);
     }
     ef_t run = ef_zero();
     for (size_t r = 0; r < h; r++) {
@@ -453,12 +483,15 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
             }
             free(xp);
             batch_inverse(den, H);
+            /* sum_c alpha^c (p_c(z) - x_c) = B - sum_c alpha^c x_c with B = sum_c alpha^c p_c(z) */
+            ef_t B = ef_zero();
+            for (size_t c = 0; c < w; c++) B = ef_add(B, ef_mul(apow[base + c], req[r].vals[p][c]));
 #pragma omp parallel for schedule(static)
             for (size_t i = 0; i < H; i++) {
                 ef_t acc = ef_zero();
-                for (size_t c = 0; c < w; c++)
-                    acc = ef_add(acc, ef_mul(apow[base + c], ef_sub(req[r].vals[p][c], ef_from_base(mm->data[i * w + c]))));
-                ro[lh][i] = ef_add(ro[lh][i], ef_mul(acc, den[i]));
+                const kb_t *row = mm->data + i * w;
+                for (size_t c = 0; c < w; c++) acc = ef_add(acc, ef_mul_base(apow[base + c], row[c]));
+                ro[lh][i] = ef_add(ro[lh][i], ef_mul(ef_sub(B, acc), den[i]));
             }
             free(den);
             pow_cnt[lh] += (int)w;

@@ -1369,7 +1369,8 @@ def _execute(prog, regs, shard, max_steps, state=None):
     U = A.UNUSED_PC
     clk = 0
     while PC_BASE <= pc < end and state.get("exit_code") is None:  # the program halts when pc leaves it
-        if split and len(steps) >= max_steps and npc == pc + 4:
+        # a continuation shard also ends before its 24-bit clk could overflow (a syscall adds <= 255 cycles)
+        if split and (len(steps) >= max_steps or clk > (1 << 24) - 1024) and npc == pc + 4:
             break
         assert len(steps) < max_steps or (split and len(steps) < max_steps + 2)
         k = (pc - PC_BASE) >> 2
