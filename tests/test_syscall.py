@@ -304,3 +304,47 @@ def test_sys_linux_gpu_proofs_identical(linux_run):
         p = gpu.prove_shard(tr, pv)
         rc, ref = cpu.prove(tr, pv)
         assert rc == 0 and p == ref
+
+
+def _two_rank_worker(rank, world, port, out_q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from zkmips_amd.dist import prove_shards_distributed
+    run = C.program_shards(C.sha_program(3, seed=7), seed=7, shard_size=90)
+    m, prep, _, _ = run[0]
+    pr = O.OracleProver(m, {k: v for k, v in prep.items() if v is not None}, num_queries=4)
+
+    def prove_one(i):
+        rc, p = pr.prove(run[i][2], run[i][3])
+        assert rc == 0
+        return p
+
+    proofs = prove_shards_distributed(prove_one, len(run), check_global_sum=True)
+    if rank == 0:
+        out_q.put((len(run), len(proofs), [i for i, (_, _, tr, _) in enumerate(run) if "Cpu" not in tr]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sha2_execution():
+    """The CPU, SHA_EXTEND, SHA_COMPRESS and memory shards of one execution dealt to two gloo ranks; rank 0
+    gathers the proofs and the machine-level global sum (syscall and memory messages) checks out."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    n, got, non_cpu = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == n and len(non_cpu) == 3  # extend shard, compress shard, memory shard
