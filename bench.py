@@ -52,6 +52,33 @@ def device_matrix(tensor, name, keep):
     return Matrix(nm, tensor.data_ptr(), tensor.shape[0], tensor.shape[1], ZKM_REPR_CANONICAL | 0x100)
 
 
+class RawDev:
+    """A device buffer from hipExtMallocWithFlags, shaped like the trace it receives (bench --h2d-dst)."""
+    _hip = None
+
+    def __init__(self, shape, flags):
+        if RawDev._hip is None:
+            h = C.CDLL("libamdhip64.so")
+            h.hipExtMallocWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+            h.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+            RawDev._hip = h
+        self.shape = tuple(shape)
+        self.nbytes = int(np.prod(shape)) * 4
+        p = C.c_void_p()
+        if RawDev._hip.hipExtMallocWithFlags(C.byref(p), max(self.nbytes, 4), flags) != 0:
+            raise RuntimeError("hipExtMallocWithFlags failed")
+        self.ptr = p.value
+
+    def data_ptr(self):
+        return self.ptr
+
+    def copy_from_host(self, host_tensor, stream):
+        RawDev._hip.hipMemcpyAsync(self.ptr, host_tensor.data_ptr(), self.nbytes, 1, stream.cuda_stream)
+
+
+H2D_FLAGS = {"uncached": 0x3, "finegrained": 0x1}
+
+
 def prove_resident(prover, dev_traces, pvs):
     """zkm_prove_shard over device-resident row-major traces (ZKM_MEM_DEVICE)."""
     from zkmips_amd._lib import Matrix, check, lib
@@ -305,6 +332,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--log-n", type=int, default=22)
     ap.add_argument("--sha-blocks", type=int, default=16384, help="sha2 workload: 64-byte blocks hashed")
+    ap.add_argument("--h2d-dst", choices=["torch", "uncached", "finegrained"], default="torch",
+                    help="memory type of the HBM buffers the pipelined H2D copies land in")
     ap.add_argument("--sha-events-per-shard", type=int, default=16384,
                     help="sha2 workload: precompile calls per precompile shard")
     ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2"], default="fib",
@@ -366,7 +395,8 @@ def main():
             pinned[kk].numpy()[...] = v.view(np.int32)
         shards.append(({kk: torch.from_numpy(v.view(np.int32)).cuda() for kk, v in traces_k.items()}, pvs_k,
                        {kk: t.numpy().view(np.uint32) for kk, t in pinned.items()}, pinned,
-                       [{kk: torch.empty_like(t, device="cuda") for kk, t in pinned.items()} for _ in range(2)],
+                       [{kk: (torch.empty_like(t, device="cuda") if args.h2d_dst == "torch" else
+                              RawDev(t.shape, H2D_FLAGS[args.h2d_dst])) for kk, t in pinned.items()} for _ in range(2)],
                        torch.cuda.Stream()))
     dev = Device(local_rank)
     prover = HipProver(dev, m, prep, num_queries=args.queries)
@@ -395,7 +425,10 @@ def main():
             b = bufs[j % 2]
             with torch.cuda.stream(cs):
                 for kk, t in host_t.items():
-                    b[kk].copy_(t, non_blocking=True)
+                    if isinstance(b[kk], RawDev):
+                        b[kk].copy_from_host(t, cs)
+                    else:
+                        b[kk].copy_(t, non_blocking=True)
                 e = torch.cuda.Event()
                 e.record(cs)
             return e

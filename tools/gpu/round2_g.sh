@@ -13,4 +13,7 @@ timeout -k 10 600 python bench.py --workload sha2 --steps 3 > $O/bench_sha2.json
 cut -c1-600 $O/bench_sha2.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --no-cpu-baseline --no-pmc > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 1; }
+
+timeout -k 10 300 python3 $R/tools/gpu/dma_uncached.py > $O/dma_uncached.txt 2>&1 || { tail -20 $O/dma_uncached.txt; exit 1; }
+cat $O/dma_uncached.txt
 echo done
