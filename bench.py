@@ -610,6 +610,9 @@ def main():
         "host_per_call": {"value": round(world * K * rows_per_shard * args.steps / elapsed_pc, 1), "unit": "rows/s",
                           "ms_per_shard": round(1e3 * elapsed_pc / (args.steps * K), 3),
                           "what": "same steps, each zkm_prove_shard copies its pinned host traces itself (no look-ahead)"},
+        "value_basis": ("host traces: H2D of the traces and D2H of the proof inside the timed region (SURVEY.md "
+                        "section 8d's definition, asked for by the round-1 review); the same steps with the inputs "
+                        "already resident in HBM when the timing starts are `resident`"),
         "resident": {"value": round(world * K * rows_per_shard * args.steps / elapsed_res, 1), "unit": "rows/s",
                      "ms_per_shard": round(1e3 * elapsed_res / (args.steps * K), 3),
                      "what": "same steps, traces already in HBM (no H2D)"},
