@@ -167,3 +167,17 @@ def test_two_adicity_limit_is_an_error(dev):
     from zkmips_amd._lib import ZkmError
     with pytest.raises(ZkmError):
         dev.bench_lde(1 << 24, 1, 1)
+
+
+@pytest.mark.parametrize("zero_copy", ["0", "1"])
+def test_pinned_host_traces(dev, zero_copy, monkeypatch):
+    """Traces in page-locked host memory (zkm_host_alloc): copied by the DMA engine, or (ZKM_ZERO_COPY=1)
+    read over PCIe by the transpose kernel itself; the proof equals the oracle's either way, for a main
+    trace and a narrow table, with the CPU-side buffers released only after the call returns."""
+    from zkmips_amd._lib import pinned_copy
+    monkeypatch.setenv("ZKM_ZERO_COPY", zero_copy)
+    gpu, cpu, traces, pvs = provers(dev, 1 << 14, seed=11)
+    held = {k: pinned_copy(v) for k, v in traces.items()}
+    p = gpu.prove_shard({k: h.array for k, h in held.items()}, pvs)
+    rc, ref = cpu.prove(traces, pvs)
+    assert rc == 0 and p == ref

@@ -36,6 +36,11 @@ int guard_status(const std::exception &e) {
     return ZKM_ERR_HIP;
 }
 
+static bool zero_copy_enabled() {  // read per call (a getenv per matrix is noise next to a shard proof)
+    const char *e = getenv("ZKM_ZERO_COPY");
+    return e && *e && *e != '0';
+}
+
 // true when p lies in page-locked host memory (zkm_host_alloc / hipHostMalloc / hipHostRegister)
 static bool host_pinned(const void *p) {
     hipPointerAttribute_t a;
@@ -63,10 +68,19 @@ void upload_matrix_into(Ctx &c, const zkm_matrix_t &m, uint32_t *col, hipStream_
         launch_to_col_major(m.data, m.height, m.width, mont, col, s);
         return;
     }
+    const bool pinned = host_pinned(m.data);
+    if (pinned && zero_copy_enabled() && m.width <= 128) {
+        // ZKM_ZERO_COPY=1: the transpose kernel reads the page-locked host rows over PCIe itself (a
+        // capped grid keeps the link busy without occupying the GPU); no DMA-engine copy
+        void *dp = nullptr;
+        HIP_CHECK(hipHostGetDevicePointer(&dp, const_cast<void *>(static_cast<const void *>(m.data)), 0));
+        launch_to_col_major((const uint32_t *)dp, m.height, m.width, mont, col, s, 128);
+        return;
+    }
     DBuf raw(n, s);
     HIP_CHECK(hipMemcpyAsync(raw.p, m.data, n * 4, hipMemcpyHostToDevice, s));
     launch_to_col_major(raw.p, m.height, m.width, mont, col, s);
-    if (!host_pinned(m.data)) HIP_CHECK(hipStreamSynchronize(s));
+    if (!pinned) HIP_CHECK(hipStreamSynchronize(s));
 }
 
 DBuf upload_matrix(Ctx &c, const zkm_matrix_t &m, hipStream_t s) {

@@ -127,8 +127,10 @@ DBuf upload_matrix(Ctx &c, const zkm_matrix_t &m, hipStream_t s);
 
 // ---------------------------------------------------------------- kernels (launchers)
 // host row-major (canonical or Montgomery) -> device column-major Montgomery
+// max_grid > 0 caps the workgroup count (grid-stride loop): used when d_rowmajor is page-locked host
+// memory read over PCIe by the kernel itself, so a few workgroups keep the link busy
 void launch_to_col_major(const uint32_t *d_rowmajor, uint64_t h, uint64_t w, bool montgomery_in,
-                         uint32_t *d_col, hipStream_t s);
+                         uint32_t *d_col, hipStream_t s, unsigned max_grid = 0);
 void launch_from_col_major(const uint32_t *d_col, uint64_t h, uint64_t w, uint32_t *d_rowmajor_canon,
                            hipStream_t s);
 void build_twiddles(Ctx &c, int log_max);

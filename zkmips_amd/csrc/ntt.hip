@@ -69,7 +69,10 @@ static constexpr int TW_ROWS = 64, TW_MAXW = 128;
 __global__ __launch_bounds__(NT) void k_to_col_major_rows(const uint32_t *__restrict__ in, uint64_t h, uint32_t w,
                                                           int mont_in, uint32_t *__restrict__ out) {
     __shared__ uint32_t tile[TW_MAXW * (TW_ROWS + 1)];  // [c][r], pitch 65: conflict-free both ways
-    const uint64_t r0 = (uint64_t)blockIdx.x * TW_ROWS;
+    const uint64_t nblk = (h + TW_ROWS - 1) / TW_ROWS;
+    for (uint64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {  // grid-stride: a capped grid for host sources
+    if (blk != blockIdx.x) __syncthreads();  // the previous block's tile has been written out
+    const uint64_t r0 = blk * TW_ROWS;
     const uint32_t nr = (uint32_t)(h - r0 < TW_ROWS ? h - r0 : TW_ROWS);
     const uint32_t n = nr * w;
     const uint32_t *src = in + r0 * w;
@@ -98,12 +101,16 @@ __global__ __launch_bounds__(NT) void k_to_col_major_rows(const uint32_t *__rest
         const uint32_t c = i / TW_ROWS, r = i % TW_ROWS;
         if (r < nr) out[(uint64_t)c * h + r0 + r] = tile[c * (TW_ROWS + 1) + r];
     }
+    }
 }
 
-void launch_to_col_major(const uint32_t *d_in, uint64_t h, uint64_t w, bool mont_in, uint32_t *d_out, hipStream_t s) {
+void launch_to_col_major(const uint32_t *d_in, uint64_t h, uint64_t w, bool mont_in, uint32_t *d_out, hipStream_t s,
+                         unsigned max_grid) {
     if (!h || !w) return;
     if (w <= TW_MAXW) {
-        hipLaunchKernelGGL(k_to_col_major_rows, dim3((unsigned)((h + TW_ROWS - 1) / TW_ROWS)), dim3(NT), 0, s, d_in, h,
+        uint64_t g = (h + TW_ROWS - 1) / TW_ROWS;
+        if (max_grid && g > max_grid) g = max_grid;
+        hipLaunchKernelGGL(k_to_col_major_rows, dim3((unsigned)g), dim3(NT), 0, s, d_in, h,
                            (uint32_t)w, (int)mont_in, d_out);
         HIP_CHECK(hipGetLastError());
         return;
