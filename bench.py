@@ -314,6 +314,64 @@ def execution_bench(args):
     print(json.dumps(line), flush=True)
 
 
+def tracegen_bench(args):
+    """Device trace generation (include/zkm_tracegen.h, §8f row 2): the Cpu chip's trace of a
+    2^log_n-row shard (the largest chip of a MIPS shard, 67 columns) from CpuEventFfi records resident
+    in HBM, Byte and Program multiplicities included; plus AddSub (19 columns) and MemoryLocal.  The
+    records are a real execution (mips_core.loop_program, 2^14 instructions) tiled to 2^log_n rows.
+    HBM-bound: per Cpu row 280 B of record read + 268 B of trace written (+ the program fetch and the
+    multiplicity atomics, served by L2)."""
+    import torch
+    from zkmips_amd import mips_core as MC
+    from zkmips_amd import tracegen as TG
+    torch.cuda.set_device(0)
+    n = 1 << args.log_n
+    cap = {}
+    MC.program_shard(MC.loop_program(24, (1 << 14) // 28, seed=3), seed=3, shard=1, capture=cap)
+    base = TG.cpu_events(cap["steps"], 1)
+    tile = lambda r: r[np.arange(n) % len(r)]  # (np.resize would repack the padded record dtype)
+    ev = tile(base)
+    prog = TG.program_ffi(cap["prog"])
+    adds = tile(TG.add_sub_records(cap["alu"]))
+    ml = tile(TG.memory_local_events(cap["entries"]))
+    d_ev, d_prog, d_add, d_ml = (TG.to_device(x) for x in (ev, prog, adds, ml))
+    bm = torch.zeros((65536, 10), dtype=torch.int32, device="cuda")
+    pm = torch.zeros((len(prog), 1), dtype=torch.int32, device="cuda")
+    chips = {
+        "Cpu": (lambda: TG.cpu_trace(d_ev, n, 1, d_prog, len(prog), height=n, byte_mult=bm, program_mult=pm),
+                280 + 4 * TG.CPU_WIDTH),
+        "AddSub": (lambda: TG.add_sub_trace(d_add, n, height=n, byte_mult=bm), 28 + 4 * TG.ADD_SUB_WIDTH),
+        "MemoryLocal": (lambda: TG.memory_local_trace(d_ml, n, height=n // 4), 28 + 4 * 14),
+    }
+    res = {}
+    for name, (fn, bytes_per_row) in chips.items():
+        for _ in range(max(1, args.warmup)):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.steps
+        gbs = n * bytes_per_row / ms / 1e6
+        res[name] = {"ms": round(ms, 4), "rows_per_s": round(n / ms * 1e3, 1), "algorithmic_bytes_per_row": bytes_per_row,
+                     "GBps": round(gbs, 1), "frac_of_hbm_peak": round(gbs / (HBM_PEAK_GBS), 3)}
+    cpu = res["Cpu"]
+    line = {
+        "metric": "Cpu trace rows generated/sec (device trace generation, zkm_cpu_events_to_trace)",
+        "value": cpu["rows_per_s"], "unit": "rows/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": cpu["ms"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "CpuEventFfi records of a real execution (loop_program, 2^14 instructions) tiled, resident in HBM",
+        "config": {"workload": f"tracegen: Cpu 2^{args.log_n} rows (67 columns) + Byte/Program multiplicities"},
+        "roofline": {"bound": "hbm", "achieved": cpu["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": cpu["frac_of_hbm_peak"], "traffic": None},
+        "chips": res,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def pmc_child(args):
     """Runs under rocprofv3 counter passes (pmc_in_run): setup, then the same shard proven twice."""
     from zkmips_amd._lib import Device
@@ -336,7 +394,7 @@ def main():
                     help="memory type of the HBM buffers the pipelined H2D copies land in")
     ap.add_argument("--sha-events-per-shard", type=int, default=16384,
                     help="sha2 workload: precompile calls per precompile shard")
-    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2"], default="fib",
+    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2", "tracegen"], default="fib",
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
                          "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
                          "zkmips_amd/mips_alu.py), 2^(log-n) "
@@ -358,6 +416,8 @@ def main():
         return pmc_child(args)
     if args.workload == "sha2":
         return execution_bench(args)
+    if args.workload == "tracegen":
+        return tracegen_bench(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

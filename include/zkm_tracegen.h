@@ -1,0 +1,136 @@
+/*
+ * zkm_tracegen.h — device trace generation (libzkm_hip.so), SURVEY.md §8f row 2.
+ *
+ * Drop-in for the reference's native trace-row ABI, crates/core/machine/src/sys.rs:14-42 →
+ * crates/core/machine/cpp/extern.cpp:6-37, which fills ONE row per call on the host:
+ *
+ *   cpu_event_to_row_koalabear(CpuEventFfi, shard, InstructionFfi, CpuCols*)      (include/cpu.hpp:37-108)
+ *   add_sub_event_to_row_koalabear(const AluEvent*, AddSubCols*)                   (include/add_sub.hpp:26-39)
+ *   memory_local_event_to_row_koalabear(const MemoryLocalEvent*, SingleMemoryLocal*) (include/memory_local.hpp:8-20)
+ *   memory_global_event_to_row_koalabear(const MemoryInitializeFinalizeEvent*, bool, MemoryInitCols*)
+ *                                                                                  (include/memory_global.hpp:9-43)
+ *   syscall_event_to_row_koalabear(const SyscallEvent*, bool, SyscallCols*)        (include/syscall.hpp:8-16)
+ *
+ * Here each entry point fills a WHOLE padded trace in GPU memory from an event array in GPU memory:
+ * one thread per row, rows staged through LDS so the row-major trace is written in full cache
+ * lines; padding rows get the chip's padding values, so the buffer needs no clearing.  The parts
+ * the reference's Rust callers add around the row ABI are done on the device too: the Byte chip's
+ * lookup multiplicities (`byte_mult`, the Byte chip's 65536 x 10 row-major main trace, added to with
+ * atomics), the Program chip's multiplicities, and the cross-row columns of MemoryGlobalInit/Finalize
+ * (`memory/global.rs:111-186`).  Output is canonical KoalaBear (the prover's ZKM_REPR_CANONICAL),
+ * ready for zkm_prove_shard with ZKM_MEM_DEVICE.
+ *
+ * The event structs are the reference's #[repr(C)] layouts (cbindgen), so a Rust caller passes its
+ * event vectors (after `.into()` for CpuEventFfi) byte for byte.  All pointers are device pointers;
+ * `stream` is a hipStream_t (NULL = the null stream).  Calls are asynchronous on `stream` and return
+ * ZKM_ERR_ARG for inconsistent sizes.
+ */
+#ifndef ZKM_TRACEGEN_H
+#define ZKM_TRACEGEN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* MemoryReadRecord / MemoryWriteRecord / MemoryRecord (core/executor/src/events/memory.rs:12-19, :49-83) */
+typedef struct { uint32_t value, shard, timestamp, prev_shard, prev_timestamp; } zkm_memory_read_record;
+typedef struct { uint32_t value, shard, timestamp, prev_value, prev_shard, prev_timestamp; } zkm_memory_write_record;
+typedef struct { uint32_t shard, timestamp, value; } zkm_memory_record;
+
+/* OptionMemoryRecordEnum (events/cpu.rs:100-139): tag 0 Read, 1 Write, 2 None */
+#define ZKM_RECORD_READ 0
+#define ZKM_RECORD_WRITE 1
+#define ZKM_RECORD_NONE 2
+typedef struct {
+    uint8_t tag;
+    zkm_memory_read_record read;
+    zkm_memory_write_record write;
+} zkm_option_memory_record;  /* 48 bytes */
+
+/* OptionU32 (core/executor/src/lib.rs:40-60): tag 0 Some, 1 None */
+typedef struct { uint8_t tag; uint32_t value; } zkm_option_u32;
+
+/* CpuEventFfi (events/cpu.rs:46-75), 280 bytes */
+typedef struct {
+    uint32_t clk, pc, next_pc, next_next_pc;
+    uint32_t a;
+    zkm_option_memory_record a_record;
+    uint32_t b;
+    zkm_option_memory_record b_record;
+    uint32_t c;
+    zkm_option_memory_record c_record;
+    zkm_option_u32 hi;
+    zkm_option_memory_record hi_record;
+    zkm_option_memory_record memory_record;
+    uint32_t exit_code;
+} zkm_cpu_event_ffi;
+
+/* InstructionFfi (core/executor/src/instruction.rs:29-45), 24 bytes; opcode = Opcode as u8 */
+typedef struct {
+    uint8_t opcode, op_a;
+    uint32_t op_b, op_c;
+    uint8_t imm_b, imm_c;
+    zkm_option_u32 raw;
+} zkm_instruction_ffi;
+
+/* AluEvent (events/instr.rs:10-27), 28 bytes */
+typedef struct { uint32_t pc, next_pc; uint8_t opcode; uint32_t hi, a, b, c; } zkm_alu_event;
+
+/* MemoryLocalEvent (events/memory.rs:225-236), 28 bytes */
+typedef struct { uint32_t addr; zkm_memory_record initial_mem_access, final_mem_access; } zkm_memory_local_event;
+
+/* MemoryInitializeFinalizeEvent (events/memory.rs:135-148), 16 bytes */
+typedef struct { uint32_t addr, value, shard, timestamp; } zkm_memory_init_final_event;
+
+/* SyscallEvent (events/syscall.rs:8-29), 56 bytes */
+typedef struct {
+    uint32_t pc, next_pc, shard, clk;
+    zkm_memory_write_record a_record;
+    uint8_t a_record_is_real;
+    uint32_t syscall_id, arg1, arg2;
+} zkm_syscall_event;
+
+/* Trace widths (columns) of the chips filled here. */
+#define ZKM_CPU_WIDTH 67
+#define ZKM_ADD_SUB_WIDTH 19
+#define ZKM_MEMORY_LOCAL_WIDTH 56      /* 4 SingleMemoryLocal of 14 per row (memory/local.rs:26) */
+#define ZKM_MEMORY_GLOBAL_WIDTH 111
+#define ZKM_SYSCALL_WIDTH 6
+#define ZKM_BYTE_MULT_WIDTH 10         /* Byte chip main trace: 65536 rows x 10 (bytes/columns.rs) */
+
+/* Cpu: rows [0, n) from events[i] with instruction program[(pc - pc_base) / 4] (Program::fetch),
+ * rows [n, height) padding (imm_b = imm_c = is_rw_a = 1, cpu/trace.rs).  byte_mult (nullable): the
+ * row's Byte lookups (shard/clk range checks, the register-access timestamp checks and op_a value
+ * bytes, cpu/trace.rs:118-250).  program_mult (nullable, program_len x 1): +1 per executed
+ * instruction (the Program chip's multiplicities, program/mod.rs:102-140). */
+int zkm_cpu_events_to_trace(const zkm_cpu_event_ffi *events, uint64_t n, uint32_t shard,
+                            const zkm_instruction_ffi *program, uint64_t program_len, uint32_t pc_base,
+                            uint32_t *trace, uint64_t height, uint32_t *byte_mult, uint32_t *program_mult,
+                            void *stream);
+
+/* AddSub (alu/add_sub/mod.rs:82-163): AddOperation carries + the U8Range checks of both operands
+ * and the sum into byte_mult (nullable). */
+int zkm_add_sub_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                uint32_t *byte_mult, void *stream);
+
+/* MemoryLocal (memory/local.rs:144-185): event i fills entry i % 4 of row i / 4; height rows. */
+int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,
+                                     uint64_t height, void *stream);
+
+/* MemoryGlobalInit (is_receive = 0) / MemoryGlobalFinalize (1) (memory/global.rs:111-186): events
+ * sorted by strictly increasing addr, all above prev_addr (the shard's previous_*_addr public value,
+ * 0 for none) — the precondition the reference establishes with sort_by_key. */
+int zkm_memory_global_events_to_trace(const zkm_memory_init_final_event *events, uint64_t n, int is_receive,
+                                      uint32_t prev_addr, uint32_t *trace, uint64_t height, void *stream);
+
+/* SyscallCore / SyscallPrecompile (syscall/chip.rs:138-183). */
+int zkm_syscall_events_to_trace(const zkm_syscall_event *events, uint64_t n, int is_receive, uint32_t *trace,
+                                uint64_t height, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZKM_TRACEGEN_H */

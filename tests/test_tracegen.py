@@ -1,0 +1,271 @@
+"""Device trace generation (include/zkm_tracegen.h): the reference's per-row trace ABI
+(crates/core/machine/src/sys.rs:14-42, include/{cpu,add_sub,memory_local,memory_global,syscall}.hpp)
+as whole-trace HIP kernels.
+
+Modelled on the reference's own FFI tests, which fill a trace through the C++ event_to_row and
+assert it equals the Rust generate_trace (cpu/trace.rs:279-314 `test_generate_cpu_trace_ffi_eq_rust`,
+alu/add_sub/mod.rs:340-380, memory/local.rs:400-460): here the device traces must equal the host
+trace builders of this repository (program_shard, mips_memory) bit for bit, the Byte and Program
+multiplicities included, and a shard proven from device traces must produce the same proof bytes.
+
+CPU tests: the record layouts equal the header's C structs (gcc offsetof), and a numpy restatement
+of cpu.hpp's event_to_row over the converted records reproduces the host Cpu trace (so the records
+carry everything the row needs)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from zkmips_amd import mips_alu as A
+from zkmips_amd import mips_core as MC
+from zkmips_amd import mips_memory as MM
+from zkmips_amd import tracegen as TG
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+LAYOUTS = {
+    "zkm_option_memory_record": (TG.RECORD, {"tag": "tag", "read": "read", "write": "write"}),
+    "zkm_cpu_event_ffi": (TG.CPU_EVENT, {f: f for f in TG.CPU_EVENT.names if f not in ("hi_tag",)} | {"hi": "hi"}),
+    "zkm_instruction_ffi": (TG.INSTRUCTION, {f: f for f in ("opcode", "op_a", "op_b", "op_c", "imm_b", "imm_c")}),
+    "zkm_alu_event": (TG.ALU_EVENT, {f: f for f in TG.ALU_EVENT.names}),
+    "zkm_memory_local_event": (TG.MEMORY_LOCAL_EVENT, {"addr": "addr", "initial": "initial_mem_access",
+                                                      "final": "final_mem_access"}),
+    "zkm_memory_init_final_event": (TG.MEMORY_INIT_FINAL_EVENT, {f: f for f in TG.MEMORY_INIT_FINAL_EVENT.names}),
+    "zkm_syscall_event": (TG.SYSCALL_EVENT, {f: f for f in TG.SYSCALL_EVENT.names}),
+}
+
+
+def test_record_layouts_match_header(tmp_path):
+    """numpy record dtypes == the C structs of include/zkm_tracegen.h (sizes and field offsets)."""
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "zkm_tracegen.h"', "int main(void) {"]
+    for st, (_, fields) in LAYOUTS.items():
+        lines.append(f'printf("{st} size %zu\\n", sizeof({st}));')
+        for np_name, c_name in fields.items():
+            # OptionU32 `hi` is {tag, value}: the record keeps the tag at the struct's offset
+            expr = f"offsetof({st}, {c_name})" + (" + 4" if (st, c_name) == ("zkm_cpu_event_ffi", "hi") else "")
+            lines.append(f'printf("{st} {np_name} %zu\\n", (size_t)({expr}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {}
+    for ln in out:
+        if ln:
+            st, f, v = ln.split()
+            got[(st, f)] = int(v)
+    for st, (dt, fields) in LAYOUTS.items():
+        assert got[(st, "size")] == dt.itemsize, st
+        for np_name in fields:
+            assert got[(st, np_name)] == dt.fields[np_name][1], (st, np_name)
+    assert TG.CPU_EVENT.fields["hi_tag"][1] == 172
+
+
+# ---------------------------------------------------------------- numpy restatement of cpu.hpp (test-only)
+def _bytes(x):
+    return A._bytes(np.asarray(x, np.uint64).astype(np.uint32))
+
+
+def _access(rec):
+    """populate_read / populate_read_write (include/memory.hpp) over an OptionMemoryRecordEnum column."""
+    tag = rec["tag"].astype(np.int64)
+    rd, wr = rec["read"].astype(np.int64), rec["write"].astype(np.int64)
+    is_w = tag == TG.REC_WRITE
+    on = tag != TG.REC_NONE
+    value = np.where(is_w, wr[:, 0], rd[:, 0])
+    shard, ts = np.where(is_w, wr[:, 1], rd[:, 1]), np.where(is_w, wr[:, 2], rd[:, 2])
+    prev_value = np.where(is_w, wr[:, 3], rd[:, 0])
+    ps, pt = np.where(is_w, wr[:, 4], rd[:, 3]), np.where(is_w, wr[:, 5], rd[:, 4])
+    cmp_ = ps == shard
+    d = (np.where(cmp_, ts, shard) - np.where(cmp_, pt, ps) - 1) & 0xFFFFFFFF
+    return on, value, prev_value, ps, pt, cmp_, d & 0xFFFF, (d >> 16) & 0xFF
+
+
+def cpu_rows(ev, prog_ffi, shard, height):
+    n = len(ev)
+    t = np.zeros((height, MC.CPU_WIDTH), np.uint32)
+    t[n:, MC.C_IMMB] = t[n:, MC.C_IMMC] = t[n:, MC.C_RW_A] = 1
+    ins = prog_ffi[(ev["pc"].astype(np.int64) - MC.PC_BASE) >> 2]
+    op = ins["opcode"].astype(np.int64)
+    clk = ev["clk"].astype(np.int64)
+    t[:n, MC.C_SHARD] = shard
+    t[:n, MC.C_CLK16], t[:n, MC.C_CLK8] = clk & 0xFFFF, (clk >> 16) & 0xFF
+    t[:n, MC.C_PC], t[:n, MC.C_NPC], t[:n, MC.C_NNPC] = ev["pc"], ev["next_pc"], ev["next_next_pc"]
+    t[:n, MC.C_OPCODE], t[:n, MC.C_OPA] = op, ins["op_a"]
+    t[:n, MC.C_OPB:MC.C_OPB + 4], t[:n, MC.C_OPC:MC.C_OPC + 4] = _bytes(ins["op_b"]), _bytes(ins["op_c"])
+    t[:n, MC.C_OPA0] = ins["op_a"] == 0
+    t[:n, MC.C_IMMB], t[:n, MC.C_IMMC] = ins["imm_b"], ins["imm_c"]
+    branch = np.isin(op, MC.BRANCH_OPS)
+    t[:n, MC.C_A_IMM] = branch | np.isin(op, (MC.OP_SB, MC.OP_SH, MC.OP_SW, MC.OP_SWL, MC.OP_SWR))
+    t[:n, MC.C_RW_A] = np.isin(op, (30, MC.OP_INS, MC.OP_MEQ, MC.OP_MNE) + MC.MADDSUB_OPS + MC.MEM_OPS)
+    check = np.isin(op, MC.MULT_DIV + (30,) + MC.MADDSUB_OPS + MC.MEM_OPS)
+    t[:n, MC.C_CHECK_MEM] = check
+    t[:n, MC.C_A_VAL:MC.C_A_VAL + 4] = _bytes(ev["a"])
+    hi_some = ev["hi_tag"] == 0
+    t[:n, MC.C_HI_PREV_A:MC.C_HI_PREV_A + 4] = np.where(hi_some[:, None], _bytes(ev["hi"]), 0)
+    t[:n, MC.C_SHARD_SEND] = np.where(check, shard, 0)
+    t[:n, MC.C_CLK_SEND] = np.where(check, clk, 0)
+    for base, val, rec in ((MC.C_A_ACC + 4, "a", "a_record"), (MC.C_B_ACC, "b", "b_record"),
+                           (MC.C_C_ACC, "c", "c_record")):
+        on, value, prev_value, ps, pt, cmp_, d16, d8 = _access(ev[rec])
+        t[:n, base:base + 4] = _bytes(np.where(on, value, ev[val]))
+        t[:n, base + MC.ACC_PREV_SHARD] = np.where(on, ps, 0)
+        t[:n, base + MC.ACC_PREV_CLK] = np.where(on, pt, 0)
+        t[:n, base + MC.ACC_COMPARE] = on & cmp_
+        t[:n, base + MC.ACC_D16] = np.where(on, d16, 0)
+        t[:n, base + MC.ACC_D8] = np.where(on, d8, 0)
+        if rec == "a_record":
+            t[:n, MC.C_A_ACC:MC.C_A_ACC + 4] = np.where(on[:, None], _bytes(prev_value), 0)
+    sys_ = op == 30
+    pa = t[:n, MC.C_A_ACC:MC.C_A_ACC + 4].astype(np.int64)
+    halt = sys_ & (((pa[:, 0] == 0) & (pa[:, 1] == 0)) | ((pa[:, 0] == 0x96) & (pa[:, 1] == 0x10)))
+    t[:n, MC.C_HALT] = halt
+    t[:n, MC.C_EXTRA] = np.where(sys_, pa[:, 3], 0)
+    t[:n, MC.C_SEQ] = ~(halt | branch | np.isin(op, MC.JUMP_OPS))
+    t[:n, MC.C_REAL] = 1
+    return t
+
+
+def expected_byte_mult(cpu, shard, add_sub=None):
+    """The Byte lookups program_shard makes for the Cpu rows (mips_core.py program_shard) and
+    alu_traces for AddSub, recomputed from the traces' columns."""
+    mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
+    look = A.byte_lookup_into(mult)
+    t = cpu[cpu[:, MC.C_REAL] == 1].astype(np.int64)
+    n = len(t)
+    look(A.B_U16RANGE, np.full(n, shard >> 8), np.full(n, shard & 0xFF))
+    look(A.B_U16RANGE, t[:, MC.C_CLK16] >> 8, t[:, MC.C_CLK16] & 0xFF)
+    look(A.B_U8RANGE, np.zeros(n, np.int64), t[:, MC.C_CLK8])
+    for base, sel in ((MC.C_C_ACC, t[:, MC.C_IMMC] == 0), (MC.C_B_ACC, t[:, MC.C_IMMB] == 0),
+                      (MC.C_A_ACC + 4, np.ones(n, bool))):
+        d16, d8 = t[sel, base + MC.ACC_D16], t[sel, base + MC.ACC_D8]
+        look(A.B_U16RANGE, d16 >> 8, d16 & 0xFF)
+        look(A.B_U8RANGE, np.zeros(len(d8), np.int64), d8)
+    wb = t[:, MC.C_A_ACC + 4:MC.C_A_ACC + 8]
+    look(A.B_U8RANGE, wb[:, 0], wb[:, 1])
+    look(A.B_U8RANGE, wb[:, 2], wb[:, 3])
+    if add_sub is not None:
+        s = add_sub[(add_sub[:, A.AS_ADD] + add_sub[:, A.AS_SUB]) == 1].astype(np.int64)
+        for b in (A.AS_OP1, A.AS_OP2, A.AS_VAL):
+            look(A.B_U8RANGE, s[:, b], s[:, b + 1])
+            look(A.B_U8RANGE, s[:, b + 2], s[:, b + 3])
+    return mult
+
+
+def _sys_linux_program():
+    from tests.test_syscall import _sys_linux_program as f
+    return f()
+
+
+PROGRAMS = {
+    "loop": lambda: MC.loop_program(24, 40, seed=3),
+    "random": lambda: MC.random_program(600, seed=4),
+    "sha_syscalls": lambda: MC.sha_program(3, seed=2),
+    "sys_linux": _sys_linux_program,
+}
+
+
+def _capture(name):
+    prog = PROGRAMS[name]()
+    cap = {}
+    m, prep, tr, pv = MC.program_shard(prog, seed=7, shard=3, capture=cap)
+    return cap, tr, pv, m, prep
+
+
+@pytest.mark.parametrize("name", sorted(PROGRAMS))
+def test_cpu_records_reproduce_host_trace(name):
+    """cpu.hpp's event_to_row (numpy restatement) over the converted CpuEventFfi records equals the
+    host Cpu trace, and the restated lookups account for the shard's byte multiplicities."""
+    cap, tr, _, _, _ = _capture(name)
+    ev = TG.cpu_events(cap["steps"], cap["shard"])
+    got = cpu_rows(ev, TG.program_ffi(cap["prog"]), cap["shard"], len(tr["Cpu"]))
+    assert np.array_equal(got, tr["Cpu"])
+    mult = expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"))
+    assert (mult <= tr["Byte"]).all()  # a part of the shard's lookups
+
+
+# ---------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(PROGRAMS))
+def test_device_shard_traces_match_host(name):
+    import torch
+    cap, tr, _, _, _ = _capture(name)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.shard_traces(cap, byte_mult=bm)
+    torch.cuda.synchronize()
+    for chip, t in dev.items():
+        host = tr[chip]
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), host), chip
+    assert set(dev) >= {"Cpu", "Program", "MemoryLocal"}
+    want = expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"))
+    assert np.array_equal(bm.cpu().numpy().astype(np.uint64), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,prev_addr,initialize", [(0, 0, True), (1, 0, True), (37, 0, False), (300, 0x1234, True),
+                                                   (1000, 0xFFFF0, False), (16, 8, False)])
+def test_device_memory_global_matches_host(n, prev_addr, initialize):
+    import torch
+    rng = np.random.default_rng(n + prev_addr)
+    addr = np.sort(rng.choice(np.arange(prev_addr + 1, prev_addr + 1 + 50 * max(n, 1), dtype=np.int64), n,
+                              replace=False))
+    if n > 2:
+        addr[-1] = 0x7EFFFFFF - 4  # the top of the KoalaBear range (and_most_sig_byte columns)
+        addr = np.sort(addr)
+    ev = np.stack([addr, rng.integers(0, 1 << 32, n), rng.integers(0, 5, n), rng.integers(0, 1 << 24, n)], axis=1)
+    host, _, _ = MM.memory_global_trace(ev, initialize, prev_addr)
+    rec = TG.memory_init_final_events(ev)
+    dev = TG.memory_global_trace(TG.to_device(rec), n, initialize, prev_addr, height=len(host))
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy().view(np.uint32), host)
+
+
+@pytest.mark.gpu
+def test_device_traces_empty_and_ragged():
+    """n = 0 gives padding rows only; n one short of / one past a block boundary fills exactly n rows."""
+    import torch
+    prog = TG.program_ffi(MC.random_program(50, seed=1))
+    for n in (0, 127, 129):
+        cap = {}
+        if n:
+            MC.program_shard(MC.random_program(n, seed=5), seed=5, capture=cap)
+            steps = cap["steps"][:n]
+            ev, p = TG.cpu_events(steps, 1), TG.program_ffi(cap["prog"])
+        else:
+            ev, p = TG.cpu_events([], 1), prog
+        h = max(16, 1 << max(0, (len(ev) - 1).bit_length()))
+        t = TG.cpu_trace(TG.to_device(ev), len(ev), 1, TG.to_device(p), len(p), height=h).cpu().numpy()
+        want = cpu_rows(ev, p, 1, h)
+        assert np.array_equal(t.view(np.uint32), want)
+    e = TG.add_sub_trace(TG.to_device(np.zeros(0, TG.ALU_EVENT)), 0).cpu().numpy()
+    assert e.shape == (16, TG.ADD_SUB_WIDTH) and not e.any()
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_device_traces_prove_identically():
+    """A shard proven from device-generated traces (ZKM_MEM_DEVICE) gives the host traces' proof bytes."""
+    import torch
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    cap, tr, pv, m, prep = _capture("sha_syscalls")
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.shard_traces(cap, byte_mult=bm)
+    rest = tr["Byte"].astype(np.int64) - expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub")).astype(np.int64)
+    bm += torch.from_numpy(rest.astype(np.int32)).cuda()  # the other chips' lookups, from the host builders
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, prep, num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
+def test_repacked_records_are_refused():
+    """np.resize repacks a padded record dtype (280 -> 262 bytes): such arrays must not reach the ABI,
+    which takes bare pointers and would read past the buffer."""
+    ev = np.zeros(3, TG.CPU_EVENT)
+    assert ev[np.arange(10) % 3].dtype == TG.CPU_EVENT
+    with pytest.raises(ValueError):
+        TG.to_device(np.resize(ev, 10))

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, "libzkm_hip.so")
 
 ZKM_OK = 0
 ZKM_REPR_CANONICAL, ZKM_REPR_MONTGOMERY = 0, 1
+ZKM_MEM_DEVICE = 0x100  # zkm_matrix_t.repr flag: data is GPU-resident
 
 
 class ZkmError(RuntimeError):

@@ -1,0 +1,542 @@
+// Device trace generation: the reference's per-row trace ABI (crates/core/machine/src/sys.rs:14-42,
+// cpp/extern.cpp:6-37, include/*.hpp) as whole-trace HIP kernels.  See include/zkm_tracegen.h.
+//
+// Every kernel is the same streaming shape, HBM-bound (no arithmetic worth the name): a workgroup
+// of 128 threads owns 128 consecutive trace rows.  (1) The block's events are copied into LDS with
+// coalesced dword loads (events are 16-280 byte structs; one thread per event would make every load
+// instruction touch 64 cache lines).  (2) Each thread builds its row in registers from its event —
+// the reference's event_to_row — and adds its Byte-chip lookups (wave-aggregated atomics: most
+// lookups of a wave hit the same entry, e.g. the shard's U16 range check).  (3) The rows go back
+// through LDS (odd pitch: conflict-free) and leave as full-line 16-byte stores of the block's
+// contiguous row-major span.  Padding rows are written too, so the output needs no clearing.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/zkm_hip.h"
+#include "../../include/zkm_tracegen.h"
+
+namespace zkm {
+extern thread_local std::string g_last_error;
+}
+using zkm::g_last_error;
+
+static_assert(sizeof(zkm_option_memory_record) == 48, "OptionMemoryRecordEnum layout");
+static_assert(sizeof(zkm_cpu_event_ffi) == 280, "CpuEventFfi layout");
+static_assert(sizeof(zkm_instruction_ffi) == 24, "InstructionFfi layout");
+static_assert(sizeof(zkm_alu_event) == 28, "AluEvent layout");
+static_assert(sizeof(zkm_memory_local_event) == 28, "MemoryLocalEvent layout");
+static_assert(sizeof(zkm_memory_init_final_event) == 16, "MemoryInitializeFinalizeEvent layout");
+static_assert(sizeof(zkm_syscall_event) == 56, "SyscallEvent layout");
+
+namespace zkm::tg {
+
+constexpr uint32_t P = 0x7f000001u;
+constexpr int NTH = 128;  // rows per workgroup
+
+// Opcode (core/executor/src/opcode.rs:15-75)
+enum Op : uint32_t {
+    ADD = 0, SUB = 1, MULT = 3, MULTU = 4, DIV = 5, DIVU = 6,
+    BEQ = 21, BGEZ = 22, BGTZ = 23, BLEZ = 24, BLTZ = 25, BNE = 26, JUMP = 27, JUMPI = 28, JUMPDIRECT = 29,
+    SYSCALL = 30, LB = 31, LBU = 32, LH = 33, LHU = 34, LW = 35, LWL = 36, LWR = 37, LL = 38,
+    SB = 39, SH = 40, SW = 41, SWL = 42, SWR = 43, SC = 44, INS = 45, MADDU = 46, MSUBU = 47, MADD = 48,
+    MSUB = 49, MEQ = 50, MNE = 51,
+};
+// ByteOpcode (core/executor/src/events/byte.rs) and the Byte chip's multiplicity columns
+constexpr uint32_t B_U8RANGE = 4, B_U16RANGE = 8, BYTE_COLS = ZKM_BYTE_MULT_WIDTH;
+constexpr uint32_t SYS_EXT_GROUP = 4246;  // SyscallCode::SYS_EXT_GROUP (syscalls/code.rs:154)
+
+// instruction predicates (include/instruction.hpp)
+__device__ __forceinline__ bool is_branch(uint32_t op) { return op >= BEQ && op <= BNE; }
+__device__ __forceinline__ bool is_jump(uint32_t op) { return op >= JUMP && op <= JUMPDIRECT; }
+__device__ __forceinline__ bool is_mem(uint32_t op) { return op >= LB && op <= SC; }
+__device__ __forceinline__ bool is_store_except_sc(uint32_t op) { return op >= SB && op <= SWR; }
+__device__ __forceinline__ bool is_maddsub(uint32_t op) { return op >= MADDU && op <= MSUB; }
+__device__ __forceinline__ bool is_mult_div(uint32_t op) { return op == MULT || op == MULTU || op == DIV || op == DIVU; }
+__device__ __forceinline__ bool is_check_memory(uint32_t op) { return op == SYSCALL || is_maddsub(op) || is_mem(op); }
+__device__ __forceinline__ bool is_rw_a(uint32_t op) {
+    return op == SYSCALL || op == INS || is_maddsub(op) || op == MEQ || op == MNE || is_mem(op);
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t x, int i) { return (x >> (8 * i)) & 0xFF; }
+__device__ __forceinline__ void put_word(uint32_t *v, uint32_t x) {  // write_word_from_u32_v2
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = byte_of(x, i);
+}
+
+// Lookup multiplicities (the Byte chip's 65536 x 10 counts, the Program chip's per-instruction
+// counts).  Real traces are skewed — a shard's lookups hit few distinct entries (zero bytes, small
+// timestamp gaps, the shard number) — so global atomics straight from every lane serialise on those
+// entries.  Instead each workgroup (persistent, looping over row tiles) accumulates into an LDS hash
+// table, after merging the lanes of a wave that agree with the first active lane; the table is
+// flushed once per workgroup with one global atomic per distinct key.  Keys that find no slot within
+// a few probes, and lookups known to be spread out (the 16-bit clk limb), go to global memory directly.
+constexpr uint32_t LOG_HS = 11, HS = 1u << LOG_HS, EMPTY = 0xFFFFFFFFu, PROG_KEY = 0x80000000u;
+
+struct Hist {
+    uint32_t *keys, *vals;             // LDS, HS each (null when the chip records no lookups)
+    uint32_t *byte_mult, *program_mult;  // global, nullable
+
+    __device__ __forceinline__ void global_add(uint32_t key, uint32_t cnt) const {
+        if (key & PROG_KEY) {
+            if (program_mult) atomicAdd(program_mult + (key & ~PROG_KEY), cnt);
+        } else if (byte_mult) {
+            atomicAdd(byte_mult + key, cnt);
+        }
+    }
+    __device__ __forceinline__ void insert(uint32_t key, uint32_t cnt) const {
+        uint32_t h = (key * 2654435761u) >> (32 - LOG_HS);
+#pragma unroll 1
+        for (int p = 0; p < 8; p++) {
+            const uint32_t k = atomicCAS(keys + h, EMPTY, key);
+            if (k == EMPTY || k == key) {
+                atomicAdd(vals + h, cnt);
+                return;
+            }
+            h = (h + 1) & (HS - 1);
+        }
+        global_add(key, cnt);
+    }
+    // +1 at `key` for every lane with `on`; called by every lane of the wave (ballots)
+    __device__ __forceinline__ void add(uint32_t key, bool on) const {
+        const uint64_t act = __ballot(on);
+        if (act == 0) return;
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const uint32_t lead = __shfl(key, leader);
+        const uint64_t same = __ballot(on && key == lead);
+        if ((int)(threadIdx.x & 63) == leader) insert(lead, (uint32_t)__popcll(same));
+        if (on && key != lead) insert(key, 1u);
+    }
+    __device__ __forceinline__ void direct(uint32_t key, bool on) const {
+        if (on) global_add(key, 1u);
+    }
+    __device__ __forceinline__ void byte(uint32_t op, uint32_t b, uint32_t c, bool on) const {
+        if (byte_mult) add(((b << 8) | c) * BYTE_COLS + op, on);
+    }
+};
+
+// Persistent workgroups over tiles of NTH rows: (1) the tile's events -> LDS (pitch EP dwords),
+// (2) chip.row(v, event or nullptr, row, hist) per thread, (3) rows -> LDS (pitch W|1) -> 16-byte
+// coalesced stores.  EVS: event stride in dwords, EVW: the leading dwords the row needs.
+template <int EVS, int EVW, int W>
+struct Tile {
+    static constexpr int EP = EVW | 1, RP = W | 1;
+    static constexpr int WORDS = NTH * (EP > RP ? EP : RP);
+};
+
+template <int EVS, int EVW, int W, bool HIST, class Chip>
+__global__ __launch_bounds__(NTH) void k_events_to_rows(const uint32_t *__restrict__ ev, uint64_t n,
+                                                        uint32_t *__restrict__ out, uint64_t nrows, Chip chip,
+                                                        uint32_t *byte_mult, uint32_t *program_mult) {
+    using T = Tile<EVS, EVW, W>;
+    __shared__ uint32_t buf[T::WORDS];
+    __shared__ uint32_t hkeys[HIST ? HS : 1], hvals[HIST ? HS : 1];
+    const uint32_t t = threadIdx.x;
+    Hist hist{hkeys, hvals, byte_mult, program_mult};
+    if constexpr (HIST) {
+        for (uint32_t i = t; i < HS; i += NTH) {
+            hkeys[i] = EMPTY;
+            hvals[i] = 0;
+        }
+    }
+    const uint64_t ntiles = (nrows + NTH - 1) / NTH;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t row0 = tile * NTH;
+        const uint32_t rows = (uint32_t)min<uint64_t>(NTH, nrows - row0);
+        const uint32_t nev = n > row0 ? (uint32_t)min<uint64_t>(rows, n - row0) : 0u;
+        const uint32_t *src = ev + row0 * EVS;
+        __syncthreads();  // the previous tile's stores have read buf; the table is initialised
+        if constexpr (EVS == EVW) {
+            for (uint32_t i = t; i < nev * EVW; i += NTH) {
+                const uint32_t r = i / EVW;
+                buf[r * T::EP + (i - r * EVW)] = src[i];
+            }
+        } else {
+            for (uint32_t i = t; i < nev * EVW; i += NTH) {
+                const uint32_t r = i / EVW, k = i - r * EVW;
+                buf[r * T::EP + k] = src[(uint64_t)r * EVS + k];
+            }
+        }
+        __syncthreads();
+        uint32_t v[W];
+        chip.row(v, t < nev ? buf + t * T::EP : nullptr, row0 + t, hist);
+        __syncthreads();
+        if (t < rows) {
+#pragma unroll
+            for (int c = 0; c < W; c++) buf[t * T::RP + c] = v[c];
+        }
+        __syncthreads();
+        uint32_t *dst = out + row0 * W;
+        const uint32_t total = rows * W;  // rows is a multiple of 16 (heights are powers of two >= 16)
+        for (uint32_t q = t; q < total / 4; q += NTH) {
+            uint32_t w4[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t i = 4 * q + j, r = i / W;
+                w4[j] = buf[r * T::RP + (i - r * W)];
+            }
+            reinterpret_cast<uint4 *>(dst)[q] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+    }
+    if constexpr (HIST) {
+        __syncthreads();
+        for (uint32_t i = t; i < HS; i += NTH)
+            if (hkeys[i] != EMPTY && hvals[i]) hist.global_add(hkeys[i], hvals[i]);
+    }
+}
+
+// ------------------------------------------------------------------ Cpu (include/cpu.hpp:37-108)
+// CpuCols (cpu/columns/mod.rs), canonical u32 per column
+enum {
+    C_SHARD = 0, C_CLK16 = 1, C_CLK8 = 2, C_SHARD_SEND = 3, C_CLK_SEND = 4, C_PC = 5, C_NPC = 6, C_NNPC = 7,
+    C_OPCODE = 8, C_OPA = 9, C_OPB = 10, C_OPC = 14, C_OPA0 = 18, C_IMMB = 19, C_IMMC = 20,
+    C_EXTRA = 21, C_RW_A = 22, C_CHECK_MEM = 23, C_HALT = 24, C_SEQ = 25, C_A_VAL = 26, C_HI_PREV_A = 30,
+    C_A_ACC = 34, C_B_ACC = 47, C_C_ACC = 56, C_REAL = 65, C_A_IMM = 66,
+};
+enum { ACC_VALUE = 0, ACC_PREV_SHARD = 4, ACC_PREV_CLK = 5, ACC_COMPARE = 6, ACC_D16 = 7, ACC_D8 = 8 };
+// CpuEventFfi dword offsets (zkm_tracegen.h): the three operand records, then hi
+enum { E_CLK = 0, E_PC = 1, E_NPC = 2, E_NNPC = 3, E_A = 4, E_AREC = 5, E_B = 17, E_BREC = 18, E_C = 30,
+       E_CREC = 31, E_HI_TAG = 43, E_HI = 44, E_WORDS = 45 };
+// OptionMemoryRecordEnum: tag, read {value, shard, ts, prev_shard, prev_ts}, write {value, shard, ts,
+// prev_value, prev_shard, prev_ts}
+enum { R_TAG = 0, R_READ = 1, R_WRITE = 6 };
+
+struct Access {  // one populated MemoryAccessCols (include/memory.hpp:10-32)
+    bool on;
+    uint32_t value, prev_value, prev_shard, prev_clk, compare, d16, d8;
+};
+
+// populate_read / populate_read_write (include/memory.hpp:34-93) of an OptionMemoryRecordEnum
+__device__ __forceinline__ Access access_of(const uint32_t *rec) {
+    Access a{};
+    const uint32_t tag = rec[R_TAG] & 0xFF;
+    if (tag != ZKM_RECORD_READ && tag != ZKM_RECORD_WRITE) return a;
+    const uint32_t *r = rec + (tag == ZKM_RECORD_READ ? R_READ : R_WRITE);
+    const uint32_t value = r[0], shard = r[1], ts = r[2];
+    const uint32_t prev_value = tag == ZKM_RECORD_READ ? value : r[3];
+    const uint32_t prev_shard = r[tag == ZKM_RECORD_READ ? 3 : 4], prev_ts = r[tag == ZKM_RECORD_READ ? 4 : 5];
+    a.on = true;
+    a.value = value;
+    a.prev_value = prev_value;
+    a.prev_shard = prev_shard;
+    a.prev_clk = prev_ts;
+    const bool cmp = prev_shard == shard;
+    a.compare = cmp;
+    const uint32_t diff_minus_one = (cmp ? ts : shard) - (cmp ? prev_ts : prev_shard) - 1u;
+    a.d16 = diff_minus_one & 0xFFFF;
+    a.d8 = (diff_minus_one >> 16) & 0xFF;
+    return a;
+}
+
+__device__ __forceinline__ void put_access(uint32_t *v, int base, const Access &a) {
+    put_word(v + base + ACC_VALUE, a.value);
+    v[base + ACC_PREV_SHARD] = a.prev_shard;
+    v[base + ACC_PREV_CLK] = a.prev_clk;
+    v[base + ACC_COMPARE] = a.compare;
+    v[base + ACC_D16] = a.d16;
+    v[base + ACC_D8] = a.d8;
+}
+
+struct CpuChip {
+    const uint32_t *program;  // InstructionFfi as 6 dwords each
+    uint64_t program_len;
+    uint32_t pc_base, shard;
+
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_CPU_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        Access acc[3] = {};  // a, b, c
+        uint32_t clk = 0, written = 0, idx = 0;
+        if (real) {
+            clk = e[E_CLK];
+            const uint32_t pc = e[E_PC];
+            idx = (pc - pc_base) >> 2;
+            if (idx >= program_len) idx = (uint32_t)program_len - 1;  // Program::fetch precondition
+            const uint32_t *ins = program + 6 * (uint64_t)idx;
+            const uint32_t opcode = ins[0] & 0xFF, op_a = (ins[0] >> 8) & 0xFF;
+            const uint32_t imm_b = ins[3] & 0xFF, imm_c = (ins[3] >> 8) & 0xFF;
+            // populate_shard_clk
+            v[C_SHARD] = shard;
+            v[C_CLK16] = clk & 0xFFFF;
+            v[C_CLK8] = (clk >> 16) & 0xFF;
+            v[C_PC] = pc;
+            v[C_NPC] = e[E_NPC];
+            v[C_NNPC] = e[E_NNPC];
+            // populate_instruction
+            v[C_OPCODE] = opcode;
+            v[C_OPA] = op_a;
+            put_word(v + C_OPB, ins[1]);
+            put_word(v + C_OPC, ins[2]);
+            v[C_OPA0] = op_a == 0;
+            v[C_IMMB] = imm_b != 0;
+            v[C_IMMC] = imm_c != 0;
+            v[C_A_IMM] = is_store_except_sc(opcode) || is_branch(opcode);
+            v[C_RW_A] = is_rw_a(opcode);
+            const bool check = is_mult_div(opcode) || is_check_memory(opcode);
+            v[C_CHECK_MEM] = check;
+            put_word(v + C_A_VAL, e[E_A]);
+            if ((e[E_HI_TAG] & 0xFF) == 0) put_word(v + C_HI_PREV_A, e[E_HI]);
+            if (check) {
+                v[C_SHARD_SEND] = shard;
+                v[C_CLK_SEND] = clk;
+            }
+            // operand values (cpu.hpp:70-72), then the access records overwrite where present
+            put_word(v + C_A_ACC + 4 + ACC_VALUE, e[E_A]);
+            put_word(v + C_B_ACC + ACC_VALUE, e[E_B]);
+            put_word(v + C_C_ACC + ACC_VALUE, e[E_C]);
+            acc[0] = access_of(e + E_AREC);
+            if ((e[E_BREC] & 0xFF) == ZKM_RECORD_READ) acc[1] = access_of(e + E_BREC);
+            if ((e[E_CREC] & 0xFF) == ZKM_RECORD_READ) acc[2] = access_of(e + E_CREC);
+            if (acc[0].on) {
+                put_word(v + C_A_ACC, acc[0].prev_value);
+                put_access(v, C_A_ACC + 4, acc[0]);
+            }
+            if (acc[1].on) put_access(v, C_B_ACC, acc[1]);
+            if (acc[2].on) put_access(v, C_C_ACC, acc[2]);
+            written = acc[0].on ? acc[0].value : e[E_A];
+            bool halt = false;
+            if (opcode == SYSCALL) {
+                const uint32_t id0 = v[C_A_ACC + 0], id1 = v[C_A_ACC + 1];
+                halt = (id0 == 0 && id1 == 0) || (id0 == (SYS_EXT_GROUP & 0xFF) && id1 == ((SYS_EXT_GROUP >> 8) & 0xFF));
+                v[C_HALT] = halt;
+                v[C_EXTRA] = v[C_A_ACC + 3];
+            }
+            v[C_SEQ] = !halt && !is_branch(opcode) && !is_jump(opcode);
+            v[C_REAL] = 1;
+        } else {  // padding row (cpu/trace.rs:60-66)
+            v[C_IMMB] = 1;
+            v[C_IMMC] = 1;
+            v[C_RW_A] = 1;
+        }
+        // Byte lookups (cpu/trace.rs:206-247, MemoryAccessCols::populate): every lane takes part
+        h.byte(B_U16RANGE, shard >> 8, shard & 0xFF, real);
+        if (h.byte_mult) h.direct(((clk & 0xFFFF) * BYTE_COLS) + B_U16RANGE, real);  // distinct per row
+        h.byte(B_U8RANGE, 0, (clk >> 16) & 0xFF, real);
+#pragma unroll
+        for (int k = 2; k >= 0; k--) {  // c, b, a: the order the executor reads them
+            h.byte(B_U16RANGE, acc[k].d16 >> 8, acc[k].d16 & 0xFF, real && acc[k].on);
+            h.byte(B_U8RANGE, 0, acc[k].d8, real && acc[k].on);
+        }
+        h.byte(B_U8RANGE, byte_of(written, 0), byte_of(written, 1), real);
+        h.byte(B_U8RANGE, byte_of(written, 2), byte_of(written, 3), real);
+        if (h.program_mult) h.add(PROG_KEY | idx, real);
+    }
+};
+
+// ------------------------------------------------------------------ AddSub (include/add_sub.hpp:9-39)
+enum { AS_PC = 0, AS_NPC = 1, AS_VAL = 2, AS_CARRY = 6, AS_OP1 = 9, AS_OP2 = 13, AS_ADD = 17, AS_SUB = 18 };
+
+struct AddSubChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_ADD_SUB_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        uint32_t x = 0, y = 0, sum = 0;
+        if (real) {  // AluEvent: pc, next_pc, opcode, hi, a, b, c
+            const bool is_add = (e[2] & 0xFF) == ADD;
+            x = is_add ? e[5] : e[4];
+            y = e[6];
+            sum = x + y;
+            v[AS_PC] = e[0];
+            v[AS_NPC] = e[1];
+            v[AS_ADD] = is_add;
+            v[AS_SUB] = !is_add;
+            uint32_t carry = 0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {  // AddOperation::populate
+                carry = (byte_of(x, k) + byte_of(y, k) + carry) > 0xFF;
+                v[AS_CARRY + k] = carry;
+            }
+            put_word(v + AS_VAL, sum);
+            put_word(v + AS_OP1, x);
+            put_word(v + AS_OP2, y);
+        }
+        const uint32_t words[3] = {x, y, sum};
+#pragma unroll
+        for (int w = 0; w < 3; w++) {
+            h.byte(B_U8RANGE, byte_of(words[w], 0), byte_of(words[w], 1), real);
+            h.byte(B_U8RANGE, byte_of(words[w], 2), byte_of(words[w], 3), real);
+        }
+    }
+};
+
+// ------------------------------------------------------------------ MemoryLocal (include/memory_local.hpp:8-20)
+// one SingleMemoryLocal (14 columns) per event; a trace row holds four
+struct MemoryLocalChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < 14; c++) v[c] = 0;
+        if (!e) return;
+        v[0] = e[0];            // addr
+        v[1] = e[1];            // initial_shard
+        v[2] = e[4];            // final_shard
+        v[3] = e[2];            // initial_clk
+        v[4] = e[5];            // final_clk
+        put_word(v + 5, e[3]);  // initial_value
+        put_word(v + 9, e[6]);  // final_value
+        v[13] = 1;              // is_real
+    }
+};
+
+// ------------------------------------------------------------------ MemoryGlobalInit/Finalize
+// (include/memory_global.hpp:9-43 per row; memory/global.rs:133-181 across rows)
+enum { MG_SHARD = 0, MG_TS = 1, MG_ADDR = 2, MG_LT = 3, MG_BITS = 35, MG_AND = 67, MG_VALUE = 73, MG_REAL = 105,
+       MG_NEXT_COMP = 106, MG_IZ_INV = 107, MG_IZ_RES = 108, MG_FIRST_COMP = 109, MG_LAST_ADDR = 110 };
+
+struct MemoryGlobalChip {
+    const uint32_t *events;  // 4 dwords each: addr, value, shard, timestamp
+    uint64_t n;
+    uint32_t prev_addr, prev_addr_inv;
+
+    __device__ __forceinline__ static void lt_flags(uint32_t *v, uint32_t a, uint32_t b) {
+        const uint32_t x = a ^ b;  // AssertLtColsBits: the most significant differing bit
+        const int top = x ? 31 - __builtin_clz(x) : -1;
+#pragma unroll
+        for (int i = 0; i < 32; i++) v[MG_LT + i] = i == top;
+    }
+
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t r, const Hist &) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_MEMORY_GLOBAL_WIDTH; c++) v[c] = 0;
+        if (r == 0) {  // IsZeroOperation(prev_addr) on the first row, also with no events
+            v[MG_IZ_INV] = prev_addr_inv;
+            v[MG_IZ_RES] = prev_addr == 0;
+        }
+        if (!e) return;
+        const uint32_t addr = e[0], value = e[1];
+        v[MG_SHARD] = e[2];
+        v[MG_TS] = e[3];
+        v[MG_ADDR] = addr;
+#pragma unroll
+        for (int i = 0; i < 32; i++) v[MG_BITS + i] = (addr >> i) & 1;
+        uint32_t acc = ((addr >> 24) & 1) * ((addr >> 25) & 1);
+        v[MG_AND] = acc;
+#pragma unroll
+        for (int k = 1; k < 6; k++) {
+            acc *= (addr >> (25 + k)) & 1;
+            v[MG_AND + k] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < 32; i++) v[MG_VALUE + i] = (value >> i) & 1;
+        v[MG_REAL] = 1;
+        if (r == 0) {
+            v[MG_FIRST_COMP] = prev_addr != 0;
+            if (prev_addr != 0) lt_flags(v, prev_addr, addr);
+        } else {
+            v[MG_NEXT_COMP] = 1;
+            lt_flags(v, events[4 * (r - 1)], addr);
+        }
+        if (r == n - 1) v[MG_LAST_ADDR] = 1;
+    }
+};
+
+// ------------------------------------------------------------------ Syscall (include/syscall.hpp:8-16)
+struct SyscallChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_SYSCALL_WIDTH; c++) v[c] = 0;
+        if (!e) return;
+        v[0] = e[2];   // shard
+        v[1] = e[3];   // clk
+        v[2] = e[11];  // syscall_id
+        v[3] = e[12];  // arg1
+        v[4] = e[13];  // arg2
+        v[5] = 1;      // is_real
+    }
+};
+
+template <int EVS, int EVW, int W, bool HIST, class Chip>
+int launch(const void *events, uint64_t n, uint32_t *trace, uint64_t nrows, const Chip &chip, void *stream,
+           const char *what, uint32_t *byte_mult = nullptr, uint32_t *program_mult = nullptr) {
+    if (!trace || (n && !events) || n > nrows || nrows < 16 || (nrows & (nrows - 1))) {
+        g_last_error = std::string(what) + ": bad arguments (need n <= height, height a power of two >= 16)";
+        return ZKM_ERR_ARG;
+    }
+    auto kern = k_events_to_rows<EVS, EVW, W, HIST, Chip>;
+    // persistent grid: as many workgroups as fit on the device at once (each loops over tiles, so the
+    // LDS tables are flushed once per resident workgroup)
+    static const uint64_t resident = [&] {
+        int dev = 0, cus = 256, per_cu = 1;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NTH, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        return (uint64_t)cus * (uint64_t)per_cu;
+    }();
+    const uint64_t tiles = (nrows + NTH - 1) / NTH;
+    const uint64_t blocks = tiles < resident ? tiles : resident;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(NTH), 0, (hipStream_t)stream, (const uint32_t *)events, n,
+                       trace, nrows, chip, byte_mult, program_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string(what) + ": " + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+uint32_t inv_mod_p(uint32_t x) {
+    uint64_t r = 1, b = x % P, e = P - 2;
+    while (e) {
+        if (e & 1) r = r * b % P;
+        b = b * b % P;
+        e >>= 1;
+    }
+    return (uint32_t)r;
+}
+
+}  // namespace zkm::tg
+
+using namespace zkm::tg;
+
+extern "C" {
+
+int zkm_cpu_events_to_trace(const zkm_cpu_event_ffi *events, uint64_t n, uint32_t shard,
+                            const zkm_instruction_ffi *program, uint64_t program_len, uint32_t pc_base,
+                            uint32_t *trace, uint64_t height, uint32_t *byte_mult, uint32_t *program_mult,
+                            void *stream) {
+    if (n && (!program || program_len == 0)) {
+        g_last_error = "zkm_cpu_events_to_trace: empty program";
+        return ZKM_ERR_ARG;
+    }
+    CpuChip chip{(const uint32_t *)program, program_len, pc_base, shard};
+    return launch<70, E_WORDS, ZKM_CPU_WIDTH, true>(events, n, trace, height, chip, stream, "zkm_cpu_events_to_trace",
+                                                    byte_mult, program_mult);
+}
+
+int zkm_add_sub_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                uint32_t *byte_mult, void *stream) {
+    AddSubChip chip{};
+    return launch<7, 7, ZKM_ADD_SUB_WIDTH, true>(events, n, trace, height, chip, stream, "zkm_add_sub_events_to_trace",
+                                                 byte_mult);
+}
+
+int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,
+                                     uint64_t height, void *stream) {
+    if (height < 16 || (height & (height - 1)) || n > 4 * height) {
+        g_last_error = "zkm_memory_local_events_to_trace: bad arguments";
+        return ZKM_ERR_ARG;
+    }
+    MemoryLocalChip chip{};
+    return launch<7, 7, 14, false>(events, n, trace, 4 * height, chip, stream, "zkm_memory_local_events_to_trace");
+}
+
+int zkm_memory_global_events_to_trace(const zkm_memory_init_final_event *events, uint64_t n, int is_receive,
+                                      uint32_t prev_addr, uint32_t *trace, uint64_t height, void *stream) {
+    (void)is_receive;  // the columns are the same for both chips (memory_global.hpp:11-20 builds an unused record)
+    MemoryGlobalChip chip{(const uint32_t *)events, n, prev_addr, prev_addr ? inv_mod_p(prev_addr) : 0u};
+    return launch<4, 4, ZKM_MEMORY_GLOBAL_WIDTH, false>(events, n, trace, height, chip, stream,
+                                                 "zkm_memory_global_events_to_trace");
+}
+
+int zkm_syscall_events_to_trace(const zkm_syscall_event *events, uint64_t n, int is_receive, uint32_t *trace,
+                                uint64_t height, void *stream) {
+    (void)is_receive;  // syscall.hpp:8-16: the same row for SyscallCore and SyscallPrecompile
+    SyscallChip chip{};
+    return launch<14, 14, ZKM_SYSCALL_WIDTH, false>(events, n, trace, height, chip, stream, "zkm_syscall_events_to_trace");
+}
+
+}  // extern "C"

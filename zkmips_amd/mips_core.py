@@ -1624,10 +1624,12 @@ def initial_registers(seed: int):
     return [0] + [int(x) for x in init[1:]]
 
 
-def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24) // 5 - 1, state=None, regs=None):
+def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24) // 5 - 1, state=None, regs=None,
+                  capture: dict = None):
     """(machine, prep_traces, traces, public_values) of one shard executing `prog` from PC_BASE to its end
     (at most max_steps instructions: the CPU clk is range-checked to 24 bits).  With `state` and `regs`
-    (program_shards), the shard continues a longer execution and stops after about max_steps."""
+    (program_shards), the shard continues a longer execution and stops after about max_steps.  With
+    `capture` (a dict), the executor's records are left there for zkmips_amd.tracegen (device traces)."""
     if state is None:
         regs = initial_registers(seed)
     start_pc = state["pc"] if state else PC_BASE
@@ -1756,6 +1758,9 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     rec = np.concatenate([np.zeros(len(smsg), np.uint8), grec])
     kinds = np.concatenate([np.full(len(smsg), SY.KIND_SYSCALL, np.uint32), np.full(len(gmsg), KIND_MEMORY, np.uint32)])
     traces["Global"], _ = MM.global_trace(msg, rec, kinds, byte_lookup)
+    if capture is not None:
+        capture.update(steps=steps, alu=ev, syscalls=sc, core_syscalls=sc[tab] if len(sc) else sc, entries=ent,
+                       shard=shard, prog=prog)
 
     assert mult.max() < P
     traces["Byte"] = mult.astype(np.uint32)

@@ -16,7 +16,8 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import ChallengerState, Config, Device, Matrix, as_u32, check, lib, matrix
+from ._lib import (ZKM_MEM_DEVICE, ZKM_REPR_CANONICAL, ChallengerState, Config, Device, Matrix, as_u32, check, lib,
+                   matrix)
 from .machine import MachineDesc
 
 # CURVE_CUMULATIVE_SUM_START_{X,Y} (crates/stark/src/septic_digest.rs:9-14): SepticDigest::zero()
@@ -35,6 +36,19 @@ class ShardMainData:
         if self.h:
             lib().zkm_main_free(self.h)
             self.h = None
+
+
+def _device_matrix(tensor, name: str, keep: list) -> Matrix:
+    """A row-major GPU tensor as a ZKM_MEM_DEVICE matrix; waits for the producing stream first (the
+    prover's kernels run on streams of their own)."""
+    import torch
+    if not tensor.is_cuda or tensor.dim() != 2 or not tensor.is_contiguous() or tensor.element_size() != 4:
+        raise ValueError(f"trace {name}: need a contiguous 2-D 32-bit tensor on the GPU")
+    torch.cuda.current_stream(tensor.device).synchronize()
+    nm = name.encode()
+    keep.append(nm)
+    keep.append(tensor)
+    return Matrix(nm, tensor.data_ptr(), tensor.shape[0], tensor.shape[1], ZKM_REPR_CANONICAL | ZKM_MEM_DEVICE)
 
 
 class HipProver:
@@ -97,9 +111,12 @@ class HipProver:
 
     def prove_shard(self, traces: Dict[str, np.ndarray], public_values: np.ndarray,
                     challenger: Optional[ChallengerState] = None) -> bytes:
+        """Traces are host arrays or GPU-resident int32 torch tensors (e.g. from zkmips_amd.tracegen),
+        which cross the ABI as ZKM_MEM_DEVICE matrices."""
         base = challenger if challenger is not None else self.base_challenger()
         keep: list = []
-        arr = (Matrix * len(traces))(*[matrix(t, n, False, keep) for n, t in traces.items()])
+        arr = (Matrix * len(traces))(*[_device_matrix(t, n, keep) if hasattr(t, "data_ptr") else
+                                       matrix(t, n, False, keep) for n, t in traces.items()])
         pv = as_u32(public_values)
         out = C.POINTER(C.c_uint8)()
         n = C.c_uint64()

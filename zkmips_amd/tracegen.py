@@ -1,0 +1,285 @@
+"""Device trace generation (include/zkm_tracegen.h).
+
+The reference fills trace rows through a native per-row ABI (crates/core/machine/src/sys.rs:14-42 ->
+cpp/extern.cpp:6-37) from its executor's event records.  Here the same records — numpy structured
+arrays with the reference's #[repr(C)] layouts, byte for byte — go to the GPU and one launch per
+chip fills the whole padded trace in HBM, plus the Byte and Program chips' multiplicities.  The
+converters below build those records from this repository's executor (mips_core._execute via
+program_shard(capture=...)); a Rust caller hands its own `Vec<CpuEvent>` (as CpuEventFfi) etc.
+
+No fallback: every call goes to libzkm_hip.so and raises if it is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from . import mips_alu as A
+from . import mips_core as MC
+
+u1, u4 = np.uint8, np.uint32
+
+# OptionMemoryRecordEnum (events/cpu.rs:100-139): tag u8, MemoryReadRecord at 4, MemoryWriteRecord at 24
+RECORD = np.dtype({"names": ["tag", "read", "write"], "formats": [u1, (u4, 5), (u4, 6)], "offsets": [0, 4, 24],
+                   "itemsize": 48})
+REC_READ, REC_WRITE, REC_NONE = 0, 1, 2
+# CpuEventFfi (events/cpu.rs:46-75)
+CPU_EVENT = np.dtype({
+    "names": ["clk", "pc", "next_pc", "next_next_pc", "a", "a_record", "b", "b_record", "c", "c_record", "hi_tag",
+              "hi", "hi_record", "memory_record", "exit_code"],
+    "formats": [u4, u4, u4, u4, u4, RECORD, u4, RECORD, u4, RECORD, u1, u4, RECORD, RECORD, u4],
+    "offsets": [0, 4, 8, 12, 16, 20, 68, 72, 120, 124, 172, 176, 180, 228, 276], "itemsize": 280})
+# InstructionFfi (instruction.rs:29-45): opcode u8, op_a u8, op_b, op_c, imm_b, imm_c, raw: OptionU32
+INSTRUCTION = np.dtype({"names": ["opcode", "op_a", "op_b", "op_c", "imm_b", "imm_c", "raw_tag", "raw"],
+                        "formats": [u1, u1, u4, u4, u1, u1, u1, u4], "offsets": [0, 1, 4, 8, 12, 13, 16, 20],
+                        "itemsize": 24})
+# AluEvent (events/instr.rs:10-27)
+ALU_EVENT = np.dtype({"names": ["pc", "next_pc", "opcode", "hi", "a", "b", "c"],
+                      "formats": [u4, u4, u1, u4, u4, u4, u4], "offsets": [0, 4, 8, 12, 16, 20, 24], "itemsize": 28})
+# MemoryLocalEvent (events/memory.rs:225-236): addr, initial (shard, timestamp, value), final (...)
+MEMORY_LOCAL_EVENT = np.dtype({"names": ["addr", "initial", "final"], "formats": [u4, (u4, 3), (u4, 3)],
+                               "offsets": [0, 4, 16], "itemsize": 28})
+# MemoryInitializeFinalizeEvent (events/memory.rs:135-148)
+MEMORY_INIT_FINAL_EVENT = np.dtype({"names": ["addr", "value", "shard", "timestamp"], "formats": [u4] * 4,
+                                    "offsets": [0, 4, 8, 12], "itemsize": 16})
+# SyscallEvent (events/syscall.rs:8-29)
+SYSCALL_EVENT = np.dtype({"names": ["pc", "next_pc", "shard", "clk", "a_record", "a_record_is_real", "syscall_id",
+                                    "arg1", "arg2"],
+                          "formats": [u4, u4, u4, u4, (u4, 6), u1, u4, u4, u4],
+                          "offsets": [0, 4, 8, 12, 16, 40, 44, 48, 52], "itemsize": 56})
+
+CPU_WIDTH, ADD_SUB_WIDTH, MEMORY_LOCAL_WIDTH, MEMORY_GLOBAL_WIDTH, SYSCALL_WIDTH = 67, 19, 56, 111, 6
+
+
+# ---------------------------------------------------------------- records from this repository's executor
+def program_ffi(prog) -> np.ndarray:
+    """Program::instructions as InstructionFfi (prog rows: opcode, op_a, op_b, op_c, imm_b, imm_c)."""
+    P_ = np.asarray(prog, np.int64).reshape(-1, 6)
+    out = np.zeros(len(P_), INSTRUCTION)
+    out["opcode"], out["op_a"] = P_[:, 0], P_[:, 1]
+    out["op_b"], out["op_c"] = P_[:, 2] & 0xFFFFFFFF, P_[:, 3] & 0xFFFFFFFF
+    out["imm_b"], out["imm_c"] = P_[:, 4], P_[:, 5]
+    out["raw_tag"] = 1  # None
+    return out
+
+
+def cpu_events(steps, shard: int) -> np.ndarray:
+    """CpuEvent records (events/cpu.rs:8-44 as CpuEventFfi) of the executor's steps: the op_a access a
+    write (a read when the value is unchanged), op_b / op_c reads unless immediate (executor.rs
+    rr/rw at MemoryAccessPosition A = 3, B = 2, C = 1)."""
+    n = len(steps)
+    e = np.zeros(n, CPU_EVENT)
+    if not n:
+        return e
+    S = np.asarray([s_[:11] for s_ in steps], np.int64)
+    ks, av, bv, cv, prev_a, written = S[:, 0], S[:, 2], S[:, 3], S[:, 4], S[:, 5], S[:, 6]
+    immb, immc = S[:, 9].astype(bool), S[:, 10].astype(bool)
+    clk = np.asarray([s_[13] for s_ in steps], np.int64)
+    prev = np.asarray([[p if p is not None else (0, 0) for p in s_[11]] for s_ in steps], np.int64)  # c, b, a
+    his = np.asarray([s_[12] for s_ in steps], np.int64)
+    e["clk"], e["pc"] = clk, MC.PC_BASE + 4 * ks
+    e["next_pc"], e["next_next_pc"] = S[:, 7], S[:, 8]
+    e["a"], e["b"], e["c"] = av, bv, cv
+    is_write = written != prev_a
+    ar = e["a_record"]
+    ar["tag"] = np.where(is_write, REC_WRITE, REC_READ)
+    w = np.stack([written, np.full(n, shard), clk + MC.POS_A, prev_a, prev[:, 2, 0], prev[:, 2, 1]], axis=1)
+    ar["write"] = np.where(is_write[:, None], w, 0)
+    ar["read"] = np.where(is_write[:, None], 0, w[:, [0, 1, 2, 4, 5]])
+    for field, val, pos, j, imm in (("b_record", bv, MC.POS_B, 1, immb), ("c_record", cv, MC.POS_C, 0, immc)):
+        r = e[field]
+        r["tag"] = np.where(imm, REC_NONE, REC_READ)
+        rd = np.stack([val, np.full(n, shard), clk + pos, prev[:, j, 0], prev[:, j, 1]], axis=1)
+        r["read"] = np.where(imm[:, None], 0, rd)
+    e["hi_tag"] = np.where(his != 0, 0, 1)
+    e["hi"] = his
+    e["hi_record"]["tag"] = REC_NONE
+    e["memory_record"]["tag"] = REC_NONE
+    return e
+
+
+def alu_events(op, a, b, c, pc, npc=None) -> np.ndarray:
+    """AluEvent records (events/instr.rs:10-27)."""
+    n = len(op)
+    e = np.zeros(n, ALU_EVENT)
+    e["pc"], e["opcode"], e["a"], e["b"], e["c"] = pc, op, a, b, c
+    e["next_pc"] = np.asarray(pc, np.int64) + 4 if npc is None else npc
+    return e
+
+
+def memory_local_events(entries) -> np.ndarray:
+    """MemoryLocalEvent records of (addr, initial shard, clk, value, final shard, clk, value) rows."""
+    E = np.asarray(entries, np.int64).reshape(-1, 7)
+    e = np.zeros(len(E), MEMORY_LOCAL_EVENT)
+    e["addr"] = E[:, 0]
+    e["initial"] = E[:, 1:4]
+    e["final"] = E[:, 4:7]
+    return e
+
+
+def memory_init_final_events(events) -> np.ndarray:
+    """MemoryInitializeFinalizeEvent records of (addr, value, shard, timestamp) rows, sorted by addr
+    (MemoryGlobalChip::generate_trace sorts them, memory/global.rs:117-121)."""
+    E = np.asarray(events, np.int64).reshape(-1, 4)
+    E = E[np.argsort(E[:, 0], kind="stable")]
+    e = np.zeros(len(E), MEMORY_INIT_FINAL_EVENT)
+    e["addr"], e["value"], e["shard"], e["timestamp"] = E[:, 0], E[:, 1], E[:, 2], E[:, 3]
+    return e
+
+
+def syscall_events(syscalls) -> np.ndarray:
+    """SyscallEvent records of the executor's syscall tuples (pc, next_pc, shard, clk, a, b, c, prev_a, id)."""
+    S = np.asarray(syscalls, np.int64).reshape(-1, 9)
+    e = np.zeros(len(S), SYSCALL_EVENT)
+    e["pc"], e["next_pc"], e["shard"], e["clk"] = S[:, 0], S[:, 1], S[:, 2], S[:, 3]
+    e["a_record"] = np.stack([S[:, 4], S[:, 2], S[:, 3] + MC.POS_A, S[:, 7], np.zeros(len(S)), np.zeros(len(S))],
+                             axis=1)
+    e["a_record_is_real"] = 1
+    e["syscall_id"], e["arg1"], e["arg2"] = S[:, 8], S[:, 5], S[:, 6]
+    return e
+
+
+def add_sub_records(alu) -> np.ndarray:
+    """The AddSub chip's AluEvents from the executor's ALU event lists (kind "add")."""
+    ev = alu["add"]
+    if not len(ev):
+        return np.zeros(0, ALU_EVENT)
+    op, a, b, c, pc, npc = MC._ev_arrays(ev)
+    return alu_events(op, a, b, c, pc, npc)
+
+
+# ---------------------------------------------------------------- device entry points
+def _bind():
+    L = _lib.lib()
+    if not getattr(L, "_tracegen_bound", False):
+        vp, u64 = C.c_void_p, C.c_uint64
+        L.zkm_cpu_events_to_trace.argtypes = [vp, u64, C.c_uint32, vp, u64, C.c_uint32, vp, u64, vp, vp, vp]
+        L.zkm_add_sub_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
+        L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
+        L.zkm_syscall_events_to_trace.argtypes = [vp, u64, C.c_int, vp, u64, vp]
+        L._tracegen_bound = True
+    return L
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def to_device(records: np.ndarray):
+    """A structured record array as a uint8 torch tensor on the current GPU (the record dtypes above:
+    numpy operations that repack a padded dtype, e.g. np.resize, must not have touched it)."""
+    torch = _torch()
+    if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
+                             SYSCALL_EVENT):
+        raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
+    raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
+    return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _records(t, n: int, dtype: np.dtype, what: str):
+    """The device pointer of n records of `dtype` in tensor t, after checking t holds them (the ABI
+    takes bare pointers: a short buffer would be read past its end)."""
+    if n and (t is None or not t.is_cuda or t.numel() * t.element_size() < n * dtype.itemsize):
+        raise ValueError(f"{what}: need {n} records of {dtype.itemsize} bytes on the GPU")
+    return _ptr(t)
+
+
+def _words(t, n: int, what: str):
+    if t is not None and (not t.is_cuda or not t.is_contiguous() or t.element_size() != 4 or t.numel() < n):
+        raise ValueError(f"{what}: need a contiguous 32-bit GPU tensor of at least {n} values")
+    return _ptr(t)
+
+
+def _stream():
+    return _torch().cuda.current_stream().cuda_stream
+
+
+def _pow2(n: int) -> int:
+    return max(16, 1 << max(0, (n - 1).bit_length()))
+
+
+def _trace(height: int, width: int):
+    torch = _torch()
+    return torch.empty((height, width), dtype=torch.int32, device="cuda")
+
+
+def cpu_trace(events_dev, n: int, shard: int, program_dev, program_len: int, height: int = None, byte_mult=None,
+              program_mult=None, pc_base: int = MC.PC_BASE):
+    """Cpu main trace (height x 67 int32 on the GPU) from n CpuEventFfi records on the GPU."""
+    height = height or _pow2(n)
+    t = _trace(height, CPU_WIDTH)
+    what = "zkm_cpu_events_to_trace"
+    _lib.check(_bind().zkm_cpu_events_to_trace(_records(events_dev, n, CPU_EVENT, what), n, shard,
+                                                _records(program_dev, program_len, INSTRUCTION, what), program_len,
+                                                pc_base, t.data_ptr(), height, _words(byte_mult, 65536 * 10, what),
+                                                _words(program_mult, program_len, what), _stream()), what)
+    return t
+
+
+def add_sub_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    height = height or _pow2(n)
+    t = _trace(height, ADD_SUB_WIDTH)
+    what = "zkm_add_sub_events_to_trace"
+    _lib.check(_bind().zkm_add_sub_events_to_trace(_records(events_dev, n, ALU_EVENT, what), n, t.data_ptr(), height,
+                                                    _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
+def memory_local_trace(events_dev, n: int, height: int = None):
+    height = height or _pow2((n + 3) // 4)
+    t = _trace(height, MEMORY_LOCAL_WIDTH)
+    what = "zkm_memory_local_events_to_trace"
+    _lib.check(_bind().zkm_memory_local_events_to_trace(_records(events_dev, n, MEMORY_LOCAL_EVENT, what), n,
+                                                         t.data_ptr(), height, _stream()), what)
+    return t
+
+
+def memory_global_trace(events_dev, n: int, initialize: bool, prev_addr: int = 0, height: int = None):
+    height = height or _pow2(n)
+    t = _trace(height, MEMORY_GLOBAL_WIDTH)
+    what = "zkm_memory_global_events_to_trace"
+    _lib.check(_bind().zkm_memory_global_events_to_trace(_records(events_dev, n, MEMORY_INIT_FINAL_EVENT, what), n,
+                                                          0 if initialize else 1, prev_addr, t.data_ptr(), height,
+                                                          _stream()), what)
+    return t
+
+
+def syscall_trace(events_dev, n: int, height: int = None):
+    height = height or _pow2(n)
+    t = _trace(height, SYSCALL_WIDTH)
+    what = "zkm_syscall_events_to_trace"
+    _lib.check(_bind().zkm_syscall_events_to_trace(_records(events_dev, n, SYSCALL_EVENT, what), n, 0, t.data_ptr(),
+                                                    height, _stream()), what)
+    return t
+
+
+def shard_traces(capture: dict, byte_mult=None):
+    """Device traces of the chips the reference's row ABI covers, for one executed shard
+    (program_shard(..., capture=c)): Cpu (+ Program multiplicities), AddSub, MemoryLocal and
+    SyscallCore, with their Byte lookups added into `byte_mult` (65536 x 10 int32 on the GPU) if
+    given.  Returns {chip name: GPU tensor}."""
+    torch = _torch()
+    shard, prog = capture["shard"], capture["prog"]
+    ev = cpu_events(capture["steps"], shard)
+    pf = program_ffi(prog)
+    pm = torch.zeros((_pow2(len(pf)), 1), dtype=torch.int32, device="cuda")
+    out = {"Cpu": cpu_trace(to_device(ev), len(ev), shard, to_device(pf), len(pf), byte_mult=byte_mult,
+                            program_mult=pm),
+           "Program": pm}
+    adds = add_sub_records(capture["alu"])
+    if len(adds):
+        out["AddSub"] = add_sub_trace(to_device(adds), len(adds), byte_mult=byte_mult)
+    ml = memory_local_events(capture["entries"])
+    out["MemoryLocal"] = memory_local_trace(to_device(ml), len(ml))
+    if len(capture["core_syscalls"]):
+        sc = syscall_events(capture["core_syscalls"])
+        out["SyscallCore"] = syscall_trace(to_device(sc), len(sc))
+    return out
