@@ -320,7 +320,8 @@ def tracegen_bench(args):
     in HBM, Byte and Program multiplicities included; plus AddSub (19 columns) and MemoryLocal.  The
     records are a real execution (mips_core.loop_program, 2^14 instructions) tiled to 2^log_n rows.
     HBM-bound: per Cpu row 280 B of record read + 268 B of trace written (+ the program fetch and the
-    multiplicity atomics, served by L2)."""
+    multiplicity atomics, served by L2).  Global: 2^log_n random messages lifted onto the septic curve
+    and scanned (compute-bound; the host restatement takes ≈18 s for 2^22 on 8 cores)."""
     import torch
     from zkmips_amd import mips_core as MC
     from zkmips_amd import tracegen as TG
@@ -337,9 +338,14 @@ def tracegen_bench(args):
     d_ev, d_prog, d_add, d_ml = (TG.to_device(x) for x in (ev, prog, adds, ml))
     bm = torch.zeros((65536, 10), dtype=torch.int32, device="cuda")
     pm = torch.zeros((len(prog), 1), dtype=torch.int32, device="cuda")
+    rng = np.random.default_rng(5)
+    gmsg = rng.integers(0, 256, (n, 7)).astype(np.uint32)
+    gmsg[:, 0], gmsg[:, 1], gmsg[:, 2] = 1, rng.integers(0, 1 << 24, n), rng.integers(0, 1 << 30, n)
+    d_glob = TG.to_device(TG.global_events(gmsg, rng.integers(0, 2, n), np.ones(n)))
     chips = {
         "Cpu": (lambda: TG.cpu_trace(d_ev, n, 1, d_prog, len(prog), height=n, byte_mult=bm, program_mult=pm),
                 280 + 4 * TG.CPU_WIDTH),
+        "Global": (lambda: TG.global_trace(d_glob, n, height=n, byte_mult=bm), 32 + 4 * TG.GLOBAL_WIDTH),
         "AddSub": (lambda: TG.add_sub_trace(d_add, n, height=n, byte_mult=bm), 28 + 4 * TG.ADD_SUB_WIDTH),
         "MemoryLocal": (lambda: TG.memory_local_trace(d_ml, n, height=n // 4), 28 + 4 * 14),
     }

@@ -11,6 +11,8 @@
  *                                                                                  (include/memory_global.hpp:9-43)
  *   syscall_event_to_row_koalabear(const SyscallEvent*, bool, SyscallCols*)        (include/syscall.hpp:8-16)
  *
+ * and, beyond that ABI, the Global chip (the reference's Rust generate_trace, global/mod.rs:77-196).
+ *
  * Here each entry point fills a WHOLE padded trace in GPU memory from an event array in GPU memory:
  * one thread per row, rows staged through LDS so the row-major trace is written in full cache
  * lines; padding rows get the chip's padding values, so the buffer needs no clearing.  The parts
@@ -93,12 +95,16 @@ typedef struct {
     uint32_t syscall_id, arg1, arg2;
 } zkm_syscall_event;
 
+/* GlobalLookupEvent (core/executor/src/events/global.rs:6-15), 32 bytes */
+typedef struct { uint32_t message[7]; uint8_t is_receive; uint8_t kind; } zkm_global_lookup_event;
+
 /* Trace widths (columns) of the chips filled here. */
 #define ZKM_CPU_WIDTH 67
 #define ZKM_ADD_SUB_WIDTH 19
 #define ZKM_MEMORY_LOCAL_WIDTH 56      /* 4 SingleMemoryLocal of 14 per row (memory/local.rs:26) */
 #define ZKM_MEMORY_GLOBAL_WIDTH 111
 #define ZKM_SYSCALL_WIDTH 6
+#define ZKM_GLOBAL_WIDTH 99
 #define ZKM_BYTE_MULT_WIDTH 10         /* Byte chip main trace: 65536 rows x 10 (bytes/columns.rs) */
 
 /* Cpu: rows [0, n) from events[i] with instruction program[(pc - pc_base) / 4] (Program::fetch),
@@ -129,6 +135,16 @@ int zkm_memory_global_events_to_trace(const zkm_memory_init_final_event *events,
 /* SyscallCore / SyscallPrecompile (syscall/chip.rs:138-183). */
 int zkm_syscall_events_to_trace(const zkm_syscall_event *events, uint64_t n, int is_receive, uint32_t *trace,
                                 uint64_t height, void *stream);
+
+/* Global (global/mod.rs:77-196): each message lifted onto the septic curve y^2 = x^3 + 3z x - 3 over
+ * F_p[z]/(z^7 + 2z - 8) with the smallest offset (GlobalLookupOperation::populate), the running sum
+ * of the points from the zero digest as a parallel scan (the reference's par_iter().scan), padding
+ * rows with the dummy point, U16Range(message[0]) into byte_mult (nullable).  final_digest (device,
+ * nullable): the shard's global cumulative sum, 14 canonical words (x then y).  Synchronises `stream`
+ * before returning; ZKM_ERR_UNSATISFIED if a message has no lift, the running sum reaches infinity
+ * or message[0] is not 16-bit. */
+int zkm_global_events_to_trace(const zkm_global_lookup_event *events, uint64_t n, uint32_t *trace,
+                               uint64_t height, uint32_t *byte_mult, uint32_t *final_digest, void *stream);
 
 #ifdef __cplusplus
 }

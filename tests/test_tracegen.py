@@ -33,6 +33,7 @@ LAYOUTS = {
                                                       "final": "final_mem_access"}),
     "zkm_memory_init_final_event": (TG.MEMORY_INIT_FINAL_EVENT, {f: f for f in TG.MEMORY_INIT_FINAL_EVENT.names}),
     "zkm_syscall_event": (TG.SYSCALL_EVENT, {f: f for f in TG.SYSCALL_EVENT.names}),
+    "zkm_global_lookup_event": (TG.GLOBAL_EVENT, {f: f for f in TG.GLOBAL_EVENT.names}),
 }
 
 
@@ -128,11 +129,14 @@ def cpu_rows(ev, prog_ffi, shard, height):
     return t
 
 
-def expected_byte_mult(cpu, shard, add_sub=None):
-    """The Byte lookups program_shard makes for the Cpu rows (mips_core.py program_shard) and
-    alu_traces for AddSub, recomputed from the traces' columns."""
+def expected_byte_mult(cpu, shard, add_sub=None, glob=None):
+    """The Byte lookups program_shard makes for the Cpu rows (mips_core.py program_shard),
+    alu_traces for AddSub and global_trace for Global, recomputed from the traces' columns."""
     mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
     look = A.byte_lookup_into(mult)
+    if glob is not None:
+        m0 = glob[glob[:, MM.G_REAL] == 1, MM.G_MSG].astype(np.int64)
+        look(A.B_U16RANGE, m0 >> 8, m0 & 0xFF)
     t = cpu[cpu[:, MC.C_REAL] == 1].astype(np.int64)
     n = len(t)
     look(A.B_U16RANGE, np.full(n, shard >> 8), np.full(n, shard & 0xFF))
@@ -198,8 +202,8 @@ def test_device_shard_traces_match_host(name):
     for chip, t in dev.items():
         host = tr[chip]
         assert np.array_equal(t.cpu().numpy().view(np.uint32), host), chip
-    assert set(dev) >= {"Cpu", "Program", "MemoryLocal"}
-    want = expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"))
+    assert set(dev) >= {"Cpu", "Program", "MemoryLocal", "Global"}
+    want = expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"), tr["Global"])
     assert np.array_equal(bm.cpu().numpy().astype(np.uint64), want)
 
 
@@ -220,6 +224,28 @@ def test_device_memory_global_matches_host(n, prev_addr, initialize):
     dev = TG.memory_global_trace(TG.to_device(rec), n, initialize, prev_addr, height=len(host))
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy().view(np.uint32), host)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 100, 2048, 2049, 5000])
+def test_device_global_matches_host(n):
+    """Global: septic-curve lift + running sum (a multi-level scan past 2048 points) == the host's
+    lift and sequential fold, trace, final digest and U16 lookups."""
+    import torch
+    rng = np.random.default_rng(11 + n)
+    msg = rng.integers(0, 256, (n, 7)).astype(np.uint32)
+    msg[:, 0] = rng.integers(0, 4, n)       # shard
+    msg[:, 1] = rng.integers(0, 1 << 24, n)  # clk
+    msg[:, 2] = rng.integers(0, 1 << 30, n)  # address
+    rec = rng.integers(0, 2, n).astype(np.uint8)
+    kinds = rng.integers(1, 3, n).astype(np.uint32)
+    mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
+    host, fin = MM.global_trace(msg, rec, kinds, A.byte_lookup_into(mult))
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev, dfin = TG.global_trace(TG.to_device(TG.global_events(msg, rec, kinds)), n, height=len(host), byte_mult=bm)
+    assert np.array_equal(dev.cpu().numpy().view(np.uint32), host)
+    assert np.array_equal(dfin, fin)
+    assert np.array_equal(bm.cpu().numpy().astype(np.uint64), mult)
 
 
 @pytest.mark.gpu
@@ -253,7 +279,8 @@ def test_device_traces_prove_identically():
     cap, tr, pv, m, prep = _capture("sha_syscalls")
     bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
     dev = TG.shard_traces(cap, byte_mult=bm)
-    rest = tr["Byte"].astype(np.int64) - expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub")).astype(np.int64)
+    rest = tr["Byte"].astype(np.int64) - expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"),
+                                                            tr["Global"]).astype(np.int64)
     bm += torch.from_numpy(rest.astype(np.int32)).cuda()  # the other chips' lookups, from the host builders
     traces = {k: v for k, v in tr.items() if k not in dev}
     traces.update(dev)

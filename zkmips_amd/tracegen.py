@@ -50,7 +50,12 @@ SYSCALL_EVENT = np.dtype({"names": ["pc", "next_pc", "shard", "clk", "a_record",
                           "formats": [u4, u4, u4, u4, (u4, 6), u1, u4, u4, u4],
                           "offsets": [0, 4, 8, 12, 16, 40, 44, 48, 52], "itemsize": 56})
 
+# GlobalLookupEvent (events/global.rs:6-15): message[7], is_receive, kind
+GLOBAL_EVENT = np.dtype({"names": ["message", "is_receive", "kind"], "formats": [(u4, 7), u1, u1],
+                         "offsets": [0, 28, 29], "itemsize": 32})
+
 CPU_WIDTH, ADD_SUB_WIDTH, MEMORY_LOCAL_WIDTH, MEMORY_GLOBAL_WIDTH, SYSCALL_WIDTH = 67, 19, 56, 111, 6
+GLOBAL_WIDTH = 99
 
 
 # ---------------------------------------------------------------- records from this repository's executor
@@ -141,6 +146,29 @@ def syscall_events(syscalls) -> np.ndarray:
     return e
 
 
+def global_events(messages, is_receive, kinds) -> np.ndarray:
+    """GlobalLookupEvent records (the Global chip's input, global/mod.rs:77-108)."""
+    M = np.asarray(messages, np.int64).reshape(-1, 7)
+    e = np.zeros(len(M), GLOBAL_EVENT)
+    e["message"] = M
+    e["is_receive"] = np.asarray(is_receive, np.int64)
+    e["kind"] = np.asarray(kinds, np.int64)
+    return e
+
+
+def shard_global_events(capture: dict) -> np.ndarray:
+    """The Global chip's records of a CPU shard, in chip order: SyscallCore's sends, then MemoryLocal's
+    receive/send pairs (program_shard)."""
+    from . import mips_memory as MM
+    from . import mips_syscall as SY
+    core_sc = capture["core_syscalls"]
+    core = core_sc[:, [2, 3, 8, 5, 6]] if len(core_sc) else np.zeros((0, 5), np.int64)
+    smsg = SY.syscall_global_messages(core)
+    gmsg, grec = MM.memory_local_global_events(np.asarray(capture["entries"], np.int64).reshape(-1, 7))
+    return global_events(np.concatenate([smsg, gmsg]), np.concatenate([np.zeros(len(smsg), np.uint8), grec]),
+                         np.concatenate([np.full(len(smsg), SY.KIND_SYSCALL), np.full(len(gmsg), MC.KIND_MEMORY)]))
+
+
 def add_sub_records(alu) -> np.ndarray:
     """The AddSub chip's AluEvents from the executor's ALU event lists (kind "add")."""
     ev = alu["add"]
@@ -160,6 +188,7 @@ def _bind():
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
         L.zkm_syscall_events_to_trace.argtypes = [vp, u64, C.c_int, vp, u64, vp]
+        L.zkm_global_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp, vp]
         L._tracegen_bound = True
     return L
 
@@ -174,7 +203,7 @@ def to_device(records: np.ndarray):
     numpy operations that repack a padded dtype, e.g. np.resize, must not have touched it)."""
     torch = _torch()
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
-                             SYSCALL_EVENT):
+                             SYSCALL_EVENT, GLOBAL_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -261,11 +290,25 @@ def syscall_trace(events_dev, n: int, height: int = None):
     return t
 
 
+def global_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    """Global main trace (height x 99 int32 on the GPU) and the shard's global cumulative sum (14
+    canonical words, numpy) from n GlobalLookupEvent records on the GPU."""
+    torch = _torch()
+    height = height or _pow2(n)
+    t = _trace(height, GLOBAL_WIDTH)
+    fin = torch.zeros(14, dtype=torch.int32, device="cuda")
+    what = "zkm_global_events_to_trace"
+    _lib.check(_bind().zkm_global_events_to_trace(_records(events_dev, n, GLOBAL_EVENT, what), n, t.data_ptr(),
+                                                   height, _words(byte_mult, 65536 * 10, what), fin.data_ptr(),
+                                                   _stream()), what)
+    return t, fin.cpu().numpy().view(np.uint32)
+
+
 def shard_traces(capture: dict, byte_mult=None):
     """Device traces of the chips the reference's row ABI covers, for one executed shard
     (program_shard(..., capture=c)): Cpu (+ Program multiplicities), AddSub, MemoryLocal and
-    SyscallCore, with their Byte lookups added into `byte_mult` (65536 x 10 int32 on the GPU) if
-    given.  Returns {chip name: GPU tensor}."""
+    SyscallCore, plus the Global chip (septic-curve lift and running sum), with their Byte lookups
+    added into `byte_mult` (65536 x 10 int32 on the GPU) if given.  Returns {chip name: GPU tensor}."""
     torch = _torch()
     shard, prog = capture["shard"], capture["prog"]
     ev = cpu_events(capture["steps"], shard)
@@ -282,4 +325,6 @@ def shard_traces(capture: dict, byte_mult=None):
     if len(capture["core_syscalls"]):
         sc = syscall_events(capture["core_syscalls"])
         out["SyscallCore"] = syscall_trace(to_device(sc), len(sc))
+    ge = shard_global_events(capture)
+    out["Global"], _ = global_trace(to_device(ge), len(ge), byte_mult=byte_mult)
     return out
