@@ -1,0 +1,99 @@
+"""Twirp ProverService (zkmips_amd/service.py; the reference's api.proto:5-13 and its client,
+crates/cuda/src/lib.rs:157-206): protobuf / JSON transport, Twirp routes and errors, the Ready poll
+the client runs, and (GPU) a shard proven through the service equal to the direct prover's bytes."""
+import base64
+import http.client
+import json
+import threading
+
+import numpy as np
+import pytest
+
+from zkmips_amd import service as SV
+from zkmips_amd import workloads as W
+
+
+@pytest.fixture
+def server():
+    def start(device_factory=None):
+        svc = SV.ProverService(device_factory=device_factory)
+        srv = SV.serve("127.0.0.1", 0, service=svc)
+        th = threading.Thread(target=srv.serve_forever, daemon=True)
+        th.start()
+        started.append(srv)
+        return srv.server_address[1]
+    started = []
+    yield start
+    for s in started:
+        s.shutdown()
+        s.server_close()
+
+
+def post(port, method, body, ctype="application/protobuf"):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=120)
+    c.request("POST", SV.PREFIX + method, body=body, headers={"Content-Type": ctype})
+    r = c.getresponse()
+    out = r.status, r.getheader("Content-Type"), r.read()
+    c.close()
+    return out
+
+
+def test_protobuf_wire_format_roundtrip():
+    for data in (b"", b"x", bytes(range(256)) * 3, b"\0" * 300):
+        enc = SV.encode_bytes_field(1, data)
+        assert SV.decode_fields(enc).get(1, b"") == data
+    assert SV.encode_bool_field(1, True) == b"\x08\x01" and SV.encode_bool_field(1, False) == b""
+    assert SV.decode_fields(b"\x08\x01") == {1: 1}
+    with pytest.raises(ValueError):
+        SV.decode_fields(b"\x0a\x05ab")  # truncated bytes field
+
+
+def test_ready_and_routes(server):
+    port = server(device_factory=lambda i: object())
+    st, ct, body = post(port, "Ready", b"")
+    assert st == 200 and ct == "application/protobuf" and SV.decode_fields(body) == {1: 1}
+    st, ct, body = post(port, "Ready", b"{}", "application/json")
+    assert st == 200 and json.loads(body) == {"ready": True}
+    for m in ("Setup", "ProveCore", "ProveCoreStateless", "Compress", "Shrink", "Wrap"):
+        st, ct, body = post(port, m, SV.encode_bytes_field(1, b"payload"))
+        assert st == 501 and json.loads(body)["code"] == "unimplemented", m
+    st, _, body = post(port, "NoSuchMethod", b"")
+    assert st == 404 and json.loads(body)["code"] == "bad_route"
+    st, _, body = post(port, "Ready", b"", "text/plain")
+    assert st == 404 and json.loads(body)["code"] == "bad_route"
+    st, _, body = post(port, "ProveShard", SV.encode_bytes_field(1, b"not an npz"))
+    assert st == 400 and json.loads(body)["code"] == "invalid_argument"
+
+
+def test_not_ready_without_device(server):
+    def no_device(i):
+        raise RuntimeError("no gfx950 device")
+    port = server(device_factory=no_device)
+    st, _, body = post(port, "Ready", b"")
+    assert st == 200 and SV.decode_fields(body) == {}  # ready = false is the proto3 default: omitted
+
+
+def test_shard_payload_roundtrip():
+    m, prep, tr, pv = W.fib_shard(1 << 6, 3)
+    data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=16)
+    blob, p2, t2, pv2, nq, lb = SV.unpack_shard(data)
+    assert np.array_equal(blob, m.blob()) and np.array_equal(pv2, pv) and nq == 16 and lb == 1
+    assert set(t2) == set(tr) and all(np.array_equal(t2[k], tr[k]) for k in tr)
+    assert set(p2) == {k for k, v in prep.items() if v is not None}
+
+
+@pytest.mark.gpu
+def test_prove_shard_through_service(server):
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    port = server()
+    st, _, body = post(port, "Ready", b"")
+    assert st == 200 and SV.decode_fields(body) == {1: 1}
+    m, prep, tr, pv = W.fib_shard(1 << 10, 3)
+    direct = HipProver(Device(0), m, prep, num_queries=16).prove_shard(tr, pv)
+    data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=16)
+    st, ct, body = post(port, "ProveShard", SV.encode_bytes_field(1, data))
+    assert st == 200 and SV.decode_fields(body)[1] == direct
+    st, ct, body = post(port, "ProveShard", json.dumps({"data": base64.b64encode(data).decode()}).encode(),
+                        "application/json")
+    assert st == 200 and base64.b64decode(json.loads(body)["result"]) == direct

@@ -51,6 +51,45 @@ def _device_matrix(tensor, name: str, keep: list) -> Matrix:
     return Matrix(nm, tensor.data_ptr(), tensor.shape[0], tensor.shape[1], ZKM_REPR_CANONICAL | ZKM_MEM_DEVICE)
 
 
+def blob_chip_names(blob: np.ndarray) -> List[str]:
+    """The chip names of a machine blob, in machine order (format: include/zkm_hip.h)."""
+    w = [int(x) for x in as_u32(blob)]
+    if len(w) < 4 or w[0] != 0x4D4D4B5A:
+        raise ValueError("not a machine blob")
+    i, names = 4, []
+    for _ in range(w[3]):
+        n = w[i]
+        nw = (n + 3) // 4
+        names.append(b"".join(x.to_bytes(4, "little") for x in w[i + 1:i + 1 + nw])[:n].decode())
+        i += 1 + nw + 6
+        i += 1 + w[i]  # code
+        nl = w[i] + w[i + 1]
+        i += 2
+        for _ in range(nl):
+            nv = w[i + 2]
+            i += 3
+            for _ in range(nv + 1):
+                i += 2 + 2 * w[i]
+    if i != len(w):
+        raise ValueError("malformed machine blob")
+    return names
+
+
+class _BlobMachine:
+    """MachineDesc stand-in over a raw blob: chip names + the blob itself."""
+
+    class _Chip:
+        def __init__(self, name):
+            self.name = name
+
+    def __init__(self, blob: np.ndarray):
+        self._blob = blob
+        self.chips = [self._Chip(n) for n in blob_chip_names(blob)]
+
+    def blob(self) -> np.ndarray:
+        return self._blob
+
+
 class HipProver:
     """MI355X drop-in for CpuProver on one GPU."""
 
@@ -75,6 +114,11 @@ class HipProver:
         check(lib().zkm_setup(device.h, self.blob.ctypes.data, self.blob.size, C.byref(self.cfg), mats,
                               len(machine.chips), pc_start, gcs.ctypes.data, C.byref(self.pk),
                               self.vk_commit.ctypes.data), "zkm_setup")
+
+    @classmethod
+    def from_blob(cls, device: Device, blob: np.ndarray, prep_traces: Dict[str, np.ndarray], **kw) -> "HipProver":
+        """A prover for a machine given only as its blob (e.g. received over the service)."""
+        return cls(device, _BlobMachine(as_u32(blob)), prep_traces, **kw)
 
     def __del__(self):
         if getattr(self, "pk", None):

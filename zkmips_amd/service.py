@@ -1,0 +1,272 @@
+"""Twirp `ProverService` server: the out-of-process GPU seam of the reference.
+
+The reference's `CudaProver` talks Twirp to a closed GPU server image (crates/cuda/proto/api.proto:5-13,
+client crates/cuda/src/lib.rs:157-206; endpoint `CUDA_ENDPOINT`, default
+http://localhost:3000/twirp/).  This is that server's transport on MI355X: Twirp over HTTP/1.1
+(`POST /twirp/api.ProverService/<Method>`, protobuf or JSON bodies, Twirp JSON errors), the message
+types of api.proto (every request/response is one `bytes` field, or `bool ready`), and the methods:
+
+* ``Ready``    — ready = the HIP library loaded and a gfx950 device initialised (the client polls this
+                 for up to 300 s, lib.rs:183-205).
+* ``ProveShard`` (an extension, not in api.proto) — one shard through zkm_prove_shard: `data` is an
+                 .npz archive (numpy, no pickles) with `machine_blob`, `public_values`, `num_queries`,
+                 optional `log_blowup`, and `prep/<chip>` / `trace/<chip>` arrays; `result` is the
+                 serialized ShardProof.  A prover per machine blob is kept (setup once).
+* ``Setup``, ``ProveCore``, ``ProveCoreStateless``, ``Compress``, ``Shrink``, ``Wrap`` — Twirp
+                 `unimplemented`: their payloads are bincode `ZKMStdin` / ELF / recursion proofs
+                 (lib.rs:57-123), which need the MIPS executor and the recursion stack, outside the
+                 §8 hot path.
+
+Run: ``python -m zkmips_amd.service --port 3000`` (then CUDA_ENDPOINT=http://<host>:3000/twirp/).
+"""
+from __future__ import annotations
+
+import argparse
+import io
+import json
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Callable, Dict, Optional, Tuple
+
+import numpy as np
+
+PREFIX = "/twirp/api.ProverService/"
+ALL_METHODS = ("Setup", "Ready", "ProveCore", "ProveCoreStateless", "Compress", "Shrink", "Wrap", "ProveShard")
+UNIMPLEMENTED = {
+    "Setup": "needs the ELF loader and executor (SetupRequestPayload { elf }, crates/cuda/src/lib.rs:60-71)",
+    "ProveCore": "needs the MIPS executor to turn ZKMStdin into shard records (lib.rs:73-79)",
+    "ProveCoreStateless": "needs the MIPS executor to turn ZKMStdin into shard records (lib.rs:81-90)",
+    "Compress": "recursion compress is outside this server (lib.rs:92-102)",
+    "Shrink": "recursion shrink is outside this server (lib.rs:104-109)",
+    "Wrap": "the BN254 wrap is outside this server (lib.rs:111-116)",
+}
+
+
+# ---------------------------------------------------------------- protobuf wire format (api.proto)
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            return bytes(out)
+
+
+def _read_varint(buf: bytes, i: int) -> Tuple[int, int]:
+    n = shift = 0
+    while True:
+        if i >= len(buf):
+            raise ValueError("truncated varint")
+        b = buf[i]
+        i += 1
+        n |= (b & 0x7F) << shift
+        shift += 7
+        if not b & 0x80:
+            return n, i
+        if shift > 63:
+            raise ValueError("varint too long")
+
+
+def decode_fields(buf: bytes) -> Dict[int, object]:
+    """Field number -> value (bytes for length-delimited, int for varint); unknown fields kept."""
+    out: Dict[int, object] = {}
+    i = 0
+    while i < len(buf):
+        key, i = _read_varint(buf, i)
+        field, wire = key >> 3, key & 7
+        if wire == 0:
+            out[field], i = _read_varint(buf, i)
+        elif wire == 2:
+            n, i = _read_varint(buf, i)
+            if i + n > len(buf):
+                raise ValueError("truncated field")
+            out[field] = buf[i:i + n]
+            i += n
+        elif wire == 1:
+            out[field] = buf[i:i + 8]
+            i += 8
+        elif wire == 5:
+            out[field] = buf[i:i + 4]
+            i += 4
+        else:
+            raise ValueError(f"unsupported wire type {wire}")
+    return out
+
+
+def encode_bytes_field(field: int, data: bytes) -> bytes:
+    return _varint((field << 3) | 2) + _varint(len(data)) + data if data else b""
+
+
+def encode_bool_field(field: int, v: bool) -> bytes:
+    return _varint(field << 3) + _varint(1) if v else b""  # proto3: default values are omitted
+
+
+# ---------------------------------------------------------------- shard payloads (ProveShard)
+def pack_shard(machine_blob, prep: dict, traces: dict, public_values, num_queries: int = 84,
+               log_blowup: int = 1) -> bytes:
+    arrs = {"machine_blob": np.asarray(machine_blob, np.uint32), "public_values": np.asarray(public_values, np.uint32),
+            "num_queries": np.asarray([num_queries], np.uint32), "log_blowup": np.asarray([log_blowup], np.uint32)}
+    for k, v in prep.items():
+        if v is not None:
+            arrs[f"prep/{k}"] = np.asarray(v, np.uint32)
+    for k, v in traces.items():
+        arrs[f"trace/{k}"] = np.asarray(v, np.uint32)
+    b = io.BytesIO()
+    np.savez(b, **arrs)
+    return b.getvalue()
+
+
+def unpack_shard(data: bytes):
+    with np.load(io.BytesIO(data), allow_pickle=False) as z:
+        files = {k: z[k] for k in z.files}
+    blob = files.pop("machine_blob")
+    pv = files.pop("public_values")
+    nq = int(files.pop("num_queries")[0])
+    lb = int(files.pop("log_blowup", np.asarray([1]))[0])
+    prep = {k[5:]: v for k, v in files.items() if k.startswith("prep/")}
+    traces = {k[6:]: v for k, v in files.items() if k.startswith("trace/")}
+    return blob, prep, traces, pv, nq, lb
+
+
+class TwirpError(Exception):
+    STATUS = {"invalid_argument": 400, "malformed": 400, "not_found": 404, "bad_route": 404,
+              "unimplemented": 501, "internal": 500, "unavailable": 503}
+
+    def __init__(self, code: str, msg: str):
+        super().__init__(msg)
+        self.code, self.msg = code, msg
+
+
+class ProverService:
+    """The method implementations; transport-independent (the HTTP handler below calls `call`)."""
+
+    def __init__(self, device: int = 0, device_factory: Optional[Callable] = None):
+        self.device_index = device
+        self._device_factory = device_factory
+        self._dev = None
+        self._provers: Dict[Tuple[bytes, int, int], object] = {}
+        self._lock = threading.Lock()
+
+    def _device(self):
+        with self._lock:
+            if self._dev is None:
+                if self._device_factory is not None:
+                    self._dev = self._device_factory(self.device_index)
+                else:
+                    from ._lib import Device
+                    self._dev = Device(self.device_index)
+            return self._dev
+
+    def ready(self) -> bool:
+        try:
+            self._device()
+            return True
+        except Exception:
+            return False
+
+    def prove_shard(self, data: bytes) -> bytes:
+        from .machine import MachineDesc  # noqa: F401  (the blob is self-describing)
+        from .prover import HipProver
+        try:
+            blob, prep, traces, pv, nq, lb = unpack_shard(data)
+        except Exception as e:
+            raise TwirpError("invalid_argument", f"ProveShard payload: {e}")
+        dev = self._device()
+        key = (blob.tobytes(), nq, lb)
+        with self._lock:
+            prover = self._provers.get(key)
+            if prover is None:
+                prover = HipProver.from_blob(dev, blob, prep, num_queries=nq, log_blowup=lb)
+                self._provers[key] = prover
+        return prover.prove_shard(traces, pv)
+
+    def call(self, method: str, payload: Dict[int, object]) -> Dict[str, object]:
+        if method == "Ready":
+            return {"ready": self.ready()}
+        if method == "ProveShard":
+            data = payload.get(1, b"")
+            return {"result": self.prove_shard(bytes(data))}
+        if method in UNIMPLEMENTED:
+            raise TwirpError("unimplemented", f"{method}: {UNIMPLEMENTED[method]}")
+        raise TwirpError("bad_route", f"no such method: {method}")
+
+
+def _handler(service: ProverService):
+    class Handler(BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def log_message(self, fmt, *args):  # quiet
+            pass
+
+        def _send(self, status: int, ctype: str, body: bytes):
+            self.send_response(status)
+            self.send_header("Content-Type", ctype)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def _error(self, e: TwirpError):
+            self._send(TwirpError.STATUS.get(e.code, 500), "application/json",
+                       json.dumps({"code": e.code, "msg": e.msg}).encode())
+
+        def do_POST(self):
+            n = int(self.headers.get("Content-Length") or 0)
+            body = self.rfile.read(n) if n else b""
+            if not self.path.startswith(PREFIX):
+                return self._error(TwirpError("bad_route", f"no handler for path {self.path}"))
+            method = self.path[len(PREFIX):]
+            ctype = (self.headers.get("Content-Type") or "").split(";")[0].strip()
+            try:
+                if ctype == "application/protobuf":
+                    payload = decode_fields(body)
+                elif ctype == "application/json":
+                    j = json.loads(body or b"{}")
+                    payload = {1: __import__("base64").b64decode(j["data"])} if "data" in j else {}
+                else:
+                    raise TwirpError("bad_route", f"unexpected Content-Type: {ctype!r}")
+            except TwirpError as e:
+                return self._error(e)
+            except Exception as e:
+                return self._error(TwirpError("malformed", f"request body: {e}"))
+            try:
+                out = service.call(method, payload)
+            except TwirpError as e:
+                return self._error(e)
+            except Exception as e:  # prover failure: Twirp internal with the library's message
+                return self._error(TwirpError("internal", str(e)))
+            if ctype == "application/protobuf":
+                if "ready" in out:
+                    resp = encode_bool_field(1, bool(out["ready"]))
+                else:
+                    resp = encode_bytes_field(1, out["result"])
+                return self._send(200, "application/protobuf", resp)
+            if "ready" in out:
+                return self._send(200, "application/json", json.dumps({"ready": bool(out["ready"])}).encode())
+            return self._send(200, "application/json", json.dumps(
+                {"result": __import__("base64").b64encode(out["result"]).decode()}).encode())
+
+        def do_GET(self):
+            self._error(TwirpError("bad_route", "Twirp accepts POST only"))
+
+    return Handler
+
+
+def serve(host: str = "127.0.0.1", port: int = 3000, device: int = 0, service: ProverService = None):
+    """A ThreadingHTTPServer for the service (caller runs serve_forever / shutdown)."""
+    return ThreadingHTTPServer((host, port), _handler(service or ProverService(device)))
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=3000)
+    ap.add_argument("--device", type=int, default=0)
+    a = ap.parse_args()
+    srv = serve(a.host, a.port, a.device)
+    print(f"ProverService on http://{a.host}:{a.port}/twirp/", flush=True)
+    srv.serve_forever()
+
+
+if __name__ == "__main__":
+    main()
