@@ -378,6 +378,98 @@ def tracegen_bench(args):
     print(json.dumps(line), flush=True)
 
 
+def compress_bench(args):
+    """BASELINE config 5: the recursion/compress stage.  A 64-leaf compress tree is 63 compress proofs
+    (32 + 16 + 8 + 4 + 2 + 1, prover/src/lib.rs:794-858); each is a shard of the recursion machine's
+    compress AIR (RecursionAir<F, 3>::compress_machine, zkmips_amd/recursion.py) under
+    compressed_fri_config (blowup 4, 42 queries), here at the reference's fixed shrink shape
+    (machine.rs:155-171: MemoryVar/Select 2^18, MemoryConst/BatchFRI/BaseAlu/ExpReverseBitsLen 2^17,
+    Poseidon2WideDeg3 2^16, ExtAlu 2^15), the program a verifier-shaped recursion program executed by the
+    restated runtime.  A step proves one tree, layer by layer (a layer's proofs in flight together);
+    traces resident in HBM.  The programs of one layer share a shape, and this bench proves one program
+    (one proving key) throughout: the reference re-runs setup per compress program (lib.rs:807)."""
+    import threading
+    import torch
+    from zkmips_amd import recursion as R
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    t0 = time.time()
+    m, prep, traces, pvs = R.shard(R.program_verifier_shaped(seed=1), R.SHRINK_SHAPE)
+    gen_s = time.time() - t0
+    torch.cuda.set_device(0)
+    prover = HipProver(Device(0), m, prep, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    dev = {k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in traces.items()}
+    torch.cuda.synchronize()
+    layers = [32, 16, 8, 4, 2, 1]
+
+    def prove_layer(n):
+        out = [None] * n
+        nxt = [0]
+        lock = threading.Lock()
+
+        def worker():
+            while True:
+                with lock:
+                    i = nxt[0]
+                    nxt[0] += 1
+                if i >= n:
+                    return
+                out[i] = prove_resident(prover, dev, pvs)
+        th = [threading.Thread(target=worker) for _ in range(max(1, min(n, args.inflight)))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return out
+
+    for _ in range(max(1, args.warmup)):
+        proofs = prove_layer(max(1, args.inflight))
+    assert all(p == proofs[0] for p in proofs)
+    torch.cuda.synchronize()
+    t1 = time.time()
+    for _ in range(args.steps):
+        for n in layers:
+            prove_layer(n)
+    torch.cuda.synchronize()
+    el = time.time() - t1
+    n_proofs = sum(layers) * args.steps
+    rows = max(v.shape[0] for v in traces.values())
+    # serial single-proof latency
+    torch.cuda.synchronize()
+    t2 = time.time()
+    for _ in range(3):
+        prove_resident(prover, dev, pvs)
+    torch.cuda.synchronize()
+    serial_ms = (time.time() - t2) / 3 * 1e3
+    cpu = None
+    if not args.no_cpu_baseline:
+        from tests import _oracle as O
+        o = O.OracleProver(m, prep, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+        tc = time.time()
+        rc, ref = o.prove(traces, pvs)
+        dt = time.time() - tc
+        assert rc == 0 and ref == proofs[0], "GPU compress proof differs from the CPU oracle"
+        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        cpu = {"value": round(1.0 / dt, 4), "unit": "compress proofs/s", "cores": cores, "kind": "port", "host": host_info(),
+               "sample": f"one shrink-shape compress proof (blowup 4, 42 queries), {dt:.2f} s wall on {cores} OpenMP threads; "
+                         "byte-identical to the GPU proof"}
+    line = {
+        "metric": "compress proofs/sec (64-leaf compress tree = 63 recursion-machine proofs, BASELINE config 5)",
+        "value": round(n_proofs / el, 3), "unit": "proofs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
+        "data": "synthetic verifier-shaped recursion program (recursion.program_verifier_shaped), traces resident in HBM",
+        "config": {"workload": "compress tree: 63 compress-machine shards at the reference shrink shape "
+                               f"({', '.join(f'{k} 2^{v}' for k, v in R.SHRINK_SHAPE.items())}), blowup 4, 42 queries",
+                   "max_rows": rows, "main_cells": int(sum(v.size for v in traces.values())),
+                   "prep_cells": int(sum(v.size for v in prep.values())), "proof_bytes": len(proofs[0]),
+                   "parallelism": f"a layer's proofs {args.inflight} in flight", "trace_generation_s": round(gen_s, 1)},
+        "ms_per_proof": round(1e3 * el / n_proofs, 3), "serial_ms_per_proof": round(serial_ms, 3),
+        "rows_per_s": round(rows * n_proofs / el, 1), "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def pmc_child(args):
     """Runs under rocprofv3 counter passes (pmc_in_run): setup, then the same shard proven twice."""
     from zkmips_amd._lib import Device
@@ -400,7 +492,7 @@ def main():
                     help="memory type of the HBM buffers the pipelined H2D copies land in")
     ap.add_argument("--sha-events-per-shard", type=int, default=16384,
                     help="sha2 workload: precompile calls per precompile shard")
-    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2", "tracegen"], default="fib",
+    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2", "tracegen", "compress"], default="fib",
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
                          "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
                          "zkmips_amd/mips_alu.py), 2^(log-n) "
@@ -424,6 +516,8 @@ def main():
         return execution_bench(args)
     if args.workload == "tracegen":
         return tracegen_bench(args)
+    if args.workload == "compress":
+        return compress_bench(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

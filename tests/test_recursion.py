@@ -1,0 +1,193 @@
+"""The recursion machine's compress AIR (BASELINE config 5; zkmips_amd/recursion.py) under
+compressed_fri_config (log_blowup 2, 42 queries; crates/stark/src/kb31_poseidon2.rs:217-227).
+
+CPU: chip shapes against the reference's column structs, the Poseidon2 trace rows against the KATs, the
+reference's own recursion test programs (mem/constant.rs:212-257, alu_base.rs:332-366,
+alu_ext.rs:339-376, select.rs:297-330, poseidon2_wide/mod.rs:135-202) satisfy every constraint and
+lookup, prove and verify at blowup 4; the reference's should_panic cases fail here too.
+GPU: proof bytes equal the oracle's for every program and a verifier-shaped shard; the reference's
+shrink shape (machine.rs:155-171) proves and verifies at full size.
+The reference tests draw their values from StdRng; ours come from numpy's seeded generator (same
+program structure, different field values)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests import _air_check as AC
+from tests import _oracle as O
+from zkmips_amd import recursion as R
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+LB, NQ = R.COMPRESS_LOG_BLOWUP, R.COMPRESS_NUM_QUERIES
+
+# name: (prep, main, perm EF columns, log_qd, local_only, reference column structs / local_only override)
+CHIPS = {
+    "MemoryConst": (12, 1, 2, 1, True, "mem/constant.rs:24-38, :137-139"),
+    "MemoryVar": (4, 8, 2, 1, True, "mem/variable.rs:25-38, :139-141"),
+    "BaseAlu": (32, 12, 7, 1, True, "alu_base.rs:28-62, :263-265"),
+    "ExtAlu": (32, 48, 7, 1, True, "alu_ext.rs:25-57, :259-261"),
+    "Poseidon2WideDeg3": (49, 313, 17, 1, True, "poseidon2_wide/columns/permutation.rs:20-72, preprocessed.rs, trace.rs:170"),
+    "BatchFRI": (6, 13, 3, 1, False, "batch_fri.rs:35-56"),
+    "Select": (8, 5, 4, 1, True, "select.rs:25-40, :220-222"),
+    "ExpReverseBitsLen": (10, 7, 3, 1, False, "exp_reverse_bits.rs:33-55"),
+    "PublicValues": (10, 1, 2, 1, False, "public_values.rs:33-44"),
+}
+
+
+def test_compress_machine_chip_table():
+    m = R.compress_machine()
+    assert [c.name for c in m.chips] == list(CHIPS)  # machine.rs:112-128 order
+    assert m.num_pv == 231
+    for c in m.chips:
+        prep, main, perm, lqd, lo, _ = CHIPS[c.name]
+        assert (c.prep_width, c.main_width, c.perm_width_ef, c.log_quotient_degree, c.local_only) == \
+            (prep, main, perm, lqd, lo), c.name
+        assert c.log_quotient_degree <= LB
+
+
+def test_poseidon2_rows_match_kats():
+    kat = json.load(open(os.path.join(GOLDEN, "poseidon2_kat.json")))
+    for v in kat.values():
+        out = R.poseidon2_permute(np.asarray(v["input"], np.uint64))[0]
+        assert [int(x) for x in out] == v["output"]
+
+
+def test_ext_inverse():
+    rng = np.random.default_rng(1)
+    a = rng.integers(1, R.P, size=(64, 4)).astype(np.uint64)
+    one = R.ext_mul(a, R.ext_inv(a))
+    assert (one[:, 0] == 1).all() and (one[:, 1:] == 0).all()
+
+
+PROGRAMS = {
+    "basic_mem": R.program_basic_mem,
+    "base_four_ops": lambda: R.program_base_four_ops(1000),
+    "ext_four_ops": lambda: R.program_ext_four_ops(1000),
+    "select": lambda: R.program_select(1000),
+    "poseidon2": R.program_poseidon2,
+    "exp_reverse_bits": lambda: R.program_exp_reverse_bits(100, 16),
+    "batch_fri": lambda: R.program_batch_fri(20, 7),
+    "public_values": R.program_public_values,
+}
+
+SMALL_SHAPE = {k: (v - 7 if k != "PublicValues" else v) for k, v in R.SHRINK_SHAPE.items()}
+
+
+@pytest.mark.parametrize("name", list(PROGRAMS))
+def test_program_air_holds(name):
+    m, pr, tr, pvs = R.shard(PROGRAMS[name]())
+    bad_c, bad_l = AC.check(m, pr, tr, pvs)
+    assert not bad_c and not bad_l
+
+
+@pytest.mark.parametrize("name", ["basic_mem", "ext_four_ops", "poseidon2", "exp_reverse_bits", "batch_fri",
+                                  "public_values"])
+def test_program_oracle_proves_and_verifies(name):
+    m, pr, tr, pvs = R.shard(PROGRAMS[name]())
+    o = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
+    rc, proof = o.prove(tr, pvs)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+def test_verifier_shaped_program():
+    prog = R.program_verifier_shaped(SMALL_SHAPE)
+    m, pr, tr, pvs = R.shard(prog, SMALL_SHAPE)
+    for name, lg in SMALL_SHAPE.items():
+        assert tr[name].shape[0] == 1 << lg
+    assert not any(AC.check(m, pr, tr, pvs))
+    o = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
+    rc, proof = o.prove(tr, pvs)
+    assert rc == 0 and o.verify(proof) == 0
+
+
+def test_reference_should_panic_cases():
+    """mem/constant.rs:222-257 / mem/variable.rs:201-242: a read of 999 copies, of address 999 and of
+    the value 999 after writing 2 at address 1 (mult 1)."""
+    p = R.RecursionProgram(num_addrs=2)
+    p.mem_write([1], [[2, 0, 0, 0]], mult=1)
+    p.mem_read([1], [[2, 0, 0, 0]], mult=999)
+    m, pr, tr, pvs = R.shard(p)
+    assert AC.check(m, pr, tr, pvs)[1], "bad mult must unbalance the memory bus"
+    o = O.OracleProver(m, pr, num_queries=8, log_blowup=LB)
+    rc, proof = o.prove(tr, pvs)
+    assert rc != 0 or o.verify(proof) != 0
+    for addr, val in ((999, 2), (1, 999)):
+        p = R.RecursionProgram(num_addrs=2)
+        p.mem_write([1], [[2, 0, 0, 0]], mult=1)
+        p.mem_read([addr], [[val, 0, 0, 0]], mult=1)
+        with pytest.raises((RuntimeError, IndexError)):
+            R.shard(p)
+
+
+@pytest.mark.parametrize("chip,row,col", [("BaseAlu", 3, 0), ("ExtAlu", 5, 13), ("Poseidon2WideDeg3", 1, 200),
+                                          ("ExpReverseBitsLen", 4, 4), ("BatchFRI", 2, 1), ("Select", 0, 1)])
+def test_tampered_traces_rejected(chip, row, col):
+    prog = R.program_verifier_shaped(SMALL_SHAPE)
+    m, pr, tr, pvs = R.shard(prog, SMALL_SHAPE)
+    tr[chip][row, col] = (int(tr[chip][row, col]) + 1) % R.P
+    assert any(AC.check(m, pr, tr, pvs))
+    o = O.OracleProver(m, pr, num_queries=8, log_blowup=LB)
+    rc, proof = o.prove(tr, pvs)
+    assert rc != 0 or o.verify(proof) != 0
+
+
+def test_public_values_digest_bound():
+    m, pr, tr, pvs = R.shard(R.program_public_values())
+    bad = pvs.copy()
+    bad[R.PV_DIGEST_START + 3] ^= 1
+    assert AC.check(m, pr, tr, bad)[0]
+    bad = pvs.copy()
+    bad[5] ^= 1  # outside the digest: not constrained by the PublicValues chip
+    assert not any(AC.check(m, pr, tr, bad))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from zkmips_amd._lib import Device
+    d = Device(0)
+    yield d
+    d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_recursion_programs_proof_bytes_identical(dev):
+    from zkmips_amd.prover import HipProver
+    for name, mk in PROGRAMS.items():
+        m, pr, tr, pvs = R.shard(mk())
+        gpu = HipProver(dev, m, pr, num_queries=NQ, log_blowup=LB)
+        cpu = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
+        assert np.array_equal(gpu.vk_commit, cpu.commit), name
+        proof = gpu.prove_shard(tr, pvs)
+        rc, ref = cpu.prove(tr, pvs)
+        assert rc == 0 and proof == ref, name
+        assert cpu.verify(proof) == 0, name
+
+
+@pytest.mark.gpu
+def test_gpu_verifier_shaped_proof_bytes_identical(dev):
+    from zkmips_amd.prover import HipProver
+    shape = {k: (v - 4 if k != "PublicValues" else v) for k, v in R.SHRINK_SHAPE.items()}
+    m, pr, tr, pvs = R.shard(R.program_verifier_shaped(shape), shape)
+    gpu = HipProver(dev, m, pr, num_queries=NQ, log_blowup=LB)
+    cpu = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
+    assert np.array_equal(gpu.vk_commit, cpu.commit)
+    proof = gpu.prove_shard(tr, pvs)
+    rc, ref = cpu.prove(tr, pvs)
+    assert rc == 0 and proof == ref and cpu.verify(proof) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_shrink_shape_full_size_verifies(dev):
+    """The reference's shrink shape (MemoryVar/Select 2^18, ..., Poseidon2WideDeg3 2^16) at full size:
+    the oracle verifier accepts the GPU proof and rejects a flipped byte."""
+    from zkmips_amd.prover import HipProver
+    m, pr, tr, pvs = R.shard(R.program_verifier_shaped(), R.SHRINK_SHAPE)
+    gpu = HipProver(dev, m, pr, num_queries=NQ, log_blowup=LB)
+    cpu = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
+    proof = gpu.prove_shard(tr, pvs)
+    assert cpu.verify(proof) == 0
+    bad = bytearray(proof)
+    bad[len(bad) // 2] ^= 1
+    assert cpu.verify(bytes(bad)) != 0

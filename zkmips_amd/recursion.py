@@ -1,0 +1,1225 @@
+"""The recursion machine's compress AIR (BASELINE config 5), restated from the
+reference, and the recursion runtime that produces its traces.
+
+The compress stage proves recursion programs with the same STARK hot path as the core shards, under
+``compressed_fri_config`` (log_blowup 2, 42 queries, 16 PoW bits; crates/stark/src/kb31_poseidon2.rs:
+217-227) and ``RecursionAir<F, COMPRESS_DEGREE = 3>::compress_machine`` (crates/prover/src/lib.rs:106,121;
+crates/recursion/core/src/machine.rs:112-128).  Its chips, in machine order:
+
+=====================  =========================================================  ====  =====
+chip                   reference                                                  prep  main
+=====================  =========================================================  ====  =====
+MemoryConst            recursion/core/src/chips/mem/constant.rs:17-155             12     1
+MemoryVar              chips/mem/variable.rs:18-160                                  4     8
+BaseAlu                chips/alu_base.rs:21-301                                     32    12
+ExtAlu                 chips/alu_ext.rs:18-303                                      32    48
+Poseidon2WideDeg3      chips/poseidon2_wide/{air.rs,trace.rs,columns/*}             49   313
+BatchFRI               chips/batch_fri.rs:30-361                                     6    13
+Select                 chips/select.rs:21-251                                        8     5
+ExpReverseBitsLen      chips/exp_reverse_bits.rs:28-452                             10     7
+PublicValues           chips/public_values.rs:24-310                                10     1
+=====================  =========================================================  ====  =====
+
+All chips talk through one bus: ``send_block`` / ``receive_block`` of (address, 4-word block) as Memory
+lookups (recursion/core/src/builder.rs:18-72); a write sends with multiplicity = number of reads, a
+read receives (or sends with a negative multiplicity).  Every chip's constraints and lookups are emitted
+in the order its ``eval`` emits them, which fixes the alpha folding and the LogUp columns.
+
+The runtime (``execute``) follows recursion/core/src/runtime/mod.rs:336-625 instruction by instruction
+semantics, but executes a program as *blocks* of same-kind, mutually independent instructions
+(numpy-vectorised): chip rows come out in program order, as the reference's trace generators emit them.
+Write multiplicities are counted from the program's reads (the recursion compiler's job in the
+reference), unless an instruction states one.
+"""
+from __future__ import annotations
+
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .machine import (ChipDesc, Expr, IS_FIRST, IS_TRANSITION, KIND_MEMORY, Lookup, MachineDesc, P,
+                      VirtualPairCol as V, main, main_next, prep, prep_next, pv)
+
+D = 4                      # extension degree, runtime/mod.rs (D)
+W_EXT = 3                  # EF = F[x]/(x^4 - 3)
+WIDTH = 16                 # Poseidon2 width
+NUM_EXTERNAL_ROUNDS = 8    # poseidon2_wide/mod.rs:22-24
+NUM_INTERNAL_ROUNDS = 13
+PROOF_MAX_NUM_PVS = 231    # crates/stark/src/types.rs:73 (= RECURSIVE_PROOF_NUM_PV_ELTS)
+PV_DIGEST_START = 223      # RecursionPublicValues.digest (air/public_values.rs:79-145): 32+8+6+128+16+8+8+14+3
+DIGEST_SIZE = 8
+PUB_VALUES_LOG_HEIGHT = 4  # chips/public_values.rs:30
+COMPRESS_LOG_BLOWUP = 2    # kb31_poseidon2.rs:217-227
+COMPRESS_NUM_QUERIES = 42
+U = np.uint64
+PU = U(P)
+
+OP_ADD, OP_SUB, OP_MUL, OP_DIV = 0, 1, 2, 3
+
+# Poseidon2 internal diagonal, poseidon2_wide/mod.rs:85-102 (canonical values)
+DIAG = [P - 2, 1, 2, (P + 1) >> 1, 3, 4, (P - 1) >> 1, P - 3, P - 4, P - ((P - 1) >> 8), P - ((P - 1) >> 3),
+        P - 127, (P - 1) >> 8, (P - 1) >> 3, (P - 1) >> 4, 127]
+
+
+def _load_rc() -> List[List[int]]:
+    """RC_16_30 (crates/primitives/src/lib.rs:19), from the generated table the HIP library is built with."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "p2_rc.inc")
+    with open(path) as f:
+        nums = [int(x, 16) for x in re.findall(r"0x([0-9a-fA-F]+)u", f.read())]
+    assert len(nums) == 30 * 16
+    return [nums[i * 16:(i + 1) * 16] for i in range(30)]
+
+
+RC = _load_rc()
+
+
+# ------------------------------------------------------------------ field helpers (numpy, canonical u64)
+
+def _m(a, b):
+    return (a * b) % PU
+
+
+def ext_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """(n,4) x (n,4) over F[x]/(x^4 - 3)."""
+    r = np.zeros(np.broadcast(a, b).shape, dtype=U)
+    for i in range(D):
+        for j in range(D):
+            t = _m(a[..., i], b[..., j])
+            if i + j >= D:
+                r[..., i + j - D] = (r[..., i + j - D] + _m(t, U(W_EXT))) % PU
+            else:
+                r[..., i + j] = (r[..., i + j] + t) % PU
+    return r
+
+
+def _pow(x: np.ndarray, e: int) -> np.ndarray:
+    r = np.ones_like(x)
+    b = x.copy()
+    while e:
+        if e & 1:
+            r = _m(r, b)
+        b = _m(b, b)
+        e >>= 1
+    return r
+
+
+def ext_inv(a: np.ndarray) -> np.ndarray:
+    """a^-1 via a(x) a(-x) = b0 + b2 x^2 and (b0 + b2 y)(b0 - b2 y) = b0^2 - 3 b2^2 in F."""
+    conj = a.copy()
+    conj[..., 1] = (PU - a[..., 1]) % PU
+    conj[..., 3] = (PU - a[..., 3]) % PU
+    b = ext_mul(a, conj)               # b1 = b3 = 0
+    n = (_m(b[..., 0], b[..., 0]) + PU - _m(U(W_EXT), _m(b[..., 2], b[..., 2]))) % PU
+    ninv = _pow(n, P - 2)
+    c = np.zeros_like(a)
+    c[..., 0] = b[..., 0]
+    c[..., 2] = (PU - b[..., 2]) % PU
+    r = ext_mul(conj, c)
+    return _m(r, ninv[..., None])
+
+
+# ------------------------------------------------------------------ Poseidon2 (for the trace)
+
+def _m4(x):
+    t01 = (x[0] + x[1]) % PU
+    t23 = (x[2] + x[3]) % PU
+    t0123 = (t01 + t23) % PU
+    t01123 = (t0123 + x[1]) % PU
+    t01233 = (t0123 + x[3]) % PU
+    y3 = (t01233 + 2 * x[0]) % PU
+    y1 = (t01123 + 2 * x[2]) % PU
+    y0 = (t01123 + t01) % PU
+    y2 = (t01233 + t23) % PU
+    return [y0, y1, y2, y3]
+
+
+def external_linear_layer(s: List[np.ndarray]) -> List[np.ndarray]:
+    """poseidon2_wide/mod.rs:56-82: M4 per 4-block, then add the column sums."""
+    out = []
+    for j in range(0, WIDTH, 4):
+        out += _m4(s[j:j + 4])
+    sums = [(out[k] + out[4 + k] + out[8 + k] + out[12 + k]) % PU for k in range(4)]
+    return [(out[j] + sums[j % 4]) % PU for j in range(WIDTH)]
+
+
+def internal_linear_layer(s: List[np.ndarray]) -> List[np.ndarray]:
+    """p3_poseidon2::matmul_internal with the diagonal above: s_i <- d_i s_i + sum."""
+    tot = s[0]
+    for j in range(1, WIDTH):
+        tot = (tot + s[j]) % PU
+    return [(_m(s[i], U(DIAG[i])) + tot) % PU for i in range(WIDTH)]
+
+
+# Poseidon2WideDeg3 main columns (PermutationSBox, columns/permutation.rs:20-72)
+P2_EXT = 0                                   # external_rounds_state [8][16]
+P2_INT = P2_EXT + NUM_EXTERNAL_ROUNDS * WIDTH  # internal_rounds_state [16]
+P2_S0 = P2_INT + WIDTH                       # internal_rounds_s0 [12]
+P2_OUT = P2_S0 + NUM_INTERNAL_ROUNDS - 1     # output_state [16]
+P2_ESBOX = P2_OUT + WIDTH                    # external_rounds_sbox_state [8][16]
+P2_ISBOX = P2_ESBOX + NUM_EXTERNAL_ROUNDS * WIDTH  # internal_rounds_sbox_state [13]
+P2_COLS = P2_ISBOX + NUM_INTERNAL_ROUNDS     # 313 = NUM_POSEIDON2_DEGREE3_COLS
+
+
+def poseidon2_rows(inputs: np.ndarray) -> np.ndarray:
+    """(n,16) canonical inputs -> (n,313) Poseidon2WideDeg3 rows (trace.rs populate_perm): the
+    permutation's round states, s-box cubes and output."""
+    n = inputs.shape[0]
+    t = np.zeros((n, P2_COLS), dtype=U)
+    ext = [inputs[:, i].astype(U) % PU for i in range(WIDTH)]
+    t[:, P2_EXT:P2_EXT + WIDTH] = np.stack(ext, 1)
+
+    def external_round(state, r):
+        if r == 0:
+            state = external_linear_layer(state)
+        rnd = r if r < NUM_EXTERNAL_ROUNDS // 2 else r + NUM_INTERNAL_ROUNDS
+        sb = []
+        for i in range(WIDTH):
+            a = (state[i] + U(RC[rnd][i])) % PU
+            sb.append(_m(_m(a, a), a))
+        t[:, P2_ESBOX + r * WIDTH:P2_ESBOX + (r + 1) * WIDTH] = np.stack(sb, 1)
+        return external_linear_layer(sb)
+
+    state = ext
+    for r in range(NUM_EXTERNAL_ROUNDS // 2):
+        state = external_round(state, r)
+        if r == NUM_EXTERNAL_ROUNDS // 2 - 1:
+            t[:, P2_INT:P2_INT + WIDTH] = np.stack(state, 1)
+        else:
+            t[:, P2_EXT + (r + 1) * WIDTH:P2_EXT + (r + 2) * WIDTH] = np.stack(state, 1)
+    for r in range(NUM_INTERNAL_ROUNDS):
+        a = (state[0] + U(RC[r + NUM_EXTERNAL_ROUNDS // 2][0])) % PU
+        sb = _m(_m(a, a), a)
+        t[:, P2_ISBOX + r] = sb
+        state = internal_linear_layer([sb] + state[1:])
+        if r < NUM_INTERNAL_ROUNDS - 1:
+            t[:, P2_S0 + r] = state[0]
+    r4 = NUM_EXTERNAL_ROUNDS // 2
+    t[:, P2_EXT + r4 * WIDTH:P2_EXT + (r4 + 1) * WIDTH] = np.stack(state, 1)
+    for r in range(r4, NUM_EXTERNAL_ROUNDS):
+        state = external_round(state, r)
+        if r == NUM_EXTERNAL_ROUNDS - 1:
+            t[:, P2_OUT:P2_OUT + WIDTH] = np.stack(state, 1)
+        else:
+            t[:, P2_EXT + (r + 1) * WIDTH:P2_EXT + (r + 2) * WIDTH] = np.stack(state, 1)
+    return t
+
+
+def poseidon2_permute(inputs: np.ndarray) -> np.ndarray:
+    return poseidon2_rows(np.atleast_2d(inputs))[:, P2_OUT:P2_OUT + WIDTH]
+
+
+# ------------------------------------------------------------------ program (blocks of instructions)
+
+@dataclass
+class Block:
+    """A run of same-kind instructions that read only what earlier blocks wrote."""
+    kind: str
+    a: Dict[str, np.ndarray] = field(default_factory=dict)
+
+    def __len__(self):
+        return len(next(iter(self.a.values())))
+
+
+@dataclass
+class RecursionProgram:
+    blocks: List[Block] = field(default_factory=list)
+    num_addrs: int = 0
+
+    # --- builders (runtime/instruction.rs helpers, vectorised) ---
+    def alloc(self, n: int) -> np.ndarray:
+        a = np.arange(self.num_addrs, self.num_addrs + n, dtype=np.int64)
+        self.num_addrs += n
+        return a
+
+    def _add(self, kind, **arrays):
+        self.blocks.append(Block(kind, {k: np.asarray(v) for k, v in arrays.items()}))
+
+    def mem_write(self, addr, vals, mult=None):
+        """Instruction::Mem Write (constant memory): vals (n,4)."""
+        addr = np.atleast_1d(np.asarray(addr, np.int64))
+        vals = np.asarray(vals, dtype=U).reshape(len(addr), D) % PU
+        self._add("mem", addr=addr, vals=vals, write=np.ones(len(addr), bool), mult=_mults(mult, len(addr)))
+
+    def mem_read(self, addr, vals, mult=1):
+        addr = np.atleast_1d(np.asarray(addr, np.int64))
+        vals = np.asarray(vals, dtype=U).reshape(len(addr), D) % PU
+        m = np.broadcast_to(np.asarray(mult, np.int64), (len(addr),)).copy()
+        self._add("mem", addr=addr, vals=vals, write=np.zeros(len(addr), bool), mult=m)
+
+    def hint(self, addr, vals, mult=None):
+        """Instruction::Hint: witness blocks written to variable memory (MemoryVar)."""
+        addr = np.atleast_1d(np.asarray(addr, np.int64))
+        vals = np.asarray(vals, dtype=U).reshape(len(addr), D) % PU
+        self._add("hint", addr=addr, vals=vals, mult=_mults(mult, len(addr)))
+
+    def base_alu(self, op, out, in1, in2, mult=None):
+        out = np.atleast_1d(np.asarray(out, np.int64))
+        n = len(out)
+        self._add("base", op=np.broadcast_to(np.asarray(op, np.int64), (n,)).copy(), out=out,
+                  in1=np.broadcast_to(np.asarray(in1, np.int64), (n,)).copy(),
+                  in2=np.broadcast_to(np.asarray(in2, np.int64), (n,)).copy(), mult=_mults(mult, n))
+
+    def ext_alu(self, op, out, in1, in2, mult=None):
+        out = np.atleast_1d(np.asarray(out, np.int64))
+        n = len(out)
+        self._add("ext", op=np.broadcast_to(np.asarray(op, np.int64), (n,)).copy(), out=out,
+                  in1=np.broadcast_to(np.asarray(in1, np.int64), (n,)).copy(),
+                  in2=np.broadcast_to(np.asarray(in2, np.int64), (n,)).copy(), mult=_mults(mult, n))
+
+    def poseidon2(self, outs, ins, mults=None):
+        outs = np.asarray(outs, np.int64).reshape(-1, WIDTH)
+        ins = np.asarray(ins, np.int64).reshape(-1, WIDTH)
+        m = None if mults is None else np.asarray(mults, np.int64).reshape(-1, WIDTH)
+        self._add("p2", out=outs, inp=ins, mult=_mults(m, outs.shape))
+
+    def select(self, bit, out1, out2, in1, in2, mult1=None, mult2=None):
+        bit = np.atleast_1d(np.asarray(bit, np.int64))
+        n = len(bit)
+        self._add("select", bit=bit, out1=np.asarray(out1, np.int64).reshape(n), out2=np.asarray(out2, np.int64).reshape(n),
+                  in1=np.asarray(in1, np.int64).reshape(n), in2=np.asarray(in2, np.int64).reshape(n),
+                  mult1=_mults(mult1, n), mult2=_mults(mult2, n))
+
+    def exp_reverse_bits(self, base, exps, result, mult=None):
+        """Instruction::ExpReverseBitsLen; exps (n, L) bit addresses (one length per block)."""
+        base = np.atleast_1d(np.asarray(base, np.int64))
+        exps = np.asarray(exps, np.int64).reshape(len(base), -1)
+        self._add("exprev", base=base, exps=exps, result=np.asarray(result, np.int64).reshape(len(base)),
+                  mult=_mults(mult, len(base)))
+
+    def batch_fri(self, acc, alpha_pow, p_at_z, p_at_x):
+        """Instruction::BatchFRI: acc = sum_i alpha_pow_i (p_at_z_i - p_at_x_i); (n, L) address arrays."""
+        acc = np.atleast_1d(np.asarray(acc, np.int64))
+        n = len(acc)
+        self._add("batchfri", acc=acc, alpha_pow=np.asarray(alpha_pow, np.int64).reshape(n, -1),
+                  p_at_z=np.asarray(p_at_z, np.int64).reshape(n, -1), p_at_x=np.asarray(p_at_x, np.int64).reshape(n, -1),
+                  mult=np.ones(n, np.int64))
+
+    def commit_public_values(self, pv_addrs):
+        pv_addrs = np.asarray(pv_addrs, np.int64).reshape(PROOF_MAX_NUM_PVS)
+        self._add("commit", pv=pv_addrs[None, :])
+
+
+def _mults(m, shape):
+    """-1 marks 'count the reads' (filled in by ``execute``)."""
+    if m is None:
+        return np.full(shape, -1, np.int64)
+    return np.broadcast_to(np.asarray(m, np.int64), shape).copy()
+
+
+# reads of each block kind: (array name, per-element multiplicity) -- runtime/mod.rs mr() calls that the
+# AIR matches with a receive
+def _reads(b: Block):
+    a = b.a
+    if b.kind == "mem":
+        return [(a["addr"][~a["write"]], a["mult"][~a["write"]])]
+    if b.kind in ("base", "ext"):
+        return [(a["in1"], 1), (a["in2"], 1)]
+    if b.kind == "p2":
+        return [(a["inp"].ravel(), 1)]
+    if b.kind == "select":
+        return [(a["bit"], 1), (a["in1"], 1), (a["in2"], 1)]
+    if b.kind == "exprev":
+        return [(a["base"], 1), (a["exps"].ravel(), 1)]
+    if b.kind == "batchfri":
+        return [(a["alpha_pow"].ravel(), 1), (a["p_at_z"].ravel(), 1), (a["p_at_x"].ravel(), 1)]
+    if b.kind == "commit":
+        return [(a["pv"][0, PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE], 1)]
+    return []
+
+
+def _writes(b: Block):
+    a = b.a
+    if b.kind == "mem":
+        return [("addr", "mult", a["write"])]
+    if b.kind in ("hint", "base", "ext"):
+        return [("out" if b.kind != "hint" else "addr", "mult", None)]
+    if b.kind == "p2":
+        return [("out", "mult", None)]
+    if b.kind == "select":
+        return [("out1", "mult1", None), ("out2", "mult2", None)]
+    if b.kind in ("exprev",):
+        return [("result", "mult", None)]
+    if b.kind == "batchfri":
+        return [("acc", "mult", None)]
+    return []
+
+
+def resolve_mults(prog: RecursionProgram) -> None:
+    """Fill every '-1' write multiplicity with the number of reads of that address."""
+    cnt = np.zeros(prog.num_addrs, np.int64)
+    for b in prog.blocks:
+        for addrs, m in _reads(b):
+            np.add.at(cnt, addrs, m)
+    for b in prog.blocks:
+        for an, mn, sel in _writes(b):
+            m = b.a[mn]
+            auto = m < 0
+            if sel is not None:
+                auto &= sel
+            m[auto] = cnt[b.a[an][auto]]
+
+
+# ------------------------------------------------------------------ runtime
+
+@dataclass
+class ExecutionRecord:
+    program: RecursionProgram
+    events: Dict[str, List[Dict[str, np.ndarray]]]
+    public_values: np.ndarray
+
+
+def execute(prog: RecursionProgram) -> ExecutionRecord:
+    """Run the program (runtime/mod.rs:336-625): memory is write-once; every value read must have been
+    written by an earlier block.  Returns per-kind event lists in program order."""
+    resolve_mults(prog)
+    mem = np.zeros((prog.num_addrs, D), U)
+    written = np.zeros(prog.num_addrs, bool)
+    ev: Dict[str, List[Dict[str, np.ndarray]]] = {k: [] for k in
+                                                 ("mem", "hint", "base", "ext", "p2", "select", "exprev", "batchfri", "commit")}
+    pvs = np.zeros(PROOF_MAX_NUM_PVS, np.uint32)
+
+    def rd(addr):
+        addr = np.asarray(addr)
+        if addr.size and (addr.min() < 0 or addr.max() >= prog.num_addrs or not written[addr].all()):
+            raise RuntimeError("read of an unassigned address")
+        return mem[addr]
+
+    def wr(addr, vals):
+        if written[addr].any() or len(np.unique(addr)) != len(addr):
+            raise RuntimeError("write to an assigned address")
+        mem[addr] = vals
+        written[addr] = True
+
+    for b in prog.blocks:
+        a = b.a
+        k = b.kind
+        if k == "mem":
+            w = a["write"]
+            if (~w).any():
+                if not np.array_equal(rd(a["addr"][~w]), a["vals"][~w]):
+                    raise RuntimeError("stored memory value should be the specified value")
+            wr(a["addr"][w], a["vals"][w])
+            ev["mem"].append({})
+        elif k == "hint":
+            wr(a["addr"], a["vals"])
+            ev["hint"].append({"vals": a["vals"]})
+        elif k == "base":
+            x, y = rd(a["in1"])[:, 0], rd(a["in2"])[:, 0]
+            op = a["op"]
+            out = np.where(op == OP_ADD, (x + y) % PU, np.where(op == OP_SUB, (x + PU - y) % PU, _m(x, y)))
+            if (op == OP_DIV).any():
+                d = op == OP_DIV
+                out[d] = _m(x[d], _pow(y[d], P - 2))
+            blk = np.zeros((len(out), D), U)
+            blk[:, 0] = out
+            wr(a["out"], blk)
+            ev["base"].append({"out": out, "in1": x, "in2": y})
+        elif k == "ext":
+            x, y = rd(a["in1"]), rd(a["in2"])
+            op = a["op"][:, None]
+            out = np.where(op == OP_ADD, (x + y) % PU, np.where(op == OP_SUB, (x + PU - y) % PU, ext_mul(x, y)))
+            d = a["op"] == OP_DIV
+            if d.any():
+                out[d] = ext_mul(x[d], ext_inv(y[d]))
+            wr(a["out"], out)
+            ev["ext"].append({"out": out, "in1": x, "in2": y})
+        elif k == "p2":
+            x = rd(a["inp"].ravel())[:, 0].reshape(-1, WIDTH)
+            rows = poseidon2_rows(x)
+            blk = np.zeros((x.size, D), U)
+            blk[:, 0] = rows[:, P2_OUT:P2_OUT + WIDTH].ravel()
+            wr(a["out"].ravel(), blk)
+            ev["p2"].append({"rows": rows})
+        elif k == "select":
+            bit, x, y = rd(a["bit"])[:, 0], rd(a["in1"])[:, 0], rd(a["in2"])[:, 0]
+            nb = (PU + 1 - bit) % PU
+            o1 = (_m(bit, y) + _m(nb, x)) % PU
+            o2 = (_m(bit, x) + _m(nb, y)) % PU
+            for nm, v in (("out1", o1), ("out2", o2)):
+                blk = np.zeros((len(v), D), U)
+                blk[:, 0] = v
+                wr(a[nm], blk)
+            ev["select"].append({"bit": bit, "out1": o1, "out2": o2, "in1": x, "in2": y})
+        elif k == "exprev":
+            base = rd(a["base"])[:, 0]
+            n, L = a["exps"].shape
+            bits = rd(a["exps"].ravel())[:, 0].reshape(n, L)
+            acc = np.ones(n, U)
+            cols = np.zeros((n, L, 7), U)
+            for i in range(L):
+                prev = acc
+                mult = np.where(bits[:, i] == 1, base, U(1))
+                psq = _m(prev, prev)
+                acc = _m(psq, mult)
+                cols[:, i] = np.stack([base, bits[:, i], psq, _m(psq, mult), acc, _m(acc, acc), mult], 1)
+            blk = np.zeros((n, D), U)
+            blk[:, 0] = acc
+            wr(a["result"], blk)
+            ev["exprev"].append({"rows": cols.reshape(n * L, 7), "L": L, "n": n})
+        elif k == "batchfri":
+            n, L = a["p_at_x"].shape
+            px = rd(a["p_at_x"].ravel())[:, 0].reshape(n, L)
+            pz = rd(a["p_at_z"].ravel()).reshape(n, L, D)
+            al = rd(a["alpha_pow"].ravel()).reshape(n, L, D)
+            acc = np.zeros((n, D), U)
+            rows = np.zeros((n, L, 13), U)
+            for i in range(L):
+                diff = pz[:, i].copy()
+                diff[:, 0] = (diff[:, 0] + PU - px[:, i]) % PU
+                acc = (acc + ext_mul(al[:, i], diff)) % PU
+                rows[:, i, 0:4] = acc
+                rows[:, i, 4:8] = al[:, i]
+                rows[:, i, 8:12] = pz[:, i]
+                rows[:, i, 12] = px[:, i]
+            wr(a["acc"], acc)
+            ev["batchfri"].append({"rows": rows.reshape(n * L, 13), "L": L, "n": n})
+        elif k == "commit":
+            vals = rd(a["pv"][0])[:, 0]
+            pvs = vals.astype(np.uint32)
+            ev["commit"].append({"pv": vals})
+        else:
+            raise ValueError(k)
+    return ExecutionRecord(prog, ev, pvs)
+
+
+# ------------------------------------------------------------------ chips (AIR restatement)
+
+def _ext_expr_mul(a, b):
+    """BinomialExtension::mul (crates/stark/src/air/extension.rs:55-75) over Expr components."""
+    r = [None] * D
+    for i in range(D):
+        for j in range(D):
+            t = a[i] * b[j]
+            if i + j >= D:
+                t = W_EXT * t
+                k = i + j - D
+            else:
+                k = i + j
+            r[k] = t if r[k] is None else r[k] + t
+    return r
+
+
+def _blk(kind, c0):
+    f = main if kind == "main" else prep
+    return [f(c0 + k) for k in range(D)]
+
+
+def _vblk(kind, c0):
+    f = V.single_main if kind == "main" else V.single_prep
+    return [f(c0 + k) for k in range(D)]
+
+
+def _single(vcol):
+    return [vcol, V.const(0), V.const(0), V.const(0)]
+
+
+def _mem(addr: V, vals: List[V], mult: V) -> Lookup:
+    return Lookup([addr] + vals, mult, KIND_MEMORY)
+
+
+def mem_const_chip() -> ChipDesc:
+    """MemoryConst (mem/constant.rs:142-155): prep = 2 x (value[4], addr, mult); send_block each."""
+    c = ChipDesc("MemoryConst", prep_width=12, main_width=1, local_only=True)
+    for e in range(2):
+        b = 6 * e
+        c.sends.append(_mem(V.single_prep(b + 4), _vblk("prep", b), V.single_prep(b + 5)))
+    return c
+
+
+def mem_var_chip() -> ChipDesc:
+    """MemoryVar (mem/variable.rs:144-160): prep = 2 x (addr, mult), main = 2 x value[4]."""
+    c = ChipDesc("MemoryVar", prep_width=4, main_width=8, local_only=True)
+    for e in range(2):
+        c.sends.append(_mem(V.single_prep(2 * e), _vblk("main", 4 * e), V.single_prep(2 * e + 1)))
+    return c
+
+
+def _alu_chip(name: str, ext: bool) -> ChipDesc:
+    """BaseAlu (alu_base.rs:268-301) / ExtAlu (alu_ext.rs:264-303): 4 entries per row; main entry =
+    (out, in1, in2) as felts or blocks; prep entry = (addr out, in1, in2, is_add, is_sub, is_mul, is_div,
+    mult)."""
+    w = D if ext else 1
+    c = ChipDesc(name, prep_width=32, main_width=12 * w, local_only=True)
+    for e in range(4):
+        mb, pb = 3 * w * e, 8 * e
+        out, in1, in2 = ([main(mb + k * w + j) for j in range(w)] for k in range(3))
+        is_add, is_sub, is_mul, is_div, mult = (prep(pb + 3 + j) for j in range(5))
+        is_real = is_add + is_sub + is_mul + is_div
+        c.assert_zero(is_real * (is_real - 1))
+        if ext:
+            s = [in1[j] + in2[j] for j in range(D)]
+            for j in range(D):
+                c.assert_zero(is_add * (s[j] - out[j]))
+            s = [in2[j] + out[j] for j in range(D)]
+            for j in range(D):
+                c.assert_zero(is_sub * (in1[j] - s[j]))
+            pr = _ext_expr_mul(in1, in2)
+            for j in range(D):
+                c.assert_zero(is_mul * (pr[j] - out[j]))
+            pr = _ext_expr_mul(in2, out)
+            for j in range(D):
+                c.assert_zero(is_div * (in1[j] - pr[j]))
+        else:
+            c.assert_zero(is_add * ((in1[0] + in2[0]) - out[0]))
+            c.assert_zero(is_sub * (in1[0] - (in2[0] + out[0])))
+            c.assert_zero(is_mul * (out[0] - in1[0] * in2[0]))
+            c.assert_zero(is_div * (in2[0] * out[0] - in1[0]))
+        real = V([("prep", pb + 3 + j, 1) for j in range(4)], 0)
+        vals = lambda k: (_vblk("main", mb + k * w) if ext else _single(V.single_main(mb + k)))
+        c.receives.append(_mem(V.single_prep(pb + 1), vals(1), real))
+        c.receives.append(_mem(V.single_prep(pb + 2), vals(2), real))
+        c.sends.append(_mem(V.single_prep(pb + 0), vals(0), V.single_prep(pb + 7)))
+    return c
+
+
+class _Lin:
+    """A linear form sum(c_v * var) + k over trace columns, so the 13 chained internal linear layers of
+    Poseidon2 stay compact (Plonky3's symbolic expressions share subterms; a postfix program cannot)."""
+
+    def __init__(self, terms=None, k=0):
+        self.t = dict(terms or {})
+        self.k = k % P
+
+    @staticmethod
+    def var(col):
+        return _Lin({col: 1})
+
+    def __add__(self, o):
+        if isinstance(o, int):
+            return _Lin(self.t, self.k + o)
+        t = dict(self.t)
+        for v, c in o.t.items():
+            t[v] = (t.get(v, 0) + c) % P
+        return _Lin(t, self.k + o.k)
+
+    def scale(self, s):
+        return _Lin({v: c * s % P for v, c in self.t.items()}, self.k * s)
+
+    def expr(self) -> Expr:
+        e = None
+        for v, c in sorted(self.t.items()):
+            if c == 0:
+                continue
+            term = main(v) if c == 1 else c * main(v)
+            e = term if e is None else e + term
+        if e is None:
+            return Expr.lift(self.k)
+        return e + self.k if self.k else e
+
+
+def _lin_m4(x):
+    t01 = x[0] + x[1]
+    t23 = x[2] + x[3]
+    t0123 = t01 + t23
+    t01123 = t0123 + x[1]
+    t01233 = t0123 + x[3]
+    return [t01123 + t01, t01123 + x[2].scale(2), t01233 + t23, t01233 + x[0].scale(2)]
+
+
+def _lin_external(s):
+    out = []
+    for j in range(0, WIDTH, 4):
+        out += _lin_m4(s[j:j + 4])
+    sums = [out[k] + out[4 + k] + out[8 + k] + out[12 + k] for k in range(4)]
+    return [out[j] + sums[j % 4] for j in range(WIDTH)]
+
+
+def _lin_internal(s):
+    tot = s[0]
+    for j in range(1, WIDTH):
+        tot = tot + s[j]
+    return [s[i].scale(DIAG[i]) + tot for i in range(WIDTH)]
+
+
+def poseidon2_wide_chip() -> ChipDesc:
+    """Poseidon2WideDeg3 (poseidon2_wide/air.rs:39-179): prep = input addrs[16], (output addr, mult)[16],
+    is_real_neg; main = PermutationSBox (313 columns)."""
+    c = ChipDesc("Poseidon2WideDeg3", prep_width=49, main_width=P2_COLS, local_only=True)
+    x = main(P2_EXT)
+    c.assert_zero(x * x * x - x * x * x)  # dummy constraint normalising the degree to 3
+    for i in range(WIDTH):
+        c.sends.append(_mem(V.single_prep(i), _single(V.single_main(P2_EXT + i)), V.single_prep(48)))
+    for i in range(WIDTH):
+        c.sends.append(_mem(V.single_prep(16 + 2 * i), _single(V.single_main(P2_OUT + i)), V.single_prep(17 + 2 * i)))
+
+    ext_state = lambda r: [_Lin.var(P2_EXT + r * WIDTH + i) for i in range(WIDTH)]
+    for r in range(NUM_EXTERNAL_ROUNDS):
+        st = ext_state(r)
+        if r == 0:
+            st = _lin_external(st)
+        rnd = r if r < NUM_EXTERNAL_ROUNDS // 2 else r + NUM_INTERNAL_ROUNDS
+        sb = []
+        for i in range(WIDTH):
+            a = (st[i] + RC[rnd][i]).expr()
+            col = P2_ESBOX + r * WIDTH + i
+            c.assert_zero(main(col) - a * a * a)
+            sb.append(_Lin.var(col))
+        st = _lin_external(sb)
+        if r == NUM_EXTERNAL_ROUNDS // 2 - 1:
+            nxt = [P2_INT + i for i in range(WIDTH)]
+        elif r == NUM_EXTERNAL_ROUNDS - 1:
+            nxt = [P2_OUT + i for i in range(WIDTH)]
+        else:
+            nxt = [P2_EXT + (r + 1) * WIDTH + i for i in range(WIDTH)]
+        for i in range(WIDTH):
+            c.assert_zero(main(nxt[i]) - st[i].expr())
+    st = [_Lin.var(P2_INT + i) for i in range(WIDTH)]
+    for r in range(NUM_INTERNAL_ROUNDS):
+        base = st[0] if r == 0 else _Lin.var(P2_S0 + r - 1)
+        a = (base + RC[r + NUM_EXTERNAL_ROUNDS // 2][0]).expr()
+        c.assert_zero(main(P2_ISBOX + r) - a * a * a)
+        st = _lin_internal([_Lin.var(P2_ISBOX + r)] + st[1:])
+        if r < NUM_INTERNAL_ROUNDS - 1:
+            c.assert_zero(main(P2_S0 + r) - st[0].expr())
+    r4 = NUM_EXTERNAL_ROUNDS // 2
+    for i in range(WIDTH):
+        c.assert_zero(main(P2_EXT + r4 * WIDTH + i) - st[i].expr())
+    return c
+
+
+def batch_fri_chip() -> ChipDesc:
+    """BatchFRI (batch_fri.rs:292-361): prep = (is_real, is_end, acc, alpha_pow, p_at_z, p_at_x addrs);
+    main = (acc[4], alpha_pow[4], p_at_z[4], p_at_x)."""
+    c = ChipDesc("BatchFRI", prep_width=6, main_width=13)
+    is_real, is_end = prep(0), prep(1)
+    c.assert_zero(is_real * is_real * is_real - is_real * is_real * is_real)
+    rv = V.single_prep(0)
+    c.receives.append(_mem(V.single_prep(3), _vblk("main", 4), rv))
+    c.receives.append(_mem(V.single_prep(4), _vblk("main", 8), rv))
+    c.receives.append(_mem(V.single_prep(5), _single(V.single_main(12)), rv))
+    c.sends.append(_mem(V.single_prep(2), _vblk("main", 0), V.single_prep(1)))
+
+    def term(f):  # alpha_pow * (p_at_z - from_base(p_at_x))
+        al = [f(4 + k) for k in range(D)]
+        z = [f(8 + k) for k in range(D)]
+        z[0] = z[0] - f(12)
+        return _ext_expr_mul(al, z)
+
+    t = term(main)
+    for k in range(D):
+        c.assert_zero(IS_FIRST * (main(k) - t[k]))
+    t = term(main_next)
+    for k in range(D):
+        c.assert_zero(IS_TRANSITION * is_end * (main_next(k) - t[k]))
+    for k in range(D):
+        c.assert_zero(IS_TRANSITION * (1 - is_end) * (main_next(k) - (main(k) + t[k])))
+    return c
+
+
+def select_chip() -> ChipDesc:
+    """Select (select.rs:229-251): prep = (is_real, bit, out1, out2, in1, in2 addrs, mult1, mult2);
+    main = (bit, out1, out2, in1, in2)."""
+    c = ChipDesc("Select", prep_width=8, main_width=5, local_only=True)
+    rv = V.single_prep(0)
+    c.receives.append(_mem(V.single_prep(1), _single(V.single_main(0)), rv))
+    c.receives.append(_mem(V.single_prep(4), _single(V.single_main(3)), rv))
+    c.receives.append(_mem(V.single_prep(5), _single(V.single_main(4)), rv))
+    c.sends.append(_mem(V.single_prep(2), _single(V.single_main(1)), V.single_prep(6)))
+    c.sends.append(_mem(V.single_prep(3), _single(V.single_main(2)), V.single_prep(7)))
+    bit, o1, o2, i1, i2 = (main(j) for j in range(5))
+    c.assert_zero(o1 - (bit * i2 + (1 - bit) * i1))
+    c.assert_zero(o2 - (bit * i1 + (1 - bit) * i2))
+    return c
+
+
+def exp_reverse_bits_chip() -> ChipDesc:
+    """ExpReverseBitsLen (exp_reverse_bits.rs:355-452): prep = (x, exponent, result) (addr, mult),
+    iteration_num, is_first, is_last, is_real; main = (x, current_bit, prev_accum_squared,
+    prev_accum_squared_times_multiplier, accum, accum_squared, multiplier)."""
+    c = ChipDesc("ExpReverseBitsLen", prep_width=10, main_width=7)
+    x, bit, psq, psqm, acc, accsq, mult = (main(j) for j in range(7))
+    is_first, is_last, is_real = prep(7), prep(8), prep(9)
+    c.sends.append(_mem(V.single_prep(0), _single(V.single_main(0)), V.single_prep(1)))
+    c.assert_zero(IS_TRANSITION * prep_next(9) * (1 - is_last) * (x - main_next(0)))
+    c.sends.append(_mem(V.single_prep(2), _single(V.single_main(1)), V.single_prep(3)))
+    c.assert_zero(is_first * (acc - mult))
+    c.assert_zero(is_real * bit * (mult - x))
+    c.assert_zero(is_real * (1 - bit) * (mult - 1))
+    c.assert_zero(is_real * (psqm - psq * mult))
+    c.assert_zero(is_real * (1 - is_first) * (acc - psqm))
+    c.assert_zero(is_real * (accsq - acc * acc))
+    c.assert_zero(IS_TRANSITION * prep_next(9) * (1 - is_last) * (main_next(2) - accsq))
+    c.sends.append(_mem(V.single_prep(4), _single(V.single_main(4)), V.single_prep(5)))
+    return c
+
+
+def public_values_chip() -> ChipDesc:
+    """PublicValues (public_values.rs:289-310): prep = (pv_idx[8], pv_mem addr, mult); main = pv_element."""
+    c = ChipDesc("PublicValues", prep_width=10, main_width=1)
+    c.sends.append(_mem(V.single_prep(8), _single(V.single_main(0)), V.single_prep(9)))
+    for i in range(DIGEST_SIZE):
+        c.assert_zero(prep(i) * (pv(PV_DIGEST_START + i) - main(0)))
+    return c
+
+
+def compress_machine() -> MachineDesc:
+    """RecursionAir::<F, 3>::compress_machine (machine.rs:112-128), observing all 231 public values."""
+    return MachineDesc([mem_const_chip(), mem_var_chip(), _alu_chip("BaseAlu", False), _alu_chip("ExtAlu", True),
+                        poseidon2_wide_chip(), batch_fri_chip(), select_chip(), exp_reverse_bits_chip(),
+                        public_values_chip()], PROOF_MAX_NUM_PVS)
+
+
+# ------------------------------------------------------------------ traces
+
+def _pow2(n: int, fixed: Optional[int] = None) -> int:
+    """core/machine/src/utils/mod.rs:99-121 next_power_of_two (>= 16) or the shape's fixed height."""
+    if fixed is not None:
+        if n > (1 << fixed):
+            raise ValueError(f"fixed log2 rows is too small: got {n}, expected {1 << fixed}")
+        return 1 << fixed
+    return max(16, 1 << max(0, (n - 1).bit_length()))
+
+
+def _neg(m):
+    return (P - np.asarray(m, np.int64) % P) % P
+
+
+def _cat(xs, shape_tail, dtype=U):
+    return np.concatenate(xs) if xs else np.zeros((0,) + shape_tail, dtype)
+
+
+def generate_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None):
+    """(prep_traces, main_traces) by chip name, row-major uint32 canonical."""
+    shape = shape or {}
+    prog = rec.program
+    bl = lambda k: [b for b in prog.blocks if b.kind == k]
+    preps, mains = {}, {}
+
+    def finish(name, pr, mn, n_rows):
+        h = _pow2(n_rows, shape.get(name))
+        P_ = np.zeros((h, pr.shape[1]), np.uint32)
+        P_[:pr.shape[0]] = pr
+        M_ = np.zeros((h, mn.shape[1]), np.uint32)
+        M_[:mn.shape[0]] = mn
+        preps[name], mains[name] = P_, M_
+        return h
+
+    # MemoryConst: (value[4], addr, mult) x 2, in instruction order
+    ent = []
+    for b in bl("mem"):
+        a = b.a
+        m = np.where(a["write"], a["mult"] % P, _neg(a["mult"]))
+        ent.append(np.concatenate([a["vals"], a["addr"][:, None].astype(U), m[:, None].astype(U)], 1))
+    ent = _cat(ent, (6,))
+    n = (len(ent) + 1) // 2
+    pr = np.zeros((n, 12), U)
+    pr.reshape(-1)[:ent.size] = ent.reshape(-1)
+    finish("MemoryConst", pr, np.zeros((n, 1), U), n)
+
+    # MemoryVar: prep (addr, mult) x 2, main value[4] x 2
+    hs = bl("hint")
+    acc = _cat([np.stack([b.a["addr"].astype(U), b.a["mult"].astype(U) % PU], 1) for b in hs], (2,))
+    vals = _cat([b.a["vals"] for b in hs], (4,))
+    n = (len(acc) + 1) // 2
+    pr = np.zeros((n, 4), U)
+    pr.reshape(-1)[:acc.size] = acc.reshape(-1)
+    mn = np.zeros((n, 8), U)
+    mn.reshape(-1)[:vals.size] = vals.reshape(-1)
+    finish("MemoryVar", pr, mn, n)
+
+    # BaseAlu / ExtAlu
+    for kind, name, w in (("base", "BaseAlu", 1), ("ext", "ExtAlu", D)):
+        bs = bl(kind)
+        evs = [e for e in rec.events[kind]]
+        pa, ma = [], []
+        for b, e in zip(bs, evs):
+            a = b.a
+            k = len(a["out"])
+            p_ = np.zeros((k, 8), U)
+            p_[:, 0], p_[:, 1], p_[:, 2] = a["out"], a["in1"], a["in2"]
+            p_[np.arange(k), 3 + a["op"]] = 1
+            p_[:, 7] = a["mult"] % P
+            pa.append(p_)
+            if w == 1:
+                ma.append(np.stack([e["out"], e["in1"], e["in2"]], 1))
+            else:
+                ma.append(np.concatenate([e["out"], e["in1"], e["in2"]], 1))
+        pa, ma = _cat(pa, (8,)), _cat(ma, (3 * w,))
+        n = (len(pa) + 3) // 4
+        pr = np.zeros((n, 32), U)
+        pr.reshape(-1)[:pa.size] = pa.reshape(-1)
+        mn = np.zeros((n, 12 * w), U)
+        mn.reshape(-1)[:ma.size] = ma.reshape(-1)
+        finish(name, pr, mn, n)
+
+    # Poseidon2WideDeg3: padding rows are the permutation of zero (trace.rs dummy row)
+    bs = bl("p2")
+    pa = []
+    for b in bs:
+        a = b.a
+        k = a["out"].shape[0]
+        p_ = np.zeros((k, 49), U)
+        p_[:, 0:16] = a["inp"]
+        p_[:, 16:48:2] = a["out"]
+        p_[:, 17:48:2] = a["mult"] % P
+        p_[:, 48] = P - 1
+        pa.append(p_)
+    pa = _cat(pa, (49,))
+    ma = _cat([e["rows"] for e in rec.events["p2"]], (P2_COLS,))
+    name = "Poseidon2WideDeg3"
+    h = _pow2(len(pa), shape.get(name))
+    mn = np.zeros((h, P2_COLS), U)
+    mn[:len(ma)] = ma
+    mn[len(ma):] = poseidon2_rows(np.zeros((1, WIDTH), U))
+    pr = np.zeros((h, 49), U)
+    pr[:len(pa)] = pa
+    preps[name], mains[name] = pr.astype(np.uint32), mn.astype(np.uint32)
+
+    # BatchFRI
+    pa = []
+    for b in bl("batchfri"):
+        a = b.a
+        n_, L = a["p_at_x"].shape
+        p_ = np.zeros((n_, L, 6), U)
+        p_[:, :, 0] = 1
+        p_[:, L - 1, 1] = 1
+        p_[:, :, 2] = a["acc"][:, None]
+        p_[:, :, 3] = a["alpha_pow"]
+        p_[:, :, 4] = a["p_at_z"]
+        p_[:, :, 5] = a["p_at_x"]
+        pa.append(p_.reshape(-1, 6))
+    pa = _cat(pa, (6,))
+    ma = _cat([e["rows"] for e in rec.events["batchfri"]], (13,))
+    finish("BatchFRI", pa, ma, len(pa))
+
+    # Select
+    pa, ma = [], []
+    for b, e in zip(bl("select"), rec.events["select"]):
+        a = b.a
+        pa.append(np.stack([np.ones(len(a["bit"]), np.int64), a["bit"], a["out1"], a["out2"], a["in1"], a["in2"],
+                            a["mult1"] % P, a["mult2"] % P], 1).astype(U))
+        ma.append(np.stack([e["bit"], e["out1"], e["out2"], e["in1"], e["in2"]], 1))
+    pa, ma = _cat(pa, (8,)), _cat(ma, (5,))
+    finish("Select", pa, ma, len(pa))
+
+    # ExpReverseBitsLen
+    pa = []
+    for b in bl("exprev"):
+        a = b.a
+        n_, L = a["exps"].shape
+        p_ = np.zeros((n_, L, 10), U)
+        i = np.arange(L)
+        p_[:, :, 0] = a["base"][:, None]
+        p_[:, 0, 1] = P - 1
+        p_[:, :, 2] = a["exps"]
+        p_[:, :, 3] = P - 1
+        p_[:, :, 4] = a["result"][:, None]
+        p_[:, L - 1, 5] = a["mult"] % P
+        p_[:, :, 6] = i[None, :]
+        p_[:, 0, 7] = 1
+        p_[:, L - 1, 8] = 1
+        p_[:, :, 9] = 1
+        pa.append(p_.reshape(-1, 10))
+    pa = _cat(pa, (10,))
+    ma = _cat([e["rows"] for e in rec.events["exprev"]], (7,))
+    finish("ExpReverseBitsLen", pa, ma, len(pa))
+
+    # PublicValues: the first CommitPublicValues' digest, 16 rows (PUB_VALUES_LOG_HEIGHT)
+    pa = np.zeros((0, 10), U)
+    ma = np.zeros((0, 1), U)
+    cs = bl("commit")
+    if cs:
+        addrs = cs[0].a["pv"][0, PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE]
+        pa = np.zeros((DIGEST_SIZE, 10), U)
+        pa[np.arange(DIGEST_SIZE), np.arange(DIGEST_SIZE)] = 1
+        pa[:, 8] = addrs
+        pa[:, 9] = P - 1
+        ma = rec.events["commit"][0]["pv"][PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE][:, None].astype(U)
+    finish("PublicValues", pa, ma, 1 << PUB_VALUES_LOG_HEIGHT)
+    return ({k: np.ascontiguousarray(v.astype(np.uint32)) for k, v in preps.items()},
+            {k: np.ascontiguousarray(v.astype(np.uint32)) for k, v in mains.items()})
+
+
+def shard(prog: RecursionProgram, shape: Optional[Dict[str, int]] = None):
+    """(machine, prep_traces, traces, public_values) of one compress-machine shard of ``prog``."""
+    rec = execute(prog)
+    pr, tr = generate_traces(rec, shape)
+    m = compress_machine()
+    pr = {c.name: pr[c.name] for c in m.chips if c.prep_width}
+    return m, pr, tr, rec.public_values
+
+
+# ------------------------------------------------------------------ programs
+
+def _rand(rng, shape):
+    return rng.integers(0, P, size=shape, dtype=np.int64).astype(U)
+
+
+def _rand_ext_nonzero(rng, n):
+    x = _rand(rng, (n, D))
+    x[:, 0] |= U(1)
+    return x
+
+
+def program_basic_mem() -> RecursionProgram:
+    """mem/constant.rs:212-221 prove_basic_mem: Write 2 at 1 (mult 1), Read it once."""
+    p = RecursionProgram(num_addrs=2)
+    p.mem_write([1], [[2, 0, 0, 0]], mult=1)
+    p.mem_read([1], [[2, 0, 0, 0]], mult=1)
+    return p
+
+
+def program_base_four_ops(n: int = 1000, seed: int = 0xDEADBEEF) -> RecursionProgram:
+    """alu_base.rs:332-366 four_ops: per round write in1 = in2*quot, in2 (mult 4), then Add/Sub/Mul/Div
+    and read each result back."""
+    rng = np.random.default_rng(seed)
+    quot, in2 = _rand(rng, n), _rand(rng, n) | U(1)
+    in1 = _m(in2, quot)
+    p = RecursionProgram()
+    a = p.alloc(6 * n).reshape(n, 6)
+    blk = lambda v: np.stack([v, v * 0, v * 0, v * 0], 1)
+    p.mem_write(a[:, 0], blk(in1), mult=4)
+    p.mem_write(a[:, 1], blk(in2), mult=4)
+    ops = [(OP_ADD, (in1 + in2) % PU), (OP_SUB, (in1 + PU - in2) % PU), (OP_MUL, _m(in1, in2)), (OP_DIV, quot)]
+    for j, (op, res) in enumerate(ops):
+        p.base_alu(op, a[:, 2 + j], a[:, 0], a[:, 1], mult=1)
+        p.mem_read(a[:, 2 + j], blk(res), 1)
+    return p
+
+
+def program_ext_four_ops(n: int = 1000, seed: int = 0xDEADBEEF) -> RecursionProgram:
+    """alu_ext.rs:339-376 four_ops over the extension field."""
+    rng = np.random.default_rng(seed)
+    quot, in2 = _rand(rng, (n, D)), _rand_ext_nonzero(rng, n)
+    in1 = ext_mul(in2, quot)
+    p = RecursionProgram()
+    a = p.alloc(6 * n).reshape(n, 6)
+    p.mem_write(a[:, 0], in1, mult=4)
+    p.mem_write(a[:, 1], in2, mult=4)
+    ops = [(OP_ADD, (in1 + in2) % PU), (OP_SUB, (in1 + PU - in2) % PU), (OP_MUL, ext_mul(in1, in2)), (OP_DIV, quot)]
+    for j, (op, res) in enumerate(ops):
+        p.ext_alu(op, a[:, 2 + j], a[:, 0], a[:, 1], mult=1)
+        p.mem_read(a[:, 2 + j], res, 1)
+    return p
+
+
+def program_select(n: int = 1000, seed: int = 0xDEADBEEF) -> RecursionProgram:
+    """select.rs:297-330 prove_select."""
+    rng = np.random.default_rng(seed)
+    in1, in2 = _rand(rng, n), _rand(rng, n)
+    bit = rng.integers(0, 2, n).astype(U)
+    o1 = np.where(bit == 1, in2, in1)
+    o2 = np.where(bit == 1, in1, in2)
+    p = RecursionProgram()
+    a = p.alloc(5 * n).reshape(n, 5)
+    blk = lambda v: np.stack([v, v * 0, v * 0, v * 0], 1)
+    p.mem_write(a[:, 0], blk(bit), 1)
+    p.mem_write(a[:, 3], blk(in1), 1)
+    p.mem_write(a[:, 4], blk(in2), 1)
+    p.select(a[:, 0], a[:, 1], a[:, 2], a[:, 3], a[:, 4], 1, 1)
+    p.mem_read(a[:, 1], blk(o1), 1)
+    p.mem_read(a[:, 2], blk(o2), 1)
+    return p
+
+
+def program_poseidon2(seed: int = 1) -> RecursionProgram:
+    """poseidon2_wide/mod.rs:135-202 test_poseidon2: perm([1;16]) and perm(random), outputs read back."""
+    rng = np.random.default_rng(seed)
+    inputs = np.stack([np.ones(WIDTH, U), _rand(rng, WIDTH)])
+    outs = poseidon2_permute(inputs)
+    p = RecursionProgram(num_addrs=4 * WIDTH)
+    for k in range(2):
+        ia = np.arange(2 * k * WIDTH, (2 * k + 1) * WIDTH)
+        oa = ia + WIDTH
+        p.mem_write(ia, np.stack([inputs[k], *(inputs[k] * 0,) * 3], 1), 1)
+        p.poseidon2(oa, ia, np.ones(WIDTH))
+        p.mem_read(oa, np.stack([outs[k], *(outs[k] * 0,) * 3], 1), 1)
+    return p
+
+
+def program_exp_reverse_bits(n: int = 100, bits: int = 16, seed: int = 7) -> RecursionProgram:
+    """exp_reverse_bits.rs tests: x^{rev_len(e)} from hinted bits, result read back."""
+    rng = np.random.default_rng(seed)
+    x = _rand(rng, n)
+    e = rng.integers(0, 1 << bits, n)
+    p = RecursionProgram()
+    xa, ea, ra = p.alloc(n), p.alloc(n * bits).reshape(n, bits), p.alloc(n)
+    blk = lambda v: np.stack([v, v * 0, v * 0, v * 0], 1)
+    p.mem_write(xa, blk(x))
+    bitv = ((e[:, None] >> np.arange(bits)[None, :]) & 1).astype(U)
+    p.hint(ea.ravel(), blk(bitv.ravel()))
+    p.exp_reverse_bits(xa, ea, ra, mult=1)
+    rev = np.array([int(format(int(v), f"0{bits}b")[::-1], 2) for v in e])
+    res = np.array([pow(int(xi), int(r), P) for xi, r in zip(x, rev)], U)
+    p.mem_read(ra, blk(res), 1)
+    return p
+
+
+def program_batch_fri(n: int = 20, length: int = 7, seed: int = 3) -> RecursionProgram:
+    """BatchFRI instances (runtime/mod.rs:535-576) over hinted alpha powers, p(z) and p(x)."""
+    rng = np.random.default_rng(seed)
+    p = RecursionProgram()
+    al, pz, px, acc = (p.alloc(n * length).reshape(n, length), p.alloc(n * length).reshape(n, length),
+                       p.alloc(n * length).reshape(n, length), p.alloc(n))
+    alv, pzv = _rand(rng, (n * length, D)), _rand(rng, (n * length, D))
+    pxv = _rand(rng, n * length)
+    p.hint(al.ravel(), alv)
+    p.hint(pz.ravel(), pzv)
+    p.mem_write(px.ravel(), np.stack([pxv, pxv * 0, pxv * 0, pxv * 0], 1))
+    p.batch_fri(acc, al, pz, px)
+    diff = pzv.copy()
+    diff[:, 0] = (diff[:, 0] + PU - pxv) % PU
+    terms = ext_mul(alv, diff).reshape(n, length, D)
+    want = terms.sum(1) % PU
+    p.mem_read(acc, want, 1)
+    return p
+
+
+def program_public_values(seed: int = 5) -> RecursionProgram:
+    """public_values.rs tests: hint 231 values and commit them; the chip checks the digest."""
+    rng = np.random.default_rng(seed)
+    p = RecursionProgram()
+    a = p.alloc(PROOF_MAX_NUM_PVS)
+    v = _rand(rng, PROOF_MAX_NUM_PVS)
+    p.hint(a, np.stack([v, v * 0, v * 0, v * 0], 1))
+    p.commit_public_values(a)
+    return p
+
+
+# The reference's fixed shape of the shrink/compress machine (machine.rs:155-171 shrink_shape)
+SHRINK_SHAPE = {"MemoryVar": 18, "Select": 18, "MemoryConst": 17, "BatchFRI": 17, "BaseAlu": 17, "ExtAlu": 15,
+                "ExpReverseBitsLen": 17, "Poseidon2WideDeg3": 16, "PublicValues": PUB_VALUES_LOG_HEIGHT}
+
+
+def program_verifier_shaped(shape: Dict[str, int] = SHRINK_SHAPE, fill: float = 0.9, seed: int = 11) -> RecursionProgram:
+    """A recursion program with the instruction mix of a verifier program that fills each chip of
+    ``shape`` to ``fill``: hinted proof data (MemoryVar), a Poseidon2 sponge over it (the transcript and
+    Merkle paths), the index bits of the queries (ExpReverseBitsLen), Merkle-path selects (Select),
+    FRI reduced openings (BatchFRI), base/extension arithmetic (BaseAlu / ExtAlu) and constants
+    (MemoryConst), ending with CommitPublicValues.  Every value is produced by the runtime."""
+    rng = np.random.default_rng(seed)
+    cap = lambda name, per_row=1: int(fill * (1 << shape[name])) * per_row
+    p = RecursionProgram()
+    blk = lambda v: np.stack([v, v * 0, v * 0, v * 0], 1)
+
+    n_p2 = cap("Poseidon2WideDeg3")
+    n_ext = cap("ExtAlu", 4)
+    n_base = cap("BaseAlu", 4)
+    n_sel = cap("Select")
+    erb_len = 22
+    n_erb = cap("ExpReverseBitsLen") // erb_len
+    fri_len = 64
+    n_fri = cap("BatchFRI") // fri_len
+    n_var = cap("MemoryVar", 2)
+    n_const = cap("MemoryConst", 2)
+
+    # hinted proof data: ext blocks (alpha powers, p(z)) and felts (p(x), sponge input, bits)
+    n_hint_ext = 2 * n_fri * fri_len
+    n_bits = n_erb * erb_len
+    n_hint_felt = max(0, n_var - n_hint_ext - n_bits - PROOF_MAX_NUM_PVS)
+    ext_a = p.alloc(n_hint_ext)
+    p.hint(ext_a, _rand(rng, (n_hint_ext, D)))
+    bits_a = p.alloc(n_bits)
+    p.hint(bits_a, blk(rng.integers(0, 2, n_bits).astype(U)))
+    felt_a = p.alloc(n_hint_felt)
+    p.hint(felt_a, blk(_rand(rng, n_hint_felt)))
+
+    # constants (MemoryConst writes, read by the ALUs); the rest of MemoryConst: read-backs below
+    n_cw = max(16, n_const // 2)
+    const_a = p.alloc(n_cw)
+    p.mem_write(const_a, blk(_rand(rng, n_cw) | U(1)))
+
+    # Poseidon2 sponge: chains of permutations absorbing hinted felts; 8 lanes of capacity carried
+    chains = 64
+    per = n_p2 // chains
+    state = np.stack([felt_a[(np.arange(chains) * 16 + i) % max(1, n_hint_felt)] for i in range(WIDTH)], 1)
+    absorb = 0
+    p2_outs = []
+    for r in range(per):
+        out = p.alloc(chains * WIDTH).reshape(chains, WIDTH)
+        p.poseidon2(out, state)
+        p2_outs.append(out)
+        nxt = out.copy()
+        idx = (chains * 8 * r + np.arange(chains * 8) + absorb) % max(1, n_hint_felt)
+        nxt[:, :8] = felt_a[idx].reshape(chains, 8)
+        state = nxt
+    p2_last = p2_outs[-1] if p2_outs else const_a[:chains * WIDTH].reshape(-1, WIDTH)
+
+    # base ALU: mix hinted felts with constants and permutation outputs (4 ops, no division by unknowns)
+    src = np.concatenate([felt_a, p2_last.ravel()]) if n_hint_felt else p2_last.ravel()
+    out_b = p.alloc(n_base)
+    ops = rng.integers(0, 3, n_base)
+    div_every = 16
+    ops[::div_every] = OP_DIV  # division by a (non-zero) constant
+    in1 = src[rng.integers(0, len(src), n_base)]
+    in2 = np.where(ops == OP_DIV, const_a[rng.integers(0, n_cw, n_base)], src[rng.integers(0, len(src), n_base)])
+    p.base_alu(ops, out_b, in1, in2, mult=None)
+
+    # selects on hinted bits (Merkle path ordering)
+    sbit = bits_a[np.arange(n_sel) % max(1, n_bits)] if n_bits else const_a[:n_sel]
+    s_in1, s_in2 = out_b[rng.integers(0, n_base, n_sel)], src[rng.integers(0, len(src), n_sel)]
+    so1, so2 = p.alloc(n_sel), p.alloc(n_sel)
+    p.select(sbit, so1, so2, s_in1, s_in2)
+
+    # exp reverse bits: query index powers of a generator-like base from the sponge
+    erb_base = src[rng.integers(0, len(src), n_erb)]
+    erb_res = p.alloc(n_erb)
+    p.exp_reverse_bits(erb_base, bits_a.reshape(n_erb, erb_len), erb_res)
+
+    # batch FRI: reduced openings over hinted alpha powers / p(z) and felt p(x)
+    fri_acc = p.alloc(n_fri)
+    px = np.concatenate([so1, so2, out_b])[:n_fri * fri_len]
+    if len(px) < n_fri * fri_len:
+        px = np.resize(px, n_fri * fri_len)
+    p.batch_fri(fri_acc, ext_a[:n_fri * fri_len].reshape(n_fri, fri_len),
+                ext_a[n_fri * fri_len:].reshape(n_fri, fri_len), px.reshape(n_fri, fri_len))
+
+    # extension ALU: each reduced opening is consumed once (BatchFRI writes acc with multiplicity 1,
+    # batch_fri.rs:113), then arithmetic over those sums and the hinted ext values
+    out_f = p.alloc(n_fri)
+    p.ext_alu(OP_ADD, out_f, fri_acc, ext_a[:n_fri])
+    ext_src = np.concatenate([out_f, ext_a])
+    n_e = max(0, n_ext - n_fri)
+    out_e = p.alloc(n_e)
+    eops = rng.integers(0, 3, n_e)
+    p.ext_alu(eops, out_e, ext_src[rng.integers(0, len(ext_src), n_e)], ext_src[rng.integers(0, len(ext_src), n_e)])
+
+    # public values: hinted, the digest is the first 8 words of a permutation output
+    pv_a = p.alloc(PROOF_MAX_NUM_PVS)
+    p.hint(pv_a, blk(_rand(rng, PROOF_MAX_NUM_PVS)))
+    pv_addrs = pv_a.copy()
+    pv_addrs[PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE] = p2_last[0, :DIGEST_SIZE]
+    p.commit_public_values(pv_addrs)
+
+    # MemoryConst read-backs of computed values (the verifier's assertions)
+    n_rb = max(0, n_const - n_cw)
+    if n_rb:
+        rec = execute(_copy_program(p))
+        pool = np.concatenate([out_b, so1, so2])[:n_rb]
+        p.mem_read(pool, rec_mem(rec, pool), 1)
+    return p
+
+
+def _copy_program(p: RecursionProgram) -> RecursionProgram:
+    return RecursionProgram([Block(b.kind, {k: v.copy() for k, v in b.a.items()}) for b in p.blocks], p.num_addrs)
+
+
+def rec_mem(rec: ExecutionRecord, addrs: np.ndarray) -> np.ndarray:
+    """Values at ``addrs`` after executing ``rec``'s program (re-derived from its events)."""
+    mem = np.zeros((rec.program.num_addrs, D), U)
+    bl = rec.program.blocks
+    ev_iter = {k: iter(v) for k, v in rec.events.items()}
+    for b in bl:
+        a, k = b.a, b.kind
+        e = next(ev_iter[k]) if k in ev_iter else None
+        if k == "mem":
+            mem[a["addr"][a["write"]]] = a["vals"][a["write"]]
+        elif k == "hint":
+            mem[a["addr"]] = a["vals"]
+        elif k == "base":
+            mem[a["out"], 0] = e["out"]
+        elif k == "ext":
+            mem[a["out"]] = e["out"]
+        elif k == "p2":
+            mem[a["out"].ravel(), 0] = e["rows"][:, P2_OUT:P2_OUT + WIDTH].ravel()
+        elif k == "select":
+            mem[a["out1"], 0] = e["out1"]
+            mem[a["out2"], 0] = e["out2"]
+        elif k == "exprev":
+            mem[a["result"], 0] = e["rows"].reshape(e["n"], e["L"], 7)[:, -1, 4]
+        elif k == "batchfri":
+            mem[a["acc"]] = e["rows"].reshape(e["n"], e["L"], 13)[:, -1, 0:4]
+    return mem[addrs]
