@@ -396,8 +396,22 @@ def compress_bench(args):
     t0 = time.time()
     m, prep, traces, pvs = R.shard(R.program_verifier_shaped(seed=1), R.SHRINK_SHAPE)
     gen_s = time.time() - t0
-    torch.cuda.set_device(0)
-    prover = HipProver(Device(0), m, prep, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch.distributed as dist
+    rehearse = os.environ.get("ZKM_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local_rank = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank)
+    coll_dev = "cpu" if rehearse else "cuda"
+    if world > 1:
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    prover = HipProver(Device(local_rank), m, prep, num_queries=R.COMPRESS_NUM_QUERIES,
+                       log_blowup=R.COMPRESS_LOG_BLOWUP)
     dev = {k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in traces.items()}
     torch.cuda.synchronize()
     layers = [32, 16, 8, 4, 2, 1]
@@ -425,13 +439,32 @@ def compress_bench(args):
     for _ in range(max(1, args.warmup)):
         proofs = prove_layer(max(1, args.inflight))
     assert all(p == proofs[0] for p in proofs)
-    torch.cuda.synchronize()
+    leaves = [proofs[0]] * 64  # stand-ins for the 64 leaf (core shard) proofs the first layer verifies
+
+    def tree():
+        if world == 1:
+            for n in layers:
+                prove_layer(n)
+        else:
+            from zkmips_amd.dist import compress_tree_distributed
+            compress_tree_distributed(None, leaves, device=coll_dev,
+                                      prove_nodes=lambda layer, work: prove_layer(len(work)))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
     t1 = time.time()
     for _ in range(args.steps):
-        for n in layers:
-            prove_layer(n)
-    torch.cuda.synchronize()
+        tree()
+    barrier()
     el = time.time() - t1
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
     n_proofs = sum(layers) * args.steps
     rows = max(v.shape[0] for v in traces.values())
     # serial single-proof latency
@@ -442,7 +475,7 @@ def compress_bench(args):
     torch.cuda.synchronize()
     serial_ms = (time.time() - t2) / 3 * 1e3
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and rank == 0 and world == 1:
         from tests import _oracle as O
         o = O.OracleProver(m, prep, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
         tc = time.time()
@@ -455,7 +488,7 @@ def compress_bench(args):
                          "byte-identical to the GPU proof"}
     line = {
         "metric": "compress proofs/sec (64-leaf compress tree = 63 recursion-machine proofs, BASELINE config 5)",
-        "value": round(n_proofs / el, 3), "unit": "proofs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "value": round(n_proofs / el, 3), "unit": "proofs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
         "data": "synthetic verifier-shaped recursion program (recursion.program_verifier_shaped), traces resident in HBM",
@@ -463,11 +496,17 @@ def compress_bench(args):
                                f"({', '.join(f'{k} 2^{v}' for k, v in R.SHRINK_SHAPE.items())}), blowup 4, 42 queries",
                    "max_rows": rows, "main_cells": int(sum(v.size for v in traces.values())),
                    "prep_cells": int(sum(v.size for v in prep.values())), "proof_bytes": len(proofs[0]),
-                   "parallelism": f"a layer's proofs {args.inflight} in flight", "trace_generation_s": round(gen_s, 1)},
+                   "parallelism": (f"a layer's proofs {args.inflight} in flight" if world == 1 else
+                                   f"node j of a layer on rank j % {world} ({args.inflight} in flight per rank), "
+                                   "each layer's proofs all-gathered (RCCL) before the next"),
+                   "trace_generation_s": round(gen_s, 1)},
         "ms_per_proof": round(1e3 * el / n_proofs, 3), "serial_ms_per_proof": round(serial_ms, 3),
         "rows_per_s": round(rows * n_proofs / el, 1), "cpu_baseline": cpu,
     }
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def pmc_child(args):
