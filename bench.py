@@ -252,34 +252,52 @@ def execution_bench(args):
     from zkmips_amd._lib import Device
     from zkmips_amd.proof import machine_global_sum_is_zero
     from zkmips_amd.prover import HipProver
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch.distributed as dist
+    rehearse = os.environ.get("ZKM_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local_rank = local_rank % max(1, torch.cuda.device_count())
+    coll_dev = "cpu" if rehearse else "cuda"
     t0 = time.time()
     max_steps = min((1 << args.log_n) * 4 // 5, (1 << 24) // 5 - 1)
     run = MC.program_shards(MC.sha_program(args.sha_blocks, seed=1), seed=1, shard_size=max_steps,
                             precompile_events_per_shard=args.sha_events_per_shard)
     gen_s = time.time() - t0
     print(f"sha2: {len(run)} shards generated in {gen_s:.1f} s", file=sys.stderr, flush=True)
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from zkmips_amd.dist import assign_shards, prove_shards_distributed
+    mine = set(assign_shards(len(run), world, rank))  # config 4: the execution's shards dealt across ranks
     m, prep, _, _ = run[0]
     prep = {k: v for k, v in prep.items() if v is not None}
-    prover = HipProver(Device(0), m, prep, num_queries=args.queries)
-    dev = [({k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in tr.items()}, pv) for _, _, tr, pv in run]
+    prover = HipProver(Device(local_rank), m, prep, num_queries=args.queries)
+    dev = [({k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in tr.items()}, pv) if i in mine else None
+           for i, (_, _, tr, pv) in enumerate(run)]
     rows = [max(v.shape[0] for v in tr.values()) for _, _, tr, _ in run]
     kinds = ["cpu" if "Cpu" in tr else "memory" if "MemoryGlobalInit" in tr else
              "sha_extend" if "ShaExtend" in tr else "sha_compress" for _, _, tr, _ in run]
     torch.cuda.synchronize()
 
-    def prove_all():
-        out = [None] * len(run)
+    def prove_local():
+        idx = sorted(mine)
+        out = {}
         nxt = [0]
         lock = threading.Lock()
 
         def worker():
             while True:
                 with lock:
-                    i = nxt[0]
+                    k = nxt[0]
                     nxt[0] += 1
-                if i >= len(run):
+                if k >= len(idx):
                     return
+                i = idx[k]
                 out[i] = prove_resident(prover, dev[i][0], dev[i][1])
         th = [threading.Thread(target=worker) for _ in range(max(1, args.inflight))]
         for t in th:
@@ -288,19 +306,38 @@ def execution_bench(args):
             t.join()
         return out
 
+    def prove_all():
+        """Every rank proves its shards; rank 0 receives all proofs in shard order (one gather, RCCL
+        over xGMI) and checks the machine-level global cumulative sum (machine.rs:639-654)."""
+        if world == 1:
+            out = prove_local()
+            proofs = [out[i] for i in range(len(run))]
+            assert machine_global_sum_is_zero(proofs), "the execution's global cumulative sums do not add to zero"
+            return proofs
+        local = prove_local()
+        return prove_shards_distributed(lambda i: local[i], len(run), device=coll_dev, check_global_sum=True)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
     for _ in range(max(1, args.warmup)):
         proofs = prove_all()
         print("sha2: warmup execution proven", file=sys.stderr, flush=True)
-    assert machine_global_sum_is_zero(proofs), "the execution's global cumulative sums do not add to zero"
-    torch.cuda.synchronize()
+    barrier()
     t1 = time.time()
     for _ in range(args.steps):
         prove_all()
-    torch.cuda.synchronize()
+    barrier()
     el = time.time() - t1
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
     line = {
         "metric": "shard trace rows proved/sec (whole sha2-precompile execution, BASELINE config 3)",
-        "value": round(sum(rows) * args.steps / el, 1), "unit": "rows/s", "n_gpus": 1, "steps": args.steps,
+        "value": round(sum(rows) * args.steps / el, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
         "data": "synthetic sha2 guest (mips_core.sha_program), traces resident in HBM",
@@ -308,10 +345,15 @@ def execution_bench(args):
                                f"({', '.join(f'{k} 2^{r.bit_length() - 1}' for k, r in zip(kinds, rows))}), "
                                f"all MIPS + syscall + SHA-256 + memory chips, full commit+open per shard",
                    "shards": len(run), "rows_per_execution": sum(rows), "fri_queries": args.queries,
-                   "proof_bytes": sum(len(p) for p in proofs), "parallelism": f"{args.inflight} shards in flight",
+                   "proof_bytes": sum(len(p) for p in proofs) if rank == 0 else None,
+                   "parallelism": f"{args.inflight} shards in flight" + (f" per rank, shards dealt over {world} ranks, "
+                                  "proofs gathered to rank 0 (global sum checked there)" if world > 1 else ""),
                    "trace_generation_s": round(gen_s, 1), "global_sum_checked": True},
     }
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def tracegen_bench(args):
@@ -342,15 +384,20 @@ def tracegen_bench(args):
     gmsg = rng.integers(0, 256, (n, 7)).astype(np.uint32)
     gmsg[:, 0], gmsg[:, 1], gmsg[:, 2] = 1, rng.integers(0, 1 << 24, n), rng.integers(0, 1 << 30, n)
     d_glob = TG.to_device(TG.global_events(gmsg, rng.integers(0, 2, n), np.ones(n)))
+    d_p2 = torch.from_numpy(rng.integers(0, 0x7F000001, (n // 4) * 32).astype(np.int32)).cuda()
     chips = {
         "Cpu": (lambda: TG.cpu_trace(d_ev, n, 1, d_prog, len(prog), height=n, byte_mult=bm, program_mult=pm),
                 280 + 4 * TG.CPU_WIDTH),
         "Global": (lambda: TG.global_trace(d_glob, n, height=n, byte_mult=bm), 32 + 4 * TG.GLOBAL_WIDTH),
         "AddSub": (lambda: TG.add_sub_trace(d_add, n, height=n, byte_mult=bm), 28 + 4 * TG.ADD_SUB_WIDTH),
         "MemoryLocal": (lambda: TG.memory_local_trace(d_ml, n, height=n // 4), 28 + 4 * 14),
+        # recursion machine: a permutation per row (compute-bound); n // 4 rows
+        "Poseidon2WideDeg3": (lambda: TG.poseidon2_wide_trace(d_p2, n // 4, height=n // 4), 64 + 4 * 313, n // 4),
     }
     res = {}
-    for name, (fn, bytes_per_row) in chips.items():
+    for name, spec in chips.items():
+        fn, bytes_per_row = spec[0], spec[1]
+        rows_n = spec[2] if len(spec) > 2 else n
         for _ in range(max(1, args.warmup)):
             fn()
         torch.cuda.synchronize()
@@ -361,8 +408,9 @@ def tracegen_bench(args):
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.steps
-        gbs = n * bytes_per_row / ms / 1e6
-        res[name] = {"ms": round(ms, 4), "rows_per_s": round(n / ms * 1e3, 1), "algorithmic_bytes_per_row": bytes_per_row,
+        gbs = rows_n * bytes_per_row / ms / 1e6
+        res[name] = {"ms": round(ms, 4), "rows": rows_n, "rows_per_s": round(rows_n / ms * 1e3, 1),
+                     "algorithmic_bytes_per_row": bytes_per_row,
                      "GBps": round(gbs, 1), "frac_of_hbm_peak": round(gbs / (HBM_PEAK_GBS), 3)}
     cpu = res["Cpu"]
     line = {

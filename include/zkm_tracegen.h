@@ -11,7 +11,9 @@
  *                                                                                  (include/memory_global.hpp:9-43)
  *   syscall_event_to_row_koalabear(const SyscallEvent*, bool, SyscallCols*)        (include/syscall.hpp:8-16)
  *
- * and, beyond that ABI, the Global chip (the reference's Rust generate_trace, global/mod.rs:77-196).
+ * and, beyond that ABI, the Global chip (the reference's Rust generate_trace, global/mod.rs:77-196), and
+ * from the recursion machine's row ABI (crates/recursion/core/src/sys.rs:22-110) the Poseidon2WideDeg3
+ *   poseidon2_wide_event_to_row_koalabear(const KoalaBear *input, KoalaBear *row, bool sbox_state)
  *
  * Here each entry point fills a WHOLE padded trace in GPU memory from an event array in GPU memory:
  * one thread per row, rows staged through LDS so the row-major trace is written in full cache
@@ -145,6 +147,23 @@ int zkm_syscall_events_to_trace(const zkm_syscall_event *events, uint64_t n, int
  * or message[0] is not 16-bit. */
 int zkm_global_events_to_trace(const zkm_global_lookup_event *events, uint64_t n, uint32_t *trace,
                                uint64_t height, uint32_t *byte_mult, uint32_t *final_digest, void *stream);
+
+/* ---- recursion machine (crates/recursion/core/src/sys.rs:22-110, include/poseidon2_wide.hpp) ---- */
+#define ZKM_POSEIDON2_WIDE_DEG3_WIDTH 313  /* PermutationSBox (poseidon2_wide/columns/permutation.rs:20-72) */
+
+/* Poseidon2Io<KoalaBear> = Poseidon2Event (recursion/core/src/lib.rs): input[16] then output[16] */
+typedef struct {
+    uint32_t input[16];
+    uint32_t output[16];
+} zkm_poseidon2_event;
+
+/* Poseidon2WideDeg3 main trace: poseidon2_wide_event_to_row_koalabear(input, row, sbox_state = true)
+ * (sys.rs:102-106, include/poseidon2_wide.hpp) for every event, rows [n, height) the permutation of
+ * zero (poseidon2_wide/trace.rs dummy row).  repr: ZKM_REPR_MONTGOMERY for a Rust
+ * Vec<Poseidon2Event<KoalaBear>> as it lies in memory, or ZKM_REPR_CANONICAL.  The output words are
+ * not read (the permutation is recomputed). */
+int zkm_poseidon2_wide_events_to_trace(const zkm_poseidon2_event *events, uint64_t n, uint32_t repr,
+                                       uint32_t *trace, uint64_t height, void *stream);
 
 #ifdef __cplusplus
 }

@@ -108,6 +108,15 @@ extern "C" {
     pub fn zkm_quotient_jit_compile(blob: *const u32, nwords: usize, code_bytes: *mut u64) -> c_int;
 
     // ---- zkm_tracegen.h (device pointers; `stream` is a hipStream_t, null = the null stream) ----
+    /// Poseidon2WideDeg3 main trace (recursion/core/src/sys.rs:102-106); `repr` 1 = Montgomery records.
+    pub fn zkm_poseidon2_wide_events_to_trace(
+        events: *const u32,
+        n: u64,
+        repr: u32,
+        trace: *mut u32,
+        height: u64,
+        stream: *mut c_void,
+    ) -> c_int;
     pub fn zkm_cpu_events_to_trace(
         events: *const CpuEventFfi,
         n: u64,

@@ -191,3 +191,56 @@ def test_gpu_shrink_shape_full_size_verifies(dev):
     bad = bytearray(proof)
     bad[len(bad) // 2] ^= 1
     assert cpu.verify(bytes(bad)) != 0
+
+
+def _p2_records(rec):
+    """Poseidon2Io records (input[16], output[16]) of a run's Poseidon2 events, canonical."""
+    rows = np.concatenate([e["rows"] for e in rec.events["p2"]])
+    return np.ascontiguousarray(np.concatenate([rows[:, R.P2_EXT:R.P2_EXT + 16], rows[:, R.P2_OUT:R.P2_OUT + 16]],
+                                               1).astype(np.uint32))
+
+
+def test_poseidon2_wide_trace_abi_declared():
+    hdr = open(os.path.join(os.path.dirname(GOLDEN), "..", "include", "zkm_tracegen.h")).read()
+    assert "#define ZKM_POSEIDON2_WIDE_DEG3_WIDTH 313" in hdr and "zkm_poseidon2_wide_events_to_trace" in hdr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("montgomery", [False, True])
+def test_gpu_poseidon2_wide_device_trace_equals_host(dev, montgomery):
+    """zkm_poseidon2_wide_events_to_trace == the host trace builder, padding rows included, for the
+    shrink-shape program's 59k permutations (height 2^16) and a ragged small case; Montgomery input
+    (a Rust Vec<Poseidon2Event<KoalaBear>> as it lies in memory) gives the same canonical trace."""
+    import torch
+    from zkmips_amd import tracegen as TG
+    for prog, shape in ((R.program_poseidon2(), None), (R.program_verifier_shaped(), R.SHRINK_SHAPE)):
+        rec = R.execute(prog)
+        _, tr = R.generate_traces(rec, shape)
+        want = tr["Poseidon2WideDeg3"]
+        recs = _p2_records(rec)
+        if montgomery:
+            recs = ((recs.astype(np.uint64) << np.uint64(32)) % np.uint64(R.P)).astype(np.uint32)
+        d = torch.from_numpy(recs.view(np.int32).reshape(-1).copy()).cuda()
+        got = TG.poseidon2_wide_trace(d, len(recs), height=want.shape[0], montgomery=montgomery)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.gpu
+def test_gpu_device_poseidon2_trace_proves_identically(dev):
+    """A compress shard whose Poseidon2WideDeg3 trace comes from the device proves to the host traces'
+    proof bytes."""
+    import torch
+    from zkmips_amd import tracegen as TG
+    from zkmips_amd.prover import HipProver
+    shape = {k: (v - 4 if k != "PublicValues" else v) for k, v in R.SHRINK_SHAPE.items()}
+    prog = R.program_verifier_shaped(shape)
+    m, pr, tr, pvs = R.shard(prog, shape)
+    rec = R.execute(R.program_verifier_shaped(shape))
+    recs = _p2_records(rec)
+    d = torch.from_numpy(recs.view(np.int32).reshape(-1).copy()).cuda()
+    dev_tr = dict(tr)
+    dev_tr["Poseidon2WideDeg3"] = TG.poseidon2_wide_trace(d, len(recs), height=tr["Poseidon2WideDeg3"].shape[0]) \
+        .cpu().numpy().view(np.uint32)
+    gpu = HipProver(dev, m, pr, num_queries=NQ, log_blowup=LB)
+    assert gpu.prove_shard(dev_tr, pvs) == gpu.prove_shard(tr, pvs)

@@ -189,6 +189,7 @@ def _bind():
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
         L.zkm_syscall_events_to_trace.argtypes = [vp, u64, C.c_int, vp, u64, vp]
         L.zkm_global_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp, vp]
+        L.zkm_poseidon2_wide_events_to_trace.argtypes = [vp, u64, C.c_uint32, vp, u64, vp]
         L._tracegen_bound = True
     return L
 
@@ -328,3 +329,18 @@ def shard_traces(capture: dict, byte_mult=None):
     ge = shard_global_events(capture)
     out["Global"], _ = global_trace(to_device(ge), len(ge), byte_mult=byte_mult)
     return out
+
+
+POSEIDON2_WIDE_WIDTH = 313  # ZKM_POSEIDON2_WIDE_DEG3_WIDTH
+
+
+def poseidon2_wide_trace(events_dev, n: int, height: int = None, montgomery: bool = False):
+    """Poseidon2WideDeg3 main trace (height x 313 int32, canonical, on the GPU) from n Poseidon2Io
+    records (32 words: input[16], output[16]) in a uint32/int32 GPU tensor; rows >= n are the
+    permutation of zero (recursion/core/src/chips/poseidon2_wide/trace.rs)."""
+    height = height or _pow2(n)
+    t = _trace(height, POSEIDON2_WIDE_WIDTH)
+    what = "zkm_poseidon2_wide_events_to_trace"
+    _lib.check(_bind().zkm_poseidon2_wide_events_to_trace(_words(events_dev, 32 * n, what) if n else None, n,
+                                                          1 if montgomery else 0, t.data_ptr(), height, _stream()), what)
+    return t
