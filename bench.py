@@ -780,7 +780,10 @@ def main():
     tb, tn = stage_traffic(pmc, dom)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": round(tb / tn) if tb else None, "kernel": dom,
+                # PMC bytes per proof over the stage's launches per proof (the stage brackets every kernel
+                # it runs, e.g. a commit's leaf hashing plus its injected shorter matrices), the same
+                # denominator as algorithmic_bytes_per_launch
+                "traffic": round(tb / (cnt / nprof)) if tb else None, "kernel": dom,
                 "launches": cnt, "avg_ms": round(ms / cnt, 4),
                 "algorithmic_bytes_per_launch": round(units / cnt),
                 "traffic_source": "rocprofv3 FETCH_SIZE/WRITE_SIZE passes in this run (2xFETCH+WRITE)" if tb else None}

@@ -1,12 +1,12 @@
-// Poseidon2 one-thread permutation throughput on MI355X: new (zkmips_amd/csrc/p2.cuh) vs the
-// previous form (p2_old.cuh).  Each thread permutes its own state ITER times (no memory traffic
-// inside the loop), so the rate is the VALU-issue-bound permutation rate.
+// Poseidon2 one-thread permutation throughput on MI355X (zkmips_amd/csrc/p2.cuh).  Each thread
+// permutes its own state ITER times (no memory traffic inside the loop), so the rate is the
+// VALU-issue-bound permutation rate.  (The A/B against the pre-optimisation form is recorded in
+// profiles/r01_p2_ab.txt; that form is gone.)
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 p2_probe.hip -o p2_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
 #include "../../zkmips_amd/csrc/p2.cuh"
-#include "p2_old.cuh"
 
 #define ITER 64
 
@@ -18,38 +18,22 @@ __global__ __launch_bounds__(256) void k_new(uint32_t *out) {
     for (int k = 0; k < 16; k++) x ^= s[k];
     out[blockIdx.x * 256 + threadIdx.x] = x;
 }
-__global__ __launch_bounds__(256) void k_old(uint32_t *out) {
-    uint32_t s[16];
-    for (int k = 0; k < 16; k++) s[k] = (threadIdx.x * 16 + k) % kb::P;
-    for (int i = 0; i < ITER; i++) p2old::permute(s);
-    uint32_t x = 0;
-    for (int k = 0; k < 16; k++) x ^= s[k];
-    out[blockIdx.x * 256 + threadIdx.x] = x;
-}
-
 int main() {
     const int blocks = 256 * 64;
-    uint32_t *out, *h = new uint32_t[blocks * 256], *h2 = new uint32_t[blocks * 256];
+    uint32_t *out;
     if (hipMalloc(&out, (size_t)blocks * 256 * 4) != hipSuccess) return 1;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    for (int v = 0; v < 2; v++) {
-        auto f = v ? k_old : k_new;
-        hipLaunchKernelGGL(f, dim3(blocks), dim3(256), 0, 0, out);
-        (void)hipDeviceSynchronize();
-        (void)hipEventRecord(e0);
-        for (int r = 0; r < 3; r++) hipLaunchKernelGGL(f, dim3(blocks), dim3(256), 0, 0, out);
-        (void)hipEventRecord(e1);
-        (void)hipEventSynchronize(e1);
-        float ms;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        (void)hipMemcpy(v ? h2 : h, out, (size_t)blocks * 256 * 4, hipMemcpyDeviceToHost);
-        const double perms = 3.0 * blocks * 256 * ITER;
-        printf("%s: %.3f ms  %.3e perms/s\n", v ? "old" : "new", ms / 3, perms / (ms * 1e-3));
-    }
-    int bad = 0;
-    for (int i = 0; i < blocks * 256; i++) bad += h[i] != h2[i];
-    printf("outputs %s (%d differ)\n", bad ? "DIFFER" : "identical", bad);
-    return bad != 0;
+    hipLaunchKernelGGL(k_new, dim3(blocks), dim3(256), 0, 0, out);
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(e0);
+    for (int r = 0; r < 3; r++) hipLaunchKernelGGL(k_new, dim3(blocks), dim3(256), 0, 0, out);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const double perms = 3.0 * blocks * 256 * ITER;
+    printf("p2: %.3f ms  %.3e perms/s\n", ms / 3, perms / (ms * 1e-3));
+    return 0;
 }
