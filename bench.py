@@ -568,6 +568,32 @@ def pmc_child(args):
     assert a == b
 
 
+def bind_near_gpu(device: int):
+    """Pin this rank's host threads to the CPUs of its GPU's NUMA node (sysfs local_cpulist of the GPU's
+    PCI function), intersected with the CPUs this process may use, so the page-locked trace buffers it
+    then allocates (first touch) and the DMA reads of them stay on the GPU's socket.  Best effort:
+    returns the CPU list used, or None when the topology is not visible."""
+    try:
+        hip = C.CDLL("libamdhip64.so")
+        buf = C.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+            return None
+        bus = buf.value.decode().lower()
+        with open(f"/sys/bus/pci/devices/{bus}/local_cpulist") as f:
+            spec = f.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        if not cpus:
+            return None
+        os.sched_setaffinity(0, cpus)
+        return f"{bus}: {len(cpus)} CPUs ({spec})"
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -617,6 +643,7 @@ def main():
     if rehearse:
         local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
+    numa = bind_near_gpu(local_rank) if os.environ.get("ZKM_NO_NUMA_BIND") != "1" else None
     coll_dev = "cpu" if rehearse else "cuda"
     if world > 1:
         if rehearse:
@@ -867,6 +894,7 @@ def main():
                      "ms_per_shard": round(1e3 * elapsed_res / (args.steps * K), 3),
                      "what": "same steps, traces already in HBM (no H2D)"},
         "h2d_bytes_per_shard": int(sum(v.nbytes for v in traces.values())),
+        "host_threads_bound_to": numa,
         "pageable_single_shard_ms": round(pageable_s * 1e3, 3),
         "roofline": roofline,
         "ntt": ntt,
