@@ -678,6 +678,8 @@ def main():
     torch.cuda.synchronize()
     rows_per_shard = max(v.shape[0] for v in traces.values())
 
+    stagger = None
+
     def slot_steps(k, nsteps, mode):
         """nsteps shard proofs of in-flight slot k; returns the last proof.
         mode "pipelined": H2D of step j+1 (pinned host -> HBM, DMA on the slot's copy stream) is in
@@ -706,10 +708,16 @@ def main():
                 e = torch.cuda.Event()
                 e.record(cs)
             return e
+        # the slots' first copies go one after another (slot k starts when slot k-1's has landed), so
+        # slot 0 proves after one copy time instead of all slots waiting for K copies sharing PCIe
+        if stagger is not None and k > 0:
+            stagger[k - 1].wait(60)  # bounded: a failing slot must not hang the others
         ev = issue(0)
         pr = b""
         for j in range(nsteps):
             ev.synchronize()
+            if j == 0 and stagger is not None:
+                stagger[k].set()
             nxt = issue(j + 1) if j + 1 < nsteps else None
             # ZKM_BENCH_DMA_PROBE=1 (experiment only): the same copies, proofs from the resident traces
             src = dev_t if os.environ.get("ZKM_BENCH_DMA_PROBE") == "1" else bufs[j % 2]
@@ -724,6 +732,9 @@ def main():
             gather(proof)
             return proof
         import threading
+        nonlocal stagger
+        stagger = ([threading.Event() for _ in range(K)]
+                   if mode == "pipelined" and os.environ.get("ZKM_NO_STAGGER") != "1" else None)
         out = [b""] * K
         def slot(k):
             out[k] = slot_steps(k, nsteps, mode)
