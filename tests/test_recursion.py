@@ -70,6 +70,7 @@ PROGRAMS = {
     "exp_reverse_bits": lambda: R.program_exp_reverse_bits(100, 16),
     "batch_fri": lambda: R.program_batch_fri(20, 7),
     "public_values": R.program_public_values,
+    "merkle_openings": lambda: R.program_merkle_openings()[0],
 }
 
 SMALL_SHAPE = {k: (v - 7 if k != "PublicValues" else v) for k, v in R.SHRINK_SHAPE.items()}
@@ -100,6 +101,29 @@ def test_verifier_shaped_program():
     o = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
     rc, proof = o.prove(tr, pvs)
     assert rc == 0 and o.verify(proof) == 0
+
+
+def test_merkle_layers_root_is_the_mmcs_root():
+    """The recursion program's hashing (sponge of a row, TruncatedPermutation of two digests) is the
+    MerkleTreeMmcs of the core prover: its root equals the oracle's MMCS root of the same matrix."""
+    for h, w in ((16, 8), (64, 21), (256, 67)):
+        m = np.random.default_rng(h).integers(0, R.P, (h, w)).astype(np.uint32)
+        assert np.array_equal(R.merkle_layers(m)[-1][0].astype(np.uint32), O.merkle_root([m]))
+
+
+def test_merkle_openings_reject_a_wrong_path():
+    """A forged sibling digest (or opened value) recomputes a different root: the runtime's read-back of
+    the root fails, and a trace built anyway leaves the memory bus unbalanced."""
+    p, mat = R.program_merkle_openings(6, 9, 4, seed=2)
+    hint = next(b for b in p.blocks if b.kind == "hint" and len(b) == 4 * 6 * 8)  # the sibling digests
+    hint.a["vals"][5, 0] = (hint.a["vals"][5, 0] + 1) % R.P
+    with pytest.raises(RuntimeError):
+        R.shard(p)
+    p2, _ = R.program_merkle_openings(6, 9, 4, seed=2)
+    rows = next(b for b in p2.blocks if b.kind == "hint" and len(b) == 4 * 9)  # the opened rows
+    rows.a["vals"][3, 0] = (rows.a["vals"][3, 0] + 1) % R.P
+    with pytest.raises(RuntimeError):
+        R.shard(p2)
 
 
 def test_reference_should_panic_cases():

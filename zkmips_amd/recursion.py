@@ -1079,6 +1079,77 @@ def program_public_values(seed: int = 5) -> RecursionProgram:
     return p
 
 
+def merkle_layers(matrix: np.ndarray) -> List[np.ndarray]:
+    """MerkleTreeMmcs over one matrix (kb31_poseidon2.rs:176-177): leaf i = PaddingFreeSponge<16,8,8>
+    of row i (state zeroed, each 8-chunk overwrites lanes [0, len), permute; out = lanes 0..8), node =
+    TruncatedPermutation(left || right)[0..8].  Layers from the leaves (h x 8) to the root (1 x 8)."""
+    M = np.asarray(matrix, U) % PU
+    h, w = M.shape
+    st = np.zeros((h, WIDTH), U)
+    for c in range(0, w, 8):
+        chunk = M[:, c:c + 8]
+        st[:, :chunk.shape[1]] = chunk
+        st = poseidon2_permute(st)
+    layers = [st[:, :8].copy()]
+    while layers[-1].shape[0] > 1:
+        x = layers[-1]
+        layers.append(poseidon2_permute(np.concatenate([x[0::2], x[1::2]], 1))[:, :8].copy())
+    return layers
+
+
+def merkle_openings(prog: RecursionProgram, matrix: np.ndarray, indices: Sequence[int], layers=None) -> None:
+    """Append the verification of `matrix`'s rows at `indices` against its MMCS root, as the recursion
+    verifier does it (recursion/circuit/src/merkle_tree.rs, hash.rs:40-50, builder.rs:167-177): the
+    opened rows and the sibling paths are hinted (MemoryVar), the index bits hinted as HintBits
+    outputs, each row is absorbed by Poseidon2 permutations, each level orders (node, sibling) by the
+    index bit with two Select lanes per digest word and compresses, and the root is read back as a
+    constant (MemoryConst): the memory bus only balances if every recomputed root equals it."""
+    layers = merkle_layers(matrix) if layers is None else layers
+    M = np.asarray(matrix, U) % PU
+    h, w = M.shape
+    depth = len(layers) - 1
+    idx = np.asarray(indices, np.int64)
+    q = len(idx)
+    blk = lambda v: np.stack([v, v * 0, v * 0, v * 0], -1).reshape(-1, D)
+    zero = prog.alloc(1)
+    prog.mem_write(zero, blk(np.zeros(1, U)))
+    rows = prog.alloc(q * w).reshape(q, w)
+    prog.hint(rows.ravel(), blk(M[idx].ravel()))
+    state = np.full((q, WIDTH), zero[0], np.int64)
+    for c in range(0, w, 8):
+        k = min(8, w - c)
+        inp = state.copy()
+        inp[:, :k] = rows[:, c:c + k]
+        out = prog.alloc(q * WIDTH).reshape(q, WIDTH)
+        prog.poseidon2(out, inp)
+        state = out
+    node = state[:, :8]
+    if depth:
+        bits = prog.alloc(q * depth).reshape(q, depth)
+        prog.hint(bits.ravel(), blk(((idx[:, None] >> np.arange(depth)[None, :]) & 1).astype(U).ravel()))
+        sib = prog.alloc(q * depth * 8).reshape(q, depth, 8)
+        sv = np.stack([layers[l][(idx >> l) ^ 1] for l in range(depth)], 1)
+        prog.hint(sib.ravel(), blk(sv.ravel()))
+        for l in range(depth):
+            left, right = prog.alloc(q * 8).reshape(q, 8), prog.alloc(q * 8).reshape(q, 8)
+            prog.select(np.repeat(bits[:, l], 8), left.ravel(), right.ravel(), node.ravel(), sib[:, l].ravel())
+            out = prog.alloc(q * WIDTH).reshape(q, WIDTH)
+            prog.poseidon2(out, np.concatenate([left, right], 1))
+            node = out[:, :8]
+    root = layers[-1][0]
+    prog.mem_read(node.ravel(), blk(np.tile(root, q)), 1)
+
+
+def program_merkle_openings(log_h: int = 8, width: int = 21, queries: int = 16, seed: int = 9):
+    """Merkle openings of a random log_h x width matrix at `queries` random rows (``merkle_openings``);
+    returns (program, matrix) so tests can pin the root to the MMCS."""
+    rng = np.random.default_rng(seed)
+    mat = _rand(rng, (1 << log_h, width))
+    p = RecursionProgram()
+    merkle_openings(p, mat, rng.integers(0, 1 << log_h, queries))
+    return p, mat
+
+
 # The reference's fixed shape of the shrink/compress machine (machine.rs:155-171 shrink_shape)
 SHRINK_SHAPE = {"MemoryVar": 18, "Select": 18, "MemoryConst": 17, "BatchFRI": 17, "BaseAlu": 17, "ExtAlu": 15,
                 "ExpReverseBitsLen": 17, "Poseidon2WideDeg3": 16, "PublicValues": PUB_VALUES_LOG_HEIGHT}
@@ -1086,8 +1157,10 @@ SHRINK_SHAPE = {"MemoryVar": 18, "Select": 18, "MemoryConst": 17, "BatchFRI": 17
 
 def program_verifier_shaped(shape: Dict[str, int] = SHRINK_SHAPE, fill: float = 0.9, seed: int = 11) -> RecursionProgram:
     """A recursion program with the instruction mix of a verifier program that fills each chip of
-    ``shape`` to ``fill``: hinted proof data (MemoryVar), a Poseidon2 sponge over it (the transcript and
-    Merkle paths), the index bits of the queries (ExpReverseBitsLen), Merkle-path selects (Select),
+    ``shape`` to ``fill``: Merkle openings of a committed matrix verified against its root
+    (``merkle_openings``: hinted rows and paths, Poseidon2 sponge and compressions, Select ordering by the
+    index bits), more hinted proof data (MemoryVar) and Poseidon2 sponge chains over it (the
+    transcript), the index bits of the queries (ExpReverseBitsLen), selects (Select),
     FRI reduced openings (BatchFRI), base/extension arithmetic (BaseAlu / ExtAlu) and constants
     (MemoryConst), ending with CommitPublicValues.  Every value is produced by the runtime."""
     rng = np.random.default_rng(seed)
@@ -1105,6 +1178,20 @@ def program_verifier_shaped(shape: Dict[str, int] = SHRINK_SHAPE, fill: float = 
     n_fri = cap("BatchFRI") // fri_len
     n_var = cap("MemoryVar", 2)
     n_const = cap("MemoryConst", 2)
+
+    # Merkle openings of a committed matrix (the inner proofs' query openings): a 2^mlog-row, 16-column
+    # matrix, rows at random indices verified against its root; they take the Select budget (8 lanes per
+    # level) and part of the Poseidon2 budget
+    mlog = max(4, min(16, shape["Poseidon2WideDeg3"] - 2))
+    per_q = 2 + mlog
+    spare_var = n_var - 2 * n_fri * fri_len - n_erb * erb_len - PROOF_MAX_NUM_PVS  # after the other hints
+    n_q = max(1, min(n_sel // (8 * mlog), n_p2 // (2 * per_q), (spare_var // 2) // (16 + 9 * mlog)))
+    mat = _rand(rng, (1 << mlog, 16))
+    merkle_openings(p, mat, rng.integers(0, 1 << mlog, n_q))
+    n_sel = max(1, n_sel - n_q * 8 * mlog)
+    n_p2 = max(64, n_p2 - n_q * per_q)
+    n_var = max(0, n_var - n_q * (16 + 9 * mlog))  # rows, index bits, sibling digests
+    n_const = max(32, n_const - 1 - 8 * n_q)  # the zero constant, the roots read back
 
     # hinted proof data: ext blocks (alpha powers, p(z)) and felts (p(x), sponge input, bits)
     n_hint_ext = 2 * n_fri * fri_len
