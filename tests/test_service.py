@@ -97,3 +97,18 @@ def test_prove_shard_through_service(server):
     st, ct, body = post(port, "ProveShard", json.dumps({"data": base64.b64encode(data).decode()}).encode(),
                         "application/json")
     assert st == 200 and base64.b64decode(json.loads(body)["result"]) == direct
+
+
+@pytest.mark.gpu
+def test_prove_compress_shard_through_service(server):
+    """A recursion-machine (compress) shard at blowup 4 / 42 queries through ProveShard equals the
+    direct prover's bytes and the CPU oracle's."""
+    from tests import _oracle as O
+    from zkmips_amd import recursion as R
+    port = server()
+    m, prep, tr, pv = R.shard(R.program_merkle_openings(6, 21, 8)[0])
+    data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    st, ct, body = post(port, "ProveShard", SV.encode_bytes_field(1, data))
+    assert st == 200
+    rc, ref = O.OracleProver(m, prep, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP).prove(tr, pv)
+    assert rc == 0 and SV.decode_fields(body)[1] == ref
