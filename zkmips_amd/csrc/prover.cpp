@@ -9,6 +9,7 @@
 // Every O(N) step runs on the GPU (open_kernels.hip, ntt.hip, merkle.hip); the host keeps the
 // Fiat-Shamir transcript (a few hundred Poseidon2 permutations) and assembles the proof.
 #include <algorithm>
+#include <tuple>
 #include <array>
 #include <cstring>
 #include <future>
@@ -515,14 +516,35 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             }
             r.vals[0].assign(q.W, ef_zero());
             r.vals[1].assign(q.W, ef_zero());
-            q.coff = ncols_all;
-            q.poff = nparts;
-            q.nseg = open_dot_nseg(q.W, q.N);
-            ncols_all += q.W;
-            nparts += q.W * q.nseg * 8;
             const ef zs = ef_mul_base(zeta, inv(q.shift));
             q.pre = ef_mul_base(ef_sub(ef_pow(zs, q.N), ef_one()), inv(to_mont((uint32_t)(q.N % P))));
-            pend.push_back(q);
+            if (q.W) pend.push_back(q);
+        }
+        // Matrices that share the height, the evaluation domain (shift) and the number of points share one
+        // weight table and one k_open_dot launch over all their columns (every chip of a height group:
+        // preprocessed, main and LogUp traces; quotient chunk j of every chip of a (height, log_qd));
+        // each group's columns are contiguous in the column table and its partial sums in `part`.
+        auto key = [](const Pend &q) { return std::make_tuple(q.N, q.bitrev, q.shift, q.r->npts); };
+        std::stable_sort(pend.begin(), pend.end(), [&](const Pend &a, const Pend &b) { return key(a) < key(b); });
+        struct Group { size_t first, last; uint64_t coff, poff, W; int nseg; };
+        std::vector<Group> groups;
+        for (size_t i = 0; i < pend.size(); i++) {
+            if (groups.empty() || key(pend[groups.back().first]) != key(pend[i])) groups.push_back({i, i, 0, 0, 0, 1});
+            groups.back().last = i;
+            groups.back().W += pend[i].W;
+        }
+        for (auto &g : groups) {
+            g.coff = ncols_all;
+            g.poff = nparts;
+            g.nseg = open_dot_nseg(g.W, pend[g.first].N);
+            for (size_t i = g.first; i <= g.last; i++) {
+                Pend &q = pend[i];
+                q.coff = ncols_all;
+                q.nseg = g.nseg;
+                q.poff = g.poff + (q.coff - g.coff) * (uint64_t)g.nseg * 8;
+                ncols_all += q.W;
+            }
+            nparts += g.W * (uint64_t)g.nseg * 8;
         }
         std::vector<uint64_t> cols(ncols_all + 1);
         for (auto &q : pend)
@@ -531,8 +553,8 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s));
         std::vector<std::pair<uint64_t, DBuf>> wtab;  // natural-order weights per trace height (shift 1)
         std::vector<DBuf> wchunk;
-        for (auto &q : pend) {
-            if (!q.W) continue;
+        for (auto &g : groups) {
+            const Pend &q = pend[g.first];
             const uint32_t *w = nullptr;
             if (!q.bitrev) {
                 for (auto &pr : wtab) if (pr.first == q.N) w = pr.second.p;
@@ -546,9 +568,9 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 w = wchunk.back().p;
                 launch_inv_points(ef_mul_base(zeta, inv(q.shift)), ONE, c.tw_fwd, q.N, true, true, (uint32_t *)w, s);
             }
-            PROF("open_eval", s, 4.0 * q.N * q.W + 16.0 * q.N);
-            launch_open_dot((const uint64_t *)dcols.p + q.coff, (uint32_t)q.W, q.N, w, q.r->npts == 2, q.nseg,
-                            part.p + q.poff, s);
+            PROF("open_eval", s, 4.0 * q.N * g.W + 16.0 * q.N);
+            launch_open_dot((const uint64_t *)dcols.p + g.coff, (uint32_t)g.W, q.N, w, q.r->npts == 2, g.nseg,
+                            part.p + g.poff, s);
         }
         std::vector<uint32_t> hp(nparts + 1);
         HIP_CHECK(hipMemcpyAsync(hp.data(), part.p, nparts * 4, hipMemcpyDeviceToHost, s));
