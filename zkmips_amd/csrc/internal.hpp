@@ -139,6 +139,10 @@ void build_twiddles(Ctx &c, int log_max);
 void lde_batch(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst, hipStream_t s);
 // same, for evaluations given in bit-reversed row order
 void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst, hipStream_t s);
+// the same, column c of the 2N-row result at dst + c * dst_stride (dst_stride >= 2N)
+void lde_batch_strided(Ctx &c, const DMat &src, uint32_t shift_mont, uint32_t *dst, uint64_t dst_stride, hipStream_t s);
+void lde_batch_bitrev_in_strided(Ctx &c, const DMat &src, uint32_t shift_mont, uint32_t *dst, uint64_t dst_stride,
+                                 hipStream_t s);
 
 // Merkle
 void tree_build(DTree &t, hipStream_t s);

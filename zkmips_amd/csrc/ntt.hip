@@ -1092,19 +1092,27 @@ static double lde_gf_ops(uint64_t N) {
 //   DIT iNTT (bit-reversed in -> natural coefficients), twist on the last pass's write into both
 //   LDE halves, then DIF in place (natural -> bit-reversed): no permutation pass at all.
 void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s) {
+    ARG_CHECK(dst.height == 2 * src.height && dst.width == src.width, "LDE destination shape");
+    lde_batch_bitrev_in_strided(c, src, shift, dst.d, 2 * src.height, s);
+}
+
+// dst column c at dst + c * dst_stride (dst_stride >= 2N): blowup 4 writes each half of a 4N-row column
+void lde_batch_bitrev_in_strided(Ctx &c, const DMat &src, uint32_t shift, uint32_t *dst_d, uint64_t dst_stride,
+                                 hipStream_t s) {
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
+    ARG_CHECK(dst_stride >= 2 * N, "LDE destination stride");
+    DMat dst{dst_d, 2 * N, W};
     PROF("lde", s, 12.0 * N * W);
     prof_add("lde_gfops", lde_gf_ops(N) * W);
     const int L = ilog2(N);
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
-    ARG_CHECK(dst.height == 2 * N && dst.width == W, "LDE destination shape");
     int logC;
     std::vector<int> sp = strided_plan(L, logC);
     const Twist tws = get_twist(c, N, L, shift, s);
     const uint32_t nv = (uint32_t)W;
-    ColMap m_src{N, 0, 1}, m_dst1{2 * N, 0, 1}, m_dst2{2 * N, N, 2};
+    ColMap m_src{N, 0, 1}, m_dst1{dst_stride, 0, 1}, m_dst2{dst_stride, N, 2};
     if (sp.empty()) {
         run_contig<true>(logC, src.d, dst.d, m_src, m_dst1, nv, L, c.tw_inv, MODE_TWIST_OUT, tws, N, s);
     } else {
@@ -1143,21 +1151,27 @@ static uint32_t lde_col_batch(uint64_t N, uint32_t nv) {
 // Natural-input LDE (traces):  [strided DIF iNTT passes] -> fused {contiguous DIF iNTT, twists,
 // contiguous DIT forward x2} -> [strided DIT forward passes, the last writing bit-reversed rows].
 void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s) {
+    ARG_CHECK(dst.height == 2 * src.height && dst.width == src.width, "LDE destination shape");
+    lde_batch_strided(c, src, shift, dst.d, 2 * src.height, s);
+}
+
+void lde_batch_strided(Ctx &c, const DMat &src, uint32_t shift, uint32_t *dst_d, uint64_t dst_stride, hipStream_t s) {
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
+    ARG_CHECK(dst_stride >= 2 * N, "LDE destination stride");
+    DMat dst{dst_d, 2 * N, W};
     PROF("lde", s, 12.0 * N * W);
     prof_add("lde_gfops", lde_gf_ops(N) * W);
     const int L = ilog2(N);
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
-    ARG_CHECK(dst.height == 2 * N && dst.width == W, "LDE destination shape");
     int logC;
     std::vector<int> sp = strided_plan(L, logC);
     const Twist tws = get_twist(c, N, L, shift, s);
     const uint32_t nv = (uint32_t)W;
-    ColMap m_src{N, 0, 1}, m_w1{2 * N, 0, 1}, m_w2{2 * N, N, 2};
+    ColMap m_src{N, 0, 1}, m_w1{2 * N, 0, 1}, m_w2{2 * N, N, 2}, m_out{dst_stride, N, 2};
     if (sp.empty()) {
-        run_fused(logC, src.d, dst.d, m_src, m_w1, nv, L, c.tw_inv, c.tw_fwd, tws, N, 1, s);
+        run_fused(logC, src.d, dst.d, m_src, ColMap{dst_stride, 0, 1}, nv, L, c.tw_inv, c.tw_fwd, tws, N, 1, s);
         return;
     }
     // Columns go through all passes in batches of `cb`: a batch's work buffer (2N words per
@@ -1168,7 +1182,7 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
     for (uint32_t c0 = 0; c0 < nv; c0 += cb) {
         const uint32_t nb = std::min(cb, nv - c0);
         const uint32_t *in = src.d + (uint64_t)c0 * N;
-        uint32_t *out = dst.d + (uint64_t)c0 * 2 * N;
+        uint32_t *out = dst.d + (uint64_t)c0 * dst_stride;
         ColMap min = m_src;
         int logS = L;
         for (size_t i = 0; i < sp.size(); i++) {
@@ -1188,7 +1202,7 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
         logS = logC;
         for (int i = (int)sp.size() - 1; i >= 0; i--) {
             const bool last = (i == 0);
-            run_strided<true>(sp[i], work.p, last ? out : work.p, m_w2, m_w2, 2 * nb, L, logS, c.tw_fwd,
+            run_strided<true>(sp[i], work.p, last ? out : work.p, m_w2, last ? m_out : m_w2, 2 * nb, L, logS, c.tw_fwd,
                               last ? MODE_BITREV_OUT : MODE_PLAIN, s, Twist{}, 0, 1u << c.tw_log);
             logS += sp[i];
         }

@@ -131,7 +131,7 @@ static std::vector<int> sort_order(const std::vector<uint64_t> &h, const std::ve
 // Bit-reversed coset LDE with blowup 2^lb of src (N x W) into dst (column stride N << lb): row i holds
 // p(shift * w_{2^lb N}^{rev(i)}).  The blowup-2 kernels give rows [0, 2N) directly; for blowup 4, rows
 // [2N, 4N) are the blowup-2 LDE with shift * w_{4N} (rev_{4N}(2N + j) = 2 rev_{2N}(j) + 1), so two
-// passes through a 2N-row buffer fill the two halves of every column.
+// passes fill the two halves of every column directly.
 static void lde_into(Ctx &c, const DMat &src, uint32_t shift, bool bitrev_in, int lb, uint32_t *dst, hipStream_t s) {
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
@@ -142,14 +142,11 @@ static void lde_into(Ctx &c, const DMat &src, uint32_t shift, bool bitrev_in, in
         else lde_batch(c, src, shift, d, s);
         return;
     }
-    DBuf tmp(2 * N * W, s);
-    DMat d{tmp.p, 2 * N, W};
+    // each blowup-2 pass writes its half of every 4N-row column in place (column stride 4N)
     for (int half = 0; half < 2; half++) {
         const uint32_t sh = half ? mul(shift, two_adic_gen(ilog2(N) + 2)) : shift;
-        if (bitrev_in) lde_batch_bitrev_in(c, src, sh, d, s);
-        else lde_batch(c, src, sh, d, s);
-        HIP_CHECK(hipMemcpy2DAsync(dst + half * 2 * N, 4 * N * 4, tmp.p, 2 * N * 4, 2 * N * 4, W,
-                                   hipMemcpyDeviceToDevice, s));
+        if (bitrev_in) lde_batch_bitrev_in_strided(c, src, sh, dst + half * 2 * N, 4 * N, s);
+        else lde_batch_strided(c, src, sh, dst + half * 2 * N, 4 * N, s);
     }
 }
 
@@ -321,6 +318,9 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         }
     }
     DTree perm_tree;
+    // each chip's local sum (last row of the last perm column) and global sum (last 14 main columns of
+    // a Global-scope chip) are read back asynchronously; tree_build below synchronises the stream
+    std::vector<uint32_t> sums_host(18 * (size_t)n + 1, 0);
     for (int i = 0; i < n; i++) {
         const ChipDesc &cd = m.chips[md.chip[i]];
         const uint64_t N = md.heights[i];
@@ -346,18 +346,13 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 }
                 launch_perm_trace(a, s, jk.fn_perm != nullptr);
             }
-            uint32_t l[4];
-            for (int e = 0; e < 4; e++)
-                HIP_CHECK(hipMemcpyAsync(&l[e], perm_traces[i] + (uint64_t)(4 * (pw - 1) + e) * N + N - 1, 4,
-                                         hipMemcpyDeviceToHost, s));
-            HIP_CHECK(hipStreamSynchronize(s));
-            co.lcs = ef{{l[0], l[1], l[2], l[3]}};
+            // the 4 words are rows N-1 of 4 columns N apart: one strided 2D copy
+            HIP_CHECK(hipMemcpy2DAsync(&sums_host[18 * i], 4, perm_traces[i] + (uint64_t)(4 * (pw - 1)) * N + N - 1,
+                                       N * 4, 4, 4, hipMemcpyDeviceToHost, s));
         }
         if (cd.scope == 1) {
-            for (int k = 0; k < 14; k++)
-                HIP_CHECK(hipMemcpyAsync(&co.gcs[k], md.trace[i] + (uint64_t)(cd.main_w - 14 + k) * N + N - 1, 4,
-                                         hipMemcpyDeviceToHost, s));
-            HIP_CHECK(hipStreamSynchronize(s));
+            HIP_CHECK(hipMemcpy2DAsync(&sums_host[18 * i + 4], 4, md.trace[i] + (uint64_t)(cd.main_w - 14) * N + N - 1,
+                                       N * 4, 4, 14, hipMemcpyDeviceToHost, s));
         } else {
             for (int k = 0; k < 14; k++) co.gcs[k] = to_mont(CURVE_START[k]);
         }
@@ -370,7 +365,13 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 perm_tree.mats.push_back(v);
         }
     }
-    tree_build(perm_tree, s);
+    tree_build(perm_tree, s);  // synchronises the stream: sums_host is filled
+    for (int i = 0; i < n; i++) {
+        const ChipDesc &cd = m.chips[md.chip[i]];
+        if (cd.perm_w) proof.chips[i].lcs = ef{{sums_host[18 * i], sums_host[18 * i + 1], sums_host[18 * i + 2],
+                                                sums_host[18 * i + 3]}};
+        if (cd.scope == 1) memcpy(proof.chips[i].gcs, &sums_host[18 * i + 4], 14 * 4);
+    }
     proof.perm_c = dig(perm_tree.root);
     ch.observe(perm_tree.root, 8);
     for (int i = 0; i < n; i++) {
@@ -405,20 +406,29 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         }
     }
     std::vector<int> chunk_chip;  // chip of each quotient chunk
+    // alpha^(n-1-k) per constraint k of every chip (folder.rs:79-102, powers reversed prover.rs:453-456),
+    // one upload for the whole shard
+    std::vector<uint64_t> pows_off(n + 1, 0);
+    for (int i = 0; i < n; i++) pows_off[i + 1] = pows_off[i] + 4 * ((uint64_t)m.chips[md.chip[i]].n_constraints + 1);
+    std::vector<uint32_t> pows_all(pows_off[n] + 1, 0);
+    for (int i = 0; i < n; i++) {
+        const int nc = m.chips[md.chip[i]].n_constraints;
+        ef a = ef_one();
+        for (int k = nc - 1; k >= 0; k--) {
+            memcpy(&pows_all[pows_off[i] + 4 * k], a.c, 16);
+            a = ef_mul(a, alpha);
+        }
+    }
+    DBuf d_pows_all(pows_all.size(), s);
+    HIP_CHECK(hipMemcpyAsync(d_pows_all.p, pows_all.data(), pows_all.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));  // pows_all (pageable) has been read
     for (int i = 0; i < n; i++) {
         const ChipDesc &cd = m.chips[md.chip[i]];
         const uint64_t N = md.heights[i];
         const int logN = ilog2(N), lqd = cd.log_qd;
         ARG_CHECK(lqd <= lb, "log_quotient_degree > log_blowup is not supported (Plonky3 asserts too)");
         const uint64_t Q = N << lqd;
-        std::vector<uint32_t> pows(4 * (cd.n_constraints + 1));
-        ef a = ef_one();
-        for (int k = cd.n_constraints - 1; k >= 0; k--) {
-            memcpy(&pows[4 * k], a.c, 16);
-            a = ef_mul(a, alpha);
-        }
-        DBuf d_pows(pows.size(), s);
-        HIP_CHECK(hipMemcpyAsync(d_pows.p, pows.data(), pows.size() * 4, hipMemcpyHostToDevice, s));
+        const uint32_t *d_pows = d_pows_all.p + pows_off[i];
         const int pki = pk.pk_index(md.chip[i]);
         QuotArgs qa{};
         qa.prog = pk.progs[md.chip[i]].p;
@@ -432,7 +442,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         qa.gen_pow_n = pow(qa.gen, N);
         qa.wn_inv = inv(two_adic_gen(logN));
         qa.pv = d_pv.p;
-        qa.pows = d_pows.p;
+        qa.pows = d_pows;
         qa.alpha_p = perm_alpha; qa.beta_pows = d_bpow.p; qa.lcs = proof.chips[i].lcs;
         memcpy(qa.gcs, proof.chips[i].gcs, sizeof qa.gcs);
         qa.batch = 1 << lqd; qa.perm_w = cd.perm_w; qa.global = cd.scope == 1; qa.main_w = cd.main_w;
@@ -453,7 +463,6 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 launch_quotient(qa, s);
             }
         }
-        HIP_CHECK(hipStreamSynchronize(s));  // d_pows lifetime
         if (i + 1 == n || q_first[i + 1] != q_first[i]) {  // last chip of its group: LDE the group's chunks
             const int a = q_first[i];
             const uint32_t wq = two_adic_gen(logN + lqd);
@@ -612,6 +621,10 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         DBuf d_apow(apow.size(), s);
         HIP_CHECK(hipMemcpyAsync(d_apow.p, apow.data(), apow.size() * 4, hipMemcpyHostToDevice, s));
         auto alpha_pow = [&](uint64_t e) { return ef_pow(fri_alpha, e); };
+        // the per-height column tables and descriptors are pageable host memory read by async copies:
+        // they live until the one synchronisation after the loop
+        std::vector<std::vector<uint64_t>> keep_cols;
+        std::vector<std::vector<uint32_t>> keep_desc;
         for (int lh = 0; lh < 32; lh++) {
             if (by_h[lh].empty()) continue;
             const uint64_t H = 1ull << lh;
@@ -623,8 +636,10 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             launch_inv_points(zeta, to_mont(GENERATOR), c.tw_fwd, H, true, false, inv0.p, s);
             const ef znext = ef_mul_base(zeta, two_adic_gen(ilog2(N)));
             bool need1 = false;
-            std::vector<uint64_t> cols;
-            std::vector<uint32_t> desc;
+            keep_cols.emplace_back();
+            keep_desc.emplace_back();
+            std::vector<uint64_t> &cols = keep_cols.back();
+            std::vector<uint32_t> &desc = keep_desc.back();
             for (auto &it : by_h[lh]) {
                 const uint64_t W = it.mat->width;
                 desc.push_back((uint32_t)W);
@@ -654,8 +669,8 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             ReduceArgs ra{(const uint64_t *)dcols.p, ddesc.p, (uint32_t)by_h[lh].size(), d_apow.p, inv0.p,
                           need1 ? inv1.p : nullptr, ro[lh].p, H};
             { PROF("fri_reduce", s, 4.0 * H * cols.size() + 16.0 * H * (need1 ? 4 : 3)); launch_fri_reduce(ra, s); }
-            HIP_CHECK(hipStreamSynchronize(s));  // host vectors / temporaries
         }
+        HIP_CHECK(hipStreamSynchronize(s));  // keep_cols / keep_desc / apow have been read
     }
 
     // ---- FRI commit phase ----
