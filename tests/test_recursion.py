@@ -47,6 +47,32 @@ def test_compress_machine_chip_table():
         assert c.log_quotient_degree <= LB
 
 
+def test_wide_machine_chip_table():
+    """machine_wide_with_all_chips (machine.rs:68-87): the compress chips with FriFold after
+    Poseidon2WideDeg3; FriFold's columns are fri_fold.rs:40-78 and it opens at zeta and g*zeta."""
+    m = R.wide_machine()
+    names = [c.name for c in m.chips]
+    assert names == ["MemoryConst", "MemoryVar", "BaseAlu", "ExtAlu", "Poseidon2WideDeg3", "FriFold", "BatchFRI",
+                     "Select", "ExpReverseBitsLen", "PublicValues"]
+    c = m.chips[m.chip_index("FriFold")]
+    assert (c.prep_width, c.main_width, c.perm_width_ef, c.log_quotient_degree, c.local_only) == (20, 33, 6, 1, False)
+
+
+def test_fri_fold_program():
+    """FriFold instructions prove on the wide machine; a forged running reduced opening is rejected; the
+    compress machine refuses them (it has no FriFold chip)."""
+    m, pr, tr, pvs = R.shard(R.program_fri_fold(), wide=True)
+    assert not any(AC.check(m, pr, tr, pvs))
+    o = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
+    rc, proof = o.prove(tr, pvs)
+    assert rc == 0 and o.verify(proof) == 0
+    bad = {k: v.copy() for k, v in tr.items()}
+    bad["FriFold"][2, 30] = (int(bad["FriFold"][2, 30]) + 1) % R.P  # ro_output word 1 of row 2
+    assert any(AC.check(m, pr, bad, pvs))
+    with pytest.raises(ValueError):
+        R.shard(R.program_fri_fold())
+
+
 def test_poseidon2_rows_match_kats():
     kat = json.load(open(os.path.join(GOLDEN, "poseidon2_kat.json")))
     for v in kat.values():
@@ -187,6 +213,17 @@ def test_gpu_recursion_programs_proof_bytes_identical(dev):
         rc, ref = cpu.prove(tr, pvs)
         assert rc == 0 and proof == ref, name
         assert cpu.verify(proof) == 0, name
+
+
+@pytest.mark.gpu
+def test_gpu_wide_machine_fri_fold_bytes_identical(dev):
+    from zkmips_amd.prover import HipProver
+    m, pr, tr, pvs = R.shard(R.program_fri_fold(64, 7), wide=True)
+    gpu = HipProver(dev, m, pr, num_queries=NQ, log_blowup=LB)
+    cpu = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
+    proof = gpu.prove_shard(tr, pvs)
+    rc, ref = cpu.prove(tr, pvs)
+    assert rc == 0 and proof == ref and cpu.verify(proof) == 0
 
 
 @pytest.mark.gpu

@@ -297,6 +297,18 @@ class RecursionProgram:
                   p_at_z=np.asarray(p_at_z, np.int64).reshape(n, -1), p_at_x=np.asarray(p_at_x, np.int64).reshape(n, -1),
                   mult=np.ones(n, np.int64))
 
+    def fri_fold(self, x, z, alpha, p_at_x, p_at_z, alpha_pow_in, ro_in, alpha_pow_out, ro_out,
+                 alpha_pow_mults=None, ro_mults=None):
+        """Instruction::FriFold (runtime/mod.rs:461-535): one instruction, m = len(p_at_z) entries;
+        ro_out = ro_in + alpha_pow_in (p_at_x - p_at_z) / (x - z), alpha_pow_out = alpha_pow_in alpha."""
+        v = lambda a: np.asarray(a, np.int64).reshape(1, -1)
+        m = v(p_at_z).shape[1]
+        self._add("frifold", x=np.asarray([x], np.int64), z=np.asarray([z], np.int64), alpha=np.asarray([alpha], np.int64),
+                  p_at_x=v(p_at_x), p_at_z=v(p_at_z), alpha_pow_in=v(alpha_pow_in), ro_in=v(ro_in),
+                  alpha_pow_out=v(alpha_pow_out), ro_out=v(ro_out),
+                  apm=_mults(None if alpha_pow_mults is None else v(alpha_pow_mults), (1, m)),
+                  rom=_mults(None if ro_mults is None else v(ro_mults), (1, m)))
+
     def commit_public_values(self, pv_addrs):
         pv_addrs = np.asarray(pv_addrs, np.int64).reshape(PROOF_MAX_NUM_PVS)
         self._add("commit", pv=pv_addrs[None, :])
@@ -327,6 +339,9 @@ def _reads(b: Block):
         return [(a["alpha_pow"].ravel(), 1), (a["p_at_z"].ravel(), 1), (a["p_at_x"].ravel(), 1)]
     if b.kind == "commit":
         return [(a["pv"][0, PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE], 1)]
+    if b.kind == "frifold":
+        return [(a["x"], 1), (a["z"], 1), (a["alpha"], 1), (a["p_at_x"].ravel(), 1), (a["p_at_z"].ravel(), 1),
+                (a["alpha_pow_in"].ravel(), 1), (a["ro_in"].ravel(), 1)]
     return []
 
 
@@ -344,6 +359,8 @@ def _writes(b: Block):
         return [("result", "mult", None)]
     if b.kind == "batchfri":
         return [("acc", "mult", None)]
+    if b.kind == "frifold":
+        return [("alpha_pow_out", "apm", None), ("ro_out", "rom", None)]
     return []
 
 
@@ -378,7 +395,8 @@ def execute(prog: RecursionProgram) -> ExecutionRecord:
     mem = np.zeros((prog.num_addrs, D), U)
     written = np.zeros(prog.num_addrs, bool)
     ev: Dict[str, List[Dict[str, np.ndarray]]] = {k: [] for k in
-                                                 ("mem", "hint", "base", "ext", "p2", "select", "exprev", "batchfri", "commit")}
+                                                 ("mem", "hint", "base", "ext", "p2", "select", "exprev", "batchfri", "commit",
+                                                  "frifold")}
     pvs = np.zeros(PROOF_MAX_NUM_PVS, np.uint32)
 
     def rd(addr):
@@ -476,6 +494,24 @@ def execute(prog: RecursionProgram) -> ExecutionRecord:
                 rows[:, i, 12] = px[:, i]
             wr(a["acc"], acc)
             ev["batchfri"].append({"rows": rows.reshape(n * L, 13), "L": L, "n": n})
+        elif k == "frifold":
+            x = rd(a["x"])[0, 0]
+            z, alpha = rd(a["z"])[0], rd(a["alpha"])[0]
+            px, pz = rd(a["p_at_x"][0]), rd(a["p_at_z"][0])
+            ap, ro = rd(a["alpha_pow_in"][0]), rd(a["ro_in"][0])
+            xz = (PU - z) % PU
+            xz[0] = (xz[0] + x) % PU                       # x - z
+            q = ext_mul((px + PU - pz) % PU, ext_inv(np.broadcast_to(xz, px.shape).copy()))
+            new_ro = (ro + ext_mul(ap, q)) % PU
+            new_ap = ext_mul(ap, np.broadcast_to(alpha, ap.shape))
+            wr(a["ro_out"][0], new_ro)
+            wr(a["alpha_pow_out"][0], new_ap)
+            mm = px.shape[0]
+            rows = np.zeros((mm, 33), U)
+            rows[:, 0:4], rows[:, 4:8], rows[:, 8] = z, alpha, x
+            rows[:, 9:13], rows[:, 13:17], rows[:, 17:21], rows[:, 21:25] = px, pz, ap, ro
+            rows[:, 25:29], rows[:, 29:33] = new_ap, new_ro
+            ev["frifold"].append({"rows": rows})
         elif k == "commit":
             vals = rd(a["pv"][0])[:, 0]
             pvs = vals.astype(np.uint32)
@@ -709,6 +745,37 @@ def batch_fri_chip() -> ChipDesc:
     return c
 
 
+def fri_fold_chip() -> ChipDesc:
+    """FriFold (fri_fold.rs:371-490): prep = is_first, (addr, mult) of z, alpha, x, alpha_pow_input,
+    ro_input, p_at_x, p_at_z, ro_output, alpha_pow_output, is_real; main = z[4], alpha[4], x,
+    p_at_x[4], p_at_z[4], alpha_pow_input[4], ro_input[4], alpha_pow_output[4], ro_output[4]."""
+    c = ChipDesc("FriFold", prep_width=20, main_width=33)
+    is_real = prep(19)
+    c.assert_zero(is_real * is_real * is_real - is_real * is_real * is_real)
+    keep = lambda: IS_TRANSITION * prep_next(19) * (1 - prep_next(0))
+    c.sends.append(_mem(V.single_prep(5), _single(V.single_main(8)), V.single_prep(6)))
+    c.assert_zero(keep() * (main(8) - main_next(8)))
+    c.sends.append(_mem(V.single_prep(1), _vblk("main", 0), V.single_prep(2)))
+    for k in range(D):
+        c.assert_zero(keep() * (main(k) - main_next(k)))
+    c.sends.append(_mem(V.single_prep(3), _vblk("main", 4), V.single_prep(4)))
+    for k in range(D):
+        c.assert_zero(keep() * (main(4 + k) - main_next(4 + k)))
+    for addr, val in ((7, 17), (9, 21), (13, 13), (11, 9), (17, 25), (15, 29)):
+        c.sends.append(_mem(V.single_prep(addr), _vblk("main", val), V.single_prep(addr + 1)))
+    alpha, old_ap, new_ap = _blk("main", 4), _blk("main", 17), _blk("main", 25)
+    t = _ext_expr_mul(old_ap, alpha)
+    for k in range(D):
+        c.assert_zero(t[k] - new_ap[k])
+    z, px, pz, old_ro, new_ro = _blk("main", 0), _blk("main", 9), _blk("main", 13), _blk("main", 21), _blk("main", 29)
+    xz = [main(8) - z[0]] + [0 - z[k] for k in range(1, D)]
+    lhs = _ext_expr_mul([new_ro[k] - old_ro[k] for k in range(D)], xz)
+    rhs = _ext_expr_mul([px[k] - pz[k] for k in range(D)], old_ap)
+    for k in range(D):
+        c.assert_zero(lhs[k] - rhs[k])
+    return c
+
+
 def select_chip() -> ChipDesc:
     """Select (select.rs:229-251): prep = (is_real, bit, out1, out2, in1, in2 addrs, mult1, mult2);
     main = (bit, out1, out2, in1, in2)."""
@@ -759,6 +826,13 @@ def compress_machine() -> MachineDesc:
     """RecursionAir::<F, 3>::compress_machine (machine.rs:112-128), observing all 231 public values."""
     return MachineDesc([mem_const_chip(), mem_var_chip(), _alu_chip("BaseAlu", False), _alu_chip("ExtAlu", True),
                         poseidon2_wide_chip(), batch_fri_chip(), select_chip(), exp_reverse_bits_chip(),
+                        public_values_chip()], PROOF_MAX_NUM_PVS)
+
+
+def wide_machine() -> MachineDesc:
+    """RecursionAir::<F, 3>::machine_wide_with_all_chips (machine.rs:68-87): the compress chips plus FriFold."""
+    return MachineDesc([mem_const_chip(), mem_var_chip(), _alu_chip("BaseAlu", False), _alu_chip("ExtAlu", True),
+                        poseidon2_wide_chip(), fri_fold_chip(), batch_fri_chip(), select_chip(), exp_reverse_bits_chip(),
                         public_values_chip()], PROOF_MAX_NUM_PVS)
 
 
@@ -885,6 +959,29 @@ def generate_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None
     ma = _cat([e["rows"] for e in rec.events["batchfri"]], (13,))
     finish("BatchFRI", pa, ma, len(pa))
 
+    # FriFold (wide machine only; the compress machine has no FriFold chip)
+    pa = []
+    for b in bl("frifold"):
+        a = b.a
+        m_ = a["p_at_z"].shape[1]
+        p_ = np.zeros((m_, 20), U)
+        first = (np.arange(m_) == 0)
+        p_[:, 0] = first
+        p_[:, 1], p_[:, 2] = a["z"][0], np.where(first, P - 1, 0)
+        p_[:, 3], p_[:, 4] = a["alpha"][0], np.where(first, P - 1, 0)
+        p_[:, 5], p_[:, 6] = a["x"][0], np.where(first, P - 1, 0)
+        p_[:, 7], p_[:, 8] = a["alpha_pow_in"][0], P - 1
+        p_[:, 9], p_[:, 10] = a["ro_in"][0], P - 1
+        p_[:, 11], p_[:, 12] = a["p_at_x"][0], P - 1
+        p_[:, 13], p_[:, 14] = a["p_at_z"][0], P - 1
+        p_[:, 15], p_[:, 16] = a["ro_out"][0], a["rom"][0] % P
+        p_[:, 17], p_[:, 18] = a["alpha_pow_out"][0], a["apm"][0] % P
+        p_[:, 19] = 1
+        pa.append(p_)
+    pa = _cat(pa, (20,))
+    ma = _cat([e["rows"] for e in rec.events["frifold"]], (33,))
+    finish("FriFold", pa, ma, len(pa))
+
     # Select
     pa, ma = [], []
     for b, e in zip(bl("select"), rec.events["select"]):
@@ -933,11 +1030,17 @@ def generate_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None
             {k: np.ascontiguousarray(v.astype(np.uint32)) for k, v in mains.items()})
 
 
-def shard(prog: RecursionProgram, shape: Optional[Dict[str, int]] = None):
-    """(machine, prep_traces, traces, public_values) of one compress-machine shard of ``prog``."""
+def shard(prog: RecursionProgram, shape: Optional[Dict[str, int]] = None, wide: bool = False):
+    """(machine, prep_traces, traces, public_values) of one compress-machine shard of ``prog`` (or of the
+    wide machine with FriFold, ``wide=True``)."""
     rec = execute(prog)
     pr, tr = generate_traces(rec, shape)
-    m = compress_machine()
+    m = wide_machine() if wide else compress_machine()
+    if not wide:
+        if rec.events["frifold"]:
+            raise ValueError("FriFold instructions need the wide machine")
+        pr.pop("FriFold", None)
+        tr.pop("FriFold", None)
     pr = {c.name: pr[c.name] for c in m.chips if c.prep_width}
     return m, pr, tr, rec.public_values
 
@@ -1148,6 +1251,34 @@ def program_merkle_openings(log_h: int = 8, width: int = 21, queries: int = 16, 
     p = RecursionProgram()
     merkle_openings(p, mat, rng.integers(0, 1 << log_h, queries))
     return p, mat
+
+
+def program_fri_fold(n: int = 8, m: int = 5, seed: int = 4) -> RecursionProgram:
+    """FriFold instructions (fri_fold.rs tests): n folds of m entries each over hinted z, alpha, x,
+    openings and running (alpha_pow, ro), the outputs read back."""
+    rng = np.random.default_rng(seed)
+    p = RecursionProgram()
+    for _ in range(n):
+        x_a, z_a, al_a = p.alloc(1), p.alloc(1), p.alloc(1)
+        ins = [p.alloc(m) for _ in range(4)]
+        outs = [p.alloc(m) for _ in range(2)]
+        xv = _rand(rng, 1)
+        p.hint(x_a, np.stack([xv, xv * 0, xv * 0, xv * 0], 1))
+        zv, alv = _rand(rng, (1, D)), _rand(rng, (1, D))
+        p.hint(z_a, zv)
+        p.hint(al_a, alv)
+        vals = [_rand(rng, (m, D)) for _ in range(4)]
+        for a_, v_ in zip(ins, vals):
+            p.hint(a_, v_)
+        p.fri_fold(x_a[0], z_a[0], al_a[0], ins[0], ins[1], ins[2], ins[3], outs[0], outs[1],
+                   alpha_pow_mults=np.ones(m), ro_mults=np.ones(m))
+        px, pz, ap, ro = vals
+        xz = (PU - zv) % PU
+        xz[0, 0] = (xz[0, 0] + xv[0]) % PU
+        q = ext_mul((px + PU - pz) % PU, ext_inv(np.repeat(xz, m, 0)))
+        p.mem_read(outs[1], (ro + ext_mul(ap, q)) % PU, 1)
+        p.mem_read(outs[0], ext_mul(ap, np.repeat(alv, m, 0)), 1)
+    return p
 
 
 # The reference's fixed shape of the shrink/compress machine (machine.rs:155-171 shrink_shape)
