@@ -14,6 +14,7 @@
  * and, beyond that ABI, the Global chip (the reference's Rust generate_trace, global/mod.rs:77-196), and
  * from the recursion machine's row ABI (crates/recursion/core/src/sys.rs:22-110) the Poseidon2WideDeg3
  *   poseidon2_wide_event_to_row_koalabear(const KoalaBear *input, KoalaBear *row, bool sbox_state)
+ *   exp_reverse_bits_event_to_row_koalabear(const ExpReverseBitsEventFFI *, size_t i, ExpReverseBitsLenCols *)
  *
  * Here each entry point fills a WHOLE padded trace in GPU memory from an event array in GPU memory:
  * one thread per row, rows staged through LDS so the row-major trace is written in full cache
@@ -164,6 +165,17 @@ typedef struct {
  * not read (the permutation is recomputed). */
 int zkm_poseidon2_wide_events_to_trace(const zkm_poseidon2_event *events, uint64_t n, uint32_t repr,
                                        uint32_t *trace, uint64_t height, void *stream);
+
+#define ZKM_EXP_REVERSE_BITS_LEN_WIDTH 7  /* ExpReverseBitsLenCols (exp_reverse_bits.rs:44-53) */
+
+/* ExpReverseBitsLen main trace: exp_reverse_bits_event_to_row_koalabear (sys.rs:50-54,
+ * include/exp_reverse_bits.hpp) plus the accumulator columns the Rust caller fills around it
+ * (exp_reverse_bits.rs:216-270): event e = (base[e], the bits at bits[offsets[e] .. offsets[e + 1]])
+ * fills rows offsets[e] .. offsets[e + 1] - 1 (x, current_bit, prev_accum_squared,
+ * prev_accum_squared_times_multiplier, accum, accum_squared, multiplier); rows from offsets[n] on are
+ * zero.  offsets has n + 1 entries, offsets[0] = 0, offsets[n] <= height.  repr as above. */
+int zkm_exp_reverse_bits_events_to_trace(const uint32_t *base, const uint32_t *bits, const uint64_t *offsets,
+                                         uint64_t n, uint32_t repr, uint32_t *trace, uint64_t height, void *stream);
 
 #ifdef __cplusplus
 }

@@ -117,6 +117,17 @@ extern "C" {
         height: u64,
         stream: *mut c_void,
     ) -> c_int;
+    /// ExpReverseBitsLen main trace (recursion/core/src/sys.rs:50-54 plus the accumulator columns).
+    pub fn zkm_exp_reverse_bits_events_to_trace(
+        base: *const u32,
+        bits: *const u32,
+        offsets: *const u64,
+        n: u64,
+        repr: u32,
+        trace: *mut u32,
+        height: u64,
+        stream: *mut c_void,
+    ) -> c_int;
     pub fn zkm_cpu_events_to_trace(
         events: *const CpuEventFfi,
         n: u64,

@@ -305,3 +305,29 @@ def test_gpu_device_poseidon2_trace_proves_identically(dev):
         .cpu().numpy().view(np.uint32)
     gpu = HipProver(dev, m, pr, num_queries=NQ, log_blowup=LB)
     assert gpu.prove_shard(dev_tr, pvs) == gpu.prove_shard(tr, pvs)
+
+
+@pytest.mark.gpu
+def test_gpu_exp_reverse_bits_device_trace_equals_host(dev):
+    """zkm_exp_reverse_bits_events_to_trace == the host ExpReverseBitsLen trace (the reference test
+    program and the shrink-shape program's 5362 events), canonical and Montgomery records."""
+    import torch
+    from zkmips_amd import tracegen as TG
+    for prog, shape in ((R.program_exp_reverse_bits(100, 16), None), (R.program_verifier_shaped(), R.SHRINK_SHAPE)):
+        rec = R.execute(prog)
+        _, tr = R.generate_traces(rec, shape)
+        want = tr["ExpReverseBitsLen"]
+        ev = rec.events["exprev"]
+        rows = np.concatenate([e["rows"] for e in ev])
+        lens = np.concatenate([np.full(e["n"], e["L"]) for e in ev])
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        base = rows[offs[:-1], 0].astype(np.uint32)
+        bits = rows[:, 1].astype(np.uint32)
+        for mont in (False, True):
+            b_, x_ = (bits, base) if not mont else tuple(
+                ((v.astype(np.uint64) << np.uint64(32)) % np.uint64(R.P)).astype(np.uint32) for v in (bits, base))
+            got = TG.exp_reverse_bits_trace(torch.from_numpy(x_.view(np.int32).copy()).cuda(),
+                                            torch.from_numpy(b_.view(np.int32).copy()).cuda(),
+                                            torch.from_numpy(offs).cuda(), len(base), want.shape[0], montgomery=mont)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), want)

@@ -91,6 +91,33 @@ __global__ __launch_bounds__(NTH) void k_p2wide_rows(const uint32_t *__restrict_
     }
 }
 
+// ExpReverseBitsLen: one thread per event walks its rows in order (accum_i = accum_{i-1}^2 * multiplier_i,
+// the square-and-multiply of x^rev(e)); events are short (one row per exponent bit).
+__global__ __launch_bounds__(256) void k_exp_rev_rows(const uint32_t *__restrict__ base, const uint32_t *__restrict__ bits,
+                                                      const uint64_t *__restrict__ off, uint64_t n, uint32_t repr,
+                                                      uint32_t *__restrict__ out) {
+    using namespace kb;
+    const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n) return;
+    auto in = [&](uint32_t v) { return repr == ZKM_REPR_MONTGOMERY ? (v < P ? v : v - P) : to_mont(v); };
+    const uint32_t x = in(base[e]);
+    uint32_t acc = ONE;
+    for (uint64_t r = off[e]; r < off[e + 1]; r++) {
+        const uint32_t b = in(bits[r]);
+        const uint32_t mult = b == ONE ? x : ONE;
+        const uint32_t psq = mul(acc, acc), psqm = mul(psq, mult);
+        acc = psqm;
+        uint32_t *row = out + r * ZKM_EXP_REVERSE_BITS_LEN_WIDTH;
+        row[0] = from_mont(x);
+        row[1] = from_mont(b);
+        row[2] = from_mont(psq);
+        row[3] = from_mont(psqm);
+        row[4] = from_mont(acc);
+        row[5] = from_mont(mul(acc, acc));
+        row[6] = from_mont(mult);
+    }
+}
+
 }  // namespace zkm::rtg
 
 using namespace zkm::rtg;
@@ -108,6 +135,29 @@ extern "C" int zkm_poseidon2_wide_events_to_trace(const zkm_poseidon2_event *eve
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_poseidon2_wide_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+extern "C" int zkm_exp_reverse_bits_events_to_trace(const uint32_t *base, const uint32_t *bits, const uint64_t *offsets,
+                                                    uint64_t n, uint32_t repr, uint32_t *trace, uint64_t height,
+                                                    void *stream) {
+    if (!trace || !offsets || (n && (!base || !bits)) || height < 16 || (height & (height - 1)) ||
+        (repr != ZKM_REPR_CANONICAL && repr != ZKM_REPR_MONTGOMERY)) {
+        g_last_error = "zkm_exp_reverse_bits_events_to_trace: bad arguments (height a power of two >= 16, repr "
+                       "canonical or Montgomery)";
+        return ZKM_ERR_ARG;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t err = hipMemsetAsync(trace, 0, (size_t)height * ZKM_EXP_REVERSE_BITS_LEN_WIDTH * 4, s);
+    if (err == hipSuccess && n) {
+        hipLaunchKernelGGL(k_exp_rev_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, base, bits, offsets, n,
+                           repr, trace);
+        err = hipGetLastError();
+    }
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_exp_reverse_bits_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;

@@ -190,6 +190,7 @@ def _bind():
         L.zkm_syscall_events_to_trace.argtypes = [vp, u64, C.c_int, vp, u64, vp]
         L.zkm_global_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp, vp]
         L.zkm_poseidon2_wide_events_to_trace.argtypes = [vp, u64, C.c_uint32, vp, u64, vp]
+        L.zkm_exp_reverse_bits_events_to_trace.argtypes = [vp, vp, vp, u64, C.c_uint32, vp, u64, vp]
         L._tracegen_bound = True
     return L
 
@@ -343,4 +344,21 @@ def poseidon2_wide_trace(events_dev, n: int, height: int = None, montgomery: boo
     what = "zkm_poseidon2_wide_events_to_trace"
     _lib.check(_bind().zkm_poseidon2_wide_events_to_trace(_words(events_dev, 32 * n, what) if n else None, n,
                                                           1 if montgomery else 0, t.data_ptr(), height, _stream()), what)
+    return t
+
+
+EXP_REVERSE_BITS_LEN_WIDTH = 7  # ZKM_EXP_REVERSE_BITS_LEN_WIDTH
+
+
+def exp_reverse_bits_trace(base_dev, bits_dev, offsets_dev, n: int, height: int, montgomery: bool = False):
+    """ExpReverseBitsLen main trace (height x 7 int32, canonical, on the GPU): event e's bits are
+    bits[offsets[e]:offsets[e+1]] (int64 offsets, n + 1 of them, on the GPU)."""
+    t = _trace(height, EXP_REVERSE_BITS_LEN_WIDTH)
+    what = "zkm_exp_reverse_bits_events_to_trace"
+    if offsets_dev is None or not offsets_dev.is_cuda or offsets_dev.element_size() != 8 or offsets_dev.numel() < n + 1:
+        raise ValueError(f"{what}: need n + 1 int64 offsets on the GPU")
+    _lib.check(_bind().zkm_exp_reverse_bits_events_to_trace(_words(base_dev, n, what) if n else None,
+                                                            _words(bits_dev, 0, what) if n else None, _ptr(offsets_dev),
+                                                            n, 1 if montgomery else 0, t.data_ptr(), height, _stream()),
+               what)
     return t
