@@ -242,13 +242,15 @@ def test_gpu_verifier_shaped_proof_bytes_identical(dev):
 @pytest.mark.gpu
 def test_gpu_shrink_shape_full_size_verifies(dev):
     """The reference's shrink shape (MemoryVar/Select 2^18, ..., Poseidon2WideDeg3 2^16) at full size:
-    the oracle verifier accepts the GPU proof and rejects a flipped byte."""
+    GPU proof bytes == the oracle's; the oracle verifier accepts the GPU proof and rejects a flipped byte."""
     from zkmips_amd.prover import HipProver
     m, pr, tr, pvs = R.shard(R.program_verifier_shaped(), R.SHRINK_SHAPE)
     gpu = HipProver(dev, m, pr, num_queries=NQ, log_blowup=LB)
     cpu = O.OracleProver(m, pr, num_queries=NQ, log_blowup=LB)
     proof = gpu.prove_shard(tr, pvs)
     assert cpu.verify(proof) == 0
+    rc, ref = cpu.prove(tr, pvs)
+    assert rc == 0 and proof == ref  # byte for byte at the reference's shrink shape
     bad = bytearray(proof)
     bad[len(bad) // 2] ^= 1
     assert cpu.verify(bytes(bad)) != 0

@@ -63,6 +63,7 @@ def test_shape_shard_gpu_proof_bytes_identical():
 
 @pytest.mark.gpu
 def test_shape_shard_full_size_gpu_proof_verifies():
+    """The full maximal 2^22 shape: GPU proof bytes == the oracle's, accepted; a tampered trace is rejected."""
     from zkmips_amd._lib import Device
     from zkmips_amd.prover import HipProver
     m, prep, tr, pv = SH.shape_shard(SH.MAXIMAL_22, seed=5, down=0)
@@ -71,6 +72,8 @@ def test_shape_shard_full_size_gpu_proof_verifies():
     p = gpu.prove_shard(tr, pv)
     cpu = O.OracleProver(m, prep, num_queries=84)
     assert cpu.verify(p) == 0
+    rc, ref = cpu.prove(tr, pv)  # the reference's maximal 2^22 shape, byte for byte (BASELINE config 3's size)
+    assert rc == 0 and p == ref
     bad = dict(tr)
     bad["Bitwise"] = tr["Bitwise"].copy()
     bad["Bitwise"][12345, 3] ^= 1
