@@ -665,4 +665,6 @@ def test_core_gpu_full_size_verifies(dev):
     cpu = O.OracleProver(m, prep, num_queries=84)
     proof = gpu.prove_shard(tr, pv)
     assert cpu.verify(proof) == 0
+    rc, ref = cpu.prove(tr, pv)  # every restated chip at the headline height, byte for byte
+    assert rc == 0 and proof == ref
     assert cpu.verify(gpu.prove_shard(_tamper(tr, "register_read"), pv)) != 0
