@@ -88,6 +88,7 @@ def test_ext_inverse():
 
 
 PROGRAMS = {
+    "empty": R.RecursionProgram,  # every chip present, all padding (height 16)
     "basic_mem": R.program_basic_mem,
     "base_four_ops": lambda: R.program_base_four_ops(1000),
     "ext_four_ops": lambda: R.program_ext_four_ops(1000),
