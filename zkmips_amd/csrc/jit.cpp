@@ -440,18 +440,63 @@ std::vector<char> compile_source(const std::string &src, const std::string &name
 
 }  // namespace
 
+namespace {
+
+// cheap identity of everything chip_source reads, so a repeated setup (the compress stage sets up a
+// program per proof, prover/src/lib.rs:807) neither regenerates the kernel source nor reloads the module
+uint64_t chip_key(const ChipDesc &c, int device) {
+    std::vector<uint32_t> w = {(uint32_t)device, (uint32_t)c.prep_w, (uint32_t)c.main_w, (uint32_t)c.scope,
+                               (uint32_t)c.local_only, (uint32_t)c.log_qd, (uint32_t)c.n_main, (uint32_t)c.perm_w,
+                               (uint32_t)c.n_constraints, (uint32_t)c.max_stack, (uint32_t)c.code.size()};
+    w.insert(w.end(), c.code.begin(), c.code.end());
+    auto vpc = [&](const VPC &v) {
+        w.push_back((uint32_t)v.cols.size());
+        w.insert(w.end(), v.cols.begin(), v.cols.end());
+        w.insert(w.end(), v.weights.begin(), v.weights.end());
+        w.push_back(v.constant);
+    };
+    w.push_back((uint32_t)c.local.size());
+    for (const LookupDesc &l : c.local) {
+        w.push_back(l.kind);
+        w.push_back(l.scope);
+        w.push_back(l.is_send);
+        w.push_back((uint32_t)l.values.size());
+        for (const VPC &v : l.values) vpc(v);
+        vpc(l.mult);
+    }
+    const std::string bytes((const char *)w.data(), w.size() * 4);
+    return fnv1a(bytes, fnv1a(c.name));
+}
+
+std::mutex g_loaded_mu;
+std::unordered_map<uint64_t, JitKernel> g_loaded;  // loaded for the process lifetime
+
+}  // namespace
+
+// The returned kernel's module belongs to the process-wide cache (mod is left null, so a proving key's
+// destructor does not unload it).
 JitKernel jit_chip(const ChipDesc &c, int device) {
+    const uint64_t key = chip_key(c, device);
+    {
+        std::lock_guard<std::mutex> g(g_loaded_mu);
+        auto it = g_loaded.find(key);
+        if (it != g_loaded.end()) return it->second;
+    }
     JitKernel k;
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     std::string arch = prop.gcnArchName;
     arch = arch.substr(0, arch.find(':'));  // "gfx950:sramecc+:xnack-" -> "gfx950"
-    k.code = jit_chip_code(c, arch);
-    HIP_CHECK(hipModuleLoadData(&k.mod, k.code.data()));
-    HIP_CHECK(hipModuleGetFunction(&k.fn, k.mod, "zkm_quot_jit"));
-    if (!c.local.empty()) HIP_CHECK(hipModuleGetFunction(&k.fn_perm, k.mod, "zkm_perm_jit"));
+    const std::vector<char> code = jit_chip_code(c, arch);
+    hipModule_t mod = nullptr;
+    HIP_CHECK(hipModuleLoadData(&mod, code.data()));
+    HIP_CHECK(hipModuleGetFunction(&k.fn, mod, "zkm_quot_jit"));
+    if (!c.local.empty()) HIP_CHECK(hipModuleGetFunction(&k.fn_perm, mod, "zkm_perm_jit"));
     k.ok = true;
-    return k;
+    std::lock_guard<std::mutex> g(g_loaded_mu);
+    auto ins = g_loaded.emplace(key, k);
+    if (!ins.second) (void)hipModuleUnload(mod);  // another thread loaded the same chip meanwhile
+    return ins.first->second;
 }
 
 void launch_quotient_jit(const JitKernel &k, const ZkmQuotJitArgs &a, hipStream_t s) {
