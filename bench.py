@@ -208,22 +208,63 @@ def host_info():
             "omp_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+def cgroup_cpu_limit():
+    """The cgroup v2 CPU quota of this process in CPUs (cpu.max "quota period"), or None if unlimited."""
+    try:
+        cg = open("/proc/self/cgroup").read().strip().split("\n")[0].split(":", 2)[2]
+        q, p = open(f"/sys/fs/cgroup{cg}/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError, IndexError):
+        return None
+
+
 def cpu_baseline(log_n, queries):
     """The CPU oracle (a C/OpenMP restatement, not the reference binary; AVX-512 Poseidon2 and LDE, batch
-    inversions, oracle/p2x16.c, oracle/lde_x16.c) on one shard of the headline size."""
+    inversions, oracle/p2x16.c, oracle/lde_x16.c) on one shard of the headline size, with one OpenMP
+    thread per CPU this process may run on (its affinity mask: the GPU's NUMA node after
+    bind_near_gpu), whatever OMP_NUM_THREADS the environment set."""
     from tests import _oracle as O
     from zkmips_amd import workloads as W
     n = 1 << log_n
     m, prep, traces, pvs = W.fib_shard(n, seed=1)
     pr = O.OracleProver(m, prep, num_queries=queries)
+    cpus = len(os.sched_getaffinity(0))
+    gomp = C.CDLL("libgomp.so.1")  # the oracle's OpenMP runtime (same soname, same instance)
+    gomp.omp_set_num_threads(cpus)
+    threads = gomp.omp_get_max_threads()
     t0 = time.time()
     rc, proof = pr.prove(traces, pvs)
     dt = time.time() - t0
     assert rc == 0
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": n / dt, "unit": "rows/s", "cores": cores, "kind": "port", "host": host_info(),
+    quota = cgroup_cpu_limit()
+    return {"value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "host": dict(host_info(), cpus_allowed=cpus, cgroup_cpu_quota=quota),
             "sample": f"one S-SHARD FibCpu 2^{log_n}-row shard (+FibTable), full commit+open, {queries} queries, "
-                      f"{dt:.2f} s wall on {cores} OpenMP threads (AVX-512 Poseidon2/LDE)"}
+                      f"{dt:.2f} s wall on {threads} OpenMP threads = every CPU of this process's affinity mask "
+                      f"(AVX-512 Poseidon2/LDE)" + (f"; cgroup CPU quota {quota} CPUs" if quota else "")}
+
+
+def maxshape_leg(args, rk, n, K):
+    """Secondary field of the default line: the reference's maximal 2^22 MIPS shard shape
+    (maximal_shapes.json["22"][2], zkmips_amd/shapes.py: 17 chips, 557M main cells, 2.23 GB of traces)
+    proven like the headline, from page-locked host traces (H2D in the timed span) and resident."""
+    sb = ShardBench(args, rk, "maxshape", n, K)
+    sb.run_steps(1, "pipelined")
+    steps = max(1, args.maxshape_steps)
+    p1, el = sb.timed(steps, "pipelined")
+    p2, el_res = sb.timed(steps, "resident")
+    assert p1 == p2, "maxshape: resident / host-trace proofs differ"
+    tr = sb.shards[0][2]
+    rows = sb.rows_per_shard
+    out = {"workload": "MIPS shard in the reference maximal shape maximal_shapes.json[\"22\"][2]: "
+                       + ", ".join(f"{k} 2^{int(np.log2(len(tr[k])))}" for k in sorted(tr, key=lambda c: -len(tr[c]))),
+           "rows_per_shard": rows, "main_cells": int(sum(v.size for v in tr.values())),
+           "h2d_bytes_per_shard": int(sum(v.nbytes for v in tr.values())), "steps": steps, "in_flight": K,
+           "value": round(K * rows * steps / el, 1), "unit": "rows/s", "ms_per_shard": round(1e3 * el / (steps * K), 3),
+           "resident": {"value": round(K * rows * steps / el_res, 1), "ms_per_shard": round(1e3 * el_res / (steps * K), 3)},
+           "proof_bytes": len(p1), "trace_generation_s": round(sb.gen_s, 1)}
+    del sb
+    return out
 
 
 def make_shard(workload, n, seed):
@@ -240,52 +281,110 @@ def make_shard(workload, n, seed):
     return W.fib_shard(n, seed=seed)
 
 
+class Ranks:
+    """This process's place in the job: RANK / LOCAL_RANK / WORLD_SIZE from the launcher (the driver's
+    torch.distributed.run, or `launch_ranks` below), the GPU it binds, and the process group (RCCL over
+    xGMI; gloo when rehearsing N ranks on fewer GPUs, ZKM_BENCH_REHEARSE=1).  `--gpus` must equal the
+    live world size."""
+
+    def __init__(self, args, bind=True):
+        import torch.distributed as dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if args.gpus is not None and args.gpus != self.world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={self.world}")
+        # ZKM_BENCH_REHEARSE=1: rehearse the N-rank flow on a box with fewer GPUs (ranks share the cards,
+        # gloo instead of RCCL); never set by the driver, so the N-GPU bench is always RCCL.
+        self.rehearse = os.environ.get("ZKM_BENCH_REHEARSE") == "1"
+        # ZKM_BENCH_REPLAY=<dir> (rehearsal only, CPU tests of the launch/deal/gather plumbing): shard
+        # proofs are read from <dir>/shard_<i>.bin instead of proven; no GPU is touched.
+        self.replay = os.environ.get("ZKM_BENCH_REPLAY") if self.rehearse else None
+        self.coll_dev = "cpu" if self.rehearse else "cuda"
+        self.numa = None
+        if not self.replay:
+            import torch
+            if self.rehearse:
+                self.local_rank %= max(1, torch.cuda.device_count())
+            torch.cuda.set_device(self.local_rank)
+            if bind and os.environ.get("ZKM_NO_NUMA_BIND") != "1":
+                self.numa = bind_near_gpu(self.local_rank)
+        if self.world > 1:
+            if self.rehearse:
+                dist.init_process_group("gloo")
+            else:
+                import torch
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+            self.world = dist.get_world_size()
+            assert self.world == (args.gpus or self.world), "process group size differs from --gpus"
+
+    def sync(self):
+        if not self.replay:
+            import torch
+            torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        self.sync()
+
+    def max_over_ranks(self, el):
+        if self.world == 1:
+            return el
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([el], dtype=torch.float64, device=self.coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+
+
 def execution_bench(args):
-    """BASELINE config 3: a whole sha2-precompile-shaped execution proven shard by shard on one GPU.
-    The guest (mips_core.sha_program) hashes `--sha-blocks` 64-byte blocks with SHA_EXTEND + SHA_COMPRESS,
-    COMMITs and HALTs; the execution splits into CPU shards of 2^log_n-ish rows, SHA_EXTEND and
-    SHA_COMPRESS precompile shards and the memory shard.  Every step proves all of them (traces resident
-    in HBM, `--inflight` shards concurrently); the machine-level global sum of the proofs is checked."""
+    """BASELINE configs 3/4: a whole execution proven shard by shard.  `sha2`: the guest
+    (mips_core.sha_program) hashes `--sha-blocks` 64-byte blocks with SHA_EXTEND + SHA_COMPRESS, COMMITs
+    and HALTs; the execution splits into CPU shards of 2^log_n-ish rows, SHA_EXTEND and SHA_COMPRESS
+    precompile shards and the memory shard.  Every step proves all of them (traces resident in HBM,
+    `--inflight` shards concurrently per GPU); with N ranks the shards are dealt by cost
+    (dist.deal_by_cost), the proofs gathered to rank 0 and the machine-level global sum checked there."""
     import threading
-    import torch
     from zkmips_amd import mips_core as MC
-    from zkmips_amd._lib import Device
+    from zkmips_amd.dist import deal_by_cost, prove_shards_distributed, shard_cost
     from zkmips_amd.proof import machine_global_sum_is_zero
-    from zkmips_amd.prover import HipProver
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch.distributed as dist
-    rehearse = os.environ.get("ZKM_BENCH_REHEARSE") == "1"
-    if rehearse:
-        local_rank = local_rank % max(1, torch.cuda.device_count())
-    coll_dev = "cpu" if rehearse else "cuda"
+    rk = Ranks(args, bind=False)
+    world, rank = rk.world, rk.rank
     t0 = time.time()
     max_steps = min((1 << args.log_n) * 4 // 5, (1 << 24) // 5 - 1)
     run = MC.program_shards(MC.sha_program(args.sha_blocks, seed=1), seed=1, shard_size=max_steps,
                             precompile_events_per_shard=args.sha_events_per_shard)
     gen_s = time.time() - t0
     print(f"sha2: {len(run)} shards generated in {gen_s:.1f} s", file=sys.stderr, flush=True)
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    from zkmips_amd.dist import assign_shards, prove_shards_distributed
-    mine = set(assign_shards(len(run), world, rank))  # config 4: the execution's shards dealt across ranks
-    m, prep, _, _ = run[0]
-    prep = {k: v for k, v in prep.items() if v is not None}
-    prover = HipProver(Device(local_rank), m, prep, num_queries=args.queries)
-    dev = [({k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in tr.items()}, pv) if i in mine else None
-           for i, (_, _, tr, pv) in enumerate(run)]
+    costs = [shard_cost(tr) for _, _, tr, _ in run]
+    deal = deal_by_cost(costs, world)
+    mine = deal[rank]  # configs 3/4: the execution's shards dealt across ranks, largest first
+    if rk.replay:
+        prove_one = lambda i: open(os.path.join(rk.replay, f"shard_{i}.bin"), "rb").read()
+    else:
+        import torch
+        from zkmips_amd._lib import Device
+        from zkmips_amd.prover import HipProver
+        m, prep, _, _ = run[0]
+        prep = {k: v for k, v in prep.items() if v is not None}
+        prover = HipProver(Device(rk.local_rank), m, prep, num_queries=args.queries)
+        dev = {i: ({k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in run[i][2].items()}, run[i][3])
+               for i in mine}
+        prove_one = lambda i: prove_resident(prover, dev[i][0], dev[i][1])
     rows = [max(v.shape[0] for v in tr.values()) for _, _, tr, _ in run]
     kinds = ["cpu" if "Cpu" in tr else "memory" if "MemoryGlobalInit" in tr else
              "sha_extend" if "ShaExtend" in tr else "sha_compress" for _, _, tr, _ in run]
-    torch.cuda.synchronize()
+    rk.sync()
 
     def prove_local():
-        idx = sorted(mine)
+        idx = sorted(mine, key=lambda i: (-costs[i], i))  # largest first within the rank too
         out = {}
         nxt = [0]
         lock = threading.Lock()
@@ -298,7 +397,7 @@ def execution_bench(args):
                 if k >= len(idx):
                     return
                 i = idx[k]
-                out[i] = prove_resident(prover, dev[i][0], dev[i][1])
+                out[i] = prove_one(i)
         th = [threading.Thread(target=worker) for _ in range(max(1, args.inflight))]
         for t in th:
             t.start()
@@ -315,45 +414,38 @@ def execution_bench(args):
             assert machine_global_sum_is_zero(proofs), "the execution's global cumulative sums do not add to zero"
             return proofs
         local = prove_local()
-        return prove_shards_distributed(lambda i: local[i], len(run), device=coll_dev, check_global_sum=True)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+        return prove_shards_distributed(lambda i: local[i], len(run), device=rk.coll_dev, check_global_sum=True,
+                                        costs=costs)
 
     for _ in range(max(1, args.warmup)):
         proofs = prove_all()
         print("sha2: warmup execution proven", file=sys.stderr, flush=True)
-    barrier()
+    rk.barrier()
     t1 = time.time()
     for _ in range(args.steps):
-        prove_all()
-    barrier()
-    el = time.time() - t1
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        proofs = prove_all()
+    rk.barrier()
+    el = rk.max_over_ranks(time.time() - t1)
     line = {
         "metric": "shard trace rows proved/sec (whole sha2-precompile execution, BASELINE config 3)",
         "value": round(sum(rows) * args.steps / el, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
-        "data": "synthetic sha2 guest (mips_core.sha_program), traces resident in HBM",
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
+        "data": "synthetic sha2 guest (mips_core.sha_program), traces resident in HBM"
+                + (" (REPLAYED proofs: launch/deal/gather rehearsal, nothing proven)" if rk.replay else ""),
         "config": {"workload": f"sha2-precompile execution: {args.sha_blocks} blocks, {len(run)} shards "
                                f"({', '.join(f'{k} 2^{r.bit_length() - 1}' for k, r in zip(kinds, rows))}), "
                                f"all MIPS + syscall + SHA-256 + memory chips, full commit+open per shard",
                    "shards": len(run), "rows_per_execution": sum(rows), "fri_queries": args.queries,
                    "proof_bytes": sum(len(p) for p in proofs) if rank == 0 else None,
-                   "parallelism": f"{args.inflight} shards in flight" + (f" per rank, shards dealt over {world} ranks, "
-                                  "proofs gathered to rank 0 (global sum checked there)" if world > 1 else ""),
+                   "parallelism": f"{args.inflight} shards in flight" + (
+                       f" per rank, shards dealt by cost (LPT) over {world} ranks {deal}, proofs gathered to rank 0 "
+                       "(global sum checked there)" if world > 1 else ""),
                    "trace_generation_s": round(gen_s, 1), "global_sum_checked": True},
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    rk.close()
 
 
 def tracegen_bench(args):
@@ -444,20 +536,8 @@ def compress_bench(args):
     t0 = time.time()
     m, prep, traces, pvs = R.shard(R.program_verifier_shaped(seed=1), R.SHRINK_SHAPE)
     gen_s = time.time() - t0
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch.distributed as dist
-    rehearse = os.environ.get("ZKM_BENCH_REHEARSE") == "1"
-    if rehearse:
-        local_rank = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_rank)
-    coll_dev = "cpu" if rehearse else "cuda"
-    if world > 1:
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    rk = Ranks(args, bind=False)
+    world, rank, local_rank, coll_dev = rk.world, rk.rank, rk.local_rank, rk.coll_dev
     prover = HipProver(Device(local_rank), m, prep, num_queries=R.COMPRESS_NUM_QUERIES,
                        log_blowup=R.COMPRESS_LOG_BLOWUP)
     dev = {k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in traces.items()}
@@ -498,21 +578,12 @@ def compress_bench(args):
             compress_tree_distributed(None, leaves, device=coll_dev,
                                       prove_nodes=lambda layer, work: prove_layer(len(work)))
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    barrier()
+    rk.barrier()
     t1 = time.time()
     for _ in range(args.steps):
         tree()
-    barrier()
-    el = time.time() - t1
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    rk.barrier()
+    el = rk.max_over_ranks(time.time() - t1)
     n_proofs = sum(layers) * args.steps
     rows = max(v.shape[0] for v in traces.values())
     # serial single-proof latency
@@ -563,8 +634,7 @@ def compress_bench(args):
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    rk.close()
 
 
 def pmc_child(args):
@@ -604,98 +674,78 @@ def bind_near_gpu(device: int):
         return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--log-n", type=int, default=22)
-    ap.add_argument("--sha-blocks", type=int, default=16384, help="sha2 workload: 64-byte blocks hashed")
-    ap.add_argument("--h2d-dst", choices=["torch", "uncached", "finegrained"], default="torch",
-                    help="memory type of the HBM buffers the pipelined H2D copies land in")
-    ap.add_argument("--sha-events-per-shard", type=int, default=16384,
-                    help="sha2 workload: precompile calls per precompile shard")
-    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2", "tracegen", "compress"], default="fib",
-                    help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
-                         "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
-                         "zkmips_amd/mips_alu.py), 2^(log-n) "
-                         "instructions per shard; core: Cpu + Program + Mul + DivRem + Branch + Jump + MovCond + MemoryInstrs + MiscInstrs chips over the ALU slice "
-                         "(zkmips_amd/mips_core.py) running a counted loop, Cpu 2^(log-n) rows; maxshape: a MIPS shard "
-                         "padded to the reference's maximal_shapes.json[\"22\"][2] (zkmips_amd/shapes.py)")
-    ap.add_argument("--queries", type=int, default=84)
-    ap.add_argument("--cpu-log-n", type=int, default=22)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 HBM counter passes")
-    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--profile-out", default="")
-    ap.add_argument("--profile-steps", type=int, default=3, help="single-shard proofs in the profiled region")
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="shards proven concurrently per GPU (one host thread + HIP stream each), as the "
-                         "reference's prove_with_context runs commit/open for all shards of a batch at once")
-    args = ap.parse_args()
-    if args.pmc_child:
-        return pmc_child(args)
-    if args.workload == "sha2":
-        return execution_bench(args)
-    if args.workload == "tracegen":
-        return tracegen_bench(args)
-    if args.workload == "compress":
-        return compress_bench(args)
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` with no external launcher: start N rank processes of this script (RANK =
+    LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1) before anything touches a GPU, wait for
+    them, and return the worst exit code.  If a rank fails, the others are stopped (by their PIDs), so
+    a failed rank cannot leave the rest waiting in a collective."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
-    # ZKM_BENCH_REHEARSE=1: rehearse the N-rank flow on a box with fewer GPUs (ranks share the
-    # cards, gloo instead of RCCL); never set by the driver, so the N-GPU bench is always RCCL
-    rehearse = os.environ.get("ZKM_BENCH_REHEARSE") == "1"
-    if rehearse:
-        local_rank = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_rank)
-    numa = bind_near_gpu(local_rank) if os.environ.get("ZKM_NO_NUMA_BIND") != "1" else None
-    coll_dev = "cpu" if rehearse else "cuda"
-    if world > 1:
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    from zkmips_amd import workloads as W
-    from zkmips_amd._lib import Device, lib
-    from zkmips_amd.prover import HipProver
+class ShardBench:
+    """`K` in-flight slots proving shards of one workload on this rank's GPU, in three modes:
+    "pipelined" (the headline: page-locked host traces, the H2D DMA of step j+1 on the slot's copy stream
+    while step j proves from the other HBM buffer), "per_call" (zkm_prove_shard copies the pinned host
+    traces itself) and "resident" (traces already in HBM)."""
 
-    n = 1 << args.log_n
-    K = max(1, args.inflight)
-    shards = []
-    core = None
-    if args.workload in ("core", "maxshape"):  # one program (one proving key), generated once, proven K times
-        core = make_shard(args.workload, n, 1)
-    for k in range(K):
-        m, prep, traces_k, pvs_k = core if core is not None else make_shard(args.workload, n, 1000 + rank * K + k)
-        pinned = {}
-        for kk, v in traces_k.items():
-            pinned[kk] = torch.empty(v.shape, dtype=torch.int32, pin_memory=True)
-            pinned[kk].numpy()[...] = v.view(np.int32)
-        shards.append(({kk: torch.from_numpy(v.view(np.int32)).cuda() for kk, v in traces_k.items()}, pvs_k,
-                       {kk: t.numpy().view(np.uint32) for kk, t in pinned.items()}, pinned,
-                       [{kk: (torch.empty_like(t, device="cuda") if args.h2d_dst == "torch" else
-                              RawDev(t.shape, H2D_FLAGS[args.h2d_dst])) for kk, t in pinned.items()} for _ in range(2)],
-                       torch.cuda.Stream()))
-    dev = Device(local_rank)
-    prover = HipProver(dev, m, prep, num_queries=args.queries)
-    dev_traces, pvs, traces = shards[0][0], shards[0][1], shards[0][2]
-    torch.cuda.synchronize()
-    rows_per_shard = max(v.shape[0] for v in traces.values())
+    def __init__(self, args, rk, workload, n, K):
+        import torch
+        from zkmips_amd._lib import Device
+        from zkmips_amd.prover import HipProver
+        self.args, self.rk, self.K = args, rk, K
+        self.shards = []
+        one = None
+        if workload in ("core", "maxshape"):  # one program (one proving key), generated once, proven K times
+            t0 = time.time()
+            one = make_shard(workload, n, 1)
+            self.gen_s = time.time() - t0
+        for k in range(K):
+            m, prep, traces_k, pvs_k = one if one is not None else make_shard(workload, n, 1000 + rk.rank * K + k)
+            pinned = {}
+            for kk, v in traces_k.items():
+                pinned[kk] = torch.empty(v.shape, dtype=torch.int32, pin_memory=True)
+                pinned[kk].numpy()[...] = v.view(np.int32)
+            self.shards.append(({kk: torch.from_numpy(v.view(np.int32)).cuda() for kk, v in traces_k.items()}, pvs_k,
+                                {kk: t.numpy().view(np.uint32) for kk, t in pinned.items()}, pinned,
+                                [{kk: (torch.empty_like(t, device="cuda") if args.h2d_dst == "torch" else
+                                       RawDev(t.shape, H2D_FLAGS[args.h2d_dst])) for kk, t in pinned.items()}
+                                 for _ in range(2)],
+                                torch.cuda.Stream()))
+        self.m = m
+        self.prover = HipProver(Device(rk.local_rank), m, prep, num_queries=args.queries)
+        torch.cuda.synchronize()
+        self.rows_per_shard = max(v.shape[0] for v in self.shards[0][2].values())
+        self.stagger = None
 
-    stagger = None
-
-    def slot_steps(k, nsteps, mode):
-        """nsteps shard proofs of in-flight slot k; returns the last proof.
-        mode "pipelined": H2D of step j+1 (pinned host -> HBM, DMA on the slot's copy stream) is in
-        flight while step j proves from the other HBM buffer; "per_call": zkm_prove_shard on the
-        pinned host traces (the copy happens inside the call); "resident": traces already in HBM."""
-        dev_t, pv, host_np, host_t, bufs, cs = shards[k]
+    def slot_steps(self, k, nsteps, mode):
+        """nsteps shard proofs of in-flight slot k; returns the last proof."""
+        import torch
+        prover = self.prover
+        dev_t, pv, host_np, host_t, bufs, cs = self.shards[k]
         if mode == "resident":
             pr = b""
             for _ in range(nsteps):
@@ -720,6 +770,7 @@ def main():
             return e
         # the slots' first copies go one after another (slot k starts when slot k-1's has landed), so
         # slot 0 proves after one copy time instead of all slots waiting for K copies sharing PCIe
+        stagger = self.stagger
         if stagger is not None and k > 0:
             stagger[k - 1].wait(60)  # bounded: a failing slot must not hang the others
         ev = issue(0)
@@ -735,65 +786,110 @@ def main():
             ev = nxt
         return pr
 
-    def run_steps(nsteps, mode="pipelined"):
-        """nsteps shard proofs per in-flight slot; returns the last proof of slot 0."""
-        if K == 1:
-            proof = slot_steps(0, nsteps, mode)
-            gather(proof)
-            return proof
+    def run_steps(self, nsteps, mode="pipelined"):
+        """nsteps shard proofs per in-flight slot; returns the last proof of slot 0, after gathering
+        every rank's to rank 0 (the MachineProof aggregation, RCCL over xGMI)."""
         import threading
-        nonlocal stagger
-        stagger = ([threading.Event() for _ in range(K)]
-                   if mode == "pipelined" and os.environ.get("ZKM_NO_STAGGER") != "1" else None)
-        out = [b""] * K
-        def slot(k):
-            out[k] = slot_steps(k, nsteps, mode)
-        th = [threading.Thread(target=slot, args=(k,)) for k in range(K)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        gather(out[0])
-        return out[0]
+        K = self.K
+        if K == 1:
+            proof = self.slot_steps(0, nsteps, mode)
+        else:
+            self.stagger = ([threading.Event() for _ in range(K)]
+                            if mode == "pipelined" and os.environ.get("ZKM_NO_STAGGER") != "1" else None)
+            out = [b""] * K
 
-    def gather(proof):
-        """MachineProof aggregation: all ranks' shard proofs over RCCL (zkmips_amd/dist.py)."""
-        if world == 1:
-            return {0: proof}
-        from zkmips_amd.dist import gather_proofs_to_root
-        return gather_proofs_to_root({rank: proof}, device=coll_dev)
+            def slot(k):
+                out[k] = self.slot_steps(k, nsteps, mode)
+            th = [threading.Thread(target=slot, args=(k,)) for k in range(K)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            proof = out[0]
+        if self.rk.world > 1:
+            from zkmips_amd.dist import gather_proofs_to_root
+            got = gather_proofs_to_root({self.rk.rank: proof}, device=self.rk.coll_dev)
+            assert self.rk.rank != 0 or sorted(got) == list(range(self.rk.world)), "a rank's proof is missing"
+        return proof
 
-    if args.warmup:
-        run_steps(args.warmup, "pipelined")
-        run_steps(1, "per_call")
-
-    def timed(mode):
-        """`steps` batches of K concurrent shard proofs, barrier + sync on both sides, max over ranks."""
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+    def timed(self, nsteps, mode):
+        """`nsteps` batches of K concurrent shard proofs, barrier + sync on both sides, max over ranks."""
+        self.rk.barrier()
         t0 = time.perf_counter()
-        pr = run_steps(args.steps, mode)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return pr, el
+        pr = self.run_steps(nsteps, mode)
+        self.rk.barrier()
+        return pr, self.rk.max_over_ranks(time.perf_counter() - t0)
 
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without an external launcher bench.py starts them itself")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--log-n", type=int, default=22)
+    ap.add_argument("--sha-blocks", type=int, default=16384, help="sha2 workload: 64-byte blocks hashed")
+    ap.add_argument("--h2d-dst", choices=["torch", "uncached", "finegrained"], default="torch",
+                    help="memory type of the HBM buffers the pipelined H2D copies land in")
+    ap.add_argument("--sha-events-per-shard", type=int, default=16384,
+                    help="sha2 workload: precompile calls per precompile shard")
+    ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2", "tracegen", "compress"], default="fib",
+                    help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
+                         "ShiftLeft, ShiftRight, CloClz, Byte restated from the reference AIRs + CPU stand-in, "
+                         "zkmips_amd/mips_alu.py), 2^(log-n) "
+                         "instructions per shard; core: Cpu + Program + Mul + DivRem + Branch + Jump + MovCond + MemoryInstrs + MiscInstrs chips over the ALU slice "
+                         "(zkmips_amd/mips_core.py) running a counted loop, Cpu 2^(log-n) rows; maxshape: a MIPS shard "
+                         "padded to the reference's maximal_shapes.json[\"22\"][2] (zkmips_amd/shapes.py)")
+    ap.add_argument("--queries", type=int, default=84)
+    ap.add_argument("--cpu-log-n", type=int, default=22)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-maxshape", action="store_true",
+                    help="skip the default line's secondary leg: the reference's maximal 2^22 MIPS shard shape")
+    ap.add_argument("--maxshape-steps", type=int, default=4)
+    ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 HBM counter passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--profile-out", default="")
+    ap.add_argument("--profile-steps", type=int, default=3, help="single-shard proofs in the profiled region")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="shards proven concurrently per GPU (one host thread + HIP stream each), as the "
+                         "reference's prove_with_context runs commit/open for all shards of a batch at once")
+    args = ap.parse_args()
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.pmc_child:
+        return pmc_child(args)
+    if args.workload == "sha2":
+        return execution_bench(args)
+    if args.workload == "tracegen":
+        return tracegen_bench(args)
+    if args.workload == "compress":
+        return compress_bench(args)
+
+    import torch
+    rk = Ranks(args)
+    world, rank, local_rank, numa = rk.world, rk.rank, rk.local_rank, rk.numa
+
+    from zkmips_amd import workloads as W
+    from zkmips_amd._lib import lib
+
+    n = 1 << args.log_n
+    K = max(1, args.inflight)
+    sb = ShardBench(args, rk, args.workload, n, K)
+    prover, m = sb.prover, sb.m
+    dev_traces, pvs, traces = sb.shards[0][0], sb.shards[0][1], sb.shards[0][2]
+    rows_per_shard = sb.rows_per_shard
+    if args.warmup:
+        sb.run_steps(args.warmup, "pipelined")
+        sb.run_steps(1, "per_call")
     # timed region (the headline): host traces, H2D + commit + open + D2H of the proof
-    proof, elapsed = timed("pipelined")
+    proof, elapsed = sb.timed(args.steps, "pipelined")
     # secondary: per-call host copies, and traces already resident in HBM
-    proof_pc, elapsed_pc = timed("per_call")
-    proof_res, elapsed_res = timed("resident")
+    proof_pc, elapsed_pc = sb.timed(args.steps, "per_call")
+    proof_res, elapsed_res = sb.timed(args.steps, "resident")
     assert proof_res == proof == proof_pc, "resident / host-trace proofs differ"
 
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
+        rk.close()
         return
 
     # profiled region: single-shard latency with per-stage HIP events on the launching stream
@@ -923,14 +1019,15 @@ def main():
         "stages_ms_per_shard": stages,
         "profiled_region": f"{nprof} single-shard proofs after the timed region (stages, roofline, ntt, serial_ms_per_shard)",
     }
+    if not args.no_maxshape and world == 1 and args.workload == "fib":
+        line["maxshape"] = maxshape_leg(args, rk, n, K)
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(args.cpu_log_n, args.queries)
     if args.profile_out:
         with open(args.profile_out, "w") as f:
             f.write(buf.value.decode())
     print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    rk.close()
 
 
 if __name__ == "__main__":

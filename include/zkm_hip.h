@@ -43,6 +43,7 @@ extern "C" {
 typedef struct zkm_ctx zkm_ctx;   /* one per GPU: device, stream pool, twiddle tables */
 typedef struct zkm_pk zkm_pk;     /* DeviceProvingKey   (prover.rs:40, machine.rs:55-75)   */
 typedef struct zkm_main zkm_main; /* ShardMainData<SC, DeviceMatrix, DeviceProverData> (types.rs:16-22) */
+typedef struct zkm_machine zkm_machine; /* a machine layout (StarkMachine chips), no preprocessed data */
 
 /* PCS / FRI configuration (crates/stark/src/kb31_poseidon2.rs:203-213). */
 typedef struct {
@@ -102,6 +103,15 @@ int zkm_pk_observe(const zkm_pk *pk, zkm_challenger_t *ch);
  * On success *main_out owns the device LDEs + Merkle tree; main_commit_out[8] = root. */
 int zkm_commit(zkm_ctx *ctx, const zkm_pk *pk, const zkm_matrix_t *traces, uint32_t ntraces,
                const uint32_t *public_values, uint32_t npv, zkm_main **main_out, uint32_t main_commit_out[8]);
+/* The same commit against a key-free machine handle: the trait's commit receives no proving key
+ * (prover.rs:111-115, called concurrently with other programs' setups by the compress workers,
+ * prover/src/lib.rs:794-824), and commit reads only the machine layout (chip names, main widths,
+ * blowup).  zkm_open rejects (ZKM_ERR_ARG) a shard committed under a different machine than its key. */
+int zkm_machine_new(const uint32_t *machine_blob, size_t nwords, const zkm_config_t *cfg, zkm_machine **out);
+void zkm_machine_free(zkm_machine *m);
+int zkm_commit_machine(zkm_ctx *ctx, const zkm_machine *m, const zkm_matrix_t *traces, uint32_t ntraces,
+                       const uint32_t *public_values, uint32_t npv, zkm_main **main_out,
+                       uint32_t main_commit_out[8]);
 void zkm_main_free(zkm_main *main);
 
 /* ---- MachineProver::open (prover.rs:132-137, :298-653) ----

@@ -46,8 +46,8 @@ impl Drop for Ctx {
     }
 }
 
-/// The device proving key plus the host key the trait's accessors read.  Shared (`Arc`): the trait's
-/// `commit` receives no key, so the prover keeps the key of its last setup for it.
+/// The device proving key plus the host key the trait's accessors read.  Shared (`Arc`) across the
+/// `prove_with_context` workers.
 pub struct PkInner {
     pk: *mut zkm_pk,
     host: StarkProvingKey<SC>,
@@ -89,12 +89,24 @@ impl Drop for HipMainData {
     }
 }
 
+/// The machine layout for `commit` (zkm_machine_new): the trait's `commit` receives no proving key,
+/// and the compress workers call `setup(program)` and `commit` concurrently for different programs
+/// (prover/src/lib.rs:794-824), so commit must not depend on whichever key was set up last.
+struct MachineHandle(*mut zkm_machine);
+unsafe impl Send for MachineHandle {}
+unsafe impl Sync for MachineHandle {}
+impl Drop for MachineHandle {
+    fn drop(&mut self) {
+        unsafe { zkm_machine_free(self.0) }
+    }
+}
+
 pub struct HipProver<A> {
     machine: StarkMachine<SC, A>,
     ctx: Ctx,
     blob: Vec<u32>,
     cfg: zkm_config_t,
-    current: std::sync::RwLock<Option<HipProvingKey>>,
+    layout: MachineHandle,
 }
 
 fn canonical(v: &[KoalaBear]) -> Vec<u32> {
@@ -166,14 +178,21 @@ where
             log_blowup: fri.log_blowup as u32,
             proof_montgomery: 0,
         };
-        Ok(Self { machine, ctx: Ctx(ctx), blob, cfg, current: std::sync::RwLock::new(None) })
+        let mut layout = ptr::null_mut();
+        check(unsafe { zkm_machine_new(blob.as_ptr(), blob.len(), &cfg, &mut layout) }, "zkm_machine_new")?;
+        Ok(Self { machine, ctx: Ctx(ctx), blob, cfg, layout: MachineHandle(layout) })
     }
 
     fn device_pk(&self, program: &A::Program, host: StarkProvingKey<SC>) -> HipProvingKey {
+        let prep: Vec<Option<RowMajorMatrix<KoalaBear>>> =
+            self.machine.chips().iter().map(|c| c.generate_preprocessed_trace(program)).collect();
+        self.upload_pk(prep, host)
+    }
+
+    /// The device key from the preprocessed traces in machine-chip order (None for chips without one).
+    fn upload_pk(&self, prep: Vec<Option<RowMajorMatrix<KoalaBear>>>, host: StarkProvingKey<SC>) -> HipProvingKey {
         let chips = self.machine.chips();
         let names: Vec<CString> = chips.iter().map(|c| CString::new(c.name()).unwrap()).collect();
-        let prep: Vec<Option<RowMajorMatrix<KoalaBear>>> =
-            chips.iter().map(|c| c.generate_preprocessed_trace(program)).collect();
         let mats: Vec<zkm_matrix_t> = prep
             .iter()
             .zip(&names)
@@ -203,9 +222,7 @@ where
         // the GPU's preprocessed commitment is the reference's (tests/test_gpu_prover.py pins it)
         let host_commit: [KoalaBear; 8] = host.commit.into();
         debug_assert_eq!(canonical(&host_commit), commit.to_vec());
-        let key = HipProvingKey(std::sync::Arc::new(PkInner { pk, host }));
-        *self.current.write().unwrap() = Some(key.clone());
-        key
+        HipProvingKey(std::sync::Arc::new(PkInner { pk, host }))
     }
 }
 
@@ -242,7 +259,15 @@ where
     }
 
     fn pk_to_device(&self, pk: &StarkProvingKey<SC>) -> Self::DeviceProvingKey {
-        unimplemented!("HipProver builds its device key from the program (setup / pk_from_vk): {}", pk.traces.len())
+        // the host key's preprocessed traces are indexed by chip_ordering (machine.rs:383-403: sorted by
+        // (height desc, name)); the ABI wants one slot per machine chip, in machine order
+        let prep: Vec<Option<RowMajorMatrix<KoalaBear>>> = self
+            .machine
+            .chips()
+            .iter()
+            .map(|c| pk.chip_ordering.get(&c.name()).map(|&i| pk.traces[i].clone()))
+            .collect();
+        self.upload_pk(prep, pk.clone())
     }
 
     fn pk_to_host(&self, pk: &Self::DeviceProvingKey) -> StarkProvingKey<SC> {
@@ -254,10 +279,8 @@ where
         record: &A::Record,
         traces: Vec<(String, RowMajorMatrix<KoalaBear>)>,
     ) -> ShardMainData<SC, Self::DeviceMatrix, Self::DeviceProverData> {
-        // zkm_commit needs the device key (chip layout); the trait passes none, so commit runs against
-        // the key of the last setup, the one prove_with_context then opens with.
-        let pk = self.current.read().unwrap().clone().expect("HipProver::commit before setup");
-        self.commit_with_key(&pk, record, traces).expect("zkm_commit")
+        // key-free: the machine layout is all commit reads; open checks it against the key's machine
+        self.commit_layout(record, traces).expect("zkm_commit_machine")
     }
 
     fn open(
@@ -294,7 +317,7 @@ where
         let mut shard_proofs = Vec::with_capacity(records.len());
         for record in records {
             let traces = self.generate_traces(&record).map_err(|_| HipProverError("generate_traces".into()))?;
-            let data = self.commit_with_key(pk, &record, traces)?;
+            let data = self.commit_layout(&record, traces)?;
             shard_proofs.push(self.open(pk, data, &mut challenger.clone())?);
         }
         Ok(MachineProof { shard_proofs })
@@ -307,9 +330,8 @@ where
     A::Record: MachineRecord,
 {
     /// MachineProver::commit with the device key (zkm_commit needs the machine layout it holds).
-    pub fn commit_with_key(
+    pub fn commit_layout(
         &self,
-        pk: &HipProvingKey,
         record: &A::Record,
         traces: Vec<(String, RowMajorMatrix<KoalaBear>)>,
     ) -> Result<ShardMainData<SC, RowMajorMatrix<KoalaBear>, HipMainData>, HipProverError> {
@@ -320,10 +342,10 @@ where
         let mut root = [0u32; 8];
         check(
             unsafe {
-                zkm_commit(self.ctx.0, pk.0.pk, mats.as_ptr(), mats.len() as u32, pv.as_ptr(), pv.len() as u32,
-                           &mut main, root.as_mut_ptr())
+                zkm_commit_machine(self.ctx.0, self.layout.0, mats.as_ptr(), mats.len() as u32, pv.as_ptr(),
+                                   pv.len() as u32, &mut main, root.as_mut_ptr())
             },
-            "zkm_commit",
+            "zkm_commit_machine",
         )?;
         // chip ordering as prover.rs:262-285 builds it: (height desc, name)
         let mut order: Vec<(usize, &String)> = traces.iter().map(|(n, m)| (m.height(), n)).collect();

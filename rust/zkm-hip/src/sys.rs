@@ -32,6 +32,10 @@ pub struct zkm_pk {
 pub struct zkm_main {
     _p: [u8; 0],
 }
+#[repr(C)]
+pub struct zkm_machine {
+    _p: [u8; 0],
+}
 
 #[repr(C)]
 #[derive(Clone, Copy, Debug)]
@@ -96,6 +100,19 @@ extern "C" {
         main_commit_out: *mut u32,
     ) -> c_int;
     pub fn zkm_main_free(main: *mut zkm_main);
+    pub fn zkm_machine_new(blob: *const u32, nwords: usize, cfg: *const zkm_config_t, out: *mut *mut zkm_machine)
+        -> c_int;
+    pub fn zkm_machine_free(m: *mut zkm_machine);
+    pub fn zkm_commit_machine(
+        ctx: *mut zkm_ctx,
+        m: *const zkm_machine,
+        traces: *const zkm_matrix_t,
+        ntraces: u32,
+        public_values: *const u32,
+        npv: u32,
+        main_out: *mut *mut zkm_main,
+        main_commit_out: *mut u32,
+    ) -> c_int;
     pub fn zkm_open(
         ctx: *mut zkm_ctx,
         pk: *const zkm_pk,

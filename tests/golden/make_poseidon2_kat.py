@@ -1,11 +1,19 @@
 """Writes tests/golden/poseidon2_kat.json.
 
-The permutation outputs are the values SURVEY.md §8c recorded from the reference's own C++
-Poseidon2 (crates/recursion/core/include/poseidon2_wide.hpp populate_perm, built in the survey
-container), cross-checked there against an independent restatement from RC_16_30_U32
-(crates/primitives/src/lib.rs:563) and INTERNAL_DIAG_MONTY_16
-(crates/core/machine/src/operations/poseidon2/air.rs:12-29).  They are copied here verbatim
-from SURVEY.md; this script only re-serialises them.
+Provenance of the three vectors:
+- ``perm_zeros`` (perm([0; 16])) is a literal in the reference itself: the expected output of the
+  gnark Poseidon2-KoalaBear circuit test, crates/recursion/gnark-ffi/go/main.go:258-275
+  (``expectedOutput`` of TestPoseidonKoalaBear2, main.go:237-275, input all zeros).  The strongest pin: reference-held
+  data, independent of any build done here.
+- ``perm_0_to_15`` and ``perm_ones`` are the values SURVEY.md §8c recorded from a build of the
+  reference's C++ Poseidon2 (crates/recursion/core/include/poseidon2_wide.hpp populate_perm) in the
+  survey container.  That build needed a stand-in for a cbindgen-generated header, so on its own it
+  pins nothing; the vectors agree with an independent restatement from RC_16_30_U32
+  (crates/primitives/src/lib.rs:563) and INTERNAL_DIAG_MONTY_16
+  (crates/core/machine/src/operations/poseidon2/air.rs:12-29), and with perm_zeros through the same
+  code.
+
+The values are copied here verbatim; this script only re-serialises them.
 """
 import json, os
 

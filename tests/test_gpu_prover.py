@@ -181,3 +181,21 @@ def test_pinned_host_traces(dev, zero_copy, monkeypatch):
     p = gpu.prove_shard({k: h.array for k, h in held.items()}, pvs)
     rc, ref = cpu.prove(traces, pvs)
     assert rc == 0 and p == ref
+
+
+def test_commit_through_machine_handle(dev):
+    """zkm_commit_machine (no proving key) + zkm_open(key) gives the key-committed bytes; a shard
+    committed under another machine is refused by open (ZKM_ERR_ARG), not proven against the key."""
+    from zkmips_amd import mips_alu as A
+    from zkmips_amd.prover import MachineHandle
+    gpu, cpu, traces, pvs = provers(dev, 1 << 10, seed=9)
+    mh = MachineHandle(gpu.machine, num_queries=16)
+    data = mh.commit(dev, traces, pvs)
+    proof = gpu.open(data, gpu.base_challenger())
+    assert proof == gpu.prove_shard(traces, pvs)
+    other = MachineHandle(A.alu_machine(), num_queries=16)
+    am, aprep, atr, apv = A.alu_shard(64, 64, seed=1)
+    bad = other.commit(dev, atr, apv)
+    from zkmips_amd._lib import ZkmError
+    with pytest.raises(ZkmError, match="different machine"):
+        gpu.open(bad, gpu.base_challenger())

@@ -1,7 +1,8 @@
 """CPU oracle checks (no GPU): the oracle is pinned before anything is compared against it.
 
-* Poseidon2-16 against the known-answer vectors of the reference's C++ permutation
-  (tests/golden/poseidon2_kat.json).
+* Poseidon2-16 against the known-answer vectors (tests/golden/poseidon2_kat.json): perm([0;16]) is a
+  literal of the reference (crates/recursion/gnark-ffi/go/main.go:258-275); the other two were recorded
+  from the reference's C++ permutation.
 * Field / two-adic generator table against the chain SURVEY.md §8c records.
 * DFT / coset LDE / MMCS / challenger against small pure-Python restatements of the semantics
   the reference's verifier pins (crates/recursion/circuit/src/{fri.rs,challenger.rs,hash.rs}).

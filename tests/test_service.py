@@ -112,3 +112,89 @@ def test_prove_compress_shard_through_service(server):
     assert st == 200
     rc, ref = O.OracleProver(m, prep, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP).prove(tr, pv)
     assert rc == 0 and SV.decode_fields(body)[1] == ref
+
+
+class _FakeProver:
+    def __init__(self, blob, prep, nq, lb):
+        self.key = SV.prover_key(blob, prep, nq, lb)
+
+    def prove_shard(self, traces, pv):
+        return self.key
+
+
+def test_prover_cache_keyed_on_preprocessed_traces():
+    """Two programs of one machine (same blob, different preprocessed traces) get two proving keys;
+    the same program is set up once; the cache is LRU-bounded; a failed setup is not cached."""
+    svc = SV.ProverService(device_factory=lambda i: object(), max_provers=2,
+                           prover_factory=lambda d, b, p, nq, lb: _FakeProver(b, p, nq, lb))
+    m, prep, tr, pv = W.fib_shard(1 << 6, 3)
+    prep2 = {k: (None if v is None else (v + 1) % 0x7F000001) for k, v in prep.items()}
+    a = svc.prove_shard(SV.pack_shard(m.blob(), prep, tr, pv, num_queries=16))
+    b = svc.prove_shard(SV.pack_shard(m.blob(), prep2, tr, pv, num_queries=16))
+    assert a != b and svc.setups == 2
+    assert svc.prove_shard(SV.pack_shard(m.blob(), prep, tr, pv, num_queries=16)) == a and svc.setups == 2
+    c = svc.prove_shard(SV.pack_shard(m.blob(), prep, tr, pv, num_queries=8))  # FRI parameters are in the key
+    assert c not in (a, b) and svc.setups == 3 and len(svc._provers) == 2
+    svc.prove_shard(SV.pack_shard(m.blob(), prep2, tr, pv, num_queries=16))  # evicted (LRU) -> set up again
+    assert svc.setups == 4
+
+    def boom(*_):
+        raise RuntimeError("setup failed")
+    bad = SV.ProverService(device_factory=lambda i: object(), prover_factory=boom)
+    with pytest.raises(RuntimeError):
+        bad.prove_shard(SV.pack_shard(m.blob(), prep, tr, pv, num_queries=16))
+    assert bad.setups == 0 and not bad._pending
+
+
+def test_ready_not_blocked_by_a_setup(server):
+    """A slow setup (e.g. first-time hiprtc compilation) does not block the client's Ready polls."""
+    gate = threading.Event()
+
+    def slow(d, b, p, nq, lb):
+        gate.wait(30)
+        return _FakeProver(b, p, nq, lb)
+    svc = SV.ProverService(device_factory=lambda i: object(), prover_factory=slow)
+    srv = SV.serve("127.0.0.1", 0, service=svc)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    port = srv.server_address[1]
+    try:
+        m, prep, tr, pv = W.fib_shard(1 << 6, 3)
+        data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=16)
+        res = {}
+        t = threading.Thread(target=lambda: res.setdefault("r", post(port, "ProveShard", SV.encode_bytes_field(1, data))))
+        t.start()
+        st, _, body = post(port, "Ready", b"")
+        assert st == 200 and SV.decode_fields(body) == {1: 1} and not gate.is_set()
+        gate.set()
+        t.join(60)
+        assert res["r"][0] == 200
+    finally:
+        gate.set()
+        srv.shutdown()
+        srv.server_close()
+
+
+@pytest.mark.gpu
+def test_two_compress_programs_through_one_server(server):
+    """two recursion programs of the same machine sent to one server each prove against
+    their own preprocessed commitment (equal to a direct HipProver's bytes and the oracle's)."""
+    from tests import _oracle as O
+    from zkmips_amd import recursion as R
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    port = server()
+    blobs = []
+    for seed in (21, 22):
+        m, prep, tr, pv = R.shard(R.program_merkle_openings(6, 21, 8, seed=seed)[0])
+        blobs.append(m.blob().tobytes())
+        data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=R.COMPRESS_NUM_QUERIES,
+                             log_blowup=R.COMPRESS_LOG_BLOWUP)
+        st, _, body = post(port, "ProveShard", SV.encode_bytes_field(1, data))
+        assert st == 200, body
+        direct = HipProver(Device(0), m, prep, num_queries=R.COMPRESS_NUM_QUERIES,
+                           log_blowup=R.COMPRESS_LOG_BLOWUP).prove_shard(tr, pv)
+        rc, ref = O.OracleProver(m, prep, num_queries=R.COMPRESS_NUM_QUERIES,
+                                 log_blowup=R.COMPRESS_LOG_BLOWUP).prove(tr, pv)
+        assert rc == 0 and SV.decode_fields(body)[1] == direct == ref
+    assert blobs[0] == blobs[1]  # one machine, two programs

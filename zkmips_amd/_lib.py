@@ -73,6 +73,9 @@ def lib():
         L.zkm_pk_observe.argtypes = [vp, C.POINTER(ChallengerState)]
         L.zkm_commit.argtypes = [vp, vp, C.POINTER(Matrix), C.c_uint32, vp, C.c_uint32, C.POINTER(vp), vp]
         L.zkm_main_free.argtypes = [vp]
+        L.zkm_machine_new.argtypes = [vp, C.c_size_t, C.POINTER(Config), C.POINTER(vp)]
+        L.zkm_machine_free.argtypes = [vp]
+        L.zkm_commit_machine.argtypes = [vp, vp, C.POINTER(Matrix), C.c_uint32, vp, C.c_uint32, C.POINTER(vp), vp]
         L.zkm_open.argtypes = [vp, vp, vp, C.POINTER(ChallengerState), C.POINTER(C.POINTER(C.c_uint8)),
                                C.POINTER(C.c_uint64)]
         L.zkm_prove_shard.argtypes = [vp, vp, C.POINTER(Matrix), C.c_uint32, vp, C.c_uint32,

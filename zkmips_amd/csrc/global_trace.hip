@@ -515,31 +515,39 @@ extern "C" int zkm_global_events_to_trace(const zkm_global_lookup_event *events,
     }
     hipStream_t s = (hipStream_t)stream;
     uint32_t *d_pts = nullptr, *d_err = nullptr;
-    HIPCHK(hipMallocAsync((void **)&d_pts, (size_t)(n ? n : 1) * PW * 4, s));
-    HIPCHK(hipMallocAsync((void **)&d_err, 4, s));
-    HIPCHK(hipMemsetAsync(d_err, 0, 4, s));
-    hipLaunchKernelGGL(k_septic_init, dim3(1), dim3(64), 0, s);
-    HIPCHK(hipGetLastError());
-    if (n) {
-        const uint64_t want = (n + 255) / 256;
-        const uint32_t grid = (uint32_t)(want < 4096 ? want : 4096);
-        hipLaunchKernelGGL(k_global_lift, dim3(grid), dim3(256), 0, s, (const uint32_t *)events, n, trace, d_pts,
-                           byte_mult, d_err);
-        HIPCHK(hipGetLastError());
-    }
-    int rc = scan_points(d_pts, n, 1, s);
-    if (rc != ZKM_OK) return rc;
-    {
-        const uint64_t want = (height + 255) / 256;
-        const uint32_t grid = (uint32_t)(want < 4096 ? want : 4096);
-        hipLaunchKernelGGL(k_global_fill, dim3(grid), dim3(256), 0, s, trace, d_pts, n, height, final_digest, d_err);
-        HIPCHK(hipGetLastError());
-    }
+    // one exit path: every failure after the first allocation drains the stream (nothing queued may
+    // still write into `err` or the buffers) and frees what was allocated
+    int rc = ZKM_OK;
     uint32_t err = 0;
-    HIPCHK(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipFreeAsync(d_pts, s));
-    HIPCHK(hipFreeAsync(d_err, s));
-    HIPCHK(hipStreamSynchronize(s));
+    auto fail = [&](hipError_t e) {
+        if (e != hipSuccess && rc == ZKM_OK) {
+            g_last_error = std::string("zkm_global_events_to_trace: ") + hipGetErrorString(e);
+            rc = ZKM_ERR_HIP;
+        }
+        return rc != ZKM_OK;
+    };
+    if (!fail(hipMallocAsync((void **)&d_pts, (size_t)(n ? n : 1) * PW * 4, s)) &&
+        !fail(hipMallocAsync((void **)&d_err, 4, s)) && !fail(hipMemsetAsync(d_err, 0, 4, s))) {
+        hipLaunchKernelGGL(k_septic_init, dim3(1), dim3(64), 0, s);
+        if (!fail(hipGetLastError()) && n) {
+            const uint64_t want = (n + 255) / 256;
+            const uint32_t grid = (uint32_t)(want < 4096 ? want : 4096);
+            hipLaunchKernelGGL(k_global_lift, dim3(grid), dim3(256), 0, s, (const uint32_t *)events, n, trace, d_pts,
+                               byte_mult, d_err);
+            fail(hipGetLastError());
+        }
+        if (rc == ZKM_OK) rc = scan_points(d_pts, n, 1, s);
+        if (rc == ZKM_OK) {
+            const uint64_t want = (height + 255) / 256;
+            const uint32_t grid = (uint32_t)(want < 4096 ? want : 4096);
+            hipLaunchKernelGGL(k_global_fill, dim3(grid), dim3(256), 0, s, trace, d_pts, n, height, final_digest, d_err);
+            if (!fail(hipGetLastError())) fail(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, s));
+        }
+    }
+    if (d_pts) fail(hipFreeAsync(d_pts, s));  // stream-ordered: after every queued use
+    if (d_err) fail(hipFreeAsync(d_err, s));
+    if (fail(hipStreamSynchronize(s))) return rc;  // before `err` is read or leaves scope
+    if (rc != ZKM_OK) return rc;
     if (err) {
         g_last_error = std::string("zkm_global_events_to_trace: ") +
                        ((err & ERR_NO_LIFT) ? "a message has no curve point within 256 offsets; " : "") +

@@ -21,6 +21,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <future>
 #include <map>
@@ -384,11 +385,45 @@ void write_file_atomic(const std::string &dir, const std::string &name, const st
 
 std::vector<char> compile_source(const std::string &src, const std::string &name, const std::string &arch_name);
 
+// the hiprtc options compile_source passes (after --offload-arch); the cache key is derived from this
+// same list, so an option change can never load a code object built with the old options
+const char *const kJitOpts[] = {"-O3", "-std=c++17"};
+
+// everything besides the source that determines the code object: arch, options, hiprtc version
+std::string toolchain_id(const std::string &arch_name) {
+    int major = 0, minor = 0;
+    hiprtcVersion(&major, &minor);
+    std::string id = arch_name + "|hiprtc " + std::to_string(major) + "." + std::to_string(minor) + "|";
+    for (const char *o : kJitOpts) id += std::string(o) + "|";
+    return id;
+}
+
+// on-disk format: 8-byte magic, 8-byte FNV-1a of the code object, the code object; a file whose
+// magic or checksum does not match is a cache miss (recompiled and rewritten), never loaded
+const char kCoMagic[8] = {'Z', 'K', 'M', 'C', 'O', '2', 0, 0};
+
+bool read_cached_code(const std::string &path, std::vector<char> &code) {
+    std::vector<char> raw;
+    if (!read_file(path, raw) || raw.size() <= 16 || memcmp(raw.data(), kCoMagic, 8) != 0) return false;
+    uint64_t want;
+    memcpy(&want, raw.data() + 8, 8);
+    code.assign(raw.begin() + 16, raw.end());
+    return fnv1a(std::string(code.begin(), code.end())) == want;
+}
+
+void write_cached_code(const std::string &dir, const std::string &name, const std::vector<char> &code) {
+    std::vector<char> raw(kCoMagic, kCoMagic + 8);
+    const uint64_t h = fnv1a(std::string(code.begin(), code.end()));
+    raw.insert(raw.end(), (const char *)&h, (const char *)&h + 8);
+    raw.insert(raw.end(), code.begin(), code.end());
+    write_file_atomic(dir, name, raw);
+}
+
 }  // namespace
 
 std::vector<char> jit_chip_code(const ChipDesc &c, const std::string &arch_name) {
     const std::string src = chip_source(c);
-    const uint64_t key = fnv1a(src, fnv1a(arch_name + "|-O3|-std=c++17|"));
+    const uint64_t key = fnv1a(src, fnv1a(toolchain_id(arch_name)));
     {
         std::lock_guard<std::mutex> g(g_cache_mu);
         auto it = g_cache.find(key);
@@ -398,9 +433,9 @@ std::vector<char> jit_chip_code(const ChipDesc &c, const std::string &arch_name)
     snprintf(kname, sizeof kname, "%016llx", (unsigned long long)key);
     const std::string dir = cache_dir(), fname = c.name + "-" + arch_name + "-" + kname + ".co";
     std::vector<char> code;
-    if (dir.empty() || !read_file(dir + "/" + fname, code)) {
+    if (dir.empty() || !read_cached_code(dir + "/" + fname, code)) {
         code = compile_source(src, c.name, arch_name);
-        if (!dir.empty()) write_file_atomic(dir, fname, code);
+        if (!dir.empty()) write_cached_code(dir, fname, code);
     }
     std::lock_guard<std::mutex> g(g_cache_mu);
     g_cache[key] = code;
@@ -420,8 +455,9 @@ std::vector<char> compile_source(const std::string &src, const std::string &name
     if (hiprtcCreateProgram(&prog, src.c_str(), "quotient_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         throw HipError("hiprtcCreateProgram failed");
     std::string arch = "--offload-arch=" + arch_name;
-    const char *opts[] = {arch.c_str(), "-O3", "-std=c++17"};
-    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    std::vector<const char *> opts = {arch.c_str()};
+    for (const char *o : kJitOpts) opts.push_back(o);
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t ls = 0;
         hiprtcGetProgramLogSize(prog, &ls);

@@ -85,10 +85,27 @@ struct Challenger {
 };
 
 // ------------------------------------------------------------------ keys and shard data
+// identity of a machine layout for commit/open: the blob words and the blowup (what commit reads)
+static uint64_t machine_digest(const uint32_t *blob, size_t n, uint32_t log_blowup) {
+    uint64_t h = 1469598103934665603ull ^ log_blowup;
+    for (size_t i = 0; i < n; i++) h = (h ^ blob[i]) * 1099511628211ull;
+    return h;
+}
+
+// zkm_machine: what MachineProver::commit needs and nothing else (no preprocessed data), so a
+// caller whose commit receives no key (the trait's commit, prover.rs:111-115) does not have to
+// guess one; zkm_open checks that the committed data and the key describe the same machine.
+struct MachineHandle {
+    Machine m;
+    zkm_config_t cfg{};
+    uint64_t digest = 0;
+};
+
 struct Pk {
     int device = 0;
     Machine m;
     zkm_config_t cfg{};
+    uint64_t digest = 0;       // machine_digest of the blob it was set up from
     uint32_t commit[8];        // Montgomery
     uint32_t pc_start;         // Montgomery
     uint32_t gcs[14];          // Montgomery
@@ -110,6 +127,7 @@ struct Pk {
 };
 
 struct MainData {
+    uint64_t machine = 0;          // machine_digest of the machine it was committed under
     std::vector<int> chip;         // machine chip index, in commit order (height desc, name)
     std::vector<uint64_t> heights;
     std::vector<DBuf> store;       // one column-major natural buffer per height group
@@ -866,6 +884,7 @@ int zkm_setup(zkm_ctx *ctx, const uint32_t *blob, size_t nwords, const zkm_confi
     pk->device = c->device;
     pk->m = parse_machine(blob, nwords);
     pk->cfg = *cfg;
+    pk->digest = machine_digest(blob, nwords, cfg->log_blowup);
     pk->pc_start = to_mont(pc_start);
     for (int k = 0; k < 14; k++) pk->gcs[k] = to_mont(gcs[k]);
     ARG_CHECK(nprep == pk->m.chips.size(), "one preprocessed matrix slot per machine chip");
@@ -945,23 +964,27 @@ int zkm_pk_observe(const zkm_pk *p, zkm_challenger_t *c) {
     GUARD_END
 }
 
-int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32_t ntraces, const uint32_t *pv,
-               uint32_t npv, zkm_main **out, uint32_t commit_out[8]) {
+}  // extern "C"
+
+// MachineProver::commit against a machine layout (from a key or a zkm_machine handle)
+static int commit_impl(zkm_ctx *ctx, const Machine &mach, uint32_t log_blowup, uint64_t digest,
+                       const zkm_matrix_t *traces, uint32_t ntraces, const uint32_t *pv, uint32_t npv,
+                       zkm_main **out, uint32_t commit_out[8]) {
     GUARD_BEGIN
-    ARG_CHECK(ctx && p && traces && ntraces && out && commit_out && (pv || !npv), "null argument");
+    ARG_CHECK(ctx && traces && ntraces && out && commit_out && (pv || !npv), "null argument");
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
-    const Pk *pk = reinterpret_cast<const Pk *>(p);
     HIP_CHECK(hipSetDevice(c->device));
     StreamLease L(c);
     auto md = std::make_unique<MainData>();
+    md->machine = digest;
     std::vector<uint64_t> hs;
     std::vector<std::string> names;
     std::vector<int> chip;
     for (uint32_t i = 0; i < ntraces; i++) {
         ARG_CHECK(traces[i].name, "trace without a chip name");
-        const int ci = pk->m.index_of(traces[i].name);
+        const int ci = mach.index_of(traces[i].name);
         ARG_CHECK(ci >= 0, std::string("unknown chip ") + traces[i].name);
-        ARG_CHECK(traces[i].width == (uint64_t)pk->m.chips[ci].main_w, "main trace width mismatch");
+        ARG_CHECK(traces[i].width == (uint64_t)mach.chips[ci].main_w, "main trace width mismatch");
         ARG_CHECK(traces[i].height >= 16 && (traces[i].height & (traces[i].height - 1)) == 0,
                   "trace heights must be powers of two >= 16");
         hs.push_back(traces[i].height);
@@ -990,7 +1013,7 @@ int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32
             ws.push_back(traces[o].width);
             off += traces[o].width;
         }
-        for (const DMat &v : lde_group(*c, md->tree, base, N, ws, to_mont(GENERATOR), false, (int)pk->cfg.log_blowup, L.s))
+        for (const DMat &v : lde_group(*c, md->tree, base, N, ws, to_mont(GENERATOR), false, (int)log_blowup, L.s))
             md->tree.mats.push_back(v);
     }
     tree_build(md->tree, L.s);
@@ -999,6 +1022,37 @@ int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32
     *out = reinterpret_cast<zkm_main *>(md.release());
     return ZKM_OK;
     GUARD_END
+}
+
+extern "C" {
+
+int zkm_commit(zkm_ctx *ctx, const zkm_pk *p, const zkm_matrix_t *traces, uint32_t ntraces, const uint32_t *pv,
+               uint32_t npv, zkm_main **out, uint32_t commit_out[8]) {
+    if (!p) { g_last_error = "null argument"; return ZKM_ERR_ARG; }
+    const Pk *pk = reinterpret_cast<const Pk *>(p);
+    return commit_impl(ctx, pk->m, pk->cfg.log_blowup, pk->digest, traces, ntraces, pv, npv, out, commit_out);
+}
+
+int zkm_machine_new(const uint32_t *blob, size_t nwords, const zkm_config_t *cfg, zkm_machine **out) {
+    GUARD_BEGIN
+    ARG_CHECK(blob && cfg && out, "null argument");
+    ARG_CHECK(cfg->log_blowup == 1 || cfg->log_blowup == 2, "log_blowup must be 1 or 2");
+    auto mh = std::make_unique<MachineHandle>();
+    mh->m = parse_machine(blob, nwords);
+    mh->cfg = *cfg;
+    mh->digest = machine_digest(blob, nwords, cfg->log_blowup);
+    *out = reinterpret_cast<zkm_machine *>(mh.release());
+    return ZKM_OK;
+    GUARD_END
+}
+
+void zkm_machine_free(zkm_machine *m) { delete reinterpret_cast<MachineHandle *>(m); }
+
+int zkm_commit_machine(zkm_ctx *ctx, const zkm_machine *m, const zkm_matrix_t *traces, uint32_t ntraces,
+                       const uint32_t *pv, uint32_t npv, zkm_main **out, uint32_t commit_out[8]) {
+    if (!m) { g_last_error = "null argument"; return ZKM_ERR_ARG; }
+    const MachineHandle *mh = reinterpret_cast<const MachineHandle *>(m);
+    return commit_impl(ctx, mh->m, mh->cfg.log_blowup, mh->digest, traces, ntraces, pv, npv, out, commit_out);
 }
 
 void zkm_main_free(zkm_main *m) {
@@ -1013,6 +1067,7 @@ int zkm_open(zkm_ctx *ctx, const zkm_pk *p, zkm_main *mainp, zkm_challenger_t *c
     ARG_CHECK(ctx && p && mainp && chs && proof_out && proof_len, "null argument");
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
     const Pk *pk = reinterpret_cast<const Pk *>(p);
+    ARG_CHECK(md->machine == pk->digest, "zkm_open: the shard was committed under a different machine than the key's");
     HIP_CHECK(hipSetDevice(c->device));
     StreamLease L(c);
     Challenger ch;

@@ -90,6 +90,35 @@ class _BlobMachine:
         return self._blob
 
 
+class MachineHandle:
+    """A key-free machine layout for commit (zkm_machine_new / zkm_commit_machine): the reference's
+    trait commit receives no proving key (prover.rs:111-115), and commit reads only chip names, main
+    widths and the blowup.  zkm_open checks the shard against the key's machine."""
+
+    def __init__(self, machine, log_blowup: int = 1, num_queries: int = 84, pow_bits: int = 16):
+        self.blob = as_u32(machine.blob() if hasattr(machine, "blob") else machine)
+        self.cfg = Config(num_queries, pow_bits, log_blowup, 0)
+        self.h = C.c_void_p()
+        check(lib().zkm_machine_new(self.blob.ctypes.data, self.blob.size, C.byref(self.cfg), C.byref(self.h)),
+              "zkm_machine_new")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().zkm_machine_free(self.h)
+            self.h = None
+
+    def commit(self, device: Device, traces: Dict[str, np.ndarray], public_values: np.ndarray,
+               montgomery_input: bool = False) -> "ShardMainData":
+        keep: list = []
+        arr = (Matrix * len(traces))(*[matrix(t, n, montgomery_input, keep) for n, t in traces.items()])
+        pv = as_u32(public_values)
+        h = C.c_void_p()
+        root = np.zeros(8, np.uint32)
+        check(lib().zkm_commit_machine(device.h, self.h, arr, len(traces), pv.ctypes.data, pv.size, C.byref(h),
+                                       root.ctypes.data), "zkm_commit_machine")
+        return ShardMainData(h, root)
+
+
 class HipProver:
     """MI355X drop-in for CpuProver on one GPU."""
 

@@ -11,7 +11,8 @@ types of api.proto (every request/response is one `bytes` field, or `bool ready`
 * ``ProveShard`` (an extension, not in api.proto) — one shard through zkm_prove_shard: `data` is an
                  .npz archive (numpy, no pickles) with `machine_blob`, `public_values`, `num_queries`,
                  optional `log_blowup`, and `prep/<chip>` / `trace/<chip>` arrays; `result` is the
-                 serialized ShardProof.  A prover per machine blob is kept (setup once).
+                 serialized ShardProof.  A prover per (machine blob, FRI parameters, preprocessed
+                 traces) is kept, LRU-bounded (setup once per program).
 * ``Setup``, ``ProveCore``, ``ProveCoreStateless``, ``Compress``, ``Shrink``, ``Wrap`` — Twirp
                  `unimplemented`: their payloads are bincode `ZKMStdin` / ELF / recursion proofs
                  (lib.rs:57-123), which need the MIPS executor and the recursion stack, outside the
@@ -138,18 +139,54 @@ class TwirpError(Exception):
         self.code, self.msg = code, msg
 
 
-class ProverService:
-    """The method implementations; transport-independent (the HTTP handler below calls `call`)."""
+def prover_key(blob, prep: dict, num_queries: int, log_blowup: int) -> bytes:
+    """Identity of a proving key: the machine blob, the FRI parameters AND the preprocessed traces.
+    A recursion (compress) program lives in its chips' preprocessed columns, so two programs of one
+    machine need two keys (the reference sets each compress program up anew, prover/src/lib.rs:807)."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(np.asarray(blob, np.uint32).tobytes())
+    h.update(np.asarray([num_queries, log_blowup], np.uint64).tobytes())
+    for name in sorted(k for k, v in prep.items() if v is not None):
+        a = np.ascontiguousarray(np.asarray(prep[name], np.uint32))
+        h.update(name.encode() + b"\0" + np.asarray(a.shape, np.uint64).tobytes())
+        h.update(a.tobytes())
+    return h.digest()
 
-    def __init__(self, device: int = 0, device_factory: Optional[Callable] = None):
+
+class _Pending:
+    """A proving key being set up: requests for the same key wait on it, others go ahead."""
+
+    def __init__(self):
+        self.done = threading.Event()
+        self.prover = None
+        self.error: Optional[BaseException] = None
+
+
+class ProverService:
+    """The method implementations; transport-independent (the HTTP handler below calls `call`).
+
+    Proving keys are cached per `prover_key` (machine, FRI parameters, preprocessed traces), at most
+    `max_provers` of them (least recently used evicted; each holds a device LDE + Merkle tree).  A key
+    is built outside the cache lock, so `Ready` polls and requests for other keys are not serialised
+    behind one setup (which may include minutes of first-time hiprtc compilation)."""
+
+    def __init__(self, device: int = 0, device_factory: Optional[Callable] = None,
+                 prover_factory: Optional[Callable] = None, max_provers: int = 8):
+        from collections import OrderedDict
         self.device_index = device
         self._device_factory = device_factory
+        self._prover_factory = prover_factory
+        self.max_provers = max(1, max_provers)
         self._dev = None
-        self._provers: Dict[Tuple[bytes, int, int], object] = {}
+        self._provers: "OrderedDict[bytes, object]" = OrderedDict()
+        self._pending: Dict[bytes, _Pending] = {}
+        self._dev_lock = threading.Lock()
         self._lock = threading.Lock()
+        self.setups = 0  # proving keys built (tests check the cache behaviour)
 
     def _device(self):
-        with self._lock:
+        with self._dev_lock:
             if self._dev is None:
                 if self._device_factory is not None:
                     self._dev = self._device_factory(self.device_index)
@@ -157,6 +194,46 @@ class ProverService:
                     from ._lib import Device
                     self._dev = Device(self.device_index)
             return self._dev
+
+    def _build(self, dev, blob, prep, nq, lb):
+        if self._prover_factory is not None:
+            return self._prover_factory(dev, blob, prep, nq, lb)
+        from .prover import HipProver
+        return HipProver.from_blob(dev, blob, prep, num_queries=nq, log_blowup=lb)
+
+    def get_prover(self, blob, prep: dict, nq: int, lb: int):
+        """The cached prover of (blob, prep, nq, lb), set up on first use."""
+        key = prover_key(blob, prep, nq, lb)
+        dev = self._device()
+        with self._lock:
+            p = self._provers.get(key)
+            if p is not None:
+                self._provers.move_to_end(key)
+                return p
+            pend = self._pending.get(key)
+            owner = pend is None
+            if owner:
+                pend = self._pending[key] = _Pending()
+        if not owner:
+            pend.done.wait()
+            if pend.error is not None:
+                raise pend.error
+            return pend.prover
+        try:
+            pend.prover = self._build(dev, blob, prep, nq, lb)
+        except BaseException as e:
+            pend.error = e
+            raise
+        finally:
+            with self._lock:
+                self._pending.pop(key, None)
+                if pend.prover is not None:
+                    self.setups += 1
+                    self._provers[key] = pend.prover
+                    while len(self._provers) > self.max_provers:
+                        self._provers.popitem(last=False)
+            pend.done.set()
+        return pend.prover
 
     def ready(self) -> bool:
         try:
@@ -166,20 +243,11 @@ class ProverService:
             return False
 
     def prove_shard(self, data: bytes) -> bytes:
-        from .machine import MachineDesc  # noqa: F401  (the blob is self-describing)
-        from .prover import HipProver
         try:
             blob, prep, traces, pv, nq, lb = unpack_shard(data)
         except Exception as e:
             raise TwirpError("invalid_argument", f"ProveShard payload: {e}")
-        dev = self._device()
-        key = (blob.tobytes(), nq, lb)
-        with self._lock:
-            prover = self._provers.get(key)
-            if prover is None:
-                prover = HipProver.from_blob(dev, blob, prep, num_queries=nq, log_blowup=lb)
-                self._provers[key] = prover
-        return prover.prove_shard(traces, pv)
+        return self.get_prover(blob, prep, nq, lb).prove_shard(traces, pv)
 
     def call(self, method: str, payload: Dict[int, object]) -> Dict[str, object]:
         if method == "Ready":
