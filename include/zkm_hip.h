@@ -164,7 +164,13 @@ size_t zkm_profile_dump(char *buf, size_t len);
  *       kind (LookupKind), scope (0 Local, 1 Global), num_values, VPC x num_values, VPC multiplicity
  *       VPC = num_terms, (col, weight) x num_terms, constant;  col bit31 = main, else preprocessed.
  *   Opcodes: 0 END, 1 MAIN_L c, 2 MAIN_N c, 3 PREP_L c, 4 PREP_N c, 5 CONST v, 6 PV i, 7 IS_FIRST,
- *            8 IS_LAST, 9 IS_TRANSITION, 10 ADD, 11 SUB, 12 MUL, 13 NEG, 14 EMIT (assert_zero).
+ *            8 IS_LAST, 9 IS_TRANSITION, 10 ADD, 11 SUB, 12 MUL, 13 NEG, 14 EMIT (assert_zero),
+ *            15 LET s (pop the top into value slot s), 16 GET s (push slot s).
+ *   Shared subexpressions (the Rc-shared nodes of Plonky3's SymbolicExpression DAG, which
+ *   get_symbolic_constraints returns) are defined once with LET, slots numbered 0, 1, 2, ... in
+ *   order of definition, and read with GET after their definition; this keeps a chip's program
+ *   linear in the size of its DAG (chained Poseidon2 layers, septic-extension products).  The JIT
+ *   keeps slots in registers; the ZKM_NO_JIT interpreter in global scratch.
  */
 
 #ifdef __cplusplus

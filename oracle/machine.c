@@ -47,6 +47,19 @@ int orc_machine_parse(orc_machine_t *m, const uint32_t *w, size_t n) {
         ch->code_len = (int)rd(&r);
         ch->code = (uint32_t *)calloc(ch->code_len + 1, sizeof(uint32_t));
         for (int i = 0; i < ch->code_len; i++) ch->code[i] = rd(&r);
+        ch->n_slots = 0;
+        for (int pc = 0; pc < ch->code_len;) {
+            uint32_t op = ch->code[pc++];
+            if (op == OP_LET || op == OP_GET) {
+                if (pc >= ch->code_len || ch->code[pc] >= (1u << 24)) return -5;
+                if (op == OP_LET && (int)ch->code[pc] + 1 > ch->n_slots) ch->n_slots = (int)ch->code[pc] + 1;
+                if (op == OP_GET && (int)ch->code[pc] >= ch->n_slots) return -5; /* use before definition */
+                pc++;
+            } else if (op == OP_MAIN_L || op == OP_MAIN_N || op == OP_PREP_L || op == OP_PREP_N || op == OP_CONST ||
+                       op == OP_PV) {
+                pc++;
+            }
+        }
         ch->nsends = (int)rd(&r);
         ch->nrecvs = (int)rd(&r);
         int total = ch->nsends + ch->nrecvs;

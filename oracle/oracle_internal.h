@@ -65,7 +65,8 @@ kb_t orc_chal_grind(orc_chal_t *c, int bits);
 
 /* -------------------------------------------------------------- machine.c */
 enum { OP_END = 0, OP_MAIN_L, OP_MAIN_N, OP_PREP_L, OP_PREP_N, OP_CONST, OP_PV,
-       OP_IS_FIRST, OP_IS_LAST, OP_IS_TRANS, OP_ADD, OP_SUB, OP_MUL, OP_NEG, OP_EMIT };
+       OP_IS_FIRST, OP_IS_LAST, OP_IS_TRANS, OP_ADD, OP_SUB, OP_MUL, OP_NEG, OP_EMIT,
+       OP_LET, OP_GET /* shared subexpressions: LET s pops into value slot s, GET s pushes it */ };
 
 typedef struct { int nterms; uint32_t *cols; kb_t *weights; kb_t constant; } orc_vpc_t;
 typedef struct { uint32_t kind, scope; int nvalues; orc_vpc_t *values; orc_vpc_t mult; int is_send; } orc_lookup_t;
@@ -74,6 +75,7 @@ typedef struct {
     char name[64];
     int prep_width, main_width, commit_scope, local_only, log_qd, num_main_constraints;
     int code_len; uint32_t *code;
+    int n_slots; /* 1 + the largest LET slot (0 without shared subexpressions) */
     int nlocal; orc_lookup_t *local; /* local-scope lookups: sends then receives (stable) */
     int nsends, nrecvs;
     int perm_width_ef; /* 0 if no local lookups, else ceil(nlocal/batch)+1 */

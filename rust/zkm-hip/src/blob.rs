@@ -31,51 +31,127 @@ const OP_MUL: u32 = 12;
 const OP_NEG: u32 = 13;
 const OP_EMIT: u32 = 14;
 
-/// Postfix code of one constraint.  Shared subexpressions of the Rc DAG are emitted once per use
-/// (the device program has no registers to keep them in); `cache` avoids re-walking them.
-fn lower<F: PrimeField32>(e: &SymbolicExpression<F>, out: &mut Vec<u32>, cache: &mut HashMap<usize, Vec<u32>>) {
-    let key = e as *const _ as usize;
-    if let Some(code) = cache.get(&key) {
-        out.extend_from_slice(code);
-        return;
-    }
-    let start = out.len();
-    match e {
-        SymbolicExpression::Variable(v) => match v.entry {
-            Entry::Main { offset } => out.extend([if offset == 0 { OP_MAIN_L } else { OP_MAIN_N }, v.index as u32]),
-            Entry::Preprocessed { offset } => {
-                out.extend([if offset == 0 { OP_PREP_L } else { OP_PREP_N }, v.index as u32])
-            }
-            Entry::Public => out.extend([OP_PV, v.index as u32]),
-            Entry::Permutation { .. } | Entry::Challenge => {
-                panic!("main-trace constraints reference no permutation columns or challenges")
-            }
-        },
-        SymbolicExpression::IsFirstRow => out.push(OP_IS_FIRST),
-        SymbolicExpression::IsLastRow => out.push(OP_IS_LAST),
-        SymbolicExpression::IsTransition => out.push(OP_IS_TRANS),
-        SymbolicExpression::Constant(c) => out.extend([OP_CONST, c.as_canonical_u32()]),
-        SymbolicExpression::Add { x, y, .. } => bin(x, y, OP_ADD, out, cache),
-        SymbolicExpression::Sub { x, y, .. } => bin(x, y, OP_SUB, out, cache),
-        SymbolicExpression::Mul { x, y, .. } => bin(x, y, OP_MUL, out, cache),
-        SymbolicExpression::Neg { x, .. } => {
-            lower(x, out, cache);
-            out.push(OP_NEG);
-        }
-    }
-    cache.insert(key, out[start..].to_vec());
+const OP_LET: u32 = 15;
+const OP_GET: u32 = 16;
+
+type Node<F> = SymbolicExpression<F>;
+
+fn key<F>(e: &Node<F>) -> usize {
+    e as *const _ as usize
 }
 
-fn bin<F: PrimeField32>(
-    x: &Rc<SymbolicExpression<F>>,
-    y: &Rc<SymbolicExpression<F>>,
-    op: u32,
-    out: &mut Vec<u32>,
-    cache: &mut HashMap<usize, Vec<u32>>,
-) {
-    lower(x, out, cache);
-    lower(y, out, cache);
-    out.push(op);
+fn children<F>(e: &Node<F>) -> Vec<&Node<F>> {
+    match e {
+        SymbolicExpression::Add { x, y, .. } | SymbolicExpression::Sub { x, y, .. } | SymbolicExpression::Mul { x, y, .. } => {
+            vec![x.as_ref(), y.as_ref()]
+        }
+        SymbolicExpression::Neg { x, .. } => vec![x.as_ref()],
+        _ => vec![],
+    }
+}
+
+/// Parent references of every node of the constraints' DAG (an Rc'd node cloned into several parents
+/// is one node with several references).
+fn count_refs<F>(e: &Node<F>, refs: &mut HashMap<usize, u32>) {
+    let n = refs.entry(key(e)).or_insert(0);
+    *n += 1;
+    if *n == 1 {
+        for c in children(e) {
+            count_refs(c, refs);
+        }
+    }
+}
+
+/// The chip program: every interior node referenced more than once becomes a shared subexpression,
+/// defined once (its code, then LET slot) in post-order -- slots 0, 1, 2, ... before their first
+/// use -- and read with GET wherever it is used; then one EMIT per constraint.  Linear in the size
+/// of the DAG, where re-emitting shared nodes per use is exponential in the depth of chained layers
+/// (e.g. Poseidon2's 13 internal rounds).
+struct Lowering {
+    refs: HashMap<usize, u32>,
+    slot: HashMap<usize, u32>,
+    defs: Vec<u32>,
+}
+
+impl Lowering {
+    fn shared<F>(&self, e: &Node<F>) -> bool {
+        !children(e).is_empty() && self.refs.get(&key(e)).copied().unwrap_or(0) > 1
+    }
+
+    /// Defines the shared nodes below (and including) `e`, children first.
+    fn define<F: PrimeField32>(&mut self, e: &Node<F>) {
+        if self.slot.contains_key(&key(e)) {
+            return;
+        }
+        for c in children(e) {
+            self.define(c);
+        }
+        if self.shared(e) {
+            let mut code = Vec::new();
+            self.emit(e, &mut code, true);
+            let s = self.slot.len() as u32;
+            code.extend([OP_LET, s]);
+            self.defs.extend(code);
+            self.slot.insert(key(e), s);
+        }
+    }
+
+    /// Postfix code of `e`, shared nodes as GET (except `e` itself when it is being defined).
+    fn emit<F: PrimeField32>(&self, e: &Node<F>, out: &mut Vec<u32>, top: bool) {
+        if !top {
+            if let Some(&s) = self.slot.get(&key(e)) {
+                out.extend([OP_GET, s]);
+                return;
+            }
+        }
+        match e {
+            SymbolicExpression::Variable(v) => match v.entry {
+                Entry::Main { offset } => out.extend([if offset == 0 { OP_MAIN_L } else { OP_MAIN_N }, v.index as u32]),
+                Entry::Preprocessed { offset } => {
+                    out.extend([if offset == 0 { OP_PREP_L } else { OP_PREP_N }, v.index as u32])
+                }
+                Entry::Public => out.extend([OP_PV, v.index as u32]),
+                Entry::Permutation { .. } | Entry::Challenge => {
+                    panic!("main-trace constraints reference no permutation columns or challenges")
+                }
+            },
+            SymbolicExpression::IsFirstRow => out.push(OP_IS_FIRST),
+            SymbolicExpression::IsLastRow => out.push(OP_IS_LAST),
+            SymbolicExpression::IsTransition => out.push(OP_IS_TRANS),
+            SymbolicExpression::Constant(c) => out.extend([OP_CONST, c.as_canonical_u32()]),
+            SymbolicExpression::Add { x, y, .. } => self.bin(x, y, OP_ADD, out),
+            SymbolicExpression::Sub { x, y, .. } => self.bin(x, y, OP_SUB, out),
+            SymbolicExpression::Mul { x, y, .. } => self.bin(x, y, OP_MUL, out),
+            SymbolicExpression::Neg { x, .. } => {
+                self.emit(x, out, false);
+                out.push(OP_NEG);
+            }
+        }
+    }
+
+    fn bin<F: PrimeField32>(&self, x: &Rc<Node<F>>, y: &Rc<Node<F>>, op: u32, out: &mut Vec<u32>) {
+        self.emit(x, out, false);
+        self.emit(y, out, false);
+        out.push(op);
+    }
+}
+
+fn chip_program<F: PrimeField32>(constraints: &[Node<F>]) -> Vec<u32> {
+    let mut l = Lowering { refs: HashMap::new(), slot: HashMap::new(), defs: Vec::new() };
+    for c in constraints {
+        count_refs(c, &mut l.refs);
+    }
+    for c in constraints {
+        for ch in children(c) {
+            l.define(ch);
+        }
+    }
+    let mut code = std::mem::take(&mut l.defs);
+    for c in constraints {
+        l.emit(c, &mut code, true);
+        code.push(OP_EMIT);
+    }
+    code
 }
 
 /// VirtualPairCol -> [num_terms, (col | main bit31, weight)..., constant], recovered through the
@@ -138,12 +214,7 @@ where
     let prep_w = chip.preprocessed_width();
     let main_w = chip.width();
     let constraints = get_symbolic_constraints(&chip.air, prep_w, PROOF_MAX_NUM_PVS);
-    let mut code = Vec::new();
-    let mut cache = HashMap::new();
-    for c in &constraints {
-        lower(c, &mut code, &mut cache);
-        code.push(OP_EMIT);
-    }
+    let code = chip_program(&constraints);
     out.extend([
         prep_w as u32,
         main_w as u32,

@@ -19,7 +19,10 @@ from zkmips_amd import machine as M
 P = M.P
 
 
-def _eval(code, main, prep, pvs, n):
+def _eval(code, main, prep, pvs, n, memo=None):
+    """Value of a builder expression's code on every row; shared definitions (OP_REF) are evaluated
+    once per `memo` (one chip)."""
+    memo = {} if memo is None else memo
     st = []
     i = 0
     nxt = lambda a: np.roll(a, -1, axis=0)
@@ -50,6 +53,12 @@ def _eval(code, main, prep, pvs, n):
             st.append((a + b) % P if op == M.OP_ADD else (a - b) % P if op == M.OP_SUB else (a * b) % P)
         elif op == M.OP_NEG:
             st.append((-st.pop()) % P)
+        elif op == M.OP_REF:
+            g = code[i]
+            i += 1
+            if g not in memo:
+                memo[g] = _eval(M._SHARED[g], main, prep, pvs, n, memo)
+            st.append(memo[g])
         else:
             raise ValueError(op)
     assert len(st) == 1
@@ -73,8 +82,9 @@ def check(machine, prep_traces, traces, pvs, max_report=5):
         main = traces[ch.name]
         n = main.shape[0]
         prep = prep_traces.get(ch.name, np.zeros((n, 0), np.uint32))
+        memo = {}
         for k, c in enumerate(ch.constraints):
-            r = _eval(c.code, main, prep, pvs, n)
+            r = _eval(c.code, main, prep, pvs, n, memo)
             nz = np.nonzero(r)[0]
             if len(nz):
                 bad.append((ch.name, k, nz[:max_report].tolist(), len(nz)))

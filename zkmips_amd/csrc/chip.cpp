@@ -70,6 +70,13 @@ Machine parse_machine(const uint32_t *w, size_t n) {
             case OP_ADD: case OP_SUB: case OP_MUL: ARG_CHECK(sp >= 2, "stack underflow"); sp--; break;
             case OP_NEG: ARG_CHECK(sp >= 1, "stack underflow"); break;
             case OP_EMIT: ARG_CHECK(sp >= 1, "stack underflow"); sp--; emits++; break;
+            case OP_LET:
+                ARG_CHECK(pc < c.code.size() && sp >= 1, "LET operand / stack underflow");
+                ARG_CHECK(c.code[pc] == (uint32_t)c.n_slots, "LET slots must be defined in order 0, 1, 2, ...");
+                c.n_slots++; pc++; sp--; break;
+            case OP_GET:
+                ARG_CHECK(pc < c.code.size() && (int)c.code[pc] < c.n_slots, "GET of an undefined slot");
+                pc++; sp++; break;
             default: ARG_CHECK(false, "bad opcode");
             }
             c.max_stack = std::max(c.max_stack, sp);
@@ -117,7 +124,8 @@ std::vector<uint32_t> flatten_chip(const ChipDesc &c) {
         uint32_t op = c.code[pc++];
         out.push_back(op);
         if (op == OP_CONST) out.push_back(kb::to_mont(c.code[pc++]));
-        else if (op == OP_MAIN_L || op == OP_MAIN_N || op == OP_PREP_L || op == OP_PREP_N || op == OP_PV)
+        else if (op == OP_MAIN_L || op == OP_MAIN_N || op == OP_PREP_L || op == OP_PREP_N || op == OP_PV ||
+                 op == OP_LET || op == OP_GET)
             out.push_back(c.code[pc++]);
     }
     out[0] = (uint32_t)(out.size() - 4);

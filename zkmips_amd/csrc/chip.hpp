@@ -11,7 +11,8 @@ namespace zkm {
 
 enum Op : uint32_t {
     OP_END = 0, OP_MAIN_L, OP_MAIN_N, OP_PREP_L, OP_PREP_N, OP_CONST, OP_PV,
-    OP_IS_FIRST, OP_IS_LAST, OP_IS_TRANS, OP_ADD, OP_SUB, OP_MUL, OP_NEG, OP_EMIT
+    OP_IS_FIRST, OP_IS_LAST, OP_IS_TRANS, OP_ADD, OP_SUB, OP_MUL, OP_NEG, OP_EMIT,
+    OP_LET, OP_GET  // shared subexpressions: LET s pops the top into value slot s, GET s pushes it
 };
 
 struct VPC {
@@ -33,6 +34,7 @@ struct ChipDesc {
     int perm_w = 0;                    // EF columns
     int n_constraints = 0;
     int max_stack = 0;
+    int n_slots = 0;                   // value slots of shared subexpressions (1 + largest LET slot)
 };
 struct Machine {
     int num_pv = 0;

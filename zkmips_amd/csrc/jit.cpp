@@ -136,6 +136,7 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
     };
     // ---- AIR program -> straight-line code ----
     std::vector<std::string> st;
+    std::vector<std::string> slot;  // shared subexpressions: slot -> the variable holding its value
     for (size_t pc = 0; pc < c.code.size();) {
         const uint32_t op = c.code[pc++];
         switch (op) {
@@ -169,6 +170,13 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
             emit_base(a);
             break;
         }
+        case OP_LET: {  // the value is already a named SSA variable; bind the slot to it
+            pc++;
+            slot.push_back(st.back());
+            st.pop_back();
+            break;
+        }
+        case OP_GET: st.push_back(slot.at(c.code[pc++])); break;
         default: throw ArgError("bad opcode in JIT");
         }
     }

@@ -174,10 +174,12 @@ static constexpr int QSTACK = 24;
 
 __global__ __launch_bounds__(NT) void k_quotient(QuotArgs a) {
     extern __shared__ uint32_t lds_stack[];  // [wave][depth][64]
-    const uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    const uint64_t tw_ = (uint64_t)blockIdx.x * NT + threadIdx.x;  // row within the window
+    const uint64_t t = a.t0 + tw_;
     const int lane = threadIdx.x & 63;
     uint32_t *stk = lds_stack + (threadIdx.x >> 6) * QSTACK * 64 + lane;
-    if (t >= a.q) return;  // q is a multiple of 64 (>= 16 rows * 2 ... checked on host)
+    if (tw_ >= a.slot_rows || t >= a.q) return;  // q is a multiple of 64 (>= 16 rows * 2 ... checked on host)
+    uint32_t *slots = a.slots + tw_;
     const uint64_t ldm = a.ld;  // LDE height (column stride)
     const uint64_t rl = t;
     const uint64_t k = rev_bits((uint32_t)t, a.log_q);
@@ -238,6 +240,12 @@ __global__ __launch_bounds__(NT) void k_quotient(QuotArgs a) {
             if (sp) { sp--; top = stk[sp * 64]; } else has = false;
             break;
         }
+        case 15: {  // LET s: pop into slot s
+            slots[(uint64_t)code[pc++] * a.slot_rows] = top;
+            if (sp) { sp--; top = stk[sp * 64]; } else has = false;
+            break;
+        }
+        case 16: { uint32_t sl = code[pc++]; PUSH(slots[(uint64_t)sl * a.slot_rows]); break; }
         default: break;
         }
     }
@@ -305,10 +313,29 @@ __global__ __launch_bounds__(NT) void k_quotient(QuotArgs a) {
     for (int e = 0; e < 4; e++) a.chunks[c * a.cstride + e * a.n + pos] = q.c[e];
 }
 
-void launch_quotient(const QuotArgs &a, hipStream_t s) {
+void launch_quotient(const QuotArgs &a0, hipStream_t s) {
     const size_t lds = (size_t)(NT / 64) * QSTACK * 64 * 4;
-    hipLaunchKernelGGL(k_quotient, dim3((unsigned)((a.q + NT - 1) / NT)), dim3(NT), lds, s, a);
-    HIP_CHECK(hipGetLastError());
+    QuotArgs a = a0;
+    if (!a.n_slots) {  // no shared subexpressions: one launch over every row
+        a.slot_rows = a.q;
+        a.t0 = 0;
+        hipLaunchKernelGGL(k_quotient, dim3((unsigned)((a.q + NT - 1) / NT)), dim3(NT), lds, s, a);
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
+    // value slots in global scratch (this interpreter is the ZKM_NO_JIT path; the JIT keeps slots in
+    // registers): windows of rows so the scratch stays within ~1 GiB
+    uint64_t rows = std::min<uint64_t>(a.q, std::max<uint64_t>(NT, (1ull << 28) / (uint64_t)a.n_slots));
+    rows = (rows + NT - 1) / NT * NT;
+    DBuf scratch((size_t)a.n_slots * rows, s);
+    a.slots = scratch.p;
+    a.slot_rows = rows;
+    for (uint64_t t0 = 0; t0 < a.q; t0 += rows) {
+        a.t0 = t0;
+        const uint64_t cnt = std::min<uint64_t>(rows, a.q - t0);
+        hipLaunchKernelGGL(k_quotient, dim3((unsigned)((cnt + NT - 1) / NT)), dim3(NT), lds, s, a);
+        HIP_CHECK(hipGetLastError());
+    }
 }
 
 // ------------------------------------------------------------------ batch inverses at points

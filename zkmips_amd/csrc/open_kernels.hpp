@@ -34,6 +34,11 @@ struct QuotArgs {
     int batch, perm_w, global, main_w;
     uint32_t *chunks;                    // 2^lqd chunks x 4 columns x n rows (bit-reversed rows)
     uint64_t cstride;                    // words from chunk j to chunk j+1
+    // shared subexpressions (OP_LET / OP_GET): value slots in global scratch, slot s of row t at
+    // slots[s * slot_rows + (t - t0)]; the rows run in windows of slot_rows starting at t0
+    int n_slots;
+    uint32_t *slots;
+    uint64_t slot_rows, t0;
 };
 void launch_quotient(const QuotArgs &a, hipStream_t s);
 

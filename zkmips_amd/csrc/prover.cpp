@@ -467,6 +467,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         qa.batch = 1 << lqd; qa.perm_w = cd.perm_w; qa.global = cd.scope == 1; qa.main_w = cd.main_w;
         qa.chunks = const_cast<uint32_t *>(q_ptr[i][0]);
         qa.cstride = q_cstride[i];
+        qa.n_slots = cd.n_slots;
         {
             PROF("quotient", s, 8.0 * Q * (cd.main_w + cd.prep_w + 4 * cd.perm_w) + 16.0 * Q);
             const JitKernel &jk = pk.jit[md.chip[i]];

@@ -25,6 +25,24 @@ VERSION = 1
 
 OP_END, OP_MAIN_L, OP_MAIN_N, OP_PREP_L, OP_PREP_N, OP_CONST, OP_PV = 0, 1, 2, 3, 4, 5, 6
 OP_IS_FIRST, OP_IS_LAST, OP_IS_TRANS, OP_ADD, OP_SUB, OP_MUL, OP_NEG, OP_EMIT = 7, 8, 9, 10, 11, 12, 13, 14
+# shared subexpressions (the Rc-shared nodes of Plonky3's SymbolicExpression DAG): LET s pops the top
+# into value slot s, GET s pushes it.  A chip's program starts with its shared definitions (each
+# evaluated once per row, in creation order, which is a topological order), then its constraints.
+OP_LET, OP_GET = 15, 16
+# builder-only opcode (never in a blob): a reference to shared definition `gid` of _SHARED
+OP_REF = 0x10000
+_OPERAND_OPS = frozenset((OP_MAIN_L, OP_MAIN_N, OP_PREP_L, OP_PREP_N, OP_CONST, OP_PV, OP_LET, OP_GET, OP_REF))
+_SHARED: List[List[int]] = []  # gid -> code of the shared definition (builder registry)
+
+
+def _refs(code: List[int]):
+    """gids of the shared definitions `code` references directly."""
+    i, n = 0, len(code)
+    while i < n:
+        op = code[i]
+        if op == OP_REF:
+            yield code[i + 1]
+        i += 2 if op in _OPERAND_OPS else 1
 
 SCOPE_GLOBAL_ENUM = 1  # commit_scope encoding in the blob: 0 = Local, 1 = Global
 LOOKUP_LOCAL, LOOKUP_GLOBAL = 0, 1
@@ -69,6 +87,15 @@ class Expr:
 
     def __neg__(self):
         return Expr(self.code + [OP_NEG], self.deg)
+
+    def share(self) -> "Expr":
+        """This expression as a shared node: every use reads one value per row (OP_GET) instead of
+        repeating its code, as Plonky3 shares Rc'd SymbolicExpression nodes.  Columns and constants are
+        returned as they are (re-reading them is as cheap as a slot)."""
+        if len(self.code) <= 2:
+            return self
+        _SHARED.append(self.code)
+        return Expr([OP_REF, len(_SHARED) - 1], self.deg)
 
 
 def main(c: int) -> Expr:
@@ -184,14 +211,45 @@ class ChipDesc:
             c += 14
         return c
 
+    def program(self) -> List[int]:
+        """The chip's postfix program: its shared definitions (LET), then one EMIT per constraint."""
+        need, stack = set(), []
+        for c in self.constraints:
+            stack.extend(_refs(c.code))
+        while stack:
+            g = stack.pop()
+            if g not in need:
+                need.add(g)
+                stack.extend(_refs(_SHARED[g]))
+        slot = {g: k for k, g in enumerate(sorted(need))}
+
+        def lower(code):
+            out, i, n = [], 0, len(code)
+            while i < n:
+                op = code[i]
+                if op == OP_REF:
+                    out += [OP_GET, slot[code[i + 1]]]
+                    i += 2
+                elif op in _OPERAND_OPS:
+                    out += code[i:i + 2]
+                    i += 2
+                else:
+                    out.append(op)
+                    i += 1
+            return out
+        prog: List[int] = []
+        for g in sorted(need):
+            prog += lower(_SHARED[g]) + [OP_LET, slot[g]]
+        for c in self.constraints:
+            prog += lower(c.code) + [OP_EMIT]
+        return prog
+
     def words(self) -> List[int]:
         nb = self.name.encode()
         w = [len(nb)]
         padded = nb + b"\0" * (-len(nb) % 4)
         w += [int.from_bytes(padded[i:i + 4], "little") for i in range(0, len(padded), 4)]
-        code: List[int] = []
-        for c in self.constraints:
-            code += c.code + [OP_EMIT]
+        code = self.program()
         w += [self.prep_width, self.main_width, self.commit_scope, int(self.local_only),
               self.log_quotient_degree, len(self.constraints), len(code)] + code
         w += [len(self.sends), len(self.receives)]

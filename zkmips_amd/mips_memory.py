@@ -69,8 +69,16 @@ def s_sub(a, b):
     return [_add(x, _neg(y)) for x, y in zip(a, b)]
 
 
+def _shared(t):
+    return t.share() if isinstance(t, Expr) else t
+
+
 def s_mul(a, b):
-    """SepticExtension::mul (septic_extension.rs:300-316): schoolbook, then z^7 = 8 - 2z."""
+    """SepticExtension::mul (septic_extension.rs:300-316): schoolbook, then z^7 = 8 - 2z.  Operands and
+    results are shared nodes (the reference clones Rc'd symbolic expressions into the 49 products, so
+    its DAG holds each coefficient once)."""
+    a = [_shared(x) for x in a]
+    b = a if b is a else [_shared(x) for x in b]
     res = [0] * 13
     for i in range(7):
         for j in range(7):
@@ -79,10 +87,11 @@ def s_mul(a, b):
     for i in range(7, 13):
         ret[i - 7] = _add(ret[i - 7], _mul(8, res[i]))
         ret[i - 6] = _add(ret[i - 6], _mul(P - 2, res[i]))
-    return ret
+    return [_shared(x) for x in ret]
 
 
 def s_square(a):
+    a = [_shared(x) for x in a]
     return s_mul(a, a)
 
 

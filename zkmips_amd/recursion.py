@@ -611,68 +611,42 @@ def _alu_chip(name: str, ext: bool) -> ChipDesc:
     return c
 
 
-class _Lin:
-    """A linear form sum(c_v * var) + k over trace columns, so the 13 chained internal linear layers of
-    Poseidon2 stay compact (Plonky3's symbolic expressions share subterms; a postfix program cannot)."""
-
-    def __init__(self, terms=None, k=0):
-        self.t = dict(terms or {})
-        self.k = k % P
-
-    @staticmethod
-    def var(col):
-        return _Lin({col: 1})
-
-    def __add__(self, o):
-        if isinstance(o, int):
-            return _Lin(self.t, self.k + o)
-        t = dict(self.t)
-        for v, c in o.t.items():
-            t[v] = (t.get(v, 0) + c) % P
-        return _Lin(t, self.k + o.k)
-
-    def scale(self, s):
-        return _Lin({v: c * s % P for v, c in self.t.items()}, self.k * s)
-
-    def expr(self) -> Expr:
-        e = None
-        for v, c in sorted(self.t.items()):
-            if c == 0:
-                continue
-            term = main(v) if c == 1 else c * main(v)
-            e = term if e is None else e + term
-        if e is None:
-            return Expr.lift(self.k)
-        return e + self.k if self.k else e
+def _m4_expr(x):
+    """Poseidon2's M4 block (the x[0..4] -> 4 outputs of apply_m_4, air.rs:31-56), intermediates shared."""
+    t01 = (x[0] + x[1]).share()
+    t23 = (x[2] + x[3]).share()
+    t0123 = (t01 + t23).share()
+    t01123 = (t0123 + x[1]).share()
+    t01233 = (t0123 + x[3]).share()
+    return [t01123 + t01, t01123 + 2 * x[2], t01233 + t23, t01233 + 2 * x[0]]
 
 
-def _lin_m4(x):
-    t01 = x[0] + x[1]
-    t23 = x[2] + x[3]
-    t0123 = t01 + t23
-    t01123 = t0123 + x[1]
-    t01233 = t0123 + x[3]
-    return [t01123 + t01, t01123 + x[2].scale(2), t01233 + t23, t01233 + x[0].scale(2)]
-
-
-def _lin_external(s):
+def _external_layer_expr(s):
+    """external_linear_layer: M4 on each 4-block, then every element plus its column's sum over the blocks.
+    Each output is a shared node, so the next round reads it once per use (the chained symbolic state
+    of air.rs:84-132, shared as Plonky3 shares Rc'd SymbolicExpression nodes)."""
     out = []
     for j in range(0, WIDTH, 4):
-        out += _lin_m4(s[j:j + 4])
-    sums = [out[k] + out[4 + k] + out[8 + k] + out[12 + k] for k in range(4)]
-    return [out[j] + sums[j % 4] for j in range(WIDTH)]
+        out += [e.share() for e in _m4_expr(s[j:j + 4])]
+    sums = [(out[k] + out[4 + k] + out[8 + k] + out[12 + k]).share() for k in range(4)]
+    return [(out[j] + sums[j % 4]).share() for j in range(WIDTH)]
 
 
-def _lin_internal(s):
+def _internal_layer_expr(s):
+    """internal_linear_layer: s_i <- d_i s_i + sum(s) with the diagonal DIAG (air.rs:12-29)."""
     tot = s[0]
     for j in range(1, WIDTH):
         tot = tot + s[j]
-    return [s[i].scale(DIAG[i]) + tot for i in range(WIDTH)]
+    tot = tot.share()
+    return [(DIAG[i] * s[i] + tot).share() for i in range(WIDTH)]
 
 
 def poseidon2_wide_chip() -> ChipDesc:
     """Poseidon2WideDeg3 (poseidon2_wide/air.rs:39-179): prep = input addrs[16], (output addr, mult)[16],
-    is_real_neg; main = PermutationSBox (313 columns)."""
+    is_real_neg; main = PermutationSBox (313 columns).  The round states are chained symbolic
+    expressions as in the reference's eval (external rounds air.rs:84-132, internal rounds :134-170),
+    each state element a shared subexpression (OP_LET/OP_GET), so the 13 chained internal layers cost
+    one node per element instead of an exponentially growing expression."""
     c = ChipDesc("Poseidon2WideDeg3", prep_width=49, main_width=P2_COLS, local_only=True)
     x = main(P2_EXT)
     c.assert_zero(x * x * x - x * x * x)  # dummy constraint normalising the degree to 3
@@ -681,19 +655,18 @@ def poseidon2_wide_chip() -> ChipDesc:
     for i in range(WIDTH):
         c.sends.append(_mem(V.single_prep(16 + 2 * i), _single(V.single_main(P2_OUT + i)), V.single_prep(17 + 2 * i)))
 
-    ext_state = lambda r: [_Lin.var(P2_EXT + r * WIDTH + i) for i in range(WIDTH)]
     for r in range(NUM_EXTERNAL_ROUNDS):
-        st = ext_state(r)
+        st = [main(P2_EXT + r * WIDTH + i) for i in range(WIDTH)]
         if r == 0:
-            st = _lin_external(st)
+            st = _external_layer_expr(st)
         rnd = r if r < NUM_EXTERNAL_ROUNDS // 2 else r + NUM_INTERNAL_ROUNDS
         sb = []
         for i in range(WIDTH):
-            a = (st[i] + RC[rnd][i]).expr()
+            a = (st[i] + RC[rnd][i]).share()
             col = P2_ESBOX + r * WIDTH + i
             c.assert_zero(main(col) - a * a * a)
-            sb.append(_Lin.var(col))
-        st = _lin_external(sb)
+            sb.append(main(col))
+        st = _external_layer_expr(sb)
         if r == NUM_EXTERNAL_ROUNDS // 2 - 1:
             nxt = [P2_INT + i for i in range(WIDTH)]
         elif r == NUM_EXTERNAL_ROUNDS - 1:
@@ -701,18 +674,18 @@ def poseidon2_wide_chip() -> ChipDesc:
         else:
             nxt = [P2_EXT + (r + 1) * WIDTH + i for i in range(WIDTH)]
         for i in range(WIDTH):
-            c.assert_zero(main(nxt[i]) - st[i].expr())
-    st = [_Lin.var(P2_INT + i) for i in range(WIDTH)]
+            c.assert_zero(main(nxt[i]) - st[i])
+    st = [main(P2_INT + i) for i in range(WIDTH)]
     for r in range(NUM_INTERNAL_ROUNDS):
-        base = st[0] if r == 0 else _Lin.var(P2_S0 + r - 1)
-        a = (base + RC[r + NUM_EXTERNAL_ROUNDS // 2][0]).expr()
+        base = st[0] if r == 0 else main(P2_S0 + r - 1)
+        a = (base + RC[r + NUM_EXTERNAL_ROUNDS // 2][0]).share()
         c.assert_zero(main(P2_ISBOX + r) - a * a * a)
-        st = _lin_internal([_Lin.var(P2_ISBOX + r)] + st[1:])
+        st = _internal_layer_expr([main(P2_ISBOX + r)] + st[1:])
         if r < NUM_INTERNAL_ROUNDS - 1:
-            c.assert_zero(main(P2_S0 + r) - st[0].expr())
+            c.assert_zero(main(P2_S0 + r) - st[0])
     r4 = NUM_EXTERNAL_ROUNDS // 2
     for i in range(WIDTH):
-        c.assert_zero(main(P2_EXT + r4 * WIDTH + i) - st[i].expr())
+        c.assert_zero(main(P2_EXT + r4 * WIDTH + i) - st[i])
     return c
 
 
