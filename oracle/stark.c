@@ -393,7 +393,7 @@ int orc_prove_shard(const orc_pk_t *pk, int n, const int *chip_idx, const kb_t *
             const kb_t *pl = prep_lde ? prep_lde->data + rl * prep_lde->width : NULL;
             const kb_t *pn = prep_lde ? prep_lde->data + rn * prep_lde->width : NULL;
             const kb_t *ml = main_lde->data + rl * main_lde->width, *mn = main_lde->data + rn * main_lde->width;
-            ef_t perm_l[64], perm_n[64];
+            ef_t perm_l[pw > 0 ? pw : 1], perm_n[pw > 0 ? pw : 1];
             for (int b = 0; b < pw; b++)
                 for (int e = 0; e < 4; e++) {
                     perm_l[b].c[e] = perm_lde->data[rl * perm_lde->width + 4 * b + e];

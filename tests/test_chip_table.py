@@ -19,6 +19,7 @@ import pytest
 from tests import _oracle as O
 from zkmips_amd import mips_alu as A
 from zkmips_amd import mips_core as MC
+from zkmips_amd import mips_edwards as ED
 from zkmips_amd import mips_memory as MM
 from zkmips_amd import mips_syscall as SY
 from zkmips_amd.machine import MachineDesc
@@ -56,6 +57,10 @@ CHIPS = {
     "ShaExtend": (SY.sha_extend_chip, 0, 176, 37, 1, False, "sha256/extend/trace.rs:18", None),
     "ShaCompress": (SY.sha_compress_chip, 0, 262, 59, 1, False, "sha256/compress/trace.rs:21", None),
     "SysLinux": (SY.sys_linux_chip, 0, 69, 12, 1, False, "sys_linux/trace.rs:21", None),
+    "EdAddAssign": (ED.ed_add_chip, 0, 1861, 442, 1, True, "syscall/precompiles/edwards/ed_add.rs:103",
+                    "syscall/precompiles/edwards/ed_add.rs:200"),
+    "EdDecompress": (ED.ed_decompress_chip, 0, 1566, 372, 1, True, "syscall/precompiles/edwards/ed_decompress.rs:202",
+                     "syscall/precompiles/edwards/ed_decompress.rs:262"),
 }
 # precompile chips are costed per call: rows per event x per-row cost (mips/mod.rs:216-222)
 ROWS_PER_EVENT = {"ShaExtend": 48, "ShaCompress": 80}

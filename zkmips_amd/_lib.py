@@ -179,14 +179,25 @@ class Device:
 
 def prefill_jit_cache(machines) -> int:
     """Compile every chip's quotient/permutation kernels of `machines` for gfx950 into the JIT's on-disk
-    code-object cache (zkmips_amd/jit_cache, see csrc/jit.cpp); no device needed.  Returns code bytes."""
-    total = 0
-    for m in machines:
-        blob = np.ascontiguousarray(m.blob(), np.uint32)
+    code-object cache (zkmips_amd/jit_cache, see csrc/jit.cpp); no device needed.  The machines compile
+    concurrently (their chips do too, inside the library).  Returns code bytes."""
+    import threading
+    blobs = [np.ascontiguousarray(m.blob(), np.uint32) for m in machines]
+    res = [None] * len(blobs)
+
+    def work(i):
         n = C.c_uint64(0)
-        rc = lib().zkm_quotient_jit_compile(blob.ctypes.data_as(C.c_void_p), C.c_size_t(blob.size), C.byref(n))
+        rc = lib().zkm_quotient_jit_compile(blobs[i].ctypes.data_as(C.c_void_p), C.c_size_t(blobs[i].size), C.byref(n))
+        res[i] = (rc, n.value)
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(blobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    total = 0
+    for rc, n in res:
         if rc != 0:
             raise ZkmError(f"quotient JIT compile failed ({rc}): {lib().zkm_last_error().decode()}")
-        total += n.value
+        total += n
     return total
 

@@ -89,6 +89,57 @@ struct Gen {
     }
 };
 
+// Chips with more local lookups than this get their LogUp code as a loop over the flattened lookup
+// table (chip.cpp flatten_chip) instead of straight-line code: hiprtc time grows much faster than
+// linearly with the unrolled lookups (ShaCompress, 116 lookups: minutes; EdAddAssign has 881), while
+// the table walk is wave-uniform (scalar loads of the descriptors, one column read per term).
+constexpr int kJitLookupUnroll = 64;
+
+// device helpers of the loop form: a VirtualPairCol at a row from the flattened table (advances off)
+const char *kLoopHelpers = R"(
+__device__ __forceinline__ uint32_t jvpc(const uint32_t *__restrict__ prog, uint32_t &off,
+                                         const uint32_t *__restrict__ m, const uint32_t *__restrict__ pp,
+                                         uint64_t ld, uint64_t row) {
+    const uint32_t nt = prog[off];
+    uint32_t acc = prog[off + 1 + 2 * nt];
+    for (uint32_t i = 0; i < nt; i++) {
+        const uint32_t col = prog[off + 1 + 2 * i], w = prog[off + 2 + 2 * i];
+        const uint32_t v = (col & 0x80000000u) ? m[(uint64_t)(col & 0x7fffffffu) * ld + row] : pp[(uint64_t)col * ld + row];
+        acc = add(acc, mul(v, w));
+    }
+    off += 2 + 2 * nt;
+    return acc;
+}
+// rlc = alpha + kind + sum_v beta^(v+1) x_v and the signed multiplicity of lookup i
+__device__ __forceinline__ ef jlookup(const uint32_t *__restrict__ prog, uint32_t i, const ef &alpha,
+                                      const uint32_t *__restrict__ bp, const uint32_t *__restrict__ m,
+                                      const uint32_t *__restrict__ pp, uint64_t ld, uint64_t row, uint32_t &mult) {
+    const uint32_t *lk = prog + prog[3] + 4 * i;
+    ef d = ef_add_base(alpha, lk[0]);
+    uint32_t off = lk[3];
+    for (uint32_t v = 0; v < lk[2]; v++) {
+        const uint32_t x = jvpc(prog, off, m, pp, ld, row);
+        d = ef_add(d, ef_mul_base(ef{{bp[4 * v], bp[4 * v + 1], bp[4 * v + 2], bp[4 * v + 3]}}, x));
+    }
+    const uint32_t mm = jvpc(prog, off, m, pp, ld, row);
+    mult = lk[1] ? mm : neg(mm);
+    return d;
+}
+// num / den of lookups [i0, i1): num = sum_i m_i prod_{j != i} d_j, den = prod_i d_i
+__device__ __forceinline__ void jbatch(const uint32_t *__restrict__ prog, uint32_t i0, uint32_t i1, const ef &alpha,
+                                       const uint32_t *__restrict__ bp, const uint32_t *__restrict__ m,
+                                       const uint32_t *__restrict__ pp, uint64_t ld, uint64_t row, ef &num, ef &den) {
+    uint32_t mu;
+    den = jlookup(prog, i0, alpha, bp, m, pp, ld, row, mu);
+    num = ef{{mu, 0u, 0u, 0u}};
+    for (uint32_t i = i0 + 1; i < i1; i++) {
+        const ef d = jlookup(prog, i, alpha, bp, m, pp, ld, row, mu);
+        num = ef_add(ef_mul(num, d), ef_mul_base(den, mu));
+        den = ef_mul(den, d);
+    }
+}
+)";
+
 // value of a VirtualPairCol at the local row
 std::string vpc_expr(Gen &g, const VPC &v) {
     std::string acc = kb::to_mont(v.constant) ? hex(kb::to_mont(v.constant)) : "";
@@ -119,6 +170,36 @@ std::string rlc_expr(Gen &g, const char *alpha, const LookupDesc &lk) {
     if (v < xs.size())
         g.body << "    " << rlc << " = ef_add(" << rlc << ", ef_mul_base(BPOW(" << v << "), " << xs[v] << "));\n";
     return rlc;
+}
+
+// One LogUp batch (lookups [i0, i1) of the chip's local lookups): num / den = sum_i m_i / rlc_i with
+// den = prod_i rlc_i and num = sum_i m_i prod_{j != i} rlc_j (permutation.rs:29-69 / :256-333), built
+// incrementally.  The first lookup sets num = m_0 (a base-field value) and den = rlc_0 directly, and
+// while num is still base-field the next step multiplies it as a base element (4 products, not 16):
+// a batch of two costs 2 EF x base products and one EF product instead of three EF products.
+void lookup_batch(Gen &g, const ChipDesc &c, int i0, int i1, const char *alpha, const std::string &num,
+                  const std::string &den) {
+    std::string num_base;  // num as a base-field variable while it is one
+    for (int i = i0; i < i1; i++) {
+        const LookupDesc &lk = c.local[i];
+        std::string d = rlc_expr(g, alpha, lk);
+        std::string m = vpc_expr(g, lk.mult);
+        if (!lk.is_send) {
+            std::string t = g.var("t");
+            g.body << "    const uint32_t " << t << " = neg(" << m << ");\n";
+            m = t;
+        }
+        if (i == i0) {
+            num_base = m;
+            g.body << "    " << den << " = " << d << ";\n";
+            continue;
+        }
+        const std::string nd = num_base.empty() ? "ef_mul(" + num + ", " + d + ")" : "ef_mul_base(" + d + ", " + num_base + ")";
+        g.body << "    " << num << " = ef_add(" << nd << ", ef_mul_base(" << den << ", " << m << "));\n";
+        g.body << "    " << den << " = ef_mul(" << den << ", " << d << ");\n";
+        num_base.clear();
+    }
+    if (!num_base.empty()) g.body << "    " << num << " = ef{{" << num_base << ", 0u, 0u, 0u}};\n";
 }
 
 std::string gen_source(const ChipDesc &c, const std::string &fname) {
@@ -182,7 +263,32 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
     }
     // ---- LogUp constraints (permutation.rs:256-333) ----
     const int nloc = (int)c.local.size();
-    if (nloc) {
+    if (nloc > kJitLookupUnroll) {
+        // loop form: batches walked at run time, constraint index k + b
+        const int batch = 1 << c.log_qd, nb = c.perm_w - 1;
+        g.body << "    {\n"
+               << "        ef sl = ef_zero(), sn = ef_zero();\n"
+               << "        for (int b = 0; b < " << nb << "; b++) {\n"
+               << "            const uint32_t i0 = (uint32_t)b * " << batch << ", i1 = min(i0 + " << batch << "u, "
+               << nloc << "u);\n"
+               << "            ef num, den;\n"
+               << "            jbatch(A.prog, i0, i1, alpha_p, A.beta_pows, A.main, A.prep, A.ld, rl, num, den);\n"
+               << "            ef el, en;\n"
+               << "            for (int e = 0; e < 4; e++) { el.c[e] = A.perm[(uint64_t)(4 * b + e) * A.ld + rl];"
+               << " en.c[e] = A.perm[(uint64_t)(4 * b + e) * A.ld + rn]; }\n"
+               << "            facc.ext(ef_sub(ef_mul(den, el), num), A.pows + 4 * (" << k << " + b));\n"
+               << "            sl = ef_add(sl, el); sn = ef_add(sn, en);\n"
+               << "        }\n"
+               << "        ef pl, pn;\n"
+               << "        for (int e = 0; e < 4; e++) { pl.c[e] = A.perm[(uint64_t)(" << 4 * nb << " + e) * A.ld + rl];"
+               << " pn.c[e] = A.perm[(uint64_t)(" << 4 * nb << " + e) * A.ld + rn]; }\n";
+        k += nb;
+        g.body << "        facc.ext(ef_mul_base(ef_sub(pl, sl), is_first), A.pows + " << 4 * k << ");\n"
+               << "        facc.ext(ef_mul_base(ef_sub(ef_sub(pn, pl), sn), is_trans), A.pows + " << 4 * (k + 1) << ");\n"
+               << "        facc.ext(ef_mul_base(ef_sub(pl, lcs), is_last), A.pows + " << 4 * (k + 2) << ");\n"
+               << "    }\n";
+        k += 3;
+    } else if (nloc) {
         const int batch = 1 << c.log_qd, nb = c.perm_w - 1;
         // perm-trace columns (local / next row) are read where they are consumed, so only the
         // running sums sl, sn stay live across the batches
@@ -197,19 +303,8 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
         g.body << "    ef " << sl << " = ef_zero(), " << sn << " = ef_zero();\n";
         for (int b = 0; b < nb; b++) {
             std::string prod = g.var("pr"), num = g.var("nu");
-            g.body << "    ef " << prod << " = ef_one(), " << num << " = ef_zero();\n";
-            for (int i = b * batch; i < nloc && i < (b + 1) * batch; i++) {
-                const LookupDesc &lk = c.local[i];
-                std::string rlc = rlc_expr(g, "alpha_p", lk);
-                std::string m = vpc_expr(g, lk.mult);
-                if (!lk.is_send) {
-                    std::string t = g.var("t");
-                    g.body << "    const uint32_t " << t << " = neg(" << m << ");\n";
-                    m = t;
-                }
-                g.body << "    " << num << " = ef_add(ef_mul(" << num << ", " << rlc << "), ef_mul_base(" << prod << ", " << m << "));\n";
-                g.body << "    " << prod << " = ef_mul(" << prod << ", " << rlc << ");\n";
-            }
+            g.body << "    ef " << prod << ", " << num << ";\n";
+            lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha_p", num, prod);
             const std::string elb = perm_ef(b, "rl");
             std::string cc = g.var("cc");
             g.body << "    const ef " << cc << " = ef_sub(ef_mul(" << prod << ", " << elb << "), " << num << ");\n";
@@ -286,27 +381,60 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
 // 156-203): per batch b, s_b = sum_i m_i / rlc_i as num_b / den_b, built incrementally exactly as
 // the interpreter kernel; the nb denominators share ONE extension-field inversion (prefix
 // products, Montgomery's trick), then the row total goes to rowsum for the running-sum scan.
+// Loop form of the LogUp trace (chips with > kJitLookupUnroll lookups): batches in groups of 8 share
+// one extension-field inversion (Montgomery's trick in registers).
+std::string gen_perm_loop_source(const ChipDesc &c, const std::string &fname) {
+    const int nloc = (int)c.local.size(), batch = 1 << c.log_qd, nb = c.perm_w - 1;
+    std::ostringstream o;
+    o << "extern \"C\" __global__ void __launch_bounds__(256) " << fname << "(const ZkmPermJitArgs A) {\n"
+      << "    const uint64_t rl = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n"
+      << "    if (rl >= A.ld) return;\n"
+      << "    const ef alpha = ef{{A.alpha[0], A.alpha[1], A.alpha[2], A.alpha[3]}};\n"
+      << "    ef total = ef_zero();\n"
+      << "    for (int g0 = 0; g0 < " << nb << "; g0 += 8) {\n"
+      << "        const int gn = min(8, " << nb << " - g0);\n"
+      << "        ef num[8], den[8], pre[8];\n"
+      << "        ef run = ef_one();\n"
+      << "#pragma unroll\n"
+      << "        for (int j = 0; j < 8; j++) {\n"
+      << "            if (j < gn) {\n"
+      << "                const uint32_t i0 = (uint32_t)(g0 + j) * " << batch << ", i1 = min(i0 + " << batch << "u, " << nloc
+      << "u);\n"
+      << "                jbatch(A.prog, i0, i1, alpha, A.beta_pows, A.main, A.prep, A.ld, rl, num[j], den[j]);\n"
+      << "            } else { num[j] = ef_zero(); den[j] = ef_one(); }\n"
+      << "            pre[j] = run;\n"
+      << "            run = ef_mul(run, den[j]);\n"
+      << "        }\n"
+      << "        ef iv = ef_inv(run);\n"
+      << "#pragma unroll\n"
+      << "        for (int j = 7; j >= 0; j--) {\n"
+      << "            const ef sj = ef_mul(num[j], ef_mul(iv, pre[j]));\n"
+      << "            iv = ef_mul(iv, den[j]);\n"
+      << "            if (j < gn) {\n"
+      << "                for (int e = 0; e < 4; e++) A.out[(uint64_t)(4 * (g0 + j) + e) * A.ld + rl] = sj.c[e];\n"
+      << "                total = ef_add(total, sj);\n"
+      << "            }\n"
+      << "        }\n"
+      << "    }\n"
+      << "    A.rowsum[4 * rl + 0] = total.c[0];\n"
+      << "    A.rowsum[4 * rl + 1] = total.c[1];\n"
+      << "    A.rowsum[4 * rl + 2] = total.c[2];\n"
+      << "    A.rowsum[4 * rl + 3] = total.c[3];\n"
+      << "}\n";
+    return o.str();
+}
+
 std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
     const int nloc = (int)c.local.size();
     if (!nloc) return "";
+    if (nloc > kJitLookupUnroll) return gen_perm_loop_source(c, fname);
     Gen g;
     const int batch = 1 << c.log_qd, nb = c.perm_w - 1;
     g.body << "    const ef alpha = ef{{A.alpha[0], A.alpha[1], A.alpha[2], A.alpha[3]}};\n";
     for (int b = 0; b < nb; b++) {
-        g.body << "    ef num" << b << " = ef_zero(), den" << b << " = ef_one();\n";
-        for (int i = b * batch; i < nloc && i < (b + 1) * batch; i++) {
-            const LookupDesc &lk = c.local[i];
-            std::string d = rlc_expr(g, "alpha", lk);
-            std::string m = vpc_expr(g, lk.mult);
-            if (!lk.is_send) {
-                std::string t = g.var("t");
-                g.body << "    const uint32_t " << t << " = neg(" << m << ");\n";
-                m = t;
-            }
-            g.body << "    num" << b << " = ef_add(ef_mul(num" << b << ", " << d << "), ef_mul_base(den" << b << ", " << m
-                   << "));\n";
-            g.body << "    den" << b << " = ef_mul(den" << b << ", " << d << ");\n";
-        }
+        g.body << "    ef num" << b << ", den" << b << ";\n";
+        lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
+                     "den" + std::to_string(b));
     }
     // one inversion for all batches
     g.body << "    ef pre0 = den0;\n";
@@ -342,6 +470,7 @@ std::string chip_source(const ChipDesc &c) {
       << kJitPrelude << "\nusing namespace kb;\n"
       << "#define POW(k) ef{{A.pows[4*(k)], A.pows[4*(k)+1], A.pows[4*(k)+2], A.pows[4*(k)+3]}}\n"
       << "#define BPOW(v) ef{{A.beta_pows[4*(v)], A.beta_pows[4*(v)+1], A.beta_pows[4*(v)+2], A.beta_pows[4*(v)+3]}}\n"
+      << ((int)c.local.size() > kJitLookupUnroll ? kLoopHelpers : "")
       << gen_source(c, "zkm_quot_jit") << gen_perm_source(c, "zkm_perm_jit");
     return o.str();
 }

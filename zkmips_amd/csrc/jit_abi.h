@@ -15,6 +15,7 @@ struct ZkmQuotJitArgs {
     unsigned gen, gen_pow_n, wn_inv, pad1;
     unsigned alpha_p[4], lcs[4];
     unsigned gcs[14];
+    const unsigned *prog;                // flattened chip program (lookup table: chips with many lookups)
 };
 struct ZkmPermJitArgs {
     const unsigned *main, *prep;  // traces, column-major natural, column stride ld
@@ -23,5 +24,6 @@ struct ZkmPermJitArgs {
     unsigned *rowsum;             // per-row EF total (scan input)
     unsigned long long ld;        // rows
     unsigned alpha[4];
+    const unsigned *prog;         // flattened chip program (lookup table: chips with many lookups)
 };
 #endif

@@ -386,12 +386,15 @@ void launch_inv_points(const ef &z, uint32_t s, const uint32_t *tw, uint64_t M, 
 }
 
 // ------------------------------------------------------------------ opening dot products
-// partial[(col * nseg + seg) * 8 + 4p .. +4] = sum_{j in seg} y_{j + p} w_j / R  (p = 1 only if with_next)
-// Each thread takes rows in pairs (j, j + NT): per EF component the two products go into one
-// v_mad_u64_u32 chain and one lazy Montgomery reduction, accumulated unreduced in 64 bits
-// (11 issue slots per pair instead of 2 x 14 for reduced multiply-adds).  OPEN_CB columns share
-// each weight load.
+// out[col * 8 + 4p .. +4] = sum_j y_{j + p} w_j / R  (p = 1 only if with_next)
+// A workgroup takes OPEN_SEG consecutive rows and stages their 16-B weights in LDS once, then walks
+// its slab of columns OPEN_CB at a time over those rows: the weight table crosses HBM once per
+// launch, not once per column block (it is as large as four columns).  Each thread takes rows in
+// pairs (j, j + NT): per EF component the two products go into one v_mad_u64_u32 chain and one lazy
+// Montgomery reduction, accumulated unreduced in 64 bits.  Per (column, segment) partial sums are
+// reduced over the segments by k_open_sum.
 static constexpr int OPEN_CB = 4;
+static constexpr int OPEN_SEG = 2048;  // rows per workgroup: 32 KB of weights in LDS
 __device__ __forceinline__ uint64_t pair_acc(uint64_t acc, uint32_t ya, uint32_t wa, uint32_t yb, uint32_t wb) {
     // ya wa + yb wb < 2P^2 < P 2^32 -> [0, 2P)
     return add_w(acc, redc2(mad64(ya, wa, prod64(yb, wb))));
@@ -399,88 +402,119 @@ __device__ __forceinline__ uint64_t pair_acc(uint64_t acc, uint32_t ya, uint32_t
 
 __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                  const uint32_t *__restrict__ w, int with_next, int nseg,
-                                                 uint32_t *partial) {
+                                                 uint32_t slab, uint32_t *partial) {
+    __shared__ uint4 wl[OPEN_SEG];
     __shared__ uint32_t red[NT / 64][OPEN_CB][8];
-    const uint64_t seg_len = (n + nseg - 1) / nseg;
-    const uint64_t j0 = (uint64_t)blockIdx.x * seg_len;
-    const uint64_t j1 = j0 + seg_len < n ? j0 + seg_len : n;
-    const uint32_t cb0 = blockIdx.y * OPEN_CB;
-    const int nc = (int)(ncols - cb0 < (uint32_t)OPEN_CB ? ncols - cb0 : OPEN_CB);
-    const uint32_t *y[OPEN_CB];
+    const uint64_t j0 = (uint64_t)blockIdx.x * OPEN_SEG;
+    const uint32_t len = (uint32_t)(n - j0 < (uint64_t)OPEN_SEG ? n - j0 : OPEN_SEG);
+    for (uint32_t r = threadIdx.x; r < len; r += NT) wl[r] = ((const uint4 *)w)[j0 + r];
+    __syncthreads();
+    const uint32_t c_begin = blockIdx.y * slab;
+    const uint32_t c_end = c_begin + slab < ncols ? c_begin + slab : ncols;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += OPEN_CB) {
+        const int nc = (int)(c_end - cb0 < (uint32_t)OPEN_CB ? c_end - cb0 : OPEN_CB);
+        const uint32_t *y[OPEN_CB];
 #pragma unroll
-    for (int k = 0; k < OPEN_CB; k++) y[k] = (const uint32_t *)cols[cb0 + (k < nc ? k : 0)];
-    uint64_t a0[OPEN_CB][4], a1[OPEN_CB][4];
-#pragma unroll
-    for (int k = 0; k < OPEN_CB; k++)
-#pragma unroll
-        for (int e = 0; e < 4; e++) { a0[k][e] = 0; a1[k][e] = 0; }
-    for (uint64_t ja = j0 + threadIdx.x; ja < j1; ja += 2 * NT) {
-        const uint64_t jb0 = ja + NT;
-        const bool hb = jb0 < j1;
-        const uint64_t jb = hb ? jb0 : ja;  // a missing second row pairs with weight 0
-        const uint4 wa = *(const uint4 *)(w + 4 * ja);
-        uint4 wb = *(const uint4 *)(w + 4 * jb);
-        if (!hb) wb = make_uint4(0, 0, 0, 0);
-        const uint32_t wav[4] = {wa.x, wa.y, wa.z, wa.w}, wbv[4] = {wb.x, wb.y, wb.z, wb.w};
-        uint32_t va[OPEN_CB], vb[OPEN_CB], na[OPEN_CB], nb[OPEN_CB];
-#pragma unroll
-        for (int k = 0; k < OPEN_CB; k++) {
-            va[k] = y[k][ja];
-            vb[k] = y[k][jb];
-            if (with_next) {
-                na[k] = y[k][(ja + 1) & (n - 1)];
-                nb[k] = y[k][(jb + 1) & (n - 1)];
-            }
-        }
+        for (int k = 0; k < OPEN_CB; k++) y[k] = (const uint32_t *)cols[cb0 + (k < nc ? k : 0)] + j0;
+        uint64_t a0[OPEN_CB][4], a1[OPEN_CB][4];
 #pragma unroll
         for (int k = 0; k < OPEN_CB; k++)
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                a0[k][e] = pair_acc(a0[k][e], va[k], wav[e], vb[k], wbv[e]);
-                if (with_next) a1[k][e] = pair_acc(a1[k][e], na[k], wav[e], nb[k], wbv[e]);
+            for (int e = 0; e < 4; e++) { a0[k][e] = 0; a1[k][e] = 0; }
+        for (uint32_t ra = threadIdx.x; ra < len; ra += 2 * NT) {
+            const uint32_t rb0 = ra + NT;
+            const bool hb = rb0 < len;
+            const uint32_t rb = hb ? rb0 : ra;  // a missing second row pairs with weight 0
+            const uint4 wa = wl[ra];
+            uint4 wb = wl[rb];
+            if (!hb) wb = make_uint4(0, 0, 0, 0);
+            const uint32_t wav[4] = {wa.x, wa.y, wa.z, wa.w}, wbv[4] = {wb.x, wb.y, wb.z, wb.w};
+            uint32_t va[OPEN_CB], vb[OPEN_CB], na[OPEN_CB], nb[OPEN_CB];
+#pragma unroll
+            for (int k = 0; k < OPEN_CB; k++) {
+                va[k] = y[k][ra];
+                vb[k] = y[k][rb];
+                if (with_next) {  // the next row wraps to row 0 at the end of the column
+                    const uint32_t *yk = y[k] - j0;
+                    na[k] = yk[(j0 + ra + 1) & (n - 1)];
+                    nb[k] = yk[(j0 + rb + 1) & (n - 1)];
+                }
             }
-    }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < OPEN_CB; k++) {
-        uint32_t r0[4], r1[4];
+            for (int k = 0; k < OPEN_CB; k++)
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            r0[e] = acc_mod(a0[k][e]);
-            r1[e] = with_next ? acc_mod(a1[k][e]) : 0u;
+                for (int e = 0; e < 4; e++) {
+                    a0[k][e] = pair_acc(a0[k][e], va[k], wav[e], vb[k], wbv[e]);
+                    if (with_next) a1[k][e] = pair_acc(a1[k][e], na[k], wav[e], nb[k], wbv[e]);
+                }
         }
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1)
+        for (int k = 0; k < OPEN_CB; k++) {
+            uint32_t r0[4], r1[4];
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                r0[e] = add(r0[e], __shfl_xor(r0[e], o, 64));
-                r1[e] = add(r1[e], __shfl_xor(r1[e], o, 64));
+                r0[e] = acc_mod(a0[k][e]);
+                r1[e] = with_next ? acc_mod(a1[k][e]) : 0u;
             }
-        if (lane == 0)
-            for (int e = 0; e < 4; e++) { red[wid][k][e] = r0[e]; red[wid][k][4 + e] = r1[e]; }
-    }
-    __syncthreads();
-    if (threadIdx.x < (unsigned)nc * 8) {
-        const int k = threadIdx.x >> 3, e = threadIdx.x & 7;
-        uint32_t acc = 0;
-        for (int q = 0; q < NT / 64; q++) acc = add(acc, red[q][k][e]);
-        partial[((uint64_t)(cb0 + k) * nseg + blockIdx.x) * 8 + e] = acc;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    r0[e] = add(r0[e], __shfl_xor(r0[e], o, 64));
+                    r1[e] = add(r1[e], __shfl_xor(r1[e], o, 64));
+                }
+            if (lane == 0)
+                for (int e = 0; e < 4; e++) { red[wid][k][e] = r0[e]; red[wid][k][4 + e] = r1[e]; }
+        }
+        __syncthreads();
+        if (threadIdx.x < (unsigned)nc * 8) {
+            const int k = threadIdx.x >> 3, e = threadIdx.x & 7;
+            uint32_t acc = 0;
+            for (int q = 0; q < NT / 64; q++) acc = add(acc, red[q][k][e]);
+            partial[((uint64_t)(cb0 + k) * nseg + blockIdx.x) * 8 + e] = acc;
+        }
+        __syncthreads();  // red is reused by the next column block
     }
 }
 
-int open_dot_nseg(uint64_t ncols, uint64_t n) {
-    const uint64_t chunks = (ncols + OPEN_CB - 1) / OPEN_CB;
-    uint64_t nseg = chunks ? (2048 + chunks - 1) / chunks : 1;
-    const uint64_t max_seg = std::max<uint64_t>(1, n / (2 * NT));  // at least one row pair per thread
-    nseg = std::min<uint64_t>(std::max<uint64_t>(nseg, 1), std::min<uint64_t>(max_seg, 4096));
-    return (int)nseg;
+// out[col * 8 + e] = sum over the nseg segments of partial[(col * nseg + seg) * 8 + e]: one wave per
+// (column, e) pair group, lanes striding over the segments
+__global__ __launch_bounds__(64) void k_open_sum(const uint32_t *__restrict__ partial, uint32_t ncols, int nseg,
+                                                 uint32_t *out) {
+    const uint32_t col = blockIdx.x;
+    const int lane = threadIdx.x;
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // < nseg P < 2^44
+    for (int sg = lane; sg < nseg; sg += 64) {
+        const uint4 *x = (const uint4 *)(partial + ((uint64_t)col * nseg + sg) * 8);
+        const uint4 lo = x[0], hi = x[1];
+        acc[0] += lo.x; acc[1] += lo.y; acc[2] += lo.z; acc[3] += lo.w;
+        acc[4] += hi.x; acc[5] += hi.y; acc[6] += hi.z; acc[7] += hi.w;
+    }
+    uint32_t r[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        r[e] = (uint32_t)(acc[e] % P);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) r[e] = add(r[e], __shfl_xor(r[e], o, 64));
+    }
+    if (lane < 8) out[(uint64_t)col * 8 + lane] = r[lane];
 }
 
-void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next, int nseg,
-                     uint32_t *partial, hipStream_t s) {
+void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next,
+                     uint32_t *out, hipStream_t s) {
     if (!ncols) return;
-    hipLaunchKernelGGL(k_open_dot, dim3(nseg, (ncols + OPEN_CB - 1) / OPEN_CB), dim3(NT), 0, s, d_cols, ncols, n, w,
-                       (int)with_next, nseg, partial);
+    const int nseg = (int)((n + OPEN_SEG - 1) / OPEN_SEG);
+    // small matrices: split the columns into slabs too, so a launch still has ~1024+ workgroups
+    const uint32_t blocks_c = (ncols + OPEN_CB - 1) / OPEN_CB;
+    uint32_t nslab = (uint32_t)std::min<uint64_t>(blocks_c, std::max<uint64_t>(1, 1024 / (uint64_t)nseg));
+    const uint32_t slab = ((blocks_c + nslab - 1) / nslab) * OPEN_CB;
+    nslab = (ncols + slab - 1) / slab;
+    DBuf part((size_t)ncols * nseg * 8, s);
+    hipLaunchKernelGGL(k_open_dot, dim3(nseg, nslab), dim3(NT), 0, s, d_cols, ncols, n, w, (int)with_next, nseg, slab,
+                       part.p);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_open_sum, dim3(ncols), dim3(64), 0, s, part.p, ncols, nseg, out);
     HIP_CHECK(hipGetLastError());
 }
 

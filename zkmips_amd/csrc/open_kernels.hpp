@@ -44,10 +44,9 @@ void launch_quotient(const QuotArgs &a, hipStream_t s);
 
 void launch_inv_points(const kb::ef &z, uint32_t s, const uint32_t *tw, uint64_t M, bool bitrev, bool mul_omega,
                        uint32_t *out, hipStream_t st);
-// row segments for k_open_dot so that a launch has ~2048 workgroups
-int open_dot_nseg(uint64_t ncols, uint64_t n);
-void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next, int nseg,
-                     uint32_t *partial, hipStream_t s);
+// out[col * 8 .. +8] = the (local, next-row) dot products of column col with the weights w (EF)
+void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next,
+                     uint32_t *out, hipStream_t s);
 
 struct ReduceArgs {
     const uint64_t *cols;      // column pointer table

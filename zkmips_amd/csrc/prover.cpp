@@ -359,7 +359,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 if (jk.fn_perm) {
                     ZkmPermJitArgs ja{};
                     ja.main = a.main; ja.prep = a.prep; ja.beta_pows = a.beta_pows; ja.out = a.out;
-                    ja.rowsum = a.rowsum; ja.ld = N;
+                    ja.rowsum = a.rowsum; ja.ld = N; ja.prog = a.prog;
                     memcpy(ja.alpha, a.alpha.c, 16);
                     launch_perm_jit(jk, ja, s);
                 }
@@ -476,7 +476,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 ja.main = qa.main; ja.prep = qa.prep; ja.perm = qa.perm; ja.pv = qa.pv; ja.pows = qa.pows;
                 ja.beta_pows = qa.beta_pows; ja.tw = qa.tw; ja.chunks = qa.chunks; ja.cstride = qa.cstride;
                 ja.ld = qa.ld; ja.n = qa.n; ja.q = qa.q; ja.log_n = qa.log_n; ja.log_q = qa.log_q; ja.step = qa.step;
-                ja.gen = qa.gen; ja.gen_pow_n = qa.gen_pow_n; ja.wn_inv = qa.wn_inv;
+                ja.gen = qa.gen; ja.gen_pow_n = qa.gen_pow_n; ja.wn_inv = qa.wn_inv; ja.prog = qa.prog;
                 memcpy(ja.alpha_p, qa.alpha_p.c, 16); memcpy(ja.lcs, qa.lcs.c, 16); memcpy(ja.gcs, qa.gcs, sizeof ja.gcs);
                 launch_quotient_jit(jk, ja, s);
             } else {
@@ -565,7 +565,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         for (auto &g : groups) {
             g.coff = ncols_all;
             g.poff = nparts;
-            g.nseg = open_dot_nseg(g.W, pend[g.first].N);
+            g.nseg = 1;  // launch_open_dot reduces its row segments on the device
             for (size_t i = g.first; i <= g.last; i++) {
                 Pend &q = pend[i];
                 q.coff = ncols_all;
@@ -598,7 +598,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                 launch_inv_points(ef_mul_base(zeta, inv(q.shift)), ONE, c.tw_fwd, q.N, true, true, (uint32_t *)w, s);
             }
             PROF("open_eval", s, 4.0 * q.N * g.W + 16.0 * q.N);
-            launch_open_dot((const uint64_t *)dcols.p + g.coff, (uint32_t)g.W, q.N, w, q.r->npts == 2, g.nseg,
+            launch_open_dot((const uint64_t *)dcols.p + g.coff, (uint32_t)g.W, q.N, w, q.r->npts == 2,
                             part.p + g.poff, s);
         }
         std::vector<uint32_t> hp(nparts + 1);

@@ -1134,7 +1134,9 @@ def core_machine() -> MachineDesc:
     # MipsAir::get_airs_and_costs order (crates/core/machine/src/mips/mod.rs:207-437): Cpu, Program, the
     # precompiles, SyscallCore/Precompile, the ALUs, Branch, Jump, SyscallInstrs, MemoryInstrs, MiscInstrs,
     # the memory chips, Global, Byte, (SysLinux,) MovCond
-    return MachineDesc([cpu_chip(), program_chip(), SY.sha_extend_chip(), SY.sha_compress_chip(), SY.syscall_chip(True),
+    from . import mips_edwards as ED
+    return MachineDesc([cpu_chip(), program_chip(), SY.sha_extend_chip(), SY.sha_compress_chip(), ED.ed_add_chip(),
+                        ED.ed_decompress_chip(), SY.syscall_chip(True),
                         SY.syscall_chip(False), divrem_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
                         A.shift_right_chip(), A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(),
                         jump_chip(), SY.syscall_instrs_chip(), memory_instructions_chip(), misc_instructions_chip(),
@@ -1841,7 +1843,8 @@ def memory_shard(state, regs, init_regs, shard: int, seed: int = 1):
     return core_machine(), prep_traces, traces, pvs
 
 
-PRECOMPILE_CHIP = {SY.SHA_EXTEND: "ShaExtend", SY.SHA_COMPRESS: "ShaCompress", SY.SYS_LINUX: "SysLinux"}
+PRECOMPILE_CHIP = {SY.SHA_EXTEND: "ShaExtend", SY.SHA_COMPRESS: "ShaCompress", SY.ED_ADD: "EdAddAssign",
+                   SY.ED_DECOMPRESS: "EdDecompress", SY.SYS_LINUX: "SysLinux"}
 
 
 def precompile_shard(code: int, events, shard: int, seed: int = 1):
@@ -1857,6 +1860,12 @@ def precompile_shard(code: int, events, shard: int, seed: int = 1):
         traces["ShaExtend"] = SY.sha_extend_trace(pevs, byte_lookup)
     elif code == SY.SHA_COMPRESS:
         traces["ShaCompress"] = SY.sha_compress_trace(pevs, byte_lookup)
+    elif code == SY.ED_ADD:
+        from . import mips_edwards as ED
+        traces["EdAddAssign"] = ED.ed_add_trace(pevs, byte_lookup)
+    elif code == SY.ED_DECOMPRESS:
+        from . import mips_edwards as ED
+        traces["EdDecompress"] = ED.ed_decompress_trace(pevs, byte_lookup)
     elif code == SY.SYS_LINUX:
         traces["SysLinux"] = SY.sys_linux_trace(pevs, byte_lookup)
     else:

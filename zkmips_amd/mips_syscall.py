@@ -1041,6 +1041,10 @@ class PrecompileMemory:
         self.local = {}
         self.reg_local = {}
 
+    def peek(self, addr):
+        """The current word without an access record (SyscallContext::slice_unsafe, ec.rs:113)."""
+        return self.mem[addr] if addr in self.mem else self.init_word(addr)
+
     def _touch_reg(self, r):
         if self.last[r] != self.reg_start[r][0]:  # the CPU's open entry for r ends here
             s0, v0 = self.reg_start[r]
@@ -1210,4 +1214,16 @@ def sha256_extend_ref(w16):
     return w
 
 
-PRECOMPILES = {SHA_EXTEND: exec_sha_extend, SHA_COMPRESS: exec_sha_compress}
+def _exec_ed_add(pm, shard, clk, a0, a1):
+    from .mips_edwards import exec_ed_add
+    return exec_ed_add(pm, shard, clk, a0, a1)
+
+
+def _exec_ed_decompress(pm, shard, clk, a0, a1):
+    from .mips_edwards import exec_ed_decompress
+    return exec_ed_decompress(pm, shard, clk, a0, a1)
+
+
+ED_ADD, ED_DECOMPRESS = 0x01_01_00_07, 0x00_01_00_08  # executor/src/syscalls/code.rs:50-54
+PRECOMPILES = {SHA_EXTEND: exec_sha_extend, SHA_COMPRESS: exec_sha_compress, ED_ADD: _exec_ed_add,
+               ED_DECOMPRESS: _exec_ed_decompress}
