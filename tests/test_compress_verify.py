@@ -1,0 +1,116 @@
+"""Compress nodes that verify their children (BASELINE config 5; zkmips_amd/recursion_verifier.py after
+crates/prover/src/lib.rs:614-954 and crates/recursion/circuit/src/{stark,fri,merkle_tree,challenger}.rs):
+the node's recursion program replays each child's transcript in Poseidon2 instructions, checks the
+proof of work and the query indices, walks every opened row and FRI sibling up its Merkle path to the
+child's commitments, recomputes the reduced openings with BatchFRI and the folds with ExtAlu, and ends
+at the final polynomial.  A valid child makes the program execute; a changed byte anywhere in a child
+proof makes it fail.  The node program is itself proven (compress machine, blowup 4, 42 queries) and a
+second layer verifies those node proofs."""
+import numpy as np
+import pytest
+
+from tests import _oracle as O
+from zkmips_amd import recursion as R
+from zkmips_amd import recursion_verifier as RV
+from zkmips_amd import workloads as W
+
+NQ = 8  # leaf FRI queries (small for CPU test speed; the bench uses the config's 84)
+
+
+@pytest.fixture(scope="module")
+def leaves():
+    m, prep, _, _ = W.fib_shard(256, seed=3)
+    pr = O.OracleProver(m, prep, num_queries=NQ)
+    proofs = []
+    for s in (3, 4):
+        _, _, tr, pv = W.fib_shard(256, seed=s)
+        rc, p = pr.prove(tr, pv)
+        assert rc == 0
+        proofs.append(p)
+    return RV.ChildVk.of(m, prep, pr.commit, num_queries=NQ), proofs
+
+
+def test_parse_roundtrip(leaves):
+    vk, proofs = leaves
+    p = RV.parse_shard_proof(proofs[0])
+    assert p.names == ["FibCpu", "FibTable"] and len(p.queries) == NQ
+    assert len(p.fri_commits) == 9 - vk.log_blowup  # 2^8 rows -> LDE 2^9, folded down to 2^log_blowup
+
+
+def test_node_program_executes(leaves):
+    vk, proofs = leaves
+    prog = RV.compress_node_program([(vk, p) for p in proofs])
+    rec = R.execute(prog)
+    assert len(rec.events["p2"]) > 100
+
+
+@pytest.mark.parametrize("where", ["commitment", "opened_row", "merkle_path", "fri_sibling", "final_poly", "pow",
+                                   "opened_value", "public_value", "cumulative_sum"])
+def test_changed_child_byte_fails(leaves, where):
+    vk, proofs = leaves
+    b = bytearray(proofs[1])
+    p = RV.parse_shard_proof(proofs[1])
+    # byte offsets of the fields (the layout parse_shard_proof reads)
+    off = {"commitment": 8 * 4 + 1}
+    # locate other fields by searching the serialized words
+    def find_words(words):
+        raw = np.asarray(words, np.uint32).tobytes()
+        i = bytes(b).find(raw)
+        assert i >= 0
+        return i
+    off["opened_row"] = find_words(p.queries[3][0][1][0][0][:4]) + 2
+    off["merkle_path"] = find_words(p.queries[2][0][1][1][1]) + 1
+    off["fri_sibling"] = find_words(p.queries[5][1][2][0]) + 3
+    off["final_poly"] = find_words(p.final_poly) + 1
+    off["pow"] = len(b) - 8 - 4 * len(p.pv) - sum(16 + len(n) for n in p.names) - 8 - 4 + 1
+    off["opened_value"] = find_words(p.chips[0].main_l[5]) + 2
+    off["public_value"] = len(b) - 4 * len(p.pv) + 4 * 3 + 1
+    off["cumulative_sum"] = find_words(p.chips[0].lcs) + 1
+    b[off[where]] ^= 0x20
+    with pytest.raises(Exception):
+        prog = RV.compress_node_program([(vk, proofs[0]), (vk, bytes(b))])
+        R.execute(prog)
+
+
+def test_node_proof_and_second_layer(leaves):
+    """The node program is a compress-machine shard the oracle proves and verifies; a second-layer node
+    verifies two such node proofs (the children are compress proofs: blowup 4)."""
+    vk, proofs = leaves
+    nq2 = 4
+    layer1 = []
+    for order in ((0, 1), (1, 0)):
+        prog = RV.compress_node_program([(vk, proofs[i]) for i in order])
+        m, prep, tr, pv = R.shard(prog)
+        pr = O.OracleProver(m, prep, num_queries=nq2, log_blowup=R.COMPRESS_LOG_BLOWUP)
+        rc, p = pr.prove(tr, pv)
+        assert rc == 0 and pr.verify(p) == 0
+        layer1.append((m, prep, pr.commit, p))
+    # both layer-1 programs have the same structure: one verifying key
+    assert np.array_equal(layer1[0][2], layer1[1][2])
+    m, prep, commit, _ = layer1[0]
+    cvk = RV.compress_vk(m, prep, commit, num_queries=nq2)
+    prog2 = RV.compress_node_program([(cvk, layer1[0][3]), (cvk, layer1[1][3])])
+    R.execute(prog2)
+
+
+@pytest.mark.gpu
+def test_gpu_two_leaf_node(leaves):
+    """Leaves proven on the GPU, the node program built from them proven on the GPU: bytes equal the
+    oracle's; with one byte of a child proof changed the program no longer executes."""
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    dev = Device(0)
+    m, prep, _, _ = W.fib_shard(1 << 12, seed=3)
+    hp = HipProver(dev, m, prep, num_queries=84)
+    leaf = [hp.prove_shard(*W.fib_shard(1 << 12, seed=s)[2:]) for s in (3, 4)]
+    vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=84)
+    prog = RV.compress_node_program([(vk, p) for p in leaf])
+    cm, cprep, ctr, cpv = R.shard(prog)
+    kw = dict(num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    gpu = HipProver(dev, cm, cprep, **kw).prove_shard(ctr, cpv)
+    rc, ref = O.OracleProver(cm, cprep, **kw).prove(ctr, cpv)
+    assert rc == 0 and gpu == ref
+    bad = bytearray(leaf[1])
+    bad[len(bad) // 3] ^= 1
+    with pytest.raises(Exception):
+        R.execute(RV.compress_node_program([(vk, leaf[0]), (vk, bytes(bad))]))

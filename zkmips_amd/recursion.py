@@ -388,12 +388,14 @@ class ExecutionRecord:
     public_values: np.ndarray
 
 
-def execute(prog: RecursionProgram) -> ExecutionRecord:
+def execute(prog: RecursionProgram, mem_out: Optional[dict] = None) -> ExecutionRecord:
     """Run the program (runtime/mod.rs:336-625): memory is write-once; every value read must have been
     written by an earlier block.  Returns per-kind event lists in program order."""
     resolve_mults(prog)
     mem = np.zeros((prog.num_addrs, D), U)
     written = np.zeros(prog.num_addrs, bool)
+    if mem_out is not None:  # diagnostics: the memory image (also after a failed check)
+        mem_out["mem"] = mem
     ev: Dict[str, List[Dict[str, np.ndarray]]] = {k: [] for k in
                                                  ("mem", "hint", "base", "ext", "p2", "select", "exprev", "batchfri", "commit",
                                                   "frifold")}
@@ -411,14 +413,14 @@ def execute(prog: RecursionProgram) -> ExecutionRecord:
         mem[addr] = vals
         written[addr] = True
 
-    for b in prog.blocks:
+    for bi, b in enumerate(prog.blocks):
         a = b.a
         k = b.kind
         if k == "mem":
             w = a["write"]
             if (~w).any():
                 if not np.array_equal(rd(a["addr"][~w]), a["vals"][~w]):
-                    raise RuntimeError("stored memory value should be the specified value")
+                    raise RuntimeError(f"stored memory value should be the specified value (block {bi})")
             wr(a["addr"][w], a["vals"][w])
             ev["mem"].append({})
         elif k == "hint":

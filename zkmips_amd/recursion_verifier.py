@@ -1,0 +1,695 @@
+"""Compress-node programs that verify their child proofs (BASELINE config 5: "batch inner-proof
+verification").
+
+The reference's compress node runs the recursion verifier program over its children's ShardProofs
+(crates/prover/src/lib.rs:614-954; the program compiled from crates/recursion/circuit/src/stark.rs:246-432,
+fri.rs, merkle_tree.rs, challenger.rs).  `verify_shard` appends that verification for one child proof
+to a RecursionProgram, with the proof's data as hints (MemoryVar) and the child's verifying key as
+constants (MemoryConst):
+
+* the Fiat-Shamir transcript (DuplexChallenger, challenger.rs:60-233) replayed in the program: every
+  observed value (public values, the three commitments, the chips' cumulative sums, the FRI commitments,
+  the final polynomial, the PoW witness) enters Poseidon2 permutations in the duplexing pattern, and
+  the challenges (zeta, the FRI alpha and betas, the query indices) are read from their outputs;
+* the proof of work: the low pow_bits bits of the sample after the witness are zero;
+* the query indices: HintBits decompositions of the sampled elements, checked by recomposition and
+  canonical (< p);
+* every query's input openings: the opened rows of the preprocessed, main, permutation and quotient
+  batches re-hashed (PaddingFreeSponge) and walked up their Merkle paths with height injection
+  (MerkleTreeMmcs verify_batch, fri.rs:363-400) to the committed roots;
+* the FRI reduced openings (fri.rs:155-203): per row x = 3 w^rev(i) (ExpReverseBitsLen), BatchFRI
+  accumulations sum alpha^k (p(z) - p(x)) over the opened values, divided by (z - x), per height;
+* the FRI commit phase (fri.rs:247-361): per round the pair (folded, sibling) ordered by the index bit,
+  its leaf hashed and walked to the round's commitment, and the fold
+  e0 + (beta - x0)(e1 - e0)/(x1 - x0) + beta^2 ro[h - 1]; the last folded value equals the final
+  polynomial, and ro[log_blowup] = 0.
+
+Not in the program (documented in DESIGN.md): the OOD evaluation of every chip's constraints at zeta
+against the quotient (verifier.rs:316-397, constraints.rs) and the shape checks the reference's
+verifier does before the transcript.  A program built from a proof executes only if every check above
+holds: a changed byte of the child proof changes a hinted value, and the runtime's memory reads
+(`mem_read` of the expected 0) fail.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import recursion as R
+from .machine import P
+
+U, PU, D = R.U, R.PU, R.D
+GENERATOR = 3
+W_EXT = 3  # EF = F[X]/(X^4 - 3)
+
+
+def two_adic_gen(bits: int) -> int:
+    return pow(3, (P - 1) >> bits, P)
+
+
+# ---------------------------------------------------------------- EF arithmetic on ints (host replay)
+def ef_mul(a, b):
+    r = [0] * 7
+    for i in range(4):
+        for j in range(4):
+            r[i + j] += a[i] * b[j]
+    return [(r[k] + (W_EXT * r[k + 4] if k + 4 < 7 else 0)) % P for k in range(4)]
+
+
+def ef_add(a, b):
+    return [(x + y) % P for x, y in zip(a, b)]
+
+
+def ef_sub(a, b):
+    return [(x - y) % P for x, y in zip(a, b)]
+
+
+def ef_inv(a):
+    return [int(v) for v in R.ext_inv(np.asarray([a], U))[0]]
+
+
+def ef_base(x):
+    return [x % P, 0, 0, 0]
+
+
+# ---------------------------------------------------------------- the proof (bincode ShardProof)
+@dataclass
+class ChipOpened:
+    prep_l: np.ndarray
+    prep_n: np.ndarray
+    main_l: np.ndarray
+    main_n: np.ndarray
+    perm_l: np.ndarray
+    perm_n: np.ndarray
+    quot: np.ndarray  # (chunks, 4, 4): chunk j, column e, EF
+    gcs: np.ndarray
+    lcs: np.ndarray
+    log_degree: int
+
+
+@dataclass
+class ShardProofData:
+    main_c: np.ndarray
+    perm_c: np.ndarray
+    quot_c: np.ndarray
+    chips: List[ChipOpened]
+    fri_commits: np.ndarray           # (rounds, 8)
+    queries: list                     # [(input: [(rows: [np.ndarray], path: (L, 8))] x 4, steps: [(sib EF, path)])]
+    final_poly: np.ndarray
+    pow_witness: int
+    names: List[str]
+    pv: np.ndarray
+
+
+def parse_shard_proof(b: bytes) -> ShardProofData:
+    """The bincode-1 layout zkm_open writes (zkmips_amd/csrc/prover.cpp `serialize`, crates/stark/src/
+    types.rs:77-83): canonical field elements, u64 lengths."""
+    pos = [0]
+
+    def u64():
+        v = int.from_bytes(b[pos[0]:pos[0] + 8], "little")
+        pos[0] += 8
+        return v
+
+    def u32s(n):
+        v = np.frombuffer(b, np.uint32, n, pos[0]).astype(np.int64)
+        pos[0] += 4 * n
+        return v
+
+    def efv():
+        n = u64()
+        return u32s(4 * n).reshape(n, 4)
+
+    def digests():
+        n = u64()
+        return u32s(8 * n).reshape(n, 8)
+
+    main_c, perm_c, quot_c = u32s(8), u32s(8), u32s(8)
+    chips = []
+    for _ in range(u64()):
+        pl, pn, ml, mn, rl, rn = (efv() for _ in range(6))
+        nq = u64()
+        quot = np.stack([efv() for _ in range(nq)]) if nq else np.zeros((0, 4, 4), np.int64)
+        gcs, lcs = u32s(14), u32s(4)
+        chips.append(ChipOpened(pl, pn, ml, mn, rl, rn, quot, gcs, lcs, u64()))
+    fri_commits = digests()
+    queries = []
+    for _ in range(u64()):
+        inputs = []
+        for _ in range(u64()):
+            rows = [u32s(u64()) for _ in range(u64())]
+            inputs.append((rows, digests()))
+        steps = []
+        for _ in range(u64()):
+            sib = u32s(4)
+            steps.append((sib, digests()))
+        queries.append((inputs, steps))
+    final_poly, pow_w = u32s(4), int(u32s(1)[0])
+    names = [None] * 0
+    order = []
+    for _ in range(u64()):
+        n = u64()
+        nm = b[pos[0]:pos[0] + n].decode()
+        pos[0] += n
+        order.append((u64(), nm))
+    names = [nm for _, nm in sorted(order)]
+    pv = u32s(u64())
+    assert pos[0] == len(b), "trailing bytes in the shard proof"
+    return ShardProofData(main_c, perm_c, quot_c, chips, fri_commits, queries, final_poly, pow_w, names, pv)
+
+
+# ---------------------------------------------------------------- the child's verifying key
+@dataclass
+class ChildVk:
+    """What a compress program knows of its child's machine: chip shapes (from the machine blob), the
+    preprocessed commitment and heights, pc_start, the initial global cumulative sum, FRI parameters."""
+    chips: Dict[str, object]          # name -> ChipDesc (prep_width, main_width, perm_width_ef, log_qd, local_only)
+    num_pv: int
+    commit: np.ndarray                # vk.commit, 8 canonical words
+    prep_order: List[str]             # preprocessed chips sorted by (height desc, name) (machine.rs:383-384)
+    prep_heights: Dict[str, int]
+    pc_start: int = 0x00400000
+    gcs: np.ndarray = None
+    log_blowup: int = 1
+    num_queries: int = 84
+    pow_bits: int = 16
+
+    @staticmethod
+    def of(machine, prep_traces: Dict[str, np.ndarray], commit, log_blowup=1, num_queries=84, pow_bits=16,
+           pc_start=0x00400000, gcs=None):
+        from . import septic as S
+        prep = {k: v for k, v in prep_traces.items() if v is not None}
+        order = sorted(prep, key=lambda k: (-prep[k].shape[0], k))
+        return ChildVk({c.name: c for c in machine.chips}, machine.num_pv, np.asarray(commit, np.int64), order,
+                       {k: prep[k].shape[0] for k in prep}, pc_start,
+                       np.asarray(S.CURVE_CUMULATIVE_SUM_START if gcs is None else gcs, np.int64), log_blowup,
+                       num_queries, pow_bits)
+
+
+# ---------------------------------------------------------------- host transcript replay
+class HostChallenger:
+    """DuplexChallenger<F, Poseidon2, 16, 8> (challenger.rs:60-233) on canonical ints."""
+
+    def __init__(self):
+        self.st = [0] * 16
+        self.inp: List[int] = []
+        self.out: List[int] = []
+
+    def duplex(self):
+        for i, v in enumerate(self.inp):
+            self.st[i] = v
+        self.inp = []
+        self.st = [int(x) for x in R.poseidon2_permute(np.asarray([self.st], U))[0]]
+        self.out = self.st[:8]
+
+    def observe(self, v):
+        self.out = []
+        self.inp.append(int(v) % P)
+        if len(self.inp) == 8:
+            self.duplex()
+
+    def sample(self):
+        if self.inp or not self.out:
+            self.duplex()
+        return self.out.pop()
+
+    def sample_ef(self):
+        return [self.sample() for _ in range(4)]
+
+
+@dataclass
+class Replay:
+    zeta: list
+    fri_alpha: list
+    betas: list
+    pow_sample: int
+    index_samples: List[int]
+    log_max: int
+
+
+def replay(vk: ChildVk, p: ShardProofData) -> Replay:
+    """The verifier's transcript (machine.rs:77-85 observe_into, then verifier.rs / the PCS)."""
+    ch = HostChallenger()
+    for v in list(vk.commit) + [vk.pc_start] + list(vk.gcs) + [0]:
+        ch.observe(v)
+    for v in p.pv[:vk.num_pv]:
+        ch.observe(v)
+    for v in p.main_c:
+        ch.observe(v)
+    ch.sample_ef(), ch.sample_ef()
+    for v in p.perm_c:
+        ch.observe(v)
+    for c in p.chips:
+        for v in list(c.lcs) + list(c.gcs):
+            ch.observe(v)
+    ch.sample_ef()
+    for v in p.quot_c:
+        ch.observe(v)
+    zeta = ch.sample_ef()
+    fa = ch.sample_ef()
+    betas = []
+    for r in p.fri_commits:
+        for v in r:
+            ch.observe(v)
+        betas.append(ch.sample_ef())
+    for v in p.final_poly:
+        ch.observe(v)
+    ch.observe(p.pow_witness)
+    pw = ch.sample()
+    idx = [ch.sample() for _ in range(vk.num_queries)]
+    return Replay(zeta, fa, betas, pw, idx, len(p.fri_commits) + vk.log_blowup)
+
+
+# ---------------------------------------------------------------- the program builder
+def _blk(vals) -> np.ndarray:
+    """Base values as memory blocks [v, 0, 0, 0]."""
+    v = np.asarray(vals, U).reshape(-1) % PU
+    out = np.zeros((len(v), D), U)
+    out[:, 0] = v
+    return out
+
+
+class Builder:
+    """A RecursionProgram with constants, hinted values and the arithmetic the verifier needs, address
+    arrays vectorised over the queries."""
+
+    def __init__(self, prog: R.RecursionProgram):
+        self.p = prog
+        self._consts: Dict[tuple, int] = {}
+        self.labels: Dict[int, str] = {}  # block index of each check -> what it checks (diagnostics)
+
+    def const(self, v) -> int:
+        """Address of a constant block (MemoryConst); v an int or 4 ints."""
+        key = tuple(int(x) % P for x in (v if isinstance(v, (list, tuple, np.ndarray)) else [v, 0, 0, 0]))
+        if key not in self._consts:
+            a = self.p.alloc(1)
+            self.p.mem_write(a, np.asarray([key], U))
+            self._consts[key] = int(a[0])
+        return self._consts[key]
+
+    def hint_base(self, vals) -> np.ndarray:
+        v = np.asarray(vals, np.int64)
+        a = self.p.alloc(v.size).reshape(v.shape)
+        if v.size:
+            self.p.hint(a.ravel(), _blk(v.ravel()))
+        return a
+
+    def hint_ext(self, vals) -> np.ndarray:
+        v = np.asarray(vals, np.int64).reshape(-1, 4)
+        a = self.p.alloc(len(v))
+        if len(v):
+            self.p.hint(a, v.astype(U) % PU)
+        return a
+
+    def base(self, op, x, y) -> np.ndarray:
+        x, y = np.broadcast_arrays(np.asarray(x, np.int64), np.asarray(y, np.int64))
+        out = self.p.alloc(x.size).reshape(x.shape)
+        if x.size:
+            self.p.base_alu(op, out.ravel(), x.ravel(), y.ravel())
+        return out
+
+    def ext(self, op, x, y) -> np.ndarray:
+        x, y = np.broadcast_arrays(np.asarray(x, np.int64), np.asarray(y, np.int64))
+        out = self.p.alloc(x.size).reshape(x.shape)
+        if x.size:
+            self.p.ext_alu(op, out.ravel(), x.ravel(), y.ravel())
+        return out
+
+    def assert_zero_base(self, addrs, label: str = ""):
+        a = np.asarray(addrs, np.int64).ravel()
+        if a.size:
+            self.labels[len(self.p.blocks)] = label
+            self.p.mem_read(a, np.zeros((a.size, D), U), 1)
+
+    def assert_eq_base(self, x, y, label: str = ""):
+        self.assert_zero_base(self.base(R.OP_SUB, x, y), label)
+
+    def assert_eq_ext(self, x, y, label: str = ""):
+        d = self.ext(R.OP_SUB, x, y)
+        self.labels[len(self.p.blocks)] = label
+        self.p.mem_read(np.asarray(d, np.int64).ravel(), np.zeros((np.asarray(d).size, D), U), 1)
+
+    def p2(self, inp: np.ndarray) -> np.ndarray:
+        """Poseidon2 permutations of (n, 16) input address rows -> (n, 16) output addresses."""
+        inp = np.asarray(inp, np.int64).reshape(-1, R.WIDTH)
+        out = self.p.alloc(inp.size).reshape(inp.shape)
+        self.p.poseidon2(out, inp)
+        return out
+
+    def sponge(self, cols: np.ndarray) -> np.ndarray:
+        """PaddingFreeSponge<P, 16, 8, 8> (hash.rs:40-50) of (n, w) base addresses -> (n, 8)."""
+        n, w = cols.shape
+        zero = self.const(0)
+        state = np.full((n, R.WIDTH), zero, np.int64)
+        for c in range(0, w, 8):
+            k = min(8, w - c)
+            inp = state.copy()
+            inp[:, :k] = cols[:, c:c + k]
+            state = self.p2(inp)
+        return state[:, :8]
+
+    def compress(self, left: np.ndarray, right: np.ndarray) -> np.ndarray:
+        return self.p2(np.concatenate([left, right], 1))[:, :8]
+
+    def select(self, bits, x, y):
+        """(bit ? y : x, bit ? x : y) per element: Select (select.rs)."""
+        bits, x, y = np.broadcast_arrays(*(np.asarray(v, np.int64) for v in (bits, x, y)))
+        o1, o2 = self.p.alloc(x.size).reshape(x.shape), self.p.alloc(x.size).reshape(x.shape)
+        if x.size:
+            self.p.select(bits.ravel(), o1.ravel(), o2.ravel(), x.ravel(), y.ravel())
+        return o1, o2
+
+    def bits_of(self, samples: np.ndarray, values: Sequence[int]) -> np.ndarray:
+        """HintBits: the 31 bits of each sampled element (lsb first), checked boolean, recomposed to the
+        sample, and canonical (not the bits of x + p): returns (n, 31) bit addresses."""
+        v = np.asarray(values, np.int64)
+        bits = self.hint_base(((v[:, None] >> np.arange(31)[None, :]) & 1))
+        sq = self.base(R.OP_MUL, bits, bits)
+        self.assert_eq_base(sq, bits, "bits boolean")
+        acc = bits[:, 0]
+        for i in range(1, 31):
+            acc = self.base(R.OP_ADD, acc, self.base(R.OP_MUL, bits[:, i], self.const(1 << i)))
+        self.assert_eq_base(acc, samples, "bits recompose the sample")
+        # x >= p iff bits 24..30 are all one and the low 24 bits are not all zero
+        top = bits[:, 24]
+        for i in range(25, 31):
+            top = self.base(R.OP_MUL, top, bits[:, i])
+        low = bits[:, 0]
+        for i in range(1, 24):
+            low = self.base(R.OP_ADD, low, bits[:, i])
+        self.assert_zero_base(self.base(R.OP_MUL, top, low), "bits canonical")
+        return bits
+
+    def ef_from_base4(self, words: np.ndarray) -> np.ndarray:
+        """(n, 4) base addresses -> EF addresses sum_k w_k X^k."""
+        x = self.const([0, 1, 0, 0])
+        acc = words[:, 3]
+        for k in (2, 1, 0):
+            acc = self.ext(R.OP_ADD, self.ext(R.OP_MUL, acc, x), words[:, k])
+        return acc
+
+
+class ProgChallenger:
+    """The DuplexChallenger inside the program: inputs overwrite the state's first lanes, permutations are
+    Poseidon2 instructions, samples are permutation output addresses."""
+
+    def __init__(self, b: Builder):
+        self.b = b
+        z = b.const(0)
+        self.st = np.full(R.WIDTH, z, np.int64)
+        self.inp: List[int] = []
+        self.out: List[int] = []
+
+    def duplex(self):
+        x = self.st.copy()
+        x[:len(self.inp)] = self.inp
+        self.inp = []
+        self.st = self.b.p2(x[None, :])[0]
+        self.out = list(self.st[:8])
+
+    def observe(self, addrs):
+        for a in np.asarray(addrs, np.int64).ravel():
+            self.out = []
+            self.inp.append(int(a))
+            if len(self.inp) == 8:
+                self.duplex()
+
+    def sample(self) -> int:
+        if self.inp or not self.out:
+            self.duplex()
+        return self.out.pop()
+
+    def sample_ef(self) -> int:
+        w = np.asarray([[self.sample() for _ in range(4)]], np.int64)
+        return int(self.b.ef_from_base4(w)[0])
+
+
+def _verify_batch(b: Builder, root, mats: List[dict], ridx: np.ndarray, ridx_bits: np.ndarray, paths: np.ndarray):
+    """MerkleTreeMmcs::verify_batch (fri.rs:363-400) for every query: mats = [{height, rows (q, w) addrs}] in
+    commit order; ridx_bits (q, L) the row index bits; paths (q, L, 8) sibling addresses; root 8 addresses."""
+    order = sorted(range(len(mats)), key=lambda k: -mats[k]["height"])
+    cur = mats[order[0]]["height"]
+    pos = 0
+    cols = []
+    while pos < len(order) and mats[order[pos]]["height"] == cur:
+        cols.append(mats[order[pos]]["rows"])
+        pos += 1
+    node = b.sponge(np.concatenate(cols, 1))
+    for lvl in range(paths.shape[1]):
+        bit = ridx_bits[:, lvl]
+        left, right = b.select(np.repeat(bit[:, None], 8, 1), node, paths[:, lvl])
+        node = b.compress(left, right)
+        cur >>= 1
+        cols = []
+        while pos < len(order) and mats[order[pos]]["height"] == cur:
+            cols.append(mats[order[pos]]["rows"])
+            pos += 1
+        if cols:
+            node = b.compress(node, b.sponge(np.concatenate(cols, 1)))
+    assert pos == len(order)
+    b.assert_eq_base(node, np.broadcast_to(np.asarray(root, np.int64), node.shape), "merkle root")
+
+
+def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optional[Builder] = None):
+    """Append the verification of one child ShardProof (module docstring).  Returns the address of the
+    transcript's final state word 0 (a digest of everything the child's proof committed to)."""
+    b = b or Builder(prog)
+    p = parse_shard_proof(proof)
+    rp = replay(vk, p)
+    lb, nq = vk.log_blowup, vk.num_queries
+    chips = [vk.chips[n] for n in p.names]
+    assert len(p.queries) == nq and len(p.chips) == len(chips)
+    ch = ProgChallenger(b)
+    # observe_into: vk commit, pc_start, initial global sum, 0 -- constants of the program
+    ch.observe([b.const(int(v)) for v in list(vk.commit) + [vk.pc_start] + list(vk.gcs) + [0]])
+    pv = b.hint_base(p.pv)
+    ch.observe(pv[:vk.num_pv])
+    main_c, perm_c, quot_c = b.hint_base(p.main_c), b.hint_base(p.perm_c), b.hint_base(p.quot_c)
+    ch.observe(main_c)
+    ch.sample_ef(), ch.sample_ef()
+    ch.observe(perm_c)
+    for c in p.chips:
+        ch.observe(b.hint_base(np.concatenate([c.lcs, c.gcs])))
+    ch.sample_ef()
+    ch.observe(quot_c)
+    zeta = ch.sample_ef()
+    fa = ch.sample_ef()
+    fri_c = b.hint_base(p.fri_commits)
+    betas = []
+    for r in range(len(p.fri_commits)):
+        ch.observe(fri_c[r])
+        betas.append(ch.sample_ef())
+    final = b.hint_ext(p.final_poly)[0]
+    fp_words = b.hint_base(p.final_poly)
+    b.assert_eq_ext(b.ef_from_base4(fp_words[None, :]), final, "final poly words")
+    ch.observe(fp_words)
+    pow_w = b.hint_base([p.pow_witness])
+    ch.observe(pow_w)
+    pow_s = ch.sample()
+    if vk.pow_bits:
+        pbits = b.bits_of(np.asarray([pow_s]), [rp.pow_sample])
+        b.assert_zero_base(pbits[0, :vk.pow_bits], "proof of work")
+    samples = np.asarray([ch.sample() for _ in range(nq)], np.int64)
+    ibits = b.bits_of(samples, rp.index_samples)  # (nq, 31)
+    log_max = rp.log_max
+    index = np.asarray(rp.index_samples, np.int64) & ((1 << log_max) - 1)
+
+    # ---- the four input rounds (verifier.rs:124-205): matrices, heights, opening points, values ----
+    g_zeta = {}
+
+    def zeta_next(log_n):
+        if log_n not in g_zeta:
+            g_zeta[log_n] = int(b.ext(R.OP_MUL, zeta, b.const(two_adic_gen(log_n))))
+        return g_zeta[log_n]
+    rounds = []
+    mats = []
+    for name in vk.prep_order:  # round 0: the vk's preprocessed traces
+        i = p.names.index(name)
+        c, o = vk.chips[name], p.chips[i]
+        pts = [(zeta, o.prep_l)] + ([] if c.local_only else [(zeta_next(o.log_degree), o.prep_n)])
+        mats.append({"log_n": int(np.log2(vk.prep_heights[name])), "width": c.prep_width, "pts": pts})
+    rounds.append(([b.const(int(v)) for v in vk.commit], mats))
+    mats = []
+    for c, o in zip(chips, p.chips):  # round 1: main
+        pts = [(zeta, o.main_l)] + ([] if c.local_only else [(zeta_next(o.log_degree), o.main_n)])
+        mats.append({"log_n": o.log_degree, "width": c.main_width, "pts": pts})
+    rounds.append((main_c, mats))
+    mats = [{"log_n": o.log_degree, "width": 4 * c.perm_width_ef,
+             "pts": [(zeta, o.perm_l), (zeta_next(o.log_degree), o.perm_n)]} for c, o in zip(chips, p.chips)]
+    rounds.append((perm_c, mats))
+    mats = []
+    for c, o in zip(chips, p.chips):  # round 3: quotient chunks
+        for j in range(1 << c.log_quotient_degree):
+            mats.append({"log_n": o.log_degree, "width": 4, "pts": [(zeta, o.quot[j])]})
+    rounds.append((quot_c, mats))
+    # host mirror of the rounds (z values as ints) for the FRI leaf words
+    zeta_h = rp.zeta
+    rounds_host = []
+    for _, ms in rounds:
+        hm = []
+        for m in ms:
+            pts = []
+            for z, vals in m["pts"]:
+                zh = zeta_h if z == zeta else ef_mul(zeta_h, ef_base(two_adic_gen(m["log_n"])))
+                pts.append((zh, np.asarray(vals, np.int64).reshape(-1, 4)))
+            hm.append((m["log_n"], m["width"], pts))
+        rounds_host.append(hm)
+    fri_pairs = host_fri_pairs(vk, p, rp, rounds_host)
+    # hinted opened values at the points (shared by the queries)
+    for _, ms in rounds:
+        for m in ms:
+            m["pts"] = [(z, b.hint_ext(np.asarray(vals, np.int64).reshape(-1, 4))) for z, vals in m["pts"]]
+    # alpha powers per height (counter per log height, fri.rs:155-203)
+    counts: Dict[int, int] = {}
+    for _, ms in rounds:
+        for m in ms:
+            lh = m["log_n"] + lb
+            counts[lh] = counts.get(lh, 0) + m["width"] * len(m["pts"])
+    apow = [b.const([1, 0, 0, 0])]
+    for _ in range(max(counts.values())):
+        apow.append(int(b.ext(R.OP_MUL, apow[-1], fa)))
+    # ---- queries, vectorised ----
+    ro = {}
+    lhp: Dict[int, int] = {}  # alpha-power counter per log height, across the rounds
+    zero_ef = b.const([0, 0, 0, 0])
+    for t, (root, ms) in enumerate(rounds):
+        q_in = [qq[0][t] for qq in p.queries]
+        lbm = max(m["log_n"] for m in ms) + lb
+        rows = []
+        for k, m in enumerate(ms):
+            vals = np.stack([qi[0][k] for qi in q_in])  # (nq, width)
+            rows.append({"height": 1 << (m["log_n"] + lb), "rows": b.hint_base(vals) if m["width"] else
+                         np.zeros((nq, 0), np.int64)})
+        paths = b.hint_base(np.stack([qi[1] for qi in q_in]))  # (nq, L, 8)
+        shift = log_max - lbm
+        _verify_batch(b, root, rows, index >> shift, ibits[:, shift:shift + lbm], paths)
+        for k, m in enumerate(ms):
+            lh = m["log_n"] + lb
+            s = log_max - lh
+            # x = 3 w_lh^rev(row): ExpReverseBitsLen over the row's bits (lsb first)
+            xr = prog.alloc(nq)
+            prog.exp_reverse_bits(np.full(nq, b.const(two_adic_gen(lh)), np.int64), ibits[:, s:s + lh], xr)
+            x = b.base(R.OP_MUL, xr, b.const(GENERATOR))
+            for z, pz in m["pts"]:
+                w = m["width"]
+                al = np.asarray(apow[lhp.get(lh, 0):lhp.get(lh, 0) + w], np.int64)
+                lhp[lh] = lhp.get(lh, 0) + w
+                if w:
+                    acc = prog.alloc(nq)
+                    prog.batch_fri(acc, np.broadcast_to(al, (nq, w)), np.broadcast_to(pz, (nq, w)), rows[k]["rows"])
+                else:
+                    acc = np.full(nq, zero_ef, np.int64)
+                zx = b.ext(R.OP_SUB, np.full(nq, z, np.int64), x)
+                term = b.ext(R.OP_DIV, acc, zx)
+                ro[lh] = term if lh not in ro else b.ext(R.OP_ADD, ro[lh], term)
+    if lb in ro:
+        b.assert_eq_ext(ro[lb], np.full(nq, zero_ef, np.int64), "ro[log_blowup] = 0")
+    # ---- FRI commit phase (fri.rs:247-361) ----
+    folded = ro[log_max]
+    xr = prog.alloc(nq)
+    prog.exp_reverse_bits(np.full(nq, b.const(two_adic_gen(log_max)), np.int64), ibits[:, :log_max], xr)
+    x = xr
+    zero = b.const(0)
+    for off in range(len(p.fri_commits)):
+        lfh = log_max - 1 - off
+        bit = ibits[:, off]
+        sib = b.hint_ext(np.stack([qq[1][off][0] for qq in p.queries]))
+        d = b.ext(R.OP_SUB, sib, folded)
+        e0 = b.ext(R.OP_ADD, folded, b.ext(R.OP_MUL, bit, d))      # bit ? sib : folded
+        e1 = b.ext(R.OP_SUB, b.ext(R.OP_ADD, folded, sib), e0)
+        # the leaf (e0 || e1) as 8 base words: hinted, recomposed to e0 and e1
+        words = b.hint_base(np.asarray([list(fri_pairs[qn][off][0]) + list(fri_pairs[qn][off][1])
+                                        for qn in range(nq)], np.int64))
+        b.assert_eq_ext(b.ef_from_base4(words[:, :4]), e0, f"fri leaf e0 round {off}")
+        b.assert_eq_ext(b.ef_from_base4(words[:, 4:]), e1, f"fri leaf e1 round {off}")
+        fpaths = b.hint_base(np.stack([qq[1][off][1] for qq in p.queries]))
+        _verify_batch(b, fri_c[off], [{"height": 1 << lfh, "rows": words}], index >> (off + 1),
+                      ibits[:, off + 1:off + 1 + lfh], fpaths)
+        xn = b.base(R.OP_SUB, zero, x)
+        x0, x1 = b.select(bit, x, xn)
+        inv = b.base(R.OP_DIV, b.const(1), b.base(R.OP_SUB, x1, x0))
+        t = b.ext(R.OP_MUL, b.ext(R.OP_SUB, np.full(nq, betas[off], np.int64), x0),
+                  b.ext(R.OP_MUL, b.ext(R.OP_SUB, e1, e0), inv))
+        folded = b.ext(R.OP_ADD, e0, t)
+        if lfh in ro:
+            bsq = b.ext(R.OP_MUL, betas[off], betas[off])
+            folded = b.ext(R.OP_ADD, folded, b.ext(R.OP_MUL, np.full(nq, bsq, np.int64), ro[lfh]))
+        x = b.base(R.OP_MUL, x, x)
+    b.assert_eq_ext(folded, np.full(nq, final, np.int64), "final fold = final poly")
+    return int(ch.st[0])
+
+
+def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> List[List[tuple]]:
+    """The verifier's reduced openings and folds on the host (fri.rs:155-203, :247-361), per query the
+    (e0, e1) leaf pair of every commit-phase round: the pair the program hashes (as hinted base words)
+    and recomposes against its own in-program fold."""
+    lb, log_max = vk.log_blowup, rp.log_max
+    fa = rp.fri_alpha
+    apow = [[1, 0, 0, 0]]
+    out = []
+    for qn in range(len(p.queries)):
+        idx = rp.index_samples[qn] & ((1 << log_max) - 1)
+        ro: Dict[int, list] = {}
+        lhp: Dict[int, int] = {}
+        for t, ms in enumerate(rounds_host):
+            rows = p.queries[qn][0][t][0]
+            for k, (log_n, width, pts) in enumerate(ms):
+                lh = log_n + lb
+                row = (idx >> (log_max - lh)) & ((1 << lh) - 1)
+                x = GENERATOR * pow(two_adic_gen(lh), int(format(row, f"0{lh}b")[::-1], 2) if lh else 0, P) % P
+                for z, vals in pts:
+                    acc = [0, 0, 0, 0]
+                    for c in range(width):
+                        pw = lhp.get(lh, 0)
+                        lhp[lh] = pw + 1
+                        while len(apow) <= pw:
+                            apow.append(ef_mul(apow[-1], fa))
+                        acc = ef_add(acc, ef_mul(apow[pw], ef_sub([int(v) for v in vals[c]], ef_base(int(rows[k][c])))))
+                    term = ef_mul(acc, ef_inv(ef_sub(z, ef_base(x))))
+                    ro[lh] = ef_add(ro.get(lh, [0, 0, 0, 0]), term)
+        folded = ro[log_max]
+        x = pow(two_adic_gen(log_max), int(format(idx, f"0{log_max}b")[::-1], 2), P)
+        pairs = []
+        for off, (sib, _) in enumerate(p.queries[qn][1]):
+            bit = (idx >> off) & 1
+            sib = [int(v) for v in sib]
+            e0, e1 = (sib, folded) if bit else (folded, sib)
+            pairs.append((e0, e1))
+            xn = (P - x) % P
+            x0, x1 = (xn, x) if bit else (x, xn)
+            t_ = ef_mul(ef_sub(rp.betas[off], ef_base(x0)), ef_mul(ef_sub(e1, e0), ef_base(pow((x1 - x0) % P, P - 2, P))))
+            folded = ef_add(e0, t_)
+            lfh = log_max - 1 - off
+            if lfh in ro:
+                folded = ef_add(folded, ef_mul(ef_mul(rp.betas[off], rp.betas[off]), ro[lfh]))
+            x = x * x % P
+        if folded != [int(v) for v in p.final_poly]:
+            raise ValueError(f"FRI query {qn}: the folds do not reach the final polynomial (invalid child proof)")
+        out.append(pairs)
+    return out
+
+
+def compress_node_program(children: Sequence[tuple]) -> R.RecursionProgram:
+    """A compress node (prover/src/lib.rs:614-954): verify every child (ChildVk, proof bytes) and commit
+    public values whose digest (RecursionPublicValues.digest) is a Poseidon2 hash of the children's
+    transcript states -- a node's public values commit to what its children committed to."""
+    prog = R.RecursionProgram()
+    b = Builder(prog)
+    states = [verify_shard(prog, vk, proof, b) for vk, proof in children]
+    zero = b.const(0)
+    x = np.full(R.WIDTH, zero, np.int64)
+    x[:len(states)] = states[:R.WIDTH]
+    digest = b.p2(x[None, :])[0, :R.DIGEST_SIZE]
+    pv = np.full(R.PROOF_MAX_NUM_PVS, zero, np.int64)
+    pv[R.PV_DIGEST_START:R.PV_DIGEST_START + R.DIGEST_SIZE] = digest
+    prog.commit_public_values(pv)
+    return prog
+
+
+def compress_vk(machine, prep_traces, commit, num_queries: int = None) -> ChildVk:
+    """The ChildVk of a compress-machine proof (compressed_fri_config: blowup 4, 42 queries) of the program
+    whose preprocessed traces are `prep_traces` and whose setup gave `commit`."""
+    return ChildVk.of(machine, prep_traces, commit, log_blowup=R.COMPRESS_LOG_BLOWUP,
+                      num_queries=num_queries or R.COMPRESS_NUM_QUERIES)
