@@ -348,3 +348,22 @@ def test_two_rank_sha2_execution():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert got == n and len(non_cpu) == 3  # extend shard, compress shard, memory shard
+
+
+@pytest.mark.gpu
+def test_sha_compress_shard_full_global_height():
+    """BASELINE config 3 at size: a SHA_COMPRESS precompile shard whose Global chip reaches
+    its full 2^22 rows (14,600 compressions: ~145 global messages each -- the syscall plus the initial
+    and final record of every word the call touched) and ShaCompress 2^21 rows proves on the GPU to
+    the oracle's bytes (16 queries keep the oracle's run to tens of seconds)."""
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    calls = 14600
+    run = C.program_shards(C.sha_program(calls, seed=3, loads=0), seed=3, shard_size=1 << 21,
+                           precompile_events_per_shard=calls)
+    m, prep, tr, pv = next(r for r in run if "ShaCompress" in r[2])
+    assert tr["Global"].shape[0] == 1 << 22 and tr["ShaCompress"].shape[0] == 1 << 21
+    prep = {k: v for k, v in prep.items() if v is not None}
+    gpu = HipProver(Device(0), m, prep, num_queries=16).prove_shard(tr, pv)
+    rc, ref = O.OracleProver(m, prep, num_queries=16).prove(tr, pv)
+    assert rc == 0 and gpu == ref

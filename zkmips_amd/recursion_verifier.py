@@ -161,11 +161,22 @@ def parse_shard_proof(b: bytes) -> ShardProofData:
 
 
 # ---------------------------------------------------------------- the child's verifying key
+@dataclass(frozen=True)
+class ChipShape:
+    """The shape of a chip the verifier needs (a picklable summary of a ChipDesc)."""
+    name: str
+    prep_width: int
+    main_width: int
+    perm_width_ef: int
+    log_quotient_degree: int
+    local_only: bool
+
+
 @dataclass
 class ChildVk:
     """What a compress program knows of its child's machine: chip shapes (from the machine blob), the
     preprocessed commitment and heights, pc_start, the initial global cumulative sum, FRI parameters."""
-    chips: Dict[str, object]          # name -> ChipDesc (prep_width, main_width, perm_width_ef, log_qd, local_only)
+    chips: Dict[str, ChipShape]
     num_pv: int
     commit: np.ndarray                # vk.commit, 8 canonical words
     prep_order: List[str]             # preprocessed chips sorted by (height desc, name) (machine.rs:383-384)
@@ -182,7 +193,9 @@ class ChildVk:
         from . import septic as S
         prep = {k: v for k, v in prep_traces.items() if v is not None}
         order = sorted(prep, key=lambda k: (-prep[k].shape[0], k))
-        return ChildVk({c.name: c for c in machine.chips}, machine.num_pv, np.asarray(commit, np.int64), order,
+        shapes = {c.name: ChipShape(c.name, c.prep_width, c.main_width, c.perm_width_ef, c.log_quotient_degree,
+                                    bool(c.local_only)) for c in machine.chips}
+        return ChildVk(shapes, machine.num_pv, np.asarray(commit, np.int64), order,
                        {k: prep[k].shape[0] for k in prep}, pc_start,
                        np.asarray(S.CURVE_CUMULATIVE_SUM_START if gcs is None else gcs, np.int64), log_blowup,
                        num_queries, pow_bits)
