@@ -102,13 +102,16 @@ STAGE_KERNELS = {  # profiled stage -> the kernels it brackets (kernel-name pref
 }
 
 
-def _counter_rows(d):
-    """(dispatch id, kernel short name, counter value) of every row of a rocprofv3 counter CSV under d."""
+def _counter_rows(d, counter=None):
+    """(dispatch id, kernel short name, counter value) of every row of a rocprofv3 counter CSV under d
+    (only the rows of `counter` when a pass collected several)."""
     import csv
     import glob
     rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
+            if counter and r.get("Counter_Name") != counter:
+                continue
             k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("zkm::", "")
             rows.append((int(r["Dispatch_Id"]), k, float(r["Counter_Value"])))
     rows.sort()
@@ -141,14 +144,23 @@ def pmc_in_run(args, timeout_s=240):
     base = tempfile.mkdtemp(prefix="zkm_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--workload", args.workload,
              "--log-n", str(args.log_n), "--queries", str(args.queries)]
-    for ctr, mult in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
-        d = os.path.join(base, ctr)
-        cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", ctr, "--output-format", "csv", "-d", d,
-               "-o", "run", "--"] + child
+    sq = {}
+    for ctr, mult in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0), (" ".join(SQ_COUNTERS), None)):
+        d = os.path.join(base, ctr.split()[0])
+        cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc"] + ctr.split() + [
+            "--output-format", "csv", "-d", d, "-o", "run", "--"] + child
         r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=base)
         if r.returncode != 0:
             sys.stderr.write(f"pmc pass {ctr} failed ({r.returncode}): {r.stderr.decode()[-400:]}\n")
+            if mult is None:
+                break  # the SQ pass is optional: keep the HBM bytes
             return None
+        if mult is None:  # SQ / GRBM counters per kernel per proof
+            for c in SQ_COUNTERS:
+                for _, k, v in _last_proof(_counter_rows(d, c)):
+                    sq.setdefault(k, {}).setdefault(c, 0.0)
+                    sq[k][c] += v
+            continue
         for _, k, v in _last_proof(_counter_rows(d)):
             e = out.setdefault(k, [0.0, 0, 0.0])
             e[0] += mult * v * 1024.0
@@ -156,8 +168,39 @@ def pmc_in_run(args, timeout_s=240):
                 e[1] += 1
             e[2] += v * 1024.0 if ctr == "FETCH_SIZE" else 0.0
     shutil.rmtree(base, ignore_errors=True)
-    return {k: {"bytes_per_proof": v[0], "launches_per_proof": v[1], "fetch_raw_per_proof": v[2]}
-            for k, v in out.items()}
+    return {k: {"bytes_per_proof": v[0], "launches_per_proof": v[1], "fetch_raw_per_proof": v[2],
+                "sq": sq.get(k)} for k, v in out.items()}
+
+
+# one rocprofv3 pass (8 SQ + 2 GRBM counters at most): VALU instructions and VALU-active quad-cycles summed
+# over the waves, waves, and the GPU-busy cycles summed over the 8 XCDs (MI355X_MICROARCH.md)
+SQ_COUNTERS = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")
+
+
+def valu_counters(pmc, kernel="k_hash_leaves"):
+    """Counter-derived VALU figures of a kernel over one proof: instructions per wave, the VALU-busy
+    fraction SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) (quad-cycles -> cycles; busy
+    cycles per XCD), and the issue fraction SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) x the static
+    mean issue cost per instruction / the same cycle budget."""
+    if not pmc or kernel not in pmc or not pmc[kernel].get("sq"):
+        return None
+    c = pmc[kernel]["sq"]
+    cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    if not cyc or not c.get("SQ_WAVES"):
+        return None
+    budget = 1024.0 * cyc
+    out = {"source": "rocprofv3 --pmc " + " ".join(SQ_COUNTERS) + " in this run",
+           "valu_insts_per_wave": round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1),
+           "active_valu_frac": round(4.0 * c["SQ_ACTIVE_INST_VALU"] / budget, 4),
+           "busy_cycles_per_xcd": round(cyc)}
+    f = os.path.join(ROOT, "zkmips_amd", "isa_p2.json")
+    if os.path.exists(f):
+        j = json.load(open(f))
+        if j.get("valu_instructions"):
+            w = j["issue_slots"] / j["valu_instructions"]
+            out["issue_frac"] = round(c["SQ_INSTS_VALU"] * 2.0 * w / budget, 4)
+            out["mean_issue_cost"] = round(w, 3)
+    return out
 
 
 def stage_traffic(pmc, stage):
@@ -1055,6 +1098,9 @@ def main():
                 "traffic_source": "rocprofv3 FETCH_SIZE/WRITE_SIZE passes in this run (2xFETCH+WRITE)" if tb else None}
     if dom == "merkle_leaves" and "merkle_leaves_perms" in prof:
         roofline["valu"] = valu_roofline(prof["merkle_leaves_perms"][2], ms)
+        vc = valu_counters(pmc)
+        if roofline["valu"] is not None and vc:
+            roofline["valu"]["counters"] = vc
 
     def measured(stage):
         """HBM utilisation of a stage's kernels: PMC bytes per proof over the stage's HIP-event time."""
@@ -1064,7 +1110,8 @@ def main():
         sms = prof[stage][1] / nprof
         gbps = b_ / (sms / 1e3) / 1e9
         return {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_shard": round(b_),
-                "algorithmic_bytes_per_shard": round(prof[stage][2] / nprof), "launches": n_,
+                "algorithmic_bytes_per_shard": round(prof[stage][2] / nprof),
+                "counter_ratio": round(b_ / (prof[stage][2] / nprof), 3), "launches": n_,
                 "stage_ms_per_shard": round(sms, 3)}
 
     ntt = None

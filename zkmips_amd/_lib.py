@@ -177,12 +177,20 @@ class Device:
         return ms.value
 
 
-def prefill_jit_cache(machines) -> int:
+def prefill_jit_cache(machines, prune: bool = True) -> int:
     """Compile every chip's quotient/permutation kernels of `machines` for gfx950 into the JIT's on-disk
     code-object cache (zkmips_amd/jit_cache, see csrc/jit.cpp); no device needed.  The machines compile
-    concurrently (their chips do too, inside the library).  Returns code bytes."""
+    concurrently (their chips do too, inside the library).  With `prune`, code objects of the default
+    cache directory that none of these machines uses any more (older kernel sources) are deleted.
+    Returns code bytes."""
     import threading
+    import time
     blobs = [np.ascontiguousarray(m.blob(), np.uint32) for m in machines]
+    cache = os.path.join(os.path.dirname(os.path.abspath(__file__)), "jit_cache")
+    prune = prune and "ZKM_JIT_CACHE" not in os.environ and os.path.isdir(cache)
+    t0 = time.time() - 1.0
+    if prune:
+        os.environ["ZKM_JIT_TOUCH"] = "1"  # cache hits refresh their file's mtime
     res = [None] * len(blobs)
 
     def work(i):
@@ -194,10 +202,17 @@ def prefill_jit_cache(machines) -> int:
         t.start()
     for t in th:
         t.join()
+    if prune:
+        del os.environ["ZKM_JIT_TOUCH"]
     total = 0
     for rc, n in res:
         if rc != 0:
             raise ZkmError(f"quotient JIT compile failed ({rc}): {lib().zkm_last_error().decode()}")
         total += n
+    if prune:
+        for f in os.listdir(cache):
+            path = os.path.join(cache, f)
+            if f.endswith(".co") and os.path.getmtime(path) < t0:
+                os.remove(path)
     return total
 

@@ -26,6 +26,7 @@
 #include <future>
 #include <map>
 #include <mutex>
+#include <utime.h>
 #include <sstream>
 #include <unordered_map>
 
@@ -381,6 +382,13 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
 // 156-203): per batch b, s_b = sum_i m_i / rlc_i as num_b / den_b, built incrementally exactly as
 // the interpreter kernel; the nb denominators share ONE extension-field inversion (prefix
 // products, Montgomery's trick), then the row total goes to rowsum for the running-sum scan.
+// launch bounds of the LogUp kernels; ZKM_JIT_PERM_WAVES=w asks for w waves per SIMD (register cap)
+std::string perm_bounds() {
+    const char *e = getenv("ZKM_JIT_PERM_WAVES");
+    const int w = e ? atoi(e) : 0;
+    return w > 0 ? "__launch_bounds__(256, " + std::to_string(w) + ")" : "__launch_bounds__(256)";
+}
+
 // Loop form of the LogUp trace (chips with > kJitLookupUnroll lookups): batches in groups of 8 share
 // one extension-field inversion (Montgomery's trick in registers).
 std::string gen_perm_loop_source(const ChipDesc &c, const std::string &fname) {
@@ -431,28 +439,36 @@ std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
     Gen g;
     const int batch = 1 << c.log_qd, nb = c.perm_w - 1;
     g.body << "    const ef alpha = ef{{A.alpha[0], A.alpha[1], A.alpha[2], A.alpha[3]}};\n";
-    for (int b = 0; b < nb; b++) {
-        g.body << "    ef num" << b << ", den" << b << ";\n";
-        lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
-                     "den" + std::to_string(b));
-    }
-    // one inversion for all batches
-    g.body << "    ef pre0 = den0;\n";
-    for (int b = 1; b < nb; b++) g.body << "    const ef pre" << b << " = ef_mul(pre" << b - 1 << ", den" << b << ");\n";
-    g.body << "    ef iv = ef_inv(pre" << nb - 1 << ");\n";
-    for (int b = nb - 1; b >= 1; b--) {
-        g.body << "    const ef s" << b << " = ef_mul(num" << b << ", ef_mul(iv, pre" << b - 1 << "));\n";
-        g.body << "    iv = ef_mul(iv, den" << b << ");\n";
-    }
-    g.body << "    const ef s0 = ef_mul(num0, iv);\n";
     g.body << "    ef total = ef_zero();\n";
-    for (int b = 0; b < nb; b++) {
-        for (int e = 0; e < 4; e++)
-            g.body << "    A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = s" << b << ".c[" << e << "];\n";
-        g.body << "    total = ef_add(total, s" << b << ");\n";
+    // batches in groups of `grp` share one inversion: fewer groups = fewer inversions, more live
+    // (num, den, prefix) registers
+    int grp = nb;
+    if (const char *e = getenv("ZKM_JIT_PERM_GROUP")) grp = std::max(1, atoi(e));
+    for (int g0 = 0; g0 < nb; g0 += grp) {
+        const int g1 = std::min(nb, g0 + grp);
+        for (int b = g0; b < g1; b++) {
+            g.body << "    ef num" << b << ", den" << b << ";\n";
+            lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
+                         "den" + std::to_string(b));
+        }
+        const std::string iv = "iv" + std::to_string(g0);
+        g.body << "    const ef pre" << g0 << " = den" << g0 << ";\n";
+        for (int b = g0 + 1; b < g1; b++)
+            g.body << "    const ef pre" << b << " = ef_mul(pre" << b - 1 << ", den" << b << ");\n";
+        g.body << "    ef " << iv << " = ef_inv(pre" << g1 - 1 << ");\n";
+        for (int b = g1 - 1; b > g0; b--) {
+            g.body << "    const ef s" << b << " = ef_mul(num" << b << ", ef_mul(" << iv << ", pre" << b - 1 << "));\n";
+            g.body << "    " << iv << " = ef_mul(" << iv << ", den" << b << ");\n";
+        }
+        g.body << "    const ef s" << g0 << " = ef_mul(num" << g0 << ", " << iv << ");\n";
+        for (int b = g0; b < g1; b++) {
+            for (int e = 0; e < 4; e++)
+                g.body << "    A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = s" << b << ".c[" << e << "];\n";
+            g.body << "    total = ef_add(total, s" << b << ");\n";
+        }
     }
     std::ostringstream o;
-    o << "extern \"C\" __global__ void __launch_bounds__(256) " << fname << "(const ZkmPermJitArgs A) {\n"
+    o << "extern \"C\" __global__ void " << perm_bounds() << " " << fname << "(const ZkmPermJitArgs A) {\n"
       << "    const uint64_t rl = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n"
       << "    if (rl >= A.ld) return;\n"
       << g.head.str() << g.pipelined(48, "ZKM_JIT_LOOKAHEAD_P")  // 48 -> 0.99 ms, 8 -> 1.37
@@ -573,6 +589,8 @@ std::vector<char> jit_chip_code(const ChipDesc &c, const std::string &arch_name)
     if (dir.empty() || !read_cached_code(dir + "/" + fname, code)) {
         code = compile_source(src, c.name, arch_name);
         if (!dir.empty()) write_cached_code(dir, fname, code);
+    } else if (getenv("ZKM_JIT_TOUCH")) {
+        utime((dir + "/" + fname).c_str(), nullptr);  // the cache prefill prunes files it did not touch
     }
     std::lock_guard<std::mutex> g(g_cache_mu);
     g_cache[key] = code;

@@ -838,17 +838,24 @@ __device__ __forceinline__ void from_ldsb(const uint32_t *x, uint32_t v[16], uin
 template <bool DIT, int MODE>
 __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                         int logS, const uint32_t *__restrict__ tw,
-                                                        uint32_t tw_words) {
+                                                        uint32_t tw_words, uint32_t nv, int remap) {
     using namespace s9;
     constexpr bool SWZ = DIT && MODE == MODE_BITREV_OUT;
     __shared__ uint32_t x[512 * 32];
     const uint32_t S = 1u << logS, S4 = S * 4;
-    const uint32_t outer = blockIdx.x >> (logS - 5);
-    const uint32_t c0 = (blockIdx.x & ((S >> 5) - 1)) * 32;
+    // XCD-aware order: workgroup i runs on XCD i mod 8, so XCD x takes the contiguous range
+    // [x total/8, (x+1) total/8) of (tile, column) pairs, columns fastest: the columns of one tile
+    // run back to back on one XCD and read the tile's twiddles from its L2 instead of HBM
+    const uint32_t total = gridDim.x, lin = blockIdx.x;
+    const uint32_t vid = (total & 7) ? lin : (lin & 7) * (total >> 3) + (lin >> 3);
+    const uint32_t ntile = total / nv;
+    const uint32_t col = remap ? vid % nv : lin / ntile, tile = remap ? vid / nv : lin % ntile;
+    const uint32_t outer = tile >> (logS - 5);
+    const uint32_t c0 = (tile & ((S >> 5) - 1)) * 32;
     const uint32_t base = outer * 512u * S;
     const uint32_t t = threadIdx.x & 31, u = threadIdx.x >> 5;
     const uint32_t ct = c0 + t;
-    const auto rsrc = mkrs(src + ms.off(blockIdx.y) + base, 512u * S4);
+    const auto rsrc = mkrs(src + ms.off(col) + base, 512u * S4);
     const auto rtw = mkrs(tw, tw_words * 4);
     const uint32_t vLL = ct * 4;                    // twiddle offsets per layout / network
     const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4, vLM1 = (((2 * u + 1) & 7) * S + ct) * 4;
@@ -874,7 +881,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
         net8b<true, LH>(v, rtw, vLH, 0, S4);
         net8b<true, LH>(v + 8, rtw, vLH, 32 * S4, S4);
         if (MODE == MODE_PLAIN) {
-            const auto rdst = mkrs(dst + md.off(blockIdx.y) + base, 512u * S4);
+            const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
 #pragma unroll
             for (int n = 0; n < 2; n++)
 #pragma unroll
@@ -883,7 +890,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
             __syncthreads();
             to_ldsb<LH, SWZ>(x, v, u, t);
             __syncthreads();
-            const auto rdst = mkrs(dst + md.off(blockIdx.y), 512u * S4);
+            const auto rdst = mkrs(dst + md.off(col), 512u * S4);
             const uint32_t q = threadIdx.x & 511, hb = threadIdx.x >> 9, rq = rev_bits(q, 9);
             const uint32_t vo = (((rev_bits(c0, logS) + (hb << (logS - 1))) << 9) + q) * 4;
 #pragma unroll
@@ -911,7 +918,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
         from_ldsb<LL, false>(x, v, u, t);
         net8b<false, LL>(v, rtw, vLL, 0, S4);
         net8b<false, LL>(v + 8, rtw, vLL, 0, S4);
-        const auto rdst = mkrs(dst + md.off(blockIdx.y) + base, 512u * S4);
+        const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
 #pragma unroll
         for (int n = 0; n < 2; n++)
 #pragma unroll
@@ -933,15 +940,17 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     ARG_CHECK((1 << logS) >= T, "strided pass narrower than its tile");
     dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
     if (logR == 9 && tw_words && mode != MODE_TWIST_OUT) {  // buffer-addressed register tiles
+        const dim3 g1(g.x * nv);  // one dimension: (tile, column) remapped in the kernel
+        static const int remap = getenv("ZKM_NTT_NOREMAP") ? 0 : 1;  // A/B knob
         if (!DIT)
-            hipLaunchKernelGGL((k_ntt_s9b<false, MODE_PLAIN>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                               tw_words);
+            hipLaunchKernelGGL((k_ntt_s9b<false, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tw_words, nv, remap);
         else if (mode == MODE_PLAIN)
-            hipLaunchKernelGGL((k_ntt_s9b<true, MODE_PLAIN>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                               tw_words);
+            hipLaunchKernelGGL((k_ntt_s9b<true, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tw_words, nv, remap);
         else
-            hipLaunchKernelGGL((k_ntt_s9b<true, MODE_BITREV_OUT>), g, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
-                               tw, tw_words);
+            hipLaunchKernelGGL((k_ntt_s9b<true, MODE_BITREV_OUT>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
+                               tw, tw_words, nv, remap);
         HIP_CHECK(hipGetLastError());
         return;
     }
