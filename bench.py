@@ -172,51 +172,36 @@ def pmc_in_run(args, timeout_s=240):
                 "sq": sq.get(k)} for k, v in out.items()}
 
 
-# one rocprofv3 pass (8 SQ + 2 GRBM counters at most): VALU instructions and VALU-active quad-cycles summed
-# over the waves, waves, and the GPU-busy cycles summed over the 8 XCDs (MI355X_MICROARCH.md)
-SQ_COUNTERS = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")
+# one rocprofv3 pass (at most 8 SQ + 2 GRBM counters): VALU instructions and waves summed over the
+# dispatch, and the GPU-busy cycles summed over the 8 XCDs (MI355X_MICROARCH.md)
+SQ_COUNTERS = ("SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE")
 
 
-def valu_counters(pmc, kernel="k_hash_leaves"):
-    """Counter-derived VALU figures of a kernel over one proof: instructions per wave, the VALU-busy
-    fraction SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) (quad-cycles -> cycles; busy
-    cycles per XCD), and the issue fraction SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) x the static
-    mean issue cost per instruction / the same cycle budget."""
+def valu_counters(pmc, ms_per_proof, kernel="k_hash_leaves"):
+    """Counter-derived VALU figures of a kernel over one proof (its PMC child run): VALU instructions per
+    wave (SQ_INSTS_VALU / SQ_WAVES), busy cycles per XCD (GRBM_GUI_ACTIVE / 8), the effective clock
+    (those cycles over the kernel's time in this run's profiled region) and the issue fraction
+    SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) x the mean issue cost per instruction of the
+    permutation's ISA / (1024 SIMDs x busy cycles): how full the VALU issue ports were at the clock the
+    chip actually ran."""
     if not pmc or kernel not in pmc or not pmc[kernel].get("sq"):
         return None
     c = pmc[kernel]["sq"]
     cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
     if not cyc or not c.get("SQ_WAVES"):
         return None
-    budget = 1024.0 * cyc
     out = {"source": "rocprofv3 --pmc " + " ".join(SQ_COUNTERS) + " in this run",
            "valu_insts_per_wave": round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1),
-           "active_valu_frac": round(4.0 * c["SQ_ACTIVE_INST_VALU"] / budget, 4),
-           "busy_cycles_per_xcd": round(cyc)}
+           "busy_cycles_per_xcd": round(cyc),
+           "effective_clock_ghz": round(cyc / (ms_per_proof / 1e3) / 1e9, 3) if ms_per_proof else None}
     f = os.path.join(ROOT, "zkmips_amd", "isa_p2.json")
     if os.path.exists(f):
         j = json.load(open(f))
         if j.get("valu_instructions"):
             w = j["issue_slots"] / j["valu_instructions"]
-            out["issue_frac"] = round(c["SQ_INSTS_VALU"] * 2.0 * w / budget, 4)
+            out["issue_frac"] = round(c["SQ_INSTS_VALU"] * 2.0 * w / (1024.0 * cyc), 4)
             out["mean_issue_cost"] = round(w, 3)
     return out
-
-
-def stage_traffic(pmc, stage):
-    """(HBM bytes per proof, launches per proof) of the kernels a profiled stage brackets."""
-    if not pmc:
-        return None, 0
-    pre = STAGE_KERNELS.get(stage, ())
-    b = n = 0
-    for k, v in pmc.items():
-        if k.startswith(pre):
-            b += v["bytes_per_proof"]
-            n += v["launches_per_proof"]
-    return (b, n) if n else (None, 0)
-
-
-VALU_PEAK_TSLOTS = 256 * 4 * 32 * 2.4e9 / 1e12  # CUs x SIMDs x SIMD-32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
 
 
 def valu_roofline(perms, ms):
@@ -1098,7 +1083,7 @@ def main():
                 "traffic_source": "rocprofv3 FETCH_SIZE/WRITE_SIZE passes in this run (2xFETCH+WRITE)" if tb else None}
     if dom == "merkle_leaves" and "merkle_leaves_perms" in prof:
         roofline["valu"] = valu_roofline(prof["merkle_leaves_perms"][2], ms)
-        vc = valu_counters(pmc)
+        vc = valu_counters(pmc, ms / nprof)
         if roofline["valu"] is not None and vc:
             roofline["valu"]["counters"] = vc
 

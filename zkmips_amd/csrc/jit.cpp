@@ -382,10 +382,11 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
 // 156-203): per batch b, s_b = sum_i m_i / rlc_i as num_b / den_b, built incrementally exactly as
 // the interpreter kernel; the nb denominators share ONE extension-field inversion (prefix
 // products, Montgomery's trick), then the row total goes to rowsum for the running-sum scan.
-// launch bounds of the LogUp kernels; ZKM_JIT_PERM_WAVES=w asks for w waves per SIMD (register cap)
+// launch bounds of the LogUp kernels: 2 waves per SIMD (a 256-register cap; the unbounded kernel takes
+// 267 and runs one wave per SIMD: FibCpu 1.10 -> 0.89 ms); ZKM_JIT_PERM_WAVES=w overrides (0: no cap)
 std::string perm_bounds() {
     const char *e = getenv("ZKM_JIT_PERM_WAVES");
-    const int w = e ? atoi(e) : 0;
+    const int w = e ? atoi(e) : 2;
     return w > 0 ? "__launch_bounds__(256, " + std::to_string(w) + ")" : "__launch_bounds__(256)";
 }
 

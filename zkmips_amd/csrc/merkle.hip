@@ -109,6 +109,7 @@ void launch_poseidon2_batch(uint32_t *d, uint64_t n, hipStream_t s) {
 static constexpr uint64_t SMALL16 = 8192;  // levels with <= SMALL16 nodes use the 16-lane form
 static constexpr int NT_TOP = 1024;
 static constexpr uint64_t TOP_MAX = NT_TOP / 16;  // levels with <= TOP_MAX nodes: one workgroup
+static constexpr uint64_t SUB16 = 32768;          // levels with <= SUB16 nodes: k_subtree16
 
 __global__ __launch_bounds__(NT) void k_compress16(const uint32_t *__restrict__ prev, uint32_t *__restrict__ out,
                                                    uint64_t h) {
@@ -148,6 +149,33 @@ __global__ __launch_bounds__(NT_TOP) void k_tree_top(const uint32_t *__restrict_
     }
 }
 
+// Up to 7 levels above `prev` (2h child digests) in one launch: workgroup b owns the subtree whose
+// bottom is nodes [m b, m b + m) of the first level (m = min(h, 64)), one node per 16-lane row; level k
+// of the launch has h >> k nodes, stored contiguously from out + 8 (h (2 - 2^(1-k))) and kept in LDS for
+// the next level.  A wave whose four rows have no node at a level skips the permutation (uniform
+// branch), so the upper levels of a subtree run with the SIMDs free for the waves that work.
+__global__ __launch_bounds__(NT_TOP) void k_subtree16(const uint32_t *__restrict__ prev, uint64_t h, int nlev,
+                                                      uint32_t *__restrict__ out) {
+    __shared__ uint32_t buf[2][TOP_MAX * 8];
+    const int g = threadIdx.x >> 4, l = threadIdx.x & 15, wave_g0 = (threadIdx.x >> 6) * 4;
+    const p2x16::Lane c = p2x16::lane_consts(l);
+    const uint64_t m = h < TOP_MAX ? h : TOP_MAX;
+    uint64_t hl = h, off = 0, mk = m;
+    for (int lev = 0; lev < nlev && mk; lev++, off += hl, hl >>= 1, mk >>= 1) {
+        if ((uint64_t)wave_g0 < mk) {
+            const uint64_t node = (uint64_t)blockIdx.x * mk + g;
+            const bool act = (uint64_t)g < mk;
+            const uint32_t in = !act ? 0u : lev == 0 ? prev[node * 16 + l] : buf[(lev - 1) & 1][g * 16 + l];
+            const uint32_t x = p2x16::permute(in, c);
+            if (act && l < 8) {
+                buf[lev & 1][g * 8 + l] = x;
+                out[(off + node) * 8 + l] = x;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 static DBuf upload_cols(const std::vector<const DMat *> &group, std::vector<uint64_t> &host, hipStream_t s) {
     host.clear();
     for (const DMat *m : group)
@@ -165,6 +193,26 @@ static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
         bool later_inj = false;
         for (int k = L; k <= t.log_max; k++) later_inj |= inj[k].second != 0;
         const int ninj = inj[L].second;
+        static const bool subtree = !getenv("ZKM_NO_SUBTREE");  // A/B knob: per-level launches
+        if (subtree && h <= SUB16 && ninj == 0) {
+            // subtree launches: one node per workgroup at the top of each (up to 7 levels), never across
+            // a level with injected matrices
+            const uint64_t m = h < TOP_MAX ? h : TOP_MAX;
+            int nlev = 1;
+            while (nlev < ilog2(m) + 1 && L + nlev <= t.log_max && inj[L + nlev].second == 0) nlev++;
+            uint64_t tot = 0;
+            for (int k = 0; k < nlev; k++) tot += h >> k;
+            t.layer_store.emplace_back(tot * 8, s);
+            uint32_t *base = t.layer_store.back().p;
+            uint64_t off = 0;
+            for (int k = 0; k < nlev; k++) { t.layers[L + k] = base + off * 8; off += h >> k; }
+            hipLaunchKernelGGL(k_subtree16, dim3((unsigned)(h / m)), dim3(NT_TOP), 0, s,
+                               (const uint32_t *)t.layers[L - 1], h, nlev, base);
+            HIP_CHECK(hipGetLastError());
+            L += nlev - 1;
+            h >>= nlev - 1;
+            continue;
+        }
         if (h <= TOP_MAX && !later_inj) {
             // remaining levels L..log_max in one workgroup, one contiguous allocation
             const int nlev = t.log_max - L + 1;

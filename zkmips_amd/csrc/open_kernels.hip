@@ -387,9 +387,10 @@ void launch_inv_points(const ef &z, uint32_t s, const uint32_t *tw, uint64_t M, 
 
 // ------------------------------------------------------------------ opening dot products
 // out[col * 8 + 4p .. +4] = sum_j y_{j + p} w_j / R  (p = 1 only if with_next)
-// A workgroup takes OPEN_SEG consecutive rows and stages their 16-B weights in LDS once, then walks
-// its slab of columns OPEN_CB at a time over those rows: the weight table crosses HBM once per
-// launch, not once per column block (it is as large as four columns).  Each thread takes rows in
+// A workgroup takes OPEN_SEG consecutive rows and computes their weights w_j = (w^idx) / (z - s w_n^idx)
+// into LDS itself (Montgomery's trick over INV_CHUNK rows per thread, one EF inversion per chunk), so no
+// weight table is written to or read from HBM; then it walks its slab of columns OPEN_CB at a time over
+// those rows.  Each thread takes rows in
 // pairs (j, j + NT): per EF component the two products go into one v_mad_u64_u32 chain and one lazy
 // Montgomery reduction, accumulated unreduced in 64 bits.  Per (column, segment) partial sums are
 // reduced over the segments by k_open_sum.
@@ -400,14 +401,46 @@ __device__ __forceinline__ uint64_t pair_acc(uint64_t acc, uint32_t ya, uint32_t
     return add_w(acc, redc2(mad64(ya, wa, prod64(yb, wb))));
 }
 
+static_assert(OPEN_SEG == NT * INV_CHUNK, "one weight chunk per thread");
+
+// rows [j0 + r0, j0 + r0 + cnt) of the weight table of launch_inv_points, into LDS
+__device__ __forceinline__ void open_weights(uint4 *wl, const OpenWeights &pw, uint64_t n, uint64_t j0, uint32_t r0,
+                                             int cnt) {
+    uint32_t om[INV_CHUNK];
+    ef d[INV_CHUNK], pre[INV_CHUNK];
+#pragma unroll
+    for (int k = 0; k < INV_CHUNK; k++) {
+        const uint64_t i = j0 + r0 + k;
+        om[k] = k < cnt ? root_pow(pw.tw, n, pw.bitrev ? rev_bits((uint32_t)i, pw.log_n) : i) : ONE;
+    }
+    ef run = ef_one();
+#pragma unroll
+    for (int k = 0; k < INV_CHUNK; k++) {
+        d[k] = k < cnt ? ef_sub(pw.z, ef_base(mul(pw.s, om[k]))) : ef_one();
+        pre[k] = run;
+        run = ef_mul(run, d[k]);
+    }
+    ef iv = ef_inv(run);
+#pragma unroll
+    for (int k = INV_CHUNK - 1; k >= 0; k--) {
+        ef v = ef_mul(iv, pre[k]);
+        iv = ef_mul(iv, d[k]);
+        if (pw.mul_omega) v = ef_mul_base(v, om[k]);
+        if (k < cnt) wl[r0 + k] = make_uint4(v.c[0], v.c[1], v.c[2], v.c[3]);
+    }
+}
+
 __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
-                                                 const uint32_t *__restrict__ w, int with_next, int nseg,
-                                                 uint32_t slab, uint32_t *partial) {
+                                                 OpenWeights pw, int with_next, int nseg, uint32_t slab,
+                                                 uint32_t *partial) {
     __shared__ uint4 wl[OPEN_SEG];
     __shared__ uint32_t red[NT / 64][OPEN_CB][8];
     const uint64_t j0 = (uint64_t)blockIdx.x * OPEN_SEG;
     const uint32_t len = (uint32_t)(n - j0 < (uint64_t)OPEN_SEG ? n - j0 : OPEN_SEG);
-    for (uint32_t r = threadIdx.x; r < len; r += NT) wl[r] = ((const uint4 *)w)[j0 + r];
+    {
+        const uint32_t r0 = threadIdx.x * INV_CHUNK;
+        if (r0 < len) open_weights(wl, pw, n, j0, r0, (int)(len - r0 < (uint32_t)INV_CHUNK ? len - r0 : INV_CHUNK));
+    }
     __syncthreads();
     const uint32_t c_begin = blockIdx.y * slab;
     const uint32_t c_end = c_begin + slab < ncols ? c_begin + slab : ncols;
@@ -501,7 +534,7 @@ __global__ __launch_bounds__(64) void k_open_sum(const uint32_t *__restrict__ pa
     if (lane < 8) out[(uint64_t)col * 8 + lane] = r[lane];
 }
 
-void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next,
+void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const OpenWeights &w, bool with_next,
                      uint32_t *out, hipStream_t s) {
     if (!ncols) return;
     const int nseg = (int)((n + OPEN_SEG - 1) / OPEN_SEG);
@@ -519,45 +552,84 @@ void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const u
 }
 
 // ------------------------------------------------------------------ FRI reduced openings
-// ro[i] += sum_m sum_p (B_{m,p} - A_{m,p} S_m(i)) * inv_p[i],  S_m(i) = sum_c alpha^c y_{m,c}[i]
-// terms: per matrix: [ncols, col table offset, npts, (pt, A(4), B(4)) x npts] (words)
+// ro[i] = sum_m sum_p (B_{m,p} - A_{m,p} S_m(i)) / (z_p - x_i),  S_m(i) = sum_c alpha^c y_{m,c}[i],
+// x_i = 3 w_h^rev(i) (the LDE row's point).  terms: per matrix: [ncols, col table offset, npts,
+// (pt, A(4), B(4)) x npts] (words).  One launch per height writes ro outright (no accumulate).  A thread
+// takes RED_ROWS rows i + k T (T = the grid's threads: every load instruction stays one coalesced row
+// range) and inverts their 2 RED_ROWS denominators together (Montgomery's trick, one EF inversion),
+// so no table of inverses crosses HBM.  One row per thread: 50 VGPRs, 8 waves per SIMD; four rows took
+// 177 VGPRs and ran 2.2x slower (the kernel is bound by the loads in flight, not the inversions).
+static constexpr int RED_ROWS = 1;
 __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (i >= a.h) return;
-    ef t0 = ef_zero(), t1 = ef_zero();
-    const uint32_t *d = a.desc;
-    for (uint32_t m = 0; m < a.nmats; m++) {
-        const uint32_t ncols = d[0], coff = d[1], npts = d[2];
-        // S = sum_c alpha^c y_c / R: the (uniform) alpha^c split into 16-bit halves, eight
-        // v_mad_u64_u32 per element (SGPR multipliers) and no reduction until the matrix ends
-        EfAcc acc;
-        acc.zero();
-        uint32_t c = 0;
-        for (; c + 8 <= ncols; c += 8) {  // 8 loads in flight
-            uint32_t v[8];
+    const uint64_t T = (uint64_t)gridDim.x * NT, i0 = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    ef t0[RED_ROWS], t1[RED_ROWS];
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = ((const uint32_t *)a.cols[coff + c + k])[i];
+    for (int k = 0; k < RED_ROWS; k++) {
+        const uint64_t i = i0 + k * T;
+        t0[k] = ef_zero();
+        t1[k] = ef_zero();
+        if (i >= a.h) continue;
+        const uint32_t *d = a.desc;
+        for (uint32_t m = 0; m < a.nmats; m++) {
+            const uint32_t ncols = d[0], coff = d[1], npts = d[2];
+            // S = sum_c alpha^c y_c / R: the (uniform) alpha^c split into 16-bit halves, eight
+            // v_mad_u64_u32 per element (SGPR multipliers) and no reduction until the matrix ends
+            EfAcc acc;
+            acc.zero();
+            uint32_t c = 0;
+            for (; c + 8 <= ncols; c += 8) {  // 8 loads in flight
+                uint32_t v[8];
 #pragma unroll
-            for (int k = 0; k < 8; k++) acc.base(v[k], a.alpha_pows + 4 * (c + k));
+                for (int q = 0; q < 8; q++) v[q] = ((const uint32_t *)a.cols[coff + c + q])[i];
+#pragma unroll
+                for (int q = 0; q < 8; q++) acc.base(v[q], a.alpha_pows + 4 * (c + q));
+            }
+            for (; c < ncols; c++) acc.base(((const uint32_t *)a.cols[coff + c])[i], a.alpha_pows + 4 * c);
+            const ef s = acc.value();
+            const uint32_t *pp = d + 3;
+            for (uint32_t p = 0; p < npts; p++, pp += 9) {
+                ef A{{pp[1], pp[2], pp[3], pp[4]}}, B{{pp[5], pp[6], pp[7], pp[8]}};
+                ef v = ef_sub(B, ef_mul(A, s));
+                if (pp[0]) t1[k] = ef_add(t1[k], v); else t0[k] = ef_add(t0[k], v);
+            }
+            d = pp;
         }
-        for (; c < ncols; c++) acc.base(((const uint32_t *)a.cols[coff + c])[i], a.alpha_pows + 4 * c);
-        const ef s = acc.value();
-        const uint32_t *pp = d + 3;
-        for (uint32_t p = 0; p < npts; p++, pp += 9) {
-            ef A{{pp[1], pp[2], pp[3], pp[4]}}, B{{pp[5], pp[6], pp[7], pp[8]}};
-            ef v = ef_sub(B, ef_mul(A, s));
-            if (pp[0]) t1 = ef_add(t1, v); else t0 = ef_add(t0, v);
-        }
-        d = pp;
     }
-    ef r = ld_ef(a.ro + 4 * i);
-    r = ef_add(r, ef_mul(t0, ld_ef(a.inv0 + 4 * i)));
-    if (a.inv1) r = ef_add(r, ef_mul(t1, ld_ef(a.inv1 + 4 * i)));
-    st_ef(a.ro + 4 * i, r);
+    // denominators z_p - x_i of the thread's rows (rows past h: 1), one inversion for all of them
+    ef den[2 * RED_ROWS], pre[2 * RED_ROWS];
+    ef run = ef_one();
+#pragma unroll
+    for (int k = 0; k < RED_ROWS; k++) {
+        const uint64_t i = i0 + k * T;
+        const bool in = i < a.h;
+        const uint32_t x = in ? mul(a.gen, root_pow(a.tw, a.h, rev_bits((uint32_t)i, a.log_h))) : 0u;
+        den[2 * k] = in ? ef_sub(a.z0, ef_base(x)) : ef_one();
+        den[2 * k + 1] = in && a.has1 ? ef_sub(a.z1, ef_base(x)) : ef_one();
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            pre[2 * k + q] = run;
+            run = ef_mul(run, den[2 * k + q]);
+        }
+    }
+    ef iv = ef_inv(run);
+#pragma unroll
+    for (int k = RED_ROWS - 1; k >= 0; k--) {
+        const ef inv1 = ef_mul(iv, pre[2 * k + 1]);
+        iv = ef_mul(iv, den[2 * k + 1]);
+        const ef inv0 = ef_mul(iv, pre[2 * k]);
+        iv = ef_mul(iv, den[2 * k]);
+        const uint64_t i = i0 + k * T;
+        if (i < a.h) {
+            ef r = ef_mul(t0[k], inv0);
+            if (a.has1) r = ef_add(r, ef_mul(t1[k], inv1));
+            st_ef(a.ro + 4 * i, r);
+        }
+    }
 }
 
 void launch_fri_reduce(const ReduceArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_fri_reduce, dim3((unsigned)((a.h + NT - 1) / NT)), dim3(NT), 0, s, a);
+    const uint64_t threads = (a.h + RED_ROWS - 1) / RED_ROWS;
+    hipLaunchKernelGGL(k_fri_reduce, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -44,8 +44,16 @@ void launch_quotient(const QuotArgs &a, hipStream_t s);
 
 void launch_inv_points(const kb::ef &z, uint32_t s, const uint32_t *tw, uint64_t M, bool bitrev, bool mul_omega,
                        uint32_t *out, hipStream_t st);
+// the weights of an opening, w_j = (mul_omega ? w_n^idx : 1) / (z - s w_n^idx), idx = bitrev ? rev(j) : j
+// (launch_inv_points' table, generated inside the opening kernel instead)
+struct OpenWeights {
+    kb::ef z;
+    uint32_t s;
+    const uint32_t *tw;  // forward twiddles
+    int log_n, bitrev, mul_omega;
+};
 // out[col * 8 .. +8] = the (local, next-row) dot products of column col with the weights w (EF)
-void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const uint32_t *w, bool with_next,
+void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const OpenWeights &w, bool with_next,
                      uint32_t *out, hipStream_t s);
 
 struct ReduceArgs {
@@ -53,8 +61,12 @@ struct ReduceArgs {
     const uint32_t *desc;      // per-matrix descriptors
     uint32_t nmats;
     const uint32_t *alpha_pows;// alpha^c, EF
-    const uint32_t *inv0, *inv1;  // 1/(z_p - x_i), EF (inv1 may be null)
-    uint32_t *ro;              // EF accumulator, h entries
+    kb::ef z0, z1;             // the opening points (z1 = zeta w_N, used when has1)
+    int has1;
+    uint32_t gen;              // coset shift of the LDE rows (Montgomery)
+    const uint32_t *tw;        // forward twiddles: x_i = gen w_h^rev(i)
+    int log_h;
+    uint32_t *ro;              // EF reduced openings, h entries (written, not accumulated)
     uint64_t h;
 };
 void launch_fri_reduce(const ReduceArgs &a, hipStream_t s);

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <future>
 #include <numeric>
+#include <optional>
 
 #include "../../include/zkm_hip.h"
 #include "chip.hpp"
@@ -580,24 +581,13 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             for (uint64_t k = 0; k < q.W; k++) cols[q.coff + k] = (uint64_t)(uintptr_t)(q.ybase + k * q.N);
         DBuf dcols(2 * cols.size(), s), part(nparts + 1, s);
         HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s));
-        std::vector<std::pair<uint64_t, DBuf>> wtab;  // natural-order weights per trace height (shift 1)
-        std::vector<DBuf> wchunk;
         for (auto &g : groups) {
             const Pend &q = pend[g.first];
-            const uint32_t *w = nullptr;
-            if (!q.bitrev) {
-                for (auto &pr : wtab) if (pr.first == q.N) w = pr.second.p;
-                if (!w) {
-                    wtab.emplace_back(q.N, DBuf(4 * q.N, s));
-                    w = wtab.back().second.p;
-                    launch_inv_points(zeta, ONE, c.tw_fwd, q.N, false, true, (uint32_t *)w, s);
-                }
-            } else {
-                wchunk.emplace_back(4 * q.N, s);
-                w = wchunk.back().p;
-                launch_inv_points(ef_mul_base(zeta, inv(q.shift)), ONE, c.tw_fwd, q.N, true, true, (uint32_t *)w, s);
-            }
-            PROF("open_eval", s, 4.0 * q.N * g.W + 16.0 * q.N);
+            // barycentric weights w^j / (zeta' - w^j): traces in natural row order (shift 1 after the
+            // zeta / shift substitution), quotient chunks bit-reversed; generated by the kernel itself
+            const OpenWeights w{q.bitrev ? ef_mul_base(zeta, inv(q.shift)) : zeta, ONE, c.tw_fwd, ilog2(q.N),
+                                q.bitrev ? 1 : 0, 1};
+            PROF("open_eval", s, 4.0 * q.N * g.W);
             launch_open_dot((const uint64_t *)dcols.p + g.coff, (uint32_t)g.W, q.N, w, q.r->npts == 2,
                             part.p + g.poff, s);
         }
@@ -649,11 +639,8 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             if (by_h[lh].empty()) continue;
             const uint64_t H = 1ull << lh;
             const uint64_t N = H >> lb;
-            ro[lh] = DBuf(4 * H, s);
-            HIP_CHECK(hipMemsetAsync(ro[lh].p, 0, 16 * H, s));
-            // denominators 1/(z - 3 w_H^rev(i)) for z = zeta and zeta * w_N
-            DBuf inv0(4 * H, s), inv1(4 * H, s);
-            launch_inv_points(zeta, to_mont(GENERATOR), c.tw_fwd, H, true, false, inv0.p, s);
+            ro[lh] = DBuf(4 * H, s);  // written whole by this height's one k_fri_reduce
+            // the denominators 1/(z - 3 w_H^rev(i)) for z = zeta and zeta * w_N are inverted in the kernel
             const ef znext = ef_mul_base(zeta, two_adic_gen(ilog2(N)));
             bool need1 = false;
             keep_cols.emplace_back();
@@ -682,13 +669,12 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
                     pow_cnt[lh] += (int)W;
                 }
             }
-            if (need1) launch_inv_points(znext, to_mont(GENERATOR), c.tw_fwd, H, true, false, inv1.p, s);
             DBuf dcols(2 * cols.size() + 2, s), ddesc(desc.size() + 1, s);
             if (!cols.empty()) HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s));
             HIP_CHECK(hipMemcpyAsync(ddesc.p, desc.data(), desc.size() * 4, hipMemcpyHostToDevice, s));
-            ReduceArgs ra{(const uint64_t *)dcols.p, ddesc.p, (uint32_t)by_h[lh].size(), d_apow.p, inv0.p,
-                          need1 ? inv1.p : nullptr, ro[lh].p, H};
-            { PROF("fri_reduce", s, 4.0 * H * cols.size() + 16.0 * H * (need1 ? 4 : 3)); launch_fri_reduce(ra, s); }
+            ReduceArgs ra{(const uint64_t *)dcols.p, ddesc.p, (uint32_t)by_h[lh].size(), d_apow.p, zeta, znext,
+                          need1 ? 1 : 0, to_mont(GENERATOR), c.tw_fwd, ilog2(H), ro[lh].p, H};
+            { PROF("fri_reduce", s, 4.0 * H * cols.size() + 16.0 * H); launch_fri_reduce(ra, s); }
         }
         HIP_CHECK(hipStreamSynchronize(s));  // keep_cols / keep_desc / apow have been read
     }
@@ -702,7 +688,9 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
         cur = DBuf(4 * cur_n, s);
         HIP_CHECK(hipMemcpyAsync(cur.p, ro[log_max].p, 16 * cur_n, hipMemcpyDeviceToDevice, s));
     }
-    PROF("fri_commit_phase", s, 0);
+    // the commit phase only (the scope ends after the readback below, before the PoW)
+    std::optional<ProfScope> fri_prof;
+    fri_prof.emplace("fri_commit_phase", s, 0);
     // transcript on the device for the whole phase: no host round trip per round
     DBuf dchal_buf((sizeof(DevChallenger) + 3) / 4, s), droots(8 * std::max(nrounds, 1), s),
         dfargs(8 * std::max(nrounds, 1), s);
@@ -733,6 +721,7 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     HIP_CHECK(hipMemcpyAsync(fin.data(), cur.p, fin.size() * 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(hroots.data(), droots.p, hroots.size() * 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(&hc, dchal, sizeof hc, hipMemcpyDeviceToHost, s));
+    fri_prof.reset();
     HIP_CHECK(hipStreamSynchronize(s));
     for (int rd = 0; rd < nrounds; rd++) {
         memcpy(ftrees[rd].root, &hroots[8 * rd], 32);
