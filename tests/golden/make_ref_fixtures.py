@@ -10,8 +10,12 @@ where /root/reference exists; the outputs are committed, the GPU box never reads
                           usize>, shapes.rs:370-379, loaded at prover/src/lib.rs:232): byte length,
                           sha256, entry count and the decoded first/last entries.  The file itself
                           is regenerated from its entries by the oracle's serializer in the test.
+* curve_params.json    <- crates/curves/src/{weierstrass/*,uint256}.rs: each base field's MODULUS bytes,
+                          WITNESS_OFFSET, Limbs / Witness sizes and, for the curves, a_int / b_int
+                          (the FieldParameters / WeierstrassParameters the precompile chips use).
 """
 import hashlib
+import re
 import json
 import os
 
@@ -44,6 +48,27 @@ def main():
         "rule_holds": bool(np.all(keys == np.arange(n)[:, None]) and np.all(vals == np.arange(n))),
     }
     json.dump(desc, open(os.path.join(HERE, "dummy_vk_map.json"), "w"), indent=1)
+
+    params = {}
+    for name, f in (("Secp256k1", "weierstrass/secp256k1.rs"), ("Secp256r1", "weierstrass/secp256r1.rs"),
+                    ("Bn254", "weierstrass/bn254.rs"), ("Bls12381", "weierstrass/bls12_381.rs"),
+                    ("U256", "uint256.rs")):
+        src = open(os.path.join(REF, "crates/curves/src", f)).read()
+        mod = re.search(r"const MODULUS: &'static \[u8\] = &\[(.*?)\];", src, re.S).group(1)
+        e = {"modulus_le": [int(x, 0) for x in re.findall(r"0x[0-9a-fA-F]+|\d+", mod)],
+             "witness_offset_log2": int(re.search(r"WITNESS_OFFSET: usize = 1usize << (\d+)", src).group(1)),
+             "limbs": int(re.search(r"type Limbs = U(\d+)", src).group(1)),
+             "witness": int(re.search(r"type Witness = U(\d+)", src).group(1))}
+        for fn in ("a_int", "b_int"):
+            m = re.search(r"fn " + fn + r"\(\) -> BigUint \{\s*BigUint::from_slice\(&\[(.*?)\]\)", src, re.S)
+            if m:
+                e[fn + "_u32_le"] = [int(x, 0) for x in re.findall(r"0x[0-9a-fA-F]+|\d+", m.group(1))]
+            else:
+                m = re.search(r"fn " + fn + r"\(\) -> BigUint \{\s*BigUint::from\((\d+)u32\)", src)
+                if m:
+                    e[fn + "_u32_le"] = [int(m.group(1))]
+        params[name] = e
+    json.dump(params, open(os.path.join(HERE, "curve_params.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":

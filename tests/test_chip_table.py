@@ -19,6 +19,7 @@ import pytest
 from tests import _oracle as O
 from zkmips_amd import mips_alu as A
 from zkmips_amd import mips_core as MC
+from zkmips_amd import mips_ec as EC
 from zkmips_amd import mips_edwards as ED
 from zkmips_amd import mips_memory as MM
 from zkmips_amd import mips_syscall as SY
@@ -62,6 +63,25 @@ CHIPS = {
     "EdDecompress": (ED.ed_decompress_chip, 0, 1566, 372, 1, True, "syscall/precompiles/edwards/ed_decompress.rs:202",
                      "syscall/precompiles/edwards/ed_decompress.rs:262"),
 }
+_PRE = "syscall/precompiles/"
+for _curve in ("Secp256k1", "Secp256r1", "Bn254", "Bls12381"):
+    _big = _curve == "Bls12381"
+    CHIPS[f"{_curve}AddAssign"] = (lambda c=_curve: EC.weierstrass_add_chip(c), 0, 3089 if _big else 2049,
+                                   737 if _big else 489, 1, True, _PRE + "weierstrass/weierstrass_add.rs:127",
+                                   _PRE + "weierstrass/weierstrass_add.rs:263")
+    CHIPS[f"{_curve}DoubleAssign"] = (lambda c=_curve: EC.weierstrass_double_chip(c), 0, 3440 if _big else 2280,
+                                      831 if _big else 551, 1, True, _PRE + "weierstrass/weierstrass_double.rs:142",
+                                      _PRE + "weierstrass/weierstrass_double.rs:288")
+for _field, _shape in (("Bn254", ((372, 81), (734, 160), (1485, 348))),
+                       ("Bls12381", ((556, 121), (1102, 240), (2237, 524)))):
+    CHIPS[EC.FP_NAME[_field]] = (lambda f=_field: EC.fp_op_chip(f), 0, *_shape[0], 1, True,
+                                 _PRE + "fptower/fp.rs:76", _PRE + "fptower/fp.rs:192")
+    CHIPS[EC.FP2_ADDSUB_NAME[_field]] = (lambda f=_field: EC.fp2_addsub_chip(f), 0, *_shape[1], 1, True,
+                                         _PRE + "fptower/fp2_addsub.rs:79", _PRE + "fptower/fp2_addsub.rs:210")
+    CHIPS[EC.FP2_MUL_NAME[_field]] = (lambda f=_field: EC.fp2_mul_chip(f), 0, *_shape[2], 1, True,
+                                      _PRE + "fptower/fp2_mul.rs:122", _PRE + "fptower/fp2_mul.rs:227")
+CHIPS["Uint256MulMod"] = (EC.uint256_mul_chip, 0, 480, 98, 1, True, _PRE + "uint256/air.rs:93",
+                          _PRE + "uint256/air.rs:218")
 # precompile chips are costed per call: rows per event x per-row cost (mips/mod.rs:216-222)
 ROWS_PER_EVENT = {"ShaExtend": 48, "ShaCompress": 80}
 

@@ -177,38 +177,47 @@ class Device:
         return ms.value
 
 
-def prefill_jit_cache(machines, prune: bool = True) -> int:
+def _compile_blob(blob) -> int:
+    """Worker of prefill_jit_cache: compile one single-chip machine blob into the code-object cache."""
+    n = C.c_uint64(0)
+    blob = np.ascontiguousarray(blob, np.uint32)
+    rc = lib().zkm_quotient_jit_compile(blob.ctypes.data_as(C.c_void_p), C.c_size_t(blob.size), C.byref(n))
+    if rc != 0:
+        raise ZkmError(f"quotient JIT compile failed ({rc}): {lib().zkm_last_error().decode()}")
+    return n.value
+
+
+def prefill_jit_cache(machines, prune: bool = True, workers: int = None) -> int:
     """Compile every chip's quotient/permutation kernels of `machines` for gfx950 into the JIT's on-disk
-    code-object cache (zkmips_amd/jit_cache, see csrc/jit.cpp); no device needed.  The machines compile
-    concurrently (their chips do too, inside the library).  With `prune`, code objects of the default
-    cache directory that none of these machines uses any more (older kernel sources) are deleted.
-    Returns code bytes."""
-    import threading
+    code-object cache (zkmips_amd/jit_cache, see csrc/jit.cpp); no device needed.  hiprtc serialises
+    compiles inside one process, so the distinct chips (one single-chip machine blob each, largest first)
+    compile in a pool of processes.  With `prune`, code objects of the default cache directory that none
+    of these machines uses any more (older kernel sources) are deleted.  Returns code bytes."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
     import time
-    blobs = [np.ascontiguousarray(m.blob(), np.uint32) for m in machines]
+    from .machine import MAGIC, VERSION
+    blobs, seen = [], set()
+    for m in machines:
+        for c in m.chips:
+            w = c.words()
+            key = (c.name, m.num_pv, hash(tuple(w)))
+            if key not in seen:
+                seen.add(key)
+                blobs.append(np.asarray([MAGIC, VERSION, m.num_pv, 1] + list(w), np.uint32))
+    blobs.sort(key=lambda b: -b.size)
     cache = os.path.join(os.path.dirname(os.path.abspath(__file__)), "jit_cache")
     prune = prune and "ZKM_JIT_CACHE" not in os.environ and os.path.isdir(cache)
     t0 = time.time() - 1.0
     if prune:
-        os.environ["ZKM_JIT_TOUCH"] = "1"  # cache hits refresh their file's mtime
-    res = [None] * len(blobs)
-
-    def work(i):
-        n = C.c_uint64(0)
-        rc = lib().zkm_quotient_jit_compile(blobs[i].ctypes.data_as(C.c_void_p), C.c_size_t(blobs[i].size), C.byref(n))
-        res[i] = (rc, n.value)
-    th = [threading.Thread(target=work, args=(i,)) for i in range(len(blobs))]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    if prune:
-        del os.environ["ZKM_JIT_TOUCH"]
-    total = 0
-    for rc, n in res:
-        if rc != 0:
-            raise ZkmError(f"quotient JIT compile failed ({rc}): {lib().zkm_last_error().decode()}")
-        total += n
+        os.environ["ZKM_JIT_TOUCH"] = "1"  # cache hits refresh their file's mtime (the workers inherit it)
+    try:
+        n = workers or max(1, min(len(blobs), os.cpu_count() or 1, 16))
+        with cf.ProcessPoolExecutor(n, mp_context=mp.get_context("spawn")) as ex:
+            total = sum(ex.map(_compile_blob, blobs))
+    finally:
+        if prune:
+            del os.environ["ZKM_JIT_TOUCH"]
     if prune:
         for f in os.listdir(cache):
             path = os.path.join(cache, f)

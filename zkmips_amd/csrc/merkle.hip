@@ -13,6 +13,7 @@
 #include "internal.hpp"
 #include "open_kernels.hpp"
 #include "p2.cuh"
+#include "fri_chal.cuh"
 #include "prof.hpp"
 
 namespace zkm {
@@ -109,7 +110,10 @@ void launch_poseidon2_batch(uint32_t *d, uint64_t n, hipStream_t s) {
 static constexpr uint64_t SMALL16 = 8192;  // levels with <= SMALL16 nodes use the 16-lane form
 static constexpr int NT_TOP = 1024;
 static constexpr uint64_t TOP_MAX = NT_TOP / 16;  // levels with <= TOP_MAX nodes: one workgroup
-static constexpr uint64_t SUB16 = 32768;          // levels with <= SUB16 nodes: k_subtree16
+static uint64_t sub16_max() {  // levels with <= this many nodes: k_subtree16 (ZKM_SUB16 overrides)
+    static const uint64_t v = getenv("ZKM_SUB16") ? strtoull(getenv("ZKM_SUB16"), nullptr, 10) : 32768;
+    return v;
+}
 
 __global__ __launch_bounds__(NT) void k_compress16(const uint32_t *__restrict__ prev, uint32_t *__restrict__ out,
                                                    uint64_t h) {
@@ -154,9 +158,13 @@ __global__ __launch_bounds__(NT_TOP) void k_tree_top(const uint32_t *__restrict_
 // of the launch has h >> k nodes, stored contiguously from out + 8 (h (2 - 2^(1-k))) and kept in LDS for
 // the next level.  A wave whose four rows have no node at a level skips the permutation (uniform
 // branch), so the upper levels of a subtree run with the SIMDs free for the waves that work.
+// With chal (the launch that ends at a FRI tree's root, one workgroup), the round's transcript step
+// follows in the same workgroup (fri_chal.cuh).
 __global__ __launch_bounds__(NT_TOP) void k_subtree16(const uint32_t *__restrict__ prev, uint64_t h, int nlev,
-                                                      uint32_t *__restrict__ out) {
+                                                      uint32_t *__restrict__ out, DevChallenger *chal,
+                                                      uint32_t *root_out, uint32_t *fargs) {
     __shared__ uint32_t buf[2][TOP_MAX * 8];
+    __shared__ ChalShared sh;
     const int g = threadIdx.x >> 4, l = threadIdx.x & 15, wave_g0 = (threadIdx.x >> 6) * 4;
     const p2x16::Lane c = p2x16::lane_consts(l);
     const uint64_t m = h < TOP_MAX ? h : TOP_MAX;
@@ -174,6 +182,7 @@ __global__ __launch_bounds__(NT_TOP) void k_subtree16(const uint32_t *__restrict
         }
         __syncthreads();
     }
+    if (chal) fri_chal_block(sh, chal, buf[(nlev - 1) & 1], root_out, fargs);
 }
 
 static DBuf upload_cols(const std::vector<const DMat *> &group, std::vector<uint64_t> &host, hipStream_t s) {
@@ -186,7 +195,9 @@ static DBuf upload_cols(const std::vector<const DMat *> &group, std::vector<uint
 }
 
 // Levels 1..log_max above layers[0]; inj[L] = column table of matrices injected at level L.
-static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<const DBuf *, int>> &inj, hipStream_t s) {
+static bool build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<const DBuf *, int>> &inj, hipStream_t s,
+                         const FriChal *fc = nullptr) {
+    bool chal_done = false;
     uint64_t h = maxh;
     for (int L = 1; L <= t.log_max; L++) {
         h >>= 1;
@@ -194,7 +205,7 @@ static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
         for (int k = L; k <= t.log_max; k++) later_inj |= inj[k].second != 0;
         const int ninj = inj[L].second;
         static const bool subtree = !getenv("ZKM_NO_SUBTREE");  // A/B knob: per-level launches
-        if (subtree && h <= SUB16 && ninj == 0) {
+        if (subtree && h <= sub16_max() && ninj == 0) {
             // subtree launches: one node per workgroup at the top of each (up to 7 levels), never across
             // a level with injected matrices
             const uint64_t m = h < TOP_MAX ? h : TOP_MAX;
@@ -206,9 +217,12 @@ static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
             uint32_t *base = t.layer_store.back().p;
             uint64_t off = 0;
             for (int k = 0; k < nlev; k++) { t.layers[L + k] = base + off * 8; off += h >> k; }
+            const bool top = fc && L + nlev - 1 == t.log_max && h / m == 1;
             hipLaunchKernelGGL(k_subtree16, dim3((unsigned)(h / m)), dim3(NT_TOP), 0, s,
-                               (const uint32_t *)t.layers[L - 1], h, nlev, base);
+                               (const uint32_t *)t.layers[L - 1], h, nlev, base, top ? fc->c : nullptr,
+                               top ? fc->root_out : nullptr, top ? fc->fargs : nullptr);
             HIP_CHECK(hipGetLastError());
+            chal_done |= top;
             L += nlev - 1;
             h >>= nlev - 1;
             continue;
@@ -249,6 +263,7 @@ static void build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
                            inj[L].first ? (const uint64_t *)inj[L].first->p : (const uint64_t *)nullptr, ninj);
         HIP_CHECK(hipGetLastError());
     }
+    return chal_done;
 }
 
 void tree_build(DTree &t, hipStream_t s) {
@@ -299,7 +314,7 @@ void tree_build(DTree &t, hipStream_t s) {
     HIP_CHECK(hipStreamSynchronize(s));
 }
 
-void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s, bool read_root) {
+bool tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s, bool read_root, const FriChal *fc) {
     ARG_CHECK(nleaves && (nleaves & (nleaves - 1)) == 0, "leaf count must be a power of two");
     t.log_max = ilog2(nleaves);
     t.layers.assign(t.log_max + 1, nullptr);
@@ -307,10 +322,12 @@ void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s, 
     t.layer_store.push_back(std::move(leaves));
     t.layers[0] = t.layer_store.back().p;
     std::vector<std::pair<const DBuf *, int>> inj(t.log_max + 1, {nullptr, 0});
-    build_levels(t, nleaves, inj, s);
-    if (!read_root) return;
-    HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max], 32, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    const bool chal = build_levels(t, nleaves, inj, s, fc);
+    if (read_root) {
+        HIP_CHECK(hipMemcpyAsync(t.root, t.layers[t.log_max], 32, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+    return chal;
 }
 
 }  // namespace zkm

@@ -13,6 +13,7 @@
 #include "internal.hpp"
 #include "open_kernels.hpp"
 #include "p2.cuh"
+#include "fri_chal.cuh"
 
 namespace zkm {
 
@@ -650,6 +651,57 @@ __global__ __launch_bounds__(NT) void k_fri_fold(const uint32_t *cur, uint64_t h
     st_ef(next + 4 * i, r);
 }
 
+// one folded element (k_fri_fold's formula) of an h-element output
+__device__ __forceinline__ ef fri_fold_one(const uint32_t *cur, uint64_t j, uint64_t h, int log_h, const ef &half_beta,
+                                           const ef &beta2, const uint32_t *__restrict__ tw_inv, const uint32_t *ro) {
+    const uint32_t half = halve(ONE);
+    const uint32_t g = tw_inv[h + rev_bits((uint32_t)j, log_h)];
+    const ef pw = ef_mul_base(half_beta, g);
+    const ef lo = ld_ef(cur + 8 * j), hi = ld_ef(cur + 8 * j + 4);
+    ef r = ef_add(ef_mul(ef_add_base(pw, half), lo), ef_mul(ef_sub(ef_base(half), pw), hi));
+    if (ro) r = ef_add(r, ef_mul(beta2, ld_ef(ro + 4 * j)));
+    return r;
+}
+
+// The fold of round r and the leaves of round r + 1 in one pass: thread i folds next[2i], next[2i + 1]
+// (stored: the queries open them) and hashes them into leaf i (one permutation)
+__global__ __launch_bounds__(NT) void k_fri_fold_leaves(const uint32_t *cur, uint64_t h, int log_h,
+                                                        const uint32_t *fargs, const uint32_t *__restrict__ tw_inv,
+                                                        const uint32_t *ro, uint32_t *next, uint32_t *leaves) {
+    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= h / 2) return;
+    const ef hb = ld_ef(fargs), b2 = ld_ef(fargs + 4);
+    const ef a = fri_fold_one(cur, 2 * i, h, log_h, hb, b2, tw_inv, ro);
+    const ef b = fri_fold_one(cur, 2 * i + 1, h, log_h, hb, b2, tw_inv, ro);
+    st_ef(next + 8 * i, a);
+    st_ef(next + 8 * i + 4, b);
+    uint32_t s[16];
+#pragma unroll
+    for (int e = 0; e < 4; e++) { s[e] = a.c[e]; s[4 + e] = b.c[e]; s[8 + e] = 0; s[12 + e] = 0; }
+    p2::permute(s);
+    uint4 *o = (uint4 *)(leaves + 8 * i);
+    o[0] = make_uint4(s[0], s[1], s[2], s[3]);
+    o[1] = make_uint4(s[4], s[5], s[6], s[7]);
+}
+// 16-lane form for small rounds: lane l < 8 folds element 2i + l / 4 and keeps component l % 4
+__global__ __launch_bounds__(NT) void k_fri_fold_leaves16(const uint32_t *cur, uint64_t h, int log_h,
+                                                          const uint32_t *fargs, const uint32_t *__restrict__ tw_inv,
+                                                          const uint32_t *ro, uint32_t *next, uint32_t *leaves) {
+    const uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    const uint64_t i = t >> 4;
+    const int l = (int)(t & 15);
+    const bool act = i < h / 2 && l < 8;
+    uint32_t v = 0;
+    if (act) {
+        const uint64_t j = 2 * i + (l >> 2);
+        const ef r = fri_fold_one(cur, j, h, log_h, ld_ef(fargs), ld_ef(fargs + 4), tw_inv, ro);
+        v = r.c[l & 3];
+        next[4 * j + (l & 3)] = v;
+    }
+    const uint32_t x = p2x16::permute(v, p2x16::lane_consts(l));  // all lanes take part
+    if (act) leaves[8 * i + l] = x;
+}
+
 // leaf i = sponge(cur[2i] || cur[2i+1]) (8 elements: one permutation)
 __global__ __launch_bounds__(NT) void k_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out) {
     const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
@@ -672,55 +724,30 @@ __global__ __launch_bounds__(NT) void k_fri_leaves16(const uint32_t *cur, uint64
     if (i < h && l < 8) out[8 * i + l] = x;
 }
 
-// One FRI round of the Fiat-Shamir transcript on the device (DuplexChallenger semantics of the
-// host Challenger: observe the 8 root words, sample beta as 4 words): keeps the commit phase free
-// of host round trips.  One wavefront; the permutation runs in the 16-lane form (all four rows
-// compute the same state).  Also records the root for the proof and the fold arguments.
+// One FRI round of the Fiat-Shamir transcript on the device (fri_chal.cuh), for rounds whose tree
+// top did not run it (a one-leaf tree)
 __global__ __launch_bounds__(64) void k_fri_chal(DevChallenger *c, const uint32_t *root, uint32_t *root_out,
                                                  uint32_t *fargs) {
-    __shared__ uint32_t st[16], in[8], out[8];
-    __shared__ int nin, nout;
-    const int tid = threadIdx.x, l = tid & 15;
-    if (tid < 16) st[tid] = c->st[tid];
-    if (tid < 8) { in[tid] = c->in[tid]; out[tid] = c->out[tid]; root_out[tid] = root[tid]; }
-    if (tid == 0) { nin = (int)c->nin; nout = (int)c->nout; }
-    __syncthreads();
-    const p2x16::Lane lc = p2x16::lane_consts(l);
-    auto duplex = [&]() {
-        const uint32_t x = p2x16::permute(l < nin ? in[l] : st[l], lc);
-        __syncthreads();
-        if (tid < 16) st[tid] = x;
-        if (tid < 8) out[tid] = x;
-        if (tid == 0) { nin = 0; nout = 8; }
-        __syncthreads();
-    };
-    for (int k = 0; k < 8; k++) {  // observe(root[k])
-        if (tid == 0) { nout = 0; in[nin] = root[k]; nin++; }
-        __syncthreads();
-        if (nin == 8) duplex();
-    }
-    uint32_t beta[4];
-    for (int k = 0; k < 4; k++) {  // sample()
-        if (nin || !nout) duplex();
-        beta[k] = out[nout - 1];
-        __syncthreads();
-        if (tid == 0) nout--;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        const ef b{{beta[0], beta[1], beta[2], beta[3]}};
-        st_ef(fargs, ef_mul_base(b, halve(ONE)));
-        st_ef(fargs + 4, ef_mul(b, b));
-    }
-    if (tid < 16) c->st[tid] = st[tid];
-    if (tid < 8) { c->in[tid] = in[tid]; c->out[tid] = out[tid]; }
-    if (tid == 0) { c->nin = (uint32_t)nin; c->nout = (uint32_t)nout; }
+    __shared__ ChalShared sh;
+    fri_chal_block(sh, c, root, root_out, fargs);
 }
 
 void launch_fri_fold(const uint32_t *cur, uint64_t h, const uint32_t *fargs, const uint32_t *tw_inv,
                      const uint32_t *ro, uint32_t *next, hipStream_t s) {
     hipLaunchKernelGGL(k_fri_fold, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s, cur, h, ilog2(h), fargs,
                        tw_inv, ro, next);
+    HIP_CHECK(hipGetLastError());
+}
+void launch_fri_fold_leaves(const uint32_t *cur, uint64_t h, const uint32_t *fargs, const uint32_t *tw_inv,
+                            const uint32_t *ro, uint32_t *next, uint32_t *leaves, hipStream_t s) {
+    ARG_CHECK(h >= 2 && (h & (h - 1)) == 0, "fold+leaves needs a power-of-two output >= 2");
+    const uint64_t nl = h / 2;
+    if (nl <= 8192)
+        hipLaunchKernelGGL(k_fri_fold_leaves16, dim3((unsigned)((nl * 16 + NT - 1) / NT)), dim3(NT), 0, s, cur, h,
+                           ilog2(h), fargs, tw_inv, ro, next, leaves);
+    else
+        hipLaunchKernelGGL(k_fri_fold_leaves, dim3((unsigned)((nl + NT - 1) / NT)), dim3(NT), 0, s, cur, h, ilog2(h),
+                           fargs, tw_inv, ro, next, leaves);
     HIP_CHECK(hipGetLastError());
 }
 void launch_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out, hipStream_t s) {

@@ -82,6 +82,14 @@ void launch_fri_chal(DevChallenger *c, const uint32_t *root, uint32_t *root_out,
 void launch_fri_fold(const uint32_t *cur, uint64_t h, const uint32_t *fargs, const uint32_t *tw_inv,
                      const uint32_t *ro, uint32_t *next, hipStream_t s);
 void launch_fri_leaves(const uint32_t *cur, uint64_t h, uint32_t *out, hipStream_t s);
+// fold into next (h elements) and hash next's pairs into the next round's h / 2 leaves
+void launch_fri_fold_leaves(const uint32_t *cur, uint64_t h, const uint32_t *fargs, const uint32_t *tw_inv,
+                            const uint32_t *ro, uint32_t *next, uint32_t *leaves, hipStream_t s);
+// the transcript step a FRI tree's top launch runs after the root (fri_chal.cuh)
+struct FriChal {
+    DevChallenger *c;
+    uint32_t *root_out, *fargs;
+};
 
 struct PowArgs {
     uint32_t state[16];
@@ -97,6 +105,8 @@ void launch_gather(const uint64_t *d_items, uint32_t nitems, uint32_t *dst, hipS
 void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst, hipStream_t s);
 // tree from a precomputed leaf digest layer (FRI commit-phase trees)
 // read_root = false: the root stays on the device (t.layers[t.log_max]); t.root is not set
-void tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s, bool read_root = true);
+// with fc, the launch that computes the root also runs the FRI transcript step; returns whether it did
+bool tree_from_leaves(DTree &t, DBuf &&leaves, uint64_t nleaves, hipStream_t s, bool read_root = true,
+                      const FriChal *fc = nullptr);
 
 }  // namespace zkm

@@ -371,6 +371,7 @@ __device__ __forceinline__ uint32_t dpp(uint32_t x) {
 }
 constexpr int QP(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }
 constexpr int ROR(int k) { return 0x120 + k; }
+constexpr int BCAST0 = 0x150;  // row_newbcast:0 (lane 0 of each 16-lane row to the whole row)
 
 // external layer: M4 = circ(2,3,1,1) per 4-lane block (n_j = quad_sum + x_j + 2 x_{j+1}),
 // then the column sums over the four blocks (lanes j, j+4, j+8, j+12)
@@ -409,13 +410,16 @@ __device__ __forceinline__ uint32_t permute(uint32_t x, const Lane &c) {
     for (int r = 0; r < 4; r++) x = external(cube(add(x, c.rc[r])));
 #pragma unroll
     for (int r = 0; r < 13; r++) {
+        // the row sum of the lanes other than 0 does not wait for lane 0's s-box: it runs beside the
+        // cube, and lane 0's s-box output joins it by one broadcast (row_newbcast:0)
         const uint32_t y = cube(add(x, p2::RC.inr[r]));
-        x = (c.l == 0) ? y : x;
-        uint32_t s = add(x, dpp<ROR(1)>(x));
+        uint32_t s = (c.l == 0) ? 0u : x;
+        s = add(s, dpp<ROR(1)>(s));
         s = add(s, dpp<ROR(2)>(s));
         s = add(s, dpp<ROR(4)>(s));
         s = add(s, dpp<ROR(8)>(s));
-        x = add(mul(x, c.dg), s);
+        s = add(s, dpp<BCAST0>(y));
+        x = add(mul((c.l == 0) ? y : x, c.dg), s);
     }
 #pragma unroll
     for (int r = 4; r < 8; r++) x = external(cube(add(x, c.rc[r])));

@@ -702,18 +702,30 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
     hc.nout = (uint32_t)ch.nout;
     DevChallenger *dchal = reinterpret_cast<DevChallenger *>(dchal_buf.p);
     HIP_CHECK(hipMemcpyAsync(dchal, &hc, sizeof hc, hipMemcpyHostToDevice, s));
+    // per round: the tree over the round's leaves, whose top launch also runs the transcript step (root
+    // observed, beta sampled), then one pass that folds and already hashes the next round's leaves
+    DBuf leaves;
     for (int rd = 0; rd < nrounds; rd++) {
         const int lf = log_max - 1 - rd;
         const uint64_t h = cur_n >> 1;
-        DBuf leaves(8 * h, s);
-        launch_fri_leaves(cur.p, h, leaves.p, s);
+        if (rd == 0) {
+            leaves = DBuf(8 * h, s);
+            launch_fri_leaves(cur.p, h, leaves.p, s);
+        }
         // keep the folded-from vector: queries open (lo, hi) pairs of it
         ftrees[rd].owned.push_back(std::move(cur));
-        tree_from_leaves(ftrees[rd], std::move(leaves), h, s, false);
-        launch_fri_chal(dchal, ftrees[rd].layers[ftrees[rd].log_max], droots.p + 8 * rd, dfargs.p + 8 * rd, s);
+        const FriChal fc{dchal, droots.p + 8 * rd, dfargs.p + 8 * rd};
+        if (!tree_from_leaves(ftrees[rd], std::move(leaves), h, s, false, &fc))
+            launch_fri_chal(dchal, ftrees[rd].layers[ftrees[rd].log_max], droots.p + 8 * rd, dfargs.p + 8 * rd, s);
         DBuf next(4 * h, s);
-        launch_fri_fold(ftrees[rd].owned.back().p, h, dfargs.p + 8 * rd, c.tw_inv, ro[lf].p ? ro[lf].p : nullptr,
-                        next.p, s);
+        const uint32_t *rof = ro[lf].p ? ro[lf].p : nullptr;
+        if (rd + 1 < nrounds) {
+            leaves = DBuf(8 * (h / 2), s);
+            launch_fri_fold_leaves(ftrees[rd].owned.back().p, h, dfargs.p + 8 * rd, c.tw_inv, rof, next.p, leaves.p,
+                                   s);
+        } else {
+            launch_fri_fold(ftrees[rd].owned.back().p, h, dfargs.p + 8 * rd, c.tw_inv, rof, next.p, s);
+        }
         cur = std::move(next);
         cur_n = h;
     }

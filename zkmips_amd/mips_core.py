@@ -1134,9 +1134,10 @@ def core_machine() -> MachineDesc:
     # MipsAir::get_airs_and_costs order (crates/core/machine/src/mips/mod.rs:207-437): Cpu, Program, the
     # precompiles, SyscallCore/Precompile, the ALUs, Branch, Jump, SyscallInstrs, MemoryInstrs, MiscInstrs,
     # the memory chips, Global, Byte, (SysLinux,) MovCond
+    from . import mips_ec as EC
     from . import mips_edwards as ED
     return MachineDesc([cpu_chip(), program_chip(), SY.sha_extend_chip(), SY.sha_compress_chip(), ED.ed_add_chip(),
-                        ED.ed_decompress_chip(), SY.syscall_chip(True),
+                        ED.ed_decompress_chip()] + EC.chips_in_machine_order() + [SY.syscall_chip(True),
                         SY.syscall_chip(False), divrem_chip(), A.add_sub_chip(), A.bitwise_chip(), mul_chip(),
                         A.shift_right_chip(), A.shift_left_chip(), A.lt_chip(), A.clo_clz_chip(), branch_chip(),
                         jump_chip(), SY.syscall_instrs_chip(), memory_instructions_chip(), misc_instructions_chip(),
@@ -1577,7 +1578,7 @@ def _execute(prog, regs, shard, max_steps, state=None):
                     key = SY.SYS_LINUX
                 else:
                     pev = SY.PRECOMPILES[code](pm, shard, clk, bv, cv)
-                    key = code
+                    key = SY.PRECOMPILE_KEY.get(code, code)  # the fp ops share one chip per field
                 state["precompile"].append((key, (shard, clk, sid, bv, cv), pev))
             else:
                 raise NotImplementedError(f"syscall {code:#x}")
@@ -1847,6 +1848,17 @@ PRECOMPILE_CHIP = {SY.SHA_EXTEND: "ShaExtend", SY.SHA_COMPRESS: "ShaCompress", S
                    SY.ED_DECOMPRESS: "EdDecompress", SY.SYS_LINUX: "SysLinux"}
 
 
+def _ec_keys():
+    from . import mips_ec as EC
+    keys = [EC.EC_ADD[c] for c in EC.FIELDS] + [EC.EC_DOUBLE[c] for c in EC.FIELDS] + [EC.UINT256_MUL]
+    for f in EC.FP_OPS:
+        keys += [EC.FP_OPS[f][0], EC.FP2_ADDSUB[f][0], EC.FP2_MUL[f]]
+    return {k: EC.chip_for_key(k) for k in keys}
+
+
+PRECOMPILE_CHIP.update(_ec_keys())  # Weierstrass curves, field towers, Uint256MulMod (mips_ec.py)
+
+
 def precompile_shard(code: int, events, shard: int, seed: int = 1):
     """A precompile shard (ExecutionRecord::split, executor/src/record.rs:130-193): the syscall events of one
     precompile, its chip's rows, SyscallPrecompile (one row per call), the calls' local memory accesses in
@@ -1869,7 +1881,8 @@ def precompile_shard(code: int, events, shard: int, seed: int = 1):
     elif code == SY.SYS_LINUX:
         traces["SysLinux"] = SY.sys_linux_trace(pevs, byte_lookup)
     else:
-        raise NotImplementedError(hex(code))
+        from . import mips_ec as EC
+        traces[EC.chip_for_key(code)] = EC.trace_for_key(code, pevs, byte_lookup)
     traces["SyscallPrecompile"] = SY.syscall_trace(sev)
     ent = np.asarray([x for e in pevs for x in e["local"]], np.int64).reshape(-1, 7)
     traces["MemoryLocal"] = MM.memory_local_trace(ent)

@@ -1,0 +1,927 @@
+"""Weierstrass-curve, field-tower and 256-bit precompiles: the chips of MipsAir (crates/core/machine/src/
+mips/mod.rs:133-173) built on the emulated-field gadgets (emulated_field.py):
+
+* WeierstrassAddAssignChip<E> / WeierstrassDoubleAssignChip<E> (syscall/precompiles/weierstrass/
+  weierstrass_add.rs, weierstrass_double.rs) for secp256k1, secp256r1, bn254 and bls12-381 (field
+  parameters crates/curves/src/weierstrass/*.rs; the affine slope formulas of sw_add / sw_double,
+  crates/curves/src/weierstrass/mod.rs:175-240);
+* FpOpChip<P>, Fp2AddSubAssignChip<P>, Fp2MulAssignChip<P> (syscall/precompiles/fptower/) over the bn254
+  and bls12-381 base fields;
+* Uint256MulChip (syscall/precompiles/uint256/air.rs): x <- x * y mod m, m = 2^256 when the modulus
+  words are zero (U256Field: 32 limbs, 63 witness limbs, crates/curves/src/uint256.rs).
+
+Column layouts follow the #[repr(C)] structs; constraint and lookup order is each chip's eval order
+(that order fixes the alpha folding and the LogUp columns).  Costs equal mips_costs.json.  The executor
+side follows crates/core/executor/src/syscalls/precompiles/{weierstrass,fptower,uint256.rs} and
+events/precompiles/ec.rs (create_ec_add_event / create_ec_double_event): the point / x operand is read
+without a record, the other operand read at clk, the result written at clk + 1 (add, field ops) or at
+clk (double).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+from . import emulated_field as EF
+from .emulated_field import FieldParams
+from .machine import ChipDesc, Expr, KIND_SYSCALL, Lookup, P, main
+from .machine import VirtualPairCol as V
+from .mips_alu import _assert_bool, _m
+
+WR_W, RD_W, ACC_VALUE = 13, 9, 0  # MemoryWriteCols, MemoryReadCols, value offset in MemoryAccessCols
+
+# ---------------------------------------------------------------- field and curve parameters
+SECP256K1_P = (1 << 256) - (1 << 32) - 977
+SECP256R1_P = (1 << 256) - (1 << 224) + (1 << 192) + (1 << 96) - 1
+BN254_P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+BLS12381_P = int("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab", 16)
+
+FIELDS: Dict[str, FieldParams] = {
+    "Secp256k1": FieldParams("Secp256k1BaseField", SECP256K1_P, 32, 62, 1 << 14),
+    "Secp256r1": FieldParams("Secp256r1BaseField", SECP256R1_P, 32, 62, 1 << 14),
+    "Bn254": FieldParams("Bn254BaseField", BN254_P, 32, 62, 1 << 14),
+    "Bls12381": FieldParams("Bls12381BaseField", BLS12381_P, 48, 94, 1 << 15),
+}
+U256 = FieldParams("U256Field", 1 << 256, 32, 63, 1 << 14)
+
+# y^2 = x^3 + a x + b (a_int / b_int of each WeierstrassParameters)
+CURVE_A = {"Secp256k1": 0, "Secp256r1": SECP256R1_P - 3, "Bn254": 0, "Bls12381": 0}
+CURVE_B = {"Secp256k1": 7,
+           "Secp256r1": 0x5AC635D8AA3A93E7B3EBBD55769886BC651D06B0CC53B0F63BCE3C3E27D2604B,
+           "Bn254": 3, "Bls12381": 4}
+
+# SyscallCode (crates/core/executor/src/syscalls/code.rs:60-141)
+SECP256K1_ADD, SECP256K1_DOUBLE = 0x01_01_00_0A, 0x00_01_00_0B
+BN254_ADD, BN254_DOUBLE = 0x01_01_00_0E, 0x00_01_00_0F
+UINT256_MUL = 0x01_01_00_1D
+BLS12381_ADD, BLS12381_DOUBLE = 0x01_01_00_1E, 0x00_01_00_1F
+BLS12381_FP_ADD, BLS12381_FP_SUB, BLS12381_FP_MUL = 0x01_01_00_20, 0x01_01_00_21, 0x01_01_00_22
+BLS12381_FP2_ADD, BLS12381_FP2_SUB, BLS12381_FP2_MUL = 0x01_01_00_23, 0x01_01_00_24, 0x01_01_00_25
+BN254_FP_ADD, BN254_FP_SUB, BN254_FP_MUL = 0x01_01_00_26, 0x01_01_00_27, 0x01_01_00_28
+BN254_FP2_ADD, BN254_FP2_SUB, BN254_FP2_MUL = 0x01_01_00_29, 0x01_01_00_2A, 0x01_01_00_2B
+SECP256R1_ADD, SECP256R1_DOUBLE = 0x01_01_00_2C, 0x00_01_00_2D
+
+EC_ADD = {"Secp256k1": SECP256K1_ADD, "Secp256r1": SECP256R1_ADD, "Bn254": BN254_ADD, "Bls12381": BLS12381_ADD}
+EC_DOUBLE = {"Secp256k1": SECP256K1_DOUBLE, "Secp256r1": SECP256R1_DOUBLE, "Bn254": BN254_DOUBLE,
+             "Bls12381": BLS12381_DOUBLE}
+FP_OPS = {"Bn254": (BN254_FP_ADD, BN254_FP_SUB, BN254_FP_MUL),
+          "Bls12381": (BLS12381_FP_ADD, BLS12381_FP_SUB, BLS12381_FP_MUL)}
+FP2_ADDSUB = {"Bn254": (BN254_FP2_ADD, BN254_FP2_SUB), "Bls12381": (BLS12381_FP2_ADD, BLS12381_FP2_SUB)}
+FP2_MUL = {"Bn254": BN254_FP2_MUL, "Bls12381": BLS12381_FP2_MUL}
+
+# chip names (the reference's `name()`, typos included)
+FP_NAME = {"Bn254": "Bn254FpOpAssign", "Bls12381": "Bls12381FpOpAssign"}
+FP2_ADDSUB_NAME = {"Bn254": "Bn254Fp2AddSubAssign", "Bls12381": "Bls12831Fp2AddSubAssign"}
+FP2_MUL_NAME = {"Bn254": "Bn254Fp2MulAssign", "Bls12381": "Bls12831Fp2MulAssign"}
+
+
+def sid(code: int) -> int:
+    return code & 0xFFFF
+
+
+# precompile events are grouped per chip (rt.add_precompile_event keys: the fp ops under their ADD code)
+PRECOMPILE_KEY = {}
+for _c in FP_OPS.values():
+    PRECOMPILE_KEY.update({k: _c[0] for k in _c})
+for _c in FP2_ADDSUB.values():
+    PRECOMPILE_KEY.update({k: _c[0] for k in _c})
+
+
+# ---------------------------------------------------------------- AIR helpers
+def _write_prev_limbs(base: int, words: int) -> List[Expr]:
+    """limbs_from_prev_access over MemoryWriteCols: the prev_value bytes (utils/mod.rs:42-49)."""
+    return [main(base + WR_W * w + i) for w in range(words) for i in range(4)]
+
+
+def _write_value_limbs(base: int, words: int) -> List[Expr]:
+    """value_as_limbs over MemoryWriteCols: the written value bytes."""
+    return [main(base + WR_W * w + 4 + ACC_VALUE + i) for w in range(words) for i in range(4)]
+
+
+def _read_limbs(base: int, words: int) -> List[Expr]:
+    return [main(base + RD_W * w + ACC_VALUE + i) for w in range(words) for i in range(4)]
+
+
+def _eval_access_slice(ch: ChipDesc, base: int, words: int, write: bool, ptr_col: int, clk_pos: int,
+                       is_real: Expr, mult: V, shard_col: int, clk_col: int, addr_off: int = 0):
+    """eval_memory_access_slice (air/memory.rs:65-82): word i at ptr + addr_off + 4 i, timestamp clk + clk_pos."""
+    from .mips_core import _eval_memory_access
+    w = WR_W if write else RD_W
+    for i in range(words):
+        acc = base + w * i + (4 if write else 0)
+        prev = base + w * i if write else acc + ACC_VALUE
+        addr = V([("main", ptr_col, 1)], addr_off + 4 * i)
+        _eval_memory_access(ch, acc, prev, clk_pos, addr, is_real, mult, shard_col=shard_col,
+                            clk_terms=((clk_col, 1),))
+
+
+def _eval_variable(ch: ChipDesc, base: int, a, b, modulus, is_add, is_sub, is_mul, mult: V, fp: FieldParams):
+    """FieldOpCols::eval_variable (field_op.rs:244-280) with is_div = 0: one constraint system for
+    add / sub / mul selected by the flag columns."""
+    res = EF.cols(base, fp.nl)
+    p_result = EF.p_add(EF.p_scale(res, is_add + is_mul), EF.p_scale(a, is_sub))
+    p_op = EF.p_add(EF.p_add(EF.p_scale(EF.p_add(a, b), is_add), EF.p_scale(EF.p_add(res, b), is_sub)),
+                    EF.p_scale(EF.p_mul(a, b), is_mul))
+    carry = EF.cols(base + fp.nl, fp.nl)
+    vanishing = EF.p_sub(EF.p_sub(p_op, p_result), EF.p_mul(carry, modulus))
+    EF.eval_field_operation(ch, vanishing, base, fp)
+    EF.field_range_checks(ch, base, mult, fp)
+
+
+# ---------------------------------------------------------------- Weierstrass add / double
+class AddLayout:
+    """WeierstrassAddAssignCols (weierstrass_add.rs:46-61)."""
+
+    def __init__(self, fp: FieldParams):
+        w = fp.words
+        self.REAL, self.SHARD, self.CLK, self.PPTR, self.QPTR = range(5)
+        self.P = 5
+        self.Q = self.P + 2 * w * WR_W
+        base = self.Q + 2 * w * RD_W
+        names = ["slope_denominator", "slope_numerator", "slope", "slope_squared", "p_x_plus_q_x", "x3_ins",
+                 "p_x_minus_x", "y3_ins", "slope_times_p_x_minus_x"]
+        self.F = {n: base + k * fp.fop_w for k, n in enumerate(names)}
+        self.WIDTH = base + len(names) * fp.fop_w
+
+
+class DoubleLayout:
+    """WeierstrassDoubleAssignCols (weierstrass_double.rs:45-62)."""
+
+    def __init__(self, fp: FieldParams):
+        w = fp.words
+        self.REAL, self.SHARD, self.CLK, self.PPTR = range(4)
+        self.P = 4
+        base = self.P + 2 * w * WR_W
+        names = ["slope_denominator", "slope_numerator", "slope", "p_x_squared", "p_x_squared_times_3",
+                 "slope_squared", "p_x_plus_p_x", "x3_ins", "p_x_minus_x", "y3_ins", "slope_times_p_x_minus_x"]
+        self.F = {n: base + k * fp.fop_w for k, n in enumerate(names)}
+        self.WIDTH = base + len(names) * fp.fop_w
+
+
+def _result_eq(ch: ChipDesc, real: Expr, x3: Sequence, y3: Sequence, pv: Sequence, nl: int):
+    """x3_ins / y3_ins results equal the written point, limb by limb (x and y interleaved)."""
+    for i in range(nl):
+        ch.assert_zero(real * (x3[i] - pv[i]))
+        ch.assert_zero(real * (y3[i] - pv[nl + i]))
+
+
+def weierstrass_add_chip(curve: str) -> ChipDesc:
+    """WeierstrassAddAssignChip::eval (weierstrass_add.rs:262-381)."""
+    fp = FIELDS[curve]
+    L = AddLayout(fp)
+    nl, w = fp.nl, fp.words
+    ch = ChipDesc(f"{curve}AddAssign", prep_width=0, main_width=L.WIDTH, local_only=True)
+    real, rv = main(L.REAL), _m(L.REAL)
+    px, py = _write_prev_limbs(L.P, w), _write_prev_limbs(L.P + w * WR_W, w)
+    qx, qy = _read_limbs(L.Q, w), _read_limbs(L.Q + w * RD_W, w)
+    F, c = L.F, lambda n: EF.cols(L.F[n], nl)
+    EF.eval_field_op(ch, F["slope_numerator"], qy, py, "sub", rv, fp)
+    EF.eval_field_op(ch, F["slope_denominator"], qx, px, "sub", rv, fp)
+    EF.eval_field_op(ch, F["slope"], c("slope_numerator"), c("slope_denominator"), "div", rv, fp)
+    slope = c("slope")
+    EF.eval_field_op(ch, F["slope_squared"], slope, slope, "mul", rv, fp)
+    EF.eval_field_op(ch, F["p_x_plus_q_x"], px, qx, "add", rv, fp)
+    EF.eval_field_op(ch, F["x3_ins"], c("slope_squared"), c("p_x_plus_q_x"), "sub", rv, fp)
+    EF.eval_field_op(ch, F["p_x_minus_x"], px, c("x3_ins"), "sub", rv, fp)
+    EF.eval_field_op(ch, F["slope_times_p_x_minus_x"], slope, c("p_x_minus_x"), "mul", rv, fp)
+    EF.eval_field_op(ch, F["y3_ins"], c("slope_times_p_x_minus_x"), py, "sub", rv, fp)
+    _result_eq(ch, real, c("x3_ins"), c("y3_ins"), _write_value_limbs(L.P, 2 * w), nl)
+    _eval_access_slice(ch, L.Q, 2 * w, False, L.QPTR, 0, real, rv, L.SHARD, L.CLK)
+    _eval_access_slice(ch, L.P, 2 * w, True, L.PPTR, 1, real, rv, L.SHARD, L.CLK)
+    ch.receives.append(Lookup([_m(L.SHARD), _m(L.CLK), V.const(sid(EC_ADD[curve])), _m(L.PPTR), _m(L.QPTR)], rv,
+                              KIND_SYSCALL))
+    return ch
+
+
+def weierstrass_double_chip(curve: str) -> ChipDesc:
+    """WeierstrassDoubleAssignChip::eval (weierstrass_double.rs:277-408)."""
+    fp = FIELDS[curve]
+    L = DoubleLayout(fp)
+    nl, w = fp.nl, fp.words
+    ch = ChipDesc(f"{curve}DoubleAssign", prep_width=0, main_width=L.WIDTH, local_only=True)
+    real, rv = main(L.REAL), _m(L.REAL)
+    px, py = _write_prev_limbs(L.P, w), _write_prev_limbs(L.P + w * WR_W, w)
+    F, c = L.F, lambda n: EF.cols(L.F[n], nl)
+    EF.eval_field_op(ch, F["p_x_squared"], px, px, "mul", rv, fp)
+    EF.eval_field_op(ch, F["p_x_squared_times_3"], c("p_x_squared"), EF.const_limbs(3, fp), "mul", rv, fp)
+    EF.eval_field_op(ch, F["slope_numerator"], EF.const_limbs(CURVE_A[curve], fp), c("p_x_squared_times_3"), "add",
+                     rv, fp)
+    EF.eval_field_op(ch, F["slope_denominator"], EF.const_limbs(2, fp), py, "mul", rv, fp)
+    EF.eval_field_op(ch, F["slope"], c("slope_numerator"), c("slope_denominator"), "div", rv, fp)
+    slope = c("slope")
+    EF.eval_field_op(ch, F["slope_squared"], slope, slope, "mul", rv, fp)
+    EF.eval_field_op(ch, F["p_x_plus_p_x"], px, px, "add", rv, fp)
+    EF.eval_field_op(ch, F["x3_ins"], c("slope_squared"), c("p_x_plus_p_x"), "sub", rv, fp)
+    EF.eval_field_op(ch, F["p_x_minus_x"], px, c("x3_ins"), "sub", rv, fp)
+    EF.eval_field_op(ch, F["slope_times_p_x_minus_x"], slope, c("p_x_minus_x"), "mul", rv, fp)
+    EF.eval_field_op(ch, F["y3_ins"], c("slope_times_p_x_minus_x"), py, "sub", rv, fp)
+    _result_eq(ch, real, c("x3_ins"), c("y3_ins"), _write_value_limbs(L.P, 2 * w), nl)
+    _eval_access_slice(ch, L.P, 2 * w, True, L.PPTR, 0, real, rv, L.SHARD, L.CLK)
+    ch.receives.append(Lookup([_m(L.SHARD), _m(L.CLK), V.const(sid(EC_DOUBLE[curve])), _m(L.PPTR), V.const(0)], rv,
+                              KIND_SYSCALL))
+    return ch
+
+
+# ---------------------------------------------------------------- field towers
+class FpLayout:
+    """FpOpCols (fptower/fp.rs:38-51)."""
+
+    def __init__(self, fp: FieldParams):
+        (self.REAL, self.SHARD, self.CLK, self.IS_ADD, self.IS_SUB, self.IS_MUL, self.XPTR,
+         self.YPTR) = range(8)
+        self.X = 8
+        self.Y = self.X + fp.words * WR_W
+        self.OUT = self.Y + fp.words * RD_W
+        self.WIDTH = self.OUT + fp.fop_w
+
+
+def fp_op_chip(field: str) -> ChipDesc:
+    """FpOpChip::eval (fptower/fp.rs:191-269)."""
+    fp = FIELDS[field]
+    L = FpLayout(fp)
+    ch = ChipDesc(FP_NAME[field], prep_width=0, main_width=L.WIDTH, local_only=True)
+    real, rv = main(L.REAL), _m(L.REAL)
+    ia, isb, im = main(L.IS_ADD), main(L.IS_SUB), main(L.IS_MUL)
+    for f in (ia, isb, im):
+        _assert_bool(ch, f)
+    ch.assert_zero(ia + isb + im - 1)
+    p = _write_prev_limbs(L.X, fp.words)
+    q = _read_limbs(L.Y, fp.words)
+    _eval_variable(ch, L.OUT, p, q, fp.mod_limbs, ia, isb, im, rv, fp)
+    for a, b in zip(EF.cols(L.OUT, fp.nl), _write_value_limbs(L.X, fp.words)):
+        ch.assert_zero(real * (a - b))
+    _eval_access_slice(ch, L.Y, fp.words, False, L.YPTR, 0, real, rv, L.SHARD, L.CLK)
+    _eval_access_slice(ch, L.X, fp.words, True, L.XPTR, 1, real, rv, L.SHARD, L.CLK)
+    add, sub, mul = (sid(c) for c in FP_OPS[field])
+    ident = V([("main", L.IS_ADD, add), ("main", L.IS_SUB, sub), ("main", L.IS_MUL, mul)], 0)
+    ch.receives.append(Lookup([_m(L.SHARD), _m(L.CLK), ident, _m(L.XPTR), _m(L.YPTR)], rv, KIND_SYSCALL))
+    return ch
+
+
+class Fp2AddSubLayout:
+    """Fp2AddSubAssignCols (fptower/fp2_addsub.rs:40-51)."""
+
+    def __init__(self, fp: FieldParams):
+        self.REAL, self.SHARD, self.CLK, self.IS_ADD, self.XPTR, self.YPTR = range(6)
+        self.X = 6
+        self.Y = self.X + 2 * fp.words * WR_W
+        self.C0 = self.Y + 2 * fp.words * RD_W
+        self.C1 = self.C0 + fp.fop_w
+        self.WIDTH = self.C1 + fp.fop_w
+
+
+def fp2_addsub_chip(field: str) -> ChipDesc:
+    """Fp2AddSubAssignChip::eval (fptower/fp2_addsub.rs:199-282)."""
+    fp = FIELDS[field]
+    L = Fp2AddSubLayout(fp)
+    w = fp.words
+    ch = ChipDesc(FP2_ADDSUB_NAME[field], prep_width=0, main_width=L.WIDTH, local_only=True)
+    real, rv = main(L.REAL), _m(L.REAL)
+    ia = main(L.IS_ADD)
+    _assert_bool(ch, ia)
+    px, py = _write_prev_limbs(L.X, w), _write_prev_limbs(L.X + w * WR_W, w)
+    qx, qy = _read_limbs(L.Y, w), _read_limbs(L.Y + w * RD_W, w)
+    _eval_variable(ch, L.C0, px, qx, fp.mod_limbs, ia, 1 - ia, 0, rv, fp)
+    _eval_variable(ch, L.C1, py, qy, fp.mod_limbs, ia, 1 - ia, 0, rv, fp)
+    xv = _write_value_limbs(L.X, 2 * w)
+    for a, b in zip(EF.cols(L.C0, fp.nl), xv[:fp.nl]):
+        ch.assert_zero(real * (a - b))
+    for a, b in zip(EF.cols(L.C1, fp.nl), xv[fp.nl:]):
+        ch.assert_zero(real * (a - b))
+    _eval_access_slice(ch, L.Y, 2 * w, False, L.YPTR, 0, real, rv, L.SHARD, L.CLK)
+    _eval_access_slice(ch, L.X, 2 * w, True, L.XPTR, 1, real, rv, L.SHARD, L.CLK)
+    add, sub = (sid(c) for c in FP2_ADDSUB[field])
+    ident = V([("main", L.IS_ADD, (add - sub) % P)], sub)
+    ch.receives.append(Lookup([_m(L.SHARD), _m(L.CLK), ident, _m(L.XPTR), _m(L.YPTR)], rv, KIND_SYSCALL))
+    return ch
+
+
+class Fp2MulLayout:
+    """Fp2MulAssignCols (fptower/fp2_mul.rs:40-55)."""
+
+    def __init__(self, fp: FieldParams):
+        self.REAL, self.SHARD, self.CLK, self.XPTR, self.YPTR = range(5)
+        self.X = 5
+        self.Y = self.X + 2 * fp.words * WR_W
+        base = self.Y + 2 * fp.words * RD_W
+        names = ["a0_mul_b0", "a1_mul_b1", "a0_mul_b1", "a1_mul_b0", "c0", "c1"]
+        self.F = {n: base + k * fp.fop_w for k, n in enumerate(names)}
+        self.WIDTH = base + len(names) * fp.fop_w
+
+
+def fp2_mul_chip(field: str) -> ChipDesc:
+    """Fp2MulAssignChip::eval (fptower/fp2_mul.rs:225-331)."""
+    fp = FIELDS[field]
+    L = Fp2MulLayout(fp)
+    w, nl = fp.words, fp.nl
+    ch = ChipDesc(FP2_MUL_NAME[field], prep_width=0, main_width=L.WIDTH, local_only=True)
+    real, rv = main(L.REAL), _m(L.REAL)
+    px, py = _write_prev_limbs(L.X, w), _write_prev_limbs(L.X + w * WR_W, w)
+    qx, qy = _read_limbs(L.Y, w), _read_limbs(L.Y + w * RD_W, w)
+    F, c = L.F, lambda n: EF.cols(L.F[n], nl)
+    EF.eval_field_op(ch, F["a0_mul_b0"], px, qx, "mul", rv, fp)
+    EF.eval_field_op(ch, F["a1_mul_b1"], py, qy, "mul", rv, fp)
+    EF.eval_field_op(ch, F["c0"], c("a0_mul_b0"), c("a1_mul_b1"), "sub", rv, fp)
+    EF.eval_field_op(ch, F["a0_mul_b1"], px, qy, "mul", rv, fp)
+    EF.eval_field_op(ch, F["a1_mul_b0"], py, qx, "mul", rv, fp)
+    EF.eval_field_op(ch, F["c1"], c("a0_mul_b1"), c("a1_mul_b0"), "add", rv, fp)
+    xv = _write_value_limbs(L.X, 2 * w)
+    for a, b in zip(c("c0"), xv[:nl]):
+        ch.assert_zero(real * (a - b))
+    for a, b in zip(c("c1"), xv[nl:]):
+        ch.assert_zero(real * (a - b))
+    _eval_access_slice(ch, L.Y, 2 * w, False, L.YPTR, 0, real, rv, L.SHARD, L.CLK)
+    _eval_access_slice(ch, L.X, 2 * w, True, L.XPTR, 1, real, rv, L.SHARD, L.CLK)
+    ch.receives.append(Lookup([_m(L.SHARD), _m(L.CLK), V.const(sid(FP2_MUL[field])), _m(L.XPTR), _m(L.YPTR)], rv,
+                              KIND_SYSCALL))
+    return ch
+
+
+# ---------------------------------------------------------------- Uint256MulMod
+class U256Layout:
+    """Uint256MulCols (uint256/air.rs:37-67)."""
+
+    def __init__(self):
+        self.SHARD, self.CLK, self.XPTR, self.YPTR = range(4)
+        self.X = 4
+        self.Y = self.X + 8 * WR_W
+        self.M = self.Y + 8 * RD_W
+        self.IZ_INV = self.M + 8 * RD_W          # modulus_is_zero: IsZeroOperation (inverse, result)
+        self.IZ_RES = self.IZ_INV + 1
+        self.NOT_ZERO = self.IZ_RES + 1          # modulus_is_not_zero
+        self.OUT = self.NOT_ZERO + 1             # FieldOpCols<U256Field>
+        self.LT = self.OUT + U256.fop_w          # FieldLtCols<U256Field>
+        self.REAL = self.LT + U256.lt_w
+        self.WIDTH = self.REAL + 1
+
+
+U256L = U256Layout()
+
+
+def uint256_mul_chip() -> ChipDesc:
+    """Uint256MulChip::eval (uint256/air.rs:189-281)."""
+    L = U256L
+    ch = ChipDesc("Uint256MulMod", prep_width=0, main_width=L.WIDTH, local_only=True)
+    real, rv = main(L.REAL), _m(L.REAL)
+    x = _write_prev_limbs(L.X, 8)
+    y = _read_limbs(L.Y, 8)
+    m = _read_limbs(L.M, 8)
+    # IsZeroOperation::eval on the modulus byte sum (operations/is_zero.rs)
+    s = Expr.lift(0)
+    for b in m:
+        s = s + b
+    iz = main(L.IZ_RES)
+    ch.assert_zero(real * ((1 - main(L.IZ_INV) * s) - iz))
+    _assert_bool(ch, iz, real)
+    ch.assert_zero(real * iz * s)
+    # p_modulus = m (1 - is_zero) + x^32 is_zero
+    p_mod = EF.p_add(EF.p_scale(m, 1 - iz), [0] * 32 + [iz])
+    EF.eval_field_op(ch, L.OUT, x, y, "mul", rv, U256, modulus=p_mod)
+    EF.eval_field_lt(ch, L.LT, EF.cols(L.OUT, 32), m, main(L.NOT_ZERO), _m(L.NOT_ZERO), U256)
+    ch.assert_zero(main(L.NOT_ZERO) - real * (1 - iz))
+    for a, b in zip(EF.cols(L.OUT, 32), _write_value_limbs(L.X, 8)):
+        ch.assert_zero(real * (a - b))
+    _eval_access_slice(ch, L.X, 8, True, L.XPTR, 1, real, rv, L.SHARD, L.CLK)
+    _eval_access_slice(ch, L.Y, 16, False, L.YPTR, 0, real, rv, L.SHARD, L.CLK)
+    ch.receives.append(Lookup([_m(L.SHARD), _m(L.CLK), V.const(sid(UINT256_MUL)), _m(L.XPTR), _m(L.YPTR)], rv,
+                              KIND_SYSCALL))
+    _assert_bool(ch, real)
+    return ch
+
+
+# ---------------------------------------------------------------- curve arithmetic (trace / executor side)
+def sw_add(curve: str, p, q):
+    """AffinePoint::sw_add (weierstrass/mod.rs:175-202); p != q."""
+    m = FIELDS[curve].modulus
+    (x1, y1), (x2, y2) = p, q
+    assert (x1, y1) != (x2, y2), "points are the same: use sw_double"
+    s = (y2 - y1) % m * pow((x2 - x1) % m, m - 2, m) % m
+    x3 = (s * s - x1 - x2) % m
+    return x3, (s * (x1 - x3) - y1) % m
+
+
+def sw_double(curve: str, p):
+    """AffinePoint::sw_double (weierstrass/mod.rs:204-240)."""
+    m = FIELDS[curve].modulus
+    x1, y1 = p
+    s = (CURVE_A[curve] + 3 * x1 * x1) % m * pow(2 * y1 % m, m - 2, m) % m
+    x3 = (s * s - 2 * x1) % m
+    return x3, (s * (x1 - x3) - y1) % m
+
+
+def point_from_x(curve: str, x: int):
+    """A curve point with abscissa x, or None (every base field here has p = 3 mod 4)."""
+    m = FIELDS[curve].modulus
+    assert m % 4 == 3
+    rhs = (x * x * x + CURVE_A[curve] * x + CURVE_B[curve]) % m
+    y = pow(rhs, (m + 1) // 4, m)
+    return (x, y) if y * y % m == rhs else None
+
+
+def random_point(curve: str, rng):
+    m = FIELDS[curve].modulus
+    while True:
+        x = int.from_bytes(rng.bytes(FIELDS[curve].nl), "little") % m
+        pt = point_from_x(curve, x)
+        if pt is not None:
+            return pt
+
+
+def point_words(curve: str, pt) -> List[int]:
+    w = FIELDS[curve].words
+    return EF.int_to_words(pt[0], w) + EF.int_to_words(pt[1], w)
+
+
+# ---------------------------------------------------------------- executor (syscalls)
+def exec_ec_add(curve: str, pm, shard: int, clk: int, p_ptr: int, q_ptr: int):
+    """create_ec_add_event (events/precompiles/ec.rs:96-139)."""
+    nw = 2 * FIELDS[curve].words
+    assert p_ptr % 4 == 0 and q_ptr % 4 == 0
+    p = [pm.peek(p_ptr + 4 * i) for i in range(nw)]
+    q = [pm.read(q_ptr + 4 * i, clk) for i in range(nw)]
+    h = nw // 2
+    pt = (EF.words_to_int(p[:h]), EF.words_to_int(p[h:]))
+    qt = (EF.words_to_int([r[0] for r in q[:h]]), EF.words_to_int([r[0] for r in q[h:]]))
+    res = point_words(curve, sw_add(curve, pt, qt))
+    pw = [pm.write(p_ptr + 4 * i, res[i], clk + 1) for i in range(nw)]
+    return {"shard": shard, "clk": clk, "p_ptr": p_ptr, "q_ptr": q_ptr, "p": p, "q": q, "pw": pw,
+            "local": pm.local_entries()}
+
+
+def exec_ec_double(curve: str, pm, shard: int, clk: int, p_ptr: int, _a1: int):
+    """create_ec_double_event (events/precompiles/ec.rs:141-173): p written at clk."""
+    nw = 2 * FIELDS[curve].words
+    assert p_ptr % 4 == 0
+    p = [pm.peek(p_ptr + 4 * i) for i in range(nw)]
+    h = nw // 2
+    res = point_words(curve, sw_double(curve, (EF.words_to_int(p[:h]), EF.words_to_int(p[h:]))))
+    pw = [pm.write(p_ptr + 4 * i, res[i], clk) for i in range(nw)]
+    return {"shard": shard, "clk": clk, "p_ptr": p_ptr, "p": p, "pw": pw, "local": pm.local_entries()}
+
+
+def exec_fp_op(field: str, op: str, pm, shard: int, clk: int, x_ptr: int, y_ptr: int):
+    """FpOpSyscall::execute (executor/src/syscalls/precompiles/fptower/fp.rs)."""
+    fp = FIELDS[field]
+    m, nw = fp.modulus, fp.words
+    assert x_ptr % 4 == 0 and y_ptr % 4 == 0
+    x = [pm.peek(x_ptr + 4 * i) for i in range(nw)]
+    yr = [pm.read(y_ptr + 4 * i, clk) for i in range(nw)]
+    a, b = EF.words_to_int(x) % m, EF.words_to_int([r[0] for r in yr]) % m
+    r = {"add": (a + b) % m, "sub": (a + m - b) % m, "mul": a * b % m}[op]
+    res = EF.int_to_words(r, nw)
+    xw = [pm.write(x_ptr + 4 * i, res[i], clk + 1) for i in range(nw)]
+    return {"shard": shard, "clk": clk, "x_ptr": x_ptr, "y_ptr": y_ptr, "op": op, "x": x, "y": yr, "xw": xw,
+            "local": pm.local_entries()}
+
+
+def exec_fp2_addsub(field: str, op: str, pm, shard: int, clk: int, x_ptr: int, y_ptr: int):
+    """Fp2AddSubSyscall::execute (executor/src/syscalls/precompiles/fptower/fp2_addsub.rs)."""
+    fp = FIELDS[field]
+    m, nw = fp.modulus, 2 * fp.words
+    x = [pm.peek(x_ptr + 4 * i) for i in range(nw)]
+    yr = [pm.read(y_ptr + 4 * i, clk) for i in range(nw)]
+    h = nw // 2
+    ac0, ac1 = EF.words_to_int(x[:h]) % m, EF.words_to_int(x[h:]) % m
+    bc0, bc1 = EF.words_to_int([r[0] for r in yr[:h]]) % m, EF.words_to_int([r[0] for r in yr[h:]]) % m
+    if op == "add":
+        c0, c1 = (ac0 + bc0) % m, (ac1 + bc1) % m
+    else:
+        c0, c1 = (ac0 + m - bc0) % m, (ac1 + m - bc1) % m
+    res = EF.int_to_words(c0, h) + EF.int_to_words(c1, h)
+    xw = [pm.write(x_ptr + 4 * i, res[i], clk + 1) for i in range(nw)]
+    return {"shard": shard, "clk": clk, "x_ptr": x_ptr, "y_ptr": y_ptr, "op": op, "x": x, "y": yr, "xw": xw,
+            "local": pm.local_entries()}
+
+
+def exec_fp2_mul(field: str, pm, shard: int, clk: int, x_ptr: int, y_ptr: int):
+    """Fp2MulSyscall::execute (executor/src/syscalls/precompiles/fptower/fp2_mul.rs): (a0 + a1 u)(b0 + b1 u)
+    with u^2 = -1."""
+    fp = FIELDS[field]
+    m, nw = fp.modulus, 2 * fp.words
+    x = [pm.peek(x_ptr + 4 * i) for i in range(nw)]
+    yr = [pm.read(y_ptr + 4 * i, clk) for i in range(nw)]
+    h = nw // 2
+    a0, a1 = EF.words_to_int(x[:h]) % m, EF.words_to_int(x[h:]) % m
+    b0, b1 = EF.words_to_int([r[0] for r in yr[:h]]) % m, EF.words_to_int([r[0] for r in yr[h:]]) % m
+    c0 = (a0 * b0 % m + m - a1 * b1 % m) % m
+    c1 = (a0 * b1 % m + a1 * b0 % m) % m
+    res = EF.int_to_words(c0, h) + EF.int_to_words(c1, h)
+    xw = [pm.write(x_ptr + 4 * i, res[i], clk + 1) for i in range(nw)]
+    return {"shard": shard, "clk": clk, "x_ptr": x_ptr, "y_ptr": y_ptr, "x": x, "y": yr, "xw": xw,
+            "local": pm.local_entries()}
+
+
+def exec_uint256_mul(pm, shard: int, clk: int, x_ptr: int, y_ptr: int):
+    """Uint256MulSyscall::execute (executor/src/syscalls/precompiles/uint256.rs)."""
+    assert x_ptr % 4 == 0 and y_ptr % 4 == 0
+    x = [pm.peek(x_ptr + 4 * i) for i in range(8)]
+    yr = [pm.read(y_ptr + 4 * i, clk) for i in range(8)]
+    mr = [pm.read(y_ptr + 32 + 4 * i, clk) for i in range(8)]
+    a, b = EF.words_to_int(x), EF.words_to_int([r[0] for r in yr])
+    m = EF.words_to_int([r[0] for r in mr])
+    res = EF.int_to_words(a * b % (m if m else 1 << 256), 8)
+    xw = [pm.write(x_ptr + 4 * i, res[i], clk + 1) for i in range(8)]
+    return {"shard": shard, "clk": clk, "x_ptr": x_ptr, "y_ptr": y_ptr, "x": x, "y": yr, "m": mr, "xw": xw,
+            "local": pm.local_entries()}
+
+
+def _bind(fn, *args):
+    return lambda pm, shard, clk, a0, a1: fn(*args, pm, shard, clk, a0, a1)
+
+
+def precompile_table():
+    """syscall code -> executor, for mips_syscall.PRECOMPILES."""
+    t = {}
+    for curve in FIELDS:
+        t[EC_ADD[curve]] = _bind(exec_ec_add, curve)
+        t[EC_DOUBLE[curve]] = _bind(exec_ec_double, curve)
+    for field in FP_OPS:
+        for code, op in zip(FP_OPS[field], ("add", "sub", "mul")):
+            t[code] = _bind(exec_fp_op, field, op)
+        for code, op in zip(FP2_ADDSUB[field], ("add", "sub")):
+            t[code] = _bind(exec_fp2_addsub, field, op)
+        t[FP2_MUL[field]] = _bind(exec_fp2_mul, field)
+    t[UINT256_MUL] = exec_uint256_mul
+    return t
+
+
+# ---------------------------------------------------------------- traces
+def _access_block(t, rows, base, recs, write: bool, shard, clk, byte_lookup):
+    """MemoryReadCols / MemoryWriteCols populate for word records at timestamp clk (per row)."""
+    from .mips_edwards import _access_block as ab
+    ab(t, rows, base, recs, write, shard, clk, byte_lookup)
+
+
+def _height(n: int) -> int:
+    return max(16, 1 << max(0, (n - 1).bit_length()))
+
+
+def _fill(t, base, fp, res_cols):
+    t[:, base:base + fp.fop_w] = res_cols
+
+
+def weierstrass_add_trace(curve: str, events, byte_lookup) -> np.ndarray:
+    """WeierstrassAddAssignChip::generate_trace + populate_row (weierstrass_add.rs:192-252, :384-420):
+    padding rows hold the field operations on zero inputs."""
+    fp = FIELDS[curve]
+    L = AddLayout(fp)
+    ne, h, hw = len(events), _height(len(events)), fp.words
+    t = np.zeros((h, L.WIDTH), np.int64)
+    rec = EF.Rec(byte_lookup)
+    px, py, qx, qy = [0] * h, [0] * h, [0] * h, [0] * h
+    for i, e in enumerate(events):
+        px[i], py[i] = EF.words_to_int(e["p"][:hw]), EF.words_to_int(e["p"][hw:])
+        qv = [r[0] for r in e["q"]]
+        qx[i], qy[i] = EF.words_to_int(qv[:hw]), EF.words_to_int(qv[hw:])
+    F = L.F
+    num, t[:, F["slope_numerator"]:F["slope_numerator"] + fp.fop_w] = EF.pop_field_op(qy, py, "sub", fp)
+    den, t[:, F["slope_denominator"]:F["slope_denominator"] + fp.fop_w] = EF.pop_field_op(qx, px, "sub", fp)
+    slope, t[:, F["slope"]:F["slope"] + fp.fop_w] = EF.pop_field_op(num, den, "div", fp)
+    s2, t[:, F["slope_squared"]:F["slope_squared"] + fp.fop_w] = EF.pop_field_op(slope, slope, "mul", fp)
+    pq, t[:, F["p_x_plus_q_x"]:F["p_x_plus_q_x"] + fp.fop_w] = EF.pop_field_op(px, qx, "add", fp)
+    x3, t[:, F["x3_ins"]:F["x3_ins"] + fp.fop_w] = EF.pop_field_op(s2, pq, "sub", fp)
+    pmx, t[:, F["p_x_minus_x"]:F["p_x_minus_x"] + fp.fop_w] = EF.pop_field_op(px, x3, "sub", fp)
+    stp, t[:, F["slope_times_p_x_minus_x"]:F["slope_times_p_x_minus_x"] + fp.fop_w] = EF.pop_field_op(
+        slope, pmx, "mul", fp)
+    y3, t[:, F["y3_ins"]:F["y3_ins"] + fp.fop_w] = EF.pop_field_op(stp, py, "sub", fp)
+    for base in F.values():
+        rec.fop(t[:ne, base:base + fp.fop_w], fp)
+    if ne:
+        rows = np.arange(ne)
+        t[rows, L.REAL] = 1
+        shard = np.array([e["shard"] for e in events], np.int64)
+        clk = np.array([e["clk"] for e in events], np.int64)
+        t[rows, L.SHARD], t[rows, L.CLK] = shard, clk
+        t[rows, L.PPTR] = [e["p_ptr"] for e in events]
+        t[rows, L.QPTR] = [e["q_ptr"] for e in events]
+        for i in range(ne):
+            assert (x3[i], y3[i]) == sw_add(curve, (px[i], py[i]), (qx[i], qy[i]))
+        _access_block(t, rows, L.Q, [e["q"] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.P, [e["pw"] for e in events], True, shard, clk + 1, byte_lookup)
+    return (t % P).astype(np.uint32)
+
+
+def weierstrass_double_trace(curve: str, events, byte_lookup) -> np.ndarray:
+    """WeierstrassDoubleAssignChip::generate_trace + populate_row (weierstrass_double.rs:201-270,
+    :411-440); padding rows: the field operations of p = (0, 1), whose y comes from a dummy write record
+    (value 1, timestamp 1, previous value 1) in the first y word."""
+    fp = FIELDS[curve]
+    L = DoubleLayout(fp)
+    ne, h, hw = len(events), _height(len(events)), fp.words
+    t = np.zeros((h, L.WIDTH), np.int64)
+    rec = EF.Rec(byte_lookup)
+    px, py = [0] * h, [1] * h
+    for i, e in enumerate(events):
+        px[i], py[i] = EF.words_to_int(e["p"][:hw]), EF.words_to_int(e["p"][hw:])
+    F = L.F
+    a = CURVE_A[curve]
+    x2, t[:, F["p_x_squared"]:F["p_x_squared"] + fp.fop_w] = EF.pop_field_op(px, px, "mul", fp)
+    x23, t[:, F["p_x_squared_times_3"]:F["p_x_squared_times_3"] + fp.fop_w] = EF.pop_field_op(x2, [3] * h, "mul",
+                                                                                                 fp)
+    num, t[:, F["slope_numerator"]:F["slope_numerator"] + fp.fop_w] = EF.pop_field_op([a] * h, x23, "add", fp)
+    den, t[:, F["slope_denominator"]:F["slope_denominator"] + fp.fop_w] = EF.pop_field_op([2] * h, py, "mul", fp)
+    slope, t[:, F["slope"]:F["slope"] + fp.fop_w] = EF.pop_field_op(num, den, "div", fp)
+    s2, t[:, F["slope_squared"]:F["slope_squared"] + fp.fop_w] = EF.pop_field_op(slope, slope, "mul", fp)
+    pp, t[:, F["p_x_plus_p_x"]:F["p_x_plus_p_x"] + fp.fop_w] = EF.pop_field_op(px, px, "add", fp)
+    x3, t[:, F["x3_ins"]:F["x3_ins"] + fp.fop_w] = EF.pop_field_op(s2, pp, "sub", fp)
+    pmx, t[:, F["p_x_minus_x"]:F["p_x_minus_x"] + fp.fop_w] = EF.pop_field_op(px, x3, "sub", fp)
+    stp, t[:, F["slope_times_p_x_minus_x"]:F["slope_times_p_x_minus_x"] + fp.fop_w] = EF.pop_field_op(
+        slope, pmx, "mul", fp)
+    y3, t[:, F["y3_ins"]:F["y3_ins"] + fp.fop_w] = EF.pop_field_op(stp, py, "sub", fp)
+    for base in F.values():
+        rec.fop(t[:ne, base:base + fp.fop_w], fp)
+    # the dummy write record of the padding rows: y word 0, prev_value 1, value 1, compare 1 (same
+    # shard 0), timestamp difference 1 - 0 - 1 = 0
+    from .mips_core import ACC_COMPARE
+    y0 = L.P + hw * WR_W
+    t[ne:, y0] = 1
+    t[ne:, y0 + 4 + ACC_VALUE] = 1
+    t[ne:, y0 + 4 + ACC_COMPARE] = 1
+    if ne:
+        rows = np.arange(ne)
+        t[rows, L.REAL] = 1
+        shard = np.array([e["shard"] for e in events], np.int64)
+        clk = np.array([e["clk"] for e in events], np.int64)
+        t[rows, L.SHARD], t[rows, L.CLK] = shard, clk
+        t[rows, L.PPTR] = [e["p_ptr"] for e in events]
+        for i in range(ne):
+            assert (x3[i], y3[i]) == sw_double(curve, (px[i], py[i]))
+        _access_block(t, rows, L.P, [e["pw"] for e in events], True, shard, clk, byte_lookup)
+    return (t % P).astype(np.uint32)
+
+
+def fp_op_trace(field: str, events, byte_lookup) -> np.ndarray:
+    """FpOpChip::generate_trace (fptower/fp.rs:90-160): padding rows are the addition 0 + 0 (is_add = 1)."""
+    fp = FIELDS[field]
+    L = FpLayout(fp)
+    ne, h, m = len(events), _height(len(events)), fp.modulus
+    t = np.zeros((h, L.WIDTH), np.int64)
+    rec = EF.Rec(byte_lookup)
+    ops = [e["op"] for e in events] + ["add"] * (h - ne)
+    a = [EF.words_to_int(e["x"]) % m for e in events] + [0] * (h - ne)
+    b = [EF.words_to_int([r[0] for r in e["y"]]) % m for e in events] + [0] * (h - ne)
+    for op in ("add", "sub", "mul"):
+        idx = [i for i in range(h) if ops[i] == op]
+        if idx:
+            _, c = EF.pop_field_op([a[i] for i in idx], [b[i] for i in idx], op, fp)
+            t[idx, L.OUT:L.OUT + fp.fop_w] = c
+    t[:, L.IS_ADD] = [o == "add" for o in ops]
+    t[:, L.IS_SUB] = [o == "sub" for o in ops]
+    t[:, L.IS_MUL] = [o == "mul" for o in ops]
+    rec.fop(t[:ne, L.OUT:L.OUT + fp.fop_w], fp)
+    if ne:
+        rows = np.arange(ne)
+        t[rows, L.REAL] = 1
+        shard = np.array([e["shard"] for e in events], np.int64)
+        clk = np.array([e["clk"] for e in events], np.int64)
+        t[rows, L.SHARD], t[rows, L.CLK] = shard, clk
+        t[rows, L.XPTR] = [e["x_ptr"] for e in events]
+        t[rows, L.YPTR] = [e["y_ptr"] for e in events]
+        _access_block(t, rows, L.Y, [e["y"] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.X, [e["xw"] for e in events], True, shard, clk + 1, byte_lookup)
+    return (t % P).astype(np.uint32)
+
+
+def fp2_addsub_trace(field: str, events, byte_lookup) -> np.ndarray:
+    """Fp2AddSubAssignChip::generate_trace (fptower/fp2_addsub.rs:93-183): padding rows add zeros."""
+    fp = FIELDS[field]
+    L = Fp2AddSubLayout(fp)
+    ne, h, m, hw = len(events), _height(len(events)), fp.modulus, fp.words
+    t = np.zeros((h, L.WIDTH), np.int64)
+    rec = EF.Rec(byte_lookup)
+    ops = [e["op"] for e in events] + ["add"] * (h - ne)
+    xs = [(EF.words_to_int(e["x"][:hw]) % m, EF.words_to_int(e["x"][hw:]) % m) for e in events]
+    ys = [(EF.words_to_int([r[0] for r in e["y"][:hw]]) % m, EF.words_to_int([r[0] for r in e["y"][hw:]]) % m)
+          for e in events]
+    xs += [(0, 0)] * (h - ne)
+    ys += [(0, 0)] * (h - ne)
+    for op in ("add", "sub"):
+        idx = [i for i in range(h) if ops[i] == op]
+        if idx:
+            for k, base in ((0, L.C0), (1, L.C1)):
+                _, c = EF.pop_field_op([xs[i][k] for i in idx], [ys[i][k] for i in idx], op, fp)
+                t[idx, base:base + fp.fop_w] = c
+    t[:, L.IS_ADD] = [o == "add" for o in ops]
+    rec.fop(t[:ne, L.C0:L.C0 + fp.fop_w], fp)
+    rec.fop(t[:ne, L.C1:L.C1 + fp.fop_w], fp)
+    if ne:
+        rows = np.arange(ne)
+        t[rows, L.REAL] = 1
+        shard = np.array([e["shard"] for e in events], np.int64)
+        clk = np.array([e["clk"] for e in events], np.int64)
+        t[rows, L.SHARD], t[rows, L.CLK] = shard, clk
+        t[rows, L.XPTR] = [e["x_ptr"] for e in events]
+        t[rows, L.YPTR] = [e["y_ptr"] for e in events]
+        _access_block(t, rows, L.Y, [e["y"] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.X, [e["xw"] for e in events], True, shard, clk + 1, byte_lookup)
+    return (t % P).astype(np.uint32)
+
+
+def fp2_mul_trace(field: str, events, byte_lookup) -> np.ndarray:
+    """Fp2MulAssignChip::generate_trace (fptower/fp2_mul.rs:122-210): padding rows multiply zeros."""
+    fp = FIELDS[field]
+    L = Fp2MulLayout(fp)
+    ne, h, m, hw = len(events), _height(len(events)), fp.modulus, fp.words
+    t = np.zeros((h, L.WIDTH), np.int64)
+    rec = EF.Rec(byte_lookup)
+    a0 = [EF.words_to_int(e["x"][:hw]) % m for e in events] + [0] * (h - ne)
+    a1 = [EF.words_to_int(e["x"][hw:]) % m for e in events] + [0] * (h - ne)
+    b0 = [EF.words_to_int([r[0] for r in e["y"][:hw]]) % m for e in events] + [0] * (h - ne)
+    b1 = [EF.words_to_int([r[0] for r in e["y"][hw:]]) % m for e in events] + [0] * (h - ne)
+    F = L.F
+    r00, t[:, F["a0_mul_b0"]:F["a0_mul_b0"] + fp.fop_w] = EF.pop_field_op(a0, b0, "mul", fp)
+    r11, t[:, F["a1_mul_b1"]:F["a1_mul_b1"] + fp.fop_w] = EF.pop_field_op(a1, b1, "mul", fp)
+    r01, t[:, F["a0_mul_b1"]:F["a0_mul_b1"] + fp.fop_w] = EF.pop_field_op(a0, b1, "mul", fp)
+    r10, t[:, F["a1_mul_b0"]:F["a1_mul_b0"] + fp.fop_w] = EF.pop_field_op(a1, b0, "mul", fp)
+    _, t[:, F["c0"]:F["c0"] + fp.fop_w] = EF.pop_field_op(r00, r11, "sub", fp)
+    _, t[:, F["c1"]:F["c1"] + fp.fop_w] = EF.pop_field_op(r01, r10, "add", fp)
+    for base in F.values():
+        rec.fop(t[:ne, base:base + fp.fop_w], fp)
+    if ne:
+        rows = np.arange(ne)
+        t[rows, L.REAL] = 1
+        shard = np.array([e["shard"] for e in events], np.int64)
+        clk = np.array([e["clk"] for e in events], np.int64)
+        t[rows, L.SHARD], t[rows, L.CLK] = shard, clk
+        t[rows, L.XPTR] = [e["x_ptr"] for e in events]
+        t[rows, L.YPTR] = [e["y_ptr"] for e in events]
+        _access_block(t, rows, L.Y, [e["y"] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.X, [e["xw"] for e in events], True, shard, clk + 1, byte_lookup)
+    return (t % P).astype(np.uint32)
+
+
+def uint256_mul_trace(events, byte_lookup) -> np.ndarray:
+    """Uint256MulChip::generate_trace (uint256/air.rs:103-186): the product mod m (2^256 when m = 0);
+    the range check result < m only when m != 0; padding rows multiply zeros modulo 2^256."""
+    L = U256L
+    ne, h = len(events), _height(len(events))
+    t = np.zeros((h, L.WIDTH), np.int64)
+    rec = EF.Rec(byte_lookup)
+    x = [EF.words_to_int(e["x"]) for e in events] + [0] * (h - ne)
+    y = [EF.words_to_int([r[0] for r in e["y"]]) for e in events] + [0] * (h - ne)
+    m = [EF.words_to_int([r[0] for r in e["m"]]) for e in events] + [0] * (h - ne)
+    eff = [mm if mm else 1 << 256 for mm in m]
+    res, c = EF.pop_field_op(x, y, "mul", U256, modulus=eff)
+    t[:, L.OUT:L.OUT + U256.fop_w] = c
+    rec.fop(t[:ne, L.OUT:L.OUT + U256.fop_w], U256)
+    real = np.zeros(h, bool)
+    real[:ne] = True
+    nz = real & np.array([mm != 0 for mm in m])
+    t[:, L.LT:L.LT + U256.lt_w] = EF.pop_field_lt(res, rec, nz, U256, rhs=[mm if mm else 0 for mm in m], fill=nz)
+    if ne:
+        rows = np.arange(ne)
+        t[rows, L.REAL] = 1
+        shard = np.array([e["shard"] for e in events], np.int64)
+        clk = np.array([e["clk"] for e in events], np.int64)
+        t[rows, L.SHARD], t[rows, L.CLK] = shard, clk
+        t[rows, L.XPTR] = [e["x_ptr"] for e in events]
+        t[rows, L.YPTR] = [e["y_ptr"] for e in events]
+        bsum = np.array([sum(int.to_bytes(mm, 32, "little")) for mm in m[:ne]], np.int64)
+        t[rows, L.IZ_RES] = bsum == 0
+        t[rows, L.IZ_INV] = [pow(int(s), P - 2, P) if s else 0 for s in bsum]
+        t[rows, L.NOT_ZERO] = bsum != 0
+        for i, e in enumerate(events):
+            assert EF.words_to_int([r[1] for r in e["xw"]]) == res[i]
+        _access_block(t, rows, L.X, [e["xw"] for e in events], True, shard, clk + 1, byte_lookup)
+        _access_block(t, rows, L.Y, [e["y"] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.M, [e["m"] for e in events], False, shard, clk, byte_lookup)
+    return (t % P).astype(np.uint32)
+
+
+# ---------------------------------------------------------------- chip registry
+def chips_in_machine_order() -> List[ChipDesc]:
+    """The chips of this module in MipsAir order (mips/mod.rs:223-318), grouped as there: secp256k1
+    add/double, secp256r1 add/double, bn254 add/double, bls12-381 add/double, Uint256MulMod, the
+    bls12-381 towers, the bn254 towers (decompress, Poseidon2Permute, KeccakSponge and U256x2048Mul sit
+    between them in the reference and are not restated)."""
+    return [weierstrass_add_chip("Secp256k1"), weierstrass_double_chip("Secp256k1"),
+            weierstrass_add_chip("Secp256r1"), weierstrass_double_chip("Secp256r1"),
+            weierstrass_add_chip("Bn254"), weierstrass_double_chip("Bn254"),
+            weierstrass_add_chip("Bls12381"), weierstrass_double_chip("Bls12381"),
+            uint256_mul_chip(),
+            fp_op_chip("Bls12381"), fp2_addsub_chip("Bls12381"), fp2_mul_chip("Bls12381"),
+            fp_op_chip("Bn254"), fp2_addsub_chip("Bn254"), fp2_mul_chip("Bn254")]
+
+
+def chip_for_key(key: int) -> str:
+    """Chip name of a precompile event key."""
+    for curve in FIELDS:
+        if key == EC_ADD[curve]:
+            return f"{curve}AddAssign"
+        if key == EC_DOUBLE[curve]:
+            return f"{curve}DoubleAssign"
+    for field in FP_OPS:
+        if key == FP_OPS[field][0]:
+            return FP_NAME[field]
+        if key == FP2_ADDSUB[field][0]:
+            return FP2_ADDSUB_NAME[field]
+        if key == FP2_MUL[field]:
+            return FP2_MUL_NAME[field]
+    if key == UINT256_MUL:
+        return "Uint256MulMod"
+    raise KeyError(hex(key))
+
+
+def trace_for_key(key: int, events, byte_lookup) -> np.ndarray:
+    for curve in FIELDS:
+        if key == EC_ADD[curve]:
+            return weierstrass_add_trace(curve, events, byte_lookup)
+        if key == EC_DOUBLE[curve]:
+            return weierstrass_double_trace(curve, events, byte_lookup)
+    for field in FP_OPS:
+        if key == FP_OPS[field][0]:
+            return fp_op_trace(field, events, byte_lookup)
+        if key == FP2_ADDSUB[field][0]:
+            return fp2_addsub_trace(field, events, byte_lookup)
+        if key == FP2_MUL[field]:
+            return fp2_mul_trace(field, events, byte_lookup)
+    if key == UINT256_MUL:
+        return uint256_mul_trace(events, byte_lookup)
+    raise KeyError(hex(key))
+
+
+# ---------------------------------------------------------------- a guest exercising every syscall here
+def ec_program(seed: int = 1, reps: int = 2, halt: bool = True):
+    """A guest that calls every precompile of this module `reps` times: per curve P <- P + Q and
+    Q <- 2 Q on random points; per tower field x <- x op y for op in add, sub, mul (Fp) and add, sub, mul
+    (Fp2); Uint256MulMod with a random modulus and with modulus 0 (2^256).  The result words are read
+    back and folded into a register that is committed, then HALT."""
+    from . import mips_alu as A
+    from . import mips_core as MC
+    from . import mips_syscall as SY
+    rng = np.random.default_rng(seed)
+    prog = []
+    acc, tmp = 10, 9
+    slot = [MC.DATA_BASE + 0x4000]
+
+    def alloc(nbytes):
+        p = slot[0]
+        slot[0] += (nbytes + 63) // 64 * 64
+        return p
+
+    def li(reg, v):
+        prog.append((A.OP_ADD, reg, 0, int(v) & 0xFFFFFFFF, 0, 1))
+
+    def store(ptr, words):
+        for i, w in enumerate(words):
+            li(8, w)
+            prog.append((MC.OP_SW, 8, 0, ptr + 4 * i, 0, 1))
+
+    def syscall(code, a0, a1):
+        li(SY.REG_V0, code)
+        li(SY.REG_A0, a0)
+        li(SY.REG_A1, a1)
+        prog.append((SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0))
+
+    def fold(ptr, n):
+        for i in range(n):
+            prog.append((MC.OP_LW, tmp, 0, ptr + 4 * i, 0, 1))
+            prog.append((A.OP_XOR, acc, acc, tmp, 0, 0))
+
+    li(acc, 0)
+    for curve in FIELDS:
+        nw = 2 * FIELDS[curve].words
+        pp, qp = alloc(4 * nw), alloc(4 * nw)
+        store(pp, point_words(curve, random_point(curve, rng)))
+        store(qp, point_words(curve, random_point(curve, rng)))
+        for _ in range(reps):
+            syscall(EC_ADD[curve], pp, qp)
+            syscall(EC_DOUBLE[curve], qp, 0)
+        fold(pp, nw)
+        fold(qp, nw)
+    for field in FP_OPS:
+        fp = FIELDS[field]
+        w = fp.words
+        xp, yp = alloc(4 * w), alloc(4 * w)
+        store(xp, EF.int_to_words(int.from_bytes(rng.bytes(fp.nl), "little") % fp.modulus, w))
+        store(yp, EF.int_to_words(int.from_bytes(rng.bytes(fp.nl), "little") % fp.modulus, w))
+        for _ in range(reps):
+            for code in FP_OPS[field]:
+                syscall(code, xp, yp)
+        fold(xp, w)
+        x2, y2 = alloc(8 * w), alloc(8 * w)
+        store(x2, EF.int_to_words(int.from_bytes(rng.bytes(fp.nl), "little") % fp.modulus, w)
+              + EF.int_to_words(int.from_bytes(rng.bytes(fp.nl), "little") % fp.modulus, w))
+        store(y2, EF.int_to_words(int.from_bytes(rng.bytes(fp.nl), "little") % fp.modulus, w)
+              + EF.int_to_words(int.from_bytes(rng.bytes(fp.nl), "little") % fp.modulus, w))
+        for _ in range(reps):
+            for code in FP2_ADDSUB[field] + (FP2_MUL[field],):
+                syscall(code, x2, y2)
+        fold(x2, 2 * w)
+    for zero_mod in (False, True):
+        # operands below the modulus (the carry has 32 limbs: x y / m < 2^256)
+        xp, yp = alloc(32), alloc(64)
+        m = 0 if zero_mod else int.from_bytes(rng.bytes(32), "little") | (1 << 255) | 1
+        bound = m if m else 1 << 256
+        store(xp, EF.int_to_words(int.from_bytes(rng.bytes(32), "little") % bound, 8))
+        store(yp, EF.int_to_words(int.from_bytes(rng.bytes(32), "little") % bound, 8) + EF.int_to_words(m, 8))
+        for _ in range(reps):
+            syscall(UINT256_MUL, xp, yp)
+        fold(xp, 8)
+    prog += [(A.OP_ADD, SY.REG_V0, 0, SY.COMMIT, 0, 1), (A.OP_ADD, SY.REG_A0, 0, 0, 0, 1),
+             (A.OP_ADD, SY.REG_A1, acc, 0, 0, 1), (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
+    if halt:
+        prog += [(A.OP_ADD, SY.REG_V0, 0, SY.HALT, 0, 1), (A.OP_ADD, SY.REG_A0, 0, 0, 0, 1),
+                 (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
+    return prog

@@ -26,6 +26,7 @@ from typing import List, Sequence
 
 import numpy as np
 
+from . import emulated_field as EF
 from . import mips_alu as A
 from .machine import ChipDesc, Expr, KIND_BYTE, KIND_SYSCALL, Lookup, P, main
 from .machine import VirtualPairCol as V
@@ -70,54 +71,13 @@ ED_NEGX = ED_SQRT_LSB + 1
 ED_WIDTH = ED_NEGX + FOP_W      # 1566
 
 
-# ---------------------------------------------------------------- polynomials over limbs (AIR side)
-# A polynomial is a list of coefficients, each an int (a constant) or an Expr.
-def _add(a, b):
-    if isinstance(a, int) and isinstance(b, int):
-        return (a + b) % P
-    if isinstance(a, int) and a % P == 0:
-        return b
-    if isinstance(b, int) and b % P == 0:
-        return a
-    return a + b
-
-
-def _mulc(a, b):
-    if isinstance(a, int) and isinstance(b, int):
-        return a * b % P
-    if isinstance(a, int):
-        a, b = b, a
-    if isinstance(b, int):
-        if b % P == 0:
-            return 0
-        if b % P == 1:
-            return a
-    return a * b
-
-
-def p_add(a: Sequence, b: Sequence) -> List:
-    return [_add(a[i] if i < len(a) else 0, b[i] if i < len(b) else 0) for i in range(max(len(a), len(b)))]
-
-
-def p_neg(a: Sequence) -> List:
-    return [(-x) % P if isinstance(x, int) else -x for x in a]
-
-
-def p_sub(a: Sequence, b: Sequence) -> List:
-    return p_add(a, p_neg(b))
-
-
-def p_mul(a: Sequence, b: Sequence) -> List:
-    """Polynomial::mul (zkm_stark air/polynomial.rs): coefficient k = sum_{i + j = k} a_i b_j."""
-    out = [0] * (len(a) + len(b) - 1)
-    for i, x in enumerate(a):
-        for j, y in enumerate(b):
-            out[i + j] = _add(out[i + j], _mulc(x, y))
-    return out
+# ---------------------------------------------------------------- emulated-field gadgets (emulated_field.py)
+ED_FP = EF.FieldParams("Ed25519BaseField", ED_P, NL, NWIT, WITNESS_OFFSET)
+p_add, p_sub, p_mul = EF.p_add, EF.p_sub, EF.p_mul
 
 
 def _cols(base: int, n: int = NL) -> List[Expr]:
-    return [main(base + i) for i in range(n)]
+    return EF.cols(base, n)
 
 
 def _write_prev_limbs(base: int, words: int) -> List[Expr]:
@@ -134,95 +94,23 @@ def _read_limbs(base: int, words: int) -> List[Expr]:
     return [main(base + RD_W * w + ACC_VALUE + i) for w in range(words) for i in range(4)]
 
 
-def _u8_range(ch: ChipDesc, cols: Sequence[V], mult: V):
-    """slice_range_check_u8 (air/word.rs:55-80): U8Range byte lookups on pairs (a trailing single with 0)."""
-    for k in range(0, len(cols) - 1, 2):
-        ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, cols[k], cols[k + 1]], mult, KIND_BYTE))
-    if len(cols) % 2:
-        ch.sends.append(Lookup([V.const(A.B_U8RANGE), ZERO, ZERO, cols[-1], ZERO], mult, KIND_BYTE))
-
-
-def _vcols(base: int, n: int) -> List[V]:
-    return [_m(base + i) for i in range(n)]
-
-
-def eval_field_operation(ch: ChipDesc, vanishing: Sequence, base: int):
-    """util_air.rs eval_field_operation: with w(x) = witness_low(x) + 2^8 witness_high(x) - OFFSET, every
-    coefficient of vanishing(x) - w(x) (x - 2^8) is zero (63 constraints for a 32-limb field)."""
-    wlo, whi = base + 2 * NL, base + 2 * NL + NWIT
-    w = [main(wlo + j) + main(whi + j) * 256 - WITNESS_OFFSET for j in range(NWIT)]
-    # w(x) * (x - 256): coefficient k = w_{k-1} - 256 w_k
-    prod = [0] * (NWIT + 1)
-    for j in range(NWIT):
-        prod[j] = _add(prod[j], w[j] * (P - 256))
-        prod[j + 1] = _add(prod[j + 1], w[j])
-    for c in p_sub(vanishing, prod):
-        ch.assert_zero(Expr.lift(c))
-
-
-def _field_range_checks(ch: ChipDesc, base: int, mult: V, result_cols: Sequence[V] = None):
-    """The four slice_range_check_u8 of an emulated-field operation (result, carry, witness low/high)."""
-    _u8_range(ch, _vcols(base, NL) if result_cols is None else result_cols, mult)
-    _u8_range(ch, _vcols(base + NL, NL), mult)
-    _u8_range(ch, _vcols(base + 2 * NL, NWIT), mult)
-    _u8_range(ch, _vcols(base + 2 * NL + NWIT, NWIT), mult)
+_u8_range, _vcols = EF.u8_range, EF.vcols
 
 
 def eval_field_op(ch: ChipDesc, base: int, a, b, op: str, mult: V, result=None, result_cols=None):
-    """FieldOpCols::eval / eval_with_modulus (field_op.rs:419-444, :365-394) with the Ed25519 modulus.
-    `result` overrides the result polynomial (FieldSqrtCols passes the input `a` there)."""
-    res = _cols(base) if result is None else result
-    carry = _cols(base + NL)
-    if op in ("add", "mul"):
-        pa, pres = a, res
-    else:  # sub / div: a = result op b
-        pa, pres = res, a
-    pop = p_add(pa, b) if op in ("add", "sub") else p_mul(pa, b)
-    vanishing = p_sub(p_sub(pop, pres), p_mul(carry, MOD_LIMBS))
-    eval_field_operation(ch, vanishing, base)
-    _field_range_checks(ch, base, mult, result_cols)
+    EF.eval_field_op(ch, base, a, b, op, mult, ED_FP, result=result, result_cols=result_cols)
 
 
 def eval_inner_product(ch: ChipDesc, base: int, a_vec, b_vec, mult: V):
-    """FieldInnerProductCols::eval (field_inner_product.rs:121-170)."""
-    acc = [0]
-    for pa, pb in zip(a_vec, b_vec):
-        acc = p_add(acc, p_mul(pa, pb))
-    vanishing = p_sub(p_sub(acc, _cols(base)), p_mul(_cols(base + NL), MOD_LIMBS))
-    eval_field_operation(ch, vanishing, base)
-    _field_range_checks(ch, base, mult)
+    EF.eval_inner_product(ch, base, a_vec, b_vec, mult, ED_FP)
 
 
 def eval_den(ch: ChipDesc, base: int, a, b, sign: bool, mult: V):
-    """FieldDenCols::eval (field_den.rs:124-175): a / (1 + b) if sign else a / (1 - b)."""
-    res, carry = _cols(base), _cols(base + NL)
-    br = p_mul(b, res)
-    lhs = p_add(br, res) if sign else p_add(br, a)
-    rhs = a if sign else res
-    vanishing = p_sub(p_sub(lhs, rhs), p_mul(carry, MOD_LIMBS))
-    eval_field_operation(ch, vanishing, base)
-    _field_range_checks(ch, base, mult)
+    EF.eval_den(ch, base, a, b, sign, mult, ED_FP)
 
 
 def eval_field_lt(ch: ChipDesc, base: int, lhs: Sequence, rhs: Sequence, is_real: Expr, mult: V):
-    """FieldLtCols::eval (range.rs:62-141): exactly one byte flag, bytes equal above it, and the LTU byte
-    lookup on the flagged pair."""
-    flags = _cols(base)
-    total = Expr.lift(0)
-    for f in flags:
-        _assert_bool(ch, f, is_real)
-        total = total + f
-    ch.assert_zero(is_real * (total - 1))
-    visited = Expr.lift(0)
-    lcmp, rcmp = Expr.lift(0), Expr.lift(0)
-    for lb, rb, f in zip(reversed(lhs), reversed(rhs), reversed(flags)):
-        visited = visited + f
-        lcmp = lcmp + Expr.lift(lb) * f
-        rcmp = rcmp + f * Expr.lift(rb)
-        ch.assert_zero(is_real * (1 - visited) * (Expr.lift(lb) - Expr.lift(rb)))
-    ch.assert_zero(is_real * (main(base + NL) - lcmp))
-    ch.assert_zero(is_real * (main(base + NL + 1) - rcmp))
-    ch.sends.append(Lookup([V.const(A.B_LTU), V.const(1), ZERO, _m(base + NL), _m(base + NL + 1)], mult, KIND_BYTE))
+    EF.eval_field_lt(ch, base, lhs, rhs, is_real, mult, ED_FP)
 
 
 def _eval_access_slice(ch: ChipDesc, base: int, words: int, write: bool, ptr_col: int, addr_off: int, clk_pos: int,
@@ -332,129 +220,26 @@ def ed_decompress_point(y: int, sign: int):
 
 
 def _limbs(xs: Sequence[int], n: int = NL) -> np.ndarray:
-    return np.array([list(int(x).to_bytes(n, "little")) for x in xs], np.int64).reshape(len(xs), n)
+    return EF.limbs(xs, n)
 
 
-def _pmul_np(a: np.ndarray, b: np.ndarray) -> np.ndarray:
-    out = np.zeros((a.shape[0], a.shape[1] + b.shape[1] - 1), np.int64)
-    for i in range(a.shape[1]):
-        out[:, i:i + b.shape[1]] += a[:, i:i + 1] * b
-    return out
-
-
-def _padd_np(*ps) -> np.ndarray:
-    n = max(p.shape[1] for p in ps)
-    out = np.zeros((ps[0].shape[0], n), np.int64)
-    for p in ps:
-        out[:, :p.shape[1]] += p
-    return out
-
-
-_MODL = np.array(MOD_LIMBS, np.int64)[None, :]
-
-
-def _witness(vanishing: np.ndarray) -> np.ndarray:
-    """compute_root_quotient_and_shift + split (util.rs:20-72): w(x) = vanishing(x) / (x - 256), shifted by
-    the offset; returns (n, 124): the low bytes then the high bytes."""
-    v = vanishing
-    assert v.shape[1] <= NWIT + 1
-    v = np.pad(v, ((0, 0), (0, NWIT + 1 - v.shape[1])))
-    q = np.zeros((v.shape[0], NWIT), np.int64)
-    q[:, NWIT - 1] = v[:, NWIT]
-    for k in range(NWIT - 1, 0, -1):
-        q[:, k - 1] = v[:, k] + 256 * q[:, k]
-    assert np.all(v[:, 0] == -256 * q[:, 0]), "the vanishing polynomial has no root at 2^8"
-    q = q + WITNESS_OFFSET
-    assert np.all((q >= 0) & (q < (1 << 16)))
-    return np.concatenate([q & 0xFF, q >> 8], axis=1)
-
-
-class _Rec:
-    """Byte lookups of one trace, recorded as (opcode, b, c) arrays (added to the Byte chip's
-    multiplicities only for real rows)."""
-
-    def __init__(self, byte_lookup):
-        self.bl = byte_lookup
-
-    def u8(self, x: np.ndarray):
-        """add_u8_range_checks_field on the columns x (n, k): pairs (and a trailing single with 0)."""
-        k = x.shape[1]
-        for j in range(0, k - 1, 2):
-            self.bl(A.B_U8RANGE, x[:, j], x[:, j + 1])
-        if k % 2:
-            self.bl(A.B_U8RANGE, x[:, k - 1], np.zeros(len(x), np.int64))
-
-
-def _fop_cols(res: np.ndarray, carry: np.ndarray, vanishing: np.ndarray) -> np.ndarray:
-    return np.concatenate([res, carry, _witness(vanishing)], axis=1)
+_Rec = EF.Rec
 
 
 def pop_field_op(a: Sequence[int], b: Sequence[int], op: str):
-    """FieldOpCols::populate_with_modulus (field_op.rs:193-266) for the Ed25519 modulus over a batch:
-    returns (result ints, (n, 188) columns).  sub / div populate as (result + b) / (result * b)."""
-    n = len(a)
-    if op == "sub":
-        r = [(ED_P + x - y) % ED_P for x, y in zip(a, b)]
-        lhs, rhs, mode = r, b, "add"
-    elif op == "div":
-        assert all(y or not x for x, y in zip(a, b)), "division by zero is allowed only when dividing zero"
-        r = [x * pow(y, ED_P - 2, ED_P) % ED_P if y else 0 for x, y in zip(a, b)]
-        lhs, rhs, mode = r, b, "mul"
-    else:
-        lhs, rhs, mode = a, b, op
-        r = [((x + y) if op == "add" else (x * y)) % ED_P for x, y in zip(a, b)]
-    full = [(x + y) if mode == "add" else (x * y) for x, y in zip(lhs, rhs)]
-    mres = [f % ED_P for f in full]
-    carry = [(f - m) // ED_P for f, m in zip(full, mres)]
-    la, lb = _limbs(lhs), _limbs(rhs)
-    pop = (la + lb) if mode == "add" else _pmul_np(la, lb)
-    van = _padd_np(pop, -_limbs(mres), -_pmul_np(_limbs(carry), _MODL))
-    return r, _fop_cols(_limbs(r), _limbs(carry), van)
+    return EF.pop_field_op(a, b, op, ED_FP)
 
 
 def pop_inner_product(a_vec, b_vec):
-    """FieldInnerProductCols::populate (field_inner_product.rs:33-94)."""
-    n = len(a_vec[0])
-    ip = [sum(a[i] * b[i] for a, b in zip(a_vec, b_vec)) for i in range(n)]
-    r = [x % ED_P for x in ip]
-    carry = [(x - y) // ED_P for x, y in zip(ip, r)]
-    acc = _padd_np(*[_pmul_np(_limbs(a), _limbs(b)) for a, b in zip(a_vec, b_vec)])
-    van = _padd_np(acc, -_limbs(r), -_pmul_np(_limbs(carry), _MODL))
-    return r, _fop_cols(_limbs(r), _limbs(carry), van)
+    return EF.pop_inner_product(a_vec, b_vec, ED_FP)
 
 
 def pop_den(a: Sequence[int], b: Sequence[int], sign: bool):
-    """FieldDenCols::populate (field_den.rs:33-94)."""
-    r, carry = [], []
-    for x, y in zip(a, b):
-        den = ((y if sign else ED_P - y) + 1) % ED_P
-        res = x * pow(den, ED_P - 2, ED_P) % ED_P
-        lhs = y * res + res if sign else y * res + x
-        rhs = x if sign else res
-        r.append(res)
-        carry.append((lhs - rhs) // ED_P)
-    lr, lb, la = _limbs(r), _limbs(b), _limbs(a)
-    br = _pmul_np(lb, lr)
-    lhs = _padd_np(br, lr) if sign else _padd_np(br, la)
-    rhs = la if sign else lr
-    van = _padd_np(lhs, -rhs, -_pmul_np(_limbs(carry), _MODL))
-    return r, _fop_cols(lr, _limbs(carry), van)
+    return EF.pop_den(a, b, sign, ED_FP)
 
 
-def pop_field_lt(lhs: Sequence[int], rec: _Rec, real: np.ndarray) -> np.ndarray:
-    """FieldLtCols::populate (range.rs:27-58) with rhs = the modulus."""
-    L = _limbs(lhs)
-    out = np.zeros((len(lhs), LT_W), np.int64)
-    for i in range(len(lhs)):
-        assert lhs[i] < ED_P
-        for k in range(NL - 1, -1, -1):
-            if L[i, k] < MOD_LIMBS[k]:
-                out[i, k] = 1
-                out[i, NL], out[i, NL + 1] = L[i, k], MOD_LIMBS[k]
-                break
-    if real.any():
-        rec.bl(A.B_LTU, out[real, NL], out[real, NL + 1])
-    return out
+def pop_field_lt(lhs: Sequence[int], rec, real: np.ndarray) -> np.ndarray:
+    return EF.pop_field_lt(lhs, rec, real, ED_FP)
 
 
 # ---------------------------------------------------------------- traces
@@ -473,8 +258,7 @@ def _access_block(t, rows, base, recs, write: bool, shard, clk, byte_lookup):
         _access_cols(t, rows, acc, value.astype(np.uint32), prev, shard, clk, np.ones(len(rows), bool), byte_lookup)
 
 
-def _words_to_int(ws) -> int:
-    return int.from_bytes(b"".join(int(w).to_bytes(4, "little") for w in ws), "little")
+_words_to_int = EF.words_to_int
 
 
 def ed_add_trace(events, byte_lookup) -> np.ndarray:

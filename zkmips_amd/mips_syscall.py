@@ -1227,3 +1227,12 @@ def _exec_ed_decompress(pm, shard, clk, a0, a1):
 ED_ADD, ED_DECOMPRESS = 0x01_01_00_07, 0x00_01_00_08  # executor/src/syscalls/code.rs:50-54
 PRECOMPILES = {SHA_EXTEND: exec_sha_extend, SHA_COMPRESS: exec_sha_compress, ED_ADD: _exec_ed_add,
                ED_DECOMPRESS: _exec_ed_decompress}
+
+
+def _ec_precompiles():
+    from . import mips_ec as EC
+    return EC.precompile_table(), EC.PRECOMPILE_KEY
+
+
+_EC_TABLE, PRECOMPILE_KEY = _ec_precompiles()  # Weierstrass curves, field towers, Uint256MulMod (mips_ec.py)
+PRECOMPILES.update(_EC_TABLE)
