@@ -67,6 +67,9 @@ def main():
                 m = re.search(r"fn " + fn + r"\(\) -> BigUint \{\s*BigUint::from\((\d+)u32\)", src)
                 if m:
                     e[fn + "_u32_le"] = [int(m.group(1))]
+        g = re.search(r"fn generator\(\) -> \(BigUint, BigUint\) \{(.*?)\n    \}", src, re.S)
+        if g:
+            e["generator"] = [str(int(v)) for v in re.findall(r'"(\d+)"', g.group(1))]
         params[name] = e
     json.dump(params, open(os.path.join(HERE, "curve_params.json"), "w"), indent=1)
 

@@ -80,6 +80,10 @@ for _field, _shape in (("Bn254", ((372, 81), (734, 160), (1485, 348))),
                                          _PRE + "fptower/fp2_addsub.rs:79", _PRE + "fptower/fp2_addsub.rs:210")
     CHIPS[EC.FP2_MUL_NAME[_field]] = (lambda f=_field: EC.fp2_mul_chip(f), 0, *_shape[2], 1, True,
                                       _PRE + "fptower/fp2_mul.rs:122", _PRE + "fptower/fp2_mul.rs:227")
+for _curve, _w, _perm in (("Secp256k1", 1378, 325), ("Secp256r1", 1378, 325), ("Bls12381", 2177, 491)):
+    CHIPS[f"{_curve}Decompress"] = (lambda c=_curve: EC.weierstrass_decompress_chip(c), 0, _w, _perm, 1, True,
+                                    _PRE + "weierstrass/weierstrass_decompress.rs:145",
+                                    _PRE + "weierstrass/weierstrass_decompress.rs:304")
 CHIPS["Uint256MulMod"] = (EC.uint256_mul_chip, 0, 480, 98, 1, True, _PRE + "uint256/air.rs:93",
                           _PRE + "uint256/air.rs:218")
 # precompile chips are costed per call: rows per event x per-row cost (mips/mod.rs:216-222)

@@ -38,6 +38,10 @@ def test_field_params_equal_reference():
         if name != "U256":
             assert _le(r.get("a_int_u32_le", [0])) == EC.CURVE_A[name], name
             assert _le(r["b_int_u32_le"]) == EC.CURVE_B[name], name
+        if name in EC.GEN_X:
+            gx, gy = (int(v) for v in r["generator"])
+            assert gx == EC.GEN_X[name], name
+            assert EC.point_from_x(name, gx)[1] in (gy, fp.modulus - gy), name
 
 
 @pytest.mark.parametrize("curve", sorted(EC.FIELDS))
@@ -50,6 +54,21 @@ def test_curve_arithmetic(curve):
     assert on(p) and on(q) and on(s) and on(d)
     assert EC.sw_add(curve, s, (q[0], (m - q[1]) % m)) == p  # (P + Q) - Q
     assert EC.sw_add(curve, d, (p[0], (m - p[1]) % m)) == p  # 2P - P
+
+
+@pytest.mark.parametrize("curve", sorted(EC.EC_DECOMPRESS))
+def test_decompress_sign_rule(curve):
+    rng = np.random.default_rng(7)
+    m = EC.FIELDS[curve].modulus
+    for _ in range(4):
+        x, y = EC.random_point(curve, rng)
+        for sign in (0, 1):
+            yy = EC.decompress_y(curve, x, sign)
+            assert yy in (y, m - y)
+            if EC.LEXICOGRAPHIC[curve]:
+                assert (yy > m - yy) == bool(sign)
+            else:
+                assert yy & 1 == sign
 
 
 @pytest.fixture(scope="module")
@@ -73,7 +92,11 @@ def test_execution_satisfies_air(run):
                                       ("Bls12381DoubleAssign",
                                        lambda: EC.DoubleLayout(EC.FIELDS["Bls12381"]).F["y3_ins"]),
                                       ("Bn254Fp2MulAssign", lambda: EC.Fp2MulLayout(EC.FIELDS["Bn254"]).F["c1"]),
-                                      ("Uint256MulMod", lambda: EC.U256L.OUT)])
+                                      ("Uint256MulMod", lambda: EC.U256L.OUT),
+                                      ("Bls12381Decompress",
+                                       lambda: EC.DecompressLayout(EC.FIELDS["Bls12381"], True).SQRT),
+                                      ("Secp256k1Decompress",
+                                       lambda: EC.DecompressLayout(EC.FIELDS["Secp256k1"], False).NEGY)])
 def test_forged_result_is_rejected(run, chip, col):
     m, prep, tr, pv = next(r for r in run if chip in r[2])
     bad_tr = dict(tr)

@@ -111,7 +111,7 @@ static constexpr uint64_t SMALL16 = 8192;  // levels with <= SMALL16 nodes use t
 static constexpr int NT_TOP = 1024;
 static constexpr uint64_t TOP_MAX = NT_TOP / 16;  // levels with <= TOP_MAX nodes: one workgroup
 static uint64_t sub16_max() {  // levels with <= this many nodes: k_subtree16 (ZKM_SUB16 overrides)
-    static const uint64_t v = getenv("ZKM_SUB16") ? strtoull(getenv("ZKM_SUB16"), nullptr, 10) : 32768;
+    static const uint64_t v = getenv("ZKM_SUB16") ? strtoull(getenv("ZKM_SUB16"), nullptr, 10) : 16384;
     return v;
 }
 

@@ -51,6 +51,12 @@ CURVE_B = {"Secp256k1": 7,
            "Secp256r1": 0x5AC635D8AA3A93E7B3EBBD55769886BC651D06B0CC53B0F63BCE3C3E27D2604B,
            "Bn254": 3, "Bls12381": 4}
 
+# the generators' abscissae (padding rows of the decompress chips decompress E::generator().0)
+GEN_X = {"Secp256k1": 0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798,
+         "Secp256r1": 0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296,
+         "Bls12381": int("17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00"
+                         "adb22c6bb", 16)}
+
 # SyscallCode (crates/core/executor/src/syscalls/code.rs:60-141)
 SECP256K1_ADD, SECP256K1_DOUBLE = 0x01_01_00_0A, 0x00_01_00_0B
 BN254_ADD, BN254_DOUBLE = 0x01_01_00_0E, 0x00_01_00_0F
@@ -61,6 +67,12 @@ BLS12381_FP2_ADD, BLS12381_FP2_SUB, BLS12381_FP2_MUL = 0x01_01_00_23, 0x01_01_00
 BN254_FP_ADD, BN254_FP_SUB, BN254_FP_MUL = 0x01_01_00_26, 0x01_01_00_27, 0x01_01_00_28
 BN254_FP2_ADD, BN254_FP2_SUB, BN254_FP2_MUL = 0x01_01_00_29, 0x01_01_00_2A, 0x01_01_00_2B
 SECP256R1_ADD, SECP256R1_DOUBLE = 0x01_01_00_2C, 0x00_01_00_2D
+SECP256K1_DECOMPRESS, SECP256R1_DECOMPRESS, BLS12381_DECOMPRESS = 0x00_01_00_0C, 0x00_01_00_2E, 0x00_01_00_1C
+EC_DECOMPRESS = {"Secp256k1": SECP256K1_DECOMPRESS, "Secp256r1": SECP256R1_DECOMPRESS,
+                 "Bls12381": BLS12381_DECOMPRESS}
+# SignChoiceRule (weierstrass_decompress.rs:82-112): the k256 / p256 chips take y's parity, bls12-381
+# the lexicographic order of y and -y
+LEXICOGRAPHIC = {"Secp256k1": False, "Secp256r1": False, "Bls12381": True}
 
 EC_ADD = {"Secp256k1": SECP256K1_ADD, "Secp256r1": SECP256R1_ADD, "Bn254": BN254_ADD, "Bls12381": BLS12381_ADD}
 EC_DOUBLE = {"Secp256k1": SECP256K1_DOUBLE, "Secp256r1": SECP256R1_DOUBLE, "Bn254": BN254_DOUBLE,
@@ -543,6 +555,8 @@ def precompile_table():
             t[code] = _bind(exec_fp2_addsub, field, op)
         t[FP2_MUL[field]] = _bind(exec_fp2_mul, field)
     t[UINT256_MUL] = exec_uint256_mul
+    for curve in EC_DECOMPRESS:
+        t[EC_DECOMPRESS[curve]] = _bind(exec_ec_decompress, curve)
     return t
 
 
@@ -791,21 +805,26 @@ def uint256_mul_trace(events, byte_lookup) -> np.ndarray:
 
 # ---------------------------------------------------------------- chip registry
 def chips_in_machine_order() -> List[ChipDesc]:
-    """The chips of this module in MipsAir order (mips/mod.rs:223-318), grouped as there: secp256k1
-    add/double, secp256r1 add/double, bn254 add/double, bls12-381 add/double, Uint256MulMod, the
-    bls12-381 towers, the bn254 towers (decompress, Poseidon2Permute, KeccakSponge and U256x2048Mul sit
+    """The chips of this module in MipsAir order (mips/mod.rs:223-318): secp256k1 decompress/add/double,
+    secp256r1 decompress/add/double, bn254 add/double, bls12-381 add/double, Uint256MulMod, the bls12-381
+    towers, the bn254 towers, bls12-381 decompress (Poseidon2Permute, KeccakSponge and U256x2048Mul sit
     between them in the reference and are not restated)."""
-    return [weierstrass_add_chip("Secp256k1"), weierstrass_double_chip("Secp256k1"),
+    return [weierstrass_decompress_chip("Secp256k1"), weierstrass_add_chip("Secp256k1"),
+            weierstrass_double_chip("Secp256k1"), weierstrass_decompress_chip("Secp256r1"),
             weierstrass_add_chip("Secp256r1"), weierstrass_double_chip("Secp256r1"),
             weierstrass_add_chip("Bn254"), weierstrass_double_chip("Bn254"),
             weierstrass_add_chip("Bls12381"), weierstrass_double_chip("Bls12381"),
             uint256_mul_chip(),
             fp_op_chip("Bls12381"), fp2_addsub_chip("Bls12381"), fp2_mul_chip("Bls12381"),
-            fp_op_chip("Bn254"), fp2_addsub_chip("Bn254"), fp2_mul_chip("Bn254")]
+            fp_op_chip("Bn254"), fp2_addsub_chip("Bn254"), fp2_mul_chip("Bn254"),
+            weierstrass_decompress_chip("Bls12381")]
 
 
 def chip_for_key(key: int) -> str:
     """Chip name of a precompile event key."""
+    for curve in EC_DECOMPRESS:
+        if key == EC_DECOMPRESS[curve]:
+            return f"{curve}Decompress"
     for curve in FIELDS:
         if key == EC_ADD[curve]:
             return f"{curve}AddAssign"
@@ -824,6 +843,9 @@ def chip_for_key(key: int) -> str:
 
 
 def trace_for_key(key: int, events, byte_lookup) -> np.ndarray:
+    for curve in EC_DECOMPRESS:
+        if key == EC_DECOMPRESS[curve]:
+            return weierstrass_decompress_trace(curve, events, byte_lookup)
     for curve in FIELDS:
         if key == EC_ADD[curve]:
             return weierstrass_add_trace(curve, events, byte_lookup)
@@ -890,6 +912,13 @@ def ec_program(seed: int = 1, reps: int = 2, halt: bool = True):
             syscall(EC_DOUBLE[curve], qp, 0)
         fold(pp, nw)
         fold(qp, nw)
+        if curve in EC_DECOMPRESS:  # decompress a fresh point's x with either sign: y lands at the slot's start
+            w = FIELDS[curve].words
+            for sign in (0, 1):
+                dp = alloc(8 * w)
+                store(dp + 4 * w, EF.int_to_words(random_point(curve, rng)[0], w))
+                syscall(EC_DECOMPRESS[curve], dp, sign)
+                fold(dp, w)
     for field in FP_OPS:
         fp = FIELDS[field]
         w = fp.words
@@ -925,3 +954,194 @@ def ec_program(seed: int = 1, reps: int = 2, halt: bool = True):
         prog += [(A.OP_ADD, SY.REG_V0, 0, SY.HALT, 0, 1), (A.OP_ADD, SY.REG_A0, 0, 0, 0, 1),
                  (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
     return prog
+
+
+# ---------------------------------------------------------------- Weierstrass decompress
+class DecompressLayout:
+    """WeierstrassDecompressCols (weierstrass_decompress.rs:49-65) + LexicographicChoiceCols (:67-80)."""
+
+    def __init__(self, fp: FieldParams, lex: bool):
+        w = fp.words
+        self.REAL, self.SHARD, self.CLK, self.PTR, self.SIGN = range(5)
+        self.X = 5                                   # x_access: MemoryReadCols
+        self.Y = self.X + w * RD_W                   # y_access: MemoryReadWriteCols (prev_value + access)
+        self.RANGE_X = self.Y + w * WR_W
+        self.X2 = self.RANGE_X + fp.lt_w
+        self.X3 = self.X2 + fp.fop_w
+        self.AXB = self.X3 + fp.fop_w                # FieldInnerProductCols
+        self.X3AXB = self.AXB + fp.fop_w
+        self.SQRT = self.X3AXB + fp.fop_w            # FieldSqrtCols: multiplication, range, lsb
+        self.SQRT_RANGE = self.SQRT + fp.fop_w
+        self.SQRT_LSB = self.SQRT_RANGE + fp.lt_w
+        self.NEGY = self.SQRT_LSB + 1
+        self.WIDTH = self.NEGY + fp.fop_w
+        if lex:
+            self.CMP = self.WIDTH                    # comparison_lt_cols
+            self.NEGY_RANGE = self.CMP + fp.lt_w     # neg_y_range_check
+            self.IS_Y_EQ = self.NEGY_RANGE + fp.lt_w
+            self.WHEN_SQRT_LT = self.IS_Y_EQ + 1
+            self.WHEN_NEG_LT = self.WHEN_SQRT_LT + 1
+            self.WIDTH = self.WHEN_NEG_LT + 1
+
+
+def weierstrass_decompress_chip(curve: str) -> ChipDesc:
+    """WeierstrassDecompressChip::eval (weierstrass_decompress.rs:327-492)."""
+    from . import mips_alu as A
+    from .machine import KIND_BYTE
+    from .mips_alu import ZERO
+    fp, lex = FIELDS[curve], LEXICOGRAPHIC[curve]
+    L = DecompressLayout(fp, lex)
+    nl, w = fp.nl, fp.words
+    ch = ChipDesc(f"{curve}Decompress", prep_width=0, main_width=L.WIDTH, local_only=True)
+    real, rv = main(L.REAL), _m(L.REAL)
+    sign = main(L.SIGN)
+    _assert_bool(ch, sign)
+    x = _read_limbs(L.X, w)
+    EF.eval_field_lt(ch, L.RANGE_X, x, fp.mod_limbs, real, rv, fp)
+    EF.eval_field_op(ch, L.X2, x, x, "mul", rv, fp)
+    EF.eval_field_op(ch, L.X3, EF.cols(L.X2, nl), x, "mul", rv, fp)
+    EF.eval_inner_product(ch, L.AXB, [EF.const_limbs(CURVE_A[curve], fp), EF.const_limbs(CURVE_B[curve], fp)],
+                          [x, EF.const_limbs(1, fp)], rv, fp)
+    EF.eval_field_op(ch, L.X3AXB, EF.cols(L.X3, nl), EF.cols(L.AXB, nl), "add", rv, fp)
+    sqrt = EF.cols(L.SQRT, nl)
+    EF.eval_field_op(ch, L.NEGY, [0], sqrt, "sub", rv, fp)
+    # FieldSqrtCols::eval (field_sqrt.rs:100-145) with is_odd = its own lsb column
+    EF.eval_field_op(ch, L.SQRT, sqrt, sqrt, "mul", rv, fp, result=EF.cols(L.X3AXB, nl),
+                     result_cols=EF.vcols(L.X3AXB, nl))
+    EF.eval_field_lt(ch, L.SQRT_RANGE, sqrt, fp.mod_limbs, real, rv, fp)
+    EF.u8_range(ch, EF.vcols(L.SQRT, nl), rv)
+    lsb = main(L.SQRT_LSB)
+    _assert_bool(ch, lsb)
+    ch.assert_zero(real * (lsb - lsb))
+    ch.sends.append(Lookup([V.const(A.B_AND), _m(L.SQRT_LSB), ZERO, _m(L.SQRT), V.const(1)], rv, KIND_BYTE))
+    y = _write_value_limbs(L.Y, w)
+    negy = EF.cols(L.NEGY, nl)
+    if not lex:
+        # when(is_real).when_ne(lsb, 1 - sign): y = sqrt; when_ne(lsb, sign): y = -sqrt
+        for a, b in zip(sqrt, y):
+            ch.assert_zero(real * (lsb - (1 - sign)) * (a - b))
+        for a, b in zip(negy, y):
+            ch.assert_zero(real * (lsb - sign) * (a - b))
+    else:
+        eq, wsq, wng = main(L.IS_Y_EQ), main(L.WHEN_SQRT_LT), main(L.WHEN_NEG_LT)
+        EF.eval_field_lt(ch, L.NEGY_RANGE, negy, fp.mod_limbs, real, rv, fp)
+        for f in (eq, wsq, wng):
+            _assert_bool(ch, f)
+        ch.assert_zero(real * (wsq + wng - 1))
+        for a, b in zip(sqrt, y):
+            ch.assert_zero(real * eq * (a - b))
+        for a, b in zip(negy, y):
+            ch.assert_zero(real * (1 - eq) * (a - b))
+        ch.assert_zero((1 - real) * wsq)
+        ch.assert_zero((1 - real) * wng)
+        ch.assert_zero(real * sign * (eq - wng))
+        ch.assert_zero(real * (1 - sign) * (eq - wsq))
+        EF.eval_field_lt(ch, L.CMP, sqrt, negy, wsq, _m(L.WHEN_SQRT_LT), fp)
+        EF.eval_field_lt(ch, L.CMP, negy, sqrt, wng, _m(L.WHEN_NEG_LT), fp)
+    # x words at ptr + nl, y words at ptr, both at clk
+    _eval_access_slice(ch, L.X, w, False, L.PTR, 0, real, rv, L.SHARD, L.CLK, addr_off=nl)
+    _eval_access_slice(ch, L.Y, w, True, L.PTR, 0, real, rv, L.SHARD, L.CLK)
+    ch.receives.append(Lookup([_m(L.SHARD), _m(L.CLK), V.const(sid(EC_DECOMPRESS[curve])), _m(L.PTR), _m(L.SIGN)],
+                              rv, KIND_SYSCALL))
+    return ch
+
+
+def field_sqrt(curve: str, a: int) -> int:
+    """secp256k1_sqrt / secp256r1_sqrt / bls12381_sqrt (crates/curves/src/weierstrass/*.rs, through the
+    k256 / p256 / miracl field types): a^((p+1)/4), every field here having p = 3 mod 4."""
+    m = FIELDS[curve].modulus
+    r = pow(a, (m + 1) // 4, m)
+    if r * r % m != a % m:
+        raise ValueError("no square root")
+    return r
+
+
+def decompress_y(curve: str, x: int, sign: int) -> int:
+    """secp256k1_decompress / secp256r1_decompress (y with parity `sign`) and bls12381_decompress (the
+    lexicographically larger of y, -y when `sign`)."""
+    m = FIELDS[curve].modulus
+    y = field_sqrt(curve, (x * x * x + CURVE_A[curve] * x + CURVE_B[curve]) % m)
+    neg = (m - y) % m
+    if LEXICOGRAPHIC[curve]:
+        return max(y, neg) if sign else min(y, neg)
+    return y if (y & 1) == sign else neg
+
+
+def exec_ec_decompress(curve: str, pm, shard: int, clk: int, ptr: int, sign: int):
+    """create_ec_decompress_event (events/precompiles/ec.rs:175-220): x read from ptr + nl at clk, the
+    decompressed y written to ptr at clk."""
+    fp = FIELDS[curve]
+    assert ptr % 4 == 0 and sign <= 1
+    xr = [pm.read(ptr + fp.nl + 4 * i, clk) for i in range(fp.words)]
+    x = EF.words_to_int([r[0] for r in xr])
+    yw = EF.int_to_words(decompress_y(curve, x, sign), fp.words)
+    yr = [pm.write(ptr + 4 * i, yw[i], clk) for i in range(fp.words)]
+    return {"shard": shard, "clk": clk, "ptr": ptr, "sign": sign, "x": xr, "y": yr, "local": pm.local_entries()}
+
+
+def weierstrass_decompress_trace(curve: str, events, byte_lookup) -> np.ndarray:
+    """WeierstrassDecompressChip::generate_trace (weierstrass_decompress.rs:161-303): padding rows
+    decompress the generator's abscissa (value words only in x_access, no choice columns)."""
+    from . import mips_alu as A
+    fp, lex = FIELDS[curve], LEXICOGRAPHIC[curve]
+    L = DecompressLayout(fp, lex)
+    ne, h, m, nl = len(events), _height(len(events)), fp.modulus, fp.nl
+    t = np.zeros((h, L.WIDTH), np.int64)
+    rec = EF.Rec(byte_lookup)
+    real = np.zeros(h, bool)
+    real[:ne] = True
+    xs = [EF.words_to_int([r[0] for r in e["x"]]) for e in events] + [GEN_X[curve]] * (h - ne)
+    t[:, L.RANGE_X:L.RANGE_X + fp.lt_w] = EF.pop_field_lt(xs, rec, real, fp)
+    x2, t[:, L.X2:L.X2 + fp.fop_w] = EF.pop_field_op(xs, xs, "mul", fp)
+    x3, t[:, L.X3:L.X3 + fp.fop_w] = EF.pop_field_op(x2, xs, "mul", fp)
+    axb, t[:, L.AXB:L.AXB + fp.fop_w] = EF.pop_inner_product([[CURVE_A[curve]] * h, [CURVE_B[curve]] * h],
+                                                             [xs, [1] * h], fp)
+    rhs, t[:, L.X3AXB:L.X3AXB + fp.fop_w] = EF.pop_field_op(x3, axb, "add", fp)
+    sq = [field_sqrt(curve, v) for v in rhs]
+    sq2, cols = EF.pop_field_op(sq, sq, "mul", fp)
+    assert sq2 == rhs
+    cols[:, :nl] = EF.limbs(sq, nl)  # FieldSqrtCols stores the root in multiplication.result
+    t[:, L.SQRT:L.SQRT + fp.fop_w] = cols
+    t[:, L.SQRT_RANGE:L.SQRT_RANGE + fp.lt_w] = EF.pop_field_lt(sq, rec, real, fp)
+    t[:, L.SQRT_LSB] = EF.limbs(sq, nl)[:, 0] & 1
+    negy, t[:, L.NEGY:L.NEGY + fp.fop_w] = EF.pop_field_op([0] * h, sq, "sub", fp)
+    # padding rows: the generator's x as the value of the x reads (x_access[i].access.value)
+    gx = EF.limbs([GEN_X[curve]], nl)[0]
+    for i in range(fp.words):
+        t[ne:, L.X + RD_W * i + ACC_VALUE:L.X + RD_W * i + ACC_VALUE + 4] = gx[4 * i:4 * i + 4]
+    # byte lookups of the real rows (populate order does not matter to the counts)
+    for base in (L.X2, L.X3, L.AXB, L.X3AXB, L.NEGY):
+        rec.fop(t[:ne, base:base + fp.fop_w], fp)
+    sqc = t[:ne, L.SQRT:L.SQRT + fp.fop_w].copy()
+    sqc[:, :nl] = t[:ne, L.X3AXB:L.X3AXB + nl]  # the multiplication's range check covers its result a
+    rec.fop(sqc, fp)
+    if ne:
+        byte_lookup(A.B_AND, t[:ne, L.SQRT], np.ones(ne, np.int64))
+    rec.u8(t[:ne, L.SQRT:L.SQRT + nl])
+    if ne:
+        rows = np.arange(ne)
+        t[rows, L.REAL] = 1
+        shard = np.array([e["shard"] for e in events], np.int64)
+        clk = np.array([e["clk"] for e in events], np.int64)
+        t[rows, L.SHARD], t[rows, L.CLK] = shard, clk
+        t[rows, L.PTR] = [e["ptr"] for e in events]
+        t[rows, L.SIGN] = [e["sign"] for e in events]
+        ys = [EF.words_to_int([r[1] for r in e["y"]]) for e in events]
+        if lex:
+            eq = np.array([(ys[i] & 1) == (sq[i] & 1) for i in range(ne)])
+            t[rows, L.IS_Y_EQ] = eq
+            sg = np.array([e["sign"] for e in events], bool)
+            t[rows, L.WHEN_SQRT_LT] = np.where(sg, ~eq, eq)
+            t[rows, L.WHEN_NEG_LT] = np.where(sg, eq, ~eq)
+            t[rows, L.NEGY_RANGE:L.NEGY_RANGE + fp.lt_w] = EF.pop_field_lt(
+                [negy[i] for i in range(ne)], rec, np.ones(ne, bool), fp)
+            for i in range(ne):
+                neg = (m - ys[i]) % m
+                lhs, rhs_ = (neg, ys[i]) if events[i]["sign"] else (ys[i], neg)
+                assert lhs < rhs_
+                t[i, L.CMP:L.CMP + fp.lt_w] = EF.pop_field_lt([lhs], rec, np.ones(1, bool), fp, rhs=[rhs_])[0]
+        for i, e in enumerate(events):
+            assert ys[i] == decompress_y(curve, xs[i], e["sign"])
+        _access_block(t, rows, L.X, [e["x"] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.Y, [e["y"] for e in events], True, shard, clk, byte_lookup)
+    return (t % P).astype(np.uint32)
