@@ -20,6 +20,7 @@ from tests import _oracle as O
 from zkmips_amd import mips_alu as A
 from zkmips_amd import mips_core as MC
 from zkmips_amd import mips_ec as EC
+from zkmips_amd import mips_p2permute as P2
 from zkmips_amd import mips_edwards as ED
 from zkmips_amd import mips_memory as MM
 from zkmips_amd import mips_syscall as SY
@@ -84,6 +85,7 @@ for _curve, _w, _perm in (("Secp256k1", 1378, 325), ("Secp256r1", 1378, 325), ("
     CHIPS[f"{_curve}Decompress"] = (lambda c=_curve: EC.weierstrass_decompress_chip(c), 0, _w, _perm, 1, True,
                                     _PRE + "weierstrass/weierstrass_decompress.rs:145",
                                     _PRE + "weierstrass/weierstrass_decompress.rs:304")
+CHIPS["Poseidon2Permute"] = (P2.poseidon2_permute_chip, 0, 973, 34, 1, False, _PRE + "poseidon2/trace.rs:21", None)
 CHIPS["Uint256MulMod"] = (EC.uint256_mul_chip, 0, 480, 98, 1, True, _PRE + "uint256/air.rs:93",
                           _PRE + "uint256/air.rs:218")
 # precompile chips are costed per call: rows per event x per-row cost (mips/mod.rs:216-222)

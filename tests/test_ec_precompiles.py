@@ -5,7 +5,7 @@ Pins: every base field's modulus, witness offset, limb / witness sizes and the c
 reference's FieldParameters / WeierstrassParameters (tests/golden/curve_params.json, extracted by
 tests/golden/make_ref_fixtures.py); chip shapes and costs equal mips_costs.json
 (tests/test_chip_table.py); the affine formulas agree with an independent projective check (the
-results lie on the curve and P + Q - Q = P).  A guest calling every syscall executes into CPU,
+results lie on the curve and P + Q - Q = P).  A guest calling every syscall (Poseidon2Permute included) executes into CPU,
 precompile and memory shards whose traces satisfy every constraint and balance every lookup; the
 oracle proves and verifies every shard with the machine-level global sum at zero; forged results are
 rejected.  On the GPU every shard's proof bytes equal the oracle's."""
@@ -158,3 +158,11 @@ def test_emulated_field_witness_roundtrip():
         r, cols = EF.pop_field_op(a, b, "mul", fp)
         assert r == [x * y % fp.modulus for x, y in zip(a, b)]
         assert cols.shape == (4, fp.fop_w) and cols.min() >= 0 and cols.max() < 256
+
+
+def test_poseidon2_permute_matches_kat():
+    """POSEIDON2_PERMUTE computes the pinned Poseidon2-16 permutation (tests/golden/poseidon2_kat.json)."""
+    from zkmips_amd import mips_p2permute as P2
+    kat = json.load(open(os.path.join(GOLDEN, "poseidon2_kat.json")))
+    for v in kat.values():
+        assert P2.permute([int(x) for x in v["input"]]) == [int(x) for x in v["output"]]

@@ -30,6 +30,7 @@ from .machine import VirtualPairCol as V
 from .mips_alu import _assert_bool, _m
 
 WR_W, RD_W, ACC_VALUE = 13, 9, 0  # MemoryWriteCols, MemoryReadCols, value offset in MemoryAccessCols
+WIDTH_P2 = 16
 
 # ---------------------------------------------------------------- field and curve parameters
 SECP256K1_P = (1 << 256) - (1 << 32) - 977
@@ -557,6 +558,7 @@ def precompile_table():
     t[UINT256_MUL] = exec_uint256_mul
     for curve in EC_DECOMPRESS:
         t[EC_DECOMPRESS[curve]] = _bind(exec_ec_decompress, curve)
+    t[_p2().POSEIDON2_PERMUTE] = _p2().exec_poseidon2_permute
     return t
 
 
@@ -807,11 +809,12 @@ def uint256_mul_trace(events, byte_lookup) -> np.ndarray:
 def chips_in_machine_order() -> List[ChipDesc]:
     """The chips of this module in MipsAir order (mips/mod.rs:223-318): secp256k1 decompress/add/double,
     secp256r1 decompress/add/double, bn254 add/double, bls12-381 add/double, Uint256MulMod, the bls12-381
-    towers, the bn254 towers, bls12-381 decompress (Poseidon2Permute, KeccakSponge and U256x2048Mul sit
-    between them in the reference and are not restated)."""
+    towers, the bn254 towers, bls12-381 decompress; Poseidon2Permute (mips_p2permute.py) sits after the
+    secp256r1 chips as in the reference (KeccakSponge and U256x2048Mul are not restated)."""
     return [weierstrass_decompress_chip("Secp256k1"), weierstrass_add_chip("Secp256k1"),
             weierstrass_double_chip("Secp256k1"), weierstrass_decompress_chip("Secp256r1"),
             weierstrass_add_chip("Secp256r1"), weierstrass_double_chip("Secp256r1"),
+            _p2().poseidon2_permute_chip(),
             weierstrass_add_chip("Bn254"), weierstrass_double_chip("Bn254"),
             weierstrass_add_chip("Bls12381"), weierstrass_double_chip("Bls12381"),
             uint256_mul_chip(),
@@ -820,8 +823,15 @@ def chips_in_machine_order() -> List[ChipDesc]:
             weierstrass_decompress_chip("Bls12381")]
 
 
+def _p2():
+    from . import mips_p2permute as P2
+    return P2
+
+
 def chip_for_key(key: int) -> str:
     """Chip name of a precompile event key."""
+    if key == _p2().POSEIDON2_PERMUTE:
+        return "Poseidon2Permute"
     for curve in EC_DECOMPRESS:
         if key == EC_DECOMPRESS[curve]:
             return f"{curve}Decompress"
@@ -843,6 +853,8 @@ def chip_for_key(key: int) -> str:
 
 
 def trace_for_key(key: int, events, byte_lookup) -> np.ndarray:
+    if key == _p2().POSEIDON2_PERMUTE:
+        return _p2().poseidon2_permute_trace(events, byte_lookup)
     for curve in EC_DECOMPRESS:
         if key == EC_DECOMPRESS[curve]:
             return weierstrass_decompress_trace(curve, events, byte_lookup)
@@ -938,6 +950,11 @@ def ec_program(seed: int = 1, reps: int = 2, halt: bool = True):
             for code in FP2_ADDSUB[field] + (FP2_MUL[field],):
                 syscall(code, x2, y2)
         fold(x2, 2 * w)
+    sp = alloc(64)  # Poseidon2Permute: 16 canonical words permuted in place
+    store(sp, [int(v) for v in rng.integers(0, P, WIDTH_P2)])
+    for _ in range(reps):
+        syscall(_p2().POSEIDON2_PERMUTE, sp, 0)
+    fold(sp, WIDTH_P2)
     for zero_mod in (False, True):
         # operands below the modulus (the carry has 32 limbs: x y / m < 2^256)
         xp, yp = alloc(32), alloc(64)
