@@ -93,6 +93,7 @@ def test_execution_satisfies_air(run):
                                        lambda: EC.DoubleLayout(EC.FIELDS["Bls12381"]).F["y3_ins"]),
                                       ("Bn254Fp2MulAssign", lambda: EC.Fp2MulLayout(EC.FIELDS["Bn254"]).F["c1"]),
                                       ("Uint256MulMod", lambda: EC.U256L.OUT),
+                                      ("U256XU2048Mul", lambda: EC.U2048L.OUT[3]),
                                       ("Bls12381Decompress",
                                        lambda: EC.DecompressLayout(EC.FIELDS["Bls12381"], True).SQRT),
                                       ("Secp256k1Decompress",

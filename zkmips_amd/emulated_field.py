@@ -353,3 +353,23 @@ def words_to_int(ws) -> int:
 def int_to_words(x: int, n_words: int) -> List[int]:
     b = int(x).to_bytes(4 * n_words, "little")
     return [int.from_bytes(b[4 * i:4 * i + 4], "little") for i in range(n_words)]
+
+
+def eval_mul_and_carry(ch: ChipDesc, base: int, a, b, c, modulus, mult: V, fp: FieldParams):
+    """FieldOpCols::eval_mul_and_carry (field_op.rs:281-303): a b + c = result + carry modulus."""
+    res, carry = cols(base, fp.nl), cols(base + fp.nl, fp.nl)
+    vanishing = p_sub(p_sub(p_add(p_mul(a, b), c), res), p_mul(carry, modulus))
+    eval_field_operation(ch, vanishing, base, fp)
+    field_range_checks(ch, base, mult, fp)
+
+
+def pop_mul_and_carry(a: Sequence[int], b: Sequence[int], c: Sequence[int], modulus: int, fp: FieldParams):
+    """FieldOpCols::populate_mul_and_carry (field_op.rs:47-101) over a batch: returns (result, carry,
+    (n, fop_w) columns)."""
+    full = [x * y + z for x, y, z in zip(a, b, c)]
+    res = [f % modulus for f in full]
+    carry = [f // modulus for f in full]
+    mlimbs = np.array(list(modulus.to_bytes((modulus.bit_length() + 7) // 8, "little")), np.int64)[None, :]
+    van = padd_np(pmul_np(limbs(a, fp.nl), limbs(b, fp.nl)), limbs(c, fp.nl), -limbs(res, fp.nl),
+                  -pmul_np(limbs(carry, fp.nl), mlimbs))
+    return res, carry, fop_cols(limbs(res, fp.nl), limbs(carry, fp.nl), van, fp)

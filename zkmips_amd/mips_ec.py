@@ -559,6 +559,7 @@ def precompile_table():
     for curve in EC_DECOMPRESS:
         t[EC_DECOMPRESS[curve]] = _bind(exec_ec_decompress, curve)
     t[_p2().POSEIDON2_PERMUTE] = _p2().exec_poseidon2_permute
+    t[U256XU2048_MUL] = exec_u256x2048_mul
     return t
 
 
@@ -817,7 +818,7 @@ def chips_in_machine_order() -> List[ChipDesc]:
             _p2().poseidon2_permute_chip(),
             weierstrass_add_chip("Bn254"), weierstrass_double_chip("Bn254"),
             weierstrass_add_chip("Bls12381"), weierstrass_double_chip("Bls12381"),
-            uint256_mul_chip(),
+            uint256_mul_chip(), u256x2048_mul_chip(),
             fp_op_chip("Bls12381"), fp2_addsub_chip("Bls12381"), fp2_mul_chip("Bls12381"),
             fp_op_chip("Bn254"), fp2_addsub_chip("Bn254"), fp2_mul_chip("Bn254"),
             weierstrass_decompress_chip("Bls12381")]
@@ -832,6 +833,8 @@ def chip_for_key(key: int) -> str:
     """Chip name of a precompile event key."""
     if key == _p2().POSEIDON2_PERMUTE:
         return "Poseidon2Permute"
+    if key == U256XU2048_MUL:
+        return "U256XU2048Mul"
     for curve in EC_DECOMPRESS:
         if key == EC_DECOMPRESS[curve]:
             return f"{curve}Decompress"
@@ -855,6 +858,8 @@ def chip_for_key(key: int) -> str:
 def trace_for_key(key: int, events, byte_lookup) -> np.ndarray:
     if key == _p2().POSEIDON2_PERMUTE:
         return _p2().poseidon2_permute_trace(events, byte_lookup)
+    if key == U256XU2048_MUL:
+        return u256x2048_mul_trace(events, byte_lookup)
     for curve in EC_DECOMPRESS:
         if key == EC_DECOMPRESS[curve]:
             return weierstrass_decompress_trace(curve, events, byte_lookup)
@@ -965,6 +970,15 @@ def ec_program(seed: int = 1, reps: int = 2, halt: bool = True):
         for _ in range(reps):
             syscall(UINT256_MUL, xp, yp)
         fold(xp, 8)
+    for _ in range(reps):  # U256XU2048_MUL: lo / hi pointers in A2 / A3
+        ap, bp, lop, hip = alloc(32), alloc(256), alloc(256), alloc(32)
+        store(ap, EF.int_to_words(int.from_bytes(rng.bytes(32), "little"), 8))
+        store(bp, EF.int_to_words(int.from_bytes(rng.bytes(256), "little"), 64))
+        li(SY.REG_A2, lop)
+        li(SY.REG_A3, hip)
+        syscall(U256XU2048_MUL, ap, bp)
+        fold(lop, 64)
+        fold(hip, 8)
     prog += [(A.OP_ADD, SY.REG_V0, 0, SY.COMMIT, 0, 1), (A.OP_ADD, SY.REG_A0, 0, 0, 0, 1),
              (A.OP_ADD, SY.REG_A1, acc, 0, 0, 1), (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
     if halt:
@@ -1161,4 +1175,112 @@ def weierstrass_decompress_trace(curve: str, events, byte_lookup) -> np.ndarray:
             assert ys[i] == decompress_y(curve, xs[i], e["sign"])
         _access_block(t, rows, L.X, [e["x"] for e in events], False, shard, clk, byte_lookup)
         _access_block(t, rows, L.Y, [e["y"] for e in events], True, shard, clk, byte_lookup)
+    return (t % P).astype(np.uint32)
+
+
+# ---------------------------------------------------------------- U256x2048Mul
+U256XU2048_MUL = 0x01_01_00_2F
+
+
+class U2048Layout:
+    """U256x2048MulCols (u256x2048_mul/air.rs:51-77)."""
+
+    def __init__(self):
+        self.SHARD, self.CLK, self.APTR, self.BPTR, self.LOPTR, self.HIPTR = range(6)
+        self.LOPTR_MEM = 6                       # MemoryReadCols of register A2
+        self.HIPTR_MEM = self.LOPTR_MEM + RD_W   # register A3
+        self.A = self.HIPTR_MEM + RD_W           # 8 x MemoryReadCols
+        self.B = self.A + 8 * RD_W               # 64 x MemoryReadCols
+        self.LO = self.B + 64 * RD_W             # 64 x MemoryWriteCols
+        self.HI = self.LO + 64 * WR_W            # 8 x MemoryWriteCols
+        self.OUT = [self.HI + 8 * WR_W + k * U256.fop_w for k in range(8)]  # a_mul_b1, ab2_plus_carry, ...
+        self.REAL = self.OUT[-1] + U256.fop_w
+        self.WIDTH = self.REAL + 1
+
+
+U2048L = U2048Layout()
+_MOD_2_256 = [0] * 32 + [1]
+
+
+def u256x2048_mul_chip() -> ChipDesc:
+    """U256x2048MulChip::eval (u256x2048_mul/air.rs:266-385): (lo, hi) = a * b over 2048 + 256 bits, the
+    eight 256-bit limbs of b multiplied in a chain whose carries feed the next."""
+    from .mips_core import _eval_memory_access
+    from .mips_syscall import REG_A2, REG_A3
+    L = U2048L
+    ch = ChipDesc("U256XU2048Mul", prep_width=0, main_width=L.WIDTH)
+    real, rv = main(L.REAL), _m(L.REAL)
+    _assert_bool(ch, real)
+    ch.receives.append(Lookup([_m(L.SHARD), _m(L.CLK), V.const(sid(U256XU2048_MUL)), _m(L.APTR), _m(L.BPTR)], rv,
+                              KIND_SYSCALL))
+    for reg, base in ((REG_A2, L.LOPTR_MEM), (REG_A3, L.HIPTR_MEM)):
+        _eval_memory_access(ch, base, base + ACC_VALUE, 0, V.const(reg), real, rv, shard_col=L.SHARD,
+                            clk_terms=((L.CLK, 1),))
+    _eval_access_slice(ch, L.A, 8, False, L.APTR, 0, real, rv, L.SHARD, L.CLK)
+    _eval_access_slice(ch, L.B, 64, False, L.BPTR, 0, real, rv, L.SHARD, L.CLK)
+    _eval_access_slice(ch, L.LO, 64, True, L.LOPTR, 1, real, rv, L.SHARD, L.CLK)
+    _eval_access_slice(ch, L.HI, 8, True, L.HIPTR, 1, real, rv, L.SHARD, L.CLK)
+    a = _read_limbs(L.A, 8)
+    prev = [0]
+    for k in range(8):
+        EF.eval_mul_and_carry(ch, L.OUT[k], a, _read_limbs(L.B + 8 * k * RD_W, 8), prev, _MOD_2_256, rv, U256)
+        prev = EF.cols(L.OUT[k] + 32, 32)
+    for x, y in zip(prev, _write_value_limbs(L.HI, 8)):
+        ch.assert_zero(real * (x - y))
+    for k in range(8):
+        for x, y in zip(EF.cols(L.OUT[k], 32), _write_value_limbs(L.LO + 8 * k * WR_W, 8)):
+            ch.assert_zero(real * (x - y))
+    for ptr, base in ((L.LOPTR, L.LOPTR_MEM), (L.HIPTR, L.HIPTR_MEM)):
+        word = sum((main(base + ACC_VALUE + j) * (1 << (8 * j)) for j in range(1, 4)), main(base + ACC_VALUE))
+        ch.assert_zero(real * (main(ptr) - word))
+    return ch
+
+
+def exec_u256x2048_mul(pm, shard: int, clk: int, a_ptr: int, b_ptr: int):
+    """U256xU2048MulSyscall::execute (executor/src/syscalls/precompiles/u256x2048_mul.rs): lo_ptr / hi_ptr
+    from registers A2 / A3, a and b read at clk, lo and hi written at clk + 1."""
+    from .mips_syscall import REG_A2, REG_A3
+    lo_reg, hi_reg = pm.reg_read(REG_A2, clk), pm.reg_read(REG_A3, clk)
+    lo_ptr, hi_ptr = lo_reg[0], hi_reg[0]
+    ar = [pm.read(a_ptr + 4 * i, clk) for i in range(8)]
+    br = [pm.read(b_ptr + 4 * i, clk) for i in range(64)]
+    prod = EF.words_to_int([r[0] for r in ar]) * EF.words_to_int([r[0] for r in br])
+    lo_w, hi_w = EF.int_to_words(prod % (1 << 2048), 64), EF.int_to_words(prod >> 2048, 8)
+    lw = [pm.write(lo_ptr + 4 * i, lo_w[i], clk + 1) for i in range(64)]
+    hw = [pm.write(hi_ptr + 4 * i, hi_w[i], clk + 1) for i in range(8)]
+    return {"shard": shard, "clk": clk, "a_ptr": a_ptr, "b_ptr": b_ptr, "lo_ptr": lo_ptr, "hi_ptr": hi_ptr,
+            "lo_reg": lo_reg, "hi_reg": hi_reg, "a": ar, "b": br, "lo": lw, "hi": hw, "local": pm.local_entries()}
+
+
+def u256x2048_mul_trace(events, byte_lookup) -> np.ndarray:
+    """U256x2048MulChip::generate_trace (u256x2048_mul/air.rs:109-213): padding rows hold the eight
+    mul-and-carry operations of zeros."""
+    L = U2048L
+    ne, h = len(events), _height(len(events))
+    t = np.zeros((h, L.WIDTH), np.int64)
+    rec = EF.Rec(byte_lookup)
+    a = [EF.words_to_int([r[0] for r in e["a"]]) for e in events] + [0] * (h - ne)
+    bs = [[EF.words_to_int([r[0] for r in e["b"][8 * k:8 * k + 8]]) for e in events] + [0] * (h - ne)
+          for k in range(8)]
+    carry = [0] * h
+    for k in range(8):
+        res, carry, c = EF.pop_mul_and_carry(a, bs[k], carry, 1 << 256, U256)
+        t[:, L.OUT[k]:L.OUT[k] + U256.fop_w] = c
+        rec.fop(t[:ne, L.OUT[k]:L.OUT[k] + U256.fop_w], U256)
+    if ne:
+        rows = np.arange(ne)
+        t[rows, L.REAL] = 1
+        shard = np.array([e["shard"] for e in events], np.int64)
+        clk = np.array([e["clk"] for e in events], np.int64)
+        t[rows, L.SHARD], t[rows, L.CLK] = shard, clk
+        for col, key in ((L.APTR, "a_ptr"), (L.BPTR, "b_ptr"), (L.LOPTR, "lo_ptr"), (L.HIPTR, "hi_ptr")):
+            t[rows, col] = [e[key] for e in events]
+        for i, e in enumerate(events):
+            assert EF.words_to_int([r[1] for r in e["hi"]]) == carry[i]
+        _access_block(t, rows, L.LOPTR_MEM, [[e["lo_reg"]] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.HIPTR_MEM, [[e["hi_reg"]] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.A, [e["a"] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.B, [e["b"] for e in events], False, shard, clk, byte_lookup)
+        _access_block(t, rows, L.LO, [e["lo"] for e in events], True, shard, clk + 1, byte_lookup)
+        _access_block(t, rows, L.HI, [e["hi"] for e in events], True, shard, clk + 1, byte_lookup)
     return (t % P).astype(np.uint32)
