@@ -21,6 +21,7 @@ from zkmips_amd import mips_alu as A
 from zkmips_amd import mips_core as MC
 from zkmips_amd import mips_ec as EC
 from zkmips_amd import mips_p2permute as P2
+from zkmips_amd import mips_keccak as K
 from zkmips_amd import mips_edwards as ED
 from zkmips_amd import mips_memory as MM
 from zkmips_amd import mips_syscall as SY
@@ -86,11 +87,12 @@ for _curve, _w, _perm in (("Secp256k1", 1378, 325), ("Secp256r1", 1378, 325), ("
                                     _PRE + "weierstrass/weierstrass_decompress.rs:145",
                                     _PRE + "weierstrass/weierstrass_decompress.rs:304")
 CHIPS["Poseidon2Permute"] = (P2.poseidon2_permute_chip, 0, 973, 34, 1, False, _PRE + "poseidon2/trace.rs:21", None)
+CHIPS["KeccakSponge"] = (K.keccak_sponge_chip, 0, 3531, 180, 1, False, _PRE + "keccak_sponge/trace.rs:23", None)
 CHIPS["U256XU2048Mul"] = (EC.u256x2048_mul_chip, 0, 3129, 678, 1, False, _PRE + "u256x2048_mul/air.rs:90", None)
 CHIPS["Uint256MulMod"] = (EC.uint256_mul_chip, 0, 480, 98, 1, True, _PRE + "uint256/air.rs:93",
                           _PRE + "uint256/air.rs:218")
 # precompile chips are costed per call: rows per event x per-row cost (mips/mod.rs:216-222)
-ROWS_PER_EVENT = {"ShaExtend": 48, "ShaCompress": 80}
+ROWS_PER_EVENT = {"ShaExtend": 48, "ShaCompress": 80, "KeccakSponge": 24}
 
 
 def _cost(ch):

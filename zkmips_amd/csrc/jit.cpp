@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <future>
 #include <map>
 #include <mutex>
@@ -203,9 +204,17 @@ void lookup_batch(Gen &g, const ChipDesc &c, int i0, int i1, const char *alpha, 
     if (!num_base.empty()) g.body << "    " << num << " = ef{{" << num_base << ", 0u, 0u, 0u}};\n";
 }
 
+// Chips whose AIR program lowers to more constraints than this get it as a chain of non-inlined
+// device functions (each a slice of consecutive constraints with its own column reads and its own
+// EfAcc, the kernel adding the slices' folded values), so no single function is huge: hiprtc -O3 time
+// grows much faster than linearly with the size of one straight-line function (KeccakSponge, 3788
+// constraints in one body: > 40 min; as slices: minutes).  The folded sum is the same field element.
+constexpr int kJitSliceConstraints = 2048;
+constexpr int kJitSliceLines = 6000;  // generated statements per slice
+
 std::string gen_source(const ChipDesc &c, const std::string &fname) {
     Gen g;
-    std::ostringstream o;
+    std::ostringstream o, slices;
     int k = 0;  // constraint index
     // folding sum_k alpha^(n-1-k) C_k: split-constant 64-bit accumulator (kb::EfAcc), reduced once
     auto emit_base = [&](const std::string &x) {
@@ -219,48 +228,114 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
     // ---- AIR program -> straight-line code ----
     std::vector<std::string> st;
     std::vector<std::string> slot;  // shared subexpressions: slot -> the variable holding its value
-    for (size_t pc = 0; pc < c.code.size();) {
+    int n_air = 0;
+    for (size_t pc = 0; pc < c.code.size();) {  // count the AIR constraints (OP_EMITs)
         const uint32_t op = c.code[pc++];
-        switch (op) {
-        case OP_MAIN_L: st.push_back(g.col("main", c.code[pc++], "rl")); break;
-        case OP_MAIN_N: st.push_back(g.col("main", c.code[pc++], "rn")); break;
-        case OP_PREP_L: st.push_back(g.col("prep", c.code[pc++], "rl")); break;
-        case OP_PREP_N: st.push_back(g.col("prep", c.code[pc++], "rn")); break;
-        case OP_CONST: st.push_back(hex(kb::to_mont(c.code[pc++]))); break;
-        case OP_PV: st.push_back("A.pv[" + std::to_string(c.code[pc++]) + "]"); break;
-        case OP_IS_FIRST: st.push_back("is_first"); break;
-        case OP_IS_LAST: st.push_back("is_last"); break;
-        case OP_IS_TRANS: st.push_back("is_trans"); break;
-        case OP_ADD: case OP_SUB: case OP_MUL: {
-            std::string b = st.back(); st.pop_back();
-            std::string a = st.back(); st.pop_back();
-            std::string t = g.var("t");
-            const char *f = op == OP_ADD ? "add" : op == OP_SUB ? "sub" : "mul";
-            g.body << "    const uint32_t " << t << " = " << f << "(" << a << ", " << b << ");\n";
-            st.push_back(t);
+        if (op == OP_EMIT) n_air++;
+        else if (op == OP_MAIN_L || op == OP_MAIN_N || op == OP_PREP_L || op == OP_PREP_N || op == OP_CONST ||
+                 op == OP_PV || op == OP_LET || op == OP_GET) pc++;
+    }
+    const bool sliced = n_air > kJitSliceConstraints;
+    // program() puts every shared definition (code, OP_LET) ahead of the first constraint.  Unsliced, each
+    // is evaluated there once; sliced, a definition is evaluated in a slice at its first OP_GET there
+    // (slices are separate functions), so no value is live across a slice boundary.
+    std::vector<std::pair<size_t, size_t>> slot_def;  // code range of each slot's definition
+    size_t first_constraint = 0;
+    for (size_t pc = 0; pc < c.code.size();) {
+        const size_t at = pc;
+        const uint32_t op = c.code[pc++];
+        if (op == OP_LET) {
+            slot_def.emplace_back(first_constraint, at);
+            first_constraint = ++pc;
+        } else if (op == OP_EMIT) {
             break;
-        }
-        case OP_NEG: {
-            std::string a = st.back(); st.pop_back();
-            std::string t = g.var("t");
-            g.body << "    const uint32_t " << t << " = neg(" << a << ");\n";
-            st.push_back(t);
-            break;
-        }
-        case OP_EMIT: {
-            std::string a = st.back(); st.pop_back();
-            emit_base(a);
-            break;
-        }
-        case OP_LET: {  // the value is already a named SSA variable; bind the slot to it
+        } else if (op == OP_MAIN_L || op == OP_MAIN_N || op == OP_PREP_L || op == OP_PREP_N || op == OP_CONST ||
+                   op == OP_PV || op == OP_GET) {
             pc++;
-            slot.push_back(st.back());
-            st.pop_back();
-            break;
         }
-        case OP_GET: st.push_back(slot.at(c.code[pc++])); break;
-        default: throw ArgError("bad opcode in JIT");
+    }
+    std::map<uint32_t, std::string> lazy;  // sliced: slot -> its variable in the current slice
+    int n_slices = 0;
+    size_t slice_lines = 0;
+    auto close_slice = [&]() {
+        slices << "__device__ __noinline__ ef zq_slice" << n_slices++ << "(const ZkmQuotJitArgs &A, uint64_t rl, uint64_t rn, "
+               << "uint32_t is_first, uint32_t is_last, uint32_t is_trans) {\n"
+               << "    (void)rl; (void)rn; (void)is_first; (void)is_last; (void)is_trans;\n"
+               << "    EfAcc facc;\n    facc.zero();\n"
+               << g.pipelined(8, "ZKM_JIT_LOOKAHEAD_Q") << "    return facc.value();\n}\n";
+        g = Gen{};
+        lazy.clear();
+        slice_lines = 0;
+    };
+    // the stack machine over code[from, to)
+    std::function<void(size_t, size_t, std::vector<std::string> &)> run;
+    run = [&](size_t from, size_t to, std::vector<std::string> &st) {
+        for (size_t pc = from; pc < to;) {
+            const uint32_t op = c.code[pc++];
+            slice_lines++;
+            switch (op) {
+            case OP_MAIN_L: st.push_back(g.col("main", c.code[pc++], "rl")); break;
+            case OP_MAIN_N: st.push_back(g.col("main", c.code[pc++], "rn")); break;
+            case OP_PREP_L: st.push_back(g.col("prep", c.code[pc++], "rl")); break;
+            case OP_PREP_N: st.push_back(g.col("prep", c.code[pc++], "rn")); break;
+            case OP_CONST: st.push_back(hex(kb::to_mont(c.code[pc++]))); break;
+            case OP_PV: st.push_back("A.pv[" + std::to_string(c.code[pc++]) + "]"); break;
+            case OP_IS_FIRST: st.push_back("is_first"); break;
+            case OP_IS_LAST: st.push_back("is_last"); break;
+            case OP_IS_TRANS: st.push_back("is_trans"); break;
+            case OP_ADD: case OP_SUB: case OP_MUL: {
+                std::string b = st.back(); st.pop_back();
+                std::string a = st.back(); st.pop_back();
+                std::string t = g.var("t");
+                const char *f = op == OP_ADD ? "add" : op == OP_SUB ? "sub" : "mul";
+                g.body << "    const uint32_t " << t << " = " << f << "(" << a << ", " << b << ");\n";
+                st.push_back(t);
+                break;
+            }
+            case OP_NEG: {
+                std::string a = st.back(); st.pop_back();
+                std::string t = g.var("t");
+                g.body << "    const uint32_t " << t << " = neg(" << a << ");\n";
+                st.push_back(t);
+                break;
+            }
+            case OP_EMIT: {
+                std::string a = st.back(); st.pop_back();
+                emit_base(a);
+                if (sliced && st.empty() && slice_lines >= (size_t)kJitSliceLines) close_slice();
+                break;
+            }
+            case OP_LET: {  // the value is already a named SSA variable; bind the slot to it
+                pc++;
+                slot.push_back(st.back());
+                st.pop_back();
+                break;
+            }
+            case OP_GET: {
+                const uint32_t sl = c.code[pc++];
+                if (!sliced) {
+                    st.push_back(slot.at(sl));
+                } else {
+                    auto it = lazy.find(sl);
+                    if (it == lazy.end()) {
+                        std::vector<std::string> sub;
+                        run(slot_def.at(sl).first, slot_def.at(sl).second, sub);
+                        it = lazy.emplace(sl, sub.back()).first;
+                    }
+                    st.push_back(it->second);
+                }
+                break;
+            }
+            default: throw ArgError("bad opcode in JIT");
+            }
         }
+    };
+    run(sliced ? first_constraint : 0, c.code.size(), st);
+    if (sliced) {
+        close_slice();
+        g.body << "    ef slices = ef_zero();\n";
+        for (int i = 0; i < n_slices; i++)
+            g.body << "    slices = ef_add(slices, zq_slice" << i << "(A, rl, rn, is_first, is_last, is_trans));\n";
     }
     // ---- LogUp constraints (permutation.rs:256-333) ----
     const int nloc = (int)c.local.size();
@@ -326,7 +401,7 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
     }
     ARG_CHECK(k == c.n_constraints, "JIT constraint count mismatch");
 
-    o << "extern \"C\" __global__ void __launch_bounds__(256) " << fname << "(const ZkmQuotJitArgs A) {\n"
+    o << slices.str() << "extern \"C\" __global__ void __launch_bounds__(256) " << fname << "(const ZkmQuotJitArgs A) {\n"
       // Each wave takes 64 consecutive LDE rows; the four waves of a workgroup take a chain of
       // row blocks B, next(B), next^2(B), next^3(B) (next = the rows holding the next-row
       // operands; in the bit-reversed block index that is +step), so three of the four waves
@@ -366,7 +441,8 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
       << "    EfAcc facc;\n"
       << "    facc.zero();\n"
       << g.pipelined(8, "ZKM_JIT_LOOKAHEAD_Q")  // measured: 8 -> 2.27 ms, 24 -> 2.44, unpipelined 2.78
-      << "    const ef qv = ef_mul_base(facc.value(), inv_z);\n"
+      << (sliced ? "    const ef qv = ef_mul_base(ef_add(facc.value(), slices), inv_z);\n"
+                 : "    const ef qv = ef_mul_base(facc.value(), inv_z);\n")
       // chunk j = k mod 2^lqd (split_evals); t = rev_Q(k) = rev_lqd(j) * n + rev_n(k >> lqd), so the
       // chunk's position t mod n is its bit-reversed row
       << "    const uint64_t c = k & (uint64_t)(A.step - 1), pos = t & (A.n - 1);\n"

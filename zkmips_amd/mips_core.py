@@ -1851,7 +1851,7 @@ PRECOMPILE_CHIP = {SY.SHA_EXTEND: "ShaExtend", SY.SHA_COMPRESS: "ShaCompress", S
 def _ec_keys():
     from . import mips_ec as EC
     keys = [EC.EC_ADD[c] for c in EC.FIELDS] + [EC.EC_DOUBLE[c] for c in EC.FIELDS] + [EC.UINT256_MUL]
-    keys += list(EC.EC_DECOMPRESS.values()) + [0x00_01_00_30, EC.U256XU2048_MUL]  # + POSEIDON2_PERMUTE
+    keys += list(EC.EC_DECOMPRESS.values()) + [0x00_01_00_30, 0x01_01_00_09, EC.U256XU2048_MUL]  # + POSEIDON2_PERMUTE, KECCAK_SPONGE
     for f in EC.FP_OPS:
         keys += [EC.FP_OPS[f][0], EC.FP2_ADDSUB[f][0], EC.FP2_MUL[f]]
     return {k: EC.chip_for_key(k) for k in keys}

@@ -559,6 +559,7 @@ def precompile_table():
     for curve in EC_DECOMPRESS:
         t[EC_DECOMPRESS[curve]] = _bind(exec_ec_decompress, curve)
     t[_p2().POSEIDON2_PERMUTE] = _p2().exec_poseidon2_permute
+    t[_keccak().KECCAK_SPONGE] = _keccak().exec_keccak_sponge
     t[U256XU2048_MUL] = exec_u256x2048_mul
     return t
 
@@ -811,11 +812,11 @@ def chips_in_machine_order() -> List[ChipDesc]:
     """The chips of this module in MipsAir order (mips/mod.rs:223-318): secp256k1 decompress/add/double,
     secp256r1 decompress/add/double, bn254 add/double, bls12-381 add/double, Uint256MulMod, the bls12-381
     towers, the bn254 towers, bls12-381 decompress; Poseidon2Permute (mips_p2permute.py) sits after the
-    secp256r1 chips as in the reference (KeccakSponge and U256x2048Mul are not restated)."""
+    secp256r1 chips as in the reference, KeccakSponge (mips_keccak.py) after it."""
     return [weierstrass_decompress_chip("Secp256k1"), weierstrass_add_chip("Secp256k1"),
             weierstrass_double_chip("Secp256k1"), weierstrass_decompress_chip("Secp256r1"),
             weierstrass_add_chip("Secp256r1"), weierstrass_double_chip("Secp256r1"),
-            _p2().poseidon2_permute_chip(),
+            _p2().poseidon2_permute_chip(), _keccak().keccak_sponge_chip(),
             weierstrass_add_chip("Bn254"), weierstrass_double_chip("Bn254"),
             weierstrass_add_chip("Bls12381"), weierstrass_double_chip("Bls12381"),
             uint256_mul_chip(), u256x2048_mul_chip(),
@@ -829,10 +830,17 @@ def _p2():
     return P2
 
 
+def _keccak():
+    from . import mips_keccak as K
+    return K
+
+
 def chip_for_key(key: int) -> str:
     """Chip name of a precompile event key."""
     if key == _p2().POSEIDON2_PERMUTE:
         return "Poseidon2Permute"
+    if key == _keccak().KECCAK_SPONGE:
+        return "KeccakSponge"
     if key == U256XU2048_MUL:
         return "U256XU2048Mul"
     for curve in EC_DECOMPRESS:
@@ -858,6 +866,8 @@ def chip_for_key(key: int) -> str:
 def trace_for_key(key: int, events, byte_lookup) -> np.ndarray:
     if key == _p2().POSEIDON2_PERMUTE:
         return _p2().poseidon2_permute_trace(events, byte_lookup)
+    if key == _keccak().KECCAK_SPONGE:
+        return _keccak().keccak_sponge_trace(events, byte_lookup)
     if key == U256XU2048_MUL:
         return u256x2048_mul_trace(events, byte_lookup)
     for curve in EC_DECOMPRESS:
