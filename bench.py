@@ -204,6 +204,22 @@ def valu_counters(pmc, ms_per_proof, kernel="k_hash_leaves"):
     return out
 
 
+def stage_traffic(pmc, stage):
+    """(HBM bytes per proof, launches per proof) of the kernels a profiled stage brackets."""
+    if not pmc:
+        return None, 0
+    pre = STAGE_KERNELS.get(stage, ())
+    b = n = 0
+    for k, v in pmc.items():
+        if k.startswith(pre):
+            b += v["bytes_per_proof"]
+            n += v["launches_per_proof"]
+    return (b, n) if n else (None, 0)
+
+
+VALU_PEAK_TSLOTS = 256 * 4 * 32 * 2.4e9 / 1e12  # CUs x SIMDs x SIMD-32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
+
+
 def valu_roofline(perms, ms):
     """Poseidon2 leaf hashing is integer-VALU bound: issue slots per permutation (static ISA count of
     the permutation weighted by the measured issue cost of each instruction class,

@@ -125,6 +125,50 @@ int zkm_cpu_events_to_trace(const zkm_cpu_event_ffi *events, uint64_t n, uint32_
 int zkm_add_sub_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
                                 uint32_t *byte_mult, void *stream);
 
+/* The other AluEvent chips, whose rows the reference fills in Rust (no C++ row ABI): Bitwise
+ * (alu/bitwise/mod.rs:140-171, the byte op of every limb), Lt (alu/lt/mod.rs:179-263: the AND 0x7F
+ * masks of both top bytes and the LTU comparison of the most significant differing byte), ShiftLeft
+ * (alu/sll/mod.rs:200-260: U8Range of the result and carries; padding rows with shift_by_n_bits[0] =
+ * shift_by_n_bytes[0] = bit_shift_multiplier = 1), ShiftRight (alu/sr/mod.rs:220-325: MSB of the operand,
+ * ShrCarry of every byte, U8Range of the byte / bit results, carries and shifted bytes; padding rows with
+ * shift_by_n_bits[0] = shift_by_n_bytes[0] = 1).  byte_mult (nullable) as above. */
+#define ZKM_BITWISE_WIDTH 18
+#define ZKM_LT_WIDTH 36
+#define ZKM_SHIFT_LEFT_WIDTH 44
+#define ZKM_SHIFT_RIGHT_WIDTH 71
+int zkm_bitwise_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                uint32_t *byte_mult, void *stream);
+int zkm_lt_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                           uint32_t *byte_mult, void *stream);
+int zkm_shift_left_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                   uint32_t *byte_mult, void *stream);
+int zkm_shift_right_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                    uint32_t *byte_mult, void *stream);
+
+/* BranchEvent (events/instr.rs:159-177, #[repr(C)]), 28 bytes */
+typedef struct { uint32_t pc, next_pc, next_next_pc; uint8_t opcode; uint32_t a, b, c; } zkm_branch_event;
+/* MemInstrEvent (events/instr.rs:112-135); its mem_access (a Rust enum MemoryRecordEnum, no fixed layout)
+ * travels as an OptionMemoryRecordEnum with tag Read (loads) or Write (stores), as in CpuEventFfi; 84 bytes */
+typedef struct {
+    uint32_t shard, clk, pc, next_pc;
+    uint8_t opcode;
+    uint32_t a, b, c;
+    zkm_option_memory_record mem_access;
+    uint32_t prev_a_val;
+} zkm_mem_instr_event;
+#define ZKM_BRANCH_WIDTH 62
+#define ZKM_MEMORY_INSTRS_WIDTH 79
+/* Branch (control_flow/branch/trace.rs:85-130): the branch decision recomputed from opcode, a, b
+ * (Executor::execute_branch), the word range checks of next_pc / next_next_pc, U8Range of both on the
+ * rows not taken.  MemoryInstrs (memory/instructions/trace.rs:88-251): address b + c, its alignment and
+ * range-check columns, the memory access (value, previous value, timestamp checks), the unsigned loaded
+ * value and sign columns of LB / LH, the is-register-address test (LTU against 35 when the top three
+ * address bytes are zero).  byte_mult (nullable) as above. */
+int zkm_branch_events_to_trace(const zkm_branch_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                               uint32_t *byte_mult, void *stream);
+int zkm_memory_instrs_events_to_trace(const zkm_mem_instr_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                      uint32_t *byte_mult, void *stream);
+
 /* MemoryLocal (memory/local.rs:144-185): event i fills entry i % 4 of row i / 4; height rows. */
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,
                                      uint64_t height, void *stream);

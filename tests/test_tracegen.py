@@ -34,6 +34,8 @@ LAYOUTS = {
     "zkm_memory_init_final_event": (TG.MEMORY_INIT_FINAL_EVENT, {f: f for f in TG.MEMORY_INIT_FINAL_EVENT.names}),
     "zkm_syscall_event": (TG.SYSCALL_EVENT, {f: f for f in TG.SYSCALL_EVENT.names}),
     "zkm_global_lookup_event": (TG.GLOBAL_EVENT, {f: f for f in TG.GLOBAL_EVENT.names}),
+    "zkm_branch_event": (TG.BRANCH_EVENT, {f: f for f in TG.BRANCH_EVENT.names}),
+    "zkm_mem_instr_event": (TG.MEM_INSTR_EVENT, {f: f for f in TG.MEM_INSTR_EVENT.names}),
 }
 
 
@@ -190,6 +192,44 @@ def test_cpu_records_reproduce_host_trace(name):
     assert (mult <= tr["Byte"]).all()  # a part of the shard's lookups
 
 
+def alu_chip_byte_mult(cap):
+    """The Byte lookups of the shard's Bitwise, Lt, ShiftLeft, ShiftRight, Branch and MemoryInstrs rows (the
+    host builders over the same events the device gets; CloClz's own lookups excluded)."""
+    mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
+    ev = {"add": tuple(np.zeros(0, np.uint32) for _ in range(6))}
+    for kind in TG.ALU_CHIPS:
+        r = TG.alu_records(cap["alu"], kind)
+        ev[kind] = (r["opcode"].astype(np.uint32), r["a"], r["b"], r["c"], r["pc"], r["next_pc"])
+    A.alu_traces(ev, mult)
+    look = A.byte_lookup_into(mult)  # Branch and MemoryInstrs (host builders)
+    if len(cap.get("branches", [])):
+        MC._branch_trace(cap["branches"], look)
+    if len(cap.get("mevs", [])):
+        MC._mem_instr_trace(cap["mevs"], cap["shard"], look)
+    return mult
+
+
+def test_records_reproduce_executor_tuples():
+    """Branch / MemInstr records round-trip the executor's tuples (decision and address recomputable)."""
+    cap, tr, _, _, _ = _capture("loop")
+    br = TG.branch_records(cap["branches"])
+    assert len(br) == len(cap["branches"]) and len(br)
+    taken = [MC._taken(int(o), int(a), int(b)) for o, a, b in zip(br["opcode"], br["a"], br["b"])]
+    assert taken == [bool(t[7]) for t in cap["branches"]]
+    mi = TG.mem_instr_records(cap["mevs"], cap["shard"])
+    assert len(mi) == len(cap["mevs"]) and len(mi)
+    load = np.isin(mi["opcode"], MC.LOAD_OPS)
+    assert (mi["mem_access"]["tag"][load] == TG.REC_READ).all() and (mi["mem_access"]["tag"][~load] == TG.REC_WRITE).all()
+
+
+def test_alu_records_carry_the_clz_dependencies():
+    """ShiftRight's records = the CPU's SRL/SRA/ROR events then the CLZ/CLO dependencies (as its host trace)."""
+    cap, tr, _, _, _ = _capture("random")
+    rec = TG.alu_records(cap["alu"], "sr")
+    assert len(rec) == int(tr["ShiftRight"][:, A.SR_REAL].sum())
+    assert np.array_equal(rec["pc"], tr["ShiftRight"][:len(rec), A.SR_PC])
+
+
 # ---------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(PROGRAMS))
@@ -203,8 +243,31 @@ def test_device_shard_traces_match_host(name):
         host = tr[chip]
         assert np.array_equal(t.cpu().numpy().view(np.uint32), host), chip
     assert set(dev) >= {"Cpu", "Program", "MemoryLocal", "Global"}
-    want = expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"), tr["Global"])
+    want = expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"), tr["Global"]) + alu_chip_byte_mult(cap)
     assert np.array_equal(bm.cpu().numpy().astype(np.uint64), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 127, 129, 5000])
+def test_device_alu_chips_match_host(n):
+    """Bitwise, Lt, ShiftLeft and ShiftRight from AluEvents (every opcode, every shift amount and
+    comparison-byte position; empty and ragged inputs) == the host builders, Byte lookups included."""
+    import torch
+    ev = A.alu_events(0, n, seed=n + 1, n_lt=n, n_sll=n, n_sr=n)
+    for kind, (_, chip, width) in TG.ALU_CHIPS.items():
+        op, a, b, c, pc = ev[kind]
+        mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
+        host = A.alu_traces({k: ev[k] if k == kind else tuple(np.zeros(0, np.uint32) for _ in range(5))
+                             for k in ("add", "bit", "lt", "sll", "sr")}, mult).get(chip)
+        h = max(16, 1 << max(0, (n - 1).bit_length()))
+        bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+        rec = TG.alu_events(op, a, b, c, pc)
+        dev = TG.alu_trace(kind, TG.to_device(rec), n, height=h, byte_mult=bm).cpu().numpy().view(np.uint32)
+        if n:
+            assert np.array_equal(dev, host), chip
+        else:
+            assert dev.shape == (16, width)
+        assert np.array_equal(bm.cpu().numpy().astype(np.uint64), mult), chip
 
 
 @pytest.mark.gpu
@@ -279,8 +342,8 @@ def test_device_traces_prove_identically():
     cap, tr, pv, m, prep = _capture("sha_syscalls")
     bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
     dev = TG.shard_traces(cap, byte_mult=bm)
-    rest = tr["Byte"].astype(np.int64) - expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"),
-                                                            tr["Global"]).astype(np.int64)
+    rest = tr["Byte"].astype(np.int64) - (expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"), tr["Global"])
+                                          + alu_chip_byte_mult(cap)).astype(np.int64)
     bm += torch.from_numpy(rest.astype(np.int32)).cuda()  # the other chips' lookups, from the host builders
     traces = {k: v for k, v in tr.items() if k not in dev}
     traces.update(dev)

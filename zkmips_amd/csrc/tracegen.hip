@@ -29,6 +29,8 @@ static_assert(sizeof(zkm_alu_event) == 28, "AluEvent layout");
 static_assert(sizeof(zkm_memory_local_event) == 28, "MemoryLocalEvent layout");
 static_assert(sizeof(zkm_memory_init_final_event) == 16, "MemoryInitializeFinalizeEvent layout");
 static_assert(sizeof(zkm_syscall_event) == 56, "SyscallEvent layout");
+static_assert(sizeof(zkm_branch_event) == 28, "BranchEvent layout");
+static_assert(sizeof(zkm_mem_instr_event) == 84, "MemInstrEvent layout");
 
 namespace zkm::tg {
 
@@ -362,6 +364,338 @@ struct AddSubChip {
     }
 };
 
+// ------------------------------------------------------------------ the other AluEvent chips
+// The reference fills these rows in Rust (no C++ row ABI): Bitwise (alu/bitwise/mod.rs:140-171), Lt
+// (alu/lt/mod.rs:179-263), ShiftLeft (alu/sll/mod.rs:200-260), ShiftRight (alu/sr/mod.rs:220-325), each
+// with its Byte lookups.  AluEvent dwords: pc, next_pc, opcode, hi, a, b, c.
+constexpr uint32_t B_AND = 0, B_OR = 1, B_XOR = 2, B_SHRCARRY = 5, B_LTU = 6, B_MSB = 7, B_NOR = 9;
+enum : uint32_t { OP_SRL = 10, OP_SRA = 11, OP_ROR = 12, OP_SLT = 13, OP_AND = 15, OP_OR = 16, OP_XOR = 17 };
+
+enum { BW_PC = 0, BW_NPC = 1, BW_A = 2, BW_B = 6, BW_C = 10, BW_NOR = 14, BW_XOR = 15, BW_OR = 16, BW_AND = 17 };
+struct BitwiseChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_BITWISE_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        const uint32_t op = real ? e[2] & 0xFF : 0u, b = real ? e[5] : 0u, c = real ? e[6] : 0u;
+        if (real) {
+            v[BW_PC] = e[0];
+            v[BW_NPC] = e[1];
+            put_word(v + BW_A, e[4]);
+            put_word(v + BW_B, b);
+            put_word(v + BW_C, c);
+            v[BW_AND] = op == OP_AND;
+            v[BW_OR] = op == OP_OR;
+            v[BW_XOR] = op == OP_XOR;
+            v[BW_NOR] = op != OP_AND && op != OP_OR && op != OP_XOR;
+        }
+        const uint32_t bop = op == OP_AND ? B_AND : op == OP_OR ? B_OR : op == OP_XOR ? B_XOR : B_NOR;
+#pragma unroll
+        for (int k = 0; k < 4; k++) h.byte(bop, byte_of(b, k), byte_of(c, k), real);
+    }
+};
+
+// (x mod p)^-1 of a canonical x (0 -> 0), by Fermat
+__device__ __forceinline__ uint32_t inv_canonical(uint32_t x) {
+    uint64_t r = 1, b = x;
+    for (uint32_t e = P - 2; e; e >>= 1) {
+        if (e & 1) r = r * b % P;
+        b = b * b % P;
+    }
+    return x ? (uint32_t)r : 0u;
+}
+
+enum { LT_PC = 0, LT_NPC = 1, LT_SLT = 2, LT_SLTU = 3, LT_A = 4, LT_B = 8, LT_C = 12, LT_FLAGS = 16, LT_BM = 20,
+       LT_CM = 21, LT_INV = 22, LT_MSB_B = 23, LT_MSB_C = 24, LT_BIT_B = 25, LT_BIT_C = 26, LT_SLTU_R = 27,
+       LT_COMP_EQ = 28, LT_SIGN_EQ = 29, LT_CMP = 30 };
+struct LtChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_LT_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        const uint32_t b = real ? e[5] : 0u, c = real ? e[6] : 0u;
+        const bool slt = real && (e[2] & 0xFF) == OP_SLT;
+        const uint32_t b3 = byte_of(b, 3), c3 = byte_of(c, 3), bm = b3 & 0x7F, cm = c3 & 0x7F;
+        h.byte(B_AND, b3, 0x7F, real);
+        h.byte(B_AND, c3, 0x7F, real);
+        uint32_t bc[4], cc[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            bc[i] = byte_of(b, i);
+            cc[i] = byte_of(c, i);
+        }
+        if (slt) {
+            bc[3] = bm;
+            cc[3] = cm;
+        }
+        int first = -1;  // the most significant differing byte
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (bc[i] != cc[i]) first = i;
+        uint32_t bcb = 0, ccb = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (i == first) {
+                bcb = bc[i];
+                ccb = cc[i];
+            }
+        h.byte(B_LTU, bcb, ccb, real);
+        if (!real) return;
+        const uint32_t msb_b = b3 >> 7, msb_c = c3 >> 7, sltu = bcb < ccb;
+        v[LT_PC] = e[0];
+        v[LT_NPC] = e[1];
+        put_word(v + LT_A, e[4]);
+        put_word(v + LT_B, b);
+        put_word(v + LT_C, c);
+        v[LT_BM] = bm;
+        v[LT_CM] = cm;
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[LT_FLAGS + i] = i == first;
+        v[LT_INV] = inv_canonical(bcb >= ccb ? bcb - ccb : P - (ccb - bcb));
+        v[LT_CMP] = bcb;
+        v[LT_CMP + 1] = ccb;
+        v[LT_SLTU_R] = sltu;
+        v[LT_COMP_EQ] = first < 0;
+        v[LT_MSB_B] = msb_b;
+        v[LT_MSB_C] = msb_c;
+        v[LT_SIGN_EQ] = slt ? msb_b == msb_c : 1u;
+        v[LT_SLT] = slt;
+        v[LT_SLTU] = !slt;
+        v[LT_BIT_B] = slt ? msb_b : 0u;
+        v[LT_BIT_C] = slt ? msb_c : 0u;
+    }
+};
+
+enum { SL_PC = 0, SL_NPC = 1, SL_A = 2, SL_B = 6, SL_C = 10, SL_CBITS = 14, SL_NBITS = 22, SL_MULT = 30, SL_RES = 31,
+       SL_CARRY = 35, SL_NBYTES = 39, SL_REAL = 43 };
+struct ShiftLeftChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_SHIFT_LEFT_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        if (!real) {  // padding: shift_by_n_bits[0] = shift_by_n_bytes[0] = bit_shift_multiplier = 1 (:142-155)
+            v[SL_NBITS] = v[SL_NBYTES] = v[SL_MULT] = 1;
+        }
+        const uint32_t b = real ? e[5] : 0u, c = real ? e[6] : 0u;
+        const uint32_t nb = c & 7, mul = 1u << nb;
+        uint32_t res = 0, cry = 0, carry = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t x = byte_of(b, i) * mul + carry;
+            carry = x >> 8;
+            res |= (x & 0xFF) << (8 * i);
+            cry |= carry << (8 * i);
+        }
+        h.byte(B_U8RANGE, byte_of(res, 0), byte_of(res, 1), real);
+        h.byte(B_U8RANGE, byte_of(res, 2), byte_of(res, 3), real);
+        h.byte(B_U8RANGE, byte_of(cry, 0), byte_of(cry, 1), real);
+        h.byte(B_U8RANGE, byte_of(cry, 2), byte_of(cry, 3), real);
+        if (!real) return;
+        v[SL_PC] = e[0];
+        v[SL_NPC] = e[1];
+        put_word(v + SL_A, e[4]);
+        put_word(v + SL_B, b);
+        put_word(v + SL_C, c);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            v[SL_CBITS + i] = (c >> i) & 1;
+            v[SL_NBITS + i] = (uint32_t)i == nb;
+        }
+        v[SL_MULT] = mul;
+        put_word(v + SL_RES, res);
+        put_word(v + SL_CARRY, cry);
+        const uint32_t nbyte = (c & 31) >> 3;
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[SL_NBYTES + i] = (uint32_t)i == nbyte;
+        v[SL_REAL] = 1;
+    }
+};
+
+enum { SR_PC = 0, SR_NPC = 1, SR_A = 2, SR_B = 6, SR_C = 10, SR_NBITS = 14, SR_NBYTES = 22, SR_BYTE_RES = 26,
+       SR_BIT_RES = 34, SR_CARRY = 42, SR_SHIFTED = 50, SR_MSB = 58, SR_CBITS = 59, SR_SRL = 67, SR_ROR = 68,
+       SR_SRA = 69, SR_REAL = 70 };
+struct ShiftRightChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_SHIFT_RIGHT_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        if (!real) {  // padding: shift_by_n_bits[0] = shift_by_n_bytes[0] = 1
+            v[SR_NBITS] = v[SR_NBYTES] = 1;
+        }
+        const uint32_t op = real ? e[2] & 0xFF : OP_SRL, b = real ? e[5] : 0u, c = real ? e[6] : 0u;
+        const uint32_t nbyte = (c & 31) >> 3, nbit = c & 7;
+        // the operand extended to 64 bits (sign for SRA, a second copy for ROR), shifted by whole bytes
+        const uint64_t ext = op == OP_SRA ? (uint64_t)(int64_t)(int32_t)b
+                             : op == OP_ROR ? ((uint64_t)b | ((uint64_t)b << 32)) : (uint64_t)b;
+        const uint64_t bsr = ext >> (8 * nbyte);
+        uint32_t byte_res[8], shifted[8], carry[8], bit_res[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            byte_res[i] = (uint32_t)(bsr >> (8 * i)) & 0xFF;
+            shifted[i] = byte_res[i] >> nbit;
+            carry[i] = byte_res[i] & ((1u << nbit) - 1);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) bit_res[i] = i < 7 ? (shifted[i] + (carry[i + 1] << (8 - nbit))) & 0xFF : shifted[i];
+        h.byte(B_MSB, byte_of(b, 3), 0, real);
+#pragma unroll
+        for (int i = 0; i < 8; i++) h.byte(B_SHRCARRY, byte_res[i], nbit, real);
+        const uint32_t *words[4] = {byte_res, bit_res, carry, shifted};
+#pragma unroll
+        for (int w = 0; w < 4; w++)
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) h.byte(B_U8RANGE, words[w][k], words[w][k + 1], real);
+        if (!real) return;
+        v[SR_PC] = e[0];
+        v[SR_NPC] = e[1];
+        put_word(v + SR_A, e[4]);
+        put_word(v + SR_B, b);
+        put_word(v + SR_C, c);
+        v[SR_MSB] = b >> 31;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            v[SR_CBITS + i] = (c >> i) & 1;
+            v[SR_NBITS + i] = (uint32_t)i == nbit;
+            v[SR_BYTE_RES + i] = byte_res[i];
+            v[SR_BIT_RES + i] = bit_res[i];
+            v[SR_CARRY + i] = carry[i];
+            v[SR_SHIFTED + i] = shifted[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[SR_NBYTES + i] = (uint32_t)i == nbyte;
+        v[SR_SRL] = op == OP_SRL;
+        v[SR_SRA] = op == OP_SRA;
+        v[SR_ROR] = op == OP_ROR;
+        v[SR_REAL] = 1;
+    }
+};
+
+// ------------------------------------------------------------------ Branch (control_flow/branch/trace.rs:85-130)
+// BranchEvent dwords: pc, next_pc, next_next_pc, opcode, a, b, c.  KoalaBearWordRangeChecker of a word
+// (operations/koala_bear_word.rs:34-52): the 8 bits of its top byte and their running products.
+__device__ __forceinline__ void put_range_check(uint32_t *v, uint32_t x) {
+    uint32_t acc = 1;
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = (x >> (24 + i)) & 1;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        acc = k == 0 ? v[0] * v[1] : acc * v[k + 1];
+        v[8 + k] = acc;
+    }
+}
+
+enum { BR_PC = 0, BR_NPC = 1, BR_NPC_RC = 5, BR_TGT = 19, BR_NNPC = 23, BR_NNPC_RC = 27, BR_A = 41, BR_B = 45,
+       BR_C = 49, BR_BEQ = 53, BR_BNE = 54, BR_BLTZ = 55, BR_BLEZ = 56, BR_BGTZ = 57, BR_BGEZ = 58, BR_BRANCHING = 59,
+       BR_GT = 60, BR_LT = 61 };
+struct BranchChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_BRANCH_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        uint32_t npc = 0, nnpc = 0;
+        bool taken = false;
+        if (real) {
+            const uint32_t op = e[3] & 0xFF, a = e[4], b = e[5], c = e[6];
+            npc = e[1];
+            nnpc = e[2];
+            const int32_t sa = (int32_t)a, sb = (int32_t)b;
+            // Executor::execute_branch (executor.rs:2098-2120)
+            taken = op == BEQ ? a == b : op == BNE ? a != b : op == BGEZ ? sa >= 0 : op == BLEZ ? sa <= 0
+                  : op == BGTZ ? sa > 0 : sa < 0;
+            v[BR_PC] = e[0];
+            v[BR_BEQ] = op == BEQ;
+            v[BR_BNE] = op == BNE;
+            v[BR_BLTZ] = op == BLTZ;
+            v[BR_BGTZ] = op == BGTZ;
+            v[BR_BLEZ] = op == BLEZ;
+            v[BR_BGEZ] = op == BGEZ;
+            put_word(v + BR_A, a);
+            put_word(v + BR_B, b);
+            put_word(v + BR_C, c);
+            v[BR_LT] = sa < sb;
+            v[BR_GT] = sa > sb;
+            put_word(v + BR_NPC, npc);
+            put_word(v + BR_TGT, npc + c);
+            put_word(v + BR_NNPC, nnpc);
+            put_range_check(v + BR_NPC_RC, npc);
+            put_range_check(v + BR_NNPC_RC, nnpc);
+            v[BR_BRANCHING] = taken;
+        }
+        const bool nt = real && !taken;  // the not-taken rows range-check next_pc and next_next_pc
+        h.byte(B_U8RANGE, byte_of(npc, 0), byte_of(npc, 1), nt);
+        h.byte(B_U8RANGE, byte_of(npc, 2), byte_of(npc, 3), nt);
+        h.byte(B_U8RANGE, byte_of(nnpc, 0), byte_of(nnpc, 1), nt);
+        h.byte(B_U8RANGE, byte_of(nnpc, 2), byte_of(nnpc, 3), nt);
+    }
+};
+
+// ------------------------------------------------------------------ MemoryInstrs (memory/instructions/trace.rs:88-251)
+// zkm_mem_instr_event dwords: shard, clk, pc, next_pc, opcode, a, b, c, mem_access (OptionMemoryRecordEnum,
+// 12 dwords), prev_a_val
+enum { MI_PC = 0, MI_NPC = 1, MI_SHARD = 2, MI_CLK = 3, MI_A = 4, MI_B = 8, MI_C = 12, MI_SEL = 16, MI_ADDR = 30,
+       MI_ALIGNED = 34, MI_LS2 = 35, MI_L1 = 36, MI_L2 = 37, MI_L3 = 38, MI_ADDR_RC = 39, MI_ACC = 53, MI_PREV_A = 66,
+       MI_UMV = 70, MI_MSBIT = 74, MI_MSBYTE = 75, MI_NEG = 76, MI_MSBZ = 77 };
+constexpr uint32_t B_LTU_NUM_REGISTERS_M1 = 35;  // REF_NUM_REGISTERS - 1 (executor/src/register.rs)
+
+struct MemoryInstrsChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_MEMORY_INSTRS_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        Access acc{};
+        uint32_t addr = 0, op = 0, umv = 0;
+        if (real) {
+            op = e[4] & 0xFF;
+            const uint32_t a = e[5], b = e[6], c = e[7];
+            addr = b + c;
+            v[MI_PC] = e[2];
+            v[MI_NPC] = e[3];
+            v[MI_SHARD] = e[0];
+            v[MI_CLK] = e[1];
+            put_word(v + MI_A, a);
+            put_word(v + MI_B, b);
+            put_word(v + MI_C, c);
+            put_word(v + MI_PREV_A, e[20]);
+            put_word(v + MI_ADDR, addr);
+#pragma unroll
+            for (int k = 0; k < 14; k++) v[MI_SEL + k] = op == LB + (uint32_t)k;
+            const uint32_t two = addr & 3;
+            v[MI_ALIGNED] = addr - two;
+            v[MI_LS2] = two;
+            v[MI_L1] = two == 1;
+            v[MI_L2] = two == 2;
+            v[MI_L3] = two == 3;
+            put_range_check(v + MI_ADDR_RC, addr);
+            acc = access_of(e + 8);
+            put_word(v + MI_ACC, acc.prev_value);
+            put_access(v, MI_ACC + 4, acc);
+            const uint32_t pmem = acc.prev_value;
+            if (op >= LB && op <= LL) {  // the loaded value before sign extension
+                umv = (op == LB || op == LBU) ? byte_of(pmem, (int)two)
+                    : (op == LH || op == LHU) ? ((two >> 1) ? pmem >> 16 : pmem & 0xFFFF)
+                    : (op == LWL || op == LWR) ? a : pmem;
+            }
+            put_word(v + MI_UMV, umv);
+        }
+        const bool sgn = real && (op == LB || op == LH);
+        const uint32_t msbyte = op == LB ? umv & 0xFF : (umv >> 8) & 0xFF, msbit = msbyte >> 7;
+        const uint32_t s = byte_of(addr, 1) + byte_of(addr, 2) + byte_of(addr, 3);
+        if (real) {
+            v[MI_MSBYTE] = sgn ? msbyte : 0u;
+            v[MI_MSBIT] = sgn ? msbit : 0u;
+            v[MI_NEG] = sgn && msbit == 1;
+            v[MI_MSBZ] = inv_canonical(s);
+            v[MI_MSBZ + 1] = s == 0;
+        }
+        h.byte(B_U16RANGE, acc.d16 >> 8, acc.d16 & 0xFF, real);
+        h.byte(B_U8RANGE, 0, acc.d8, real);
+        h.byte(B_AND, byte_of(addr, 0), 3, real);
+        h.byte(B_MSB, msbyte, 0, sgn);
+        h.byte(B_U8RANGE, byte_of(addr, 1), byte_of(addr, 2), real);
+        h.byte(B_LTU, B_LTU_NUM_REGISTERS_M1, byte_of(addr, 0), real && s == 0);
+    }
+};
+
 // ------------------------------------------------------------------ MemoryLocal (include/memory_local.hpp:8-20)
 // one SingleMemoryLocal (14 columns) per event; a trace row holds four
 struct MemoryLocalChip {
@@ -512,6 +846,42 @@ int zkm_add_sub_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_
     AddSubChip chip{};
     return launch<7, 7, ZKM_ADD_SUB_WIDTH, true>(events, n, trace, height, chip, stream, "zkm_add_sub_events_to_trace",
                                                  byte_mult);
+}
+
+int zkm_bitwise_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                uint32_t *byte_mult, void *stream) {
+    return launch<7, 7, ZKM_BITWISE_WIDTH, true>(events, n, trace, height, BitwiseChip{}, stream,
+                                                 "zkm_bitwise_events_to_trace", byte_mult);
+}
+
+int zkm_lt_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                           uint32_t *byte_mult, void *stream) {
+    return launch<7, 7, ZKM_LT_WIDTH, true>(events, n, trace, height, LtChip{}, stream, "zkm_lt_events_to_trace",
+                                            byte_mult);
+}
+
+int zkm_shift_left_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                   uint32_t *byte_mult, void *stream) {
+    return launch<7, 7, ZKM_SHIFT_LEFT_WIDTH, true>(events, n, trace, height, ShiftLeftChip{}, stream,
+                                                    "zkm_shift_left_events_to_trace", byte_mult);
+}
+
+int zkm_shift_right_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                    uint32_t *byte_mult, void *stream) {
+    return launch<7, 7, ZKM_SHIFT_RIGHT_WIDTH, true>(events, n, trace, height, ShiftRightChip{}, stream,
+                                                     "zkm_shift_right_events_to_trace", byte_mult);
+}
+
+int zkm_branch_events_to_trace(const zkm_branch_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                               uint32_t *byte_mult, void *stream) {
+    return launch<7, 7, ZKM_BRANCH_WIDTH, true>(events, n, trace, height, BranchChip{}, stream,
+                                                "zkm_branch_events_to_trace", byte_mult);
+}
+
+int zkm_memory_instrs_events_to_trace(const zkm_mem_instr_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                      uint32_t *byte_mult, void *stream) {
+    return launch<21, 21, ZKM_MEMORY_INSTRS_WIDTH, true>(events, n, trace, height, MemoryInstrsChip{}, stream,
+                                                         "zkm_memory_instrs_events_to_trace", byte_mult);
 }
 
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,

@@ -543,6 +543,18 @@ def alu_shard_from(ev, seed: int = 3):
     return alu_machine(), {"Byte": byte_prep_trace()}, traces, pvs
 
 
+def clz_dependencies(op, a, b):
+    """The SRL events a CLZ / CLO event adds for ShiftRight (executor/src/dependencies.rs:107-122):
+    bb >> (31 - a) for a nonzero operand bb (b, or ~b for CLO), pc = UNUSED_PC."""
+    bbv = np.where(op == OP_CLO, ~b, b).astype(np.uint32)
+    nz = bbv != 0
+    sh = np.where(nz, 31 - a.astype(np.int64), 0).astype(np.uint32)
+    sr1 = np.where(nz, bbv >> sh, 0).astype(np.uint32)
+    nd = int(nz.sum())
+    return (np.full(nd, OP_SRL, np.uint32), sr1[nz], bbv[nz], sh[nz], np.full(nd, UNUSED_PC, np.uint32),
+            np.full(nd, UNUSED_PC + DEFAULT_PC_INC, np.uint32))
+
+
 def alu_traces(ev, mult: np.ndarray) -> dict:
     """Traces of the ALU chips that have events in `ev` ({kind: (opcode, a, b, c, pc[, next_pc])}); their Byte
     lookups are added to `mult`."""
@@ -712,9 +724,7 @@ def alu_traces(ev, mult: np.ndarray) -> dict:
         byte_lookup(B_U8RANGE, bbb[:, 2], bbb[:, 3])
         byte_lookup(B_LTU, a, np.full(n_cz, 33))
         traces["CloClz"] = t
-        nd = int(nz.sum())
-        dep = (np.full(nd, OP_SRL, np.uint32), sr1[nz], bbv[nz], sh[nz], np.full(nd, UNUSED_PC, np.uint32),
-               np.full(nd, UNUSED_PC + DEFAULT_PC_INC, np.uint32))
+        dep = clz_dependencies(op, a, b)
 
     # ShiftRight (alu/sr/mod.rs:220-325); padded rows: shift_by_n_bits[0] = shift_by_n_bytes[0] = 1
     cpu_sr = ev.get("sr", none)

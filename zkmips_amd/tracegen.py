@@ -54,7 +54,17 @@ SYSCALL_EVENT = np.dtype({"names": ["pc", "next_pc", "shard", "clk", "a_record",
 GLOBAL_EVENT = np.dtype({"names": ["message", "is_receive", "kind"], "formats": [(u4, 7), u1, u1],
                          "offsets": [0, 28, 29], "itemsize": 32})
 
+# BranchEvent (events/instr.rs:159-177): pc, next_pc, next_next_pc, opcode, a, b, c
+BRANCH_EVENT = np.dtype({"names": ["pc", "next_pc", "next_next_pc", "opcode", "a", "b", "c"],
+                         "formats": [u4, u4, u4, u1, u4, u4, u4], "offsets": [0, 4, 8, 12, 16, 20, 24], "itemsize": 28})
+# MemInstrEvent (events/instr.rs:112-135), mem_access as an OptionMemoryRecordEnum (zkm_tracegen.h)
+MEM_INSTR_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode", "a", "b", "c", "mem_access",
+                                      "prev_a_val"],
+                            "formats": [u4, u4, u4, u4, u1, u4, u4, u4, RECORD, u4],
+                            "offsets": [0, 4, 8, 12, 16, 20, 24, 28, 32, 80], "itemsize": 84})
+
 CPU_WIDTH, ADD_SUB_WIDTH, MEMORY_LOCAL_WIDTH, MEMORY_GLOBAL_WIDTH, SYSCALL_WIDTH = 67, 19, 56, 111, 6
+BRANCH_WIDTH, MEMORY_INSTRS_WIDTH = 62, 79
 GLOBAL_WIDTH = 99
 
 
@@ -171,10 +181,46 @@ def shard_global_events(capture: dict) -> np.ndarray:
 
 def add_sub_records(alu) -> np.ndarray:
     """The AddSub chip's AluEvents from the executor's ALU event lists (kind "add")."""
-    ev = alu["add"]
-    if not len(ev):
-        return np.zeros(0, ALU_EVENT)
-    op, a, b, c, pc, npc = MC._ev_arrays(ev)
+    return alu_records(alu, "add")
+
+
+def branch_records(branches) -> np.ndarray:
+    """BranchEvents of the executor's branch tuples (pc, op, a, b, c, next_pc, next_next_pc, taken)."""
+    B = np.asarray(branches, np.int64).reshape(-1, 8)
+    e = np.zeros(len(B), BRANCH_EVENT)
+    e["pc"], e["opcode"], e["a"], e["b"], e["c"] = B[:, 0], B[:, 1], B[:, 2], B[:, 3], B[:, 4]
+    e["next_pc"], e["next_next_pc"] = B[:, 5], B[:, 6]
+    return e
+
+
+def mem_instr_records(mevs, shard: int) -> np.ndarray:
+    """MemInstrEvents of the executor's memory-instruction tuples (pc, npc, op, a, b, c, prev_a, clk, addr,
+    prev_mem, mem, mem_prev_shard, mem_prev_clk): loads carry a Read record, stores a Write record."""
+    E = np.asarray(mevs, np.int64).reshape(-1, 13)
+    n = len(E)
+    assert np.array_equal(E[:, 8], (E[:, 4] + E[:, 5]) & 0xFFFFFFFF), "address = b + c"
+    e = np.zeros(n, MEM_INSTR_EVENT)
+    e["shard"], e["clk"], e["pc"], e["next_pc"], e["opcode"] = shard, E[:, 7], E[:, 0], E[:, 1], E[:, 2]
+    e["a"], e["b"], e["c"], e["prev_a_val"] = E[:, 3], E[:, 4], E[:, 5], E[:, 6]
+    load = np.isin(E[:, 2], MC.LOAD_OPS)
+    m = e["mem_access"]
+    m["tag"] = np.where(load, REC_READ, REC_WRITE)
+    m["read"] = np.where(load[:, None], np.stack([E[:, 10], np.full(n, shard), E[:, 7], E[:, 11], E[:, 12]], 1), 0)
+    m["write"] = np.where(load[:, None], 0, np.stack([E[:, 10], np.full(n, shard), E[:, 7], E[:, 9], E[:, 11], E[:, 12]], 1))
+    e["mem_access"] = m
+    return e
+
+
+def alu_records(alu, kind: str) -> np.ndarray:
+    """The AluEvents of one ALU chip (kind "add", "bit", "lt", "sll" or "sr") from the executor's event
+    lists; ShiftRight's include the SRL dependencies of the CLZ / CLO events."""
+    ev = alu.get(kind, [])
+    arrs = MC._ev_arrays(ev) if len(ev) else tuple(np.zeros(0, np.uint32) for _ in range(6))
+    if kind == "sr" and len(alu.get("clz", [])):
+        op, a, b = MC._ev_arrays(alu["clz"])[:3]
+        dep = A.clz_dependencies(op, a, b)
+        arrs = tuple(np.concatenate([x, d]).astype(np.uint32) for x, d in zip(arrs, dep))
+    op, a, b, c, pc, npc = arrs
     return alu_events(op, a, b, c, pc, npc)
 
 
@@ -185,6 +231,10 @@ def _bind():
         vp, u64 = C.c_void_p, C.c_uint64
         L.zkm_cpu_events_to_trace.argtypes = [vp, u64, C.c_uint32, vp, u64, C.c_uint32, vp, u64, vp, vp, vp]
         L.zkm_add_sub_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        for f in ALU_CHIPS.values():
+            getattr(L, f[0]).argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_branch_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
         L.zkm_syscall_events_to_trace.argtypes = [vp, u64, C.c_int, vp, u64, vp]
@@ -205,7 +255,7 @@ def to_device(records: np.ndarray):
     numpy operations that repack a padded dtype, e.g. np.resize, must not have touched it)."""
     torch = _torch()
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
-                             SYSCALL_EVENT, GLOBAL_EVENT):
+                             SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -261,6 +311,41 @@ def add_sub_trace(events_dev, n: int, height: int = None, byte_mult=None):
     what = "zkm_add_sub_events_to_trace"
     _lib.check(_bind().zkm_add_sub_events_to_trace(_records(events_dev, n, ALU_EVENT, what), n, t.data_ptr(), height,
                                                     _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
+# ALU chips on the AluEvent ABI beside AddSub: executor kind -> (entry point, chip, width)
+ALU_CHIPS = {"bit": ("zkm_bitwise_events_to_trace", "Bitwise", 18), "lt": ("zkm_lt_events_to_trace", "Lt", 36),
+             "sll": ("zkm_shift_left_events_to_trace", "ShiftLeft", 44),
+             "sr": ("zkm_shift_right_events_to_trace", "ShiftRight", 71)}
+
+
+def alu_trace(kind: str, events_dev, n: int, height: int = None, byte_mult=None):
+    """Bitwise / Lt / ShiftLeft / ShiftRight main trace (height x width int32 on the GPU) from n AluEvents."""
+    fn, _, width = ALU_CHIPS[kind]
+    height = height or _pow2(n)
+    t = _trace(height, width)
+    _lib.check(getattr(_bind(), fn)(_records(events_dev, n, ALU_EVENT, fn), n, t.data_ptr(), height,
+                                    _words(byte_mult, 65536 * 10, fn), _stream()), fn)
+    return t
+
+
+def branch_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    height = height or _pow2(n)
+    t = _trace(height, BRANCH_WIDTH)
+    what = "zkm_branch_events_to_trace"
+    _lib.check(_bind().zkm_branch_events_to_trace(_records(events_dev, n, BRANCH_EVENT, what), n, t.data_ptr(), height,
+                                                   _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
+def memory_instrs_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    height = height or _pow2(n)
+    t = _trace(height, MEMORY_INSTRS_WIDTH)
+    what = "zkm_memory_instrs_events_to_trace"
+    _lib.check(_bind().zkm_memory_instrs_events_to_trace(_records(events_dev, n, MEM_INSTR_EVENT, what), n,
+                                                          t.data_ptr(), height, _words(byte_mult, 65536 * 10, what),
+                                                          _stream()), what)
     return t
 
 
@@ -322,6 +407,16 @@ def shard_traces(capture: dict, byte_mult=None):
     adds = add_sub_records(capture["alu"])
     if len(adds):
         out["AddSub"] = add_sub_trace(to_device(adds), len(adds), byte_mult=byte_mult)
+    for kind, (_, chip, _) in ALU_CHIPS.items():
+        rec = alu_records(capture["alu"], kind)
+        if len(rec):
+            out[chip] = alu_trace(kind, to_device(rec), len(rec), byte_mult=byte_mult)
+    if len(capture.get("branches", [])):
+        rec = branch_records(capture["branches"])
+        out["Branch"] = branch_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    if len(capture.get("mevs", [])):
+        rec = mem_instr_records(capture["mevs"], shard)
+        out["MemoryInstrs"] = memory_instrs_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     ml = memory_local_events(capture["entries"])
     out["MemoryLocal"] = memory_local_trace(to_device(ml), len(ml))
     if len(capture["core_syscalls"]):
