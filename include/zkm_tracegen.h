@@ -169,6 +169,32 @@ int zkm_branch_events_to_trace(const zkm_branch_event *events, uint64_t n, uint3
 int zkm_memory_instrs_events_to_trace(const zkm_mem_instr_event *events, uint64_t n, uint32_t *trace, uint64_t height,
                                       uint32_t *byte_mult, void *stream);
 
+/* JumpEvent (events/instr.rs:198-216, #[repr(C)]) and MovCondEvent (:283-301, #[repr(C)]), 28 bytes each */
+typedef struct { uint32_t pc, next_pc, next_next_pc; uint8_t opcode; uint32_t a, b, c; } zkm_jump_event;
+typedef struct { uint32_t pc, next_pc; uint8_t opcode; uint32_t a, b, c, prev_a; } zkm_movcond_event;
+/* CompAluEvent (events/instr.rs:44-72; not #[repr(C)] there, so this is its field order with C layout):
+ * the HI register write of MULT / MULTU (hi_record_is_real = 0 for MUL), 64 bytes */
+typedef struct {
+    uint32_t shard, clk, pc, next_pc;
+    uint8_t opcode;
+    uint32_t hi, a, b, c;
+    zkm_memory_write_record hi_record;
+    uint8_t hi_record_is_real;
+} zkm_comp_alu_event;
+#define ZKM_JUMP_WIDTH 66
+#define ZKM_MOVCOND_WIDTH 32
+#define ZKM_MUL_WIDTH 58
+/* Jump (control_flow/jump/trace.rs:83-102) and MovCond (misc/mov_cond/mod.rs: IsZeroWordOperation of c)
+ * record no Byte lookups.  Mul (alu/mul/mod.rs:218-318): the 64-bit product of the (sign-extended for
+ * MULT) operands by byte limbs with carries, MSB of both top bytes, U16Range of the carries, U8Range of the
+ * product bytes, and the HI write's access columns and timestamp checks. */
+int zkm_jump_events_to_trace(const zkm_jump_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                             void *stream);
+int zkm_movcond_events_to_trace(const zkm_movcond_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                void *stream);
+int zkm_mul_events_to_trace(const zkm_comp_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                            uint32_t *byte_mult, void *stream);
+
 /* MemoryLocal (memory/local.rs:144-185): event i fills entry i % 4 of row i / 4; height rows. */
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,
                                      uint64_t height, void *stream);

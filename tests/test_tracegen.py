@@ -36,6 +36,9 @@ LAYOUTS = {
     "zkm_global_lookup_event": (TG.GLOBAL_EVENT, {f: f for f in TG.GLOBAL_EVENT.names}),
     "zkm_branch_event": (TG.BRANCH_EVENT, {f: f for f in TG.BRANCH_EVENT.names}),
     "zkm_mem_instr_event": (TG.MEM_INSTR_EVENT, {f: f for f in TG.MEM_INSTR_EVENT.names}),
+    "zkm_jump_event": (TG.JUMP_EVENT, {f: f for f in TG.JUMP_EVENT.names}),
+    "zkm_movcond_event": (TG.MOVCOND_EVENT, {f: f for f in TG.MOVCOND_EVENT.names}),
+    "zkm_comp_alu_event": (TG.COMP_ALU_EVENT, {f: f for f in TG.COMP_ALU_EVENT.names}),
 }
 
 
@@ -206,6 +209,8 @@ def alu_chip_byte_mult(cap):
         MC._branch_trace(cap["branches"], look)
     if len(cap.get("mevs", [])):
         MC._mem_instr_trace(cap["mevs"], cap["shard"], look)
+    if len(cap.get("muls", [])):
+        MC._mul_trace(cap["muls"], cap["shard"], look)
     return mult
 
 
@@ -334,12 +339,13 @@ def test_device_traces_empty_and_ragged():
 
 
 @pytest.mark.gpu
-def test_device_traces_prove_identically():
+@pytest.mark.parametrize("name", ["sha_syscalls", "loop", "random"])
+def test_device_traces_prove_identically(name):
     """A shard proven from device-generated traces (ZKM_MEM_DEVICE) gives the host traces' proof bytes."""
     import torch
     from zkmips_amd._lib import Device
     from zkmips_amd.prover import HipProver
-    cap, tr, pv, m, prep = _capture("sha_syscalls")
+    cap, tr, pv, m, prep = _capture(name)
     bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
     dev = TG.shard_traces(cap, byte_mult=bm)
     rest = tr["Byte"].astype(np.int64) - (expected_byte_mult(tr["Cpu"], cap["shard"], tr.get("AddSub"), tr["Global"])

@@ -31,6 +31,9 @@ static_assert(sizeof(zkm_memory_init_final_event) == 16, "MemoryInitializeFinali
 static_assert(sizeof(zkm_syscall_event) == 56, "SyscallEvent layout");
 static_assert(sizeof(zkm_branch_event) == 28, "BranchEvent layout");
 static_assert(sizeof(zkm_mem_instr_event) == 84, "MemInstrEvent layout");
+static_assert(sizeof(zkm_jump_event) == 28, "JumpEvent layout");
+static_assert(sizeof(zkm_movcond_event) == 28, "MovCondEvent layout");
+static_assert(sizeof(zkm_comp_alu_event) == 64, "CompAluEvent layout");
 
 namespace zkm::tg {
 
@@ -696,6 +699,152 @@ struct MemoryInstrsChip {
     }
 };
 
+// ------------------------------------------------------------------ Jump (control_flow/jump/trace.rs:83-102)
+// JumpEvent dwords: pc, next_pc, next_next_pc, opcode, a, b, c; no Byte lookups
+enum { J_PC = 0, J_NPC = 1, J_NPC_RC = 5, J_NNPC = 19, J_NNPC_RC = 23, J_A = 37, J_B = 41, J_C = 45, J_JUMP = 49,
+       J_JUMPI = 50, J_JDIRECT = 51, J_A_RC = 52 };
+struct JumpChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_JUMP_WIDTH; c++) v[c] = 0;
+        if (!e) return;
+        const uint32_t op = e[3] & 0xFF;
+        v[J_PC] = e[0];
+        v[J_JUMP] = op == JUMP;
+        v[J_JUMPI] = op == JUMPI;
+        v[J_JDIRECT] = op == JUMPDIRECT;
+        put_word(v + J_A, e[4]);
+        put_word(v + J_B, e[5]);
+        put_word(v + J_C, e[6]);
+        put_word(v + J_NPC, e[1]);
+        put_word(v + J_NNPC, e[2]);
+        put_range_check(v + J_A_RC, e[4]);
+        put_range_check(v + J_NPC_RC, e[1]);
+        put_range_check(v + J_NNPC_RC, e[2]);
+    }
+};
+
+// ------------------------------------------------------------------ MovCond (misc/mov_cond/mod.rs)
+// MovCondEvent dwords: pc, next_pc, opcode, a, b, c, prev_a; IsZeroWordOperation of c's bytes
+enum { MC_PC = 0, MC_NPC = 1, MC_A = 2, MC_PREV_A = 6, MC_B = 10, MC_C = 14, MC_C0 = 18, MC_MNE = 29, MC_MEQ = 30,
+       MC_WSBH = 31 };
+constexpr uint32_t OP_MEQ = 50, OP_MNE = 51, OP_WSBH = 52;
+struct MovCondChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_MOVCOND_WIDTH; c++) v[c] = 0;
+        if (!e) return;
+        const uint32_t op = e[2] & 0xFF, c = e[5];
+        v[MC_PC] = e[0];
+        v[MC_NPC] = e[1];
+        put_word(v + MC_A, e[3]);
+        put_word(v + MC_B, e[4]);
+        put_word(v + MC_C, c);
+        put_word(v + MC_PREV_A, e[6]);
+        uint32_t z[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {  // IsZeroWordOperation::populate_from_field_element
+            const uint32_t x = byte_of(c, i);
+            z[i] = x == 0;
+            v[MC_C0 + 2 * i] = inv_canonical(x);
+            v[MC_C0 + 2 * i + 1] = z[i];
+        }
+        v[MC_C0 + 8] = z[0] * z[1];
+        v[MC_C0 + 9] = z[2] * z[3];
+        v[MC_C0 + 10] = z[0] * z[1] * z[2] * z[3];
+        v[MC_MEQ] = op == OP_MEQ;
+        v[MC_MNE] = op == OP_MNE;
+        v[MC_WSBH] = op == OP_WSBH;
+    }
+};
+
+// ------------------------------------------------------------------ Mul (alu/mul/mod.rs:218-318)
+// zkm_comp_alu_event dwords: shard, clk, pc, next_pc, opcode, hi, a, b, c, hi_record (6), hi_record_is_real
+enum { MU_PC = 0, MU_NPC = 1, MU_HI = 2, MU_A = 6, MU_B = 10, MU_C = 14, MU_CARRY = 18, MU_PROD = 26, MU_BMSB = 34,
+       MU_CMSB = 35, MU_BSE = 36, MU_CSE = 37, MU_MUL = 38, MU_MULT = 39, MU_MULTU = 40, MU_REAL = 41,
+       MU_HI_ACC = 42, MU_HRR = 55, MU_SHARD = 56, MU_CLK = 57 };
+constexpr uint32_t OP_MUL = 2;
+struct MulChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_MUL_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        const uint32_t op = real ? e[4] & 0xFF : 0u, b = real ? e[7] : 0u, c = real ? e[8] : 0u;
+        const uint32_t bmsb = byte_of(b, 3) >> 7, cmsb = byte_of(c, 3) >> 7;
+        const bool bse = op == MULT && bmsb, cse = op == MULT && cmsb;
+        uint32_t b8[8], c8[8], prod[8], carry[8];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            b8[i] = byte_of(b, i);
+            c8[i] = byte_of(c, i);
+            b8[4 + i] = bse ? 255u : 0u;
+            c8[4 + i] = cse ? 255u : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) prod[i] = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 8 - i; j++) prod[i + j] += b8[i] * c8[j];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            carry[i] = prod[i] >> 8;
+            prod[i] &= 0xFF;
+            if (i + 1 < 8) prod[i + 1] += carry[i];
+        }
+        Access acc{};
+        const bool hrr = real && (e[15] & 0xFF);
+        if (hrr) {  // the HI register write (MemoryWriteRecord: value, shard, timestamp, prev_value, prev_shard, prev_ts)
+            const uint32_t *r = e + 9;
+            acc.on = true;
+            acc.value = r[0];
+            acc.prev_value = r[3];
+            acc.prev_shard = r[4];
+            acc.prev_clk = r[5];
+            const bool cmp = r[4] == r[1];
+            acc.compare = cmp;
+            const uint32_t d = (cmp ? r[2] : r[1]) - (cmp ? r[5] : r[4]) - 1u;
+            acc.d16 = d & 0xFFFF;
+            acc.d8 = (d >> 16) & 0xFF;
+        }
+        h.byte(B_MSB, byte_of(b, 3), 0, real);
+        h.byte(B_MSB, byte_of(c, 3), 0, real);
+#pragma unroll
+        for (int i = 0; i < 8; i++) h.byte(B_U16RANGE, carry[i] >> 8, carry[i] & 0xFF, real);
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) h.byte(B_U8RANGE, prod[k], prod[k + 1], real);
+        h.byte(B_U16RANGE, acc.d16 >> 8, acc.d16 & 0xFF, hrr);
+        h.byte(B_U8RANGE, 0, acc.d8, hrr);
+        if (!real) return;
+        v[MU_PC] = e[2];
+        v[MU_NPC] = e[3];
+        put_word(v + MU_HI, e[5]);
+        put_word(v + MU_A, e[6]);
+        put_word(v + MU_B, b);
+        put_word(v + MU_C, c);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            v[MU_CARRY + i] = carry[i];
+            v[MU_PROD + i] = prod[i];
+        }
+        v[MU_BMSB] = bmsb;
+        v[MU_CMSB] = cmsb;
+        v[MU_BSE] = bse;
+        v[MU_CSE] = cse;
+        v[MU_MUL] = op == OP_MUL;
+        v[MU_MULT] = op == MULT;
+        v[MU_MULTU] = op == MULTU;
+        v[MU_REAL] = 1;
+        v[MU_HRR] = hrr;
+        if (hrr) {
+            v[MU_SHARD] = e[0];
+            v[MU_CLK] = e[1];
+            put_word(v + MU_HI_ACC, acc.prev_value);
+            put_access(v, MU_HI_ACC + 4, acc);
+        }
+    }
+};
+
 // ------------------------------------------------------------------ MemoryLocal (include/memory_local.hpp:8-20)
 // one SingleMemoryLocal (14 columns) per event; a trace row holds four
 struct MemoryLocalChip {
@@ -882,6 +1031,23 @@ int zkm_memory_instrs_events_to_trace(const zkm_mem_instr_event *events, uint64_
                                       uint32_t *byte_mult, void *stream) {
     return launch<21, 21, ZKM_MEMORY_INSTRS_WIDTH, true>(events, n, trace, height, MemoryInstrsChip{}, stream,
                                                          "zkm_memory_instrs_events_to_trace", byte_mult);
+}
+
+int zkm_jump_events_to_trace(const zkm_jump_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                             void *stream) {
+    return launch<7, 7, ZKM_JUMP_WIDTH, false>(events, n, trace, height, JumpChip{}, stream, "zkm_jump_events_to_trace");
+}
+
+int zkm_movcond_events_to_trace(const zkm_movcond_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                void *stream) {
+    return launch<7, 7, ZKM_MOVCOND_WIDTH, false>(events, n, trace, height, MovCondChip{}, stream,
+                                                  "zkm_movcond_events_to_trace");
+}
+
+int zkm_mul_events_to_trace(const zkm_comp_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                            uint32_t *byte_mult, void *stream) {
+    return launch<16, 16, ZKM_MUL_WIDTH, true>(events, n, trace, height, MulChip{}, stream, "zkm_mul_events_to_trace",
+                                               byte_mult);
 }
 
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,

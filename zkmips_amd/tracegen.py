@@ -63,8 +63,18 @@ MEM_INSTR_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode",
                             "formats": [u4, u4, u4, u4, u1, u4, u4, u4, RECORD, u4],
                             "offsets": [0, 4, 8, 12, 16, 20, 24, 28, 32, 80], "itemsize": 84})
 
+# JumpEvent (events/instr.rs:198-216) = BranchEvent's layout; MovCondEvent (:283-301)
+JUMP_EVENT = BRANCH_EVENT
+MOVCOND_EVENT = np.dtype({"names": ["pc", "next_pc", "opcode", "a", "b", "c", "prev_a"],
+                          "formats": [u4, u4, u1, u4, u4, u4, u4], "offsets": [0, 4, 8, 12, 16, 20, 24], "itemsize": 28})
+# CompAluEvent (events/instr.rs:44-72) with C layout (zkm_tracegen.h)
+COMP_ALU_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode", "hi", "a", "b", "c", "hi_record",
+                                     "hi_record_is_real"],
+                           "formats": [u4, u4, u4, u4, u1, u4, u4, u4, u4, (u4, 6), u1],
+                           "offsets": [0, 4, 8, 12, 16, 20, 24, 28, 32, 36, 60], "itemsize": 64})
+
 CPU_WIDTH, ADD_SUB_WIDTH, MEMORY_LOCAL_WIDTH, MEMORY_GLOBAL_WIDTH, SYSCALL_WIDTH = 67, 19, 56, 111, 6
-BRANCH_WIDTH, MEMORY_INSTRS_WIDTH = 62, 79
+BRANCH_WIDTH, MEMORY_INSTRS_WIDTH, JUMP_WIDTH, MOVCOND_WIDTH, MUL_WIDTH = 62, 79, 66, 32, 58
 GLOBAL_WIDTH = 99
 
 
@@ -211,6 +221,40 @@ def mem_instr_records(mevs, shard: int) -> np.ndarray:
     return e
 
 
+def jump_records(jumps) -> np.ndarray:
+    """JumpEvents of the executor's jump tuples (pc, op, a, b, c, next_pc, next_next_pc)."""
+    J = np.asarray(jumps, np.int64).reshape(-1, 7)
+    e = np.zeros(len(J), JUMP_EVENT)
+    e["pc"], e["opcode"], e["a"], e["b"], e["c"] = J[:, 0], J[:, 1], J[:, 2], J[:, 3], J[:, 4]
+    e["next_pc"], e["next_next_pc"] = J[:, 5], J[:, 6]
+    return e
+
+
+def movcond_records(movs) -> np.ndarray:
+    """MovCondEvents of the executor's tuples (pc, next_pc, op, a, b, c, prev_a)."""
+    E = np.asarray(movs, np.int64).reshape(-1, 7)
+    e = np.zeros(len(E), MOVCOND_EVENT)
+    for j, f in enumerate(("pc", "next_pc", "opcode", "a", "b", "c", "prev_a")):
+        e[f] = E[:, j]
+    return e
+
+
+def mul_records(muls, shard: int) -> np.ndarray:
+    """CompAluEvents of the executor's Mul tuples (op, a, b, c, pc, npc, hi, clk, prev_hi, prev_shard, prev_clk;
+    clk < 0: no HI write): the HI record written at clk + POS_HI."""
+    E = np.asarray(muls, np.int64).reshape(-1, 11)
+    n = len(E)
+    e = np.zeros(n, COMP_ALU_EVENT)
+    hrr = E[:, 7] >= 0
+    e["opcode"], e["a"], e["b"], e["c"], e["pc"], e["next_pc"], e["hi"] = (E[:, j] for j in range(7))
+    e["shard"] = np.where(hrr, shard, 0)
+    e["clk"] = np.where(hrr, E[:, 7], 0)
+    e["hi_record"] = np.where(hrr[:, None], np.stack([E[:, 6], np.full(n, shard), E[:, 7] + MC.POS_HI, E[:, 8], E[:, 9],
+                                                      E[:, 10]], 1), 0)
+    e["hi_record_is_real"] = hrr
+    return e
+
+
 def alu_records(alu, kind: str) -> np.ndarray:
     """The AluEvents of one ALU chip (kind "add", "bit", "lt", "sll" or "sr") from the executor's event
     lists; ShiftRight's include the SRL dependencies of the CLZ / CLO events."""
@@ -234,6 +278,9 @@ def _bind():
         for f in ALU_CHIPS.values():
             getattr(L, f[0]).argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_branch_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_jump_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
+        L.zkm_movcond_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
+        L.zkm_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -255,7 +302,8 @@ def to_device(records: np.ndarray):
     numpy operations that repack a padded dtype, e.g. np.resize, must not have touched it)."""
     torch = _torch()
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
-                             SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT):
+                             SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
+                             COMP_ALU_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -349,6 +397,33 @@ def memory_instrs_trace(events_dev, n: int, height: int = None, byte_mult=None):
     return t
 
 
+def jump_trace(events_dev, n: int, height: int = None):
+    height = height or _pow2(n)
+    t = _trace(height, JUMP_WIDTH)
+    what = "zkm_jump_events_to_trace"
+    _lib.check(_bind().zkm_jump_events_to_trace(_records(events_dev, n, JUMP_EVENT, what), n, t.data_ptr(), height,
+                                                 _stream()), what)
+    return t
+
+
+def movcond_trace(events_dev, n: int, height: int = None):
+    height = height or _pow2(n)
+    t = _trace(height, MOVCOND_WIDTH)
+    what = "zkm_movcond_events_to_trace"
+    _lib.check(_bind().zkm_movcond_events_to_trace(_records(events_dev, n, MOVCOND_EVENT, what), n, t.data_ptr(),
+                                                    height, _stream()), what)
+    return t
+
+
+def mul_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    height = height or _pow2(n)
+    t = _trace(height, MUL_WIDTH)
+    what = "zkm_mul_events_to_trace"
+    _lib.check(_bind().zkm_mul_events_to_trace(_records(events_dev, n, COMP_ALU_EVENT, what), n, t.data_ptr(), height,
+                                                _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
 def memory_local_trace(events_dev, n: int, height: int = None):
     height = height or _pow2((n + 3) // 4)
     t = _trace(height, MEMORY_LOCAL_WIDTH)
@@ -392,9 +467,10 @@ def global_trace(events_dev, n: int, height: int = None, byte_mult=None):
 
 
 def shard_traces(capture: dict, byte_mult=None):
-    """Device traces of the chips the reference's row ABI covers, for one executed shard
-    (program_shard(..., capture=c)): Cpu (+ Program multiplicities), AddSub, MemoryLocal and
-    SyscallCore, plus the Global chip (septic-curve lift and running sum), with their Byte lookups
+    """Device traces of one executed shard (program_shard(..., capture=c)): the chips of the reference's
+    row ABI — Cpu (+ Program multiplicities), AddSub, MemoryLocal, SyscallCore — and beyond it Bitwise,
+    Lt, ShiftLeft, ShiftRight, Branch, MemoryInstrs, Jump, MovCond, Mul and the Global chip (septic-curve
+    lift and running sum), with their Byte lookups
     added into `byte_mult` (65536 x 10 int32 on the GPU) if given.  Returns {chip name: GPU tensor}."""
     torch = _torch()
     shard, prog = capture["shard"], capture["prog"]
@@ -417,6 +493,15 @@ def shard_traces(capture: dict, byte_mult=None):
     if len(capture.get("mevs", [])):
         rec = mem_instr_records(capture["mevs"], shard)
         out["MemoryInstrs"] = memory_instrs_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    if len(capture.get("jumps", [])):
+        rec = jump_records(capture["jumps"])
+        out["Jump"] = jump_trace(to_device(rec), len(rec))
+    if len(capture.get("movs", [])):
+        rec = movcond_records(capture["movs"])
+        out["MovCond"] = movcond_trace(to_device(rec), len(rec))
+    if len(capture.get("muls", [])):
+        rec = mul_records(capture["muls"], shard)
+        out["Mul"] = mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     ml = memory_local_events(capture["entries"])
     out["MemoryLocal"] = memory_local_trace(to_device(ml), len(ml))
     if len(capture["core_syscalls"]):
