@@ -575,6 +575,21 @@ def tracegen_bench(args):
         # recursion machine: a permutation per row (compute-bound); n // 4 rows
         "Poseidon2WideDeg3": (lambda: TG.poseidon2_wide_trace(d_p2, n // 4, height=n // 4), 64 + 4 * 313, n // 4),
     }
+    # the other core chips at their heights in the reference's maximal 2^22 shape (maximal_shapes.json["22"][2],
+    # relative to Cpu 2^22): records of the same execution (plus random ALU events for the shifts) tiled
+    ev_alu = MC.A.alu_events(0, 1 << 12, seed=9, n_lt=1 << 12, n_sll=1 << 12, n_sr=1 << 12)
+    for kind, (_, chip, width), lg in (("bit", TG.ALU_CHIPS["bit"], 2), ("lt", TG.ALU_CHIPS["lt"], 2),
+                                       ("sll", TG.ALU_CHIPS["sll"], 4), ("sr", TG.ALU_CHIPS["sr"], 3)):
+        m_ = n >> lg
+        op, a, b, c, pc = ev_alu[kind]
+        d = TG.to_device(tile(TG.alu_events(op, a, b, c, pc))[:m_])
+        chips[chip] = ((lambda k=kind, d=d, m_=m_: TG.alu_trace(k, d, m_, height=m_, byte_mult=bm)), 28 + 4 * width, m_)
+    d_br = TG.to_device(tile(TG.branch_records(cap["branches"]))[:n >> 3])
+    chips["Branch"] = (lambda: TG.branch_trace(d_br, n >> 3, height=n >> 3, byte_mult=bm), 28 + 4 * TG.BRANCH_WIDTH,
+                       n >> 3)
+    d_mi = TG.to_device(tile(TG.mem_instr_records(cap["mevs"], 1))[:n >> 2])
+    chips["MemoryInstrs"] = (lambda: TG.memory_instrs_trace(d_mi, n >> 2, height=n >> 2, byte_mult=bm),
+                             84 + 4 * TG.MEMORY_INSTRS_WIDTH, n >> 2)
     res = {}
     for name, spec in chips.items():
         fn, bytes_per_row = spec[0], spec[1]
