@@ -195,6 +195,27 @@ int zkm_movcond_events_to_trace(const zkm_movcond_event *events, uint64_t n, uin
 int zkm_mul_events_to_trace(const zkm_comp_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
                             uint32_t *byte_mult, void *stream);
 
+#define ZKM_DIVREM_WIDTH 106
+#define ZKM_CLO_CLZ_WIDTH 22
+/* DivRem (alu/divrem/mod.rs:240-390) from CompAluEvents: quotient and remainder recomputed from b, c
+ * (get_quotient_and_remainder, executor/src/utils.rs:33-43: c = 0 gives q = 0xFFFFFFFF, r = b; INT_MIN / -1
+ * wraps), the is-zero / overflow word tests, |c|, |r|, max(1, |c|), c q + r by bytes with carries, the HI
+ * write of DIV / DIVU; MSB of b, c, r, U8Range of q, r and the product bytes.  CloClz (alu/clo_clz/mod.rs:
+ * 85-160) from AluEvents (a = the count): b or ~b, its shift by 31 - a, U8Range of it and LTU(a, 33); padding
+ * rows clz(0) = 32.  Its SRL dependencies are ShiftRight events (zkm_shift_right_events_to_trace). */
+int zkm_divrem_events_to_trace(const zkm_comp_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                               uint32_t *byte_mult, void *stream);
+int zkm_clo_clz_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                uint32_t *byte_mult, void *stream);
+
+#define ZKM_SYSCALL_INSTRS_WIDTH 64
+/* SyscallInstrs (syscall/instructions/trace.rs:82-162) from the shard's SyscallEvents (every syscall the
+ * CPU executed): the syscall-id tests (IsZero against ENTER_UNCONSTRAINED, HINT_LEN, HALT, SYS_EXT_GROUP,
+ * COMMIT, COMMIT_DEFERRED_PROOFS), the COMMIT word bitmap, the HALT / COMMIT_DEFERRED_PROOFS operand's
+ * word range check; no Byte lookups. */
+int zkm_syscall_instrs_events_to_trace(const zkm_syscall_event *events, uint64_t n, uint32_t *trace,
+                                       uint64_t height, void *stream);
+
 /* MemoryLocal (memory/local.rs:144-185): event i fills entry i % 4 of row i / 4; height rows. */
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,
                                      uint64_t height, void *stream);

@@ -200,8 +200,9 @@ def alu_chip_byte_mult(cap):
     host builders over the same events the device gets; CloClz's own lookups excluded)."""
     mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
     ev = {"add": tuple(np.zeros(0, np.uint32) for _ in range(6))}
-    for kind in TG.ALU_CHIPS:
-        r = TG.alu_records(cap["alu"], kind)
+    for kind in list(TG.ALU_CHIPS) + ["clz"]:  # ShiftRight's CLZ dependencies come from the "clz" events
+        r = TG.alu_events(*MC._ev_arrays(cap["alu"][kind])[:5]) if len(cap["alu"].get(kind, [])) else \
+            np.zeros(0, TG.ALU_EVENT)
         ev[kind] = (r["opcode"].astype(np.uint32), r["a"], r["b"], r["c"], r["pc"], r["next_pc"])
     A.alu_traces(ev, mult)
     look = A.byte_lookup_into(mult)  # Branch and MemoryInstrs (host builders)
@@ -211,6 +212,8 @@ def alu_chip_byte_mult(cap):
         MC._mem_instr_trace(cap["mevs"], cap["shard"], look)
     if len(cap.get("muls", [])):
         MC._mul_trace(cap["muls"], cap["shard"], look)
+    if len(cap.get("divs", [])):
+        MC._divrem_trace(cap["divs"], cap["shard"], look)
     return mult
 
 

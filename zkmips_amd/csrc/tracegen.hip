@@ -845,6 +845,230 @@ struct MulChip {
     }
 };
 
+// ------------------------------------------------------------------ DivRem (alu/divrem/mod.rs:240-390)
+// zkm_comp_alu_event as for Mul; quotient and remainder recomputed (get_quotient_and_remainder,
+// executor/src/utils.rs:33-43), the HI write (DIV / DIVU) carries the remainder
+enum { DV_PC = 0, DV_NPC = 1, DV_B = 2, DV_C = 6, DV_Q = 10, DV_R = 14, DV_ABS_R = 18, DV_ABS_C = 22, DV_MAXC = 26,
+       DV_CTQ = 30, DV_CARRY = 38, DV_IS_C0 = 46, DV_DIV = 57, DV_DIVU = 58, DV_MOD = 59, DV_MODU = 60, DV_OVF = 61,
+       DV_OVF_B = 62, DV_OVF_C = 73, DV_BMSB = 84, DV_RMSB = 85, DV_CMSB = 86, DV_BNEG = 87, DV_RNEG = 88,
+       DV_CNEG = 89, DV_RCM = 90, DV_HI_ACC = 91, DV_SHARD = 104, DV_CLK = 105 };
+constexpr uint32_t OP_MOD = 7, OP_MODU = 8;
+
+// IsZeroWordOperation::populate_from_field_element of four field elements (11 columns)
+__device__ __forceinline__ void put_is_zero_word(uint32_t *v, const uint32_t x[4]) {
+    uint32_t z[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        z[i] = x[i] == 0;
+        v[2 * i] = inv_canonical(x[i]);
+        v[2 * i + 1] = z[i];
+    }
+    v[8] = z[0] * z[1];
+    v[9] = z[2] * z[3];
+    v[10] = z[0] * z[1] * z[2] * z[3];
+}
+
+struct DivRemChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_DIVREM_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        const uint32_t op = real ? e[4] & 0xFF : 0u, b = real ? e[7] : 0u, c = real ? e[8] : 0u;
+        const bool sgn = op == DIV || op == OP_MOD;
+        uint32_t q, r;
+        if (c == 0) {
+            q = 0xFFFFFFFFu;
+            r = b;
+        } else if (sgn) {
+            if (b == 0x80000000u && c == 0xFFFFFFFFu) {  // wrapping_div / wrapping_rem
+                q = b;
+                r = 0;
+            } else {
+                q = (uint32_t)((int32_t)b / (int32_t)c);
+                r = (uint32_t)((int32_t)b % (int32_t)c);
+            }
+        } else {
+            q = b / c;
+            r = b % c;
+        }
+        const uint32_t bmsb = b >> 31, cmsb = c >> 31, rmsb = r >> 31;
+        const uint32_t abs_r = sgn && rmsb ? 0u - r : r, abs_c = sgn && cmsb ? 0u - c : c;
+        // c * q + r in 64 bits, as bytes (signed operands sign-extended)
+        const uint64_t ctq = sgn ? (uint64_t)((int64_t)(int32_t)q * (int64_t)(int32_t)c) : (uint64_t)q * (uint64_t)c;
+        const uint64_t r64 = sgn ? (uint64_t)(int64_t)(int32_t)r : (uint64_t)r;
+        uint32_t ctq_b[8], carry[8];
+        uint32_t cy = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            ctq_b[i] = (uint32_t)(ctq >> (8 * i)) & 0xFF;
+            cy = (ctq_b[i] + ((uint32_t)(r64 >> (8 * i)) & 0xFF) + cy) >> 8;
+            carry[i] = cy;
+        }
+        Access acc{};
+        const bool hrr = real && (e[15] & 0xFF);
+        if (hrr) {
+            const uint32_t *rr = e + 9;
+            acc.on = true;
+            acc.value = rr[0];
+            acc.prev_value = rr[3];
+            acc.prev_shard = rr[4];
+            acc.prev_clk = rr[5];
+            const bool cmp = rr[4] == rr[1];
+            acc.compare = cmp;
+            const uint32_t d = (cmp ? rr[2] : rr[1]) - (cmp ? rr[5] : rr[4]) - 1u;
+            acc.d16 = d & 0xFFFF;
+            acc.d8 = (d >> 16) & 0xFF;
+        }
+        h.byte(B_U16RANGE, acc.d16 >> 8, acc.d16 & 0xFF, hrr);
+        h.byte(B_U8RANGE, 0, acc.d8, hrr);
+        h.byte(B_MSB, byte_of(b, 3), 0, real);
+        h.byte(B_MSB, byte_of(c, 3), 0, real);
+        h.byte(B_MSB, byte_of(r, 3), 0, real);
+        h.byte(B_U8RANGE, byte_of(q, 0), byte_of(q, 1), real);
+        h.byte(B_U8RANGE, byte_of(q, 2), byte_of(q, 3), real);
+        h.byte(B_U8RANGE, byte_of(r, 0), byte_of(r, 1), real);
+        h.byte(B_U8RANGE, byte_of(r, 2), byte_of(r, 3), real);
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) h.byte(B_U8RANGE, ctq_b[k], ctq_b[k + 1], real);
+        if (!real) return;
+        v[DV_PC] = e[2];
+        v[DV_NPC] = e[3];
+        put_word(v + DV_B, b);
+        put_word(v + DV_C, c);
+        put_word(v + DV_Q, q);
+        put_word(v + DV_R, r);
+        v[DV_DIV] = op == DIV;
+        v[DV_DIVU] = op == DIVU;
+        v[DV_MOD] = op == OP_MOD;
+        v[DV_MODU] = op == OP_MODU;
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) x[i] = byte_of(c, i);
+        put_is_zero_word(v + DV_IS_C0, x);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {  // bytes of b minus (0, 0, 0, 0x80), as field elements
+            const uint32_t bi = byte_of(b, i), k = i == 3 ? 0x80u : 0u;
+            x[i] = bi >= k ? bi - k : P - (k - bi);
+        }
+        put_is_zero_word(v + DV_OVF_B, x);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {  // bytes of c minus 255
+            const uint32_t ci = byte_of(c, i);
+            x[i] = ci == 255 ? 0u : P - (255 - ci);
+        }
+        put_is_zero_word(v + DV_OVF_C, x);
+        v[DV_BMSB] = bmsb;
+        v[DV_CMSB] = cmsb;
+        v[DV_RMSB] = rmsb;
+        v[DV_BNEG] = sgn ? bmsb : 0u;
+        v[DV_CNEG] = sgn ? cmsb : 0u;
+        v[DV_RNEG] = sgn ? rmsb : 0u;
+        v[DV_OVF] = sgn && b == 0x80000000u && c == 0xFFFFFFFFu;
+        put_word(v + DV_ABS_R, abs_r);
+        put_word(v + DV_ABS_C, abs_c);
+        put_word(v + DV_MAXC, abs_c > 1u ? abs_c : 1u);
+        v[DV_RCM] = c != 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            v[DV_CTQ + i] = ctq_b[i];
+            v[DV_CARRY + i] = carry[i];
+        }
+        if (hrr) {
+            v[DV_SHARD] = e[0];
+            v[DV_CLK] = e[1];
+            put_word(v + DV_HI_ACC, acc.prev_value);
+            put_access(v, DV_HI_ACC + 4, acc);
+        }
+    }
+};
+
+// ------------------------------------------------------------------ CloClz (alu/clo_clz/mod.rs:85-160)
+enum { CZ_PC = 0, CZ_NPC = 1, CZ_A = 2, CZ_B = 6, CZ_BB = 10, CZ_BB_ZERO = 14, CZ_SR1 = 15, CZ_CLZ = 19, CZ_CLO = 20,
+       CZ_REAL = 21 };
+constexpr uint32_t OP_CLO = 20;
+struct CloClzChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_CLO_CLZ_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        const uint32_t a = real ? e[4] : 32u, b = real ? e[5] : 0u;
+        const bool clo = real && (e[2] & 0xFF) == OP_CLO;
+        const uint32_t bb = clo ? ~b : b;
+        h.byte(B_U8RANGE, byte_of(bb, 0), byte_of(bb, 1), real);
+        h.byte(B_U8RANGE, byte_of(bb, 2), byte_of(bb, 3), real);
+        h.byte(B_LTU, a & 0xFF, 33, real);
+        if (!real) {  // padding: clz(0) = 32
+            v[CZ_A] = 32;
+            v[CZ_CLZ] = 1;
+            v[CZ_BB_ZERO] = 1;
+            return;
+        }
+        v[CZ_PC] = e[0];
+        v[CZ_NPC] = e[1];
+        put_word(v + CZ_A, a);
+        put_word(v + CZ_B, b);
+        put_word(v + CZ_BB, bb);
+        v[CZ_BB_ZERO] = bb == 0;
+        put_word(v + CZ_SR1, bb ? bb >> (31 - a) : 0u);
+        v[CZ_CLZ] = !clo;
+        v[CZ_CLO] = clo;
+        v[CZ_REAL] = 1;
+    }
+};
+
+// ------------------------------------------------------------------ SyscallInstrs (syscall/instructions/trace.rs:82-162)
+// from SyscallEvents (a = a_record.value, prev_a = a_record.prev_value, b = arg1, c = arg2); no Byte lookups
+enum { SI_PC = 0, SI_NPC = 1, SI_SHARD = 2, SI_CLK = 3, SI_EXTRA = 4, SI_HALT = 5, SI_LINUX = 6, SI_ID = 7, SI_A = 8,
+       SI_B = 12, SI_C = 16, SI_PREV_A = 20, SI_IZ = 24, SI_BITMAP = 36, SI_RC_BITS = 44, SI_RC_AND = 52,
+       SI_OPERAND = 58, SI_RCOP = 62, SI_REAL = 63 };
+// syscall ids of the IsZero columns in order: ENTER_UNCONSTRAINED, HINT_LEN, HALT, SYS_EXT_GROUP, COMMIT,
+// COMMIT_DEFERRED_PROOFS (syscalls/code.rs)
+__constant__ uint32_t kSiCodes[6] = {0x03, 0xF0, 0x00, SYS_EXT_GROUP, 0x10, 0x1A};
+struct SyscallInstrsChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_SYSCALL_INSTRS_WIDTH; c++) v[c] = 0;
+        if (!e) return;
+        const uint32_t a = e[4], prev = e[7], b = e[12], c = e[13], sid = prev & 0xFFFF;
+        v[SI_PC] = e[0];
+        v[SI_NPC] = e[1];
+        v[SI_SHARD] = e[2];
+        v[SI_CLK] = e[3];
+        put_word(v + SI_A, a);
+        put_word(v + SI_B, b);
+        put_word(v + SI_C, c);
+        put_word(v + SI_PREV_A, prev);
+        v[SI_ID] = e[11];
+        v[SI_EXTRA] = prev >> 24;
+        const bool halt = sid == 0 || sid == SYS_EXT_GROUP;
+        v[SI_HALT] = halt;
+        v[SI_LINUX] = (prev & 0xFF00) != 0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) {  // IsZeroOperation of sid - code (as a field element)
+            const uint32_t code = kSiCodes[k], x = sid >= code ? sid - code : P - (code - sid);
+            v[SI_IZ + 2 * k] = inv_canonical(x);
+            v[SI_IZ + 2 * k + 1] = x == 0;
+        }
+        const bool cdp = sid == 0x1A;
+        if ((sid == 0x10 || cdp) && b < 8) v[SI_BITMAP + b] = 1;
+        const bool chk = halt || cdp;
+        if (chk) {
+            const uint32_t operand = halt ? b : c, msb = byte_of(operand, 3);
+            put_word(v + SI_OPERAND, operand);
+            uint32_t acc = 1;
+#pragma unroll
+            for (int i = 0; i < 8; i++) v[SI_RC_BITS + i] = (msb >> i) & 1;
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                acc = k == 0 ? v[SI_RC_BITS] * v[SI_RC_BITS + 1] : acc * v[SI_RC_BITS + k + 1];
+                v[SI_RC_AND + k] = acc;
+            }
+        }
+        v[SI_RCOP] = chk;
+        v[SI_REAL] = 1;
+    }
+};
+
 // ------------------------------------------------------------------ MemoryLocal (include/memory_local.hpp:8-20)
 // one SingleMemoryLocal (14 columns) per event; a trace row holds four
 struct MemoryLocalChip {
@@ -1048,6 +1272,24 @@ int zkm_mul_events_to_trace(const zkm_comp_alu_event *events, uint64_t n, uint32
                             uint32_t *byte_mult, void *stream) {
     return launch<16, 16, ZKM_MUL_WIDTH, true>(events, n, trace, height, MulChip{}, stream, "zkm_mul_events_to_trace",
                                                byte_mult);
+}
+
+int zkm_divrem_events_to_trace(const zkm_comp_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                               uint32_t *byte_mult, void *stream) {
+    return launch<16, 16, ZKM_DIVREM_WIDTH, true>(events, n, trace, height, DivRemChip{}, stream,
+                                                  "zkm_divrem_events_to_trace", byte_mult);
+}
+
+int zkm_clo_clz_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                uint32_t *byte_mult, void *stream) {
+    return launch<7, 7, ZKM_CLO_CLZ_WIDTH, true>(events, n, trace, height, CloClzChip{}, stream,
+                                                 "zkm_clo_clz_events_to_trace", byte_mult);
+}
+
+int zkm_syscall_instrs_events_to_trace(const zkm_syscall_event *events, uint64_t n, uint32_t *trace,
+                                       uint64_t height, void *stream) {
+    return launch<14, 14, ZKM_SYSCALL_INSTRS_WIDTH, false>(events, n, trace, height, SyscallInstrsChip{}, stream,
+                                                          "zkm_syscall_instrs_events_to_trace");
 }
 
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,

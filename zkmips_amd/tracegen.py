@@ -75,6 +75,7 @@ COMP_ALU_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode", 
 
 CPU_WIDTH, ADD_SUB_WIDTH, MEMORY_LOCAL_WIDTH, MEMORY_GLOBAL_WIDTH, SYSCALL_WIDTH = 67, 19, 56, 111, 6
 BRANCH_WIDTH, MEMORY_INSTRS_WIDTH, JUMP_WIDTH, MOVCOND_WIDTH, MUL_WIDTH = 62, 79, 66, 32, 58
+DIVREM_WIDTH, CLO_CLZ_WIDTH, SYSCALL_INSTRS_WIDTH = 106, 22, 64
 GLOBAL_WIDTH = 99
 
 
@@ -255,6 +256,25 @@ def mul_records(muls, shard: int) -> np.ndarray:
     return e
 
 
+def divrem_records(divs, shard: int) -> np.ndarray:
+    """CompAluEvents of the executor's DivRem tuples (op, b, c, pc, npc, clk, prev_hi, prev_shard, prev_clk;
+    clk < 0: no HI write): a = quotient, hi = remainder, the HI record (the remainder) written at clk + POS_HI."""
+    E = np.asarray(divs, np.int64).reshape(-1, 9)
+    n = len(E)
+    qr = np.asarray([MC._qr(int(o), int(x), int(y)) for o, x, y in zip(E[:, 0], E[:, 1], E[:, 2])],
+                    np.int64).reshape(n, 2)
+    e = np.zeros(n, COMP_ALU_EVENT)
+    hrr = E[:, 5] >= 0
+    e["opcode"], e["b"], e["c"], e["pc"], e["next_pc"] = E[:, 0], E[:, 1], E[:, 2], E[:, 3], E[:, 4]
+    e["a"], e["hi"] = qr[:, 0], qr[:, 1]
+    e["shard"] = np.where(hrr, shard, 0)
+    e["clk"] = np.where(hrr, E[:, 5], 0)
+    e["hi_record"] = np.where(hrr[:, None], np.stack([qr[:, 1], np.full(n, shard), E[:, 5] + MC.POS_HI, E[:, 6],
+                                                      E[:, 7], E[:, 8]], 1), 0)
+    e["hi_record_is_real"] = hrr
+    return e
+
+
 def alu_records(alu, kind: str) -> np.ndarray:
     """The AluEvents of one ALU chip (kind "add", "bit", "lt", "sll" or "sr") from the executor's event
     lists; ShiftRight's include the SRL dependencies of the CLZ / CLO events."""
@@ -281,6 +301,9 @@ def _bind():
         L.zkm_jump_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_movcond_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_divrem_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_clo_clz_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_syscall_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -424,6 +447,33 @@ def mul_trace(events_dev, n: int, height: int = None, byte_mult=None):
     return t
 
 
+def divrem_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    height = height or _pow2(n)
+    t = _trace(height, DIVREM_WIDTH)
+    what = "zkm_divrem_events_to_trace"
+    _lib.check(_bind().zkm_divrem_events_to_trace(_records(events_dev, n, COMP_ALU_EVENT, what), n, t.data_ptr(),
+                                                   height, _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
+def clo_clz_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    height = height or _pow2(n)
+    t = _trace(height, CLO_CLZ_WIDTH)
+    what = "zkm_clo_clz_events_to_trace"
+    _lib.check(_bind().zkm_clo_clz_events_to_trace(_records(events_dev, n, ALU_EVENT, what), n, t.data_ptr(), height,
+                                                    _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
+def syscall_instrs_trace(events_dev, n: int, height: int = None):
+    height = height or _pow2(n)
+    t = _trace(height, SYSCALL_INSTRS_WIDTH)
+    what = "zkm_syscall_instrs_events_to_trace"
+    _lib.check(_bind().zkm_syscall_instrs_events_to_trace(_records(events_dev, n, SYSCALL_EVENT, what), n,
+                                                           t.data_ptr(), height, _stream()), what)
+    return t
+
+
 def memory_local_trace(events_dev, n: int, height: int = None):
     height = height or _pow2((n + 3) // 4)
     t = _trace(height, MEMORY_LOCAL_WIDTH)
@@ -469,7 +519,7 @@ def global_trace(events_dev, n: int, height: int = None, byte_mult=None):
 def shard_traces(capture: dict, byte_mult=None):
     """Device traces of one executed shard (program_shard(..., capture=c)): the chips of the reference's
     row ABI — Cpu (+ Program multiplicities), AddSub, MemoryLocal, SyscallCore — and beyond it Bitwise,
-    Lt, ShiftLeft, ShiftRight, Branch, MemoryInstrs, Jump, MovCond, Mul and the Global chip (septic-curve
+    Lt, ShiftLeft, ShiftRight, CloClz, Branch, MemoryInstrs, Jump, MovCond, Mul, DivRem, SyscallInstrs and the Global chip (septic-curve
     lift and running sum), with their Byte lookups
     added into `byte_mult` (65536 x 10 int32 on the GPU) if given.  Returns {chip name: GPU tensor}."""
     torch = _torch()
@@ -502,11 +552,20 @@ def shard_traces(capture: dict, byte_mult=None):
     if len(capture.get("muls", [])):
         rec = mul_records(capture["muls"], shard)
         out["Mul"] = mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    if len(capture.get("divs", [])):
+        rec = divrem_records(capture["divs"], shard)
+        out["DivRem"] = divrem_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    if len(capture["alu"].get("clz", [])):
+        rec = alu_records(capture["alu"], "clz")
+        out["CloClz"] = clo_clz_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     ml = memory_local_events(capture["entries"])
     out["MemoryLocal"] = memory_local_trace(to_device(ml), len(ml))
     if len(capture["core_syscalls"]):
         sc = syscall_events(capture["core_syscalls"])
         out["SyscallCore"] = syscall_trace(to_device(sc), len(sc))
+    if len(capture["syscalls"]):
+        sc = syscall_events(capture["syscalls"])
+        out["SyscallInstrs"] = syscall_instrs_trace(to_device(sc), len(sc))
     ge = shard_global_events(capture)
     out["Global"], _ = global_trace(to_device(ge), len(ge), byte_mult=byte_mult)
     return out
