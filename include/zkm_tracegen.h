@@ -216,6 +216,20 @@ int zkm_clo_clz_events_to_trace(const zkm_alu_event *events, uint64_t n, uint32_
 int zkm_syscall_instrs_events_to_trace(const zkm_syscall_event *events, uint64_t n, uint32_t *trace,
                                        uint64_t height, void *stream);
 
+/* MiscEvent (events/instr.rs:236-260, #[repr(C)]), 60 bytes */
+typedef struct {
+    uint32_t shard, clk, pc, next_pc;
+    uint8_t opcode;
+    uint32_t a, b, c, prev_a;
+    zkm_memory_write_record hi_record;
+} zkm_misc_event;
+#define ZKM_MISC_INSTRS_WIDTH 72
+/* MiscInstrs (misc/others/trace.rs:81-262): SEXT / TEQ (sign bit and byte, a == b), EXT (lsb, msbd, the
+ * shifted operand), INS (lsb, msb, the rotate / shift / sum chain), MADDU / MSUBU / MADD / MSUB (the product,
+ * the (HI, LO) addend, the 64-bit AddDouble with its carries, the HI write), their Byte lookups. */
+int zkm_misc_instrs_events_to_trace(const zkm_misc_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                    uint32_t *byte_mult, void *stream);
+
 /* MemoryLocal (memory/local.rs:144-185): event i fills entry i % 4 of row i / 4; height rows. */
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,
                                      uint64_t height, void *stream);

@@ -39,6 +39,7 @@ LAYOUTS = {
     "zkm_jump_event": (TG.JUMP_EVENT, {f: f for f in TG.JUMP_EVENT.names}),
     "zkm_movcond_event": (TG.MOVCOND_EVENT, {f: f for f in TG.MOVCOND_EVENT.names}),
     "zkm_comp_alu_event": (TG.COMP_ALU_EVENT, {f: f for f in TG.COMP_ALU_EVENT.names}),
+    "zkm_misc_event": (TG.MISC_EVENT, {f: f for f in TG.MISC_EVENT.names}),
 }
 
 
@@ -214,6 +215,8 @@ def alu_chip_byte_mult(cap):
         MC._mul_trace(cap["muls"], cap["shard"], look)
     if len(cap.get("divs", [])):
         MC._divrem_trace(cap["divs"], cap["shard"], look)
+    if len(cap.get("misc", [])):
+        MC._misc_trace(cap["misc"], cap["shard"], look)
     return mult
 
 
@@ -355,6 +358,8 @@ def test_device_traces_prove_identically(name):
                                           + alu_chip_byte_mult(cap)).astype(np.int64)
     bm += torch.from_numpy(rest.astype(np.int32)).cuda()  # the other chips' lookups, from the host builders
     traces = {k: v for k, v in tr.items() if k not in dev}
+    if name in ("loop", "random"):  # every main trace and every Byte lookup of these shards came from the device
+        assert not rest.any() and set(traces) == {"Byte"}, sorted(traces)
     traces.update(dev)
     traces["Byte"] = bm
     prover = HipProver(Device(0), m, prep, num_queries=16)

@@ -34,6 +34,7 @@ static_assert(sizeof(zkm_mem_instr_event) == 84, "MemInstrEvent layout");
 static_assert(sizeof(zkm_jump_event) == 28, "JumpEvent layout");
 static_assert(sizeof(zkm_movcond_event) == 28, "MovCondEvent layout");
 static_assert(sizeof(zkm_comp_alu_event) == 64, "CompAluEvent layout");
+static_assert(sizeof(zkm_misc_event) == 60, "MiscEvent layout");
 
 namespace zkm::tg {
 
@@ -1069,6 +1070,122 @@ struct SyscallInstrsChip {
     }
 };
 
+// ------------------------------------------------------------------ MiscInstrs (misc/others/trace.rs:81-262)
+// MiscEvent dwords: shard, clk, pc, next_pc, opcode, a, b, c, prev_a, hi_record (6: value, shard, timestamp,
+// prev_value, prev_shard, prev_timestamp); the opcode-specific columns share one union (MS_SPEC)
+enum { MS_SHARD = 0, MS_CLK = 1, MS_PC = 2, MS_NPC = 3, MS_A = 4, MS_PREV_A = 8, MS_B = 12, MS_C = 16, MS_SPEC = 20,
+       MS_SEL = 64 };
+enum { MD_LO = 0, MD_HI = 4, MD_VAL = 8, MD_VALHI = 12, MD_CARRY = 16, MD_S2HI = 23, MD_S2LO = 27, MD_HIACC = 31 };
+constexpr uint32_t OP_INS = 45, OP_MADDU = 46, OP_MSUBU = 47, OP_MADD = 48, OP_MSUB = 49, OP_EXT = 53, OP_TEQ = 54,
+                   OP_SEXT = 55;
+struct MiscInstrsChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_MISC_INSTRS_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        const uint32_t op = real ? e[4] & 0xFF : 0u, a = real ? e[5] : 0u, b = real ? e[6] : 0u;
+        const uint32_t c = real ? e[7] : 0u, pa = real ? e[8] : 0u;
+        uint32_t *S = v + MS_SPEC;
+        // SEXT / TEQ (sext view: most_sig_bit, sig_byte, a_eq_b, is_seb, is_seh)
+        const bool half = c > 0;
+        const uint32_t sbyte = half ? (b >> 8) & 0xFF : b & 0xFF;
+        h.byte(B_MSB, sbyte, 0, real && op == OP_SEXT);
+        // EXT (lsb, msbd, sll_val) and INS (lsb, msb, ror_val, srl_val, sll_val, add_val)
+        const uint32_t lsb = c & 31, hi5 = c >> 5;
+        const bool ext = real && op == OP_EXT, ins = real && op == OP_INS;
+        h.byte(B_U8RANGE, lsb, hi5, ext || ins);
+        h.byte(B_LTU, lsb + hi5, 32, ext);
+        h.byte(B_LTU, lsb, hi5 + 1, ins);
+        h.byte(B_LTU, hi5, 32, ins);
+        // MADDU / MSUBU / MADD / MSUB: the product plus the (HI, LO) addend as a 64-bit AddDouble
+        const bool md = real && op >= OP_MADDU && op <= OP_MSUB;
+        const bool sgn = op == OP_MADD || op == OP_MSUB, is_add = op == OP_MADDU || op == OP_MADD;
+        const uint64_t prod = sgn ? (uint64_t)((int64_t)(int32_t)b * (int64_t)(int32_t)c) : (uint64_t)b * (uint64_t)c;
+        const uint32_t hi_prev = real ? e[12] : 0u, hi_new = real ? e[9] : 0u;
+        const uint32_t s2lo = is_add ? pa : a, s2hi = is_add ? hi_prev : hi_new;
+        const uint64_t addend = ((uint64_t)s2hi << 32) | s2lo, tot = prod + addend;
+        const uint32_t words[6] = {(uint32_t)prod, (uint32_t)(prod >> 32), s2lo, s2hi, (uint32_t)tot,
+                                   (uint32_t)(tot >> 32)};
+#pragma unroll
+        for (int w = 0; w < 6; w++) {
+            h.byte(B_U8RANGE, byte_of(words[w], 0), byte_of(words[w], 1), md);
+            h.byte(B_U8RANGE, byte_of(words[w], 2), byte_of(words[w], 3), md);
+        }
+        Access acc{};
+        if (md) {  // the HI write at clk + POS_HI
+            const uint32_t *r = e + 9;
+            acc.on = true;
+            acc.value = r[0];
+            acc.prev_value = r[3];
+            acc.prev_shard = r[4];
+            acc.prev_clk = r[5];
+            const bool cmp = r[4] == r[1];
+            acc.compare = cmp;
+            const uint32_t d = (cmp ? r[2] : r[1]) - (cmp ? r[5] : r[4]) - 1u;
+            acc.d16 = d & 0xFFFF;
+            acc.d8 = (d >> 16) & 0xFF;
+        }
+        h.byte(B_U16RANGE, acc.d16 >> 8, acc.d16 & 0xFF, md);
+        h.byte(B_U8RANGE, 0, acc.d8, md);
+        if (!real) return;
+        v[MS_PC] = e[2];
+        v[MS_NPC] = e[3];
+        put_word(v + MS_A, a);
+        put_word(v + MS_B, b);
+        put_word(v + MS_C, c);
+        put_word(v + MS_PREV_A, pa);
+        // selectors in MISC_OPS order: SEXT, INS, EXT, MADDU, MSUBU, MADD, MSUB, TEQ
+        v[MS_SEL + 0] = op == OP_SEXT;
+        v[MS_SEL + 1] = op == OP_INS;
+        v[MS_SEL + 2] = op == OP_EXT;
+        v[MS_SEL + 3] = op == OP_MADDU;
+        v[MS_SEL + 4] = op == OP_MSUBU;
+        v[MS_SEL + 5] = op == OP_MADD;
+        v[MS_SEL + 6] = op == OP_MSUB;
+        v[MS_SEL + 7] = op == OP_TEQ;
+        if (op == OP_SEXT || op == OP_TEQ) {
+            S[0] = half ? (b & 0xFFFF) >> 15 : (b & 0xFF) >> 7;
+            S[1] = sbyte;
+            S[2] = a == b;
+            S[3] = !half;
+            S[4] = half;
+        } else if (ext) {
+            S[0] = lsb;
+            S[1] = hi5;
+            const int sh = 31 - (int)lsb - (int)hi5;
+            put_word(S + 2, sh >= 0 ? b << sh : 0u);
+        } else if (ins) {
+            S[0] = lsb;
+            S[1] = hi5;
+            const uint64_t p = pa;
+            const uint32_t ror = (uint32_t)(((p >> lsb) | (p << (32 - lsb))) & 0xFFFFFFFFull);
+            const uint32_t srl = (uint32_t)((uint64_t)ror >> (hi5 - lsb + 1));
+            const uint32_t sll = (uint32_t)(((uint64_t)b << (31 - hi5 + lsb)) & 0xFFFFFFFFull);
+            put_word(S + 2, ror);
+            put_word(S + 6, srl);
+            put_word(S + 10, sll);
+            put_word(S + 14, srl + sll);
+        } else if (md) {
+            v[MS_SHARD] = e[0];
+            v[MS_CLK] = e[1];
+            uint32_t cy = 0;
+#pragma unroll
+            for (int j = 0; j < 7; j++) {
+                cy = ((uint32_t)(prod >> (8 * j)) & 0xFF) + ((uint32_t)(addend >> (8 * j)) & 0xFF) + cy > 255;
+                S[MD_CARRY + j] = cy;
+            }
+            put_word(S + MD_LO, words[0]);
+            put_word(S + MD_HI, words[1]);
+            put_word(S + MD_VAL, words[4]);
+            put_word(S + MD_VALHI, words[5]);
+            put_word(S + MD_S2HI, s2hi);
+            put_word(S + MD_S2LO, s2lo);
+            put_word(S + MD_HIACC, acc.prev_value);
+            put_access(S, MD_HIACC + 4, acc);
+        }
+    }
+};
+
 // ------------------------------------------------------------------ MemoryLocal (include/memory_local.hpp:8-20)
 // one SingleMemoryLocal (14 columns) per event; a trace row holds four
 struct MemoryLocalChip {
@@ -1290,6 +1407,12 @@ int zkm_syscall_instrs_events_to_trace(const zkm_syscall_event *events, uint64_t
                                        uint64_t height, void *stream) {
     return launch<14, 14, ZKM_SYSCALL_INSTRS_WIDTH, false>(events, n, trace, height, SyscallInstrsChip{}, stream,
                                                           "zkm_syscall_instrs_events_to_trace");
+}
+
+int zkm_misc_instrs_events_to_trace(const zkm_misc_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                    uint32_t *byte_mult, void *stream) {
+    return launch<15, 15, ZKM_MISC_INSTRS_WIDTH, true>(events, n, trace, height, MiscInstrsChip{}, stream,
+                                                       "zkm_misc_instrs_events_to_trace", byte_mult);
 }
 
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,

@@ -1764,7 +1764,7 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     if capture is not None:
         capture.update(steps=steps, alu=ev, syscalls=sc, core_syscalls=sc[tab] if len(sc) else sc, entries=ent,
                        shard=shard, prog=prog, branches=branches, mevs=mevs, jumps=jumps, movs=movs,
-                       muls=muls, divs=divs)
+                       muls=muls, divs=divs, misc=misc)
 
     assert mult.max() < P
     traces["Byte"] = mult.astype(np.uint32)

@@ -75,7 +75,11 @@ COMP_ALU_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode", 
 
 CPU_WIDTH, ADD_SUB_WIDTH, MEMORY_LOCAL_WIDTH, MEMORY_GLOBAL_WIDTH, SYSCALL_WIDTH = 67, 19, 56, 111, 6
 BRANCH_WIDTH, MEMORY_INSTRS_WIDTH, JUMP_WIDTH, MOVCOND_WIDTH, MUL_WIDTH = 62, 79, 66, 32, 58
-DIVREM_WIDTH, CLO_CLZ_WIDTH, SYSCALL_INSTRS_WIDTH = 106, 22, 64
+DIVREM_WIDTH, CLO_CLZ_WIDTH, SYSCALL_INSTRS_WIDTH, MISC_INSTRS_WIDTH = 106, 22, 64, 72
+# MiscEvent (events/instr.rs:236-260)
+MISC_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode", "a", "b", "c", "prev_a", "hi_record"],
+                       "formats": [u4, u4, u4, u4, u1, u4, u4, u4, u4, (u4, 6)],
+                       "offsets": [0, 4, 8, 12, 16, 20, 24, 28, 32, 36], "itemsize": 60})
 GLOBAL_WIDTH = 99
 
 
@@ -275,6 +279,21 @@ def divrem_records(divs, shard: int) -> np.ndarray:
     return e
 
 
+def misc_records(misc, shard: int) -> np.ndarray:
+    """MiscEvents of the executor's tuples (op, a, b, c, prev_a, pc, npc, clk, hi_prev, hi_new, hi_prev_shard,
+    hi_prev_clk): MADDU / MSUBU / MADD / MSUB carry the HI write at clk + POS_HI."""
+    E = np.asarray(misc, np.int64).reshape(-1, 12)
+    n = len(E)
+    e = np.zeros(n, MISC_EVENT)
+    md = np.isin(E[:, 0], MC.MADDSUB_OPS)
+    e["opcode"], e["a"], e["b"], e["c"], e["prev_a"], e["pc"], e["next_pc"] = (E[:, j] for j in range(7))
+    e["shard"] = np.where(md, shard, 0)
+    e["clk"] = E[:, 7]
+    e["hi_record"] = np.where(md[:, None], np.stack([E[:, 9], np.full(n, shard), E[:, 7] + MC.POS_HI, E[:, 8],
+                                                     E[:, 10], E[:, 11]], 1), 0)
+    return e
+
+
 def alu_records(alu, kind: str) -> np.ndarray:
     """The AluEvents of one ALU chip (kind "add", "bit", "lt", "sll" or "sr") from the executor's event
     lists; ShiftRight's include the SRL dependencies of the CLZ / CLO events."""
@@ -304,6 +323,7 @@ def _bind():
         L.zkm_divrem_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_clo_clz_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_syscall_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
+        L.zkm_misc_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -326,7 +346,7 @@ def to_device(records: np.ndarray):
     torch = _torch()
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
                              SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
-                             COMP_ALU_EVENT):
+                             COMP_ALU_EVENT, MISC_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -474,6 +494,15 @@ def syscall_instrs_trace(events_dev, n: int, height: int = None):
     return t
 
 
+def misc_instrs_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    height = height or _pow2(n)
+    t = _trace(height, MISC_INSTRS_WIDTH)
+    what = "zkm_misc_instrs_events_to_trace"
+    _lib.check(_bind().zkm_misc_instrs_events_to_trace(_records(events_dev, n, MISC_EVENT, what), n, t.data_ptr(),
+                                                        height, _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
 def memory_local_trace(events_dev, n: int, height: int = None):
     height = height or _pow2((n + 3) // 4)
     t = _trace(height, MEMORY_LOCAL_WIDTH)
@@ -519,7 +548,7 @@ def global_trace(events_dev, n: int, height: int = None, byte_mult=None):
 def shard_traces(capture: dict, byte_mult=None):
     """Device traces of one executed shard (program_shard(..., capture=c)): the chips of the reference's
     row ABI — Cpu (+ Program multiplicities), AddSub, MemoryLocal, SyscallCore — and beyond it Bitwise,
-    Lt, ShiftLeft, ShiftRight, CloClz, Branch, MemoryInstrs, Jump, MovCond, Mul, DivRem, SyscallInstrs and the Global chip (septic-curve
+    Lt, ShiftLeft, ShiftRight, CloClz, Branch, MemoryInstrs, Jump, MovCond, Mul, DivRem, MiscInstrs, SyscallInstrs and the Global chip (septic-curve
     lift and running sum), with their Byte lookups
     added into `byte_mult` (65536 x 10 int32 on the GPU) if given.  Returns {chip name: GPU tensor}."""
     torch = _torch()
@@ -555,6 +584,9 @@ def shard_traces(capture: dict, byte_mult=None):
     if len(capture.get("divs", [])):
         rec = divrem_records(capture["divs"], shard)
         out["DivRem"] = divrem_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    if len(capture.get("misc", [])):
+        rec = misc_records(capture["misc"], shard)
+        out["MiscInstrs"] = misc_instrs_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     if len(capture["alu"].get("clz", [])):
         rec = alu_records(capture["alu"], "clz")
         out["CloClz"] = clo_clz_trace(to_device(rec), len(rec), byte_mult=byte_mult)
