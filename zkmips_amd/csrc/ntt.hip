@@ -926,6 +926,129 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
     }
 }
 
+// Persistent form of k_ntt_s9b: each workgroup walks the (tile, column) work items w = blockIdx.x,
+// blockIdx.x + gridDim.x, ... (gridDim.x a multiple of 8, so item w stays on XCD w mod 8 as in k_ntt_s9b's
+// remap), and issues the next item's 16 loads into a second register set before the current item's
+// butterflies, LDS exchanges and stores: the loads are in flight while the block computes, instead of the
+// block alternating between waiting on HBM and issuing VALU.  Barriers wait on LDS only (the prefetched
+// loads are not drained at them).
+namespace s9 {
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt left at their maxima
+    __builtin_amdgcn_s_barrier();
+}
+}  // namespace s9
+
+template <bool DIT, int MODE>
+__global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9p(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+                                                        int logS, const uint32_t *__restrict__ tw,
+                                                        uint32_t tw_words, uint32_t nv, uint32_t total) {
+    using namespace s9;
+    constexpr bool SWZ = DIT && MODE == MODE_BITREV_OUT;
+    __shared__ uint32_t x[512 * 32];
+    const uint32_t S = 1u << logS, S4 = S * 4;
+    const uint32_t ntile = total / nv;
+    const uint32_t t = threadIdx.x & 31, u = threadIdx.x >> 5;
+    const auto rtw = mkrs(tw, tw_words * 4);
+    // the work item's (column, tile) from its linear index, k_ntt_s9b's XCD-aware remap
+    auto item = [&](uint32_t lin, uint32_t &col, uint32_t &tile) {
+        const uint32_t vid = (lin & 7) * (total >> 3) + (lin >> 3);
+        col = vid % nv;
+        tile = vid / nv;
+        (void)ntile;
+    };
+    auto load = [&](uint32_t lin, uint32_t *v) {
+        uint32_t col, tile;
+        item(lin, col, tile);
+        const uint32_t outer = tile >> (logS - 5), c0 = (tile & ((S >> 5) - 1)) * 32, base = outer * 512u * S;
+        const auto rsrc = mkrs(src + ms.off(col) + base, 512u * S4);
+        const uint32_t ct = c0 + t;
+        if (DIT) {
+            const uint32_t vL16 = (16 * u * S + ct) * 4;
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = bld(rsrc, vL16, (uint32_t)k * S4);
+        } else {
+            const uint32_t vLH = (u * S + ct) * 4;
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, vLH, (uint32_t)(32 * n + 64 * k) * S4);
+        }
+    };
+    uint32_t v[16], vn[16];
+    uint32_t lin = blockIdx.x;
+    if (lin < total) load(lin, v);
+    for (; lin < total; lin += gridDim.x) {
+        const uint32_t nxt = lin + gridDim.x;
+        if (nxt < total) load(nxt, vn);
+        uint32_t col, tile;
+        item(lin, col, tile);
+        const uint32_t outer = tile >> (logS - 5), c0 = (tile & ((S >> 5) - 1)) * 32, base = outer * 512u * S;
+        const uint32_t ct = c0 + t;
+        const uint32_t vLL = ct * 4;
+        const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4, vLM1 = (((2 * u + 1) & 7) * S + ct) * 4;
+        const uint32_t vLH = (u * S + ct) * 4;
+        const uint32_t vL16 = (16 * u * S + ct) * 4;
+        lds_barrier();  // the previous item's last LDS reads are done
+        if (DIT) {
+            net8b<true, LL>(v, rtw, vLL, 0, S4);
+            net8b<true, LL>(v + 8, rtw, vLL, 0, S4);
+            to_ldsb<LL, false>(x, v, u, t);
+            lds_barrier();
+            from_ldsb<LM, false>(x, v, u, t);
+            net8b<true, LM>(v, rtw, vLM0, 0, S4);
+            net8b<true, LM>(v + 8, rtw, vLM1, 0, S4);
+            lds_barrier();
+            to_ldsb<LM, false>(x, v, u, t);
+            lds_barrier();
+            from_ldsb<LH, false>(x, v, u, t);
+            net8b<true, LH>(v, rtw, vLH, 0, S4);
+            net8b<true, LH>(v + 8, rtw, vLH, 32 * S4, S4);
+            if (MODE == MODE_PLAIN) {
+                const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+#pragma unroll
+                    for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, vLH, (uint32_t)(32 * n + 64 * k) * S4);
+            } else {  // BITREV_OUT (as k_ntt_s9b)
+                lds_barrier();
+                to_ldsb<LH, SWZ>(x, v, u, t);
+                lds_barrier();
+                const auto rdst = mkrs(dst + md.off(col), 512u * S4);
+                const uint32_t q = threadIdx.x & 511, hb = threadIdx.x >> 9, rq = rev_bits(q, 9);
+                const uint32_t vo = (((rev_bits(c0, logS) + (hb << (logS - 1))) << 9) + q) * 4;
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const uint32_t tc = 2 * i + hb;
+                    const uint32_t so = (rev_bits((uint32_t)(2 * i), 5) << (logS - 5)) << 11;
+                    bst(x[atb<SWZ>(rq, tc)], rdst, vo, so);
+                }
+            }
+        } else {
+            net8b<false, LH>(v, rtw, vLH, 0, S4);
+            net8b<false, LH>(v + 8, rtw, vLH, 32 * S4, S4);
+            to_ldsb<LH, false>(x, v, u, t);
+            lds_barrier();
+            from_ldsb<LM, false>(x, v, u, t);
+            net8b<false, LM>(v, rtw, vLM0, 0, S4);
+            net8b<false, LM>(v + 8, rtw, vLM1, 0, S4);
+            lds_barrier();
+            to_ldsb<LM, false>(x, v, u, t);
+            lds_barrier();
+            from_ldsb<LL, false>(x, v, u, t);
+            net8b<false, LL>(v, rtw, vLL, 0, S4);
+            net8b<false, LL>(v + 8, rtw, vLL, 0, S4);
+            const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, vL16, (uint32_t)(8 * n + k) * S4);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = vn[k];
+    }
+}
+
 // ------------------------------------------------------------------ dispatch
 static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
 static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
@@ -942,6 +1065,28 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     if (logR == 9 && tw_words && mode != MODE_TWIST_OUT) {  // buffer-addressed register tiles
         const dim3 g1(g.x * nv);  // one dimension: (tile, column) remapped in the kernel
         static const int remap = getenv("ZKM_NTT_NOREMAP") ? 0 : 1;  // A/B knob
+        // persistent prefetching form: ZKM_NTT_PERSIST = workgroups per CU (0 = the one-item-per-workgroup kernel)
+        static const int persist = [] {
+            const char *e = getenv("ZKM_NTT_PERSIST");
+            return e ? atoi(e) : 0;
+        }();
+        const uint32_t total = g1.x;
+        if (persist > 0 && remap && (total & 7) == 0) {
+            uint32_t grid = 256u * (uint32_t)persist;
+            if (grid > total) grid = total & ~7u;
+            const dim3 gp(grid);
+            if (!DIT)
+                hipLaunchKernelGGL((k_ntt_s9p<false, MODE_PLAIN>), gp, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                                   tw_words, nv, total);
+            else if (mode == MODE_PLAIN)
+                hipLaunchKernelGGL((k_ntt_s9p<true, MODE_PLAIN>), gp, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                                   tw_words, nv, total);
+            else
+                hipLaunchKernelGGL((k_ntt_s9p<true, MODE_BITREV_OUT>), gp, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
+                                   tw, tw_words, nv, total);
+            HIP_CHECK(hipGetLastError());
+            return;
+        }
         if (!DIT)
             hipLaunchKernelGGL((k_ntt_s9b<false, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
                                tw_words, nv, remap);
