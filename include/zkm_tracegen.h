@@ -230,6 +230,20 @@ typedef struct {
 int zkm_misc_instrs_events_to_trace(const zkm_misc_event *events, uint64_t n, uint32_t *trace, uint64_t height,
                                     uint32_t *byte_mult, void *stream);
 
+/* ShaExtend (syscall/precompiles/sha256/extend/trace.rs:29-150): ShaExtendEvent holds Vecs (one read of
+ * w[i-15], w[i-2], w[i-16], w[i-7] and one write of w[i] per step i = 16..63), so its rows travel flattened,
+ * one record per step in call order (48 per call): the call's shard, clk and w_ptr, the four reads, the write.
+ * Every row gets the 16/48-cycle flags (flags.rs:13-34), real rows the access columns, the rotate / shift
+ * carries (ShrCarry lookups), the XORs and the Add4 of w[i-16] + s0 + w[i-7] + s1 (U8 range checks). */
+typedef struct {
+    uint32_t shard, clk, w_ptr;
+    zkm_memory_read_record w_i_minus_15, w_i_minus_2, w_i_minus_16, w_i_minus_7;
+    zkm_memory_write_record w_i;
+} zkm_sha_extend_row;  /* 116 bytes */
+#define ZKM_SHA_EXTEND_WIDTH 176
+int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, uint32_t *trace, uint64_t height,
+                                   uint32_t *byte_mult, void *stream);
+
 /* MemoryLocal (memory/local.rs:144-185): event i fills entry i % 4 of row i / 4; height rows. */
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,
                                      uint64_t height, void *stream);

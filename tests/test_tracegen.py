@@ -20,6 +20,7 @@ import pytest
 from zkmips_amd import mips_alu as A
 from zkmips_amd import mips_core as MC
 from zkmips_amd import mips_memory as MM
+from zkmips_amd import mips_syscall as SY
 from zkmips_amd import tracegen as TG
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -40,6 +41,9 @@ LAYOUTS = {
     "zkm_movcond_event": (TG.MOVCOND_EVENT, {f: f for f in TG.MOVCOND_EVENT.names}),
     "zkm_comp_alu_event": (TG.COMP_ALU_EVENT, {f: f for f in TG.COMP_ALU_EVENT.names}),
     "zkm_misc_event": (TG.MISC_EVENT, {f: f for f in TG.MISC_EVENT.names}),
+    "zkm_sha_extend_row": (TG.SHA_EXTEND_ROW, {"shard": "shard", "clk": "clk", "w_ptr": "w_ptr", "r15": "w_i_minus_15",
+                                               "r2": "w_i_minus_2", "r16": "w_i_minus_16", "r7": "w_i_minus_7",
+                                               "w": "w_i"}),
 }
 
 
@@ -373,3 +377,28 @@ def test_repacked_records_are_refused():
     assert ev[np.arange(10) % 3].dtype == TG.CPU_EVENT
     with pytest.raises(ValueError):
         TG.to_device(np.resize(ev, 10))
+
+
+def _sha_extend_events(calls):
+    prog = MC.sha_program(calls, seed=4, compress=False)
+    state = MC.fresh_state()
+    regs = MC.initial_registers(1)
+    MC.program_shard(prog, 1, 1, 1 << 14, state=state, regs=regs)
+    return [e for code, _, e in state["precompile"] if code == SY.SHA_EXTEND]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("calls", [1, 3, 7])
+def test_device_sha_extend_matches_host(calls):
+    """ShaExtend rows from the executor's SHA_EXTEND events == the host builder (flags of the padding rows,
+    access columns, rotate / shift carries, XORs, Add4), Byte lookups included."""
+    import torch
+    evs = _sha_extend_events(calls)
+    assert len(evs) == calls
+    mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
+    host = SY.sha_extend_trace(evs, A.byte_lookup_into(mult))
+    rows = TG.sha_extend_records(evs)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.sha_extend_trace(TG.to_device(rows), len(rows), height=len(host), byte_mult=bm)
+    assert np.array_equal(dev.cpu().numpy().view(np.uint32), host)
+    assert np.array_equal(bm.cpu().numpy().astype(np.uint64), mult)

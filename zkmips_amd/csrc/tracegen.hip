@@ -35,6 +35,7 @@ static_assert(sizeof(zkm_jump_event) == 28, "JumpEvent layout");
 static_assert(sizeof(zkm_movcond_event) == 28, "MovCondEvent layout");
 static_assert(sizeof(zkm_comp_alu_event) == 64, "CompAluEvent layout");
 static_assert(sizeof(zkm_misc_event) == 60, "MiscEvent layout");
+static_assert(sizeof(zkm_sha_extend_row) == 116, "ShaExtend row record layout");
 
 namespace zkm::tg {
 
@@ -1186,6 +1187,168 @@ struct MiscInstrsChip {
     }
 };
 
+// ------------------------------------------------------------------ ShaExtend (sha256/extend/trace.rs:29-150)
+// One row per extension step: zkm_sha_extend_row dwords: shard, clk (the call's), w_ptr, then the reads of
+// w[i-15], w[i-2], w[i-16], w[i-7] (MemoryReadRecord: value, shard, timestamp, prev_shard, prev_timestamp)
+// and the write of w[i] (MemoryWriteRecord: value, shard, timestamp, prev_value, prev_shard, prev_timestamp)
+enum { SE_SHARD = 0, SE_CLK = 1, SE_WPTR = 2, SE_I = 3, SE_C16 = 4, SE_C16S = 5, SE_C16E = 7, SE_C48 = 9, SE_C48S = 12,
+       SE_C48E = 13, SE_W15 = 14, SE_RR7 = 23, SE_RR18 = 35, SE_RS3 = 47, SE_S0I = 59, SE_S0 = 63, SE_W2 = 67,
+       SE_RR17 = 76, SE_RR19 = 88, SE_RS10 = 100, SE_S1I = 112, SE_S1 = 116, SE_W16 = 120, SE_W7 = 129, SE_S2 = 138,
+       SE_WI = 162, SE_REAL = 175 };
+constexpr uint32_t G16 = 148625052u;  // KoalaBear::two_adic_generator(4), order 16
+
+__device__ __forceinline__ uint32_t pow_canonical(uint32_t b, uint32_t e) {
+    uint64_t r = 1, x = b;
+    for (; e; e >>= 1) {
+        if (e & 1) r = r * x % P;
+        x = x * x % P;
+    }
+    return (uint32_t)r;
+}
+
+// MemoryAccessCols of a read record (value, shard, timestamp, prev_shard, prev_timestamp) at its timestamp
+__device__ __forceinline__ Access access_read(const uint32_t *r) {
+    Access a{};
+    a.on = true;
+    a.value = a.prev_value = r[0];
+    a.prev_shard = r[3];
+    a.prev_clk = r[4];
+    const bool cmp = r[3] == r[1];
+    a.compare = cmp;
+    const uint32_t d = (cmp ? r[2] : r[1]) - (cmp ? r[4] : r[3]) - 1u;
+    a.d16 = d & 0xFFFF;
+    a.d8 = (d >> 16) & 0xFF;
+    return a;
+}
+__device__ __forceinline__ Access access_write(const uint32_t *r) {  // MemoryWriteRecord
+    Access a{};
+    a.on = true;
+    a.value = r[0];
+    a.prev_value = r[3];
+    a.prev_shard = r[4];
+    a.prev_clk = r[5];
+    const bool cmp = r[4] == r[1];
+    a.compare = cmp;
+    const uint32_t d = (cmp ? r[2] : r[1]) - (cmp ? r[5] : r[4]) - 1u;
+    a.d16 = d & 0xFFFF;
+    a.d8 = (d >> 16) & 0xFF;
+    return a;
+}
+
+// FixedRotateRightOperation / FixedShiftRightOperation::populate: value, shift, carry (4 bytes each) at v,
+// ShrCarry lookups; returns the result word
+template <int ROT, bool ROTATE>
+__device__ __forceinline__ uint32_t shr_carry(uint32_t *v, uint32_t x, const Hist &h, bool on) {
+    constexpr int NB = ROT / 8, NBITS = ROT % 8;
+    constexpr uint32_t MULT = 1u << (8 - NBITS);
+    uint32_t rb[4], sh[4], ca[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        rb[i] = ROTATE ? byte_of(x, (i + NB) % 4) : (i + NB < 4 ? byte_of(x, i + NB) : 0u);
+        sh[i] = rb[i] >> NBITS;
+        ca[i] = rb[i] & ((1u << NBITS) - 1);
+        h.byte(B_SHRCARRY, rb[i], NBITS, on);
+    }
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t val = i < 3 ? sh[i] + ca[i + 1] * MULT : sh[3] + (ROTATE ? ca[0] * MULT : 0u);
+        v[i] = val;
+        v[4 + i] = sh[i];
+        v[8 + i] = ca[i];
+        w |= (val & 0xFF) << (8 * i);
+    }
+    return w;
+}
+__device__ __forceinline__ uint32_t xor_word(uint32_t *v, uint32_t a, uint32_t b, const Hist &h, bool on) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        v[i] = byte_of(a, i) ^ byte_of(b, i);
+        h.byte(B_XOR, byte_of(a, i), byte_of(b, i), on);
+    }
+    return a ^ b;
+}
+
+struct ShaExtendChip {
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t r, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_SHA_EXTEND_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        // populate_flags(i) (flags.rs:13-34), for every row
+        const uint32_t c16 = pow_canonical(G16, (uint32_t)((r + 1) % 16));
+        const uint32_t xs = c16 >= G16 ? c16 - G16 : P - (G16 - c16), xe = c16 >= 1 ? c16 - 1 : P - 1;
+        const uint32_t j = 16 + (uint32_t)(r % 48);
+        v[SE_I] = j;
+        v[SE_C16] = c16;
+        v[SE_C16S] = inv_canonical(xs);
+        v[SE_C16S + 1] = xs == 0;
+        v[SE_C16E] = inv_canonical(xe);
+        v[SE_C16E + 1] = xe == 0;
+        const uint32_t third = (j - 16) / 16;
+        v[SE_C48 + third] = 1;
+        v[SE_C48S] = (third == 0 && xs == 0 && real);
+        v[SE_C48E] = (third == 2 && xe == 0 && real);
+        Access acc[5] = {};
+        if (real) {
+            v[SE_SHARD] = e[0];
+            v[SE_CLK] = e[1];
+            v[SE_WPTR] = e[2];
+            const int bases[4] = {SE_W15, SE_W2, SE_W16, SE_W7};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                acc[k] = access_read(e + 3 + 5 * k);
+                put_access(v, bases[k], acc[k]);
+            }
+            acc[4] = access_write(e + 23);
+            put_word(v + SE_WI, acc[4].prev_value);
+            put_access(v, SE_WI + 4, acc[4]);
+        }
+        const uint32_t w15 = acc[0].value, w2 = acc[1].value, w16 = acc[2].value, w7 = acc[3].value;
+        const uint32_t rr7 = shr_carry<7, true>(v + SE_RR7, w15, h, real);
+        const uint32_t rr18 = shr_carry<18, true>(v + SE_RR18, w15, h, real);
+        const uint32_t rs3 = shr_carry<3, false>(v + SE_RS3, w15, h, real);
+        const uint32_t s0 = xor_word(v + SE_S0, xor_word(v + SE_S0I, rr7, rr18, h, real), rs3, h, real);
+        const uint32_t rr17 = shr_carry<17, true>(v + SE_RR17, w2, h, real);
+        const uint32_t rr19 = shr_carry<19, true>(v + SE_RR19, w2, h, real);
+        const uint32_t rs10 = shr_carry<10, false>(v + SE_RS10, w2, h, real);
+        const uint32_t s1 = xor_word(v + SE_S1, xor_word(v + SE_S1I, rr17, rr19, h, real), rs10, h, real);
+        // Add4Operation::populate(w[i-16], s0, w[i-7], s1): bytes, carries, one-hot carries, U8 range checks
+        const uint32_t ins[4] = {w16, s0, w7, s1};
+        uint32_t carry = 0, sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t t = carry;
+#pragma unroll
+            for (int k = 0; k < 4; k++) t += byte_of(ins[k], i);
+            carry = t >> 8;
+            sum |= (t & 0xFF) << (8 * i);
+            if (real) {
+                v[SE_S2 + i] = t & 0xFF;
+#pragma unroll
+                for (int k = 0; k < 4; k++) v[SE_S2 + 4 + 4 * k + i] = carry == (uint32_t)k;
+                v[SE_S2 + 20 + i] = carry;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            h.byte(B_U8RANGE, byte_of(ins[k], 0), byte_of(ins[k], 1), real);
+            h.byte(B_U8RANGE, byte_of(ins[k], 2), byte_of(ins[k], 3), real);
+        }
+        h.byte(B_U8RANGE, byte_of(sum, 0), byte_of(sum, 1), real);
+        h.byte(B_U8RANGE, byte_of(sum, 2), byte_of(sum, 3), real);
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            h.byte(B_U16RANGE, acc[k].d16 >> 8, acc[k].d16 & 0xFF, real);
+            h.byte(B_U8RANGE, 0, acc[k].d8, real);
+        }
+        if (real) v[SE_REAL] = 1;
+        else {  // padding rows keep only the flags
+#pragma unroll
+            for (int c = SE_W15; c < ZKM_SHA_EXTEND_WIDTH; c++) v[c] = 0;
+        }
+    }
+};
+
 // ------------------------------------------------------------------ MemoryLocal (include/memory_local.hpp:8-20)
 // one SingleMemoryLocal (14 columns) per event; a trace row holds four
 struct MemoryLocalChip {
@@ -1413,6 +1576,16 @@ int zkm_misc_instrs_events_to_trace(const zkm_misc_event *events, uint64_t n, ui
                                     uint32_t *byte_mult, void *stream) {
     return launch<15, 15, ZKM_MISC_INSTRS_WIDTH, true>(events, n, trace, height, MiscInstrsChip{}, stream,
                                                        "zkm_misc_instrs_events_to_trace", byte_mult);
+}
+
+int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, uint32_t *trace, uint64_t height,
+                                   uint32_t *byte_mult, void *stream) {
+    if (n % 48) {
+        g_last_error = "zkm_sha_extend_events_to_trace: the rows of whole calls (a multiple of 48) are needed";
+        return ZKM_ERR_ARG;
+    }
+    return launch<29, 29, ZKM_SHA_EXTEND_WIDTH, true>(rows, n, trace, height, ShaExtendChip{}, stream,
+                                                      "zkm_sha_extend_events_to_trace", byte_mult);
 }
 
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,

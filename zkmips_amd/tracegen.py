@@ -76,6 +76,11 @@ COMP_ALU_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode", 
 CPU_WIDTH, ADD_SUB_WIDTH, MEMORY_LOCAL_WIDTH, MEMORY_GLOBAL_WIDTH, SYSCALL_WIDTH = 67, 19, 56, 111, 6
 BRANCH_WIDTH, MEMORY_INSTRS_WIDTH, JUMP_WIDTH, MOVCOND_WIDTH, MUL_WIDTH = 62, 79, 66, 32, 58
 DIVREM_WIDTH, CLO_CLZ_WIDTH, SYSCALL_INSTRS_WIDTH, MISC_INSTRS_WIDTH = 106, 22, 64, 72
+# the flattened ShaExtendEvent row (zkm_tracegen.h): shard, clk, w_ptr, four MemoryReadRecords, a MemoryWriteRecord
+SHA_EXTEND_ROW = np.dtype({"names": ["shard", "clk", "w_ptr", "r15", "r2", "r16", "r7", "w"],
+                           "formats": [u4, u4, u4, (u4, 5), (u4, 5), (u4, 5), (u4, 5), (u4, 6)],
+                           "offsets": [0, 4, 8, 12, 32, 52, 72, 92], "itemsize": 116})
+SHA_EXTEND_WIDTH = 176
 # MiscEvent (events/instr.rs:236-260)
 MISC_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode", "a", "b", "c", "prev_a", "hi_record"],
                        "formats": [u4, u4, u4, u4, u1, u4, u4, u4, u4, (u4, 6)],
@@ -294,6 +299,32 @@ def misc_records(misc, shard: int) -> np.ndarray:
     return e
 
 
+def sha_extend_records(events) -> np.ndarray:
+    """The ShaExtend rows of the executor's SHA_EXTEND events (mips_syscall.exec_sha_extend), 48 per call."""
+    out = np.zeros(48 * len(events), SHA_EXTEND_ROW)
+    for k, ev in enumerate(events):
+        rows = out[48 * k:48 * (k + 1)]
+        ts = ev["clk"] + np.arange(48)
+        rows["shard"], rows["clk"], rows["w_ptr"] = ev["shard"], ev["clk"], ev["w_ptr"]
+        for key in ("r15", "r2", "r16", "r7"):
+            rd = np.asarray(ev[key], np.int64).reshape(48, 3)  # value, prev_shard, prev_clk
+            rows[key] = np.stack([rd[:, 0], np.full(48, ev["shard"]), ts, rd[:, 1], rd[:, 2]], 1)
+        wr = np.asarray(ev["wr"], np.int64).reshape(48, 4)  # prev_value, value, prev_shard, prev_clk
+        rows["w"] = np.stack([wr[:, 1], np.full(48, ev["shard"]), ts, wr[:, 0], wr[:, 2], wr[:, 3]], 1)
+        out[48 * k:48 * (k + 1)] = rows
+    return out
+
+
+def sha_extend_trace(rows_dev, n: int, height: int = None, byte_mult=None):
+    """ShaExtend main trace (height x 176 int32 on the GPU) from n flattened rows (n a multiple of 48)."""
+    height = height or max(16, 1 << max(2, (n - 1).bit_length()))
+    t = _trace(height, SHA_EXTEND_WIDTH)
+    what = "zkm_sha_extend_events_to_trace"
+    _lib.check(_bind().zkm_sha_extend_events_to_trace(_records(rows_dev, n, SHA_EXTEND_ROW, what), n, t.data_ptr(),
+                                                       height, _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
 def alu_records(alu, kind: str) -> np.ndarray:
     """The AluEvents of one ALU chip (kind "add", "bit", "lt", "sll" or "sr") from the executor's event
     lists; ShiftRight's include the SRL dependencies of the CLZ / CLO events."""
@@ -324,6 +355,7 @@ def _bind():
         L.zkm_clo_clz_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_syscall_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_misc_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_sha_extend_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -346,7 +378,7 @@ def to_device(records: np.ndarray):
     torch = _torch()
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
                              SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
-                             COMP_ALU_EVENT, MISC_EVENT):
+                             COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
