@@ -244,6 +244,21 @@ typedef struct {
 int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, uint32_t *trace, uint64_t height,
                                    uint32_t *byte_mult, void *stream);
 
+/* ShaCompress (syscall/precompiles/sha256/compress/trace.rs:32-305): ShaCompressEvent's records (its w is a
+ * Vec) as one fixed record per call: shard, clk, w_ptr, h_ptr, the 8 reads of h, the 64 reads of w, the 8
+ * writes of h.  80 rows per call (init, 64 rounds, finalize): the round state is expanded on the device, then
+ * every row gets its octet flags, access, state words, the Sigma rotations (ShrCarry), the ch / maj
+ * AND / XOR bytes, the Add5 of temp1, the adds of temp2, d + temp1, temp1 + temp2 and the finalize add. */
+typedef struct {
+    uint32_t shard, clk, w_ptr, h_ptr;
+    zkm_memory_read_record h_read_records[8];
+    zkm_memory_read_record w_i_read_records[64];
+    zkm_memory_write_record h_write_records[8];
+} zkm_sha_compress_event;  /* 1648 bytes */
+#define ZKM_SHA_COMPRESS_WIDTH 262
+int zkm_sha_compress_events_to_trace(const zkm_sha_compress_event *events, uint64_t n, uint32_t *trace,
+                                     uint64_t height, uint32_t *byte_mult, void *stream);
+
 /* MemoryLocal (memory/local.rs:144-185): event i fills entry i % 4 of row i / 4; height rows. */
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,
                                      uint64_t height, void *stream);

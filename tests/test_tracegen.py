@@ -44,6 +44,9 @@ LAYOUTS = {
     "zkm_sha_extend_row": (TG.SHA_EXTEND_ROW, {"shard": "shard", "clk": "clk", "w_ptr": "w_ptr", "r15": "w_i_minus_15",
                                                "r2": "w_i_minus_2", "r16": "w_i_minus_16", "r7": "w_i_minus_7",
                                                "w": "w_i"}),
+    "zkm_sha_compress_event": (TG.SHA_COMPRESS_EVENT, {"shard": "shard", "clk": "clk", "w_ptr": "w_ptr", "h_ptr": "h_ptr",
+                                                       "h_read": "h_read_records", "w_read": "w_i_read_records",
+                                                       "h_write": "h_write_records"}),
 }
 
 
@@ -400,5 +403,24 @@ def test_device_sha_extend_matches_host(calls):
     rows = TG.sha_extend_records(evs)
     bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
     dev = TG.sha_extend_trace(TG.to_device(rows), len(rows), height=len(host), byte_mult=bm)
+    assert np.array_equal(dev.cpu().numpy().view(np.uint32), host)
+    assert np.array_equal(bm.cpu().numpy().astype(np.uint64), mult)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("calls", [1, 2, 5])
+def test_device_sha_compress_matches_host(calls):
+    """ShaCompress rows (round state expanded on the device) == the host builder, Byte lookups included."""
+    import torch
+    prog = MC.sha_program(calls, seed=6)
+    state = MC.fresh_state()
+    MC.program_shard(prog, 1, 1, 1 << 14, state=state, regs=MC.initial_registers(1))
+    evs = [e for code, _, e in state["precompile"] if code == SY.SHA_COMPRESS]
+    assert len(evs) == calls
+    mult = np.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), np.uint64)
+    host = SY.sha_compress_trace(evs, A.byte_lookup_into(mult))
+    rec = TG.sha_compress_records(evs)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.sha_compress_trace(TG.to_device(rec), len(rec), height=len(host), byte_mult=bm)
     assert np.array_equal(dev.cpu().numpy().view(np.uint32), host)
     assert np.array_equal(bm.cpu().numpy().astype(np.uint64), mult)

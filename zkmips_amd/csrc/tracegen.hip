@@ -36,6 +36,7 @@ static_assert(sizeof(zkm_movcond_event) == 28, "MovCondEvent layout");
 static_assert(sizeof(zkm_comp_alu_event) == 64, "CompAluEvent layout");
 static_assert(sizeof(zkm_misc_event) == 60, "MiscEvent layout");
 static_assert(sizeof(zkm_sha_extend_row) == 116, "ShaExtend row record layout");
+static_assert(sizeof(zkm_sha_compress_event) == 1648, "ShaCompress call record layout");
 
 namespace zkm::tg {
 
@@ -1349,6 +1350,200 @@ struct ShaExtendChip {
     }
 };
 
+// ------------------------------------------------------------------ ShaCompress (sha256/compress/trace.rs:32-305)
+// 80 rows per call (8 reads of h, 64 rounds, 8 writes of h + the state).  The round state is sequential
+// within a call, so a first kernel (one thread per call) expands each call into 80 row records: shard,
+// clk, w_ptr, h_ptr, the row's memory access as a MemoryWriteRecord (reads: prev_value = value), the state
+// a..h the row shows, w[j] and h[j]; the row kernel then fills every column from its record.
+enum { SC2_SHARD = 0, SC2_CLK = 1, SC2_WPTR = 2, SC2_HPTR = 3, SC2_START = 4, SC2_OCTET = 5, SC2_OCTNUM = 13,
+       SC2_MEM = 23, SC2_ADDR = 36, SC2_A = 37, SC2_K = 69, SC2_ERR6 = 73, SC2_ERR11 = 85, SC2_ERR25 = 97,
+       SC2_S1I = 109, SC2_S1 = 113, SC2_EANDF = 117, SC2_ENOT = 121, SC2_ENOTG = 125, SC2_CH = 129, SC2_TEMP1 = 133,
+       SC2_ARR2 = 161, SC2_ARR13 = 173, SC2_ARR22 = 185, SC2_S0I = 197, SC2_S0 = 201, SC2_AANDB = 205,
+       SC2_AANDC = 209, SC2_BANDC = 213, SC2_MAJI = 217, SC2_MAJ = 221, SC2_TEMP2 = 225, SC2_DT1 = 232,
+       SC2_T1T2 = 239, SC2_FOP = 246, SC2_FADD = 250, SC2_INIT = 257, SC2_COMP = 258, SC2_FIN = 259, SC2_LAST = 260,
+       SC2_REAL = 261 };
+__constant__ uint32_t kShaK[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, 0xd807aa98,
+    0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
+    0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8,
+    0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13,
+    0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819,
+    0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a,
+    0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+    0xc67178f2};
+constexpr int SCR = 20;  // dwords of an expanded row record
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, int s) { return (x >> s) | (x << (32 - s)); }
+
+// zkm_sha_compress_event dwords: shard, clk, w_ptr, h_ptr, h reads (8 x 5), w reads (64 x 5), h writes (8 x 6)
+__global__ __launch_bounds__(64) void k_sha_compress_expand(const uint32_t *__restrict__ ev, uint64_t ncalls,
+                                                            uint32_t *__restrict__ rows) {
+    const uint64_t k = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (k >= ncalls) return;
+    const uint32_t *e = ev + k * 412;
+    const uint32_t *hr = e + 4, *wr = e + 44, *hw = e + 364;
+    uint32_t st[8], h0[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = h0[i] = hr[5 * i];
+    for (int p = 0; p < 80; p++) {
+        uint32_t *o = rows + (k * 80 + (uint64_t)p) * SCR;
+        o[0] = e[0];
+        o[1] = e[1];
+        o[2] = e[2];
+        o[3] = e[3];
+        uint32_t wj = 0, hj = 0;
+        if (p < 8) {  // init: read h[p] (prev_value = value)
+            const uint32_t *r = hr + 5 * p;
+            o[4] = r[0]; o[5] = r[1]; o[6] = r[2]; o[7] = r[0]; o[8] = r[3]; o[9] = r[4];
+        } else if (p < 72) {  // compression: read w[p - 8]
+            const uint32_t *r = wr + 5 * (p - 8);
+            o[4] = r[0]; o[5] = r[1]; o[6] = r[2]; o[7] = r[0]; o[8] = r[3]; o[9] = r[4];
+            wj = r[0];
+        } else {  // finalize: write h[p - 72]
+            const uint32_t *r = hw + 6 * (p - 72);
+#pragma unroll
+            for (int q = 0; q < 6; q++) o[4 + q] = r[q];
+            hj = h0[p - 72];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) o[10 + i] = st[i];
+        o[18] = wj;
+        o[19] = hj;
+        if (p >= 8 && p < 72) {  // the round (the row shows the state before it)
+            const uint32_t a = st[0], b = st[1], c = st[2], d = st[3], ee = st[4], f = st[5], g = st[6], hh = st[7];
+            const uint32_t s1 = rotr32(ee, 6) ^ rotr32(ee, 11) ^ rotr32(ee, 25), ch = (ee & f) ^ (~ee & g);
+            const uint32_t t1 = hh + s1 + ch + kShaK[p - 8] + wj;
+            const uint32_t s0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22), maj = (a & b) ^ (a & c) ^ (b & c);
+            const uint32_t t2 = s0 + maj;
+            st[7] = g; st[6] = f; st[5] = ee; st[4] = d + t1; st[3] = c; st[2] = b; st[1] = a; st[0] = t1 + t2;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t and_word(uint32_t *v, uint32_t a, uint32_t b, const Hist &h, bool on) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        v[i] = byte_of(a, i) & byte_of(b, i);
+        h.byte(B_AND, byte_of(a, i), byte_of(b, i), on);
+    }
+    return a & b;
+}
+// AddOperation::populate: value bytes, 3 carries, U8 range checks of a, b and the sum
+__device__ __forceinline__ uint32_t add_word(uint32_t *v, uint32_t a, uint32_t b, const Hist &h, bool on) {
+    const uint32_t sum = a + b;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        v[i] = byte_of(sum, i);
+        if (i < 3) {
+            c = (byte_of(a, i) + byte_of(b, i) + c) >> 8;
+            v[4 + i] = c;
+        }
+    }
+    const uint32_t w3[3] = {a, b, sum};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        h.byte(B_U8RANGE, byte_of(w3[k], 0), byte_of(w3[k], 1), on);
+        h.byte(B_U8RANGE, byte_of(w3[k], 2), byte_of(w3[k], 3), on);
+    }
+    return sum;
+}
+
+struct ShaCompressChip {
+    uint64_t n;  // real rows (80 per call)
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t r, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_SHA_COMPRESS_WIDTH; c++) v[c] = 0;
+        const bool real = e != nullptr;
+        const uint32_t pos = (uint32_t)(r < n ? r % 80 : (r - n) % 80), oc = pos % 8, on = pos / 8;
+        v[SC2_OCTET + oc] = 1;
+        v[SC2_OCTNUM + on] = 1;
+        const bool compr = on >= 1 && on <= 8;
+        if (compr) put_word(v + SC2_K, kShaK[(on - 1) * 8 + oc]);
+        v[SC2_LAST] = oc == 7 && on == 9;
+        Access acc{};
+        if (real) {
+            v[SC2_REAL] = 1;
+            v[SC2_INIT] = on == 0;
+            v[SC2_COMP] = compr;
+            v[SC2_FIN] = on == 9;
+            v[SC2_START] = on == 0 && oc == 0;
+            v[SC2_SHARD] = e[0];
+            v[SC2_CLK] = e[1];
+            v[SC2_WPTR] = e[2];
+            v[SC2_HPTR] = e[3];
+            acc = access_write(e + 4);
+            put_word(v + SC2_MEM, acc.prev_value);
+            put_access(v, SC2_MEM + 4, acc);
+            v[SC2_ADDR] = pos < 8 ? e[3] + 4 * pos : pos < 72 ? e[2] + 4 * (pos - 8) : e[3] + 4 * (pos - 72);
+#pragma unroll
+            for (int i = 0; i < 8; i++) put_word(v + SC2_A + 4 * i, e[10 + i]);
+        }
+        h.byte(B_U16RANGE, acc.d16 >> 8, acc.d16 & 0xFF, real);
+        h.byte(B_U8RANGE, 0, acc.d8, real);
+        const bool cr = real && compr;
+        uint32_t st[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) st[i] = real ? e[10 + i] : 0u;
+        const uint32_t a = st[0], b = st[1], c = st[2], d = st[3], ee = st[4], f = st[5], g = st[6], hh = st[7];
+        uint32_t tmp[12];
+        const uint32_t e6 = shr_carry<6, true>(cr ? v + SC2_ERR6 : tmp, ee, h, cr);
+        const uint32_t e11 = shr_carry<11, true>(cr ? v + SC2_ERR11 : tmp, ee, h, cr);
+        const uint32_t e25 = shr_carry<25, true>(cr ? v + SC2_ERR25 : tmp, ee, h, cr);
+        const uint32_t s1i = xor_word(cr ? v + SC2_S1I : tmp, e6, e11, h, cr);
+        const uint32_t s1 = xor_word(cr ? v + SC2_S1 : tmp, s1i, e25, h, cr);
+        const uint32_t eandf = and_word(cr ? v + SC2_EANDF : tmp, ee, f, h, cr);
+        const uint32_t enot = ~ee;
+        if (cr) put_word(v + SC2_ENOT, enot);
+        h.byte(B_U8RANGE, byte_of(ee, 0), byte_of(ee, 1), cr);
+        h.byte(B_U8RANGE, byte_of(ee, 2), byte_of(ee, 3), cr);
+        const uint32_t enotg = and_word(cr ? v + SC2_ENOTG : tmp, enot, g, h, cr);
+        const uint32_t ch = xor_word(cr ? v + SC2_CH : tmp, eandf, enotg, h, cr);
+        // Add5Operation (h, s1, ch, k, w): bytes, one-hot carries (5 x 4), carries, U8 range checks
+        const uint32_t kj = compr ? kShaK[(on - 1) * 8 + oc] : 0u, wj = real ? e[18] : 0u;
+        const uint32_t ins[5] = {hh, s1, ch, kj, wj};
+        uint32_t carry = 0, t1 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t t = carry;
+#pragma unroll
+            for (int k = 0; k < 5; k++) t += byte_of(ins[k], i);
+            carry = t >> 8;
+            t1 |= (t & 0xFF) << (8 * i);
+            if (cr) {
+                v[SC2_TEMP1 + i] = t & 0xFF;
+#pragma unroll
+                for (int k = 0; k < 5; k++) v[SC2_TEMP1 + 4 + 4 * k + i] = carry == (uint32_t)k;
+                v[SC2_TEMP1 + 24 + i] = carry;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            h.byte(B_U8RANGE, byte_of(ins[k], 0), byte_of(ins[k], 1), cr);
+            h.byte(B_U8RANGE, byte_of(ins[k], 2), byte_of(ins[k], 3), cr);
+        }
+        h.byte(B_U8RANGE, byte_of(t1, 0), byte_of(t1, 1), cr);
+        h.byte(B_U8RANGE, byte_of(t1, 2), byte_of(t1, 3), cr);
+        const uint32_t a2 = shr_carry<2, true>(cr ? v + SC2_ARR2 : tmp, a, h, cr);
+        const uint32_t a13 = shr_carry<13, true>(cr ? v + SC2_ARR13 : tmp, a, h, cr);
+        const uint32_t a22 = shr_carry<22, true>(cr ? v + SC2_ARR22 : tmp, a, h, cr);
+        const uint32_t s0i = xor_word(cr ? v + SC2_S0I : tmp, a2, a13, h, cr);
+        const uint32_t s0 = xor_word(cr ? v + SC2_S0 : tmp, s0i, a22, h, cr);
+        const uint32_t ab = and_word(cr ? v + SC2_AANDB : tmp, a, b, h, cr);
+        const uint32_t ac = and_word(cr ? v + SC2_AANDC : tmp, a, c, h, cr);
+        const uint32_t bc = and_word(cr ? v + SC2_BANDC : tmp, b, c, h, cr);
+        const uint32_t maji = xor_word(cr ? v + SC2_MAJI : tmp, ab, ac, h, cr);
+        const uint32_t maj = xor_word(cr ? v + SC2_MAJ : tmp, maji, bc, h, cr);
+        const uint32_t t2 = add_word(cr ? v + SC2_TEMP2 : tmp, s0, maj, h, cr);
+        add_word(cr ? v + SC2_DT1 : tmp, d, t1, h, cr);
+        add_word(cr ? v + SC2_T1T2 : tmp, t1, t2, h, cr);
+        // finalize rows: the final state word j and h[j] + it
+        const bool fr = real && on == 9;
+        const uint32_t opnd = st[oc];
+        if (fr) put_word(v + SC2_FOP, opnd);
+        add_word(fr ? v + SC2_FADD : tmp, real ? e[19] : 0u, opnd, h, fr);
+    }
+};
+
 // ------------------------------------------------------------------ MemoryLocal (include/memory_local.hpp:8-20)
 // one SingleMemoryLocal (14 columns) per event; a trace row holds four
 struct MemoryLocalChip {
@@ -1586,6 +1781,29 @@ int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, u
     }
     return launch<29, 29, ZKM_SHA_EXTEND_WIDTH, true>(rows, n, trace, height, ShaExtendChip{}, stream,
                                                       "zkm_sha_extend_events_to_trace", byte_mult);
+}
+
+int zkm_sha_compress_events_to_trace(const zkm_sha_compress_event *events, uint64_t n, uint32_t *trace,
+                                     uint64_t height, uint32_t *byte_mult, void *stream) {
+    const uint64_t nrows = 80 * n;
+    if (!trace || (n && !events) || nrows > height || height < 16 || (height & (height - 1))) {
+        g_last_error = "zkm_sha_compress_events_to_trace: bad arguments (need 80 n <= height, a power of two >= 16)";
+        return ZKM_ERR_ARG;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t *rows = nullptr;
+    if (n) {
+        if (hipMallocAsync((void **)&rows, nrows * SCR * 4, s) != hipSuccess) {
+            g_last_error = "zkm_sha_compress_events_to_trace: out of device memory";
+            return ZKM_ERR_HIP;
+        }
+        hipLaunchKernelGGL(k_sha_compress_expand, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s,
+                           (const uint32_t *)events, n, rows);
+    }
+    const int rc = launch<SCR, SCR, ZKM_SHA_COMPRESS_WIDTH, true>(rows, nrows, trace, height, ShaCompressChip{nrows},
+                                                                  stream, "zkm_sha_compress_events_to_trace", byte_mult);
+    if (rows) (void)hipFreeAsync(rows, s);  // stream-ordered: after the row kernel
+    return rc;
 }
 
 int zkm_memory_local_events_to_trace(const zkm_memory_local_event *events, uint64_t n, uint32_t *trace,

@@ -81,6 +81,11 @@ SHA_EXTEND_ROW = np.dtype({"names": ["shard", "clk", "w_ptr", "r15", "r2", "r16"
                            "formats": [u4, u4, u4, (u4, 5), (u4, 5), (u4, 5), (u4, 5), (u4, 6)],
                            "offsets": [0, 4, 8, 12, 32, 52, 72, 92], "itemsize": 116})
 SHA_EXTEND_WIDTH = 176
+# the ShaCompress call record (zkm_tracegen.h): shard, clk, w_ptr, h_ptr, 8 h reads, 64 w reads, 8 h writes
+SHA_COMPRESS_EVENT = np.dtype({"names": ["shard", "clk", "w_ptr", "h_ptr", "h_read", "w_read", "h_write"],
+                               "formats": [u4, u4, u4, u4, (u4, (8, 5)), (u4, (64, 5)), (u4, (8, 6))],
+                               "offsets": [0, 4, 8, 12, 16, 176, 1456], "itemsize": 1648})
+SHA_COMPRESS_WIDTH = 262
 # MiscEvent (events/instr.rs:236-260)
 MISC_EVENT = np.dtype({"names": ["shard", "clk", "pc", "next_pc", "opcode", "a", "b", "c", "prev_a", "hi_record"],
                        "formats": [u4, u4, u4, u4, u1, u4, u4, u4, u4, (u4, 6)],
@@ -325,6 +330,33 @@ def sha_extend_trace(rows_dev, n: int, height: int = None, byte_mult=None):
     return t
 
 
+def sha_compress_records(events) -> np.ndarray:
+    """ShaCompress call records of the executor's SHA_COMPRESS events (mips_syscall.exec_sha_compress): h and
+    w read at clk, h written at clk + 1."""
+    out = np.zeros(len(events), SHA_COMPRESS_EVENT)
+    for k, ev in enumerate(events):
+        sh, clk = ev["shard"], ev["clk"]
+        hr = np.asarray(ev["hr"], np.int64).reshape(8, 3)
+        wr = np.asarray(ev["wr"], np.int64).reshape(64, 3)
+        hw = np.asarray(ev["hw"], np.int64).reshape(8, 4)  # prev_value, value, prev_shard, prev_clk
+        out[k]["shard"], out[k]["clk"], out[k]["w_ptr"], out[k]["h_ptr"] = sh, clk, ev["w_ptr"], ev["h_ptr"]
+        out[k]["h_read"] = np.stack([hr[:, 0], np.full(8, sh), np.full(8, clk), hr[:, 1], hr[:, 2]], 1)
+        out[k]["w_read"] = np.stack([wr[:, 0], np.full(64, sh), np.full(64, clk), wr[:, 1], wr[:, 2]], 1)
+        out[k]["h_write"] = np.stack([hw[:, 1], np.full(8, sh), np.full(8, clk + 1), hw[:, 0], hw[:, 2], hw[:, 3]], 1)
+    return out
+
+
+def sha_compress_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    """ShaCompress main trace (height x 262 int32 on the GPU) from n call records (80 rows each)."""
+    height = height or _pow2(80 * n)
+    t = _trace(height, SHA_COMPRESS_WIDTH)
+    what = "zkm_sha_compress_events_to_trace"
+    _lib.check(_bind().zkm_sha_compress_events_to_trace(_records(events_dev, n, SHA_COMPRESS_EVENT, what), n,
+                                                         t.data_ptr(), height, _words(byte_mult, 65536 * 10, what),
+                                                         _stream()), what)
+    return t
+
+
 def alu_records(alu, kind: str) -> np.ndarray:
     """The AluEvents of one ALU chip (kind "add", "bit", "lt", "sll" or "sr") from the executor's event
     lists; ShiftRight's include the SRL dependencies of the CLZ / CLO events."""
@@ -356,6 +388,7 @@ def _bind():
         L.zkm_syscall_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_misc_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_sha_extend_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_sha_compress_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -378,7 +411,7 @@ def to_device(records: np.ndarray):
     torch = _torch()
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
                              SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
-                             COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW):
+                             COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
