@@ -424,3 +424,44 @@ def test_device_sha_compress_matches_host(calls):
     dev = TG.sha_compress_trace(TG.to_device(rec), len(rec), height=len(host), byte_mult=bm)
     assert np.array_equal(dev.cpu().numpy().view(np.uint32), host)
     assert np.array_equal(bm.cpu().numpy().astype(np.uint64), mult)
+
+
+@pytest.mark.gpu
+def test_sha_precompile_shards_from_device_traces_prove_identically():
+    """The SHA_EXTEND and SHA_COMPRESS precompile shards of a sha2 guest, every main trace and Byte lookup
+    generated on the device (precompile chip, SyscallPrecompile, MemoryLocal, Global), prove to the host
+    traces' bytes."""
+    import torch
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    prog = MC.sha_program(3, seed=2)
+    run = MC.program_shards(prog, seed=2, shard_size=1 << 12, precompile_events_per_shard=2)
+    state = MC.fresh_state()
+    regs = MC.initial_registers(2)
+    while MC.PC_BASE <= state["pc"] < MC.PC_BASE + 4 * len(prog) and state["exit_code"] is None:
+        MC.program_shard(prog, 2, 1, 1 << 12, state=state, regs=regs)
+    by_code = {}
+    for ev in state["precompile"]:
+        by_code.setdefault(ev[0], []).append(ev)
+    m, prep, _, _ = run[0]
+    prep = {k: v for k, v in prep.items() if v is not None}
+    prover = HipProver(Device(0), m, prep, num_queries=16)
+    checked = 0
+    for code in (SY.SHA_EXTEND, SY.SHA_COMPRESS):
+        chip = "ShaExtend" if code == SY.SHA_EXTEND else "ShaCompress"
+        shards = [r for r in run if chip in r[2]]
+        evs = by_code[code]
+        for k, (_, _, tr, pv) in enumerate(shards):
+            bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+            dev = TG.precompile_shard_traces(code, evs[2 * k:2 * k + 2], byte_mult=bm)
+            torch.cuda.synchronize()
+            for name, t in dev.items():
+                assert np.array_equal(t.cpu().numpy().view(np.uint32), tr[name]), name
+            assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+            traces = {k_: v for k_, v in tr.items() if k_ not in dev}
+            assert set(traces) <= {"Byte", "Program"}, sorted(traces)
+            traces.update(dev)
+            traces["Byte"] = bm
+            assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+            checked += 1
+    assert checked >= 2

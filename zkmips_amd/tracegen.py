@@ -698,3 +698,35 @@ def exp_reverse_bits_trace(base_dev, bits_dev, offsets_dev, n: int, height: int,
                                                             n, 1 if montgomery else 0, t.data_ptr(), height, _stream()),
                what)
     return t
+
+
+def precompile_shard_traces(code: int, events, byte_mult=None):
+    """Device traces of a SHA precompile shard (mips_core.precompile_shard's chips for SHA_EXTEND /
+    SHA_COMPRESS): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
+    lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
+    from . import mips_memory as MM
+    from . import mips_syscall as SY
+    pevs = [e for _, _, e in events]
+    sev = np.asarray([s_ for _, s_, _ in events], np.int64).reshape(-1, 5)  # shard, clk, id, arg1, arg2
+    out = {}
+    if code == SY.SHA_EXTEND:
+        rows = sha_extend_records(pevs)
+        out["ShaExtend"] = sha_extend_trace(to_device(rows), len(rows), byte_mult=byte_mult)
+    elif code == SY.SHA_COMPRESS:
+        rec = sha_compress_records(pevs)
+        out["ShaCompress"] = sha_compress_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    else:
+        raise ValueError(f"no device trace for precompile {code:#x}")
+    sc = np.zeros(len(sev), SYSCALL_EVENT)
+    sc["shard"], sc["clk"], sc["syscall_id"], sc["arg1"], sc["arg2"] = (sev[:, j] for j in range(5))
+    out["SyscallPrecompile"] = syscall_trace(to_device(sc), len(sc))
+    ent = np.asarray([x for e in pevs for x in e["local"]], np.int64).reshape(-1, 7)
+    ml = memory_local_events(ent)
+    out["MemoryLocal"] = memory_local_trace(to_device(ml), len(ml))
+    gmsg, grec = MM.memory_local_global_events(ent)
+    smsg = SY.syscall_global_messages(sev)
+    ge = global_events(np.concatenate([smsg, gmsg]), np.concatenate([np.ones(len(smsg), np.uint8), grec]),
+                       np.concatenate([np.full(len(smsg), SY.KIND_SYSCALL), np.full(len(gmsg), MC.KIND_MEMORY)]))
+    out["Global"], _ = global_trace(to_device(ge), len(ge), byte_mult=byte_mult)
+    return out
