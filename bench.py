@@ -590,6 +590,20 @@ def tracegen_bench(args):
     d_mi = TG.to_device(tile(TG.mem_instr_records(cap["mevs"], 1))[:n >> 2])
     chips["MemoryInstrs"] = (lambda: TG.memory_instrs_trace(d_mi, n >> 2, height=n >> 2, byte_mult=bm),
                              84 + 4 * TG.MEMORY_INSTRS_WIDTH, n >> 2)
+    # the SHA precompile chips at a 2^20-row precompile shard (config 3): a sha2 guest's calls tiled
+    from zkmips_amd import mips_syscall as SY
+    st = MC.fresh_state()
+    MC.program_shard(MC.sha_program(4, seed=5), 5, 1, 1 << 14, state=st, regs=MC.initial_registers(5))
+    ext = [e for code, _, e in st["precompile"] if code == SY.SHA_EXTEND]
+    cmp_ = [e for code, _, e in st["precompile"] if code == SY.SHA_COMPRESS]
+    n_ext, n_cmp = (n >> 2) // 48, (n >> 2) // 80
+    se_rows = TG.sha_extend_records(ext)
+    d_se = TG.to_device(se_rows[np.arange(48 * n_ext) % len(se_rows)])
+    d_sc = TG.to_device(TG.sha_compress_records(cmp_)[np.arange(n_cmp) % len(cmp_)])
+    chips["ShaExtend"] = (lambda: TG.sha_extend_trace(d_se, 48 * n_ext, height=n >> 2, byte_mult=bm),
+                          116 + 4 * TG.SHA_EXTEND_WIDTH, 48 * n_ext)
+    chips["ShaCompress"] = (lambda: TG.sha_compress_trace(d_sc, n_cmp, height=n >> 2, byte_mult=bm),
+                            1648 / 80 + 4 * TG.SHA_COMPRESS_WIDTH, 80 * n_cmp)
     res = {}
     for name, spec in chips.items():
         fn, bytes_per_row = spec[0], spec[1]
