@@ -1198,15 +1198,6 @@ enum { SE_SHARD = 0, SE_CLK = 1, SE_WPTR = 2, SE_I = 3, SE_C16 = 4, SE_C16S = 5,
        SE_WI = 162, SE_REAL = 175 };
 constexpr uint32_t G16 = 148625052u;  // KoalaBear::two_adic_generator(4), order 16
 
-__device__ __forceinline__ uint32_t pow_canonical(uint32_t b, uint32_t e) {
-    uint64_t r = 1, x = b;
-    for (; e; e >>= 1) {
-        if (e & 1) r = r * x % P;
-        x = x * x % P;
-    }
-    return (uint32_t)r;
-}
-
 // MemoryAccessCols of a read record (value, shard, timestamp, prev_shard, prev_timestamp) at its timestamp
 __device__ __forceinline__ Access access_read(const uint32_t *r) {
     Access a{};
@@ -1271,24 +1262,28 @@ __device__ __forceinline__ uint32_t xor_word(uint32_t *v, uint32_t a, uint32_t b
 }
 
 struct ShaExtendChip {
+    // the 16-cycle flag values by (row + 1) mod 16: g^k and the inverses of g^k - g and g^k - 1 (0 for 0),
+    // computed once on the host (16 distinct values: no per-row field inversion)
+    uint32_t c16[16], inv_s[16], inv_e[16];
     __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t r, const Hist &h) const {
 #pragma unroll
         for (int c = 0; c < ZKM_SHA_EXTEND_WIDTH; c++) v[c] = 0;
         const bool real = e != nullptr;
         // populate_flags(i) (flags.rs:13-34), for every row
-        const uint32_t c16 = pow_canonical(G16, (uint32_t)((r + 1) % 16));
-        const uint32_t xs = c16 >= G16 ? c16 - G16 : P - (G16 - c16), xe = c16 >= 1 ? c16 - 1 : P - 1;
+        const uint32_t k16 = (uint32_t)((r + 1) % 16);
+        const uint32_t c16v = c16[k16];
         const uint32_t j = 16 + (uint32_t)(r % 48);
+        const bool xs0 = k16 == 1, xe0 = k16 == 0;  // g^k = g, g^k = 1
         v[SE_I] = j;
-        v[SE_C16] = c16;
-        v[SE_C16S] = inv_canonical(xs);
-        v[SE_C16S + 1] = xs == 0;
-        v[SE_C16E] = inv_canonical(xe);
-        v[SE_C16E + 1] = xe == 0;
+        v[SE_C16] = c16v;
+        v[SE_C16S] = inv_s[k16];
+        v[SE_C16S + 1] = xs0;
+        v[SE_C16E] = inv_e[k16];
+        v[SE_C16E + 1] = xe0;
         const uint32_t third = (j - 16) / 16;
         v[SE_C48 + third] = 1;
-        v[SE_C48S] = (third == 0 && xs == 0 && real);
-        v[SE_C48E] = (third == 2 && xe == 0 && real);
+        v[SE_C48S] = (third == 0 && xs0 && real);
+        v[SE_C48E] = (third == 2 && xe0 && real);
         Access acc[5] = {};
         if (real) {
             v[SE_SHARD] = e[0];
@@ -1670,6 +1665,8 @@ uint32_t inv_mod_p(uint32_t x) {
     return (uint32_t)r;
 }
 
+uint32_t inv_or_zero(uint32_t x) { return x ? inv_mod_p(x) : 0u; }
+
 }  // namespace zkm::tg
 
 using namespace zkm::tg;
@@ -1779,7 +1776,14 @@ int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, u
         g_last_error = "zkm_sha_extend_events_to_trace: the rows of whole calls (a multiple of 48) are needed";
         return ZKM_ERR_ARG;
     }
-    return launch<29, 29, ZKM_SHA_EXTEND_WIDTH, true>(rows, n, trace, height, ShaExtendChip{}, stream,
+    ShaExtendChip chip{};
+    uint64_t gk = 1;
+    for (int k = 0; k < 16; k++, gk = gk * G16 % P) {
+        chip.c16[k] = (uint32_t)gk;
+        chip.inv_s[k] = inv_or_zero((uint32_t)((gk + P - G16) % P));
+        chip.inv_e[k] = inv_or_zero((uint32_t)((gk + P - 1) % P));
+    }
+    return launch<29, 29, ZKM_SHA_EXTEND_WIDTH, true>(rows, n, trace, height, chip, stream,
                                                       "zkm_sha_extend_events_to_trace", byte_mult);
 }
 
