@@ -16,6 +16,7 @@
 
 #include "../../include/zkm_hip.h"
 #include "../../include/zkm_tracegen.h"
+#include "kb31.cuh"
 
 namespace zkm {
 extern thread_local std::string g_last_error;
@@ -401,14 +402,10 @@ struct BitwiseChip {
     }
 };
 
-// (x mod p)^-1 of a canonical x (0 -> 0), by Fermat
+// (x mod p)^-1 of a canonical x (0 -> 0), by Fermat in Montgomery form (32-bit products, no 64-bit
+// modulo)
 __device__ __forceinline__ uint32_t inv_canonical(uint32_t x) {
-    uint64_t r = 1, b = x;
-    for (uint32_t e = P - 2; e; e >>= 1) {
-        if (e & 1) r = r * b % P;
-        b = b * b % P;
-    }
-    return x ? (uint32_t)r : 0u;
+    return x ? kb::from_mont(kb::inv(kb::to_mont(x))) : 0u;
 }
 
 enum { LT_PC = 0, LT_NPC = 1, LT_SLT = 2, LT_SLTU = 3, LT_A = 4, LT_B = 8, LT_C = 12, LT_FLAGS = 16, LT_BM = 20,
