@@ -134,6 +134,8 @@ struct Tile {
     static constexpr int WORDS = NTH * (EP > RP ? EP : RP);
 };
 
+constexpr int WIDE_ROW = 128;  // rows wider than this are built in LDS, not registers
+
 template <int EVS, int EVW, int W, bool HIST, class Chip>
 __global__ __launch_bounds__(NTH) void k_events_to_rows(const uint32_t *__restrict__ ev, uint64_t n,
                                                         uint32_t *__restrict__ out, uint64_t nrows, Chip chip,
@@ -168,12 +170,24 @@ __global__ __launch_bounds__(NTH) void k_events_to_rows(const uint32_t *__restri
             }
         }
         __syncthreads();
-        uint32_t v[W];
-        chip.row(v, t < nev ? buf + t * T::EP : nullptr, row0 + t, hist);
-        __syncthreads();
-        if (t < rows) {
+        if constexpr (W > WIDE_ROW) {
+            // wide rows (ShaExtend 176, ShaCompress 262 columns) would not fit in registers: the thread takes
+            // its event into registers, then the chip writes the row straight into the LDS tile
+            uint32_t ev[EVW];
+            if (t < nev) {
 #pragma unroll
-            for (int c = 0; c < W; c++) buf[t * T::RP + c] = v[c];
+                for (int k = 0; k < EVW; k++) ev[k] = buf[t * T::EP + k];
+            }
+            __syncthreads();
+            chip.row(buf + t * T::RP, t < nev ? ev : nullptr, row0 + t, hist);
+        } else {
+            uint32_t v[W];
+            chip.row(v, t < nev ? buf + t * T::EP : nullptr, row0 + t, hist);
+            __syncthreads();
+            if (t < rows) {
+#pragma unroll
+                for (int c = 0; c < W; c++) buf[t * T::RP + c] = v[c];
+            }
         }
         __syncthreads();
         uint32_t *dst = out + row0 * W;
