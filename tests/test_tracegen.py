@@ -465,3 +465,28 @@ def test_sha_precompile_shards_from_device_traces_prove_identically():
             assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
             checked += 1
     assert checked >= 2
+
+
+@pytest.mark.gpu
+def test_maxshape_shard_from_device_traces():
+    """The reference's maximal 2^22 shard shape (scaled to Cpu 2^16): every chip's trace built on the device
+    at the shape's height from the executor's records equals the host trace padded to the shape, the Byte
+    multiplicities equal, and the proof bytes are identical."""
+    import torch
+    from zkmips_amd import shapes as SH
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    cap = {}
+    m, prep, tr, pv = SH.shape_shard(SH.MAXIMAL_22, seed=3, down=6, capture=cap)
+    heights = {k: len(v) for k, v in tr.items() if k not in ("Byte", "Program")}
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.shard_traces(cap, byte_mult=bm, heights=heights)
+    torch.cuda.synchronize()
+    for name, t in dev.items():
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), tr[name]), name
+    assert set(dev) >= set(heights), sorted(set(heights) - set(dev))
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = dict(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, {k: v for k, v in prep.items() if v is not None}, num_queries=16)
+    assert prover.prove_shard({k: v for k, v in traces.items() if k in tr}, pv) == prover.prove_shard(tr, pv)

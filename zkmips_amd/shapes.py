@@ -122,13 +122,13 @@ def pad_to_shape(machine, traces: dict, shape: dict) -> dict:
     return out
 
 
-def shape_shard(shape: dict, seed: int = 1, down: int = 0, fill: float = 0.8):
+def shape_shard(shape: dict, seed: int = 1, down: int = 0, fill: float = 0.8, capture: dict = None):
     """(machine, prep_traces, traces, public_values) of one CPU shard padded to `shape` scaled down by
     2^down.  The execution halts in the shard (HALT), so its MemoryLocal/Global close the shard's
-    accesses like any continuation shard."""
+    accesses like any continuation shard.  `capture` receives the executor's records (program_shard)."""
     sh = scaled(shape, down)
     prog = shape_program(sh, seed, fill=fill)
-    m, prep, traces, pvs = C.program_shard(prog, seed, 1, (1 << 24) // 5 - 1)
+    m, prep, traces, pvs = C.program_shard(prog, seed, 1, (1 << 24) // 5 - 1, capture=capture)
     for name, t in traces.items():
         if name not in sh and name not in ("Program", "Byte"):
             raise ValueError(f"{name} ({len(t)} rows) is not in the shape")

@@ -610,62 +610,84 @@ def global_trace(events_dev, n: int, height: int = None, byte_mult=None):
     return t, fin.cpu().numpy().view(np.uint32)
 
 
-def shard_traces(capture: dict, byte_mult=None):
+def shard_records(capture: dict) -> dict:
+    """The event records of one executed shard (program_shard(..., capture=c)) by chip, as the header's
+    structs (numpy): what a host hands the device before its traces are built."""
+    shard = capture["shard"]
+    r = {"Cpu": cpu_events(capture["steps"], shard), "Program": program_ffi(capture["prog"]),
+         "AddSub": add_sub_records(capture["alu"])}
+    for kind, (_, chip, _) in ALU_CHIPS.items():
+        r[chip] = alu_records(capture["alu"], kind)
+    r["CloClz"] = alu_records(capture["alu"], "clz")
+    r["Branch"] = branch_records(capture.get("branches", []))
+    r["MemoryInstrs"] = mem_instr_records(capture.get("mevs", []), shard)
+    r["Jump"] = jump_records(capture.get("jumps", []))
+    r["MovCond"] = movcond_records(capture.get("movs", []))
+    r["Mul"] = mul_records(capture.get("muls", []), shard)
+    r["DivRem"] = divrem_records(capture.get("divs", []), shard)
+    r["MiscInstrs"] = misc_records(capture.get("misc", []), shard)
+    r["MemoryLocal"] = memory_local_events(capture["entries"])
+    r["SyscallCore"] = syscall_events(capture["core_syscalls"]) if len(capture["core_syscalls"]) else \
+        np.zeros(0, SYSCALL_EVENT)
+    r["SyscallInstrs"] = syscall_events(capture["syscalls"]) if len(capture["syscalls"]) else np.zeros(0, SYSCALL_EVENT)
+    r["Global"] = shard_global_events(capture)
+    return r
+
+
+def shard_traces(capture: dict, byte_mult=None, heights: dict = None, records: dict = None):
     """Device traces of one executed shard (program_shard(..., capture=c)): the chips of the reference's
     row ABI — Cpu (+ Program multiplicities), AddSub, MemoryLocal, SyscallCore — and beyond it Bitwise,
-    Lt, ShiftLeft, ShiftRight, CloClz, Branch, MemoryInstrs, Jump, MovCond, Mul, DivRem, MiscInstrs, SyscallInstrs and the Global chip (septic-curve
-    lift and running sum), with their Byte lookups
-    added into `byte_mult` (65536 x 10 int32 on the GPU) if given.  Returns {chip name: GPU tensor}."""
+    Lt, ShiftLeft, ShiftRight, CloClz, Branch, MemoryInstrs, Jump, MovCond, Mul, DivRem, MiscInstrs,
+    SyscallInstrs and the Global chip (septic-curve lift and running sum), with their Byte lookups added
+    into `byte_mult` (65536 x 10 int32 on the GPU) if given.  heights: chip -> trace height (e.g. a
+    reference shard shape; default the next power of two); records: the shard_records already on the GPU
+    (uploaded here otherwise).  Chips with no events are left out unless heights names them.  Returns
+    {chip name: GPU tensor}."""
     torch = _torch()
-    shard, prog = capture["shard"], capture["prog"]
-    ev = cpu_events(capture["steps"], shard)
-    pf = program_ffi(prog)
-    pm = torch.zeros((_pow2(len(pf)), 1), dtype=torch.int32, device="cuda")
-    out = {"Cpu": cpu_trace(to_device(ev), len(ev), shard, to_device(pf), len(pf), byte_mult=byte_mult,
-                            program_mult=pm),
+    heights = heights or {}
+    host = shard_records(capture) if records is None else None
+    nrec = {k: len(v) for k, v in (host or {}).items()}
+    if records is None:
+        records = {k: to_device(v) for k, v in host.items()}
+    else:
+        nrec = records.get("_n", nrec)
+    n = lambda k: nrec[k] if nrec else 0
+    h = lambda k, default: heights.get(k, default)
+    want = lambda k: n(k) > 0 or k in heights
+    shard = capture["shard"]
+    npf = n("Program")
+    pm = torch.zeros((h("Program", _pow2(npf)), 1), dtype=torch.int32, device="cuda")
+    out = {"Cpu": cpu_trace(records["Cpu"], n("Cpu"), shard, records["Program"], npf, height=h("Cpu", None),
+                            byte_mult=byte_mult, program_mult=pm),
            "Program": pm}
-    adds = add_sub_records(capture["alu"])
-    if len(adds):
-        out["AddSub"] = add_sub_trace(to_device(adds), len(adds), byte_mult=byte_mult)
+    if want("AddSub"):
+        out["AddSub"] = add_sub_trace(records["AddSub"], n("AddSub"), height=h("AddSub", None), byte_mult=byte_mult)
     for kind, (_, chip, _) in ALU_CHIPS.items():
-        rec = alu_records(capture["alu"], kind)
-        if len(rec):
-            out[chip] = alu_trace(kind, to_device(rec), len(rec), byte_mult=byte_mult)
-    if len(capture.get("branches", [])):
-        rec = branch_records(capture["branches"])
-        out["Branch"] = branch_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    if len(capture.get("mevs", [])):
-        rec = mem_instr_records(capture["mevs"], shard)
-        out["MemoryInstrs"] = memory_instrs_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    if len(capture.get("jumps", [])):
-        rec = jump_records(capture["jumps"])
-        out["Jump"] = jump_trace(to_device(rec), len(rec))
-    if len(capture.get("movs", [])):
-        rec = movcond_records(capture["movs"])
-        out["MovCond"] = movcond_trace(to_device(rec), len(rec))
-    if len(capture.get("muls", [])):
-        rec = mul_records(capture["muls"], shard)
-        out["Mul"] = mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    if len(capture.get("divs", [])):
-        rec = divrem_records(capture["divs"], shard)
-        out["DivRem"] = divrem_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    if len(capture.get("misc", [])):
-        rec = misc_records(capture["misc"], shard)
-        out["MiscInstrs"] = misc_instrs_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    if len(capture["alu"].get("clz", [])):
-        rec = alu_records(capture["alu"], "clz")
-        out["CloClz"] = clo_clz_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    ml = memory_local_events(capture["entries"])
-    out["MemoryLocal"] = memory_local_trace(to_device(ml), len(ml))
-    if len(capture["core_syscalls"]):
-        sc = syscall_events(capture["core_syscalls"])
-        out["SyscallCore"] = syscall_trace(to_device(sc), len(sc))
-    if len(capture["syscalls"]):
-        sc = syscall_events(capture["syscalls"])
-        out["SyscallInstrs"] = syscall_instrs_trace(to_device(sc), len(sc))
-    ge = shard_global_events(capture)
-    out["Global"], _ = global_trace(to_device(ge), len(ge), byte_mult=byte_mult)
+        if want(chip):
+            out[chip] = alu_trace(kind, records[chip], n(chip), height=h(chip, None), byte_mult=byte_mult)
+    simple = (("Branch", branch_trace, True), ("MemoryInstrs", memory_instrs_trace, True), ("Jump", jump_trace, False),
+              ("MovCond", movcond_trace, False), ("Mul", mul_trace, True), ("DivRem", divrem_trace, True),
+              ("MiscInstrs", misc_instrs_trace, True), ("CloClz", clo_clz_trace, True))
+    for chip, fn, bytes_ in simple:
+        if want(chip):
+            kw = {"byte_mult": byte_mult} if bytes_ else {}
+            out[chip] = fn(records[chip], n(chip), height=h(chip, None), **kw)
+    out["MemoryLocal"] = memory_local_trace(records["MemoryLocal"], n("MemoryLocal"), height=h("MemoryLocal", None))
+    if want("SyscallCore"):
+        out["SyscallCore"] = syscall_trace(records["SyscallCore"], n("SyscallCore"), height=h("SyscallCore", None))
+    if want("SyscallInstrs"):
+        out["SyscallInstrs"] = syscall_instrs_trace(records["SyscallInstrs"], n("SyscallInstrs"),
+                                                    height=h("SyscallInstrs", None))
+    out["Global"], _ = global_trace(records["Global"], n("Global"), height=h("Global", None), byte_mult=byte_mult)
     return out
+
+
+def shard_records_to_device(capture: dict) -> dict:
+    """shard_records uploaded (the `records` argument of shard_traces), with their counts under "_n"."""
+    host = shard_records(capture)
+    d = {k: to_device(v) for k, v in host.items()}
+    d["_n"] = {k: len(v) for k, v in host.items()}
+    return d
 
 
 POSEIDON2_WIDE_WIDTH = 313  # ZKM_POSEIDON2_WIDE_DEG3_WIDTH
