@@ -340,8 +340,60 @@ def maxshape_leg(args, rk, n, K):
            "value": round(K * rows * steps / el, 1), "unit": "rows/s", "ms_per_shard": round(1e3 * el / (steps * K), 3),
            "resident": {"value": round(K * rows * steps / el_res, 1), "ms_per_shard": round(1e3 * el_res / (steps * K), 3)},
            "proof_bytes": len(p1), "trace_generation_s": round(sb.gen_s, 1)}
+    out["from_device_traces"] = maxshape_from_records(sb, steps)
     del sb
     return out
+
+
+_CAPTURE = {}
+
+
+def maxshape_from_records(sb, steps):
+    """The maximal-shape shard's traces built on the device from the executor's records (every chip at the
+    shape's height, Byte and Program multiplicities included), then proven from them: device trace time
+    (records already in HBM; their H2D timed apart), per-shard proof time from the device traces, and the
+    proof bytes checked against the host-trace proof."""
+    import torch
+    from zkmips_amd import mips_alu as A
+    from zkmips_amd import tracegen as TG
+    cap = _CAPTURE.get("maxshape")
+    if not cap:
+        return None
+    dev_t, pv = sb.shards[0][0], sb.shards[0][1]
+    heights = {k: int(v.shape[0]) for k, v in dev_t.items() if k not in ("Byte", "Program")}
+    t0 = time.perf_counter()
+    recs = TG.shard_records_to_device(cap)
+    torch.cuda.synchronize()
+    h2d_s = time.perf_counter() - t0
+    rec_bytes = sum(int(v.numel()) for k, v in recs.items() if k != "_n")
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    TG.shard_traces(cap, byte_mult=bm, heights=heights, records=recs)  # warm (JIT of nothing; allocator)
+    reps = 3
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        bm.zero_()
+        tr = TG.shard_traces(cap, byte_mult=bm, heights=heights, records=recs)
+    e1.record()
+    torch.cuda.synchronize()
+    gen_ms = e0.elapsed_time(e1) / reps
+    tr["Byte"] = bm
+    tr = {k: v for k, v in tr.items() if k in dev_t}
+    ref = sb.prover.prove_shard(dev_t, pv)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        p = sb.prover.prove_shard(tr, pv)
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.perf_counter() - t0) / steps
+    assert p == ref, "maxshape: device-trace proof differs from the host-trace proof"
+    trace_bytes = sum(int(v.numel()) * 4 for v in tr.values())
+    return {"device_tracegen_ms": round(gen_ms, 3), "records_bytes": rec_bytes, "records_h2d_s": round(h2d_s, 3),
+            "trace_bytes": trace_bytes, "serial_ms_per_shard_from_device_traces": round(ms, 3),
+            "proof_bytes_equal_host_trace_proof": True,
+            "what": "every chip of the shard built on the device from the executor's event records at the shape's "
+                    "heights (zkmips_amd/tracegen.shard_traces), then one shard proof at a time from them"}
 
 
 def make_shard(workload, n, seed):
@@ -351,7 +403,8 @@ def make_shard(workload, n, seed):
         return MC.loop_shard(60, (3 * n // 4) // 104, seed=1)  # ~98 instructions per iteration
     if workload == "maxshape":  # the reference's 2^22 maximal shape, scaled to 2^log_n Cpu rows
         from zkmips_amd import shapes as SH
-        return SH.shape_shard(SH.MAXIMAL_22, seed=1, down=22 - (n.bit_length() - 1))
+        _CAPTURE["maxshape"] = cap = {}  # the executor's records, for the device-trace sub-leg
+        return SH.shape_shard(SH.MAXIMAL_22, seed=1, down=22 - (n.bit_length() - 1), capture=cap)
     if workload == "alu":
         from zkmips_amd import mips_alu as A
         return A.alu_shard(n // 4, n // 4, seed=seed, n_lt=n // 4, n_sll=n // 8, n_sr=n // 16, n_clz=n // 16)
