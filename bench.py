@@ -389,7 +389,8 @@ def maxshape_from_records(sb, steps):
     ms = 1e3 * (time.perf_counter() - t0) / steps
     assert p == ref, "maxshape: device-trace proof differs from the host-trace proof"
     trace_bytes = sum(int(v.numel()) * 4 for v in tr.values())
-    return {"device_tracegen_ms": round(gen_ms, 3), "records_bytes": rec_bytes, "records_h2d_s": round(h2d_s, 3),
+    return {"device_tracegen_ms": round(gen_ms, 3), "records_bytes": rec_bytes,
+            "records_convert_and_upload_s": round(h2d_s, 3),  # Python executor tuples -> structs, then H2D
             "trace_bytes": trace_bytes, "serial_ms_per_shard_from_device_traces": round(ms, 3),
             "proof_bytes_equal_host_trace_proof": True,
             "what": "every chip of the shard built on the device from the executor's event records at the shape's "
