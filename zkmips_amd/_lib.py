@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzkm_hip.so")
+LIB_PATH = os.environ.get("ZKM_LIB") or os.path.join(HERE, "libzkm_hip.so")  # ZKM_LIB: A/B of a second build
 
 ZKM_OK = 0
 ZKM_REPR_CANONICAL, ZKM_REPR_MONTGOMERY = 0, 1
