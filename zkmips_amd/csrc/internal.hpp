@@ -143,6 +143,9 @@ void lde_batch_bitrev_in(Ctx &c, const DMat &src, uint32_t shift_mont, DMat &dst
 void lde_batch_strided(Ctx &c, const DMat &src, uint32_t shift_mont, uint32_t *dst, uint64_t dst_stride, hipStream_t s);
 void lde_batch_bitrev_in_strided(Ctx &c, const DMat &src, uint32_t shift_mont, uint32_t *dst, uint64_t dst_stride,
                                  hipStream_t s);
+// blowup 4 (dst: 4h x w col-major) from natural-order src, one shared inverse transform
+void lde_batch_blowup4(Ctx &c, const DMat &src, uint32_t shift0_mont, uint32_t shift1_mont, uint32_t *dst,
+                       hipStream_t s);
 
 // Merkle
 void tree_build(DTree &t, hipStream_t s);

@@ -1289,8 +1289,9 @@ void lde_batch_bitrev_in_strided(Ctx &c, const DMat &src, uint32_t shift, uint32
     run_contig<false>(logC, dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, c.tw_fwd, MODE_PLAIN, Twist{}, 0, s);
 }
 
-// Columns per pass batch of the natural-input LDE (16: measured 4.62 ms vs 4.67 ms for all 67
-// columns of a 2^22 trace at once, and a 16x smaller work buffer); ZKM_LDE_CB overrides (0 = all).
+// Columns per pass batch of the natural-input LDE: at least 16 (measured 4.62 ms vs 4.67 ms for all
+// 67 columns of a 2^22 trace at once), and up to a 256 MB work buffer for short traces (compress
+// shapes, 2^14..2^18 rows: fewer launches; profiles/r03_lde_cb_ab.txt); ZKM_LDE_CB overrides (0 = all).
 static uint32_t lde_col_batch(uint64_t N, uint32_t nv) {
     static const long env = [] {
         const char *e = getenv("ZKM_LDE_CB");
@@ -1298,7 +1299,7 @@ static uint32_t lde_col_batch(uint64_t N, uint32_t nv) {
     }();
     uint64_t cb;
     if (env >= 0) cb = env ? (uint64_t)env : nv;
-    else cb = 16;
+    else cb = std::max<uint64_t>(16, (1ull << 25) / N);
     return (uint32_t)std::min<uint64_t>(cb, nv);
 }
 
@@ -1309,23 +1310,27 @@ void lde_batch(Ctx &c, const DMat &src, uint32_t shift, DMat &dst, hipStream_t s
     lde_batch_strided(c, src, shift, dst.d, 2 * src.height, s);
 }
 
-void lde_batch_strided(Ctx &c, const DMat &src, uint32_t shift, uint32_t *dst_d, uint64_t dst_stride, hipStream_t s) {
+// nsh coset shifts (1, or 2 for blowup 4): the strided inverse passes run once per column batch
+// into `winv` and each shift's fused + forward passes read it, writing the LDE of shift e at
+// dst + e * half_off (column stride dst_stride).
+static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh, uint32_t *dst_d,
+                        uint64_t dst_stride, uint64_t half_off, hipStream_t s) {
     const uint64_t N = src.height, W = src.width;
     if (!W) return;
-    ARG_CHECK(dst_stride >= 2 * N, "LDE destination stride");
-    DMat dst{dst_d, 2 * N, W};
-    PROF("lde", s, 12.0 * N * W);
-    prof_add("lde_gfops", lde_gf_ops(N) * W);
+    ARG_CHECK(dst_stride >= (uint64_t)nsh * 2 * N, "LDE destination stride");
+    PROF("lde", s, 12.0 * N * W * nsh);
+    prof_add("lde_gfops", lde_gf_ops(N) * W * nsh);
     const int L = ilog2(N);
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
     int logC;
     std::vector<int> sp = strided_plan(L, logC);
-    const Twist tws = get_twist(c, N, L, shift, s);
     const uint32_t nv = (uint32_t)W;
     ColMap m_src{N, 0, 1}, m_w1{2 * N, 0, 1}, m_w2{2 * N, N, 2}, m_out{dst_stride, N, 2};
     if (sp.empty()) {
-        run_fused(logC, src.d, dst.d, m_src, ColMap{dst_stride, 0, 1}, nv, L, c.tw_inv, c.tw_fwd, tws, N, 1, s);
+        for (int e = 0; e < nsh; e++)
+            run_fused(logC, src.d, dst_d + e * half_off, m_src, ColMap{dst_stride, 0, 1}, nv, L, c.tw_inv, c.tw_fwd,
+                      get_twist(c, N, L, shifts[e], s), N, 1, s);
         return;
     }
     // Columns go through all passes in batches of `cb`: a batch's work buffer (2N words per
@@ -1333,34 +1338,52 @@ void lde_batch_strided(Ctx &c, const DMat &src, uint32_t shift, uint32_t *dst_d,
     // sits in the 256 MB Infinity Cache, so only the first read and the last write reach HBM.
     const uint32_t cb = lde_col_batch(N, nv);
     DBuf work(2 * N * cb, s);
+    DBuf winv(nsh > 1 ? N * cb : 0, s);
     for (uint32_t c0 = 0; c0 < nv; c0 += cb) {
         const uint32_t nb = std::min(cb, nv - c0);
         const uint32_t *in = src.d + (uint64_t)c0 * N;
-        uint32_t *out = dst.d + (uint64_t)c0 * dst_stride;
+        // one shift: the inverse passes run in the work buffer's first half (fused in place)
+        uint32_t *ibuf = nsh > 1 ? winv.p : work.p;
+        const ColMap m_i = nsh > 1 ? m_src : m_w1;
         ColMap min = m_src;
         int logS = L;
         for (size_t i = 0; i < sp.size(); i++) {
             logS -= sp[i];
-            run_strided<false>(sp[i], in, work.p, min, m_w1, nb, L, logS, c.tw_inv, MODE_PLAIN, s, Twist{}, 0,
+            run_strided<false>(sp[i], in, ibuf, min, m_i, nb, L, logS, c.tw_inv, MODE_PLAIN, s, Twist{}, 0,
                                1u << c.tw_log);
-            in = work.p;
-            min = m_w1;
+            in = ibuf;
+            min = m_i;
         }
-        if (logC == 13) {
-            hipLaunchKernelGGL(k_lde_fused13, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, work.p, work.p,
-                               m_w1, m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
-            HIP_CHECK(hipGetLastError());
-        } else {
-            run_fused(logC, work.p, work.p, m_w1, m_w1, nb, L, c.tw_inv, c.tw_fwd, tws, N, 0, s);
-        }
-        logS = logC;
-        for (int i = (int)sp.size() - 1; i >= 0; i--) {
-            const bool last = (i == 0);
-            run_strided<true>(sp[i], work.p, last ? out : work.p, m_w2, last ? m_out : m_w2, 2 * nb, L, logS, c.tw_fwd,
-                              last ? MODE_BITREV_OUT : MODE_PLAIN, s, Twist{}, 0, 1u << c.tw_log);
-            logS += sp[i];
+        for (int e = 0; e < nsh; e++) {
+            const Twist tws = get_twist(c, N, L, shifts[e], s);
+            uint32_t *out = dst_d + (uint64_t)c0 * dst_stride + e * half_off;
+            if (logC == 13) {
+                hipLaunchKernelGGL(k_lde_fused13, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf, work.p,
+                                   m_i, m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
+                HIP_CHECK(hipGetLastError());
+            } else {
+                run_fused(logC, ibuf, work.p, m_i, m_w1, nb, L, c.tw_inv, c.tw_fwd, tws, N, 0, s);
+            }
+            logS = logC;
+            for (int i = (int)sp.size() - 1; i >= 0; i--) {
+                const bool last = (i == 0);
+                run_strided<true>(sp[i], work.p, last ? out : work.p, m_w2, last ? m_out : m_w2, 2 * nb, L, logS,
+                                  c.tw_fwd, last ? MODE_BITREV_OUT : MODE_PLAIN, s, Twist{}, 0, 1u << c.tw_log);
+                logS += sp[i];
+            }
         }
     }
+}
+
+void lde_batch_strided(Ctx &c, const DMat &src, uint32_t shift, uint32_t *dst_d, uint64_t dst_stride, hipStream_t s) {
+    lde_natural(c, src, &shift, 1, dst_d, dst_stride, 0, s);
+}
+
+// Blowup 4 of natural-order evaluations: rows [0, 2N) of every 4N-row column are the blowup-2 LDE
+// with shift0, rows [2N, 4N) the one with shift1; the inverse transform is shared.
+void lde_batch_blowup4(Ctx &c, const DMat &src, uint32_t shift0, uint32_t shift1, uint32_t *dst_d, hipStream_t s) {
+    const uint32_t sh[2] = {shift0, shift1};
+    lde_natural(c, src, sh, 2, dst_d, 4 * src.height, 2 * src.height, s);
 }
 
 }  // namespace zkm

@@ -161,7 +161,16 @@ static void lde_into(Ctx &c, const DMat &src, uint32_t shift, bool bitrev_in, in
         else lde_batch(c, src, shift, d, s);
         return;
     }
-    // each blowup-2 pass writes its half of every 4N-row column in place (column stride 4N)
+    // each blowup-2 pass writes its half of every 4N-row column in place (column stride 4N); natural
+    // input shares the inverse transform between the halves (ZKM_LDE4_SHARED=0: two full passes)
+    static const bool shared = [] {
+        const char *e = getenv("ZKM_LDE4_SHARED");
+        return !(e && e[0] == '0');
+    }();
+    if (!bitrev_in && shared) {
+        lde_batch_blowup4(c, src, shift, mul(shift, two_adic_gen(ilog2(N) + 2)), dst, s);
+        return;
+    }
     for (int half = 0; half < 2; half++) {
         const uint32_t sh = half ? mul(shift, two_adic_gen(ilog2(N) + 2)) : shift;
         if (bitrev_in) lde_batch_bitrev_in_strided(c, src, sh, dst + half * 2 * N, 4 * N, s);
