@@ -78,3 +78,32 @@ def test_gpu_rejects_quotient_degree_above_blowup(dev):
     gpu = HipProver(dev, m, prep, num_queries=8, log_blowup=1)
     with pytest.raises(ZkmError):
         gpu.prove_shard(tr, pv)
+
+
+_BATCHED = r"""
+import hashlib, sys
+from zkmips_amd import workloads as W
+from zkmips_amd._lib import Device
+from zkmips_amd.prover import HipProver
+m, prep, tr, pv = W.deg5_shard(1 << 14, 5)
+d = Device(0)
+print(hashlib.sha256(HipProver(d, m, prep, num_queries=42, log_blowup=2).prove_shard(tr, pv)).hexdigest())
+d.close()
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"ZKM_LDE_CB": "3"}, {"ZKM_LDE_CB": "3", "ZKM_LDE4_SHARED": "0"}])
+def test_gpu_blowup4_column_batches(env):
+    """The natural-order LDE in batches of 3 columns (several batches per trace, the shared inverse
+    transform's buffer reused across them), and the unshared two-pass form: bytes equal the oracle's.
+    Both switches are read once per process, hence the child process."""
+    import hashlib, os, subprocess, sys
+    m, prep, tr, pv = W.deg5_shard(1 << 14, 5)
+    rc, ref = O.OracleProver(m, prep, num_queries=42, log_blowup=2).prove(tr, pv)
+    assert rc == 0
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _BATCHED], cwd=root, env={**os.environ, **env},
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split()[-1] == hashlib.sha256(ref).hexdigest()
