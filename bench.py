@@ -7,20 +7,20 @@ the reference's Cpu chip) plus the preprocessed FibTable chip — proven end to 
 reference's CpuProver::commit + CpuProver::open would (LDE, Poseidon2 MMCS, LogUp trace, quotient,
 openings, FRI with 84 queries and 16 PoW bits).
 
-One step = one batch of --inflight concurrent shard proofs per GPU, each from HOST traces: the
-SURVEY.md §8d metric counts the H2D copy of the traces and the D2H of the proof inside the timed
-span (prove.rs:426-497 hands commit() host RowMajorMatrix traces).  The traces sit in page-locked
-host memory, and each in-flight slot runs the reference's pipeline shape (prove.rs:162-526: the
-next shard's traces travel while the current one proves): the H2D DMA of shard j+1 into one of two
-HBM buffers is issued before shard j is proven from the other, so PCIe (≈57 GB/s, 1.13 GB per
-2^22 shard) overlaps the kernels.  Every copy is inside the timed span; the first one of each slot
-is not hidden.  For N > 1 every rank proves its own shards (shards are independent,
-prove.rs:208-209) and the proofs are gathered to rank 0 over RCCL inside the timed region.
+One step = one batch of --inflight concurrent shard proofs per GPU.  `value` is the throughput with
+the traces already resident in HBM when the timed region starts (the benchmark contract: inputs in
+HBM; the proof's D2H is inside the span).  The PCIe-inclusive rate is reported beside it as
+`host_traces`: the traces sit in page-locked host memory and each in-flight slot runs the
+reference's pipeline shape (prove.rs:162-526: the next shard's traces travel while the current one
+proves) — the H2D DMA of shard j+1 into one of two HBM buffers is issued before shard j is proven
+from the other, so PCIe (≈57 GB/s, 1.13 GB per 2^22 shard) overlaps the kernels.  For N > 1 every
+rank proves its own shards (shards are independent, prove.rs:208-209) and the proofs are gathered
+to rank 0 over RCCL inside the timed region.
 
 Also reported: `host_per_call` (each zkm_prove_shard call copies its own pinned host traces, no
-look-ahead), `resident` (traces already in HBM, no H2D), the roofline of the dominant stage (HIP
-events on the launching stream, PMC traffic from rocprofv3 passes in this run) and the CPU baseline
-on a bounded sample.
+look-ahead), `sizes` (the same resident measurement at 2^20, 2^21 and 2^23 rows; 2^24 has no LDE
+domain), the roofline of the dominant stage (HIP events on the launching stream, PMC traffic from
+rocprofv3 passes in this run) and the CPU baseline on a bounded sample.
 """
 import argparse
 import ctypes as C
@@ -319,6 +319,72 @@ def cpu_baseline(log_n, queries):
                       f"{dt:.2f} s wall on {threads} OpenMP threads, the fastest count for this box among "
                       f"{sorted(table)} (2^18-row calibration proofs; {cpus} CPUs in the affinity mask) "
                       "(AVX-512 Poseidon2/LDE)"}
+
+
+def profile_proofs(prover, dev_traces, pvs, nprof):
+    """nprof single-shard resident proofs with the per-stage HIP events on: (stage table, ms per proof)."""
+    import torch
+    from zkmips_amd._lib import lib
+    lib().zkm_profile_reset()
+    lib().zkm_profile_enable(1)
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for _ in range(nprof):
+        prove_resident(prover, dev_traces, pvs)
+    torch.cuda.synchronize()
+    serial_ms = (time.perf_counter() - ts) / nprof * 1e3
+    lib().zkm_profile_enable(0)
+    need = lib().zkm_profile_dump(None, 0)
+    buf = C.create_string_buffer(need)
+    lib().zkm_profile_dump(buf, need)
+    return parse_profile(buf.value.decode()), serial_ms, buf.value.decode()
+
+
+def size_series(args, prover0, K, logs=(20, 21, 23)):
+    """north_star's 2^20..2^24 sweep beside the 2^22 headline: for each size one FibCpu shard resident in
+    HBM, K concurrent slots proving it `steps` times (timed like `value`), then single-shard proofs with
+    the stage events (LDE stage time and its NTT GF-ops/s).  2^24 rows need a 2^25-point LDE domain,
+    beyond KoalaBear's two-adicity 24: not provable by the reference either."""
+    import threading
+    import torch
+    from zkmips_amd import workloads as W
+    from zkmips_amd.prover import HipProver
+    out = {}
+    for lg in logs:
+        n = 1 << lg
+        m, prep, tr, pvs = W.fib_shard(n, seed=1)
+        dev = {k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in tr.items()}
+        pr = HipProver(prover0.dev, m, prep, num_queries=args.queries)
+        steps = max(2, args.steps // (2 if lg > 22 else 1))
+        proofs = [b""] * K
+        prove_resident(pr, dev, pvs)  # warm (allocator pool at this size)
+
+        def slot(k):
+            for _ in range(steps):
+                proofs[k] = prove_resident(pr, dev, pvs)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=slot, args=(k,)) for k in range(K)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        assert all(p == proofs[0] for p in proofs), "size series: slots' proofs differ"
+        prof, serial_ms, _ = profile_proofs(pr, dev, pvs, 2)
+        e = {"value": round(K * n * steps / el, 1), "unit": "rows/s", "ms_per_shard": round(1e3 * el / (K * steps), 3),
+             "serial_ms_per_shard": round(serial_ms, 3), "steps": steps, "in_flight": K, "proof_bytes": len(proofs[0])}
+        if "lde" in prof and "lde_gfops" in prof:
+            lcnt, lms, lbytes = prof["lde"]
+            e["lde_ms_per_shard"] = round(lms / 2, 3)
+            e["ntt_gf_ops_per_s"] = float(f"{prof['lde_gfops'][2] / (lms / 1e3):.4g}")
+            e["lde_algorithmic_GBps"] = round(lbytes / (lms / 1e3) / 1e9, 1)
+        out[f"2^{lg}"] = e
+        del pr, dev
+        torch.cuda.synchronize()
+    out["2^24"] = "N/A: a 2^24-row trace needs a 2^25-point coset LDE (blowup 2); KoalaBear's two-adicity is 24"
+    return out
 
 
 def maxshape_leg(args, rk, n, K):
@@ -690,192 +756,168 @@ def tracegen_bench(args):
     print(json.dumps(line), flush=True)
 
 
-def _gen_node(children):
-    """Worker (spawned process, no GPU): a compress node's program from its children's proofs, executed,
-    and its compress-machine shard (machine, preprocessed traces, traces, public values)."""
-    from zkmips_amd import recursion as R
+def start_witness_pool(n: int):
+    """The compress witness-generation process pool, its workers spawned NOW (before anything in this
+    process touches the GPU: they are started as fresh interpreters, never forked from a GPU process)."""
+    import multiprocessing as mpc
+    from concurrent.futures import ProcessPoolExecutor
+    pool = ProcessPoolExecutor(n, mp_context=mpc.get_context("spawn"))
+    for f in [pool.submit(time.sleep, 0.3) for _ in range(n)]:
+        f.result()
+    return pool
+
+
+def mips_leaves(dev, queries: int, n_leaves: int = 64, distinct: int = 4, down: int = 6):
+    """Config 5's leaves: core shard proofs of MIPS shards in the reference's maximal 2^22 shape scaled to
+    Cpu 2^(22-down) (all 17 chips of maximal_shapes.json["22"][2], zkmips_amd/shapes.py), proven on this
+    GPU before the timed region; `distinct` different executions, dealt cyclically to the leaves."""
     from zkmips_amd import recursion_verifier as RV
-    _, prep, traces, pvs = R.shard(RV.compress_node_program(children))
-    return prep, traces, pvs  # the machine is rebuilt by the parent (its expressions are per-process)
+    from zkmips_amd import shapes as SH
+    from zkmips_amd.prover import HipProver
+    t0 = time.perf_counter()
+    shards = [SH.shape_shard(SH.MAXIMAL_22, seed=1 + i, down=down) for i in range(distinct)]
+    gen_s = time.perf_counter() - t0
+    m, prep = shards[0][0], shards[0][1]
+    hp = HipProver(dev, m, prep, num_queries=queries)
+    vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=queries)
+    proofs = [hp.prove_shard(sh[2], sh[3]) for sh in shards]
+    info = {"leaf_shape": {k: int(v.shape[0]) for k, v in shards[0][2].items()}, "distinct_leaf_shards": distinct,
+            "leaf_queries": queries, "leaf_generation_s": round(gen_s, 1), "leaf_proof_bytes": len(proofs[0])}
+    return [(vk, proofs[i % distinct]) for i in range(n_leaves)], info
 
 
-def prep_digest(prep) -> bytes:
-    """Identity of a program's proving key: xxh3-128 over its preprocessed traces (name, shape, words)."""
-    try:
-        import xxhash
-        h = xxhash.xxh3_128()
-    except ImportError:  # pragma: no cover
-        import hashlib
-        h = hashlib.sha256()
-    for k in sorted(prep):
-        v = prep[k]
-        if v is None:
-            continue
-        h.update(k.encode() + np.asarray(v.shape, np.int64).tobytes())
-        h.update(np.ascontiguousarray(v).view(np.uint8).data)
-    return h.digest()
+def _union_s(intervals) -> float:
+    """Length of the union of (start, end) intervals: the time at least one proof was on the GPU."""
+    tot, cur_s, cur_e = 0.0, None, None
+    for s_, e_ in sorted(intervals):
+        if cur_e is None or s_ > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = s_, e_
+        else:
+            cur_e = max(cur_e, e_)
+    return tot + (cur_e - cur_s if cur_e is not None else 0.0)
+
+
+def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = False):
+    """One 64-leaf compress tree, dependency-driven (zkmips_amd/compress_tree.py): witness generation in
+    the pool overlapping GPU proving.  Returns (root (vk, proof), result dict)."""
+    import threading
+    from zkmips_amd import compress_tree as CT
+    provers = CT.GpuProvers(dev)
+    stats = CT.TreeStats()
+    lock = threading.Lock()
+    spans = []
+    shapes = {}
+
+    def prove(wit):
+        prep, traces, pvs, shape, times = wit
+        pr = provers.get(prep, stats)
+        t = time.perf_counter()
+        proof = pr.prove_shard(traces, pvs)
+        e = time.perf_counter()
+        with lock:
+            spans.append((t, e))
+            stats.prove_s += e - t
+            stats.proofs += 1
+            stats.build_s += times["build_s"]
+            stats.execute_s += times["execute_and_traces_s"]
+            k = ",".join(f"{c}:{shape[c]}" for c in sorted(shape))
+            shapes[k] = shapes.get(k, 0) + 1
+            shapes.setdefault("_rows", {})[k] = max(int(v.shape[0]) for v in traces.values())
+        return CT.compress_child_vk(pr.vk_commit, shape), proof
+
+    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, ch), prove, inflight)
+    t0 = time.perf_counter()
+    root = CT.reduce_distributed(leaves, reducer) if distributed else CT.reduce_serial(leaves, reducer)
+    wall = time.perf_counter() - t0
+    rows = shapes.pop("_rows")
+    from zkmips_amd import recursion as R
+    names = {",".join(f"{c}:{sh[c]}" for c in sorted(sh)): i for i, sh in enumerate(R.RECURSION_SHAPES)}
+    res = {"wall_s": wall, "gpu_busy_s": _union_s(spans), "proofs": stats.proofs,
+           "witness_build_s": stats.build_s, "witness_execute_and_traces_s": stats.execute_s,
+           "setups": stats.setups, "setup_s": stats.setup_s, "lookups": stats.lookups,
+           "shapes": {f"RecursionShapeConfig[{names.get(k, '?')}]" + (" (fastest)" if names.get(k) == 0 else ""):
+                      {"nodes": v, "max_rows": rows[k], "log_heights": dict(kv.split(":") for kv in k.split(","))}
+                      for k, v in shapes.items()}}
+    return root, res
+
+
+def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int = 3):
+    """BASELINE config 5 as a field of a bench line: 64 MIPS leaf proofs reduced by the compress tree.
+    Node programs verify their children in full (transcript, PoW, Merkle paths, FRI, and the out-of-domain
+    constraint check, zkmips_amd/recursion_verifier.py), are padded to the first fitting
+    RecursionShapeConfig shape, and are set up (proving key by preprocessed-trace digest, zkm_setup when
+    new) and proven on the GPU as soon as their witness exists.  `value` is end to end (witness generation
+    overlapped with proving, every setup inside), `prove_only` counts the time a proof was on the GPU."""
+    from zkmips_amd import compress_tree as CT
+    leaves, info = mips_leaves(dev, args.queries, down=22 - args.leaf_log)
+    # warm-up (untimed): one node's witness and proof (JIT modules, allocator pools); its key is dropped
+    wit = CT.node_witness(leaves[:2])
+    warm = CT.GpuProvers(dev)
+    warm.get(wit[0], CT.TreeStats()).prove_shard(wit[1], wit[2])
+    del warm
+    (rvk, rproof), r = compress_tree_run(pool, dev, leaves, inflight, distributed=world > 1)
+    n = r["proofs"]
+    out = {"metric": "compress proofs/sec, end to end (64-leaf compress tree = 63 recursion-machine proofs, "
+                     "BASELINE config 5)",
+           "value": round(63 / r["wall_s"], 3), "unit": "proofs/s", "tree_wall_s": round(r["wall_s"], 3),
+           "prove_only": {"value": round(63 / r["gpu_busy_s"], 3), "unit": "proofs/s",
+                          "gpu_busy_s": round(r["gpu_busy_s"], 3),
+                          "what": "63 proofs over the time at least one node proof was on the GPU"},
+           "witness_generation": {"build_s_per_node": round(r["witness_build_s"] / max(1, n), 3),
+                                  "execute_and_traces_s_per_node": round(r["witness_execute_and_traces_s"] / max(1, n), 3),
+                                  "workers": args.node_workers,
+                                  "what": "host: node program (verifying both children) + recursion runtime + traces, "
+                                          "in a process pool, overlapped with proving"},
+           "setups": r["setups"], "setup_ms_total": round(1e3 * r["setup_s"], 3), "setup_lookups": r["lookups"],
+           "node_shapes": r["shapes"], "root_proof_bytes": len(rproof), "proofs_this_rank": n,
+           "leaves": info, "in_flight": inflight,
+           "node_program": "verifies each child: transcript replay, PoW, query bits, Merkle paths of every opening, "
+                           "FRI reduced openings and folds, out-of-domain constraint check of every chip against the "
+                           "quotient, local cumulative sum; RecursionShapeConfig::fix_shape padding"}
+    return out, (rvk, rproof)
 
 
 def compress_bench(args):
-    """BASELINE config 5: the recursion/compress stage over REAL leaves.  64 leaf proofs (FibCpu 2^leaf_log
-    core shards, 84 queries, proven on this GPU before the timed region) are reduced by a 64-leaf compress
-    tree, 63 compress proofs (32 + 16 + 8 + 4 + 2 + 1, prover/src/lib.rs:794-858): each node's recursion
-    program VERIFIES its two children (zkmips_amd/recursion_verifier.py: transcript replay, PoW, query
-    bits, Merkle paths of every opening, BatchFRI reduced openings, folds to the final polynomial), is
-    executed by the restated runtime, and is proven as a compress-machine shard (compressed_fri_config:
-    blowup 4, 42 queries).  Layer L >= 2 verifies layer L-1's compress proofs.
-
-    Per layer: witness generation (program build + execution + traces: host, a process pool, the
-    reference's trace-generation side of the pipeline split, reported separately), then the proving key:
-    looked up by the program's preprocessed-trace digest (the programs of one layer share their structure,
-    so one zkm_setup per layer; the lookup and any setup are inside the timed region), then the layer's
-    proofs, --inflight concurrently.  value = compress proofs / (setup lookups + proving time)."""
-    import threading
-    import multiprocessing as mpc
-    from concurrent.futures import ProcessPoolExecutor
-    # the witness-generation pool starts (spawn) before anything touches the GPU
-    workers = max(1, min(args.node_workers, 32))
-    pool = ProcessPoolExecutor(workers, mp_context=mpc.get_context("spawn"))
+    """BASELINE config 5 as its own bench line (`--workload compress`): compress_leg on N ranks (the tree
+    dealt by leaf blocks, zkmips_amd/compress_tree.reduce_distributed), plus the CPU oracle on one node
+    proof (the CPU baseline, byte-identical to the GPU's)."""
+    pool = start_witness_pool(max(1, min(args.node_workers, 32)))
     import torch
-    from zkmips_amd import recursion as R
-    from zkmips_amd import recursion_verifier as RV
-    from zkmips_amd import workloads as W
+    from zkmips_amd import compress_tree as CT
     from zkmips_amd._lib import Device
-    from zkmips_amd.prover import HipProver
     rk = Ranks(args, bind=False)
-    world, rank, local_rank, coll_dev = rk.world, rk.rank, rk.local_rank, rk.coll_dev
-    dev = Device(local_rank)
-    # ---- the 64 leaves: core shard proofs (untimed) ----
-    n_leaf = 1 << args.leaf_log
-    lm, lprep, _, _ = W.fib_shard(n_leaf, seed=1)
-    leaf_prover = HipProver(dev, lm, lprep, num_queries=args.queries)
-    leaves = [leaf_prover.prove_shard(*W.fib_shard(n_leaf, seed=1000 + i)[2:]) for i in range(64)]
-    leaf_vk = RV.ChildVk.of(lm, lprep, leaf_prover.vk_commit, num_queries=args.queries)
-    kw = dict(num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
-    cm = R.compress_machine()
-    pk_cache = {}  # preprocessed-trace digest -> HipProver (zkm_setup once per program structure)
-    stats = {"witness_s": 0.0, "setup_lookup_s": 0.0, "setups": 0, "setup_s": 0.0, "prove_s": 0.0, "proofs": 0}
-
-    def prover_for(m, prep):
-        t = time.perf_counter()
-        key = prep_digest(prep)
-        pr = pk_cache.get(key)
-        if pr is None:
-            t1 = time.perf_counter()
-            pr = HipProver(dev, m, prep, **kw)
-            stats["setups"] += 1
-            stats["setup_s"] += time.perf_counter() - t1
-            pk_cache[key] = pr
-        stats["setup_lookup_s"] += time.perf_counter() - t
-        return pr
-
-    def prove_nodes(layer, work):
-        """This rank's nodes of one layer: work = [(j, children proofs)]."""
-        vk = leaf_vk if layer == 1 else prove_nodes.child_vk
-        t = time.perf_counter()
-        shards = [(cm,) + r for r in pool.map(_gen_node, [[(vk, c) for c in ch] for _, ch in work])]
-        stats["witness_s"] += time.perf_counter() - t
-        out = [None] * len(shards)
-        provers = [prover_for(m, prep) for m, prep, _, _ in shards]
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        nxt = [0]
-        lock = threading.Lock()
-
-        def worker():
-            while True:
-                with lock:
-                    i = nxt[0]
-                    nxt[0] += 1
-                if i >= len(shards):
-                    return
-                out[i] = provers[i].prove_shard(shards[i][2], shards[i][3])
-        th = [threading.Thread(target=worker) for _ in range(max(1, min(len(shards), args.inflight)))]
-        for t_ in th:
-            t_.start()
-        for t_ in th:
-            t_.join()
-        stats["prove_s"] += time.perf_counter() - t
-        stats["proofs"] += len(shards)
-        m, prep = shards[0][0], shards[0][1]
-        # the next layer verifies proofs of this layer's program structure (one verifying key)
-        prove_nodes.child_vk = RV.compress_vk(m, prep, provers[0].vk_commit)
-        prove_nodes.last = shards[0]
-        return out
-
-    def tree():
-        if world == 1:
-            cur, layer = leaves, 0
-            while len(cur) > 1:
-                layer += 1
-                work = [(j, cur[2 * j:2 * j + 2]) for j in range(len(cur) // 2)]
-                cur = prove_nodes(layer, work)
-            return cur[0]
-        from zkmips_amd.dist import compress_tree_distributed
-        return compress_tree_distributed(None, leaves, device=coll_dev, prove_nodes=prove_nodes)
-
-    for _ in range(max(0, args.warmup)):
-        tree()
-    for k in stats:
-        stats[k] = 0 if isinstance(stats[k], int) else 0.0
+    dev = Device(rk.local_rank)
     rk.barrier()
-    t1 = time.time()
-    for _ in range(args.steps):
-        root = tree()
+    res, root = compress_leg(args, pool, dev, rk.world, rk.rank, args.inflight)
+    res["ms_per_proof"] = round(1e3 * res["tree_wall_s"] / 63, 3)
     rk.barrier()
-    wall = rk.max_over_ranks(time.time() - t1)
-    timed = rk.max_over_ranks(stats["prove_s"] + stats["setup_lookup_s"])
-    n_proofs = 63 * args.steps
-    m, prep, traces, pvs = prove_nodes.last
-    rows = max(v.shape[0] for v in traces.values())
-    # serial single-proof latency of one node
-    pr = prover_for(m, prep)
-    torch.cuda.synchronize()
-    t2 = time.time()
-    for _ in range(3):
-        pr.prove_shard(traces, pvs)
-    torch.cuda.synchronize()
-    serial_ms = (time.time() - t2) / 3 * 1e3
+    wall = rk.max_over_ranks(res["tree_wall_s"])
+    line = {"metric": res.pop("metric"), "value": round(63 / wall, 3), "unit": "proofs/s", "n_gpus": rk.world,
+            "steps": 1, "warmup": 1, "ms_per_step": round(1e3 * wall, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
+            "data": "64 real MIPS leaf proofs (reference maximal shape scaled to Cpu 2^16, 84 queries)",
+            "config": {"workload": "compress tree: 63 compress-machine shards verifying two child proofs each, "
+                                   "blowup 4, 42 queries", "parallelism": f"tree dealt by leaf blocks over {rk.world} ranks"}}
+    line.update({k: v for k, v in res.items() if k != "value"})
     cpu = None
-    if not args.no_cpu_baseline and rank == 0 and world == 1:
+    if not args.no_cpu_baseline and rk.rank == 0 and rk.world == 1:
         from tests import _oracle as O
-        o = O.OracleProver(m, prep, **kw)
+        wit = CT.node_witness([root, root])
+        cm = CT.GpuProvers(dev)
+        gpu = cm.get(wit[0], CT.TreeStats()).prove_shard(wit[1], wit[2])
+        o = O.OracleProver(cm.machine, wit[0], **cm.kw)
         tc = time.time()
-        rc, ref = o.prove(traces, pvs)
+        rc, ref = o.prove(wit[1], wit[2])
         dt = time.time() - tc
-        assert rc == 0 and ref == pr.prove_shard(traces, pvs), "GPU compress proof differs from the CPU oracle"
+        assert rc == 0 and ref == gpu, "GPU compress proof differs from the CPU oracle"
         cpu = {"value": round(1.0 / dt, 4), "unit": "compress proofs/s", "cores": cpu_threads(), "kind": "port",
-               "host": host_info(), "sample": f"one compress-node proof (blowup 4, 42 queries), {dt:.2f} s wall; "
-                                               "byte-identical to the GPU proof"}
+               "host": host_info(), "sample": f"one layer-7 compress-node proof (verifying the root twice; blowup 4, "
+                                               f"42 queries), {dt:.2f} s wall; byte-identical to the GPU proof"}
+    line["cpu_baseline"] = cpu
     pool.shutdown()
-    line = {
-        "metric": "compress proofs/sec (64-leaf compress tree = 63 recursion-machine proofs, BASELINE config 5)",
-        "value": round(n_proofs / timed, 3), "unit": "proofs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(1e3 * timed / args.steps, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
-        "data": f"64 real leaf proofs (FibCpu 2^{args.leaf_log} core shards, {args.queries} queries, proven on the GPU "
-                "before the timed region); every node's program verifies its two children",
-        "config": {"workload": "compress tree: 63 compress-machine shards, each verifying two child proofs "
-                               "(zkmips_amd/recursion_verifier.py), blowup 4, 42 queries",
-                   "node_shape": {k: int(v.shape[0]) for k, v in traces.items()}, "max_rows": rows,
-                   "main_cells": int(sum(v.size for v in traces.values())),
-                   "prep_cells": int(sum(v.size for v in prep.values() if v is not None)),
-                   "proof_bytes": len(root) if root else None,
-                   "parallelism": (f"a layer's proofs {args.inflight} in flight" if world == 1 else
-                                   f"node j of a layer on rank j % {world} ({args.inflight} in flight per rank), "
-                                   "each layer's proofs all-gathered (RCCL) before the next")},
-        "timed_region": "per layer: proving-key lookup by preprocessed-trace digest (+ zkm_setup when new) and the "
-                        "layer's commit+open; witness generation (program build, execution, traces) is reported "
-                        "beside it, as trace generation is outside the reference's prove span",
-        "wall_s_per_tree_incl_witness_generation": round(wall / args.steps, 3),
-        "witness_generation_s_per_tree": round(stats["witness_s"] / args.steps, 3),
-        "witness_workers": workers,
-        "setup_lookup_ms_per_tree": round(1e3 * stats["setup_lookup_s"] / args.steps, 3),
-        "setups_per_tree": stats["setups"] / args.steps, "setup_ms_total": round(1e3 * stats["setup_s"], 3),
-        "ms_per_proof": round(1e3 * timed / n_proofs, 3), "serial_ms_per_proof": round(serial_ms, 3),
-        "rows_per_s": round(rows * n_proofs / timed, 1), "cpu_baseline": cpu,
-    }
-    if rank == 0:
+    if rk.rank == 0:
         print(json.dumps(line), flush=True)
     rk.close()
 
@@ -1092,7 +1134,11 @@ def main():
     ap.add_argument("--no-maxshape", action="store_true",
                     help="skip the default line's secondary leg: the reference's maximal 2^22 MIPS shard shape")
     ap.add_argument("--maxshape-steps", type=int, default=4)
-    ap.add_argument("--leaf-log", type=int, default=16, help="compress workload: leaf core shards of 2^leaf_log rows")
+    ap.add_argument("--no-compress", action="store_true",
+                    help="skip the default line's compress leg (config 5: 64 MIPS leaves, 63 node proofs)")
+    ap.add_argument("--no-sizes", action="store_true",
+                    help="skip the default line's size series (resident rows/s and LDE time at 2^20, 2^21, 2^23)")
+    ap.add_argument("--leaf-log", type=int, default=16, help="compress leg: MIPS leaf shards in the maximal shape scaled to Cpu 2^leaf_log rows")
     ap.add_argument("--node-workers", type=int, default=16,
                     help="compress workload: processes generating node witnesses (the box allots 16 CPUs per GPU)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 HBM counter passes")
@@ -1113,6 +1159,11 @@ def main():
         return tracegen_bench(args)
     if args.workload == "compress":
         return compress_bench(args)
+    # the default line's compress leg (config 5): its witness pool starts before the GPU is touched
+    pool = None
+    if (not args.no_compress and args.workload == "fib" and int(os.environ.get("WORLD_SIZE", "1")) == 1
+            and not args.pmc_child):
+        pool = start_witness_pool(max(1, min(args.node_workers, 32)))
 
     import torch
     rk = Ranks(args)
@@ -1128,13 +1179,14 @@ def main():
     dev_traces, pvs, traces = sb.shards[0][0], sb.shards[0][1], sb.shards[0][2]
     rows_per_shard = sb.rows_per_shard
     if args.warmup:
-        sb.run_steps(args.warmup, "pipelined")
+        sb.run_steps(args.warmup, "resident")
+        sb.run_steps(1, "pipelined")
         sb.run_steps(1, "per_call")
-    # timed region (the headline): host traces, H2D + commit + open + D2H of the proof
-    proof, elapsed = sb.timed(args.steps, "pipelined")
-    # secondary: per-call host copies, and traces already resident in HBM
-    proof_pc, elapsed_pc = sb.timed(args.steps, "per_call")
+    # timed region (the headline `value`): traces resident in HBM, commit + open + D2H of the proof
     proof_res, elapsed_res = sb.timed(args.steps, "resident")
+    # secondary: host traces with the look-ahead H2D pipeline, and per-call host copies
+    proof, elapsed = sb.timed(args.steps, "pipelined")
+    proof_pc, elapsed_pc = sb.timed(args.steps, "per_call")
     assert proof_res == proof == proof_pc, "resident / host-trace proofs differ"
 
     if rank != 0:
@@ -1145,19 +1197,7 @@ def main():
     # (one shard in flight, so a stage's events bracket only its own kernels); the roofline and
     # the stage table come from here, the throughput `value` from the timed region above
     nprof = max(1, args.profile_steps)
-    lib().zkm_profile_reset()
-    lib().zkm_profile_enable(1)
-    torch.cuda.synchronize()
-    ts = time.perf_counter()
-    for _ in range(nprof):
-        prove_resident(prover, dev_traces, pvs)
-    torch.cuda.synchronize()
-    serial_ms = (time.perf_counter() - ts) / nprof * 1e3
-    lib().zkm_profile_enable(0)
-    need = lib().zkm_profile_dump(None, 0)
-    buf = C.create_string_buffer(need)
-    lib().zkm_profile_dump(buf, need)
-    prof = parse_profile(buf.value.decode())
+    prof, serial_ms, prof_text = profile_proofs(prover, dev_traces, pvs, nprof)
 
     # single-shard latency from pageable host memory (the runtime stages the copy)
     tp = time.perf_counter()
@@ -1218,7 +1258,7 @@ def main():
     stages = {k: {"count": v[0], "ms_per_shard": round(v[1] / nprof, 3)}
               for k, v in sorted(prof.items()) if not k.endswith("_perms") and not k.endswith("_gfops")}
 
-    value = world * K * rows_per_shard * args.steps / elapsed
+    value = world * K * rows_per_shard * args.steps / elapsed_res
     line = {
         "metric": "shard trace rows proved/sec at 2^22 rows",
         "value": round(value, 1),
@@ -1226,14 +1266,14 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-        "ms_per_shard": round(1e3 * elapsed / (args.steps * K), 3),
+        "ms_per_step": round(1e3 * elapsed_res / args.steps, 3),
+        "ms_per_shard": round(1e3 * elapsed_res / (args.steps * K), 3),
         "serial_ms_per_shard": round(serial_ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
-        "data": "synthetic (seeded S-SHARD traces, SURVEY.md §8d), host page-locked memory, H2D + proof D2H timed",
+        "data": "synthetic (seeded S-SHARD traces, SURVEY.md §8d), resident in HBM when the timed region starts; proof D2H timed",
         "config": {"workload": (f"S-SHARD FibCpu 2^{args.log_n} rows (main 67, LogUp 11 EF, quotient 2) + FibTable "
                                 f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard")
                    if args.workload == "fib" else
@@ -1257,12 +1297,14 @@ def main():
         "host_per_call": {"value": round(world * K * rows_per_shard * args.steps / elapsed_pc, 1), "unit": "rows/s",
                           "ms_per_shard": round(1e3 * elapsed_pc / (args.steps * K), 3),
                           "what": "same steps, each zkm_prove_shard copies its pinned host traces itself (no look-ahead)"},
-        "value_basis": ("host traces: H2D of the traces and D2H of the proof inside the timed region (SURVEY.md "
-                        "section 8d's definition, asked for by the round-1 review); the same steps with the inputs "
-                        "already resident in HBM when the timing starts are `resident`"),
-        "resident": {"value": round(world * K * rows_per_shard * args.steps / elapsed_res, 1), "unit": "rows/s",
-                     "ms_per_shard": round(1e3 * elapsed_res / (args.steps * K), 3),
-                     "what": "same steps, traces already in HBM (no H2D)"},
+        "value_basis": ("traces resident in HBM when the timed region starts (the benchmark contract), D2H of "
+                        "each proof inside it; the PCIe-inclusive rate of the same steps (SURVEY.md section 8d's "
+                        "host-trace definition) is `host_traces`"),
+        "host_traces": {"value": round(world * K * rows_per_shard * args.steps / elapsed, 1), "unit": "rows/s",
+                        "ms_per_shard": round(1e3 * elapsed / (args.steps * K), 3),
+                        "vs_resident": round(elapsed / elapsed_res, 3),
+                        "what": "same steps from page-locked host traces: the H2D DMA of each slot's next shard "
+                                "overlaps the current proof, every copy inside the timed span"},
         "h2d_bytes_per_shard": int(sum(v.nbytes for v in traces.values())),
         "host_threads_bound_to": numa,
         "pageable_single_shard_ms": round(pageable_s * 1e3, 3),
@@ -1272,13 +1314,18 @@ def main():
         "stages_ms_per_shard": stages,
         "profiled_region": f"{nprof} single-shard proofs after the timed region (stages, roofline, ntt, serial_ms_per_shard)",
     }
+    if not args.no_sizes and world == 1 and args.workload == "fib":
+        line["sizes"] = size_series(args, prover, K)
     if not args.no_maxshape and world == 1 and args.workload == "fib":
         line["maxshape"] = maxshape_leg(args, rk, n, K)
+    if pool is not None:
+        line["compress"], _ = compress_leg(args, pool, prover.dev)
+        pool.shutdown()
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(args.cpu_log_n, args.queries)
     if args.profile_out:
         with open(args.profile_out, "w") as f:
-            f.write(buf.value.decode())
+            f.write(prof_text)
     print(json.dumps(line), flush=True)
     rk.close()
 

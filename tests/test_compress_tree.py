@@ -1,0 +1,145 @@
+"""Config 5's compress tree (zkmips_amd/compress_tree.py): RecursionShapeConfig::fix_shape
+(crates/recursion/core/src/shape.rs:50-75,115-170), the dependency-driven reduction with witness
+generation in a process pool, and — on the GPU — a node verifying two real MIPS-shard leaves, padded to
+a reference recursion shape, proven byte-identically to the oracle."""
+import multiprocessing as mpc
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+import pytest
+
+from tests import _oracle as O
+from zkmips_amd import compress_tree as CT
+from zkmips_amd import recursion as R
+from zkmips_amd import recursion_verifier as RV
+from zkmips_amd import workloads as W
+
+NQ = 8
+
+
+def test_shapes_are_the_references():
+    # shape.rs:126-166, fastest first; every compress chip named, PublicValues at PUB_VALUES_LOG_HEIGHT
+    names = {c.name for c in R.compress_machine().chips}
+    assert [sorted(s) for s in R.RECURSION_SHAPES] == [sorted(names)] * 3
+    assert R.RECURSION_SHAPES[0]["MemoryVar"] == 18 and R.RECURSION_SHAPES[1]["BatchFRI"] == 19
+    assert R.RECURSION_SHAPES[2]["ExtAlu"] == 19 and all(s["PublicValues"] == 4 for s in R.RECURSION_SHAPES)
+
+
+def test_fix_shape_first_fit():
+    prog = R.program_ext_four_ops(100)
+    h = R.program_heights(prog)
+    assert R.fix_shape(prog) == R.RECURSION_SHAPES[0]
+    # the heights are what generate_traces pads: natural traces have next_pow2 of them
+    _, _, tr, _ = R.shard(prog)
+    for k, v in tr.items():
+        assert v.shape[0] == max(16, 1 << max(0, (h[k] - 1).bit_length())), k
+    # a program needing ExtAlu 2^16 rows skips the fastest shape; 2^20 fits none
+    assert R.fix_shape(prog, [dict(R.RECURSION_SHAPES[0], ExtAlu=4)] + R.RECURSION_SHAPES[1:]) == R.RECURSION_SHAPES[1]
+    with pytest.raises(ValueError):
+        R.fix_shape(prog, [dict(s, ExtAlu=4) for s in R.RECURSION_SHAPES])
+    # padding to the shape keeps the program's proof valid
+    m, prep, tr, pv = R.shard(prog, R.RECURSION_SHAPES[0])
+    assert tr["ExtAlu"].shape[0] == 1 << 15 and tr["MemoryVar"].shape[0] == 1 << 18
+
+
+@pytest.fixture(scope="module")
+def fib_leaves():
+    m, prep, _, _ = W.fib_shard(256, seed=3)
+    pr = O.OracleProver(m, prep, num_queries=NQ)
+    vk = RV.ChildVk.of(m, prep, pr.commit, num_queries=NQ)
+    out = []
+    for s in range(4):
+        _, _, tr, pv = W.fib_shard(256, seed=10 + s)
+        rc, p = pr.prove(tr, pv)
+        assert rc == 0
+        out.append((vk, p))
+    return out
+
+
+def _oracle_prove_factory(nq):
+    cm = R.compress_machine()
+    kw = dict(num_queries=nq, log_blowup=R.COMPRESS_LOG_BLOWUP)
+
+    def prove(wit):
+        prep, traces, pvs, shape, _ = wit
+        pr = O.OracleProver(cm, prep, **kw)
+        rc, p = pr.prove(traces, pvs)
+        assert rc == 0 and pr.verify(p) == 0
+        return CT.compress_child_vk(pr.commit, shape, num_queries=nq), p
+    return prove
+
+
+def _witness_small(children):
+    return CT.node_witness(children, fix=False)
+
+
+def test_tree_with_witness_pool_matches_serial(fib_leaves):
+    """4 leaves -> 3 node proofs: the event-driven reduction (witnesses in a spawn process pool, proofs in
+    2 threads) gives the same root as proving the layers one after another."""
+    prove = _oracle_prove_factory(4)
+    with ProcessPoolExecutor(2, mp_context=mpc.get_context("spawn")) as pool:
+        red = CT.Reducer(lambda ch: pool.submit(_witness_small, ch), prove, inflight=2)
+        root = CT.reduce_serial(fib_leaves, red)
+    a = prove(_witness_small(fib_leaves[:2]))
+    b = prove(_witness_small(fib_leaves[2:]))
+    want = prove(_witness_small([a, b]))
+    assert root[1] == want[1]
+    assert np.array_equal(root[0].commit, want[0].commit)
+
+
+def test_node_rejects_malformed_child(fib_leaves):
+    """Shape checks before the program is built (verifier.rs:248-312): a proof with a dropped query, or
+    claimed for a different verifying key, is a ValueError, not a different program."""
+    vk, proof = fib_leaves[0]
+    import dataclasses
+    with pytest.raises(ValueError):
+        RV.compress_node_program([(dataclasses.replace(vk, num_queries=NQ + 1), proof)])
+    bad_heights = dict(vk.prep_heights)
+    bad_heights["FibTable"] *= 2
+    with pytest.raises(ValueError):
+        RV.compress_node_program([(dataclasses.replace(vk, prep_heights=bad_heights), proof)])
+
+
+def test_ood_check_binds_the_air(fib_leaves):
+    """The out-of-domain check (verifier.rs:316-397): a node whose verifying key describes a different AIR
+    (one constraint constant changed) no longer executes on a valid child proof."""
+    import dataclasses
+    from zkmips_amd import machine as M
+    vk, proof = fib_leaves[0]
+    R.execute(RV.compress_node_program([(vk, proof)]))
+    c = vk.chips["FibCpu"]
+    code = list(c.code)
+    i = code.index(M.OP_CONST)
+    code[i + 1] = (code[i + 1] + 1) % M.P
+    vk2 = dataclasses.replace(vk, chips=dict(vk.chips, FibCpu=dataclasses.replace(c, code=tuple(code))))
+    with pytest.raises(RuntimeError):
+        R.execute(RV.compress_node_program([(vk2, proof)]))
+    # and a node built without the check accepts it (the check is what binds the AIR)
+    R.execute(RV.compress_node_program([(vk2, proof)], ood=False))
+
+
+@pytest.mark.gpu
+def test_gpu_mips_node_reference_shape():
+    """One compress node over two real MIPS leaf proofs (the reference's maximal 2^22 shape scaled to Cpu
+    2^16, 17 chips, 84 queries, proven on the GPU), its program padded to the first fitting
+    RecursionShapeConfig shape: the GPU proof bytes equal the oracle's, and the oracle verifies them."""
+    from zkmips_amd import shapes as SH
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    dev = Device(0)
+    sh = [SH.shape_shard(SH.MAXIMAL_22, seed=s, down=6) for s in (1, 2)]
+    m, prep = sh[0][0], sh[0][1]
+    hp = HipProver(dev, m, prep, num_queries=84)
+    vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=84)
+    leaves = [(vk, hp.prove_shard(s[2], s[3])) for s in sh]
+    prep_c, tr, pv, shape, _ = CT.node_witness(leaves)
+    assert shape in R.RECURSION_SHAPES
+    for k, v in tr.items():
+        assert v.shape[0] == 1 << shape[k], k
+    cm = R.compress_machine()
+    kw = dict(num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    gpu = HipProver(dev, cm, prep_c, **kw).prove_shard(tr, pv)
+    o = O.OracleProver(cm, prep_c, **kw)
+    rc, ref = o.prove(tr, pv)
+    assert rc == 0 and gpu == ref
+    assert o.verify(gpu) == 0

@@ -75,20 +75,23 @@ def test_two_rank_gloo_matches_sequential():
     assert got == seq
 
 
-def _tree_node(layer, j, children):
+def _fake_reducer(calls):
+    """A Reducer whose witness step passes the children through (a thread pool stands in for the process
+    pool) and whose prove step hashes them: the tree's shape decides the root."""
     import hashlib
-    h = hashlib.sha256(f"{layer}:{j}:".encode())
-    for c in children:
-        h.update(len(c).to_bytes(8, "little") + c)
-    return h.digest() * (1 + j % 3)  # ragged proof sizes
+    from concurrent.futures import ThreadPoolExecutor
+    from zkmips_amd.compress_tree import Reducer
+    tp = ThreadPoolExecutor(4)
 
+    def prove(children):
+        h = hashlib.sha256()
+        for _, c in children:
+            h.update(len(c).to_bytes(8, "little") + c)
+        calls.append(1)
+        d = h.digest()
+        return ("vk", d * (1 + d[0] % 3))  # ragged proof sizes
 
-def _tree_serial(leaves):
-    cur, layer = list(leaves), 0
-    while len(cur) > 1:
-        layer += 1
-        cur = [_tree_node(layer, j, cur[2 * j:2 * j + 2]) for j in range((len(cur) + 1) // 2)]
-    return cur[0]
+    return Reducer(lambda ch: tp.submit(lambda: ch), prove, inflight=2)
 
 
 def _tree_worker(rank, world, port, out_q):
@@ -96,25 +99,21 @@ def _tree_worker(rank, world, port, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from zkmips_amd.dist import compress_tree_distributed
-    calls = []
-
-    def node(layer, j, children):
-        calls.append((layer, j))
-        return _tree_node(layer, j, children)
-
+    from zkmips_amd.compress_tree import reduce_distributed
     for nleaves in (64, 5):
-        leaves = [bytes([i]) * (i + 1) for i in range(nleaves)]
-        root = compress_tree_distributed(node, leaves)
-        out_q.put((rank, nleaves, root, list(calls)))
-        calls.clear()
+        calls = []
+        leaves = [("vk", bytes([i]) * (i + 1)) for i in range(nleaves)]
+        root = reduce_distributed(leaves, _fake_reducer(calls))
+        out_q.put((rank, nleaves, root, len(calls)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_compress_tree_distributed(world):
-    """Config 5's layer-by-layer compress tree on `world` gloo ranks: every rank ends with the serial
-    tree's root, each node is proved exactly once, on rank j % world."""
+    """Config 5's dependency-driven compress tree on `world` gloo ranks: every rank ends with the serial
+    tree's root, and each rank proves exactly the nodes it owns (the owner of a node's leftmost leaf), so
+    every node is proven once."""
+    from zkmips_amd.compress_tree import owner, reduce_serial, tree_nodes
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -126,10 +125,11 @@ def test_compress_tree_distributed(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     for nleaves in (64, 5):
-        want = _tree_serial([bytes([i]) * (i + 1) for i in range(nleaves)])
+        calls = []
+        want = reduce_serial([("vk", bytes([i]) * (i + 1)) for i in range(nleaves)], _fake_reducer(calls))
         got = [r for r in res if r[1] == nleaves]
         assert all(r[2] == want for r in got)
-        nodes = sorted(c for r in got for c in r[3])
-        assert len(nodes) == len(set(nodes)) == (63 if nleaves == 64 else 6)
+        nodes = [nd for l in tree_nodes(nleaves) for nd in l]
+        assert sum(r[3] for r in got) == len(nodes) == len(calls) == (63 if nleaves == 64 else 6)
         for r in got:
-            assert all(j % world == r[0] for _, j in r[3])
+            assert r[3] == sum(1 for nd in nodes if owner(nd, nleaves, world) == r[0])

@@ -1,0 +1,30 @@
+"""H2D attribution: run the headline ShardBench in ONE mode (pipelined = host traces with the look-ahead
+DMA, resident = traces in HBM) for a few steps, so that a rocprofv3 kernel trace of each mode can be
+compared kernel by kernel (tools/kdelta.py).
+python tools/h2d_attrib.py {pipelined|resident|per_call} [steps] [log_n]"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def main():
+    mode = sys.argv[1]
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    log_n = int(sys.argv[3]) if len(sys.argv) > 3 else 22
+    args = argparse.Namespace(gpus=None, queries=84, h2d_dst="torch", inflight=3)
+    rk = bench.Ranks(args)
+    sb = bench.ShardBench(args, rk, "fib", 1 << log_n, 3)
+    sb.run_steps(1, mode)
+    _, el = sb.timed(steps, mode)
+    print(f"{mode}: {1e3 * el / (3 * steps):.3f} ms per shard ({steps} steps x 3 in flight)", flush=True)
+    time.sleep(0.1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,337 @@
+"""The compress stage as a dependency-driven tree (BASELINE config 5; crates/prover/src/lib.rs:614-954).
+
+The reference reduces shard proofs two at a time (REDUCE_BATCH_SIZE = 2, lib.rs:111): trace workers build
+and execute each node's recursion program and generate its traces (lib.rs:718-790), prover workers set up
+the program and prove it (`compress_prover.setup(&program)`, `commit`, `open`, lib.rs:806-829), and a node
+enters the queue as soon as its two children exist.  Here:
+
+* witness generation (the node program verifying its children, zkmips_amd/recursion_verifier.py; its
+  execution, RecursionShapeConfig::fix_shape and the traces, zkmips_amd/recursion.py) runs in a process
+  pool, `node_witness`;
+* proving runs on the GPU in `inflight` host threads, each node as soon as its witness lands;
+* a node's witness job is submitted the moment its second child's proof exists, so witness generation of
+  one part of the tree overlaps proving of another (no per-layer barrier).
+
+Across ranks (`reduce_distributed`) node (L, j) belongs to the rank owning its leftmost leaf (leaves are
+dealt in contiguous blocks), so every subtree inside one block is reduced locally with no communication;
+only a node whose right child lives on another rank receives that child's proof, point to point.  The tree
+(which children pair up) is the serial tree's, so the root is the same proof on any number of ranks.
+"""
+from __future__ import annotations
+
+import pickle
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+Node = Tuple[int, int]  # (layer, index); leaves are layer 0
+
+
+def node_witness(children: Sequence[tuple], fix: bool = True):
+    """Worker body (no GPU): the compress node's program from its (ChildVk, proof) children, executed,
+    padded to the first allowed recursion shape (fix=False: natural power-of-two heights, for small
+    tests), as a compress-machine shard.  Returns (prep traces, main traces, public values, shape,
+    seconds)."""
+    from . import recursion as R
+    from . import recursion_verifier as RV
+    t0 = time.perf_counter()
+    prog = RV.compress_node_program(children)
+    t1 = time.perf_counter()
+    shape = R.fix_shape(prog) if fix else {k: max(4, (h - 1).bit_length()) for k, h in R.program_heights(prog).items()}
+    _, prep, traces, pvs = R.shard(prog, shape)
+    t2 = time.perf_counter()
+    return prep, traces, pvs, shape, {"build_s": t1 - t0, "execute_and_traces_s": t2 - t1}
+
+
+_CVK_LOCK = threading.Lock()
+_CVK_CHIPS: Dict[int, dict] = {}
+
+
+def compress_child_vk(commit, shape: Dict[str, int], num_queries: int = None):
+    """The ChildVk of a compress-machine proof from what a parent needs to know of it: the program's
+    preprocessed commitment and its recursion shape (every preprocessed height is 2^shape).  The chip
+    descriptions are the compress machine's (built once per process)."""
+    from . import recursion as R
+    from . import recursion_verifier as RV
+    with _CVK_LOCK:
+        chips = _CVK_CHIPS.get(0)
+        if chips is None:
+            m = R.compress_machine()
+            chips = {"shapes": {c.name: RV.ChipShape.of(c) for c in m.chips}, "num_pv": m.num_pv,
+                     "prep": [c.name for c in m.chips if c.prep_width]}
+            _CVK_CHIPS[0] = chips
+    heights = {k: 1 << shape[k] for k in chips["prep"]}
+    order = sorted(heights, key=lambda k: (-heights[k], k))
+    from .septic import CURVE_CUMULATIVE_SUM_START
+    return RV.ChildVk(chips["shapes"], chips["num_pv"], np.asarray(commit, np.int64), order, heights,
+                      gcs=np.asarray(CURVE_CUMULATIVE_SUM_START, np.int64), log_blowup=R.COMPRESS_LOG_BLOWUP,
+                      num_queries=num_queries or R.COMPRESS_NUM_QUERIES)
+
+
+@dataclass
+class TreeStats:
+    witness_s: float = 0.0            # summed worker seconds (program build + execution + traces)
+    build_s: float = 0.0
+    execute_s: float = 0.0
+    prove_s: float = 0.0              # summed GPU-thread seconds inside prove_shard
+    setup_s: float = 0.0              # zkm_setup of new programs
+    setups: int = 0
+    lookups: int = 0
+    proofs: int = 0
+    shapes: Dict[str, int] = field(default_factory=dict)  # chosen shape -> nodes
+
+
+class GpuProvers:
+    """Proving keys of node programs, looked up by a digest of the preprocessed traces (programs with the
+    same structure share one zkm_setup), as `compress_prover.setup(&program)` (lib.rs:807) would compute
+    the same key for them."""
+
+    def __init__(self, dev, num_queries=None):
+        from . import recursion as R
+        self.dev = dev
+        self.machine = R.compress_machine()
+        self.kw = dict(num_queries=num_queries or R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+        self.cache: Dict[bytes, object] = {}
+        self.lock = threading.Lock()
+
+    def get(self, prep, stats: TreeStats):
+        from .prover import HipProver
+        key = prep_digest(prep)
+        with self.lock:
+            stats.lookups += 1
+            pr = self.cache.get(key)
+            if pr is None:
+                t = time.perf_counter()
+                pr = HipProver(self.dev, self.machine, prep, **self.kw)
+                stats.setup_s += time.perf_counter() - t
+                stats.setups += 1
+                self.cache[key] = pr
+        return pr
+
+
+def prep_digest(prep) -> bytes:
+    """Identity of a program's proving key: xxh3-128 over its preprocessed traces (name, shape, words)."""
+    try:
+        import xxhash
+        h = xxhash.xxh3_128()
+    except ImportError:  # pragma: no cover
+        import hashlib
+        h = hashlib.sha256()
+    for k in sorted(prep):
+        v = prep[k]
+        if v is None:
+            continue
+        h.update(k.encode() + np.asarray(v.shape, np.int64).tobytes())
+        h.update(np.ascontiguousarray(v).view(np.uint8).data)
+    return h.digest()
+
+
+def tree_nodes(n_leaves: int) -> List[List[Node]]:
+    """The serial tree's layers: layer L has ceil(n_{L-1} / 2) nodes; node (L, j) has children
+    (L-1, 2j) and (L-1, 2j + 1) when the latter exists (a last odd node has one child)."""
+    layers, n, L = [], n_leaves, 0
+    while n > 1:
+        L += 1
+        n = (n + 1) // 2
+        layers.append([(L, j) for j in range(n)])
+    return layers
+
+
+def children_of(node: Node, width_below: int) -> List[Node]:
+    L, j = node
+    return [(L - 1, c) for c in (2 * j, 2 * j + 1) if c < width_below]
+
+
+class Reducer:
+    """The event-driven reduction of one rank's part of the tree.
+
+    witness(children) -> concurrent.futures.Future of node_witness's result;
+    prove(witness) -> (child vk, proof bytes) for the parent (GPU, called from `inflight` threads)."""
+
+    def __init__(self, submit_witness: Callable, prove: Callable, inflight: int = 3):
+        self.submit_witness = submit_witness
+        self.prove = prove
+        self.inflight = max(1, inflight)
+        self.events: "queue.Queue" = queue.Queue()
+        self.gpu_q: "queue.Queue" = queue.Queue()
+
+    def _gpu_worker(self):
+        while True:
+            item = self.gpu_q.get()
+            if item is None:
+                return
+            node, wit = item
+            try:
+                self.events.put(("proof", node, self.prove(wit)))
+            except BaseException as e:  # surfaced by the event loop
+                self.events.put(("error", node, e))
+
+    def run(self, done: Dict[Node, tuple], mine: Sequence[Node], widths: Dict[int, int],
+            remote: Optional[Callable] = None, on_done: Optional[Callable] = None) -> Dict[Node, tuple]:
+        """Prove every node in `mine` (a set closed under 'left child'), given `done` (leaves and anything
+        already known).  remote(poll) -> [(node, (vk, proof))] delivers children other ranks prove;
+        on_done(node, result) is called for every node proven here."""
+        pending = set(mine)
+        submitted = set()
+        threads = [threading.Thread(target=self._gpu_worker, daemon=True) for _ in range(self.inflight)]
+        for t in threads:
+            t.start()
+
+        def ready(node):
+            ch = children_of(node, widths[node[0] - 1])
+            return all(c in done for c in ch), ch
+
+        def try_submit():
+            for node in sorted(pending - submitted):
+                ok, ch = ready(node)
+                if ok:
+                    submitted.add(node)
+                    fut = self.submit_witness([done[c] for c in ch])
+                    fut.add_done_callback(lambda f, n=node: self.events.put(("witness", n, f)))
+        try:
+            try_submit()
+            while pending:
+                if remote is not None:
+                    got = remote()
+                    for node, res in got:
+                        done[node] = res
+                    if got:
+                        try_submit()
+                try:
+                    kind, node, val = self.events.get(timeout=0.005 if remote is not None else 60.0)
+                except queue.Empty:
+                    continue
+                if kind == "witness":
+                    self.gpu_q.put((node, val.result()))
+                elif kind == "proof":
+                    done[node] = val
+                    pending.discard(node)
+                    if on_done:
+                        on_done(node, val)
+                    try_submit()
+                else:
+                    raise val
+        finally:
+            for _ in threads:
+                self.gpu_q.put(None)
+            for t in threads:
+                t.join(timeout=60)
+        return done
+
+
+def owner(node: Node, n_leaves: int, world: int) -> int:
+    """The rank that proves node (L, j): the owner of its leftmost leaf j * 2^L, leaves dealt to ranks in
+    contiguous blocks."""
+    L, j = node
+    return min(world - 1, ((j << L) * world) // n_leaves)
+
+
+def reduce_serial(leaves: Sequence[tuple], reducer: Reducer) -> tuple:
+    """The whole tree on one GPU: returns the root's (vk, proof) (a single leaf is its own root)."""
+    layers = tree_nodes(len(leaves))
+    if not layers:
+        return leaves[0]
+    widths = {0: len(leaves)}
+    widths.update({i + 1: len(l) for i, l in enumerate(layers)})
+    done = {(0, i): leaves[i] for i in range(len(leaves))}
+    mine = [n for l in layers for n in l]
+    reducer.run(done, mine, widths)
+    return done[layers[-1][0]]
+
+
+MSG_BYTES = 8 << 20  # fixed point-to-point message: a pickled (vk, proof) of a node (KB-MB)
+
+
+def _pack(obj) -> np.ndarray:
+    raw = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+    if len(raw) + 8 > MSG_BYTES:
+        raise ValueError(f"compress node message of {len(raw)} bytes exceeds {MSG_BYTES}")
+    buf = np.zeros(MSG_BYTES, np.uint8)
+    buf[:8] = np.frombuffer(len(raw).to_bytes(8, "little"), np.uint8)
+    buf[8:8 + len(raw)] = np.frombuffer(raw, np.uint8)
+    return buf
+
+
+def _unpack(buf: np.ndarray):
+    n = int.from_bytes(buf[:8].tobytes(), "little")
+    return pickle.loads(buf[8:8 + n].tobytes())
+
+
+_GLOO = {}
+
+
+def _exchange_group():
+    """Proof messages go over gloo (host memory, KB-MB each): a gloo subgroup when the default group is
+    RCCL, whose p2p receives would otherwise sit on the GPU waiting for the sender."""
+    import torch.distributed as dist
+    if dist.get_backend() == "gloo":
+        return None
+    if "g" not in _GLOO:
+        _GLOO["g"] = dist.new_group(backend="gloo")
+    return _GLOO["g"]
+
+
+def reduce_distributed(leaves: Sequence[tuple], reducer: Reducer, broadcast_root: bool = True):
+    """The tree across the ranks of the default process group (module docstring).  Every rank passes the
+    same leaves; returns the root's (vk, proof) on every rank (broadcast from the rank that proves it), or
+    on the root's owner only with broadcast_root=False (None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    grp = _exchange_group()
+    n = len(leaves)
+    layers = tree_nodes(n)
+    if not layers:
+        return leaves[0]
+    widths = {0: n}
+    widths.update({i + 1: len(l) for i, l in enumerate(layers)})
+    nodes = [nd for l in layers for nd in l]
+    mine = [nd for nd in nodes if owner(nd, n, world) == rank]
+    # children proven elsewhere that my nodes need, and my nodes others need
+    need = [(c, owner(c, n, world)) for nd in mine for c in children_of(nd, widths[nd[0] - 1])
+            if c[0] > 0 and owner(c, n, world) != rank]
+    give = {nd: owner((nd[0] + 1, nd[1] // 2), n, world) for nd in mine
+            if nd[0] < len(layers) and owner((nd[0] + 1, nd[1] // 2), n, world) != rank}
+    done = {(0, i): leaves[i] for i in range(n)}
+    arrived: "queue.Queue" = queue.Queue()
+
+    def receiver(c, buf, work):
+        work.wait()
+        arrived.put((c, _unpack(buf.numpy())))
+    rthreads = []
+    for c, src in need:  # one message per (sender, receiver) pair and node: posted up front, waited in threads
+        buf = torch.empty(MSG_BYTES, dtype=torch.uint8)
+        t = threading.Thread(target=receiver, args=(c, buf, dist.irecv(buf, src=src, group=grp)), daemon=True)
+        t.start()
+        rthreads.append(t)
+    sends = []
+
+    def remote():
+        got = []
+        while True:
+            try:
+                got.append(arrived.get_nowait())
+            except queue.Empty:
+                return got
+
+    def on_done(node, res):
+        if node in give:
+            t = torch.from_numpy(_pack(res))
+            sends.append((t, dist.isend(t, dst=give[node], group=grp)))
+
+    reducer.run(done, mine, widths, remote=remote if need else None, on_done=on_done)
+    for t, w in sends:
+        w.wait()
+    for t in rthreads:
+        t.join(timeout=60)
+    root = layers[-1][0]
+    ro = owner(root, n, world)
+    if not broadcast_root:
+        return done[root] if rank == ro else None
+    obj = [done[root] if rank == ro else None]
+    dist.broadcast_object_list(obj, src=ro, group=grp)
+    return obj[0]

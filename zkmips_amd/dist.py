@@ -126,28 +126,3 @@ def prove_shards_distributed(prove_one: Callable[[int], bytes], num_shards: int,
         if not machine_global_sum_is_zero(proofs):
             raise ValueError("the shards' global cumulative sums do not add up to zero")
     return proofs
-
-
-def compress_tree_distributed(prove_node: Callable[[int, int, Sequence[bytes]], bytes], leaves: Sequence[bytes],
-                              arity: int = 2, device="cpu", prove_nodes=None) -> bytes:
-    """The compress stage across ranks (BASELINE config 5; crates/prover/src/lib.rs:794-858): the leaf
-    proofs are reduced `arity` at a time, layer by layer, until one proof remains.  Node j of a layer is
-    proved on rank j % world by ``prove_node(layer, j, children_proofs)`` (or, for a rank's whole share
-    of a layer at once, e.g. several proofs in flight, ``prove_nodes(layer, [(j, children), ...])`` ->
-    [proof, ...]); the nodes of a layer are independent, so the only exchange is each layer's finished
-    proofs, all-gathered before the next layer (its inputs are the children's proof bytes, which the
-    recursion program verifies).  Returns the root proof on every rank."""
-    import torch.distributed as dist
-    world, rank = dist.get_world_size(), dist.get_rank()
-    if prove_nodes is None:
-        prove_nodes = lambda layer, work: [prove_node(layer, j, ch) for j, ch in work]
-    cur = list(leaves)
-    layer = 0
-    while len(cur) > 1:
-        layer += 1
-        n = (len(cur) + arity - 1) // arity
-        work = [(j, cur[j * arity:(j + 1) * arity]) for j in assign_shards(n, world, rank)]
-        local = dict(zip([j for j, _ in work], prove_nodes(layer, work))) if work else {}
-        allp = gather_proofs(local, device)
-        cur = [allp[j] for j in range(n)]
-    return cur[0]

@@ -106,6 +106,18 @@ def _pow(x: np.ndarray, e: int) -> np.ndarray:
     return r
 
 
+def _pow_vec(x: np.ndarray, e: np.ndarray) -> np.ndarray:
+    """x ** e elementwise (per-element exponents)."""
+    r = np.ones_like(x)
+    b = x.copy()
+    e = np.asarray(e, np.int64).copy()
+    while (e > 0).any():
+        r = np.where(e & 1, _m(r, b), r)
+        b = _m(b, b)
+        e >>= 1
+    return r
+
+
 def ext_inv(a: np.ndarray) -> np.ndarray:
     """a^-1 via a(x) a(-x) = b0 + b2 x^2 and (b0 + b2 y)(b0 - b2 y) = b0^2 - 3 b2^2 in F."""
     conj = a.copy()
@@ -1003,6 +1015,49 @@ def generate_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None
     finish("PublicValues", pa, ma, 1 << PUB_VALUES_LOG_HEIGHT)
     return ({k: np.ascontiguousarray(v.astype(np.uint32)) for k, v in preps.items()},
             {k: np.ascontiguousarray(v.astype(np.uint32)) for k, v in mains.items()})
+
+
+# RecursionShapeConfig::default (crates/recursion/core/src/shape.rs:115-170): the compress programs'
+# allowed shapes (log2 heights), fastest first
+RECURSION_SHAPES = [
+    {"MemoryVar": 18, "Select": 18, "MemoryConst": 16, "BatchFRI": 17, "BaseAlu": 15, "ExtAlu": 15,
+     "ExpReverseBitsLen": 17, "Poseidon2WideDeg3": 16, "PublicValues": PUB_VALUES_LOG_HEIGHT},
+    {"MemoryVar": 19, "Select": 19, "MemoryConst": 17, "BatchFRI": 19, "BaseAlu": 16, "ExtAlu": 16,
+     "ExpReverseBitsLen": 18, "Poseidon2WideDeg3": 17, "PublicValues": PUB_VALUES_LOG_HEIGHT},
+    {"MemoryVar": 20, "Select": 20, "MemoryConst": 18, "BatchFRI": 21, "BaseAlu": 16, "ExtAlu": 19,
+     "ExpReverseBitsLen": 18, "Poseidon2WideDeg3": 18, "PublicValues": PUB_VALUES_LOG_HEIGHT},
+]
+
+
+def program_heights(prog: RecursionProgram) -> Dict[str, int]:
+    """RecursionAir::heights (crates/recursion/core/src/machine.rs): the rows each compress-machine chip
+    needs for the program's instructions, before padding."""
+    n = {k: 0 for k in ("mem", "hint", "base", "ext", "p2", "batchfri", "select", "exprev")}
+    for b in prog.blocks:
+        a = b.a
+        if b.kind == "mem":
+            n["mem"] += len(a["addr"])
+        elif b.kind in ("hint", "base", "ext", "select"):
+            n[b.kind] += len(next(iter(a.values())))
+        elif b.kind == "p2":
+            n["p2"] += a["out"].shape[0]
+        elif b.kind == "batchfri":
+            n["batchfri"] += a["p_at_x"].size
+        elif b.kind == "exprev":
+            n["exprev"] += a["exps"].size
+    return {"MemoryConst": (n["mem"] + 1) // 2, "MemoryVar": (n["hint"] + 1) // 2, "BaseAlu": (n["base"] + 3) // 4,
+            "ExtAlu": (n["ext"] + 3) // 4, "Poseidon2WideDeg3": n["p2"], "BatchFRI": n["batchfri"],
+            "Select": n["select"], "ExpReverseBitsLen": n["exprev"], "PublicValues": 1 << PUB_VALUES_LOG_HEIGHT}
+
+
+def fix_shape(prog: RecursionProgram, shapes=None) -> Dict[str, int]:
+    """RecursionShapeConfig::fix_shape (shape.rs:50-75): the first allowed shape every chip's height fits;
+    an error (the reference panics) when none does."""
+    heights = program_heights(prog)
+    for sh in (shapes or RECURSION_SHAPES):
+        if all(h <= (1 << sh[k]) for k, h in heights.items()):
+            return dict(sh)
+    raise ValueError(f"no recursion shape found for heights: {heights}")
 
 
 def shard(prog: RecursionProgram, shape: Optional[Dict[str, int]] = None, wide: bool = False):

@@ -39,6 +39,7 @@ import numpy as np
 
 from . import recursion as R
 from .machine import P
+from .septic import CURVE_CUMULATIVE_SUM_START as S_CURVE_START
 
 U, PU, D = R.U, R.PU, R.D
 GENERATOR = 3
@@ -162,14 +163,42 @@ def parse_shard_proof(b: bytes) -> ShardProofData:
 
 # ---------------------------------------------------------------- the child's verifying key
 @dataclass(frozen=True)
+class LookupVk:
+    """A local lookup as the constraint folder sees it (permutation.rs:205-347): the kind, the value
+    VirtualPairCols and the multiplicity, each (terms ((is_main, col, weight), ...), constant)."""
+    kind: int
+    values: tuple
+    mult: tuple
+    is_send: bool
+
+
+def _vpc(v) -> tuple:
+    return (tuple((k == "main", int(c), int(w) % P) for k, c, w in v.terms), int(v.constant) % P)
+
+
+@dataclass(frozen=True)
 class ChipShape:
-    """The shape of a chip the verifier needs (a picklable summary of a ChipDesc)."""
+    """What the verifier needs of a chip (a picklable summary of a ChipDesc): its shape, and for the
+    out-of-domain check its constraint program (the blob's postfix code, machine.py) and local lookups."""
     name: str
     prep_width: int
     main_width: int
     perm_width_ef: int
     log_quotient_degree: int
     local_only: bool
+    code: tuple = ()
+    lookups: tuple = ()
+    num_constraints: int = 0
+    commit_scope: int = 0
+
+    @staticmethod
+    def of(c) -> "ChipShape":
+        from .machine import LOOKUP_LOCAL
+        lks = tuple(LookupVk(int(l.kind), tuple(_vpc(v) for v in l.values), _vpc(l.multiplicity), i < len(c.sends))
+                    for i, l in enumerate(c.sends + c.receives) if l.scope == LOOKUP_LOCAL)
+        return ChipShape(c.name, c.prep_width, c.main_width, c.perm_width_ef, c.log_quotient_degree,
+                         bool(c.local_only), tuple(int(x) for x in c.program()), lks, c.num_constraints,
+                         int(c.commit_scope))
 
 
 @dataclass
@@ -193,8 +222,7 @@ class ChildVk:
         from . import septic as S
         prep = {k: v for k, v in prep_traces.items() if v is not None}
         order = sorted(prep, key=lambda k: (-prep[k].shape[0], k))
-        shapes = {c.name: ChipShape(c.name, c.prep_width, c.main_width, c.perm_width_ef, c.log_quotient_degree,
-                                    bool(c.local_only)) for c in machine.chips}
+        shapes = {c.name: ChipShape.of(c) for c in machine.chips}
         return ChildVk(shapes, machine.num_pv, np.asarray(commit, np.int64), order,
                        {k: prep[k].shape[0] for k in prep}, pc_start,
                        np.asarray(S.CURVE_CUMULATIVE_SUM_START if gcs is None else gcs, np.int64), log_blowup,
@@ -439,6 +467,271 @@ class ProgChallenger:
         return int(self.b.ef_from_base4(w)[0])
 
 
+class ExtDag:
+    """Extension-field arithmetic recorded as a DAG and emitted level by level: every node of one depth
+    is one ExtAlu block (the runtime runs a block as one vectorised step), so the thousands of
+    operations of a machine's constraint programs cost as many blocks as the DAG is deep."""
+
+    def __init__(self, b: Builder):
+        self.b = b
+        self.op: List[int] = []
+        self.x: List[int] = []
+        self.y: List[int] = []
+        self.lvl: List[int] = []
+        self.addr: List[int] = []
+        self._leaf: Dict[int, int] = {}
+        self._const: Dict[tuple, int] = {}
+
+    def leaf(self, addr: int) -> int:
+        a = int(addr)
+        n = self._leaf.get(a)
+        if n is None:
+            n = len(self.op)
+            self.op.append(-1), self.x.append(-1), self.y.append(-1), self.lvl.append(0), self.addr.append(a)
+            self._leaf[a] = n
+        return n
+
+    def const(self, v) -> int:
+        return self.leaf(self.b.const(v))
+
+    def _node(self, op, x, y) -> int:
+        n = len(self.op)
+        self.op.append(op), self.x.append(x), self.y.append(y)
+        self.lvl.append(max(self.lvl[x], self.lvl[y]) + 1)
+        self.addr.append(-1)
+        return n
+
+    def add(self, x, y):
+        return self._node(R.OP_ADD, x, y)
+
+    def sub(self, x, y):
+        return self._node(R.OP_SUB, x, y)
+
+    def mul(self, x, y):
+        return self._node(R.OP_MUL, x, y)
+
+    def div(self, x, y):
+        return self._node(R.OP_DIV, x, y)
+
+    def sum(self, xs: List[int]) -> int:
+        xs = list(xs)
+        if not xs:
+            return self.const([0, 0, 0, 0])
+        while len(xs) > 1:  # balanced: depth log2(n)
+            nxt = [self.add(xs[i], xs[i + 1]) for i in range(0, len(xs) - 1, 2)]
+            if len(xs) & 1:
+                nxt.append(xs[-1])
+            xs = nxt
+        return xs[0]
+
+    def prod(self, xs: List[int]) -> int:
+        xs = list(xs)
+        if not xs:
+            return self.const([1, 0, 0, 0])
+        while len(xs) > 1:
+            nxt = [self.mul(xs[i], xs[i + 1]) for i in range(0, len(xs) - 1, 2)]
+            if len(xs) & 1:
+                nxt.append(xs[-1])
+            xs = nxt
+        return xs[0]
+
+    def powers(self, base: int, n: int) -> List[int]:
+        """base^0 .. base^(n-1) at depth ~ 64 + n / 64 (two chains and one product level)."""
+        one = self.const([1, 0, 0, 0])
+        lo = [one]
+        for _ in range(1, min(n, 64)):
+            lo.append(self.mul(lo[-1], base))
+        if n <= 64:
+            return lo[:n]
+        b64 = self.mul(lo[63], base)
+        hi = [one, b64]
+        while len(hi) * 64 < n:
+            hi.append(self.mul(hi[-1], b64))
+        return [lo[k] if k < 64 else self.mul(hi[k >> 6], lo[k & 63]) for k in range(n)]
+
+    def emit(self):
+        """Allocate and append every not-yet-emitted node, one ExtAlu block per depth."""
+        pend = [i for i, a in enumerate(self.addr) if a < 0]
+        if not pend:
+            return
+        by = {}
+        for i in pend:
+            by.setdefault(self.lvl[i], []).append(i)
+        for lv in sorted(by):
+            ids = by[lv]
+            out = self.b.p.alloc(len(ids))
+            for i, a in zip(ids, out):
+                self.addr[i] = int(a)
+            self.b.p.ext_alu(np.asarray([self.op[i] for i in ids], np.int64), out,
+                             np.asarray([self.addr[self.x[i]] for i in ids], np.int64),
+                             np.asarray([self.addr[self.y[i]] for i in ids], np.int64))
+
+    def address(self, n: int) -> int:
+        assert self.addr[n] >= 0, "node not emitted"
+        return self.addr[n]
+
+
+def _chip_constraints(dag: ExtDag, c: ChipShape, prep_l, prep_n, main_l, main_n, perm_l, perm_n, is_first,
+                      is_last, is_trans, pv, alpha_perm, beta_pows, lcs, gcs) -> List[int]:
+    """The chip's constraint values at zeta in folding order (air_eval of the oracle; crates/stark/src/
+    folder.rs:79-102 for the AIR, permutation.rs:205-347 for LogUp, the Global-scope digest rows last)."""
+    out: List[int] = []
+    st: List[int] = []
+    slots: Dict[int, int] = {}
+    code = c.code
+    pc = 0
+    from . import machine as M
+    while pc < len(code):
+        op = code[pc]
+        pc += 1
+        if op == M.OP_MAIN_L:
+            st.append(main_l[code[pc]]); pc += 1
+        elif op == M.OP_MAIN_N:
+            st.append(main_n[code[pc]]); pc += 1
+        elif op == M.OP_PREP_L:
+            st.append(prep_l[code[pc]]); pc += 1
+        elif op == M.OP_PREP_N:
+            st.append(prep_n[code[pc]]); pc += 1
+        elif op == M.OP_CONST:
+            st.append(dag.const(code[pc] % P)); pc += 1
+        elif op == M.OP_PV:
+            st.append(pv[code[pc]]); pc += 1
+        elif op == M.OP_IS_FIRST:
+            st.append(is_first)
+        elif op == M.OP_IS_LAST:
+            st.append(is_last)
+        elif op == M.OP_IS_TRANS:
+            st.append(is_trans)
+        elif op in (M.OP_ADD, M.OP_SUB, M.OP_MUL):
+            y = st.pop()
+            x = st.pop()
+            st.append(dag.add(x, y) if op == M.OP_ADD else dag.sub(x, y) if op == M.OP_SUB else dag.mul(x, y))
+        elif op == M.OP_NEG:
+            st.append(dag.sub(dag.const(0), st.pop()))
+        elif op == M.OP_EMIT:
+            out.append(st.pop())
+        elif op == M.OP_LET:
+            slots[code[pc]] = st.pop(); pc += 1
+        elif op == M.OP_GET:
+            st.append(slots[code[pc]]); pc += 1
+        else:
+            raise ValueError(f"bad opcode {op} in the constraint program of {c.name}")
+    if c.lookups:
+        def vpc(v):
+            terms, k = v
+            acc = [dag.const(k)] if k else []
+            for is_main, col, w in terms:
+                x = main_l[col] if is_main else prep_l[col]
+                acc.append(x if w == 1 else dag.mul(x, dag.const(w)))
+            return dag.sum(acc) if acc else dag.const(0)
+        batch = 1 << c.log_quotient_degree
+        nb = c.perm_width_ef - 1
+        for bi in range(nb):
+            rlcs, ms = [], []
+            for lk in c.lookups[bi * batch:(bi + 1) * batch]:
+                terms = [dag.add(alpha_perm, dag.const(lk.kind))]
+                for v, val in enumerate(lk.values):
+                    terms.append(dag.mul(beta_pows[v], vpc(val)))
+                rlcs.append(dag.sum(terms))
+                m = vpc(lk.mult)
+                ms.append(m if lk.is_send else dag.sub(dag.const(0), m))
+            prod = dag.prod(rlcs)
+            num = dag.sum([dag.mul(dag.prod([r for j, r in enumerate(rlcs) if j != i]), ms[i]) for i in range(len(rlcs))])
+            out.append(dag.sub(dag.mul(prod, perm_l[bi]), num))
+        sum_l, sum_n = dag.sum(perm_l[:nb]), dag.sum(perm_n[:nb])
+        phi_l, phi_n = perm_l[nb], perm_n[nb]
+        out.append(dag.mul(dag.sub(phi_l, sum_l), is_first))
+        out.append(dag.mul(dag.sub(dag.sub(phi_n, phi_l), sum_n), is_trans))
+        out.append(dag.mul(dag.sub(phi_l, lcs), is_last))
+    if c.commit_scope == 1:
+        w = c.main_width
+        for i in range(7):
+            out.append(dag.mul(dag.sub(main_l[w - 14 + i], gcs[i]), is_last))
+            out.append(dag.mul(dag.sub(main_l[w - 7 + i], gcs[7 + i]), is_last))
+    if len(out) != c.num_constraints:
+        raise ValueError(f"{c.name}: {len(out)} constraint values, the vk says {c.num_constraints}")
+    return out
+
+
+def _zp_base(log_n: int, shift: int, x: int) -> int:
+    """Z of the coset shift * H_(2^log_n) at a base-field point: (x / shift)^(2^log_n) - 1."""
+    return (pow(x * pow(shift, P - 2, P) % P, 1 << log_n, P) - 1) % P
+
+
+def verify_constraints(b: Builder, vk: ChildVk, p: ShardProofData, chips: List[ChipShape], opened, zeta: int,
+                       alpha: int, perm_ch, pv, lcs_words, gcs_words):
+    """The out-of-domain check (crates/stark/src/verifier.rs:316-397; recursion/circuit/src/stark.rs:
+    246-432 / constraints.rs:39-196 in the reference's recursion program): for every chip, its folded
+    constraints at zeta times 1/Z_H(zeta) equal the quotient recombined from the opened chunks, and the
+    chips' local cumulative sums add to zero.  `opened[name]` holds the hinted EF addresses of the
+    chip's opened values: prep/main/perm at zeta and at g*zeta, and the quotient chunks."""
+    dag = ExtDag(b)
+    zl = dag.leaf(zeta)
+    al = dag.leaf(alpha)
+    ap, bp = dag.leaf(perm_ch[0]), dag.leaf(perm_ch[1])
+    max_ln = max(o.log_degree for o in p.chips)
+    zsq = [zl]  # zeta^(2^k)
+    for _ in range(max_ln):
+        zsq.append(dag.mul(zsq[-1], zsq[-1]))
+    one = dag.const([1, 0, 0, 0])
+    mono = [dag.const([1 if e == k else 0 for e in range(4)]) for k in range(4)]
+    max_nc = max((c.num_constraints for c in chips), default=1)
+    apows = dag.powers(al, max(1, max_nc))
+    max_vals = max((len(lk.values) for c in chips for lk in c.lookups), default=0)
+    bpows = dag.powers(bp, max_vals + 1)[1:] if max_vals else []
+    pv_n = [dag.leaf(a) for a in pv]
+    checks = []
+    lcs_all = []
+    for i, (c, o) in enumerate(zip(chips, p.chips)):
+        ln = o.log_degree
+        op = opened[c.name]
+        prep_l = [dag.leaf(a) for a in op["prep_l"]]
+        prep_n = [dag.leaf(a) for a in op["prep_n"]]
+        main_l = [dag.leaf(a) for a in op["main_l"]]
+        main_n = [dag.leaf(a) for a in op["main_n"]]
+        pl_w = [dag.leaf(a) for a in op["perm_l"]]
+        pn_w = [dag.leaf(a) for a in op["perm_n"]]
+        perm_l = [dag.sum([dag.mul(mono[e], pl_w[4 * k + e]) for e in range(4)]) for k in range(c.perm_width_ef)]
+        perm_n = [dag.sum([dag.mul(mono[e], pn_w[4 * k + e]) for e in range(4)]) for k in range(c.perm_width_ef)]
+        lw = [dag.leaf(a) for a in lcs_words[i]]
+        lcs = dag.sum([dag.mul(mono[e], lw[e]) for e in range(4)])
+        lcs_all.append(lcs)
+        gcs = [dag.leaf(a) for a in gcs_words[i]]
+        ginv = pow(two_adic_gen(ln), P - 2, P)
+        zh = dag.sub(zsq[ln], one)
+        is_first = dag.div(zh, dag.sub(zl, one))
+        is_last = dag.div(zh, dag.sub(zl, dag.const(ginv)))
+        is_trans = dag.sub(zl, dag.const(ginv))
+        vals = _chip_constraints(dag, c, prep_l, prep_n, main_l, main_n, perm_l, perm_n, is_first, is_last, is_trans,
+                                 pv_n, ap, bpows, lcs, gcs)
+        nc = len(vals)
+        folded = dag.sum([dag.mul(apows[nc - 1 - k], v) for k, v in enumerate(vals)])
+        # recompute_quotient (verifier.rs:400-436): chunk a's domain is the coset g_a H_n, g_a = 3 w_Q^a
+        nq = 1 << c.log_quotient_degree
+        wq = two_adic_gen(ln + c.log_quotient_degree)
+        shifts = [GENERATOR * pow(wq, a, P) % P for a in range(nq)]
+        chunks = []
+        for a in range(nq):
+            fac = []
+            for bb in range(nq):
+                if bb == a:
+                    continue
+                # zp_b(zeta) = zeta^n * shift_b^-n - 1, divided by zp_b(shift_a) (a base constant)
+                sbn = pow(pow(shifts[bb], P - 2, P), 1 << ln, P)
+                num = dag.sub(dag.mul(zsq[ln], dag.const(sbn)), one)
+                fac.append(dag.mul(num, dag.const(pow(_zp_base(ln, shifts[bb], shifts[a]), P - 2, P))))
+            qw = [dag.leaf(x) for x in op["quot"][a]]
+            chunk = dag.sum([dag.mul(mono[e], qw[e]) for e in range(4)])
+            chunks.append(dag.mul(dag.prod(fac), chunk) if fac else chunk)
+        quotient = dag.sum(chunks)
+        checks.append((c.name, dag.div(folded, zh), quotient))
+    total_lcs = dag.sum(lcs_all)
+    dag.emit()
+    for name, lhs, rhs in checks:
+        b.assert_eq_ext([dag.address(lhs)], [dag.address(rhs)], f"ood evaluation {name}")
+    b.assert_eq_ext([dag.address(total_lcs)], [int(b.const([0, 0, 0, 0]))], "local cumulative sum")
+
+
 def _verify_batch(b: Builder, root, mats: List[dict], ridx: np.ndarray, ridx_bits: np.ndarray, paths: np.ndarray):
     """MerkleTreeMmcs::verify_batch (fri.rs:363-400) for every query: mats = [{height, rows (q, w) addrs}] in
     commit order; ridx_bits (q, L) the row index bits; paths (q, L, 8) sibling addresses; root 8 addresses."""
@@ -465,15 +758,54 @@ def _verify_batch(b: Builder, root, mats: List[dict], ridx: np.ndarray, ridx_bit
     b.assert_eq_base(node, np.broadcast_to(np.asarray(root, np.int64), node.shape), "merkle root")
 
 
-def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optional[Builder] = None):
-    """Append the verification of one child ShardProof (module docstring).  Returns the address of the
-    transcript's final state word 0 (a digest of everything the child's proof committed to)."""
+def check_shape(vk: ChildVk, p: ShardProofData):
+    """verify_opening_shape and the proof-shape checks the reference's verifier makes before the transcript
+    (verifier.rs:248-312, fri.rs): the chip set and widths against the vk, preprocessed heights, query and
+    FRI round counts, Merkle path lengths.  Raises ValueError (the program's structure is derived from the
+    proof, so a malformed proof must be rejected here, not turned into a different program)."""
+    if len(p.chips) != len(p.names) or len(set(p.names)) != len(p.names):
+        raise ValueError("chip ordering does not match the opened values")
+    for name, o in zip(p.names, p.chips):
+        c = vk.chips.get(name)
+        if c is None:
+            raise ValueError(f"chip {name} is not in the verifying key")
+        if (o.prep_l.shape[0] != c.prep_width or o.main_l.shape[0] != c.main_width
+                or o.perm_l.shape[0] != 4 * c.perm_width_ef or o.quot.shape[0] != 1 << c.log_quotient_degree
+                or not 0 <= o.log_degree <= 24):
+            raise ValueError(f"{name}: opening shape")
+        if name in vk.prep_heights and (1 << o.log_degree) != vk.prep_heights[name]:
+            raise ValueError(f"{name}: height differs from its preprocessed trace")
+        if (not c.local_only and (o.main_n.shape[0] != c.main_width or o.prep_n.shape[0] != c.prep_width)):
+            raise ValueError(f"{name}: next-row opening shape")
+    for name in vk.prep_order:
+        if name not in p.names:
+            raise ValueError(f"preprocessed chip {name} missing from the shard")
+    if len(p.queries) != vk.num_queries:
+        raise ValueError("query count")
+    log_max = len(p.fri_commits) + vk.log_blowup
+    if log_max > 25 or max(o.log_degree for o in p.chips) + vk.log_blowup != log_max:
+        raise ValueError("FRI round count does not match the tallest trace")
+    for inputs, steps in p.queries:
+        if len(inputs) != 4 or len(steps) != len(p.fri_commits):
+            raise ValueError("query proof shape")
+        for off, (_, path) in enumerate(steps):
+            if path.shape[0] != log_max - 1 - off:
+                raise ValueError("FRI commit-phase path length")
+        for rows, path in inputs:
+            if path.shape[0] > log_max:
+                raise ValueError("input opening path length")
+
+
+def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optional[Builder] = None,
+                 ood: bool = True):
+    """Append the verification of one child ShardProof (module docstring).  Returns the addresses of the
+    transcript's final state words 0..7 (a digest of everything the child's proof committed to)."""
     b = b or Builder(prog)
     p = parse_shard_proof(proof)
+    check_shape(vk, p)
     rp = replay(vk, p)
     lb, nq = vk.log_blowup, vk.num_queries
     chips = [vk.chips[n] for n in p.names]
-    assert len(p.queries) == nq and len(p.chips) == len(chips)
     ch = ProgChallenger(b)
     # observe_into: vk commit, pc_start, initial global sum, 0 -- constants of the program
     ch.observe([b.const(int(v)) for v in list(vk.commit) + [vk.pc_start] + list(vk.gcs) + [0]])
@@ -481,11 +813,20 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
     ch.observe(pv[:vk.num_pv])
     main_c, perm_c, quot_c = b.hint_base(p.main_c), b.hint_base(p.perm_c), b.hint_base(p.quot_c)
     ch.observe(main_c)
-    ch.sample_ef(), ch.sample_ef()
+    perm_ch = (ch.sample_ef(), ch.sample_ef())
     ch.observe(perm_c)
-    for c in p.chips:
-        ch.observe(b.hint_base(np.concatenate([c.lcs, c.gcs])))
-    ch.sample_ef()
+    lcs_words, gcs_words = [], []
+    start = [int(b.const(int(v))) for v in S_CURVE_START]
+    for c, cs in zip(p.chips, chips):
+        sums = b.hint_base(np.concatenate([c.lcs, c.gcs]))
+        ch.observe(sums)
+        lcs_words.append(sums[:4])
+        gcs_words.append(sums[4:])
+        if cs.commit_scope == 0:  # verifier.rs: a Local-scope chip's global sum is the zero digest
+            b.assert_eq_base(sums[4:], np.asarray(start, np.int64), f"{cs.name} global sum")
+        if not cs.lookups:  # no local lookups: no local sum
+            b.assert_zero_base(sums[:4], f"{cs.name} local sum")
+    alpha = ch.sample_ef()
     ch.observe(quot_c)
     zeta = ch.sample_ef()
     fa = ch.sample_ef()
@@ -550,10 +891,26 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
             hm.append((m["log_n"], m["width"], pts))
         rounds_host.append(hm)
     fri_pairs = host_fri_pairs(vk, p, rp, rounds_host)
-    # hinted opened values at the points (shared by the queries)
+    # hinted opened values at the points (shared by the queries and the out-of-domain check)
     for _, ms in rounds:
         for m in ms:
             m["pts"] = [(z, b.hint_ext(np.asarray(vals, np.int64).reshape(-1, 4))) for z, vals in m["pts"]]
+    if ood:
+        none = np.zeros(0, np.int64)
+        opened = {c.name: {"prep_l": none, "prep_n": none, "quot": []} for c in chips}
+        for name, m in zip(vk.prep_order, rounds[0][1]):
+            opened[name]["prep_l"] = m["pts"][0][1]
+            opened[name]["prep_n"] = m["pts"][1][1] if len(m["pts"]) > 1 else none
+        for c, mm, pm in zip(chips, rounds[1][1], rounds[2][1]):
+            d = opened[c.name]
+            d["main_l"], d["main_n"] = mm["pts"][0][1], (mm["pts"][1][1] if len(mm["pts"]) > 1 else none)
+            d["perm_l"], d["perm_n"] = pm["pts"][0][1], pm["pts"][1][1]
+        qi = 0
+        for c in chips:
+            for _ in range(1 << c.log_quotient_degree):
+                opened[c.name]["quot"].append(rounds[3][1][qi]["pts"][0][1])
+                qi += 1
+        verify_constraints(b, vk, p, chips, opened, zeta, alpha, perm_ch, pv, lcs_words, gcs_words)
     # alpha powers per height (counter per log height, fri.rs:155-203)
     counts: Dict[int, int] = {}
     for _, ms in rounds:
@@ -631,70 +988,115 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
             folded = b.ext(R.OP_ADD, folded, b.ext(R.OP_MUL, np.full(nq, bsq, np.int64), ro[lfh]))
         x = b.base(R.OP_MUL, x, x)
     b.assert_eq_ext(folded, np.full(nq, final, np.int64), "final fold = final poly")
-    return int(ch.st[0])
+    return np.asarray(ch.st[:8], np.int64)
+
+
+def _bitrev_arr(v: np.ndarray, bits: int) -> np.ndarray:
+    r = np.zeros_like(v)
+    for i in range(bits):
+        r |= ((v >> i) & 1) << (bits - 1 - i)
+    return r
+
+
+def _base_dot_ef(rows: np.ndarray, ef: np.ndarray) -> np.ndarray:
+    """sum_c rows[q, c] * ef[c] mod p for every q: (nq, w) canonical base values x (w, 4) EF -> (nq, 4).
+    The EF words are split into 16-bit halves so that a uint64 matmul cannot overflow (w < 2^15)."""
+    rows = np.asarray(rows, U)
+    lo, hi = ef & U(0xFFFF), ef >> U(16)
+    a = (rows @ lo) % PU
+    b = (rows @ hi) % PU
+    return (a + _m_u(b, U(1 << 16))) % PU
+
+
+def _m_u(a, b):
+    return (a * b) % PU
 
 
 def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> List[List[tuple]]:
     """The verifier's reduced openings and folds on the host (fri.rs:155-203, :247-361), per query the
     (e0, e1) leaf pair of every commit-phase round: the pair the program hashes (as hinted base words)
-    and recomposes against its own in-program fold."""
+    and recomposes against its own in-program fold.  Vectorised over the queries: per matrix and point
+    the reduced opening is A - B[q] with A = sum_c alpha^c p_c(z) (query-independent) and
+    B[q] = sum_c alpha^c p_c(x_q) (a base x EF dot product), divided by (z - x_q)."""
     lb, log_max = vk.log_blowup, rp.log_max
-    fa = rp.fri_alpha
-    apow = [[1, 0, 0, 0]]
-    out = []
-    for qn in range(len(p.queries)):
-        idx = rp.index_samples[qn] & ((1 << log_max) - 1)
-        ro: Dict[int, list] = {}
-        lhp: Dict[int, int] = {}
-        for t, ms in enumerate(rounds_host):
-            rows = p.queries[qn][0][t][0]
-            for k, (log_n, width, pts) in enumerate(ms):
-                lh = log_n + lb
-                row = (idx >> (log_max - lh)) & ((1 << lh) - 1)
-                x = GENERATOR * pow(two_adic_gen(lh), int(format(row, f"0{lh}b")[::-1], 2) if lh else 0, P) % P
-                for z, vals in pts:
-                    acc = [0, 0, 0, 0]
-                    for c in range(width):
-                        pw = lhp.get(lh, 0)
-                        lhp[lh] = pw + 1
-                        while len(apow) <= pw:
-                            apow.append(ef_mul(apow[-1], fa))
-                        acc = ef_add(acc, ef_mul(apow[pw], ef_sub([int(v) for v in vals[c]], ef_base(int(rows[k][c])))))
-                    term = ef_mul(acc, ef_inv(ef_sub(z, ef_base(x))))
-                    ro[lh] = ef_add(ro.get(lh, [0, 0, 0, 0]), term)
-        folded = ro[log_max]
-        x = pow(two_adic_gen(log_max), int(format(idx, f"0{log_max}b")[::-1], 2), P)
-        pairs = []
-        for off, (sib, _) in enumerate(p.queries[qn][1]):
-            bit = (idx >> off) & 1
-            sib = [int(v) for v in sib]
-            e0, e1 = (sib, folded) if bit else (folded, sib)
-            pairs.append((e0, e1))
-            xn = (P - x) % P
-            x0, x1 = (xn, x) if bit else (x, xn)
-            t_ = ef_mul(ef_sub(rp.betas[off], ef_base(x0)), ef_mul(ef_sub(e1, e0), ef_base(pow((x1 - x0) % P, P - 2, P))))
-            folded = ef_add(e0, t_)
-            lfh = log_max - 1 - off
-            if lfh in ro:
-                folded = ef_add(folded, ef_mul(ef_mul(rp.betas[off], rp.betas[off]), ro[lfh]))
-            x = x * x % P
-        if folded != [int(v) for v in p.final_poly]:
-            raise ValueError(f"FRI query {qn}: the folds do not reach the final polynomial (invalid child proof)")
-        out.append(pairs)
-    return out
+    nq = len(p.queries)
+    fa = np.asarray(rp.fri_alpha, U)
+    idx = np.asarray(rp.index_samples, np.int64) & ((1 << log_max) - 1)
+    total = {}
+    for ms in rounds_host:
+        for log_n, width, pts in ms:
+            total[log_n + lb] = total.get(log_n + lb, 0) + width * len(pts)
+    npow = max(total.values()) if total else 0
+    apow = np.zeros((max(npow, 1), 4), U)
+    apow[0, 0] = 1
+    for k in range(1, npow):
+        apow[k] = R.ext_mul(apow[k - 1], fa)
+    ro: Dict[int, np.ndarray] = {}
+    lhp: Dict[int, int] = {}
+    for t, ms in enumerate(rounds_host):
+        for k, (log_n, width, pts) in enumerate(ms):
+            lh = log_n + lb
+            row = (idx >> (log_max - lh)) & ((1 << lh) - 1)
+            g = np.full(nq, two_adic_gen(lh), U)
+            x = _m_u(R._pow_vec(g, _bitrev_arr(row, lh)), U(GENERATOR)) if lh else np.full(nq, GENERATOR, U)
+            rows = np.stack([np.asarray(p.queries[qn][0][t][0][k], np.int64) for qn in range(nq)]) if width else None
+            for z, vals in pts:
+                pw = lhp.get(lh, 0)
+                lhp[lh] = pw + width
+                if width:
+                    al = apow[pw:pw + width]
+                    A = R.ext_mul(al, np.asarray(vals, U) % PU).sum(axis=0) % PU
+                    B = _base_dot_ef(rows, al)
+                    acc = (A[None, :] + PU - B) % PU
+                else:
+                    acc = np.zeros((nq, 4), U)
+                zx = np.broadcast_to(np.asarray(z, U) % PU, (nq, 4)).copy()
+                zx[:, 0] = (zx[:, 0] + PU - x) % PU
+                term = R.ext_mul(acc, R.ext_inv(zx))
+                ro[lh] = term if lh not in ro else (ro[lh] + term) % PU
+    folded = ro[log_max]
+    x = R._pow_vec(np.full(nq, two_adic_gen(log_max), U), _bitrev_arr(idx, log_max))
+    pairs = [[] for _ in range(nq)]
+    for off, _ in enumerate(p.queries[0][1]):
+        bit = ((idx >> off) & 1).astype(bool)
+        sib = np.stack([np.asarray(p.queries[qn][1][off][0], U) for qn in range(nq)])
+        e0 = np.where(bit[:, None], sib, folded)
+        e1 = np.where(bit[:, None], folded, sib)
+        for qn in range(nq):
+            pairs[qn].append(([int(v) for v in e0[qn]], [int(v) for v in e1[qn]]))
+        xn = (PU - x) % PU
+        x0, x1 = np.where(bit, xn, x), np.where(bit, x, xn)
+        inv = R._pow(((x1 + PU - x0) % PU).astype(U), P - 2)
+        beta = np.asarray(rp.betas[off], U)
+        bx = np.broadcast_to(beta, (nq, 4)).copy()
+        bx[:, 0] = (bx[:, 0] + PU - x0) % PU
+        d = (e1 + PU - e0) % PU
+        t_ = R.ext_mul(bx, _m_u(d, inv[:, None]))
+        folded = (e0 + t_) % PU
+        lfh = log_max - 1 - off
+        if lfh in ro:
+            b2 = R.ext_mul(beta[None, :], beta[None, :])
+            folded = (folded + R.ext_mul(np.broadcast_to(b2, (nq, 4)), ro[lfh])) % PU
+        x = _m_u(x, x)
+    fp = np.asarray(p.final_poly, U)
+    bad = np.nonzero((folded != fp[None, :]).any(axis=1))[0]
+    if len(bad):
+        raise ValueError(f"FRI query {int(bad[0])}: the folds do not reach the final polynomial (invalid child proof)")
+    return pairs
 
 
-def compress_node_program(children: Sequence[tuple]) -> R.RecursionProgram:
+def compress_node_program(children: Sequence[tuple], ood: bool = True) -> R.RecursionProgram:
     """A compress node (prover/src/lib.rs:614-954): verify every child (ChildVk, proof bytes) and commit
     public values whose digest (RecursionPublicValues.digest) is a Poseidon2 hash of the children's
     transcript states -- a node's public values commit to what its children committed to."""
     prog = R.RecursionProgram()
     b = Builder(prog)
-    states = [verify_shard(prog, vk, proof, b) for vk, proof in children]
+    if not children:
+        raise ValueError("a compress node needs at least one child")
+    states = [verify_shard(prog, vk, proof, b, ood=ood) for vk, proof in children]
     zero = b.const(0)
-    x = np.full(R.WIDTH, zero, np.int64)
-    x[:len(states)] = states[:R.WIDTH]
-    digest = b.p2(x[None, :])[0, :R.DIGEST_SIZE]
+    # the children's full 8-word transcript states, absorbed by the sponge (PaddingFreeSponge, any count)
+    digest = b.sponge(np.concatenate(states)[None, :])[0, :R.DIGEST_SIZE]
     pv = np.full(R.PROOF_MAX_NUM_PVS, zero, np.int64)
     pv[R.PV_DIGEST_START:R.PV_DIGEST_START + R.DIGEST_SIZE] = digest
     prog.commit_public_values(pv)
