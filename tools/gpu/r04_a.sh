@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 O=gpurun_out
-timeout -k 10 700 python3 -u bench.py --steps 10 --warmup 2 > $O/r04a_bench.log 2>&1 || { tail -30 $O/r04a_bench.log; exit 1; }
+timeout -k 10 700 python3 -u bench.py --steps 10 --warmup 2 --no-compress > $O/r04a_bench.log 2>&1 || { tail -30 $O/r04a_bench.log; exit 1; }
 tail -1 $O/r04a_bench.log | cut -c1-400
 for mode in resident pipelined; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/r04a_kt_$mode -o run -- \
@@ -32,4 +32,9 @@ timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --output-
 if grep -q 'TA_BUSY_avr' $R/r04a_counters.txt && grep -q 'TA_TA_BUSY' $R/r04a_counters.txt; then
   timeout -s KILL 90 rocprofv3 --pmc TA_BUSY_avr TA_BUFFER_READ_WAVEFRONTS_sum --output-format csv -d $R/r04a_pmc5 -o run -- python3 /tmp/ldeb.py > $R/r04a_pmc5.log 2>&1 || { tail -5 $R/r04a_pmc5.log; exit 1; }
 fi
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_compress_tree.py -m gpu > $O/r04a_gpu_compress_test.log 2>&1 || { tail -30 $O/r04a_gpu_compress_test.log; exit 1; }
+tail -3 $O/r04a_gpu_compress_test.log
+timeout -k 10 500 python3 -u bench.py --workload compress --no-cpu-baseline > $O/r04a_compress.log 2>&1 || { tail -30 $O/r04a_compress.log; exit 1; }
+tail -1 $O/r04a_compress.log | cut -c1-600
 echo done

@@ -1565,6 +1565,8 @@ def _execute(prog, regs, shard, max_steps, state=None):
                 state["exit_code"] = bv
             elif sid == SY.COMMIT:
                 commits[bv] = cv
+            elif sid == SY.COMMIT_DEFERRED_PROOFS:  # syscalls/commit.rs: deferred_proofs_digest[idx]
+                commits[("deferred", bv)] = cv
             elif code in SY.PRECOMPILES or SY.is_linux(code):
                 pm = SY.PrecompileMemory(mem, mem_init, mem_last, cpu_first, cpu_done, shard, _mem_word,
                                          regs, last, reg_start, reg_done)
@@ -1773,7 +1775,10 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
     pvs[PV_NEXT_PC] = int(npc[-1])  # where the program left off (its end, a jump out of it, or 0 on HALT)
     pvs[PV_EXECUTION_SHARD] = shard
     for idx, word in sysinfo["commits"].items():  # COMMIT: committed_value_digest[idx] (syscalls/commit.rs)
-        pvs[4 * idx:4 * idx + 4] = A._bytes(np.asarray([word], np.uint32))[0]
+        if isinstance(idx, tuple):  # COMMIT_DEFERRED_PROOFS: deferred_proofs_digest[idx]
+            pvs[SY.PV_DEFERRED + idx[1]] = word
+        else:
+            pvs[4 * idx:4 * idx + 4] = A._bytes(np.asarray([word], np.uint32))[0]
     if halt.any():
         pvs[PV_EXIT_CODE] = int(bv[halt][0])
     prep_traces = {"Program": prep, "Byte": A.byte_prep_trace()}
