@@ -541,32 +541,49 @@ class Ranks:
             dist.destroy_process_group()
 
 
-def execution_bench(args):
-    """BASELINE configs 3/4: a whole execution proven shard by shard.  `sha2`: the guest
-    (mips_core.sha_program) hashes `--sha-blocks` 64-byte blocks with SHA_EXTEND + SHA_COMPRESS, COMMITs
-    and HALTs; the execution splits into CPU shards of 2^log_n-ish rows, SHA_EXTEND and SHA_COMPRESS
-    precompile shards and the memory shard.  Every step proves all of them (traces resident in HBM,
-    `--inflight` shards concurrently per GPU); with N ranks the shards are dealt by cost
-    (dist.deal_by_cost), the proofs gathered to rank 0 and the machine-level global sum checked there."""
-    import threading
+def _tendermint_job(outdir: str):
+    """Pool worker (no GPU): the tendermint guest on the reference's blocks executed and traced
+    (zkmips_amd/tendermint.tendermint_shards), the traces written as .npy files under outdir (a
+    /dev/shm directory the bench process memory-maps).  Returns (chip names per shard, info, seconds)."""
+    from zkmips_amd import tendermint as T
+    t0 = time.perf_counter()
+    shards, info = T.tendermint_shards()
+    gen_s = time.perf_counter() - t0
+    meta = []
+    for i, (_, prep, tr, pv) in enumerate(shards):
+        for k, v in tr.items():
+            np.save(os.path.join(outdir, f"s{i}_{k}.npy"), v)
+        np.save(os.path.join(outdir, f"s{i}__pv.npy"), pv)
+        meta.append(sorted(tr))
+    for k, v in shards[0][1].items():
+        if v is not None:
+            np.save(os.path.join(outdir, f"prep_{k}.npy"), v)
+    info = {k: (v.hex() if isinstance(v, bytes) else v) for k, v in info.items()}
+    return meta, info, gen_s
+
+
+def _load_tendermint(outdir: str, meta):
     from zkmips_amd import mips_core as MC
+    m = MC.core_machine()
+    prep = {c.name: np.load(os.path.join(outdir, f"prep_{c.name}.npy"))
+            for c in m.chips if os.path.exists(os.path.join(outdir, f"prep_{c.name}.npy"))}
+    run = [(m, prep, {k: np.load(os.path.join(outdir, f"s{i}_{k}.npy")) for k in names},
+            np.load(os.path.join(outdir, f"s{i}__pv.npy"))) for i, names in enumerate(meta)]
+    return run
+
+
+def prove_execution(args, rk, run, steps: int, warmup: int):
+    """Configs 3/4: every shard of one execution proven (traces resident in HBM, `--inflight` shards at once
+    per GPU, largest first); with N ranks the shards are dealt by cost (dist.deal_by_cost), the proofs
+    gathered to rank 0 and the machine-level global cumulative sum checked there (machine.rs:639-654).
+    Returns (seconds per execution, proofs on rank 0, rows per shard, shard kinds, the deal)."""
+    import threading
     from zkmips_amd.dist import deal_by_cost, prove_shards_distributed, shard_cost
     from zkmips_amd.proof import machine_global_sum_is_zero
-    rk = Ranks(args, bind=False)
     world, rank = rk.world, rk.rank
-    t0 = time.time()
-    max_steps = min((1 << args.log_n) * 4 // 5, (1 << 24) // 5 - 1)
-    if args.workload == "tendermint":
-        from zkmips_amd import mips_edwards as ED
-        prog = ED.ed25519_program(args.sigs, seed=1, sha_blocks=args.tm_sha_blocks)
-    else:
-        prog = MC.sha_program(args.sha_blocks, seed=1)
-    run = MC.program_shards(prog, seed=1, shard_size=max_steps, precompile_events_per_shard=args.sha_events_per_shard)
-    gen_s = time.time() - t0
-    print(f"{args.workload}: {len(run)} shards generated in {gen_s:.1f} s", file=sys.stderr, flush=True)
     costs = [shard_cost(tr) for _, _, tr, _ in run]
     deal = deal_by_cost(costs, world)
-    mine = deal[rank]  # configs 3/4: the execution's shards dealt across ranks, largest first
+    mine = deal[rank]
     if rk.replay:
         prove_one = lambda i: open(os.path.join(rk.replay, f"shard_{i}.bin"), "rb").read()
     else:
@@ -576,13 +593,14 @@ def execution_bench(args):
         m, prep, _, _ = run[0]
         prep = {k: v for k, v in prep.items() if v is not None}
         prover = HipProver(Device(rk.local_rank), m, prep, num_queries=args.queries)
-        dev = {i: ({k: torch.from_numpy(v.view(np.int32)).cuda() for k, v in run[i][2].items()}, run[i][3])
-               for i in mine}
+        dev = {i: ({k: torch.from_numpy(np.ascontiguousarray(v).view(np.int32)).cuda() for k, v in run[i][2].items()},
+                   run[i][3]) for i in mine}
         prove_one = lambda i: prove_resident(prover, dev[i][0], dev[i][1])
     rows = [max(v.shape[0] for v in tr.values()) for _, _, tr, _ in run]
     kinds = ["cpu" if "Cpu" in tr else "memory" if "MemoryGlobalInit" in tr else "sha_extend" if "ShaExtend" in tr
              else "sha_compress" if "ShaCompress" in tr else "ed_add" if "EdAddAssign" in tr
-             else "ed_decompress" if "EdDecompress" in tr else "precompile" for _, _, tr, _ in run]
+             else "ed_decompress" if "EdDecompress" in tr else "uint256_mul" if "Uint256MulMod" in tr
+             else "precompile" for _, _, tr, _ in run]
     rk.sync()
 
     def prove_local():
@@ -608,8 +626,6 @@ def execution_bench(args):
         return out
 
     def prove_all():
-        """Every rank proves its shards; rank 0 receives all proofs in shard order (one gather, RCCL
-        over xGMI) and checks the machine-level global cumulative sum (machine.rs:639-654)."""
         if world == 1:
             out = prove_local()
             proofs = [out[i] for i in range(len(run))]
@@ -619,26 +635,67 @@ def execution_bench(args):
         return prove_shards_distributed(lambda i: local[i], len(run), device=rk.coll_dev, check_global_sum=True,
                                         costs=costs)
 
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         proofs = prove_all()
-        print("sha2: warmup execution proven", file=sys.stderr, flush=True)
     rk.barrier()
     t1 = time.time()
-    for _ in range(args.steps):
+    for _ in range(steps):
         proofs = prove_all()
     rk.barrier()
     el = rk.max_over_ranks(time.time() - t1)
-    what = (f"tendermint-shaped execution: {args.sigs} ed25519 signature verifications (ED_DECOMPRESS of A and R, "
-            f"[S]B and R + [k]A by ED_ADD double-and-add, compared) + {args.tm_sha_blocks} SHA-256 blocks"
+    return el / steps, proofs, rows, kinds, deal
+
+
+def tendermint_leg(args, pool_result, outdir, rk):
+    """Config 4 as a field of the default line: the tendermint guest on examples/tendermint's two blocks
+    (traces generated in the witness pool while the GPU legs ran), every shard proven, global sum checked."""
+    meta, info, gen_s = pool_result
+    run = _load_tendermint(outdir, meta)
+    sec, proofs, rows, kinds, _ = prove_execution(args, rk, run, 1, 1)
+    return {"metric": "shard trace rows proved/sec (tendermint light-client execution on the reference's blocks, "
+                      "BASELINE config 4)",
+            "value": round(sum(rows) / sec, 1), "unit": "rows/s", "ms_per_execution": round(1e3 * sec, 3),
+            "shards": len(run), "shard_rows": [f"{k} 2^{r.bit_length() - 1}" for k, r in zip(kinds, rows)],
+            "rows_per_execution": sum(rows), "proof_bytes": sum(len(p) for p in proofs),
+            "global_sum_checked": True, "exit_code": info["exit_code"],
+            "public_values_digest_matches_host": info["pv_digest"] == info["expected_digest"],
+            "votes_verified": info["votes"], "trace_generation_s": round(gen_s, 1),
+            "workload": "examples/tendermint guest restated (zkmips_amd/tendermint.py) on block_2279100.json -> "
+                        "block_2279130.json: both header hashes (SHA-256 Merkle), three validator-set hashes, "
+                        "100 vote signatures (SHA-512 in MIPS, ED_DECOMPRESS/ED_ADD, k mod L by UINT256_MUL), "
+                        "voting-power thresholds, public-values digest committed"}
+
+
+def execution_bench(args):
+    """BASELINE configs 3/4 as their own bench line: a whole execution proven shard by shard.  `sha2`: the
+    guest (mips_core.sha_program) hashes `--sha-blocks` 64-byte blocks with SHA_EXTEND + SHA_COMPRESS;
+    `tendermint`: the light-client check of examples/tendermint on the reference's two block fixtures
+    (zkmips_amd/tendermint.py).  See prove_execution."""
+    from zkmips_amd import mips_core as MC
+    rk = Ranks(args, bind=False)
+    world, rank = rk.world, rk.rank
+    t0 = time.time()
+    info = None
+    if args.workload == "tendermint":
+        from zkmips_amd import tendermint as T
+        run, info = T.tendermint_shards()
+    else:
+        max_steps = min((1 << args.log_n) * 4 // 5, (1 << 24) // 5 - 1)
+        prog = MC.sha_program(args.sha_blocks, seed=1)
+        run = MC.program_shards(prog, seed=1, shard_size=max_steps, precompile_events_per_shard=args.sha_events_per_shard)
+    gen_s = time.time() - t0
+    print(f"{args.workload}: {len(run)} shards generated in {gen_s:.1f} s", file=sys.stderr, flush=True)
+    sec, proofs, rows, kinds, deal = prove_execution(args, rk, run, args.steps, args.warmup)
+    what = ("tendermint light-client check on the reference's blocks 2279100 -> 2279130 (100 vote signatures)"
             if args.workload == "tendermint" else f"sha2-precompile execution: {args.sha_blocks} blocks")
     line = {
-        "metric": ("shard trace rows proved/sec (whole tendermint-shaped execution, BASELINE config 4)"
+        "metric": ("shard trace rows proved/sec (whole tendermint execution, BASELINE config 4)"
                    if args.workload == "tendermint" else
                    "shard trace rows proved/sec (whole sha2-precompile execution, BASELINE config 3)"),
-        "value": round(sum(rows) * args.steps / el, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True,
+        "value": round(sum(rows) / sec, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * sec, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
-        "data": ("synthetic tendermint-shaped guest (mips_edwards.ed25519_program: real RFC 8032 signatures)"
+        "data": ("examples/tendermint/host/files block fixtures (zkmips_amd/tendermint.py)"
                  if args.workload == "tendermint" else "synthetic sha2 guest (mips_core.sha_program)")
                 + ", traces resident in HBM"
                 + (" (REPLAYED proofs: launch/deal/gather rehearsal, nothing proven)" if rk.replay else ""),
@@ -652,6 +709,9 @@ def execution_bench(args):
                        "(global sum checked there)" if world > 1 else ""),
                    "trace_generation_s": round(gen_s, 1), "global_sum_checked": True},
     }
+    if info:
+        line["config"]["exit_code"] = info["exit_code"]
+        line["config"]["public_values_digest"] = info["pv_digest"].hex()
     if rank == 0:
         print(json.dumps(line), flush=True)
     rk.close()
@@ -770,12 +830,13 @@ def start_witness_pool(n: int):
 def mips_leaves(dev, queries: int, n_leaves: int = 64, distinct: int = 4, down: int = 6):
     """Config 5's leaves: core shard proofs of MIPS shards in the reference's maximal 2^22 shape scaled to
     Cpu 2^(22-down) (all 17 chips of maximal_shapes.json["22"][2], zkmips_amd/shapes.py), proven on this
-    GPU before the timed region; `distinct` different executions, dealt cyclically to the leaves."""
+    GPU before the timed region; `distinct` executions of one program (one proving key) from different
+    initial registers, dealt cyclically to the leaves."""
     from zkmips_amd import recursion_verifier as RV
     from zkmips_amd import shapes as SH
     from zkmips_amd.prover import HipProver
     t0 = time.perf_counter()
-    shards = [SH.shape_shard(SH.MAXIMAL_22, seed=1 + i, down=down) for i in range(distinct)]
+    shards = SH.shape_shards(SH.MAXIMAL_22, [1 + i for i in range(distinct)], down=down)
     gen_s = time.perf_counter() - t0
     m, prep = shards[0][0], shards[0][1]
     hp = HipProver(dev, m, prep, num_queries=queries)
@@ -1118,8 +1179,6 @@ def main():
                     help="memory type of the HBM buffers the pipelined H2D copies land in")
     ap.add_argument("--sha-events-per-shard", type=int, default=16384,
                     help="sha2 workload: precompile calls per precompile shard")
-    ap.add_argument("--sigs", type=int, default=32, help="tendermint workload: ed25519 signatures verified")
-    ap.add_argument("--tm-sha-blocks", type=int, default=256, help="tendermint workload: SHA-256 blocks hashed")
     ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2", "tendermint", "tracegen", "compress"],
                     default="fib",
                     help="fib: S-SHARD FibCpu (the headline config); alu: MIPS ALU slice (AddSub, Bitwise, Lt, "
@@ -1136,6 +1195,8 @@ def main():
     ap.add_argument("--maxshape-steps", type=int, default=4)
     ap.add_argument("--no-compress", action="store_true",
                     help="skip the default line's compress leg (config 5: 64 MIPS leaves, 63 node proofs)")
+    ap.add_argument("--no-tendermint", action="store_true",
+                    help="skip the default line's config-4 leg (the tendermint guest on the reference's blocks)")
     ap.add_argument("--no-sizes", action="store_true",
                     help="skip the default line's size series (resident rows/s and LDE time at 2^20, 2^21, 2^23)")
     ap.add_argument("--leaf-log", type=int, default=16, help="compress leg: MIPS leaf shards in the maximal shape scaled to Cpu 2^leaf_log rows")
@@ -1160,10 +1221,14 @@ def main():
     if args.workload == "compress":
         return compress_bench(args)
     # the default line's compress leg (config 5): its witness pool starts before the GPU is touched
-    pool = None
-    if (not args.no_compress and args.workload == "fib" and int(os.environ.get("WORLD_SIZE", "1")) == 1
-            and not args.pmc_child):
+    pool = tm_future = tm_dir = None
+    if (not (args.no_compress and args.no_tendermint) and args.workload == "fib"
+            and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.pmc_child):
         pool = start_witness_pool(max(1, min(args.node_workers, 32)))
+        if not args.no_tendermint:  # config 4's traces are generated on the host while the GPU legs run
+            import tempfile
+            tm_dir = tempfile.mkdtemp(prefix="zkm_tm_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+            tm_future = pool.submit(_tendermint_job, tm_dir)
 
     import torch
     rk = Ranks(args)
@@ -1318,8 +1383,15 @@ def main():
         line["sizes"] = size_series(args, prover, K)
     if not args.no_maxshape and world == 1 and args.workload == "fib":
         line["maxshape"] = maxshape_leg(args, rk, n, K)
-    if pool is not None:
+    if pool is not None and not args.no_compress:
         line["compress"], _ = compress_leg(args, pool, prover.dev)
+    if tm_future is not None:
+        import shutil
+        try:
+            line["tendermint"] = tendermint_leg(args, tm_future.result(), tm_dir, rk)
+        finally:
+            shutil.rmtree(tm_dir, ignore_errors=True)
+    if pool is not None:
         pool.shutdown()
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(args.cpu_log_n, args.queries)

@@ -127,7 +127,7 @@ def test_gpu_mips_node_reference_shape():
     from zkmips_amd._lib import Device
     from zkmips_amd.prover import HipProver
     dev = Device(0)
-    sh = [SH.shape_shard(SH.MAXIMAL_22, seed=s, down=6) for s in (1, 2)]
+    sh = SH.shape_shards(SH.MAXIMAL_22, [1, 2], down=6)
     m, prep = sh[0][0], sh[0][1]
     hp = HipProver(dev, m, prep, num_queries=84)
     vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=84)

@@ -280,7 +280,7 @@ def pop_field_op(a: Sequence[int], b: Sequence[int], op: str, fp: FieldParams, m
         lhs, rhs, mode = r, b, "add"
     elif op == "div":
         assert all(y or not x for x, y in zip(a, b)), "division by zero is allowed only when dividing zero"
-        r = [x * pow(y, m - 2, m) % m if y else 0 for x, y, m in zip(a, b, mods)]
+        r = [x * pow(y, -1, m) % m if y else 0 for x, y, m in zip(a, b, mods)]
         lhs, rhs, mode = r, b, "mul"
     else:
         lhs, rhs, mode = a, b, op
@@ -312,7 +312,7 @@ def pop_den(a: Sequence[int], b: Sequence[int], sign: bool, fp: FieldParams):
     r, carry = [], []
     for x, y in zip(a, b):
         den = ((y if sign else p - y) + 1) % p
-        res = x * pow(den, p - 2, p) % p
+        res = x * pow(den, -1, p) % p
         lhs = y * res + res if sign else y * res + x
         rhs = x if sign else res
         r.append(res)

@@ -1130,7 +1130,19 @@ def _jump_trace(jumps):
     return t
 
 
+_CORE_MACHINE = []
+
+
 def core_machine() -> MachineDesc:
+    """The MIPS machine (its chip descriptions are built once per process: the precompile AIRs take seconds
+    to assemble; callers get their own chip list)."""
+    if not _CORE_MACHINE:
+        _CORE_MACHINE.append(_build_core_machine())
+    m = _CORE_MACHINE[0]
+    return MachineDesc(list(m.chips), m.num_pv)
+
+
+def _build_core_machine() -> MachineDesc:
     # MipsAir::get_airs_and_costs order (crates/core/machine/src/mips/mod.rs:207-437): Cpu, Program, the
     # precompiles, SyscallCore/Precompile, the ALUs, Branch, Jump, SyscallInstrs, MemoryInstrs, MiscInstrs,
     # the memory chips, Global, Byte, (SysLinux,) MovCond

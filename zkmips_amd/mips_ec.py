@@ -409,7 +409,7 @@ def sw_add(curve: str, p, q):
     m = FIELDS[curve].modulus
     (x1, y1), (x2, y2) = p, q
     assert (x1, y1) != (x2, y2), "points are the same: use sw_double"
-    s = (y2 - y1) % m * pow((x2 - x1) % m, m - 2, m) % m
+    s = (y2 - y1) % m * pow((x2 - x1) % m, -1, m) % m
     x3 = (s * s - x1 - x2) % m
     return x3, (s * (x1 - x3) - y1) % m
 
@@ -418,7 +418,7 @@ def sw_double(curve: str, p):
     """AffinePoint::sw_double (weierstrass/mod.rs:204-240)."""
     m = FIELDS[curve].modulus
     x1, y1 = p
-    s = (CURVE_A[curve] + 3 * x1 * x1) % m * pow(2 * y1 % m, m - 2, m) % m
+    s = (CURVE_A[curve] + 3 * x1 * x1) % m * pow(2 * y1 % m, -1, m) % m
     x3 = (s * s - 2 * x1) % m
     return x3, (s * (x1 - x3) - y1) % m
 

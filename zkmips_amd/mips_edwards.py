@@ -207,7 +207,7 @@ def ed_add_points(p, q):
     x3n = (x1 * y2 + y1 * x2) % ED_P
     y3n = (y1 * y2 + x1 * x2) % ED_P
     dxy = ED_D * (x1 * y1 % ED_P * x2 % ED_P * y2) % ED_P
-    return (x3n * pow((1 + dxy) % ED_P, ED_P - 2, ED_P) % ED_P, y3n * pow((1 - dxy) % ED_P, ED_P - 2, ED_P) % ED_P)
+    return (x3n * pow((1 + dxy) % ED_P, -1, ED_P) % ED_P, y3n * pow((1 - dxy) % ED_P, -1, ED_P) % ED_P)
 
 
 def ed_decompress_point(y: int, sign: int):
@@ -215,7 +215,7 @@ def ed_decompress_point(y: int, sign: int):
     yy = y * y % ED_P
     u = (yy - 1) % ED_P
     v = (yy * ED_D + 1) % ED_P
-    x = ed25519_sqrt(u * pow(v, ED_P - 2, ED_P) % ED_P)
+    x = ed25519_sqrt(u * pow(v, -1, ED_P) % ED_P)
     return ((ED_P - x) % ED_P if sign else x), y
 
 

@@ -135,6 +135,19 @@ def shape_shard(shape: dict, seed: int = 1, down: int = 0, fill: float = 0.8, ca
     return m, prep, pad_to_shape(m, traces, sh), pvs
 
 
+def shape_shards(shape: dict, seeds, down: int = 0, fill: float = 0.8):
+    """Several CPU shards of ONE program (one proving key, as the shards of one ELF's executions share it)
+    padded to `shape`: the program of shape_shard(seeds[0]) run from the initial registers of each seed, so
+    the traces differ while the preprocessed Program table is the same."""
+    sh = scaled(shape, down)
+    prog = shape_program(sh, seeds[0], fill=fill)
+    out = []
+    for s in seeds:
+        m, prep, traces, pvs = C.program_shard(prog, s, 1, (1 << 24) // 5 - 1)
+        out.append((m, prep, pad_to_shape(m, traces, sh), pvs))
+    return out
+
+
 # maximal_shapes.json["22"][2] (crates/core/machine/src/shape/maximal_shapes.json; tests/golden pins it):
 # Cpu 22 / AddSub 21 / Lt, MemoryInstrs, Bitwise 20 / Branch, ShiftRight 19 / ShiftLeft 18 / Global 17 /
 # MemoryLocal, MovCond 14 / Jump 6 / Mul, SyscallInstrs, SyscallCore 1

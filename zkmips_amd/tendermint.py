@@ -841,11 +841,14 @@ class Ed25519:
         _xor_acc(a, self.acc, y_ptr=self.pr, n=16)
 
 
-def tendermint_program(trusted: dict, untrusted: dict) -> Tuple[List[tuple], dict]:
+def tendermint_program(trusted: dict, untrusted: dict, votes: Optional[slice] = None,
+                       tamper: Optional[int] = None) -> Tuple[List[tuple], dict]:
     """The guest of examples/tendermint (module docstring) for the two light blocks: MIPS instructions for
     this repository's executor (mips_core).  ACC (r31) collects every failed comparison; the exit code is
     ACC, so a verifying execution halts with 0.  Returns (program, expected) with the public values the
-    reference host expects (header hash 1 || header hash 2 || CBOR verdict) and their SHA-256 digest."""
+    reference host expects (header hash 1 || header hash 2 || CBOR verdict) and their SHA-256 digest.
+    Tests only: `votes` restricts the signature checks to a slice of the votes (the voting-power thresholds
+    are then skipped), `tamper` flips a bit of that vote's signature."""
     from . import mips_core as MC
     from . import mips_syscall as SY
     a = Asm(MC.DATA_BASE + 0x1000)
@@ -879,11 +882,15 @@ def tendermint_program(trusted: dict, untrusted: dict) -> Tuple[List[tuple], dic
     t_keys = [base64.b64decode(v["pub_key"]["value"]) for v in trusted["next_validator_set"]["validators"]]
     t_index = {k: i for i, k in enumerate(t_keys)}
     tal = a.alloc(2)  # the two tallies live in memory (SHA-512 uses every spare register)
-    votes = signed_votes(untrusted)
+    full = votes is None
+    votes = signed_votes(untrusted)[votes if votes is not None else slice(None)]
     sig_bufs = []
-    for v in votes:
+    for n, v in enumerate(votes):
         sp = a.alloc(16)
-        a.store_words(sp, _le_words(v["sig"]))
+        sig = bytearray(v["sig"])
+        if tamper is not None and n == tamper:
+            sig[33] ^= 0x10  # in S: R stays a curve point, [S]B no longer equals R + [k]A
+        a.store_words(sp, _le_words(bytes(sig)))
         sig_bufs.append(sp)
     a.sw(0, 0, tal)
     a.sw(0, 0, tal + 4)
@@ -894,7 +901,7 @@ def tendermint_program(trusted: dict, untrusted: dict) -> Tuple[List[tuple], dic
         hash_at = (20, hh[1]) if v["commit"] else None
         if v["commit"]:
             assert m[14:16] == b"\x0a\x20" and m[16:48] == bytes.fromhex(commit["block_id"]["hash"])
-        ed.verify(uv.keys[i], sp, mw, hash_at)
+        ed.verify(uv.keys[i], sp, mw, hash_at)  # the signature as input, R || S
         if v["commit"]:
             for k, (pw, idx) in enumerate(((uv.powers_ptr, i), (tn.powers_ptr, t_index.get(v["pub"])))):
                 if idx is None:
@@ -907,7 +914,7 @@ def tendermint_program(trusted: dict, untrusted: dict) -> Tuple[List[tuple], dic
                 a.sw(t[1], 0, tal + 4 * k)
     # thresholds: 3 tallied > 2 total (untrusted), 3 trusted_tallied > trusted_total (trust level 1/3)
     for pw, n, k, num in ((uv.powers_ptr, len(untrusted["validator_set"]["validators"]), 0, 2),
-                          (tn.powers_ptr, len(trusted["next_validator_set"]["validators"]), 1, 1)):
+                          (tn.powers_ptr, len(trusted["next_validator_set"]["validators"]), 1, 1)) if full else ():
         reg = t[7]
         a.lw(reg, 0, tal + 4 * k)
         a.li(t[2], 0)
@@ -960,3 +967,29 @@ def tendermint_program(trusted: dict, untrusted: dict) -> Tuple[List[tuple], dic
 
 def _sha512_tail(msg: bytes) -> bytes:
     return msg + b"\x80" + b"\0" * ((111 - len(msg)) % 128) + (8 * len(msg)).to_bytes(16, "big")
+
+
+def tendermint_shards(shard_size: int = 1 << 21, precompile_events_per_shard: int = 1 << 14, seed: int = 1):
+    """The whole execution of the tendermint guest on the reference's two blocks as continuation shards
+    (mips_core.program_shards: CPU shards, the SHA_EXTEND / SHA_COMPRESS / ED_ADD / ED_DECOMPRESS /
+    UINT256_MUL precompile shards, the memory shard).  Returns (shards, info); info carries the expected
+    public-values digest, which the last CPU shard's committed digest must equal (checked here), and the
+    exit code (0: every check of the guest held)."""
+    from . import mips_alu as A
+    from . import mips_core as MC
+    trusted, untrusted = load_block(2279100), load_block(2279130)
+    prog, exp = tendermint_program(trusted, untrusted)
+    shards = MC.program_shards(prog, seed=seed, shard_size=shard_size,
+                               precompile_events_per_shard=precompile_events_per_shard)
+    cpu = [s for s in shards if "Cpu" in s[2]]
+    last = cpu[-1][3]
+    words = [int.from_bytes(bytes(int(b) for b in last[4 * i:4 * i + 4]), "little") for i in range(8)]
+    digest = b"".join(w.to_bytes(4, "little") for w in words)
+    info = {"exit_code": int(last[MC.PV_EXIT_CODE]), "pv_digest": digest, "expected_digest": exp["digest"],
+            "votes": exp["votes"], "public_values": exp["public_values"], "program_len": len(prog),
+            "shards": len(shards)}
+    if info["exit_code"] != 0 or digest != exp["digest"]:
+        raise ValueError(f"tendermint guest failed: exit {info['exit_code']}, digest {digest.hex()} vs "
+                         f"{exp['digest'].hex()}")
+    del A
+    return shards, info
