@@ -926,6 +926,180 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
     }
 }
 
+// Two-column form of k_ntt_s9b: the same 512-row x 32-column tile and nine stages, but each thread holds
+// 8 rows of TWO adjacent columns (lane t' = tid & 15 -> columns c0 + 2t', c0 + 2t' + 1; u = tid >> 4 ->
+// one radix-8 network per column in the layouts LL / LM / LH with g = u), so every data and twiddle access
+// is one 8-byte buffer op (the twiddles of adjacent columns are adjacent in the table) and the LDS exchanges
+// are 8-byte: half the vector-memory and LDS instructions of k_ntt_s9b for the same bytes.  LDS rows are
+// stored at row ^ bit3(row) (a permutation of the tile's rows), so the two rows a 32-lane half touches in
+// every layout fall in different halves of the 64 banks.
+namespace s9 {
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 bld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+}
+__device__ __forceinline__ void bst2(u32x2 v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, 0);
+}
+__device__ __forceinline__ uint32_t atc(uint32_t r, uint32_t c) { return (r ^ ((r >> 3) & 1)) * 32 + c; }
+template <int LAY>
+__device__ __forceinline__ uint32_t row0c(uint32_t u) {
+    if constexpr (LAY == LH) return u;
+    else if constexpr (LAY == LM) return (u >> 3) * 64 + (u & 7);
+    else return 8 * u;
+}
+// three stages of the radix-8 networks of both columns; twiddle pair at voff + soff0 + (rs (span + m)) S4
+template <bool DIT, int LAY>
+__device__ __forceinline__ void net8c(uint32_t *v0, uint32_t *v1, __amdgpu_buffer_rsrc_t rtw, uint32_t voff,
+                                      uint32_t S4) {
+    constexpr uint32_t rs = RS<LAY>;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const int st = DIT ? q : 2 - q;
+        const int span = 1 << st;
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+            const u32x2 w = bld2(rtw, voff, (rs * (uint32_t)(span + m)) * S4);
+#pragma unroll
+            for (int k = m; k < 8; k += 2 * span) {
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    uint32_t *v = c ? v1 : v0;
+                    const uint32_t wc = c ? w.y : w.x;
+                    const uint32_t a = v[k], b = v[k + span];
+                    if (DIT) {
+                        const uint32_t tt = mul(b, wc);
+                        if (q < 2 && ((k >> (st + 1)) & 1)) {
+                            v[k] = a + tt;
+                            v[k + span] = a + (P - tt);
+                        } else {
+                            v[k] = add(a, tt);
+                            v[k + span] = sub(a, tt);
+                        }
+                    } else {
+                        v[k] = add(a, b);
+                        v[k + span] = mul(a + (P - b), wc);
+                    }
+                }
+            }
+        }
+    }
+}
+template <int LAY>
+__device__ __forceinline__ void to_ldsc(uint32_t *x, const uint32_t *v0, const uint32_t *v1, uint32_t u, uint32_t c) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        u32x2 p;
+        p.x = v0[k];
+        p.y = v1[k];
+        *(u32x2 *)&x[atc(row0c<LAY>(u) + RS<LAY> * k, c)] = p;
+    }
+}
+template <int LAY>
+__device__ __forceinline__ void from_ldsc(const uint32_t *x, uint32_t *v0, uint32_t *v1, uint32_t u, uint32_t c) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const u32x2 p = *(const u32x2 *)&x[atc(row0c<LAY>(u) + RS<LAY> * k, c)];
+        v0[k] = p.x;
+        v1[k] = p.y;
+    }
+}
+}  // namespace s9
+
+template <bool DIT, int MODE>
+__global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9c(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+                                                        int logS, const uint32_t *__restrict__ tw,
+                                                        uint32_t tw_words, uint32_t nv, int remap) {
+    using namespace s9;
+    __shared__ uint32_t x[512 * 32];
+    const uint32_t S = 1u << logS, S4 = S * 4;
+    const uint32_t total = gridDim.x, lin = blockIdx.x;
+    const uint32_t vid = (total & 7) ? lin : (lin & 7) * (total >> 3) + (lin >> 3);
+    const uint32_t ntile = total / nv;
+    const uint32_t col = remap ? vid % nv : lin / ntile, tile = remap ? vid / nv : lin % ntile;
+    const uint32_t outer = tile >> (logS - 5);
+    const uint32_t c0 = (tile & ((S >> 5) - 1)) * 32;
+    const uint32_t base = outer * 512u * S;
+    const uint32_t c = 2 * (threadIdx.x & 15), u = threadIdx.x >> 4;
+    const uint32_t ct = c0 + c;
+    const auto rsrc = mkrs(src + ms.off(col) + base, 512u * S4);
+    const auto rtw = mkrs(tw, tw_words * 4);
+    const uint32_t vLL = ct * 4, vLM = ((u & 7) * S + ct) * 4, vLH = (u * S + ct) * 4;
+    const uint32_t vL8 = (8 * u * S + ct) * 4;  // rows 8u + k
+    uint32_t v0[8], v1[8];
+    if (DIT) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const u32x2 p = bld2(rsrc, vL8, (uint32_t)k * S4);
+            v0[k] = p.x;
+            v1[k] = p.y;
+        }
+        net8c<true, LL>(v0, v1, rtw, vLL, S4);
+        to_ldsc<LL>(x, v0, v1, u, c);
+        __syncthreads();
+        from_ldsc<LM>(x, v0, v1, u, c);
+        net8c<true, LM>(v0, v1, rtw, vLM, S4);
+        __syncthreads();
+        to_ldsc<LM>(x, v0, v1, u, c);
+        __syncthreads();
+        from_ldsc<LH>(x, v0, v1, u, c);
+        net8c<true, LH>(v0, v1, rtw, vLH, S4);
+        if (MODE == MODE_PLAIN) {
+            const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                u32x2 p;
+                p.x = v0[k];
+                p.y = v1[k];
+                bst2(p, rdst, vLH, (uint32_t)(64 * k) * S4);
+            }
+        } else {  // BITREV_OUT through the swizzled tile of k_ntt_s9b
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t r = row0c<LH>(u) + 64 * k;
+                x[atb<true>(r, c)] = v0[k];
+                x[atb<true>(r, c + 1)] = v1[k];
+            }
+            __syncthreads();
+            const auto rdst = mkrs(dst + md.off(col), 512u * S4);
+            const uint32_t q = threadIdx.x & 511, hb = threadIdx.x >> 9, rq = rev_bits(q, 9);
+            const uint32_t vo = (((rev_bits(c0, logS) + (hb << (logS - 1))) << 9) + q) * 4;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t tc = 2 * i + hb;
+                const uint32_t so = (rev_bits((uint32_t)(2 * i), 5) << (logS - 5)) << 11;
+                bst(x[atb<true>(rq, tc)], rdst, vo, so);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const u32x2 p = bld2(rsrc, vLH, (uint32_t)(64 * k) * S4);
+            v0[k] = p.x;
+            v1[k] = p.y;
+        }
+        net8c<false, LH>(v0, v1, rtw, vLH, S4);
+        to_ldsc<LH>(x, v0, v1, u, c);
+        __syncthreads();
+        from_ldsc<LM>(x, v0, v1, u, c);
+        net8c<false, LM>(v0, v1, rtw, vLM, S4);
+        __syncthreads();
+        to_ldsc<LM>(x, v0, v1, u, c);
+        __syncthreads();
+        from_ldsc<LL>(x, v0, v1, u, c);
+        net8c<false, LL>(v0, v1, rtw, vLL, S4);
+        const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            u32x2 p;
+            p.x = v0[k];
+            p.y = v1[k];
+            bst2(p, rdst, vL8, (uint32_t)k * S4);
+        }
+    }
+}
+
 // Persistent form of k_ntt_s9b: each workgroup walks the (tile, column) work items w = blockIdx.x,
 // blockIdx.x + gridDim.x, ... (gridDim.x a multiple of 8, so item w stays on XCD w mod 8 as in k_ntt_s9b's
 // remap), and issues the next item's 16 loads into a second register set before the current item's
@@ -1084,6 +1258,24 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
             else
                 hipLaunchKernelGGL((k_ntt_s9p<true, MODE_BITREV_OUT>), gp, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
                                    tw, tw_words, nv, total);
+            HIP_CHECK(hipGetLastError());
+            return;
+        }
+        // two-column tiles (8-byte accesses): ZKM_NTT_S9C=0 selects the one-column k_ntt_s9b (A/B knob)
+        static const int s9c = [] {
+            const char *e = getenv("ZKM_NTT_S9C");
+            return e ? atoi(e) : 0;
+        }();
+        if (s9c) {
+            if (!DIT)
+                hipLaunchKernelGGL((k_ntt_s9c<false, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                                   tw_words, nv, remap);
+            else if (mode == MODE_PLAIN)
+                hipLaunchKernelGGL((k_ntt_s9c<true, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                                   tw_words, nv, remap);
+            else
+                hipLaunchKernelGGL((k_ntt_s9c<true, MODE_BITREV_OUT>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
+                                   tw, tw_words, nv, remap);
             HIP_CHECK(hipGetLastError());
             return;
         }
