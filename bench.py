@@ -875,6 +875,7 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
         prep, traces, pvs, shape, times = wit
         pr = provers.get(prep, stats)
         t = time.perf_counter()
+        traces = CT.materialize(traces)  # the Poseidon2 trace built on the device from its inputs
         proof = pr.prove_shard(traces, pvs)
         e = time.perf_counter()
         with lock:
@@ -888,7 +889,7 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
             shapes.setdefault("_rows", {})[k] = max(int(v.shape[0]) for v in traces.values())
         return CT.compress_child_vk(pr.vk_commit, shape), proof
 
-    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, ch), prove, inflight)
+    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, ch, True, True), prove, inflight)
     t0 = time.perf_counter()
     root = CT.reduce_distributed(leaves, reducer) if distributed else CT.reduce_serial(leaves, reducer)
     wall = time.perf_counter() - t0
@@ -914,9 +915,9 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
     from zkmips_amd import compress_tree as CT
     leaves, info = mips_leaves(dev, args.queries, down=22 - args.leaf_log)
     # warm-up (untimed): one node's witness and proof (JIT modules, allocator pools); its key is dropped
-    wit = CT.node_witness(leaves[:2])
+    wit = CT.node_witness(leaves[:2], True, True)
     warm = CT.GpuProvers(dev)
-    warm.get(wit[0], CT.TreeStats()).prove_shard(wit[1], wit[2])
+    warm.get(wit[0], CT.TreeStats()).prove_shard(CT.materialize(wit[1]), wit[2])
     del warm
     (rvk, rproof), r = compress_tree_run(pool, dev, leaves, inflight, distributed=world > 1)
     n = r["proofs"]

@@ -143,3 +143,7 @@ def test_gpu_mips_node_reference_shape():
     rc, ref = o.prove(tr, pv)
     assert rc == 0 and gpu == ref
     assert o.verify(gpu) == 0
+    # the bench's form: the Poseidon2WideDeg3 trace built on the device from the permutation inputs
+    prep_d, tr_d, pv_d, shape_d, _ = CT.node_witness(leaves, True, True)
+    assert isinstance(tr_d["Poseidon2WideDeg3"], CT.DeviceP2) and shape_d == shape
+    assert HipProver(dev, cm, prep_d, **kw).prove_shard(CT.materialize(tr_d), pv_d) == gpu

@@ -187,12 +187,13 @@ def _compile_blob(blob) -> int:
     return n.value
 
 
-def prefill_jit_cache(machines, prune: bool = True, workers: int = None) -> int:
+def prefill_jit_cache(machines, prune: bool = False, workers: int = None) -> int:
     """Compile every chip's quotient/permutation kernels of `machines` for gfx950 into the JIT's on-disk
     code-object cache (zkmips_amd/jit_cache, see csrc/jit.cpp); no device needed.  hiprtc serialises
     compiles inside one process, so the distinct chips (one single-chip machine blob each, largest first)
-    compile in a pool of processes.  With `prune`, code objects of the default cache directory that none
-    of these machines uses any more (older kernel sources) are deleted.  Returns code bytes."""
+    compile in a pool of processes.  With `prune` (opt-in: only the build step, which prefills every
+    shipped machine while nothing else runs, passes it), code objects of the default cache directory that
+    none of these machines uses (older kernel sources, other machines) are deleted.  Returns code bytes."""
     import concurrent.futures as cf
     import multiprocessing as mp
     import time

@@ -31,20 +31,49 @@ import numpy as np
 Node = Tuple[int, int]  # (layer, index); leaves are layer 0
 
 
-def node_witness(children: Sequence[tuple], fix: bool = True):
+@dataclass
+class DeviceP2:
+    """A Poseidon2WideDeg3 main trace to be built on the GPU (tracegen.poseidon2_wide_trace) from the
+    program's permutation inputs: 8 MB of inputs instead of a 160 MB host trace per node."""
+    inputs: np.ndarray   # n x 16 canonical
+    height: int
+
+
+def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool = False):
     """Worker body (no GPU): the compress node's program from its (ChildVk, proof) children, executed,
     padded to the first allowed recursion shape (fix=False: natural power-of-two heights, for small
     tests), as a compress-machine shard.  Returns (prep traces, main traces, public values, shape,
-    seconds)."""
+    seconds); with p2_on_device the Poseidon2WideDeg3 entry is a DeviceP2 (see materialize)."""
     from . import recursion as R
     from . import recursion_verifier as RV
     t0 = time.perf_counter()
     prog = RV.compress_node_program(children)
     t1 = time.perf_counter()
     shape = R.fix_shape(prog) if fix else {k: max(4, (h - 1).bit_length()) for k, h in R.program_heights(prog).items()}
-    _, prep, traces, pvs = R.shard(prog, shape)
+    if p2_on_device:
+        _, prep, traces, pvs, p2in, p2h = R.shard_parts(prog, shape)
+        traces["Poseidon2WideDeg3"] = DeviceP2(p2in, p2h)
+    else:
+        _, prep, traces, pvs = R.shard(prog, shape)
     t2 = time.perf_counter()
     return prep, traces, pvs, shape, {"build_s": t1 - t0, "execute_and_traces_s": t2 - t1}
+
+
+def materialize(traces: dict) -> dict:
+    """Build every DeviceP2 entry's trace on the current GPU (rows past the inputs: the permutation of
+    zero) and wait for it; other entries pass through."""
+    out = dict(traces)
+    for k, v in traces.items():
+        if isinstance(v, DeviceP2):
+            import torch
+            from . import tracegen as TG
+            n = len(v.inputs)
+            ev = np.zeros((max(n, 1), 32), np.uint32)
+            ev[:n, :16] = v.inputs
+            evd = torch.from_numpy(ev.view(np.int32)).cuda()
+            out[k] = TG.poseidon2_wide_trace(evd, n, v.height)
+            torch.cuda.current_stream().synchronize()
+    return out
 
 
 _CVK_LOCK = threading.Lock()

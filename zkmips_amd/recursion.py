@@ -219,6 +219,31 @@ def poseidon2_rows(inputs: np.ndarray) -> np.ndarray:
     return t
 
 
+def p2_inputs(rec: ExecutionRecord) -> np.ndarray:
+    """The program's Poseidon2 inputs in instruction order (n x 16 canonical): the Poseidon2WideDeg3 events."""
+    return _cat([e["inputs"] for e in rec.events["p2"]], (WIDTH,)).astype(np.uint32)
+
+
+_P2_HOST = []
+
+
+def poseidon2_permute_host(inputs: np.ndarray) -> np.ndarray:
+    """Poseidon2-16 of every row (canonical): the product permutation (p2.cuh) compiled for the host,
+    zkm_host_poseidon2_permute in libzkm_trace.so -- the runtime's Poseidon2 instruction."""
+    if not _P2_HOST:
+        import ctypes as C
+        from . import septic
+        L = septic.lib()
+        u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+        L.zkm_host_poseidon2_permute.argtypes = [u32p, u32p, C.c_uint64]
+        _P2_HOST.append(L.zkm_host_poseidon2_permute)
+    x = np.ascontiguousarray(inputs, dtype=np.uint32).reshape(-1, WIDTH)
+    out = np.empty_like(x)
+    if len(x):
+        _P2_HOST[0](x, out, len(x))
+    return out.astype(U)
+
+
 def poseidon2_permute(inputs: np.ndarray) -> np.ndarray:
     return poseidon2_rows(np.atleast_2d(inputs))[:, P2_OUT:P2_OUT + WIDTH]
 
@@ -460,11 +485,11 @@ def execute(prog: RecursionProgram, mem_out: Optional[dict] = None) -> Execution
             ev["ext"].append({"out": out, "in1": x, "in2": y})
         elif k == "p2":
             x = rd(a["inp"].ravel())[:, 0].reshape(-1, WIDTH)
-            rows = poseidon2_rows(x)
+            out = poseidon2_permute_host(x)
             blk = np.zeros((x.size, D), U)
-            blk[:, 0] = rows[:, P2_OUT:P2_OUT + WIDTH].ravel()
+            blk[:, 0] = out.ravel()
             wr(a["out"].ravel(), blk)
-            ev["p2"].append({"rows": rows})
+            ev["p2"].append({"inputs": x, "outputs": out})  # the trace rows are built with the traces
         elif k == "select":
             bit, x, y = rd(a["bit"])[:, 0], rd(a["in1"])[:, 0], rd(a["in2"])[:, 0]
             nb = (PU + 1 - bit) % PU
@@ -842,8 +867,10 @@ def _cat(xs, shape_tail, dtype=U):
     return np.concatenate(xs) if xs else np.zeros((0,) + shape_tail, dtype)
 
 
-def generate_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None):
-    """(prep_traces, main_traces) by chip name, row-major uint32 canonical."""
+def generate_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None, p2_main: bool = True):
+    """(prep_traces, main_traces) by chip name, row-major uint32 canonical.  p2_main=False leaves out the
+    Poseidon2WideDeg3 main trace (313 columns, the largest) for the caller to build on the device from the
+    permutation inputs (`p2_inputs`, tracegen.poseidon2_wide_trace)."""
     shape = shape or {}
     prog = rec.program
     bl = lambda k: [b for b in prog.blocks if b.kind == k]
@@ -919,15 +946,17 @@ def generate_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None
         p_[:, 48] = P - 1
         pa.append(p_)
     pa = _cat(pa, (49,))
-    ma = _cat([e["rows"] for e in rec.events["p2"]], (P2_COLS,))
     name = "Poseidon2WideDeg3"
     h = _pow2(len(pa), shape.get(name))
-    mn = np.zeros((h, P2_COLS), U)
-    mn[:len(ma)] = ma
-    mn[len(ma):] = poseidon2_rows(np.zeros((1, WIDTH), U))
+    if p2_main:
+        ma = _cat([poseidon2_rows(e["inputs"]) for e in rec.events["p2"]], (P2_COLS,))
+        mn = np.zeros((h, P2_COLS), U)
+        mn[:len(ma)] = ma
+        mn[len(ma):] = poseidon2_rows(np.zeros((1, WIDTH), U))
+        mains[name] = mn.astype(np.uint32)
     pr = np.zeros((h, 49), U)
     pr[:len(pa)] = pa
-    preps[name], mains[name] = pr.astype(np.uint32), mn.astype(np.uint32)
+    preps[name] = pr.astype(np.uint32)
 
     # BatchFRI
     pa = []
@@ -1058,6 +1087,19 @@ def fix_shape(prog: RecursionProgram, shapes=None) -> Dict[str, int]:
         if all(h <= (1 << sh[k]) for k, h in heights.items()):
             return dict(sh)
     raise ValueError(f"no recursion shape found for heights: {heights}")
+
+
+def shard_parts(prog: RecursionProgram, shape: Optional[Dict[str, int]] = None):
+    """A compress-machine shard whose Poseidon2WideDeg3 main trace is left for the device: (machine,
+    prep_traces, traces without that chip, public values, the permutation inputs (n x 16), its height)."""
+    rec = execute(prog)
+    pr, tr = generate_traces(rec, shape, p2_main=False)
+    m = compress_machine()
+    if rec.events["frifold"]:
+        raise ValueError("FriFold instructions need the wide machine")
+    pr = {c.name: pr[c.name] for c in m.chips if c.prep_width}
+    tr.pop("FriFold", None)
+    return m, pr, tr, rec.public_values, p2_inputs(rec), pr["Poseidon2WideDeg3"].shape[0]
 
 
 def shard(prog: RecursionProgram, shape: Optional[Dict[str, int]] = None, wide: bool = False):
@@ -1462,7 +1504,7 @@ def rec_mem(rec: ExecutionRecord, addrs: np.ndarray) -> np.ndarray:
         elif k == "ext":
             mem[a["out"]] = e["out"]
         elif k == "p2":
-            mem[a["out"].ravel(), 0] = e["rows"][:, P2_OUT:P2_OUT + WIDTH].ravel()
+            mem[a["out"].ravel(), 0] = e["outputs"].ravel()
         elif k == "select":
             mem[a["out1"], 0] = e["out1"]
             mem[a["out2"], 0] = e["out2"]
