@@ -1,0 +1,45 @@
+"""Serial timing of one compress-node proof over two MIPS leaves (config 5's layer-1 node): host traces vs
+the Poseidon2WideDeg3 trace built on the device, with the per-stage profile of the device form.
+python tools/compress_node_timing.py"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import bench
+    from zkmips_amd import compress_tree as CT
+    from zkmips_amd._lib import Device
+    dev = Device(0)
+    leaves, info = bench.mips_leaves(dev, 84, n_leaves=2, distinct=2)
+    for p2dev in (False, True):
+        t = time.perf_counter()
+        prep, tr, pv, shape, times = CT.node_witness(leaves, True, p2dev)
+        wit_s = time.perf_counter() - t
+        provers = CT.GpuProvers(dev)
+        pr = provers.get(prep, CT.TreeStats())
+        for _ in range(2):
+            pr.prove_shard(CT.materialize(tr), pv)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(5):
+            proof = pr.prove_shard(CT.materialize(tr), pv)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t) / 5 * 1e3
+        print(f"p2_on_device={p2dev}: witness {wit_s:.2f} s ({times}), proof {ms:.2f} ms serial, "
+              f"{len(proof)} bytes, max rows {max(v.shape[0] for v in CT.materialize(tr).values())}", flush=True)
+    dt = {k: torch.from_numpy(v.view('int32')).cuda() if not isinstance(v, CT.DeviceP2) else v for k, v in tr.items()}
+    dt = CT.materialize(dt)
+    prof, serial_ms, text = bench.profile_proofs(pr, dt, pv, 3)
+    print(f"all traces resident: {serial_ms:.2f} ms serial")
+    for k, v in sorted(prof.items(), key=lambda kv: -kv[1][1]):
+        if not k.endswith(("_perms", "_gfops")):
+            print(f"   {k:24s} {v[1] / 3:8.3f} ms")
+
+
+if __name__ == "__main__":
+    main()

@@ -82,8 +82,32 @@ def _m(a, b):
     return (a * b) % PU
 
 
+_HOST = {}
+
+
+def _host(name: str):
+    """A batch helper of libzkm_trace.so (zkmips_amd/csrc/host/ef_host.cpp, p2_host.cpp)."""
+    f = _HOST.get(name)
+    if f is None:
+        import ctypes as C
+        from . import septic
+        f = getattr(septic.lib(), name)
+        u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+        f.argtypes = {"zkm_host_ef_mul": [u32p, u32p, u32p, C.c_uint64],
+                      "zkm_host_batch_fri": [u32p, u32p, u32p, C.c_uint64, C.c_uint64, u32p],
+                      "zkm_host_poseidon2_permute": [u32p, u32p, C.c_uint64]}[name]
+        _HOST[name] = f
+    return f
+
+
 def ext_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """(n,4) x (n,4) over F[x]/(x^4 - 3)."""
+    if a.shape == b.shape and a.ndim == 2 and a.shape[0] >= 16:  # batches: host C++ (ef_host.cpp)
+        x = np.ascontiguousarray(a, dtype=np.uint32)
+        y = np.ascontiguousarray(b, dtype=np.uint32)
+        out = np.empty_like(x)
+        _host("zkm_host_ef_mul")(x, y, out, len(x))
+        return out.astype(U)
     r = np.zeros(np.broadcast(a, b).shape, dtype=U)
     for i in range(D):
         for j in range(D):
@@ -224,23 +248,13 @@ def p2_inputs(rec: ExecutionRecord) -> np.ndarray:
     return _cat([e["inputs"] for e in rec.events["p2"]], (WIDTH,)).astype(np.uint32)
 
 
-_P2_HOST = []
-
-
 def poseidon2_permute_host(inputs: np.ndarray) -> np.ndarray:
     """Poseidon2-16 of every row (canonical): the product permutation (p2.cuh) compiled for the host,
     zkm_host_poseidon2_permute in libzkm_trace.so -- the runtime's Poseidon2 instruction."""
-    if not _P2_HOST:
-        import ctypes as C
-        from . import septic
-        L = septic.lib()
-        u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
-        L.zkm_host_poseidon2_permute.argtypes = [u32p, u32p, C.c_uint64]
-        _P2_HOST.append(L.zkm_host_poseidon2_permute)
     x = np.ascontiguousarray(inputs, dtype=np.uint32).reshape(-1, WIDTH)
     out = np.empty_like(x)
     if len(x):
-        _P2_HOST[0](x, out, len(x))
+        _host("zkm_host_poseidon2_permute")(x, out, len(x))
     return out.astype(U)
 
 
@@ -521,16 +535,15 @@ def execute(prog: RecursionProgram, mem_out: Optional[dict] = None) -> Execution
             px = rd(a["p_at_x"].ravel())[:, 0].reshape(n, L)
             pz = rd(a["p_at_z"].ravel()).reshape(n, L, D)
             al = rd(a["alpha_pow"].ravel()).reshape(n, L, D)
-            acc = np.zeros((n, D), U)
+            runs = np.empty((n, L, D), np.uint32)
+            _host("zkm_host_batch_fri")(np.ascontiguousarray(al, dtype=np.uint32), np.ascontiguousarray(pz, dtype=np.uint32),
+                                        np.ascontiguousarray(px, dtype=np.uint32), n, L, runs)
             rows = np.zeros((n, L, 13), U)
-            for i in range(L):
-                diff = pz[:, i].copy()
-                diff[:, 0] = (diff[:, 0] + PU - px[:, i]) % PU
-                acc = (acc + ext_mul(al[:, i], diff)) % PU
-                rows[:, i, 0:4] = acc
-                rows[:, i, 4:8] = al[:, i]
-                rows[:, i, 8:12] = pz[:, i]
-                rows[:, i, 12] = px[:, i]
+            rows[:, :, 0:4] = runs
+            rows[:, :, 4:8] = al
+            rows[:, :, 8:12] = pz
+            rows[:, :, 12] = px
+            acc = rows[:, L - 1, 0:4].copy() if L else np.zeros((n, D), U)
             wr(a["acc"], acc)
             ev["batchfri"].append({"rows": rows.reshape(n * L, 13), "L": L, "n": n})
         elif k == "frifold":

@@ -242,7 +242,7 @@ class HostChallenger:
         for i, v in enumerate(self.inp):
             self.st[i] = v
         self.inp = []
-        self.st = [int(x) for x in R.poseidon2_permute(np.asarray([self.st], U))[0]]
+        self.st = [int(x) for x in R.poseidon2_permute_host(np.asarray([self.st], U))[0]]
         self.out = self.st[:8]
 
     def observe(self, v):
