@@ -1201,7 +1201,7 @@ def main():
     ap.add_argument("--no-sizes", action="store_true",
                     help="skip the default line's size series (resident rows/s and LDE time at 2^20, 2^21, 2^23)")
     ap.add_argument("--leaf-log", type=int, default=16, help="compress leg: MIPS leaf shards in the maximal shape scaled to Cpu 2^leaf_log rows")
-    ap.add_argument("--node-workers", type=int, default=16,
+    ap.add_argument("--node-workers", type=int, default=12,
                     help="compress workload: processes generating node witnesses (the box allots 16 CPUs per GPU)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 HBM counter passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)

@@ -259,9 +259,9 @@ def test_gpu_shrink_shape_full_size_verifies(dev):
 
 def _p2_records(rec):
     """Poseidon2Io records (input[16], output[16]) of a run's Poseidon2 events, canonical."""
-    rows = np.concatenate([e["rows"] for e in rec.events["p2"]])
-    return np.ascontiguousarray(np.concatenate([rows[:, R.P2_EXT:R.P2_EXT + 16], rows[:, R.P2_OUT:R.P2_OUT + 16]],
-                                               1).astype(np.uint32))
+    ins = np.concatenate([e["inputs"] for e in rec.events["p2"]])
+    outs = np.concatenate([e["outputs"] for e in rec.events["p2"]])
+    return np.ascontiguousarray(np.concatenate([ins, outs], 1).astype(np.uint32))
 
 
 def test_poseidon2_wide_trace_abi_declared():

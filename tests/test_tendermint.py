@@ -107,3 +107,59 @@ def test_gpu_tendermint_bytes(tm_proofs, part):
         _, _, tr, pv = shards[i]
         rc, ref = o.prove(tr, pv)
         assert rc == 0 and ref == proofs[i], f"shard {i}"
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _two_rank_worker(rank, world, port, out_q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tests import _oracle as O
+    from zkmips_amd.dist import deal_by_cost, prove_shards_distributed, shard_cost
+    prog, _ = T.tendermint_program(T.load_block(2279100), T.load_block(2279130), votes=slice(99, 100))
+    run = MC.program_shards(prog, seed=1, shard_size=1 << 16, precompile_events_per_shard=512)
+    m, prep, _, _ = run[0]
+    pr = O.OracleProver(m, {k: v for k, v in prep.items() if v is not None}, num_queries=4)
+    costs = [shard_cost(tr) for _, _, tr, _ in run]
+    mine = deal_by_cost(costs, world)[rank]
+
+    def prove_one(i):
+        assert i in mine
+        rc, p = pr.prove(run[i][2], run[i][3])
+        assert rc == 0
+        return p
+    proofs = prove_shards_distributed(prove_one, len(run), check_global_sum=True, costs=costs)
+    if rank == 0:
+        out_q.put((len(proofs), len(run), sorted(set(k for _, _, tr, _ in run for k in tr))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_tendermint_execution():
+    """A tendermint execution on the reference's blocks (headers and validator sets hashed, the nil vote's
+    signature verified) split into CPU, SHA_EXTEND, SHA_COMPRESS, ED_ADD, ED_DECOMPRESS, UINT256_MUL and
+    memory shards, dealt by cost to two gloo ranks; rank 0 gathers every proof and the machine-level global
+    cumulative sum checks out (machine.rs:639-654)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=900)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got[0] == got[1] >= 7
+    assert {"ShaExtend", "ShaCompress", "EdAddAssign", "EdDecompress", "Uint256MulMod"} <= set(got[2])
