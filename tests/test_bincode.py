@@ -1,0 +1,101 @@
+"""bincode codecs of the Twirp `Compress` route (zkmips_amd/bincode.py; CompressRequestPayload
+crates/cuda/src/lib.rs:92-102, ZKMReduceProof crates/core/executor/src/reduce.rs:7-12, StarkVerifyingKey
+crates/stark/src/machine.rs:93-104) and the core verifying key -> ChildVk mapping the route uses."""
+import struct
+
+import numpy as np
+import pytest
+
+from tests import _oracle as O
+from zkmips_amd import bincode as B
+from zkmips_amd import recursion_verifier as RV
+from zkmips_amd import service as SV
+from zkmips_amd import workloads as W
+
+
+@pytest.fixture(scope="module")
+def fib_proofs():
+    m, prep, _, _ = W.fib_shard(256, seed=3)
+    pr = O.OracleProver(m, prep, num_queries=4)
+    out = []
+    for s in (3, 4, 5):
+        _, _, tr, pv = W.fib_shard(256, seed=s)
+        rc, p = pr.prove(tr, pv)
+        assert rc == 0
+        out.append(p)
+    return m, prep, pr.commit, out
+
+
+def test_vk_layout_is_bincode_fixint():
+    vk = B.StarkVk(list(range(8)), 0x400000, list(range(100, 114)), [("Program", 10, 1, 8, 1024)], {"Program": 0})
+    w = B.Writer()
+    vk.write(w)
+    b = w.bytes()
+    # commit 8 x u32, pc_start u32, 14 x u32 cumulative sum, Vec len u64, String (u64 len + utf8), log_n u64,
+    # shift u32, width u64, height u64, HashMap len u64, key String, value u64
+    want = (struct.pack("<8I", *range(8)) + struct.pack("<I", 0x400000) + struct.pack("<14I", *range(100, 114))
+            + struct.pack("<Q", 1) + struct.pack("<Q", 7) + b"Program" + struct.pack("<QIQQ", 10, 1, 8, 1024)
+            + struct.pack("<Q", 1) + struct.pack("<Q", 7) + b"Program" + struct.pack("<Q", 0))
+    assert b == want
+    assert B.StarkVk.read(B.Reader(b)) == vk
+
+
+def test_compress_request_roundtrip(fib_proofs):
+    m, prep, commit, proofs = fib_proofs
+    vk = B.StarkVk.of_program(m, prep, commit, 0x400000, [0] * 14)
+    assert [c[0] for c in vk.chips] == sorted(k for k, v in prep.items() if v is not None)
+    req = B.write_compress_request(vk, proofs, stdin=[b"abc", b""], public_values=b"\x01\x02", cycles=99)
+    vk2, shards, nd = B.read_compress_request(req)
+    assert vk2 == vk and shards == proofs and nd == 0
+    # the shard proofs are split by parsing them, so each is the exact byte string
+    assert all(RV.parse_shard_proof(s).names == ["FibCpu", "FibTable"] for s in shards)
+    with pytest.raises(Exception):
+        B.read_compress_request(req[:len(req) // 2])
+
+
+def test_reduce_proof_roundtrip(fib_proofs):
+    m, prep, commit, proofs = fib_proofs
+    vk = B.StarkVk.of_program(m, prep, commit, 0, [5] * 14)
+    b = B.write_reduce_proof(vk, proofs[0])
+    assert B.read_reduce_proof(b) == (vk, proofs[0])
+    with pytest.raises(ValueError):
+        B.read_reduce_proof(b + b"\0")
+
+
+def test_core_child_vk_from_request_key():
+    """The route's ChildVk of a MIPS program equals the one built from the machine and its traces, and a
+    key naming dimensions the machine does not have is rejected."""
+    from zkmips_amd import shapes as SH
+    from zkmips_amd.septic import CURVE_CUMULATIVE_SUM_START as GCS
+    m, prep, _, _ = SH.shape_shards(SH.MAXIMAL_22, [1], down=8)[0]
+    commit = np.arange(8) * 7 + 1
+    vk = B.StarkVk.of_program(m, prep, commit, 0x00400000, GCS)
+    got = SV.core_child_vk(vk)
+    want = RV.ChildVk.of(m, prep, commit)
+    assert got.prep_order == want.prep_order and got.prep_heights == want.prep_heights
+    assert np.array_equal(got.commit, want.commit) and np.array_equal(got.gcs, want.gcs)
+    assert got.chips == want.chips and got.num_pv == want.num_pv and got.pc_start == want.pc_start
+    name, log_n, shift, width, height = vk.chips[0]
+    bad = B.StarkVk(vk.commit, vk.pc_start, vk.gcs, [(name, log_n, shift, width + 1, height)] + vk.chips[1:],
+                    vk.ordering)
+    with pytest.raises(ValueError):
+        SV.core_child_vk(bad)
+    bad = B.StarkVk(vk.commit, vk.pc_start, vk.gcs, vk.chips + [("Cpu", 4, 1, 1, 16)], vk.ordering)
+    with pytest.raises(ValueError):
+        SV.core_child_vk(bad)
+
+
+def test_compress_route_errors():
+    svc = SV.ProverService(device_factory=lambda i: object())
+    with pytest.raises(SV.TwirpError) as e:
+        svc.call("Compress", {1: b"not bincode"})
+    assert e.value.code == "invalid_argument"
+    vk = B.StarkVk([0] * 8, 0, [0] * 14, [], {})
+    req = bytearray(B.write_compress_request(vk, []))
+    with pytest.raises(SV.TwirpError) as e:
+        svc.call("Compress", {1: bytes(req)})
+    assert e.value.code == "invalid_argument"  # no shards
+    req[-8:] = struct.pack("<Q", 1)  # one deferred proof (its bytes are never read: refused first)
+    with pytest.raises(SV.TwirpError) as e:
+        svc.call("Compress", {1: bytes(req)})
+    assert e.value.code == "unimplemented"

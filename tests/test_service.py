@@ -54,9 +54,11 @@ def test_ready_and_routes(server):
     assert st == 200 and ct == "application/protobuf" and SV.decode_fields(body) == {1: 1}
     st, ct, body = post(port, "Ready", b"{}", "application/json")
     assert st == 200 and json.loads(body) == {"ready": True}
-    for m in ("Setup", "ProveCore", "ProveCoreStateless", "Compress", "Shrink", "Wrap"):
+    for m in ("Setup", "ProveCore", "ProveCoreStateless", "Shrink", "Wrap"):
         st, ct, body = post(port, m, SV.encode_bytes_field(1, b"payload"))
         assert st == 501 and json.loads(body)["code"] == "unimplemented", m
+    st, ct, body = post(port, "Compress", SV.encode_bytes_field(1, b"payload"))  # not a bincode payload
+    assert st == 400 and json.loads(body)["code"] == "invalid_argument"
     st, _, body = post(port, "NoSuchMethod", b"")
     assert st == 404 and json.loads(body)["code"] == "bad_route"
     st, _, body = post(port, "Ready", b"", "text/plain")
@@ -198,3 +200,39 @@ def test_two_compress_programs_through_one_server(server):
                                  log_blowup=R.COMPRESS_LOG_BLOWUP).prove(tr, pv)
         assert rc == 0 and SV.decode_fields(body)[1] == direct == ref
     assert blobs[0] == blobs[1]  # one machine, two programs
+
+
+@pytest.mark.gpu
+def test_compress_two_mips_shards_through_service(server):
+    """Compress (lib.rs:92-102): two MIPS shard proofs (84 queries, the reference's 2^22 shape scaled to
+    Cpu 2^16) sent as a bincode CompressRequestPayload come back as a ZKMReduceProof whose proof is the
+    node proof a direct HipProver makes from the same children, the oracle verifies it, and its vk is
+    that node program's StarkVerifyingKey."""
+    from tests import _oracle as O
+    from zkmips_amd import bincode as B
+    from zkmips_amd import compress_tree as CT
+    from zkmips_amd import recursion as R
+    from zkmips_amd import recursion_verifier as RV
+    from zkmips_amd import shapes as SH
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    from zkmips_amd.septic import CURVE_CUMULATIVE_SUM_START as GCS
+    dev = Device(0)
+    sh = SH.shape_shards(SH.MAXIMAL_22, [1, 2], down=6)
+    m, prep = sh[0][0], sh[0][1]
+    hp = HipProver(dev, m, prep, num_queries=84)
+    proofs = [hp.prove_shard(s[2], s[3]) for s in sh]
+    req = B.write_compress_request(B.StarkVk.of_program(m, prep, hp.vk_commit, 0x00400000, GCS), proofs)
+    port = server()
+    st, _, body = post(port, "Compress", SV.encode_bytes_field(1, req))
+    assert st == 200, body
+    rvk, rproof = B.read_reduce_proof(SV.decode_fields(body)[1])
+    vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=84)
+    cprep, tr, pv, shape, _ = CT.node_witness([(vk, p) for p in proofs])
+    cm = R.compress_machine()
+    kw = dict(num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    direct = HipProver(dev, cm, cprep, **kw)
+    assert rproof == direct.prove_shard(tr, pv)
+    assert O.OracleProver(cm, cprep, **kw).verify(rproof) == 0
+    assert rvk.commit == [int(x) for x in direct.vk_commit]
+    assert {c[0]: c[1] for c in rvk.chips} == {k: shape[k] for k in rvk.ordering}

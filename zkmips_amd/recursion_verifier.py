@@ -107,7 +107,15 @@ class ShardProofData:
 def parse_shard_proof(b: bytes) -> ShardProofData:
     """The bincode-1 layout zkm_open writes (zkmips_amd/csrc/prover.cpp `serialize`, crates/stark/src/
     types.rs:77-83): canonical field elements, u64 lengths."""
-    pos = [0]
+    p, end = parse_shard_proof_at(b, 0)
+    if end != len(b):
+        raise ValueError("trailing bytes in the shard proof")
+    return p
+
+
+def parse_shard_proof_at(b: bytes, start: int):
+    """One ShardProof starting at byte `start` of b (e.g. inside a Vec<ShardProof>): (data, end offset)."""
+    pos = [start]
 
     def u64():
         v = int.from_bytes(b[pos[0]:pos[0] + 8], "little")
@@ -157,8 +165,7 @@ def parse_shard_proof(b: bytes) -> ShardProofData:
         order.append((u64(), nm))
     names = [nm for _, nm in sorted(order)]
     pv = u32s(u64())
-    assert pos[0] == len(b), "trailing bytes in the shard proof"
-    return ShardProofData(main_c, perm_c, quot_c, chips, fri_commits, queries, final_poly, pow_w, names, pv)
+    return ShardProofData(main_c, perm_c, quot_c, chips, fri_commits, queries, final_poly, pow_w, names, pv), pos[0]
 
 
 # ---------------------------------------------------------------- the child's verifying key

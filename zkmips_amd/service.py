@@ -13,10 +13,16 @@ types of api.proto (every request/response is one `bytes` field, or `bool ready`
                  optional `log_blowup`, and `prep/<chip>` / `trace/<chip>` arrays; `result` is the
                  serialized ShardProof.  A prover per (machine blob, FRI parameters, preprocessed
                  traces) is kept, LRU-bounded (setup once per program).
-* ``Setup``, ``ProveCore``, ``ProveCoreStateless``, ``Compress``, ``Shrink``, ``Wrap`` — Twirp
-                 `unimplemented`: their payloads are bincode `ZKMStdin` / ELF / recursion proofs
-                 (lib.rs:57-123), which need the MIPS executor and the recursion stack, outside the
-                 §8 hot path.
+* ``Compress`` — `data` is a bincode CompressRequestPayload (lib.rs:92-102: the core verifying key, the
+                 ZKMCoreProof's shard proofs, deferred proofs), `result` a bincode ZKMReduceProof (the
+                 root compress proof and its StarkVerifyingKey, zkmips_amd/bincode.py).  The shard
+                 proofs are the leaves of the compress tree (zkmips_amd/compress_tree.py): node
+                 programs verifying their children in full, padded to a RecursionShapeConfig shape,
+                 set up and proven on the GPU; a single shard is still wrapped by one node.  Deferred
+                 proofs are `unimplemented`.
+* ``Setup``, ``ProveCore``, ``ProveCoreStateless``, ``Shrink``, ``Wrap`` — Twirp `unimplemented`: their
+                 payloads are bincode `ZKMStdin` / ELF (lib.rs:57-90) or the shrink / BN254 wrap
+                 stages (lib.rs:104-116), outside the §8 rows.
 
 Run: ``python -m zkmips_amd.service --port 3000`` (then CUDA_ENDPOINT=http://<host>:3000/twirp/).
 """
@@ -37,7 +43,6 @@ UNIMPLEMENTED = {
     "Setup": "needs the ELF loader and executor (SetupRequestPayload { elf }, crates/cuda/src/lib.rs:60-71)",
     "ProveCore": "needs the MIPS executor to turn ZKMStdin into shard records (lib.rs:73-79)",
     "ProveCoreStateless": "needs the MIPS executor to turn ZKMStdin into shard records (lib.rs:81-90)",
-    "Compress": "recursion compress is outside this server (lib.rs:92-102)",
     "Shrink": "recursion shrink is outside this server (lib.rs:104-109)",
     "Wrap": "the BN254 wrap is outside this server (lib.rs:111-116)",
 }
@@ -154,6 +159,42 @@ def prover_key(blob, prep: dict, num_queries: int, log_blowup: int) -> bytes:
     return h.digest()
 
 
+def core_child_vk(vk):
+    """The ChildVk a compress node verifies a core shard proof against, from the request's
+    StarkVerifyingKey<CoreSC>: the MIPS machine's chips (zkmips_amd/mips_core.py), the key's preprocessed
+    commitment, heights, order, pc_start and initial global cumulative sum; core FRI parameters (84
+    queries, blowup 2, 16 PoW bits).  A chip the MIPS machine does not preprocess, or a width that is not
+    the chip's, is a ValueError."""
+    from . import mips_core as MC
+    from . import recursion_verifier as RV
+    m = MC.core_machine()
+    chips = {c.name: c for c in m.chips}
+    heights = {}
+    for name, log_n, shift, width, height in vk.chips:
+        c = chips.get(name)
+        if c is None or not c.prep_width:
+            raise ValueError(f"chip {name!r} has no preprocessed trace in the MIPS machine")
+        if width != c.prep_width or height != 1 << log_n or shift != 1:
+            raise ValueError(f"chip {name!r}: preprocessed dimensions {width}x{height} (log_n {log_n}, "
+                             f"shift {shift}) are not the machine's")
+        heights[name] = height
+    order = sorted(heights, key=lambda k: (-heights[k], k))
+    if vk.ordering and sorted(vk.ordering, key=lambda k: vk.ordering[k]) != order:
+        raise ValueError("chip_ordering is not the preprocessed order")
+    return RV.ChildVk({k: RV.ChipShape.of(c) for k, c in chips.items()}, m.num_pv, np.asarray(vk.commit, np.int64),
+                      order, heights, int(vk.pc_start), np.asarray(vk.gcs, np.int64))
+
+
+def reduce_vk(cvk):
+    """StarkVerifyingKey<InnerSC> of a compress proof's program (the vk field of ZKMReduceProof)."""
+    from . import bincode as B
+    from . import recursion as R
+    widths = {c.name: c.prep_width for c in R.compress_machine().chips}
+    chips = [(k, cvk.prep_heights[k].bit_length() - 1, 1, widths[k], cvk.prep_heights[k]) for k in cvk.prep_order]
+    return B.StarkVk([int(x) for x in cvk.commit], int(cvk.pc_start), [int(x) for x in cvk.gcs], chips,
+                     {k: i for i, k in enumerate(cvk.prep_order)})
+
+
 class _Pending:
     """A proving key being set up: requests for the same key wait on it, others go ahead."""
 
@@ -172,7 +213,8 @@ class ProverService:
     behind one setup (which may include minutes of first-time hiprtc compilation)."""
 
     def __init__(self, device: int = 0, device_factory: Optional[Callable] = None,
-                 prover_factory: Optional[Callable] = None, max_provers: int = 8):
+                 prover_factory: Optional[Callable] = None, max_provers: int = 8, compress_workers: int = 0,
+                 compress_inflight: int = 2):
         from collections import OrderedDict
         self.device_index = device
         self._device_factory = device_factory
@@ -184,6 +226,15 @@ class ProverService:
         self._dev_lock = threading.Lock()
         self._lock = threading.Lock()
         self.setups = 0  # proving keys built (tests check the cache behaviour)
+        # compress: node witnesses in a spawn process pool started here, before this process touches the
+        # GPU (0 workers: a thread pool), node proofs in `compress_inflight` threads
+        self._pool = None
+        if compress_workers > 0:
+            import multiprocessing as mpc
+            from concurrent.futures import ProcessPoolExecutor
+            self._pool = ProcessPoolExecutor(compress_workers, mp_context=mpc.get_context("spawn"))
+        self.compress_inflight = compress_inflight
+        self._compress_provers = None
 
     def _device(self):
         with self._dev_lock:
@@ -249,12 +300,63 @@ class ProverService:
             raise TwirpError("invalid_argument", f"ProveShard payload: {e}")
         return self.get_prover(blob, prep, nq, lb).prove_shard(traces, pv)
 
+    def compress(self, data: bytes) -> bytes:
+        """CompressRequestPayload -> ZKMReduceProof (prover/src/lib.rs:614-954 on the GPU)."""
+        from . import bincode as B
+        from . import compress_tree as CT
+        try:
+            vk, shards, n_deferred = B.read_compress_request(data)
+        except Exception as e:
+            raise TwirpError("invalid_argument", f"Compress payload: {e}")
+        if n_deferred:
+            raise TwirpError("unimplemented", "Compress: deferred proofs are not supported")
+        if not shards:
+            raise TwirpError("invalid_argument", "Compress: the core proof has no shards")
+        try:
+            cvk = core_child_vk(vk)
+        except ValueError as e:
+            raise TwirpError("invalid_argument", f"Compress: {e}")
+        leaves = [(cvk, s) for s in shards]
+        dev = self._device()
+        with self._lock:
+            if self._compress_provers is None:
+                self._compress_provers = CT.GpuProvers(dev)
+        provers, stats = self._compress_provers, CT.TreeStats()
+
+        def prove(wit):
+            prep, traces, pvs, shape, _ = wit
+            pr = provers.get(prep, stats)
+            proof = pr.prove_shard(CT.materialize(traces), pvs)
+            return CT.compress_child_vk(pr.vk_commit, shape), proof
+
+        if self._pool is not None:
+            submit = lambda ch: self._pool.submit(CT.node_witness, ch, True, True)
+        else:
+            from concurrent.futures import ThreadPoolExecutor
+            tp = ThreadPoolExecutor(2)
+            submit = lambda ch: tp.submit(CT.node_witness, ch, True, True)
+        reducer = CT.Reducer(submit, prove, self.compress_inflight)
+        try:
+            if len(leaves) == 1:  # one shard is still wrapped by a compress node
+                rvk, rproof = prove(submit(leaves).result())
+            else:
+                try:
+                    rvk, rproof = CT.reduce_serial(leaves, reducer)
+                except ValueError as e:  # a child proof the node verifier rejects
+                    raise TwirpError("invalid_argument", f"Compress: {e}")
+        finally:
+            if self._pool is None:
+                tp.shutdown(wait=False)
+        return B.write_reduce_proof(reduce_vk(rvk), rproof)
+
     def call(self, method: str, payload: Dict[int, object]) -> Dict[str, object]:
         if method == "Ready":
             return {"ready": self.ready()}
         if method == "ProveShard":
             data = payload.get(1, b"")
             return {"result": self.prove_shard(bytes(data))}
+        if method == "Compress":
+            return {"result": self.compress(bytes(payload.get(1, b"")))}
         if method in UNIMPLEMENTED:
             raise TwirpError("unimplemented", f"{method}: {UNIMPLEMENTED[method]}")
         raise TwirpError("bad_route", f"no such method: {method}")
@@ -330,8 +432,9 @@ def main():
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=3000)
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--compress-workers", type=int, default=8, help="witness processes of the Compress route")
     a = ap.parse_args()
-    srv = serve(a.host, a.port, a.device)
+    srv = serve(a.host, a.port, service=ProverService(a.device, compress_workers=a.compress_workers))
     print(f"ProverService on http://{a.host}:{a.port}/twirp/", flush=True)
     srv.serve_forever()
 
