@@ -889,7 +889,8 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
             shapes.setdefault("_rows", {})[k] = max(int(v.shape[0]) for v in traces.values())
         return CT.compress_child_vk(pr.vk_commit, shape), proof
 
-    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, ch, True, True), prove, inflight)
+    # compact witnesses: main traces as event rows laid out on the device, prep traces once per program
+    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, ch, True, True, True), prove, inflight)
     t0 = time.perf_counter()
     root = CT.reduce_distributed(leaves, reducer) if distributed else CT.reduce_serial(leaves, reducer)
     wall = time.perf_counter() - t0
@@ -915,7 +916,7 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
     from zkmips_amd import compress_tree as CT
     leaves, info = mips_leaves(dev, args.queries, down=22 - args.leaf_log)
     # warm-up (untimed): one node's witness and proof (JIT modules, allocator pools); its key is dropped
-    wit = CT.node_witness(leaves[:2], True, True)
+    wit = CT.node_witness(leaves[:2], True, True, True, False)
     warm = CT.GpuProvers(dev)
     warm.get(wit[0], CT.TreeStats()).prove_shard(CT.materialize(wit[1]), wit[2])
     del warm
@@ -1087,6 +1088,7 @@ class ShardBench:
         torch.cuda.synchronize()
         self.rows_per_shard = max(v.shape[0] for v in self.shards[0][2].values())
         self.stagger = None
+        self.slot_waits = {}
 
     def slot_steps(self, k, nsteps, mode):
         """nsteps shard proofs of in-flight slot k; returns the last proof."""
@@ -1122,8 +1124,11 @@ class ShardBench:
             stagger[k - 1].wait(60)  # bounded: a failing slot must not hang the others
         ev = issue(0)
         pr = b""
+        waits = []
         for j in range(nsteps):
+            t = time.perf_counter()
             ev.synchronize()
+            waits.append(time.perf_counter() - t)
             if j == 0 and stagger is not None:
                 stagger[k].set()
             nxt = issue(j + 1) if j + 1 < nsteps else None
@@ -1131,6 +1136,7 @@ class ShardBench:
             src = dev_t if os.environ.get("ZKM_BENCH_DMA_PROBE") == "1" else bufs[j % 2]
             pr = prove_resident(prover, src, pv)
             ev = nxt
+        self.slot_waits[k] = waits  # host seconds each step waited for its traces' copy
         return pr
 
     def run_steps(self, nsteps, mode="pipelined"):
@@ -1252,6 +1258,7 @@ def main():
     proof_res, elapsed_res = sb.timed(args.steps, "resident")
     # secondary: host traces with the look-ahead H2D pipeline, and per-call host copies
     proof, elapsed = sb.timed(args.steps, "pipelined")
+    copy_waits = {k: list(v) for k, v in sb.slot_waits.items()}
     proof_pc, elapsed_pc = sb.timed(args.steps, "per_call")
     assert proof_res == proof == proof_pc, "resident / host-trace proofs differ"
 
@@ -1264,6 +1271,21 @@ def main():
     # the stage table come from here, the throughput `value` from the timed region above
     nprof = max(1, args.profile_steps)
     prof, serial_ms, prof_text = profile_proofs(prover, dev_traces, pvs, nprof)
+
+    # the PCIe ceiling of the host-trace mode: one shard's page-locked traces copied alone
+    import torch
+    h2d_s = []
+    for _ in range(3):
+        _, _, _, host_t, bufs, cs = sb.shards[0]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(cs):
+            for kk, t in host_t.items():
+                b = bufs[0][kk]
+                b.copy_from_host(t, cs) if isinstance(b, RawDev) else b.copy_(t, non_blocking=True)
+        cs.synchronize()
+        h2d_s.append(time.perf_counter() - t0)
+    h2d_alone_s = min(h2d_s)
 
     # single-shard latency from pageable host memory (the runtime stages the copy)
     tp = time.perf_counter()
@@ -1369,8 +1391,15 @@ def main():
         "host_traces": {"value": round(world * K * rows_per_shard * args.steps / elapsed, 1), "unit": "rows/s",
                         "ms_per_shard": round(1e3 * elapsed / (args.steps * K), 3),
                         "vs_resident": round(elapsed / elapsed_res, 3),
+                        "h2d_alone_ms_per_shard": round(h2d_alone_s * 1e3, 3),
+                        "h2d_GBps": round(sum(v.nbytes for v in traces.values()) / h2d_alone_s / 1e9, 2),
+                        "copy_wait_ms": {"first_step_per_slot": [round(1e3 * v[0], 2) for _, v in sorted(copy_waits.items())],
+                                         "later_steps_per_slot": [round(1e3 * sum(v[1:]), 2)
+                                                                  for _, v in sorted(copy_waits.items())]},
                         "what": "same steps from page-locked host traces: the H2D DMA of each slot's next shard "
-                                "overlaps the current proof, every copy inside the timed span"},
+                                "overlaps the current proof, every copy inside the timed span; copy_wait_ms = host "
+                                "time each slot waited for its traces (the first step's copies cannot overlap a "
+                                "proof), h2d_alone_ms_per_shard = one shard's copy with nothing else running"},
         "h2d_bytes_per_shard": int(sum(v.nbytes for v in traces.values())),
         "host_threads_bound_to": numa,
         "pageable_single_shard_ms": round(pageable_s * 1e3, 3),

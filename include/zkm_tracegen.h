@@ -311,6 +311,33 @@ int zkm_poseidon2_wide_events_to_trace(const zkm_poseidon2_event *events, uint64
 int zkm_exp_reverse_bits_events_to_trace(const uint32_t *base, const uint32_t *bits, const uint64_t *offsets,
                                          uint64_t n, uint32_t repr, uint32_t *trace, uint64_t height, void *stream);
 
+/* Recursion chips whose main rows are their events (cols.vals = event), several events per row for the
+ * memory and ALU chips:
+ *   BaseAlu      alu_base_event_to_row_koalabear   (sys.rs:22-25, include/alu_base.hpp)   3 words x 4 per row
+ *   ExtAlu       alu_ext_event_to_row_koalabear    (sys.rs:31-34, include/alu_ext.hpp)   12 words x 4 per row
+ *   BatchFRI     batch_fri_event_to_row_koalabear  (sys.rs:40-43, include/batch_fri.hpp) 13 words (acc[4],
+ *                alpha_pow[4], p_at_z[4], p_at_x) x 1
+ *   Select       select_event_to_row_koalabear     (sys.rs:83-86, include/select.hpp)     5 words x 1
+ *   FriFold      fri_fold_event_to_row_koalabear   (sys.rs:62-65, include/fri_fold.hpp)  33 words x 1
+ *   PublicValues public_values_event_to_row_koalabear (sys.rs:72-76, include/public_values.hpp): the
+ *                digest's 8 elements, 1 word x 1
+ *   MemoryVar    mem/variable.rs generate_trace: a hinted block, 4 words x 2 per row
+ *   MemoryConst  mem/constant.rs generate_trace: main width 1, all zero (n = 0)
+ * `events` holds n events of the chip's width back to back; row r gets events r*k .. r*k + k - 1 side by side;
+ * rows past the events are zero (the chips' padding rows).  repr as above (the words are converted to
+ * canonical on the way).  ZKM_ERR_ARG for an unknown chip, n events not fitting height rows, or a
+ * height that is not a power of two >= 16. */
+#define ZKM_REC_CHIP_BASE_ALU 0
+#define ZKM_REC_CHIP_EXT_ALU 1
+#define ZKM_REC_CHIP_BATCH_FRI 2
+#define ZKM_REC_CHIP_SELECT 3
+#define ZKM_REC_CHIP_FRI_FOLD 4
+#define ZKM_REC_CHIP_PUBLIC_VALUES 5
+#define ZKM_REC_CHIP_MEMORY_VAR 6
+#define ZKM_REC_CHIP_MEMORY_CONST 7
+int zkm_recursion_events_to_trace(uint32_t chip, const uint32_t *events, uint64_t n, uint32_t repr, uint32_t *trace,
+                                  uint64_t height, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -87,6 +87,73 @@ def test_tree_with_witness_pool_matches_serial(fib_leaves):
     assert np.array_equal(root[0].commit, want[0].commit)
 
 
+def _host_layout(v):
+    """A compact witness's device work item laid out on the host (what the kernels must produce)."""
+    if isinstance(v, CT.DeviceRows):
+        from zkmips_amd import tracegen as TG
+        _, w, k = TG.RECURSION_EVENT_CHIPS[v.chip]
+        return R._lay_out(v.events, max(k, 1), v.height) if k else np.zeros((v.height, 1), np.uint32)
+    if isinstance(v, CT.DeviceP2):
+        t = np.zeros((v.height, R.P2_COLS), np.uint32)
+        t[:len(v.inputs)] = R.poseidon2_rows(v.inputs.astype(np.uint64)).astype(np.uint32)
+        t[len(v.inputs):] = R.poseidon2_rows(np.zeros((1, R.WIDTH), np.uint64)).astype(np.uint32)
+        return t
+    assert isinstance(v, CT.DeviceExpRev)
+    t = np.zeros((v.height, 7), np.uint32)
+    for e in range(len(v.base)):
+        acc = 1
+        x = int(v.base[e])
+        for r in range(v.offsets[e], v.offsets[e + 1]):
+            b = int(v.bits[r])
+            mult = x if b == 1 else 1
+            psq = acc * acc % R.P
+            acc = psq * mult % R.P
+            t[r] = [x, b, psq, acc, acc, acc * acc % R.P, mult]
+    return t
+
+
+def test_compact_witness_is_the_full_witness(fib_leaves):
+    """node_witness(compact=True): its device work items laid out as the kernels lay them out are the host
+    main traces, its Prep carries the host prep traces, and a second node of the same structure from the
+    same worker omits them (same prep_key), to be filled in by register_prep."""
+    CT._SENT_KEYS.clear()
+    full = CT.node_witness(fib_leaves[:2], fix=False)
+    comp = CT.node_witness(fib_leaves[:2], fix=False, compact=True)
+    assert isinstance(comp[0], CT.Prep) and comp[0].traces is not None
+    assert set(comp[0].traces) == set(full[0]) and all(np.array_equal(comp[0].traces[k], full[0][k]) for k in full[0])
+    assert set(comp[1]) == set(full[1])
+    for k, v in comp[1].items():
+        assert np.array_equal(_host_layout(v), full[1][k]), k
+    assert np.array_equal(comp[2], full[2]) and comp[3] == full[3]
+    # the other two leaves: a different witness, the same program structure -> same key, prep omitted
+    other = CT.node_witness(fib_leaves[2:], fix=False, compact=True)
+    assert other[0].key == comp[0].key and other[0].traces is None
+    assert not np.array_equal(_host_layout(other[1]["MemoryVar"]), _host_layout(comp[1]["MemoryVar"]))
+    CT.register_prep(comp)
+    assert CT._prep_traces_of(other[0]) is comp[0].traces
+    # dedup off: always sent
+    assert CT.node_witness(fib_leaves[2:], fix=False, compact=True, dedup=False)[0].traces is not None
+
+
+def test_prep_key_tracks_the_prep_traces(fib_leaves):
+    """prep_key follows what the preprocessed traces are made of: a changed constant or shape changes the
+    key, a changed hinted (witness) value does not."""
+    prog = RV.compress_node_program(fib_leaves[:2])
+    rec = R.execute(prog)
+    h = {k: max(4, (v - 1).bit_length()) for k, v in R.program_heights(prog).items()}
+
+    def key(p):  # the key of p's instructions (prep_key reads only the flattened program and heights)
+        return R.prep_key(R.ExecutionRecord(p, R.flatten(p), rec.ev, rec.public_values), h)
+    k0 = R.prep_key(rec, h)
+    assert key(prog) == k0
+    assert R.prep_key(rec, dict(h, MemoryVar=h["MemoryVar"] + 1)) != k0
+    for kind, same in (("mem", False), ("hint", True)):
+        p = R._copy_program(prog)
+        b = next(b for b in p.blocks if b.kind == kind)
+        b.a["vals"][0, 0] = (int(b.a["vals"][0, 0]) + 1) % R.P
+        assert (key(p) == k0) == same, kind
+
+
 def test_node_rejects_malformed_child(fib_leaves):
     """Shape checks before the program is built (verifier.rs:248-312): a proof with a dropped query, or
     claimed for a different verifying key, is a ValueError, not a different program."""
@@ -143,7 +210,16 @@ def test_gpu_mips_node_reference_shape():
     rc, ref = o.prove(tr, pv)
     assert rc == 0 and gpu == ref
     assert o.verify(gpu) == 0
-    # the bench's form: the Poseidon2WideDeg3 trace built on the device from the permutation inputs
+    # the device-P2 form: the Poseidon2WideDeg3 trace built on the device from the permutation inputs
     prep_d, tr_d, pv_d, shape_d, _ = CT.node_witness(leaves, True, True)
     assert isinstance(tr_d["Poseidon2WideDeg3"], CT.DeviceP2) and shape_d == shape
     assert HipProver(dev, cm, prep_d, **kw).prove_shard(CT.materialize(tr_d), pv_d) == gpu
+    # the bench's compact form: every main trace laid out on the device from its events, the proving key
+    # found by prep_key (GpuProvers)
+    wit = CT.node_witness(leaves, True, True, True, False)
+    assert all(isinstance(v, (CT.DeviceRows, CT.DeviceExpRev, CT.DeviceP2)) for v in wit[1].values())
+    dt = CT.materialize(wit[1])
+    for k, v in dt.items():
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), tr[k]), k
+    pr = CT.GpuProvers(dev).get(wit[0], CT.TreeStats())
+    assert pr.prove_shard(dt, wit[2]) == gpu

@@ -119,6 +119,49 @@ def test_program_oracle_proves_and_verifies(name):
     assert rc == 0 and o.verify(proof) == 0
 
 
+@pytest.mark.parametrize("name", list(PROGRAMS) + ["fri_fold", "verifier_shaped"])
+def test_native_runtime_equals_numpy_runtime(name):
+    """The native runtime (csrc/host/rec_exec.cpp) against the numpy one: the same event rows, resolved
+    multiplicities and public values, so the same traces."""
+    make = {"fri_fold": R.program_fri_fold, "verifier_shaped": lambda: R.program_verifier_shaped(SMALL_SHAPE)}
+    prog = make[name]() if name in make else PROGRAMS[name]()
+    a = R.execute(prog)
+    b = R.execute_numpy(R._copy_program(prog))
+    for k in b.ev:
+        assert a.ev[k].shape == b.ev[k].shape and np.array_equal(a.ev[k], b.ev[k]), k
+    for k in b.flat.a:
+        for nm, v in b.flat.a[k].items():
+            assert np.array_equal(a.flat.a[k][nm], v), (k, nm)
+    assert np.array_equal(a.public_values, b.public_values)
+    for x, y in zip(R.generate_traces(a), R.generate_traces(b)):
+        assert set(x) == set(y) and all(np.array_equal(x[k], y[k]) for k in x)
+    # the per-block event view of the native record is the numpy runtime's
+    for k, evs in b.events.items():
+        for e, f in zip(a.events[k], evs):
+            assert set(e) == set(f) and all(np.array_equal(e[nm], f[nm]) for nm in e), k
+
+
+def test_native_runtime_rejects_what_the_numpy_one_rejects():
+    """Write-once memory: a second write, a read of an unwritten address, a read inside the block that
+    writes it, and a constant-memory read of a different value are RuntimeErrors naming the block."""
+    def prog(build):
+        p = R.RecursionProgram(num_addrs=8)
+        p.mem_write([0, 1], [[2, 0, 0, 0], [3, 0, 0, 0]])
+        build(p)
+        return p
+    bad = [lambda p: p.base_alu(R.OP_ADD, [0], [0], [1]),                  # writes address 0 again
+           lambda p: p.base_alu(R.OP_MUL, [2], [5], [1]),                  # reads unwritten address 5
+           lambda p: p.base_alu(R.OP_ADD, [2, 3], [0, 2], [1, 1]),         # reads 2 in the block writing it
+           lambda p: p.mem_read([1], [[4, 0, 0, 0]]),                      # constant read of a wrong value
+           lambda p: p.select([0], [2], [2], [0], [1])]                    # both outputs to one address
+    for f in bad:
+        with pytest.raises(RuntimeError, match="block 1"):
+            R.execute(prog(f))
+        with pytest.raises(RuntimeError):
+            R.execute_numpy(prog(f))
+    R.execute(prog(lambda p: p.base_alu(R.OP_DIV, [2], [0], [1])))
+
+
 def test_verifier_shaped_program():
     prog = R.program_verifier_shaped(SMALL_SHAPE)
     m, pr, tr, pvs = R.shard(prog, SMALL_SHAPE)
@@ -308,6 +351,30 @@ def test_gpu_device_poseidon2_trace_proves_identically(dev):
         .cpu().numpy().view(np.uint32)
     gpu = HipProver(dev, m, pr, num_queries=NQ, log_blowup=LB)
     assert gpu.prove_shard(dev_tr, pvs) == gpu.prove_shard(tr, pvs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("montgomery", [False, True])
+def test_gpu_recursion_event_rows_equal_host(dev, montgomery):
+    """zkm_recursion_events_to_trace (BaseAlu, ExtAlu, BatchFRI, Select, FriFold, PublicValues, MemoryVar,
+    MemoryConst) == the host main traces, padding rows included, for the wide machine's programs and the
+    verifier-shaped program at its shape; canonical and Montgomery event words."""
+    import torch
+    from zkmips_amd import tracegen as TG
+    for prog, shape in ((R.program_fri_fold(), None), (R.program_batch_fri(), None), (R.program_select(300), None),
+                        (R.program_verifier_shaped(SMALL_SHAPE), SMALL_SHAPE), (R.RecursionProgram(), None)):
+        rec = R.execute(prog)
+        want = R.main_traces(rec, shape, p2_main=False)
+        h = R._heights(rec, shape or {})
+        for chip in TG.RECURSION_EVENT_CHIPS:
+            ev = (np.zeros((0, 1), np.uint32) if chip == "MemoryConst" else np.ascontiguousarray(R.main_events(rec, chip)))
+            words = ev if not montgomery else ((ev.astype(np.uint64) << np.uint64(32)) % np.uint64(R.P)).astype(np.uint32)
+            t = torch.from_numpy(words.reshape(-1).view(np.int32).copy() if words.size else np.zeros(1, np.int32)).cuda()
+            got = TG.recursion_events_trace(chip, t, len(ev), h[chip], montgomery=montgomery)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), want[chip]), chip
+    with pytest.raises(Exception):
+        TG.recursion_events_trace("BaseAlu", torch.zeros(3 * 65, dtype=torch.int32, device="cuda"), 65, 16)
 
 
 @pytest.mark.gpu

@@ -16,10 +16,13 @@ def main():
     from zkmips_amd._lib import Device
     dev = Device(0)
     leaves, info = bench.mips_leaves(dev, 84, n_leaves=2, distinct=2)
-    for p2dev in (False, True):
+    import pickle
+    for p2dev, compact in ((False, False), (True, False), (True, True)):
         t = time.perf_counter()
-        prep, tr, pv, shape, times = CT.node_witness(leaves, True, p2dev)
+        wit = CT.node_witness(leaves, True, p2dev, compact, False)
         wit_s = time.perf_counter() - t
+        prep, tr, pv, shape, times = wit
+        mb = len(pickle.dumps(wit, protocol=pickle.HIGHEST_PROTOCOL)) / 1e6
         provers = CT.GpuProvers(dev)
         pr = provers.get(prep, CT.TreeStats())
         for _ in range(2):
@@ -30,10 +33,10 @@ def main():
             proof = pr.prove_shard(CT.materialize(tr), pv)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) / 5 * 1e3
-        print(f"p2_on_device={p2dev}: witness {wit_s:.2f} s ({times}), proof {ms:.2f} ms serial, "
+        print(f"p2_on_device={p2dev} compact={compact}: witness {wit_s:.2f} s ({times}), {mb:.1f} MB pickled, "
+              f"proof {ms:.2f} ms serial, "
               f"{len(proof)} bytes, max rows {max(v.shape[0] for v in CT.materialize(tr).values())}", flush=True)
-    dt = {k: torch.from_numpy(v.view('int32')).cuda() if not isinstance(v, CT.DeviceP2) else v for k, v in tr.items()}
-    dt = CT.materialize(dt)
+    dt = CT.materialize(tr)  # the compact witness: every trace built on the device
     prof, serial_ms, text = bench.profile_proofs(pr, dt, pv, 3)
     print(f"all traces resident: {serial_ms:.2f} ms serial")
     for k, v in sorted(prof.items(), key=lambda kv: -kv[1][1]):

@@ -39,17 +39,105 @@ class DeviceP2:
     height: int
 
 
-def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool = False):
+@dataclass
+class DeviceRows:
+    """A recursion chip's main trace laid out on the GPU from its event rows (tracegen.recursion_events_trace,
+    zkm_recursion_events_to_trace): n x width canonical words, no padding rows."""
+    chip: str
+    events: np.ndarray
+    height: int
+
+
+@dataclass
+class DeviceExpRev:
+    """ExpReverseBitsLen's main trace built on the GPU (tracegen.exp_reverse_bits_trace): each event's base,
+    its exponent bits and the events' row offsets."""
+    base: np.ndarray
+    bits: np.ndarray
+    offsets: np.ndarray
+    height: int
+
+
+@dataclass
+class Prep:
+    """A node program's proving-key identity (recursion.prep_key) and its preprocessed traces -- None when the
+    worker that built this witness already sent them with an earlier one (register_prep keeps them)."""
+    key: bytes
+    traces: Optional[dict]
+
+
+_SENT_KEYS: set = set()          # worker side: keys whose traces this process already returned
+_PREP_STORE: Dict[bytes, dict] = {}  # consumer side: traces of every key seen
+_STORE_LOCK = threading.Lock()
+
+
+def register_prep(wit):
+    """Record a compact witness's preprocessed traces on the consuming side (called in arrival order, before
+    any witness of the same worker that omits them is proven)."""
+    p = wit[0]
+    if isinstance(p, Prep) and p.traces is not None:
+        with _STORE_LOCK:
+            _PREP_STORE[p.key] = p.traces
+    return wit
+
+
+def _prep_traces_of(p: "Prep") -> dict:
+    if p.traces is not None:
+        return p.traces
+    with _STORE_LOCK:
+        t = _PREP_STORE.get(p.key)
+    if t is None:
+        raise RuntimeError("compress node: preprocessed traces of this program were never received")
+    return t
+
+
+def compact_traces(rec, shape) -> dict:
+    """The node's main traces as device work items: the event-row chips (DeviceRows), ExpReverseBitsLen
+    (DeviceExpRev) and Poseidon2WideDeg3 (DeviceP2) -- the events only, no padding rows."""
+    from . import recursion as R
+    h = R._heights(rec, shape)
+    out = {"MemoryConst": DeviceRows("MemoryConst", np.zeros((0, 1), np.uint32), h["MemoryConst"])}
+    for name in ("MemoryVar", "BaseAlu", "ExtAlu", "BatchFRI", "Select", "PublicValues"):
+        out[name] = DeviceRows(name, np.ascontiguousarray(R.main_events(rec, name)), h[name])
+    er = rec.ev["exprev"]
+    L = rec.flat.a["exprev"]["L"]
+    off = np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
+    out["ExpReverseBitsLen"] = DeviceExpRev(np.ascontiguousarray(er[off[:-1], 0]), np.ascontiguousarray(er[:, 1]), off,
+                                            h["ExpReverseBitsLen"])
+    out["Poseidon2WideDeg3"] = DeviceP2(R.p2_inputs(rec), h["Poseidon2WideDeg3"])
+    return out
+
+
+def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool = False, compact: bool = False,
+                 dedup: bool = True):
     """Worker body (no GPU): the compress node's program from its (ChildVk, proof) children, executed,
     padded to the first allowed recursion shape (fix=False: natural power-of-two heights, for small
     tests), as a compress-machine shard.  Returns (prep traces, main traces, public values, shape,
-    seconds); with p2_on_device the Poseidon2WideDeg3 entry is a DeviceP2 (see materialize)."""
+    seconds); with p2_on_device the Poseidon2WideDeg3 entry is a DeviceP2 (see materialize).  compact:
+    every main trace is a device work item (compact_traces) and the prep traces a Prep, sent once per
+    program structure and worker process (dedup; a consumer must pass the witnesses of one worker through
+    register_prep in the order they were made, as Reducer does) -- a fraction of the bytes through the
+    pool's pipe."""
     from . import recursion as R
     from . import recursion_verifier as RV
     t0 = time.perf_counter()
     prog = RV.compress_node_program(children)
     t1 = time.perf_counter()
     shape = R.fix_shape(prog) if fix else {k: max(4, (h - 1).bit_length()) for k, h in R.program_heights(prog).items()}
+    if compact:
+        rec = R.execute(prog)
+        if rec.flat.n["frifold"]:
+            raise ValueError("FriFold instructions need the wide machine")
+        key = R.prep_key(rec, shape)
+        prep = None
+        if not dedup or key not in _SENT_KEYS:
+            pt = R.prep_traces(rec, shape)
+            prep = {c.name: pt[c.name] for c in R.compress_machine().chips if c.prep_width}
+            if dedup:
+                _SENT_KEYS.add(key)
+        traces = compact_traces(rec, shape)
+        t2 = time.perf_counter()
+        return Prep(key, prep), traces, rec.public_values, shape, {"build_s": t1 - t0, "execute_and_traces_s": t2 - t1}
     if p2_on_device:
         _, prep, traces, pvs, p2in, p2h = R.shard_parts(prog, shape)
         traces["Poseidon2WideDeg3"] = DeviceP2(p2in, p2h)
@@ -60,19 +148,30 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
 
 
 def materialize(traces: dict) -> dict:
-    """Build every DeviceP2 entry's trace on the current GPU (rows past the inputs: the permutation of
-    zero) and wait for it; other entries pass through."""
+    """Build every device work item's trace on the current GPU (DeviceP2: rows past the inputs the
+    permutation of zero; DeviceRows / DeviceExpRev: zero padding rows) and wait for them; other entries
+    pass through."""
     out = dict(traces)
-    for k, v in traces.items():
+    todo = [(k, v) for k, v in traces.items() if isinstance(v, (DeviceP2, DeviceRows, DeviceExpRev))]
+    if not todo:
+        return out
+    import torch
+    from . import tracegen as TG
+
+    def up(a, dtype=np.int32):
+        a = np.ascontiguousarray(a)
+        return torch.from_numpy(a.view(dtype).reshape(-1) if a.size else np.zeros(1, dtype)).cuda()
+    for k, v in todo:
         if isinstance(v, DeviceP2):
-            import torch
-            from . import tracegen as TG
             n = len(v.inputs)
             ev = np.zeros((max(n, 1), 32), np.uint32)
             ev[:n, :16] = v.inputs
-            evd = torch.from_numpy(ev.view(np.int32)).cuda()
-            out[k] = TG.poseidon2_wide_trace(evd, n, v.height)
-            torch.cuda.current_stream().synchronize()
+            out[k] = TG.poseidon2_wide_trace(up(ev), n, v.height)
+        elif isinstance(v, DeviceRows):
+            out[k] = TG.recursion_events_trace(v.chip, up(v.events), len(v.events), v.height)
+        else:
+            out[k] = TG.exp_reverse_bits_trace(up(v.base), up(v.bits), up(v.offsets, np.int64), len(v.base), v.height)
+    torch.cuda.current_stream().synchronize()
     return out
 
 
@@ -128,14 +227,20 @@ class GpuProvers:
         self.lock = threading.Lock()
 
     def get(self, prep, stats: TreeStats):
+        """The prover of a node's program: prep is its preprocessed traces, or a Prep (compact witness)."""
         from .prover import HipProver
-        key = prep_digest(prep)
+        if isinstance(prep, Prep):
+            register_prep((prep,))
+            key = prep.key
+        else:
+            key = prep_digest(prep)
         with self.lock:
             stats.lookups += 1
             pr = self.cache.get(key)
             if pr is None:
                 t = time.perf_counter()
-                pr = HipProver(self.dev, self.machine, prep, **self.kw)
+                pt = _prep_traces_of(prep) if isinstance(prep, Prep) else prep
+                pr = HipProver(self.dev, self.machine, pt, **self.kw)
                 stats.setup_s += time.perf_counter() - t
                 stats.setups += 1
                 self.cache[key] = pr
@@ -181,9 +286,11 @@ class Reducer:
     witness(children) -> concurrent.futures.Future of node_witness's result;
     prove(witness) -> (child vk, proof bytes) for the parent (GPU, called from `inflight` threads)."""
 
-    def __init__(self, submit_witness: Callable, prove: Callable, inflight: int = 3):
+    def __init__(self, submit_witness: Callable, prove: Callable, inflight: int = 3,
+                 on_witness: Callable = register_prep):
         self.submit_witness = submit_witness
         self.prove = prove
+        self.on_witness = on_witness  # called on each witness in arrival order, before it is queued
         self.inflight = max(1, inflight)
         self.events: "queue.Queue" = queue.Queue()
         self.gpu_q: "queue.Queue" = queue.Queue()
@@ -235,7 +342,7 @@ class Reducer:
                 except queue.Empty:
                     continue
                 if kind == "witness":
-                    self.gpu_q.put((node, val.result()))
+                    self.gpu_q.put((node, self.on_witness(val.result())))
                 elif kind == "proof":
                     done[node] = val
                     pending.discard(node)

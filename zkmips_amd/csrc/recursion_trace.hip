@@ -118,9 +118,48 @@ __global__ __launch_bounds__(256) void k_exp_rev_rows(const uint32_t *__restrict
     }
 }
 
+// Recursion chips whose main rows are their events (zkm_recursion_events_to_trace): with k events of w words
+// per row the trace's word j (row-major) is event word j, so one pass writes every word of the trace, 16
+// bytes per thread: event words converted to canonical, zero past the events.
+__global__ __launch_bounds__(256) void k_event_rows(const uint32_t *__restrict__ ev, uint64_t n_words, uint32_t repr,
+                                                    uint32_t *__restrict__ out, uint64_t total_words) {
+    using namespace kb;
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t w0 = 4 * q;
+    if (w0 >= total_words) return;
+    auto canon = [&](uint32_t v) { return repr == ZKM_REPR_MONTGOMERY ? from_mont(v < P ? v : v - P) : (v < P ? v : v - P); };
+    uint32_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = w0 + i < n_words ? canon(ev[w0 + i]) : 0u;
+    reinterpret_cast<uint4 *>(out)[q] = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 }  // namespace zkm::rtg
 
 using namespace zkm::rtg;
+
+extern "C" int zkm_recursion_events_to_trace(uint32_t chip, const uint32_t *events, uint64_t n, uint32_t repr,
+                                             uint32_t *trace, uint64_t height, void *stream) {
+    // (words per event, events per row), indexed by ZKM_REC_CHIP_*
+    static const uint32_t layout[8][2] = {{3, 4}, {12, 4}, {13, 1}, {5, 1}, {33, 1}, {1, 1}, {4, 2}, {1, 0}};
+    if (chip > ZKM_REC_CHIP_MEMORY_CONST || !trace || (n && !events) || height < 16 || (height & (height - 1)) ||
+        (repr != ZKM_REPR_CANONICAL && repr != ZKM_REPR_MONTGOMERY) ||
+        (chip == ZKM_REC_CHIP_MEMORY_CONST ? n != 0 : n > height * layout[chip][1])) {
+        g_last_error = "zkm_recursion_events_to_trace: bad arguments (known chip, n events fitting height rows, "
+                       "height a power of two >= 16, repr canonical or Montgomery)";
+        return ZKM_ERR_ARG;
+    }
+    const uint64_t w = layout[chip][0], width = chip == ZKM_REC_CHIP_MEMORY_CONST ? 1 : w * layout[chip][1];
+    const uint64_t total = height * width;  // a multiple of 16: height is
+    hipLaunchKernelGGL(k_event_rows, dim3((uint32_t)((total / 4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       events, n * w, repr, trace, total);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_recursion_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
 
 extern "C" int zkm_poseidon2_wide_events_to_trace(const zkm_poseidon2_event *events, uint64_t n, uint32_t repr,
                                                   uint32_t *trace, uint64_t height, void *stream) {

@@ -95,7 +95,12 @@ def _host(name: str):
         u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
         f.argtypes = {"zkm_host_ef_mul": [u32p, u32p, u32p, C.c_uint64],
                       "zkm_host_batch_fri": [u32p, u32p, u32p, C.c_uint64, C.c_uint64, u32p],
-                      "zkm_host_poseidon2_permute": [u32p, u32p, C.c_uint64]}[name]
+                      "zkm_host_poseidon2_permute": [u32p, u32p, C.c_uint64],
+                      "zkm_host_recursion_execute": [C.c_uint64, C.c_uint64,
+                                                     np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS"),
+                                                     C.c_void_p, C.c_char_p, C.c_uint64]}[name]
+        if name == "zkm_host_recursion_execute":
+            f.restype = C.c_int
         _HOST[name] = f
     return f
 
@@ -245,7 +250,7 @@ def poseidon2_rows(inputs: np.ndarray) -> np.ndarray:
 
 def p2_inputs(rec: ExecutionRecord) -> np.ndarray:
     """The program's Poseidon2 inputs in instruction order (n x 16 canonical): the Poseidon2WideDeg3 events."""
-    return _cat([e["inputs"] for e in rec.events["p2"]], (WIDTH,)).astype(np.uint32)
+    return np.ascontiguousarray(rec.ev["p2"][:, :WIDTH])
 
 
 def poseidon2_permute_host(inputs: np.ndarray) -> np.ndarray:
@@ -432,16 +437,235 @@ def resolve_mults(prog: RecursionProgram) -> None:
 
 # ------------------------------------------------------------------ runtime
 
+KINDS = ("mem", "hint", "base", "ext", "p2", "select", "exprev", "batchfri", "frifold", "commit")
+_KIND_CODE = {k: i for i, k in enumerate(KINDS)}
+# zkm_host_recursion_execute's pointer slots (csrc/host/rec_exec.cpp enum Slot), in order
+_RX_SLOTS = ("mem.addr", "mem.vals", "mem.write", "hint.addr", "hint.vals",
+             "base.op", "base.out", "base.in1", "base.in2", "ev.base",
+             "ext.op", "ext.out", "ext.in1", "ext.in2", "ev.ext",
+             "p2.out", "p2.inp", "ev.p2",
+             "select.bit", "select.out1", "select.out2", "select.in1", "select.in2", "ev.select",
+             "exprev.base", "exprev.result", "exprev.exps", "ev.exprev",
+             "batchfri.acc", "batchfri.alpha_pow", "batchfri.p_at_z", "batchfri.p_at_x", "ev.batchfri",
+             "frifold.x", "frifold.z", "frifold.alpha", "frifold.p_at_x", "frifold.p_at_z", "frifold.alpha_pow_in",
+             "frifold.ro_in", "frifold.alpha_pow_out", "frifold.ro_out", "ev.frifold",
+             "commit.pv", "ev.commit", "mem_image")
+# event row widths (the chips' main-trace rows; p2: input[16] + output[16]; commit: all public values)
+EV_WIDTH = {"base": 3, "ext": 3 * D, "p2": 2 * WIDTH, "select": 5, "exprev": 7, "batchfri": 13, "frifold": 33,
+            "commit": PROOF_MAX_NUM_PVS}
+
+
 @dataclass
+class FlatProgram:
+    """A program flattened by instruction kind: every kind's operand arrays concatenated in program order
+    (`a[kind][name]`), and a block table (nblocks x 5 int64: kind code, first entry, entries, row length L,
+    first flat row) -- the form the native runtime and the vectorised trace builders take.  Entries of
+    exprev / batchfri have L rows each (their address matrices are flattened to rows); a frifold block is
+    one entry of L rows; `mult` arrays are resolved (no -1 left)."""
+    num_addrs: int
+    table: np.ndarray
+    a: Dict[str, Dict[str, np.ndarray]]
+    n: Dict[str, int]       # entries per kind
+    rows: Dict[str, int]    # flat rows per kind (exprev, batchfri, frifold)
+
+
+_FLAT_FIELDS = {
+    "mem": (("addr", np.int64), ("vals", np.uint32), ("write", np.uint8), ("mult", np.int64)),
+    "hint": (("addr", np.int64), ("vals", np.uint32), ("mult", np.int64)),
+    "base": (("op", np.int64), ("out", np.int64), ("in1", np.int64), ("in2", np.int64), ("mult", np.int64)),
+    "ext": (("op", np.int64), ("out", np.int64), ("in1", np.int64), ("in2", np.int64), ("mult", np.int64)),
+    "p2": (("out", np.int64), ("inp", np.int64), ("mult", np.int64)),
+    "select": (("bit", np.int64), ("out1", np.int64), ("out2", np.int64), ("in1", np.int64), ("in2", np.int64),
+               ("mult1", np.int64), ("mult2", np.int64)),
+    "exprev": (("base", np.int64), ("result", np.int64), ("mult", np.int64)),
+    "batchfri": (("acc", np.int64), ("mult", np.int64)),
+    "frifold": (("x", np.int64), ("z", np.int64), ("alpha", np.int64)),
+    "commit": (("pv", np.int64),),
+}
+_FLAT_ROWS = {"exprev": ("exps",), "batchfri": ("alpha_pow", "p_at_z", "p_at_x"),
+              "frifold": ("p_at_x", "p_at_z", "alpha_pow_in", "ro_in", "alpha_pow_out", "ro_out", "apm", "rom")}
+_FLAT_TAIL = {("mem", "vals"): (D,), ("hint", "vals"): (D,), ("p2", "out"): (WIDTH,), ("p2", "inp"): (WIDTH,),
+              ("p2", "mult"): (WIDTH,), ("commit", "pv"): (PROOF_MAX_NUM_PVS,)}
+
+
+def flatten(prog: RecursionProgram) -> FlatProgram:
+    """The program's FlatProgram, with the write multiplicities resolved (recursion compiler's job in the
+    reference): -1 becomes the number of reads of the address."""
+    parts = {k: {nm: [] for nm, _ in _FLAT_FIELDS[k]} for k in KINDS}
+    rparts = {k: {nm: [] for nm in v} for k, v in _FLAT_ROWS.items()}
+    lens = {k: [] for k in _FLAT_ROWS}
+    table = np.zeros((len(prog.blocks), 5), np.int64)
+    n = {k: 0 for k in KINDS}
+    rows = {k: 0 for k in _FLAT_ROWS}
+    for bi, b in enumerate(prog.blocks):
+        k, a = b.kind, b.a
+        if k == "frifold":
+            cnt, L = 1, a["p_at_z"].shape[1]
+        elif k in ("exprev", "batchfri"):
+            key = "exps" if k == "exprev" else "p_at_x"
+            cnt, L = a[key].shape
+        elif k == "commit":
+            cnt, L = 1, 0
+        else:
+            cnt, L = len(next(iter(a.values()))), 0
+        table[bi] = (_KIND_CODE[k], n[k], cnt, L, rows.get(k, 0))
+        for nm, _ in _FLAT_FIELDS[k]:
+            parts[k][nm].append(a[nm])
+        if k in _FLAT_ROWS:
+            for nm in _FLAT_ROWS[k]:
+                rparts[k][nm].append(a[nm].reshape(-1))
+            lens[k].append(np.full(cnt, L, np.int64))
+            rows[k] += cnt * L
+        n[k] += cnt
+    out = {}
+    for k in KINDS:
+        d = {}
+        for nm, dt in _FLAT_FIELDS[k]:
+            xs = parts[k][nm]
+            tail = _FLAT_TAIL.get((k, nm), ())
+            if k in ("frifold",) or k == "commit":
+                xs = [np.asarray(x).reshape((-1,) + tail) for x in xs]
+            d[nm] = (np.ascontiguousarray(np.concatenate(xs).astype(dt, copy=False)) if xs
+                     else np.zeros((0,) + tail, dt))
+        if k in _FLAT_ROWS:
+            for nm in _FLAT_ROWS[k]:
+                xs = rparts[k][nm]
+                d[nm] = np.ascontiguousarray(np.concatenate(xs).astype(np.int64)) if xs else np.zeros(0, np.int64)
+            d["L"] = np.concatenate(lens[k]) if lens[k] else np.zeros(0, np.int64)
+        out[k] = d
+    fp = FlatProgram(prog.num_addrs, table, out, n, rows)
+    _resolve_mults_flat(fp)
+    return fp
+
+
+def _resolve_mults_flat(fp: FlatProgram) -> None:
+    """resolve_mults on the flat arrays, vectorised: one count of every read (runtime/mod.rs mr() calls the
+    AIR matches with a receive), then every '-1' write multiplicity set to its address's count."""
+    a = fp.a
+    na = fp.num_addrs
+    reads = [a["base"]["in1"], a["base"]["in2"], a["ext"]["in1"], a["ext"]["in2"], a["p2"]["inp"].ravel(),
+             a["select"]["bit"], a["select"]["in1"], a["select"]["in2"], a["exprev"]["base"], a["exprev"]["exps"],
+             a["batchfri"]["alpha_pow"], a["batchfri"]["p_at_z"], a["batchfri"]["p_at_x"],
+             a["commit"]["pv"][:, PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE].ravel(),
+             a["frifold"]["x"], a["frifold"]["z"], a["frifold"]["alpha"], a["frifold"]["p_at_x"],
+             a["frifold"]["p_at_z"], a["frifold"]["alpha_pow_in"], a["frifold"]["ro_in"]]
+    cnt = np.bincount(np.concatenate(reads).astype(np.int64), minlength=na).astype(np.int64)
+    rd = a["mem"]["write"] == 0
+    if rd.any():
+        np.add.at(cnt, a["mem"]["addr"][rd], a["mem"]["mult"][rd])
+    for k, an, mn, sel in (("mem", "addr", "mult", "write"), ("hint", "addr", "mult", None),
+                           ("base", "out", "mult", None), ("ext", "out", "mult", None), ("p2", "out", "mult", None),
+                           ("select", "out1", "mult1", None), ("select", "out2", "mult2", None),
+                           ("exprev", "result", "mult", None), ("batchfri", "acc", "mult", None),
+                           ("frifold", "alpha_pow_out", "apm", None), ("frifold", "ro_out", "rom", None)):
+        m = a[k][mn]
+        auto = m < 0
+        if sel is not None:
+            auto &= a[k][sel].astype(bool)
+        if auto.any():
+            m[auto] = cnt[a[k][an][auto]]
+
+
 class ExecutionRecord:
-    program: RecursionProgram
-    events: Dict[str, List[Dict[str, np.ndarray]]]
-    public_values: np.ndarray
+    """A program's execution: its FlatProgram, the events per kind (`ev`: the chips' main-trace rows,
+    uint32 canonical, concatenated in program order; EV_WIDTH columns) and the committed public values.
+    `events` gives the per-block view (lists of dicts, as the numpy runtime produced them)."""
+
+    def __init__(self, program, flat, ev, public_values, events=None):
+        self.program, self.flat, self.ev, self.public_values = program, flat, ev, public_values
+        self._events = events
+
+    @property
+    def events(self) -> Dict[str, List[Dict[str, np.ndarray]]]:
+        if self._events is None:
+            self._events = _legacy_events(self)
+        return self._events
+
+
+def _legacy_events(rec: ExecutionRecord):
+    ev, out = rec.ev, {k: [] for k in KINDS}
+    for kc, s, n, L, fs in rec.flat.table:
+        k = KINDS[kc]
+        e = ev.get(k)
+        if k == "mem":
+            out[k].append({})
+        elif k == "hint":
+            out[k].append({"vals": rec.flat.a["hint"]["vals"][s:s + n].astype(U)})
+        elif k == "base":
+            x = e[s:s + n].astype(U)
+            out[k].append({"out": x[:, 0], "in1": x[:, 1], "in2": x[:, 2]})
+        elif k == "ext":
+            x = e[s:s + n].astype(U)
+            out[k].append({"out": x[:, 0:4], "in1": x[:, 4:8], "in2": x[:, 8:12]})
+        elif k == "p2":
+            x = e[s:s + n].astype(U)
+            out[k].append({"inputs": x[:, :WIDTH], "outputs": x[:, WIDTH:]})
+        elif k == "select":
+            x = e[s:s + n].astype(U)
+            out[k].append({nm: x[:, j] for j, nm in enumerate(("bit", "out1", "out2", "in1", "in2"))})
+        elif k in ("exprev", "batchfri"):
+            out[k].append({"rows": e[fs:fs + n * L].astype(U), "L": int(L), "n": int(n)})
+        elif k == "frifold":
+            out[k].append({"rows": e[fs:fs + L].astype(U)})
+        elif k == "commit":
+            out[k].append({"pv": e[s].astype(U)})
+    return out
+
+
+def _ev_from_legacy(fp: FlatProgram, events) -> Dict[str, np.ndarray]:
+    ev = {}
+    for k in ("base", "ext", "p2", "select", "exprev", "batchfri", "frifold", "commit"):
+        w = EV_WIDTH[k]
+        es = events[k]
+        if k == "base":
+            xs = [np.stack([e["out"], e["in1"], e["in2"]], 1) for e in es]
+        elif k == "ext":
+            xs = [np.concatenate([e["out"], e["in1"], e["in2"]], 1) for e in es]
+        elif k == "p2":
+            xs = [np.concatenate([e["inputs"], e["outputs"]], 1) for e in es]
+        elif k == "select":
+            xs = [np.stack([e[nm] for nm in ("bit", "out1", "out2", "in1", "in2")], 1) for e in es]
+        elif k == "commit":
+            xs = [e["pv"][None, :] for e in es]
+        else:
+            xs = [e["rows"] for e in es]
+        ev[k] = (np.ascontiguousarray(np.concatenate(xs).astype(np.uint32)) if xs else np.zeros((0, w), np.uint32))
+    return ev
 
 
 def execute(prog: RecursionProgram, mem_out: Optional[dict] = None) -> ExecutionRecord:
-    """Run the program (runtime/mod.rs:336-625): memory is write-once; every value read must have been
-    written by an earlier block.  Returns per-kind event lists in program order."""
+    """Run the program (runtime/mod.rs:336-625) in the native runtime (csrc/host/rec_exec.cpp,
+    libzkm_trace.so): memory is write-once, every value read must have been written by an earlier
+    block, constant-memory reads must match; a violation is a RuntimeError naming the block."""
+    import ctypes as C
+    fp = flatten(prog)
+    a = fp.a
+    ev = {k: np.zeros((fp.rows[k] if k in fp.rows else fp.n[k], EV_WIDTH[k]), np.uint32) for k in EV_WIDTH}
+    img = np.zeros((prog.num_addrs, D), np.uint32) if mem_out is not None else None
+    ptrs = (C.c_void_p * len(_RX_SLOTS))()
+    for i, nm in enumerate(_RX_SLOTS):
+        if nm == "mem_image":
+            arr = img
+        elif nm.startswith("ev."):
+            arr = ev[nm[3:]]
+        else:
+            k, f = nm.split(".")
+            arr = a[k][f]
+        ptrs[i] = None if arr is None or arr.size == 0 else arr.ctypes.data
+    err = C.create_string_buffer(256)
+    f = _host("zkm_host_recursion_execute")
+    rc = f(prog.num_addrs, len(fp.table), np.ascontiguousarray(fp.table), C.cast(ptrs, C.c_void_p), err, 256)
+    if mem_out is not None:
+        mem_out["mem"] = img.astype(U)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    pvs = ev["commit"][-1].copy() if len(ev["commit"]) else np.zeros(PROOF_MAX_NUM_PVS, np.uint32)
+    return ExecutionRecord(prog, fp, ev, pvs)
+
+
+def execute_numpy(prog: RecursionProgram, mem_out: Optional[dict] = None) -> ExecutionRecord:
+    """The same runtime as numpy blocks (the native runtime's cross-check in tests/test_recursion.py):
+    returns per-kind event lists in program order."""
     resolve_mults(prog)
     mem = np.zeros((prog.num_addrs, D), U)
     written = np.zeros(prog.num_addrs, bool)
@@ -570,7 +794,8 @@ def execute(prog: RecursionProgram, mem_out: Optional[dict] = None) -> Execution
             ev["commit"].append({"pv": vals})
         else:
             raise ValueError(k)
-    return ExecutionRecord(prog, ev, pvs)
+    fp = flatten(prog)
+    return ExecutionRecord(prog, fp, _ev_from_legacy(fp, ev), pvs, ev)
 
 
 # ------------------------------------------------------------------ chips (AIR restatement)
@@ -880,183 +1105,177 @@ def _cat(xs, shape_tail, dtype=U):
     return np.concatenate(xs) if xs else np.zeros((0,) + shape_tail, dtype)
 
 
+# main-trace layouts of the chips whose rows are their events (event_to_row of alu_base.hpp, alu_ext.hpp,
+# batch_fri.hpp, select.hpp, fri_fold.hpp, exp_reverse_bits.hpp, public_values.hpp, mem/variable.rs):
+# chip -> (event kind, entries per row); a row is its entries' event rows side by side, padding rows zero
+MAIN_LAYOUT = {"MemoryVar": ("hint", 2), "BaseAlu": ("base", 4), "ExtAlu": ("ext", 4), "BatchFRI": ("batchfri", 1),
+               "Select": ("select", 1), "ExpReverseBitsLen": ("exprev", 1), "FriFold": ("frifold", 1),
+               "PublicValues": ("commit", 1)}
+
+
+def _heights(rec: ExecutionRecord, shape: Dict[str, int]) -> Dict[str, int]:
+    n, rows = rec.flat.n, rec.flat.rows
+    need = {"MemoryConst": (n["mem"] + 1) // 2, "MemoryVar": (n["hint"] + 1) // 2, "BaseAlu": (n["base"] + 3) // 4,
+            "ExtAlu": (n["ext"] + 3) // 4, "Poseidon2WideDeg3": n["p2"], "BatchFRI": rows["batchfri"],
+            "FriFold": rows["frifold"], "Select": n["select"], "ExpReverseBitsLen": rows["exprev"],
+            "PublicValues": 1 << PUB_VALUES_LOG_HEIGHT}
+    return {k: _pow2(v, shape.get(k)) for k, v in need.items()}
+
+
+def main_events(rec: ExecutionRecord, name: str) -> np.ndarray:
+    """The event rows (entries x width, uint32 canonical) chip `name`'s main trace lays out (MAIN_LAYOUT)."""
+    kind, _ = MAIN_LAYOUT[name]
+    if kind == "hint":
+        return rec.flat.a["hint"]["vals"]
+    if kind == "commit":
+        e = rec.ev["commit"]
+        return (e[0, PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE][:, None] if len(e)
+                else np.zeros((0, 1), np.uint32))
+    return rec.ev[kind]
+
+
+def _lay_out(entries: np.ndarray, epr: int, h: int) -> np.ndarray:
+    t = np.zeros((h, epr * entries.shape[1]), np.uint32)
+    t.reshape(-1)[:entries.size] = entries.reshape(-1)
+    return t
+
+
+def _mod(m):
+    return (np.asarray(m, np.int64) % P).astype(np.uint32)
+
+
+def prep_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None) -> Dict[str, np.ndarray]:
+    """The preprocessed traces (instr_to_row of the reference's include/*.hpp, mem/{constant,variable}.rs),
+    row-major uint32 canonical, padded to the shape's heights (zero rows)."""
+    shape = shape or {}
+    a, h = rec.flat.a, _heights(rec, shape)
+    out = {}
+    m = a["mem"]
+    mm = np.where(m["write"].astype(bool), _mod(m["mult"]), _mod(-np.asarray(m["mult"], np.int64)))
+    ent = np.concatenate([m["vals"], m["addr"][:, None].astype(np.uint32), mm[:, None]], 1) if len(mm) else \
+        np.zeros((0, 6), np.uint32)
+    out["MemoryConst"] = _lay_out(ent, 2, h["MemoryConst"])
+    hn = a["hint"]
+    out["MemoryVar"] = _lay_out(np.stack([hn["addr"].astype(np.uint32), _mod(hn["mult"])], 1).reshape(-1, 2), 2,
+                                h["MemoryVar"])
+    for kind, name in (("base", "BaseAlu"), ("ext", "ExtAlu")):
+        x = a[kind]
+        k = len(x["out"])
+        e = np.zeros((k, 8), np.uint32)
+        e[:, 0], e[:, 1], e[:, 2] = x["out"], x["in1"], x["in2"]
+        e[np.arange(k), 3 + x["op"]] = 1
+        e[:, 7] = _mod(x["mult"])
+        out[name] = _lay_out(e, 4, h[name])
+    x = a["p2"]
+    k = len(x["out"])
+    e = np.zeros((k, 49), np.uint32)
+    e[:, 0:16] = x["inp"]
+    e[:, 16:48:2] = x["out"]
+    e[:, 17:48:2] = _mod(x["mult"])
+    e[:, 48] = P - 1
+    out["Poseidon2WideDeg3"] = _lay_out(e, 1, h["Poseidon2WideDeg3"])
+    # BatchFRI / ExpReverseBitsLen: entry q spans L_q rows; i = row within the entry
+    for kind, name in (("batchfri", "BatchFRI"), ("exprev", "ExpReverseBitsLen")):
+        x = a[kind]
+        L = x["L"]
+        q = np.repeat(np.arange(len(L)), L)
+        i = np.arange(len(q)) - np.repeat(np.cumsum(L) - L, L)
+        first, last = i == 0, i == L[q] - 1
+        if kind == "batchfri":
+            e = np.zeros((len(q), 6), np.uint32)
+            e[:, 0] = 1
+            e[:, 1] = last
+            e[:, 2] = x["acc"][q]
+            e[:, 3], e[:, 4], e[:, 5] = x["alpha_pow"], x["p_at_z"], x["p_at_x"]
+        else:
+            e = np.zeros((len(q), 10), np.uint32)
+            e[:, 0] = x["base"][q]
+            e[:, 1] = np.where(first, P - 1, 0)
+            e[:, 2] = x["exps"]
+            e[:, 3] = P - 1
+            e[:, 4] = x["result"][q]
+            e[:, 5] = np.where(last, _mod(x["mult"])[q], 0)
+            e[:, 6] = i
+            e[:, 7], e[:, 8], e[:, 9] = first, last, 1
+        out[name] = _lay_out(e, 1, h[name])
+    x = a["frifold"]
+    L = x["L"]
+    q = np.repeat(np.arange(len(L)), L)
+    first = (np.arange(len(q)) - np.repeat(np.cumsum(L) - L, L)) == 0
+    e = np.zeros((len(q), 20), np.uint32)
+    fm = np.where(first, P - 1, 0)
+    e[:, 0] = first
+    e[:, 1], e[:, 2] = x["z"][q], fm
+    e[:, 3], e[:, 4] = x["alpha"][q], fm
+    e[:, 5], e[:, 6] = x["x"][q], fm
+    for c, nm in ((7, "alpha_pow_in"), (9, "ro_in"), (11, "p_at_x"), (13, "p_at_z")):
+        e[:, c], e[:, c + 1] = x[nm], P - 1
+    e[:, 15], e[:, 16] = x["ro_out"], _mod(x["rom"])
+    e[:, 17], e[:, 18] = x["alpha_pow_out"], _mod(x["apm"])
+    e[:, 19] = 1
+    out["FriFold"] = _lay_out(e, 1, h["FriFold"])
+    x = a["select"]
+    e = np.stack([np.ones(len(x["bit"]), np.int64), x["bit"], x["out1"], x["out2"], x["in1"], x["in2"],
+                  np.asarray(x["mult1"]) % P, np.asarray(x["mult2"]) % P], 1).astype(np.uint32).reshape(-1, 8)
+    out["Select"] = _lay_out(e, 1, h["Select"])
+    e = np.zeros((0, 10), np.uint32)
+    if len(a["commit"]["pv"]):
+        e = np.zeros((DIGEST_SIZE, 10), np.uint32)
+        e[np.arange(DIGEST_SIZE), np.arange(DIGEST_SIZE)] = 1
+        e[:, 8] = a["commit"]["pv"][0, PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE]
+        e[:, 9] = P - 1
+    out["PublicValues"] = _lay_out(e, 1, h["PublicValues"])
+    return out
+
+
+# the FlatProgram arrays prep_traces reads (everything but the hinted values): with the heights they fix
+# the preprocessed traces, so nodes with equal keys share one proving key
+_PREP_INPUTS = {"mem": ("addr", "vals", "write", "mult"), "hint": ("addr", "mult"),
+                "base": ("op", "out", "in1", "in2", "mult"), "ext": ("op", "out", "in1", "in2", "mult"),
+                "p2": ("inp", "out", "mult"), "batchfri": ("acc", "alpha_pow", "p_at_z", "p_at_x", "L"),
+                "exprev": ("base", "exps", "result", "mult", "L"),
+                "frifold": ("x", "z", "alpha", "p_at_x", "p_at_z", "alpha_pow_in", "ro_in", "alpha_pow_out", "ro_out",
+                            "apm", "rom", "L"),
+                "select": ("bit", "out1", "out2", "in1", "in2", "mult1", "mult2"), "commit": ("pv",)}
+
+
+def prep_key(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None) -> bytes:
+    """Identity of the program's preprocessed traces without building them: xxh3-128 over the heights and
+    every array prep_traces reads (tests/test_recursion.py checks equal keys give equal traces)."""
+    import xxhash
+    h = xxhash.xxh3_128()
+    h.update(repr(sorted(_heights(rec, shape or {}).items())).encode())
+    for k in sorted(_PREP_INPUTS):
+        for nm in _PREP_INPUTS[k]:
+            v = np.ascontiguousarray(rec.flat.a[k][nm])
+            h.update(f"{k}.{nm}{v.shape}{v.dtype}".encode())
+            h.update(v.view(np.uint8).data)
+    return h.digest()
+
+
+def main_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None, p2_main: bool = True):
+    """The main traces on the host (event_to_row layouts, padding rows zero; Poseidon2WideDeg3's padding
+    rows are the permutation of zero, trace.rs), row-major uint32 canonical."""
+    shape = shape or {}
+    h = _heights(rec, shape)
+    out = {"MemoryConst": np.zeros((h["MemoryConst"], 1), np.uint32)}
+    for name, (_, epr) in MAIN_LAYOUT.items():
+        out[name] = _lay_out(main_events(rec, name), epr, h[name])
+    if p2_main:
+        hp = h["Poseidon2WideDeg3"]
+        mn = np.zeros((hp, P2_COLS), np.uint32)
+        ins = rec.ev["p2"][:, :WIDTH]
+        mn[:len(ins)] = poseidon2_rows(ins.astype(U)).astype(np.uint32)
+        mn[len(ins):] = poseidon2_rows(np.zeros((1, WIDTH), U)).astype(np.uint32)
+        out["Poseidon2WideDeg3"] = mn
+    return out
+
+
 def generate_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None, p2_main: bool = True):
     """(prep_traces, main_traces) by chip name, row-major uint32 canonical.  p2_main=False leaves out the
     Poseidon2WideDeg3 main trace (313 columns, the largest) for the caller to build on the device from the
     permutation inputs (`p2_inputs`, tracegen.poseidon2_wide_trace)."""
-    shape = shape or {}
-    prog = rec.program
-    bl = lambda k: [b for b in prog.blocks if b.kind == k]
-    preps, mains = {}, {}
-
-    def finish(name, pr, mn, n_rows):
-        h = _pow2(n_rows, shape.get(name))
-        P_ = np.zeros((h, pr.shape[1]), np.uint32)
-        P_[:pr.shape[0]] = pr
-        M_ = np.zeros((h, mn.shape[1]), np.uint32)
-        M_[:mn.shape[0]] = mn
-        preps[name], mains[name] = P_, M_
-        return h
-
-    # MemoryConst: (value[4], addr, mult) x 2, in instruction order
-    ent = []
-    for b in bl("mem"):
-        a = b.a
-        m = np.where(a["write"], a["mult"] % P, _neg(a["mult"]))
-        ent.append(np.concatenate([a["vals"], a["addr"][:, None].astype(U), m[:, None].astype(U)], 1))
-    ent = _cat(ent, (6,))
-    n = (len(ent) + 1) // 2
-    pr = np.zeros((n, 12), U)
-    pr.reshape(-1)[:ent.size] = ent.reshape(-1)
-    finish("MemoryConst", pr, np.zeros((n, 1), U), n)
-
-    # MemoryVar: prep (addr, mult) x 2, main value[4] x 2
-    hs = bl("hint")
-    acc = _cat([np.stack([b.a["addr"].astype(U), b.a["mult"].astype(U) % PU], 1) for b in hs], (2,))
-    vals = _cat([b.a["vals"] for b in hs], (4,))
-    n = (len(acc) + 1) // 2
-    pr = np.zeros((n, 4), U)
-    pr.reshape(-1)[:acc.size] = acc.reshape(-1)
-    mn = np.zeros((n, 8), U)
-    mn.reshape(-1)[:vals.size] = vals.reshape(-1)
-    finish("MemoryVar", pr, mn, n)
-
-    # BaseAlu / ExtAlu
-    for kind, name, w in (("base", "BaseAlu", 1), ("ext", "ExtAlu", D)):
-        bs = bl(kind)
-        evs = [e for e in rec.events[kind]]
-        pa, ma = [], []
-        for b, e in zip(bs, evs):
-            a = b.a
-            k = len(a["out"])
-            p_ = np.zeros((k, 8), U)
-            p_[:, 0], p_[:, 1], p_[:, 2] = a["out"], a["in1"], a["in2"]
-            p_[np.arange(k), 3 + a["op"]] = 1
-            p_[:, 7] = a["mult"] % P
-            pa.append(p_)
-            if w == 1:
-                ma.append(np.stack([e["out"], e["in1"], e["in2"]], 1))
-            else:
-                ma.append(np.concatenate([e["out"], e["in1"], e["in2"]], 1))
-        pa, ma = _cat(pa, (8,)), _cat(ma, (3 * w,))
-        n = (len(pa) + 3) // 4
-        pr = np.zeros((n, 32), U)
-        pr.reshape(-1)[:pa.size] = pa.reshape(-1)
-        mn = np.zeros((n, 12 * w), U)
-        mn.reshape(-1)[:ma.size] = ma.reshape(-1)
-        finish(name, pr, mn, n)
-
-    # Poseidon2WideDeg3: padding rows are the permutation of zero (trace.rs dummy row)
-    bs = bl("p2")
-    pa = []
-    for b in bs:
-        a = b.a
-        k = a["out"].shape[0]
-        p_ = np.zeros((k, 49), U)
-        p_[:, 0:16] = a["inp"]
-        p_[:, 16:48:2] = a["out"]
-        p_[:, 17:48:2] = a["mult"] % P
-        p_[:, 48] = P - 1
-        pa.append(p_)
-    pa = _cat(pa, (49,))
-    name = "Poseidon2WideDeg3"
-    h = _pow2(len(pa), shape.get(name))
-    if p2_main:
-        ma = _cat([poseidon2_rows(e["inputs"]) for e in rec.events["p2"]], (P2_COLS,))
-        mn = np.zeros((h, P2_COLS), U)
-        mn[:len(ma)] = ma
-        mn[len(ma):] = poseidon2_rows(np.zeros((1, WIDTH), U))
-        mains[name] = mn.astype(np.uint32)
-    pr = np.zeros((h, 49), U)
-    pr[:len(pa)] = pa
-    preps[name] = pr.astype(np.uint32)
-
-    # BatchFRI
-    pa = []
-    for b in bl("batchfri"):
-        a = b.a
-        n_, L = a["p_at_x"].shape
-        p_ = np.zeros((n_, L, 6), U)
-        p_[:, :, 0] = 1
-        p_[:, L - 1, 1] = 1
-        p_[:, :, 2] = a["acc"][:, None]
-        p_[:, :, 3] = a["alpha_pow"]
-        p_[:, :, 4] = a["p_at_z"]
-        p_[:, :, 5] = a["p_at_x"]
-        pa.append(p_.reshape(-1, 6))
-    pa = _cat(pa, (6,))
-    ma = _cat([e["rows"] for e in rec.events["batchfri"]], (13,))
-    finish("BatchFRI", pa, ma, len(pa))
-
-    # FriFold (wide machine only; the compress machine has no FriFold chip)
-    pa = []
-    for b in bl("frifold"):
-        a = b.a
-        m_ = a["p_at_z"].shape[1]
-        p_ = np.zeros((m_, 20), U)
-        first = (np.arange(m_) == 0)
-        p_[:, 0] = first
-        p_[:, 1], p_[:, 2] = a["z"][0], np.where(first, P - 1, 0)
-        p_[:, 3], p_[:, 4] = a["alpha"][0], np.where(first, P - 1, 0)
-        p_[:, 5], p_[:, 6] = a["x"][0], np.where(first, P - 1, 0)
-        p_[:, 7], p_[:, 8] = a["alpha_pow_in"][0], P - 1
-        p_[:, 9], p_[:, 10] = a["ro_in"][0], P - 1
-        p_[:, 11], p_[:, 12] = a["p_at_x"][0], P - 1
-        p_[:, 13], p_[:, 14] = a["p_at_z"][0], P - 1
-        p_[:, 15], p_[:, 16] = a["ro_out"][0], a["rom"][0] % P
-        p_[:, 17], p_[:, 18] = a["alpha_pow_out"][0], a["apm"][0] % P
-        p_[:, 19] = 1
-        pa.append(p_)
-    pa = _cat(pa, (20,))
-    ma = _cat([e["rows"] for e in rec.events["frifold"]], (33,))
-    finish("FriFold", pa, ma, len(pa))
-
-    # Select
-    pa, ma = [], []
-    for b, e in zip(bl("select"), rec.events["select"]):
-        a = b.a
-        pa.append(np.stack([np.ones(len(a["bit"]), np.int64), a["bit"], a["out1"], a["out2"], a["in1"], a["in2"],
-                            a["mult1"] % P, a["mult2"] % P], 1).astype(U))
-        ma.append(np.stack([e["bit"], e["out1"], e["out2"], e["in1"], e["in2"]], 1))
-    pa, ma = _cat(pa, (8,)), _cat(ma, (5,))
-    finish("Select", pa, ma, len(pa))
-
-    # ExpReverseBitsLen
-    pa = []
-    for b in bl("exprev"):
-        a = b.a
-        n_, L = a["exps"].shape
-        p_ = np.zeros((n_, L, 10), U)
-        i = np.arange(L)
-        p_[:, :, 0] = a["base"][:, None]
-        p_[:, 0, 1] = P - 1
-        p_[:, :, 2] = a["exps"]
-        p_[:, :, 3] = P - 1
-        p_[:, :, 4] = a["result"][:, None]
-        p_[:, L - 1, 5] = a["mult"] % P
-        p_[:, :, 6] = i[None, :]
-        p_[:, 0, 7] = 1
-        p_[:, L - 1, 8] = 1
-        p_[:, :, 9] = 1
-        pa.append(p_.reshape(-1, 10))
-    pa = _cat(pa, (10,))
-    ma = _cat([e["rows"] for e in rec.events["exprev"]], (7,))
-    finish("ExpReverseBitsLen", pa, ma, len(pa))
-
-    # PublicValues: the first CommitPublicValues' digest, 16 rows (PUB_VALUES_LOG_HEIGHT)
-    pa = np.zeros((0, 10), U)
-    ma = np.zeros((0, 1), U)
-    cs = bl("commit")
-    if cs:
-        addrs = cs[0].a["pv"][0, PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE]
-        pa = np.zeros((DIGEST_SIZE, 10), U)
-        pa[np.arange(DIGEST_SIZE), np.arange(DIGEST_SIZE)] = 1
-        pa[:, 8] = addrs
-        pa[:, 9] = P - 1
-        ma = rec.events["commit"][0]["pv"][PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE][:, None].astype(U)
-    finish("PublicValues", pa, ma, 1 << PUB_VALUES_LOG_HEIGHT)
-    return ({k: np.ascontiguousarray(v.astype(np.uint32)) for k, v in preps.items()},
-            {k: np.ascontiguousarray(v.astype(np.uint32)) for k, v in mains.items()})
+    return prep_traces(rec, shape), main_traces(rec, shape, p2_main)
 
 
 # RecursionShapeConfig::default (crates/recursion/core/src/shape.rs:115-170): the compress programs'
@@ -1108,7 +1327,7 @@ def shard_parts(prog: RecursionProgram, shape: Optional[Dict[str, int]] = None):
     rec = execute(prog)
     pr, tr = generate_traces(rec, shape, p2_main=False)
     m = compress_machine()
-    if rec.events["frifold"]:
+    if rec.flat.n["frifold"]:
         raise ValueError("FriFold instructions need the wide machine")
     pr = {c.name: pr[c.name] for c in m.chips if c.prep_width}
     tr.pop("FriFold", None)
@@ -1122,7 +1341,7 @@ def shard(prog: RecursionProgram, shape: Optional[Dict[str, int]] = None, wide: 
     pr, tr = generate_traces(rec, shape)
     m = wide_machine() if wide else compress_machine()
     if not wide:
-        if rec.events["frifold"]:
+        if rec.flat.n["frifold"]:
             raise ValueError("FriFold instructions need the wide machine")
         pr.pop("FriFold", None)
         tr.pop("FriFold", None)

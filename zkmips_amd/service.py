@@ -330,11 +330,12 @@ class ProverService:
             return CT.compress_child_vk(pr.vk_commit, shape), proof
 
         if self._pool is not None:
-            submit = lambda ch: self._pool.submit(CT.node_witness, ch, True, True)
+            submit = lambda ch: self._pool.submit(CT.node_witness, ch, True, True, True)
         else:
             from concurrent.futures import ThreadPoolExecutor
             tp = ThreadPoolExecutor(2)
-            submit = lambda ch: tp.submit(CT.node_witness, ch, True, True)
+            # threads of this process: no once-per-program prep (arrival order is not completion order)
+            submit = lambda ch: tp.submit(CT.node_witness, ch, True, True, True, False)
         reducer = CT.Reducer(submit, prove, self.compress_inflight)
         try:
             if len(leaves) == 1:  # one shard is still wrapped by a compress node

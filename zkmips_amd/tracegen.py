@@ -396,6 +396,7 @@ def _bind():
         L.zkm_global_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp, vp]
         L.zkm_poseidon2_wide_events_to_trace.argtypes = [vp, u64, C.c_uint32, vp, u64, vp]
         L.zkm_exp_reverse_bits_events_to_trace.argtypes = [vp, vp, vp, u64, C.c_uint32, vp, u64, vp]
+        L.zkm_recursion_events_to_trace.argtypes = [C.c_uint32, vp, u64, C.c_uint32, vp, u64, vp]
         L._tracegen_bound = True
     return L
 
@@ -719,6 +720,23 @@ def exp_reverse_bits_trace(base_dev, bits_dev, offsets_dev, n: int, height: int,
                                                             _words(bits_dev, 0, what) if n else None, _ptr(offsets_dev),
                                                             n, 1 if montgomery else 0, t.data_ptr(), height, _stream()),
                what)
+    return t
+
+
+# zkm_recursion_events_to_trace chips: name -> (ZKM_REC_CHIP_*, words per event, events per row)
+RECURSION_EVENT_CHIPS = {"BaseAlu": (0, 3, 4), "ExtAlu": (1, 12, 4), "BatchFRI": (2, 13, 1), "Select": (3, 5, 1),
+                         "FriFold": (4, 33, 1), "PublicValues": (5, 1, 1), "MemoryVar": (6, 4, 2),
+                         "MemoryConst": (7, 1, 0)}
+
+
+def recursion_events_trace(chip: str, events_dev, n: int, height: int, montgomery: bool = False):
+    """Main trace (height x width int32, canonical, on the GPU) of a recursion chip whose rows are its events
+    (RECURSION_EVENT_CHIPS): n events of the chip's width back to back in a 32-bit GPU tensor."""
+    code, w, k = RECURSION_EVENT_CHIPS[chip]
+    t = _trace(height, w * k if k else 1)
+    what = "zkm_recursion_events_to_trace"
+    _lib.check(_bind().zkm_recursion_events_to_trace(code, _words(events_dev, n * w, what) if n else None, n,
+                                                     1 if montgomery else 0, t.data_ptr(), height, _stream()), what)
     return t
 
 
