@@ -890,7 +890,9 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
         return CT.compress_child_vk(pr.vk_commit, shape), proof
 
     # compact witnesses: main traces as event rows laid out on the device, prep traces once per program
-    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, ch, True, True, True), prove, inflight)
+    # (children's verifying keys by reference: each worker loads a key's file once)
+    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, CT.by_ref(ch), True, True, True), prove,
+                         inflight)
     t0 = time.perf_counter()
     root = CT.reduce_distributed(leaves, reducer) if distributed else CT.reduce_serial(leaves, reducer)
     wall = time.perf_counter() - t0

@@ -78,7 +78,8 @@ def test_tree_with_witness_pool_matches_serial(fib_leaves):
     2 threads) gives the same root as proving the layers one after another."""
     prove = _oracle_prove_factory(4)
     with ProcessPoolExecutor(2, mp_context=mpc.get_context("spawn")) as pool:
-        red = CT.Reducer(lambda ch: pool.submit(_witness_small, ch), prove, inflight=2)
+        # verifying keys by reference (VkRef: written once, loaded once per worker)
+        red = CT.Reducer(lambda ch: pool.submit(_witness_small, CT.by_ref(ch)), prove, inflight=2)
         root = CT.reduce_serial(fib_leaves, red)
     a = prove(_witness_small(fib_leaves[:2]))
     b = prove(_witness_small(fib_leaves[2:]))
@@ -152,6 +153,20 @@ def test_prep_key_tracks_the_prep_traces(fib_leaves):
         b = next(b for b in p.blocks if b.kind == kind)
         b.a["vals"][0, 0] = (int(b.a["vals"][0, 0]) + 1) % R.P
         assert (key(p) == k0) == same, kind
+
+
+def test_vk_by_reference(fib_leaves):
+    """by_ref / resolve_vk: one file per distinct key, the same ChildVk back (a fresh process loads it)."""
+    vk, proof = fib_leaves[0]
+    refs = CT.by_ref(fib_leaves)
+    assert len({r.digest for r, _ in refs}) == 1 and refs[0][1] == proof
+    assert CT.resolve_vk(refs[0][0]) is vk and CT.resolve_vk(vk) is vk
+    import pickle
+    with open(refs[0][0].path, "rb") as f:
+        again = pickle.loads(f.read())
+    assert again.prep_heights == vk.prep_heights and np.array_equal(again.commit, vk.commit)
+    assert CT.compress_child_vk(np.arange(8), R.RECURSION_SHAPES[0]) is CT.compress_child_vk(np.arange(8),
+                                                                                              R.RECURSION_SHAPES[0])
 
 
 def test_node_rejects_malformed_child(fib_leaves):

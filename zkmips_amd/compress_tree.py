@@ -66,6 +66,76 @@ class Prep:
     traces: Optional[dict]
 
 
+@dataclass(frozen=True)
+class VkRef:
+    """A ChildVk passed to a witness worker by reference: its pickle is written once to a file (a few MB
+    for a MIPS child: every chip's constraint program and lookups) and each worker process loads it once,
+    instead of the submitting process pickling it into every witness job."""
+    digest: bytes
+    path: str
+
+
+_VK_DIR: List[str] = []
+_VK_REFS: Dict[int, tuple] = {}      # id(vk) -> (vk, VkRef) on the submitting side (keeps vk alive)
+_VK_CACHE: Dict[bytes, object] = {}  # digest -> ChildVk on the loading side
+_VK_LOCK = threading.Lock()
+
+
+def _vk_dir() -> str:
+    if not _VK_DIR:
+        import atexit
+        import os
+        import shutil
+        import tempfile
+        d = tempfile.mkdtemp(prefix="zkm_vk_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        atexit.register(shutil.rmtree, d, True)
+        _VK_DIR.append(d)
+    return _VK_DIR[0]
+
+
+def vk_ref(vk) -> VkRef:
+    """The VkRef of vk (its file written on first use)."""
+    with _VK_LOCK:
+        hit = _VK_REFS.get(id(vk))
+        if hit is not None and hit[0] is vk:
+            return hit[1]
+    import os
+    import xxhash
+    data = pickle.dumps(vk, protocol=pickle.HIGHEST_PROTOCOL)
+    digest = xxhash.xxh3_128(data).digest()
+    path = os.path.join(_vk_dir(), digest.hex() + ".pkl")
+    if not os.path.exists(path):
+        tmp = f"{path}.{os.getpid()}.{threading.get_ident()}"
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, path)
+    ref = VkRef(digest, path)
+    with _VK_LOCK:
+        _VK_REFS[id(vk)] = (vk, ref)
+        _VK_CACHE.setdefault(digest, vk)
+    return ref
+
+
+def resolve_vk(v):
+    """A ChildVk from a VkRef (loaded once per process; the file is this run's own, written by vk_ref) or
+    the ChildVk itself."""
+    if not isinstance(v, VkRef):
+        return v
+    with _VK_LOCK:
+        vk = _VK_CACHE.get(v.digest)
+    if vk is None:
+        with open(v.path, "rb") as f:
+            vk = pickle.loads(f.read())
+        with _VK_LOCK:
+            _VK_CACHE[v.digest] = vk
+    return vk
+
+
+def by_ref(children: Sequence[tuple]) -> List[tuple]:
+    """Children with their verifying keys passed by reference (see VkRef)."""
+    return [(vk_ref(vk), proof) for vk, proof in children]
+
+
 _SENT_KEYS: set = set()          # worker side: keys whose traces this process already returned
 _PREP_STORE: Dict[bytes, dict] = {}  # consumer side: traces of every key seen
 _STORE_LOCK = threading.Lock()
@@ -121,6 +191,7 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
     from . import recursion as R
     from . import recursion_verifier as RV
     t0 = time.perf_counter()
+    children = [(resolve_vk(vk), proof) for vk, proof in children]
     prog = RV.compress_node_program(children)
     t1 = time.perf_counter()
     shape = R.fix_shape(prog) if fix else {k: max(4, (h - 1).bit_length()) for k, h in R.program_heights(prog).items()}
@@ -176,7 +247,7 @@ def materialize(traces: dict) -> dict:
 
 
 _CVK_LOCK = threading.Lock()
-_CVK_CHIPS: Dict[int, dict] = {}
+_CVK_CHIPS: Dict[object, object] = {}  # 0 -> the compress machine's chip shapes; (commit, shape, nq) -> ChildVk
 
 
 def compress_child_vk(commit, shape: Dict[str, int], num_queries: int = None):
@@ -192,12 +263,19 @@ def compress_child_vk(commit, shape: Dict[str, int], num_queries: int = None):
             chips = {"shapes": {c.name: RV.ChipShape.of(c) for c in m.chips}, "num_pv": m.num_pv,
                      "prep": [c.name for c in m.chips if c.prep_width]}
             _CVK_CHIPS[0] = chips
+        # one object per (program, shape): parents pass it by reference (vk_ref) without re-pickling it
+        key = (tuple(int(x) for x in commit), tuple(sorted(shape.items())), num_queries)
+        vk = _CVK_CHIPS.get(key)
+        if vk is not None:
+            return vk
     heights = {k: 1 << shape[k] for k in chips["prep"]}
     order = sorted(heights, key=lambda k: (-heights[k], k))
     from .septic import CURVE_CUMULATIVE_SUM_START
-    return RV.ChildVk(chips["shapes"], chips["num_pv"], np.asarray(commit, np.int64), order, heights,
-                      gcs=np.asarray(CURVE_CUMULATIVE_SUM_START, np.int64), log_blowup=R.COMPRESS_LOG_BLOWUP,
-                      num_queries=num_queries or R.COMPRESS_NUM_QUERIES)
+    vk = RV.ChildVk(chips["shapes"], chips["num_pv"], np.asarray(commit, np.int64), order, heights,
+                    gcs=np.asarray(CURVE_CUMULATIVE_SUM_START, np.int64), log_blowup=R.COMPRESS_LOG_BLOWUP,
+                    num_queries=num_queries or R.COMPRESS_NUM_QUERIES)
+    with _CVK_LOCK:
+        return _CVK_CHIPS.setdefault(key, vk)
 
 
 @dataclass
