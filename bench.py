@@ -1091,6 +1091,7 @@ class ShardBench:
         self.rows_per_shard = max(v.shape[0] for v in self.shards[0][2].values())
         self.stagger = None
         self.slot_waits = {}
+        self.copy_stream = torch.cuda.Stream() if os.environ.get("ZKM_BENCH_COPY_STREAMS") != "slot" else None
 
     def slot_steps(self, k, nsteps, mode):
         """nsteps shard proofs of in-flight slot k; returns the last proof."""
@@ -1108,6 +1109,10 @@ class ShardBench:
                 pr = prover.prove_shard(host_np, pv)
             return pr
 
+        # one copy stream for all slots (ZKM_BENCH_COPY_STREAMS=slot: one per slot): copies run FIFO at the full
+        # PCIe rate in the order the slots issue them, instead of sharing the link and all landing late
+        cs = self.copy_stream if self.copy_stream is not None else cs
+
         def issue(j):
             b = bufs[j % 2]
             with torch.cuda.stream(cs):
@@ -1119,9 +1124,10 @@ class ShardBench:
                 e = torch.cuda.Event()
                 e.record(cs)
             return e
-        # the slots' first copies go one after another (slot k starts when slot k-1's has landed), so
-        # slot 0 proves after one copy time instead of all slots waiting for K copies sharing PCIe
-        stagger = self.stagger
+        # per-slot copy streams: the slots' first copies go one after another (slot k starts when slot k-1's
+        # has landed), so slot 0 proves after one copy time instead of all slots waiting for K copies sharing
+        # PCIe (the shared FIFO stream orders them by itself)
+        stagger = self.stagger if self.copy_stream is None else None
         if stagger is not None and k > 0:
             stagger[k - 1].wait(60)  # bounded: a failing slot must not hang the others
         ev = issue(0)
@@ -1234,10 +1240,6 @@ def main():
     if (not (args.no_compress and args.no_tendermint) and args.workload == "fib"
             and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.pmc_child):
         pool = start_witness_pool(max(1, min(args.node_workers, 32)))
-        if not args.no_tendermint:  # config 4's traces are generated on the host while the GPU legs run
-            import tempfile
-            tm_dir = tempfile.mkdtemp(prefix="zkm_tm_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
-            tm_future = pool.submit(_tendermint_job, tm_dir)
 
     import torch
     rk = Ranks(args)
@@ -1263,6 +1265,12 @@ def main():
     copy_waits = {k: list(v) for k, v in sb.slot_waits.items()}
     proof_pc, elapsed_pc = sb.timed(args.steps, "per_call")
     assert proof_res == proof == proof_pc, "resident / host-trace proofs differ"
+    if pool is not None and not args.no_tendermint and rank == 0:
+        # config 4's traces are generated on the host (a pool worker) while the later GPU legs run -- after
+        # the timed regions above, so that they measure the prover alone
+        import tempfile
+        tm_dir = tempfile.mkdtemp(prefix="zkm_tm_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        tm_future = pool.submit(_tendermint_job, tm_dir)
 
     if rank != 0:
         rk.close()
@@ -1398,6 +1406,7 @@ def main():
                         "copy_wait_ms": {"first_step_per_slot": [round(1e3 * v[0], 2) for _, v in sorted(copy_waits.items())],
                                          "later_steps_per_slot": [round(1e3 * sum(v[1:]), 2)
                                                                   for _, v in sorted(copy_waits.items())]},
+                        "copy_streams": "one FIFO stream for all slots" if sb.copy_stream is not None else "one per slot",
                         "what": "same steps from page-locked host traces: the H2D DMA of each slot's next shard "
                                 "overlaps the current proof, every copy inside the timed span; copy_wait_ms = host "
                                 "time each slot waited for its traces (the first step's copies cannot overlap a "

@@ -1,7 +1,7 @@
 """H2D attribution: run the headline ShardBench in ONE mode (pipelined = host traces with the look-ahead
 DMA, resident = traces in HBM) for a few steps, so that a rocprofv3 kernel trace of each mode can be
 compared kernel by kernel (tools/kdelta.py).
-python tools/h2d_attrib.py {pipelined|resident|per_call} [steps] [log_n]"""
+python tools/h2d_attrib.py {pipelined|resident|per_call} [steps] [log_n] [in_flight]"""
 import argparse
 import os
 import sys
@@ -17,12 +17,15 @@ def main():
     mode = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     log_n = int(sys.argv[3]) if len(sys.argv) > 3 else 22
-    args = argparse.Namespace(gpus=None, queries=84, h2d_dst="torch", inflight=3)
+    k = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    args = argparse.Namespace(gpus=None, queries=84, h2d_dst="torch", inflight=k)
     rk = bench.Ranks(args)
-    sb = bench.ShardBench(args, rk, "fib", 1 << log_n, 3)
+    sb = bench.ShardBench(args, rk, "fib", 1 << log_n, k)
     sb.run_steps(1, mode)
     _, el = sb.timed(steps, mode)
-    print(f"{mode}: {1e3 * el / (3 * steps):.3f} ms per shard ({steps} steps x 3 in flight)", flush=True)
+    waits = {k: [round(1e3 * w, 1) for w in v] for k, v in sorted(sb.slot_waits.items())}
+    print(f"{mode}: {1e3 * el / (k * steps):.3f} ms per shard ({steps} steps x {k} in flight)"
+          + (f"; copy waits per slot and step (ms): {waits}" if mode == "pipelined" else ""), flush=True)
     time.sleep(0.1)
 
 
