@@ -1091,6 +1091,9 @@ class ShardBench:
         self.rows_per_shard = max(v.shape[0] for v in self.shards[0][2].values())
         self.stagger = None
         self.slot_waits = {}
+        self.slot_proof_s = {}  # (mode, slot) -> host seconds of each zkm_prove_shard call
+        import threading
+        self.copy_lock = threading.Lock()
         self.copy_stream = torch.cuda.Stream() if os.environ.get("ZKM_BENCH_COPY_STREAMS") != "slot" else None
 
     def slot_steps(self, k, nsteps, mode):
@@ -1100,8 +1103,12 @@ class ShardBench:
         dev_t, pv, host_np, host_t, bufs, cs = self.shards[k]
         if mode == "resident":
             pr = b""
+            ts = []
             for _ in range(nsteps):
+                t = time.perf_counter()
                 pr = prove_resident(prover, dev_t, pv)
+                ts.append(time.perf_counter() - t)
+            self.slot_proof_s[(mode, k)] = ts
             return pr
         if mode == "per_call":
             pr = b""
@@ -1115,7 +1122,8 @@ class ShardBench:
 
         def issue(j):
             b = bufs[j % 2]
-            with torch.cuda.stream(cs):
+            # one slot's copies go into the shared stream together (FIFO per slot, not interleaved per trace)
+            with self.copy_lock, torch.cuda.stream(cs):
                 for kk, t in host_t.items():
                     if isinstance(b[kk], RawDev):
                         b[kk].copy_from_host(t, cs)
@@ -1132,7 +1140,7 @@ class ShardBench:
             stagger[k - 1].wait(60)  # bounded: a failing slot must not hang the others
         ev = issue(0)
         pr = b""
-        waits = []
+        waits, ts = [], []
         for j in range(nsteps):
             t = time.perf_counter()
             ev.synchronize()
@@ -1142,9 +1150,12 @@ class ShardBench:
             nxt = issue(j + 1) if j + 1 < nsteps else None
             # ZKM_BENCH_DMA_PROBE=1 (experiment only): the same copies, proofs from the resident traces
             src = dev_t if os.environ.get("ZKM_BENCH_DMA_PROBE") == "1" else bufs[j % 2]
+            t = time.perf_counter()
             pr = prove_resident(prover, src, pv)
+            ts.append(time.perf_counter() - t)
             ev = nxt
         self.slot_waits[k] = waits  # host seconds each step waited for its traces' copy
+        self.slot_proof_s[(mode, k)] = ts
         return pr
 
     def run_steps(self, nsteps, mode="pipelined"):
@@ -1263,6 +1274,8 @@ def main():
     # secondary: host traces with the look-ahead H2D pipeline, and per-call host copies
     proof, elapsed = sb.timed(args.steps, "pipelined")
     copy_waits = {k: list(v) for k, v in sb.slot_waits.items()}
+    proof_ms = {m: round(1e3 * float(np.mean([t for (mm, _), v in sb.slot_proof_s.items() if mm == m for t in v])), 3)
+                for m in ("resident", "pipelined")}
     proof_pc, elapsed_pc = sb.timed(args.steps, "per_call")
     assert proof_res == proof == proof_pc, "resident / host-trace proofs differ"
     if pool is not None and not args.no_tendermint and rank == 0:
@@ -1407,6 +1420,7 @@ def main():
                                          "later_steps_per_slot": [round(1e3 * sum(v[1:]), 2)
                                                                   for _, v in sorted(copy_waits.items())]},
                         "copy_streams": "one FIFO stream for all slots" if sb.copy_stream is not None else "one per slot",
+                        "proof_call_ms_mean": proof_ms,
                         "what": "same steps from page-locked host traces: the H2D DMA of each slot's next shard "
                                 "overlaps the current proof, every copy inside the timed span; copy_wait_ms = host "
                                 "time each slot waited for its traces (the first step's copies cannot overlap a "

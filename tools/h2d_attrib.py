@@ -24,6 +24,10 @@ def main():
     sb.run_steps(1, mode)
     _, el = sb.timed(steps, mode)
     waits = {k: [round(1e3 * w, 1) for w in v] for k, v in sorted(sb.slot_waits.items())}
+    calls = [t for (m, _), v in sb.slot_proof_s.items() if m == mode for t in v]
+    if calls:
+        print(f"{mode}: zkm_prove_shard calls {1e3 * sum(calls) / len(calls):.2f} ms mean, "
+              f"{1e3 * min(calls):.2f} min, {1e3 * max(calls):.2f} max", flush=True)
     print(f"{mode}: {1e3 * el / (k * steps):.3f} ms per shard ({steps} steps x {k} in flight)"
           + (f"; copy waits per slot and step (ms): {waits}" if mode == "pipelined" else ""), flush=True)
     time.sleep(0.1)
