@@ -174,7 +174,34 @@ def pmc_in_run(args, timeout_s=240):
 
 # one rocprofv3 pass (at most 8 SQ + 2 GRBM counters): VALU instructions and waves summed over the
 # dispatch, and the GPU-busy cycles summed over the 8 XCDs (MI355X_MICROARCH.md)
-SQ_COUNTERS = ("SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE")
+SQ_COUNTERS = ("SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT",
+               "SQ_LDS_IDX_ACTIVE")
+P2_KERNELS = ("k_hash_leaves", "k_compress_level", "k_subtree16", "k_compress_inject")
+
+
+def lds_counters(pmc):
+    """LDS use of the Poseidon2 kernels over one proof (the same SQ pass): LDS instructions per wave and the
+    bank-conflict cycles per LDS-active cycle (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; 0 = every LDS
+    access served conflict-free).  The throughput kernels hold the permutation state in registers (one
+    lane per state), so their LDS use is the row staging of the leaf loads and the subtree levels."""
+    if not pmc:
+        return None
+    out = {}
+    for k, v in pmc.items():
+        c = v.get("sq") or {}
+        if not k.startswith(P2_KERNELS) or not c.get("SQ_WAVES") or "SQ_INSTS_LDS" not in c:
+            continue
+        name = next(p for p in P2_KERNELS if k.startswith(p))
+        e = out.setdefault(name, {"SQ_WAVES": 0.0, "SQ_INSTS_LDS": 0.0, "SQ_LDS_BANK_CONFLICT": 0.0,
+                                  "SQ_LDS_IDX_ACTIVE": 0.0})
+        for f in e:
+            e[f] += c.get(f, 0.0)
+    res = {}
+    for name, e in out.items():
+        res[name] = {"lds_insts_per_wave": round(e["SQ_INSTS_LDS"] / e["SQ_WAVES"], 2) if e["SQ_WAVES"] else None,
+                     "bank_conflict_per_active_cycle": (round(e["SQ_LDS_BANK_CONFLICT"] / e["SQ_LDS_IDX_ACTIVE"], 4)
+                                                        if e["SQ_LDS_IDX_ACTIVE"] else 0.0)}
+    return res or None
 
 
 def valu_counters(pmc, ms_per_proof, kernel="k_hash_leaves"):
@@ -896,10 +923,19 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
     t0 = time.perf_counter()
     root = CT.reduce_distributed(leaves, reducer) if distributed else CT.reduce_serial(leaves, reducer)
     wall = time.perf_counter() - t0
+    tl = [v for v in reducer.times.values() if len(v) == 3]
+    timeline = None
+    if tl:
+        # per node: submit -> witness back (worker queue + build + execute + transfer), witness -> proof
+        # (GPU queue + materialise + prove); and the depth of the tree's last node
+        timeline = {"witness_latency_s_mean": round(float(np.mean([v["witness"] - v["submit"] for v in tl])), 3),
+                    "prove_latency_s_mean": round(float(np.mean([v["proved"] - v["witness"] for v in tl])), 3),
+                    "first_witness_back_s": round(min(v["witness"] for v in tl) - t0, 3),
+                    "last_layer_submit_s": round(max(v["submit"] for v in tl) - t0, 3)}
     rows = shapes.pop("_rows")
     from zkmips_amd import recursion as R
     names = {",".join(f"{c}:{sh[c]}" for c in sorted(sh)): i for i, sh in enumerate(R.RECURSION_SHAPES)}
-    res = {"wall_s": wall, "gpu_busy_s": _union_s(spans), "proofs": stats.proofs,
+    res = {"wall_s": wall, "gpu_busy_s": _union_s(spans), "proofs": stats.proofs, "timeline": timeline,
            "witness_build_s": stats.build_s, "witness_execute_and_traces_s": stats.execute_s,
            "setups": stats.setups, "setup_s": stats.setup_s, "lookups": stats.lookups,
            "shapes": {f"RecursionShapeConfig[{names.get(k, '?')}]" + (" (fastest)" if names.get(k) == 0 else ""):
@@ -935,6 +971,7 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
                                   "workers": args.node_workers,
                                   "what": "host: node program (verifying both children) + recursion runtime + traces, "
                                           "in a process pool, overlapped with proving"},
+           "timeline": r["timeline"],
            "setups": r["setups"], "setup_ms_total": round(1e3 * r["setup_s"], 3), "setup_lookups": r["lookups"],
            "node_shapes": r["shapes"], "root_proof_bytes": len(rproof), "proofs_this_rank": n,
            "leaves": info, "in_flight": inflight,
@@ -1336,6 +1373,9 @@ def main():
         vc = valu_counters(pmc, ms / nprof)
         if roofline["valu"] is not None and vc:
             roofline["valu"]["counters"] = vc
+        lds = lds_counters(pmc)
+        if roofline["valu"] is not None and lds:
+            roofline["valu"]["lds"] = lds
 
     def measured(stage):
         """HBM utilisation of a stage's kernels: PMC bytes per proof over the stage's HIP-event time."""

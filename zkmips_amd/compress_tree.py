@@ -369,6 +369,7 @@ class Reducer:
         self.submit_witness = submit_witness
         self.prove = prove
         self.on_witness = on_witness  # called on each witness in arrival order, before it is queued
+        self.times: Dict[Node, Dict[str, float]] = {}  # node -> perf_counter of submit / witness / proved
         self.inflight = max(1, inflight)
         self.events: "queue.Queue" = queue.Queue()
         self.gpu_q: "queue.Queue" = queue.Queue()
@@ -404,6 +405,7 @@ class Reducer:
                 ok, ch = ready(node)
                 if ok:
                     submitted.add(node)
+                    self.times.setdefault(node, {})["submit"] = time.perf_counter()
                     fut = self.submit_witness([done[c] for c in ch])
                     fut.add_done_callback(lambda f, n=node: self.events.put(("witness", n, f)))
         try:
@@ -420,8 +422,10 @@ class Reducer:
                 except queue.Empty:
                     continue
                 if kind == "witness":
+                    self.times.setdefault(node, {})["witness"] = time.perf_counter()
                     self.gpu_q.put((node, self.on_witness(val.result())))
                 elif kind == "proof":
+                    self.times.setdefault(node, {})["proved"] = time.perf_counter()
                     done[node] = val
                     pending.discard(node)
                     if on_done:
