@@ -314,16 +314,12 @@ class RecursionProgram:
     def base_alu(self, op, out, in1, in2, mult=None):
         out = np.atleast_1d(np.asarray(out, np.int64))
         n = len(out)
-        self._add("base", op=np.broadcast_to(np.asarray(op, np.int64), (n,)).copy(), out=out,
-                  in1=np.broadcast_to(np.asarray(in1, np.int64), (n,)).copy(),
-                  in2=np.broadcast_to(np.asarray(in2, np.int64), (n,)).copy(), mult=_mults(mult, n))
+        self._add("base", op=_vec(op, n), out=out, in1=_vec(in1, n), in2=_vec(in2, n), mult=_mults(mult, n))
 
     def ext_alu(self, op, out, in1, in2, mult=None):
         out = np.atleast_1d(np.asarray(out, np.int64))
         n = len(out)
-        self._add("ext", op=np.broadcast_to(np.asarray(op, np.int64), (n,)).copy(), out=out,
-                  in1=np.broadcast_to(np.asarray(in1, np.int64), (n,)).copy(),
-                  in2=np.broadcast_to(np.asarray(in2, np.int64), (n,)).copy(), mult=_mults(mult, n))
+        self._add("ext", op=_vec(op, n), out=out, in1=_vec(in1, n), in2=_vec(in2, n), mult=_mults(mult, n))
 
     def poseidon2(self, outs, ins, mults=None):
         outs = np.asarray(outs, np.int64).reshape(-1, WIDTH)
@@ -368,6 +364,13 @@ class RecursionProgram:
     def commit_public_values(self, pv_addrs):
         pv_addrs = np.asarray(pv_addrs, np.int64).reshape(PROOF_MAX_NUM_PVS)
         self._add("commit", pv=pv_addrs[None, :])
+
+
+def _vec(x, n: int) -> np.ndarray:
+    """x as an int64 vector of n entries (address arrays are never modified after a block is added, so an
+    array of the right shape is kept as it is)."""
+    a = np.asarray(x, np.int64)
+    return a if a.shape == (n,) else np.broadcast_to(a, (n,)).copy()
 
 
 def _mults(m, shape):
