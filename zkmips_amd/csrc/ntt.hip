@@ -567,6 +567,14 @@ __device__ __forceinline__ void dit13x2(uint32_t v0[16], uint32_t v1[16], uint32
 }
 }  // namespace t13
 
+// TILED: source and destination tile-major (k_ntt_s9b TILE): element e of 8192-run b (b < 512) at
+// (e / 32) * 16384 + b * 32 + e % 32 -- the strided passes on either side then move contiguous 64 KB tiles,
+// and this VALU-bound kernel takes the 128-B segments instead
+__device__ __forceinline__ uint32_t tiled13(uint32_t b, uint32_t t, uint32_t j) {
+    return ((t >> 5) + 16 * j) * 16384u + b * 32u + (t & 31);
+}
+
+template <bool TILED>
 __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src, uint32_t *dst, ColMap ms,
                                                             ColMap md, int L, const uint32_t *__restrict__ tt_inv,
                                                             const uint32_t *__restrict__ tt_fwd, Twist tws,
@@ -574,11 +582,11 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
     using namespace t13;
     __shared__ uint32_t x[2 * LDS13];
     const uint32_t t = threadIdx.x;
-    const uint32_t base = blockIdx.x * 8192u;
+    const uint32_t base = TILED ? 0u : blockIdx.x * 8192u;
     const uint32_t *sp = src + ms.off(blockIdx.y) + base;
     uint32_t v0[16], v1[16];
 #pragma unroll
-    for (int j = 0; j < 16; j++) v0[j] = sp[lay_idx<512>(t, j)];
+    for (int j = 0; j < 16; j++) v0[j] = sp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)];
     dif13(v0, x, t, tt_inv);
     {
         const uint32_t g0 = tws.g0[blockIdx.x], g1 = tws.g1[blockIdx.x];
@@ -598,9 +606,9 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
     dit13x2(v0, v1, x, t, tt_fwd);
     uint32_t *dp = dst + md.off(blockIdx.y) + base;
 #pragma unroll
-    for (int j = 0; j < 16; j++) dp[lay_idx<512>(t, j)] = v0[j];
+    for (int j = 0; j < 16; j++) dp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)] = v0[j];
 #pragma unroll
-    for (int j = 0; j < 16; j++) dp[dst_half + lay_idx<512>(t, j)] = v1[j];
+    for (int j = 0; j < 16; j++) dp[dst_half + (TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j))] = v1[j];
 }
 
 // ------------------------------------------------------------------ 512-row strided register tiles
@@ -835,12 +843,16 @@ __device__ __forceinline__ void from_ldsb(const uint32_t *x, uint32_t v[16], uin
 }
 }  // namespace s9
 
-template <bool DIT, int MODE>
+// TILE (bit 0: source, bit 1: destination; only for the one-pass case 512 x S = the column): that side is
+// tile-major -- the tile's 512 rows x 32 columns contiguous (64 KB, row pitch 32 words) at tile index
+// c0 / 32 -- instead of row-major with pitch S (the LDE's intermediates, lde_natural ZKM_LDE_TILED).
+template <bool DIT, int MODE, int TILE = 0>
 __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                         int logS, const uint32_t *__restrict__ tw,
                                                         uint32_t tw_words, uint32_t nv, int remap) {
     using namespace s9;
     constexpr bool SWZ = DIT && MODE == MODE_BITREV_OUT;
+    constexpr bool TS = TILE & 1, TD = (TILE & 2) != 0;
     __shared__ uint32_t x[512 * 32];
     const uint32_t S = 1u << logS, S4 = S * 4;
     // XCD-aware order: workgroup i runs on XCD i mod 8, so XCD x takes the contiguous range
@@ -855,18 +867,23 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
     const uint32_t base = outer * 512u * S;
     const uint32_t t = threadIdx.x & 31, u = threadIdx.x >> 5;
     const uint32_t ct = c0 + t;
-    const auto rsrc = mkrs(src + ms.off(col) + base, 512u * S4);
+    const uint64_t tbase = (uint64_t)(c0 >> 5) * (512u * 32u);  // tile-major: the tile's 64 KB
+    const auto rsrc = TS ? mkrs(src + ms.off(col) + tbase, 512u * 128u) : mkrs(src + ms.off(col) + base, 512u * S4);
     const auto rtw = mkrs(tw, tw_words * 4);
     const uint32_t vLL = ct * 4;                    // twiddle offsets per layout / network
     const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4, vLM1 = (((2 * u + 1) & 7) * S + ct) * 4;
     const uint32_t vLH = (u * S + ct) * 4;          // also rows u + 32 n + 64 k of the tile
     const uint32_t vL16 = (16 * u * S + ct) * 4;    // rows 16 u + 8 n + k of the tile
+    // data offsets of the source / destination side (row pitch S words, or 32 when tile-major)
+    const uint32_t sP4 = TS ? 128u : S4, dP4 = TD ? 128u : S4;
+    const uint32_t sLH = TS ? (u * 32 + t) * 4 : vLH, sL16 = TS ? (16 * u * 32 + t) * 4 : vL16;
+    const uint32_t dLH = TD ? (u * 32 + t) * 4 : vLH, dL16 = TD ? (16 * u * 32 + t) * 4 : vL16;
     uint32_t v[16];
     if (DIT) {
 #pragma unroll
         for (int n = 0; n < 2; n++)
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, vL16, (uint32_t)(8 * n + k) * S4);
+            for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, sL16, (uint32_t)(8 * n + k) * sP4);
         net8b<true, LL>(v, rtw, vLL, 0, S4);
         net8b<true, LL>(v + 8, rtw, vLL, 0, S4);
         to_ldsb<LL, false>(x, v, u, t);
@@ -881,11 +898,11 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
         net8b<true, LH>(v, rtw, vLH, 0, S4);
         net8b<true, LH>(v + 8, rtw, vLH, 32 * S4, S4);
         if (MODE == MODE_PLAIN) {
-            const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
+            const auto rdst = TD ? mkrs(dst + md.off(col) + tbase, 512u * 128u) : mkrs(dst + md.off(col) + base, 512u * S4);
 #pragma unroll
             for (int n = 0; n < 2; n++)
 #pragma unroll
-                for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, vLH, (uint32_t)(32 * n + 64 * k) * S4);
+                for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, dLH, (uint32_t)(32 * n + 64 * k) * dP4);
         } else {  // BITREV_OUT: natural n = r S + c -> row rev_L(n) = rev_logS(c) * 512 + rev_9(r)
             __syncthreads();
             to_ldsb<LH, SWZ>(x, v, u, t);
@@ -904,7 +921,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
 #pragma unroll
         for (int n = 0; n < 2; n++)
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, vLH, (uint32_t)(32 * n + 64 * k) * S4);
+            for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, sLH, (uint32_t)(32 * n + 64 * k) * sP4);
         net8b<false, LH>(v, rtw, vLH, 0, S4);
         net8b<false, LH>(v + 8, rtw, vLH, 32 * S4, S4);
         to_ldsb<LH, false>(x, v, u, t);
@@ -918,11 +935,11 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
         from_ldsb<LL, false>(x, v, u, t);
         net8b<false, LL>(v, rtw, vLL, 0, S4);
         net8b<false, LL>(v + 8, rtw, vLL, 0, S4);
-        const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
+        const auto rdst = TD ? mkrs(dst + md.off(col) + tbase, 512u * 128u) : mkrs(dst + md.off(col) + base, 512u * S4);
 #pragma unroll
         for (int n = 0; n < 2; n++)
 #pragma unroll
-            for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, vL16, (uint32_t)(8 * n + k) * S4);
+            for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, dL16, (uint32_t)(8 * n + k) * dP4);
     }
 }
 
@@ -1232,10 +1249,29 @@ static int strided_T(int logR) { return logR >= 9 ? 32 : 64; }  // >= 32: the sw
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
                         int logS, const uint32_t *tw, int mode, hipStream_t s, Twist tws = Twist{},
-                        uint64_t dst_half = 0, uint32_t tw_words = 0) {
+                        uint64_t dst_half = 0, uint32_t tw_words = 0, int tile = 0) {
     const int T = strided_T(logR);
     ARG_CHECK((1 << logS) >= T, "strided pass narrower than its tile");
+    ARG_CHECK(!tile || (logR == 9 && logS + 9 == L && tw_words && mode != MODE_TWIST_OUT),
+              "tile-major sides need the one-pass 512-row strided kernel");
     dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
+    if (tile) {  // k_ntt_s9b with a tile-major source (bit 0) and / or destination (bit 1)
+        const dim3 g1(g.x * nv);
+#define S9T(TL)                                                                                                   \
+    if (!DIT)                                                                                                     \
+        hipLaunchKernelGGL((k_ntt_s9b<false, MODE_PLAIN, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw, \
+                           tw_words, nv, 1);                                                                      \
+    else if (mode == MODE_PLAIN)                                                                                  \
+        hipLaunchKernelGGL((k_ntt_s9b<true, MODE_PLAIN, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,  \
+                           tw_words, nv, 1);                                                                      \
+    else                                                                                                          \
+        hipLaunchKernelGGL((k_ntt_s9b<true, MODE_BITREV_OUT, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, \
+                           tw, tw_words, nv, 1);
+        if (tile == 1) { S9T(1) } else if (tile == 2) { S9T(2) } else { S9T(3) }
+#undef S9T
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
     if (logR == 9 && tw_words && mode != MODE_TWIST_OUT) {  // buffer-addressed register tiles
         const dim3 g1(g.x * nv);  // one dimension: (tile, column) remapped in the kernel
         static const int remap = getenv("ZKM_NTT_NOREMAP") ? 0 : 1;  // A/B knob
@@ -1531,6 +1567,13 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
     const uint32_t cb = lde_col_batch(N, nv);
     DBuf work(2 * N * cb, s);
     DBuf winv(nsh > 1 ? N * cb : 0, s);
+    // the intermediates tile-major (the one-strided-pass size, 2^22): the strided passes read / write whole
+    // 64 KB tiles, the VALU-bound fused pass takes the 128-B segments (opt-in: ZKM_LDE_TILED=1)
+    static const int tiled_env = [] {
+        const char *e = getenv("ZKM_LDE_TILED");
+        return e ? atoi(e) : 0;
+    }();
+    const bool tiled = tiled_env && logC == 13 && sp.size() == 1 && sp[0] == 9;
     for (uint32_t c0 = 0; c0 < nv; c0 += cb) {
         const uint32_t nb = std::min(cb, nv - c0);
         const uint32_t *in = src.d + (uint64_t)c0 * N;
@@ -1542,7 +1585,7 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
         for (size_t i = 0; i < sp.size(); i++) {
             logS -= sp[i];
             run_strided<false>(sp[i], in, ibuf, min, m_i, nb, L, logS, c.tw_inv, MODE_PLAIN, s, Twist{}, 0,
-                               1u << c.tw_log);
+                               1u << c.tw_log, tiled ? 2 : 0);
             in = ibuf;
             min = m_i;
         }
@@ -1550,8 +1593,12 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
             const Twist tws = get_twist(c, N, L, shifts[e], s);
             uint32_t *out = dst_d + (uint64_t)c0 * dst_stride + e * half_off;
             if (logC == 13) {
-                hipLaunchKernelGGL(k_lde_fused13, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf, work.p,
-                                   m_i, m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
+                if (tiled)
+                    hipLaunchKernelGGL(k_lde_fused13<true>, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf,
+                                       work.p, m_i, m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
+                else
+                    hipLaunchKernelGGL(k_lde_fused13<false>, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf,
+                                       work.p, m_i, m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
                 HIP_CHECK(hipGetLastError());
             } else {
                 run_fused(logC, ibuf, work.p, m_i, m_w1, nb, L, c.tw_inv, c.tw_fwd, tws, N, 0, s);
@@ -1560,7 +1607,8 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
             for (int i = (int)sp.size() - 1; i >= 0; i--) {
                 const bool last = (i == 0);
                 run_strided<true>(sp[i], work.p, last ? out : work.p, m_w2, last ? m_out : m_w2, 2 * nb, L, logS,
-                                  c.tw_fwd, last ? MODE_BITREV_OUT : MODE_PLAIN, s, Twist{}, 0, 1u << c.tw_log);
+                                  c.tw_fwd, last ? MODE_BITREV_OUT : MODE_PLAIN, s, Twist{}, 0, 1u << c.tw_log,
+                                  tiled ? 1 : 0);
                 logS += sp[i];
             }
         }
