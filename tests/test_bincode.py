@@ -99,3 +99,21 @@ def test_compress_route_errors():
     with pytest.raises(SV.TwirpError) as e:
         svc.call("Compress", {1: bytes(req)})
     assert e.value.code == "unimplemented"
+
+
+def test_compress_route_rejects_a_tampered_shard():
+    """A Compress request whose shard proof has a changed byte fails in the node program (before any GPU
+    work) and answers invalid_argument, not internal."""
+    from zkmips_amd import shapes as SH
+    from zkmips_amd.septic import CURVE_CUMULATIVE_SUM_START as GCS
+    m, prep, tr, pv = SH.shape_shards(SH.MAXIMAL_22, [1], down=8)[0]
+    o = O.OracleProver(m, prep, num_queries=84)
+    rc, proof = o.prove(tr, pv)
+    assert rc == 0
+    vk = B.StarkVk.of_program(m, prep, o.commit, 0x00400000, GCS)
+    bad = bytearray(proof)
+    bad[len(bad) // 2] ^= 1
+    svc = SV.ProverService(device_factory=lambda i: object())
+    with pytest.raises(SV.TwirpError) as e:
+        svc.call("Compress", {1: B.write_compress_request(vk, [bytes(bad)])})
+    assert e.value.code == "invalid_argument"

@@ -339,12 +339,17 @@ class ProverService:
         reducer = CT.Reducer(submit, prove, self.compress_inflight)
         try:
             if len(leaves) == 1:  # one shard is still wrapped by a compress node
-                rvk, rproof = prove(submit(leaves).result())
+                rvk, rproof = prove(CT.register_prep(submit(leaves).result()))
             else:
-                try:
-                    rvk, rproof = CT.reduce_serial(leaves, reducer)
-                except ValueError as e:  # a child proof the node verifier rejects
-                    raise TwirpError("invalid_argument", f"Compress: {e}")
+                rvk, rproof = CT.reduce_serial(leaves, reducer)
+        except ValueError as e:  # a child proof of the wrong shape for its verifying key
+            raise TwirpError("invalid_argument", f"Compress: {e}")
+        except RuntimeError as e:
+            from ._lib import ZkmError
+            if isinstance(e, ZkmError):  # the device side: Twirp internal
+                raise
+            # the node program's runtime check failed: a child proof that does not verify
+            raise TwirpError("invalid_argument", f"Compress: a child proof does not verify ({e})")
         finally:
             if self._pool is None:
                 tp.shutdown(wait=False)
