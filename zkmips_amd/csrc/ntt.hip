@@ -1568,10 +1568,11 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
     DBuf work(2 * N * cb, s);
     DBuf winv(nsh > 1 ? N * cb : 0, s);
     // the intermediates tile-major (the one-strided-pass size, 2^22): the strided passes read / write whole
-    // 64 KB tiles, the VALU-bound fused pass takes the 128-B segments (opt-in: ZKM_LDE_TILED=1)
+    // 64 KB tiles, the VALU-bound fused pass takes the 128-B segments: LDE 4.05-4.13 -> 3.92-3.94 ms for 2^22 x 67
+    // (profiles/r04_lde_tiled_plain_ab.txt; the pattern alone: profiles/r04_tile_probe.txt); ZKM_LDE_TILED=0 row-major
     static const int tiled_env = [] {
         const char *e = getenv("ZKM_LDE_TILED");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     const bool tiled = tiled_env && logC == 13 && sp.size() == 1 && sp[0] == 9;
     for (uint32_t c0 = 0; c0 < nv; c0 += cb) {
