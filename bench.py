@@ -32,6 +32,12 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+# Hardware queues per process (read by the HIP runtime at initialisation).  HIP's default of 4 is fewer than
+# the streams of the host-trace mode (3 prover slots, the copy stream, torch's own): the copy stream then
+# shares a queue with a prover stream, whose kernels wait behind each 19.6 ms copy (34 ms per shard instead
+# of 27.5; profiles/r04_hw_queues.txt).  8 gives every stream its own queue; the resident rate is unchanged.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
