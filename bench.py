@@ -1390,10 +1390,23 @@ def main():
             return None
         sms = prof[stage][1] / nprof
         gbps = b_ / (sms / 1e3) / 1e9
-        return {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_shard": round(b_),
-                "algorithmic_bytes_per_shard": round(prof[stage][2] / nprof),
-                "counter_ratio": round(b_ / (prof[stage][2] / nprof), 3), "launches": n_,
-                "stage_ms_per_shard": round(sms, 3)}
+        out = {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_shard": round(b_),
+               "algorithmic_bytes_per_shard": round(prof[stage][2] / nprof),
+               "counter_ratio": round(b_ / (prof[stage][2] / nprof), 3), "launches": n_,
+               "stage_ms_per_shard": round(sms, 3)}
+        # the same kernels' VALU side from the SQ pass: VALU instructions x 2 cycles (wave64 on SIMD-32) over
+        # the 1024 SIMDs x busy cycles -- a lower bound on the issue fraction (half-rate 64-bit products
+        # count once)
+        pre = STAGE_KERNELS.get(stage, ())
+        vi = cy = 0.0
+        for k, v in (pmc or {}).items():
+            c = v.get("sq") or {}
+            if k.startswith(pre) and c.get("GRBM_GUI_ACTIVE"):
+                vi += c.get("SQ_INSTS_VALU", 0.0)
+                cy += c["GRBM_GUI_ACTIVE"] / 8.0
+        if cy:
+            out["valu_issue_lower_bound"] = round(vi * 2.0 / (1024.0 * cy), 4)
+        return out
 
     ntt = None
     if "lde" in prof and "lde_gfops" in prof:
