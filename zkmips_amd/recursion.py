@@ -107,7 +107,7 @@ def _host(name: str):
 
 def ext_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """(n,4) x (n,4) over F[x]/(x^4 - 3)."""
-    if a.shape == b.shape and a.ndim == 2 and a.shape[0] >= 16:  # batches: host C++ (ef_host.cpp)
+    if a.shape == b.shape and a.ndim == 2 and a.shape[0] >= 1:  # host C++ (ef_host.cpp): one ctypes call
         x = np.ascontiguousarray(a, dtype=np.uint32)
         y = np.ascontiguousarray(b, dtype=np.uint32)
         out = np.empty_like(x)

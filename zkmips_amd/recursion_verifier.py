@@ -977,8 +977,7 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
         e0 = b.ext(R.OP_ADD, folded, b.ext(R.OP_MUL, bit, d))      # bit ? sib : folded
         e1 = b.ext(R.OP_SUB, b.ext(R.OP_ADD, folded, sib), e0)
         # the leaf (e0 || e1) as 8 base words: hinted, recomposed to e0 and e1
-        words = b.hint_base(np.asarray([list(fri_pairs[qn][off][0]) + list(fri_pairs[qn][off][1])
-                                        for qn in range(nq)], np.int64))
+        words = b.hint_base(fri_pairs[off].astype(np.int64))
         b.assert_eq_ext(b.ef_from_base4(words[:, :4]), e0, f"fri leaf e0 round {off}")
         b.assert_eq_ext(b.ef_from_base4(words[:, 4:]), e1, f"fri leaf e1 round {off}")
         fpaths = b.hint_base(np.stack([qq[1][off][1] for qq in p.queries]))
@@ -1019,9 +1018,9 @@ def _m_u(a, b):
     return (a * b) % PU
 
 
-def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> List[List[tuple]]:
-    """The verifier's reduced openings and folds on the host (fri.rs:155-203, :247-361), per query the
-    (e0, e1) leaf pair of every commit-phase round: the pair the program hashes (as hinted base words)
+def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> List[np.ndarray]:
+    """The verifier's reduced openings and folds on the host (fri.rs:155-203, :247-361), per commit-phase
+    round the queries' (e0 || e1) leaf pairs as an (nq, 8) word array: the pair the program hashes (as hinted base words)
     and recomposes against its own in-program fold.  Vectorised over the queries: per matrix and point
     the reduced opening is A - B[q] with A = sum_c alpha^c p_c(z) (query-independent) and
     B[q] = sum_c alpha^c p_c(x_q) (a base x EF dot product), divided by (z - x_q)."""
@@ -1034,18 +1033,24 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
         for log_n, width, pts in ms:
             total[log_n + lb] = total.get(log_n + lb, 0) + width * len(pts)
     npow = max(total.values()) if total else 0
-    apow = np.zeros((max(npow, 1), 4), U)
-    apow[0, 0] = 1
-    for k in range(1, npow):
-        apow[k] = R.ext_mul(apow[k - 1], fa)
+    pw_list = [[1, 0, 0, 0]]
+    fa_i = [int(v) for v in fa]
+    for _ in range(1, npow):  # Python-int EF products: a (4,) numpy product costs 16 array ops
+        pw_list.append(ef_mul(pw_list[-1], fa_i))
+    apow = np.asarray(pw_list, U)
     ro: Dict[int, np.ndarray] = {}
     lhp: Dict[int, int] = {}
+    xs: Dict[int, np.ndarray] = {}        # per LDE height: the queries' points x_q (one per height)
+    inv_zx: Dict[tuple, np.ndarray] = {}  # per (opening point, height): 1 / (z - x_q)
     for t, ms in enumerate(rounds_host):
         for k, (log_n, width, pts) in enumerate(ms):
             lh = log_n + lb
-            row = (idx >> (log_max - lh)) & ((1 << lh) - 1)
-            g = np.full(nq, two_adic_gen(lh), U)
-            x = _m_u(R._pow_vec(g, _bitrev_arr(row, lh)), U(GENERATOR)) if lh else np.full(nq, GENERATOR, U)
+            x = xs.get(lh)
+            if x is None:
+                row = (idx >> (log_max - lh)) & ((1 << lh) - 1)
+                g = np.full(nq, two_adic_gen(lh), U)
+                x = _m_u(R._pow_vec(g, _bitrev_arr(row, lh)), U(GENERATOR)) if lh else np.full(nq, GENERATOR, U)
+                xs[lh] = x
             rows = np.stack([np.asarray(p.queries[qn][0][t][0][k], np.int64) for qn in range(nq)]) if width else None
             for z, vals in pts:
                 pw = lhp.get(lh, 0)
@@ -1057,20 +1062,23 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
                     acc = (A[None, :] + PU - B) % PU
                 else:
                     acc = np.zeros((nq, 4), U)
-                zx = np.broadcast_to(np.asarray(z, U) % PU, (nq, 4)).copy()
-                zx[:, 0] = (zx[:, 0] + PU - x) % PU
-                term = R.ext_mul(acc, R.ext_inv(zx))
+                key = (tuple(int(v) for v in z), lh)
+                iz = inv_zx.get(key)
+                if iz is None:
+                    zx = np.broadcast_to(np.asarray(z, U) % PU, (nq, 4)).copy()
+                    zx[:, 0] = (zx[:, 0] + PU - x) % PU
+                    iz = inv_zx[key] = R.ext_inv(zx)
+                term = R.ext_mul(acc, iz)
                 ro[lh] = term if lh not in ro else (ro[lh] + term) % PU
     folded = ro[log_max]
     x = R._pow_vec(np.full(nq, two_adic_gen(log_max), U), _bitrev_arr(idx, log_max))
-    pairs = [[] for _ in range(nq)]
+    pairs = []
     for off, _ in enumerate(p.queries[0][1]):
         bit = ((idx >> off) & 1).astype(bool)
         sib = np.stack([np.asarray(p.queries[qn][1][off][0], U) for qn in range(nq)])
         e0 = np.where(bit[:, None], sib, folded)
         e1 = np.where(bit[:, None], folded, sib)
-        for qn in range(nq):
-            pairs[qn].append(([int(v) for v in e0[qn]], [int(v) for v in e1[qn]]))
+        pairs.append(np.concatenate([e0, e1], 1))
         xn = (PU - x) % PU
         x0, x1 = np.where(bit, xn, x), np.where(bit, x, xn)
         inv = R._pow(((x1 + PU - x0) % PU).astype(U), P - 2)
