@@ -1574,7 +1574,7 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
         const char *e = getenv("ZKM_LDE_TILED");
         return e ? atoi(e) : 1;
     }();
-    const bool tiled = tiled_env && logC == 13 && sp.size() == 1 && sp[0] == 9;
+    const bool tiled = tiled_env && nsh == 1 && logC == 13 && sp.size() == 1 && sp[0] == 9;  // (the tested case)
     for (uint32_t c0 = 0; c0 < nv; c0 += cb) {
         const uint32_t nb = std::min(cb, nv - c0);
         const uint32_t *in = src.d + (uint64_t)c0 * N;
