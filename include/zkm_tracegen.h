@@ -338,6 +338,27 @@ int zkm_exp_reverse_bits_events_to_trace(const uint32_t *base, const uint32_t *b
 int zkm_recursion_events_to_trace(uint32_t chip, const uint32_t *events, uint64_t n, uint32_t repr, uint32_t *trace,
                                   uint64_t height, void *stream);
 
+/* Preprocessed traces of the recursion chips: the *_instr_to_row_koalabear functions of sys.rs:22-110
+ * (include/alu_base.hpp, alu_ext.hpp, batch_fri.hpp, select.hpp, fri_fold.hpp, public_values.hpp,
+ * exp_reverse_bits.hpp, poseidon2_wide.hpp; mem/{constant,variable}.rs) from n instruction records of
+ * u32 words, field words in `repr`, integer words (opcodes, flags, indices) plain:
+ *   BaseAlu / ExtAlu   5: addr out, in1, in2, opcode (0 add, 1 sub, 2 mul, 3 div), mult  -> 4 per row, 32 cols
+ *   BatchFRI           5 per row: acc, alpha_pow, p_at_z, p_at_x addrs, is_end           -> 6 cols
+ *   Select             7: bit, out1, out2, in1, in2 addrs, mult1, mult2                   -> 8 cols
+ *   FriFold           12 per row: z, alpha, x, alpha_pow_in, ro_in, p_at_x, p_at_z, ro_out addrs, ro mult,
+ *                      alpha_pow_out addr, alpha_pow mult, is_first                       -> 20 cols
+ *   PublicValues       1: the digest element's address (n <= 8)                           -> 10 cols
+ *   MemoryVar          2: addr, mult                                                      -> 2 per row, 4 cols
+ *   MemoryConst        6: value[4], addr, mult (negative for a read)                      -> 2 per row, 12 cols
+ *   ExpReverseBitsLen  6 per row: base addr, exponent-bit addr, result addr, mult, row index i, length L
+ *                                                                                          -> 10 cols
+ *   Poseidon2WideDeg3 48: input addrs[16], output addrs[16], output mults[16]             -> 49 cols
+ * Rows past the records are zero. */
+#define ZKM_REC_CHIP_EXP_REVERSE_BITS 8
+#define ZKM_REC_CHIP_POSEIDON2_WIDE 9
+int zkm_recursion_instrs_to_trace(uint32_t chip, const uint32_t *instrs, uint64_t n, uint32_t repr, uint32_t *trace,
+                                  uint64_t height, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

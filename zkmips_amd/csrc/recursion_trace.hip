@@ -134,9 +134,136 @@ __global__ __launch_bounds__(256) void k_event_rows(const uint32_t *__restrict__
     reinterpret_cast<uint4 *>(out)[q] = make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// Preprocessed rows of the recursion chips from their instruction records (zkm_recursion_instrs_to_trace):
+// one thread per trace row, the chip's instr_to_row for each of the row's entries, zero padding rows.
+template <int CHIP>
+__global__ __launch_bounds__(256) void k_instr_rows(const uint32_t *__restrict__ rec, uint64_t n, uint32_t repr,
+                                                    uint32_t *__restrict__ out, uint64_t height, uint32_t width) {
+    using namespace kb;
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= height) return;
+    auto F = [&](uint32_t v) { return repr == ZKM_REPR_MONTGOMERY ? from_mont(v < P ? v : v - P) : (v < P ? v : v - P); };
+    uint32_t *row = out + r * width;
+    for (uint32_t c = 0; c < width; c++) row[c] = 0;
+    constexpr uint32_t NEG1 = P - 1;
+    if constexpr (CHIP == ZKM_REC_CHIP_BASE_ALU || CHIP == ZKM_REC_CHIP_EXT_ALU) {
+        // alu_base.hpp / alu_ext.hpp instr_to_row: addrs, one-hot opcode, mult; four entries per row
+        for (int e = 0; e < 4; e++) {
+            const uint64_t i = 4 * r + e;
+            if (i >= n) break;
+            const uint32_t *q = rec + 5 * i;
+            uint32_t *o = row + 8 * e;
+            o[0] = F(q[0]); o[1] = F(q[1]); o[2] = F(q[2]);
+            if (q[3] < 4) o[3 + q[3]] = 1;
+            o[7] = F(q[4]);
+        }
+    } else if constexpr (CHIP == ZKM_REC_CHIP_BATCH_FRI) {  // batch_fri.hpp: is_real, is_end, the four addrs
+        if (r < n) {
+            const uint32_t *q = rec + 5 * r;
+            row[0] = 1; row[1] = q[4] ? 1u : 0u;
+            row[2] = F(q[0]); row[3] = F(q[1]); row[4] = F(q[2]); row[5] = F(q[3]);
+        }
+    } else if constexpr (CHIP == ZKM_REC_CHIP_SELECT) {  // select.hpp: is_real, addrs, mults
+        if (r < n) {
+            row[0] = 1;
+            for (int c = 0; c < 7; c++) row[1 + c] = F(rec[7 * r + c]);
+        }
+    } else if constexpr (CHIP == ZKM_REC_CHIP_FRI_FOLD) {  // fri_fold.hpp (z, alpha, x read once per instruction)
+        if (r < n) {
+            const uint32_t *q = rec + 12 * r;
+            const uint32_t first = q[11] ? 1u : 0u, nf = first ? NEG1 : 0u;
+            row[0] = first;
+            row[1] = F(q[0]); row[2] = nf;
+            row[3] = F(q[1]); row[4] = nf;
+            row[5] = F(q[2]); row[6] = nf;
+            row[7] = F(q[3]); row[8] = NEG1;
+            row[9] = F(q[4]); row[10] = NEG1;
+            row[11] = F(q[5]); row[12] = NEG1;
+            row[13] = F(q[6]); row[14] = NEG1;
+            row[15] = F(q[7]); row[16] = F(q[8]);
+            row[17] = F(q[9]); row[18] = F(q[10]);
+            row[19] = 1;
+        }
+    } else if constexpr (CHIP == ZKM_REC_CHIP_PUBLIC_VALUES) {  // public_values.hpp: digest element r
+        if (r < n) {
+            row[r] = 1;
+            row[8] = F(rec[r]);
+            row[9] = NEG1;
+        }
+    } else if constexpr (CHIP == ZKM_REC_CHIP_MEMORY_VAR) {  // mem/variable.rs: (addr, mult) x 2
+        for (int e = 0; e < 2; e++) {
+            const uint64_t i = 2 * r + e;
+            if (i >= n) break;
+            row[2 * e] = F(rec[2 * i]);
+            row[2 * e + 1] = F(rec[2 * i + 1]);
+        }
+    } else if constexpr (CHIP == ZKM_REC_CHIP_MEMORY_CONST) {  // mem/constant.rs: (value[4], addr, mult) x 2
+        for (int e = 0; e < 2; e++) {
+            const uint64_t i = 2 * r + e;
+            if (i >= n) break;
+            for (int c = 0; c < 6; c++) row[6 * e + c] = F(rec[6 * i + c]);
+        }
+    } else if constexpr (CHIP == ZKM_REC_CHIP_EXP_REVERSE_BITS) {  // exp_reverse_bits.hpp, row i of an event
+        if (r < n) {
+            const uint32_t *q = rec + 6 * r;
+            const uint32_t i = q[4], L = q[5];
+            const bool first = i == 0, last = i + 1 == L;
+            row[0] = F(q[0]); row[1] = first ? NEG1 : 0u;
+            row[2] = F(q[1]); row[3] = NEG1;
+            row[4] = F(q[2]); row[5] = last ? F(q[3]) : 0u;
+            row[6] = i; row[7] = first; row[8] = last; row[9] = 1;
+        }
+    } else {  // ZKM_REC_CHIP_POSEIDON2_WIDE: poseidon2_wide.hpp instr_to_row
+        if (r < n) {
+            const uint32_t *q = rec + 48 * r;
+            for (int c = 0; c < 16; c++) {
+                row[c] = F(q[c]);
+                row[16 + 2 * c] = F(q[16 + c]);
+                row[17 + 2 * c] = F(q[32 + c]);
+            }
+            row[48] = NEG1;
+        }
+    }
+}
+
 }  // namespace zkm::rtg
 
 using namespace zkm::rtg;
+
+extern "C" int zkm_recursion_instrs_to_trace(uint32_t chip, const uint32_t *instrs, uint64_t n, uint32_t repr,
+                                             uint32_t *trace, uint64_t height, void *stream) {
+    // (record words, entries per row, preprocessed width), indexed by ZKM_REC_CHIP_*
+    static const uint32_t layout[10][3] = {{5, 4, 32}, {5, 4, 32}, {5, 1, 6},  {7, 1, 8},  {12, 1, 20},
+                                           {1, 1, 10}, {2, 2, 4}, {6, 2, 12}, {6, 1, 10}, {48, 1, 49}};
+    if (chip > ZKM_REC_CHIP_POSEIDON2_WIDE || !trace || (n && !instrs) || height < 16 || (height & (height - 1)) ||
+        (repr != ZKM_REPR_CANONICAL && repr != ZKM_REPR_MONTGOMERY) || n > height * layout[chip][1] ||
+        (chip == ZKM_REC_CHIP_PUBLIC_VALUES && n > 8)) {
+        g_last_error = "zkm_recursion_instrs_to_trace: bad arguments (known chip, n instructions fitting height "
+                       "rows, height a power of two >= 16, repr canonical or Montgomery)";
+        return ZKM_ERR_ARG;
+    }
+    const dim3 g((uint32_t)((height + 255) / 256)), b(256);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t w = layout[chip][2];
+    switch (chip) {
+        case 0: hipLaunchKernelGGL(k_instr_rows<0>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        case 1: hipLaunchKernelGGL(k_instr_rows<1>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        case 2: hipLaunchKernelGGL(k_instr_rows<2>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        case 3: hipLaunchKernelGGL(k_instr_rows<3>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        case 4: hipLaunchKernelGGL(k_instr_rows<4>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        case 5: hipLaunchKernelGGL(k_instr_rows<5>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        case 6: hipLaunchKernelGGL(k_instr_rows<6>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        case 7: hipLaunchKernelGGL(k_instr_rows<7>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        case 8: hipLaunchKernelGGL(k_instr_rows<8>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+        default: hipLaunchKernelGGL(k_instr_rows<9>, g, b, 0, s, instrs, n, repr, trace, height, w); break;
+    }
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_recursion_instrs_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
 
 extern "C" int zkm_recursion_events_to_trace(uint32_t chip, const uint32_t *events, uint64_t n, uint32_t repr,
                                              uint32_t *trace, uint64_t height, void *stream) {

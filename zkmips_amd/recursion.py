@@ -1256,6 +1256,52 @@ def prep_key(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None) -> by
     return h.digest()
 
 
+def prep_records(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None) -> Dict[str, tuple]:
+    """The preprocessed traces as instruction records for the device (tracegen.recursion_instrs_trace,
+    zkm_recursion_instrs_to_trace): chip -> (records n x words uint32, height).  Laid out by the kernel they
+    are prep_traces (tests/test_recursion.py checks it on the GPU)."""
+    shape = shape or {}
+    a, h = rec.flat.a, _heights(rec, shape)
+    u = lambda x: np.asarray(x, np.int64).astype(np.uint32)
+    out = {}
+    m = a["mem"]
+    mm = np.where(m["write"].astype(bool), _mod(m["mult"]), _mod(-np.asarray(m["mult"], np.int64)))
+    out["MemoryConst"] = np.concatenate([m["vals"].astype(np.uint32).reshape(-1, 4), u(m["addr"])[:, None],
+                                         mm[:, None]], 1)
+    out["MemoryVar"] = np.stack([u(a["hint"]["addr"]), _mod(a["hint"]["mult"])], 1)
+    for kind, name in (("base", "BaseAlu"), ("ext", "ExtAlu")):
+        x = a[kind]
+        out[name] = np.stack([u(x["out"]), u(x["in1"]), u(x["in2"]), u(x["op"]), _mod(x["mult"])], 1)
+    x = a["p2"]
+    out["Poseidon2WideDeg3"] = np.concatenate([u(x["inp"]).reshape(-1, WIDTH), u(x["out"]).reshape(-1, WIDTH),
+                                               _mod(x["mult"]).reshape(-1, WIDTH)], 1)
+    for kind, name in (("batchfri", "BatchFRI"), ("exprev", "ExpReverseBitsLen")):
+        x = a[kind]
+        L = x["L"]
+        q = np.repeat(np.arange(len(L)), L)
+        i = np.arange(len(q)) - np.repeat(np.cumsum(L) - L, L)
+        if kind == "batchfri":
+            out[name] = np.stack([u(x["acc"][q]), u(x["alpha_pow"]), u(x["p_at_z"]), u(x["p_at_x"]),
+                                  (i == L[q] - 1).astype(np.uint32)], 1)
+        else:
+            out[name] = np.stack([u(x["base"][q]), u(x["exps"]), u(x["result"][q]), _mod(x["mult"])[q],
+                                  i.astype(np.uint32), L[q].astype(np.uint32)], 1)
+    x = a["frifold"]
+    L = x["L"]
+    q = np.repeat(np.arange(len(L)), L)
+    first = (np.arange(len(q)) - np.repeat(np.cumsum(L) - L, L)) == 0
+    out["FriFold"] = np.stack([u(x["z"][q]), u(x["alpha"][q]), u(x["x"][q]), u(x["alpha_pow_in"]), u(x["ro_in"]),
+                               u(x["p_at_x"]), u(x["p_at_z"]), u(x["ro_out"]), _mod(x["rom"]), u(x["alpha_pow_out"]),
+                               _mod(x["apm"]), first.astype(np.uint32)], 1)
+    pv = a["commit"]["pv"]
+    out["Select"] = np.stack([u(a["select"][f]) for f in ("bit", "out1", "out2", "in1", "in2")]
+                             + [_mod(a["select"]["mult1"]), _mod(a["select"]["mult2"])], 1)
+    out["PublicValues"] = (u(pv[0, PV_DIGEST_START:PV_DIGEST_START + DIGEST_SIZE])[:, None] if len(pv)
+                           else np.zeros((0, 1), np.uint32))
+    from .tracegen import RECURSION_INSTR_CHIPS as RIC
+    return {k: (np.ascontiguousarray(v.reshape(len(v), RIC[k][1]).astype(np.uint32)), h[k]) for k, v in out.items()}
+
+
 def main_traces(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None, p2_main: bool = True):
     """The main traces on the host (event_to_row layouts, padding rows zero; Poseidon2WideDeg3's padding
     rows are the permutation of zero, trace.rs), row-major uint32 canonical."""

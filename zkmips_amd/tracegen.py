@@ -397,6 +397,7 @@ def _bind():
         L.zkm_poseidon2_wide_events_to_trace.argtypes = [vp, u64, C.c_uint32, vp, u64, vp]
         L.zkm_exp_reverse_bits_events_to_trace.argtypes = [vp, vp, vp, u64, C.c_uint32, vp, u64, vp]
         L.zkm_recursion_events_to_trace.argtypes = [C.c_uint32, vp, u64, C.c_uint32, vp, u64, vp]
+        L.zkm_recursion_instrs_to_trace.argtypes = [C.c_uint32, vp, u64, C.c_uint32, vp, u64, vp]
         L._tracegen_bound = True
     return L
 
@@ -736,6 +737,25 @@ def recursion_events_trace(chip: str, events_dev, n: int, height: int, montgomer
     t = _trace(height, w * k if k else 1)
     what = "zkm_recursion_events_to_trace"
     _lib.check(_bind().zkm_recursion_events_to_trace(code, _words(events_dev, n * w, what) if n else None, n,
+                                                     1 if montgomery else 0, t.data_ptr(), height, _stream()), what)
+    return t
+
+
+# zkm_recursion_instrs_to_trace chips: name -> (ZKM_REC_CHIP_*, words per record, preprocessed width, the
+# record words that are plain integers rather than field elements)
+RECURSION_INSTR_CHIPS = {"BaseAlu": (0, 5, 32, (3,)), "ExtAlu": (1, 5, 32, (3,)), "BatchFRI": (2, 5, 6, (4,)),
+                         "Select": (3, 7, 8, ()), "FriFold": (4, 12, 20, (11,)), "PublicValues": (5, 1, 10, ()),
+                         "MemoryVar": (6, 2, 4, ()), "MemoryConst": (7, 6, 12, ()),
+                         "ExpReverseBitsLen": (8, 6, 10, (4, 5)), "Poseidon2WideDeg3": (9, 48, 49, ())}
+
+
+def recursion_instrs_trace(chip: str, records_dev, n: int, height: int, montgomery: bool = False):
+    """Preprocessed trace (height x width int32, canonical, on the GPU) of a recursion chip from n instruction
+    records (RECURSION_INSTR_CHIPS; recursion.prep_records builds them) in a 32-bit GPU tensor."""
+    code, w, width, _ = RECURSION_INSTR_CHIPS[chip]
+    t = _trace(height, width)
+    what = "zkm_recursion_instrs_to_trace"
+    _lib.check(_bind().zkm_recursion_instrs_to_trace(code, _words(records_dev, n * w, what) if n else None, n,
                                                      1 if montgomery else 0, t.data_ptr(), height, _stream()), what)
     return t
 
