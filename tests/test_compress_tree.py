@@ -121,7 +121,9 @@ def test_compact_witness_is_the_full_witness(fib_leaves):
     full = CT.node_witness(fib_leaves[:2], fix=False)
     comp = CT.node_witness(fib_leaves[:2], fix=False, compact=True)
     assert isinstance(comp[0], CT.Prep) and comp[0].traces is not None
-    assert set(comp[0].traces) == set(full[0]) and all(np.array_equal(comp[0].traces[k], full[0][k]) for k in full[0])
+    from tests import _rec_model as RM
+    prep = RM.prep_from_records(comp[0].traces)  # the device layout's host model
+    assert set(prep) == set(full[0]) and all(np.array_equal(prep[k], full[0][k]) for k in full[0])
     assert set(comp[1]) == set(full[1])
     for k, v in comp[1].items():
         assert np.array_equal(_host_layout(v), full[1][k]), k

@@ -60,8 +60,10 @@ class DeviceExpRev:
 
 @dataclass
 class Prep:
-    """A node program's proving-key identity (recursion.prep_key) and its preprocessed traces -- None when the
-    worker that built this witness already sent them with an earlier one (register_prep keeps them)."""
+    """A node program's proving-key identity (recursion.prep_key) and its preprocessed traces as instruction
+    records ({chip: (records, height)}, recursion.prep_records; laid out on the GPU at setup by
+    tracegen.recursion_instrs_trace) -- None when the worker that built this witness already sent them with
+    an earlier one (register_prep keeps them)."""
     key: bytes
     traces: Optional[dict]
 
@@ -161,6 +163,20 @@ def _prep_traces_of(p: "Prep") -> dict:
     return t
 
 
+def device_prep(records: dict) -> dict:
+    """A program's preprocessed traces laid out on the current GPU from its instruction records
+    (zkm_recursion_instrs_to_trace), waited for."""
+    import torch
+    from . import tracegen as TG
+    out = {}
+    for name, (recs, h) in records.items():
+        r = np.ascontiguousarray(recs, np.uint32)
+        t = torch.from_numpy(r.reshape(-1).view(np.int32) if r.size else np.zeros(1, np.int32)).cuda()
+        out[name] = TG.recursion_instrs_trace(name, t, len(r), h)
+    torch.cuda.current_stream().synchronize()
+    return out
+
+
 def compact_traces(rec, shape) -> dict:
     """The node's main traces as device work items: the event-row chips (DeviceRows), ExpReverseBitsLen
     (DeviceExpRev) and Poseidon2WideDeg3 (DeviceP2) -- the events only, no padding rows."""
@@ -202,8 +218,8 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
         key = R.prep_key(rec, shape)
         prep = None
         if not dedup or key not in _SENT_KEYS:
-            pt = R.prep_traces(rec, shape)
-            prep = {c.name: pt[c.name] for c in R.compress_machine().chips if c.prep_width}
+            pr = R.prep_records(rec, shape)
+            prep = {c.name: pr[c.name] for c in R.compress_machine().chips if c.prep_width}
             if dedup:
                 _SENT_KEYS.add(key)
         traces = compact_traces(rec, shape)
@@ -317,7 +333,7 @@ class GpuProvers:
             pr = self.cache.get(key)
             if pr is None:
                 t = time.perf_counter()
-                pt = _prep_traces_of(prep) if isinstance(prep, Prep) else prep
+                pt = device_prep(_prep_traces_of(prep)) if isinstance(prep, Prep) else prep
                 pr = HipProver(self.dev, self.machine, pt, **self.kw)
                 stats.setup_s += time.perf_counter() - t
                 stats.setups += 1

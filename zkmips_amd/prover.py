@@ -134,7 +134,8 @@ class HipProver:
         mats = (Matrix * len(machine.chips))()
         for i, c in enumerate(machine.chips):
             if c.name in prep_traces:
-                mats[i] = matrix(prep_traces[c.name], c.name, keep=keep)
+                t = prep_traces[c.name]  # a host array, or a GPU-resident int32 tensor (ZKM_MEM_DEVICE)
+                mats[i] = _device_matrix(t, c.name, keep) if hasattr(t, "data_ptr") else matrix(t, c.name, keep=keep)
             else:
                 mats[i] = Matrix(c.name.encode(), None, 0, 0, 0)
         gcs = as_u32(ZERO_DIGEST if initial_global_cumulative_sum is None else initial_global_cumulative_sum)
