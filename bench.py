@@ -152,6 +152,7 @@ def pmc_in_run(args, timeout_s=240):
              "--log-n", str(args.log_n), "--queries", str(args.queries)]
     sq = {}
     for ctr, mult in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0), (" ".join(SQ_COUNTERS), None)):
+        progress(f"counter pass {ctr.split()[0]}")
         d = os.path.join(base, ctr.split()[0])
         cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc"] + ctr.split() + [
             "--output-format", "csv", "-d", d, "-o", "run", "--"] + child
@@ -1236,6 +1237,17 @@ class ShardBench:
         return pr, self.rk.max_over_ranks(time.perf_counter() - t0)
 
 
+_T0 = time.time()
+
+
+def progress(msg: str):
+    """A progress line on stderr (rank 0): the one JSON line stays alone on stdout, and a long default run
+    keeps writing while it works."""
+    if os.environ.get("RANK", "0") == "0":
+        sys.stderr.write(f"[bench {time.time() - _T0:7.1f} s] {msg}\n")
+        sys.stderr.flush()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -1304,6 +1316,7 @@ def main():
 
     n = 1 << args.log_n
     K = max(1, args.inflight)
+    progress(f"{args.workload} 2^{args.log_n}: generating the shard, setting up")
     sb = ShardBench(args, rk, args.workload, n, K)
     prover, m = sb.prover, sb.m
     dev_traces, pvs, traces = sb.shards[0][0], sb.shards[0][1], sb.shards[0][2]
@@ -1313,6 +1326,7 @@ def main():
         sb.run_steps(1, "pipelined")
         sb.run_steps(1, "per_call")
     # timed region (the headline `value`): traces resident in HBM, commit + open + D2H of the proof
+    progress("timed regions: resident, host traces, per-call copies")
     proof_res, elapsed_res = sb.timed(args.steps, "resident")
     # secondary: host traces with the look-ahead H2D pipeline, and per-call host copies
     proof, elapsed = sb.timed(args.steps, "pipelined")
@@ -1336,6 +1350,7 @@ def main():
     # (one shard in flight, so a stage's events bracket only its own kernels); the roofline and
     # the stage table come from here, the throughput `value` from the timed region above
     nprof = max(1, args.profile_steps)
+    progress("profiled region")
     prof, serial_ms, prof_text = profile_proofs(prover, dev_traces, pvs, nprof)
 
     # the PCIe ceiling of the host-trace mode: one shard's page-locked traces copied alone
@@ -1359,6 +1374,8 @@ def main():
     pageable_s = time.perf_counter() - tp
 
     # HBM bytes per kernel of one shard proof, measured on this box now (rank 0, N = 1 only)
+    if not (args.no_pmc or world > 1 or args.workload == "maxshape"):
+        progress("rocprofv3 counter passes")
     pmc = None if (args.no_pmc or world > 1 or args.workload == "maxshape") else pmc_in_run(args)
     kernel_stages = ["lde", "merkle_leaves", "merkle_nodes", "quotient", "perm_trace", "open_eval", "fri_reduce"]
     dom = max((s for s in kernel_stages if s in prof), key=lambda s: prof[s][1])
@@ -1494,20 +1511,25 @@ def main():
         "profiled_region": f"{nprof} single-shard proofs after the timed region (stages, roofline, ntt, serial_ms_per_shard)",
     }
     if not args.no_sizes and world == 1 and args.workload == "fib":
+        progress("size series")
         line["sizes"] = size_series(args, prover, K)
     if not args.no_maxshape and world == 1 and args.workload == "fib":
+        progress("maximal-shape leg")
         line["maxshape"] = maxshape_leg(args, rk, n, K)
     if pool is not None and not args.no_compress:
+        progress("compress leg")
         line["compress"], _ = compress_leg(args, pool, prover.dev)
     if tm_future is not None:
         import shutil
         try:
+            progress("tendermint leg")
             line["tendermint"] = tendermint_leg(args, tm_future.result(), tm_dir, rk)
         finally:
             shutil.rmtree(tm_dir, ignore_errors=True)
     if pool is not None:
         pool.shutdown()
     if not args.no_cpu_baseline and world == 1:
+        progress("CPU baseline")
         line["cpu_baseline"] = cpu_baseline(args.cpu_log_n, args.queries)
     if args.profile_out:
         with open(args.profile_out, "w") as f:
