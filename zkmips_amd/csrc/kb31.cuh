@@ -48,7 +48,7 @@ KB_HD uint32_t umulhi(uint32_t a, uint32_t b) {
 // (the quotient is the high word of the mad), so a reduction costs 4 issue slots, and the lazy
 // result needs no offset to stay non-negative.
 constexpr uint32_t MUN = 0x7effffffu;  // -P^{-1} mod 2^32
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(KB_PLAIN_MAD)
+#ifdef __HIP_DEVICE_COMPILE__
 __device__ __forceinline__ uint32_t redc2(uint64_t t) {  // t < P 2^32 -> [0, 2P)
     const uint32_t m = (uint32_t)t * MUN;
     uint64_t u, cc;
