@@ -114,3 +114,49 @@ def test_gpu_two_leaf_node(leaves):
     bad[len(bad) // 3] ^= 1
     with pytest.raises(Exception):
         R.execute(RV.compress_node_program([(vk, leaf[0]), (vk, bytes(bad))]))
+
+
+def _flat_equal(x, y):
+    assert x.num_addrs == y.num_addrs and x.n == y.n and x.rows == y.rows
+    assert np.array_equal(x.table, y.table)
+    for k in x.a:
+        assert x.a[k].keys() == y.a[k].keys()
+        for f in x.a[k]:
+            assert np.array_equal(x.a[k][f], y.a[k][f]), (k, f)
+
+
+def test_node_flat_template(leaves, monkeypatch):
+    """node_flat builds a structure's program once; a later node of the same structure (same vk, proof
+    shapes) replays only the hints into it -- the result equals the full build of that node, executes, and
+    a changed child byte still fails."""
+    vk, proofs = leaves
+    RV._TEMPLATES.clear()
+    a = RV.node_flat([(vk, proofs[0]), (vk, proofs[1])])
+    assert len(RV._TEMPLATES) == 1
+    b = RV.node_flat([(vk, proofs[1]), (vk, proofs[0])])
+    assert len(RV._TEMPLATES) == 1 and b is not a
+    _flat_equal(a, R.flatten(RV.compress_node_program([(vk, proofs[0]), (vk, proofs[1])])))
+    _flat_equal(b, R.flatten(RV.compress_node_program([(vk, proofs[1]), (vk, proofs[0])])))
+    ra, rb = R.execute(a), R.execute(b)
+    assert not np.array_equal(ra.public_values, rb.public_values)
+    assert np.array_equal(rb.public_values, R.execute(RV.compress_node_program([(vk, proofs[1]), (vk, proofs[0])])).public_values)
+    bad = bytearray(proofs[1])
+    p = RV.parse_shard_proof(proofs[1])
+    i = bytes(bad).find(np.asarray(p.chips[0].main_l[5], np.uint32).tobytes())
+    bad[i + 2] ^= 0x20
+    with pytest.raises(Exception):
+        R.execute(RV.node_flat([(vk, proofs[0]), (vk, bytes(bad))]))
+    assert len(RV._TEMPLATES) == 1
+    # a single-child node is another structure
+    RV.node_flat([(vk, proofs[0])])
+    assert len(RV._TEMPLATES) == 2
+    # a child vk differing only in its commitment (the next layer's vk) shares the template; the result is
+    # still exactly its own full build (the commitment's constant block replaced).  The proofs do not verify
+    # under that vk, so the host's FRI replay (hint values only) is stubbed for both builds.
+    import dataclasses
+    monkeypatch.setattr(RV, "host_fri_pairs",
+                        lambda vk_, p, rp, rh: [np.zeros((vk_.num_queries, 8), np.int64) for _ in p.fri_commits])
+    vk2 = dataclasses.replace(vk, commit=(np.asarray(vk.commit) + 1) % RV.P)
+    c = RV.node_flat([(vk2, proofs[0]), (vk2, proofs[1])])
+    assert len(RV._TEMPLATES) == 2
+    _flat_equal(c, R.flatten(RV.compress_node_program([(vk2, proofs[0]), (vk2, proofs[1])])))

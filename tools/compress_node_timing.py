@@ -37,6 +37,22 @@ def main():
               f"proof {ms:.2f} ms serial, "
               f"{len(proof)} bytes, max rows {max(v.shape[0] for v in CT.materialize(tr).values())}", flush=True)
     dt = CT.materialize(tr)  # the compact witness: every trace built on the device
+    # the node program: a full build vs node_flat's template (verify_shard against a hint tape only)
+    from zkmips_amd import recursion as R
+    from zkmips_amd import recursion_verifier as RV
+    children = [(CT.resolve_vk(vk), p) for vk, p in leaves]
+    t = time.perf_counter()
+    R.flatten(RV.compress_node_program(children))
+    full_s = time.perf_counter() - t
+    RV._TEMPLATES.clear()
+    t = time.perf_counter()
+    RV.node_flat(children)
+    first_s = time.perf_counter() - t
+    t = time.perf_counter()
+    RV.node_flat(children)
+    tpl_s = time.perf_counter() - t
+    print(f"node program: full build + flatten {full_s:.3f} s, node_flat first {first_s:.3f} s, "
+          f"node_flat from the template {tpl_s:.3f} s", flush=True)
     prof, serial_ms, text = bench.profile_proofs(pr, dt, pv, 3)
     print(f"all traces resident: {serial_ms:.2f} ms serial")
     for k, v in sorted(prof.items(), key=lambda kv: -kv[1][1]):

@@ -208,7 +208,7 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
     from . import recursion_verifier as RV
     t0 = time.perf_counter()
     children = [(resolve_vk(vk), proof) for vk, proof in children]
-    prog = RV.compress_node_program(children)
+    prog = RV.node_flat(children)  # a FlatProgram: built once per program structure, then hints only
     t1 = time.perf_counter()
     shape = R.fix_shape(prog) if fix else {k: max(4, (h - 1).bit_length()) for k, h in R.program_heights(prog).items()}
     if compact:

@@ -527,36 +527,48 @@ std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
     // consecutive banks) while the denominators stay in registers: the 256-register cap no longer
     // spills to scratch (HBM).  Up to kPermLdsBatches batches (80 KB per workgroup, two per CU).
     const bool lds = grp == nb && nb >= 2 && nb <= kPermLdsBatches && !getenv("ZKM_JIT_PERM_NOLDS");
+    // ZKM_JIT_PERM_LDS_SPLIT=k: k inversions per row over consecutive groups of the batches, so LDS holds one
+    // group (80/k KB per workgroup at 10 batches: k workgroups more per CU) for k - 1 more EF inversions
+    const int parts = lds && getenv("ZKM_JIT_PERM_LDS_SPLIT") ? std::max(1, atoi(getenv("ZKM_JIT_PERM_LDS_SPLIT"))) : 1;
+    const int gsz = (nb + parts - 1) / parts;
     if (lds) {
-        for (int b = 0; b < nb; b++) {
-            g.body << "    ef num" << b << ", den" << b << ";\n";
-            lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
-                         "den" + std::to_string(b));
-            // num_b -> LDS rows 4b..4b+3; the prefix product before b -> rows 4(nb + b)..
-            g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * b << " + e) * 256 + threadIdx.x] = num" << b
-                   << ".c[e];\n";
-            if (b == 0) {
-                g.body << "    ef run = den0;\n";
-            } else {
-                g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * (nb + b) << " + e) * 256 + threadIdx.x] = run.c[e];\n"
-                       << "    run = ef_mul(run, den" << b << ");\n";
+        for (int g0 = 0; g0 < nb; g0 += gsz) {
+            const int g1 = std::min(nb, g0 + gsz);
+            // (one group keeps the original names: the source text keys the code-object cache)
+            const std::string sfx = parts == 1 ? "" : std::to_string(g0), run = "run" + sfx, iv = "iv" + sfx;
+            for (int b = g0; b < g1; b++) {
+                const int sl = b - g0;
+                g.body << "    ef num" << b << ", den" << b << ";\n";
+                lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
+                             "den" + std::to_string(b));
+                // num_b -> LDS rows 4 sl..; the group's prefix product before b -> rows 4(gsz + sl)..
+                g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * sl << " + e) * 256 + threadIdx.x] = num" << b
+                       << ".c[e];\n";
+                if (b == g0) {
+                    g.body << "    ef " << run << " = den" << b << ";\n";
+                } else {
+                    g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * (gsz + sl)
+                           << " + e) * 256 + threadIdx.x] = " << run << ".c[e];\n"
+                           << "    " << run << " = ef_mul(" << run << ", den" << b << ");\n";
+                }
             }
-        }
-        g.body << "    ef iv = ef_inv(run);\n";
-        for (int b = nb - 1; b >= 0; b--) {
-            g.body << "    {\n        ef nm, pr;\n"
-                   << "        for (int e = 0; e < 4; e++) nm.c[e] = pl_lds[(" << 4 * b << " + e) * 256 + threadIdx.x];\n";
-            if (b > 0) {
-                g.body << "        for (int e = 0; e < 4; e++) pr.c[e] = pl_lds[(" << 4 * (nb + b)
-                       << " + e) * 256 + threadIdx.x];\n"
-                       << "        const ef sb = ef_mul(nm, ef_mul(iv, pr));\n"
-                       << "        iv = ef_mul(iv, den" << b << ");\n";
-            } else {
-                g.body << "        const ef sb = ef_mul(nm, iv);\n";
+            g.body << "    ef " << iv << " = ef_inv(" << run << ");\n";
+            for (int b = g1 - 1; b >= g0; b--) {
+                const int sl = b - g0;
+                g.body << "    {\n        ef nm, pr;\n"
+                       << "        for (int e = 0; e < 4; e++) nm.c[e] = pl_lds[(" << 4 * sl << " + e) * 256 + threadIdx.x];\n";
+                if (b > g0) {
+                    g.body << "        for (int e = 0; e < 4; e++) pr.c[e] = pl_lds[(" << 4 * (gsz + sl)
+                           << " + e) * 256 + threadIdx.x];\n"
+                           << "        const ef sb = ef_mul(nm, ef_mul(" << iv << ", pr));\n"
+                           << "        " << iv << " = ef_mul(" << iv << ", den" << b << ");\n";
+                } else {
+                    g.body << "        const ef sb = ef_mul(nm, " << iv << ");\n";
+                }
+                for (int e = 0; e < 4; e++)
+                    g.body << "        A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = sb.c[" << e << "];\n";
+                g.body << "        total = ef_add(total, sb);\n    }\n";
             }
-            for (int e = 0; e < 4; e++)
-                g.body << "        A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = sb.c[" << e << "];\n";
-            g.body << "        total = ef_add(total, sb);\n    }\n";
         }
         grp = 0;  // the groups below are done
     }
@@ -585,7 +597,7 @@ std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
     }
     std::ostringstream o;
     o << "extern \"C\" __global__ void " << perm_bounds() << " " << fname << "(const ZkmPermJitArgs A) {\n"
-      << (lds ? "    __shared__ uint32_t pl_lds[" + std::to_string(8 * nb) + " * 256];\n" : std::string())
+      << (lds ? "    __shared__ uint32_t pl_lds[" + std::to_string(8 * gsz) + " * 256];\n" : std::string())
       << "    const uint64_t rl = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n"
       << "    if (rl >= A.ld) return;\n"
       << g.head.str() << g.pipelined(48, "ZKM_JIT_LOOKAHEAD_P")  // 48 -> 0.99 ms, 8 -> 1.37

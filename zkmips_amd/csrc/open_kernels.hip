@@ -512,6 +512,93 @@ __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ co
     }
 }
 
+// Full segments (n a multiple of OPEN_SEG): thread t owns rows 4t..4t+3 and 4(NT + t)..+3 of its segment
+// for every column, so it computes those eight weights once (Montgomery's trick over the eight, one EF
+// inversion) and keeps them in registers: no LDS weight table, two 16-byte loads per column and thread
+// (each a whole 1 KB range per wave), the next row of the last element by a shuffle from the neighbouring
+// lane (the wave's last lane loads it).  The per-thread sums of a column block are reduced through LDS
+// (eight threads per output word, 32 partial sums each) instead of a 6-step shuffle tree per word.
+static constexpr int OPEN_RED_LD = NT + 8;  // padded row: the eight outputs a wave sums sit on distinct banks
+__global__ __launch_bounds__(NT) void k_open_dot_regs(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
+                                                      OpenWeights pw, int with_next, int nseg, uint32_t slab,
+                                                      uint32_t *partial) {
+    __shared__ uint32_t red[OPEN_CB * 8][OPEN_RED_LD];
+    const uint64_t j0 = (uint64_t)blockIdx.x * OPEN_SEG;
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    const uint32_t ra = 4 * t, rb = 4 * NT + 4 * t;
+    ef w[8];
+    {
+        uint32_t om[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint64_t i = j0 + (k < 4 ? ra + k : rb + k - 4);
+            om[k] = root_pow(pw.tw, n, pw.bitrev ? rev_bits((uint32_t)i, pw.log_n) : i);
+        }
+        ef d[8];
+        ef run = ef_one();
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            d[k] = ef_sub(pw.z, ef_base(mul(pw.s, om[k])));
+            w[k] = run;
+            run = ef_mul(run, d[k]);
+        }
+        ef iv = ef_inv(run);
+#pragma unroll
+        for (int k = 7; k >= 0; k--) {
+            ef v = ef_mul(iv, w[k]);
+            iv = ef_mul(iv, d[k]);
+            w[k] = pw.mul_omega ? ef_mul_base(v, om[k]) : v;
+        }
+    }
+    const uint32_t c_begin = blockIdx.y * slab;
+    const uint32_t c_end = c_begin + slab < ncols ? c_begin + slab : ncols;
+    for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += OPEN_CB) {
+        const int nc = (int)(c_end - cb0 < (uint32_t)OPEN_CB ? c_end - cb0 : OPEN_CB);
+#pragma unroll
+        for (int k = 0; k < OPEN_CB; k++) {
+            const uint32_t *y = (const uint32_t *)cols[cb0 + (k < nc ? k : 0)];
+            const uint4 va = *(const uint4 *)(y + j0 + ra), vb = *(const uint4 *)(y + j0 + rb);
+            const uint32_t v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+            uint64_t a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+#pragma unroll
+                for (int m = 0; m < 4; m++) a0[e] = pair_acc(a0[e], v[m], w[m].c[e], v[m + 4], w[m + 4].c[e]);
+            if (with_next) {  // the next row wraps to row 0 at the end of the column
+                uint32_t xa = __shfl_down(va.x, 1, 64), xb = __shfl_down(vb.x, 1, 64);
+                if (lane == 63) {
+                    xa = y[(j0 + ra + 4) & (n - 1)];
+                    xb = y[(j0 + rb + 4) & (n - 1)];
+                }
+                const uint32_t u[8] = {va.y, va.z, va.w, xa, vb.y, vb.z, vb.w, xb};
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+#pragma unroll
+                    for (int m = 0; m < 4; m++) a1[e] = pair_acc(a1[e], u[m], w[m].c[e], u[m + 4], w[m + 4].c[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                red[k * 8 + e][t] = acc_mod(a0[e]);
+                red[k * 8 + 4 + e][t] = with_next ? acc_mod(a1[e]) : 0u;
+            }
+        }
+        __syncthreads();
+        {
+            const uint32_t o = t >> 3, q = t & 7;  // output word o (column o / 8), partial sums q, q + 8, ...
+            uint64_t acc = 0;
+#pragma unroll
+            for (int i = 0; i < NT / 8; i++) acc += red[o][q + 8 * i];  // < 32 P
+            uint32_t r = acc_mod(acc);
+            r = add(r, __shfl_xor(r, 1, 64));
+            r = add(r, __shfl_xor(r, 2, 64));
+            r = add(r, __shfl_xor(r, 4, 64));
+            if (q == 0 && (int)(o >> 3) < nc) partial[((uint64_t)(cb0 + (o >> 3)) * nseg + blockIdx.x) * 8 + (o & 7)] = r;
+        }
+        __syncthreads();  // red is reused by the next column block
+    }
+}
+static_assert(OPEN_CB * 8 * 8 == NT, "one reduction thread group per output word");
+
 // out[col * 8 + e] = sum over the nseg segments of partial[(col * nseg + seg) * 8 + e]: one wave per
 // (column, e) pair group, lanes striding over the segments
 __global__ __launch_bounds__(64) void k_open_sum(const uint32_t *__restrict__ partial, uint32_t ncols, int nseg,
@@ -545,8 +632,13 @@ void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const O
     const uint32_t slab = ((blocks_c + nslab - 1) / nslab) * OPEN_CB;
     nslab = (ncols + slab - 1) / slab;
     DBuf part((size_t)ncols * nseg * 8, s);
-    hipLaunchKernelGGL(k_open_dot, dim3(nseg, nslab), dim3(NT), 0, s, d_cols, ncols, n, w, (int)with_next, nseg, slab,
-                       part.p);
+    static const bool lds_weights = getenv("ZKM_OPEN_LDS_WEIGHTS") && atoi(getenv("ZKM_OPEN_LDS_WEIGHTS"));
+    if (n % OPEN_SEG == 0 && !lds_weights)
+        hipLaunchKernelGGL(k_open_dot_regs, dim3(nseg, nslab), dim3(NT), 0, s, d_cols, ncols, n, w, (int)with_next, nseg,
+                           slab, part.p);
+    else
+        hipLaunchKernelGGL(k_open_dot, dim3(nseg, nslab), dim3(NT), 0, s, d_cols, ncols, n, w, (int)with_next, nseg,
+                           slab, part.p);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_open_sum, dim3(ncols), dim3(64), 0, s, part.p, ncols, nseg, out);
     HIP_CHECK(hipGetLastError());

@@ -636,15 +636,17 @@ def _ev_from_legacy(fp: FlatProgram, events) -> Dict[str, np.ndarray]:
     return ev
 
 
-def execute(prog: RecursionProgram, mem_out: Optional[dict] = None) -> ExecutionRecord:
+def execute(prog, mem_out: Optional[dict] = None) -> ExecutionRecord:
     """Run the program (runtime/mod.rs:336-625) in the native runtime (csrc/host/rec_exec.cpp,
     libzkm_trace.so): memory is write-once, every value read must have been written by an earlier
-    block, constant-memory reads must match; a violation is a RuntimeError naming the block."""
+    block, constant-memory reads must match; a violation is a RuntimeError naming the block.  `prog` is a
+    RecursionProgram or an already flattened FlatProgram (then the record's `program` is None)."""
     import ctypes as C
-    fp = flatten(prog)
+    flat_in = isinstance(prog, FlatProgram)
+    fp = prog if flat_in else flatten(prog)
     a = fp.a
     ev = {k: np.zeros((fp.rows[k] if k in fp.rows else fp.n[k], EV_WIDTH[k]), np.uint32) for k in EV_WIDTH}
-    img = np.zeros((prog.num_addrs, D), np.uint32) if mem_out is not None else None
+    img = np.zeros((fp.num_addrs, D), np.uint32) if mem_out is not None else None
     ptrs = (C.c_void_p * len(_RX_SLOTS))()
     for i, nm in enumerate(_RX_SLOTS):
         if nm == "mem_image":
@@ -657,13 +659,13 @@ def execute(prog: RecursionProgram, mem_out: Optional[dict] = None) -> Execution
         ptrs[i] = None if arr is None or arr.size == 0 else arr.ctypes.data
     err = C.create_string_buffer(256)
     f = _host("zkm_host_recursion_execute")
-    rc = f(prog.num_addrs, len(fp.table), np.ascontiguousarray(fp.table), C.cast(ptrs, C.c_void_p), err, 256)
+    rc = f(fp.num_addrs, len(fp.table), np.ascontiguousarray(fp.table), C.cast(ptrs, C.c_void_p), err, 256)
     if mem_out is not None:
         mem_out["mem"] = img.astype(U)
     if rc != 0:
         raise RuntimeError(err.value.decode())
     pvs = ev["commit"][-1].copy() if len(ev["commit"]) else np.zeros(PROOF_MAX_NUM_PVS, np.uint32)
-    return ExecutionRecord(prog, fp, ev, pvs)
+    return ExecutionRecord(None if flat_in else prog, fp, ev, pvs)
 
 
 def execute_numpy(prog: RecursionProgram, mem_out: Optional[dict] = None) -> ExecutionRecord:
@@ -1343,7 +1345,10 @@ def program_heights(prog: RecursionProgram) -> Dict[str, int]:
     """RecursionAir::heights (crates/recursion/core/src/machine.rs): the rows each compress-machine chip
     needs for the program's instructions, before padding."""
     n = {k: 0 for k in ("mem", "hint", "base", "ext", "p2", "batchfri", "select", "exprev")}
-    for b in prog.blocks:
+    if isinstance(prog, FlatProgram):
+        n.update({k: prog.n[k] for k in ("mem", "hint", "base", "ext", "p2", "select")})
+        n.update({k: prog.rows[k] for k in ("batchfri", "exprev")})
+    for b in ([] if isinstance(prog, FlatProgram) else prog.blocks):
         a = b.a
         if b.kind == "mem":
             n["mem"] += len(a["addr"])

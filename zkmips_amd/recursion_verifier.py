@@ -32,6 +32,7 @@ holds: a changed byte of the child proof changes a hinted value, and the runtime
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -325,6 +326,7 @@ class Builder:
 
     def __init__(self, prog: R.RecursionProgram):
         self.p = prog
+        self._tape = isinstance(prog, _HintTape)  # addresses only: no operand arrays to build
         self._consts: Dict[tuple, int] = {}
         self.labels: Dict[int, str] = {}  # block index of each check -> what it checks (diagnostics)
 
@@ -336,6 +338,18 @@ class Builder:
             self.p.mem_write(a, np.asarray([key], U))
             self._consts[key] = int(a[0])
         return self._consts[key]
+
+    def const_fresh(self, vals) -> np.ndarray:
+        """Addresses of a new constant block per call holding `vals` (base values), never shared with an
+        equal constant: node_flat's templates take its values like hints (the child vk's commitment)."""
+        blk = _blk(vals)
+        a = self.p.alloc(len(blk))
+        if isinstance(self.p, _HintTape):
+            self.p.fresh.append(blk)
+        else:
+            self.p.__dict__.setdefault("fresh_blocks", []).append(len(self.p.blocks))
+        self.p.mem_write(a, blk)
+        return a
 
     def hint_base(self, vals) -> np.ndarray:
         v = np.asarray(vals, np.int64)
@@ -351,7 +365,13 @@ class Builder:
             self.p.hint(a, v.astype(U) % PU)
         return a
 
+    def _out(self, x, y) -> np.ndarray:
+        shp = np.broadcast_shapes(np.shape(x), np.shape(y))
+        return self.p.alloc(math.prod(shp)).reshape(shp)
+
     def base(self, op, x, y) -> np.ndarray:
+        if self._tape:
+            return self._out(x, y)
         x, y = np.broadcast_arrays(np.asarray(x, np.int64), np.asarray(y, np.int64))
         out = self.p.alloc(x.size).reshape(x.shape)
         if x.size:
@@ -359,6 +379,8 @@ class Builder:
         return out
 
     def ext(self, op, x, y) -> np.ndarray:
+        if self._tape:
+            return self._out(x, y)
         x, y = np.broadcast_arrays(np.asarray(x, np.int64), np.asarray(y, np.int64))
         out = self.p.alloc(x.size).reshape(x.shape)
         if x.size:
@@ -810,12 +832,16 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
     b = b or Builder(prog)
     p = parse_shard_proof(proof)
     check_shape(vk, p)
+    if isinstance(prog, _HintTape):  # the chip order and heights: part of a template's key (node_flat)
+        prog.shapes.append((tuple(p.names), tuple(int(o.log_degree) for o in p.chips)))
     rp = replay(vk, p)
     lb, nq = vk.log_blowup, vk.num_queries
     chips = [vk.chips[n] for n in p.names]
     ch = ProgChallenger(b)
-    # observe_into: vk commit, pc_start, initial global sum, 0 -- constants of the program
-    ch.observe([b.const(int(v)) for v in list(vk.commit) + [vk.pc_start] + list(vk.gcs) + [0]])
+    # observe_into: vk commit, pc_start, initial global sum, 0 -- constants of the program (the commit's own
+    # constant block, not shared with equal values: the program's structure does not depend on it)
+    vkc = [int(a) for a in b.const_fresh(vk.commit)]
+    ch.observe(vkc + [b.const(int(v)) for v in [vk.pc_start] + list(vk.gcs) + [0]])
     pv = b.hint_base(p.pv)
     ch.observe(pv[:vk.num_pv])
     main_c, perm_c, quot_c = b.hint_base(p.main_c), b.hint_base(p.perm_c), b.hint_base(p.quot_c)
@@ -871,7 +897,7 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
         c, o = vk.chips[name], p.chips[i]
         pts = [(zeta, o.prep_l)] + ([] if c.local_only else [(zeta_next(o.log_degree), o.prep_n)])
         mats.append({"log_n": int(np.log2(vk.prep_heights[name])), "width": c.prep_width, "pts": pts})
-    rounds.append(([b.const(int(v)) for v in vk.commit], mats))
+    rounds.append((vkc, mats))
     mats = []
     for c, o in zip(chips, p.chips):  # round 1: main
         pts = [(zeta, o.main_l)] + ([] if c.local_only else [(zeta_next(o.log_degree), o.main_n)])
@@ -902,7 +928,7 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
     for _, ms in rounds:
         for m in ms:
             m["pts"] = [(z, b.hint_ext(np.asarray(vals, np.int64).reshape(-1, 4))) for z, vals in m["pts"]]
-    if ood:
+    if ood and not isinstance(prog, _HintTape):  # (no hints in the constraint check)
         none = np.zeros(0, np.int64)
         opened = {c.name: {"prep_l": none, "prep_n": none, "quot": []} for c in chips}
         for name, m in zip(vk.prep_order, rounds[0][1]):
@@ -1116,6 +1142,82 @@ def compress_node_program(children: Sequence[tuple], ood: bool = True) -> R.Recu
     pv[R.PV_DIGEST_START:R.PV_DIGEST_START + R.DIGEST_SIZE] = digest
     prog.commit_public_values(pv)
     return prog
+
+
+class _HintTape(R.RecursionProgram):
+    """A RecursionProgram that keeps only its hints' values, in program order: verify_shard run against it
+    yields a node's witness without building the instructions (node_flat).  The out-of-domain check, which
+    adds no hints, is skipped."""
+
+    def __init__(self):
+        super().__init__()
+        self.vals: List[np.ndarray] = []
+        self.fresh: List[np.ndarray] = []  # const_fresh blocks
+        self.shapes: List[tuple] = []
+
+    def _add(self, kind, **arrays):
+        if kind == "hint":
+            self.vals.append(np.asarray(arrays["vals"], np.uint32))
+
+    def _skip(self, *args, **kwargs):
+        pass
+
+    mem_write = mem_read = base_alu = ext_alu = poseidon2 = select = exp_reverse_bits = batch_fri = _skip
+    fri_fold = commit_public_values = _skip
+
+
+def _vk_key(vk: ChildVk) -> bytes:
+    """Digest of everything in a ChildVk but its commitment (memoised on the object), which the program
+    holds in a const_fresh block: with the hint sizes it keys node_flat's program templates."""
+    k = vk.__dict__.get("_struct_key")
+    if k is None:
+        import hashlib
+        chips = sorted((n, repr(c)) for n, c in vk.chips.items())
+        k = hashlib.blake2b(repr((chips, vk.num_pv, list(vk.prep_order),
+                                  sorted(vk.prep_heights.items()), vk.pc_start, np.asarray(vk.gcs).tolist(),
+                                  vk.log_blowup, vk.num_queries, vk.pow_bits)).encode(), digest_size=16).digest()
+        vk.__dict__["_struct_key"] = k
+    return k
+
+
+_TEMPLATES: Dict[tuple, tuple] = {}  # per process: structure key -> (FlatProgram, const_fresh mem rows)
+
+
+def node_flat(children: Sequence[tuple], ood: bool = True) -> "R.FlatProgram":
+    """compress_node_program(children) flattened, built once per program structure.  The verifier program
+    depends on the children's vks and proof shapes only; the proofs themselves enter as hints.  So the
+    first node of a structure is built in full and its FlatProgram kept; a later node with the same vks and
+    the same hint sizes (which fix the proof shape: chips, heights, FRI rounds, path lengths) runs
+    verify_shard against a _HintTape and gets the template with its hint values replaced.  The result is
+    the FlatProgram of compress_node_program(children) (tests/test_compress_verify.py)."""
+    tape = _HintTape()
+    b = Builder(tape)
+    if not children:
+        raise ValueError("a compress node needs at least one child")
+    for vk, proof in children:
+        verify_shard(tape, vk, proof, b, ood=ood)
+    sizes = tuple(len(v) for v in tape.vals)
+    key = (tuple(_vk_key(vk) for vk, _ in children), tuple(tape.shapes), bool(ood), sizes,
+           tuple(len(v) for v in tape.fresh))
+    hit = _TEMPLATES.get(key)
+    if hit is None:
+        prog = compress_node_program(children, ood=ood)
+        tpl = R.flatten(prog)
+        hint_rows = tuple(int(n) for kc, _, n, _, _ in tpl.table if R.KINDS[kc] == "hint")
+        fresh = [(int(tpl.table[bi][1]), int(tpl.table[bi][2])) for bi in prog.__dict__.get("fresh_blocks", [])]
+        if hint_rows != sizes or [n for _, n in fresh] != [len(v) for v in tape.fresh]:
+            raise AssertionError("hint tape and program disagree")
+        _TEMPLATES[key] = (tpl, fresh)
+        return tpl
+    tpl, fresh = hit
+    a = dict(tpl.a)
+    a["hint"] = dict(a["hint"], vals=np.concatenate(tape.vals) if tape.vals else a["hint"]["vals"])
+    if fresh:
+        mv = a["mem"]["vals"].copy()
+        for (s0, n), v in zip(fresh, tape.fresh):
+            mv[s0:s0 + n] = v
+        a["mem"] = dict(a["mem"], vals=mv)
+    return R.FlatProgram(tpl.num_addrs, tpl.table, a, tpl.n, tpl.rows)
 
 
 def compress_vk(machine, prep_traces, commit, num_queries: int = None) -> ChildVk:
