@@ -853,9 +853,8 @@ def tracegen_bench(args):
 def start_witness_pool(n: int):
     """The compress witness-generation process pool, its workers spawned NOW (before anything in this
     process touches the GPU: they are started as fresh interpreters, never forked from a GPU process)."""
-    import multiprocessing as mpc
-    from concurrent.futures import ProcessPoolExecutor
-    pool = ProcessPoolExecutor(n, mp_context=mpc.get_context("spawn"))
+    from zkmips_amd.compress_tree import AffinityPool
+    pool = AffinityPool(n)
     for f in [pool.submit(time.sleep, 0.3) for _ in range(n)]:
         f.result()
     return pool
@@ -925,8 +924,9 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
 
     # compact witnesses: main traces as event rows laid out on the device, prep traces once per program
     # (children's verifying keys by reference: each worker loads a key's file once)
-    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, CT.by_ref(ch), True, True, True), prove,
-                         inflight)
+    # (a node's job preferably to a worker holding its program's template: CT.AffinityPool)
+    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, CT.by_ref(ch), True, True, True,
+                                                tag=CT.node_tag(ch)), prove, inflight)
     t0 = time.perf_counter()
     root = CT.reduce_distributed(leaves, reducer) if distributed else CT.reduce_serial(leaves, reducer)
     wall = time.perf_counter() - t0

@@ -88,6 +88,39 @@ def test_tree_with_witness_pool_matches_serial(fib_leaves):
     assert np.array_equal(root[0].commit, want[0].commit)
 
 
+def test_tree_with_affinity_pool_matches_serial(fib_leaves):
+    """The same tree through CT.AffinityPool (single-process workers, jobs routed by node_tag to a worker
+    that has built the structure's program template): the same root."""
+    prove = _oracle_prove_factory(4)
+    pool = CT.AffinityPool(2)
+    try:
+        red = CT.Reducer(lambda ch: pool.submit(_witness_small, CT.by_ref(ch), tag=CT.node_tag(ch)), prove,
+                         inflight=2)
+        root = CT.reduce_serial(fib_leaves, red)
+    finally:
+        pool.shutdown()
+    a = prove(_witness_small(fib_leaves[:2]))
+    b = prove(_witness_small(fib_leaves[2:]))
+    assert root[1] == prove(_witness_small([a, b]))[1]
+
+
+def test_affinity_pool_routing():
+    """Least loaded first; among equally loaded workers, one that has run the tag."""
+    import os
+    import time
+    pool = CT.AffinityPool(2)
+    try:
+        p0 = pool.submit(os.getpid, tag="a").result()
+        busy = pool.submit(time.sleep, 1.0, tag="a")      # worker 0 (has "a") busy
+        p1 = pool.submit(os.getpid, tag="x").result()     # -> the idle worker 1
+        busy.result()
+        assert p1 != p0
+        assert pool.submit(os.getpid, tag="x").result() == p1  # both idle: the one that ran "x"
+        assert pool.submit(os.getpid, tag="a").result() == p0
+    finally:
+        pool.shutdown()
+
+
 def _host_layout(v):
     """A compact witness's device work item laid out on the host (what the kernels must produce)."""
     if isinstance(v, CT.DeviceRows):

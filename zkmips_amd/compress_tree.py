@@ -374,6 +374,48 @@ def children_of(node: Node, width_below: int) -> List[Node]:
     return [(L - 1, c) for c in (2 * j, 2 * j + 1) if c < width_below]
 
 
+def node_tag(children) -> tuple:
+    """A cheap stand-in for a node's program structure (node_flat's template key), for AffinityPool: the
+    number of children and their proofs' lengths (a proof's length is fixed by its shape)."""
+    return (len(children),) + tuple(len(p) for _, p in children)
+
+
+class AffinityPool:
+    """The witness workers as single-process executors (spawned: fresh interpreters, safe beside a GPU
+    process), so a node's job can go to a worker that already holds its program's template
+    (recursion_verifier.node_flat, built once per structure and process): submit(fn, *args, tag=t) takes
+    the least loaded worker, among those preferring one that has run tag t.  Otherwise the surface of a
+    ProcessPoolExecutor (submit / shutdown)."""
+
+    def __init__(self, n: int):
+        import multiprocessing as mpc
+        from concurrent.futures import ProcessPoolExecutor
+        ctx = mpc.get_context("spawn")
+        self._ex = [ProcessPoolExecutor(1, mp_context=ctx) for _ in range(max(1, n))]
+        self._load = [0] * len(self._ex)
+        self._tags = [set() for _ in self._ex]
+        self._lock = threading.Lock()
+
+    def submit(self, fn, *args, tag=None, **kwargs):
+        with self._lock:
+            i = min(range(len(self._ex)),
+                    key=lambda k: (self._load[k], 0 if tag is not None and tag in self._tags[k] else 1, k))
+            self._load[i] += 1
+            if tag is not None:
+                self._tags[i].add(tag)
+        fut = self._ex[i].submit(fn, *args, **kwargs)
+        fut.add_done_callback(lambda f, k=i: self._release(k))
+        return fut
+
+    def _release(self, k: int):
+        with self._lock:
+            self._load[k] -= 1
+
+    def shutdown(self, wait: bool = True):
+        for e in self._ex:
+            e.shutdown(wait=wait)
+
+
 class Reducer:
     """The event-driven reduction of one rank's part of the tree.
 

@@ -230,9 +230,8 @@ class ProverService:
         # GPU (0 workers: a thread pool), node proofs in `compress_inflight` threads
         self._pool = None
         if compress_workers > 0:
-            import multiprocessing as mpc
-            from concurrent.futures import ProcessPoolExecutor
-            self._pool = ProcessPoolExecutor(compress_workers, mp_context=mpc.get_context("spawn"))
+            from .compress_tree import AffinityPool
+            self._pool = AffinityPool(compress_workers)
         self.compress_inflight = compress_inflight
         self._compress_provers = None
 
@@ -330,7 +329,8 @@ class ProverService:
             return CT.compress_child_vk(pr.vk_commit, shape), proof
 
         if self._pool is not None:
-            submit = lambda ch: self._pool.submit(CT.node_witness, CT.by_ref(ch), True, True, True)
+            submit = lambda ch: self._pool.submit(CT.node_witness, CT.by_ref(ch), True, True, True,
+                                                  tag=CT.node_tag(ch))
         else:
             from concurrent.futures import ThreadPoolExecutor
             tp = ThreadPoolExecutor(2)
