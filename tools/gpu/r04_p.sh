@@ -8,6 +8,10 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 O=gpurun_out
+timeout -k 10 900 python3 -u -m pytest tests/test_compress_verify.py tests/test_compress_tree.py tests/test_gpu_prover.py -m gpu -v --timeout 600 --timeout-method thread > $O/r04p_gpu_tests.log 2>&1 || { tail -40 $O/r04p_gpu_tests.log; exit 1; }
+tail -2 $O/r04p_gpu_tests.log
+timeout -k 10 600 python3 -u tools/compress_node_timing.py > $O/r04p_node_timing.txt 2>&1 || { tail -20 $O/r04p_node_timing.txt; exit 1; }
+grep -E "witness|node program" $O/r04p_node_timing.txt
 ARGS="--steps 8 --warmup 2 --no-cpu-baseline --no-maxshape --no-compress --no-tendermint --no-sizes --no-pmc"
 for v in "base:" "s2w3:ZKM_JIT_PERM_LDS_SPLIT=2 ZKM_JIT_PERM_WAVES=3" "s2w4:ZKM_JIT_PERM_LDS_SPLIT=2 ZKM_JIT_PERM_WAVES=4" "openlds:ZKM_OPEN_LDS_WEIGHTS=1" "s3w4:ZKM_JIT_PERM_LDS_SPLIT=3 ZKM_JIT_PERM_WAVES=4" "base2:"; do
   tag=${v%%:*}
