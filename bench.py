@@ -925,7 +925,7 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
     # compact witnesses: main traces as event rows laid out on the device, prep traces once per program
     # (children's verifying keys by reference: each worker loads a key's file once)
     # (a node's job preferably to a worker holding its program's template: CT.AffinityPool)
-    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness, CT.by_ref(ch), True, True, True,
+    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness_shm, CT.by_ref(ch), True, True, True,
                                                 tag=CT.node_tag(ch)), prove, inflight)
     t0 = time.perf_counter()
     root = CT.reduce_distributed(leaves, reducer) if distributed else CT.reduce_serial(leaves, reducer)

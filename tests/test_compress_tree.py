@@ -104,6 +104,34 @@ def test_tree_with_affinity_pool_matches_serial(fib_leaves):
     assert root[1] == prove(_witness_small([a, b]))[1]
 
 
+def _packed_job(n):
+    arrs = {"a": np.arange(n, dtype=np.uint32), "b": np.arange(2 * n, dtype=np.int64).reshape(2, n)[:, ::2]}
+    return CT.shm_pack((CT.Prep(b"k", arrs), "small", 3))
+
+
+def test_witness_through_shared_memory():
+    """shm_pack in a worker / shm_unpack here: the same arrays (non-contiguous ones too), writable, the
+    /dev/shm file gone once mapped; small objects go through the pipe as themselves."""
+    import glob
+    import os
+    pool = CT.AffinityPool(1)
+    try:
+        x = pool.submit(_packed_job, 1 << 19).result()
+        assert isinstance(x, CT.Packed) and os.path.exists(x.path)
+        wit = CT.register_prep(x)
+        assert not os.path.exists(x.path)
+        n = 1 << 19
+        assert np.array_equal(wit[0].traces["a"], np.arange(n, dtype=np.uint32)) and wit[1:] == ("small", 3)
+        assert np.array_equal(wit[0].traces["b"], np.arange(2 * n, dtype=np.int64).reshape(2, n)[:, ::2])
+        wit[0].traces["a"][0] = 7  # copy on write
+        assert not isinstance(pool.submit(_packed_job, 16).result(), CT.Packed)
+        y = pool.submit(_packed_job, 1 << 19).result()  # never unpacked: removed at shutdown
+    finally:
+        pool.shutdown()
+    assert not os.path.exists(y.path)
+    assert not glob.glob(f"/dev/shm/zkm_wit_{os.getpid()}_*")
+
+
 def test_affinity_pool_routing():
     """Least loaded first; among equally loaded workers, one that has run the tag."""
     import os

@@ -329,7 +329,7 @@ class ProverService:
             return CT.compress_child_vk(pr.vk_commit, shape), proof
 
         if self._pool is not None:
-            submit = lambda ch: self._pool.submit(CT.node_witness, CT.by_ref(ch), True, True, True,
+            submit = lambda ch: self._pool.submit(CT.node_witness_shm, CT.by_ref(ch), True, True, True,
                                                   tag=CT.node_tag(ch))
         else:
             from concurrent.futures import ThreadPoolExecutor
