@@ -854,10 +854,7 @@ def start_witness_pool(n: int):
     """The compress witness-generation process pool, its workers spawned NOW (before anything in this
     process touches the GPU: they are started as fresh interpreters, never forked from a GPU process)."""
     from zkmips_amd.compress_tree import AffinityPool
-    pool = AffinityPool(n)
-    for f in [pool.submit(time.sleep, 0.3) for _ in range(n)]:
-        f.result()
-    return pool
+    return AffinityPool(n).warm()
 
 
 def mips_leaves(dev, queries: int, n_leaves: int = 64, distinct: int = 4, down: int = 6):

@@ -310,6 +310,17 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
     return prep, traces, pvs, shape, {"build_s": t1 - t0, "execute_and_traces_s": t2 - t1}
 
 
+def warm_worker() -> int:
+    """A witness worker's one-time start-up, outside any timed region: the verifier / runtime modules and the
+    native host library (libzkm_trace.so) loaded, as the first node job would otherwise do."""
+    import os
+    from . import recursion as R
+    from . import recursion_verifier as RV  # noqa: F401
+    for name in ("zkm_host_recursion_execute", "zkm_host_poseidon2_permute", "zkm_host_ef_mul"):
+        R._host(name)
+    return os.getpid()
+
+
 def node_witness_shm(*args, **kwargs):
     """node_witness through shared memory (shm_pack): the pool's job for a consumer whose Reducer unpacks
     (register_prep)."""
@@ -488,6 +499,12 @@ class AffinityPool:
         fut = self._ex[i].submit(fn, *args, **kwargs)
         fut.add_done_callback(lambda f, k=i: self._release(k))
         return fut
+
+    def warm(self):
+        """warm_worker on every worker (each its own executor), waited for."""
+        for f in [e.submit(warm_worker) for e in self._ex]:
+            f.result()
+        return self
 
     def _release(self, k: int):
         with self._lock:

@@ -231,7 +231,7 @@ class ProverService:
         self._pool = None
         if compress_workers > 0:
             from .compress_tree import AffinityPool
-            self._pool = AffinityPool(compress_workers)
+            self._pool = AffinityPool(compress_workers).warm()
         self.compress_inflight = compress_inflight
         self._compress_provers = None
 
