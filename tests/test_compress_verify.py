@@ -37,6 +37,31 @@ def test_parse_roundtrip(leaves):
     assert len(p.fri_commits) == 9 - vk.log_blowup  # 2^8 rows -> LDE 2^9, folded down to 2^log_blowup
 
 
+def test_parse_queries_block(leaves):
+    """The queries read as one matrix equal the field-by-field layout; a query with a different layout
+    (a changed length prefix) falls back to field-by-field parsing and the shape check rejects it."""
+    vk, proofs = leaves
+    p = RV.parse_shard_proof(proofs[0])
+    assert p.q_rows is not None and len(p.q_rows) == 4 and len(p.q_sib) == len(p.fri_commits)
+    for q, (inputs, steps) in enumerate(p.queries):
+        for t, (rows, path) in enumerate(inputs):
+            assert np.array_equal(path, p.q_paths[t][q])
+            for k, r in enumerate(rows):
+                assert np.array_equal(r, p.q_rows[t][k][q])
+        for s_, (sib, fpath) in enumerate(steps):
+            assert np.array_equal(sib, p.q_sib[s_][q]) and np.array_equal(fpath, p.q_fpath[s_][q])
+    # the Merkle path length prefix of query 3's first input round, made one longer
+    b = bytearray(proofs[0])
+    raw = np.asarray(p.queries[3][0][0][1][0], np.uint32).tobytes()  # first sibling digest of that path
+    i = bytes(b).find(raw)
+    n = int.from_bytes(b[i - 8:i], "little")
+    b[i - 8:i] = (n + 1).to_bytes(8, "little")
+    with pytest.raises(ValueError):
+        bad = RV.parse_shard_proof(bytes(b))
+        assert bad.q_rows is None
+        RV.check_shape(vk, bad)
+
+
 def test_node_program_executes(leaves):
     vk, proofs = leaves
     prog = RV.compress_node_program([(vk, p) for p in proofs])

@@ -103,6 +103,13 @@ class ShardProofData:
     pow_witness: int
     names: List[str]
     pv: np.ndarray
+    # the queries' sections stacked over the queries (what the verifier consumes): per input round t the
+    # opened rows of matrix k (nq, width) and the Merkle paths (nq, L, 8); per commit-phase step the
+    # siblings (nq, 4) and paths (nq, L, 8)
+    q_rows: list = None
+    q_paths: list = None
+    q_sib: list = None
+    q_fpath: list = None
 
 
 def parse_shard_proof(b: bytes) -> ShardProofData:
@@ -145,17 +152,7 @@ def parse_shard_proof_at(b: bytes, start: int):
         gcs, lcs = u32s(14), u32s(4)
         chips.append(ChipOpened(pl, pn, ml, mn, rl, rn, quot, gcs, lcs, u64()))
     fri_commits = digests()
-    queries = []
-    for _ in range(u64()):
-        inputs = []
-        for _ in range(u64()):
-            rows = [u32s(u64()) for _ in range(u64())]
-            inputs.append((rows, digests()))
-        steps = []
-        for _ in range(u64()):
-            sib = u32s(4)
-            steps.append((sib, digests()))
-        queries.append((inputs, steps))
+    queries, stacked = _parse_queries(b, pos, u64, u32s, digests)
     final_poly, pow_w = u32s(4), int(u32s(1)[0])
     names = [None] * 0
     order = []
@@ -166,7 +163,76 @@ def parse_shard_proof_at(b: bytes, start: int):
         order.append((u64(), nm))
     names = [nm for _, nm in sorted(order)]
     pv = u32s(u64())
-    return ShardProofData(main_c, perm_c, quot_c, chips, fri_commits, queries, final_poly, pow_w, names, pv), pos[0]
+    return ShardProofData(main_c, perm_c, quot_c, chips, fri_commits, queries, final_poly, pow_w, names, pv,
+                          *stacked), pos[0]
+
+
+def _parse_queries(b: bytes, pos: list, u64, u32s, digests):
+    """The query proofs: (per-query list, (q_rows, q_paths, q_sib, q_fpath)).  Query 0 is parsed field by
+    field, recording each field's word offset; when every query repeats its layout (all length prefixes
+    equal -- a proof of one shape) the rest are read as one (nq, words) matrix and sliced per field."""
+    nq = u64()
+    if nq == 0:
+        return [], ([], [], [], [])
+    q0 = pos[0]
+    prefixes, fields = [], []  # word offsets (from q0) of the u64 length prefixes; (kind, t, off, count)
+
+    def pre():
+        prefixes.append((pos[0] - q0) // 4)
+        return u64()
+
+    def take(kind, t, n_words):
+        fields.append((kind, t, (pos[0] - q0) // 4, n_words))
+        pos[0] += 4 * n_words
+
+    for t in range(pre()):
+        for _ in range(pre()):
+            take("row", t, pre())
+        take("path", t, 8 * pre())
+    for s_ in range(pre()):
+        take("sib", s_, 4)
+        take("fpath", s_, 8 * pre())
+    qw = (pos[0] - q0) // 4
+    if q0 + 4 * nq * qw > len(b):
+        raise ValueError("truncated query proofs")
+    M = np.frombuffer(b, np.uint32, nq * qw, q0).reshape(nq, qw)
+    pcols = np.asarray(sorted(set(prefixes) | {o + 1 for o in prefixes}), np.int64)
+    if not (M[:, pcols] == M[0, pcols]).all():
+        # queries of different shapes (a malformed proof): field by field, check_shape rejects it
+        pos[0] = q0
+        queries = []
+        for _ in range(nq):
+            inputs = []
+            for _ in range(u64()):
+                rows = [u32s(u64()) for _ in range(u64())]
+                inputs.append((rows, digests()))
+            steps = []
+            for _ in range(u64()):
+                sib = u32s(4)
+                steps.append((sib, digests()))
+            queries.append((inputs, steps))
+        return queries, (None, None, None, None)
+    pos[0] = q0 + 4 * nq * qw
+    M = M.astype(np.int64)
+    q_rows, q_paths, q_sib, q_fpath = [], [], [], []
+    for kind, t, off, n in fields:
+        blk = M[:, off:off + n]
+        if kind == "row":
+            while len(q_rows) <= t:
+                q_rows.append([])
+            q_rows[t].append(blk)
+        elif kind == "path":
+            q_paths.append(blk.reshape(nq, n // 8, 8))
+        elif kind == "sib":
+            q_sib.append(blk)
+        else:
+            q_fpath.append(blk.reshape(nq, n // 8, 8))
+    for t in range(len(q_paths)):
+        while len(q_rows) <= t:
+            q_rows.append([])
+    queries = [([([r[q] for r in q_rows[t]], q_paths[t][q]) for t in range(len(q_paths))],
+                [(q_sib[s_][q], q_fpath[s_][q]) for s_ in range(len(q_sib))]) for q in range(nq)]
+    return queries, (q_rows, q_paths, q_sib, q_fpath)
 
 
 # ---------------------------------------------------------------- the child's verifying key
@@ -958,14 +1024,14 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
     lhp: Dict[int, int] = {}  # alpha-power counter per log height, across the rounds
     zero_ef = b.const([0, 0, 0, 0])
     for t, (root, ms) in enumerate(rounds):
-        q_in = [qq[0][t] for qq in p.queries]
         lbm = max(m["log_n"] for m in ms) + lb
         rows = []
         for k, m in enumerate(ms):
-            vals = np.stack([qi[0][k] for qi in q_in])  # (nq, width)
+            vals = _q_rows(p, t, k)  # (nq, width)
             rows.append({"height": 1 << (m["log_n"] + lb), "rows": b.hint_base(vals) if m["width"] else
                          np.zeros((nq, 0), np.int64)})
-        paths = b.hint_base(np.stack([qi[1] for qi in q_in]))  # (nq, L, 8)
+        paths = b.hint_base(p.q_paths[t] if p.q_paths is not None else
+                            np.stack([qq[0][t][1] for qq in p.queries]))  # (nq, L, 8)
         shift = log_max - lbm
         _verify_batch(b, root, rows, index >> shift, ibits[:, shift:shift + lbm], paths)
         for k, m in enumerate(ms):
@@ -998,7 +1064,7 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
     for off in range(len(p.fri_commits)):
         lfh = log_max - 1 - off
         bit = ibits[:, off]
-        sib = b.hint_ext(np.stack([qq[1][off][0] for qq in p.queries]))
+        sib = b.hint_ext(p.q_sib[off] if p.q_sib is not None else np.stack([qq[1][off][0] for qq in p.queries]))
         d = b.ext(R.OP_SUB, sib, folded)
         e0 = b.ext(R.OP_ADD, folded, b.ext(R.OP_MUL, bit, d))      # bit ? sib : folded
         e1 = b.ext(R.OP_SUB, b.ext(R.OP_ADD, folded, sib), e0)
@@ -1006,7 +1072,8 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
         words = b.hint_base(fri_pairs[off].astype(np.int64))
         b.assert_eq_ext(b.ef_from_base4(words[:, :4]), e0, f"fri leaf e0 round {off}")
         b.assert_eq_ext(b.ef_from_base4(words[:, 4:]), e1, f"fri leaf e1 round {off}")
-        fpaths = b.hint_base(np.stack([qq[1][off][1] for qq in p.queries]))
+        fpaths = b.hint_base(p.q_fpath[off] if p.q_fpath is not None else
+                             np.stack([qq[1][off][1] for qq in p.queries]))
         _verify_batch(b, fri_c[off], [{"height": 1 << lfh, "rows": words}], index >> (off + 1),
                       ibits[:, off + 1:off + 1 + lfh], fpaths)
         xn = b.base(R.OP_SUB, zero, x)
@@ -1044,6 +1111,13 @@ def _m_u(a, b):
     return (a * b) % PU
 
 
+def _q_rows(p: ShardProofData, t: int, k: int) -> np.ndarray:
+    """The queries' opened rows of matrix k of input round t, (nq, width) int64."""
+    if p.q_rows is not None:
+        return p.q_rows[t][k]
+    return np.stack([np.asarray(qq[0][t][0][k], np.int64) for qq in p.queries])
+
+
 def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> List[np.ndarray]:
     """The verifier's reduced openings and folds on the host (fri.rs:155-203, :247-361), per commit-phase
     round the queries' (e0 || e1) leaf pairs as an (nq, 8) word array: the pair the program hashes (as hinted base words)
@@ -1077,7 +1151,7 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
                 g = np.full(nq, two_adic_gen(lh), U)
                 x = _m_u(R._pow_vec(g, _bitrev_arr(row, lh)), U(GENERATOR)) if lh else np.full(nq, GENERATOR, U)
                 xs[lh] = x
-            rows = np.stack([np.asarray(p.queries[qn][0][t][0][k], np.int64) for qn in range(nq)]) if width else None
+            rows = _q_rows(p, t, k) if width else None
             for z, vals in pts:
                 pw = lhp.get(lh, 0)
                 lhp[lh] = pw + width
@@ -1101,7 +1175,7 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
     pairs = []
     for off, _ in enumerate(p.queries[0][1]):
         bit = ((idx >> off) & 1).astype(bool)
-        sib = np.stack([np.asarray(p.queries[qn][1][off][0], U) for qn in range(nq)])
+        sib = (p.q_sib[off] if p.q_sib is not None else np.stack([p.queries[qn][1][off][0] for qn in range(nq)])).astype(U)
         e0 = np.where(bit[:, None], sib, folded)
         e1 = np.where(bit[:, None], folded, sib)
         pairs.append(np.concatenate([e0, e1], 1))
