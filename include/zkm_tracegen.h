@@ -244,6 +244,21 @@ typedef struct {
 int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, uint32_t *trace, uint64_t height,
                                    uint32_t *byte_mult, void *stream);
 
+/* Poseidon2Permute (syscall/precompiles/poseidon2/trace.rs event_to_row, columns.rs Poseidon2MemCols):
+ * Poseidon2PermuteEvent as one fixed record: the call's shard, clk and state pointer, the 16 state words'
+ * MemoryWriteRecords (prev_value = the word permuted, value = the permutation's output word).  Each row:
+ * Poseidon2Degree3Cols of the permutation (the PermutationSBox layout of Poseidon2WideDeg3 above), shard,
+ * clk, ptr, 16 MemoryWriteCols, the KoalaBearWordRangeChecker of every pre- and post-state word, is_real;
+ * rows [n, height) the permutation of zero and zero elsewhere.  byte_mult (nullable): the accesses'
+ * timestamp range checks (U16Range, U8Range).  973 columns. */
+typedef struct {
+    uint32_t shard, clk, ptr;
+    zkm_memory_write_record state[16];
+} zkm_poseidon2_permute_event;  /* 396 bytes */
+#define ZKM_POSEIDON2_PERMUTE_WIDTH 973
+int zkm_poseidon2_permute_events_to_trace(const zkm_poseidon2_permute_event *events, uint64_t n, uint32_t *trace,
+                                          uint64_t height, uint32_t *byte_mult, void *stream);
+
 /* ShaCompress (syscall/precompiles/sha256/compress/trace.rs:32-305): ShaCompressEvent's records (its w is a
  * Vec) as one fixed record per call: shard, clk, w_ptr, h_ptr, the 8 reads of h, the 64 reads of w, the 8
  * writes of h.  80 rows per call (init, 64 rounds, finalize): the round state is expanded on the device, then

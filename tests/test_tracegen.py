@@ -467,6 +467,60 @@ def test_sha_precompile_shards_from_device_traces_prove_identically():
     assert checked >= 2
 
 
+def _p2permute_events(n: int = 37, seed: int = 5):
+    """POSEIDON2_PERMUTE calls through the executor's syscall memory (mips_p2permute.exec_poseidon2_permute):
+    states at five reused addresses over several shards, so the accesses' previous records are of the same
+    shard (compare) and of earlier ones."""
+    from zkmips_amd import mips_p2permute as P2
+    mem, mem_init, mem_last = {}, {}, {}
+    evs = []
+    for k in range(n):
+        shard, clk, ptr = 1 + k // 10, 100 + 7 * k, 0x1000 + 64 * (k % 5)
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: (a * 2654435761 + seed) % MC.P)
+        evs.append((P2.POSEIDON2_PERMUTE, (shard, clk, SY.syscall_id(P2.POSEIDON2_PERMUTE), ptr, 0),
+                    P2.exec_poseidon2_permute(pm, shard, clk, ptr, 0)))
+    return evs
+
+
+def test_poseidon2_permute_records_layout():
+    """zkm_poseidon2_permute_event records: shard, clk, ptr, then each state word's MemoryWriteRecord
+    (value = the permuted word, prev_value = the word before)."""
+    evs = _p2permute_events(3)
+    rec = TG.poseidon2_permute_records([e for _, _, e in evs])
+    raw = rec.view(np.uint32).reshape(3, 99)
+    for k, (_, _, e) in enumerate(evs):
+        assert list(raw[k, :3]) == [e["shard"], e["clk"], e["ptr"]]
+        st = raw[k, 3:].reshape(16, 6)
+        assert list(st[:, 0]) == e["post"] and list(st[:, 3]) == e["pre"]
+        assert (st[:, 1] == e["shard"]).all() and (st[:, 2] == e["clk"]).all()
+
+
+@pytest.mark.gpu
+def test_poseidon2_permute_shard_from_device_traces():
+    """A POSEIDON2_PERMUTE precompile shard with every main trace and Byte lookup built on the device
+    (Poseidon2Permute, SyscallPrecompile, MemoryLocal, Global) equals the host builders' traces and
+    multiplicities and proves to the same bytes."""
+    import torch
+    from zkmips_amd import mips_p2permute as P2
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _p2permute_events()
+    m, prep, tr, pv = MC.precompile_shard(P2.POSEIDON2_PERMUTE, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(P2.POSEIDON2_PERMUTE, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert "Poseidon2Permute" in dev
+    for name, t in dev.items():
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), tr[name]), name
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    assert set(traces) <= {"Byte", "Program"}, sorted(traces)
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, {k: v for k, v in prep.items() if v is not None}, num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 @pytest.mark.gpu
 def test_maxshape_shard_from_device_traces():
     """The reference's maximal 2^22 shard shape (scaled to Cpu 2^16): every chip's trace built on the device

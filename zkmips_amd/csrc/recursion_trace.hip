@@ -19,6 +19,7 @@
 #include "../../include/zkm_tracegen.h"
 #include "kb31.cuh"
 #include "p2.cuh"
+#include "p2_rows.cuh"
 
 namespace zkm {
 extern thread_local std::string g_last_error;
@@ -29,9 +30,7 @@ static_assert(sizeof(zkm_poseidon2_event) == 128, "Poseidon2Io<KoalaBear> layout
 
 namespace zkm::rtg {
 
-constexpr int W = 16, NE = 8, NI = 13;
-constexpr int C_EXT = 0, C_INT = C_EXT + NE * W, C_S0 = C_INT + W, C_OUT = C_S0 + NI - 1, C_ESB = C_OUT + W,
-              C_ISB = C_ESB + NE * W, COLS = C_ISB + NI;
+using p2rows::COLS;
 static_assert(COLS == ZKM_POSEIDON2_WIDE_DEG3_WIDTH, "PermutationSBox width");
 constexpr int ROWS = 16, NTH = 16 * ROWS;  // rows per workgroup, 16 lanes per row
 
@@ -48,40 +47,8 @@ __global__ __launch_bounds__(NTH) void k_p2wide_rows(const uint32_t *__restrict_
     const uint32_t t = threadIdx.x, rl = t >> 4, l = t & 15;
     const uint64_t row0 = (uint64_t)blockIdx.x * ROWS, row = row0 + rl;
     uint32_t *my = tile + rl * COLS;
-    const p2x16::Lane c = p2x16::lane_consts((int)l);
     const uint32_t x0 = row < n ? ev[row * 32 + l] : 0u;  // Poseidon2Io: input[16] then output[16]
-    uint32_t x = repr == ZKM_REPR_MONTGOMERY ? (x0 < P ? x0 : x0 - P) : to_mont(x0);
-    my[C_EXT + l] = from_mont(x);
-    x = p2x16::external(x);
-#pragma unroll
-    for (int r = 0; r < NE / 2; r++) {
-        x = cube(add(x, c.rc[r]));
-        my[C_ESB + r * W + l] = from_mont(x);
-        x = p2x16::external(x);
-        my[(r == NE / 2 - 1 ? C_INT : C_EXT + (r + 1) * W) + l] = from_mont(x);
-    }
-#pragma unroll
-    for (int r = 0; r < NI; r++) {
-        const uint32_t y = cube(add(x, p2::RC.inr[r]));
-        if (l == 0) {
-            x = y;
-            my[C_ISB + r] = from_mont(y);
-        }
-        uint32_t sum = add(x, p2x16::dpp<p2x16::ROR(1)>(x));
-        sum = add(sum, p2x16::dpp<p2x16::ROR(2)>(sum));
-        sum = add(sum, p2x16::dpp<p2x16::ROR(4)>(sum));
-        sum = add(sum, p2x16::dpp<p2x16::ROR(8)>(sum));
-        x = add(mul(x, c.dg), sum);
-        if (l == 0 && r < NI - 1) my[C_S0 + r] = from_mont(x);
-    }
-    my[C_EXT + (NE / 2) * W + l] = from_mont(x);
-#pragma unroll
-    for (int r = NE / 2; r < NE; r++) {
-        x = cube(add(x, c.rc[r]));
-        my[C_ESB + r * W + l] = from_mont(x);
-        x = p2x16::external(x);
-        my[(r == NE - 1 ? C_OUT : C_EXT + (r + 1) * W) + l] = from_mont(x);
-    }
+    p2rows::fill(repr == ZKM_REPR_MONTGOMERY ? (x0 < P ? x0 : x0 - P) : to_mont(x0), l, my);
     __syncthreads();
     // the tile's rows are one contiguous span of the row-major trace (nrows is a multiple of 16)
     uint4 *dst = reinterpret_cast<uint4 *>(out + row0 * COLS);

@@ -17,6 +17,7 @@
 #include "../../include/zkm_hip.h"
 #include "../../include/zkm_tracegen.h"
 #include "kb31.cuh"
+#include "p2_rows.cuh"
 
 namespace zkm {
 extern thread_local std::string g_last_error;
@@ -1356,6 +1357,54 @@ struct ShaExtendChip {
     }
 };
 
+// ------------------------------------------------------------------ Poseidon2Permute (poseidon2/trace.rs)
+// Poseidon2MemCols (poseidon2/columns.rs:9-20): Poseidon2Degree3Cols (the 313 PermutationSBox columns),
+// shard, clk, ptr, 16 MemoryWriteCols (prev_value word + MemoryAccessCols), the range checkers of the
+// pre- and post-state words, is_real.  Each 16-lane DPP row of a wavefront builds one trace row (lane l:
+// state word l, as in the recursion chip's kernel); 16 rows per workgroup in a 62 KB LDS tile that leaves
+// as one contiguous span of 16-byte stores.
+enum { PM_SHARD = 313, PM_CLK = 314, PM_ADDR = 315, PM_MEM = 316, PM_PRE = PM_MEM + 16 * 13, PM_POST = PM_PRE + 16 * 14,
+       PM_REAL = PM_POST + 16 * 14, PM_EV = 3 + 16 * 6, PM_ROWS = 16 };
+static_assert(p2rows::COLS == PM_SHARD && PM_REAL + 1 == ZKM_POSEIDON2_PERMUTE_WIDTH, "Poseidon2MemCols layout");
+static_assert(PM_ROWS * ZKM_POSEIDON2_PERMUTE_WIDTH % 4 == 0, "tile of whole 16-byte stores");
+
+__global__ __launch_bounds__(16 * PM_ROWS) void k_p2permute_rows(const uint32_t *__restrict__ ev, uint64_t n,
+                                                                 uint32_t *__restrict__ out, uint32_t *byte_mult) {
+    constexpr int WD = ZKM_POSEIDON2_PERMUTE_WIDTH;
+    __shared__ uint32_t tile[PM_ROWS * WD];
+    const uint32_t t = threadIdx.x, rl = t >> 4, l = t & 15;
+    const uint64_t row0 = (uint64_t)blockIdx.x * PM_ROWS, row = row0 + rl;
+    uint32_t *my = tile + rl * WD;
+    const bool real = row < n;
+    const uint32_t *e = ev + row * PM_EV, *w = e + 3 + 6 * l;  // dereferenced for real rows only
+    p2rows::fill(kb::to_mont(real ? w[3] : 0u), l, my);       // the state word: its write's previous value
+    for (int c = p2rows::COLS + (int)l; c < WD; c += 16) my[c] = 0;
+    __syncthreads();
+    if (real) {
+        if (l == 0) {
+            my[PM_SHARD] = e[0];
+            my[PM_CLK] = e[1];
+            my[PM_ADDR] = e[2];
+            my[PM_REAL] = 1;
+        }
+        const Access a = access_write(w);
+        put_word(my + PM_MEM + 13 * l, a.prev_value);
+        put_access(my, PM_MEM + 13 * l + 4, a);
+        put_range_check(my + PM_PRE + 14 * l, a.prev_value);
+        put_range_check(my + PM_POST + 14 * l, a.value);
+        if (byte_mult) {  // the access's timestamp-difference range checks (memory/consistency/trace.rs)
+            atomicAdd(byte_mult + (a.d16 * BYTE_COLS + B_U16RANGE), 1u);
+            atomicAdd(byte_mult + (a.d8 * BYTE_COLS + B_U8RANGE), 1u);
+        }
+    }
+    __syncthreads();
+    uint4 *dst = reinterpret_cast<uint4 *>(out + row0 * WD);
+    for (uint32_t q = t; q < PM_ROWS * WD / 4; q += 16 * PM_ROWS) {
+        const uint32_t *src = tile + 4 * q;
+        dst[q] = make_uint4(src[0], src[1], src[2], src[3]);
+    }
+}
+
 // ------------------------------------------------------------------ ShaCompress (sha256/compress/trace.rs:32-305)
 // 80 rows per call (8 reads of h, 64 rounds, 8 writes of h + the state).  The round state is sequential
 // within a call, so a first kernel (one thread per call) expands each call into 80 row records: shard,
@@ -1796,6 +1845,23 @@ int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, u
     }
     return launch<29, 29, ZKM_SHA_EXTEND_WIDTH, true>(rows, n, trace, height, chip, stream,
                                                       "zkm_sha_extend_events_to_trace", byte_mult);
+}
+
+int zkm_poseidon2_permute_events_to_trace(const zkm_poseidon2_permute_event *events, uint64_t n, uint32_t *trace,
+                                          uint64_t height, uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_poseidon2_permute_event) == 4 * PM_EV, "Poseidon2PermuteEvent record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1))) {
+        g_last_error = "zkm_poseidon2_permute_events_to_trace: bad arguments (need n <= height, a power of two >= 16)";
+        return ZKM_ERR_ARG;
+    }
+    hipLaunchKernelGGL(k_p2permute_rows, dim3((unsigned)(height / PM_ROWS)), dim3(16 * PM_ROWS), 0, (hipStream_t)stream,
+                       (const uint32_t *)events, n, trace, byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_poseidon2_permute_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
 }
 
 int zkm_sha_compress_events_to_trace(const zkm_sha_compress_event *events, uint64_t n, uint32_t *trace,

@@ -320,6 +320,35 @@ def sha_extend_records(events) -> np.ndarray:
     return out
 
 
+POSEIDON2_PERMUTE_EVENT = np.dtype({"names": ["shard", "clk", "ptr", "state"], "formats": [u4, u4, u4, (u4, (16, 6))],
+                                    "offsets": [0, 4, 8, 12], "itemsize": 396})
+POSEIDON2_PERMUTE_WIDTH = 973  # ZKM_POSEIDON2_PERMUTE_WIDTH
+
+
+def poseidon2_permute_records(events) -> np.ndarray:
+    """zkm_poseidon2_permute_event records of the executor's POSEIDON2_PERMUTE events
+    (mips_p2permute.exec_poseidon2_permute): the 16 state words written at the call's clk."""
+    out = np.zeros(len(events), POSEIDON2_PERMUTE_EVENT)
+    for k, ev in enumerate(events):
+        w = np.asarray(ev["w"], np.int64).reshape(16, 4)  # prev_value, value, prev_shard, prev_clk
+        out[k]["shard"], out[k]["clk"], out[k]["ptr"] = ev["shard"], ev["clk"], ev["ptr"]
+        out[k]["state"] = np.stack([w[:, 1], np.full(16, ev["shard"]), np.full(16, ev["clk"]), w[:, 0], w[:, 2],
+                                    w[:, 3]], 1)
+    return out
+
+
+def poseidon2_permute_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    """Poseidon2Permute main trace (height x 973 int32, on the GPU) from n zkm_poseidon2_permute_event
+    records; its accesses' Byte lookups added into byte_mult (nullable)."""
+    height = height or _pow2(n)
+    t = _trace(height, POSEIDON2_PERMUTE_WIDTH)
+    what = "zkm_poseidon2_permute_events_to_trace"
+    _lib.check(_bind().zkm_poseidon2_permute_events_to_trace(_records(events_dev, n, POSEIDON2_PERMUTE_EVENT, what), n,
+                                                             t.data_ptr(), height, _words(byte_mult, 65536 * 10, what),
+                                                             _stream()), what)
+    return t
+
+
 def sha_extend_trace(rows_dev, n: int, height: int = None, byte_mult=None):
     """ShaExtend main trace (height x 176 int32 on the GPU) from n flattened rows (n a multiple of 48)."""
     height = height or max(16, 1 << max(2, (n - 1).bit_length()))
@@ -389,6 +418,7 @@ def _bind():
         L.zkm_misc_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_sha_extend_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_sha_compress_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_poseidon2_permute_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -761,11 +791,12 @@ def recursion_instrs_trace(chip: str, records_dev, n: int, height: int, montgome
 
 
 def precompile_shard_traces(code: int, events, byte_mult=None):
-    """Device traces of a SHA precompile shard (mips_core.precompile_shard's chips for SHA_EXTEND /
-    SHA_COMPRESS): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    """Device traces of a SHA or Poseidon2 precompile shard (mips_core.precompile_shard's chips for
+    SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
     from . import mips_memory as MM
+    from . import mips_p2permute as P2P
     from . import mips_syscall as SY
     pevs = [e for _, _, e in events]
     sev = np.asarray([s_ for _, s_, _ in events], np.int64).reshape(-1, 5)  # shard, clk, id, arg1, arg2
@@ -776,6 +807,9 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     elif code == SY.SHA_COMPRESS:
         rec = sha_compress_records(pevs)
         out["ShaCompress"] = sha_compress_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    elif code == P2P.POSEIDON2_PERMUTE:
+        rec = poseidon2_permute_records(pevs)
+        out["Poseidon2Permute"] = poseidon2_permute_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     else:
         raise ValueError(f"no device trace for precompile {code:#x}")
     sc = np.zeros(len(sev), SYSCALL_EVENT)
