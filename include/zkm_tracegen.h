@@ -244,6 +244,20 @@ typedef struct {
 int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, uint32_t *trace, uint64_t height,
                                    uint32_t *byte_mult, void *stream);
 
+/* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
+ * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
+ * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /
+ * MMAP2 with a0 = 0), unused otherwise.  One row per call (flags per syscall kind, GtColsBytes of BRK);
+ * rows [n, height) zero.  byte_mult (nullable): the accesses' timestamp range checks and BRK's LTU / U8
+ * lookups.  69 columns. */
+typedef struct {
+    uint32_t shard, clk, code, a0, a1, result;
+    zkm_memory_write_record a3, io;
+} zkm_sys_linux_event;  /* 72 bytes */
+#define ZKM_SYS_LINUX_WIDTH 69
+int zkm_sys_linux_events_to_trace(const zkm_sys_linux_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                  uint32_t *byte_mult, void *stream);
+
 /* Poseidon2Permute (syscall/precompiles/poseidon2/trace.rs event_to_row, columns.rs Poseidon2MemCols):
  * Poseidon2PermuteEvent as one fixed record: the call's shard, clk and state pointer, the 16 state words'
  * MemoryWriteRecords (prev_value = the word permuted, value = the permutation's output word).  Each row:

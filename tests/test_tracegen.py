@@ -517,7 +517,76 @@ def test_poseidon2_permute_shard_from_device_traces():
     assert set(traces) <= {"Byte", "Program"}, sorted(traces)
     traces.update(dev)
     traces["Byte"] = bm
-    prover = HipProver(Device(0), m, {k: v for k, v in prep.items() if v is not None}, num_queries=16)
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
+def _core_prep():
+    """The core machine's preprocessed traces of a small program (the Program chip's rows), the proving key
+    the precompile shards above are proven under."""
+    _, prep, _, _ = MC.program_shards(MC.sha_program(1, seed=1), seed=1, shard_size=1 << 12)[0]
+    return {k: v for k, v in prep.items() if v is not None}
+
+
+def _sys_linux_events():
+    """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
+    MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,
+    other; good and bad fds), READ (stdin, other fd), WRITE and a no-op syscall, over two shards."""
+    regs = [(0x1000 * r + 7) % (1 << 32) for r in range(MC.NUM_REGS)]
+    regs[MC.REG_BRK], regs[MC.REG_HEAP] = 0x10000000, 0x20000000
+    last = [(1, r) for r in range(MC.NUM_REGS)]
+    reg_start, reg_done = [(last[r], regs[r]) for r in range(MC.NUM_REGS)], []
+    mem, mem_init, mem_last = {}, {}, {}
+    calls = [(SY.SYS_BRK, 0x10001000, 0), (SY.SYS_BRK, 0x0FFF0000, 0), (SY.SYS_MMAP, 0, 0x3000),
+             (SY.SYS_MMAP, 0, 0x2801), (SY.SYS_MMAP2, 0x4000, 0x1000), (SY.SYS_MMAP2, 0, 0x10), (SY.SYS_CLONE, 0, 0),
+             (SY.SYS_FCNTL, 1, 3), (SY.SYS_FCNTL, 2, 1), (SY.SYS_FCNTL, 7, 3), (SY.SYS_FCNTL, 0, 4), (SY.SYS_READ, 0, 0),
+             (SY.SYS_READ, 3, 0), (SY.SYS_WRITE, 1, 0), (SY.SYS_NOPS[0], 5, 6), (SY.SYS_EXT_GROUP, 0, 0)]
+    evs = []
+    for k, (code, a0, a1) in enumerate(calls * 2):
+        shard, clk = 2 + k // 20, 40 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: 0, regs, last, reg_start,
+                                 reg_done)
+        _, ev = SY.exec_sys_linux(pm, shard, clk, code, a0, a1)
+        evs.append((SY.SYS_LINUX, (shard, clk, SY.syscall_id(code), a0, a1), ev))
+    return evs
+
+
+def test_sys_linux_records_layout():
+    """zkm_sys_linux_event records: the call, the A3 write, the io access of BRK / WRITE / MMAP with a0 = 0."""
+    evs = _sys_linux_events()
+    rec = TG.sys_linux_records([e for _, _, e in evs])
+    assert rec.dtype.itemsize == 72
+    for r, (_, _, e) in zip(rec, evs):
+        assert (r["code"], r["a0"], r["a1"], r["result"]) == (e["code"], e["a0"], e["a1"], e["v0"])
+        assert r["a3"][3] == e["writes"][0][0] and r["a3"][0] == e["writes"][0][1]
+        if e["code"] == SY.SYS_BRK:
+            assert r["io"][0] == r["io"][3] == e["reads"][0][0]
+        elif e["code"] in (SY.SYS_MMAP, SY.SYS_MMAP2) and e["a0"] == 0:
+            assert list(r["io"][[3, 0]]) == list(e["writes"][1][:2])
+        elif e["code"] != SY.SYS_WRITE:
+            assert not r["io"].any()
+
+
+@pytest.mark.gpu
+def test_sys_linux_shard_from_device_traces():
+    """A Linux-syscall precompile shard with every main trace and Byte lookup built on the device equals the
+    host builders' traces and multiplicities and proves to the same bytes."""
+    import torch
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _sys_linux_events()
+    m, prep, tr, pv = MC.precompile_shard(SY.SYS_LINUX, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(SY.SYS_LINUX, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert "SysLinux" in dev
+    for name, t in dev.items():
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), tr[name]), name
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 

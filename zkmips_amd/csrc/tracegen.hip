@@ -1357,6 +1357,109 @@ struct ShaExtendChip {
     }
 };
 
+// ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
+// SysLinuxCols (sys_linux/columns.rs); zkm_sys_linux_event dwords: shard, clk, code, a0, a1, result, the A3
+// write, the io record
+enum { LX_SHARD = 0, LX_CLK = 1, LX_ID = 2, LX_A0 = 3, LX_A1 = 7, LX_RES = 11, LX_IO = 15, LX_OUT = 28, LX_A0_0 = 41,
+       LX_A0_1 = 42, LX_A0_2 = 43, LX_MMAP = 44, LX_MMAP2 = 45, LX_MMAP_A0_0 = 46, LX_PAGE_OFF = 47, LX_OFF_0 = 48,
+       LX_UPPER = 49, LX_CLONE = 50, LX_EXIT = 51, LX_BRK = 52, LX_GT = 53, LX_FCNTL = 60, LX_A1_1 = 61, LX_A1_3 = 62,
+       LX_F_A1_1 = 63, LX_F_A1_3 = 64, LX_READ = 65, LX_WRITE = 66, LX_NOP = 67, LX_REAL = 68, LX_EV = 18 };
+static_assert(LX_REAL + 1 == ZKM_SYS_LINUX_WIDTH, "SysLinuxCols layout");
+constexpr uint32_t SYS_READ_ = 4003, SYS_WRITE_ = 4004, SYS_BRK_ = 4045, SYS_FCNTL_ = 4055, SYS_MMAP2_ = 4090,
+                   SYS_CLONE_ = 4120, SYS_MMAP_ = 4210, SYS_EXT_GROUP_ = 4246;  // executor/src/syscalls/code.rs
+
+struct SysLinuxChip {
+    // MemoryWriteCols at `base` (prev_value word, then MemoryAccessCols) with its range-check lookups
+    __device__ __forceinline__ static void write(uint32_t *v, int base, const uint32_t *rec, const Hist &h) {
+        const Access a = access_write(rec);
+        put_word(v + base, a.prev_value);
+        put_access(v, base + 4, a);
+        h.byte(B_U16RANGE, a.d16 >> 8, a.d16 & 0xFF, true);
+        h.byte(B_U8RANGE, 0, a.d8, true);
+    }
+    __device__ __forceinline__ void row(uint32_t *v, const uint32_t *e, uint64_t, const Hist &h) const {
+#pragma unroll
+        for (int c = 0; c < ZKM_SYS_LINUX_WIDTH; c++) v[c] = 0;
+        // every lane takes part in the ballots of Hist::byte, with `on` false for the padding rows
+        const bool real = e != nullptr;
+        const uint32_t code = real ? e[2] : 0u, a0 = real ? e[3] : 0u, a1 = real ? e[4] : 0u;
+        if (real) {
+            v[LX_SHARD] = e[0];
+            v[LX_CLK] = e[1];
+            v[LX_ID] = code;
+            v[LX_REAL] = 1;
+            put_word(v + LX_A0, a0);
+            put_word(v + LX_A1, a1);
+            put_word(v + LX_RES, e[5]);
+            v[LX_A0_0] = a0 == 0;
+            v[LX_A0_1] = a0 == 1;
+            v[LX_A0_2] = a0 == 2;
+        }
+        const Access out = real ? access_write(e + 6) : Access{};
+        if (real) {
+            put_word(v + LX_OUT, out.prev_value);
+            put_access(v, LX_OUT + 4, out);
+        }
+        h.byte(B_U16RANGE, out.d16 >> 8, out.d16 & 0xFF, real);
+        h.byte(B_U8RANGE, 0, out.d8, real);
+        const bool brk = real && code == SYS_BRK_, wr = real && code == SYS_WRITE_;
+        const bool mmap = real && (code == SYS_MMAP_ || code == SYS_MMAP2_);
+        const bool io = brk || wr || (mmap && a0 == 0);
+        const Access ia = io ? access_write(e + 12) : Access{};
+        if (io) {
+            put_word(v + LX_IO, ia.prev_value);
+            put_access(v, LX_IO + 4, ia);
+        }
+        h.byte(B_U16RANGE, ia.d16 >> 8, ia.d16 & 0xFF, io);
+        h.byte(B_U8RANGE, 0, ia.d8, io);
+        // BRK: GtColsBytes::populate(a0, brk): the most significant differing byte, its values and a0 > brk
+        uint32_t ac = 0, bc = 0;
+        if (brk) {
+            v[LX_BRK] = 1;
+            const uint32_t b = ia.value;
+            for (int j = 3; j >= 0; j--) {
+                if (byte_of(a0, j) != byte_of(b, j)) {
+                    v[LX_GT + j] = 1;
+                    ac = byte_of(a0, j);
+                    bc = byte_of(b, j);
+                    v[LX_GT + 6] = ac > bc;
+                    break;
+                }
+            }
+            v[LX_GT + 4] = ac;
+            v[LX_GT + 5] = bc;
+        }
+        h.byte(B_LTU, bc, ac, brk);
+        h.byte(B_U8RANGE, byte_of(a0, 0), byte_of(a0, 1), brk);
+        h.byte(B_U8RANGE, byte_of(a0, 2), byte_of(a0, 3), brk);
+        h.byte(B_U8RANGE, byte_of(ia.value, 0), byte_of(ia.value, 1), brk);
+        h.byte(B_U8RANGE, byte_of(ia.value, 2), byte_of(ia.value, 3), brk);
+        if (!real || brk) return;
+        if (code == SYS_CLONE_) {
+            v[LX_CLONE] = 1;
+        } else if (code == SYS_EXT_GROUP_) {
+            v[LX_EXIT] = 1;
+        } else if (code == SYS_FCNTL_) {
+            v[LX_FCNTL] = 1;
+            v[LX_A1_1] = v[LX_F_A1_1] = a1 == 1;
+            v[LX_A1_3] = v[LX_F_A1_3] = a1 == 3;
+        } else if (mmap) {
+            v[LX_MMAP] = 1;
+            v[LX_MMAP2] = code == SYS_MMAP2_;
+            v[LX_MMAP_A0_0] = a0 == 0;
+            v[LX_PAGE_OFF] = a1 & 0xFFF;
+            v[LX_OFF_0] = (a1 & 0xFFF) == 0;
+            v[LX_UPPER] = (a1 >> 12) << 12;
+        } else if (code == SYS_READ_) {
+            v[LX_READ] = 1;
+        } else if (code == SYS_WRITE_) {
+            v[LX_WRITE] = 1;
+        } else {
+            v[LX_NOP] = 1;
+        }
+    }
+};
+
 // ------------------------------------------------------------------ Poseidon2Permute (poseidon2/trace.rs)
 // Poseidon2MemCols (poseidon2/columns.rs:9-20): Poseidon2Degree3Cols (the 313 PermutationSBox columns),
 // shard, clk, ptr, 16 MemoryWriteCols (prev_value word + MemoryAccessCols), the range checkers of the
@@ -1845,6 +1948,13 @@ int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, u
     }
     return launch<29, 29, ZKM_SHA_EXTEND_WIDTH, true>(rows, n, trace, height, chip, stream,
                                                       "zkm_sha_extend_events_to_trace", byte_mult);
+}
+
+int zkm_sys_linux_events_to_trace(const zkm_sys_linux_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                                  uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_sys_linux_event) == 4 * LX_EV, "LinuxEvent record");
+    return launch<LX_EV, LX_EV, ZKM_SYS_LINUX_WIDTH, true>(events, n, trace, height, SysLinuxChip{}, stream,
+                                                          "zkm_sys_linux_events_to_trace", byte_mult);
 }
 
 int zkm_poseidon2_permute_events_to_trace(const zkm_poseidon2_permute_event *events, uint64_t n, uint32_t *trace,

@@ -320,6 +320,43 @@ def sha_extend_records(events) -> np.ndarray:
     return out
 
 
+SYS_LINUX_EVENT = np.dtype({"names": ["shard", "clk", "code", "a0", "a1", "result", "a3", "io"],
+                            "formats": [u4, u4, u4, u4, u4, u4, (u4, 6), (u4, 6)],
+                            "offsets": [0, 4, 8, 12, 16, 20, 24, 48], "itemsize": 72})
+SYS_LINUX_WIDTH = 69  # ZKM_SYS_LINUX_WIDTH
+
+
+def sys_linux_records(events) -> np.ndarray:
+    """zkm_sys_linux_event records of the executor's Linux syscall events (mips_syscall.exec_sys_linux):
+    the A3 write and the io access (BRK / WRITE: the register read, MMAP(2) with a0 = 0: the heap write)."""
+    from . import mips_syscall as SY
+    out = np.zeros(len(events), SYS_LINUX_EVENT)
+    for k, e in enumerate(events):
+        sh, clk, code = e["shard"], e["clk"], e["code"]
+        r = out[k]
+        r["shard"], r["clk"], r["code"], r["a0"], r["a1"], r["result"] = sh, clk, code, e["a0"], e["a1"], e["v0"]
+        prev, val, ps, pc = e["writes"][0]
+        r["a3"] = [val, sh, clk, prev, ps, pc]
+        if code in (SY.SYS_BRK, SY.SYS_WRITE):
+            val, ps, pc = e["reads"][0]
+            r["io"] = [val, sh, clk, val, ps, pc]
+        elif code in (SY.SYS_MMAP, SY.SYS_MMAP2) and e["a0"] == 0:
+            prev, val, ps, pc = e["writes"][1]
+            r["io"] = [val, sh, clk, prev, ps, pc]
+    return out
+
+
+def sys_linux_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    """SysLinux main trace (height x 69 int32, on the GPU) from n zkm_sys_linux_event records; the Byte
+    lookups added into byte_mult (nullable)."""
+    height = height or _pow2(n)
+    t = _trace(height, SYS_LINUX_WIDTH)
+    what = "zkm_sys_linux_events_to_trace"
+    _lib.check(_bind().zkm_sys_linux_events_to_trace(_records(events_dev, n, SYS_LINUX_EVENT, what), n, t.data_ptr(),
+                                                     height, _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
 POSEIDON2_PERMUTE_EVENT = np.dtype({"names": ["shard", "clk", "ptr", "state"], "formats": [u4, u4, u4, (u4, (16, 6))],
                                     "offsets": [0, 4, 8, 12], "itemsize": 396})
 POSEIDON2_PERMUTE_WIDTH = 973  # ZKM_POSEIDON2_PERMUTE_WIDTH
@@ -419,6 +456,7 @@ def _bind():
         L.zkm_sha_extend_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_sha_compress_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_poseidon2_permute_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_sys_linux_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -443,7 +481,8 @@ def to_device(records: np.ndarray):
     torch = _torch()
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
                              SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
-                             COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT, POSEIDON2_PERMUTE_EVENT):
+                             COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT, POSEIDON2_PERMUTE_EVENT,
+                             SYS_LINUX_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -791,8 +830,8 @@ def recursion_instrs_trace(chip: str, records_dev, n: int, height: int, montgome
 
 
 def precompile_shard_traces(code: int, events, byte_mult=None):
-    """Device traces of a SHA or Poseidon2 precompile shard (mips_core.precompile_shard's chips for
-    SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    """Device traces of a SHA, Poseidon2 or Linux-syscall precompile shard (mips_core.precompile_shard's chips
+    for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
     from . import mips_memory as MM
@@ -807,6 +846,9 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     elif code == SY.SHA_COMPRESS:
         rec = sha_compress_records(pevs)
         out["ShaCompress"] = sha_compress_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    elif code == SY.SYS_LINUX:
+        rec = sys_linux_records(pevs)
+        out["SysLinux"] = sys_linux_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     elif code == P2P.POSEIDON2_PERMUTE:
         rec = poseidon2_permute_records(pevs)
         out["Poseidon2Permute"] = poseidon2_permute_trace(to_device(rec), len(rec), byte_mult=byte_mult)
