@@ -244,6 +244,21 @@ typedef struct {
 int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, uint32_t *trace, uint64_t height,
                                    uint32_t *byte_mult, void *stream);
 
+/* Uint256MulMod (syscall/precompiles/uint256/air.rs:103-186): Uint256MulEvent as one fixed record: shard, clk,
+ * x_ptr, y_ptr, the 8 reads of y and the 8 reads of the modulus (at clk), the 8 writes of x (at clk + 1; each
+ * prev_value a word of x).  Each row: the accesses, IsZeroOperation of the modulus's byte sum, FieldOpCols of
+ * x y mod m (2^256 when m = 0: result, carry, the vanishing polynomial's witness limbs), FieldLtCols
+ * result < m when m != 0; padding rows multiply zeros modulo 2^256.  byte_mult (nullable): the U8 range
+ * checks of the FieldOpCols limbs, the LTU comparison and the accesses' range checks.  480 columns. */
+typedef struct {
+    uint32_t shard, clk, x_ptr, y_ptr;
+    zkm_memory_read_record y[8], modulus[8];
+    zkm_memory_write_record x[8];
+} zkm_uint256_mul_event;  /* 528 bytes */
+#define ZKM_UINT256_MUL_WIDTH 480
+int zkm_uint256_mul_events_to_trace(const zkm_uint256_mul_event *events, uint64_t n, uint32_t *trace,
+                                    uint64_t height, uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

@@ -528,6 +528,69 @@ def _core_prep():
     return {k: v for k, v in prep.items() if v is not None}
 
 
+def _uint256_events(seed: int = 11):
+    """UINT256_MUL calls through the executor (mips_ec.exec_uint256_mul): full-width, one-limb and
+    two-limb moduli, the zero modulus (2^256), operands below the modulus, over two shards."""
+    from zkmips_amd import emulated_field as EF
+    from zkmips_amd import mips_ec as EC
+    rng = np.random.default_rng(seed)
+    words = {}
+    mem, mem_init, mem_last = {}, {}, {}
+    evs = []
+    mods = [int.from_bytes(rng.bytes(32), "little") | (1 << 255) | 1 for _ in range(6)]
+    mods += [0, 0, 0xFFFFFFFB, 7, (1 << 40) + 3, int.from_bytes(rng.bytes(20), "little") | 1, 1 << 255]
+    for k, m in enumerate(mods * 2):
+        bound = m if m else 1 << 256
+        x, y = (int.from_bytes(rng.bytes(32), "little") % bound for _ in range(2))
+        xp, yp = 0x4000 + 0x100 * k, 0x8000 + 0x100 * k
+        for i, w in enumerate(EF.int_to_words(x, 8)):
+            words[xp + 4 * i] = w
+        for i, w in enumerate(EF.int_to_words(y, 8) + EF.int_to_words(m, 8)):
+            words[yp + 4 * i] = w
+        shard, clk = 3 + k // 10, 50 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: words.get(a, 0))
+        evs.append((EC.UINT256_MUL, (shard, clk, SY.syscall_id(EC.UINT256_MUL), xp, yp),
+                    EC.exec_uint256_mul(pm, shard, clk, xp, yp)))
+    return evs
+
+
+def test_uint256_mul_records_layout():
+    """zkm_uint256_mul_event records: y and the modulus read at clk, x written at clk + 1."""
+    evs = _uint256_events()
+    rec = TG.uint256_mul_records([e for _, _, e in evs])
+    assert rec.dtype.itemsize == 528
+    for r, (_, _, e) in zip(rec, evs):
+        assert list(r["y"][:, 0]) == [v[0] for v in e["y"]] and list(r["modulus"][:, 0]) == [v[0] for v in e["m"]]
+        assert list(r["x"][:, 3]) == e["x"] and (r["x"][:, 2] == e["clk"] + 1).all()
+
+
+@pytest.mark.gpu
+def test_uint256_mul_shard_from_device_traces():
+    """A UINT256_MUL precompile shard with every main trace and Byte lookup built on the device (the
+    product divided by the modulus on the device, the vanishing polynomial's witness) equals the host
+    builders' traces and multiplicities and proves to the same bytes."""
+    import torch
+    from zkmips_amd import mips_ec as EC
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _uint256_events()
+    m, prep, tr, pv = MC.precompile_shard(EC.UINT256_MUL, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(EC.UINT256_MUL, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert "Uint256MulMod" in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

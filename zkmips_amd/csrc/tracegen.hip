@@ -1357,6 +1357,184 @@ struct ShaExtendChip {
     }
 };
 
+// ------------------------------------------------------------------ Uint256MulMod (uint256/air.rs:103-186)
+// Uint256MulCols: shard, clk, x_ptr, y_ptr, x (8 MemoryWriteCols), y and modulus (8 MemoryReadCols each),
+// IsZeroOperation (inverse, result), modulus_is_not_zero, FieldOpCols<U256Field> (result 32, carry 32,
+// witness low 63, witness high 63), FieldLtCols (byte flags 32, the compared bytes), is_real.  One thread
+// per row (the big-integer work is sequential): x y as 16 32-bit limbs, divided by the modulus (Knuth's
+// algorithm D), the vanishing polynomial x(X) y(X) - r(X) - c(X) m(X) over byte limbs divided by X - 256
+// (field_op.rs populate_with_modulus, util.rs compute_root_quotient_and_shift).
+enum { U2_SHARD = 0, U2_CLK = 1, U2_XPTR = 2, U2_YPTR = 3, U2_X = 4, U2_Y = U2_X + 8 * 13, U2_M = U2_Y + 8 * 9,
+       U2_IZINV = U2_M + 8 * 9, U2_IZRES = U2_IZINV + 1, U2_NZ = U2_IZRES + 1, U2_OUT = U2_NZ + 1, U2_LT = U2_OUT + 190,
+       U2_REAL = U2_LT + 34, U2_EV = 4 + 40 + 40 + 48, U2_NW = 63, U2_OFFSET = 1 << 14 };
+static_assert(U2_REAL + 1 == ZKM_UINT256_MUL_WIDTH, "Uint256MulCols layout");
+
+// u (m limbs) = q v + r, v (n limbs, v[n-1] != 0); q gets m - n + 1 limbs, r n limbs (Knuth D, base 2^32)
+__device__ inline void divmod_limbs(const uint32_t *u, int m, const uint32_t *v, int n, uint32_t *q, uint32_t *r) {
+    if (n == 1) {
+        uint64_t k = 0;
+        for (int j = m - 1; j >= 0; j--) {
+            const uint64_t t = (k << 32) | u[j];
+            q[j] = (uint32_t)(t / v[0]);
+            k = t - (uint64_t)q[j] * v[0];
+        }
+        r[0] = (uint32_t)k;
+        return;
+    }
+    uint32_t un[17], vn[8];
+    const int s = __clz(v[n - 1]);
+    for (int i = n - 1; i > 0; i--) vn[i] = (uint32_t)(((uint64_t)v[i] << s) | ((uint64_t)v[i - 1] >> (32 - s)));
+    vn[0] = v[0] << s;
+    un[m] = (uint32_t)((uint64_t)u[m - 1] >> (32 - s));
+    for (int i = m - 1; i > 0; i--) un[i] = (uint32_t)(((uint64_t)u[i] << s) | ((uint64_t)u[i - 1] >> (32 - s)));
+    un[0] = u[0] << s;
+    for (int j = m - n; j >= 0; j--) {
+        const uint64_t num = ((uint64_t)un[j + n] << 32) | un[j + n - 1];
+        uint64_t qhat = num / vn[n - 1], rhat = num - qhat * vn[n - 1];
+        while (qhat >> 32 || qhat * vn[n - 2] > ((rhat << 32) | un[j + n - 2])) {
+            qhat--;
+            rhat += vn[n - 1];
+            if (rhat >> 32) break;
+        }
+        int64_t t;
+        uint64_t k = 0;
+        for (int i = 0; i < n; i++) {  // un[j..j+n] -= qhat vn
+            const uint64_t p = qhat * vn[i];
+            t = (int64_t)un[i + j] - (int64_t)k - (int64_t)(p & 0xFFFFFFFFu);
+            un[i + j] = (uint32_t)t;
+            k = (p >> 32) - (uint64_t)(t >> 32);
+        }
+        t = (int64_t)un[j + n] - (int64_t)k;
+        un[j + n] = (uint32_t)t;
+        q[j] = (uint32_t)qhat;
+        if (t < 0) {  // qhat was one too large: add vn back
+            q[j]--;
+            uint64_t c = 0;
+            for (int i = 0; i < n; i++) {
+                const uint64_t w = (uint64_t)un[i + j] + vn[i] + c;
+                un[i + j] = (uint32_t)w;
+                c = w >> 32;
+            }
+            un[j + n] += (uint32_t)c;
+        }
+    }
+    for (int i = 0; i < n - 1; i++) r[i] = (uint32_t)(((uint64_t)un[i] >> s) | ((uint64_t)un[i + 1] << (32 - s)));
+    r[n - 1] = un[n - 1] >> s;
+}
+
+__device__ __forceinline__ void byte_add(uint32_t *bm, uint32_t op, uint32_t b, uint32_t c) {
+    if (bm) atomicAdd(bm + (((b << 8) | c) * BYTE_COLS + op), 1u);
+}
+
+__global__ __launch_bounds__(128) void k_uint256_rows(const uint32_t *__restrict__ ev, uint64_t n,
+                                                      uint32_t *__restrict__ out, uint64_t height, uint32_t *bm) {
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * ZKM_UINT256_MUL_WIDTH;
+    for (int c = 0; c < ZKM_UINT256_MUL_WIDTH; c++) v[c] = 0;
+    if (row >= n) {  // x = y = 0 mod 2^256: result, carry, vanishing 0; witness limbs = the offset
+        for (int k = 0; k < U2_NW; k++) v[U2_OUT + 64 + U2_NW + k] = U2_OFFSET >> 8;
+        return;
+    }
+    const uint32_t *e = ev + row * U2_EV;
+    const uint32_t shard = e[0], clk = e[1];
+    v[U2_SHARD] = shard;
+    v[U2_CLK] = clk;
+    v[U2_XPTR] = e[2];
+    v[U2_YPTR] = e[3];
+    v[U2_REAL] = 1;
+    uint32_t x[8], y[8], m[8];
+    for (int i = 0; i < 8; i++) {
+        const Access ya = access_read(e + 4 + 5 * i), ma = access_read(e + 44 + 5 * i), xa = access_write(e + 84 + 6 * i);
+        y[i] = ya.value;
+        m[i] = ma.value;
+        x[i] = xa.prev_value;
+        put_access(v, U2_Y + 9 * i, ya);
+        put_access(v, U2_M + 9 * i, ma);
+        put_word(v + U2_X + 13 * i, xa.prev_value);
+        put_access(v, U2_X + 13 * i + 4, xa);
+        const Access as[3] = {ya, ma, xa};
+        for (int k = 0; k < 3; k++) {
+            byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
+            byte_add(bm, B_U8RANGE, 0, as[k].d8);
+        }
+    }
+    // IsZeroOperation on the modulus's byte sum
+    uint32_t bsum = 0;
+    for (int i = 0; i < 32; i++) bsum += byte_of(m[i >> 2], i & 3);
+    const bool mz = bsum == 0;
+    v[U2_IZRES] = mz;
+    v[U2_NZ] = !mz;
+    v[U2_IZINV] = mz ? 0u : kb::from_mont(kb::inv(kb::to_mont(bsum)));
+    // x y = carry m + result (m = 2^256 when zero)
+    uint32_t prod[16];
+    for (int i = 0; i < 16; i++) prod[i] = 0;
+    for (int i = 0; i < 8; i++) {
+        uint64_t c = 0;
+        for (int j = 0; j < 8; j++) {
+            const uint64_t t = (uint64_t)x[i] * y[j] + prod[i + j] + c;
+            prod[i + j] = (uint32_t)t;
+            c = t >> 32;
+        }
+        prod[i + 8] = (uint32_t)c;
+    }
+    uint32_t res[8] = {0, 0, 0, 0, 0, 0, 0, 0}, car[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (mz) {
+        for (int i = 0; i < 8; i++) {
+            res[i] = prod[i];
+            car[i] = prod[8 + i];
+        }
+    } else {
+        int nm = 8;
+        while (m[nm - 1] == 0) nm--;
+        uint32_t q[16], r[8];
+        divmod_limbs(prod, 16, m, nm, q, r);
+        for (int i = 0; i < nm; i++) res[i] = r[i];
+        for (int i = 0; i < 8; i++) car[i] = q[i];  // below 2^256 for operands below the modulus
+    }
+    // vanishing polynomial over byte limbs, then its quotient by (X - 256) shifted by the offset
+    int64_t van[U2_NW + 1];
+    for (int k = 0; k <= U2_NW; k++) van[k] = 0;
+    for (int i = 0; i < 32; i++) {
+        const int64_t xi = byte_of(x[i >> 2], i & 3), ci = byte_of(car[i >> 2], i & 3);
+        for (int j = 0; j < 32; j++) van[i + j] += xi * (int64_t)byte_of(y[j >> 2], j & 3) - ci * (int64_t)byte_of(m[j >> 2], j & 3);
+        van[i] -= byte_of(res[i >> 2], i & 3);
+        if (mz) van[i + 32] -= ci;  // m(X) = X^32
+    }
+    int64_t qw = van[U2_NW];
+    uint32_t *W = v + U2_OUT + 64;
+    for (int k = U2_NW - 1; k >= 0; k--) {  // q_k = van_{k+1} + 256 q_{k+1}; column k = q_k + offset
+        const uint32_t w = (uint32_t)(qw + U2_OFFSET);
+        W[k] = w & 0xFF;
+        W[U2_NW + k] = w >> 8;
+        if (k) qw = van[k] + 256 * qw;
+    }
+    for (int i = 0; i < 32; i++) {
+        v[U2_OUT + i] = byte_of(res[i >> 2], i & 3);
+        v[U2_OUT + 32 + i] = byte_of(car[i >> 2], i & 3);
+    }
+    // add_u8_range_checks_field of result, carry, witness low, witness high (pairs; a trailing single with 0)
+    for (int blk = 0; blk < 4; blk++) {
+        const uint32_t *c = v + U2_OUT + (blk < 2 ? 32 * blk : 64 + U2_NW * (blk - 2));
+        const int len = blk < 2 ? 32 : U2_NW;
+        for (int j = 0; j + 1 < len; j += 2) byte_add(bm, B_U8RANGE, c[j], c[j + 1]);
+        if (len & 1) byte_add(bm, B_U8RANGE, c[len - 1], 0);
+    }
+    // FieldLtCols: result < m at its most significant differing byte (only when m != 0)
+    if (!mz) {
+        for (int k = 31; k >= 0; k--) {
+            const uint32_t a = byte_of(res[k >> 2], k & 3), b = byte_of(m[k >> 2], k & 3);
+            if (a < b) {
+                v[U2_LT + k] = 1;
+                v[U2_LT + 32] = a;
+                v[U2_LT + 33] = b;
+                break;
+            }
+        }
+        byte_add(bm, B_LTU, v[U2_LT + 32], v[U2_LT + 33]);
+    }
+}
+
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
 // SysLinuxCols (sys_linux/columns.rs); zkm_sys_linux_event dwords: shard, clk, code, a0, a1, result, the A3
 // write, the io record
@@ -1948,6 +2126,23 @@ int zkm_sha_extend_events_to_trace(const zkm_sha_extend_row *rows, uint64_t n, u
     }
     return launch<29, 29, ZKM_SHA_EXTEND_WIDTH, true>(rows, n, trace, height, chip, stream,
                                                       "zkm_sha_extend_events_to_trace", byte_mult);
+}
+
+int zkm_uint256_mul_events_to_trace(const zkm_uint256_mul_event *events, uint64_t n, uint32_t *trace,
+                                    uint64_t height, uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_uint256_mul_event) == 4 * U2_EV, "Uint256MulEvent record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1))) {
+        g_last_error = "zkm_uint256_mul_events_to_trace: bad arguments (need n <= height, a power of two >= 16)";
+        return ZKM_ERR_ARG;
+    }
+    hipLaunchKernelGGL(k_uint256_rows, dim3((unsigned)((height + 127) / 128)), dim3(128), 0, (hipStream_t)stream,
+                       (const uint32_t *)events, n, trace, height, byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_uint256_mul_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
 }
 
 int zkm_sys_linux_events_to_trace(const zkm_sys_linux_event *events, uint64_t n, uint32_t *trace, uint64_t height,

@@ -320,6 +320,40 @@ def sha_extend_records(events) -> np.ndarray:
     return out
 
 
+UINT256_MUL_EVENT = np.dtype({"names": ["shard", "clk", "x_ptr", "y_ptr", "y", "modulus", "x"],
+                              "formats": [u4, u4, u4, u4, (u4, (8, 5)), (u4, (8, 5)), (u4, (8, 6))],
+                              "offsets": [0, 4, 8, 12, 16, 176, 336], "itemsize": 528})
+UINT256_MUL_WIDTH = 480  # ZKM_UINT256_MUL_WIDTH
+
+
+def uint256_mul_records(events) -> np.ndarray:
+    """zkm_uint256_mul_event records of the executor's UINT256_MUL events (mips_ec.exec_uint256_mul): y and
+    the modulus read at clk, x written at clk + 1."""
+    out = np.zeros(len(events), UINT256_MUL_EVENT)
+    for k, e in enumerate(events):
+        sh, clk = e["shard"], e["clk"]
+        r = out[k]
+        r["shard"], r["clk"], r["x_ptr"], r["y_ptr"] = sh, clk, e["x_ptr"], e["y_ptr"]
+        for key, name in (("y", "y"), ("m", "modulus")):
+            rd = np.asarray(e[key], np.int64).reshape(8, 3)  # value, prev_shard, prev_clk
+            r[name] = np.stack([rd[:, 0], np.full(8, sh), np.full(8, clk), rd[:, 1], rd[:, 2]], 1)
+        wr = np.asarray(e["xw"], np.int64).reshape(8, 4)  # prev_value, value, prev_shard, prev_clk
+        r["x"] = np.stack([wr[:, 1], np.full(8, sh), np.full(8, clk + 1), wr[:, 0], wr[:, 2], wr[:, 3]], 1)
+    return out
+
+
+def uint256_mul_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    """Uint256MulMod main trace (height x 480 int32, on the GPU) from n zkm_uint256_mul_event records; the
+    Byte lookups added into byte_mult (nullable)."""
+    height = height or _pow2(n)
+    t = _trace(height, UINT256_MUL_WIDTH)
+    what = "zkm_uint256_mul_events_to_trace"
+    _lib.check(_bind().zkm_uint256_mul_events_to_trace(_records(events_dev, n, UINT256_MUL_EVENT, what), n,
+                                                       t.data_ptr(), height, _words(byte_mult, 65536 * 10, what),
+                                                       _stream()), what)
+    return t
+
+
 SYS_LINUX_EVENT = np.dtype({"names": ["shard", "clk", "code", "a0", "a1", "result", "a3", "io"],
                             "formats": [u4, u4, u4, u4, u4, u4, (u4, 6), (u4, 6)],
                             "offsets": [0, 4, 8, 12, 16, 20, 24, 48], "itemsize": 72})
@@ -457,6 +491,7 @@ def _bind():
         L.zkm_sha_compress_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_poseidon2_permute_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_sys_linux_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_uint256_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -482,7 +517,7 @@ def to_device(records: np.ndarray):
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
                              SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
                              COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT, POSEIDON2_PERMUTE_EVENT,
-                             SYS_LINUX_EVENT):
+                             SYS_LINUX_EVENT, UINT256_MUL_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -830,10 +865,12 @@ def recursion_instrs_trace(chip: str, records_dev, n: int, height: int, montgome
 
 
 def precompile_shard_traces(code: int, events, byte_mult=None):
-    """Device traces of a SHA, Poseidon2 or Linux-syscall precompile shard (mips_core.precompile_shard's chips
-    for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    """Device traces of a SHA, Poseidon2, Uint256MulMod or Linux-syscall precompile shard
+    (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE / UINT256_MUL / the
+    Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
+    from . import mips_ec as EC
     from . import mips_memory as MM
     from . import mips_p2permute as P2P
     from . import mips_syscall as SY
@@ -846,6 +883,9 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     elif code == SY.SHA_COMPRESS:
         rec = sha_compress_records(pevs)
         out["ShaCompress"] = sha_compress_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    elif code == EC.UINT256_MUL:
+        rec = uint256_mul_records(pevs)
+        out["Uint256MulMod"] = uint256_mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     elif code == SY.SYS_LINUX:
         rec = sys_linux_records(pevs)
         out["SysLinux"] = sys_linux_trace(to_device(rec), len(rec), byte_mult=byte_mult)
