@@ -259,6 +259,21 @@ typedef struct {
 int zkm_uint256_mul_events_to_trace(const zkm_uint256_mul_event *events, uint64_t n, uint32_t *trace,
                                     uint64_t height, uint32_t *byte_mult, void *stream);
 
+/* U256XU2048Mul (syscall/precompiles/u256x2048_mul/air.rs:109-213): U256xU2048MulEvent as one fixed record:
+ * shard, clk, a_ptr, b_ptr, lo_ptr, hi_ptr, the A2 / A3 register reads, the 8 reads of a and 64 of b (at
+ * clk), the 64 writes of lo and 8 of hi (at clk + 1).  Each row: the accesses and the eight FieldOpCols
+ * mul-and-carry operations a b_k + carry = lo_k + carry' 2^256 (field_op.rs populate_mul_and_carry); padding
+ * rows hold them for zeros.  byte_mult (nullable): the limbs' U8 and the accesses' range checks.  3129
+ * columns. */
+typedef struct {
+    uint32_t shard, clk, a_ptr, b_ptr, lo_ptr, hi_ptr;
+    zkm_memory_read_record lo_ptr_reg, hi_ptr_reg, a[8], b[64];
+    zkm_memory_write_record lo[64], hi[8];
+} zkm_u256x2048_mul_event;  /* 3232 bytes */
+#define ZKM_U256XU2048_MUL_WIDTH 3129
+int zkm_u256x2048_mul_events_to_trace(const zkm_u256x2048_mul_event *events, uint64_t n, uint32_t *trace,
+                                      uint64_t height, uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

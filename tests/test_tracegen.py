@@ -591,6 +591,72 @@ def test_uint256_mul_shard_from_device_traces():
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 
+def _u256x2048_events(seed: int = 13):
+    """U256XU2048_MUL calls through the executor (mips_ec.exec_u256x2048_mul): random a and b, all-ones
+    operands (every carry at its largest), zeros, over two shards."""
+    from zkmips_amd import emulated_field as EF
+    from zkmips_amd import mips_ec as EC
+    rng = np.random.default_rng(seed)
+    words = {}
+    regs = [0] * MC.NUM_REGS
+    last = [(1, r) for r in range(MC.NUM_REGS)]
+    reg_start, reg_done = [(last[r], regs[r]) for r in range(MC.NUM_REGS)], []
+    mem, mem_init, mem_last = {}, {}, {}
+    ops = [(int.from_bytes(rng.bytes(32), "little"), int.from_bytes(rng.bytes(256), "little")) for _ in range(7)]
+    ops += [((1 << 256) - 1, (1 << 2048) - 1), (0, 0), (1, (1 << 2048) - 1)]
+    evs = []
+    for k, (a, b) in enumerate(ops * 2):
+        ap, bp, lo, hi = 0x10000 + 0x1000 * k, 0x10100 + 0x1000 * k, 0x10200 + 0x1000 * k, 0x10400 + 0x1000 * k
+        for i, w in enumerate(EF.int_to_words(a, 8)):
+            words[ap + 4 * i] = w
+        for i, w in enumerate(EF.int_to_words(b, 64)):
+            words[bp + 4 * i] = w
+        regs[SY.REG_A2], regs[SY.REG_A3] = lo, hi
+        shard, clk = 3 + k // 10, 60 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda x: words.get(x, 0), regs, last,
+                                 reg_start, reg_done)
+        evs.append((EC.U256XU2048_MUL, (shard, clk, SY.syscall_id(EC.U256XU2048_MUL), ap, bp),
+                    EC.exec_u256x2048_mul(pm, shard, clk, ap, bp)))
+    return evs
+
+
+def test_u256x2048_mul_records_layout():
+    """zkm_u256x2048_mul_event records: registers, a, b read at clk, lo and hi written at clk + 1."""
+    evs = _u256x2048_events()
+    rec = TG.u256x2048_mul_records([e for _, _, e in evs])
+    assert rec.dtype.itemsize == 3232
+    for r, (_, _, e) in zip(rec, evs):
+        assert r["lo_ptr_reg"][0] == e["lo_ptr"] and r["hi_ptr_reg"][0] == e["hi_ptr"]
+        assert list(r["b"][:, 0]) == [v[0] for v in e["b"]] and list(r["hi"][:, 0]) == [v[1] for v in e["hi"]]
+        assert (r["lo"][:, 2] == e["clk"] + 1).all()
+
+
+@pytest.mark.gpu
+def test_u256x2048_mul_shard_from_device_traces():
+    """A U256XU2048_MUL precompile shard built on the device (the eight chained mul-and-carry field ops)
+    equals the host builders' traces and multiplicities and proves to the same bytes."""
+    import torch
+    from zkmips_amd import mips_ec as EC
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _u256x2048_events()
+    m, prep, tr, pv = MC.precompile_shard(EC.U256XU2048_MUL, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(EC.U256XU2048_MUL, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert "U256XU2048Mul" in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

@@ -1426,6 +1426,45 @@ __device__ __forceinline__ void byte_add(uint32_t *bm, uint32_t op, uint32_t b, 
     if (bm) atomicAdd(bm + (((b << 8) | c) * BYTE_COLS + op), 1u);
 }
 
+// FieldOpCols<U256Field> at o for a b + c = res + car M (c nullable; M = the byte limbs of m, or X^32 for
+// 2^256 when m is null): result and carry bytes, the witness limbs of the vanishing polynomial
+// a(X) b(X) + c(X) - res(X) - car(X) M(X) divided by X - 256 and shifted by the offset (field_op.rs
+// populate_with_modulus / populate_mul_and_carry, util.rs compute_root_quotient_and_shift), and the U8
+// range checks of the four limb groups (pairs, a trailing single with 0) into bm (nullable)
+__device__ inline void u256_field_op(uint32_t *o, const uint32_t a[8], const uint32_t b[8], const uint32_t *c,
+                                     const uint32_t res[8], const uint32_t car[8], const uint32_t *m, uint32_t *bm) {
+    int64_t van[U2_NW + 1];
+    for (int k = 0; k <= U2_NW; k++) van[k] = 0;
+    for (int i = 0; i < 32; i++) {
+        const int64_t ai = byte_of(a[i >> 2], i & 3), ci = byte_of(car[i >> 2], i & 3);
+        for (int j = 0; j < 32; j++) {
+            van[i + j] += ai * (int64_t)byte_of(b[j >> 2], j & 3);
+            if (m) van[i + j] -= ci * (int64_t)byte_of(m[j >> 2], j & 3);
+        }
+        van[i] -= byte_of(res[i >> 2], i & 3);
+        if (c) van[i] += byte_of(c[i >> 2], i & 3);
+        if (!m) van[i + 32] -= ci;  // M(X) = X^32
+    }
+    int64_t qw = van[U2_NW];
+    uint32_t *W = o + 64;
+    for (int k = U2_NW - 1; k >= 0; k--) {  // q_k = van_{k+1} + 256 q_{k+1}; column k = q_k + offset
+        const uint32_t w = (uint32_t)(qw + U2_OFFSET);
+        W[k] = w & 0xFF;
+        W[U2_NW + k] = w >> 8;
+        if (k) qw = van[k] + 256 * qw;
+    }
+    for (int i = 0; i < 32; i++) {
+        o[i] = byte_of(res[i >> 2], i & 3);
+        o[32 + i] = byte_of(car[i >> 2], i & 3);
+    }
+    for (int blk = 0; blk < 4; blk++) {
+        const uint32_t *g = o + (blk < 2 ? 32 * blk : 64 + U2_NW * (blk - 2));
+        const int len = blk < 2 ? 32 : U2_NW;
+        for (int j = 0; j + 1 < len; j += 2) byte_add(bm, B_U8RANGE, g[j], g[j + 1]);
+        if (len & 1) byte_add(bm, B_U8RANGE, g[len - 1], 0);
+    }
+}
+
 __global__ __launch_bounds__(128) void k_uint256_rows(const uint32_t *__restrict__ ev, uint64_t n,
                                                       uint32_t *__restrict__ out, uint64_t height, uint32_t *bm) {
     const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
@@ -1492,34 +1531,7 @@ __global__ __launch_bounds__(128) void k_uint256_rows(const uint32_t *__restrict
         for (int i = 0; i < nm; i++) res[i] = r[i];
         for (int i = 0; i < 8; i++) car[i] = q[i];  // below 2^256 for operands below the modulus
     }
-    // vanishing polynomial over byte limbs, then its quotient by (X - 256) shifted by the offset
-    int64_t van[U2_NW + 1];
-    for (int k = 0; k <= U2_NW; k++) van[k] = 0;
-    for (int i = 0; i < 32; i++) {
-        const int64_t xi = byte_of(x[i >> 2], i & 3), ci = byte_of(car[i >> 2], i & 3);
-        for (int j = 0; j < 32; j++) van[i + j] += xi * (int64_t)byte_of(y[j >> 2], j & 3) - ci * (int64_t)byte_of(m[j >> 2], j & 3);
-        van[i] -= byte_of(res[i >> 2], i & 3);
-        if (mz) van[i + 32] -= ci;  // m(X) = X^32
-    }
-    int64_t qw = van[U2_NW];
-    uint32_t *W = v + U2_OUT + 64;
-    for (int k = U2_NW - 1; k >= 0; k--) {  // q_k = van_{k+1} + 256 q_{k+1}; column k = q_k + offset
-        const uint32_t w = (uint32_t)(qw + U2_OFFSET);
-        W[k] = w & 0xFF;
-        W[U2_NW + k] = w >> 8;
-        if (k) qw = van[k] + 256 * qw;
-    }
-    for (int i = 0; i < 32; i++) {
-        v[U2_OUT + i] = byte_of(res[i >> 2], i & 3);
-        v[U2_OUT + 32 + i] = byte_of(car[i >> 2], i & 3);
-    }
-    // add_u8_range_checks_field of result, carry, witness low, witness high (pairs; a trailing single with 0)
-    for (int blk = 0; blk < 4; blk++) {
-        const uint32_t *c = v + U2_OUT + (blk < 2 ? 32 * blk : 64 + U2_NW * (blk - 2));
-        const int len = blk < 2 ? 32 : U2_NW;
-        for (int j = 0; j + 1 < len; j += 2) byte_add(bm, B_U8RANGE, c[j], c[j + 1]);
-        if (len & 1) byte_add(bm, B_U8RANGE, c[len - 1], 0);
-    }
+    u256_field_op(v + U2_OUT, x, y, nullptr, res, car, mz ? nullptr : m, bm);
     // FieldLtCols: result < m at its most significant differing byte (only when m != 0)
     if (!mz) {
         for (int k = 31; k >= 0; k--) {
@@ -1532,6 +1544,73 @@ __global__ __launch_bounds__(128) void k_uint256_rows(const uint32_t *__restrict
             }
         }
         byte_add(bm, B_LTU, v[U2_LT + 32], v[U2_LT + 33]);
+    }
+}
+
+// ------------------------------------------------------------------ U256XU2048Mul (u256x2048_mul/air.rs:109-213)
+// U256x2048MulCols: shard, clk, a_ptr, b_ptr, lo_ptr, hi_ptr, the A2 / A3 register reads, a (8 reads), b (64
+// reads), lo (64 writes), hi (8 writes), eight FieldOpCols (a b_k + carry_{k-1} = lo_k + carry_k 2^256), is_real.
+enum { UX_APTR = 2, UX_BPTR = 3, UX_LOPTR = 4, UX_HIPTR = 5, UX_LOREG = 6, UX_HIREG = 15, UX_A = 24, UX_B = UX_A + 8 * 9,
+       UX_LO = UX_B + 64 * 9, UX_HI = UX_LO + 64 * 13, UX_OUT = UX_HI + 8 * 13, UX_REAL = UX_OUT + 8 * 190,
+       UX_EV = 6 + 10 + 40 + 320 + 384 + 48 };
+static_assert(UX_REAL + 1 == ZKM_U256XU2048_MUL_WIDTH, "U256x2048MulCols layout");
+
+__global__ __launch_bounds__(128) void k_u256x2048_rows(const uint32_t *__restrict__ ev, uint64_t n,
+                                                        uint32_t *__restrict__ out, uint64_t height, uint32_t *bm) {
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * ZKM_U256XU2048_MUL_WIDTH;
+    for (int c = 0; c < ZKM_U256XU2048_MUL_WIDTH; c++) v[c] = 0;
+    if (row >= n) {  // eight mul-and-carry operations of zeros: witness limbs = the offset
+        for (int k = 0; k < 8; k++)
+            for (int j = 0; j < U2_NW; j++) v[UX_OUT + 190 * k + 64 + U2_NW + j] = U2_OFFSET >> 8;
+        return;
+    }
+    const uint32_t *e = ev + row * UX_EV;
+    for (int i = 0; i < 6; i++) v[i] = e[i];
+    v[UX_REAL] = 1;
+    auto acc = [&](int col, const Access &a) {
+        put_access(v, col, a);
+        byte_add(bm, B_U16RANGE, a.d16 >> 8, a.d16 & 0xFF);
+        byte_add(bm, B_U8RANGE, 0, a.d8);
+    };
+    acc(UX_LOREG, access_read(e + 6));
+    acc(UX_HIREG, access_read(e + 11));
+    uint32_t a[8];
+    for (int i = 0; i < 8; i++) {
+        const Access r = access_read(e + 16 + 5 * i);
+        a[i] = r.value;
+        acc(UX_A + 9 * i, r);
+    }
+    for (int i = 0; i < 64; i++) acc(UX_B + 9 * i, access_read(e + 56 + 5 * i));
+    for (int i = 0; i < 72; i++) {
+        const Access w = access_write(e + 376 + 6 * i);
+        const int col = i < 64 ? UX_LO + 13 * i : UX_HI + 13 * (i - 64);
+        put_word(v + col, w.prev_value);
+        acc(col + 4, w);
+    }
+    uint32_t carry[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < 8; k++) {
+        uint32_t b[8], p[16];
+        for (int i = 0; i < 8; i++) b[i] = e[56 + 5 * (8 * k + i)];
+        for (int i = 0; i < 16; i++) p[i] = i < 8 ? carry[i] : 0u;  // a b_k + carry
+        for (int i = 0; i < 8; i++) {
+            uint64_t c = 0;
+            for (int j = 0; j < 8; j++) {
+                const uint64_t t = (uint64_t)a[i] * b[j] + p[i + j] + c;
+                p[i + j] = (uint32_t)t;
+                c = t >> 32;
+            }
+            for (int j = i + 8; c && j < 16; j++) {
+                const uint64_t t = (uint64_t)p[j] + c;
+                p[j] = (uint32_t)t;
+                c = t >> 32;
+            }
+        }
+        uint32_t prev[8];
+        for (int i = 0; i < 8; i++) prev[i] = carry[i];
+        u256_field_op(v + UX_OUT + 190 * k, a, b, prev, p, p + 8, nullptr, bm);
+        for (int i = 0; i < 8; i++) carry[i] = p[8 + i];
     }
 }
 
@@ -2140,6 +2219,23 @@ int zkm_uint256_mul_events_to_trace(const zkm_uint256_mul_event *events, uint64_
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_uint256_mul_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_u256x2048_mul_events_to_trace(const zkm_u256x2048_mul_event *events, uint64_t n, uint32_t *trace,
+                                      uint64_t height, uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_u256x2048_mul_event) == 4 * UX_EV, "U256xU2048MulEvent record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1))) {
+        g_last_error = "zkm_u256x2048_mul_events_to_trace: bad arguments (need n <= height, a power of two >= 16)";
+        return ZKM_ERR_ARG;
+    }
+    hipLaunchKernelGGL(k_u256x2048_rows, dim3((unsigned)((height + 127) / 128)), dim3(128), 0, (hipStream_t)stream,
+                       (const uint32_t *)events, n, trace, height, byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_u256x2048_mul_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;

@@ -354,6 +354,49 @@ def uint256_mul_trace(events_dev, n: int, height: int = None, byte_mult=None):
     return t
 
 
+U256X2048_MUL_EVENT = np.dtype({"names": ["shard", "clk", "a_ptr", "b_ptr", "lo_ptr", "hi_ptr", "lo_ptr_reg", "hi_ptr_reg",
+                                         "a", "b", "lo", "hi"],
+                                "formats": [u4] * 6 + [(u4, 5), (u4, 5), (u4, (8, 5)), (u4, (64, 5)), (u4, (64, 6)),
+                                                       (u4, (8, 6))],
+                                "offsets": [0, 4, 8, 12, 16, 20, 24, 44, 64, 224, 1504, 3040], "itemsize": 3232})
+U256X2048_MUL_WIDTH = 3129  # ZKM_U256XU2048_MUL_WIDTH
+
+
+def u256x2048_mul_records(events) -> np.ndarray:
+    """zkm_u256x2048_mul_event records of the executor's U256XU2048_MUL events (mips_ec.exec_u256x2048_mul):
+    the registers, a and b read at clk, lo and hi written at clk + 1."""
+    out = np.zeros(len(events), U256X2048_MUL_EVENT)
+
+    def reads(recs, sh, clk):
+        rd = np.asarray(recs, np.int64).reshape(-1, 3)  # value, prev_shard, prev_clk
+        return np.stack([rd[:, 0], np.full(len(rd), sh), np.full(len(rd), clk), rd[:, 1], rd[:, 2]], 1)
+
+    def writes(recs, sh, clk):
+        wr = np.asarray(recs, np.int64).reshape(-1, 4)  # prev_value, value, prev_shard, prev_clk
+        return np.stack([wr[:, 1], np.full(len(wr), sh), np.full(len(wr), clk), wr[:, 0], wr[:, 2], wr[:, 3]], 1)
+    for k, e in enumerate(events):
+        sh, clk = e["shard"], e["clk"]
+        r = out[k]
+        for f in ("shard", "clk", "a_ptr", "b_ptr", "lo_ptr", "hi_ptr"):
+            r[f] = e[f]
+        r["lo_ptr_reg"], r["hi_ptr_reg"] = reads([e["lo_reg"]], sh, clk)[0], reads([e["hi_reg"]], sh, clk)[0]
+        r["a"], r["b"] = reads(e["a"], sh, clk), reads(e["b"], sh, clk)
+        r["lo"], r["hi"] = writes(e["lo"], sh, clk + 1), writes(e["hi"], sh, clk + 1)
+    return out
+
+
+def u256x2048_mul_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    """U256XU2048Mul main trace (height x 3129 int32, on the GPU) from n zkm_u256x2048_mul_event records; the
+    Byte lookups added into byte_mult (nullable)."""
+    height = height or _pow2(n)
+    t = _trace(height, U256X2048_MUL_WIDTH)
+    what = "zkm_u256x2048_mul_events_to_trace"
+    _lib.check(_bind().zkm_u256x2048_mul_events_to_trace(_records(events_dev, n, U256X2048_MUL_EVENT, what), n,
+                                                         t.data_ptr(), height, _words(byte_mult, 65536 * 10, what),
+                                                         _stream()), what)
+    return t
+
+
 SYS_LINUX_EVENT = np.dtype({"names": ["shard", "clk", "code", "a0", "a1", "result", "a3", "io"],
                             "formats": [u4, u4, u4, u4, u4, u4, (u4, 6), (u4, 6)],
                             "offsets": [0, 4, 8, 12, 16, 20, 24, 48], "itemsize": 72})
@@ -492,6 +535,7 @@ def _bind():
         L.zkm_poseidon2_permute_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_sys_linux_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_uint256_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_u256x2048_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -517,7 +561,7 @@ def to_device(records: np.ndarray):
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
                              SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
                              COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT, POSEIDON2_PERMUTE_EVENT,
-                             SYS_LINUX_EVENT, UINT256_MUL_EVENT):
+                             SYS_LINUX_EVENT, UINT256_MUL_EVENT, U256X2048_MUL_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -865,9 +909,9 @@ def recursion_instrs_trace(chip: str, records_dev, n: int, height: int, montgome
 
 
 def precompile_shard_traces(code: int, events, byte_mult=None):
-    """Device traces of a SHA, Poseidon2, Uint256MulMod or Linux-syscall precompile shard
-    (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE / UINT256_MUL / the
-    Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    """Device traces of a SHA, Poseidon2, 256-bit multiplication or Linux-syscall precompile shard
+    (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE / UINT256_MUL /
+    U256XU2048_MUL / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
     from . import mips_ec as EC
@@ -886,6 +930,9 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     elif code == EC.UINT256_MUL:
         rec = uint256_mul_records(pevs)
         out["Uint256MulMod"] = uint256_mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    elif code == EC.U256XU2048_MUL:
+        rec = u256x2048_mul_records(pevs)
+        out["U256XU2048Mul"] = u256x2048_mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     elif code == SY.SYS_LINUX:
         rec = sys_linux_records(pevs)
         out["SysLinux"] = sys_linux_trace(to_device(rec), len(rec), byte_mult=byte_mult)
