@@ -274,6 +274,24 @@ typedef struct {
 int zkm_u256x2048_mul_events_to_trace(const zkm_u256x2048_mul_event *events, uint64_t n, uint32_t *trace,
                                       uint64_t height, uint32_t *byte_mult, void *stream);
 
+/* FpOpAssign of the bn254 / bls12-381 base fields (syscall/precompiles/fptower/fp.rs:90-160): FpOpEvent as
+ * one fixed record: shard, clk, x_ptr, y_ptr, op (0 add, 1 sub, 2 mul), the reads of y (at clk) and the
+ * writes of x (at clk + 1) -- 8 words each for bn254, 12 for bls12-381, in slots of 12.  Each row: op flags,
+ * the accesses, FieldOpCols of x op y mod p (sub populated as r + y, field_op.rs populate_with_modulus);
+ * padding rows are 0 + 0.  byte_mult (nullable): the limbs' U8 and the accesses' range checks.  372 (bn254)
+ * or 556 (bls12-381) columns. */
+#define ZKM_FIELD_BN254 0
+#define ZKM_FIELD_BLS12381 1
+typedef struct {
+    uint32_t shard, clk, x_ptr, y_ptr, op;
+    zkm_memory_read_record y[12];
+    zkm_memory_write_record x[12];
+} zkm_fp_op_event;  /* 548 bytes */
+#define ZKM_FP_OP_WIDTH_BN254 372
+#define ZKM_FP_OP_WIDTH_BLS12381 556
+int zkm_fp_op_events_to_trace(int field, const zkm_fp_op_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                              uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

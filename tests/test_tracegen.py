@@ -657,6 +657,74 @@ def test_u256x2048_mul_shard_from_device_traces():
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 
+def _fp_op_events(field: str, seed: int = 17):
+    """FpOp calls of one field through the executor (mips_ec.exec_fp_op): add, sub, mul on random words
+    (operands at or above the modulus included, reduced by the call), zeros and p - 1."""
+    from zkmips_amd import emulated_field as EF
+    from zkmips_amd import mips_ec as EC
+    rng = np.random.default_rng(seed)
+    fp = EC.FIELDS[field]
+    words = {}
+    mem, mem_init, mem_last = {}, {}, {}
+    vals = [int.from_bytes(rng.bytes(fp.nl), "little") for _ in range(10)] + [0, fp.modulus - 1, fp.modulus]
+    evs = []
+    for k in range(2 * len(vals)):
+        op = ("add", "sub", "mul")[k % 3]
+        x, y = vals[k % len(vals)], vals[(3 * k + 1) % len(vals)]
+        xp, yp = 0x20000 + 0x100 * k, 0x30000 + 0x100 * k
+        for i, w in enumerate(EF.int_to_words(x, fp.words)):
+            words[xp + 4 * i] = w
+        for i, w in enumerate(EF.int_to_words(y, fp.words)):
+            words[yp + 4 * i] = w
+        shard, clk = 3 + k // 12, 70 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: words.get(a, 0))
+        code = EC.FP_OPS[field][("add", "sub", "mul").index(op)]
+        evs.append((EC.FP_OPS[field][0], (shard, clk, SY.syscall_id(code), xp, yp),
+                    EC.exec_fp_op(field, op, pm, shard, clk, xp, yp)))
+    return evs
+
+
+@pytest.mark.parametrize("field", ["Bn254", "Bls12381"])
+def test_fp_op_records_layout(field):
+    """zkm_fp_op_event records: the op code, y read at clk, x written at clk + 1, in slots of 12 words."""
+    evs = _fp_op_events(field)
+    rec = TG.fp_op_records([e for _, _, e in evs])
+    assert rec.dtype.itemsize == 548
+    w = 8 if field == "Bn254" else 12
+    for r, (_, _, e) in zip(rec, evs):
+        assert r["op"] == ("add", "sub", "mul").index(e["op"])
+        assert list(r["x"][:w, 3]) == e["x"] and (r["x"][:w, 2] == e["clk"] + 1).all() and not r["x"][w:].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field", ["Bn254", "Bls12381"])
+def test_fp_op_shard_from_device_traces(field):
+    """A base-field FpOp precompile shard built on the device (operands reduced, the sum / difference /
+    product divided by the modulus, the field op's witness) equals the host builders' traces and
+    multiplicities and proves to the same bytes."""
+    import torch
+    from zkmips_amd import mips_ec as EC
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _fp_op_events(field)
+    key = EC.FP_OPS[field][0]
+    m, prep, tr, pv = MC.precompile_shard(key, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(key, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert EC.FP_NAME[field] in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

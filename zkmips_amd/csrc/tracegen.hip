@@ -1614,6 +1614,218 @@ __global__ __launch_bounds__(128) void k_u256x2048_rows(const uint32_t *__restri
     }
 }
 
+// ------------------------------------------------------------------ FpOpAssign (fptower/fp.rs:90-160)
+// Generic emulated-field pieces over NL-byte limbs (bn254: 32, bls12-381: 48): big integers as 32-bit words.
+// u (MU words) = q v + r with v of NV words, the top one nonzero (Knuth D; q MU - NV + 1 words, r NV words)
+template <int MU, int NVMAX>
+__device__ inline void divmod_words(const uint32_t *u, const uint32_t *v, int nv, uint32_t *q, uint32_t *r) {
+    if (nv == 1) {
+        uint64_t k = 0;
+        for (int j = MU - 1; j >= 0; j--) {
+            const uint64_t t = (k << 32) | u[j];
+            q[j] = (uint32_t)(t / v[0]);
+            k = t - (uint64_t)q[j] * v[0];
+        }
+        r[0] = (uint32_t)k;
+        return;
+    }
+    uint32_t un[MU + 1], vn[NVMAX];
+    const int s = __clz(v[nv - 1]);
+    for (int i = nv - 1; i > 0; i--) vn[i] = (uint32_t)(((uint64_t)v[i] << s) | ((uint64_t)v[i - 1] >> (32 - s)));
+    vn[0] = v[0] << s;
+    un[MU] = (uint32_t)((uint64_t)u[MU - 1] >> (32 - s));
+    for (int i = MU - 1; i > 0; i--) un[i] = (uint32_t)(((uint64_t)u[i] << s) | ((uint64_t)u[i - 1] >> (32 - s)));
+    un[0] = u[0] << s;
+    for (int j = MU - nv; j >= 0; j--) {
+        const uint64_t num = ((uint64_t)un[j + nv] << 32) | un[j + nv - 1];
+        uint64_t qhat = num / vn[nv - 1], rhat = num - qhat * vn[nv - 1];
+        while (qhat >> 32 || qhat * vn[nv - 2] > ((rhat << 32) | un[j + nv - 2])) {
+            qhat--;
+            rhat += vn[nv - 1];
+            if (rhat >> 32) break;
+        }
+        int64_t t;
+        uint64_t k = 0;
+        for (int i = 0; i < nv; i++) {
+            const uint64_t p = qhat * vn[i];
+            t = (int64_t)un[i + j] - (int64_t)k - (int64_t)(p & 0xFFFFFFFFu);
+            un[i + j] = (uint32_t)t;
+            k = (p >> 32) - (uint64_t)(t >> 32);
+        }
+        t = (int64_t)un[j + nv] - (int64_t)k;
+        un[j + nv] = (uint32_t)t;
+        q[j] = (uint32_t)qhat;
+        if (t < 0) {
+            q[j]--;
+            uint64_t c = 0;
+            for (int i = 0; i < nv; i++) {
+                const uint64_t w = (uint64_t)un[i + j] + vn[i] + c;
+                un[i + j] = (uint32_t)w;
+                c = w >> 32;
+            }
+            un[j + nv] += (uint32_t)c;
+        }
+    }
+    for (int i = 0; i < nv - 1; i++) r[i] = (uint32_t)(((uint64_t)un[i] >> s) | ((uint64_t)un[i + 1] << (32 - s)));
+    r[nv - 1] = un[nv - 1] >> s;
+}
+
+// x (NX words) mod m (W words, canonical modulus): r (W words), q (NX - nv + 1 words, may be null)
+template <int NX, int W>
+__device__ inline void mod_words(const uint32_t *x, const uint32_t *m, uint32_t *r, uint32_t *qout) {
+    int nv = W;
+    while (m[nv - 1] == 0) nv--;
+    uint32_t q[NX], rr[W];
+    for (int i = 0; i < W; i++) rr[i] = 0;
+    divmod_words<NX, W>(x, m, nv, q, rr);
+    for (int i = 0; i < W; i++) r[i] = rr[i];
+    if (qout)
+        for (int i = 0; i < NX - nv + 1 && i < W; i++) qout[i] = q[i];
+}
+
+// FieldOpCols<NL bytes, NW witness limbs> at o: result `res_col`, carry, and the witness of the vanishing
+// polynomial of a (op) b + c - mres - carry m, op = mul or add (field_op.rs populate_with_modulus: sub and div
+// are populated as additions / products of the result); U8 range checks into bm
+template <int NL, int NW, int OFF>
+__device__ inline void field_op_cols(uint32_t *o, const uint32_t *a, const uint32_t *b, bool mul, const uint32_t *res_col,
+                                     const uint32_t *mres, const uint32_t *car, const uint32_t *m, uint32_t *bm) {
+    int64_t van[NW + 1];
+    for (int k = 0; k <= NW; k++) van[k] = 0;
+    for (int i = 0; i < NL; i++) {
+        const int64_t ai = byte_of(a[i >> 2], i & 3), ci = byte_of(car[i >> 2], i & 3);
+        if (mul) {
+            for (int j = 0; j < NL; j++) van[i + j] += ai * (int64_t)byte_of(b[j >> 2], j & 3);
+        } else {
+            van[i] += ai + (int64_t)byte_of(b[i >> 2], i & 3);
+        }
+        for (int j = 0; j < NL; j++) van[i + j] -= ci * (int64_t)byte_of(m[j >> 2], j & 3);
+        van[i] -= byte_of(mres[i >> 2], i & 3);
+    }
+    int64_t qw = van[NW];
+    uint32_t *Wc = o + 2 * NL;
+    for (int k = NW - 1; k >= 0; k--) {
+        const uint32_t w = (uint32_t)(qw + OFF);
+        Wc[k] = w & 0xFF;
+        Wc[NW + k] = w >> 8;
+        if (k) qw = van[k] + 256 * qw;
+    }
+    for (int i = 0; i < NL; i++) {
+        o[i] = byte_of(res_col[i >> 2], i & 3);
+        o[NL + i] = byte_of(car[i >> 2], i & 3);
+    }
+    for (int blk = 0; blk < 4; blk++) {
+        const uint32_t *g = o + (blk < 2 ? NL * blk : 2 * NL + NW * (blk - 2));
+        const int len = blk < 2 ? NL : NW;
+        for (int j = 0; j + 1 < len; j += 2) byte_add(bm, B_U8RANGE, g[j], g[j + 1]);
+        if (len & 1) byte_add(bm, B_U8RANGE, g[len - 1], 0);
+    }
+}
+
+// FpOpCols: is_real, shard, clk, is_add, is_sub, is_mul, x_ptr, y_ptr, x (W MemoryWriteCols), y (W
+// MemoryReadCols), FieldOpCols.  zkm_fp_op_event dwords: shard, clk, x_ptr, y_ptr, op, y reads (12 x 5), x
+// writes (12 x 6) -- the first W of each used
+enum { FO_REAL = 0, FO_SHARD = 1, FO_CLK = 2, FO_ADD = 3, FO_SUB = 4, FO_MUL = 5, FO_XPTR = 6, FO_YPTR = 7, FO_X = 8,
+       FO_EV = 5 + 60 + 72 };
+struct FpMod {
+    uint32_t w[12];
+};
+template <int W, int NW, int OFF>
+__global__ __launch_bounds__(128) void k_fp_op_rows(const uint32_t *__restrict__ ev, uint64_t n, uint32_t *__restrict__ out,
+                                                    uint64_t height, FpMod mod, uint32_t *bm) {
+    constexpr int NL = 4 * W, Y = FO_X + 13 * W, OUT = Y + 9 * W, WIDTH = OUT + 2 * NL + 2 * NW;
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WIDTH;
+    for (int c = 0; c < WIDTH; c++) v[c] = 0;
+    v[FO_ADD] = 1;
+    if (row >= n) {  // 0 + 0: witness limbs = the offset
+        for (int k = 0; k < NW; k++) {
+            v[OUT + 2 * NL + k] = OFF & 0xFF;
+            v[OUT + 2 * NL + NW + k] = OFF >> 8;
+        }
+        return;
+    }
+    const uint32_t *e = ev + row * FO_EV;
+    const uint32_t op = e[4];
+    v[FO_REAL] = 1;
+    v[FO_SHARD] = e[0];
+    v[FO_CLK] = e[1];
+    v[FO_XPTR] = e[2];
+    v[FO_YPTR] = e[3];
+    v[FO_ADD] = op == 0;
+    v[FO_SUB] = op == 1;
+    v[FO_MUL] = op == 2;
+    uint32_t x[W], y[W];
+    for (int i = 0; i < W; i++) {
+        const Access ya = access_read(e + 5 + 5 * i), xa = access_write(e + 65 + 6 * i);
+        y[i] = ya.value;
+        x[i] = xa.prev_value;
+        put_access(v, Y + 9 * i, ya);
+        put_word(v + FO_X + 13 * i, xa.prev_value);
+        put_access(v, FO_X + 13 * i + 4, xa);
+        const Access as[2] = {ya, xa};
+        for (int k = 0; k < 2; k++) {
+            byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
+            byte_add(bm, B_U8RANGE, 0, as[k].d8);
+        }
+    }
+    uint32_t a[W], b[W];
+    mod_words<W, W>(x, mod.w, a, nullptr);
+    mod_words<W, W>(y, mod.w, b, nullptr);
+    uint32_t r[W], lhs[W], full[2 * W], mres[W], car[W];
+    for (int i = 0; i < W; i++) car[i] = 0;
+    for (int i = 0; i < 2 * W; i++) full[i] = 0;
+    if (op == 2) {  // mul: a b = carry m + result
+        for (int i = 0; i < W; i++) {
+            uint64_t c = 0;
+            for (int j = 0; j < W; j++) {
+                const uint64_t t = (uint64_t)a[i] * b[j] + full[i + j] + c;
+                full[i + j] = (uint32_t)t;
+                c = t >> 32;
+            }
+            full[i + W] = (uint32_t)c;
+        }
+        mod_words<2 * W, W>(full, mod.w, mres, car);
+        for (int i = 0; i < W; i++) {
+            r[i] = mres[i];
+            lhs[i] = a[i];
+        }
+    } else {
+        if (op == 1) {  // sub: r = a - b mod m, populated as r + b = a + carry m
+            uint64_t c = 0;
+            uint32_t t[W + 1];
+            for (int i = 0; i < W; i++) {  // a + m - b (< 2m)
+                const uint64_t s_ = (uint64_t)a[i] + mod.w[i] + c;
+                t[i] = (uint32_t)s_;
+                c = s_ >> 32;
+            }
+            t[W] = (uint32_t)c;
+            int64_t bw = 0;
+            for (int i = 0; i <= W; i++) {
+                const int64_t d = (int64_t)t[i] - (i < W ? b[i] : 0u) - bw;
+                t[i] = (uint32_t)d;
+                bw = d < 0;
+            }
+            uint32_t rr[W];
+            mod_words<W + 1, W>(t, mod.w, rr, nullptr);
+            for (int i = 0; i < W; i++) r[i] = lhs[i] = rr[i];
+        } else {
+            for (int i = 0; i < W; i++) r[i] = lhs[i] = a[i];
+        }
+        uint64_t c = 0;  // lhs + b
+        for (int i = 0; i < W; i++) {
+            const uint64_t s_ = (uint64_t)lhs[i] + b[i] + c;
+            full[i] = (uint32_t)s_;
+            c = s_ >> 32;
+        }
+        full[W] = (uint32_t)c;
+        mod_words<W + 1, W>(full, mod.w, mres, car);
+        if (op == 0)
+            for (int i = 0; i < W; i++) r[i] = mres[i];
+    }
+    field_op_cols<NL, NW, OFF>(v + OUT, lhs, b, op == 2, r, mres, car, mod.w, bm);
+}
+
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
 // SysLinuxCols (sys_linux/columns.rs); zkm_sys_linux_event dwords: shard, clk, code, a0, a1, result, the A3
 // write, the io record
@@ -2236,6 +2448,34 @@ int zkm_u256x2048_mul_events_to_trace(const zkm_u256x2048_mul_event *events, uin
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_u256x2048_mul_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_fp_op_events_to_trace(int field, const zkm_fp_op_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                              uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_fp_op_event) == 4 * FO_EV, "FpOpEvent record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1)) ||
+        (field != ZKM_FIELD_BN254 && field != ZKM_FIELD_BLS12381)) {
+        g_last_error = "zkm_fp_op_events_to_trace: bad arguments (need n <= height, a power of two >= 16, a known field)";
+        return ZKM_ERR_ARG;
+    }
+    // the base field moduli (crates/curves/src/weierstrass/{bn254,bls12_381}.rs FieldParameters), 32-bit words
+    static const FpMod bn254{{0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u, 0x8181585du, 0xb85045b6u,
+                              0xe131a029u, 0x30644e72u, 0, 0, 0, 0}};
+    static const FpMod bls{{0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,
+                            0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau}};
+    const dim3 grid((unsigned)((height + 127) / 128)), block(128);
+    if (field == ZKM_FIELD_BN254)
+        hipLaunchKernelGGL((k_fp_op_rows<8, 62, 1 << 14>), grid, block, 0, (hipStream_t)stream, (const uint32_t *)events, n,
+                           trace, height, bn254, byte_mult);
+    else
+        hipLaunchKernelGGL((k_fp_op_rows<12, 94, 1 << 15>), grid, block, 0, (hipStream_t)stream, (const uint32_t *)events,
+                           n, trace, height, bls, byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_fp_op_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;

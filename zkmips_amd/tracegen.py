@@ -397,6 +397,41 @@ def u256x2048_mul_trace(events_dev, n: int, height: int = None, byte_mult=None):
     return t
 
 
+FP_OP_EVENT = np.dtype({"names": ["shard", "clk", "x_ptr", "y_ptr", "op", "y", "x"],
+                        "formats": [u4, u4, u4, u4, u4, (u4, (12, 5)), (u4, (12, 6))],
+                        "offsets": [0, 4, 8, 12, 16, 20, 260], "itemsize": 548})
+FP_OP_FIELDS = {"Bn254": (0, 372), "Bls12381": (1, 556)}  # ZKM_FIELD_*, ZKM_FP_OP_WIDTH_*
+_FP_OP_CODE = {"add": 0, "sub": 1, "mul": 2}
+
+
+def fp_op_records(events) -> np.ndarray:
+    """zkm_fp_op_event records of the executor's FpOp events (mips_ec.exec_fp_op): y read at clk, x written at
+    clk + 1 (8 or 12 words, in slots of 12)."""
+    out = np.zeros(len(events), FP_OP_EVENT)
+    for k, e in enumerate(events):
+        sh, clk = e["shard"], e["clk"]
+        r = out[k]
+        r["shard"], r["clk"], r["x_ptr"], r["y_ptr"], r["op"] = sh, clk, e["x_ptr"], e["y_ptr"], _FP_OP_CODE[e["op"]]
+        rd = np.asarray(e["y"], np.int64).reshape(-1, 3)
+        wr = np.asarray(e["xw"], np.int64).reshape(-1, 4)
+        w = len(rd)
+        r["y"][:w] = np.stack([rd[:, 0], np.full(w, sh), np.full(w, clk), rd[:, 1], rd[:, 2]], 1)
+        r["x"][:w] = np.stack([wr[:, 1], np.full(w, sh), np.full(w, clk + 1), wr[:, 0], wr[:, 2], wr[:, 3]], 1)
+    return out
+
+
+def fp_op_trace(field: str, events_dev, n: int, height: int = None, byte_mult=None):
+    """FpOpAssign main trace of the bn254 / bls12-381 base field (height x 372 / 556 int32, on the GPU) from n
+    zkm_fp_op_event records; the Byte lookups added into byte_mult (nullable)."""
+    code, width = FP_OP_FIELDS[field]
+    height = height or _pow2(n)
+    t = _trace(height, width)
+    what = "zkm_fp_op_events_to_trace"
+    _lib.check(_bind().zkm_fp_op_events_to_trace(code, _records(events_dev, n, FP_OP_EVENT, what), n, t.data_ptr(),
+                                                 height, _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
 SYS_LINUX_EVENT = np.dtype({"names": ["shard", "clk", "code", "a0", "a1", "result", "a3", "io"],
                             "formats": [u4, u4, u4, u4, u4, u4, (u4, 6), (u4, 6)],
                             "offsets": [0, 4, 8, 12, 16, 20, 24, 48], "itemsize": 72})
@@ -536,6 +571,7 @@ def _bind():
         L.zkm_sys_linux_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_uint256_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_u256x2048_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_fp_op_events_to_trace.argtypes = [C.c_int, vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -561,7 +597,7 @@ def to_device(records: np.ndarray):
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
                              SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
                              COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT, POSEIDON2_PERMUTE_EVENT,
-                             SYS_LINUX_EVENT, UINT256_MUL_EVENT, U256X2048_MUL_EVENT):
+                             SYS_LINUX_EVENT, UINT256_MUL_EVENT, U256X2048_MUL_EVENT, FP_OP_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -909,9 +945,9 @@ def recursion_instrs_trace(chip: str, records_dev, n: int, height: int, montgome
 
 
 def precompile_shard_traces(code: int, events, byte_mult=None):
-    """Device traces of a SHA, Poseidon2, 256-bit multiplication or Linux-syscall precompile shard
-    (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE / UINT256_MUL /
-    U256XU2048_MUL / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    """Device traces of a SHA, Poseidon2, 256-bit multiplication, base-field (FpOp) or Linux-syscall
+    precompile shard (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE /
+    UINT256_MUL / U256XU2048_MUL / the bn254 and bls12-381 FP ops / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
     from . import mips_ec as EC
@@ -933,6 +969,10 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     elif code == EC.U256XU2048_MUL:
         rec = u256x2048_mul_records(pevs)
         out["U256XU2048Mul"] = u256x2048_mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    elif any(code == EC.FP_OPS[f][0] for f in FP_OP_FIELDS):
+        field = next(f for f in FP_OP_FIELDS if code == EC.FP_OPS[f][0])
+        rec = fp_op_records(pevs)
+        out[EC.FP_NAME[field]] = fp_op_trace(field, to_device(rec), len(rec), byte_mult=byte_mult)
     elif code == SY.SYS_LINUX:
         rec = sys_linux_records(pevs)
         out["SysLinux"] = sys_linux_trace(to_device(rec), len(rec), byte_mult=byte_mult)
