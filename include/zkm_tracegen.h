@@ -292,6 +292,20 @@ typedef struct {
 int zkm_fp_op_events_to_trace(int field, const zkm_fp_op_event *events, uint64_t n, uint32_t *trace, uint64_t height,
                               uint32_t *byte_mult, void *stream);
 
+/* Fp2AddSubAssign / Fp2MulAssign of the bn254 / bls12-381 quadratic extensions (fptower/fp2_addsub.rs:93-183,
+ * fp2_mul.rs:122-210): one fixed record per call: shard, clk, x_ptr, y_ptr, op (0 add, 1 sub; unused for mul),
+ * the reads of y = (y0, y1) at clk and the writes of x = (x0, x1) at clk + 1 (16 words for bn254, 24 for
+ * bls12-381, in slots of 24).  Rows: AddSub c0 = x0 +- y0, c1 = x1 +- y1 (two FieldOpCols), Mul a0 b0, a1 b1,
+ * a0 b1, a1 b0 and c0 = a0 b0 - a1 b1, c1 = a0 b1 + a1 b0 (six); padding rows the operations on zeros.
+ * byte_mult (nullable): the limbs' U8 and the accesses' range checks.  mul: 0 AddSub, 1 Mul. */
+typedef struct {
+    uint32_t shard, clk, x_ptr, y_ptr, op;
+    zkm_memory_read_record y[24];
+    zkm_memory_write_record x[24];
+} zkm_fp2_event;  /* 1076 bytes */
+int zkm_fp2_events_to_trace(int field, int mul, const zkm_fp2_event *events, uint64_t n, uint32_t *trace,
+                            uint64_t height, uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

@@ -725,6 +725,67 @@ def test_fp_op_shard_from_device_traces(field):
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 
+def _fp2_events(field: str, mul: bool, seed: int = 19):
+    """Fp2AddSub (add and sub) or Fp2Mul calls of one field through the executor (mips_ec.exec_fp2_addsub /
+    exec_fp2_mul): random coordinates (some at or above the modulus), zeros and p - 1."""
+    from zkmips_amd import emulated_field as EF
+    from zkmips_amd import mips_ec as EC
+    rng = np.random.default_rng(seed)
+    fp = EC.FIELDS[field]
+    words = {}
+    mem, mem_init, mem_last = {}, {}, {}
+    vals = [int.from_bytes(rng.bytes(fp.nl), "little") for _ in range(8)] + [0, fp.modulus - 1, fp.modulus]
+    evs = []
+    for k in range(22):
+        op = "mul" if mul else ("add", "sub")[k % 2]
+        x = [vals[(k + j) % len(vals)] for j in (0, 3)]
+        y = [vals[(5 * k + j) % len(vals)] for j in (1, 7)]
+        xp, yp = 0x40000 + 0x200 * k, 0x50000 + 0x200 * k
+        for i, w in enumerate(EF.int_to_words(x[0], fp.words) + EF.int_to_words(x[1], fp.words)):
+            words[xp + 4 * i] = w
+        for i, w in enumerate(EF.int_to_words(y[0], fp.words) + EF.int_to_words(y[1], fp.words)):
+            words[yp + 4 * i] = w
+        shard, clk = 3 + k // 12, 90 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: words.get(a, 0))
+        if mul:
+            key = code = EC.FP2_MUL[field]
+            ev = EC.exec_fp2_mul(field, pm, shard, clk, xp, yp)
+        else:
+            key, code = EC.FP2_ADDSUB[field][0], EC.FP2_ADDSUB[field][k % 2]
+            ev = EC.exec_fp2_addsub(field, op, pm, shard, clk, xp, yp)
+        evs.append((key, (shard, clk, SY.syscall_id(code), xp, yp), ev))
+    return evs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field", ["Bn254", "Bls12381"])
+@pytest.mark.parametrize("mul", [False, True])
+def test_fp2_shard_from_device_traces(field, mul):
+    """Fp2AddSub / Fp2Mul precompile shards built on the device (two / six chained base-field ops per row)
+    equal the host builders' traces and multiplicities and prove to the same bytes."""
+    import torch
+    from zkmips_amd import mips_ec as EC
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _fp2_events(field, mul)
+    key = evs[0][0]
+    m, prep, tr, pv = MC.precompile_shard(key, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(key, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert (EC.FP2_MUL_NAME if mul else EC.FP2_ADDSUB_NAME)[field] in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

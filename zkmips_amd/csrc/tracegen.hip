@@ -1729,46 +1729,17 @@ enum { FO_REAL = 0, FO_SHARD = 1, FO_CLK = 2, FO_ADD = 3, FO_SUB = 4, FO_MUL = 5
 struct FpMod {
     uint32_t w[12];
 };
+// the base field moduli (crates/curves/src/weierstrass/{bn254,bls12_381}.rs FieldParameters), 32-bit words
+constexpr FpMod kBn254{{0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u, 0x8181585du, 0xb85045b6u, 0xe131a029u,
+                        0x30644e72u, 0, 0, 0, 0}};
+constexpr FpMod kBls{{0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu,
+                      0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau}};
+// One FieldOpCols of x op y in the base field (x, y: W words, reduced here; op 0 add, 1 sub, 2 mul), its
+// result r (mod p) into res (nullable) -- FieldOpCols::populate_with_modulus as pop_field_op
 template <int W, int NW, int OFF>
-__global__ __launch_bounds__(128) void k_fp_op_rows(const uint32_t *__restrict__ ev, uint64_t n, uint32_t *__restrict__ out,
-                                                    uint64_t height, FpMod mod, uint32_t *bm) {
-    constexpr int NL = 4 * W, Y = FO_X + 13 * W, OUT = Y + 9 * W, WIDTH = OUT + 2 * NL + 2 * NW;
-    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
-    if (row >= height) return;
-    uint32_t *v = out + row * WIDTH;
-    for (int c = 0; c < WIDTH; c++) v[c] = 0;
-    v[FO_ADD] = 1;
-    if (row >= n) {  // 0 + 0: witness limbs = the offset
-        for (int k = 0; k < NW; k++) {
-            v[OUT + 2 * NL + k] = OFF & 0xFF;
-            v[OUT + 2 * NL + NW + k] = OFF >> 8;
-        }
-        return;
-    }
-    const uint32_t *e = ev + row * FO_EV;
-    const uint32_t op = e[4];
-    v[FO_REAL] = 1;
-    v[FO_SHARD] = e[0];
-    v[FO_CLK] = e[1];
-    v[FO_XPTR] = e[2];
-    v[FO_YPTR] = e[3];
-    v[FO_ADD] = op == 0;
-    v[FO_SUB] = op == 1;
-    v[FO_MUL] = op == 2;
-    uint32_t x[W], y[W];
-    for (int i = 0; i < W; i++) {
-        const Access ya = access_read(e + 5 + 5 * i), xa = access_write(e + 65 + 6 * i);
-        y[i] = ya.value;
-        x[i] = xa.prev_value;
-        put_access(v, Y + 9 * i, ya);
-        put_word(v + FO_X + 13 * i, xa.prev_value);
-        put_access(v, FO_X + 13 * i + 4, xa);
-        const Access as[2] = {ya, xa};
-        for (int k = 0; k < 2; k++) {
-            byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
-            byte_add(bm, B_U8RANGE, 0, as[k].d8);
-        }
-    }
+__device__ inline void fp_op(uint32_t *o, const uint32_t *x, const uint32_t *y, uint32_t op, const FpMod &mod,
+                             uint32_t *bm, uint32_t *res) {
+    constexpr int NL = 4 * W;
     uint32_t a[W], b[W];
     mod_words<W, W>(x, mod.w, a, nullptr);
     mod_words<W, W>(y, mod.w, b, nullptr);
@@ -1823,7 +1794,112 @@ __global__ __launch_bounds__(128) void k_fp_op_rows(const uint32_t *__restrict__
         if (op == 0)
             for (int i = 0; i < W; i++) r[i] = mres[i];
     }
-    field_op_cols<NL, NW, OFF>(v + OUT, lhs, b, op == 2, r, mres, car, mod.w, bm);
+    field_op_cols<NL, NW, OFF>(o, lhs, b, op == 2, r, mres, car, mod.w, bm);
+    if (res)
+        for (int i = 0; i < W; i++) res[i] = r[i];
+}
+
+template <int W, int NW, int OFF>
+__global__ __launch_bounds__(128) void k_fp_op_rows(const uint32_t *__restrict__ ev, uint64_t n, uint32_t *__restrict__ out,
+                                                    uint64_t height, FpMod mod, uint32_t *bm) {
+    constexpr int NL = 4 * W, Y = FO_X + 13 * W, OUT = Y + 9 * W, WIDTH = OUT + 2 * NL + 2 * NW;
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WIDTH;
+    for (int c = 0; c < WIDTH; c++) v[c] = 0;
+    v[FO_ADD] = 1;
+    if (row >= n) {  // 0 + 0: witness limbs = the offset
+        for (int k = 0; k < NW; k++) {
+            v[OUT + 2 * NL + k] = OFF & 0xFF;
+            v[OUT + 2 * NL + NW + k] = OFF >> 8;
+        }
+        return;
+    }
+    const uint32_t *e = ev + row * FO_EV;
+    const uint32_t op = e[4];
+    v[FO_REAL] = 1;
+    v[FO_SHARD] = e[0];
+    v[FO_CLK] = e[1];
+    v[FO_XPTR] = e[2];
+    v[FO_YPTR] = e[3];
+    v[FO_ADD] = op == 0;
+    v[FO_SUB] = op == 1;
+    v[FO_MUL] = op == 2;
+    uint32_t x[W], y[W];
+    for (int i = 0; i < W; i++) {
+        const Access ya = access_read(e + 5 + 5 * i), xa = access_write(e + 65 + 6 * i);
+        y[i] = ya.value;
+        x[i] = xa.prev_value;
+        put_access(v, Y + 9 * i, ya);
+        put_word(v + FO_X + 13 * i, xa.prev_value);
+        put_access(v, FO_X + 13 * i + 4, xa);
+        const Access as[2] = {ya, xa};
+        for (int k = 0; k < 2; k++) {
+            byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
+            byte_add(bm, B_U8RANGE, 0, as[k].d8);
+        }
+    }
+    fp_op<W, NW, OFF>(v + OUT, x, y, op, mod, bm, nullptr);
+}
+
+// Fp2AddSubAssign / Fp2MulAssign (fptower/fp2_addsub.rs:93-183, fp2_mul.rs:122-210): x = (x0, x1), y = (y0, y1)
+// of 2W words.  AddSub: is_real, shard, clk, is_add, x_ptr, y_ptr, x (2W writes), y (2W reads), c0, c1.  Mul:
+// is_real, shard, clk, x_ptr, y_ptr, x, y, a0 b0, a1 b1, a0 b1, a1 b0, c0 = a0 b0 - a1 b1, c1 = a0 b1 + a1 b0.
+// zkm_fp2_event dwords: shard, clk, x_ptr, y_ptr, op (0 add, 1 sub; mul: unused), y reads (24 x 5), x writes
+// (24 x 6), the first 2W of each used
+enum { F2_EV = 5 + 120 + 144 };
+template <int W, int NW, int OFF, bool MUL>
+__global__ __launch_bounds__(128) void k_fp2_rows(const uint32_t *__restrict__ ev, uint64_t n, uint32_t *__restrict__ out,
+                                                  uint64_t height, FpMod mod, uint32_t *bm) {
+    constexpr int NL = 4 * W, FW = 2 * NL + 2 * NW, H = MUL ? 5 : 6, X = H, Y = X + 2 * W * 13, OUT = Y + 2 * W * 9,
+                  NOPS = MUL ? 6 : 2, WIDTH = OUT + NOPS * FW;
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WIDTH;
+    for (int c = 0; c < WIDTH; c++) v[c] = 0;
+    if (!MUL) v[3] = 1;  // is_add (padding rows add zeros)
+    if (row >= n) {      // the operations on zeros: witness limbs = the offset
+        for (int k = 0; k < NOPS; k++)
+            for (int j = 0; j < NW; j++) {
+                v[OUT + k * FW + 2 * NL + j] = OFF & 0xFF;
+                v[OUT + k * FW + 2 * NL + NW + j] = OFF >> 8;
+            }
+        return;
+    }
+    const uint32_t *e = ev + row * F2_EV;
+    v[0] = 1;
+    v[1] = e[0];
+    v[2] = e[1];
+    v[H - 2] = e[2];
+    v[H - 1] = e[3];
+    const uint32_t op = e[4];
+    if (!MUL) v[3] = op == 0;
+    uint32_t x[2 * W], y[2 * W];
+    for (int i = 0; i < 2 * W; i++) {
+        const Access ya = access_read(e + 5 + 5 * i), xa = access_write(e + 125 + 6 * i);
+        y[i] = ya.value;
+        x[i] = xa.prev_value;
+        put_access(v, Y + 9 * i, ya);
+        put_word(v + X + 13 * i, xa.prev_value);
+        put_access(v, X + 13 * i + 4, xa);
+        const Access as[2] = {ya, xa};
+        for (int k = 0; k < 2; k++) {
+            byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
+            byte_add(bm, B_U8RANGE, 0, as[k].d8);
+        }
+    }
+    if (!MUL) {
+        fp_op<W, NW, OFF>(v + OUT, x, y, op, mod, bm, nullptr);
+        fp_op<W, NW, OFF>(v + OUT + FW, x + W, y + W, op, mod, bm, nullptr);
+    } else {
+        uint32_t r00[W], r11[W], r01[W], r10[W];
+        fp_op<W, NW, OFF>(v + OUT, x, y, 2, mod, bm, r00);
+        fp_op<W, NW, OFF>(v + OUT + FW, x + W, y + W, 2, mod, bm, r11);
+        fp_op<W, NW, OFF>(v + OUT + 2 * FW, x, y + W, 2, mod, bm, r01);
+        fp_op<W, NW, OFF>(v + OUT + 3 * FW, x + W, y, 2, mod, bm, r10);
+        fp_op<W, NW, OFF>(v + OUT + 4 * FW, r00, r11, 1, mod, bm, nullptr);
+        fp_op<W, NW, OFF>(v + OUT + 5 * FW, r01, r10, 0, mod, bm, nullptr);
+    }
 }
 
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
@@ -2461,21 +2537,42 @@ int zkm_fp_op_events_to_trace(int field, const zkm_fp_op_event *events, uint64_t
         g_last_error = "zkm_fp_op_events_to_trace: bad arguments (need n <= height, a power of two >= 16, a known field)";
         return ZKM_ERR_ARG;
     }
-    // the base field moduli (crates/curves/src/weierstrass/{bn254,bls12_381}.rs FieldParameters), 32-bit words
-    static const FpMod bn254{{0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u, 0x8181585du, 0xb85045b6u,
-                              0xe131a029u, 0x30644e72u, 0, 0, 0, 0}};
-    static const FpMod bls{{0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,
-                            0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau}};
     const dim3 grid((unsigned)((height + 127) / 128)), block(128);
     if (field == ZKM_FIELD_BN254)
         hipLaunchKernelGGL((k_fp_op_rows<8, 62, 1 << 14>), grid, block, 0, (hipStream_t)stream, (const uint32_t *)events, n,
-                           trace, height, bn254, byte_mult);
+                           trace, height, kBn254, byte_mult);
     else
         hipLaunchKernelGGL((k_fp_op_rows<12, 94, 1 << 15>), grid, block, 0, (hipStream_t)stream, (const uint32_t *)events,
-                           n, trace, height, bls, byte_mult);
+                           n, trace, height, kBls, byte_mult);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_fp_op_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_fp2_events_to_trace(int field, int mul, const zkm_fp2_event *events, uint64_t n, uint32_t *trace,
+                            uint64_t height, uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_fp2_event) == 4 * F2_EV, "Fp2 event record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1)) ||
+        (field != ZKM_FIELD_BN254 && field != ZKM_FIELD_BLS12381)) {
+        g_last_error = "zkm_fp2_events_to_trace: bad arguments (need n <= height, a power of two >= 16, a known field)";
+        return ZKM_ERR_ARG;
+    }
+    const dim3 grid((unsigned)((height + 127) / 128)), block(128);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t *ev = (const uint32_t *)events;
+    if (field == ZKM_FIELD_BN254) {
+        if (mul) hipLaunchKernelGGL((k_fp2_rows<8, 62, 1 << 14, true>), grid, block, 0, s, ev, n, trace, height, kBn254, byte_mult);
+        else hipLaunchKernelGGL((k_fp2_rows<8, 62, 1 << 14, false>), grid, block, 0, s, ev, n, trace, height, kBn254, byte_mult);
+    } else {
+        if (mul) hipLaunchKernelGGL((k_fp2_rows<12, 94, 1 << 15, true>), grid, block, 0, s, ev, n, trace, height, kBls, byte_mult);
+        else hipLaunchKernelGGL((k_fp2_rows<12, 94, 1 << 15, false>), grid, block, 0, s, ev, n, trace, height, kBls, byte_mult);
+    }
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_fp2_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;

@@ -432,6 +432,42 @@ def fp_op_trace(field: str, events_dev, n: int, height: int = None, byte_mult=No
     return t
 
 
+FP2_EVENT = np.dtype({"names": ["shard", "clk", "x_ptr", "y_ptr", "op", "y", "x"],
+                      "formats": [u4, u4, u4, u4, u4, (u4, (24, 5)), (u4, (24, 6))],
+                      "offsets": [0, 4, 8, 12, 16, 20, 500], "itemsize": 1076})
+FP2_WIDTHS = {("Bn254", False): 734, ("Bls12381", False): 1102, ("Bn254", True): 1485, ("Bls12381", True): 2237}
+
+
+def fp2_records(events) -> np.ndarray:
+    """zkm_fp2_event records of the executor's Fp2AddSub / Fp2Mul events (mips_ec.exec_fp2_addsub /
+    exec_fp2_mul): y read at clk, x written at clk + 1 (16 or 24 words, in slots of 24)."""
+    out = np.zeros(len(events), FP2_EVENT)
+    for k, e in enumerate(events):
+        sh, clk = e["shard"], e["clk"]
+        r = out[k]
+        r["shard"], r["clk"], r["x_ptr"], r["y_ptr"] = sh, clk, e["x_ptr"], e["y_ptr"]
+        r["op"] = _FP_OP_CODE.get(e.get("op", "add"), 0)
+        rd = np.asarray(e["y"], np.int64).reshape(-1, 3)
+        wr = np.asarray(e["xw"], np.int64).reshape(-1, 4)
+        w = len(rd)
+        r["y"][:w] = np.stack([rd[:, 0], np.full(w, sh), np.full(w, clk), rd[:, 1], rd[:, 2]], 1)
+        r["x"][:w] = np.stack([wr[:, 1], np.full(w, sh), np.full(w, clk + 1), wr[:, 0], wr[:, 2], wr[:, 3]], 1)
+    return out
+
+
+def fp2_trace(field: str, mul: bool, events_dev, n: int, height: int = None, byte_mult=None):
+    """Fp2AddSubAssign (mul False) or Fp2MulAssign main trace of the bn254 / bls12-381 extension (on the GPU)
+    from n zkm_fp2_event records; the Byte lookups added into byte_mult (nullable)."""
+    code = FP_OP_FIELDS[field][0]
+    height = height or _pow2(n)
+    t = _trace(height, FP2_WIDTHS[(field, bool(mul))])
+    what = "zkm_fp2_events_to_trace"
+    _lib.check(_bind().zkm_fp2_events_to_trace(code, int(bool(mul)), _records(events_dev, n, FP2_EVENT, what), n,
+                                               t.data_ptr(), height, _words(byte_mult, 65536 * 10, what), _stream()),
+               what)
+    return t
+
+
 SYS_LINUX_EVENT = np.dtype({"names": ["shard", "clk", "code", "a0", "a1", "result", "a3", "io"],
                             "formats": [u4, u4, u4, u4, u4, u4, (u4, 6), (u4, 6)],
                             "offsets": [0, 4, 8, 12, 16, 20, 24, 48], "itemsize": 72})
@@ -572,6 +608,7 @@ def _bind():
         L.zkm_uint256_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_u256x2048_mul_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_fp_op_events_to_trace.argtypes = [C.c_int, vp, u64, vp, u64, vp, vp]
+        L.zkm_fp2_events_to_trace.argtypes = [C.c_int, C.c_int, vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -597,7 +634,8 @@ def to_device(records: np.ndarray):
     if records.dtype not in (CPU_EVENT, INSTRUCTION, ALU_EVENT, MEMORY_LOCAL_EVENT, MEMORY_INIT_FINAL_EVENT,
                              SYSCALL_EVENT, GLOBAL_EVENT, BRANCH_EVENT, MEM_INSTR_EVENT, MOVCOND_EVENT,
                              COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT, POSEIDON2_PERMUTE_EVENT,
-                             SYS_LINUX_EVENT, UINT256_MUL_EVENT, U256X2048_MUL_EVENT, FP_OP_EVENT):
+                             SYS_LINUX_EVENT, UINT256_MUL_EVENT, U256X2048_MUL_EVENT, FP_OP_EVENT,
+                             FP2_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -947,7 +985,8 @@ def recursion_instrs_trace(chip: str, records_dev, n: int, height: int, montgome
 def precompile_shard_traces(code: int, events, byte_mult=None):
     """Device traces of a SHA, Poseidon2, 256-bit multiplication, base-field (FpOp) or Linux-syscall
     precompile shard (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE /
-    UINT256_MUL / U256XU2048_MUL / the bn254 and bls12-381 FP ops / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    UINT256_MUL / U256XU2048_MUL / the bn254 and bls12-381 FP, FP2 add/sub and FP2 mul ops / the Linux
+    syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
     from . import mips_ec as EC
@@ -973,6 +1012,12 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
         field = next(f for f in FP_OP_FIELDS if code == EC.FP_OPS[f][0])
         rec = fp_op_records(pevs)
         out[EC.FP_NAME[field]] = fp_op_trace(field, to_device(rec), len(rec), byte_mult=byte_mult)
+    elif any(code in (EC.FP2_ADDSUB[f][0], EC.FP2_MUL[f]) for f in FP_OP_FIELDS):
+        field = next(f for f in FP_OP_FIELDS if code in (EC.FP2_ADDSUB[f][0], EC.FP2_MUL[f]))
+        mul = code == EC.FP2_MUL[field]
+        rec = fp2_records(pevs)
+        name = EC.FP2_MUL_NAME[field] if mul else EC.FP2_ADDSUB_NAME[field]
+        out[name] = fp2_trace(field, mul, to_device(rec), len(rec), byte_mult=byte_mult)
     elif code == SY.SYS_LINUX:
         rec = sys_linux_records(pevs)
         out["SysLinux"] = sys_linux_trace(to_device(rec), len(rec), byte_mult=byte_mult)
