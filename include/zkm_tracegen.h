@@ -306,6 +306,23 @@ typedef struct {
 int zkm_fp2_events_to_trace(int field, int mul, const zkm_fp2_event *events, uint64_t n, uint32_t *trace,
                             uint64_t height, uint32_t *byte_mult, void *stream);
 
+/* WeierstrassAddAssign on secp256k1 / secp256r1 / bn254 / bls12-381 (weierstrass/weierstrass_add.rs:192-252,
+ * :384-420): EllipticCurveAddEvent as one fixed record: shard, clk, p_ptr, q_ptr, the reads of q at clk and
+ * the writes of p at clk + 1 (16 words for the 256-bit curves, 24 for bls12-381, in slots of 24).  Each row:
+ * the accesses and the nine FieldOpCols of the affine addition (the slope by a modular inverse on the
+ * device); padding rows the operations on zero inputs.  byte_mult (nullable) as above. */
+#define ZKM_CURVE_SECP256K1 0
+#define ZKM_CURVE_SECP256R1 1
+#define ZKM_CURVE_BN254 2
+#define ZKM_CURVE_BLS12381 3
+typedef struct {
+    uint32_t shard, clk, p_ptr, q_ptr;
+    zkm_memory_read_record q[24];
+    zkm_memory_write_record p[24];
+} zkm_ec_add_event;  /* 1072 bytes */
+int zkm_ec_add_events_to_trace(int curve, const zkm_ec_add_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                               uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

@@ -1732,69 +1732,140 @@ struct FpMod {
 // the base field moduli (crates/curves/src/weierstrass/{bn254,bls12_381}.rs FieldParameters), 32-bit words
 constexpr FpMod kBn254{{0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u, 0x8181585du, 0xb85045b6u, 0xe131a029u,
                         0x30644e72u, 0, 0, 0, 0}};
+constexpr FpMod kSecp256k1{{0xfffffc2fu, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu,
+                            0xffffffffu, 0, 0, 0, 0}};
+constexpr FpMod kSecp256r1{{0xffffffffu, 0xffffffffu, 0xffffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000001u,
+                            0xffffffffu, 0, 0, 0, 0}};
 constexpr FpMod kBls{{0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu,
                       0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau}};
-// One FieldOpCols of x op y in the base field (x, y: W words, reduced here; op 0 add, 1 sub, 2 mul), its
-// result r (mod p) into res (nullable) -- FieldOpCols::populate_with_modulus as pop_field_op
+// W-word helpers for the modular inverse (binary extended Euclid; p odd)
+template <int W>
+__device__ inline bool w_is(const uint32_t *u, uint32_t x) {
+    bool r = u[0] == x;
+    for (int i = 1; i < W; i++) r = r && u[i] == 0;
+    return r;
+}
+template <int W>
+__device__ inline void w_shr1(uint32_t *u, uint32_t top) {
+    for (int i = 0; i < W - 1; i++) u[i] = (u[i] >> 1) | (u[i + 1] << 31);
+    u[W - 1] = (u[W - 1] >> 1) | (top << 31);
+}
+template <int W>
+__device__ inline bool w_ge(const uint32_t *a, const uint32_t *b) {
+    for (int i = W - 1; i >= 0; i--)
+        if (a[i] != b[i]) return a[i] > b[i];
+    return true;
+}
+template <int W>
+__device__ inline uint32_t w_sub(uint32_t *a, const uint32_t *b) {  // a -= b, returns the borrow
+    int64_t bw = 0;
+    for (int i = 0; i < W; i++) {
+        const int64_t d = (int64_t)a[i] - b[i] - bw;
+        a[i] = (uint32_t)d;
+        bw = d < 0;
+    }
+    return (uint32_t)bw;
+}
+template <int W>
+__device__ inline uint32_t w_add(uint32_t *a, const uint32_t *b) {  // a += b, returns the carry
+    uint64_t c = 0;
+    for (int i = 0; i < W; i++) {
+        const uint64_t t = (uint64_t)a[i] + b[i] + c;
+        a[i] = (uint32_t)t;
+        c = t >> 32;
+    }
+    return (uint32_t)c;
+}
+// a^-1 mod p for 0 < a < p
+template <int W>
+__device__ inline void modinv(const uint32_t *a, const uint32_t *p, uint32_t *out) {
+    uint32_t u[W], v[W], x1[W], x2[W];
+    for (int i = 0; i < W; i++) {
+        u[i] = a[i];
+        v[i] = p[i];
+        x1[i] = i == 0;
+        x2[i] = 0;
+    }
+    while (!w_is<W>(u, 1) && !w_is<W>(v, 1)) {
+        while (!(u[0] & 1)) {
+            w_shr1<W>(u, 0);
+            w_shr1<W>(x1, (x1[0] & 1) ? w_add<W>(x1, p) : 0u);  // x1 / 2 mod p
+        }
+        while (!(v[0] & 1)) {
+            w_shr1<W>(v, 0);
+            w_shr1<W>(x2, (x2[0] & 1) ? w_add<W>(x2, p) : 0u);
+        }
+        if (w_ge<W>(u, v)) {
+            w_sub<W>(u, v);
+            if (w_sub<W>(x1, x2)) w_add<W>(x1, p);
+        } else {
+            w_sub<W>(v, u);
+            if (w_sub<W>(x2, x1)) w_add<W>(x2, p);
+        }
+    }
+    const uint32_t *r = w_is<W>(u, 1) ? x1 : x2;
+    for (int i = 0; i < W; i++) out[i] = r[i];
+}
+
+// One FieldOpCols of x op y in the base field (x, y: W words, reduced here; op 0 add, 1 sub, 2 mul, 3 div),
+// its result r (mod p) into res (nullable) -- FieldOpCols::populate_with_modulus as pop_field_op: sub is
+// populated as r + y = x + carry p, div as r y = x + carry p (r = 0 for 0 / 0)
 template <int W, int NW, int OFF>
 __device__ inline void fp_op(uint32_t *o, const uint32_t *x, const uint32_t *y, uint32_t op, const FpMod &mod,
                              uint32_t *bm, uint32_t *res) {
     constexpr int NL = 4 * W;
-    uint32_t a[W], b[W];
+    uint32_t a[W], b[W], lhs[W], full[2 * W], mres[W], car[W];
     mod_words<W, W>(x, mod.w, a, nullptr);
     mod_words<W, W>(y, mod.w, b, nullptr);
-    uint32_t r[W], lhs[W], full[2 * W], mres[W], car[W];
-    for (int i = 0; i < W; i++) car[i] = 0;
+    const bool mul = op >= 2;
+    if (op == 1) {  // r = a + p - b mod p (a + p - b < 2p: one conditional subtraction)
+        for (int i = 0; i < W; i++) lhs[i] = a[i];
+        const uint32_t c = w_add<W>(lhs, mod.w);
+        const uint32_t bw = w_sub<W>(lhs, b);
+        uint32_t t[W];
+        for (int i = 0; i < W; i++) t[i] = lhs[i];
+        if ((c != bw) || w_ge<W>(t, mod.w)) w_sub<W>(lhs, mod.w);  // value >= p
+    } else if (op == 3) {  // r = a / b
+        for (int i = 0; i < W; i++) lhs[i] = 0;
+        if (!w_is<W>(b, 0)) {
+            uint32_t ib[W], pr[2 * W];
+            modinv<W>(b, mod.w, ib);
+            for (int i = 0; i < 2 * W; i++) pr[i] = 0;
+            for (int i = 0; i < W; i++) {
+                uint64_t c = 0;
+                for (int j = 0; j < W; j++) {
+                    const uint64_t t = (uint64_t)a[i] * ib[j] + pr[i + j] + c;
+                    pr[i + j] = (uint32_t)t;
+                    c = t >> 32;
+                }
+                pr[i + W] = (uint32_t)c;
+            }
+            mod_words<2 * W, W>(pr, mod.w, lhs, nullptr);
+        }
+    } else {
+        for (int i = 0; i < W; i++) lhs[i] = a[i];
+    }
     for (int i = 0; i < 2 * W; i++) full[i] = 0;
-    if (op == 2) {  // mul: a b = carry m + result
+    for (int i = 0; i < W; i++) car[i] = 0;
+    if (mul) {  // lhs b = carry p + mres
         for (int i = 0; i < W; i++) {
             uint64_t c = 0;
             for (int j = 0; j < W; j++) {
-                const uint64_t t = (uint64_t)a[i] * b[j] + full[i + j] + c;
+                const uint64_t t = (uint64_t)lhs[i] * b[j] + full[i + j] + c;
                 full[i + j] = (uint32_t)t;
                 c = t >> 32;
             }
             full[i + W] = (uint32_t)c;
         }
         mod_words<2 * W, W>(full, mod.w, mres, car);
-        for (int i = 0; i < W; i++) {
-            r[i] = mres[i];
-            lhs[i] = a[i];
-        }
-    } else {
-        if (op == 1) {  // sub: r = a - b mod m, populated as r + b = a + carry m
-            uint64_t c = 0;
-            uint32_t t[W + 1];
-            for (int i = 0; i < W; i++) {  // a + m - b (< 2m)
-                const uint64_t s_ = (uint64_t)a[i] + mod.w[i] + c;
-                t[i] = (uint32_t)s_;
-                c = s_ >> 32;
-            }
-            t[W] = (uint32_t)c;
-            int64_t bw = 0;
-            for (int i = 0; i <= W; i++) {
-                const int64_t d = (int64_t)t[i] - (i < W ? b[i] : 0u) - bw;
-                t[i] = (uint32_t)d;
-                bw = d < 0;
-            }
-            uint32_t rr[W];
-            mod_words<W + 1, W>(t, mod.w, rr, nullptr);
-            for (int i = 0; i < W; i++) r[i] = lhs[i] = rr[i];
-        } else {
-            for (int i = 0; i < W; i++) r[i] = lhs[i] = a[i];
-        }
-        uint64_t c = 0;  // lhs + b
-        for (int i = 0; i < W; i++) {
-            const uint64_t s_ = (uint64_t)lhs[i] + b[i] + c;
-            full[i] = (uint32_t)s_;
-            c = s_ >> 32;
-        }
-        full[W] = (uint32_t)c;
+    } else {  // lhs + b
+        for (int i = 0; i < W; i++) full[i] = lhs[i];
+        full[W] = w_add<W>(full, b);
         mod_words<W + 1, W>(full, mod.w, mres, car);
-        if (op == 0)
-            for (int i = 0; i < W; i++) r[i] = mres[i];
     }
-    field_op_cols<NL, NW, OFF>(o, lhs, b, op == 2, r, mres, car, mod.w, bm);
+    // the result column: add / mul the reduced value, sub / div the populated left-hand side
+    const uint32_t *r = (op == 1 || op == 3) ? lhs : mres;
+    field_op_cols<NL, NW, OFF>(o, lhs, b, mul, r, mres, car, mod.w, bm);
     if (res)
         for (int i = 0; i < W; i++) res[i] = r[i];
 }
@@ -1900,6 +1971,62 @@ __global__ __launch_bounds__(128) void k_fp2_rows(const uint32_t *__restrict__ e
         fp_op<W, NW, OFF>(v + OUT + 4 * FW, r00, r11, 1, mod, bm, nullptr);
         fp_op<W, NW, OFF>(v + OUT + 5 * FW, r01, r10, 0, mod, bm, nullptr);
     }
+}
+
+// WeierstrassAddAssign (weierstrass_add.rs:192-252, :384-420): is_real, shard, clk, p_ptr, q_ptr, p (2W writes),
+// q (2W reads), nine FieldOpCols in column order slope_denominator = qx - px, slope_numerator = qy - py,
+// slope = num / den, slope_squared, p_x_plus_q_x, x3_ins = s^2 - (px + qx), p_x_minus_x = px - x3,
+// y3_ins = s (px - x3) - py, slope_times_p_x_minus_x; padding rows: the operations on zero inputs.
+// zkm_ec_add_event dwords: shard, clk, p_ptr, q_ptr, q reads (24 x 5), p writes (24 x 6)
+enum { EA_EV = 4 + 120 + 144 };
+template <int W, int NW, int OFF>
+__global__ __launch_bounds__(128) void k_ec_add_rows(const uint32_t *__restrict__ ev, uint64_t n, uint32_t *__restrict__ out,
+                                                     uint64_t height, FpMod mod, uint32_t *bm) {
+    constexpr int NL = 4 * W, FW = 2 * NL + 2 * NW, PC = 5, QC = PC + 2 * W * 13, OUT = QC + 2 * W * 9, WIDTH = OUT + 9 * FW;
+    enum { DEN = 0, NUM, SLOPE, S2, PXQX, X3, PMX, Y3, STP };
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WIDTH;
+    for (int c = 0; c < WIDTH; c++) v[c] = 0;
+    if (row >= n) {
+        for (int k = 0; k < 9; k++)
+            for (int j = 0; j < NW; j++) {
+                v[OUT + k * FW + 2 * NL + j] = OFF & 0xFF;
+                v[OUT + k * FW + 2 * NL + NW + j] = OFF >> 8;
+            }
+        return;
+    }
+    const uint32_t *e = ev + row * EA_EV;
+    v[0] = 1;
+    v[1] = e[0];
+    v[2] = e[1];
+    v[3] = e[2];
+    v[4] = e[3];
+    uint32_t pw[2 * W], qw[2 * W];
+    for (int i = 0; i < 2 * W; i++) {
+        const Access qa = access_read(e + 4 + 5 * i), pa = access_write(e + 124 + 6 * i);
+        qw[i] = qa.value;
+        pw[i] = pa.prev_value;
+        put_access(v, QC + 9 * i, qa);
+        put_word(v + PC + 13 * i, pa.prev_value);
+        put_access(v, PC + 13 * i + 4, pa);
+        const Access as[2] = {qa, pa};
+        for (int k = 0; k < 2; k++) {
+            byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
+            byte_add(bm, B_U8RANGE, 0, as[k].d8);
+        }
+    }
+    const uint32_t *px = pw, *py = pw + W, *qx = qw, *qy = qw + W;
+    uint32_t num[W], den[W], slope[W], s2[W], pq[W], x3[W], pmx[W], stp[W];
+    fp_op<W, NW, OFF>(v + OUT + NUM * FW, qy, py, 1, mod, bm, num);
+    fp_op<W, NW, OFF>(v + OUT + DEN * FW, qx, px, 1, mod, bm, den);
+    fp_op<W, NW, OFF>(v + OUT + SLOPE * FW, num, den, 3, mod, bm, slope);
+    fp_op<W, NW, OFF>(v + OUT + S2 * FW, slope, slope, 2, mod, bm, s2);
+    fp_op<W, NW, OFF>(v + OUT + PXQX * FW, px, qx, 0, mod, bm, pq);
+    fp_op<W, NW, OFF>(v + OUT + X3 * FW, s2, pq, 1, mod, bm, x3);
+    fp_op<W, NW, OFF>(v + OUT + PMX * FW, px, x3, 1, mod, bm, pmx);
+    fp_op<W, NW, OFF>(v + OUT + STP * FW, slope, pmx, 2, mod, bm, stp);
+    fp_op<W, NW, OFF>(v + OUT + Y3 * FW, stp, py, 1, mod, bm, nullptr);
 }
 
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
@@ -2573,6 +2700,30 @@ int zkm_fp2_events_to_trace(int field, int mul, const zkm_fp2_event *events, uin
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_fp2_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_ec_add_events_to_trace(int curve, const zkm_ec_add_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                               uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_ec_add_event) == 4 * EA_EV, "EllipticCurveAddEvent record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1)) || curve < 0 || curve > 3) {
+        g_last_error = "zkm_ec_add_events_to_trace: bad arguments (need n <= height, a power of two >= 16, a known curve)";
+        return ZKM_ERR_ARG;
+    }
+    const dim3 grid((unsigned)((height + 127) / 128)), block(128);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t *ev = (const uint32_t *)events;
+    if (curve == ZKM_CURVE_BLS12381)
+        hipLaunchKernelGGL((k_ec_add_rows<12, 94, 1 << 15>), grid, block, 0, s, ev, n, trace, height, kBls, byte_mult);
+    else
+        hipLaunchKernelGGL((k_ec_add_rows<8, 62, 1 << 14>), grid, block, 0, s, ev, n, trace, height,
+                           curve == ZKM_CURVE_SECP256K1 ? kSecp256k1 : curve == ZKM_CURVE_SECP256R1 ? kSecp256r1 : kBn254,
+                           byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_ec_add_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;
