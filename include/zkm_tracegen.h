@@ -323,6 +323,17 @@ typedef struct {
 int zkm_ec_add_events_to_trace(int curve, const zkm_ec_add_event *events, uint64_t n, uint32_t *trace, uint64_t height,
                                uint32_t *byte_mult, void *stream);
 
+/* WeierstrassDoubleAssign on the same curves (weierstrass/weierstrass_double.rs:201-270, :411-440):
+ * EllipticCurveDoubleEvent as one fixed record: shard, clk, p_ptr, the writes of p at clk (16 or 24 words, in
+ * slots of 24).  Each row: the accesses and the eleven FieldOpCols of the affine doubling; padding rows: the
+ * operations of p = (0, 1) and the dummy write record of y's first word.  byte_mult (nullable) as above. */
+typedef struct {
+    uint32_t shard, clk, p_ptr;
+    zkm_memory_write_record p[24];
+} zkm_ec_double_event;  /* 588 bytes */
+int zkm_ec_double_events_to_trace(int curve, const zkm_ec_double_event *events, uint64_t n, uint32_t *trace,
+                                  uint64_t height, uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

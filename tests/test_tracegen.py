@@ -835,6 +835,52 @@ def test_ec_add_shard_from_device_traces(curve):
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 
+def _ec_double_events(curve: str, seed: int = 29):
+    """Weierstrass doublings of random points through the executor (mips_ec.exec_ec_double)."""
+    from zkmips_amd import mips_ec as EC
+    rng = np.random.default_rng(seed)
+    words = {}
+    mem, mem_init, mem_last = {}, {}, {}
+    evs = []
+    for k in range(20):
+        pp = 0x80000 + 0x200 * k
+        for i, w in enumerate(EC.point_words(curve, EC.random_point(curve, rng))):
+            words[pp + 4 * i] = w
+        shard, clk = 3 + k // 12, 130 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: words.get(a, 0))
+        evs.append((EC.EC_DOUBLE[curve], (shard, clk, SY.syscall_id(EC.EC_DOUBLE[curve]), pp, 0),
+                    EC.exec_ec_double(curve, pm, shard, clk, pp, 0)))
+    return evs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("curve", ["Secp256k1", "Secp256r1", "Bn254", "Bls12381"])
+def test_ec_double_shard_from_device_traces(curve):
+    """Weierstrass doubling shards built on the device (eleven chained field ops; padding rows double
+    (0, 1) with the dummy y record) equal the host builders' traces and multiplicities and prove to the same
+    bytes."""
+    import torch
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _ec_double_events(curve)
+    key = evs[0][0]
+    m, prep, tr, pv = MC.precompile_shard(key, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(key, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert f"{curve}DoubleAssign" in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

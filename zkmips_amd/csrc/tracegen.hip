@@ -2029,6 +2029,66 @@ __global__ __launch_bounds__(128) void k_ec_add_rows(const uint32_t *__restrict_
     fp_op<W, NW, OFF>(v + OUT + Y3 * FW, stp, py, 1, mod, bm, nullptr);
 }
 
+// WeierstrassDoubleAssign (weierstrass_double.rs:201-270, :411-440): is_real, shard, clk, p_ptr, p (2W writes
+// at clk), eleven FieldOpCols in column order slope_denominator = 2 py, slope_numerator = a + 3 px^2, slope,
+// p_x_squared, p_x_squared_times_3, slope_squared, p_x_plus_p_x, x3_ins, p_x_minus_x, y3_ins,
+// slope_times_p_x_minus_x.  Padding rows: the operations of p = (0, 1) (no lookups) and the dummy write
+// record of the first y word (prev_value 1, value 1, compare 1).  zkm_ec_double_event dwords: shard, clk,
+// p_ptr, p writes (24 x 6)
+enum { ED2_EV = 3 + 144 };
+template <int W, int NW, int OFF>
+__global__ __launch_bounds__(128) void k_ec_double_rows(const uint32_t *__restrict__ ev, uint64_t n,
+                                                        uint32_t *__restrict__ out, uint64_t height, FpMod mod,
+                                                        FpMod curve_a, uint32_t *bm) {
+    constexpr int NL = 4 * W, FW = 2 * NL + 2 * NW, PC = 4, OUT = PC + 2 * W * 13, WIDTH = OUT + 11 * FW;
+    enum { DEN = 0, NUM, SLOPE, X2, X23, S2, PP, X3, PMX, Y3, STP };
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WIDTH;
+    for (int c = 0; c < WIDTH; c++) v[c] = 0;
+    const bool real = row < n;
+    uint32_t *b = real ? bm : nullptr;  // padding rows record no lookups
+    uint32_t pw[2 * W];
+    for (int i = 0; i < 2 * W; i++) pw[i] = 0;
+    if (real) {
+        const uint32_t *e = ev + row * ED2_EV;
+        v[0] = 1;
+        v[1] = e[0];
+        v[2] = e[1];
+        v[3] = e[2];
+        for (int i = 0; i < 2 * W; i++) {
+            const Access pa = access_write(e + 3 + 6 * i);
+            pw[i] = pa.prev_value;
+            put_word(v + PC + 13 * i, pa.prev_value);
+            put_access(v, PC + 13 * i + 4, pa);
+            byte_add(bm, B_U16RANGE, pa.d16 >> 8, pa.d16 & 0xFF);
+            byte_add(bm, B_U8RANGE, 0, pa.d8);
+        }
+    } else {  // p = (0, 1) and the dummy record of y's first word
+        pw[W] = 1;
+        v[PC + 13 * W] = 1;
+        v[PC + 13 * W + 4 + ACC_VALUE] = 1;
+        v[PC + 13 * W + 4 + ACC_COMPARE] = 1;
+    }
+    const uint32_t *px = pw, *py = pw + W;
+    uint32_t k2[W], k3[W];
+    for (int i = 0; i < W; i++) k2[i] = k3[i] = 0;
+    k2[0] = 2;
+    k3[0] = 3;
+    uint32_t x2[W], x23[W], num[W], den[W], slope[W], s2[W], pp[W], x3[W], pmx[W], stp[W];
+    fp_op<W, NW, OFF>(v + OUT + X2 * FW, px, px, 2, mod, b, x2);
+    fp_op<W, NW, OFF>(v + OUT + X23 * FW, x2, k3, 2, mod, b, x23);
+    fp_op<W, NW, OFF>(v + OUT + NUM * FW, curve_a.w, x23, 0, mod, b, num);
+    fp_op<W, NW, OFF>(v + OUT + DEN * FW, k2, py, 2, mod, b, den);
+    fp_op<W, NW, OFF>(v + OUT + SLOPE * FW, num, den, 3, mod, b, slope);
+    fp_op<W, NW, OFF>(v + OUT + S2 * FW, slope, slope, 2, mod, b, s2);
+    fp_op<W, NW, OFF>(v + OUT + PP * FW, px, px, 0, mod, b, pp);
+    fp_op<W, NW, OFF>(v + OUT + X3 * FW, s2, pp, 1, mod, b, x3);
+    fp_op<W, NW, OFF>(v + OUT + PMX * FW, px, x3, 1, mod, b, pmx);
+    fp_op<W, NW, OFF>(v + OUT + STP * FW, slope, pmx, 2, mod, b, stp);
+    fp_op<W, NW, OFF>(v + OUT + Y3 * FW, stp, py, 1, mod, b, nullptr);
+}
+
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
 // SysLinuxCols (sys_linux/columns.rs); zkm_sys_linux_event dwords: shard, clk, code, a0, a1, result, the A3
 // write, the io record
@@ -2724,6 +2784,34 @@ int zkm_ec_add_events_to_trace(int curve, const zkm_ec_add_event *events, uint64
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_ec_add_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_ec_double_events_to_trace(int curve, const zkm_ec_double_event *events, uint64_t n, uint32_t *trace,
+                                  uint64_t height, uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_ec_double_event) == 4 * ED2_EV, "EllipticCurveDoubleEvent record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1)) || curve < 0 || curve > 3) {
+        g_last_error = "zkm_ec_double_events_to_trace: bad arguments (need n <= height, a power of two >= 16, a known curve)";
+        return ZKM_ERR_ARG;
+    }
+    // the curves' a: 0 except secp256r1 (p - 3)
+    constexpr FpMod a0{{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
+    constexpr FpMod a_r1{{0xfffffffcu, 0xffffffffu, 0xffffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000001u,
+                          0xffffffffu, 0, 0, 0, 0}};
+    const dim3 grid((unsigned)((height + 127) / 128)), block(128);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t *ev = (const uint32_t *)events;
+    if (curve == ZKM_CURVE_BLS12381)
+        hipLaunchKernelGGL((k_ec_double_rows<12, 94, 1 << 15>), grid, block, 0, s, ev, n, trace, height, kBls, a0, byte_mult);
+    else
+        hipLaunchKernelGGL((k_ec_double_rows<8, 62, 1 << 14>), grid, block, 0, s, ev, n, trace, height,
+                           curve == ZKM_CURVE_SECP256K1 ? kSecp256k1 : curve == ZKM_CURVE_SECP256R1 ? kSecp256r1 : kBn254,
+                           curve == ZKM_CURVE_SECP256R1 ? a_r1 : a0, byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_ec_double_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;
