@@ -334,6 +334,20 @@ typedef struct {
 int zkm_ec_double_events_to_trace(int curve, const zkm_ec_double_event *events, uint64_t n, uint32_t *trace,
                                   uint64_t height, uint32_t *byte_mult, void *stream);
 
+/* WeierstrassDecompress on secp256k1 / secp256r1 / bls12-381 (weierstrass/weierstrass_decompress.rs:161-303):
+ * EllipticCurveDecompressEvent as one fixed record: shard, clk, ptr, sign, the reads of x (at ptr + nl) and
+ * the writes of y (at ptr), both at clk (8 or 12 words, in slots of 12).  Each row: the accesses, x < p,
+ * x^2, x^3, a x + b, the square root of x^3 + a x + b (a^((p+1)/4) on the device), its range and lsb, -y,
+ * and for bls12-381 the lexicographic choice columns; padding rows decompress the generator's x.  byte_mult
+ * (nullable) as above. */
+typedef struct {
+    uint32_t shard, clk, ptr, sign;
+    zkm_memory_read_record x[12];
+    zkm_memory_write_record y[12];
+} zkm_ec_decompress_event;  /* 544 bytes */
+int zkm_ec_decompress_events_to_trace(int curve, const zkm_ec_decompress_event *events, uint64_t n, uint32_t *trace,
+                                      uint64_t height, uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

@@ -881,6 +881,55 @@ def test_ec_double_shard_from_device_traces(curve):
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 
+def _ec_decompress_events(curve: str, seed: int = 31):
+    """Weierstrass decompressions through the executor (mips_ec.exec_ec_decompress): random points' x with
+    both signs."""
+    from zkmips_amd import emulated_field as EF
+    from zkmips_amd import mips_ec as EC
+    rng = np.random.default_rng(seed)
+    fp = EC.FIELDS[curve]
+    words = {}
+    mem, mem_init, mem_last = {}, {}, {}
+    evs = []
+    for k in range(20):
+        ptr = 0x90000 + 0x200 * k
+        for i, w in enumerate(EF.int_to_words(EC.random_point(curve, rng)[0], fp.words)):
+            words[ptr + fp.nl + 4 * i] = w
+        shard, clk = 3 + k // 12, 150 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: words.get(a, 0))
+        evs.append((EC.EC_DECOMPRESS[curve], (shard, clk, SY.syscall_id(EC.EC_DECOMPRESS[curve]), ptr, k % 2),
+                    EC.exec_ec_decompress(curve, pm, shard, clk, ptr, k % 2)))
+    return evs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("curve", ["Secp256k1", "Secp256r1", "Bls12381"])
+def test_ec_decompress_shard_from_device_traces(curve):
+    """Weierstrass decompression shards built on the device (the square root by exponentiation, the inner
+    product a x + b, bls12-381's lexicographic choice) equal the host builders' traces and multiplicities
+    and prove to the same bytes."""
+    import torch
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _ec_decompress_events(curve)
+    key = evs[0][0]
+    m, prep, tr, pv = MC.precompile_shard(key, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(key, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert f"{curve}Decompress" in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

@@ -1686,21 +1686,13 @@ __device__ inline void mod_words(const uint32_t *x, const uint32_t *m, uint32_t 
 // FieldOpCols<NL bytes, NW witness limbs> at o: result `res_col`, carry, and the witness of the vanishing
 // polynomial of a (op) b + c - mres - carry m, op = mul or add (field_op.rs populate_with_modulus: sub and div
 // are populated as additions / products of the result); U8 range checks into bm
+// FieldOpCols-shaped columns at o from a vanishing polynomial van (NW + 1 coefficients): result `res_col`,
+// carry, the witness limbs of van / (X - 256) shifted by the offset, and the U8 range checks of the four limb
+// groups (pairs, a trailing single with 0) into bm; `u8res` (nullable) replaces the result limbs in the range
+// check (FieldSqrtCols checks its multiplication's result)
 template <int NL, int NW, int OFF>
-__device__ inline void field_op_cols(uint32_t *o, const uint32_t *a, const uint32_t *b, bool mul, const uint32_t *res_col,
-                                     const uint32_t *mres, const uint32_t *car, const uint32_t *m, uint32_t *bm) {
-    int64_t van[NW + 1];
-    for (int k = 0; k <= NW; k++) van[k] = 0;
-    for (int i = 0; i < NL; i++) {
-        const int64_t ai = byte_of(a[i >> 2], i & 3), ci = byte_of(car[i >> 2], i & 3);
-        if (mul) {
-            for (int j = 0; j < NL; j++) van[i + j] += ai * (int64_t)byte_of(b[j >> 2], j & 3);
-        } else {
-            van[i] += ai + (int64_t)byte_of(b[i >> 2], i & 3);
-        }
-        for (int j = 0; j < NL; j++) van[i + j] -= ci * (int64_t)byte_of(m[j >> 2], j & 3);
-        van[i] -= byte_of(mres[i >> 2], i & 3);
-    }
+__device__ inline void field_cols(uint32_t *o, const int64_t *van, const uint32_t *res_col, const uint32_t *car,
+                                  uint32_t *bm, const uint32_t *u8res = nullptr) {
     int64_t qw = van[NW];
     uint32_t *Wc = o + 2 * NL;
     for (int k = NW - 1; k >= 0; k--) {
@@ -1716,9 +1708,40 @@ __device__ inline void field_op_cols(uint32_t *o, const uint32_t *a, const uint3
     for (int blk = 0; blk < 4; blk++) {
         const uint32_t *g = o + (blk < 2 ? NL * blk : 2 * NL + NW * (blk - 2));
         const int len = blk < 2 ? NL : NW;
-        for (int j = 0; j + 1 < len; j += 2) byte_add(bm, B_U8RANGE, g[j], g[j + 1]);
+        for (int j = 0; j + 1 < len; j += 2) {
+            if (blk == 0 && u8res) byte_add(bm, B_U8RANGE, byte_of(u8res[j >> 2], j & 3), byte_of(u8res[(j + 1) >> 2], (j + 1) & 3));
+            else byte_add(bm, B_U8RANGE, g[j], g[j + 1]);
+        }
         if (len & 1) byte_add(bm, B_U8RANGE, g[len - 1], 0);
     }
+}
+
+// van += sign a(X) b(X) over byte limbs
+template <int NL, int NW>
+__device__ inline void van_mul(int64_t *van, const uint32_t *a, const uint32_t *b, int sign) {
+    for (int i = 0; i < NL; i++) {
+        const int64_t ai = sign * (int64_t)byte_of(a[i >> 2], i & 3);
+        for (int j = 0; j < NL; j++) van[i + j] += ai * (int64_t)byte_of(b[j >> 2], j & 3);
+    }
+}
+
+// FieldOpCols<NL bytes, NW witness limbs> at o: result `res_col`, carry, and the witness of the vanishing
+// polynomial of a (op) b - mres - carry m, op = mul or add (field_op.rs populate_with_modulus: sub and div
+// are populated as additions / products of the result); U8 range checks into bm
+template <int NL, int NW, int OFF>
+__device__ inline void field_op_cols(uint32_t *o, const uint32_t *a, const uint32_t *b, bool mul, const uint32_t *res_col,
+                                     const uint32_t *mres, const uint32_t *car, const uint32_t *m, uint32_t *bm,
+                                     const uint32_t *u8res = nullptr) {
+    int64_t van[NW + 1];
+    for (int k = 0; k <= NW; k++) van[k] = 0;
+    if (mul) {
+        van_mul<NL, NW>(van, a, b, 1);
+    } else {
+        for (int i = 0; i < NL; i++) van[i] += (int64_t)byte_of(a[i >> 2], i & 3) + byte_of(b[i >> 2], i & 3);
+    }
+    van_mul<NL, NW>(van, car, m, -1);
+    for (int i = 0; i < NL; i++) van[i] -= byte_of(mres[i >> 2], i & 3);
+    field_cols<NL, NW, OFF>(o, van, res_col, car, bm, u8res);
 }
 
 // FpOpCols: is_real, shard, clk, is_add, is_sub, is_mul, x_ptr, y_ptr, x (W MemoryWriteCols), y (W
@@ -1736,6 +1759,18 @@ constexpr FpMod kSecp256k1{{0xfffffc2fu, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 
                             0xffffffffu, 0, 0, 0, 0}};
 constexpr FpMod kSecp256r1{{0xffffffffu, 0xffffffffu, 0xffffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000001u,
                             0xffffffffu, 0, 0, 0, 0}};
+constexpr FpMod kSqrtExpK1{{0xbfffff0cu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x3fffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kGenXK1{{0x16f81798u, 0x59f2815bu, 0x2dce28d9u, 0x029bfcdbu, 0xce870b07u, 0x55a06295u, 0xf9dcbbacu, 0x79be667eu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kCurveAK1{{0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kCurveBK1{{0x00000007u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kSqrtExpR1{{0x00000000u, 0x00000000u, 0x40000000u, 0x00000000u, 0x00000000u, 0x40000000u, 0xc0000000u, 0x3fffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kGenXR1{{0xd898c296u, 0xf4a13945u, 0x2deb33a0u, 0x77037d81u, 0x63a440f2u, 0xf8bce6e5u, 0xe12c4247u, 0x6b17d1f2u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kCurveAR1{{0xfffffffcu, 0xffffffffu, 0xffffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kCurveBR1{{0x27d2604bu, 0x3bce3c3eu, 0xcc53b0f6u, 0x651d06b0u, 0x769886bcu, 0xb3ebbd55u, 0xaa3a93e7u, 0x5ac635d8u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kSqrtExpBLS{{0xffffeaabu, 0xee7fbfffu, 0xac54ffffu, 0x07aaffffu, 0x3dac3d89u, 0xd9cc34a8u, 0x3ce144afu, 0xd91dd2e1u, 0x90d2eb35u, 0x92c6e9edu, 0x8e5ff9a6u, 0x0680447au}};
+constexpr FpMod kGenXBLS{{0xdb22c6bbu, 0xfb3af00au, 0xf97a1aefu, 0x6c55e83fu, 0x171bac58u, 0xa14e3a3fu, 0x9774b905u, 0xc3688c4fu, 0x4fa9ac0fu, 0x2695638cu, 0x3197d794u, 0x17f1d3a7u}};
+constexpr FpMod kCurveABLS{{0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kCurveBBLS{{0x00000004u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
 constexpr FpMod kBls{{0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu,
                       0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau}};
 // W-word helpers for the modular inverse (binary extended Euclid; p odd)
@@ -2087,6 +2122,187 @@ __global__ __launch_bounds__(128) void k_ec_double_rows(const uint32_t *__restri
     fp_op<W, NW, OFF>(v + OUT + PMX * FW, px, x3, 1, mod, b, pmx);
     fp_op<W, NW, OFF>(v + OUT + STP * FW, slope, pmx, 2, mod, b, stp);
     fp_op<W, NW, OFF>(v + OUT + Y3 * FW, stp, py, 1, mod, b, nullptr);
+}
+
+// W-word modular multiplication and exponentiation (square and multiply over the exponent's bits)
+template <int W>
+__device__ inline void mulmod(const uint32_t *a, const uint32_t *b, const uint32_t *m, uint32_t *r) {
+    uint32_t pr[2 * W];
+    for (int i = 0; i < 2 * W; i++) pr[i] = 0;
+    for (int i = 0; i < W; i++) {
+        uint64_t c = 0;
+        for (int j = 0; j < W; j++) {
+            const uint64_t t = (uint64_t)a[i] * b[j] + pr[i + j] + c;
+            pr[i + j] = (uint32_t)t;
+            c = t >> 32;
+        }
+        pr[i + W] = (uint32_t)c;
+    }
+    mod_words<2 * W, W>(pr, m, r, nullptr);
+}
+template <int W>
+__device__ inline void powmod(const uint32_t *a, const uint32_t *e, const uint32_t *m, uint32_t *r) {
+    uint32_t acc[W];
+    for (int i = 0; i < W; i++) acc[i] = i == 0;
+    for (int bit = 32 * W - 1; bit >= 0; bit--) {
+        mulmod<W>(acc, acc, m, acc);
+        if ((e[bit >> 5] >> (bit & 31)) & 1) mulmod<W>(acc, a, m, acc);
+    }
+    for (int i = 0; i < W; i++) r[i] = acc[i];
+}
+
+// FieldLtCols at o for lhs < rhs (the most significant differing byte), its LTU lookup into bm
+template <int NL>
+__device__ inline void field_lt(uint32_t *o, const uint32_t *lhs, const uint32_t *rhs, uint32_t *bm) {
+    for (int k = NL - 1; k >= 0; k--) {
+        const uint32_t a = byte_of(lhs[k >> 2], k & 3), b = byte_of(rhs[k >> 2], k & 3);
+        if (a != b) {
+            if (a < b) {
+                o[k] = 1;
+                o[NL] = a;
+                o[NL + 1] = b;
+            }
+            break;
+        }
+    }
+    byte_add(bm, B_LTU, o[NL], o[NL + 1]);
+}
+
+// WeierstrassDecompress (weierstrass_decompress.rs:161-303): is_real, shard, clk, ptr, sign, x (W reads), y (W
+// writes at clk), range_x (x < p), x^2, x^3, a x + b (FieldInnerProductCols), x^3 + a x + b, FieldSqrtCols
+// (the root times itself, the root in its result; range; lsb), -y; bls12-381 adds LexicographicChoiceCols.
+// Padding rows decompress the generator's x (its words as the x reads' values) without lookups.
+// zkm_ec_decompress_event dwords: shard, clk, ptr, sign, x reads (12 x 5), y writes (12 x 6)
+enum { EDC_EV = 4 + 60 + 72 };
+struct CurveConsts {
+    FpMod p, sqrt_exp, gen_x, a, b;
+};
+template <int W, int NW, int OFF, bool LEX>
+__global__ __launch_bounds__(128) void k_ec_decompress_rows(const uint32_t *__restrict__ ev, uint64_t n,
+                                                            uint32_t *__restrict__ out, uint64_t height, CurveConsts cc,
+                                                            uint32_t *bm) {
+    constexpr int NL = 4 * W, FW = 2 * NL + 2 * NW, LW = NL + 2, XC = 5, YC = XC + 9 * W, RX = YC + 13 * W, X2 = RX + LW,
+                  X3 = X2 + FW, AXB = X3 + FW, X3AXB = AXB + FW, SQ = X3AXB + FW, SQR = SQ + FW, LSB = SQR + LW,
+                  NEGY = LSB + 1, CMP = NEGY + FW, NEGR = CMP + LW, ISEQ = NEGR + LW, WSQ = ISEQ + 1, WNEG = WSQ + 1,
+                  WIDTH = LEX ? WNEG + 1 : NEGY + FW;
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WIDTH;
+    for (int c = 0; c < WIDTH; c++) v[c] = 0;
+    const bool real = row < n;
+    uint32_t *b = real ? bm : nullptr;
+    const uint32_t *m = cc.p.w;
+    const uint32_t *e = ev + row * EDC_EV;
+    uint32_t x[W], y[W];
+    for (int i = 0; i < W; i++) y[i] = 0;
+    if (real) {
+        v[0] = 1;
+        v[1] = e[0];
+        v[2] = e[1];
+        v[3] = e[2];
+        v[4] = e[3];
+        for (int i = 0; i < W; i++) {
+            const Access xa = access_read(e + 4 + 5 * i), ya = access_write(e + 64 + 6 * i);
+            x[i] = xa.value;
+            y[i] = ya.value;
+            put_access(v, XC + 9 * i, xa);
+            put_word(v + YC + 13 * i, ya.prev_value);
+            put_access(v, YC + 13 * i + 4, ya);
+            const Access as[2] = {xa, ya};
+            for (int k = 0; k < 2; k++) {
+                byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
+                byte_add(bm, B_U8RANGE, 0, as[k].d8);
+            }
+        }
+    } else {
+        for (int i = 0; i < W; i++) {
+            x[i] = cc.gen_x.w[i];
+            put_word(v + XC + 9 * i + ACC_VALUE, x[i]);
+        }
+    }
+    field_lt<NL>(v + RX, x, m, b);
+    uint32_t x2[W], x3[W], axb[W], rhs[W], sq[W], zero[W], one[W];
+    for (int i = 0; i < W; i++) zero[i] = one[i] = 0;
+    one[0] = 1;
+    fp_op<W, NW, OFF>(v + X2, x, x, 2, cc.p, b, x2);
+    fp_op<W, NW, OFF>(v + X3, x2, x, 2, cc.p, b, x3);
+    {  // a x + b 1 (field_inner_product.rs populate)
+        uint32_t ip[2 * W + 1], car[W], t[2 * W];
+        for (int i = 0; i < 2 * W + 1; i++) ip[i] = 0;
+        for (int i = 0; i < W; i++) {
+            uint64_t c = 0;
+            for (int j = 0; j < W; j++) {
+                const uint64_t u = (uint64_t)cc.a.w[i] * x[j] + ip[i + j] + c;
+                ip[i + j] = (uint32_t)u;
+                c = u >> 32;
+            }
+            ip[i + W] = (uint32_t)c;
+        }
+        for (int i = 0; i < 2 * W; i++) t[i] = ip[i];
+        const uint32_t cb = w_add<W>(t, cc.b.w);
+        uint64_t c = cb;
+        for (int i = W; i < 2 * W; i++) {
+            const uint64_t u = (uint64_t)t[i] + c;
+            t[i] = (uint32_t)u;
+            c = u >> 32;
+        }
+        for (int i = 0; i < W; i++) car[i] = 0;
+        uint32_t qd[2 * W];
+        {
+            int nv = W;
+            while (m[nv - 1] == 0) nv--;
+            uint32_t rr[W];
+            for (int i = 0; i < W; i++) rr[i] = 0;
+            divmod_words<2 * W, W>(t, m, nv, qd, rr);
+            for (int i = 0; i < W; i++) {
+                axb[i] = rr[i];
+                car[i] = qd[i];
+            }
+        }
+        int64_t van[NW + 1];
+        for (int k = 0; k <= NW; k++) van[k] = 0;
+        van_mul<NL, NW>(van, cc.a.w, x, 1);
+        van_mul<NL, NW>(van, cc.b.w, one, 1);
+        van_mul<NL, NW>(van, car, m, -1);
+        for (int i = 0; i < NL; i++) van[i] -= byte_of(axb[i >> 2], i & 3);
+        field_cols<NL, NW, OFF>(v + AXB, van, axb, car, b);
+    }
+    fp_op<W, NW, OFF>(v + X3AXB, x3, axb, 0, cc.p, b, rhs);
+    powmod<W>(rhs, cc.sqrt_exp.w, m, sq);
+    {  // FieldSqrtCols: sq sq = rhs + carry p, the root in the result columns, the U8 check over rhs's limbs
+        uint32_t pr[2 * W], mres[W], car[W];
+        for (int i = 0; i < 2 * W; i++) pr[i] = 0;
+        for (int i = 0; i < W; i++) {
+            uint64_t c = 0;
+            for (int j = 0; j < W; j++) {
+                const uint64_t u = (uint64_t)sq[i] * sq[j] + pr[i + j] + c;
+                pr[i + j] = (uint32_t)u;
+                c = u >> 32;
+            }
+            pr[i + W] = (uint32_t)c;
+        }
+        for (int i = 0; i < W; i++) car[i] = 0;
+        mod_words<2 * W, W>(pr, m, mres, car);
+        field_op_cols<NL, NW, OFF>(v + SQ, sq, sq, true, sq, mres, car, m, b, rhs);
+    }
+    field_lt<NL>(v + SQR, sq, m, b);
+    v[LSB] = sq[0] & 1;
+    byte_add(b, B_AND, sq[0] & 0xFF, 1);
+    for (int j = 0; j < NL; j += 2) byte_add(b, B_U8RANGE, byte_of(sq[j >> 2], j & 3), byte_of(sq[(j + 1) >> 2], (j + 1) & 3));
+    uint32_t negy[W];
+    fp_op<W, NW, OFF>(v + NEGY, zero, sq, 1, cc.p, b, negy);
+    if (LEX && real) {
+        const bool eq = (y[0] & 1) == (sq[0] & 1), sg = e[3] != 0;
+        v[ISEQ] = eq;
+        v[WSQ] = sg ? !eq : eq;
+        v[WNEG] = sg ? eq : !eq;
+        field_lt<NL>(v + NEGR, negy, m, bm);
+        uint32_t neg[W];  // (p - y) mod p
+        for (int i = 0; i < W; i++) neg[i] = m[i];
+        w_sub<W>(neg, y);
+        if (w_ge<W>(neg, m)) w_sub<W>(neg, m);
+        field_lt<NL>(v + CMP, sg ? neg : y, sg ? y : neg, bm);
+    }
 }
 
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
@@ -2812,6 +3028,37 @@ int zkm_ec_double_events_to_trace(int curve, const zkm_ec_double_event *events, 
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_ec_double_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_ec_decompress_events_to_trace(int curve, const zkm_ec_decompress_event *events, uint64_t n, uint32_t *trace,
+                                      uint64_t height, uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_ec_decompress_event) == 4 * EDC_EV, "EllipticCurveDecompressEvent record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1)) ||
+        (curve != ZKM_CURVE_SECP256K1 && curve != ZKM_CURVE_SECP256R1 && curve != ZKM_CURVE_BLS12381)) {
+        g_last_error = "zkm_ec_decompress_events_to_trace: bad arguments (need n <= height, a power of two >= 16, "
+                       "secp256k1, secp256r1 or bls12-381)";
+        return ZKM_ERR_ARG;
+    }
+    const dim3 grid((unsigned)((height + 127) / 128)), block(128);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t *ev = (const uint32_t *)events;
+    if (curve == ZKM_CURVE_BLS12381) {
+        const CurveConsts cc{kBls, kSqrtExpBLS, kGenXBLS, kCurveABLS, kCurveBBLS};
+        hipLaunchKernelGGL((k_ec_decompress_rows<12, 94, 1 << 15, true>), grid, block, 0, s, ev, n, trace, height, cc,
+                           byte_mult);
+    } else {
+        const CurveConsts cc = curve == ZKM_CURVE_SECP256K1
+                                   ? CurveConsts{kSecp256k1, kSqrtExpK1, kGenXK1, kCurveAK1, kCurveBK1}
+                                   : CurveConsts{kSecp256r1, kSqrtExpR1, kGenXR1, kCurveAR1, kCurveBR1};
+        hipLaunchKernelGGL((k_ec_decompress_rows<8, 62, 1 << 14, false>), grid, block, 0, s, ev, n, trace, height, cc,
+                           byte_mult);
+    }
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_ec_decompress_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;
