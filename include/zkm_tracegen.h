@@ -348,6 +348,20 @@ typedef struct {
 int zkm_ec_decompress_events_to_trace(int curve, const zkm_ec_decompress_event *events, uint64_t n, uint32_t *trace,
                                       uint64_t height, uint32_t *byte_mult, void *stream);
 
+/* EdAddAssign (syscall/precompiles/edwards/ed_add.rs:111-238): the Ed25519 EllipticCurveAddEvent as one fixed
+ * record: shard, clk, p_ptr, q_ptr, the 16 reads of q at clk, the 16 writes of p at clk + 1.  Each row: the
+ * accesses, the two FieldInnerProductCols of the numerators, four FieldOpCols (x1 y1, x2 y2, f, d f) and the
+ * two FieldDenCols of x3 and y3 (inverses on the device); padding rows the operations on zero inputs.
+ * byte_mult (nullable) as above.  1861 columns. */
+typedef struct {
+    uint32_t shard, clk, p_ptr, q_ptr;
+    zkm_memory_read_record q[16];
+    zkm_memory_write_record p[16];
+} zkm_ed_add_event;  /* 720 bytes */
+#define ZKM_ED_ADD_WIDTH 1861
+int zkm_ed_add_events_to_trace(const zkm_ed_add_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                               uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

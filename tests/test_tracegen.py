@@ -930,6 +930,53 @@ def test_ec_decompress_shard_from_device_traces(curve):
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 
+def _ed_add_events(seed: int = 37):
+    """Ed25519 additions through the executor (mips_edwards.exec_ed_add): multiples of the base point,
+    a point added to itself, the identity."""
+    from zkmips_amd import mips_edwards as ED
+    rng = np.random.default_rng(seed)
+    words = {}
+    mem, mem_init, mem_last = {}, {}, {}
+    pts = [ED._scalar_mul(int(rng.integers(1, 1 << 62)), (ED.BASE_X, ED.BASE_Y)) for _ in range(8)] + [(0, 1)]
+    evs = []
+    for k in range(20):
+        p, q = pts[k % len(pts)], pts[(k * 5 + 2) % len(pts)]
+        pp, qp = 0xA0000 + 0x200 * k, 0xB0000 + 0x200 * k
+        for i, w in enumerate(ED._point_words(*p)):
+            words[pp + 4 * i] = w
+        for i, w in enumerate(ED._point_words(*q)):
+            words[qp + 4 * i] = w
+        shard, clk = 3 + k // 12, 170 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: words.get(a, 0))
+        evs.append((SY.ED_ADD, (shard, clk, SY.syscall_id(SY.ED_ADD), pp, qp), ED.exec_ed_add(pm, shard, clk, pp, qp)))
+    return evs
+
+
+@pytest.mark.gpu
+def test_ed_add_shard_from_device_traces():
+    """An ED_ADD precompile shard built on the device (inner products, products, the two denominators'
+    inverses) equals the host builders' traces and multiplicities and proves to the same bytes."""
+    import torch
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _ed_add_events()
+    m, prep, tr, pv = MC.precompile_shard(SY.ED_ADD, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(SY.ED_ADD, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert "EdAddAssign" in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

@@ -1771,6 +1771,8 @@ constexpr FpMod kSqrtExpBLS{{0xffffeaabu, 0xee7fbfffu, 0xac54ffffu, 0x07aaffffu,
 constexpr FpMod kGenXBLS{{0xdb22c6bbu, 0xfb3af00au, 0xf97a1aefu, 0x6c55e83fu, 0x171bac58u, 0xa14e3a3fu, 0x9774b905u, 0xc3688c4fu, 0x4fa9ac0fu, 0x2695638cu, 0x3197d794u, 0x17f1d3a7u}};
 constexpr FpMod kCurveABLS{{0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
 constexpr FpMod kCurveBBLS{{0x00000004u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kEd25519{{0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kEdD{{0x135978a3u, 0x75eb4dcau, 0x4141d8abu, 0x00700a4du, 0x7779e898u, 0x8cc74079u, 0x2b6ffe73u, 0x52036ceeu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
 constexpr FpMod kBls{{0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu,
                       0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau}};
 // W-word helpers for the modular inverse (binary extended Euclid; p odd)
@@ -2303,6 +2305,147 @@ __global__ __launch_bounds__(128) void k_ec_decompress_rows(const uint32_t *__re
         if (w_ge<W>(neg, m)) w_sub<W>(neg, m);
         field_lt<NL>(v + CMP, sg ? neg : y, sg ? y : neg, bm);
     }
+}
+
+// FieldInnerProductCols (field_inner_product.rs:33-94) of a0 b0 + a1 b1 and FieldDenCols (field_den.rs:33-94)
+// of a / (1 +- b) (sign: 1 + b, else 1 - b) at o, their results into res; W-word operands below p
+template <int W, int NW, int OFF>
+__device__ inline void fp_ip2(uint32_t *o, const uint32_t *a0, const uint32_t *b0, const uint32_t *a1, const uint32_t *b1,
+                              const uint32_t *m, uint32_t *bm, uint32_t *res) {
+    constexpr int NL = 4 * W;
+    uint32_t t0[2 * W], t1[2 * W + 1], car[W], r[W];
+    for (int i = 0; i < 2 * W; i++) t0[i] = t1[i] = 0;
+    t1[2 * W] = 0;
+    for (int i = 0; i < W; i++) {
+        uint64_t c = 0, d = 0;
+        for (int j = 0; j < W; j++) {
+            const uint64_t u = (uint64_t)a0[i] * b0[j] + t0[i + j] + c;
+            t0[i + j] = (uint32_t)u;
+            c = u >> 32;
+            const uint64_t v = (uint64_t)a1[i] * b1[j] + t1[i + j] + d;
+            t1[i + j] = (uint32_t)v;
+            d = v >> 32;
+        }
+        t0[i + W] = (uint32_t)c;
+        t1[i + W] = (uint32_t)d;
+    }
+    t1[2 * W] = w_add<2 * W>(t1, t0);
+    for (int i = 0; i < W; i++) car[i] = 0;
+    mod_words<2 * W + 1, W>(t1, m, r, car);
+    int64_t van[NW + 1];
+    for (int k = 0; k <= NW; k++) van[k] = 0;
+    van_mul<NL, NW>(van, a0, b0, 1);
+    van_mul<NL, NW>(van, a1, b1, 1);
+    van_mul<NL, NW>(van, car, m, -1);
+    for (int i = 0; i < NL; i++) van[i] -= byte_of(r[i >> 2], i & 3);
+    field_cols<NL, NW, OFF>(o, van, r, car, bm);
+    for (int i = 0; i < W; i++) res[i] = r[i];
+}
+template <int W, int NW, int OFF>
+__device__ inline void fp_den(uint32_t *o, const uint32_t *a, const uint32_t *b, bool sign, const FpMod &mod,
+                              uint32_t *bm, uint32_t *res) {
+    constexpr int NL = 4 * W;
+    const uint32_t *m = mod.w;
+    uint32_t den[W], one[W], r[W];
+    for (int i = 0; i < W; i++) one[i] = i == 0;
+    if (sign) {  // b + 1 mod p
+        for (int i = 0; i < W; i++) den[i] = b[i];
+    } else {     // p - b + 1 mod p
+        for (int i = 0; i < W; i++) den[i] = m[i];
+        w_sub<W>(den, b);
+    }
+    const uint32_t c = w_add<W>(den, one);
+    if (c || w_ge<W>(den, m)) w_sub<W>(den, m);
+    for (int i = 0; i < W; i++) r[i] = 0;
+    if (!w_is<W>(den, 0)) {
+        uint32_t inv[W];
+        modinv<W>(den, m, inv);
+        mulmod<W>(a, inv, m, r);
+    }
+    // lhs = b r + (sign ? r : a), rhs = sign ? a : r; carry = (lhs - rhs) / p
+    uint32_t l[2 * W + 1], q[2 * W + 1], rr[W], car[W];
+    for (int i = 0; i < 2 * W + 1; i++) l[i] = 0;
+    for (int i = 0; i < W; i++) {
+        uint64_t cc = 0;
+        for (int j = 0; j < W; j++) {
+            const uint64_t u = (uint64_t)b[i] * r[j] + l[i + j] + cc;
+            l[i + j] = (uint32_t)u;
+            cc = u >> 32;
+        }
+        l[i + W] = (uint32_t)cc;
+    }
+    uint32_t add_t[2 * W];
+    for (int i = 0; i < 2 * W; i++) add_t[i] = i < W ? (sign ? r[i] : a[i]) : 0u;
+    l[2 * W] = w_add<2 * W>(l, add_t);
+    uint32_t sub_t[2 * W + 1];
+    for (int i = 0; i < 2 * W + 1; i++) sub_t[i] = i < W ? (sign ? a[i] : r[i]) : 0u;
+    w_sub<2 * W + 1>(l, sub_t);  // lhs - rhs, a multiple of p
+    int nv = W;
+    while (m[nv - 1] == 0) nv--;
+    for (int i = 0; i < W; i++) rr[i] = 0;
+    divmod_words<2 * W + 1, W>(l, m, nv, q, rr);
+    for (int i = 0; i < W; i++) car[i] = q[i];
+    int64_t van[NW + 1];
+    for (int k = 0; k <= NW; k++) van[k] = 0;
+    van_mul<NL, NW>(van, b, r, 1);
+    for (int i = 0; i < NL; i++) {
+        const int64_t ri = byte_of(r[i >> 2], i & 3), ai = byte_of(a[i >> 2], i & 3);
+        van[i] += sign ? ri - ai : ai - ri;
+    }
+    van_mul<NL, NW>(van, car, m, -1);
+    field_cols<NL, NW, OFF>(o, van, r, car, bm);
+    for (int i = 0; i < W; i++) res[i] = r[i];
+}
+
+// EdAddAssign (edwards/ed_add.rs:111-238): is_real, shard, clk, p_ptr, q_ptr, p (16 writes at clk + 1), q (16
+// reads at clk), x3_numerator = x1 y2 + x2 y1, y3_numerator = y1 y2 + x1 x2, x1 y1, x2 y2, f = x1 y1 x2 y2,
+// d f, x3 = x3n / (1 + d f), y3 = y3n / (1 - d f); padding rows: the operations on zero inputs.
+// zkm_ed_add_event dwords: shard, clk, p_ptr, q_ptr, q reads (16 x 5), p writes (16 x 6)
+enum { EDA_EV = 4 + 80 + 96 };
+__global__ __launch_bounds__(128) void k_ed_add_rows(const uint32_t *__restrict__ ev, uint64_t n, uint32_t *__restrict__ out,
+                                                     uint64_t height, uint32_t *bm) {
+    constexpr int W = 8, NW = 62, OFF = 1 << 14, NL = 32, FW = 2 * NL + 2 * NW, PC = 5, QC = PC + 16 * 13,
+                  OUT = QC + 16 * 9, WIDTH = OUT + 8 * FW;
+    static_assert(WIDTH == ZKM_ED_ADD_WIDTH, "EdAddAssignCols layout");
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WIDTH;
+    for (int c = 0; c < WIDTH; c++) v[c] = 0;
+    const bool real = row < n;
+    uint32_t *b = real ? bm : nullptr;
+    uint32_t pw[16], qw[16];
+    for (int i = 0; i < 16; i++) pw[i] = qw[i] = 0;
+    if (real) {
+        const uint32_t *e = ev + row * EDA_EV;
+        v[0] = 1;
+        v[1] = e[0];
+        v[2] = e[1];
+        v[3] = e[2];
+        v[4] = e[3];
+        for (int i = 0; i < 16; i++) {
+            const Access qa = access_read(e + 4 + 5 * i), pa = access_write(e + 84 + 6 * i);
+            qw[i] = qa.value;
+            pw[i] = pa.prev_value;
+            put_access(v, QC + 9 * i, qa);
+            put_word(v + PC + 13 * i, pa.prev_value);
+            put_access(v, PC + 13 * i + 4, pa);
+            const Access as[2] = {qa, pa};
+            for (int k = 0; k < 2; k++) {
+                byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
+                byte_add(bm, B_U8RANGE, 0, as[k].d8);
+            }
+        }
+    }
+    const uint32_t *x1 = pw, *y1 = pw + 8, *x2 = qw, *y2 = qw + 8, *m = kEd25519.w;
+    uint32_t x3n[W], y3n[W], x1y1[W], x2y2[W], f[W], df[W], t[W];
+    fp_ip2<W, NW, OFF>(v + OUT, x1, y2, x2, y1, m, b, x3n);
+    fp_ip2<W, NW, OFF>(v + OUT + FW, y1, y2, x1, x2, m, b, y3n);
+    fp_op<W, NW, OFF>(v + OUT + 2 * FW, x1, y1, 2, kEd25519, b, x1y1);
+    fp_op<W, NW, OFF>(v + OUT + 3 * FW, x2, y2, 2, kEd25519, b, x2y2);
+    fp_op<W, NW, OFF>(v + OUT + 4 * FW, x1y1, x2y2, 2, kEd25519, b, f);
+    fp_op<W, NW, OFF>(v + OUT + 5 * FW, f, kEdD.w, 2, kEd25519, b, df);
+    fp_den<W, NW, OFF>(v + OUT + 6 * FW, x3n, df, true, kEd25519, b, t);
+    fp_den<W, NW, OFF>(v + OUT + 7 * FW, y3n, df, false, kEd25519, b, t);
 }
 
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
@@ -3059,6 +3202,23 @@ int zkm_ec_decompress_events_to_trace(int curve, const zkm_ec_decompress_event *
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_ec_decompress_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_ed_add_events_to_trace(const zkm_ed_add_event *events, uint64_t n, uint32_t *trace, uint64_t height,
+                               uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_ed_add_event) == 4 * EDA_EV, "EllipticCurveAddEvent (Ed25519) record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1))) {
+        g_last_error = "zkm_ed_add_events_to_trace: bad arguments (need n <= height, a power of two >= 16)";
+        return ZKM_ERR_ARG;
+    }
+    hipLaunchKernelGGL(k_ed_add_rows, dim3((unsigned)((height + 127) / 128)), dim3(128), 0, (hipStream_t)stream,
+                       (const uint32_t *)events, n, trace, height, byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_ed_add_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;
