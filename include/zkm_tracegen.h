@@ -362,6 +362,20 @@ typedef struct {
 int zkm_ed_add_events_to_trace(const zkm_ed_add_event *events, uint64_t n, uint32_t *trace, uint64_t height,
                                uint32_t *byte_mult, void *stream);
 
+/* EdDecompress (syscall/precompiles/edwards/ed_decompress.rs:64-101, :214-247): EdDecompressEvent as one fixed
+ * record: shard, clk, ptr, sign, the 8 reads of y (at ptr + 32) and the 8 writes of x (at ptr), both at clk.
+ * Each row: the accesses, y < p, y^2, u, d y^2, v, u / v, its square root (lsb 0, ed25519.rs:75-113) as
+ * FieldSqrtCols with range and lsb, -x; padding rows the operations of y = 0.  byte_mult (nullable) as
+ * above.  1566 columns. */
+typedef struct {
+    uint32_t shard, clk, ptr, sign;
+    zkm_memory_read_record y[8];
+    zkm_memory_write_record x[8];
+} zkm_ed_decompress_event;  /* 368 bytes */
+#define ZKM_ED_DECOMPRESS_WIDTH 1566
+int zkm_ed_decompress_events_to_trace(const zkm_ed_decompress_event *events, uint64_t n, uint32_t *trace,
+                                      uint64_t height, uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

@@ -977,6 +977,51 @@ def test_ed_add_shard_from_device_traces():
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 
+def _ed_decompress_events(seed: int = 41):
+    """Ed25519 decompressions through the executor (mips_edwards.exec_ed_decompress): y of multiples of the
+    base point with both signs."""
+    from zkmips_amd import mips_edwards as ED
+    rng = np.random.default_rng(seed)
+    words = {}
+    mem, mem_init, mem_last = {}, {}, {}
+    evs = []
+    for k in range(20):
+        _, y = ED._scalar_mul(int(rng.integers(1, 1 << 62)), (ED.BASE_X, ED.BASE_Y))
+        ptr = 0xC0000 + 0x200 * k
+        for i, w in enumerate(ED._point_words(0, y)[8:]):
+            words[ptr + 32 + 4 * i] = w
+        shard, clk = 3 + k // 12, 190 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: words.get(a, 0))
+        evs.append((SY.ED_DECOMPRESS, (shard, clk, SY.syscall_id(SY.ED_DECOMPRESS), ptr, k % 2),
+                    ED.exec_ed_decompress(pm, shard, clk, ptr, k % 2)))
+    return evs
+
+
+@pytest.mark.gpu
+def test_ed_decompress_shard_from_device_traces():
+    """An ED_DECOMPRESS precompile shard built on the device (the square root with lsb 0, its FieldSqrtCols)
+    equals the host builders' traces and multiplicities and proves to the same bytes."""
+    import torch
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _ed_decompress_events()
+    m, prep, tr, pv = MC.precompile_shard(SY.ED_DECOMPRESS, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(SY.ED_DECOMPRESS, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert "EdDecompress" in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

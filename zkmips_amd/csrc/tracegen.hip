@@ -1773,6 +1773,8 @@ constexpr FpMod kCurveABLS{{0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 
 constexpr FpMod kCurveBBLS{{0x00000004u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
 constexpr FpMod kEd25519{{0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
 constexpr FpMod kEdD{{0x135978a3u, 0x75eb4dcau, 0x4141d8abu, 0x00700a4du, 0x7779e898u, 0x8cc74079u, 0x2b6ffe73u, 0x52036ceeu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kEdSqrtExp{{0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x0fffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
+constexpr FpMod kEdSqrtM1{{0x4a0ea0b0u, 0xc4ee1b27u, 0xad2fe478u, 0x2f431806u, 0x3dfbd7a7u, 0x2b4d0099u, 0x4fc1df0bu, 0x2b832480u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}};
 constexpr FpMod kBls{{0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu,
                       0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau}};
 // W-word helpers for the modular inverse (binary extended Euclid; p odd)
@@ -2446,6 +2448,96 @@ __global__ __launch_bounds__(128) void k_ed_add_rows(const uint32_t *__restrict_
     fp_op<W, NW, OFF>(v + OUT + 5 * FW, f, kEdD.w, 2, kEd25519, b, df);
     fp_den<W, NW, OFF>(v + OUT + 6 * FW, x3n, df, true, kEd25519, b, t);
     fp_den<W, NW, OFF>(v + OUT + 7 * FW, y3n, df, false, kEd25519, b, t);
+}
+
+// EdDecompress (edwards/ed_decompress.rs:64-101, :214-247): is_real, shard, clk, ptr, sign, x (8 writes at clk),
+// y (8 reads at clk), y < p, y^2, u = y^2 - 1, d y^2, v = 1 + d y^2, u / v, FieldSqrtCols of u / v (the root
+// with lsb 0: ed25519.rs:75-113), its range and lsb, -x; padding rows: the operations of y = 0, no lookups.
+// zkm_ed_decompress_event dwords: shard, clk, ptr, sign, y reads (8 x 5), x writes (8 x 6)
+enum { EDD_EV = 4 + 40 + 48 };
+__global__ __launch_bounds__(128) void k_ed_decompress_rows(const uint32_t *__restrict__ ev, uint64_t n,
+                                                            uint32_t *__restrict__ out, uint64_t height, uint32_t *bm) {
+    constexpr int W = 8, NW = 62, OFF = 1 << 14, NL = 32, FW = 2 * NL + 2 * NW, LW = NL + 2, XC = 5, YC = XC + 8 * 13,
+                  YR = YC + 8 * 9, YY = YR + LW, U = YY + FW, DYY = U + FW, V = DYY + FW, UDV = V + FW, SQ = UDV + FW,
+                  SQR = SQ + FW, LSB = SQR + LW, NEGX = LSB + 1, WIDTH = NEGX + FW;
+    static_assert(WIDTH == ZKM_ED_DECOMPRESS_WIDTH, "EdDecompressCols layout");
+    const uint64_t row = (uint64_t)blockIdx.x * 128 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WIDTH;
+    for (int c = 0; c < WIDTH; c++) v[c] = 0;
+    const bool real = row < n;
+    uint32_t *b = real ? bm : nullptr;
+    const uint32_t *m = kEd25519.w;
+    uint32_t y[W];
+    for (int i = 0; i < W; i++) y[i] = 0;
+    if (real) {
+        const uint32_t *e = ev + row * EDD_EV;
+        v[0] = 1;
+        v[1] = e[0];
+        v[2] = e[1];
+        v[3] = e[2];
+        v[4] = e[3];
+        for (int i = 0; i < W; i++) {
+            const Access ya = access_read(e + 4 + 5 * i), xa = access_write(e + 44 + 6 * i);
+            y[i] = ya.value;
+            put_access(v, YC + 9 * i, ya);
+            put_word(v + XC + 13 * i, xa.prev_value);
+            put_access(v, XC + 13 * i + 4, xa);
+            const Access as[2] = {ya, xa};
+            for (int k = 0; k < 2; k++) {
+                byte_add(bm, B_U16RANGE, as[k].d16 >> 8, as[k].d16 & 0xFF);
+                byte_add(bm, B_U8RANGE, 0, as[k].d8);
+            }
+        }
+    }
+    field_lt<NL>(v + YR, y, m, b);
+    uint32_t one[W], zero[W], yy[W], u[W], dyy[W], vv[W], udv[W], sq[W], t[W];
+    for (int i = 0; i < W; i++) one[i] = zero[i] = 0;
+    one[0] = 1;
+    fp_op<W, NW, OFF>(v + YY, y, y, 2, kEd25519, b, yy);
+    fp_op<W, NW, OFF>(v + U, yy, one, 1, kEd25519, b, u);
+    fp_op<W, NW, OFF>(v + DYY, kEdD.w, yy, 2, kEd25519, b, dyy);
+    fp_op<W, NW, OFF>(v + V, one, dyy, 0, kEd25519, b, vv);
+    fp_op<W, NW, OFF>(v + UDV, u, vv, 3, kEd25519, b, udv);
+    {  // ed25519_sqrt: beta = a^((p+3)/8), times sqrt(-1) when beta^2 = -a, negated when odd
+        powmod<W>(udv, kEdSqrtExp.w, m, sq);
+        mulmod<W>(sq, sq, m, t);
+        uint32_t na[W];
+        for (int i = 0; i < W; i++) na[i] = m[i];
+        w_sub<W>(na, udv);
+        if (w_ge<W>(na, m)) w_sub<W>(na, m);
+        bool eq = true;
+        for (int i = 0; i < W; i++) eq = eq && t[i] == na[i];
+        if (eq) mulmod<W>(sq, kEdSqrtM1.w, m, sq);
+        if (sq[0] & 1) {
+            uint32_t r[W];
+            for (int i = 0; i < W; i++) r[i] = m[i];
+            w_sub<W>(r, sq);
+            if (w_ge<W>(r, m)) w_sub<W>(r, m);
+            for (int i = 0; i < W; i++) sq[i] = r[i];
+        }
+    }
+    {  // FieldSqrtCols: sq sq = u / v + carry p, the root in the result columns, the U8 check over u / v's limbs
+        uint32_t pr[2 * W], mres[W], car[W];
+        for (int i = 0; i < 2 * W; i++) pr[i] = 0;
+        for (int i = 0; i < W; i++) {
+            uint64_t c = 0;
+            for (int j = 0; j < W; j++) {
+                const uint64_t q = (uint64_t)sq[i] * sq[j] + pr[i + j] + c;
+                pr[i + j] = (uint32_t)q;
+                c = q >> 32;
+            }
+            pr[i + W] = (uint32_t)c;
+        }
+        for (int i = 0; i < W; i++) car[i] = 0;
+        mod_words<2 * W, W>(pr, m, mres, car);
+        field_op_cols<NL, NW, OFF>(v + SQ, sq, sq, true, sq, mres, car, m, b, udv);
+    }
+    field_lt<NL>(v + SQR, sq, m, b);
+    v[LSB] = sq[0] & 1;
+    byte_add(b, B_AND, sq[0] & 0xFF, 1);
+    for (int j = 0; j < NL; j += 2) byte_add(b, B_U8RANGE, byte_of(sq[j >> 2], j & 3), byte_of(sq[(j + 1) >> 2], (j + 1) & 3));
+    fp_op<W, NW, OFF>(v + NEGX, zero, sq, 1, kEd25519, b, t);
 }
 
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
@@ -3219,6 +3311,23 @@ int zkm_ed_add_events_to_trace(const zkm_ed_add_event *events, uint64_t n, uint3
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_ed_add_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_ed_decompress_events_to_trace(const zkm_ed_decompress_event *events, uint64_t n, uint32_t *trace,
+                                      uint64_t height, uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_ed_decompress_event) == 4 * EDD_EV, "EdDecompressEvent record");
+    if (!trace || (n && !events) || n > height || height < 16 || (height & (height - 1))) {
+        g_last_error = "zkm_ed_decompress_events_to_trace: bad arguments (need n <= height, a power of two >= 16)";
+        return ZKM_ERR_ARG;
+    }
+    hipLaunchKernelGGL(k_ed_decompress_rows, dim3((unsigned)((height + 127) / 128)), dim3(128), 0, (hipStream_t)stream,
+                       (const uint32_t *)events, n, trace, height, byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_ed_decompress_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;

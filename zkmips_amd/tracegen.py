@@ -601,6 +601,39 @@ def ed_add_trace(events_dev, n: int, height: int = None, byte_mult=None):
     return t
 
 
+ED_DECOMPRESS_EVENT = np.dtype({"names": ["shard", "clk", "ptr", "sign", "y", "x"],
+                                "formats": [u4, u4, u4, u4, (u4, (8, 5)), (u4, (8, 6))],
+                                "offsets": [0, 4, 8, 12, 16, 176], "itemsize": 368})
+ED_DECOMPRESS_WIDTH = 1566  # ZKM_ED_DECOMPRESS_WIDTH
+
+
+def ed_decompress_records(events) -> np.ndarray:
+    """zkm_ed_decompress_event records of the executor's ED_DECOMPRESS events (mips_edwards.exec_ed_decompress):
+    y read and x written at clk."""
+    out = np.zeros(len(events), ED_DECOMPRESS_EVENT)
+    for k, e in enumerate(events):
+        sh, clk = e["shard"], e["clk"]
+        r = out[k]
+        r["shard"], r["clk"], r["ptr"], r["sign"] = sh, clk, e["ptr"], e["sign"]
+        rd = np.asarray(e["y"], np.int64).reshape(8, 3)
+        wr = np.asarray(e["x"], np.int64).reshape(8, 4)
+        r["y"] = np.stack([rd[:, 0], np.full(8, sh), np.full(8, clk), rd[:, 1], rd[:, 2]], 1)
+        r["x"] = np.stack([wr[:, 1], np.full(8, sh), np.full(8, clk), wr[:, 0], wr[:, 2], wr[:, 3]], 1)
+    return out
+
+
+def ed_decompress_trace(events_dev, n: int, height: int = None, byte_mult=None):
+    """EdDecompress main trace (height x 1566 int32, on the GPU) from n zkm_ed_decompress_event records; the
+    Byte lookups added into byte_mult (nullable)."""
+    height = height or _pow2(n)
+    t = _trace(height, ED_DECOMPRESS_WIDTH)
+    what = "zkm_ed_decompress_events_to_trace"
+    _lib.check(_bind().zkm_ed_decompress_events_to_trace(_records(events_dev, n, ED_DECOMPRESS_EVENT, what), n,
+                                                         t.data_ptr(), height, _words(byte_mult, 65536 * 10, what),
+                                                         _stream()), what)
+    return t
+
+
 SYS_LINUX_EVENT = np.dtype({"names": ["shard", "clk", "code", "a0", "a1", "result", "a3", "io"],
                             "formats": [u4, u4, u4, u4, u4, u4, (u4, 6), (u4, 6)],
                             "offsets": [0, 4, 8, 12, 16, 20, 24, 48], "itemsize": 72})
@@ -746,6 +779,7 @@ def _bind():
         L.zkm_ec_double_events_to_trace.argtypes = [C.c_int, vp, u64, vp, u64, vp, vp]
         L.zkm_ec_decompress_events_to_trace.argtypes = [C.c_int, vp, u64, vp, u64, vp, vp]
         L.zkm_ed_add_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_ed_decompress_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -773,7 +807,7 @@ def to_device(records: np.ndarray):
                              COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT, POSEIDON2_PERMUTE_EVENT,
                              SYS_LINUX_EVENT, UINT256_MUL_EVENT, U256X2048_MUL_EVENT, FP_OP_EVENT,
                              FP2_EVENT, EC_ADD_EVENT, EC_DOUBLE_EVENT, EC_DECOMPRESS_EVENT,
-                             ED_ADD_EVENT):
+                             ED_ADD_EVENT, ED_DECOMPRESS_EVENT):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -1124,7 +1158,7 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     """Device traces of a SHA, Poseidon2, 256-bit multiplication, base-field (FpOp) or Linux-syscall
     precompile shard (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE /
     UINT256_MUL / U256XU2048_MUL / the bn254 and bls12-381 FP, FP2 add/sub and FP2 mul ops / the Weierstrass
-    additions, doublings and decompressions / the Ed25519 addition / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    additions, doublings and decompressions / the Ed25519 addition and decompression / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
     from . import mips_ec as EC
@@ -1171,6 +1205,9 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     elif code == SY.ED_ADD:
         rec = ed_add_records(pevs)
         out["EdAddAssign"] = ed_add_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    elif code == SY.ED_DECOMPRESS:
+        rec = ed_decompress_records(pevs)
+        out["EdDecompress"] = ed_decompress_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     elif code == SY.SYS_LINUX:
         rec = sys_linux_records(pevs)
         out["SysLinux"] = sys_linux_trace(to_device(rec), len(rec), byte_mult=byte_mult)
