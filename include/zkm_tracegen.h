@@ -376,6 +376,23 @@ typedef struct {
 int zkm_ed_decompress_events_to_trace(const zkm_ed_decompress_event *events, uint64_t n, uint32_t *trace,
                                       uint64_t height, uint32_t *byte_mult, void *stream);
 
+/* KeccakSponge (syscall/precompiles/keccak_sponge/trace.rs:62-196): KeccakSpongeEvent holds Vecs, so it travels
+ * as one record per absorbed block: the call's shard, clk, this block's input address, the output address,
+ * the input length (words), the block's index and the call's block count, the xored state after absorbing
+ * this block and the previous block's (zero for the first; the original state is its Keccak-f, computed on
+ * the device), the block's 36 input reads, the length read, the 16 output writes (at clk + 1).  24 rows per
+ * block (the p3-keccak-air round columns and the sponge columns); padding rows the zero input's rounds.
+ * byte_mult (nullable): the XORs of the rate and the accesses' range checks.  3531 columns. */
+typedef struct {
+    uint32_t shard, clk, in_ptr, out_ptr, in_len, block, nblocks;
+    uint32_t xored[50], prev_xored[50];
+    zkm_memory_read_record in[36], len;
+    zkm_memory_write_record out[16];
+} zkm_keccak_block;  /* 1552 bytes */
+#define ZKM_KECCAK_SPONGE_WIDTH 3531
+int zkm_keccak_sponge_events_to_trace(const zkm_keccak_block *blocks, uint64_t n, uint32_t *trace, uint64_t height,
+                                      uint32_t *byte_mult, void *stream);
+
 /* SysLinux (syscall/precompiles/sys_linux/trace.rs:106-167): LinuxEvent as one fixed record: the call's
  * shard, clk, syscall code, a0, a1, the value returned in V0; the A3 (error) write; `io`: the brk register
  * read (BRK), the A2 read (WRITE; a read as a write record with prev_value = value), the heap write (MMAP /

@@ -1022,6 +1022,63 @@ def test_ed_decompress_shard_from_device_traces():
     assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
 
 
+def _keccak_events(seed: int = 43):
+    """KECCAK_SPONGE calls through the executor (mips_keccak.exec_keccak_sponge): one, two and three
+    absorbed blocks, repeated over two shards."""
+    from zkmips_amd import mips_keccak as KS
+    rng = np.random.default_rng(seed)
+    words = {}
+    mem, mem_init, mem_last = {}, {}, {}
+    evs = []
+    for k, nb in enumerate([1, 2, 3, 1, 2]):
+        ip, op = 0xD0000 + 0x1000 * k, 0xE0000 + 0x1000 * k
+        for i in range(36 * nb):
+            words[ip + 4 * i] = int(rng.integers(0, 1 << 32))
+        words[op + 64] = 36 * nb
+        shard, clk = 3 + k // 3, 210 + 8 * k
+        pm = SY.PrecompileMemory(mem, mem_init, mem_last, {}, [], shard, lambda a: words.get(a, 0))
+        evs.append((KS.KECCAK_SPONGE, (shard, clk, SY.syscall_id(KS.KECCAK_SPONGE), ip, op),
+                    KS.exec_keccak_sponge(pm, shard, clk, ip, op)))
+    return evs
+
+
+def test_keccak_block_records():
+    """zkm_keccak_block records: one per absorbed block, the previous block's xored state, the block's reads."""
+    evs = _keccak_events()
+    rec = TG.keccak_blocks([e for _, _, e in evs])
+    assert rec.dtype.itemsize == 1552 and len(rec) == 9
+    assert list(rec["block"]) == [0, 0, 1, 0, 1, 2, 0, 0, 1] and list(rec["nblocks"]) == [1, 2, 2, 3, 3, 3, 1, 2, 2]
+    assert (rec["prev_xored"][rec["block"] == 0] == 0).all()
+    assert np.array_equal(rec["prev_xored"][2], rec["xored"][1])
+
+
+@pytest.mark.gpu
+def test_keccak_sponge_shard_from_device_traces():
+    """A KECCAK_SPONGE precompile shard built on the device (the rounds recomputed per row, the sponge
+    columns, the XOR and access lookups) equals the host builders' traces and multiplicities and proves to
+    the same bytes."""
+    import torch
+    from zkmips_amd import mips_keccak as KS
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    evs = _keccak_events()
+    m, prep, tr, pv = MC.precompile_shard(KS.KECCAK_SPONGE, evs, shard=5)
+    bm = torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+    dev = TG.precompile_shard_traces(KS.KECCAK_SPONGE, evs, byte_mult=bm)
+    torch.cuda.synchronize()
+    assert "KeccakSponge" in dev
+    for name, t in dev.items():
+        got = t.cpu().numpy().view(np.uint32)
+        bad = np.argwhere(got != tr[name])
+        assert not len(bad), (name, bad[:8].tolist())
+    assert np.array_equal(bm.cpu().numpy().view(np.uint32), tr["Byte"])
+    traces = {k: v for k, v in tr.items() if k not in dev}
+    traces.update(dev)
+    traces["Byte"] = bm
+    prover = HipProver(Device(0), m, _core_prep(), num_queries=16)
+    assert prover.prove_shard(traces, pv) == prover.prove_shard(tr, pv)
+
+
 def _sys_linux_events():
     """Linux syscalls through the executor (mips_syscall.exec_sys_linux): BRK above and below the break,
     MMAP / MMAP2 with a0 = 0 (aligned and unaligned sizes) and a0 != 0, CLONE, EXIT_GROUP, FCNTL (a1 = 1, 3,

@@ -2540,6 +2540,144 @@ __global__ __launch_bounds__(128) void k_ed_decompress_rows(const uint32_t *__re
     fp_op<W, NW, OFF>(v + NEGX, zero, sq, 1, kEd25519, b, t);
 }
 
+// ------------------------------------------------------------------ KeccakSponge (keccak_sponge/trace.rs:62-196)
+// 24 rows per absorbed block.  Each row is built by its own thread: the block's xored state run through the
+// rounds before it (Keccak-f[1600], lane index 5y + x), then the p3-keccak-air columns of that round (step
+// flags, preimage, A limbs, C / C-prime / A-prime bits, A2 limbs, the bits of A2[0][0], the limbs of
+// A3[0][0] = A2[0][0] ^ RC) and the sponge columns (flags, addresses, original state, on the block's first
+// row the block reads and the xored rate, on the call's first row the length read, on its last row the
+// output writes).  Padding rows: the zero input's rows, round = row mod 24.  zkm_keccak_block dwords: shard,
+// clk, in_ptr (of this block), out_ptr, in_len (words), block index, blocks in the call, the xored state
+// (50), the previous block's xored state (50; zero for the first), the block's 36 reads (5 each), the length
+// read (5), the 16 output writes (6 each)
+enum { KS_EV = 7 + 50 + 50 + 180 + 5 + 96, KK_STEP = 0, KK_PRE = 25, KK_A = 125, KK_C = 225, KK_CP = 545, KK_AP = 865,
+       KK_APP = 2465, KK_APP00 = 2565, KK_APPP00 = 2629, KS_BLOCK_MEM = 2633, KS_SHARD = 2957, KS_CLK = 2958,
+       KS_REAL = 2959, KS_READ_BLOCK = 2960, KS_IN_ADDR = 2961, KS_OUT_ADDR = 2962, KS_IN_LEN = 2963,
+       KS_ABSORBED = 2964, KS_IS_ABSORBED = 2965, KS_RECV = 2966, KS_WRITE_OUT = 2967, KS_FIRST = 2968,
+       KS_FINAL = 2969, KS_ORIG = 2970, KS_XORED = 3170, KS_LEN_MEM = 3314, KS_OUT_MEM = 3323 };
+static_assert(KS_OUT_MEM + 16 * 13 == ZKM_KECCAK_SPONGE_WIDTH, "KeccakSpongeCols layout");
+__constant__ uint64_t kKeccakRC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull, 0x000000000000808bull,
+    0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull, 0x000000000000008aull, 0x0000000000000088ull,
+    0x0000000080008009ull, 0x000000008000000aull, 0x000000008000808bull, 0x800000000000008bull, 0x8000000000008089ull,
+    0x8000000000008003ull, 0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+__constant__ uint8_t kKeccakR[5][5] = {{0, 36, 3, 41, 18}, {1, 44, 10, 45, 2}, {62, 6, 43, 15, 61}, {28, 55, 25, 21, 56},
+                                       {27, 20, 39, 8, 14}};
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int s) { return s ? (x << s) | (x >> (64 - s)) : x; }
+
+// one round on a (in place); c, cp, ap, app filled when c is non-null
+__device__ inline void keccak_round(uint64_t a[25], int r, uint64_t *c, uint64_t *cp, uint64_t *ap, uint64_t *app) {
+    uint64_t C[5], D[5], A1[25], B[25];
+    for (int x = 0; x < 5; x++) C[x] = a[x] ^ a[5 + x] ^ a[10 + x] ^ a[15 + x] ^ a[20 + x];
+    for (int x = 0; x < 5; x++) D[x] = C[x] ^ C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
+    for (int y = 0; y < 5; y++)
+        for (int x = 0; x < 5; x++) A1[5 * y + x] = a[5 * y + x] ^ C[x] ^ D[x];
+    for (int y = 0; y < 5; y++)
+        for (int x = 0; x < 5; x++) {
+            const int sx = (x + 3 * y) % 5;
+            B[5 * y + x] = rotl64(A1[5 * x + sx], kKeccakR[sx][x]);
+        }
+    for (int y = 0; y < 5; y++)
+        for (int x = 0; x < 5; x++) a[5 * y + x] = B[5 * y + x] ^ (~B[5 * y + (x + 1) % 5] & B[5 * y + (x + 2) % 5]);
+    if (c) {
+        for (int x = 0; x < 5; x++) {
+            c[x] = C[x];
+            cp[x] = D[x];
+        }
+        for (int i = 0; i < 25; i++) {
+            ap[i] = A1[i];
+            app[i] = a[i];
+        }
+    }
+    a[0] ^= kKeccakRC[r];
+}
+
+__global__ __launch_bounds__(64) void k_keccak_sponge_rows(const uint32_t *__restrict__ ev, uint64_t nblocks,
+                                                           uint32_t *__restrict__ out, uint64_t height, uint32_t *bm) {
+    constexpr int WD = ZKM_KECCAK_SPONGE_WIDTH;
+    const uint64_t row = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (row >= height) return;
+    uint32_t *v = out + row * WD;
+    for (int c = 0; c < WD; c++) v[c] = 0;
+    const uint64_t blk = row / 24;
+    const int r = (int)(row % 24);
+    const bool real = blk < nblocks;
+    const uint32_t *e = ev + blk * KS_EV;  // dereferenced for real rows only
+    uint64_t a[25];
+    for (int i = 0; i < 25; i++) a[i] = real ? ((uint64_t)e[7 + 2 * i] | ((uint64_t)e[8 + 2 * i] << 32)) : 0ull;
+    v[KK_STEP + r] = 1;
+    for (int i = 0; i < 25; i++)
+        for (int l = 0; l < 4; l++) v[KK_PRE + 4 * i + l] = (uint32_t)((a[i] >> (16 * l)) & 0xFFFF);
+    for (int k = 0; k < r; k++) keccak_round(a, k, nullptr, nullptr, nullptr, nullptr);
+    for (int i = 0; i < 25; i++)
+        for (int l = 0; l < 4; l++) v[KK_A + 4 * i + l] = (uint32_t)((a[i] >> (16 * l)) & 0xFFFF);
+    uint64_t c[5], cp[5], ap[25], app[25];
+    keccak_round(a, r, c, cp, ap, app);
+    for (int x = 0; x < 5; x++)
+        for (int b = 0; b < 64; b++) {
+            v[KK_C + 64 * x + b] = (uint32_t)((c[x] >> b) & 1);
+            v[KK_CP + 64 * x + b] = (uint32_t)((cp[x] >> b) & 1);
+        }
+    for (int i = 0; i < 25; i++) {
+        for (int b = 0; b < 64; b++) v[KK_AP + 64 * i + b] = (uint32_t)((ap[i] >> b) & 1);
+        for (int l = 0; l < 4; l++) v[KK_APP + 4 * i + l] = (uint32_t)((app[i] >> (16 * l)) & 0xFFFF);
+    }
+    for (int b = 0; b < 64; b++) v[KK_APP00 + b] = (uint32_t)((app[0] >> b) & 1);
+    for (int l = 0; l < 4; l++) v[KK_APPP00 + l] = (uint32_t)((a[0] >> (16 * l)) & 0xFFFF);
+    if (!real) return;
+    const uint32_t shard = e[0], clk = e[1], k = e[5], nblk = e[6];
+    const bool first = k == 0, final = k + 1 == nblk;
+    v[KS_SHARD] = shard;
+    v[KS_CLK] = clk;
+    v[KS_REAL] = 1;
+    v[KS_IN_LEN] = e[4];
+    v[KS_ABSORBED] = k * 36;
+    v[KS_IS_ABSORBED] = r == 23 && !final;
+    v[KS_FIRST] = first;
+    v[KS_FINAL] = final;
+    v[KS_READ_BLOCK] = r == 0;
+    v[KS_RECV] = r == 0 && first;
+    v[KS_WRITE_OUT] = r == 23 && final;
+    v[KS_OUT_ADDR] = e[3];
+    v[KS_IN_ADDR] = e[2];
+    // the state before this block's absorption: Keccak-f of the previous block's xored state
+    uint64_t o[25];
+    for (int i = 0; i < 25; i++) o[i] = (uint64_t)e[57 + 2 * i] | ((uint64_t)e[58 + 2 * i] << 32);
+    if (!first)
+        for (int k2 = 0; k2 < 24; k2++) keccak_round(o, k2, nullptr, nullptr, nullptr, nullptr);
+    uint32_t ow[50];
+    for (int i = 0; i < 25; i++) {
+        ow[2 * i] = (uint32_t)o[i];
+        ow[2 * i + 1] = (uint32_t)(o[i] >> 32);
+    }
+    for (int i = 0; i < 50; i++) put_word(v + KS_ORIG + 4 * i, ow[i]);
+    auto acc = [&](int col, const Access &x) {
+        put_access(v, col, x);
+        byte_add(bm, B_U16RANGE, x.d16 >> 8, x.d16 & 0xFF);
+        byte_add(bm, B_U8RANGE, 0, x.d8);
+    };
+    if (r == 0) {
+        for (int i = 0; i < 36; i++) {
+            const Access x = access_read(e + 107 + 5 * i);
+            acc(KS_BLOCK_MEM + 9 * i, x);
+            for (int b = 0; b < 4; b++) {  // XorOperation of the original word and the input word
+                const uint32_t ob = byte_of(ow[i], b), ib = byte_of(x.value, b);
+                v[KS_XORED + 4 * i + b] = ob ^ ib;
+                byte_add(bm, B_XOR, ob, ib);
+            }
+        }
+        if (first) acc(KS_LEN_MEM, access_read(e + 287));
+    }
+    if (r == 23 && final) {
+        for (int i = 0; i < 16; i++) {
+            const Access w = access_write(e + 292 + 6 * i);
+            put_word(v + KS_OUT_MEM + 13 * i, w.prev_value);
+            acc(KS_OUT_MEM + 13 * i + 4, w);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ SysLinux (sys_linux/trace.rs:106-167)
 // SysLinuxCols (sys_linux/columns.rs); zkm_sys_linux_event dwords: shard, clk, code, a0, a1, result, the A3
 // write, the io record
@@ -3328,6 +3466,23 @@ int zkm_ed_decompress_events_to_trace(const zkm_ed_decompress_event *events, uin
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         g_last_error = std::string("zkm_ed_decompress_events_to_trace: ") + hipGetErrorString(err);
+        return ZKM_ERR_HIP;
+    }
+    return ZKM_OK;
+}
+
+int zkm_keccak_sponge_events_to_trace(const zkm_keccak_block *blocks, uint64_t n, uint32_t *trace, uint64_t height,
+                                      uint32_t *byte_mult, void *stream) {
+    static_assert(sizeof(zkm_keccak_block) == 4 * KS_EV, "KeccakSponge block record");
+    if (!trace || (n && !blocks) || 24 * n > height || height < 16 || (height & (height - 1))) {
+        g_last_error = "zkm_keccak_sponge_events_to_trace: bad arguments (need 24 n <= height, a power of two >= 16)";
+        return ZKM_ERR_ARG;
+    }
+    hipLaunchKernelGGL(k_keccak_sponge_rows, dim3((unsigned)((height + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                       (const uint32_t *)blocks, n, trace, height, byte_mult);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        g_last_error = std::string("zkm_keccak_sponge_events_to_trace: ") + hipGetErrorString(err);
         return ZKM_ERR_HIP;
     }
     return ZKM_OK;

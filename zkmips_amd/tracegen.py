@@ -634,6 +634,52 @@ def ed_decompress_trace(events_dev, n: int, height: int = None, byte_mult=None):
     return t
 
 
+KECCAK_BLOCK = np.dtype({"names": ["shard", "clk", "in_ptr", "out_ptr", "in_len", "block", "nblocks", "xored",
+                                   "prev_xored", "in", "len", "out"],
+                         "formats": [u4] * 7 + [(u4, 50), (u4, 50), (u4, (36, 5)), (u4, 5), (u4, (16, 6))],
+                         "offsets": [0, 4, 8, 12, 16, 20, 24, 28, 228, 428, 1148, 1168], "itemsize": 1552})
+KECCAK_SPONGE_WIDTH = 3531  # ZKM_KECCAK_SPONGE_WIDTH
+
+
+def keccak_blocks(events) -> np.ndarray:
+    """zkm_keccak_block records (one per absorbed block) of the executor's KECCAK_SPONGE events
+    (mips_keccak.exec_keccak_sponge): input and length read at clk, output written at clk + 1."""
+    def lanes(st):
+        v = np.asarray(st, np.uint64)
+        return np.stack([v & np.uint64(0xFFFFFFFF), v >> np.uint64(32)], 1).reshape(-1).astype(np.uint32)
+    rows = []
+    for e in events:
+        sh, clk, nb = e["shard"], e["clk"], len(e["xored"])
+        rd = np.asarray(e["in"], np.int64).reshape(-1, 3)
+        ln = e["len"]
+        wr = np.asarray(e["w"], np.int64).reshape(16, 4)
+        out = np.stack([wr[:, 1], np.full(16, sh), np.full(16, clk + 1), wr[:, 0], wr[:, 2], wr[:, 3]], 1)
+        for k in range(nb):
+            r = np.zeros(1, KECCAK_BLOCK)[0]
+            r["shard"], r["clk"], r["in_ptr"], r["out_ptr"] = sh, clk, e["in_ptr"] + 144 * k, e["out_ptr"]
+            r["in_len"], r["block"], r["nblocks"] = len(e["in"]), k, nb
+            r["xored"] = lanes(e["xored"][k])
+            if k:
+                r["prev_xored"] = lanes(e["xored"][k - 1])
+            b = rd[36 * k:36 * (k + 1)]
+            r["in"] = np.stack([b[:, 0], np.full(36, sh), np.full(36, clk), b[:, 1], b[:, 2]], 1)
+            r["len"] = [ln[0], sh, clk, ln[1], ln[2]]
+            r["out"] = out
+            rows.append(r)
+    return np.array(rows, KECCAK_BLOCK) if rows else np.zeros(0, KECCAK_BLOCK)
+
+
+def keccak_sponge_trace(blocks_dev, n: int, height: int = None, byte_mult=None):
+    """KeccakSponge main trace (height x 3531 int32, on the GPU) from n zkm_keccak_block records (24 rows
+    each); the Byte lookups added into byte_mult (nullable)."""
+    height = height or _pow2(24 * n)
+    t = _trace(height, KECCAK_SPONGE_WIDTH)
+    what = "zkm_keccak_sponge_events_to_trace"
+    _lib.check(_bind().zkm_keccak_sponge_events_to_trace(_records(blocks_dev, n, KECCAK_BLOCK, what), n, t.data_ptr(),
+                                                         height, _words(byte_mult, 65536 * 10, what), _stream()), what)
+    return t
+
+
 SYS_LINUX_EVENT = np.dtype({"names": ["shard", "clk", "code", "a0", "a1", "result", "a3", "io"],
                             "formats": [u4, u4, u4, u4, u4, u4, (u4, 6), (u4, 6)],
                             "offsets": [0, 4, 8, 12, 16, 20, 24, 48], "itemsize": 72})
@@ -780,6 +826,7 @@ def _bind():
         L.zkm_ec_decompress_events_to_trace.argtypes = [C.c_int, vp, u64, vp, u64, vp, vp]
         L.zkm_ed_add_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_ed_decompress_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.zkm_keccak_sponge_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_instrs_events_to_trace.argtypes = [vp, u64, vp, u64, vp, vp]
         L.zkm_memory_local_events_to_trace.argtypes = [vp, u64, vp, u64, vp]
         L.zkm_memory_global_events_to_trace.argtypes = [vp, u64, C.c_int, C.c_uint32, vp, u64, vp]
@@ -807,7 +854,7 @@ def to_device(records: np.ndarray):
                              COMP_ALU_EVENT, MISC_EVENT, SHA_EXTEND_ROW, SHA_COMPRESS_EVENT, POSEIDON2_PERMUTE_EVENT,
                              SYS_LINUX_EVENT, UINT256_MUL_EVENT, U256X2048_MUL_EVENT, FP_OP_EVENT,
                              FP2_EVENT, EC_ADD_EVENT, EC_DOUBLE_EVENT, EC_DECOMPRESS_EVENT,
-                             ED_ADD_EVENT, ED_DECOMPRESS_EVENT):
+                             ED_ADD_EVENT, ED_DECOMPRESS_EVENT, KECCAK_BLOCK):
         raise ValueError(f"not a record array of zkm_tracegen.h: {records.dtype}")
     raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
     return torch.from_numpy(raw.copy()).cuda() if raw.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
@@ -1158,10 +1205,11 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     """Device traces of a SHA, Poseidon2, 256-bit multiplication, base-field (FpOp) or Linux-syscall
     precompile shard (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE /
     UINT256_MUL / U256XU2048_MUL / the bn254 and bls12-381 FP, FP2 add/sub and FP2 mul ops / the Weierstrass
-    additions, doublings and decompressions / the Ed25519 addition and decompression / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
+    additions, doublings and decompressions / the Ed25519 addition and decompression / the Keccak sponge / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
     from . import mips_ec as EC
+    from . import mips_keccak as KS
     from . import mips_memory as MM
     from . import mips_p2permute as P2P
     from . import mips_syscall as SY
@@ -1208,6 +1256,9 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     elif code == SY.ED_DECOMPRESS:
         rec = ed_decompress_records(pevs)
         out["EdDecompress"] = ed_decompress_trace(to_device(rec), len(rec), byte_mult=byte_mult)
+    elif code == KS.KECCAK_SPONGE:
+        rec = keccak_blocks(pevs)
+        out["KeccakSponge"] = keccak_sponge_trace(to_device(rec), len(rec), byte_mult=byte_mult)
     elif code == SY.SYS_LINUX:
         rec = sys_linux_records(pevs)
         out["SysLinux"] = sys_linux_trace(to_device(rec), len(rec), byte_mult=byte_mult)
