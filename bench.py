@@ -818,6 +818,28 @@ def tracegen_bench(args):
                           116 + 4 * TG.SHA_EXTEND_WIDTH, 48 * n_ext)
     chips["ShaCompress"] = (lambda: TG.sha_compress_trace(d_sc, n_cmp, height=n >> 2, byte_mult=bm),
                             1648 / 80 + 4 * TG.SHA_COMPRESS_WIDTH, 80 * n_cmp)
+    # every other precompile chip (one thread per row; the emulated-field chips compute their witnesses):
+    # the calls of the all-precompile guest, a Keccak guest and an Ed25519 guest, each chip's records tiled
+    # to n >> 6 rows (KeccakSponge: 24 rows per absorbed block)
+    import collections
+    from zkmips_amd import mips_ec as EC
+    from zkmips_amd import mips_edwards as ED
+    from zkmips_amd import mips_keccak as KS
+    calls = collections.defaultdict(list)
+    for prog, seed in ((EC.ec_program(1, reps=1), 1), (KS.keccak_program([bytes(range(256)) * 2, b"abc" * 100]), 1),
+                       (ED.ed25519_program(1, seed=3, scalar_bits=6), 3)):
+        st = MC.fresh_state()
+        MC._execute(prog, MC.initial_registers(seed), 1, 1 << 22, st)
+        for code, _, e in st["precompile"]:
+            calls[code].append(e)
+    for code, evs in calls.items():
+        name, rec, fn = TG.precompile_chip(code, evs)
+        per = 24 if name == "KeccakSponge" else 1
+        m_ = max(1, (n >> 6) // per)
+        d = TG.to_device(rec[np.arange(m_) % len(rec)])
+        width = fn(d, m_, byte_mult=bm).shape[1]
+        chips[name] = ((lambda fn=fn, d=d, m_=m_: fn(d, m_, byte_mult=bm)), rec.dtype.itemsize / per + 4 * width,
+                       m_ * per)
     res = {}
     for name, spec in chips.items():
         fn, bytes_per_row = spec[0], spec[1]

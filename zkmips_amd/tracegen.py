@@ -13,6 +13,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import functools
+
 import numpy as np
 
 from . import _lib
@@ -1201,6 +1203,66 @@ def recursion_instrs_trace(chip: str, records_dev, n: int, height: int, montgome
     return t
 
 
+def precompile_chip(code: int, pevs):
+    """The precompile chip of a syscall code: (chip name, its zkm_tracegen.h records of the calls pevs, the
+    trace builder fn(records_dev, n, height=None, byte_mult=None))."""
+    from . import mips_ec as EC
+    from . import mips_keccak as KS
+    from . import mips_p2permute as P2P
+    from . import mips_syscall as SY
+    if code == SY.SHA_EXTEND:
+        rows = sha_extend_records(pevs)
+        return "ShaExtend", rows, sha_extend_trace
+    elif code == SY.SHA_COMPRESS:
+        rec = sha_compress_records(pevs)
+        return "ShaCompress", rec, sha_compress_trace
+    elif code == EC.UINT256_MUL:
+        rec = uint256_mul_records(pevs)
+        return "Uint256MulMod", rec, uint256_mul_trace
+    elif code == EC.U256XU2048_MUL:
+        rec = u256x2048_mul_records(pevs)
+        return "U256XU2048Mul", rec, u256x2048_mul_trace
+    elif any(code == EC.FP_OPS[f][0] for f in FP_OP_FIELDS):
+        field = next(f for f in FP_OP_FIELDS if code == EC.FP_OPS[f][0])
+        rec = fp_op_records(pevs)
+        return EC.FP_NAME[field], rec, functools.partial(fp_op_trace, field)
+    elif any(code in (EC.FP2_ADDSUB[f][0], EC.FP2_MUL[f]) for f in FP_OP_FIELDS):
+        field = next(f for f in FP_OP_FIELDS if code in (EC.FP2_ADDSUB[f][0], EC.FP2_MUL[f]))
+        mul = code == EC.FP2_MUL[field]
+        rec = fp2_records(pevs)
+        name = EC.FP2_MUL_NAME[field] if mul else EC.FP2_ADDSUB_NAME[field]
+        return name, rec, functools.partial(fp2_trace, field, mul)
+    elif any(code == EC.EC_ADD[c] for c in EC_CURVES):
+        curve = next(c for c in EC_CURVES if code == EC.EC_ADD[c])
+        rec = ec_add_records(pevs)
+        return f"{curve}AddAssign", rec, functools.partial(ec_add_trace, curve)
+    elif any(code == EC.EC_DOUBLE[c] for c in EC_CURVES):
+        curve = next(c for c in EC_CURVES if code == EC.EC_DOUBLE[c])
+        rec = ec_double_records(pevs)
+        return f"{curve}DoubleAssign", rec, functools.partial(ec_double_trace, curve)
+    elif any(code == EC.EC_DECOMPRESS[c] for c in EC.EC_DECOMPRESS):
+        curve = next(c for c in EC.EC_DECOMPRESS if code == EC.EC_DECOMPRESS[c])
+        rec = ec_decompress_records(pevs)
+        return f"{curve}Decompress", rec, functools.partial(ec_decompress_trace, curve)
+    elif code == SY.ED_ADD:
+        rec = ed_add_records(pevs)
+        return "EdAddAssign", rec, ed_add_trace
+    elif code == SY.ED_DECOMPRESS:
+        rec = ed_decompress_records(pevs)
+        return "EdDecompress", rec, ed_decompress_trace
+    elif code == KS.KECCAK_SPONGE:
+        rec = keccak_blocks(pevs)
+        return "KeccakSponge", rec, keccak_sponge_trace
+    elif code == SY.SYS_LINUX:
+        rec = sys_linux_records(pevs)
+        return "SysLinux", rec, sys_linux_trace
+    elif code == P2P.POSEIDON2_PERMUTE:
+        rec = poseidon2_permute_records(pevs)
+        return "Poseidon2Permute", rec, poseidon2_permute_trace
+    else:
+        raise ValueError(f"no device trace for precompile {code:#x}")
+
+
 def precompile_shard_traces(code: int, events, byte_mult=None):
     """Device traces of a SHA, Poseidon2, 256-bit multiplication, base-field (FpOp) or Linux-syscall
     precompile shard (mips_core.precompile_shard's chips for SHA_EXTEND / SHA_COMPRESS / POSEIDON2_PERMUTE /
@@ -1208,65 +1270,13 @@ def precompile_shard_traces(code: int, events, byte_mult=None):
     additions, doublings and decompressions / the Ed25519 addition and decompression / the Keccak sponge / the Linux syscalls): the precompile chip, SyscallPrecompile (one row per call), MemoryLocal (the calls' local
     memory accesses) and the Global chip (the syscall receives and the memory messages), with their Byte
     lookups added into byte_mult.  events: the shard's (code, syscall tuple, event) list."""
-    from . import mips_ec as EC
-    from . import mips_keccak as KS
     from . import mips_memory as MM
-    from . import mips_p2permute as P2P
     from . import mips_syscall as SY
     pevs = [e for _, _, e in events]
     sev = np.asarray([s_ for _, s_, _ in events], np.int64).reshape(-1, 5)  # shard, clk, id, arg1, arg2
     out = {}
-    if code == SY.SHA_EXTEND:
-        rows = sha_extend_records(pevs)
-        out["ShaExtend"] = sha_extend_trace(to_device(rows), len(rows), byte_mult=byte_mult)
-    elif code == SY.SHA_COMPRESS:
-        rec = sha_compress_records(pevs)
-        out["ShaCompress"] = sha_compress_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    elif code == EC.UINT256_MUL:
-        rec = uint256_mul_records(pevs)
-        out["Uint256MulMod"] = uint256_mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    elif code == EC.U256XU2048_MUL:
-        rec = u256x2048_mul_records(pevs)
-        out["U256XU2048Mul"] = u256x2048_mul_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    elif any(code == EC.FP_OPS[f][0] for f in FP_OP_FIELDS):
-        field = next(f for f in FP_OP_FIELDS if code == EC.FP_OPS[f][0])
-        rec = fp_op_records(pevs)
-        out[EC.FP_NAME[field]] = fp_op_trace(field, to_device(rec), len(rec), byte_mult=byte_mult)
-    elif any(code in (EC.FP2_ADDSUB[f][0], EC.FP2_MUL[f]) for f in FP_OP_FIELDS):
-        field = next(f for f in FP_OP_FIELDS if code in (EC.FP2_ADDSUB[f][0], EC.FP2_MUL[f]))
-        mul = code == EC.FP2_MUL[field]
-        rec = fp2_records(pevs)
-        name = EC.FP2_MUL_NAME[field] if mul else EC.FP2_ADDSUB_NAME[field]
-        out[name] = fp2_trace(field, mul, to_device(rec), len(rec), byte_mult=byte_mult)
-    elif any(code == EC.EC_ADD[c] for c in EC_CURVES):
-        curve = next(c for c in EC_CURVES if code == EC.EC_ADD[c])
-        rec = ec_add_records(pevs)
-        out[f"{curve}AddAssign"] = ec_add_trace(curve, to_device(rec), len(rec), byte_mult=byte_mult)
-    elif any(code == EC.EC_DOUBLE[c] for c in EC_CURVES):
-        curve = next(c for c in EC_CURVES if code == EC.EC_DOUBLE[c])
-        rec = ec_double_records(pevs)
-        out[f"{curve}DoubleAssign"] = ec_double_trace(curve, to_device(rec), len(rec), byte_mult=byte_mult)
-    elif any(code == EC.EC_DECOMPRESS[c] for c in EC.EC_DECOMPRESS):
-        curve = next(c for c in EC.EC_DECOMPRESS if code == EC.EC_DECOMPRESS[c])
-        rec = ec_decompress_records(pevs)
-        out[f"{curve}Decompress"] = ec_decompress_trace(curve, to_device(rec), len(rec), byte_mult=byte_mult)
-    elif code == SY.ED_ADD:
-        rec = ed_add_records(pevs)
-        out["EdAddAssign"] = ed_add_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    elif code == SY.ED_DECOMPRESS:
-        rec = ed_decompress_records(pevs)
-        out["EdDecompress"] = ed_decompress_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    elif code == KS.KECCAK_SPONGE:
-        rec = keccak_blocks(pevs)
-        out["KeccakSponge"] = keccak_sponge_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    elif code == SY.SYS_LINUX:
-        rec = sys_linux_records(pevs)
-        out["SysLinux"] = sys_linux_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    elif code == P2P.POSEIDON2_PERMUTE:
-        rec = poseidon2_permute_records(pevs)
-        out["Poseidon2Permute"] = poseidon2_permute_trace(to_device(rec), len(rec), byte_mult=byte_mult)
-    else:
-        raise ValueError(f"no device trace for precompile {code:#x}")
+    name, rec, fn = precompile_chip(code, pevs)
+    out[name] = fn(to_device(rec), len(rec), byte_mult=byte_mult)
     sc = np.zeros(len(sev), SYSCALL_EVENT)
     sc["shard"], sc["clk"], sc["syscall_id"], sc["arg1"], sc["arg2"] = (sev[:, j] for j in range(5))
     out["SyscallPrecompile"] = syscall_trace(to_device(sc), len(sc))
