@@ -826,10 +826,10 @@ def tracegen_bench(args):
     from zkmips_amd import mips_edwards as ED
     from zkmips_amd import mips_keccak as KS
     calls = collections.defaultdict(list)
-    for prog, seed in ((EC.ec_program(1, reps=1), 1), (KS.keccak_program([bytes(range(256)) * 2, b"abc" * 100]), 1),
-                       (ED.ed25519_program(1, seed=3, scalar_bits=6), 3)):
-        st = MC.fresh_state()
-        MC._execute(prog, MC.initial_registers(seed), 1, 1 << 22, st)
+    for gprog, seed in ((EC.ec_program(1, reps=1), 1), (KS.keccak_program([bytes(range(256)) * 2, b"abc" * 100]), 1),
+                        (ED.ed25519_program(1, seed=3, scalar_bits=6), 3)):
+        st = MC.fresh_state()  # (gprog: the Cpu lambda above reads prog when it runs)
+        MC._execute(gprog, MC.initial_registers(seed), 1, 1 << 22, st)
         for code, _, e in st["precompile"]:
             calls[code].append(e)
     for code, evs in calls.items():
