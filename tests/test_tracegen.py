@@ -1164,3 +1164,25 @@ def test_maxshape_shard_from_device_traces():
     traces["Byte"] = bm
     prover = HipProver(Device(0), m, {k: v for k, v in prep.items() if v is not None}, num_queries=16)
     assert prover.prove_shard({k: v for k, v in traces.items() if k in tr}, pv) == prover.prove_shard(tr, pv)
+
+
+def test_every_precompile_has_a_device_chip():
+    """tracegen.precompile_chip maps every precompile the all-precompile, Keccak, Ed25519 and sha2 guests
+    call to its chip, records of the header's layout and a trace builder (no chip left host-built)."""
+    import collections
+    from zkmips_amd import mips_ec as EC
+    from zkmips_amd import mips_edwards as ED
+    from zkmips_amd import mips_keccak as KS
+    calls = collections.defaultdict(list)
+    for prog, seed in ((EC.ec_program(1, reps=1), 1), (KS.keccak_program([b"abc" * 50]), 1),
+                       (ED.ed25519_program(1, seed=3, scalar_bits=6), 3), (MC.sha_program(1, seed=5), 5)):
+        st = MC.fresh_state()
+        MC._execute(prog, MC.initial_registers(seed), 1, 1 << 22, st)
+        for code, _, e in st["precompile"]:
+            calls[code].append(e)
+    names = set()
+    for code, evs in calls.items():
+        name, rec, fn = TG.precompile_chip(code, evs)
+        assert callable(fn) and len(rec) >= len(evs) and rec.dtype.itemsize % 4 == 0
+        names.add(name)
+    assert len(names) == 25 and {"KeccakSponge", "EdAddAssign", "Bls12381Decompress", "ShaCompress"} <= names
