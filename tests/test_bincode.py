@@ -53,6 +53,32 @@ def test_compress_request_roundtrip(fib_proofs):
         B.read_compress_request(req[:len(req) // 2])
 
 
+def test_compress_request_layout_is_the_serde_field_list(fib_proofs):
+    """CompressRequestPayload built byte by byte from the reference's serde fields:
+    vk (StarkVerifyingKey), proof = ZKMCoreProof { proof: Vec<ShardProof>, stdin: ZKMStdin { buffer:
+    Vec<Vec<u8>>, ptr: usize, proofs: Vec<..> }, public_values: ZKMPublicValues { buffer: Buffer { data:
+    Vec<u8> } } (Buffer.ptr is #[serde(skip)], crates/primitives/src/types.rs:13-18), cycles: u64 },
+    deferred_proofs: Vec<..> (crates/cuda/src/lib.rs:92-102, crates/prover/src/types.rs:114-119,
+    crates/core/machine/src/io.rs:7-13)."""
+    m, prep, commit, proofs = fib_proofs
+    vk = B.StarkVk.of_program(m, prep, commit, 0x400000, [0] * 14)
+    w = B.Writer()
+    vk.write(w)
+    want = (w.bytes() + struct.pack("<Q", 2) + proofs[0] + proofs[1]
+            + struct.pack("<Q", 1) + struct.pack("<Q", 3) + b"abc"   # stdin.buffer
+            + struct.pack("<Q", 5)                                  # stdin.ptr
+            + struct.pack("<Q", 0)                                  # stdin.proofs
+            + struct.pack("<Q", 2) + b"\x07\x08"                    # public_values.buffer.data
+            + struct.pack("<Q", 1234)                               # cycles
+            + struct.pack("<Q", 0))                                 # deferred_proofs
+    vk2, shards, nd = B.read_compress_request(want)
+    assert vk2 == vk and shards == proofs[:2] and nd == 0
+    got = B.write_compress_request(vk, proofs[:2], stdin=[b"abc"], public_values=b"\x07\x08", cycles=1234)
+    # the writer's stdin.ptr is 0; everything else is the same bytes
+    assert got == want.replace(struct.pack("<Q", 3) + b"abc" + struct.pack("<Q", 5),
+                               struct.pack("<Q", 3) + b"abc" + struct.pack("<Q", 0))
+
+
 def test_reduce_proof_roundtrip(fib_proofs):
     m, prep, commit, proofs = fib_proofs
     vk = B.StarkVk.of_program(m, prep, commit, 0, [5] * 14)

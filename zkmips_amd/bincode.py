@@ -154,9 +154,9 @@ def read_compress_request(b: bytes):
         StarkVk.read(r)
         r.pos = shard_proof_end(b, r.pos)
         StarkVk.read(r)
-    # ZKMPublicValues { buffer: Buffer { data: Vec<u8>, ptr: usize } }, cycles u64
+    # ZKMPublicValues { buffer: Buffer { data: Vec<u8> } } -- Buffer.ptr is #[serde(skip)]
+    # (crates/primitives/src/types.rs:13-18) -- then cycles u64
     r.raw(r.u64())
-    r.u64()
     r.u64()
     n_deferred = r.u64()
     return vk, shards, n_deferred + n_stdin_proofs
@@ -178,8 +178,7 @@ def write_compress_request(vk: StarkVk, shards: List[bytes], stdin: List[bytes] 
     w.u64(0)
     w.u64(0)
     w.u64(len(public_values))
-    w.raw(public_values)
-    w.u64(0)
+    w.raw(public_values)  # Buffer.ptr is not serialized
     w.u64(cycles)
     w.u64(0)
     return w.bytes()
