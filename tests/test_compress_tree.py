@@ -197,6 +197,46 @@ def test_compact_witness_is_the_full_witness(fib_leaves):
     assert CT._prep_traces_of(other[0]) is comp[0].traces
     # dedup off: always sent
     assert CT.node_witness(fib_leaves[2:], fix=False, compact=True, dedup=False)[0].traces is not None
+    # a new session (another tree / Compress request) gets the traces again, once
+    sid = CT.new_session()
+    assert CT.node_witness(fib_leaves[2:], fix=False, compact=True, session=sid)[0].traces is not None
+    assert CT.node_witness(fib_leaves[:2], fix=False, compact=True, session=sid)[0].traces is None
+
+
+def test_failed_tree_discards_in_flight_witnesses(tmp_path):
+    """A tree whose proving fails drops the witnesses still in flight: their /dev/shm files are unlinked
+    when they land, and nothing else is proven."""
+    import threading
+    from concurrent.futures import Future
+    gate = threading.Event()
+    files = []
+
+    def submit(ch):
+        f = Future()
+        f.set_running_or_notify_cancel()  # as an executor's job that has started: cannot be cancelled
+        path = tmp_path / f"w{len(files)}"
+        path.write_bytes(b"x")
+        files.append(path)
+
+        def land():
+            if len(files) > 1:
+                gate.wait(10)  # the second witness lands after the first proof failed
+            f.set_result(CT.Packed(b"", str(path), []))
+        threading.Thread(target=land, daemon=True).start()
+        return f
+
+    def prove(w):
+        raise RuntimeError("device failure")
+    red = CT.Reducer(submit, prove, inflight=1, on_witness=lambda w: w)
+    with pytest.raises(RuntimeError):
+        CT.reduce_serial([("vk", b"a"), ("vk", b"b"), ("vk", b"c"), ("vk", b"d")], red)
+    gate.set()
+    import time
+    for _ in range(100):
+        if not files[1].exists():
+            break
+        time.sleep(0.02)
+    assert len(files) == 2 and not files[1].exists()
 
 
 def test_prep_key_tracks_the_prep_traces(fib_leaves):

@@ -75,15 +75,19 @@ def test_two_rank_gloo_matches_sequential():
     assert got == seq
 
 
-def _fake_reducer(calls):
+def _fake_reducer(calls, slow=None):
     """A Reducer whose witness step passes the children through (a thread pool stands in for the process
-    pool) and whose prove step hashes them: the tree's shape decides the root."""
+    pool) and whose prove step hashes them: the tree's shape decides the root.  slow: a first child's proof
+    bytes whose node takes 3 s to prove (so nodes finish out of order)."""
     import hashlib
+    import time
     from concurrent.futures import ThreadPoolExecutor
     from zkmips_amd.compress_tree import Reducer
     tp = ThreadPoolExecutor(4)
 
     def prove(children):
+        if slow is not None and children[0][1] == slow:
+            time.sleep(3.0)
         h = hashlib.sha256()
         for _, c in children:
             h.update(len(c).to_bytes(8, "little") + c)
@@ -94,16 +98,16 @@ def _fake_reducer(calls):
     return Reducer(lambda ch: tp.submit(lambda: ch), prove, inflight=2)
 
 
-def _tree_worker(rank, world, port, out_q):
+def _tree_worker(rank, world, port, out_q, sizes=(64, 5), slow=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from zkmips_amd.compress_tree import reduce_distributed
-    for nleaves in (64, 5):
+    for nleaves in sizes:
         calls = []
         leaves = [("vk", bytes([i]) * (i + 1)) for i in range(nleaves)]
-        root = reduce_distributed(leaves, _fake_reducer(calls))
+        root = reduce_distributed(leaves, _fake_reducer(calls, slow))
         out_q.put((rank, nleaves, root, len(calls)))
     dist.destroy_process_group()
 
@@ -133,3 +137,24 @@ def test_compress_tree_distributed(world):
         assert sum(r[3] for r in got) == len(nodes) == len(calls) == (63 if nleaves == 64 else 6)
         for r in got:
             assert r[3] == sum(1 for nd in nodes if owner(nd, nleaves, world) == r[0])
+
+
+def test_compress_tree_distributed_out_of_order():
+    """world 3, 16 leaves: rank 1 sends nodes (1,3) and (3,1) to rank 0, and (1,3) (leaves 6, 7) is made
+    slow, so (3,1) arrives first; each message names its node, so rank 0 still pairs them correctly and
+    every rank ends with the serial tree's root."""
+    from zkmips_amd.compress_tree import owner, reduce_serial
+    assert owner((1, 3), 16, 3) == owner((3, 1), 16, 3) == 1 and owner((2, 1), 16, 3) == owner((4, 0), 16, 3) == 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    slow = bytes([6]) * 7
+    ps = [ctx.Process(target=_tree_worker, args=(r, 3, port, q, (16,), slow)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(3)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = reduce_serial([("vk", bytes([i]) * (i + 1)) for i in range(16)], _fake_reducer([]))
+    assert all(r[2] == want for r in res)

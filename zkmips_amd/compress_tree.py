@@ -23,6 +23,7 @@ import pickle
 import queue
 import threading
 import time
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -78,9 +79,18 @@ class VkRef:
 
 
 _VK_DIR: List[str] = []
-_VK_REFS: Dict[int, tuple] = {}      # id(vk) -> (vk, VkRef) on the submitting side (keeps vk alive)
-_VK_CACHE: Dict[bytes, object] = {}  # digest -> ChildVk on the loading side
+# Both bounded (a long-running service sees an unbounded stream of programs): least recently used out.
+_VK_REFS: "OrderedDict[int, tuple]" = OrderedDict()    # id(vk) -> (vk, VkRef), submitting side (keeps vk alive)
+_VK_CACHE: "OrderedDict[bytes, object]" = OrderedDict()  # digest -> ChildVk on the loading side
 _VK_LOCK = threading.Lock()
+CACHE_ENTRIES = 64
+
+
+def _lru_put(d: OrderedDict, k, v, cap: int = CACHE_ENTRIES):
+    d[k] = v
+    d.move_to_end(k)
+    while len(d) > cap:
+        d.popitem(last=False)
 
 
 def _vk_dir() -> str:
@@ -100,6 +110,7 @@ def vk_ref(vk) -> VkRef:
     with _VK_LOCK:
         hit = _VK_REFS.get(id(vk))
         if hit is not None and hit[0] is vk:
+            _VK_REFS.move_to_end(id(vk))
             return hit[1]
     import os
     import xxhash
@@ -113,8 +124,9 @@ def vk_ref(vk) -> VkRef:
         os.replace(tmp, path)
     ref = VkRef(digest, path)
     with _VK_LOCK:
-        _VK_REFS[id(vk)] = (vk, ref)
-        _VK_CACHE.setdefault(digest, vk)
+        _lru_put(_VK_REFS, id(vk), (vk, ref))
+        if digest not in _VK_CACHE:
+            _lru_put(_VK_CACHE, digest, vk)
     return ref
 
 
@@ -129,7 +141,7 @@ def resolve_vk(v):
         with open(v.path, "rb") as f:
             vk = pickle.loads(f.read())
         with _VK_LOCK:
-            _VK_CACHE[v.digest] = vk
+            _lru_put(_VK_CACHE, v.digest, vk)
     return vk
 
 
@@ -138,9 +150,28 @@ def by_ref(children: Sequence[tuple]) -> List[tuple]:
     return [(vk_ref(vk), proof) for vk, proof in children]
 
 
-_SENT_KEYS: set = set()          # worker side: keys whose traces this process already returned
-_PREP_STORE: Dict[bytes, dict] = {}  # consumer side: traces of every key seen
+# Worker side: per session (one tree / one Compress request), the keys whose traces this process already
+# returned.  A session's consumer registers its witnesses in arrival order (Reducer.on_witness), so within
+# a session "sent once" is safe; a new session (a new request, or a retry after a failed tree whose
+# in-flight witnesses were dropped) starts empty, so it never depends on traces another session consumed.
+_SENT_KEYS: "OrderedDict[object, set]" = OrderedDict()
+_PREP_STORE: "OrderedDict[bytes, dict]" = OrderedDict()  # consumer side: traces by key (content-addressed)
 _STORE_LOCK = threading.Lock()
+SESSIONS_KEPT = 16
+
+
+def new_session() -> str:
+    """A fresh dedup session id for node_witness (one per tree)."""
+    import uuid
+    return uuid.uuid4().hex
+
+
+def _sent_keys(session) -> set:
+    got = _SENT_KEYS.get(session)
+    if got is None:
+        got = set()
+        _lru_put(_SENT_KEYS, session, got, SESSIONS_KEPT)
+    return got
 
 
 @dataclass
@@ -225,7 +256,7 @@ def register_prep(wit):
     p = wit[0]
     if isinstance(p, Prep) and p.traces is not None:
         with _STORE_LOCK:
-            _PREP_STORE[p.key] = p.traces
+            _lru_put(_PREP_STORE, p.key, p.traces)
     return wit
 
 
@@ -271,15 +302,15 @@ def compact_traces(rec, shape) -> dict:
 
 
 def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool = False, compact: bool = False,
-                 dedup: bool = True):
+                 dedup: bool = True, session=None):
     """Worker body (no GPU): the compress node's program from its (ChildVk, proof) children, executed,
     padded to the first allowed recursion shape (fix=False: natural power-of-two heights, for small
     tests), as a compress-machine shard.  Returns (prep traces, main traces, public values, shape,
     seconds); with p2_on_device the Poseidon2WideDeg3 entry is a DeviceP2 (see materialize).  compact:
     every main trace is a device work item (compact_traces) and the prep traces a Prep, sent once per
-    program structure and worker process (dedup; a consumer must pass the witnesses of one worker through
-    register_prep in the order they were made, as Reducer does) -- a fraction of the bytes through the
-    pool's pipe."""
+    program structure, worker process and `session` (dedup; a consumer must pass the witnesses of one worker
+    through register_prep in the order they were made, as Reducer does; one session per tree) -- a fraction
+    of the bytes through the pool's pipe."""
     from . import recursion as R
     from . import recursion_verifier as RV
     t0 = time.perf_counter()
@@ -293,11 +324,11 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
             raise ValueError("FriFold instructions need the wide machine")
         key = R.prep_key(rec, shape)
         prep = None
-        if not dedup or key not in _SENT_KEYS:
+        sent = _sent_keys(session) if dedup else set()
+        if key not in sent:
             pr = R.prep_records(rec, shape)
             prep = {c.name: pr[c.name] for c in R.compress_machine().chips if c.prep_width}
-            if dedup:
-                _SENT_KEYS.add(key)
+            sent.add(key)
         traces = compact_traces(rec, shape)
         t2 = time.perf_counter()
         return Prep(key, prep), traces, rec.public_values, shape, {"build_s": t1 - t0, "execute_and_traces_s": t2 - t1}
@@ -357,6 +388,7 @@ def materialize(traces: dict) -> dict:
 
 _CVK_LOCK = threading.Lock()
 _CVK_CHIPS: Dict[object, object] = {}  # 0 -> the compress machine's chip shapes; (commit, shape, nq) -> ChildVk
+# (insertion-ordered; bounded to CACHE_ENTRIES child keys, oldest out)
 
 
 def compress_child_vk(commit, shape: Dict[str, int], num_queries: int = None):
@@ -384,7 +416,13 @@ def compress_child_vk(commit, shape: Dict[str, int], num_queries: int = None):
                     gcs=np.asarray(CURVE_CUMULATIVE_SUM_START, np.int64), log_blowup=R.COMPRESS_LOG_BLOWUP,
                     num_queries=num_queries or R.COMPRESS_NUM_QUERIES)
     with _CVK_LOCK:
-        return _CVK_CHIPS.setdefault(key, vk)
+        got = _CVK_CHIPS.get(key)
+        if got is not None:
+            return got
+        _CVK_CHIPS[key] = vk
+        while len(_CVK_CHIPS) > CACHE_ENTRIES + 1:  # entry 0 (the chip shapes) is kept
+            _CVK_CHIPS.pop(next(k for k in _CVK_CHIPS if k != 0))
+        return vk
 
 
 @dataclass
@@ -405,12 +443,16 @@ class GpuProvers:
     same structure share one zkm_setup), as `compress_prover.setup(&program)` (lib.rs:807) would compute
     the same key for them."""
 
-    def __init__(self, dev, num_queries=None):
+    def __init__(self, dev, num_queries=None, max_provers: int = 16):
         from . import recursion as R
         self.dev = dev
         self.machine = R.compress_machine()
         self.kw = dict(num_queries=num_queries or R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
-        self.cache: Dict[bytes, object] = {}
+        # least recently used out: each prover holds its program's preprocessed LDE and tree on the GPU,
+        # and a long-running service sees a new program for every distinct core program (its vk commit
+        # is in MemoryConst)
+        self.cache: "OrderedDict[bytes, object]" = OrderedDict()
+        self.max_provers = max(1, max_provers)
         self.lock = threading.Lock()
 
     def get(self, prep, stats: TreeStats):
@@ -430,7 +472,9 @@ class GpuProvers:
                 pr = HipProver(self.dev, self.machine, pt, **self.kw)
                 stats.setup_s += time.perf_counter() - t
                 stats.setups += 1
-                self.cache[key] = pr
+                _lru_put(self.cache, key, pr, self.max_provers)  # an evicted prover in use stays alive
+            else:
+                self.cache.move_to_end(key)
         return pr
 
 
@@ -550,6 +594,7 @@ class Reducer:
         on_done(node, result) is called for every node proven here."""
         pending = set(mine)
         submitted = set()
+        futs: Dict[Node, object] = {}  # witness jobs whose result has not been taken yet
         threads = [threading.Thread(target=self._gpu_worker, daemon=True) for _ in range(self.inflight)]
         for t in threads:
             t.start()
@@ -565,7 +610,9 @@ class Reducer:
                     submitted.add(node)
                     self.times.setdefault(node, {})["submit"] = time.perf_counter()
                     fut = self.submit_witness([done[c] for c in ch])
+                    futs[node] = fut
                     fut.add_done_callback(lambda f, n=node: self.events.put(("witness", n, f)))
+        ok = False
         try:
             try_submit()
             while pending:
@@ -580,6 +627,7 @@ class Reducer:
                 except queue.Empty:
                     continue
                 if kind == "witness":
+                    futs.pop(node, None)
                     self.times.setdefault(node, {})["witness"] = time.perf_counter()
                     self.gpu_q.put((node, self.on_witness(val.result())))
                 elif kind == "proof":
@@ -591,12 +639,30 @@ class Reducer:
                     try_submit()
                 else:
                     raise val
+            ok = True
         finally:
+            if not ok:  # a failed tree: its in-flight witnesses are discarded when they land
+                for f in futs.values():
+                    f.cancel()
+                    f.add_done_callback(_discard_witness)
             for _ in threads:
                 self.gpu_q.put(None)
             for t in threads:
                 t.join(timeout=60)
         return done
+
+
+def _discard_witness(f):
+    """Drop a witness nobody will prove: unlink its /dev/shm file (a Packed one)."""
+    if f.cancelled() or f.exception() is not None:
+        return
+    x = f.result()
+    if isinstance(x, Packed):
+        import os
+        try:
+            os.unlink(x.path)
+        except OSError:
+            pass
 
 
 def owner(node: Node, n_leaves: int, world: int) -> int:
@@ -675,13 +741,15 @@ def reduce_distributed(leaves: Sequence[tuple], reducer: Reducer, broadcast_root
     done = {(0, i): leaves[i] for i in range(n)}
     arrived: "queue.Queue" = queue.Queue()
 
-    def receiver(c, buf, work):
+    def receiver(buf, work):
         work.wait()
-        arrived.put((c, _unpack(buf.numpy())))
+        # the message names its node: one sender may send two nodes to this rank, completed in either
+        # order, and untagged receives from one source match in posting order, not by node
+        arrived.put(_unpack(buf.numpy()))
     rthreads = []
     for c, src in need:  # one message per (sender, receiver) pair and node: posted up front, waited in threads
         buf = torch.empty(MSG_BYTES, dtype=torch.uint8)
-        t = threading.Thread(target=receiver, args=(c, buf, dist.irecv(buf, src=src, group=grp)), daemon=True)
+        t = threading.Thread(target=receiver, args=(buf, dist.irecv(buf, src=src, group=grp)), daemon=True)
         t.start()
         rthreads.append(t)
     sends = []
@@ -696,7 +764,7 @@ def reduce_distributed(leaves: Sequence[tuple], reducer: Reducer, broadcast_root
 
     def on_done(node, res):
         if node in give:
-            t = torch.from_numpy(_pack(res))
+            t = torch.from_numpy(_pack((node, res)))
             sends.append((t, dist.isend(t, dst=give[node], group=grp)))
 
     reducer.run(done, mine, widths, remote=remote if need else None, on_done=on_done)
