@@ -37,7 +37,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # the streams of the host-trace mode (3 prover slots, the copy stream, torch's own): the copy stream then
 # shares a queue with a prover stream, whose kernels wait behind each 19.6 ms copy (34 ms per shard instead
 # of 27.5; profiles/r04_hw_queues.txt).  8 gives every stream its own queue; the resident rate is unchanged.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Forced, not a default: the GPU box exports GPU_MAX_HW_QUEUES=4, which a setdefault left in place (round 4's
+# bench line ran its host-trace mode with 4 queues: 1.27x resident, against 1.03-1.04x with 8 in the
+# controlled runs).  ZKM_BENCH_HW_QUEUES overrides (A/B only).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZKM_BENCH_HW_QUEUES", "8")
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -422,22 +425,37 @@ def size_series(args, prover0, K, logs=(20, 21, 23)):
 
 
 def maxshape_leg(args, rk, n, K):
-    """Secondary field of the default line: the reference's maximal 2^22 MIPS shard shape
-    (maximal_shapes.json["22"][2], zkmips_amd/shapes.py: 17 chips, 557M main cells, 2.23 GB of traces)
-    proven like the headline, from page-locked host traces (H2D in the timed span) and resident."""
-    sb = ShardBench(args, rk, "maxshape", n, K)
+    """Secondary field of the default line (BASELINE config 3's shape): the reference's maximal 2^22 MIPS shard
+    shape (maximal_shapes.json["22"][2], zkmips_amd/shapes.py: 17 chips, 557M main cells, 2.23 GB of traces).
+    `value`: the executor's event records (1.09 GB) in page-locked host memory, their H2D inside the span and
+    pipelined like the headline's, each shard's traces built on the device from them and proven (the trait's
+    generate_traces + commit + open, prover.rs:70-108,111-137); beside it the same steps from page-locked host
+    traces (2.23 GB of H2D per shard) and from traces resident in HBM."""
+    sb = ShardBench(args, rk, "maxshape", n, K, records=True)
+    sb.run_steps(1, "records")
     sb.run_steps(1, "pipelined")
     steps = max(1, args.maxshape_steps)
+    p0, el_rec = sb.timed(steps, "records")
+    rec_waits = {k: list(v) for k, v in sb.slot_waits.items()}
     p1, el = sb.timed(steps, "pipelined")
     p2, el_res = sb.timed(steps, "resident")
-    assert p1 == p2, "maxshape: resident / host-trace proofs differ"
+    assert p0 == p1 == p2, "maxshape: records / host-trace / resident proofs differ"
     tr = sb.shards[0][2]
     rows = sb.rows_per_shard
+    rec_bytes = int(sum(int(t.numel()) for t in sb.records["pinned"].values()))
     out = {"workload": "MIPS shard in the reference maximal shape maximal_shapes.json[\"22\"][2]: "
                        + ", ".join(f"{k} 2^{int(np.log2(len(tr[k])))}" for k in sorted(tr, key=lambda c: -len(tr[c]))),
-           "rows_per_shard": rows, "main_cells": int(sum(v.size for v in tr.values())),
-           "h2d_bytes_per_shard": int(sum(v.nbytes for v in tr.values())), "steps": steps, "in_flight": K,
-           "value": round(K * rows * steps / el, 1), "unit": "rows/s", "ms_per_shard": round(1e3 * el / (steps * K), 3),
+           "rows_per_shard": rows, "main_cells": int(sum(v.size for v in tr.values())), "steps": steps, "in_flight": K,
+           "value": round(K * rows * steps / el_rec, 1), "unit": "rows/s",
+           "ms_per_shard": round(1e3 * el_rec / (steps * K), 3),
+           "value_basis": "event records in page-locked host memory, H2D of the records + device trace generation + "
+                          "commit + open + proof D2H inside the span",
+           "h2d_bytes_per_shard": rec_bytes,
+           "vs_resident": round(el_rec / el_res, 3),
+           "records_copy_wait_ms": [round(1e3 * sum(v), 2) for _, v in sorted(rec_waits.items())],
+           "host_traces": {"value": round(K * rows * steps / el, 1), "ms_per_shard": round(1e3 * el / (steps * K), 3),
+                           "h2d_bytes_per_shard": int(sum(v.nbytes for v in tr.values())),
+                           "vs_resident": round(el / el_res, 3)},
            "resident": {"value": round(K * rows * steps / el_res, 1), "ms_per_shard": round(1e3 * el_res / (steps * K), 3)},
            "proof_bytes": len(p1), "trace_generation_s": round(sb.gen_s, 1)}
     out["from_device_traces"] = maxshape_from_records(sb, steps)
@@ -1120,12 +1138,14 @@ def launch_ranks(n: int, argv) -> int:
 
 
 class ShardBench:
-    """`K` in-flight slots proving shards of one workload on this rank's GPU, in three modes:
-    "pipelined" (the headline: page-locked host traces, the H2D DMA of step j+1 on the slot's copy stream
-    while step j proves from the other HBM buffer), "per_call" (zkm_prove_shard copies the pinned host
-    traces itself) and "resident" (traces already in HBM)."""
+    """`K` in-flight slots proving shards of one workload on this rank's GPU, in four modes:
+    "pipelined" (the headline: page-locked host traces, the H2D DMA of steps j+1..j+depth on the copy
+    stream while step j proves from another HBM buffer), "records" (maximal shape: the executor's event
+    records are what crosses PCIe, pipelined the same way, and each step builds its traces on the device
+    from them -- the trait's own generate_traces, prover.rs:70-108 -- before proving), "per_call"
+    (zkm_prove_shard copies the pinned host traces itself) and "resident" (traces already in HBM)."""
 
-    def __init__(self, args, rk, workload, n, K):
+    def __init__(self, args, rk, workload, n, K, records: bool = False):
         import torch
         from zkmips_amd._lib import Device
         from zkmips_amd.prover import HipProver
@@ -1136,18 +1156,38 @@ class ShardBench:
             t0 = time.time()
             one = make_shard(workload, n, 1)
             self.gen_s = time.time() - t0
+        self.depth = max(1, getattr(args, "h2d_depth", 2))  # copies in flight ahead of the proving step
+        nbuf = self.depth + 1
+        self.records = None
+        if records:
+            # the executor's records as the header's structs (converted once, outside any timed region: the
+            # reference's executor hands its event vectors as they lie), page-locked
+            from zkmips_amd import tracegen as TG
+            host = TG.shard_records(_CAPTURE[workload])
+            self.records = {"_n": {kk: len(v) for kk, v in host.items()}, "pinned": {}}
+            for kk, v in host.items():
+                raw = np.ascontiguousarray(v).view(np.uint8).reshape(-1)
+                t = torch.empty(max(1, raw.size), dtype=torch.uint8, pin_memory=True)
+                t.numpy()[:raw.size] = raw
+                self.records["pinned"][kk] = t
         for k in range(K):
             m, prep, traces_k, pvs_k = one if one is not None else make_shard(workload, n, 1000 + rk.rank * K + k)
             pinned = {}
             for kk, v in traces_k.items():
                 pinned[kk] = torch.empty(v.shape, dtype=torch.int32, pin_memory=True)
                 pinned[kk].numpy()[...] = v.view(np.int32)
+            src = self.records["pinned"] if records else pinned
             self.shards.append(({kk: torch.from_numpy(v.view(np.int32)).cuda() for kk, v in traces_k.items()}, pvs_k,
                                 {kk: t.numpy().view(np.uint32) for kk, t in pinned.items()}, pinned,
                                 [{kk: (torch.empty_like(t, device="cuda") if args.h2d_dst == "torch" else
-                                       RawDev(t.shape, H2D_FLAGS[args.h2d_dst])) for kk, t in pinned.items()}
-                                 for _ in range(2)],
+                                       RawDev(t.shape, H2D_FLAGS[args.h2d_dst])) for kk, t in src.items()}
+                                 for _ in range(nbuf)],
                                 torch.cuda.Stream()))
+        if records:
+            from zkmips_amd import mips_alu as A
+            self.heights = {kk: int(v.shape[0]) for kk, v in self.shards[0][0].items() if kk not in ("Byte", "Program")}
+            self.byte_mult = [torch.zeros((A.BYTE_ROWS, A.BYTE_MULT_WIDTH), dtype=torch.int32, device="cuda")
+                              for _ in range(K)]
         self.m = m
         self.prover = HipProver(Device(rk.local_rank), m, prep, num_queries=args.queries)
         torch.cuda.synchronize()
@@ -1181,13 +1221,16 @@ class ShardBench:
 
         # one copy stream for all slots (ZKM_BENCH_COPY_STREAMS=slot: one per slot): copies run FIFO at the full
         # PCIe rate in the order the slots issue them, instead of sharing the link and all landing late
+        slot_stream = cs
         cs = self.copy_stream if self.copy_stream is not None else cs
+        nbuf = len(bufs)
+        src_t = self.records["pinned"] if mode == "records" else host_t
 
         def issue(j):
-            b = bufs[j % 2]
+            b = bufs[j % nbuf]
             # one slot's copies go into the shared stream together (FIFO per slot, not interleaved per trace)
             with self.copy_lock, torch.cuda.stream(cs):
-                for kk, t in host_t.items():
+                for kk, t in src_t.items():
                     if isinstance(b[kk], RawDev):
                         b[kk].copy_from_host(t, cs)
                     else:
@@ -1201,25 +1244,43 @@ class ShardBench:
         stagger = self.stagger if self.copy_stream is None else None
         if stagger is not None and k > 0:
             stagger[k - 1].wait(60)  # bounded: a failing slot must not hang the others
-        ev = issue(0)
+        evs = {0: issue(0)}  # step -> its copies' event; the look-ahead copies are issued once step 0's landed
         pr = b""
         waits, ts = [], []
         for j in range(nsteps):
             t = time.perf_counter()
-            ev.synchronize()
+            evs.pop(j).synchronize()
             waits.append(time.perf_counter() - t)
             if j == 0 and stagger is not None:
                 stagger[k].set()
-            nxt = issue(j + 1) if j + 1 < nsteps else None
+            for jj in range(j + 1, min(nsteps, j + 1 + self.depth)):
+                if jj not in evs:  # buffer jj % nbuf last served step jj - nbuf <= j - 1: proven already
+                    evs[jj] = issue(jj)
             # ZKM_BENCH_DMA_PROBE=1 (experiment only): the same copies, proofs from the resident traces
-            src = dev_t if os.environ.get("ZKM_BENCH_DMA_PROBE") == "1" else bufs[j % 2]
+            src = dev_t if os.environ.get("ZKM_BENCH_DMA_PROBE") == "1" else bufs[j % nbuf]
             t = time.perf_counter()
+            if mode == "records":
+                src = self.traces_from_records(k, src, slot_stream)
             pr = prove_resident(prover, src, pv)
             ts.append(time.perf_counter() - t)
-            ev = nxt
         self.slot_waits[k] = waits  # host seconds each step waited for its traces' copy
         self.slot_proof_s[(mode, k)] = ts
         return pr
+
+    def traces_from_records(self, k, recs, stream):
+        """Slot k's shard traces built on the device (zkmips_amd/tracegen.shard_traces, every chip at the
+        shape's height, Byte and Program multiplicities included) from its records in HBM, on its stream,
+        waited for."""
+        import torch
+        from zkmips_amd import tracegen as TG
+        bm = self.byte_mult[k]
+        with torch.cuda.stream(stream):
+            bm.zero_()
+            tr = TG.shard_traces(_CAPTURE["maxshape"], byte_mult=bm, heights=self.heights,
+                                 records=dict(recs, _n=self.records["_n"]))
+            tr["Byte"] = bm
+            stream.synchronize()
+        return {kk: tr[kk] for kk in self.shards[k][0]}  # the shard's chips, in the host-trace order
 
     def run_steps(self, nsteps, mode="pipelined"):
         """nsteps shard proofs per in-flight slot; returns the last proof of slot 0, after gathering
@@ -1277,6 +1338,8 @@ def main():
     ap.add_argument("--sha-blocks", type=int, default=16384, help="sha2 workload: 64-byte blocks hashed")
     ap.add_argument("--h2d-dst", choices=["torch", "uncached", "finegrained"], default="torch",
                     help="memory type of the HBM buffers the pipelined H2D copies land in")
+    ap.add_argument("--h2d-depth", type=int, default=2,
+                    help="host-trace / records modes: steps whose copies are issued ahead of the proving step")
     ap.add_argument("--sha-events-per-shard", type=int, default=16384,
                     help="sha2 workload: precompile calls per precompile shard")
     ap.add_argument("--workload", choices=["fib", "alu", "core", "maxshape", "sha2", "tendermint", "tracegen", "compress"],
@@ -1341,15 +1404,17 @@ def main():
     dev_traces, pvs, traces = sb.shards[0][0], sb.shards[0][1], sb.shards[0][2]
     rows_per_shard = sb.rows_per_shard
     if args.warmup:
-        sb.run_steps(args.warmup, "resident")
-        sb.run_steps(1, "pipelined")
+        sb.run_steps(args.warmup, "pipelined")
+        sb.run_steps(1, "resident")
         sb.run_steps(1, "per_call")
-    # timed region (the headline `value`): traces resident in HBM, commit + open + D2H of the proof
-    progress("timed regions: resident, host traces, per-call copies")
-    proof_res, elapsed_res = sb.timed(args.steps, "resident")
-    # secondary: host traces with the look-ahead H2D pipeline, and per-call host copies
+    # timed region (the headline `value`): traces in page-locked host memory, their H2D
+    # inside the span (pipelined: the next shards' copies overlap the current proof), commit + open + D2H of
+    # the proof
+    progress("timed regions: host traces (headline), resident, per-call copies")
     proof, elapsed = sb.timed(args.steps, "pipelined")
     copy_waits = {k: list(v) for k, v in sb.slot_waits.items()}
+    # secondary: the same steps with the traces already in HBM, and with per-call host copies
+    proof_res, elapsed_res = sb.timed(args.steps, "resident")
     proof_ms = {m: round(1e3 * float(np.mean([t for (mm, _), v in sb.slot_proof_s.items() if mm == m for t in v])), 3)
                 for m in ("resident", "pipelined")}
     proof_pc, elapsed_pc = sb.timed(args.steps, "per_call")
@@ -1464,7 +1529,7 @@ def main():
     stages = {k: {"count": v[0], "ms_per_shard": round(v[1] / nprof, 3)}
               for k, v in sorted(prof.items()) if not k.endswith("_perms") and not k.endswith("_gfops")}
 
-    value = world * K * rows_per_shard * args.steps / elapsed_res
+    value = world * K * rows_per_shard * args.steps / elapsed
     line = {
         "metric": "shard trace rows proved/sec at 2^22 rows",
         "value": round(value, 1),
@@ -1472,14 +1537,15 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed_res / args.steps, 3),
-        "ms_per_shard": round(1e3 * elapsed_res / (args.steps * K), 3),
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "ms_per_shard": round(1e3 * elapsed / (args.steps * K), 3),
         "serial_ms_per_shard": round(serial_ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32 (KoalaBear mod p, EF = F[X]/(X^4-3))",
-        "data": "synthetic (seeded S-SHARD traces, SURVEY.md §8d), resident in HBM when the timed region starts; proof D2H timed",
+        "data": ("synthetic (seeded S-SHARD traces, SURVEY.md §8d) in page-locked host memory: their H2D and the "
+                 "proof's D2H inside the timed span"),
         "config": {"workload": (f"S-SHARD FibCpu 2^{args.log_n} rows (main 67, LogUp 11 EF, quotient 2) + FibTable "
                                 f"2^{W.fib_table_height(n).bit_length() - 1} (prep 2): full commit+open per shard")
                    if args.workload == "fib" else
@@ -1503,12 +1569,17 @@ def main():
         "host_per_call": {"value": round(world * K * rows_per_shard * args.steps / elapsed_pc, 1), "unit": "rows/s",
                           "ms_per_shard": round(1e3 * elapsed_pc / (args.steps * K), 3),
                           "what": "same steps, each zkm_prove_shard copies its pinned host traces itself (no look-ahead)"},
-        "value_basis": ("traces resident in HBM when the timed region starts (the benchmark contract), D2H of "
-                        "each proof inside it; the PCIe-inclusive rate of the same steps (SURVEY.md section 8d's "
-                        "host-trace definition) is `host_traces`"),
+        "value_basis": ("SURVEY.md section 8d: traces in page-locked host memory when the timed region starts, "
+                        "every H2D copy and each proof's D2H inside it (copies of the next shards overlap the "
+                        "current proofs); the same steps from traces already in HBM are `resident`"),
+        "resident": {"value": round(world * K * rows_per_shard * args.steps / elapsed_res, 1), "unit": "rows/s",
+                     "ms_per_shard": round(1e3 * elapsed_res / (args.steps * K), 3),
+                     "ms_per_step": round(1e3 * elapsed_res / args.steps, 3)},
         "host_traces": {"value": round(world * K * rows_per_shard * args.steps / elapsed, 1), "unit": "rows/s",
                         "ms_per_shard": round(1e3 * elapsed / (args.steps * K), 3),
                         "vs_resident": round(elapsed / elapsed_res, 3),
+                        "copies_ahead": sb.depth,
+                        "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                         "h2d_alone_ms_per_shard": round(h2d_alone_s * 1e3, 3),
                         "h2d_GBps": round(sum(v.nbytes for v in traces.values()) / h2d_alone_s / 1e9, 2),
                         "copy_wait_ms": {"first_step_per_slot": [round(1e3 * v[0], 2) for _, v in sorted(copy_waits.items())],

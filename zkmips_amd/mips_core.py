@@ -1632,7 +1632,8 @@ def _mem_word(addr):
 
 
 def _ev_arrays(lst):
-    arr = np.asarray(lst, np.uint64).reshape(-1, 6)
+    from itertools import chain
+    arr = np.fromiter(chain.from_iterable(lst), np.int64, count=6 * len(lst)).reshape(-1, 6)
     return tuple(arr[:, i].astype(np.uint32) for i in range(6))
 
 

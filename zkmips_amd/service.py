@@ -329,8 +329,11 @@ class ProverService:
             return CT.compress_child_vk(pr.vk_commit, shape), proof
 
         if self._pool is not None:
+            # one dedup session per request: a worker resends a program's prep traces to each request
+            # (a failed or concurrent request never leaves another depending on traces it consumed)
+            sid = CT.new_session()
             submit = lambda ch: self._pool.submit(CT.node_witness_shm, CT.by_ref(ch), True, True, True,
-                                                  tag=CT.node_tag(ch))
+                                                  session=sid, tag=CT.node_tag(ch))
         else:
             from concurrent.futures import ThreadPoolExecutor
             tp = ThreadPoolExecutor(2)

@@ -115,12 +115,18 @@ def cpu_events(steps, shard: int) -> np.ndarray:
     e = np.zeros(n, CPU_EVENT)
     if not n:
         return e
-    S = np.asarray([s_[:11] for s_ in steps], np.int64)
+    # one flat pass over the step tuples per field group (np.fromiter over chained item getters: ~4x faster
+    # than np.asarray of per-step lists)
+    from itertools import chain
+    from operator import itemgetter
+    S = np.fromiter(chain.from_iterable(map(itemgetter(*range(11), 12, 13), steps)), np.int64,
+                    count=13 * n).reshape(n, 13)
     ks, av, bv, cv, prev_a, written = S[:, 0], S[:, 2], S[:, 3], S[:, 4], S[:, 5], S[:, 6]
     immb, immc = S[:, 9].astype(bool), S[:, 10].astype(bool)
-    clk = np.asarray([s_[13] for s_ in steps], np.int64)
-    prev = np.asarray([[p if p is not None else (0, 0) for p in s_[11]] for s_ in steps], np.int64)  # c, b, a
-    his = np.asarray([s_[12] for s_ in steps], np.int64)
+    clk, his = S[:, 12], S[:, 11]
+    Z = (0, 0)
+    prev = np.fromiter(chain.from_iterable(x or Z for x in chain.from_iterable(map(itemgetter(11), steps))),
+                       np.int64, count=6 * n).reshape(n, 3, 2)  # c, b, a
     e["clk"], e["pc"] = clk, MC.PC_BASE + 4 * ks
     e["next_pc"], e["next_next_pc"] = S[:, 7], S[:, 8]
     e["a"], e["b"], e["c"] = av, bv, cv
