@@ -827,6 +827,69 @@ __device__ __forceinline__ void net8b(uint32_t *v, __amdgpu_buffer_rsrc_t rtw, u
         }
     }
 }
+// The same network with its twiddles generated in registers from ONE loaded value.  Stage st of the network
+// (half-size h = rs 2^st S rows) uses w_{st,m} = w_{2h}^{(off + rs m) S + ct} = w_{st,0} * w_{2^(st+1)}^m, and
+// w_{st,0} = w_{st+1,0}^2 (the same exponent, a root of half the order); so only w_{2,0} is read and the other
+// six twiddles cost two squarings and four products by the constants w_4^1, w_8^1..3 of the table's direction
+// (the strided passes spent 35 of 51 vector-memory instructions per wave on twiddle loads with the VALU ~9 %
+// busy, profiles/r04_lde_pmc.txt).
+struct TwC {
+    uint32_t w4, w8[3];  // w_4^1 = tw[3], w_8^m = tw[4 + m]
+};
+__device__ __forceinline__ TwC twc(const uint32_t *__restrict__ tw) {
+    return TwC{tw[3], {tw[5], tw[6], tw[7]}};
+}
+struct Tw8 {
+    uint32_t w[3][4];  // w[st][m], m < 2^st
+};
+__device__ __forceinline__ Tw8 tw8(uint32_t wtop, const TwC &c) {
+    Tw8 r;
+    r.w[2][0] = wtop;
+    r.w[1][0] = mul(wtop, wtop);
+    r.w[0][0] = mul(r.w[1][0], r.w[1][0]);
+    r.w[1][1] = mul(r.w[1][0], c.w4);
+#pragma unroll
+    for (int m = 1; m < 4; m++) r.w[2][m] = mul(wtop, c.w8[m - 1]);
+    return r;
+}
+template <bool DIT>
+__device__ __forceinline__ void net8r(uint32_t *v, const Tw8 &W) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const int st = DIT ? q : 2 - q;
+        const int span = 1 << st;
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+            const uint32_t w = W.w[st][m];
+#pragma unroll
+            for (int k = m; k < 8; k += 2 * span) {
+                const uint32_t a = v[k], b = v[k + span];
+                if (DIT) {
+                    const uint32_t tt = mul(b, w);
+                    if (q < 2 && ((k >> (st + 1)) & 1)) {
+                        v[k] = a + tt;
+                        v[k + span] = a + (P - tt);
+                    } else {
+                        v[k] = add(a, tt);
+                        v[k + span] = sub(a, tt);
+                    }
+                } else {
+                    v[k] = add(a, b);
+                    v[k + span] = mul(a + (P - b), w);
+                }
+            }
+        }
+    }
+}
+// one network's stages: twiddles loaded (net8b) or generated from w_{2,0} (net8r); the top twiddle sits at
+// voff + soff0 + 4 rs S words
+template <bool DIT, int LAY, bool TWG>
+__device__ __forceinline__ void net8x(uint32_t *v, __amdgpu_buffer_rsrc_t rtw, uint32_t voff, uint32_t soff0,
+                                      uint32_t S4, const TwC &c) {
+    if constexpr (TWG) net8r<DIT>(v, tw8(bld(rtw, voff, soff0 + 4 * RS<LAY> * S4), c));
+    else net8b<DIT, LAY>(v, rtw, voff, soff0, S4);
+}
+
 template <int LAY, bool SWZ>
 __device__ __forceinline__ void to_ldsb(uint32_t *x, const uint32_t v[16], uint32_t u, uint32_t t) {
 #pragma unroll
@@ -846,7 +909,7 @@ __device__ __forceinline__ void from_ldsb(const uint32_t *x, uint32_t v[16], uin
 // TILE (bit 0: source, bit 1: destination; only for the one-pass case 512 x S = the column): that side is
 // tile-major -- the tile's 512 rows x 32 columns contiguous (64 KB, row pitch 32 words) at tile index
 // c0 / 32 -- instead of row-major with pitch S (the LDE's intermediates, lde_natural ZKM_LDE_TILED).
-template <bool DIT, int MODE, int TILE = 0>
+template <bool DIT, int MODE, int TILE = 0, bool TWG = true>
 __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                         int logS, const uint32_t *__restrict__ tw,
                                                         uint32_t tw_words, uint32_t nv, int remap) {
@@ -870,6 +933,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
     const uint64_t tbase = (uint64_t)(c0 >> 5) * (512u * 32u);  // tile-major: the tile's 64 KB
     const auto rsrc = TS ? mkrs(src + ms.off(col) + tbase, 512u * 128u) : mkrs(src + ms.off(col) + base, 512u * S4);
     const auto rtw = mkrs(tw, tw_words * 4);
+    const TwC twk = TWG ? twc(tw) : TwC{};
     const uint32_t vLL = ct * 4;                    // twiddle offsets per layout / network
     const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4, vLM1 = (((2 * u + 1) & 7) * S + ct) * 4;
     const uint32_t vLH = (u * S + ct) * 4;          // also rows u + 32 n + 64 k of the tile
@@ -884,19 +948,25 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
         for (int n = 0; n < 2; n++)
 #pragma unroll
             for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, sL16, (uint32_t)(8 * n + k) * sP4);
-        net8b<true, LL>(v, rtw, vLL, 0, S4);
-        net8b<true, LL>(v + 8, rtw, vLL, 0, S4);
+        if constexpr (TWG) {  // both networks of LL share their twiddles (off = 0)
+            const Tw8 W = tw8(bld(rtw, vLL, 4 * S4), twk);
+            net8r<true>(v, W);
+            net8r<true>(v + 8, W);
+        } else {
+            net8b<true, LL>(v, rtw, vLL, 0, S4);
+            net8b<true, LL>(v + 8, rtw, vLL, 0, S4);
+        }
         to_ldsb<LL, false>(x, v, u, t);
         __syncthreads();
         from_ldsb<LM, false>(x, v, u, t);
-        net8b<true, LM>(v, rtw, vLM0, 0, S4);
-        net8b<true, LM>(v + 8, rtw, vLM1, 0, S4);
+        net8x<true, LM, TWG>(v, rtw, vLM0, 0, S4, twk);
+        net8x<true, LM, TWG>(v + 8, rtw, vLM1, 0, S4, twk);
         __syncthreads();
         to_ldsb<LM, false>(x, v, u, t);
         __syncthreads();
         from_ldsb<LH, false>(x, v, u, t);
-        net8b<true, LH>(v, rtw, vLH, 0, S4);
-        net8b<true, LH>(v + 8, rtw, vLH, 32 * S4, S4);
+        net8x<true, LH, TWG>(v, rtw, vLH, 0, S4, twk);
+        net8x<true, LH, TWG>(v + 8, rtw, vLH, 32 * S4, S4, twk);
         if (MODE == MODE_PLAIN) {
             const auto rdst = TD ? mkrs(dst + md.off(col) + tbase, 512u * 128u) : mkrs(dst + md.off(col) + base, 512u * S4);
 #pragma unroll
@@ -922,19 +992,25 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
         for (int n = 0; n < 2; n++)
 #pragma unroll
             for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, sLH, (uint32_t)(32 * n + 64 * k) * sP4);
-        net8b<false, LH>(v, rtw, vLH, 0, S4);
-        net8b<false, LH>(v + 8, rtw, vLH, 32 * S4, S4);
+        net8x<false, LH, TWG>(v, rtw, vLH, 0, S4, twk);
+        net8x<false, LH, TWG>(v + 8, rtw, vLH, 32 * S4, S4, twk);
         to_ldsb<LH, false>(x, v, u, t);
         __syncthreads();
         from_ldsb<LM, false>(x, v, u, t);
-        net8b<false, LM>(v, rtw, vLM0, 0, S4);
-        net8b<false, LM>(v + 8, rtw, vLM1, 0, S4);
+        net8x<false, LM, TWG>(v, rtw, vLM0, 0, S4, twk);
+        net8x<false, LM, TWG>(v + 8, rtw, vLM1, 0, S4, twk);
         __syncthreads();
         to_ldsb<LM, false>(x, v, u, t);
         __syncthreads();
         from_ldsb<LL, false>(x, v, u, t);
-        net8b<false, LL>(v, rtw, vLL, 0, S4);
-        net8b<false, LL>(v + 8, rtw, vLL, 0, S4);
+        if constexpr (TWG) {  // both networks of LL share their twiddles (off = 0)
+            const Tw8 W = tw8(bld(rtw, vLL, 4 * S4), twk);
+            net8r<false>(v, W);
+            net8r<false>(v + 8, W);
+        } else {
+            net8b<false, LL>(v, rtw, vLL, 0, S4);
+            net8b<false, LL>(v + 8, rtw, vLL, 0, S4);
+        }
         const auto rdst = TD ? mkrs(dst + md.off(col) + tbase, 512u * 128u) : mkrs(dst + md.off(col) + base, 512u * S4);
 #pragma unroll
         for (int n = 0; n < 2; n++)
@@ -1246,6 +1322,20 @@ static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 column
 
 static int strided_T(int logR) { return logR >= 9 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
 
+// k_ntt_s9b with its twiddles generated in registers (default) or loaded per butterfly group
+// (ZKM_NTT_TWLOAD=1, the round-4 form: A/B knob)
+template <bool DIT, int MODE, int TL>
+static void launch_s9b(dim3 g1, hipStream_t s, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, int logS,
+                       const uint32_t *tw, uint32_t tw_words, uint32_t nv, int remap) {
+    static const bool twload = getenv("ZKM_NTT_TWLOAD") != nullptr;
+    if (twload)
+        hipLaunchKernelGGL((k_ntt_s9b<DIT, MODE, TL, false>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                           tw_words, nv, remap);
+    else
+        hipLaunchKernelGGL((k_ntt_s9b<DIT, MODE, TL, true>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
+                           tw_words, nv, remap);
+}
+
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
                         int logS, const uint32_t *tw, int mode, hipStream_t s, Twist tws = Twist{},
@@ -1257,16 +1347,13 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
     if (tile) {  // k_ntt_s9b with a tile-major source (bit 0) and / or destination (bit 1)
         const dim3 g1(g.x * nv);
-#define S9T(TL)                                                                                                   \
-    if (!DIT)                                                                                                     \
-        hipLaunchKernelGGL((k_ntt_s9b<false, MODE_PLAIN, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw, \
-                           tw_words, nv, 1);                                                                      \
-    else if (mode == MODE_PLAIN)                                                                                  \
-        hipLaunchKernelGGL((k_ntt_s9b<true, MODE_PLAIN, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,  \
-                           tw_words, nv, 1);                                                                      \
-    else                                                                                                          \
-        hipLaunchKernelGGL((k_ntt_s9b<true, MODE_BITREV_OUT, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, \
-                           tw, tw_words, nv, 1);
+#define S9T(TL)                                                                                 \
+    if (!DIT)                                                                                   \
+        launch_s9b<false, MODE_PLAIN, TL>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, 1);  \
+    else if (mode == MODE_PLAIN)                                                                \
+        launch_s9b<true, MODE_PLAIN, TL>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, 1);   \
+    else                                                                                        \
+        launch_s9b<true, MODE_BITREV_OUT, TL>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, 1);
         if (tile == 1) { S9T(1) } else if (tile == 2) { S9T(2) } else { S9T(3) }
 #undef S9T
         HIP_CHECK(hipGetLastError());
@@ -1316,14 +1403,11 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
             return;
         }
         if (!DIT)
-            hipLaunchKernelGGL((k_ntt_s9b<false, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                               tw_words, nv, remap);
+            launch_s9b<false, MODE_PLAIN, 0>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, remap);
         else if (mode == MODE_PLAIN)
-            hipLaunchKernelGGL((k_ntt_s9b<true, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                               tw_words, nv, remap);
+            launch_s9b<true, MODE_PLAIN, 0>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, remap);
         else
-            hipLaunchKernelGGL((k_ntt_s9b<true, MODE_BITREV_OUT>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
-                               tw, tw_words, nv, remap);
+            launch_s9b<true, MODE_BITREV_OUT, 0>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, remap);
         HIP_CHECK(hipGetLastError());
         return;
     }
