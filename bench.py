@@ -1176,13 +1176,15 @@ class ShardBench:
             for kk, v in traces_k.items():
                 pinned[kk] = torch.empty(v.shape, dtype=torch.int32, pin_memory=True)
                 pinned[kk].numpy()[...] = v.view(np.int32)
-            src = self.records["pinned"] if records else pinned
             self.shards.append(({kk: torch.from_numpy(v.view(np.int32)).cuda() for kk, v in traces_k.items()}, pvs_k,
                                 {kk: t.numpy().view(np.uint32) for kk, t in pinned.items()}, pinned,
                                 [{kk: (torch.empty_like(t, device="cuda") if args.h2d_dst == "torch" else
-                                       RawDev(t.shape, H2D_FLAGS[args.h2d_dst])) for kk, t in src.items()}
+                                       RawDev(t.shape, H2D_FLAGS[args.h2d_dst])) for kk, t in pinned.items()}
                                  for _ in range(nbuf)],
-                                torch.cuda.Stream()))
+                                torch.cuda.Stream(),
+                                # the records mode's HBM buffers (one set per step in flight)
+                                [{kk: torch.empty_like(t, device="cuda") for kk, t in self.records["pinned"].items()}
+                                 for _ in range(nbuf)] if records else None))
         if records:
             from zkmips_amd import mips_alu as A
             self.heights = {kk: int(v.shape[0]) for kk, v in self.shards[0][0].items() if kk not in ("Byte", "Program")}
@@ -1203,7 +1205,9 @@ class ShardBench:
         """nsteps shard proofs of in-flight slot k; returns the last proof."""
         import torch
         prover = self.prover
-        dev_t, pv, host_np, host_t, bufs, cs = self.shards[k]
+        dev_t, pv, host_np, host_t, bufs, cs, rbufs = self.shards[k]
+        if mode == "records":
+            bufs = rbufs
         if mode == "resident":
             pr = b""
             ts = []
@@ -1441,7 +1445,7 @@ def main():
     import torch
     h2d_s = []
     for _ in range(3):
-        _, _, _, host_t, bufs, cs = sb.shards[0]
+        _, _, _, host_t, bufs, cs, _ = sb.shards[0]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with torch.cuda.stream(cs):

@@ -163,7 +163,7 @@ def test_node_flat_template(leaves, monkeypatch):
     _flat_equal(a, R.flatten(RV.compress_node_program([(vk, proofs[0]), (vk, proofs[1])])))
     _flat_equal(b, R.flatten(RV.compress_node_program([(vk, proofs[1]), (vk, proofs[0])])))
     ra, rb = R.execute(a), R.execute(b)
-    assert not np.array_equal(ra.public_values, rb.public_values)
+    assert not np.array_equal(a.a["hint"]["vals"], b.a["hint"]["vals"])  # the same program, other hints
     assert np.array_equal(rb.public_values, R.execute(RV.compress_node_program([(vk, proofs[1]), (vk, proofs[0])])).public_values)
     bad = bytearray(proofs[1])
     p = RV.parse_shard_proof(proofs[1])

@@ -1,0 +1,494 @@
+"""Public-value semantics of a compress node program: what a node asserts about its children's public values
+and the `RecursionPublicValues` it commits (BASELINE config 5).
+
+The reference reduces an execution's shard proofs in two kinds of recursion program:
+
+* the core program (`ZKMRecursiveVerifier::verify`, crates/recursion/circuit/src/machine/core.rs:120-560) verifies
+  a batch of consecutive MIPS shard proofs and checks that they chain: shard numbers, execution-shard numbers,
+  pc continuity (start_pc = previous next_pc, a CPU-less shard keeps its pc), exit code zero, the MemoryInit /
+  MemoryFinalize address bits, committed-value and deferred-proof digests that only change in a CPU shard, the
+  first shard's boundary conditions (shard 1, pc = vk.pc_start, zero address bits, the vk's initial global sum),
+  shard < 2^16; it sums the shards' Global-scope cumulative sums on the septic curve and commits a
+  `RecursionPublicValues` (the vk digest, the range of shards, pcs and address bits it covers, the sum);
+* the compress program (`ZKMCompressWithVKeyVerifier` = `ZKMMerkleProofVerifier` + `ZKMCompressVerifier`,
+  machine/vkey_proof.rs:120-145, machine/compress.rs:93-436) verifies recursion proofs: each child's vk is a
+  member of the vk Merkle tree (zkmips_amd/vk_tree.py), each child's public-value digest is the Poseidon2 hash of
+  its first 223 values (`assert_recursion_public_values_valid`), its vk_root is the node's, and consecutive
+  children chain (start_pc = previous next_pc, start_shard = previous next_shard, execution shards,
+  address bits, digests, reconstruct-deferred digests); the node commits their aggregate.
+
+Both end with `assert_complete` (machine/complete.rs) when the node is the root of the whole execution.
+
+Children that are neither MIPS shards nor recursion proofs (this repository's synthetic FibCpu machine) get the
+structural part only: the node commits a RecursionPublicValues with the vk digest, the Global-scope sum and zero
+chaining fields, so that the compress layers above it apply the same checks to every tree.
+
+Everything is built with the verifier Builder (recursion_verifier.py) and carried twice: program addresses and
+the host's values (from the child proofs), so hints (inverses, curve sums, bits, Merkle paths) are known when the
+program is built and a failed check raises ValueError on the host before anything runs (the runtime would stop
+at the same check).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import recursion as R
+from . import septic as SP
+from . import vk_tree as VT
+from .machine import P
+
+# core PublicValues (crates/stark/src/air/public_values.rs:19-56): 8 words x 4 bytes, deferred digest 8, then
+C_COMMITTED, C_DEFERRED, C_START_PC, C_NEXT_PC, C_EXIT, C_SHARD, C_EXEC = 0, 32, 40, 41, 42, 43, 44
+C_PREV_INIT, C_LAST_INIT, C_PREV_FIN, C_LAST_FIN = 45, 77, 109, 141
+
+# RecursionPublicValues (crates/recursion/core/src/air/public_values.rs:79-145)
+R_COMMITTED, R_DEFERRED = 0, 32
+R_START_PC, R_NEXT_PC, R_START_SHARD, R_NEXT_SHARD, R_START_EXEC, R_NEXT_EXEC = 40, 41, 42, 43, 44, 45
+R_PREV_INIT, R_LAST_INIT, R_PREV_FIN, R_LAST_FIN = 46, 78, 110, 142
+R_START_RECON, R_END_RECON, R_VK_DIGEST, R_VK_ROOT, R_GCS = 174, 182, 190, 198, 206
+R_IS_COMPLETE, R_CONTAINS_EXEC, R_EXIT, R_DIGEST = 220, 221, 222, 223
+NUM_PV_ELMS_TO_HASH = R_DIGEST  # public_values.rs:33
+assert R_DIGEST == R.PV_DIGEST_START
+
+MAX_LOG_NUMBER_OF_SHARDS = 16  # core/machine/src/mips/mod.rs:65
+MAX_CPU_LOG_DEGREE = 22        # core/machine/src/cpu/mod.rs:8
+
+
+@dataclass
+class V:
+    """A vector of program values: addresses `a` and the host's canonical values `v` (same shape)."""
+    a: np.ndarray
+    v: np.ndarray
+
+    def __getitem__(self, k):
+        return V(np.asarray(self.a)[k], np.asarray(self.v)[k])
+
+    def __len__(self):
+        return len(np.asarray(self.a).reshape(-1))
+
+
+def cat(*xs: V) -> V:
+    return V(np.concatenate([np.asarray(x.a, np.int64).reshape(-1) for x in xs]),
+             np.concatenate([np.asarray(x.v, np.int64).reshape(-1) for x in xs]))
+
+
+@dataclass
+class ChildVars:
+    """What verify_shard leaves for the public-value checks of one child."""
+    pv: V                      # the proof's public values (hinted), full length
+    vk_commit: np.ndarray      # addresses of the vk commitment (its const_fresh block)
+    names: List[str]           # chips of the shard, in proof order
+    log_degrees: List[int]
+    global_sums: List[V] = field(default_factory=list)  # 14 words per Global-scope chip, in proof order
+
+
+class Ops:
+    """Base-field arithmetic on V with host values alongside."""
+
+    def __init__(self, b):
+        self.b = b
+
+    def const(self, vals) -> V:
+        v = np.asarray(vals, np.int64) % P
+        return V(np.vectorize(self.b.const, otypes=[np.int64])(v) if v.ndim else np.int64(self.b.const(int(v))), v)
+
+    def hint(self, vals) -> V:
+        v = np.asarray(vals, np.int64) % P
+        return V(np.asarray(self.b.hint_base(v), np.int64).reshape(v.shape), v)
+
+    def _op(self, op, x: V, y: V, f) -> V:
+        xa, ya = np.broadcast_arrays(np.asarray(x.a, np.int64), np.asarray(y.a, np.int64))
+        xv, yv = np.broadcast_arrays(np.asarray(x.v, np.int64), np.asarray(y.v, np.int64))
+        return V(np.asarray(self.b.base(op, xa, ya), np.int64).reshape(xa.shape), f(xv, yv) % P)
+
+    def add(self, x, y):
+        return self._op(R.OP_ADD, x, y, lambda p, q: p + q)
+
+    def sub(self, x, y):
+        return self._op(R.OP_SUB, x, y, lambda p, q: p - q)
+
+    def mul(self, x, y):
+        return self._op(R.OP_MUL, x, y, lambda p, q: p * q)  # canonical operands: the product fits int64
+
+    def sum(self, x: V, axis: int = -1) -> V:
+        """Sum along an axis by a tree of vectorised adds."""
+        a, v = np.asarray(x.a, np.int64), np.asarray(x.v, np.int64)
+        a, v = np.moveaxis(a, axis, -1), np.moveaxis(v, axis, -1)
+        cur = V(a, v)
+        while cur.a.shape[-1] > 1:
+            n = cur.a.shape[-1]
+            h = n // 2
+            s = self.add(cur[..., :h], cur[..., h:2 * h])
+            if n % 2:
+                s = V(np.concatenate([s.a, cur.a[..., 2 * h:]], -1), np.concatenate([s.v, cur.v[..., 2 * h:]], -1))
+            cur = s
+        return cur[..., 0]
+
+    def assert_zero(self, x: V, label: str):
+        v = np.asarray(x.v, np.int64).reshape(-1)
+        if v.size and np.any(v % P):
+            raise ValueError(f"compress node: {label}")
+        self.b.assert_zero_base(np.asarray(x.a, np.int64).reshape(-1), label)
+
+    def assert_eq(self, x: V, y: V, label: str):
+        self.assert_zero(self.sub(x, y), label)
+
+    def assert_ne(self, x: V, c: int, label: str):
+        """x != c: a hinted inverse of x - c (assert_felt_ne)."""
+        d = self.sub(x, self.const(c))
+        dv = int(np.asarray(d.v).reshape(-1)[0]) % P
+        if dv == 0:
+            raise ValueError(f"compress node: {label}")
+        inv = self.hint(pow(dv, P - 2, P))
+        self.assert_eq(self.mul(d, inv), self.const(1), label)
+
+    def assert_bool(self, x: V, label: str):
+        self.assert_zero(self.mul(x, self.sub(x, self.const(1))), label)
+
+    def select(self, bit: V, x: V, y: V) -> V:
+        """bit ? x : y, i.e. y + bit (x - y)."""
+        return self.add(y, self.mul(bit, self.sub(x, y)))
+
+    def range_check(self, x: V, bits: int, label: str):
+        """x < 2^bits: its bits hinted, boolean, recomposed (C::range_check_felt)."""
+        xv = int(np.asarray(x.v).reshape(-1)[0])
+        if xv >> bits:
+            raise ValueError(f"compress node: {label}")
+        bs = self.hint([(xv >> i) & 1 for i in range(bits)])
+        self.assert_bool(bs, label)
+        acc = self.sum(self.mul(bs, self.const([1 << i for i in range(bits)])))
+        self.assert_eq(acc, x, label)
+
+    def hash(self, x: V) -> V:
+        """poseidon2_hash of a slice (PaddingFreeSponge)."""
+        a = np.asarray(x.a, np.int64).reshape(1, -1)
+        return V(np.asarray(self.b.sponge(a)[0, :VT.DIGEST], np.int64), VT.hash_slice(np.asarray(x.v).reshape(-1)))
+
+    def compress(self, left: V, right: V) -> V:
+        a = self.b.compress(np.asarray(left.a, np.int64)[None, :], np.asarray(right.a, np.int64)[None, :])[0]
+        return V(np.asarray(a, np.int64), VT.compress(np.asarray(left.v, np.uint32), np.asarray(right.v, np.uint32))[0])
+
+
+# ------------------------------------------------------------------ septic curve (sum_digest_v2)
+def _septic_weights():
+    """Output coefficient k of a product in F_p[z]/(z^7 + 2z - 8) as a weighted sum of the 49 partial
+    products p_ij (z^{7+j} = 8 z^j - 2 z^{j+1}): (index i*7+j, weight) lists padded to one length."""
+    terms = [[] for _ in range(7)]
+    for i in range(7):
+        for j in range(7):
+            d = i + j
+            if d < 7:
+                terms[d].append((7 * i + j, 1))
+            else:
+                terms[d - 7].append((7 * i + j, 8))
+                terms[d - 6].append((7 * i + j, P - 2))
+    L = max(len(t) for t in terms)
+    idx = np.full((7, L), 49, np.int64)  # 49 -> an appended zero product
+    w = np.zeros((7, L), np.int64)
+    for k, t in enumerate(terms):
+        for m, (ii, ww) in enumerate(t):
+            idx[k, m], w[k, m] = ii, ww
+    return idx, w
+
+
+_SW = _septic_weights()
+
+
+def septic_mul(o: Ops, x: V, y: V) -> V:
+    prods = o.mul(V(np.asarray(x.a)[:, None], np.asarray(x.v)[:, None]), V(np.asarray(y.a)[None, :], np.asarray(y.v)[None, :]))
+    flat = cat(prods, o.const([0]))
+    idx, w = _SW
+    terms = o.mul(V(flat.a[idx], flat.v[idx]), o.const(w))
+    return o.sum(terms)
+
+
+def _host_add(p1, p2):
+    """Affine sum of two curve points (14 canonical words each) with the host library's complete addition."""
+    out = SP.cumsum(np.asarray(p2, np.uint32)[None, :], start=np.asarray(p1, np.uint32))
+    if out[1, 14]:
+        raise ValueError("compress node: a global-sum addition reached the point at infinity")
+    return out[1, :14].astype(np.int64)
+
+
+def add_curve(o: Ops, p1: V, p2: V) -> V:
+    """add_curve_v2 (compiler/src/circuit/builder.rs:208-245): the sum hinted, then sum_checker_x and
+    sum_checker_y (septic_curve.rs:159-176) asserted zero."""
+    p3 = o.hint(_host_add(p1.v, p2.v))
+    x1, y1, x2, y2, x3, y3 = p1[:7], p1[7:], p2[:7], p2[7:], p3[:7], p3[7:]
+    dx = o.sub(x2, x1)
+    dy = o.sub(y2, y1)
+    cx = o.sub(septic_mul(o, o.add(o.add(x1, x2), x3), septic_mul(o, dx, dx)), septic_mul(o, dy, dy))
+    o.assert_zero(cx, "septic sum checker x")
+    cy = o.sub(septic_mul(o, o.add(y1, y3), dx), septic_mul(o, dy, o.sub(x1, x3)))
+    o.assert_zero(cy, "septic sum checker y")
+    return p3
+
+
+def _neg(pt) -> np.ndarray:
+    pt = np.asarray(pt, np.int64)
+    return np.concatenate([pt[:7], (P - pt[7:]) % P])
+
+
+def sum_digest(o: Ops, digests: Sequence[V]) -> V:
+    """sum_digest_v2 (builder.rs:276-301): from DIGEST_SUM_START add each digest, subtracting the zero digest
+    between them, then subtract the start; the empty sum is the zero digest."""
+    if not digests:
+        return o.const(SP.CURVE_CUMULATIVE_SUM_START)
+    ret = o.const(SP.DIGEST_SUM_START)
+    neg_zero = o.const(_neg(SP.CURVE_CUMULATIVE_SUM_START))
+    for i, d in enumerate(digests):
+        ret = add_curve(o, ret, d)
+        if i != len(digests) - 1:
+            ret = add_curve(o, ret, neg_zero)
+    return add_curve(o, ret, o.const(_neg(SP.DIGEST_SUM_START)))
+
+
+# ------------------------------------------------------------------ shared pieces
+def vk_digest_in_program(o: Ops, vk, vk_commit: np.ndarray) -> V:
+    """VerifyingKeyVariable::hash (recursion/circuit/src/types.rs:96-119) of a child vk."""
+    logs = [int(vk.prep_heights[k]).bit_length() - 1 for k in vk.prep_order]
+    words = VT.vk_hash_inputs(vk.commit, vk.pc_start, vk.gcs, logs)
+    rest = o.const(words[VT.DIGEST:])
+    return o.hash(cat(V(np.asarray(vk_commit, np.int64), np.asarray(vk.commit, np.int64) % P), rest))
+
+
+def vk_root_const(o: Ops) -> V:
+    return o.const(VT.dummy_tree().root)
+
+
+def verify_vk_membership(o: Ops, vk, vk_commit, root: V):
+    """ZKMMerkleProofVerifier::verify with value_assertions = false (the dummy vk map): the child's vk digest
+    computed, its dummy leaf [i; 8] at i = digest[0] mod 10000 opened, the path checked up to the root
+    (merkle_tree.rs:136-150: sibling order by the index bits, most significant first)."""
+    dig = vk_digest_in_program(o, vk, vk_commit)
+    index, value, path = VT.dummy_opening(dig.v)
+    h = len(path)
+    val = o.hint(value)
+    bits = o.hint([(index >> i) & 1 for i in range(h)])
+    o.assert_bool(bits, "vk index bits")
+    sib = o.hint(np.asarray(path, np.int64))
+    cur = val
+    for i in range(h):
+        bit = bits[h - 1 - i]
+        s = sib[i]
+        left = o.select(V(np.full(8, bit.a), np.full(8, bit.v)), s, cur)
+        right = o.select(V(np.full(8, bit.a), np.full(8, bit.v)), cur, s)
+        cur = o.compress(left, right)
+    o.assert_eq(cur, root, "vk Merkle path")
+
+
+def nonzero_equal(o: Ops, cur: V, pub: V, label: str):
+    """For every element x of cur: x * (cur_j - pub_j) = 0 for all j (core.rs:408-424 / compress.rs:300-318):
+    once any element is nonzero the vectors must agree."""
+    d = o.sub(cur, pub)
+    o.assert_zero(o.mul(V(np.asarray(cur.a)[:, None], np.asarray(cur.v)[:, None]),
+                        V(np.asarray(d.a)[None, :], np.asarray(d.v)[None, :])), label)
+
+
+def assert_complete(o: Ops, pv: V, is_complete: V):
+    """machine/complete.rs:13-65."""
+    o.assert_bool(is_complete, "is_complete boolean")
+    o.assert_zero(o.mul(is_complete, pv[R_NEXT_PC]), "complete: next_pc = 0")
+    o.assert_zero(o.mul(is_complete, o.sub(pv[R_START_SHARD], o.const(1))), "complete: start shard 1")
+    o.assert_ne(o.mul(is_complete, pv[R_NEXT_SHARD]), 1, "complete: next shard != 1")
+    o.assert_zero(o.mul(is_complete, o.sub(pv[R_CONTAINS_EXEC], o.const(1))), "complete: an execution shard")
+    o.assert_zero(o.mul(is_complete, o.sub(pv[R_START_EXEC], o.const(1))), "complete: start execution shard 1")
+    o.assert_zero(o.mul(is_complete, pv[R_START_RECON:R_START_RECON + 8]), "complete: start deferred digest 0")
+    o.assert_zero(o.mul(is_complete, o.sub(pv[R_END_RECON:R_END_RECON + 8], pv[R_DEFERRED:R_DEFERRED + 8])),
+                  "complete: end deferred digest = deferred proofs digest")
+    # assert_digest_zero_v2: is_complete * (digest - zero digest) = 0
+    o.assert_zero(o.mul(is_complete, o.sub(pv[R_GCS:R_GCS + 14], o.const(SP.CURVE_CUMULATIVE_SUM_START))),
+                  "complete: global cumulative sum is the zero digest")
+
+
+def _finish(o: Ops, out: dict, is_complete: V) -> V:
+    """Assemble the RecursionPublicValues, digest the first 223 values, assert_complete."""
+    zero = o.const(0)
+    pv = V(np.full(R.PROOF_MAX_NUM_PVS, zero.a, np.int64), np.zeros(R.PROOF_MAX_NUM_PVS, np.int64))
+    for off, x in out.items():
+        n = len(x)
+        pv.a[off:off + n] = np.asarray(x.a, np.int64).reshape(-1)
+        pv.v[off:off + n] = np.asarray(x.v, np.int64).reshape(-1)
+    pv.a[R_IS_COMPLETE], pv.v[R_IS_COMPLETE] = is_complete.a, is_complete.v
+    dig = o.hash(pv[:NUM_PV_ELMS_TO_HASH])
+    pv.a[R_DIGEST:R_DIGEST + 8], pv.v[R_DIGEST:R_DIGEST + 8] = dig.a, dig.v
+    assert_complete(o, pv, is_complete)
+    return pv
+
+
+# ------------------------------------------------------------------ the three node kinds
+def child_kind(vk) -> str:
+    """'core' (a MIPS shard proof), 'recursion' (a compress-machine proof) or 'synthetic' (any other machine)."""
+    if "Cpu" in vk.chips and "MemoryGlobalInit" in vk.chips:
+        return "core"
+    if "BatchFRI" in vk.chips and vk.num_pv == R.PROOF_MAX_NUM_PVS:
+        return "recursion"
+    return "synthetic"
+
+
+def core_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars], is_first: bool, is_complete: bool) -> V:
+    """ZKMRecursiveVerifier::verify (machine/core.rs:120-560) over the node's MIPS shard children (one vk)."""
+    vk0 = children[0][0]
+    if any(vk is not vk0 and VT.vk_digest(vk).tolist() != VT.vk_digest(vk0).tolist() for vk, _ in children[1:]):
+        raise ValueError("compress node: core shards of one batch share one verifying key")
+    vk = vk0
+    pv0 = cvs[0].pv
+    initial_shard = cur_shard = pv0[C_SHARD]
+    initial_exec = cur_exec = pv0[C_EXEC]
+    start_pc = cur_pc = pv0[C_START_PC]
+    cur_init = init0 = pv0[C_PREV_INIT:C_PREV_INIT + 32]
+    cur_fin = fin0 = pv0[C_PREV_FIN:C_PREV_FIN + 32]
+    exit_code = pv0[C_EXIT]
+    committed = pv0[C_COMMITTED:C_COMMITTED + 32]
+    deferred = pv0[C_DEFERRED:C_DEFERRED + 8]
+    first = o.hint(1 if is_first else 0)
+    o.assert_bool(first, "is_first_shard boolean")
+    o.assert_zero(o.mul(first, o.sub(initial_shard, o.const(1))), "first batch starts at shard 1")
+    o.assert_ne(o.mul(o.sub(o.const(1), first), initial_shard), 1, "a later batch does not start at shard 1")
+    o.assert_zero(o.mul(first, o.sub(start_pc, o.const(int(vk.pc_start)))), "first shard starts at vk.pc_start")
+    gsums = [o.select(first, o.const(np.asarray(vk.gcs, np.int64)), o.const(SP.CURVE_CUMULATIVE_SUM_START))]
+    o.assert_zero(o.mul(first, cat(cur_init, cur_fin)), "first shard: zero address bits")
+    cpu_seen = False
+    one = o.const(1)
+    for cv in cvs:
+        pv = cv.pv
+        contains_cpu = "Cpu" in cv.names
+        has_init = "MemoryGlobalInit" in cv.names
+        has_fin = "MemoryGlobalFinalize" in cv.names
+        if not contains_cpu:
+            o.assert_ne(cur_shard, 1, "a shard without CPU is not shard 1")
+        else:
+            if cv.log_degrees[cv.names.index("Cpu")] > MAX_CPU_LOG_DEGREE:
+                raise ValueError("compress node: CPU log degree above MAX_CPU_LOG_DEGREE")
+        o.assert_eq(cur_shard, pv[C_SHARD], "shard numbers are consecutive")
+        cur_shard = o.add(cur_shard, one)
+        if contains_cpu:
+            if not cpu_seen:
+                initial_exec = cur_exec = pv[C_EXEC]
+                cpu_seen = True
+            o.assert_eq(cur_exec, pv[C_EXEC], "execution shard numbers are consecutive")
+            cur_exec = o.add(cur_exec, one)
+        o.assert_eq(cur_pc, pv[C_START_PC], "start_pc = the previous shard's next_pc")
+        if not contains_cpu:
+            o.assert_eq(pv[C_START_PC], pv[C_NEXT_PC], "a shard without CPU keeps its pc")
+        else:
+            o.assert_ne(pv[C_START_PC], 0, "a CPU shard's start_pc is not zero")
+        cur_pc = pv[C_NEXT_PC]
+        o.assert_zero(exit_code, "exit code zero")
+        o.assert_eq(cur_init, pv[C_PREV_INIT:C_PREV_INIT + 32], "MemoryInit address bits chain")
+        o.assert_eq(cur_fin, pv[C_PREV_FIN:C_PREV_FIN + 32], "MemoryFinalize address bits chain")
+        if not has_init:
+            o.assert_eq(pv[C_PREV_INIT:C_PREV_INIT + 32], pv[C_LAST_INIT:C_LAST_INIT + 32],
+                        "no MemoryInit: address bits unchanged")
+        if not has_fin:
+            o.assert_eq(pv[C_PREV_FIN:C_PREV_FIN + 32], pv[C_LAST_FIN:C_LAST_FIN + 32],
+                        "no MemoryFinalize: address bits unchanged")
+        cur_init, cur_fin = pv[C_LAST_INIT:C_LAST_INIT + 32], pv[C_LAST_FIN:C_LAST_FIN + 32]
+        pub_c = pv[C_COMMITTED:C_COMMITTED + 32]
+        nonzero_equal(o, committed, pub_c, "committed value digest")
+        if not contains_cpu:
+            o.assert_eq(committed, pub_c, "a shard without CPU keeps the committed value digest")
+        committed = pub_c
+        exit_code = pv[C_EXIT]
+        pub_d = pv[C_DEFERRED:C_DEFERRED + 8]
+        nonzero_equal(o, deferred, pub_d, "deferred proofs digest")
+        if not contains_cpu:
+            o.assert_eq(deferred, pub_d, "a shard without CPU keeps the deferred proofs digest")
+        deferred = pub_d
+        o.range_check(pv[C_SHARD], MAX_LOG_NUMBER_OF_SHARDS, "shard < 2^16")
+        gsums += cv.global_sums
+    gcs = sum_digest(o, gsums)
+    o.assert_zero(exit_code, "exit code zero")
+    zeros8 = o.const(np.zeros(8, np.int64))
+    out = {R_COMMITTED: committed, R_DEFERRED: deferred, R_START_PC: start_pc, R_NEXT_PC: cur_pc,
+           R_START_SHARD: initial_shard, R_NEXT_SHARD: cur_shard, R_START_EXEC: initial_exec, R_NEXT_EXEC: cur_exec,
+           R_PREV_INIT: init0, R_LAST_INIT: cur_init, R_PREV_FIN: fin0, R_LAST_FIN: cur_fin,
+           R_VK_DIGEST: vk_digest_in_program(o, vk, cvs[0].vk_commit), R_GCS: gcs,
+           R_START_RECON: zeros8, R_END_RECON: zeros8, R_EXIT: exit_code,
+           R_CONTAINS_EXEC: o.const(1 if cpu_seen else 0), R_VK_ROOT: vk_root_const(o)}
+    return _finish(o, out, o.hint(1 if is_complete else 0))
+
+
+def compress_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars], is_complete: bool) -> V:
+    """ZKMCompressWithVKeyVerifier::verify (vkey_proof.rs:120-145 + compress.rs:93-436) over recursion proofs."""
+    root = vk_root_const(o)
+    for (vk, _), cv in zip(children, cvs):
+        verify_vk_membership(o, vk, cv.vk_commit, root)
+    one = o.const(1)
+    acc = {}
+    contains = o.const(0)
+    for i, cv in enumerate(cvs):
+        pv = cv.pv
+        # assert_recursion_public_values_valid + the witnessed vk root
+        o.assert_eq(o.hash(pv[:NUM_PV_ELMS_TO_HASH]), pv[R_DIGEST:R_DIGEST + 8], "child public-value digest")
+        o.assert_eq(pv[R_VK_ROOT:R_VK_ROOT + 8], root, "child vk_root")
+        exit_code = pv[R_EXIT]
+        if i == 0:
+            recon = acc["start_recon"] = pv[R_START_RECON:R_START_RECON + 8]
+            vkd = pv[R_VK_DIGEST:R_VK_DIGEST + 8]
+            acc["start_pc"] = pc = pv[R_START_PC]
+            acc["start_shard"] = shard = pv[R_START_SHARD]
+            acc["start_exec"] = exe = pv[R_START_EXEC]
+            acc["prev_init"] = init = pv[R_PREV_INIT:R_PREV_INIT + 32]
+            acc["prev_fin"] = fin = pv[R_PREV_FIN:R_PREV_FIN + 32]
+            committed = pv[R_COMMITTED:R_COMMITTED + 32]
+            deferred = pv[R_DEFERRED:R_DEFERRED + 8]
+            gsums = []
+        o.assert_eq(recon, pv[R_START_RECON:R_START_RECON + 8], "reconstruct deferred digest chains")
+        o.assert_eq(vkd, pv[R_VK_DIGEST:R_VK_DIGEST + 8], "one program vk digest")
+        o.assert_eq(pc, pv[R_START_PC], "start_pc = the previous child's next_pc")
+        o.assert_eq(shard, pv[R_START_SHARD], "start_shard = the previous child's next_shard")
+        ce = pv[R_CONTAINS_EXEC]
+        o.assert_bool(ce, "contains_execution_shard boolean")
+        first_seen = o.mul(ce, o.sub(one, contains))
+        acc["start_exec"] = o.select(first_seen, pv[R_START_EXEC], acc["start_exec"])
+        exe = o.select(first_seen, pv[R_START_EXEC], exe)
+        o.assert_zero(o.mul(ce, o.sub(exe, pv[R_START_EXEC])), "execution shards chain")
+        o.assert_eq(init, pv[R_PREV_INIT:R_PREV_INIT + 32], "MemoryInit address bits chain")
+        o.assert_eq(fin, pv[R_PREV_FIN:R_PREV_FIN + 32], "MemoryFinalize address bits chain")
+        pub_c = pv[R_COMMITTED:R_COMMITTED + 32]
+        nonzero_equal(o, committed, pub_c, "committed value digest")
+        committed = pub_c
+        pub_d = pv[R_DEFERRED:R_DEFERRED + 8]
+        nonzero_equal(o, deferred, pub_d, "deferred proofs digest")
+        deferred = pub_d
+        contains = o.add(contains, o.mul(ce, o.sub(one, contains)))
+        exe = o.select(ce, pv[R_NEXT_EXEC], exe)
+        recon = pv[R_END_RECON:R_END_RECON + 8]
+        pc, shard = pv[R_NEXT_PC], pv[R_NEXT_SHARD]
+        init, fin = pv[R_LAST_INIT:R_LAST_INIT + 32], pv[R_LAST_FIN:R_LAST_FIN + 32]
+        gsums.append(pv[R_GCS:R_GCS + 14])
+    out = {R_COMMITTED: committed, R_DEFERRED: deferred, R_START_PC: acc["start_pc"], R_NEXT_PC: pc,
+           R_START_SHARD: acc["start_shard"], R_NEXT_SHARD: shard, R_START_EXEC: acc["start_exec"], R_NEXT_EXEC: exe,
+           R_PREV_INIT: acc["prev_init"], R_LAST_INIT: init, R_PREV_FIN: acc["prev_fin"], R_LAST_FIN: fin,
+           R_VK_DIGEST: vkd, R_GCS: sum_digest(o, gsums), R_START_RECON: acc["start_recon"], R_END_RECON: recon,
+           R_EXIT: exit_code, R_CONTAINS_EXEC: contains, R_VK_ROOT: root}
+    return _finish(o, out, o.hint(1 if is_complete else 0))
+
+
+def synthetic_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars]) -> V:
+    """Children of a machine with no MIPS public values: the vk digest and the Global-scope sum, zero chaining
+    fields (so the compress layers above apply their checks uniformly)."""
+    vk0 = children[0][0]
+    gsums = [g for cv in cvs for g in cv.global_sums]
+    out = {R_VK_DIGEST: vk_digest_in_program(o, vk0, cvs[0].vk_commit), R_GCS: sum_digest(o, gsums),
+           R_VK_ROOT: vk_root_const(o)}
+    return _finish(o, out, o.hint(0))
+
+
+def node_public_values(b, children: Sequence[tuple], cvs: Sequence[ChildVars], is_first: bool = False,
+                       is_complete: bool = False) -> V:
+    """The node's RecursionPublicValues after its kind's checks (module docstring)."""
+    kinds = {child_kind(vk) for vk, _ in children}
+    if len(kinds) != 1:
+        raise ValueError(f"compress node: children of different kinds {sorted(kinds)}")
+    kind = kinds.pop()
+    o = Ops(b)
+    if kind == "core":
+        return core_node(o, children, cvs, is_first, is_complete)
+    if kind == "recursion":
+        return compress_node(o, children, cvs, is_complete)
+    return synthetic_node(o, children, cvs)

@@ -893,8 +893,10 @@ def check_shape(vk: ChildVk, p: ShardProofData):
 
 def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optional[Builder] = None,
                  ood: bool = True):
-    """Append the verification of one child ShardProof (module docstring).  Returns the addresses of the
-    transcript's final state words 0..7 (a digest of everything the child's proof committed to)."""
+    """Append the verification of one child ShardProof (module docstring).  Returns what the node's
+    public-value checks read of the child (zkmips_amd/node_pv.ChildVars: its hinted public values, the vk
+    commitment's addresses, chip names and heights, the Global-scope chips' cumulative sums)."""
+    from .node_pv import V, ChildVars
     b = b or Builder(prog)
     p = parse_shard_proof(proof)
     check_shape(vk, p)
@@ -910,6 +912,8 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
     ch.observe(vkc + [b.const(int(v)) for v in [vk.pc_start] + list(vk.gcs) + [0]])
     pv = b.hint_base(p.pv)
     ch.observe(pv[:vk.num_pv])
+    cvars = ChildVars(V(np.asarray(pv, np.int64), np.asarray(p.pv, np.int64) % P), np.asarray(vkc, np.int64),
+                      list(p.names), [int(o.log_degree) for o in p.chips])
     main_c, perm_c, quot_c = b.hint_base(p.main_c), b.hint_base(p.perm_c), b.hint_base(p.quot_c)
     ch.observe(main_c)
     perm_ch = (ch.sample_ef(), ch.sample_ef())
@@ -921,6 +925,8 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
         ch.observe(sums)
         lcs_words.append(sums[:4])
         gcs_words.append(sums[4:])
+        if cs.commit_scope != 0:  # a Global-scope chip's cumulative sum joins the node's sum (core.rs:543-547)
+            cvars.global_sums.append(V(np.asarray(sums[4:], np.int64), np.asarray(c.gcs, np.int64) % P))
         if cs.commit_scope == 0:  # verifier.rs: a Local-scope chip's global sum is the zero digest
             b.assert_eq_base(sums[4:], np.asarray(start, np.int64), f"{cs.name} global sum")
         if not cs.lookups:  # no local lookups: no local sum
@@ -1087,7 +1093,7 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
             folded = b.ext(R.OP_ADD, folded, b.ext(R.OP_MUL, np.full(nq, bsq, np.int64), ro[lfh]))
         x = b.base(R.OP_MUL, x, x)
     b.assert_eq_ext(folded, np.full(nq, final, np.int64), "final fold = final poly")
-    return np.asarray(ch.st[:8], np.int64)
+    return cvars
 
 
 def _bitrev_arr(v: np.ndarray, bits: int) -> np.ndarray:
@@ -1200,21 +1206,25 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
     return pairs
 
 
-def compress_node_program(children: Sequence[tuple], ood: bool = True) -> R.RecursionProgram:
-    """A compress node (prover/src/lib.rs:614-954): verify every child (ChildVk, proof bytes) and commit
-    public values whose digest (RecursionPublicValues.digest) is a Poseidon2 hash of the children's
-    transcript states -- a node's public values commit to what its children committed to."""
-    prog = R.RecursionProgram()
-    b = Builder(prog)
+def _build_node(prog, b, children: Sequence[tuple], ood: bool, is_first: bool, is_complete: bool):
+    from .node_pv import node_public_values
     if not children:
         raise ValueError("a compress node needs at least one child")
-    states = [verify_shard(prog, vk, proof, b, ood=ood) for vk, proof in children]
-    zero = b.const(0)
-    # the children's full 8-word transcript states, absorbed by the sponge (PaddingFreeSponge, any count)
-    digest = b.sponge(np.concatenate(states)[None, :])[0, :R.DIGEST_SIZE]
-    pv = np.full(R.PROOF_MAX_NUM_PVS, zero, np.int64)
-    pv[R.PV_DIGEST_START:R.PV_DIGEST_START + R.DIGEST_SIZE] = digest
-    prog.commit_public_values(pv)
+    cvs = [verify_shard(prog, vk, proof, b, ood=ood) for vk, proof in children]
+    pv = node_public_values(b, children, cvs, is_first=is_first, is_complete=is_complete)
+    prog.commit_public_values(np.asarray(pv.a, np.int64))
+    return pv
+
+
+def compress_node_program(children: Sequence[tuple], ood: bool = True, is_first: bool = False,
+                          is_complete: bool = False) -> R.RecursionProgram:
+    """A compress node (prover/src/lib.rs:614-954): verify every child (ChildVk, proof bytes), check their
+    public values the way the reference's core / compress recursion programs do, and commit the node's
+    RecursionPublicValues (zkmips_amd/node_pv.py).  is_first: the node's first child is the execution's first
+    batch (core.rs `is_first_shard`); is_complete: the node is the root of the whole execution."""
+    prog = R.RecursionProgram()
+    b = Builder(prog)
+    _build_node(prog, b, children, ood, is_first, is_complete)
     return prog
 
 
@@ -1257,7 +1267,8 @@ def _vk_key(vk: ChildVk) -> bytes:
 _TEMPLATES: Dict[tuple, tuple] = {}  # per process: structure key -> (FlatProgram, const_fresh mem rows)
 
 
-def node_flat(children: Sequence[tuple], ood: bool = True) -> "R.FlatProgram":
+def node_flat(children: Sequence[tuple], ood: bool = True, is_first: bool = False,
+              is_complete: bool = False) -> "R.FlatProgram":
     """compress_node_program(children) flattened, built once per program structure.  The verifier program
     depends on the children's vks and proof shapes only; the proofs themselves enter as hints.  So the
     first node of a structure is built in full and its FlatProgram kept; a later node with the same vks and
@@ -1266,16 +1277,13 @@ def node_flat(children: Sequence[tuple], ood: bool = True) -> "R.FlatProgram":
     the FlatProgram of compress_node_program(children) (tests/test_compress_verify.py)."""
     tape = _HintTape()
     b = Builder(tape)
-    if not children:
-        raise ValueError("a compress node needs at least one child")
-    for vk, proof in children:
-        verify_shard(tape, vk, proof, b, ood=ood)
+    _build_node(tape, b, children, ood, is_first, is_complete)
     sizes = tuple(len(v) for v in tape.vals)
     key = (tuple(_vk_key(vk) for vk, _ in children), tuple(tape.shapes), bool(ood), sizes,
            tuple(len(v) for v in tape.fresh))
     hit = _TEMPLATES.get(key)
     if hit is None:
-        prog = compress_node_program(children, ood=ood)
+        prog = compress_node_program(children, ood=ood, is_first=is_first, is_complete=is_complete)
         tpl = R.flatten(prog)
         hint_rows = tuple(int(n) for kc, _, n, _, _ in tpl.table if R.KINDS[kc] == "hint")
         fresh = [(int(tpl.table[bi][1]), int(tpl.table[bi][2])) for bi in prog.__dict__.get("fresh_blocks", [])]

@@ -46,10 +46,10 @@ _OPS = {"add": [(A.OP_ADD, 0), (A.OP_ADD, 1), (A.OP_SUB, 0)],
 _AVOID = (C.COUNTER,)
 
 
-def shape_program(shape: dict, seed: int = 1, body: int = 512, fill: float = 0.8):
+def shape_program(shape: dict, seed: int = 1, body: int = 512, fill: float = 0.8, rows: int = None):
     """A counted loop (`r3` counts down) whose body mixes ALU, memory, forward-branch and conditional-move
     instructions in the proportions `_fractions(shape)`; iterations sized to `fill` of the shape's Cpu
-    rows (capped by the 24-bit clk)."""
+    rows (capped by the 24-bit clk), or to `rows` instructions in all (an execution of several shards)."""
     frac = _fractions(shape)
     kinds = list(frac)
     p = np.asarray([frac[k] for k in kinds])
@@ -92,7 +92,8 @@ def shape_program(shape: dict, seed: int = 1, body: int = 512, fill: float = 0.8
     prog.append((A.OP_ADD, 0, 0, 0, 0, 1))  # delay slot
     prog += [(A.OP_ADD, SY.REG_V0, 0, SY.HALT, 0, 1), (A.OP_ADD, SY.REG_A0, 0, 0, 0, 1),
              (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
-    rows = min(int(fill * (1 << shape["Cpu"])), (1 << 24) // 5 - 64)
+    if rows is None:
+        rows = min(int(fill * (1 << shape["Cpu"])), (1 << 24) // 5 - 64)
     per_iter = len(prog) - 4  # the body's untaken-branch path, roughly
     iters = max(1, rows // per_iter - 1)
     prog[0] = (A.OP_ADD, C.COUNTER, 0, iters, 0, 1)
@@ -133,6 +134,34 @@ def shape_shard(shape: dict, seed: int = 1, down: int = 0, fill: float = 0.8, ca
         if name not in sh and name not in ("Program", "Byte"):
             raise ValueError(f"{name} ({len(t)} rows) is not in the shape")
     return m, prep, pad_to_shape(m, traces, sh), pvs
+
+
+def shape_execution(shape: dict, cpu_shards: int, down: int = 0, seed: int = 1, fill: float = 0.8):
+    """One execution of a shape_program loop cut into `cpu_shards` consecutive CPU shards (continuations,
+    mips_core.program_shards: registers, memory and access records carry over; each shard about `fill` of
+    the scaled shape's Cpu rows) each padded to the scaled `shape`, then the memory shard that closes the
+    execution -- the leaves the reference's recursion chains (consecutive shard numbers and pcs, one proving
+    key, global sums adding to zero).  Returns the list of (machine, prep_traces, traces, public_values)."""
+    sh = scaled(shape, down)
+    per = min(int(fill * (1 << sh["Cpu"])), (1 << 24) // 5 - 64)
+    prog = shape_program(sh, seed, fill=fill, rows=per * cpu_shards - per // 4)
+    out = C.program_shards(prog, seed, shard_size=per)
+    # one shape for every CPU shard (one recursion program structure): the scaled shape, raised where a small
+    # scale's fixed per-shard records (the register entries of MemoryLocal, ...) need more rows
+    common = dict(sh)
+    for m, prep, traces, pvs in out:
+        if "Cpu" in traces:
+            for name, t in traces.items():
+                if name not in sh and name not in ("Program", "Byte"):
+                    raise ValueError(f"{name} ({len(t)} rows) is not in the shape")
+                if name in common:
+                    common[name] = max(common[name], (len(t) - 1).bit_length())
+    res = []
+    for m, prep, traces, pvs in out:
+        if "Cpu" in traces:
+            traces = pad_to_shape(m, traces, common)
+        res.append((m, prep, traces, pvs))
+    return res
 
 
 def shape_shards(shape: dict, seeds, down: int = 0, fill: float = 0.8):
