@@ -614,6 +614,28 @@ def _tendermint_job(outdir: str):
     return meta, info, gen_s
 
 
+def _compress_leaves_job(outdir: str, n_leaves: int, down: int):
+    """Pool worker (no GPU): config 5's leaves -- ONE execution of a loop in the reference's maximal 2^22 shape
+    scaled to Cpu 2^(22-down), cut into n_leaves - 1 consecutive CPU shards (each padded to the scaled shape)
+    plus the memory shard that closes it (zkmips_amd/shapes.shape_execution), so the compress nodes' chaining
+    checks (shard numbers, pcs, address bits, global sums) hold and the root is a complete proof.  Traces as
+    .npy files under outdir, as _tendermint_job."""
+    from zkmips_amd import shapes as SH
+    t0 = time.perf_counter()
+    shards = SH.shape_execution(SH.MAXIMAL_22, n_leaves - 1, down=down)
+    gen_s = time.perf_counter() - t0
+    meta = []
+    for i, (_, prep, tr, pv) in enumerate(shards):
+        for k, v in tr.items():
+            np.save(os.path.join(outdir, f"s{i}_{k}.npy"), v)
+        np.save(os.path.join(outdir, f"s{i}__pv.npy"), pv)
+        meta.append(sorted(tr))
+    for k, v in shards[0][1].items():
+        if v is not None:
+            np.save(os.path.join(outdir, f"prep_{k}.npy"), v)
+    return meta, {"cpu_shards": n_leaves - 1, "leaf_shape": {k: int(v.shape[0]) for k, v in shards[0][2].items()}}, gen_s
+
+
 def _load_tendermint(outdir: str, meta):
     from zkmips_amd import mips_core as MC
     m = MC.core_machine()
@@ -897,24 +919,20 @@ def start_witness_pool(n: int):
     return AffinityPool(n).warm()
 
 
-def mips_leaves(dev, queries: int, n_leaves: int = 64, distinct: int = 4, down: int = 6):
-    """Config 5's leaves: core shard proofs of MIPS shards in the reference's maximal 2^22 shape scaled to
-    Cpu 2^(22-down) (all 17 chips of maximal_shapes.json["22"][2], zkmips_amd/shapes.py), proven on this
-    GPU before the timed region; `distinct` executions of one program (one proving key) from different
-    initial registers, dealt cyclically to the leaves."""
+def mips_leaves(dev, queries: int, run, info: dict):
+    """Config 5's leaves: the core shard proofs of one execution (_compress_leaves_job's shards, in shard
+    order), proven on this GPU before the timed region with one proving key."""
     from zkmips_amd import recursion_verifier as RV
-    from zkmips_amd import shapes as SH
     from zkmips_amd.prover import HipProver
-    t0 = time.perf_counter()
-    shards = SH.shape_shards(SH.MAXIMAL_22, [1 + i for i in range(distinct)], down=down)
-    gen_s = time.perf_counter() - t0
-    m, prep = shards[0][0], shards[0][1]
+    m, prep = run[0][0], run[0][1]
     hp = HipProver(dev, m, prep, num_queries=queries)
     vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=queries)
-    proofs = [hp.prove_shard(sh[2], sh[3]) for sh in shards]
-    info = {"leaf_shape": {k: int(v.shape[0]) for k, v in shards[0][2].items()}, "distinct_leaf_shards": distinct,
-            "leaf_queries": queries, "leaf_generation_s": round(gen_s, 1), "leaf_proof_bytes": len(proofs[0])}
-    return [(vk, proofs[i % distinct]) for i in range(n_leaves)], info
+    proofs = [hp.prove_shard(tr, pv) for _, _, tr, pv in run]
+    from zkmips_amd.proof import machine_global_sum_is_zero
+    assert machine_global_sum_is_zero(proofs), "compress leaves: the execution's global sums do not add to zero"
+    info = dict(info, leaves=len(proofs), leaf_queries=queries, leaf_proof_bytes=len(proofs[0]),
+                memory_shard_chips=sorted(run[-1][2]))
+    return [(vk, p) for p in proofs], info
 
 
 def _union_s(intervals) -> float:
@@ -962,8 +980,8 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
     # compact witnesses: main traces as event rows laid out on the device, prep traces once per program
     # (children's verifying keys by reference: each worker loads a key's file once)
     # (a node's job preferably to a worker holding its program's template: CT.AffinityPool)
-    reducer = CT.Reducer(lambda ch: pool.submit(CT.node_witness_shm, CT.by_ref(ch), True, True, True,
-                                                tag=CT.node_tag(ch)), prove, inflight)
+    reducer = CT.Reducer(lambda ch, fl: pool.submit(CT.node_witness_shm, CT.by_ref(ch), True, True, True, **fl,
+                                                    tag=CT.node_tag(ch)), prove, inflight)
     t0 = time.perf_counter()
     root = CT.reduce_distributed(leaves, reducer) if distributed else CT.reduce_serial(leaves, reducer)
     wall = time.perf_counter() - t0
@@ -988,7 +1006,7 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
     return root, res
 
 
-def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int = 3):
+def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int = 3, leaves_job=None):
     """BASELINE config 5 as a field of a bench line: 64 MIPS leaf proofs reduced by the compress tree.
     Node programs verify their children in full (transcript, PoW, Merkle paths, FRI, and the out-of-domain
     constraint check, zkmips_amd/recursion_verifier.py), are padded to the first fitting
@@ -996,9 +1014,21 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
     new) and proven on the GPU as soon as their witness exists.  `value` is end to end (witness generation
     overlapped with proving, every setup inside), `prove_only` counts the time a proof was on the GPU."""
     from zkmips_amd import compress_tree as CT
-    leaves, info = mips_leaves(dev, args.queries, down=22 - args.leaf_log)
+    from zkmips_amd import recursion_verifier as RV
+    import shutil
+    import tempfile
+    if leaves_job is None:  # generated here (the default line submits it to the pool at the start)
+        d = tempfile.mkdtemp(prefix="zkm_cl_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        leaves_job = (pool.submit(_compress_leaves_job, d, 64, 22 - args.leaf_log), d)
+    fut, d = leaves_job
+    try:
+        meta, info, gen_s = fut.result()
+        run = _load_tendermint(d, meta)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    leaves, info = mips_leaves(dev, args.queries, run, dict(info, leaf_generation_s=round(gen_s, 1)))
     # warm-up (untimed): one node's witness and proof (JIT modules, allocator pools); its key is dropped
-    wit = CT.node_witness(leaves[:2], True, True, True, False)
+    wit = CT.node_witness(leaves[:2], True, True, True, False, is_first=True)
     warm = CT.GpuProvers(dev)
     warm.get(wit[0], CT.TreeStats()).prove_shard(CT.materialize(wit[1]), wit[2])
     del warm
@@ -1021,7 +1051,12 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
            "leaves": info, "in_flight": inflight,
            "node_program": "verifies each child: transcript replay, PoW, query bits, Merkle paths of every opening, "
                            "FRI reduced openings and folds, out-of-domain constraint check of every chip against the "
-                           "quotient, local cumulative sum; RecursionShapeConfig::fix_shape padding"}
+                           "quotient, local cumulative sum; then the reference's public-value checks (core.rs over "
+                           "shard leaves: shard / execution-shard / pc chaining, address bits, digests, exit code, "
+                           "first-shard conditions; compress.rs over node children: vk membership in the dummy vk "
+                           "Merkle tree, child digests, chaining) and the septic-curve sum of the global sums; "
+                           "assert_complete at the root; RecursionShapeConfig::fix_shape padding",
+           "root_is_complete": bool(int(RV.parse_shard_proof(rproof).pv[220]))}
     return out, (rvk, rproof)
 
 
@@ -1392,6 +1427,7 @@ def main():
     if (not (args.no_compress and args.no_tendermint) and args.workload == "fib"
             and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.pmc_child):
         pool = start_witness_pool(max(1, min(args.node_workers, 32)))
+    leaves_job = None
 
     import torch
     rk = Ranks(args)
@@ -1429,6 +1465,11 @@ def main():
         import tempfile
         tm_dir = tempfile.mkdtemp(prefix="zkm_tm_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
         tm_future = pool.submit(_tendermint_job, tm_dir)
+    if pool is not None and not args.no_compress and rank == 0:
+        # config 5's leaf execution is traced on the host in a pool worker while the later GPU legs run
+        import tempfile
+        d = tempfile.mkdtemp(prefix="zkm_cl_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        leaves_job = (pool.submit(_compress_leaves_job, d, 64, 22 - args.leaf_log), d)
 
     if rank != 0:
         rk.close()
@@ -1604,27 +1645,31 @@ def main():
         "stages_ms_per_shard": stages,
         "profiled_region": f"{nprof} single-shard proofs after the timed region (stages, roofline, ntt, serial_ms_per_shard)",
     }
+    def leg(name, fn):
+        """A secondary leg: its failure is recorded in the line (and on stderr), not fatal to the headline."""
+        progress(f"{name} leg")
+        try:
+            line[name] = fn()
+        except Exception as e:  # noqa: BLE001 -- reported, the headline stands
+            import traceback
+            traceback.print_exc()
+            line[name] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_sizes and world == 1 and args.workload == "fib":
-        progress("size series")
-        line["sizes"] = size_series(args, prover, K)
+        leg("sizes", lambda: size_series(args, prover, K))
     if not args.no_maxshape and world == 1 and args.workload == "fib":
-        progress("maximal-shape leg")
-        line["maxshape"] = maxshape_leg(args, rk, n, K)
+        leg("maxshape", lambda: maxshape_leg(args, rk, n, K))
     if pool is not None and not args.no_compress:
-        progress("compress leg")
-        line["compress"], _ = compress_leg(args, pool, prover.dev)
+        leg("compress", lambda: compress_leg(args, pool, prover.dev, leaves_job=leaves_job)[0])
     if tm_future is not None:
         import shutil
         try:
-            progress("tendermint leg")
-            line["tendermint"] = tendermint_leg(args, tm_future.result(), tm_dir, rk)
+            leg("tendermint", lambda: tendermint_leg(args, tm_future.result(), tm_dir, rk))
         finally:
             shutil.rmtree(tm_dir, ignore_errors=True)
     if pool is not None:
         pool.shutdown()
     if not args.no_cpu_baseline and world == 1:
-        progress("CPU baseline")
-        line["cpu_baseline"] = cpu_baseline(args.cpu_log_n, args.queries)
+        leg("cpu_baseline", lambda: cpu_baseline(args.cpu_log_n, args.queries))
     if args.profile_out:
         with open(args.profile_out, "w") as f:
             f.write(prof_text)

@@ -143,3 +143,25 @@ def test_compress_route_rejects_a_tampered_shard():
     with pytest.raises(SV.TwirpError) as e:
         svc.call("Compress", {1: B.write_compress_request(vk, [bytes(bad)])})
     assert e.value.code == "invalid_argument"
+
+
+def test_compress_route_rejects_unchained_shards():
+    """A Compress request whose shards are not one consecutive execution in order (swapped here) fails in
+    the first node's public-value checks (core.rs: shard numbers, pcs) before any GPU work: invalid_argument;
+    an incomplete set (the memory shard dropped) fails the root's assert_complete the same way."""
+    from zkmips_amd import shapes as SH
+    from zkmips_amd.septic import CURVE_CUMULATIVE_SUM_START as GCS
+    sh = SH.shape_execution(SH.MAXIMAL_22, 2, down=12)
+    m, prep = sh[0][0], sh[0][1]
+    o = O.OracleProver(m, prep, num_queries=4)
+    proofs = []
+    for _, _, tr, pv in sh:
+        rc, p = o.prove(tr, pv)
+        assert rc == 0
+        proofs.append(p)
+    vk = B.StarkVk.of_program(m, prep, o.commit, 0x00400000, GCS)
+    svc = SV.ProverService(device_factory=lambda i: object())
+    for bad in ([proofs[1], proofs[0], proofs[2]], proofs[:2]):
+        with pytest.raises(SV.TwirpError) as e:
+            svc.call("Compress", {1: B.write_compress_request(vk, bad)})
+        assert e.value.code == "invalid_argument", e.value

@@ -69,8 +69,8 @@ def _oracle_prove_factory(nq):
     return prove
 
 
-def _witness_small(children):
-    return CT.node_witness(children, fix=False)
+def _witness_small(children, **flags):
+    return CT.node_witness(children, fix=False, **flags)
 
 
 def test_tree_with_witness_pool_matches_serial(fib_leaves):
@@ -79,7 +79,7 @@ def test_tree_with_witness_pool_matches_serial(fib_leaves):
     prove = _oracle_prove_factory(4)
     with ProcessPoolExecutor(2, mp_context=mpc.get_context("spawn")) as pool:
         # verifying keys by reference (VkRef: written once, loaded once per worker)
-        red = CT.Reducer(lambda ch: pool.submit(_witness_small, CT.by_ref(ch)), prove, inflight=2)
+        red = CT.Reducer(lambda ch, fl: pool.submit(_witness_small, CT.by_ref(ch), **fl), prove, inflight=2)
         root = CT.reduce_serial(fib_leaves, red)
     a = prove(_witness_small(fib_leaves[:2]))
     b = prove(_witness_small(fib_leaves[2:]))
@@ -94,7 +94,7 @@ def test_tree_with_affinity_pool_matches_serial(fib_leaves):
     prove = _oracle_prove_factory(4)
     pool = CT.AffinityPool(2)
     try:
-        red = CT.Reducer(lambda ch: pool.submit(_witness_small, CT.by_ref(ch), tag=CT.node_tag(ch)), prove,
+        red = CT.Reducer(lambda ch, fl: pool.submit(_witness_small, CT.by_ref(ch), **fl, tag=CT.node_tag(ch)), prove,
                          inflight=2)
         root = CT.reduce_serial(fib_leaves, red)
     finally:
@@ -211,7 +211,7 @@ def test_failed_tree_discards_in_flight_witnesses(tmp_path):
     gate = threading.Event()
     files = []
 
-    def submit(ch):
+    def submit(ch, flags):
         f = Future()
         f.set_running_or_notify_cancel()  # as an executor's job that has started: cannot be cancelled
         path = tmp_path / f"w{len(files)}"
@@ -305,19 +305,22 @@ def test_ood_check_binds_the_air(fib_leaves):
 
 @pytest.mark.gpu
 def test_gpu_mips_node_reference_shape():
-    """One compress node over two real MIPS leaf proofs (the reference's maximal 2^22 shape scaled to Cpu
-    2^16, 17 chips, 84 queries, proven on the GPU), its program padded to the first fitting
-    RecursionShapeConfig shape: the GPU proof bytes equal the oracle's, and the oracle verifies them."""
+    """One compress node over the first two shards of a real MIPS execution (the reference's maximal 2^22
+    shape scaled to Cpu 2^16, 17 chips, 84 queries, proven on the GPU), with the reference's public-value
+    checks (core.rs), its program padded to the first fitting RecursionShapeConfig shape: the GPU proof
+    bytes equal the oracle's, and the oracle verifies them."""
     from zkmips_amd import shapes as SH
     from zkmips_amd._lib import Device
     from zkmips_amd.prover import HipProver
     dev = Device(0)
-    sh = SH.shape_shards(SH.MAXIMAL_22, [1, 2], down=6)
+    sh = SH.shape_execution(SH.MAXIMAL_22, 2, down=6)[:2]
     m, prep = sh[0][0], sh[0][1]
     hp = HipProver(dev, m, prep, num_queries=84)
     vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=84)
     leaves = [(vk, hp.prove_shard(s[2], s[3])) for s in sh]
-    prep_c, tr, pv, shape, _ = CT.node_witness(leaves)
+    with pytest.raises(ValueError):  # the shards out of order do not chain
+        CT.node_witness(leaves[::-1], is_first=True)
+    prep_c, tr, pv, shape, _ = CT.node_witness(leaves, is_first=True)
     assert shape in R.RECURSION_SHAPES
     for k, v in tr.items():
         assert v.shape[0] == 1 << shape[k], k
@@ -329,15 +332,126 @@ def test_gpu_mips_node_reference_shape():
     assert rc == 0 and gpu == ref
     assert o.verify(gpu) == 0
     # the device-P2 form: the Poseidon2WideDeg3 trace built on the device from the permutation inputs
-    prep_d, tr_d, pv_d, shape_d, _ = CT.node_witness(leaves, True, True)
+    prep_d, tr_d, pv_d, shape_d, _ = CT.node_witness(leaves, True, True, is_first=True)
     assert isinstance(tr_d["Poseidon2WideDeg3"], CT.DeviceP2) and shape_d == shape
     assert HipProver(dev, cm, prep_d, **kw).prove_shard(CT.materialize(tr_d), pv_d) == gpu
     # the bench's compact form: every main trace laid out on the device from its events, the proving key
     # found by prep_key (GpuProvers)
-    wit = CT.node_witness(leaves, True, True, True, False)
+    wit = CT.node_witness(leaves, True, True, True, False, is_first=True)
     assert all(isinstance(v, (CT.DeviceRows, CT.DeviceExpRev, CT.DeviceP2)) for v in wit[1].values())
     dt = CT.materialize(wit[1])
     for k, v in dt.items():
         assert np.array_equal(v.cpu().numpy().view(np.uint32), tr[k]), k
     pr = CT.GpuProvers(dev).get(wit[0], CT.TreeStats())
     assert pr.prove_shard(dt, wit[2]) == gpu
+
+
+@pytest.mark.gpu
+def test_gpu_mips_node_2e21_leaves():
+    """BASELINE config 5 at the reference's default shard size (2^21 Cpu rows, crates/stark/src/opts.rs:6): a
+    node over the first two shards of one execution in the maximal shape scaled to Cpu 2^21.  The leaves are
+    GPU proofs that the oracle's verifier accepts; the node's program (fix_shape picks its
+    RecursionShapeConfig shape) proves to the oracle's bytes on the GPU."""
+    from zkmips_amd import shapes as SH
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    dev = Device(0)
+    sh = SH.shape_execution(SH.MAXIMAL_22, 2, down=1)[:2]
+    m, prep = sh[0][0], sh[0][1]
+    assert sh[0][2]["Cpu"].shape[0] == 1 << 21
+    hp = HipProver(dev, m, prep, num_queries=84)
+    vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=84)
+    leaves = [(vk, hp.prove_shard(s[2], s[3])) for s in sh]
+    ov = O.OracleProver(m, prep, num_queries=84)
+    assert all(ov.verify(p) == 0 for _, p in leaves)
+    wit = CT.node_witness(leaves, True, True, True, False, is_first=True)
+    print("2^21 leaves: node shape", wit[3], flush=True)
+    assert wit[3] in R.RECURSION_SHAPES
+    pr = CT.GpuProvers(dev).get(wit[0], CT.TreeStats())
+    dt = CT.materialize(wit[1])
+    gpu = pr.prove_shard(dt, wit[2])
+    prep_c, tr, pv, shape, _ = CT.node_witness(leaves, is_first=True)
+    assert shape == wit[3] and np.array_equal(pv, wit[2])
+    cm = R.compress_machine()
+    o = O.OracleProver(cm, prep_c, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    rc, ref = o.prove(tr, pv)
+    assert rc == 0 and gpu == ref
+    assert o.verify(gpu) == 0
+
+
+@pytest.fixture(scope="module")
+def mips_execution():
+    """One MIPS execution in the maximal shape scaled to Cpu 2^10: three consecutive CPU shards and the
+    memory shard, oracle-proven with one key (leaves whose public values chain)."""
+    from zkmips_amd import shapes as SH
+    sh = SH.shape_execution(SH.MAXIMAL_22, 3, down=12)
+    m, prep = sh[0][0], sh[0][1]
+    pr = O.OracleProver(m, prep, num_queries=NQ)
+    proofs = []
+    for _, _, tr, pv in sh:
+        rc, p = pr.prove(tr, pv)
+        assert rc == 0
+        proofs.append(p)
+    from zkmips_amd.proof import machine_global_sum_is_zero
+    assert machine_global_sum_is_zero(proofs)
+    return RV.ChildVk.of(m, prep, pr.commit, num_queries=NQ), proofs
+
+
+def test_core_node_chaining(mips_execution):
+    """A node over MIPS shard leaves checks what the reference's core recursion program checks
+    (machine/core.rs): consecutive shards in order pass and commit the covered range; reordered, gapped or
+    wrongly flagged batches are rejected; the whole execution in one node is complete."""
+    from zkmips_amd import node_pv as NP
+    vk, proofs = mips_execution
+    ok = [([0, 1], True), ([1, 2], False), ([2, 3], False), ([0, 1, 2, 3], True)]
+    for order, first in ok:
+        complete = len(order) == len(proofs)
+        rec = R.execute(RV.compress_node_program([(vk, proofs[i]) for i in order], is_first=first,
+                                                 is_complete=complete))
+        pv = rec.public_values.astype(np.int64)
+        assert pv[NP.R_START_SHARD] == order[0] + 1 and pv[NP.R_NEXT_SHARD] == order[-1] + 2
+        assert pv[NP.R_IS_COMPLETE] == int(complete) and pv[NP.R_CONTAINS_EXEC] == int(order[0] < 3)
+        assert pv[NP.R_DIGEST:NP.R_DIGEST + 8].tolist() == NP.VT.hash_slice(pv[:NP.R_DIGEST]).tolist()
+        assert pv[NP.R_VK_DIGEST:NP.R_VK_DIGEST + 8].tolist() == NP.VT.vk_digest(vk).tolist()
+    bad = [([1, 0], True, False), ([0, 2], True, False), ([1, 2], True, False), ([0, 1], False, False),
+           ([0, 1], True, True),  # not the whole execution: incomplete
+           ([3, 2], False, False)]
+    for order, first, complete in bad:
+        with pytest.raises(ValueError):
+            RV.compress_node_program([(vk, proofs[i]) for i in order], is_first=first, is_complete=complete)
+
+
+def test_compress_node_chaining(mips_execution):
+    """Nodes over node proofs (machine/compress.rs + vkey_proof.rs): two consecutive nodes reduce to a
+    complete root whose global sum is the zero digest; the same nodes swapped do not chain; a child node
+    vk's Merkle opening in the dummy vk tree is checked."""
+    from zkmips_amd import node_pv as NP
+    from zkmips_amd import vk_tree as VT
+    vk, proofs = mips_execution
+    prove = _oracle_prove_factory(4)
+    a = prove(CT.node_witness([(vk, p) for p in proofs[:2]], fix=False, is_first=True))
+    b = prove(CT.node_witness([(vk, p) for p in proofs[2:]], fix=False))
+    rec = R.execute(RV.compress_node_program([a, b], is_complete=True))
+    pv = rec.public_values.astype(np.int64)
+    assert pv[NP.R_IS_COMPLETE] == 1 and pv[NP.R_START_SHARD] == 1 and pv[NP.R_NEXT_SHARD] == 5
+    assert pv[NP.R_GCS:NP.R_GCS + 14].tolist() == NP.SP.CURVE_CUMULATIVE_SUM_START.astype(np.int64).tolist()
+    assert pv[NP.R_VK_ROOT:NP.R_VK_ROOT + 8].tolist() == VT.dummy_tree().root.astype(np.int64).tolist()
+    with pytest.raises(ValueError):
+        RV.compress_node_program([b, a])
+    # the template path (node_flat) gives the same program for the same children
+    _flat = RV.node_flat([a, b], is_complete=True)
+    assert np.array_equal(R.execute(_flat).public_values, rec.public_values)
+
+
+def test_dummy_vk_tree():
+    """The dummy vk map's tree (prover/src/lib.rs:223-233, merkle_tree.rs): 10000 leaves [i; 8] padded to
+    2^14; open / verify agree for the first, last and a middle leaf; a wrong sibling fails."""
+    from zkmips_amd import vk_tree as VT
+    t = VT.dummy_tree()
+    assert t.height == 14
+    for i in (0, 4321, 9999):
+        v, path = t.open(i)
+        assert np.all(v == i) and VT.MerkleTree.verify(i, v, path, t.root)
+        path = path.copy()
+        path[3, 0] ^= 1
+        assert not VT.MerkleTree.verify(i, v, path, t.root)

@@ -95,7 +95,7 @@ def _fake_reducer(calls, slow=None):
         d = h.digest()
         return ("vk", d * (1 + d[0] % 3))  # ragged proof sizes
 
-    return Reducer(lambda ch: tp.submit(lambda: ch), prove, inflight=2)
+    return Reducer(lambda ch, fl: tp.submit(lambda: ch), prove, inflight=2)
 
 
 def _tree_worker(rank, world, port, out_q, sizes=(64, 5), slow=None):

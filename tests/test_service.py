@@ -204,10 +204,10 @@ def test_two_compress_programs_through_one_server(server):
 
 @pytest.mark.gpu
 def test_compress_two_mips_shards_through_service(server):
-    """Compress (lib.rs:92-102): two MIPS shard proofs (84 queries, the reference's 2^22 shape scaled to
-    Cpu 2^16) sent as a bincode CompressRequestPayload come back as a ZKMReduceProof whose proof is the
-    node proof a direct HipProver makes from the same children, the oracle verifies it, and its vk is
-    that node program's StarkVerifyingKey."""
+    """Compress (lib.rs:92-102): the two shard proofs of a whole MIPS execution (a CPU shard in the reference's
+    2^22 shape scaled to Cpu 2^16 and the memory shard, 84 queries) sent as a bincode CompressRequestPayload
+    come back as a ZKMReduceProof whose proof is the complete root node proof a direct HipProver makes from the
+    same children, the oracle verifies it, and its vk is that node program's StarkVerifyingKey."""
     from tests import _oracle as O
     from zkmips_amd import bincode as B
     from zkmips_amd import compress_tree as CT
@@ -218,7 +218,8 @@ def test_compress_two_mips_shards_through_service(server):
     from zkmips_amd.prover import HipProver
     from zkmips_amd.septic import CURVE_CUMULATIVE_SUM_START as GCS
     dev = Device(0)
-    sh = SH.shape_shards(SH.MAXIMAL_22, [1, 2], down=6)
+    sh = SH.shape_execution(SH.MAXIMAL_22, 1, down=6)
+    assert len(sh) == 2
     m, prep = sh[0][0], sh[0][1]
     hp = HipProver(dev, m, prep, num_queries=84)
     proofs = [hp.prove_shard(s[2], s[3]) for s in sh]
@@ -228,7 +229,8 @@ def test_compress_two_mips_shards_through_service(server):
     assert st == 200, body
     rvk, rproof = B.read_reduce_proof(SV.decode_fields(body)[1])
     vk = RV.ChildVk.of(m, prep, hp.vk_commit, num_queries=84)
-    cprep, tr, pv, shape, _ = CT.node_witness([(vk, p) for p in proofs])
+    cprep, tr, pv, shape, _ = CT.node_witness([(vk, p) for p in proofs], is_first=True, is_complete=True)
+    assert int(pv[220]) == 1  # RecursionPublicValues.is_complete
     cm = R.compress_machine()
     kw = dict(num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
     direct = HipProver(dev, cm, cprep, **kw)

@@ -302,7 +302,7 @@ def compact_traces(rec, shape) -> dict:
 
 
 def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool = False, compact: bool = False,
-                 dedup: bool = True, session=None):
+                 dedup: bool = True, session=None, is_first: bool = False, is_complete: bool = False):
     """Worker body (no GPU): the compress node's program from its (ChildVk, proof) children, executed,
     padded to the first allowed recursion shape (fix=False: natural power-of-two heights, for small
     tests), as a compress-machine shard.  Returns (prep traces, main traces, public values, shape,
@@ -310,12 +310,14 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
     every main trace is a device work item (compact_traces) and the prep traces a Prep, sent once per
     program structure, worker process and `session` (dedup; a consumer must pass the witnesses of one worker
     through register_prep in the order they were made, as Reducer does; one session per tree) -- a fraction
-    of the bytes through the pool's pipe."""
+    of the bytes through the pool's pipe.  is_first / is_complete: the node covers the execution's first
+    shard / is the root of the whole tree (node_flags)."""
     from . import recursion as R
     from . import recursion_verifier as RV
     t0 = time.perf_counter()
     children = [(resolve_vk(vk), proof) for vk, proof in children]
-    prog = RV.node_flat(children)  # a FlatProgram: built once per program structure, then hints only
+    # a FlatProgram: built once per program structure, then hints only
+    prog = RV.node_flat(children, is_first=is_first, is_complete=is_complete)
     t1 = time.perf_counter()
     shape = R.fix_shape(prog) if fix else {k: max(4, (h - 1).bit_length()) for k, h in R.program_heights(prog).items()}
     if compact:
@@ -560,10 +562,16 @@ class AffinityPool:
         shm_cleanup()
 
 
+def node_flags(node: Node, root: Node) -> dict:
+    """node_witness's flags for node (L, j): its first leaf is the execution's first shard (core.rs
+    `is_first_shard`, lib.rs:543 batch_idx == 0) and it is the tree's root (is_complete, lib.rs:901-909)."""
+    return {"is_first": node[1] == 0, "is_complete": node == root}
+
+
 class Reducer:
     """The event-driven reduction of one rank's part of the tree.
 
-    witness(children) -> concurrent.futures.Future of node_witness's result;
+    witness(children, flags) -> concurrent.futures.Future of node_witness's result (flags: node_flags);
     prove(witness) -> (child vk, proof bytes) for the parent (GPU, called from `inflight` threads)."""
 
     def __init__(self, submit_witness: Callable, prove: Callable, inflight: int = 3,
@@ -594,6 +602,8 @@ class Reducer:
         on_done(node, result) is called for every node proven here."""
         pending = set(mine)
         submitted = set()
+        top = max(widths)
+        root = (top, 0)
         futs: Dict[Node, object] = {}  # witness jobs whose result has not been taken yet
         threads = [threading.Thread(target=self._gpu_worker, daemon=True) for _ in range(self.inflight)]
         for t in threads:
@@ -609,7 +619,7 @@ class Reducer:
                 if ok:
                     submitted.add(node)
                     self.times.setdefault(node, {})["submit"] = time.perf_counter()
-                    fut = self.submit_witness([done[c] for c in ch])
+                    fut = self.submit_witness([done[c] for c in ch], node_flags(node, root))
                     futs[node] = fut
                     fut.add_done_callback(lambda f, n=node: self.events.put(("witness", n, f)))
         ok = False

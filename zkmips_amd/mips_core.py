@@ -1626,6 +1626,29 @@ def _execute(prog, regs, shard, max_steps, state=None):
     return steps, ev, branches, jumps, muls, divs, movs, last, (mevs, mem_init, mem, mem_last), misc, sysinfo
 
 
+def _commit_pvs(pvs, commits: dict):
+    """committed_value_digest / deferred_proofs_digest words from COMMIT / COMMIT_DEFERRED_PROOFS calls."""
+    for idx, word in commits.items():  # COMMIT: committed_value_digest[idx] (syscalls/commit.rs)
+        if isinstance(idx, tuple):  # COMMIT_DEFERRED_PROOFS: deferred_proofs_digest[idx]
+            pvs[SY.PV_DEFERRED + idx[1]] = word
+        else:
+            pvs[4 * idx:4 * idx + 4] = A._bytes(np.asarray([word], np.uint32))[0]
+
+
+def _deferred_shard_pvs(state, shard: int) -> np.ndarray:
+    """A shard without CPU (precompile or memory shard, prove.rs:300-320): the running state -- its pc where
+    the execution stopped (start_pc = next_pc), the digests and exit code so far -- and its shard number."""
+    pvs = np.zeros(PROOF_MAX_NUM_PVS, np.uint32)
+    st = state or {}
+    pc = 0 if st.get("exit_code") is not None else int(st.get("pc", 0))
+    pvs[PV_START_PC] = pvs[PV_NEXT_PC] = pc
+    pvs[PV_EXIT_CODE] = int(st.get("exit_code") or 0)
+    pvs[PV_SHARD] = shard
+    pvs[PV_EXECUTION_SHARD] = int(st.get("cpu_shards", 0)) + 1
+    _commit_pvs(pvs, st.get("commits", {}))
+    return pvs
+
+
 def _mem_word(addr):
     """Initial content of a data word (synthetic, deterministic in the address)."""
     return (addr * 0x9E3779B1 + 0x7F4A7C15) & M32
@@ -1783,15 +1806,18 @@ def program_shard(prog, seed: int = 1, shard: int = 1, max_steps: int = (1 << 24
 
     assert mult.max() < P
     traces["Byte"] = mult.astype(np.uint32)
-    pvs = (splitmix64(0xC0DE100 + seed, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
+    # The public values as the reference's prover state gives them to a CPU shard (prove.rs:266-280): the
+    # running shard and execution-shard numbers, the shard's pcs, the digests committed so far (carried from
+    # shard to shard: once committed, every later shard holds them), the exit code; no MemoryInit/Finalize
+    # in a CPU shard, so its address bits stay zero.
+    pvs = np.zeros(PROOF_MAX_NUM_PVS, np.uint32)
     pvs[PV_START_PC] = start_pc
     pvs[PV_NEXT_PC] = int(npc[-1])  # where the program left off (its end, a jump out of it, or 0 on HALT)
+    pvs[PV_SHARD] = shard
     pvs[PV_EXECUTION_SHARD] = shard
-    for idx, word in sysinfo["commits"].items():  # COMMIT: committed_value_digest[idx] (syscalls/commit.rs)
-        if isinstance(idx, tuple):  # COMMIT_DEFERRED_PROOFS: deferred_proofs_digest[idx]
-            pvs[SY.PV_DEFERRED + idx[1]] = word
-        else:
-            pvs[4 * idx:4 * idx + 4] = A._bytes(np.asarray([word], np.uint32))[0]
+    commits = state.setdefault("commits", {}) if state is not None else {}
+    commits.update(sysinfo["commits"])
+    _commit_pvs(pvs, commits)
     if halt.any():
         pvs[PV_EXIT_CODE] = int(bv[halt][0])
     prep_traces = {"Program": prep, "Byte": A.byte_prep_trace()}
@@ -1852,7 +1878,7 @@ def memory_shard(state, regs, init_regs, shard: int, seed: int = 1):
     msg, rec = np.concatenate([mi, mf]), np.concatenate([ri, rf])
     tg, _ = MM.global_trace(msg, rec, np.full(len(msg), KIND_MEMORY, np.uint32), byte_lookup)
     traces = {"MemoryGlobalInit": ti, "MemoryGlobalFinalize": tf, "Global": tg, "Byte": mult.astype(np.uint32)}
-    pvs = (splitmix64(0xC0DE100 + seed + shard, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
+    pvs = _deferred_shard_pvs(state, shard)
     last_addr = max(a for a, *_ in init)
     pvs[MM.PV_PREV_INIT_BITS:MM.PV_PREV_INIT_BITS + 32] = 0
     pvs[MM.PV_PREV_FIN_BITS:MM.PV_PREV_FIN_BITS + 32] = 0
@@ -1879,7 +1905,7 @@ def _ec_keys():
 PRECOMPILE_CHIP.update(_ec_keys())  # Weierstrass curves, field towers, Uint256MulMod (mips_ec.py)
 
 
-def precompile_shard(code: int, events, shard: int, seed: int = 1):
+def precompile_shard(code: int, events, shard: int, seed: int = 1, state=None):
     """A precompile shard (ExecutionRecord::split, executor/src/record.rs:130-193): the syscall events of one
     precompile, its chip's rows, SyscallPrecompile (one row per call), the calls' local memory accesses in
     MemoryLocal and the Global chip accumulating the syscall receives and the memory messages."""
@@ -1914,8 +1940,7 @@ def precompile_shard(code: int, events, shard: int, seed: int = 1):
     traces["Global"], _ = MM.global_trace(msg, rec, kinds, byte_lookup)
     assert mult.max() < P
     traces["Byte"] = mult.astype(np.uint32)
-    pvs = (splitmix64(0xC0DE100 + seed + shard, PROOF_MAX_NUM_PVS) % np.uint64(P)).astype(np.uint32)
-    pvs[PV_SHARD] = shard
+    pvs = _deferred_shard_pvs(state, shard)
     return core_machine(), {"Program": None, "Byte": A.byte_prep_trace()}, traces, pvs
 
 
@@ -1932,6 +1957,7 @@ def program_shards(prog, seed: int = 1, shard_size: int = 1 << 12, precompile_ev
     out, shard = [], 1
     while PC_BASE <= state["pc"] < end and state["exit_code"] is None:
         out.append(program_shard(prog, seed, shard, shard_size, state=state, regs=regs))
+        state["cpu_shards"] = shard
         shard += 1
     by_code = {}
     for ev in state["precompile"]:
@@ -1939,7 +1965,7 @@ def program_shards(prog, seed: int = 1, shard_size: int = 1 << 12, precompile_ev
     for code in sorted(by_code, key=lambda c: list(PRECOMPILE_CHIP).index(c)):
         evs = by_code[code]
         for k in range(0, len(evs), precompile_events_per_shard):
-            out.append(precompile_shard(code, evs[k:k + precompile_events_per_shard], shard, seed))
+            out.append(precompile_shard(code, evs[k:k + precompile_events_per_shard], shard, seed, state=state))
             shard += 1
     out.append(memory_shard(state, regs, init_regs, shard, seed))
     # every shard holds the preprocessed chips (the verifier opens each vk chip in every shard,

@@ -300,7 +300,14 @@ class ProverService:
         return self.get_prover(blob, prep, nq, lb).prove_shard(traces, pv)
 
     def compress(self, data: bytes) -> bytes:
-        """CompressRequestPayload -> ZKMReduceProof (prover/src/lib.rs:614-954 on the GPU)."""
+        """CompressRequestPayload -> ZKMReduceProof (prover/src/lib.rs:614-954 on the GPU).  The shards must be
+        one whole execution in order: the node programs check what the reference's recursion programs check
+        (zkmips_amd/node_pv.py: consecutive shard numbers and pcs, address bits, digests, exit code, the
+        first-shard conditions, the child vks' membership in the dummy vk tree) and the root asserts the
+        proof complete (start shard 1, next_pc 0, global sum zero); a request that fails them answers
+        invalid_argument before any GPU work.  Not supported: deferred proofs (unimplemented), the real vk
+        map (`vk_map.bin` is absent from the reference snapshot; the dummy map's tree is used, as
+        VERIFY_VK=false does)."""
         from . import bincode as B
         from . import compress_tree as CT
         try:
@@ -332,17 +339,17 @@ class ProverService:
             # one dedup session per request: a worker resends a program's prep traces to each request
             # (a failed or concurrent request never leaves another depending on traces it consumed)
             sid = CT.new_session()
-            submit = lambda ch: self._pool.submit(CT.node_witness_shm, CT.by_ref(ch), True, True, True,
-                                                  session=sid, tag=CT.node_tag(ch))
+            submit = lambda ch, fl: self._pool.submit(CT.node_witness_shm, CT.by_ref(ch), True, True, True,
+                                                      session=sid, **fl, tag=CT.node_tag(ch))
         else:
             from concurrent.futures import ThreadPoolExecutor
             tp = ThreadPoolExecutor(2)
             # threads of this process: no once-per-program prep (arrival order is not completion order)
-            submit = lambda ch: tp.submit(CT.node_witness, ch, True, True, True, False)
+            submit = lambda ch, fl: tp.submit(CT.node_witness, ch, True, True, True, False, **fl)
         reducer = CT.Reducer(submit, prove, self.compress_inflight)
         try:
             if len(leaves) == 1:  # one shard is still wrapped by a compress node
-                rvk, rproof = prove(CT.register_prep(submit(leaves).result()))
+                rvk, rproof = prove(CT.register_prep(submit(leaves, {"is_first": True, "is_complete": True}).result()))
             else:
                 rvk, rproof = CT.reduce_serial(leaves, reducer)
         except ValueError as e:  # a child proof of the wrong shape for its verifying key

@@ -144,8 +144,20 @@ def shape_execution(shape: dict, cpu_shards: int, down: int = 0, seed: int = 1, 
     key, global sums adding to zero).  Returns the list of (machine, prep_traces, traces, public_values)."""
     sh = scaled(shape, down)
     per = min(int(fill * (1 << sh["Cpu"])), (1 << 24) // 5 - 64)
-    prog = shape_program(sh, seed, fill=fill, rows=per * cpu_shards - per // 4)
+    prog = shape_program(sh, seed, fill=fill, rows=per)
+    # the loop's executed instructions per iteration (branches skip part of the body), measured on two short
+    # runs, set the iteration count: the last CPU shard about half full
+    def steps(iters):
+        q = list(prog)
+        q[0] = (A.OP_ADD, C.COUNTER, 0, iters, 0, 1)
+        return len(C._execute(q, C.initial_registers(seed), 1, 1 << 30)[0])
+    s2, s3 = steps(2), steps(3)
+    per_iter, fixed = s3 - s2, s2 - 2 * (s3 - s2)
+    iters = max(1, (per * cpu_shards - per // 2 - fixed) // per_iter)
+    prog[0] = (A.OP_ADD, C.COUNTER, 0, iters, 0, 1)
     out = C.program_shards(prog, seed, shard_size=per)
+    if sum("Cpu" in t for _, _, t, _ in out) != cpu_shards:
+        raise AssertionError("shape_execution: CPU shard count")
     # one shape for every CPU shard (one recursion program structure): the scaled shape, raised where a small
     # scale's fixed per-shard records (the register entries of MemoryLocal, ...) need more rows
     common = dict(sh)
