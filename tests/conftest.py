@@ -24,6 +24,7 @@ _PRIORITY = [
     "test_shapes.py::test_shape_shard_gpu_proof_bytes_identical",
     "test_tendermint.py::test_gpu_tendermint",
     "test_compress_tree.py::test_gpu_mips_node",
+    "test_service.py::test_compress_two_mips_shards",
     "test_tracegen.py::",
 ]
 
