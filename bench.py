@@ -1006,7 +1006,8 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
     return root, res
 
 
-def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int = 3, leaves_job=None):
+def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int = 3, leaves_job=None,
+                 n_leaves: int = 64, leaf_log: int = None):
     """BASELINE config 5 as a field of a bench line: 64 MIPS leaf proofs reduced by the compress tree.
     Node programs verify their children in full (transcript, PoW, Merkle paths, FRI, and the out-of-domain
     constraint check, zkmips_amd/recursion_verifier.py), are padded to the first fitting
@@ -1017,9 +1018,10 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
     from zkmips_amd import recursion_verifier as RV
     import shutil
     import tempfile
-    if leaves_job is None:  # generated here (the default line submits it to the pool at the start)
+    leaf_log = leaf_log or args.leaf_log
+    if leaves_job is None:  # generated here (the default line submits it to the pool earlier)
         d = tempfile.mkdtemp(prefix="zkm_cl_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
-        leaves_job = (pool.submit(_compress_leaves_job, d, 64, 22 - args.leaf_log), d)
+        leaves_job = (pool.submit(_compress_leaves_job, d, n_leaves, 22 - leaf_log), d)
     fut, d = leaves_job
     try:
         meta, info, gen_s = fut.result()
@@ -1034,12 +1036,13 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
     del warm
     (rvk, rproof), r = compress_tree_run(pool, dev, leaves, inflight, distributed=world > 1)
     n = r["proofs"]
-    out = {"metric": "compress proofs/sec, end to end (64-leaf compress tree = 63 recursion-machine proofs, "
-                     "BASELINE config 5)",
-           "value": round(63 / r["wall_s"], 3), "unit": "proofs/s", "tree_wall_s": round(r["wall_s"], 3),
-           "prove_only": {"value": round(63 / r["gpu_busy_s"], 3), "unit": "proofs/s",
+    nodes = len(leaves) - 1  # a binary tree over the leaves (odd nodes carried up) has leaves - 1 nodes
+    out = {"metric": f"compress proofs/sec, end to end ({len(leaves)}-leaf compress tree = {nodes} recursion-machine "
+                     f"proofs, BASELINE config 5), leaves of Cpu 2^{leaf_log} rows",
+           "value": round(nodes / r["wall_s"], 3), "unit": "proofs/s", "tree_wall_s": round(r["wall_s"], 3),
+           "prove_only": {"value": round(nodes / r["gpu_busy_s"], 3), "unit": "proofs/s",
                           "gpu_busy_s": round(r["gpu_busy_s"], 3),
-                          "what": "63 proofs over the time at least one node proof was on the GPU"},
+                          "what": f"{nodes} proofs over the time at least one node proof was on the GPU"},
            "witness_generation": {"build_s_per_node": round(r["witness_build_s"] / max(1, n), 3),
                                   "execute_and_traces_s_per_node": round(r["witness_execute_and_traces_s"] / max(1, n), 3),
                                   "workers": args.node_workers,
@@ -1401,6 +1404,8 @@ def main():
                     help="skip the default line's config-4 leg (the tendermint guest on the reference's blocks)")
     ap.add_argument("--no-sizes", action="store_true",
                     help="skip the default line's size series (resident rows/s and LDE time at 2^20, 2^21, 2^23)")
+    ap.add_argument("--no-leaf21", dest="leaf21", action="store_false",
+                    help="skip the default line's compress_2e21 leg (a 4-leaf tree of 2^21-row MIPS shards)")
     ap.add_argument("--leaf-log", type=int, default=16, help="compress leg: MIPS leaf shards in the maximal shape scaled to Cpu 2^leaf_log rows")
     ap.add_argument("--node-workers", type=int, default=12,
                     help="compress workload: processes generating node witnesses (the box allots 16 CPUs per GPU)")
@@ -1427,7 +1432,7 @@ def main():
     if (not (args.no_compress and args.no_tendermint) and args.workload == "fib"
             and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.pmc_child):
         pool = start_witness_pool(max(1, min(args.node_workers, 32)))
-    leaves_job = None
+    leaves_job = leaves21_job = None
 
     import torch
     rk = Ranks(args)
@@ -1470,6 +1475,9 @@ def main():
         import tempfile
         d = tempfile.mkdtemp(prefix="zkm_cl_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
         leaves_job = (pool.submit(_compress_leaves_job, d, 64, 22 - args.leaf_log), d)
+        if args.leaf21:
+            d21 = tempfile.mkdtemp(prefix="zkm_cl21_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+            leaves21_job = (pool.submit(_compress_leaves_job, d21, 4, 1), d21)
 
     if rank != 0:
         rk.close()
@@ -1660,6 +1668,11 @@ def main():
         leg("maxshape", lambda: maxshape_leg(args, rk, n, K))
     if pool is not None and not args.no_compress:
         leg("compress", lambda: compress_leg(args, pool, prover.dev, leaves_job=leaves_job)[0])
+    if pool is not None and not args.no_compress and args.leaf21:
+        # the reference's default shard size (2^21 Cpu rows, crates/stark/src/opts.rs:6): a 4-leaf tree (3 CPU
+        # shards + the memory shard of one execution), so the node programs verify 2^21-row leaves
+        leg("compress_2e21", lambda: compress_leg(args, pool, prover.dev, leaves_job=leaves21_job, n_leaves=4,
+                                                  leaf_log=21)[0])
     if tm_future is not None:
         import shutil
         try:
