@@ -453,6 +453,10 @@ def maxshape_leg(args, rk, n, K):
            "h2d_bytes_per_shard": rec_bytes,
            "vs_resident": round(el_rec / el_res, 3),
            "records_copy_wait_ms": [round(1e3 * sum(v), 2) for _, v in sorted(rec_waits.items())],
+           "call_ms_mean": {m_: round(1e3 * float(np.mean([t for (mm, _), v in sb.slot_proof_s.items() if mm == m_
+                                                           for t in v])), 3)
+                            for m_ in ("records", "pipelined", "resident")},
+           "tracegen_ms_mean_per_step": round(1e3 * float(np.mean([t for v in sb.slot_tracegen_s.values() for t in v])), 3),
            "host_traces": {"value": round(K * rows * steps / el, 1), "ms_per_shard": round(1e3 * el / (steps * K), 3),
                            "h2d_bytes_per_shard": int(sum(v.nbytes for v in tr.values())),
                            "vs_resident": round(el / el_res, 3)},
@@ -1235,6 +1239,7 @@ class ShardBench:
         self.stagger = None
         self.slot_waits = {}
         self.slot_proof_s = {}  # (mode, slot) -> host seconds of each zkm_prove_shard call
+        self.slot_tracegen_s = {}  # slot -> host seconds of each records-mode trace build (waited for)
         import threading
         self.copy_lock = threading.Lock()
         self.copy_stream = torch.cuda.Stream() if os.environ.get("ZKM_BENCH_COPY_STREAMS") != "slot" else None
@@ -1303,6 +1308,7 @@ class ShardBench:
             t = time.perf_counter()
             if mode == "records":
                 src = self.traces_from_records(k, src, slot_stream)
+                self.slot_tracegen_s.setdefault(k, []).append(time.perf_counter() - t)
             pr = prove_resident(prover, src, pv)
             ts.append(time.perf_counter() - t)
         self.slot_waits[k] = waits  # host seconds each step waited for its traces' copy
@@ -1397,7 +1403,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-maxshape", action="store_true",
                     help="skip the default line's secondary leg: the reference's maximal 2^22 MIPS shard shape")
-    ap.add_argument("--maxshape-steps", type=int, default=4)
+    ap.add_argument("--maxshape-steps", type=int, default=8)
     ap.add_argument("--no-compress", action="store_true",
                     help="skip the default line's compress leg (config 5: 64 MIPS leaves, 63 node proofs)")
     ap.add_argument("--no-tendermint", action="store_true",
