@@ -13,13 +13,14 @@
 //   M_E y = C_0 + 2^8 C_1 + 2^16 C_2 + 2^24 C_3 + K   (|C_l| <= 35 * 128, the sum < 2^37).
 // 16 MFMAs per layer per wave (4 groups x 4 limbs) and ~5 VALU ops per word.
 //
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 p2_mfma_probe.hip -o p2_mfma_probe
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form p2_mfma_probe.hip -o p2_mfma_probe
+// (the flag keeps the MFMA results in VGPRs: without it every result word costs a v_accvgpr_read)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 
-#include "../../zkmips_amd/csrc/p2.cuh"
+#include "../../zkmips_amd/csrc/p2_mfma.cuh"
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -135,6 +136,33 @@ __global__ __launch_bounds__(NT) void k_mfma(uint32_t *out) {
         for (int r = 0; r < 4; r++) out[(uint64_t)(base + 16 * g + n) * 16 + 4 * h + r] = y[g][r];
 }
 
+// The whole permutation: p2::permute (one lane per state) against p2m::permute (zkmips_amd/csrc/p2_mfma.cuh:
+// the external layers on the matrix cores, 64 states per wave), ITERP permutations per state.
+template <int ITERP>
+__global__ __launch_bounds__(NT) void k_perm_valu(uint32_t *out) {
+    const uint32_t st = blockIdx.x * NT + threadIdx.x;
+    uint32_t s[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) s[w] = init_word(st, w) % kb::P;
+    for (int it = 0; it < ITERP; it++) p2::permute(s);
+#pragma unroll
+    for (int w = 0; w < 16; w++) out[(uint64_t)st * 16 + w] = s[w];
+}
+template <int ITERP>
+__global__ __launch_bounds__(NT) void k_perm_mfma(uint32_t *out) {
+    __shared__ uint32_t tile[NT / 64 * p2m::WAVE_WORDS];
+    __shared__ uint64_t ct[p2m::NCONST * 16];
+    const p2m::Ctx c = p2m::make_ctx(tile + (threadIdx.x >> 6) * p2m::WAVE_WORDS, ct);
+    __syncthreads();
+    const uint32_t st = blockIdx.x * NT + threadIdx.x;
+    uint32_t s[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) s[w] = init_word(st, w) % kb::P;
+    for (int it = 0; it < ITERP; it++) p2m::permute(c, s);
+#pragma unroll
+    for (int w = 0; w < 16; w++) out[(uint64_t)st * 16 + w] = s[w];
+}
+
 #define CK(x)                                                                  \
     do {                                                                       \
         hipError_t e_ = (x);                                                   \
@@ -192,5 +220,18 @@ int main(int argc, char **argv) {
     rep("valu32", t32);
     rep("mfma", tmf);
     printf("states %zu  iterations %d  mismatches: mfma %zu  valu32 %zu\n", states, ITER, bad_mf, bad_32);
-    return (bad_mf || bad_32) ? 2 : 0;
+    // whole permutations
+    constexpr int ITERP = 16;
+    const double pv = time_ms([&] { hipLaunchKernelGGL(k_perm_valu<ITERP>, dim3(blocks), dim3(NT), 0, 0, o64); }, reps);
+    const double pm = time_ms([&] { hipLaunchKernelGGL(k_perm_mfma<ITERP>, dim3(blocks), dim3(NT), 0, 0, omf); }, reps);
+    CK(hipMemcpy(a.data(), o64, states * 64, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(c.data(), omf, states * 64, hipMemcpyDeviceToHost));
+    size_t bad_p = 0;
+    for (size_t i = 0; i < a.size(); i++) bad_p += a[i] != c[i];
+    const double perms = (double)states * ITERP;
+    printf("permute  valu %8.3f ms  %.4e perms/s  %6.0f slot-equivalents/perm\n", pv, perms / (pv * 1e-3),
+           pv * 1e-3 * slots_per_s / perms);
+    printf("permute  mfma %8.3f ms  %.4e perms/s  %6.0f slot-equivalents/perm  (%.3fx)  mismatches %zu\n", pm,
+           perms / (pm * 1e-3), pm * 1e-3 * slots_per_s / perms, pv / pm, bad_p);
+    return (bad_mf || bad_32 || bad_p) ? 2 : 0;
 }
