@@ -290,13 +290,28 @@ def host_info():
 
 
 def cgroup_cpu_limit():
-    """The cgroup v2 CPU quota of this process in CPUs (cpu.max "quota period"), or None if unlimited."""
+    """The cgroup v2 CPU quota of this process in CPUs, or None if unlimited: the tightest cpu.max ("quota
+    period") on the path from the process's cgroup up to the mount root.  On the GPU box the process's own
+    cgroup has no cpu.max and the quota (1600000 100000 = 16 CPUs) sits on /sys/fs/cgroup itself
+    (profiles/r05_cpu_cliff.txt), so reading only the leaf misses it."""
     try:
         cg = open("/proc/self/cgroup").read().strip().split("\n")[0].split(":", 2)[2]
-        q, p = open(f"/sys/fs/cgroup{cg}/cpu.max").read().split()
-        return None if q == "max" else round(int(q) / int(p), 2)
-    except (OSError, ValueError, IndexError):
-        return None
+    except (OSError, IndexError):
+        cg = "/"
+    best = None
+    path = cg.rstrip("/")
+    while True:
+        try:
+            q, p = open(f"/sys/fs/cgroup{path}/cpu.max").read().split()
+            if q != "max":
+                c = int(q) / int(p)
+                best = c if best is None else min(best, c)
+        except (OSError, ValueError):
+            pass
+        if not path:
+            break
+        path = path.rsplit("/", 1)[0]
+    return None if best is None else round(best, 2)
 
 
 def _omp(threads=None) -> int:
@@ -317,10 +332,12 @@ def calibrate_cpu_threads(log_n=18, queries=84):
     from tests import _oracle as O
     from zkmips_amd import workloads as W
     cpus = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_limit()
+    allot = {int(quota)} if quota and quota >= 1 else set()
     m, prep, traces, pvs = W.fib_shard(1 << log_n, seed=2)
     pr = O.OracleProver(m, prep, num_queries=queries)
     table = {}
-    for c in sorted({c for c in (8, 16, 24, 32, 48, 64, 128, cpus) if c <= cpus}):
+    for c in sorted({c for c in {8, 16, 24, 32, 48, 64, 128, cpus} | allot if c <= cpus}):
         _omp(c)
         t = time.time()
         rc, _ = pr.prove(traces, pvs)
@@ -350,12 +367,14 @@ def cpu_baseline(log_n, queries):
     cpus = len(os.sched_getaffinity(0))
     quota = cgroup_cpu_limit()
     return {"value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "cpus_allotted": quota if quota is not None else cpus,
             "host": dict(host_info(), cpus_allowed=cpus, cgroup_cpu_quota=quota),
             "thread_calibration_s": {str(k): v for k, v in table.items()},
             "sample": f"one S-SHARD FibCpu 2^{log_n}-row shard (+FibTable), full commit+open, {queries} queries, "
                       f"{dt:.2f} s wall on {threads} OpenMP threads, the fastest count for this box among "
-                      f"{sorted(table)} (2^18-row calibration proofs; {cpus} CPUs in the affinity mask) "
-                      "(AVX-512 Poseidon2/LDE)"}
+                      f"{sorted(table)} (2^18-row calibration proofs; {cpus} CPUs in the affinity mask, "
+                      f"CFS quota {quota} CPUs: more threads than the quota spin-wait against the throttle, "
+                      "DESIGN.md §7) (AVX-512 Poseidon2/LDE)"}
 
 
 def profile_proofs(prover, dev_traces, pvs, nprof):
