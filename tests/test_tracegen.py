@@ -240,6 +240,33 @@ def test_records_reproduce_executor_tuples():
     assert (mi["mem_access"]["tag"][load] == TG.REC_READ).all() and (mi["mem_access"]["tag"][~load] == TG.REC_WRITE).all()
 
 
+@pytest.mark.parametrize("name", sorted(PROGRAMS))
+def test_native_record_conversion_is_the_numpy_one(name):
+    """libzkm_pyconv.so (csrc/host/pyconv.cpp) writes the same CpuEventFfi bytes as the numpy conversion, and
+    its generic flattener the same rows as numpy's; malformed rows raise instead of being read."""
+    cap, _, _, _, _ = _capture(name)
+    a = TG.cpu_events(cap["steps"], cap["shard"])
+    b = TG.cpu_events_numpy(cap["steps"], cap["shard"])
+    assert len(a) == len(cap["steps"]) and a.tobytes() == b.tobytes()
+    for key, w in (("branches", 8), ("mevs", 13), ("jumps", 7), ("movs", 7), ("muls", 11), ("divs", 9),
+                   ("misc", 12)):
+        lst = cap.get(key, [])
+        if len(lst):
+            assert np.array_equal(TG._rows(lst, w), np.asarray(lst, np.int64).reshape(-1, w)), key
+    assert np.array_equal(TG._rows(cap["entries"], 7), np.asarray(cap["entries"], np.int64).reshape(-1, 7))
+    assert np.array_equal(TG._rows([(1, (2, 3), None), [4, [5, 6], (7, 8)]], 5, none_w=2),
+                          [[1, 2, 3, 0, 0], [4, 5, 6, 7, 8]])
+    assert TG._rows([], 4).shape == (0, 4)
+    with pytest.raises(ValueError):
+        TG._rows([(1, 2), (3,)], 2)
+    with pytest.raises(TypeError):
+        TG._rows([(1, "x")], 2)
+    with pytest.raises(OverflowError):
+        TG._rows([(1, 1 << 70)], 2)
+    with pytest.raises(ValueError):
+        TG.cpu_events([(1, 2, 3)], 1)
+
+
 def test_alu_records_carry_the_clz_dependencies():
     """ShiftRight's records = the CPU's SRL/SRA/ROR events then the CLZ/CLO dependencies (as its host trace)."""
     cap, tr, _, _, _ = _capture("random")

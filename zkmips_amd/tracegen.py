@@ -12,8 +12,8 @@ No fallback: every call goes to libzkm_hip.so and raises if it is missing.
 from __future__ import annotations
 
 import ctypes as C
-
 import functools
+import os
 
 import numpy as np
 
@@ -96,9 +96,39 @@ GLOBAL_WIDTH = 99
 
 
 # ---------------------------------------------------------------- records from this repository's executor
+PYCONV_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libzkm_pyconv.so")
+
+
+@functools.lru_cache(maxsize=None)
+def _pyconv():
+    """libzkm_pyconv.so (csrc/host/pyconv.cpp): the executor's tuples walked natively.  PyDLL keeps the GIL
+    held through each call and turns an error set there into a Python exception."""
+    if not os.path.exists(PYCONV_PATH):
+        raise RuntimeError(f"{PYCONV_PATH} is not built (make -C zkmips_amd/csrc, or __graft_entry__.build())")
+    L = C.PyDLL(PYCONV_PATH)
+    L.zkm_py_flatten_i64.argtypes = [C.py_object, C.c_int64, C.c_int64, C.c_void_p, C.c_int64]
+    L.zkm_py_flatten_i64.restype = C.c_int64
+    L.zkm_py_cpu_events.argtypes = [C.py_object] + [C.c_uint32] * 5 + [C.c_void_p, C.c_int64]
+    L.zkm_py_cpu_events.restype = C.c_int64
+    return L
+
+
+def _rows(x, width: int, none_w: int = 0) -> np.ndarray:
+    """An (n, width) int64 array of the executor's record tuples (or an array already), flattened natively
+    (nested tuples allowed; None stands for none_w zeros)."""
+    if isinstance(x, np.ndarray):
+        return x.astype(np.int64, copy=False).reshape(-1, width)
+    if not isinstance(x, (list, tuple)):
+        x = list(x)
+    out = np.empty((len(x), width), np.int64)
+    if len(x):
+        _pyconv().zkm_py_flatten_i64(x, width, none_w, out.ctypes.data, len(x))
+    return out
+
+
 def program_ffi(prog) -> np.ndarray:
     """Program::instructions as InstructionFfi (prog rows: opcode, op_a, op_b, op_c, imm_b, imm_c)."""
-    P_ = np.asarray(prog, np.int64).reshape(-1, 6)
+    P_ = _rows(prog, 6)
     out = np.zeros(len(P_), INSTRUCTION)
     out["opcode"], out["op_a"] = P_[:, 0], P_[:, 1]
     out["op_b"], out["op_c"] = P_[:, 2] & 0xFFFFFFFF, P_[:, 3] & 0xFFFFFFFF
@@ -110,7 +140,18 @@ def program_ffi(prog) -> np.ndarray:
 def cpu_events(steps, shard: int) -> np.ndarray:
     """CpuEvent records (events/cpu.rs:8-44 as CpuEventFfi) of the executor's steps: the op_a access a
     write (a read when the value is unchanged), op_b / op_c reads unless immediate (executor.rs
-    rr/rw at MemoryAccessPosition A = 3, B = 2, C = 1)."""
+    rr/rw at MemoryAccessPosition A = 3, B = 2, C = 1).  Written natively (zkm_py_cpu_events), struct by
+    struct; cpu_events_numpy is the same conversion in numpy (the tests compare the bytes)."""
+    n = len(steps)
+    e = np.empty(n, CPU_EVENT)  # every byte written by the converter
+    if n:
+        _pyconv().zkm_py_cpu_events(steps if isinstance(steps, (list, tuple)) else list(steps), shard, MC.PC_BASE,
+                                    MC.POS_A, MC.POS_B, MC.POS_C, e.ctypes.data, n)
+    return e
+
+
+def cpu_events_numpy(steps, shard: int) -> np.ndarray:
+    """cpu_events in numpy (the reference for the native converter's bytes)."""
     n = len(steps)
     e = np.zeros(n, CPU_EVENT)
     if not n:
@@ -159,7 +200,7 @@ def alu_events(op, a, b, c, pc, npc=None) -> np.ndarray:
 
 def memory_local_events(entries) -> np.ndarray:
     """MemoryLocalEvent records of (addr, initial shard, clk, value, final shard, clk, value) rows."""
-    E = np.asarray(entries, np.int64).reshape(-1, 7)
+    E = _rows(entries, 7)
     e = np.zeros(len(E), MEMORY_LOCAL_EVENT)
     e["addr"] = E[:, 0]
     e["initial"] = E[:, 1:4]
@@ -179,7 +220,7 @@ def memory_init_final_events(events) -> np.ndarray:
 
 def syscall_events(syscalls) -> np.ndarray:
     """SyscallEvent records of the executor's syscall tuples (pc, next_pc, shard, clk, a, b, c, prev_a, id)."""
-    S = np.asarray(syscalls, np.int64).reshape(-1, 9)
+    S = _rows(syscalls, 9)
     e = np.zeros(len(S), SYSCALL_EVENT)
     e["pc"], e["next_pc"], e["shard"], e["clk"] = S[:, 0], S[:, 1], S[:, 2], S[:, 3]
     e["a_record"] = np.stack([S[:, 4], S[:, 2], S[:, 3] + MC.POS_A, S[:, 7], np.zeros(len(S)), np.zeros(len(S))],
@@ -207,7 +248,7 @@ def shard_global_events(capture: dict) -> np.ndarray:
     core_sc = capture["core_syscalls"]
     core = core_sc[:, [2, 3, 8, 5, 6]] if len(core_sc) else np.zeros((0, 5), np.int64)
     smsg = SY.syscall_global_messages(core)
-    gmsg, grec = MM.memory_local_global_events(np.asarray(capture["entries"], np.int64).reshape(-1, 7))
+    gmsg, grec = MM.memory_local_global_events(_rows(capture["entries"], 7))
     return global_events(np.concatenate([smsg, gmsg]), np.concatenate([np.zeros(len(smsg), np.uint8), grec]),
                          np.concatenate([np.full(len(smsg), SY.KIND_SYSCALL), np.full(len(gmsg), MC.KIND_MEMORY)]))
 
@@ -219,7 +260,7 @@ def add_sub_records(alu) -> np.ndarray:
 
 def branch_records(branches) -> np.ndarray:
     """BranchEvents of the executor's branch tuples (pc, op, a, b, c, next_pc, next_next_pc, taken)."""
-    B = np.asarray(branches, np.int64).reshape(-1, 8)
+    B = _rows(branches, 8)
     e = np.zeros(len(B), BRANCH_EVENT)
     e["pc"], e["opcode"], e["a"], e["b"], e["c"] = B[:, 0], B[:, 1], B[:, 2], B[:, 3], B[:, 4]
     e["next_pc"], e["next_next_pc"] = B[:, 5], B[:, 6]
@@ -229,7 +270,7 @@ def branch_records(branches) -> np.ndarray:
 def mem_instr_records(mevs, shard: int) -> np.ndarray:
     """MemInstrEvents of the executor's memory-instruction tuples (pc, npc, op, a, b, c, prev_a, clk, addr,
     prev_mem, mem, mem_prev_shard, mem_prev_clk): loads carry a Read record, stores a Write record."""
-    E = np.asarray(mevs, np.int64).reshape(-1, 13)
+    E = _rows(mevs, 13)
     n = len(E)
     assert np.array_equal(E[:, 8], (E[:, 4] + E[:, 5]) & 0xFFFFFFFF), "address = b + c"
     e = np.zeros(n, MEM_INSTR_EVENT)
@@ -246,7 +287,7 @@ def mem_instr_records(mevs, shard: int) -> np.ndarray:
 
 def jump_records(jumps) -> np.ndarray:
     """JumpEvents of the executor's jump tuples (pc, op, a, b, c, next_pc, next_next_pc)."""
-    J = np.asarray(jumps, np.int64).reshape(-1, 7)
+    J = _rows(jumps, 7)
     e = np.zeros(len(J), JUMP_EVENT)
     e["pc"], e["opcode"], e["a"], e["b"], e["c"] = J[:, 0], J[:, 1], J[:, 2], J[:, 3], J[:, 4]
     e["next_pc"], e["next_next_pc"] = J[:, 5], J[:, 6]
@@ -255,7 +296,7 @@ def jump_records(jumps) -> np.ndarray:
 
 def movcond_records(movs) -> np.ndarray:
     """MovCondEvents of the executor's tuples (pc, next_pc, op, a, b, c, prev_a)."""
-    E = np.asarray(movs, np.int64).reshape(-1, 7)
+    E = _rows(movs, 7)
     e = np.zeros(len(E), MOVCOND_EVENT)
     for j, f in enumerate(("pc", "next_pc", "opcode", "a", "b", "c", "prev_a")):
         e[f] = E[:, j]
@@ -265,7 +306,7 @@ def movcond_records(movs) -> np.ndarray:
 def mul_records(muls, shard: int) -> np.ndarray:
     """CompAluEvents of the executor's Mul tuples (op, a, b, c, pc, npc, hi, clk, prev_hi, prev_shard, prev_clk;
     clk < 0: no HI write): the HI record written at clk + POS_HI."""
-    E = np.asarray(muls, np.int64).reshape(-1, 11)
+    E = _rows(muls, 11)
     n = len(E)
     e = np.zeros(n, COMP_ALU_EVENT)
     hrr = E[:, 7] >= 0
@@ -281,7 +322,7 @@ def mul_records(muls, shard: int) -> np.ndarray:
 def divrem_records(divs, shard: int) -> np.ndarray:
     """CompAluEvents of the executor's DivRem tuples (op, b, c, pc, npc, clk, prev_hi, prev_shard, prev_clk;
     clk < 0: no HI write): a = quotient, hi = remainder, the HI record (the remainder) written at clk + POS_HI."""
-    E = np.asarray(divs, np.int64).reshape(-1, 9)
+    E = _rows(divs, 9)
     n = len(E)
     qr = np.asarray([MC._qr(int(o), int(x), int(y)) for o, x, y in zip(E[:, 0], E[:, 1], E[:, 2])],
                     np.int64).reshape(n, 2)
@@ -300,7 +341,7 @@ def divrem_records(divs, shard: int) -> np.ndarray:
 def misc_records(misc, shard: int) -> np.ndarray:
     """MiscEvents of the executor's tuples (op, a, b, c, prev_a, pc, npc, clk, hi_prev, hi_new, hi_prev_shard,
     hi_prev_clk): MADDU / MSUBU / MADD / MSUB carry the HI write at clk + POS_HI."""
-    E = np.asarray(misc, np.int64).reshape(-1, 12)
+    E = _rows(misc, 12)
     n = len(E)
     e = np.zeros(n, MISC_EVENT)
     md = np.isin(E[:, 0], MC.MADDSUB_OPS)
@@ -794,10 +835,13 @@ def sha_compress_trace(events_dev, n: int, height: int = None, byte_mult=None):
 def alu_records(alu, kind: str) -> np.ndarray:
     """The AluEvents of one ALU chip (kind "add", "bit", "lt", "sll" or "sr") from the executor's event
     lists; ShiftRight's include the SRL dependencies of the CLZ / CLO events."""
+    def cols(lst):
+        R = _rows(lst, 6).astype(np.uint32)
+        return tuple(R[:, i] for i in range(6))
     ev = alu.get(kind, [])
-    arrs = MC._ev_arrays(ev) if len(ev) else tuple(np.zeros(0, np.uint32) for _ in range(6))
+    arrs = cols(ev) if len(ev) else tuple(np.zeros(0, np.uint32) for _ in range(6))
     if kind == "sr" and len(alu.get("clz", [])):
-        op, a, b = MC._ev_arrays(alu["clz"])[:3]
+        op, a, b = cols(alu["clz"])[:3]
         dep = A.clz_dependencies(op, a, b)
         arrs = tuple(np.concatenate([x, d]).astype(np.uint32) for x, d in zip(arrs, dep))
     op, a, b, c, pc, npc = arrs
