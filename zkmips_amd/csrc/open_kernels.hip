@@ -431,19 +431,19 @@ __device__ __forceinline__ void open_weights(uint4 *wl, const OpenWeights &pw, u
     }
 }
 
-__global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
+__device__ __forceinline__ void open_dot_lds(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                  OpenWeights pw, int with_next, int nseg, uint32_t slab,
-                                                 uint32_t *partial) {
+                                                 uint32_t *partial, uint32_t bx, uint32_t by) {
     __shared__ uint4 wl[OPEN_SEG];
     __shared__ uint32_t red[NT / 64][OPEN_CB][8];
-    const uint64_t j0 = (uint64_t)blockIdx.x * OPEN_SEG;
+    const uint64_t j0 = (uint64_t)bx * OPEN_SEG;
     const uint32_t len = (uint32_t)(n - j0 < (uint64_t)OPEN_SEG ? n - j0 : OPEN_SEG);
     {
         const uint32_t r0 = threadIdx.x * INV_CHUNK;
         if (r0 < len) open_weights(wl, pw, n, j0, r0, (int)(len - r0 < (uint32_t)INV_CHUNK ? len - r0 : INV_CHUNK));
     }
     __syncthreads();
-    const uint32_t c_begin = blockIdx.y * slab;
+    const uint32_t c_begin = by * slab;
     const uint32_t c_end = c_begin + slab < ncols ? c_begin + slab : ncols;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += OPEN_CB) {
@@ -506,10 +506,15 @@ __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ co
             const int k = threadIdx.x >> 3, e = threadIdx.x & 7;
             uint32_t acc = 0;
             for (int q = 0; q < NT / 64; q++) acc = add(acc, red[q][k][e]);
-            partial[((uint64_t)(cb0 + k) * nseg + blockIdx.x) * 8 + e] = acc;
+            partial[((uint64_t)(cb0 + k) * nseg + bx) * 8 + e] = acc;
         }
         __syncthreads();  // red is reused by the next column block
     }
+}
+__global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
+                                                 OpenWeights pw, int with_next, int nseg, uint32_t slab,
+                                                 uint32_t *partial) {
+    open_dot_lds(cols, ncols, n, pw, with_next, nseg, slab, partial, blockIdx.x, blockIdx.y);
 }
 
 // Full segments (n a multiple of OPEN_SEG): thread t owns rows 4t..4t+3 and 4(NT + t)..+3 of its segment
@@ -519,11 +524,11 @@ __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ co
 // lane (the wave's last lane loads it).  The per-thread sums of a column block are reduced through LDS
 // (eight threads per output word, 32 partial sums each) instead of a 6-step shuffle tree per word.
 static constexpr int OPEN_RED_LD = NT + 8;  // padded row: the eight outputs a wave sums sit on distinct banks
-__global__ __launch_bounds__(NT) void k_open_dot_regs(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
+__device__ __forceinline__ void open_dot_regs(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                       OpenWeights pw, int with_next, int nseg, uint32_t slab,
-                                                      uint32_t *partial) {
+                                                      uint32_t *partial, uint32_t bx, uint32_t by) {
     __shared__ uint32_t red[OPEN_CB * 8][OPEN_RED_LD];
-    const uint64_t j0 = (uint64_t)blockIdx.x * OPEN_SEG;
+    const uint64_t j0 = (uint64_t)bx * OPEN_SEG;
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t ra = 4 * t, rb = 4 * NT + 4 * t;
     ef w[8];
@@ -550,7 +555,7 @@ __global__ __launch_bounds__(NT) void k_open_dot_regs(const uint64_t *__restrict
             w[k] = pw.mul_omega ? ef_mul_base(v, om[k]) : v;
         }
     }
-    const uint32_t c_begin = blockIdx.y * slab;
+    const uint32_t c_begin = by * slab;
     const uint32_t c_end = c_begin + slab < ncols ? c_begin + slab : ncols;
     for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += OPEN_CB) {
         const int nc = (int)(c_end - cb0 < (uint32_t)OPEN_CB ? c_end - cb0 : OPEN_CB);
@@ -592,18 +597,154 @@ __global__ __launch_bounds__(NT) void k_open_dot_regs(const uint64_t *__restrict
             r = add(r, __shfl_xor(r, 1, 64));
             r = add(r, __shfl_xor(r, 2, 64));
             r = add(r, __shfl_xor(r, 4, 64));
-            if (q == 0 && (int)(o >> 3) < nc) partial[((uint64_t)(cb0 + (o >> 3)) * nseg + blockIdx.x) * 8 + (o & 7)] = r;
+            if (q == 0 && (int)(o >> 3) < nc) partial[((uint64_t)(cb0 + (o >> 3)) * nseg + bx) * 8 + (o & 7)] = r;
         }
         __syncthreads();  // red is reused by the next column block
     }
 }
+__global__ __launch_bounds__(NT) void k_open_dot_regs(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
+                                                      OpenWeights pw, int with_next, int nseg, uint32_t slab,
+                                                      uint32_t *partial) {
+    open_dot_regs(cols, ncols, n, pw, with_next, nseg, slab, partial, blockIdx.x, blockIdx.y);
+}
 static_assert(OPEN_CB * 8 * 8 == NT, "one reduction thread group per output word");
+
+// k_open_dot_regs with the next column block's loads issued before the current block's products (two
+// register sets used alternately): 152 VGPRs, 3 waves per SIMD
+__device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
+                                                      OpenWeights pw, int with_next, int nseg, uint32_t slab,
+                                                      uint32_t *partial, uint32_t bx, uint32_t by) {
+    __shared__ uint32_t red[OPEN_CB * 8][OPEN_RED_LD];
+    const uint64_t j0 = (uint64_t)bx * OPEN_SEG;
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    const uint32_t ra = 4 * t, rb = 4 * NT + 4 * t;
+    ef w[8];
+    {
+        // w_n^idx of the two quads: natural order, one aligned 16-byte twiddle load per quad; bit-reversed,
+        // idx(i0 + {0, 1, 2, 3}) = rev(i0) + {0, n/2, n/4, 3n/4}: one twiddle, its negation, one product
+        // with w_n^(n/4) and that one's negation
+        uint32_t om[8];
+        const uint64_t h = n >> 1;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint64_t i0 = j0 + (q ? rb : ra);
+            uint32_t *o = om + 4 * q;
+            if (pw.bitrev) {
+                o[0] = root_pow(pw.tw, n, rev_bits((uint32_t)i0, pw.log_n));
+                o[1] = neg(o[0]);
+                o[2] = mul(o[0], pw.tw[h + (n >> 2)]);
+                o[3] = neg(o[2]);
+            } else {
+                const bool hi = i0 >= h;
+                const uint4 v = *(const uint4 *)(pw.tw + h + (hi ? i0 - h : i0));
+                o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+                if (hi)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) o[k] = neg(o[k]);
+            }
+        }
+        ef d[8];
+        ef run = ef_one();
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            d[k] = ef_sub(pw.z, ef_base(mul(pw.s, om[k])));
+            w[k] = run;
+            run = ef_mul(run, d[k]);
+        }
+        ef iv = ef_inv(run);
+#pragma unroll
+        for (int k = 7; k >= 0; k--) {
+            ef v = ef_mul(iv, w[k]);
+            iv = ef_mul(iv, d[k]);
+            w[k] = pw.mul_omega ? ef_mul_base(v, om[k]) : v;
+        }
+    }
+    const uint32_t c_begin = by * slab;
+    const uint32_t c_end = c_begin + slab < ncols ? c_begin + slab : ncols;
+    // the next column block's rows are loaded before this block's products (software pipelining: the
+    // loads of block b + 1 are in flight while block b is multiplied and reduced; two register sets used
+    // alternately, so no copy forces an early wait).  Global (not flat) loads: flat ones also count on
+    // lgkmcnt, and the LDS reduction's waits would drain the prefetched block.  The wave's last lane also
+    // loads the row after each of its two quads (the next-row products; the wrap-around) in the same batch.
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(1))) u32x4 *g4;
+    typedef const __attribute__((address_space(1))) uint32_t *g1;
+    struct Blk {
+        uint4 a[OPEN_CB], b[OPEN_CB];
+        uint32_t xa[OPEN_CB], xb[OPEN_CB];
+    };
+    auto load_block = [&](uint32_t cb, Blk &d) {
+        const int nc = (int)(c_end - cb < (uint32_t)OPEN_CB ? c_end - cb : OPEN_CB);
+#pragma unroll
+        for (int k = 0; k < OPEN_CB; k++) {
+            const uint64_t y = cols[cb + (k < nc ? k : 0)];
+            const u32x4 qa = *(g4)(y + 4 * (j0 + ra)), qb = *(g4)(y + 4 * (j0 + rb));
+            d.a[k] = make_uint4(qa.x, qa.y, qa.z, qa.w);
+            d.b[k] = make_uint4(qb.x, qb.y, qb.z, qb.w);
+            // every lane, unconditionally: a predicated load would leave the wait counts path-dependent
+            // (the compiler then waits for the prefetch too); the neighbours' copies hit the cache
+            d.xa[k] = *(g1)(y + 4 * ((j0 + ra + 4) & (n - 1)));
+            d.xb[k] = *(g1)(y + 4 * ((j0 + rb + 4) & (n - 1)));
+        }
+    };
+    auto process = [&](uint32_t cb0, const Blk &c) {
+        const int nc = (int)(c_end - cb0 < (uint32_t)OPEN_CB ? c_end - cb0 : OPEN_CB);
+#pragma unroll
+        for (int k = 0; k < OPEN_CB; k++) {
+            const uint4 va = c.a[k], vb = c.b[k];
+            const uint32_t v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+            uint64_t a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+#pragma unroll
+                for (int m = 0; m < 4; m++) a0[e] = pair_acc(a0[e], v[m], w[m].c[e], v[m + 4], w[m + 4].c[e]);
+            if (with_next) {  // the next row wraps to row 0 at the end of the column
+                const uint32_t u[8] = {va.y, va.z, va.w, c.xa[k], vb.y, vb.z, vb.w, c.xb[k]};
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+#pragma unroll
+                    for (int m = 0; m < 4; m++) a1[e] = pair_acc(a1[e], u[m], w[m].c[e], u[m + 4], w[m + 4].c[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                red[k * 8 + e][t] = acc_mod(a0[e]);
+                red[k * 8 + 4 + e][t] = with_next ? acc_mod(a1[e]) : 0u;
+            }
+        }
+        __syncthreads();
+        {
+            const uint32_t o = t >> 3, q = t & 7;  // output word o (column o / 8), partial sums q, q + 8, ...
+            uint64_t acc = 0;
+#pragma unroll
+            for (int i = 0; i < NT / 8; i++) acc += red[o][q + 8 * i];  // < 32 P
+            uint32_t r = acc_mod(acc);
+            r = add(r, __shfl_xor(r, 1, 64));
+            r = add(r, __shfl_xor(r, 2, 64));
+            r = add(r, __shfl_xor(r, 4, 64));
+            if (q == 0 && (int)(o >> 3) < nc) partial[((uint64_t)(cb0 + (o >> 3)) * nseg + bx) * 8 + (o & 7)] = r;
+        }
+        __syncthreads();  // red is reused by the next column block
+    };
+    Blk b0, b1;
+    if (c_begin < c_end) load_block(c_begin, b0);
+    for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += 2 * OPEN_CB) {
+        const uint32_t cb1 = cb0 + OPEN_CB;
+        if (cb1 < c_end) load_block(cb1, b1);
+        process(cb0, b0);
+        if (cb1 >= c_end) break;
+        if (cb1 + OPEN_CB < c_end) load_block(cb1 + OPEN_CB, b0);
+        process(cb1, b1);
+    }
+}
+__global__ __launch_bounds__(NT) void k_open_dot_pf(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
+                                                      OpenWeights pw, int with_next, int nseg, uint32_t slab,
+                                                      uint32_t *partial) {
+    open_dot_pf(cols, ncols, n, pw, with_next, nseg, slab, partial, blockIdx.x, blockIdx.y);
+}
 
 // out[col * 8 + e] = sum over the nseg segments of partial[(col * nseg + seg) * 8 + e]: one wave per
 // (column, e) pair group, lanes striding over the segments
-__global__ __launch_bounds__(64) void k_open_sum(const uint32_t *__restrict__ partial, uint32_t ncols, int nseg,
-                                                 uint32_t *out) {
-    const uint32_t col = blockIdx.x;
+__device__ __forceinline__ void open_sum(const uint32_t *__restrict__ partial, int nseg, uint32_t *out, uint32_t col) {
     const int lane = threadIdx.x;
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // < nseg P < 2^44
     for (int sg = lane; sg < nseg; sg += 64) {
@@ -621,26 +762,94 @@ __global__ __launch_bounds__(64) void k_open_sum(const uint32_t *__restrict__ pa
     }
     if (lane < 8) out[(uint64_t)col * 8 + lane] = r[lane];
 }
+__global__ __launch_bounds__(64) void k_open_sum(const uint32_t *__restrict__ partial, uint32_t ncols, int nseg,
+                                                 uint32_t *out) {
+    open_sum(partial, nseg, out, blockIdx.x);
+}
+
+// Every group of an opening in one grid per kernel kind (blockIdx.z = group; a group's workgroups beyond its
+// own segments / slabs, or of another kind, return at once): one launch instead of one per (height,
+// domain, points) group, so the small groups (short chips, quotient chunks) run beside each other
+template <int KIND>
+__global__ __launch_bounds__(NT) void k_open_dot_groups(const OpenGroup *__restrict__ gs) {
+    const OpenGroup g = gs[blockIdx.z];
+    if (g.kind != KIND || blockIdx.x >= (uint32_t)g.nseg || blockIdx.y >= g.nslab) return;
+    if constexpr (KIND == 0)
+        open_dot_lds(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
+    else if constexpr (KIND == 1)
+        open_dot_regs(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
+    else
+        open_dot_pf(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
+}
+__global__ __launch_bounds__(64) void k_open_sum_groups(const OpenGroup *__restrict__ gs) {
+    const OpenGroup g = gs[blockIdx.z];
+    if (blockIdx.x >= g.ncols) return;
+    open_sum(g.partial, g.nseg, g.out, blockIdx.x);
+}
+
+// grid shape and kernel kind of one group: row segments of OPEN_SEG, and for small matrices the columns split
+// into slabs too, so a launch still has ~1024+ workgroups
+static void open_group_shape(OpenGroup &g) {
+    g.nseg = (int)((g.n + OPEN_SEG - 1) / OPEN_SEG);
+    const uint32_t blocks_c = (g.ncols + OPEN_CB - 1) / OPEN_CB;
+    uint32_t nslab = (uint32_t)std::min<uint64_t>(blocks_c, std::max<uint64_t>(1, 1024 / (uint64_t)g.nseg));
+    g.slab = ((blocks_c + nslab - 1) / nslab) * OPEN_CB;
+    g.nslab = (g.ncols + g.slab - 1) / g.slab;
+    static const bool lds_weights = getenv("ZKM_OPEN_LDS_WEIGHTS") && atoi(getenv("ZKM_OPEN_LDS_WEIGHTS"));
+    static const bool prefetch = !getenv("ZKM_OPEN_PREFETCH") || atoi(getenv("ZKM_OPEN_PREFETCH"));
+    g.kind = (g.n % OPEN_SEG == 0 && !lds_weights) ? (prefetch ? 2 : 1) : 0;
+}
 
 void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const OpenWeights &w, bool with_next,
                      uint32_t *out, hipStream_t s) {
     if (!ncols) return;
-    const int nseg = (int)((n + OPEN_SEG - 1) / OPEN_SEG);
-    // small matrices: split the columns into slabs too, so a launch still has ~1024+ workgroups
-    const uint32_t blocks_c = (ncols + OPEN_CB - 1) / OPEN_CB;
-    uint32_t nslab = (uint32_t)std::min<uint64_t>(blocks_c, std::max<uint64_t>(1, 1024 / (uint64_t)nseg));
-    const uint32_t slab = ((blocks_c + nslab - 1) / nslab) * OPEN_CB;
-    nslab = (ncols + slab - 1) / slab;
-    DBuf part((size_t)ncols * nseg * 8, s);
-    static const bool lds_weights = getenv("ZKM_OPEN_LDS_WEIGHTS") && atoi(getenv("ZKM_OPEN_LDS_WEIGHTS"));
-    if (n % OPEN_SEG == 0 && !lds_weights)
-        hipLaunchKernelGGL(k_open_dot_regs, dim3(nseg, nslab), dim3(NT), 0, s, d_cols, ncols, n, w, (int)with_next, nseg,
-                           slab, part.p);
+    OpenGroup g{d_cols, n, w, ncols, 0, 0, 0, (int)with_next, 0, nullptr, out};
+    open_group_shape(g);
+    DBuf part((size_t)ncols * g.nseg * 8, s);
+    const dim3 grid(g.nseg, g.nslab);
+    if (g.kind == 2)
+        hipLaunchKernelGGL(k_open_dot_pf, grid, dim3(NT), 0, s, d_cols, ncols, n, w, g.with_next, g.nseg, g.slab, part.p);
+    else if (g.kind == 1)
+        hipLaunchKernelGGL(k_open_dot_regs, grid, dim3(NT), 0, s, d_cols, ncols, n, w, g.with_next, g.nseg, g.slab, part.p);
     else
-        hipLaunchKernelGGL(k_open_dot, dim3(nseg, nslab), dim3(NT), 0, s, d_cols, ncols, n, w, (int)with_next, nseg,
-                           slab, part.p);
+        hipLaunchKernelGGL(k_open_dot, grid, dim3(NT), 0, s, d_cols, ncols, n, w, g.with_next, g.nseg, g.slab, part.p);
     HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(k_open_sum, dim3(ncols), dim3(64), 0, s, part.p, ncols, nseg, out);
+    hipLaunchKernelGGL(k_open_sum, dim3(ncols), dim3(64), 0, s, part.p, ncols, g.nseg, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s) {
+    std::vector<OpenGroup> live;
+    for (const OpenGroup &g : gs)
+        if (g.ncols) live.push_back(g);
+    gs.swap(live);
+    if (gs.empty()) return;
+    size_t tot = 0;
+    uint32_t gx = 1, gy = 1, maxc = 1;
+    bool kinds[3] = {false, false, false};
+    for (OpenGroup &g : gs) {
+        open_group_shape(g);
+        tot += (size_t)g.ncols * g.nseg * 8;
+        gx = std::max<uint32_t>(gx, (uint32_t)g.nseg);
+        gy = std::max(gy, g.nslab);
+        maxc = std::max(maxc, g.ncols);
+        kinds[g.kind] = true;
+    }
+    ARG_CHECK(gs.size() <= 65535, "too many opening groups");
+    DBuf part(tot, s), dg((gs.size() * sizeof(OpenGroup) + 3) / 4, s);
+    size_t off = 0;
+    for (OpenGroup &g : gs) {
+        g.partial = part.p + off;
+        off += (size_t)g.ncols * g.nseg * 8;
+    }
+    HIP_CHECK(hipMemcpyAsync(dg.p, gs.data(), gs.size() * sizeof(OpenGroup), hipMemcpyHostToDevice, s));
+    const OpenGroup *d = reinterpret_cast<const OpenGroup *>(dg.p);
+    const dim3 grid(gx, gy, (unsigned)gs.size());
+    if (kinds[0]) hipLaunchKernelGGL(k_open_dot_groups<0>, grid, dim3(NT), 0, s, d);
+    if (kinds[1]) hipLaunchKernelGGL(k_open_dot_groups<1>, grid, dim3(NT), 0, s, d);
+    if (kinds[2]) hipLaunchKernelGGL(k_open_dot_groups<2>, grid, dim3(NT), 0, s, d);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_open_sum_groups, dim3(maxc, 1, (unsigned)gs.size()), dim3(64), 0, s, d);
     HIP_CHECK(hipGetLastError());
 }
 

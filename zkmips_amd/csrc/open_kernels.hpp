@@ -1,5 +1,6 @@
 // Kernel argument blocks and launchers of open_kernels.hip.
 #pragma once
+#include <vector>
 #include "internal.hpp"
 
 namespace zkm {
@@ -55,6 +56,20 @@ struct OpenWeights {
 // out[col * 8 .. +8] = the (local, next-row) dot products of column col with the weights w (EF)
 void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const OpenWeights &w, bool with_next,
                      uint32_t *out, hipStream_t s);
+// One opening group: the columns of one (height, evaluation domain, point set), whose weights are shared.
+// The caller fills cols (device column pointer table), n, w, ncols, with_next and out; the launcher sets
+// the grid shape, kernel kind and partial-sum buffer.
+struct OpenGroup {
+    const uint64_t *cols;
+    uint64_t n;
+    OpenWeights w;
+    uint32_t ncols, slab, nslab;
+    int nseg, with_next, kind;
+    uint32_t *partial, *out;
+};
+// Every group's dot products in one launch per kernel kind (+ one segment-sum launch); `gs` is uploaded
+// asynchronously from host memory, so it must outlive the stream's execution of these launches.
+void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s);
 
 struct ReduceArgs {
     const uint64_t *cols;      // column pointer table

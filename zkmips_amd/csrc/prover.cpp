@@ -590,15 +590,23 @@ static std::vector<uint8_t> open_shard(Ctx &c, const Pk &pk, MainData &md, Chall
             for (uint64_t k = 0; k < q.W; k++) cols[q.coff + k] = (uint64_t)(uintptr_t)(q.ybase + k * q.N);
         DBuf dcols(2 * cols.size(), s), part(nparts + 1, s);
         HIP_CHECK(hipMemcpyAsync(dcols.p, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s));
+        // every group in one launch per kernel kind (blockIdx.z = group): the short chips' and the quotient
+        // chunks' groups run beside each other instead of as a chain of latency-bound launches
+        std::vector<OpenGroup> ogs;
+        double open_bytes = 0;
         for (auto &g : groups) {
             const Pend &q = pend[g.first];
             // barycentric weights w^j / (zeta' - w^j): traces in natural row order (shift 1 after the
             // zeta / shift substitution), quotient chunks bit-reversed; generated by the kernel itself
             const OpenWeights w{q.bitrev ? ef_mul_base(zeta, inv(q.shift)) : zeta, ONE, c.tw_fwd, ilog2(q.N),
                                 q.bitrev ? 1 : 0, 1};
-            PROF("open_eval", s, 4.0 * q.N * g.W);
-            launch_open_dot((const uint64_t *)dcols.p + g.coff, (uint32_t)g.W, q.N, w, q.r->npts == 2,
-                            part.p + g.poff, s);
+            ogs.push_back(OpenGroup{(const uint64_t *)dcols.p + g.coff, q.N, w, (uint32_t)g.W, 0, 0, 0,
+                                    q.r->npts == 2 ? 1 : 0, 0, nullptr, part.p + g.poff});
+            open_bytes += 4.0 * q.N * g.W;
+        }
+        {
+            PROF("open_eval", s, open_bytes);
+            launch_open_dot_groups(ogs, s);  // ogs lives to the synchronisation below
         }
         std::vector<uint32_t> hp(nparts + 1);
         HIP_CHECK(hipMemcpyAsync(hp.data(), part.p, nparts * 4, hipMemcpyDeviceToHost, s));
