@@ -327,17 +327,21 @@ def cpu_threads() -> int:
 
 def calibrate_cpu_threads(log_n=18, queries=84):
     """How many OpenMP threads the oracle actually profits from on this box: one 2^log_n FibCpu proof at
-    each candidate count up to every CPU of the affinity mask, fastest wins.  (A box may show 256 CPUs
-    while the job's share is far smaller: there 128 threads ran a 2^22 proof 9x slower than 16.)"""
+    each candidate count up to the CPUs the job is allotted (the affinity mask, capped by the cgroup's CFS
+    quota), fastest wins.  (The GPU box shows 256 CPUs with a 16-CPU quota: there 128 threads ran a proof
+    ~100x slower than 16, spin-waiting against the throttle; profiles/r05_cpu_cliff.txt.)"""
     from tests import _oracle as O
     from zkmips_amd import workloads as W
     cpus = len(os.sched_getaffinity(0))
     quota = cgroup_cpu_limit()
     allot = {int(quota)} if quota and quota >= 1 else set()
+    # counts up to the CPUs the job may use: the affinity mask, capped by the CFS quota when there is one (above
+    # the quota the spinning OpenMP barriers are throttled, profiles/r05_cpu_cliff.txt)
+    cap = min(cpus, int(quota)) if allot else cpus
     m, prep, traces, pvs = W.fib_shard(1 << log_n, seed=2)
     pr = O.OracleProver(m, prep, num_queries=queries)
     table = {}
-    for c in sorted({c for c in {8, 16, 24, 32, 48, 64, 128, cpus} | allot if c <= cpus}):
+    for c in sorted({c for c in {8, 16, 24, 32, 48, 64, 128, cpus} | allot if c <= cap}):
         _omp(c)
         t = time.time()
         rc, _ = pr.prove(traces, pvs)
