@@ -15,7 +15,7 @@ for i in 1 2; do
 import json
 d = json.loads(open('$O/r05j_bench_$pf.json').read().strip().splitlines()[-1])
 st = d['stages_ms_per_shard']
-print('prefetch $pf', 'open_eval', st['open_eval']['ms_per_shard'], 'open_total', st['open_total']['ms_per_shard'], 'resident', d['resident']['ms_per_shard'])
+print('prefetch $pf', 'open_eval', st['open_eval']['ms_per_shard'], 'fri_reduce', st['fri_reduce']['ms_per_shard'], 'open_total', st['open_total']['ms_per_shard'], 'resident', d['resident']['ms_per_shard'])
 " | tee -a $O/r05j_ab.txt
   done
 done

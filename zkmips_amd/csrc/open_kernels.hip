@@ -609,6 +609,14 @@ __global__ __launch_bounds__(NT) void k_open_dot_regs(const uint64_t *__restrict
 }
 static_assert(OPEN_CB * 8 * 8 == NT, "one reduction thread group per output word");
 
+// 32-bit representative of a lazy dot-product sum v < 2^34 (four pair_acc terms, each < 2P): v mod 2^31 plus
+// (v >> 31)(2^24 - 1), since 2^31 = 2^24 - 1 mod p; < 2^31 + 2^27.  Congruent, not canonical: three VALU
+// operations instead of acc_mod's reduction and product, the block sum is reduced once
+__device__ __forceinline__ uint32_t fold_acc(uint64_t v) {
+    const uint32_t hi = (uint32_t)(v >> 31), lo = (uint32_t)v & 0x7fffffffu;
+    return lo + (hi << 24) - hi;
+}
+
 // k_open_dot_regs with the next column block's loads issued before the current block's products (two
 // register sets used alternately): 152 VGPRs, 3 waves per SIMD
 __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
@@ -707,8 +715,9 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
             }
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                red[k * 8 + e][t] = acc_mod(a0[e]);
-                red[k * 8 + 4 + e][t] = with_next ? acc_mod(a1[e]) : 0u;
+                // a 32-bit representative, not the canonical value: the sum over the block is reduced once
+                red[k * 8 + e][t] = fold_acc(a0[e]);
+                red[k * 8 + 4 + e][t] = with_next ? fold_acc(a1[e]) : 0u;
             }
         }
         __syncthreads();
@@ -716,7 +725,7 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
             const uint32_t o = t >> 3, q = t & 7;  // output word o (column o / 8), partial sums q, q + 8, ...
             uint64_t acc = 0;
 #pragma unroll
-            for (int i = 0; i < NT / 8; i++) acc += red[o][q + 8 * i];  // < 32 P
+            for (int i = 0; i < NT / 8; i++) acc += red[o][q + 8 * i];  // < 32 * 2^32
             uint32_t r = acc_mod(acc);
             r = add(r, __shfl_xor(r, 1, 64));
             r = add(r, __shfl_xor(r, 2, 64));
@@ -904,7 +913,20 @@ __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
     for (int k = 0; k < RED_ROWS; k++) {
         const uint64_t i = i0 + k * T;
         const bool in = i < a.h;
-        const uint32_t x = in ? mul(a.gen, root_pow(a.tw, a.h, rev_bits((uint32_t)i, a.log_h))) : 0u;
+        // x = gen w_h^rev(i).  The wave's 64 rows share i >> 6, so rev(i) = rev6(i & 63) 2^(L-6) + rev_{L-6}(i >> 6):
+        // w_h^rev(i) = w_64^rev6(lane) (a 64-entry table) times a factor uniform over the wave, instead of 64
+        // scattered loads from the 2^L-entry table (one cache line per lane)
+        uint32_t x = 0u;
+        if (in) {
+            if (a.log_h >= 6) {
+                const uint32_t lo = (uint32_t)i & 63u, hi = (uint32_t)(i >> 6);
+                const uint32_t wl = root_pow(a.tw, 64, rev_bits(lo, 6));
+                const uint32_t wh = root_pow(a.tw, a.h, a.log_h > 6 ? rev_bits(hi, a.log_h - 6) : 0u);
+                x = mul(a.gen, mul(wh, wl));
+            } else {
+                x = mul(a.gen, root_pow(a.tw, a.h, rev_bits((uint32_t)i, a.log_h)));
+            }
+        }
         den[2 * k] = in ? ef_sub(a.z0, ef_base(x)) : ef_one();
         den[2 * k + 1] = in && a.has1 ? ef_sub(a.z1, ef_base(x)) : ef_one();
 #pragma unroll
