@@ -289,20 +289,20 @@ def host_info():
             "omp_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cgroup_cpu_limit():
+def cgroup_cpu_limit(proc_cgroup="/proc/self/cgroup", mount="/sys/fs/cgroup"):
     """The cgroup v2 CPU quota of this process in CPUs, or None if unlimited: the tightest cpu.max ("quota
     period") on the path from the process's cgroup up to the mount root.  On the GPU box the process's own
     cgroup has no cpu.max and the quota (1600000 100000 = 16 CPUs) sits on /sys/fs/cgroup itself
     (profiles/r05_cpu_cliff.txt), so reading only the leaf misses it."""
     try:
-        cg = open("/proc/self/cgroup").read().strip().split("\n")[0].split(":", 2)[2]
+        cg = open(proc_cgroup).read().strip().split("\n")[0].split(":", 2)[2]
     except (OSError, IndexError):
         cg = "/"
     best = None
     path = cg.rstrip("/")
     while True:
         try:
-            q, p = open(f"/sys/fs/cgroup{path}/cpu.max").read().split()
+            q, p = open(f"{mount}{path}/cpu.max").read().split()
             if q != "max":
                 c = int(q) / int(p)
                 best = c if best is None else min(best, c)

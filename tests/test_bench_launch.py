@@ -95,3 +95,22 @@ def test_bench_two_ranks_on_one_gpu():
                                                   "--no-pmc", "--no-maxshape", "--profile-steps", "1"])
     assert r.returncode == 0, r.stderr[-2000:]
     assert line["n_gpus"] == 2 and line["value"] > 0
+
+
+def test_cgroup_cpu_limit_walks_up_to_the_root(tmp_path):
+    """bench.cgroup_cpu_limit: the tightest cpu.max from the process's cgroup up to the mount root (the GPU box
+    keeps its 16-CPU quota on the root cgroup, the process's own cgroup has no cpu.max)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    mount = tmp_path / "cg"
+    leaf = mount / "a" / "b"
+    leaf.mkdir(parents=True)
+    proc = tmp_path / "cgroup"
+    proc.write_text("0::/a/b\n")
+    assert bench.cgroup_cpu_limit(str(proc), str(mount)) is None  # no cpu.max anywhere
+    (mount / "cpu.max").write_text("1600000 100000\n")
+    assert bench.cgroup_cpu_limit(str(proc), str(mount)) == 16.0  # root only (the box)
+    (mount / "a" / "cpu.max").write_text("max 100000\n")
+    assert bench.cgroup_cpu_limit(str(proc), str(mount)) == 16.0  # "max" does not lift the root's quota
+    (leaf / "cpu.max").write_text("400000 100000\n")
+    assert bench.cgroup_cpu_limit(str(proc), str(mount)) == 4.0  # the tightest wins
