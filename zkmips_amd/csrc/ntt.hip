@@ -785,8 +785,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void *p, uint32_t b
 __device__ __forceinline__ uint32_t bld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
 }
+// cache-policy bits of the strided passes' stores (A/B builds: -DZKM_NTT_STORE_AUX=2 marks them non-temporal)
+#ifndef ZKM_NTT_STORE_AUX
+#define ZKM_NTT_STORE_AUX 0
+#endif
 __device__ __forceinline__ void bst(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, ZKM_NTT_STORE_AUX);
 }
 template <bool SWZ>
 __device__ __forceinline__ uint32_t atb(uint32_t r, uint32_t t) {
