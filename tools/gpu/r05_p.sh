@@ -29,3 +29,11 @@ st = d['stages_ms_per_shard']
 print('${L:+nt}', 'resident', d['resident']['ms_per_shard'], 'value', round(d['value']), {k: st[k]['ms_per_shard'] for k in ('lde', 'merkle_leaves', 'quotient')})
 "
 done
+# the maximal shape's serial stage table (its own line)
+timeout -k 10 600 python3 bench.py --workload maxshape --steps 3 --no-cpu-baseline --no-pmc > $O/r05p_maxshape.json 2> $O/r05p_maxshape.err || { tail -20 $O/r05p_maxshape.err; exit 1; }
+python3 -c "
+import json
+d = json.loads(open('$O/r05p_maxshape.json').read().strip().splitlines()[-1])
+st = d['stages_ms_per_shard']
+print('maxshape', d['value'], d.get('ms_per_shard'), d.get('serial_ms_per_shard'), {k: v['ms_per_shard'] for k, v in st.items()})
+"

@@ -785,9 +785,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void *p, uint32_t b
 __device__ __forceinline__ uint32_t bld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
 }
-// cache-policy bits of the strided passes' stores (A/B builds: -DZKM_NTT_STORE_AUX=2 marks them non-temporal)
+// cache-policy bits of the strided passes' stores: non-temporal (nt).  Their output is the LDE (read much later, by
+// the leaf hashing) or the inverse pass's intermediate (2^22 x 16 x 4 B per batch, larger than the Infinity Cache
+// with the fused pass's own traffic): LDE 2^22 x 64 3.66-3.67 vs 3.71-3.72 ms with the default policy
+// (profiles/r05_ntt_nt_store_ab.txt); -DZKM_NTT_STORE_AUX=0 restores it
 #ifndef ZKM_NTT_STORE_AUX
-#define ZKM_NTT_STORE_AUX 0
+#define ZKM_NTT_STORE_AUX 2
 #endif
 __device__ __forceinline__ void bst(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, ZKM_NTT_STORE_AUX);
