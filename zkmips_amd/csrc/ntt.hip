@@ -605,10 +605,13 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
     }
     dit13x2(v0, v1, x, t, tt_fwd);
     uint32_t *dp = dst + md.off(blockIdx.y) + base;
+    // non-temporal, like the strided passes' stores (LDE 2^22 x 64 3.653-3.667 -> 3.634-3.645 ms,
+    // profiles/r05_ntt_nt_store_ab.txt)
 #pragma unroll
-    for (int j = 0; j < 16; j++) dp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)] = v0[j];
+    for (int j = 0; j < 16; j++) __builtin_nontemporal_store(v0[j], &dp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)]);
 #pragma unroll
-    for (int j = 0; j < 16; j++) dp[dst_half + (TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j))] = v1[j];
+    for (int j = 0; j < 16; j++)
+        __builtin_nontemporal_store(v1[j], &dp[dst_half + (TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j))]);
 }
 
 // ------------------------------------------------------------------ 512-row strided register tiles
