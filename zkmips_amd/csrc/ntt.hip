@@ -1486,8 +1486,22 @@ static void run_fused(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, C
     HIP_CHECK(hipGetLastError());
 }
 
-// strided pass radices for the bits above the contiguous tile (top to bottom, i.e. DIF order)
+// strided pass radices for the bits above the contiguous tile (top to bottom, i.e. DIF order).
+// 2^20: one 9-stage buffer-addressed pass (k_ntt_s9b) and an 11-stage contiguous tile instead of the 13-stage tile
+// and a 7-stage k_ntt_strided pass -- 1.155 -> 1.095 ms for 2^20 x 67; every other height measured slower that way
+// (profiles/r05_lde_plan_ab.txt).  ZKM_LDE_PLAN=0: the balanced plan everywhere; =1: 9-stage first for every L
+// in [14, 23] but 22 (A/B)
 static std::vector<int> strided_plan(int L, int &logC) {
+    static const int plan = [] {
+        const char *e = getenv("ZKM_LDE_PLAN");
+        return e ? atoi(e) : -1;
+    }();
+    if ((plan == 1 && L >= 14 && L != 22) || (plan < 0 && L == 20)) {  // (the 9-stage pass needs L - 9 >= 5)
+        logC = L - 9 < LOGC ? L - 9 : LOGC;
+        std::vector<int> p{9};
+        if (L - 9 - logC > 0) p.push_back(L - 9 - logC);
+        return p;
+    }
     logC = L < LOGC ? L : LOGC;
     int rem = L - logC;
     std::vector<int> p;
