@@ -775,6 +775,174 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9(const uint32_t *src, uint
     }
 }
 
+// LOGR = 6..8 strided stages as register tiles of R = 2^LOGR rows x 32 columns, 2R threads x two 8-element
+// networks: the k_ntt_s9 design for the passes of the 2^19 and 2^21 LDEs (13-stage tile + 6 / 8) and of the
+// recursion shards' heights.  The LDS-staged k_ntt_strided these replace ran at about half the bytes per second
+// of the 9-stage kernels (2^21 x 67 LDE 2.55 -> 2.01 ms, profiles/r05_lde_s8_ab.txt).  Layouts (u = tid >> 5,
+// network n in {0,1}, g = 2u + n < R/8, element k < 8), three stages per layout except where noted:
+//   LOGR 8: LH row g + 32k (h_r 32..128) | LM row (g>>2)*32 + (g&3) + 4k (4..16) | LL row 8g + k (1, 2)
+//   LOGR 7: LH row g + 16k (16..64)      | LM row (g>>1)*16 + (g&1) + 2k (2..8)  | LL row 8g + k (1)
+//   LOGR 6: LH row g + 8k (8..32)        |                                        | LL row 8g + k (1..4)
+namespace sr {
+enum { LH = 0, LM = 1, LL = 2 };
+template <int LOGR>
+__device__ __forceinline__ uint32_t at(uint32_t r, uint32_t t) {
+    // columns XOR-swizzled by row bits LOGR-5..LOGR-1: a half-wave's 32 lanes touch one row (any swizzle is
+    // conflict-free), and the bit-reversed output walk's rows base + 2^(LOGR-5) m (m < 32) land on 32 banks
+    return r * 32 + (t ^ ((r >> (LOGR - 5)) & 31));
+}
+template <int LOGR, int LAY> constexpr uint32_t RS = LAY == LH ? (1u << (LOGR - 3)) : LAY == LL ? 1u : (LOGR == 8 ? 4u : 2u);
+template <int LOGR, int LAY> constexpr int NST = LAY != LL ? 3 : LOGR == 8 ? 2 : LOGR == 7 ? 1 : 3;  // 8 = 3+3+2, 7 = 3+3+1, 6 = 3+3
+template <int LOGR, int LAY>
+__device__ __forceinline__ uint32_t row0(uint32_t u, int n) {
+    const uint32_t g = 2 * u + n;
+    if constexpr (LAY == LH) return g;
+    else if constexpr (LAY == LM) return LOGR == 8 ? (g >> 2) * 32 + (g & 3) : (g >> 1) * 16 + (g & 1);
+    else return 8 * g;
+}
+
+// NST stages of one 8-element network (as s9::net8; fewer stages: independent groups of 2^NST elements)
+template <int LOGR, bool DIT, int LAY>
+__device__ __forceinline__ void net8(uint32_t *v, uint32_t off, uint32_t S, uint32_t ct,
+                                     const uint32_t *__restrict__ tw) {
+    constexpr uint32_t rs = RS<LOGR, LAY>;
+    constexpr int ns = NST<LOGR, LAY>;
+#pragma unroll
+    for (int q = 0; q < ns; q++) {
+        const int st = DIT ? q : ns - 1 - q;
+        const int span = 1 << st;
+        const uint32_t h = (rs << st) * S;
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+            const uint32_t w = tw[h + (off + rs * m) * S + ct];
+#pragma unroll
+            for (int k = m; k < 8; k += 2 * span) {
+                const uint32_t a = v[k], b = v[k + span];
+                if (DIT) {
+                    const uint32_t tt = mul(b, w);
+                    if (q < ns - 1 && ((k >> (st + 1)) & 1)) {  // next stage multiplies both: lazy [0, 2P)
+                        v[k] = a + tt;
+                        v[k + span] = a + (P - tt);
+                    } else {
+                        v[k] = add(a, tt);
+                        v[k + span] = sub(a, tt);
+                    }
+                } else {
+                    v[k] = add(a, b);
+                    v[k + span] = mul(a + (P - b), w);
+                }
+            }
+        }
+    }
+}
+template <int LOGR, bool DIT, int LAY>
+__device__ __forceinline__ void nets(uint32_t v[16], uint32_t u, uint32_t S, uint32_t ct,
+                                     const uint32_t *__restrict__ tw) {
+#pragma unroll
+    for (int n = 0; n < 2; n++) net8<LOGR, DIT, LAY>(v + 8 * n, row0<LOGR, LAY>(u, n) % RS<LOGR, LAY>, S, ct, tw);
+}
+template <int LOGR, int LAY>
+__device__ __forceinline__ void to_lds(uint32_t *x, const uint32_t v[16], uint32_t u, uint32_t t) {
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[at<LOGR>(row0<LOGR, LAY>(u, n) + RS<LOGR, LAY> * k, t)] = v[8 * n + k];
+}
+template <int LOGR, int LAY>
+__device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint32_t u, uint32_t t) {
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[8 * n + k] = x[at<LOGR>(row0<LOGR, LAY>(u, n) + RS<LOGR, LAY> * k, t)];
+}
+}  // namespace sr
+
+template <int LOGR, bool DIT, int MODE>
+__global__ __launch_bounds__(2 << LOGR) void k_ntt_sr(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+                                                       int logS, const uint32_t *__restrict__ tw, Twist tws,
+                                                       uint64_t dst_half) {
+    using namespace sr;
+    constexpr uint32_t R = 1u << LOGR, NTH = 2 * R;
+    constexpr bool MID = LOGR > 6;  // a middle layout (two LDS exchanges) or only LH and LL (one)
+    __shared__ uint32_t x[R * 32];
+    const uint32_t S = 1u << logS;
+    const uint32_t groups = S >> 5;
+    const uint32_t outer = blockIdx.x / groups;
+    const uint32_t c0 = (blockIdx.x % groups) * 32;
+    const uint32_t base = outer * R * S;
+    const uint32_t t = threadIdx.x & 31, u = threadIdx.x >> 5;
+    const uint32_t ct = c0 + t;
+    const uint32_t *sp = src + ms.off(blockIdx.y) + base + ct;
+    uint32_t *dp = dst + md.off(blockIdx.y);
+    constexpr uint32_t HS = RS<LOGR, LH>;  // LH row stride
+    uint32_t v[16];
+    if (DIT) {
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[8 * n + k] = sp[(row0<LOGR, LL>(u, n) + k) * S];
+        nets<LOGR, true, LL>(v, u, S, ct, tw);
+        to_lds<LOGR, LL>(x, v, u, t);
+        __syncthreads();
+        if constexpr (MID) {
+            from_lds<LOGR, LM>(x, v, u, t);
+            nets<LOGR, true, LM>(v, u, S, ct, tw);
+            __syncthreads();
+            to_lds<LOGR, LM>(x, v, u, t);
+            __syncthreads();
+        }
+        from_lds<LOGR, LH>(x, v, u, t);
+        nets<LOGR, true, LH>(v, u, S, ct, tw);
+        if (MODE == MODE_PLAIN) {
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) dp[base + (row0<LOGR, LH>(u, n) + HS * k) * S + ct] = v[8 * n + k];
+        } else if (MODE == MODE_TWIST_OUT) {
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t i = base + (row0<LOGR, LH>(u, n) + HS * k) * S + ct;
+                    dp[i] = mul(v[8 * n + k], tws.f(0, i));
+                    dp[dst_half + i] = mul(v[8 * n + k], tws.f(1, i));
+                }
+        } else {  // BITREV_OUT: natural n = r S + c -> row rev_L(n) = rev_logS(c) * R + rev_LOGR(r)
+            __syncthreads();
+            to_lds<LOGR, LH>(x, v, u, t);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t idx = (uint32_t)i * NTH + threadIdx.x;
+                const uint32_t tc = idx >> LOGR, q = idx & (R - 1);
+                __builtin_nontemporal_store(x[at<LOGR>(rev_bits(q, LOGR), tc)],
+                                            &dp[(uint64_t)rev_bits(c0 + tc, logS) * R + q]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[8 * n + k] = sp[(row0<LOGR, LH>(u, n) + HS * k) * S];
+        nets<LOGR, false, LH>(v, u, S, ct, tw);
+        to_lds<LOGR, LH>(x, v, u, t);
+        __syncthreads();
+        if constexpr (MID) {
+            from_lds<LOGR, LM>(x, v, u, t);
+            nets<LOGR, false, LM>(v, u, S, ct, tw);
+            __syncthreads();
+            to_lds<LOGR, LM>(x, v, u, t);
+            __syncthreads();
+        }
+        from_lds<LOGR, LL>(x, v, u, t);
+        nets<LOGR, false, LL>(v, u, S, ct, tw);
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) dp[base + (row0<LOGR, LL>(u, n) + k) * S + ct] = v[8 * n + k];
+    }
+}
+
 // Same tiles and networks as k_ntt_s9, addressed through buffer descriptors: every global access
 // (data, twiddles, stores) is one per-thread 32-bit voffset fixed for the kernel plus a
 // wave-uniform soffset (k S words, twiddle stage bases) computed on the scalar unit, so the
@@ -1330,7 +1498,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9p(const uint32_t *src, uin
 static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
 static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
 
-static int strided_T(int logR) { return logR >= 9 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
+static int strided_T(int logR) { return logR >= 6 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
 
 // k_ntt_s9b with its twiddles generated in registers (default) or loaded per butterfly group
 // (ZKM_NTT_TWLOAD=1, the round-4 form: A/B knob)
@@ -1437,6 +1605,29 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
         HIP_CHECK(hipGetLastError());
         return;
     }
+    if (logR >= 6 && logR <= 8) {  // register tiles of 2^logR rows x 32 columns (k_ntt_sr)
+        static const bool generic = getenv("ZKM_NTT_GENERIC8") && atoi(getenv("ZKM_NTT_GENERIC8"));  // A/B knob
+        if (!generic) {
+#define SRL(LR)                                                                                                   \
+    if (!DIT)                                                                                                     \
+        hipLaunchKernelGGL((k_ntt_sr<LR, false, MODE_PLAIN>), g, dim3(2 << LR), 0, s, src, dst, ms, md, logS, tw, tws, \
+                           dst_half);                                                                             \
+    else if (mode == MODE_PLAIN)                                                                                  \
+        hipLaunchKernelGGL((k_ntt_sr<LR, true, MODE_PLAIN>), g, dim3(2 << LR), 0, s, src, dst, ms, md, logS, tw, tws,  \
+                           dst_half);                                                                             \
+    else if (mode == MODE_TWIST_OUT)                                                                              \
+        hipLaunchKernelGGL((k_ntt_sr<LR, true, MODE_TWIST_OUT>), g, dim3(2 << LR), 0, s, src, dst, ms, md, logS, tw,   \
+                           tws, dst_half);                                                                        \
+    else                                                                                                          \
+        hipLaunchKernelGGL((k_ntt_sr<LR, true, MODE_BITREV_OUT>), g, dim3(2 << LR), 0, s, src, dst, ms, md, logS, tw,  \
+                           tws, dst_half);
+            if (logR == 8) { SRL(8) } else if (logR == 7) { SRL(7) } else { SRL(6) }
+#undef SRL
+            HIP_CHECK(hipGetLastError());
+            return;
+        }
+        g.x = (unsigned)(((1ull << L) >> logR) / 64);  // the generic kernel's 64-column tiles
+    }
 #define SCASE(k, t)                                                                                             \
     case k:                                                                                                     \
         hipLaunchKernelGGL((k_ntt_strided<k, t, DIT, NT>), g, dim3(NT), 0, s, src, dst, ms, md, logS, tw, mode, tws, \
@@ -1486,17 +1677,16 @@ static void run_fused(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, C
     HIP_CHECK(hipGetLastError());
 }
 
-// strided pass radices for the bits above the contiguous tile (top to bottom, i.e. DIF order).
-// 2^20: one 9-stage buffer-addressed pass (k_ntt_s9b) and an 11-stage contiguous tile instead of the 13-stage tile
-// and a 7-stage k_ntt_strided pass -- 1.155 -> 1.095 ms for 2^20 x 67; every other height measured slower that way
-// (profiles/r05_lde_plan_ab.txt).  ZKM_LDE_PLAN=0: the balanced plan everywhere; =1: 9-stage first for every L
-// in [14, 23] but 22 (A/B)
+// strided pass radices for the bits above the contiguous tile (top to bottom, i.e. DIF order): the 13-stage tile and
+// the rest in passes of at most 9 stages.  ZKM_LDE_PLAN=1 (A/B): a 9-stage pass first and the tile taking the rest
+// -- faster only at 2^20 while that height's 7-stage pass was the LDS-staged kernel; with the register-tiled
+// k_ntt_sr the balanced plan wins there too (profiles/r05_lde_plan_ab.txt, r05_lde_s8_ab.txt)
 static std::vector<int> strided_plan(int L, int &logC) {
     static const int plan = [] {
         const char *e = getenv("ZKM_LDE_PLAN");
-        return e ? atoi(e) : -1;
+        return e ? atoi(e) : 0;
     }();
-    if ((plan == 1 && L >= 14 && L != 22) || (plan < 0 && L == 20)) {  // (the 9-stage pass needs L - 9 >= 5)
+    if (plan == 1 && L >= 14 && L != 22) {  // (the 9-stage pass needs L - 9 >= 5)
         logC = L - 9 < LOGC ? L - 9 : LOGC;
         std::vector<int> p{9};
         if (L - 9 - logC > 0) p.push_back(L - 9 - logC);
