@@ -484,20 +484,38 @@ __device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint
     for (int j = 0; j < 16; j++) v[j] = x[sw13(lay_idx<SE>(t, j))];
 }
 
+// Exchange ordering between the layouts.  L512 spreads a wave's elements over the whole tile, but L32
+// and L2 of wave w both hold exactly tile elements [1024 w, 1024 w + 1024) (a wave is threads 64 w ..
+// 64 w + 63: L32 rows t >> 5 in {2w, 2w + 1}, L2 groups t >> 1 in [32 w, 32 w + 32)), so the L32 <-> L2
+// exchanges only touch the wave's own LDS words: a DS instruction stream of one wave executes in
+// order, and the compiler only has to keep the accesses in program order -- no workgroup barrier.
+// WL = false keeps the barriers (A/B, ZKM_T13_BARRIERS=1).
+template <bool WL>
+__device__ __forceinline__ void own_sync() {
+    if constexpr (WL) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 // DIF over all 13 stages: v in L512 (natural) -> v in L2 (bit-reversed within the tile)
+template <bool WL = false>
 __device__ __forceinline__ void dif13(uint32_t v[16], uint32_t *x, uint32_t t, const uint32_t *__restrict__ tw) {
     net16<false, 512>(v, lay_off<512>(t), tw);
     to_lds<512>(x, v, t);
     __syncthreads();
     from_lds<32>(x, v, t);
     net16<false, 32>(v, lay_off<32>(t), tw);
-    __syncthreads();
+    own_sync<WL>();
     to_lds<32>(x, v, t);
-    __syncthreads();
+    own_sync<WL>();
     from_lds<2>(x, v, t);
     net16<false, 2>(v, lay_off<2>(t), tw);
     stage_h1(v, t & 1);
-    __syncthreads();  // LDS free for the next user
+    own_sync<WL>();  // LDS free for the next user (WL: its next writes are this wave's own L2 / L32 words)
 }
 
 }  // namespace t13
@@ -545,6 +563,7 @@ __device__ __forceinline__ void net16x2(uint32_t v0[16], uint32_t v1[16], uint32
     }
 }
 
+template <bool WL>
 __device__ __forceinline__ void dit13x2(uint32_t v0[16], uint32_t v1[16], uint32_t *x, uint32_t t,
                                         const uint32_t *__restrict__ tw) {
     uint32_t *x1 = x + LDS13;
@@ -553,11 +572,11 @@ __device__ __forceinline__ void dit13x2(uint32_t v0[16], uint32_t v1[16], uint32
     net16x2<true, 2>(v0, v1, lay_off<2>(t), tw);
     to_lds<2>(x, v0, t);
     to_lds<2>(x1, v1, t);
-    __syncthreads();
+    own_sync<WL>();
     from_lds<32>(x, v0, t);
     from_lds<32>(x1, v1, t);
     net16x2<true, 32>(v0, v1, lay_off<32>(t), tw);
-    __syncthreads();
+    own_sync<WL>();
     to_lds<32>(x, v0, t);
     to_lds<32>(x1, v1, t);
     __syncthreads();
@@ -574,7 +593,7 @@ __device__ __forceinline__ uint32_t tiled13(uint32_t b, uint32_t t, uint32_t j) 
     return ((t >> 5) + 16 * j) * 16384u + b * 32u + (t & 31);
 }
 
-template <bool TILED>
+template <bool TILED, bool WL>
 __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src, uint32_t *dst, ColMap ms,
                                                             ColMap md, int L, const uint32_t *__restrict__ tt_inv,
                                                             const uint32_t *__restrict__ tt_fwd, Twist tws,
@@ -587,7 +606,7 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
     uint32_t v0[16], v1[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) v0[j] = sp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)];
-    dif13(v0, x, t, tt_inv);
+    dif13<WL>(v0, x, t, tt_inv);
     {
         const uint32_t g0 = tws.g0[blockIdx.x], g1 = tws.g1[blockIdx.x];
         const uint4 *u0 = (const uint4 *)(tws.u0 + t * 16), *u1 = (const uint4 *)(tws.u1 + t * 16);
@@ -603,7 +622,7 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
             }
         }
     }
-    dit13x2(v0, v1, x, t, tt_fwd);
+    dit13x2<WL>(v0, v1, x, t, tt_fwd);
     uint32_t *dp = dst + md.off(blockIdx.y) + base;
     // non-temporal, like the strided passes' stores (LDE 2^22 x 64 3.653-3.667 -> 3.634-3.645 ms,
     // profiles/r05_ntt_nt_store_ab.txt)
@@ -1892,12 +1911,14 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
             const Twist tws = get_twist(c, N, L, shifts[e], s);
             uint32_t *out = dst_d + (uint64_t)c0 * dst_stride + e * half_off;
             if (logC == 13) {
-                if (tiled)
-                    hipLaunchKernelGGL(k_lde_fused13<true>, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf,
-                                       work.p, m_i, m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
-                else
-                    hipLaunchKernelGGL(k_lde_fused13<false>, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf,
-                                       work.p, m_i, m_w1, L, c.tt_inv, c.tt_fwd, tws, N);
+                static const bool barriers = [] {
+                    const char *e = getenv("ZKM_T13_BARRIERS");
+                    return e && atoi(e) != 0;
+                }();
+                auto k = tiled ? (barriers ? k_lde_fused13<true, false> : k_lde_fused13<true, true>)
+                               : (barriers ? k_lde_fused13<false, false> : k_lde_fused13<false, true>);
+                hipLaunchKernelGGL(k, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf, work.p, m_i, m_w1, L,
+                                   c.tt_inv, c.tt_fwd, tws, N);
                 HIP_CHECK(hipGetLastError());
             } else {
                 run_fused(logC, ibuf, work.p, m_i, m_w1, nb, L, c.tw_inv, c.tw_fwd, tws, N, 0, s);
