@@ -1390,97 +1390,138 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9c(const uint32_t *src, uin
     }
 }
 
-// Persistent form of k_ntt_s9b: each workgroup walks the (tile, column) work items w = blockIdx.x,
-// blockIdx.x + gridDim.x, ... (gridDim.x a multiple of 8, so item w stays on XCD w mod 8 as in k_ntt_s9b's
-// remap), and issues the next item's 16 loads into a second register set before the current item's
-// butterflies, LDS exchanges and stores: the loads are in flight while the block computes, instead of the
-// block alternating between waiting on HBM and issuing VALU.  Barriers wait on LDS only (the prefetched
-// loads are not drained at them).
+// Persistent prefetching form of k_ntt_s9b (same tiles, TILE sides, register-generated twiddles; opt-in
+// ZKM_NTT_PF = workgroups per CU): each workgroup walks the work items lin = blockIdx.x, + gridDim.x, ...
+// (gridDim.x a multiple of 8, so every item stays on XCD lin mod 8 under k_ntt_s9b's remap) and keeps the NEXT
+// item's 16 loads in flight while it computes the current one.  vmcnt retires in issue order, so the item's
+// twiddle loads go out before the prefetch (a scheduling barrier keeps them there) and the barriers fence LDS
+// only ("local"), so the prefetch is not drained at them; 57-61 VGPRs, no spills, two workgroups per CU.  The
+// waits in the ISA are the intended ones, and still the LDE runs 2-3 % slower with PF=2 and 12 % with PF=1
+// (profiles/r05_ntt_prefetch_ab.txt): like round 3's k_ntt_s9p (which drained its prefetch at every wait), the
+// one-item-per-workgroup kernel with two resident workgroups already keeps HBM as busy as this layout allows.
 namespace s9 {
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt left at their maxima
+__device__ __forceinline__ void lds_bar() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
-}  // namespace s9
 
-template <bool DIT, int MODE>
-__global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9p(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
-                                                        int logS, const uint32_t *__restrict__ tw,
-                                                        uint32_t tw_words, uint32_t nv, uint32_t total) {
-    using namespace s9;
-    constexpr bool SWZ = DIT && MODE == MODE_BITREV_OUT;
-    __shared__ uint32_t x[512 * 32];
-    const uint32_t S = 1u << logS, S4 = S * 4;
-    const uint32_t ntile = total / nv;
-    const uint32_t t = threadIdx.x & 31, u = threadIdx.x >> 5;
-    const auto rtw = mkrs(tw, tw_words * 4);
-    // the work item's (column, tile) from its linear index, k_ntt_s9b's XCD-aware remap
-    auto item = [&](uint32_t lin, uint32_t &col, uint32_t &tile) {
-        const uint32_t vid = (lin & 7) * (total >> 3) + (lin >> 3);
-        col = vid % nv;
-        tile = vid / nv;
-        (void)ntile;
-    };
-    auto load = [&](uint32_t lin, uint32_t *v) {
-        uint32_t col, tile;
-        item(lin, col, tile);
-        const uint32_t outer = tile >> (logS - 5), c0 = (tile & ((S >> 5) - 1)) * 32, base = outer * 512u * S;
-        const auto rsrc = mkrs(src + ms.off(col) + base, 512u * S4);
-        const uint32_t ct = c0 + t;
-        if (DIT) {
-            const uint32_t vL16 = (16 * u * S + ct) * 4;
+// a * b with b wave-uniform, read from an SGPR (the "v" operands of prod64 would pin a VGPR copy of every such
+// constant for the whole kernel -- six of them in k_ntt_s9q, which runs at the 64-VGPR limit)
+__device__ __forceinline__ uint32_t mul_s(uint32_t a, uint32_t b) {
+    uint64_t p, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(cc) : "v"(a), "s"(b));
+    return redc(p);
+}
+__device__ __forceinline__ Tw8 tw8s(uint32_t wtop, const TwC &c) {
+    Tw8 r;
+    r.w[2][0] = wtop;
+    r.w[1][0] = mul(wtop, wtop);
+    r.w[0][0] = mul(r.w[1][0], r.w[1][0]);
+    r.w[1][1] = mul_s(r.w[1][0], c.w4);
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = bld(rsrc, vL16, (uint32_t)k * S4);
+    for (int m = 1; m < 4; m++) r.w[2][m] = mul_s(wtop, c.w8[m - 1]);
+    return r;
+}
+
+template <bool DIT, int MODE, int TILE>
+struct S9Q {
+    static constexpr bool SWZ = DIT && MODE == MODE_BITREV_OUT;
+    static constexpr bool TS = TILE & 1, TD = (TILE & 2) != 0;
+    const uint32_t *src;
+    uint32_t *dst;
+    ColMap ms, md;
+    int logS;
+    uint32_t S, S4, nv, total, t, u;
+    __amdgpu_buffer_rsrc_t rtw;
+    TwC twk;
+    uint32_t w64, w16;
+
+    struct Item {
+        uint32_t col, c0, base, ct;
+        uint64_t tbase;
+    };
+    __device__ __forceinline__ Item item(uint32_t lin, uint32_t t) const {
+        const uint32_t vid = (lin & 7) * (total >> 3) + (lin >> 3);
+        Item it;
+        it.col = vid % nv;
+        const uint32_t tile = vid / nv;
+        it.c0 = (tile & ((S >> 5) - 1)) * 32;
+        it.base = (tile >> (logS - 5)) * 512u * S;
+        it.ct = it.c0 + t;
+        it.tbase = (uint64_t)(it.c0 >> 5) * (512u * 32u);
+        return it;
+    }
+    // live = false (past the last item): 16 loads of one cached word, so that every step has the same loads in
+    // flight and the waits can count them (a conditional prefetch makes the waits assume the worst path)
+    __device__ __forceinline__ void load(uint32_t lin, uint32_t (&v)[16], bool live = true) const {
+        const Item it = item(lin, t);
+        const auto rsrc = TS ? mkrs(src + ms.off(it.col) + it.tbase, 512u * 128u)
+                             : mkrs(src + ms.off(it.col) + it.base, 512u * S4);
+        const uint32_t sP4 = !live ? 0u : TS ? 128u : S4;
+        if (DIT) {
+            const uint32_t sL16 = TS ? (16 * u * 32 + t) * 4 : (16 * u * S + it.ct) * 4;
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = bld(rsrc, sL16, (uint32_t)k * sP4);
         } else {
-            const uint32_t vLH = (u * S + ct) * 4;
+            const uint32_t sLH = TS ? (u * 32 + t) * 4 : (u * S + it.ct) * 4;
 #pragma unroll
             for (int n = 0; n < 2; n++)
 #pragma unroll
-                for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, vLH, (uint32_t)(32 * n + 64 * k) * S4);
+                for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, sLH, (uint32_t)(32 * n + 64 * k) * sP4);
         }
-    };
-    uint32_t v[16], vn[16];
-    uint32_t lin = blockIdx.x;
-    if (lin < total) load(lin, v);
-    for (; lin < total; lin += gridDim.x) {
-        const uint32_t nxt = lin + gridDim.x;
-        if (nxt < total) load(nxt, vn);
-        uint32_t col, tile;
-        item(lin, col, tile);
-        const uint32_t outer = tile >> (logS - 5), c0 = (tile & ((S >> 5) - 1)) * 32, base = outer * 512u * S;
-        const uint32_t ct = c0 + t;
+    }
+    // one work item on v, with the next item's loads into vn in flight
+    __device__ __forceinline__ void step(uint32_t *x, uint32_t lin, uint32_t (&v)[16], uint32_t (&vn)[16]) const {
+        // per-item copies of the lane coordinates, opaque to the compiler: the LDS and global addresses derived from
+        // them are recomputed in every item instead of being hoisted out of the item loop into ~16 live registers
+        uint32_t t = this->t, u = this->u;
+        asm volatile("" : "+v"(t), "+v"(u));
+        const Item it = item(lin, t);
+        const uint32_t ct = it.ct;
         const uint32_t vLL = ct * 4;
-        const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4, vLM1 = (((2 * u + 1) & 7) * S + ct) * 4;
+        const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4;
         const uint32_t vLH = (u * S + ct) * 4;
-        const uint32_t vL16 = (16 * u * S + ct) * 4;
-        lds_barrier();  // the previous item's last LDS reads are done
+        // the top twiddles (net8x's TWG form) before the prefetch; each layout's second network is one row
+        // offset further (LM: +1 row of h = 32 S, LH: +32 rows of h = 256 S), i.e. its top twiddle is the first's
+        // times w_64 = tw[33] or w_16 = tw[9]
+        const uint32_t wLL = bld(rtw, vLL, 4 * S4), wLM0 = bld(rtw, vLM0, 32 * S4), wLH0 = bld(rtw, vLH, 256 * S4);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t nxt = lin + gridDim.x;
+        load(nxt < total ? nxt : lin, vn, nxt < total);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t wLM1 = mul_s(wLM0, w64), wLH1 = mul_s(wLH0, w16);
+        lds_bar();  // the previous item's last LDS reads are done
         if (DIT) {
-            net8b<true, LL>(v, rtw, vLL, 0, S4);
-            net8b<true, LL>(v + 8, rtw, vLL, 0, S4);
+            const Tw8 W = tw8s(wLL, twk);
+            net8r<true>(v, W);
+            net8r<true>(v + 8, W);
             to_ldsb<LL, false>(x, v, u, t);
-            lds_barrier();
+            lds_bar();
             from_ldsb<LM, false>(x, v, u, t);
-            net8b<true, LM>(v, rtw, vLM0, 0, S4);
-            net8b<true, LM>(v + 8, rtw, vLM1, 0, S4);
-            lds_barrier();
+            net8r<true>(v, tw8s(wLM0, twk));
+            net8r<true>(v + 8, tw8s(wLM1, twk));
+            lds_bar();
             to_ldsb<LM, false>(x, v, u, t);
-            lds_barrier();
+            lds_bar();
             from_ldsb<LH, false>(x, v, u, t);
-            net8b<true, LH>(v, rtw, vLH, 0, S4);
-            net8b<true, LH>(v + 8, rtw, vLH, 32 * S4, S4);
+            net8r<true>(v, tw8s(wLH0, twk));
+            net8r<true>(v + 8, tw8s(wLH1, twk));
             if (MODE == MODE_PLAIN) {
-                const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
+                const auto rdst = TD ? mkrs(dst + md.off(it.col) + it.tbase, 512u * 128u)
+                                     : mkrs(dst + md.off(it.col) + it.base, 512u * S4);
+                const uint32_t dP4 = TD ? 128u : S4, dLH = TD ? (u * 32 + t) * 4 : vLH;
 #pragma unroll
                 for (int n = 0; n < 2; n++)
 #pragma unroll
-                    for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, vLH, (uint32_t)(32 * n + 64 * k) * S4);
+                    for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, dLH, (uint32_t)(32 * n + 64 * k) * dP4);
             } else {  // BITREV_OUT (as k_ntt_s9b)
-                lds_barrier();
+                lds_bar();
                 to_ldsb<LH, SWZ>(x, v, u, t);
-                lds_barrier();
-                const auto rdst = mkrs(dst + md.off(col), 512u * S4);
-                const uint32_t q = threadIdx.x & 511, hb = threadIdx.x >> 9, rq = rev_bits(q, 9);
-                const uint32_t vo = (((rev_bits(c0, logS) + (hb << (logS - 1))) << 9) + q) * 4;
+                lds_bar();
+                const auto rdst = mkrs(dst + md.off(it.col), 512u * S4);
+                const uint32_t q = (u << 5 | t) & 511, hb = u >> 4, rq = rev_bits(q, 9);
+                const uint32_t vo = (((rev_bits(it.c0, logS) + (hb << (logS - 1))) << 9) + q) * 4;
 #pragma unroll
                 for (int i = 0; i < 16; i++) {
                     const uint32_t tc = 2 * i + hb;
@@ -1489,27 +1530,50 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9p(const uint32_t *src, uin
                 }
             }
         } else {
-            net8b<false, LH>(v, rtw, vLH, 0, S4);
-            net8b<false, LH>(v + 8, rtw, vLH, 32 * S4, S4);
+            net8r<false>(v, tw8s(wLH0, twk));
+            net8r<false>(v + 8, tw8s(wLH1, twk));
             to_ldsb<LH, false>(x, v, u, t);
-            lds_barrier();
+            lds_bar();
             from_ldsb<LM, false>(x, v, u, t);
-            net8b<false, LM>(v, rtw, vLM0, 0, S4);
-            net8b<false, LM>(v + 8, rtw, vLM1, 0, S4);
-            lds_barrier();
+            net8r<false>(v, tw8s(wLM0, twk));
+            net8r<false>(v + 8, tw8s(wLM1, twk));
+            lds_bar();
             to_ldsb<LM, false>(x, v, u, t);
-            lds_barrier();
+            lds_bar();
             from_ldsb<LL, false>(x, v, u, t);
-            net8b<false, LL>(v, rtw, vLL, 0, S4);
-            net8b<false, LL>(v + 8, rtw, vLL, 0, S4);
-            const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
+            const Tw8 W = tw8s(wLL, twk);
+            net8r<false>(v, W);
+            net8r<false>(v + 8, W);
+            const auto rdst = TD ? mkrs(dst + md.off(it.col) + it.tbase, 512u * 128u)
+                                 : mkrs(dst + md.off(it.col) + it.base, 512u * S4);
+            const uint32_t dP4 = TD ? 128u : S4, dL16 = TD ? (16 * u * 32 + t) * 4 : (16 * u * S + ct) * 4;
 #pragma unroll
             for (int n = 0; n < 2; n++)
 #pragma unroll
-                for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, vL16, (uint32_t)(8 * n + k) * S4);
+                for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, dL16, (uint32_t)(8 * n + k) * dP4);
         }
+    }
+};
+}  // namespace s9
+
+template <bool DIT, int MODE, int TILE, int MINW>
+__global__ __launch_bounds__(s9::NTH, MINW) void k_ntt_s9q(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+                                                        int logS, const uint32_t *__restrict__ tw, uint32_t tw_words,
+                                                        uint32_t nv, uint32_t total) {
+    using namespace s9;
+    __shared__ uint32_t x[512 * 32];
+    S9Q<DIT, MODE, TILE> q{src, dst, ms, md, logS, 1u << logS, 4u << logS, nv, total, threadIdx.x & 31u,
+                           threadIdx.x >> 5, mkrs(tw, tw_words * 4), twc(tw), tw[33], tw[9]};
+    uint32_t va[16], vb[16];
+    uint32_t lin = blockIdx.x;  // gridDim.x <= total: every workgroup has an item
+    q.load(lin, va);
+    // (the copy waits on the prefetch just where the next item needs it; an unrolled ping-pong of va / vb, tried
+    // first, doubled the code and spilled more at the 64-VGPR limit)
+#pragma unroll 1
+    for (; lin < total; lin += gridDim.x) {
+        q.step(x, lin, va, vb);
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = vn[k];
+        for (int k = 0; k < 16; k++) va[k] = vb[k];
     }
 }
 
@@ -1525,6 +1589,23 @@ template <bool DIT, int MODE, int TL>
 static void launch_s9b(dim3 g1, hipStream_t s, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, int logS,
                        const uint32_t *tw, uint32_t tw_words, uint32_t nv, int remap) {
     static const bool twload = getenv("ZKM_NTT_TWLOAD") != nullptr;
+    // persistent prefetching form (A/B): ZKM_NTT_PF = workgroups per CU (0: one item per workgroup)
+    static const int pf = [] {
+        const char *e = getenv("ZKM_NTT_PF");
+        return e ? atoi(e) : 0;
+    }();
+    const uint32_t total = g1.x;
+    if (pf > 0 && !twload && remap && (total & 7) == 0) {
+        const uint32_t grid = std::min<uint32_t>(total, 256u * (uint32_t)pf) & ~7u;
+        // two workgroups per CU: 8 waves per SIMD, at most 64 VGPRs; one: 128
+        if (pf >= 2)
+            hipLaunchKernelGGL((k_ntt_s9q<DIT, MODE, TL, 8>), dim3(grid), dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
+                               tw, tw_words, nv, total);
+        else
+            hipLaunchKernelGGL((k_ntt_s9q<DIT, MODE, TL, 4>), dim3(grid), dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
+                               tw, tw_words, nv, total);
+        return;
+    }
     if (twload)
         hipLaunchKernelGGL((k_ntt_s9b<DIT, MODE, TL, false>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
                            tw_words, nv, remap);
@@ -1559,28 +1640,6 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     if (logR == 9 && tw_words && mode != MODE_TWIST_OUT) {  // buffer-addressed register tiles
         const dim3 g1(g.x * nv);  // one dimension: (tile, column) remapped in the kernel
         static const int remap = getenv("ZKM_NTT_NOREMAP") ? 0 : 1;  // A/B knob
-        // persistent prefetching form: ZKM_NTT_PERSIST = workgroups per CU (0 = the one-item-per-workgroup kernel)
-        static const int persist = [] {
-            const char *e = getenv("ZKM_NTT_PERSIST");
-            return e ? atoi(e) : 0;
-        }();
-        const uint32_t total = g1.x;
-        if (persist > 0 && remap && (total & 7) == 0) {
-            uint32_t grid = 256u * (uint32_t)persist;
-            if (grid > total) grid = total & ~7u;
-            const dim3 gp(grid);
-            if (!DIT)
-                hipLaunchKernelGGL((k_ntt_s9p<false, MODE_PLAIN>), gp, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                                   tw_words, nv, total);
-            else if (mode == MODE_PLAIN)
-                hipLaunchKernelGGL((k_ntt_s9p<true, MODE_PLAIN>), gp, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                                   tw_words, nv, total);
-            else
-                hipLaunchKernelGGL((k_ntt_s9p<true, MODE_BITREV_OUT>), gp, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
-                                   tw, tw_words, nv, total);
-            HIP_CHECK(hipGetLastError());
-            return;
-        }
         // two-column tiles (8-byte accesses): ZKM_NTT_S9C=0 selects the one-column k_ntt_s9b (A/B knob)
         static const int s9c = [] {
             const char *e = getenv("ZKM_NTT_S9C");
