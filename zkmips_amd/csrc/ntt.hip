@@ -802,6 +802,8 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9(const uint32_t *src, uint
 //   LOGR 8: LH row g + 32k (h_r 32..128) | LM row (g>>2)*32 + (g&3) + 4k (4..16) | LL row 8g + k (1, 2)
 //   LOGR 7: LH row g + 16k (16..64)      | LM row (g>>1)*16 + (g&1) + 2k (2..8)  | LL row 8g + k (1)
 //   LOGR 6: LH row g + 8k (8..32)        |                                        | LL row 8g + k (1..4)
+//   LOGR 5: LH row g + 4k (4..16)        |                                        | LL row 8g + k (1, 2)
+// (LOGR 5 is one wave per workgroup: the 2^18 LDE's pass and both of the 2^23 LDE's; 2^18 -9 %, profiles/r05_lde_s5_ab.txt)
 namespace sr {
 enum { LH = 0, LM = 1, LL = 2 };
 template <int LOGR>
@@ -811,7 +813,8 @@ __device__ __forceinline__ uint32_t at(uint32_t r, uint32_t t) {
     return r * 32 + (t ^ ((r >> (LOGR - 5)) & 31));
 }
 template <int LOGR, int LAY> constexpr uint32_t RS = LAY == LH ? (1u << (LOGR - 3)) : LAY == LL ? 1u : (LOGR == 8 ? 4u : 2u);
-template <int LOGR, int LAY> constexpr int NST = LAY != LL ? 3 : LOGR == 8 ? 2 : LOGR == 7 ? 1 : 3;  // 8 = 3+3+2, 7 = 3+3+1, 6 = 3+3
+template <int LOGR, int LAY>
+constexpr int NST = LAY != LL ? 3 : LOGR == 8 ? 2 : LOGR == 7 ? 1 : LOGR == 5 ? 2 : 3;  // 8 = 3+3+2, 7 = 3+3+1, 6 = 3+3, 5 = 3+2
 template <int LOGR, int LAY>
 __device__ __forceinline__ uint32_t row0(uint32_t u, int n) {
     const uint32_t g = 2 * u + n;
@@ -1581,7 +1584,7 @@ __global__ __launch_bounds__(s9::NTH, MINW) void k_ntt_s9q(const uint32_t *src, 
 static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
 static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
 
-static int strided_T(int logR) { return logR >= 6 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
+static int strided_T(int logR) { return logR >= 5 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
 
 // k_ntt_s9b with its twiddles generated in registers (default) or loaded per butterfly group
 // (ZKM_NTT_TWLOAD=1, the round-4 form: A/B knob)
@@ -1683,7 +1686,7 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
         HIP_CHECK(hipGetLastError());
         return;
     }
-    if (logR >= 6 && logR <= 8) {  // register tiles of 2^logR rows x 32 columns (k_ntt_sr)
+    if (logR >= 5 && logR <= 8) {  // register tiles of 2^logR rows x 32 columns (k_ntt_sr)
         static const bool generic = getenv("ZKM_NTT_GENERIC8") && atoi(getenv("ZKM_NTT_GENERIC8"));  // A/B knob
         if (!generic) {
 #define SRL(LR)                                                                                                   \
@@ -1699,11 +1702,12 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     else                                                                                                          \
         hipLaunchKernelGGL((k_ntt_sr<LR, true, MODE_BITREV_OUT>), g, dim3(2 << LR), 0, s, src, dst, ms, md, logS, tw,  \
                            tws, dst_half);
-            if (logR == 8) { SRL(8) } else if (logR == 7) { SRL(7) } else { SRL(6) }
+            if (logR == 8) { SRL(8) } else if (logR == 7) { SRL(7) } else if (logR == 6) { SRL(6) } else { SRL(5) }
 #undef SRL
             HIP_CHECK(hipGetLastError());
             return;
         }
+        ARG_CHECK((1 << logS) >= 64, "strided pass narrower than its tile");
         g.x = (unsigned)(((1ull << L) >> logR) / 64);  // the generic kernel's 64-column tiles
     }
 #define SCASE(k, t)                                                                                             \
