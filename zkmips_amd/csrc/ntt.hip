@@ -626,11 +626,16 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
     uint32_t *dp = dst + md.off(blockIdx.y) + base;
     // non-temporal, like the strided passes' stores (LDE 2^22 x 64 3.653-3.667 -> 3.634-3.645 ms,
     // profiles/r05_ntt_nt_store_ab.txt)
+#if ZKM_LDE_MID_AUX
+#define ZKM_ST13(v, p) __builtin_nontemporal_store(v, p)
+#else
+#define ZKM_ST13(v, p) (*(p) = (v))
+#endif
 #pragma unroll
-    for (int j = 0; j < 16; j++) __builtin_nontemporal_store(v0[j], &dp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)]);
+    for (int j = 0; j < 16; j++) ZKM_ST13(v0[j], &dp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)]);
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-        __builtin_nontemporal_store(v1[j], &dp[dst_half + (TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j))]);
+    for (int j = 0; j < 16; j++) ZKM_ST13(v1[j], &dp[dst_half + (TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j))]);
+#undef ZKM_ST13
 }
 
 // ------------------------------------------------------------------ 512-row strided register tiles
@@ -988,6 +993,16 @@ __device__ __forceinline__ uint32_t bld(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 __device__ __forceinline__ void bst(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, ZKM_NTT_STORE_AUX);
 }
+// the LDE's intermediate stores (strided MODE_PLAIN passes and the fused tile's output, read again by the next
+// pass) keep the default policy, so that 8-column batches of a 2^22 trace find part of them in the Infinity
+// Cache: 2^22 x 64 LDE 3.49 -> 3.43 ms, shard resident 26.46 -> 26.04 ms (profiles/r05_lde_mall_ab.txt);
+// -DZKM_LDE_MID_AUX=2 makes them non-temporal like the final passes' stores
+#ifndef ZKM_LDE_MID_AUX
+#define ZKM_LDE_MID_AUX 0
+#endif
+__device__ __forceinline__ void bst_mid(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, ZKM_LDE_MID_AUX);
+}
 template <bool SWZ>
 __device__ __forceinline__ uint32_t atb(uint32_t r, uint32_t t) {
     if constexpr (SWZ) return r * 32 + (t ^ ((r >> 4) & 31));
@@ -1172,7 +1187,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
 #pragma unroll
             for (int n = 0; n < 2; n++)
 #pragma unroll
-                for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, dLH, (uint32_t)(32 * n + 64 * k) * dP4);
+                for (int k = 0; k < 8; k++) bst_mid(v[8 * n + k], rdst, dLH, (uint32_t)(32 * n + 64 * k) * dP4);
         } else {  // BITREV_OUT: natural n = r S + c -> row rev_L(n) = rev_logS(c) * 512 + rev_9(r)
             __syncthreads();
             to_ldsb<LH, SWZ>(x, v, u, t);
@@ -1215,7 +1230,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
 #pragma unroll
         for (int n = 0; n < 2; n++)
 #pragma unroll
-            for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, dL16, (uint32_t)(8 * n + k) * dP4);
+            for (int k = 0; k < 8; k++) bst_mid(v[8 * n + k], rdst, dL16, (uint32_t)(8 * n + k) * dP4);
     }
 }
 
@@ -1897,9 +1912,11 @@ void lde_batch_bitrev_in_strided(Ctx &c, const DMat &src, uint32_t shift, uint32
     run_contig<false>(logC, dst.d, dst.d, m_dst2, m_dst2, 2 * nv, L, c.tw_fwd, MODE_PLAIN, Twist{}, 0, s);
 }
 
-// Columns per pass batch of the natural-input LDE: at least 16 (measured 4.62 ms vs 4.67 ms for all
-// 67 columns of a 2^22 trace at once), and up to a 256 MB work buffer for short traces (compress
-// shapes, 2^14..2^18 rows: fewer launches; profiles/r03_lde_cb_ab.txt); ZKM_LDE_CB overrides (0 = all).
+// Columns per pass batch of the natural-input LDE: 16 (measured 4.62 ms vs 4.67 ms for all 67 columns of a
+// 2^22 trace at once), 8 at 2^22 rows (with default-policy intermediate stores part of a batch's
+// intermediates stay in the Infinity Cache: 2^22 x 64 3.49 -> 3.43 ms against 16, 3.47 at 4, 3.75 at 2;
+// profiles/r05_lde_mall_ab.txt), and up to a 256 MB work buffer for short traces (compress shapes,
+// 2^14..2^18 rows: fewer launches; profiles/r03_lde_cb_ab.txt); ZKM_LDE_CB overrides (0 = all).
 static uint32_t lde_col_batch(uint64_t N, uint32_t nv) {
     static const long env = [] {
         const char *e = getenv("ZKM_LDE_CB");
@@ -1907,7 +1924,7 @@ static uint32_t lde_col_batch(uint64_t N, uint32_t nv) {
     }();
     uint64_t cb;
     if (env >= 0) cb = env ? (uint64_t)env : nv;
-    else cb = std::max<uint64_t>(16, (1ull << 25) / N);
+    else cb = N == (1ull << 22) ? 8 : std::max<uint64_t>(16, (1ull << 25) / N);
     return (uint32_t)std::min<uint64_t>(cb, nv);
 }
 
