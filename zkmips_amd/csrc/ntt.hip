@@ -263,6 +263,14 @@ __device__ __forceinline__ void tile_stages(uint32_t *x, const uint32_t *__restr
     }
 }
 
+// the LDE's intermediate stores (strided MODE_PLAIN passes and the fused tile's output, read again by the next
+// pass) keep the default policy, so that 8-column batches of a 2^22 trace find part of them in the Infinity
+// Cache: 2^22 x 64 LDE 3.49 -> 3.43 ms, shard resident 26.46 -> 26.04 ms (profiles/r05_lde_mall_ab.txt);
+// -DZKM_LDE_MID_AUX=2 makes them non-temporal like the final passes' stores
+#ifndef ZKM_LDE_MID_AUX
+#define ZKM_LDE_MID_AUX 0
+#endif
+
 struct ColMap {
     // virtual column v -> offset (v / nsub) * col_stride + (v % nsub) * sub_stride
     uint64_t col_stride, sub_stride;
@@ -624,7 +632,7 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
     }
     dit13x2<WL>(v0, v1, x, t, tt_fwd);
     uint32_t *dp = dst + md.off(blockIdx.y) + base;
-    // non-temporal, like the strided passes' stores (LDE 2^22 x 64 3.653-3.667 -> 3.634-3.645 ms,
+    // an intermediate: default policy (ZKM_LDE_MID_AUX above; non-temporal measured -0.6 % with 16-column batches,
     // profiles/r05_ntt_nt_store_ab.txt)
 #if ZKM_LDE_MID_AUX
 #define ZKM_ST13(v, p) __builtin_nontemporal_store(v, p)
@@ -983,23 +991,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void *p, uint32_t b
 __device__ __forceinline__ uint32_t bld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
 }
-// cache-policy bits of the strided passes' stores: non-temporal (nt).  Their output is the LDE (read much later, by
-// the leaf hashing) or the inverse pass's intermediate (2^22 x 16 x 4 B per batch, larger than the Infinity Cache
-// with the fused pass's own traffic): LDE 2^22 x 64 3.66-3.67 vs 3.71-3.72 ms with the default policy
-// (profiles/r05_ntt_nt_store_ab.txt); -DZKM_NTT_STORE_AUX=0 restores it
+// cache-policy bits of the strided passes' final stores: non-temporal (nt).  Their output is the LDE, read much
+// later by the leaf hashing: LDE 2^22 x 64 3.66-3.67 vs 3.71-3.72 ms with the default policy when every pass stored
+// nt (profiles/r05_ntt_nt_store_ab.txt); -DZKM_NTT_STORE_AUX=0 restores it.  Intermediate stores: bst_mid.
 #ifndef ZKM_NTT_STORE_AUX
 #define ZKM_NTT_STORE_AUX 2
 #endif
 __device__ __forceinline__ void bst(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, ZKM_NTT_STORE_AUX);
 }
-// the LDE's intermediate stores (strided MODE_PLAIN passes and the fused tile's output, read again by the next
-// pass) keep the default policy, so that 8-column batches of a 2^22 trace find part of them in the Infinity
-// Cache: 2^22 x 64 LDE 3.49 -> 3.43 ms, shard resident 26.46 -> 26.04 ms (profiles/r05_lde_mall_ab.txt);
-// -DZKM_LDE_MID_AUX=2 makes them non-temporal like the final passes' stores
-#ifndef ZKM_LDE_MID_AUX
-#define ZKM_LDE_MID_AUX 0
-#endif
 __device__ __forceinline__ void bst_mid(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, ZKM_LDE_MID_AUX);
 }
