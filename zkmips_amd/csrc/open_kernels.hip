@@ -868,9 +868,13 @@ void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s) {
 // (pt, A(4), B(4)) x npts] (words).  One launch per height writes ro outright (no accumulate).  A thread
 // takes RED_ROWS rows i + k T (T = the grid's threads: every load instruction stays one coalesced row
 // range) and inverts their 2 RED_ROWS denominators together (Montgomery's trick, one EF inversion),
-// so no table of inverses crosses HBM.  One row per thread: 50 VGPRs, 8 waves per SIMD; four rows took
+// so no table of inverses crosses HBM.  One row per thread: ~50 VGPRs, 8 waves per SIMD; four rows took
 // 177 VGPRs and ran 2.2x slower (the kernel is bound by the loads in flight, not the inversions).
 static constexpr int RED_ROWS = 1;
+// LB column loads in flight per thread: 4 (ZKM_RED_LOADS = 1 / 2 / 8 / 16 for A/B): per shard 0.93-0.96 ms against
+// 1.12 (8), 1.08 (2), 1.41 (1), 1.34 (16): each load instruction of a wave reads 256 B of one column, and fewer
+// columns per thread at a time keep more of the concurrent waves on the same columns (profiles/r05_fri_reduce_ab.txt)
+template <int LB>
 __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
     const uint64_t T = (uint64_t)gridDim.x * NT, i0 = (uint64_t)blockIdx.x * NT + threadIdx.x;
     ef t0[RED_ROWS], t1[RED_ROWS];
@@ -888,12 +892,12 @@ __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
             EfAcc acc;
             acc.zero();
             uint32_t c = 0;
-            for (; c + 8 <= ncols; c += 8) {  // 8 loads in flight
-                uint32_t v[8];
+            for (; c + LB <= ncols; c += LB) {  // LB loads in flight
+                uint32_t v[LB];
 #pragma unroll
-                for (int q = 0; q < 8; q++) v[q] = ((const uint32_t *)a.cols[coff + c + q])[i];
+                for (int q = 0; q < LB; q++) v[q] = ((const uint32_t *)a.cols[coff + c + q])[i];
 #pragma unroll
-                for (int q = 0; q < 8; q++) acc.base(v[q], a.alpha_pows + 4 * (c + q));
+                for (int q = 0; q < LB; q++) acc.base(v[q], a.alpha_pows + 4 * (c + q));
             }
             for (; c < ncols; c++) acc.base(((const uint32_t *)a.cols[coff + c])[i], a.alpha_pows + 4 * c);
             const ef s = acc.value();
@@ -953,7 +957,20 @@ __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
 
 void launch_fri_reduce(const ReduceArgs &a, hipStream_t s) {
     const uint64_t threads = (a.h + RED_ROWS - 1) / RED_ROWS;
-    hipLaunchKernelGGL(k_fri_reduce, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
+    static const int lb = [] {
+        const char *e = getenv("ZKM_RED_LOADS");
+        return e ? atoi(e) : 4;
+    }();
+    if (lb >= 16)
+        hipLaunchKernelGGL(k_fri_reduce<16>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
+    else if (lb <= 1)
+        hipLaunchKernelGGL(k_fri_reduce<1>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
+    else if (lb <= 2)
+        hipLaunchKernelGGL(k_fri_reduce<2>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
+    else if (lb >= 8)
+        hipLaunchKernelGGL(k_fri_reduce<8>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_fri_reduce<4>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
     HIP_CHECK(hipGetLastError());
 }
 
