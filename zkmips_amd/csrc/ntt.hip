@@ -481,15 +481,27 @@ __device__ __forceinline__ void stage_h1(uint32_t v[16], bool odd) {
     }
 }
 
+// sw13(lay_idx<SE>(t, j)) written as a per-thread base plus a constant stride (544, 34 or 2 words): element j's
+// LDS address is the base plus an immediate offset, one base register per layout, which the compiler does not
+// derive from sw13's shift by itself
+template <int SE>
+__device__ __forceinline__ uint32_t lds_base(uint32_t t) {
+    if constexpr (SE == 512) return t + 2 * (t >> 5);
+    else if constexpr (SE == 32) return (t >> 5) * 544 + (t & 31);
+    else return (t >> 1) * 34 + (t & 1);
+}
+template <int SE> constexpr uint32_t LDS_STRIDE = SE == 512 ? 544 : SE == 32 ? 34 : 2;
 template <int SE>
 __device__ __forceinline__ void to_lds(uint32_t *x, const uint32_t v[16], uint32_t t) {
+    uint32_t *p = x + lds_base<SE>(t);
 #pragma unroll
-    for (int j = 0; j < 16; j++) x[sw13(lay_idx<SE>(t, j))] = v[j];
+    for (int j = 0; j < 16; j++) p[LDS_STRIDE<SE> * j] = v[j];
 }
 template <int SE>
 __device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint32_t t) {
+    const uint32_t *p = x + lds_base<SE>(t);
 #pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = x[sw13(lay_idx<SE>(t, j))];
+    for (int j = 0; j < 16; j++) v[j] = p[LDS_STRIDE<SE> * j];
 }
 
 // Exchange ordering between the layouts.  L512 spreads a wave's elements over the whole tile, but L32
@@ -645,6 +657,64 @@ __global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src
     for (int j = 0; j < 16; j++) ZKM_ST13(v1[j], &dp[dst_half + (TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j))]);
 #undef ZKM_ST13
 }
+
+// Sequential-coset form (the default; ZKM_T13_SEQ=0 selects k_lde_fused13): the coefficients stay in registers
+// while each coset is twisted, transformed and stored in turn through ONE 34.8 KB LDS tile, so a workgroup needs
+// half the LDS and fewer registers than k_lde_fused13 (no second 16-element state, no twiddle set held across
+// two transforms): 64 VGPRs, four workgroups (32 waves) per CU instead of two, for one more workgroup barrier and
+// the twiddle loads done twice.  Per 8-column batch of a 2^22 LDE 202 vs 208 us, LDE 2^22 x 67 -0.8 %
+// (profiles/r05_t13_seq_ab.txt): doubling the waves barely moves it, the tile is at ~0.74 of the VALU issue rate.
+namespace t13 {
+// net16 with each stage's twiddles loaded just before the stage (at most 8 live instead of 15)
+template <bool DIT, int SE>
+__device__ __forceinline__ void net16s(uint32_t v[16], uint32_t off, const uint32_t *__restrict__ tt) {
+    const uint32_t *row = tt + (tt_row(SE) + off) * 16;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int st = DIT ? q : 3 - q;
+        const int span = 1 << st;
+        uint32_t w[8];
+#pragma unroll
+        for (int m = 0; m < span; m++) w[m] = row[span - 1 + m];
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+#pragma unroll
+            for (int j = m; j < 16; j += 2 * span) {
+                // at most four butterflies' products in flight (the 80-register budget; other waves hide the latency)
+                if (((j >> (st + 1)) * span + m) % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+                const uint32_t a = v[j], b = v[j + span];
+                if (DIT) {
+                    const uint32_t tt = mul(b, w[m]);
+                    if (q < 3 && ((j >> (st + 1)) & 1)) {
+                        v[j] = a + tt;
+                        v[j + span] = a + (P - tt);
+                    } else {
+                        v[j] = add(a, tt);
+                        v[j + span] = sub(a, tt);
+                    }
+                } else {
+                    v[j] = add(a, b);
+                    v[j + span] = mul(a + (P - b), w[m]);
+                }
+            }
+        }
+    }
+}
+template <bool WL>
+__device__ __forceinline__ void dit13(uint32_t v[16], uint32_t *x, uint32_t t, const uint32_t *__restrict__ tw) {
+    stage_h1(v, t & 1);
+    net16s<true, 2>(v, lay_off<2>(t), tw);
+    to_lds<2>(x, v, t);
+    own_sync<WL>();
+    from_lds<32>(x, v, t);
+    net16s<true, 32>(v, lay_off<32>(t), tw);
+    own_sync<WL>();
+    to_lds<32>(x, v, t);
+    __syncthreads();
+    from_lds<512>(x, v, t);
+    net16s<true, 512>(v, lay_off<512>(t), tw);
+}
+}  // namespace t13
 
 // ------------------------------------------------------------------ 512-row strided register tiles
 // One workgroup of 1024 threads: 512 rows (stride S) x 32 consecutive columns, 16 elements per
@@ -1595,6 +1665,48 @@ __global__ __launch_bounds__(s9::NTH, MINW) void k_ntt_s9q(const uint32_t *src, 
     }
 }
 
+// (k_lde_fused13s: global accesses through buffer descriptors -- a per-thread voffset and a uniform soffset per
+// element -- so the 16 element addresses of the tile-major layout, 1 MB apart, are not 16 live 64-bit pointers)
+template <bool TILED>
+__global__ __launch_bounds__(t13::NTH, 6) void k_lde_fused13s(const uint32_t *src, uint32_t *dst, ColMap ms,
+                                                             ColMap md, int L, const uint32_t *__restrict__ tt_inv,
+                                                             const uint32_t *__restrict__ tt_fwd, Twist tws,
+                                                             uint64_t dst_half) {
+    using namespace t13;
+    __shared__ uint32_t x[LDS13];
+    const uint32_t t = threadIdx.x;
+    const uint32_t N = 1u << L;
+    // element j of thread t: word voff / 4 + j * SJ of the column (TILED: tiled13; else lay_idx<512> + base)
+    const uint32_t voff = TILED ? (((t >> 5) * 16384u) + blockIdx.x * 32u + (t & 31)) * 4u : (blockIdx.x * 8192u + t) * 4u;
+    constexpr uint32_t SJ4 = TILED ? 16u * 16384u * 4u : 512u * 4u;
+    const auto rs = s9::mkrs(src + ms.off(blockIdx.y), N * 4u);
+    uint32_t c[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) c[j] = s9::bld(rs, voff, (uint32_t)j * SJ4);
+    dif13<true>(c, x, t, tt_inv);
+    const auto rd = s9::mkrs(dst + md.off(blockIdx.y), (uint32_t)((dst_half + N) * 4u));
+#pragma unroll 1
+    for (int e = 0; e < 2; e++) {
+        uint32_t v[16];
+        {
+            const uint32_t g = e ? tws.g1[blockIdx.x] : tws.g0[blockIdx.x];
+            const uint4 *u = (const uint4 *)((e ? tws.u1 : tws.u0) + t * 16);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint4 a = u[q];
+                const uint32_t au[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                for (int r = 0; r < 4; r++) v[4 * q + r] = mul(mul_lazy(c[4 * q + r], g), au[r]);
+            }
+        }
+        if (e) __syncthreads();  // the first coset's cross-wave L512 reads are done before this one's LDS writes
+        dit13<true>(v, x, t, tt_fwd);
+        const uint32_t so = e ? (uint32_t)(dst_half * 4u) : 0u;
+#pragma unroll
+        for (int j = 0; j < 16; j++) s9::bst_mid(v[j], rd, voff, so + (uint32_t)j * SJ4);
+    }
+}
+
 // ------------------------------------------------------------------ dispatch
 static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
 static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
@@ -1995,8 +2107,13 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
                     const char *e = getenv("ZKM_T13_BARRIERS");
                     return e && atoi(e) != 0;
                 }();
-                auto k = tiled ? (barriers ? k_lde_fused13<true, false> : k_lde_fused13<true, true>)
-                               : (barriers ? k_lde_fused13<false, false> : k_lde_fused13<false, true>);
+                static const bool seq = [] {  // sequential cosets (default) or both at once (ZKM_T13_SEQ=0)
+                    const char *e = getenv("ZKM_T13_SEQ");
+                    return !e || atoi(e) != 0;
+                }();
+                auto k = seq ? (tiled ? k_lde_fused13s<true> : k_lde_fused13s<false>)
+                         : tiled ? (barriers ? k_lde_fused13<true, false> : k_lde_fused13<true, true>)
+                                 : (barriers ? k_lde_fused13<false, false> : k_lde_fused13<false, true>);
                 hipLaunchKernelGGL(k, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf, work.p, m_i, m_w1, L,
                                    c.tt_inv, c.tt_fwd, tws, N);
                 HIP_CHECK(hipGetLastError());
