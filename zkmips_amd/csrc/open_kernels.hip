@@ -619,10 +619,12 @@ __device__ __forceinline__ uint32_t fold_acc(uint64_t v) {
 
 // k_open_dot_regs with the next column block's loads issued before the current block's products (two
 // register sets used alternately): 152 VGPRs, 3 waves per SIMD
+template <int CB>
 __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                       OpenWeights pw, int with_next, int nseg, uint32_t slab,
                                                       uint32_t *partial, uint32_t bx, uint32_t by) {
-    __shared__ uint32_t red[OPEN_CB * 8][OPEN_RED_LD];
+    __shared__ uint32_t red[CB * 8][OPEN_RED_LD];
+    constexpr int TPW = NT / (CB * 8);  // reduction threads per output word
     const uint64_t j0 = (uint64_t)bx * OPEN_SEG;
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t ra = 4 * t, rb = 4 * NT + 4 * t;
@@ -678,13 +680,13 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
     typedef const __attribute__((address_space(1))) u32x4 *g4;
     typedef const __attribute__((address_space(1))) uint32_t *g1;
     struct Blk {
-        uint4 a[OPEN_CB], b[OPEN_CB];
-        uint32_t xa[OPEN_CB], xb[OPEN_CB];
+        uint4 a[CB], b[CB];
+        uint32_t xa[CB], xb[CB];
     };
     auto load_block = [&](uint32_t cb, Blk &d) {
-        const int nc = (int)(c_end - cb < (uint32_t)OPEN_CB ? c_end - cb : OPEN_CB);
+        const int nc = (int)(c_end - cb < (uint32_t)CB ? c_end - cb : CB);
 #pragma unroll
-        for (int k = 0; k < OPEN_CB; k++) {
+        for (int k = 0; k < CB; k++) {
             const uint64_t y = cols[cb + (k < nc ? k : 0)];
             const u32x4 qa = *(g4)(y + 4 * (j0 + ra)), qb = *(g4)(y + 4 * (j0 + rb));
             d.a[k] = make_uint4(qa.x, qa.y, qa.z, qa.w);
@@ -696,9 +698,9 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
         }
     };
     auto process = [&](uint32_t cb0, const Blk &c) {
-        const int nc = (int)(c_end - cb0 < (uint32_t)OPEN_CB ? c_end - cb0 : OPEN_CB);
+        const int nc = (int)(c_end - cb0 < (uint32_t)CB ? c_end - cb0 : CB);
 #pragma unroll
-        for (int k = 0; k < OPEN_CB; k++) {
+        for (int k = 0; k < CB; k++) {
             const uint4 va = c.a[k], vb = c.b[k];
             const uint32_t v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
             uint64_t a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
@@ -722,33 +724,32 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
         }
         __syncthreads();
         {
-            const uint32_t o = t >> 3, q = t & 7;  // output word o (column o / 8), partial sums q, q + 8, ...
+            const uint32_t o = t / TPW, q = t % TPW;  // output word o (column o / 8), partial sums q, q + TPW, ...
             uint64_t acc = 0;
 #pragma unroll
-            for (int i = 0; i < NT / 8; i++) acc += red[o][q + 8 * i];  // < 32 * 2^32
+            for (int i = 0; i < NT / TPW; i++) acc += red[o][q + TPW * i];  // < 32 * 2^32
             uint32_t r = acc_mod(acc);
-            r = add(r, __shfl_xor(r, 1, 64));
-            r = add(r, __shfl_xor(r, 2, 64));
-            r = add(r, __shfl_xor(r, 4, 64));
+#pragma unroll
+            for (int sh = 1; sh < TPW; sh <<= 1) r = add(r, __shfl_xor(r, sh, 64));
             if (q == 0 && (int)(o >> 3) < nc) partial[((uint64_t)(cb0 + (o >> 3)) * nseg + bx) * 8 + (o & 7)] = r;
         }
         __syncthreads();  // red is reused by the next column block
     };
     Blk b0, b1;
     if (c_begin < c_end) load_block(c_begin, b0);
-    for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += 2 * OPEN_CB) {
-        const uint32_t cb1 = cb0 + OPEN_CB;
+    for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += 2 * CB) {
+        const uint32_t cb1 = cb0 + CB;
         if (cb1 < c_end) load_block(cb1, b1);
         process(cb0, b0);
         if (cb1 >= c_end) break;
-        if (cb1 + OPEN_CB < c_end) load_block(cb1 + OPEN_CB, b0);
+        if (cb1 + CB < c_end) load_block(cb1 + CB, b0);
         process(cb1, b1);
     }
 }
 __global__ __launch_bounds__(NT) void k_open_dot_pf(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                       OpenWeights pw, int with_next, int nseg, uint32_t slab,
                                                       uint32_t *partial) {
-    open_dot_pf(cols, ncols, n, pw, with_next, nseg, slab, partial, blockIdx.x, blockIdx.y);
+    open_dot_pf<OPEN_CB>(cols, ncols, n, pw, with_next, nseg, slab, partial, blockIdx.x, blockIdx.y);
 }
 
 // out[col * 8 + e] = sum over the nseg segments of partial[(col * nseg + seg) * 8 + e]: one wave per
@@ -787,8 +788,10 @@ __global__ __launch_bounds__(NT) void k_open_dot_groups(const OpenGroup *__restr
         open_dot_lds(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
     else if constexpr (KIND == 1)
         open_dot_regs(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
+    else if constexpr (KIND == 2)
+        open_dot_pf<OPEN_CB>(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
     else
-        open_dot_pf(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
+        open_dot_pf<2>(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
 }
 __global__ __launch_bounds__(64) void k_open_sum_groups(const OpenGroup *__restrict__ gs) {
     const OpenGroup g = gs[blockIdx.z];
@@ -806,7 +809,10 @@ static void open_group_shape(OpenGroup &g) {
     g.nslab = (g.ncols + g.slab - 1) / g.slab;
     static const bool lds_weights = getenv("ZKM_OPEN_LDS_WEIGHTS") && atoi(getenv("ZKM_OPEN_LDS_WEIGHTS"));
     static const bool prefetch = !getenv("ZKM_OPEN_PREFETCH") || atoi(getenv("ZKM_OPEN_PREFETCH"));
-    g.kind = (g.n % OPEN_SEG == 0 && !lds_weights) ? (prefetch ? 2 : 1) : 0;
+    // the prefetching kernel walks its columns two at a time (kind 3: 116 VGPRs, 4 waves per SIMD; openings
+    // 0.600-0.606 vs 0.608-0.614 ms per shard with 4, profiles/r05_open_cb_ab.txt); ZKM_OPEN_CB=4 selects kind 2
+    static const int ocb = getenv("ZKM_OPEN_CB") ? atoi(getenv("ZKM_OPEN_CB")) : 2;
+    g.kind = (g.n % OPEN_SEG == 0 && !lds_weights) ? (prefetch ? (ocb == 2 ? 3 : 2) : 1) : 0;
 }
 
 void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const OpenWeights &w, bool with_next,
@@ -816,7 +822,7 @@ void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const O
     open_group_shape(g);
     DBuf part((size_t)ncols * g.nseg * 8, s);
     const dim3 grid(g.nseg, g.nslab);
-    if (g.kind == 2)
+    if (g.kind >= 2)
         hipLaunchKernelGGL(k_open_dot_pf, grid, dim3(NT), 0, s, d_cols, ncols, n, w, g.with_next, g.nseg, g.slab, part.p);
     else if (g.kind == 1)
         hipLaunchKernelGGL(k_open_dot_regs, grid, dim3(NT), 0, s, d_cols, ncols, n, w, g.with_next, g.nseg, g.slab, part.p);
@@ -835,7 +841,7 @@ void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s) {
     if (gs.empty()) return;
     size_t tot = 0;
     uint32_t gx = 1, gy = 1, maxc = 1;
-    bool kinds[3] = {false, false, false};
+    bool kinds[4] = {false, false, false, false};
     for (OpenGroup &g : gs) {
         open_group_shape(g);
         tot += (size_t)g.ncols * g.nseg * 8;
@@ -857,6 +863,7 @@ void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s) {
     if (kinds[0]) hipLaunchKernelGGL(k_open_dot_groups<0>, grid, dim3(NT), 0, s, d);
     if (kinds[1]) hipLaunchKernelGGL(k_open_dot_groups<1>, grid, dim3(NT), 0, s, d);
     if (kinds[2]) hipLaunchKernelGGL(k_open_dot_groups<2>, grid, dim3(NT), 0, s, d);
+    if (kinds[3]) hipLaunchKernelGGL(k_open_dot_groups<3>, grid, dim3(NT), 0, s, d);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_open_sum_groups, dim3(maxc, 1, (unsigned)gs.size()), dim3(64), 0, s, d);
     HIP_CHECK(hipGetLastError());
