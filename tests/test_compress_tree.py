@@ -3,7 +3,7 @@
 generation in a process pool, and — on the GPU — a node verifying two real MIPS-shard leaves, padded to
 a reference recursion shape, proven byte-identically to the oracle."""
 import multiprocessing as mpc
-from concurrent.futures import ProcessPoolExecutor
+from concurrent.futures import Future, ProcessPoolExecutor
 
 import numpy as np
 import pytest
@@ -79,13 +79,18 @@ def test_tree_with_witness_pool_matches_serial(fib_leaves):
     prove = _oracle_prove_factory(4)
     with ProcessPoolExecutor(2, mp_context=mpc.get_context("spawn")) as pool:
         # verifying keys by reference (VkRef: written once, loaded once per worker)
-        red = CT.Reducer(lambda ch, fl: pool.submit(_witness_small, CT.by_ref(ch), **fl), prove, inflight=2)
+        # (Fibonacci leaves are no MIPS execution: the root is not asserted complete)
+        red = CT.Reducer(lambda ch, fl: pool.submit(_witness_small, CT.by_ref(ch), **fl), prove, inflight=2,
+                         complete=False)
         root = CT.reduce_serial(fib_leaves, red)
     a = prove(_witness_small(fib_leaves[:2]))
     b = prove(_witness_small(fib_leaves[2:]))
     want = prove(_witness_small([a, b]))
     assert root[1] == want[1]
     assert np.array_equal(root[0].commit, want[0].commit)
+    # a complete root needs an execution shard (assert_complete): over these children it is refused
+    with pytest.raises(ValueError, match="execution shard"):
+        _witness_small([a, b], is_complete=True)
 
 
 def test_tree_with_affinity_pool_matches_serial(fib_leaves):
@@ -95,7 +100,7 @@ def test_tree_with_affinity_pool_matches_serial(fib_leaves):
     pool = CT.AffinityPool(2)
     try:
         red = CT.Reducer(lambda ch, fl: pool.submit(_witness_small, CT.by_ref(ch), **fl, tag=CT.node_tag(ch)), prove,
-                         inflight=2)
+                         inflight=2, complete=False)
         root = CT.reduce_serial(fib_leaves, red)
     finally:
         pool.shutdown()
@@ -201,6 +206,41 @@ def test_compact_witness_is_the_full_witness(fib_leaves):
     sid = CT.new_session()
     assert CT.node_witness(fib_leaves[2:], fix=False, compact=True, session=sid)[0].traces is not None
     assert CT.node_witness(fib_leaves[:2], fix=False, compact=True, session=sid)[0].traces is None
+
+
+def test_prep_store_keeps_live_sessions_keys():
+    """More than CACHE_ENTRIES programs through the consumer's store across interleaved sessions: a key a live
+    session received (its traces sent once per session) survives every eviction until the session ends;
+    afterwards it is evicted like any other."""
+    CT._PREP_STORE.clear()
+    CT._PINS.clear()
+    a, b = CT.new_session(), CT.new_session()
+    t0 = {"MemoryConst": np.arange(4, dtype=np.uint32)}
+    CT.register_prep((CT.Prep(b"k0", t0, a), None))
+    for i in range(CT.CACHE_ENTRIES + 10):  # session b: many programs, each sent with its traces
+        CT.register_prep((CT.Prep(b"b%d" % i, {"x": np.zeros(1, np.uint32)}, b), None))
+        if i % 7 == 0:  # session a's later nodes of k0 arrive in between, traces omitted
+            CT.register_prep((CT.Prep(b"k0", None, a), None))
+    assert CT._prep_traces_of(CT.Prep(b"k0", None, a)) is t0
+    # b's keys are pinned too (b is live): the store grew past the bound instead of dropping them
+    assert all(CT._prep_traces_of(CT.Prep(b"b%d" % i, None, b)) is not None for i in range(CT.CACHE_ENTRIES + 10))
+    # a Reducer over witnesses of session a releases it when its tree ends
+    red = CT.Reducer(lambda ch, fl: _done_future((CT.Prep(b"k0", None, a), ch)), lambda w: ("vk", b"p"),
+                     inflight=1, complete=False)
+    CT.reduce_serial([("vk", b"l0"), ("vk", b"l1")], red)
+    assert a not in CT._PINS and b in CT._PINS
+    CT.release_session(b)
+    for i in range(CT.CACHE_ENTRIES + 1):
+        CT.register_prep((CT.Prep(b"c%d" % i, {"x": np.zeros(1, np.uint32)}, None), None))
+    assert b"k0" not in CT._PREP_STORE and len(CT._PREP_STORE) <= CT.CACHE_ENTRIES + 1  # (session None: pinned)
+    CT._PREP_STORE.clear()
+    CT._PINS.clear()
+
+
+def _done_future(v):
+    f = Future()
+    f.set_result(v)
+    return f
 
 
 def test_failed_tree_discards_in_flight_witnesses(tmp_path):
@@ -445,7 +485,8 @@ def test_compress_node_chaining(mips_execution):
 
 def test_dummy_vk_tree():
     """The dummy vk map's tree (prover/src/lib.rs:223-233, merkle_tree.rs): 10000 leaves [i; 8] padded to
-    2^14; open / verify agree for the first, last and a middle leaf; a wrong sibling fails."""
+    2^14; open / verify agree for the first, last and a middle leaf; a wrong sibling fails.  The root itself
+    and vk_digest are parity unpinned (the reference holds no vk_root / vk digest value; vk_tree.py)."""
     from zkmips_amd import vk_tree as VT
     t = VT.dummy_tree()
     assert t.height == 14

@@ -110,6 +110,15 @@ def test_syscall_shards_satisfy_air(run):
     assert int(cmp_["ShaCompress"][:, SY.SC2_REAL].sum()) == 5 * 80
 
 
+def test_closing_shards_keep_the_last_execution_shard(run):
+    """The precompile and memory shards of a finished execution carry the last CPU shard's execution_shard
+    (crates/core/machine/src/utils/prove.rs:308-311: no increment on the `done` path)."""
+    cpu = [pv for _, _, tr, pv in run if "Cpu" in tr]
+    rest = [pv for _, _, tr, pv in run if "Cpu" not in tr]
+    assert len(rest) == 3 and [int(pv[C.PV_EXECUTION_SHARD]) for pv in cpu] == list(range(1, len(cpu) + 1))
+    assert all(int(pv[C.PV_EXECUTION_SHARD]) == len(cpu) for pv in rest)
+
+
 def test_halt_and_commit_public_values(run):
     _, _, tr, pv = [r for r in run if "Cpu" in r[2]][-1]
     assert pv[C.PV_NEXT_PC] == 0 and pv[SY.PV_EXIT_CODE] == 0

@@ -67,6 +67,7 @@ class Prep:
     an earlier one (register_prep keeps them)."""
     key: bytes
     traces: Optional[dict]
+    session: object = None  # node_witness's dedup session: register_prep pins `key` for it (release_session)
 
 
 @dataclass(frozen=True)
@@ -156,6 +157,11 @@ def by_ref(children: Sequence[tuple]) -> List[tuple]:
 # in-flight witnesses were dropped) starts empty, so it never depends on traces another session consumed.
 _SENT_KEYS: "OrderedDict[object, set]" = OrderedDict()
 _PREP_STORE: "OrderedDict[bytes, dict]" = OrderedDict()  # consumer side: traces by key (content-addressed)
+# consumer side: session -> the keys its witnesses named.  A pinned key is never evicted from _PREP_STORE: a
+# worker sends a program's traces once per session, so a later node of that session may need them however
+# many other programs went through the store meanwhile.  release_session unpins (the end of a tree); the
+# session None (callers without sessions: a worker's dedup set lives as long as the worker) is never released.
+_PINS: Dict[object, set] = {}
 _STORE_LOCK = threading.Lock()
 SESSIONS_KEPT = 16
 
@@ -249,15 +255,38 @@ def shm_cleanup():
             pass
 
 
+def _store_put(key: bytes, traces: dict):
+    """_PREP_STORE[key] = traces, then least recently used unpinned keys out down to CACHE_ENTRIES (pinned
+    keys stay, beyond the bound if need be).  Caller holds _STORE_LOCK."""
+    _PREP_STORE[key] = traces
+    _PREP_STORE.move_to_end(key)
+    excess = len(_PREP_STORE) - CACHE_ENTRIES
+    if excess > 0:
+        pinned = set().union(*_PINS.values()) if _PINS else set()
+        for k in [k for k in _PREP_STORE if k not in pinned][:excess]:
+            del _PREP_STORE[k]
+
+
 def register_prep(wit):
     """Record a compact witness's preprocessed traces on the consuming side (called in arrival order, before
-    any witness of the same worker that omits them is proven).  A Packed witness is unpacked first."""
+    any witness of the same worker that omits them is proven) and pin its key for the witness's session.  A
+    Packed witness is unpacked first."""
     wit = shm_unpack(wit)
     p = wit[0]
-    if isinstance(p, Prep) and p.traces is not None:
+    if isinstance(p, Prep):
         with _STORE_LOCK:
-            _lru_put(_PREP_STORE, p.key, p.traces)
+            _PINS.setdefault(p.session, set()).add(p.key)
+            if p.traces is not None:
+                _store_put(p.key, p.traces)
     return wit
+
+
+def release_session(session):
+    """Unpin the keys of a finished session (Reducer.run does this for the sessions of its witnesses)."""
+    if session is None:
+        return
+    with _STORE_LOCK:
+        _PINS.pop(session, None)
 
 
 def _prep_traces_of(p: "Prep") -> dict:
@@ -333,7 +362,7 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
             sent.add(key)
         traces = compact_traces(rec, shape)
         t2 = time.perf_counter()
-        return Prep(key, prep), traces, rec.public_values, shape, {"build_s": t1 - t0, "execute_and_traces_s": t2 - t1}
+        return Prep(key, prep, session), traces, rec.public_values, shape, {"build_s": t1 - t0, "execute_and_traces_s": t2 - t1}
     if p2_on_device:
         _, prep, traces, pvs, p2in, p2h = R.shard_parts(prog, shape)
         traces["Poseidon2WideDeg3"] = DeviceP2(p2in, p2h)
@@ -562,23 +591,29 @@ class AffinityPool:
         shm_cleanup()
 
 
-def node_flags(node: Node, root: Node) -> dict:
+def node_flags(node: Node, root: Node, complete: bool = True) -> dict:
     """node_witness's flags for node (L, j): its first leaf is the execution's first shard (core.rs
-    `is_first_shard`, lib.rs:543 batch_idx == 0) and it is the tree's root (is_complete, lib.rs:901-909)."""
-    return {"is_first": node[1] == 0, "is_complete": node == root}
+    `is_first_shard`, lib.rs:543 batch_idx == 0) and it is the tree's root (is_complete, lib.rs:901-909).
+    complete=False: the root is not asserted complete either (trees of leaves that are not a whole MIPS
+    execution, e.g. synthetic test machines, whose root assert_complete would reject)."""
+    return {"is_first": node[1] == 0, "is_complete": complete and node == root}
 
 
 class Reducer:
     """The event-driven reduction of one rank's part of the tree.
 
     witness(children, flags) -> concurrent.futures.Future of node_witness's result (flags: node_flags);
-    prove(witness) -> (child vk, proof bytes) for the parent (GPU, called from `inflight` threads)."""
+    prove(witness) -> (child vk, proof bytes) for the parent (GPU, called from `inflight` threads).
+    complete: the root is asserted complete (node_flags).  The dedup sessions named by the witnesses'
+    Prep are released when run() ends."""
 
     def __init__(self, submit_witness: Callable, prove: Callable, inflight: int = 3,
-                 on_witness: Callable = register_prep):
+                 on_witness: Callable = register_prep, complete: bool = True):
         self.submit_witness = submit_witness
         self.prove = prove
         self.on_witness = on_witness  # called on each witness in arrival order, before it is queued
+        self.complete = complete
+        self.sessions: set = set()
         self.times: Dict[Node, Dict[str, float]] = {}  # node -> perf_counter of submit / witness / proved
         self.inflight = max(1, inflight)
         self.events: "queue.Queue" = queue.Queue()
@@ -619,7 +654,7 @@ class Reducer:
                 if ok:
                     submitted.add(node)
                     self.times.setdefault(node, {})["submit"] = time.perf_counter()
-                    fut = self.submit_witness([done[c] for c in ch], node_flags(node, root))
+                    fut = self.submit_witness([done[c] for c in ch], node_flags(node, root, self.complete))
                     futs[node] = fut
                     fut.add_done_callback(lambda f, n=node: self.events.put(("witness", n, f)))
         ok = False
@@ -639,7 +674,10 @@ class Reducer:
                 if kind == "witness":
                     futs.pop(node, None)
                     self.times.setdefault(node, {})["witness"] = time.perf_counter()
-                    self.gpu_q.put((node, self.on_witness(val.result())))
+                    wit = self.on_witness(val.result())
+                    if isinstance(wit, tuple) and wit and isinstance(wit[0], Prep) and wit[0].session is not None:
+                        self.sessions.add(wit[0].session)
+                    self.gpu_q.put((node, wit))
                 elif kind == "proof":
                     self.times.setdefault(node, {})["proved"] = time.perf_counter()
                     done[node] = val
@@ -659,6 +697,9 @@ class Reducer:
                 self.gpu_q.put(None)
             for t in threads:
                 t.join(timeout=60)
+            for sid in self.sessions:  # every node of the sessions has been proven (or the tree failed)
+                release_session(sid)
+            self.sessions.clear()
         return done
 
 

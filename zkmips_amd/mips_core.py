@@ -1637,14 +1637,17 @@ def _commit_pvs(pvs, commits: dict):
 
 def _deferred_shard_pvs(state, shard: int) -> np.ndarray:
     """A shard without CPU (precompile or memory shard, prove.rs:300-320): the running state -- its pc where
-    the execution stopped (start_pc = next_pc), the digests and exit code so far -- and its shard number."""
+    the execution stopped (start_pc = next_pc), the digests and exit code so far -- and its shard number.
+    program_shards emits these shards after the execution has finished, i.e. on the reference's `done` path,
+    which skips `state.execution_shard += 1` (prove.rs:308-311): they keep the last CPU shard's
+    execution_shard."""
     pvs = np.zeros(PROOF_MAX_NUM_PVS, np.uint32)
     st = state or {}
     pc = 0 if st.get("exit_code") is not None else int(st.get("pc", 0))
     pvs[PV_START_PC] = pvs[PV_NEXT_PC] = pc
     pvs[PV_EXIT_CODE] = int(st.get("exit_code") or 0)
     pvs[PV_SHARD] = shard
-    pvs[PV_EXECUTION_SHARD] = int(st.get("cpu_shards", 0)) + 1
+    pvs[PV_EXECUTION_SHARD] = int(st.get("cpu_shards", 0))
     _commit_pvs(pvs, st.get("commits", {}))
     return pvs
 

@@ -466,9 +466,11 @@ def compress_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars], i
            R_PREV_INIT: acc["prev_init"], R_LAST_INIT: init, R_PREV_FIN: acc["prev_fin"], R_LAST_FIN: fin,
            R_VK_DIGEST: vkd, R_GCS: sum_digest(o, gsums), R_START_RECON: acc["start_recon"], R_END_RECON: recon,
            R_EXIT: exit_code, R_CONTAINS_EXEC: contains, R_VK_ROOT: root}
-    # a tree with no execution shard (leaves of a machine other than MIPS, synthetic_node) is never complete
-    complete = bool(is_complete) and int(np.asarray(contains.v)) == 1
-    return _finish(o, out, o.hint(1 if complete else 0))
+    # assert_complete (machine/complete.rs) requires an execution shard: a complete root over children that
+    # contain none (leaves of a machine other than MIPS, synthetic_node) is a bad witness, not an incomplete root
+    if is_complete and int(np.asarray(contains.v)) != 1:
+        raise ValueError("compress node: is_complete requested but no child contains an execution shard")
+    return _finish(o, out, o.hint(1 if is_complete else 0))
 
 
 def synthetic_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars]) -> V:

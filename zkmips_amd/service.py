@@ -363,6 +363,8 @@ class ProverService:
         finally:
             if self._pool is None:
                 tp.shutdown(wait=False)
+            else:
+                CT.release_session(sid)  # (the one-leaf path pins its program's key outside a Reducer)
         return B.write_reduce_proof(reduce_vk(rvk), rproof)
 
     def call(self, method: str, payload: Dict[int, object]) -> Dict[str, object]:

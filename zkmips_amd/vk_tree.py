@@ -14,6 +14,12 @@ program (recursion_verifier.compress_node_program) verifies the openings in-prog
 Tree layout (MerkleTree::commit): leaves padded with [0; 8] to a power of two, stored bit-reversed, each layer
 `constant_compress([l, r])` = Poseidon2(l || r)[0..8] (TruncatedPermutation); open(index) walks the bit-reversed
 index; verify swaps the pair when the reversed index is odd.
+
+Parity: the dummy map's keys are pinned by dummy_vk_map.bin, but the tree's root and the vk digest
+(vk_digest) are **parity unpinned**: the reference holds no vk_root or hash_koalabear value to compare with
+(no golden vector, no test literal), so the bit-reversed leaf order, the layer compression and the order of the
+preprocessed domains in the digest rest on the restated code alone; the tests check open / verify against each
+other and the node programs against this module.
 """
 from __future__ import annotations
 
