@@ -21,7 +21,7 @@
 // Every lane of the wave must call it (MFMA and the LDS exchange are wave-wide); the outputs are the same
 // bits as p2::permute_lam's fold31 (tools/probe/p2_mfma_probe.hip checks them).
 #pragma once
-#include "p2.cuh"
+#include "../../zkmips_amd/csrc/p2.cuh"
 
 namespace p2m {
 

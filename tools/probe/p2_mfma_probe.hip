@@ -20,7 +20,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../../zkmips_amd/csrc/p2_mfma.cuh"
+#include "p2_mfma.cuh"
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 

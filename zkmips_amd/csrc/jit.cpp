@@ -67,10 +67,10 @@ struct Gen {
         loads[key] = v;
         return v;
     }
-    // body with the load markers replaced by the pipelined reads; `env` overrides the window
-    std::string pipelined(int look, const char *env) const {
-        if (const char *e = getenv(env)) look = atoi(e);
-        const bool barrier = !getenv("ZKM_JIT_NOBARRIER");
+    // body with the load markers replaced by the pipelined reads (each read issued `look` reads ahead of its
+    // first use and pinned there by a scheduling barrier)
+    std::string pipelined(int look) const {
+        const bool barrier = true;
         std::istringstream in(body.str());
         std::ostringstream out;
         std::string line;
@@ -263,7 +263,7 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
                << "uint32_t is_first, uint32_t is_last, uint32_t is_trans) {\n"
                << "    (void)rl; (void)rn; (void)is_first; (void)is_last; (void)is_trans;\n"
                << "    EfAcc facc;\n    facc.zero();\n"
-               << g.pipelined(8, "ZKM_JIT_LOOKAHEAD_Q") << "    return facc.value();\n}\n";
+               << g.pipelined(8) << "    return facc.value();\n}\n";
         g = Gen{};
         lazy.clear();
         slice_lines = 0;
@@ -441,7 +441,7 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
       << g.head.str()
       << "    EfAcc facc;\n"
       << "    facc.zero();\n"
-      << g.pipelined(8, "ZKM_JIT_LOOKAHEAD_Q")  // measured: 8 -> 2.27 ms, 24 -> 2.44, unpipelined 2.78
+      << g.pipelined(8)  // measured: 8 -> 2.27 ms, 24 -> 2.44, unpipelined 2.78
       << (sliced ? "    const ef qv = ef_mul_base(ef_add(facc.value(), slices), inv_z);\n"
                  : "    const ef qv = ef_mul_base(facc.value(), inv_z);\n")
       // chunk j = k mod 2^lqd (split_evals); t = rev_Q(k) = rev_lqd(j) * n + rev_n(k >> lqd), so the
@@ -460,12 +460,8 @@ std::string gen_source(const ChipDesc &c, const std::string &fname) {
 // the interpreter kernel; the nb denominators share ONE extension-field inversion (prefix
 // products, Montgomery's trick), then the row total goes to rowsum for the running-sum scan.
 // launch bounds of the LogUp kernels: 2 waves per SIMD (a 256-register cap; the unbounded kernel takes
-// 267 and runs one wave per SIMD: FibCpu 1.10 -> 0.89 ms); ZKM_JIT_PERM_WAVES=w overrides (0: no cap)
-std::string perm_bounds() {
-    const char *e = getenv("ZKM_JIT_PERM_WAVES");
-    const int w = e ? atoi(e) : 2;
-    return w > 0 ? "__launch_bounds__(256, " + std::to_string(w) + ")" : "__launch_bounds__(256)";
-}
+// 267 and runs one wave per SIMD: FibCpu 1.10 -> 0.89 ms; profiles/r03_perm_waves_sweep.txt)
+std::string perm_bounds() { return "__launch_bounds__(256, 2)"; }
 
 // Loop form of the LogUp trace (chips with > kJitLookupUnroll lookups): batches in groups of 8 share
 // one extension-field inversion (Montgomery's trick in registers).
@@ -518,78 +514,61 @@ std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
     const int batch = 1 << c.log_qd, nb = c.perm_w - 1;
     g.body << "    const ef alpha = ef{{A.alpha[0], A.alpha[1], A.alpha[2], A.alpha[3]}};\n";
     g.body << "    ef total = ef_zero();\n";
-    // batches in groups of `grp` share one inversion: fewer groups = fewer inversions, more live
-    // (num, den, prefix) registers
-    int grp = nb;
-    if (const char *e = getenv("ZKM_JIT_PERM_GROUP")) grp = std::max(1, atoi(e));
     // One inversion per row with each batch's numerator and the running prefix product parked in LDS
     // (each thread its own column of a [2 nb x 4][256] word array: no barriers, consecutive threads on
     // consecutive banks) while the denominators stay in registers: the 256-register cap no longer
-    // spills to scratch (HBM).  Up to kPermLdsBatches batches (80 KB per workgroup, two per CU).
-    const bool lds = grp == nb && nb >= 2 && nb <= kPermLdsBatches && !getenv("ZKM_JIT_PERM_NOLDS");
-    // ZKM_JIT_PERM_LDS_SPLIT=k: k inversions per row over consecutive groups of the batches, so LDS holds one
-    // group (80/k KB per workgroup at 10 batches: k workgroups more per CU) for k - 1 more EF inversions
-    const int parts = lds && getenv("ZKM_JIT_PERM_LDS_SPLIT") ? std::max(1, atoi(getenv("ZKM_JIT_PERM_LDS_SPLIT"))) : 1;
-    const int gsz = (nb + parts - 1) / parts;
+    // spills to scratch (HBM).  Up to kPermLdsBatches batches (80 KB per workgroup, two per CU).  Splitting
+    // the batches into groups with one inversion each (less LDS, more waves) measured slower, 0.97-1.03 vs
+    // 0.79 ms (profiles/r04_logup_open_ab.txt), as did smaller register-only groups (r03_perm_group_sweep.txt).
+    const bool lds = nb >= 2 && nb <= kPermLdsBatches;
     if (lds) {
-        for (int g0 = 0; g0 < nb; g0 += gsz) {
-            const int g1 = std::min(nb, g0 + gsz);
-            // (one group keeps the original names: the source text keys the code-object cache)
-            const std::string sfx = parts == 1 ? "" : std::to_string(g0), run = "run" + sfx, iv = "iv" + sfx;
-            for (int b = g0; b < g1; b++) {
-                const int sl = b - g0;
-                g.body << "    ef num" << b << ", den" << b << ";\n";
-                lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
-                             "den" + std::to_string(b));
-                // num_b -> LDS rows 4 sl..; the group's prefix product before b -> rows 4(gsz + sl)..
-                g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * sl << " + e) * 256 + threadIdx.x] = num" << b
-                       << ".c[e];\n";
-                if (b == g0) {
-                    g.body << "    ef " << run << " = den" << b << ";\n";
-                } else {
-                    g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * (gsz + sl)
-                           << " + e) * 256 + threadIdx.x] = " << run << ".c[e];\n"
-                           << "    " << run << " = ef_mul(" << run << ", den" << b << ");\n";
-                }
-            }
-            g.body << "    ef " << iv << " = ef_inv(" << run << ");\n";
-            for (int b = g1 - 1; b >= g0; b--) {
-                const int sl = b - g0;
-                g.body << "    {\n        ef nm, pr;\n"
-                       << "        for (int e = 0; e < 4; e++) nm.c[e] = pl_lds[(" << 4 * sl << " + e) * 256 + threadIdx.x];\n";
-                if (b > g0) {
-                    g.body << "        for (int e = 0; e < 4; e++) pr.c[e] = pl_lds[(" << 4 * (gsz + sl)
-                           << " + e) * 256 + threadIdx.x];\n"
-                           << "        const ef sb = ef_mul(nm, ef_mul(" << iv << ", pr));\n"
-                           << "        " << iv << " = ef_mul(" << iv << ", den" << b << ");\n";
-                } else {
-                    g.body << "        const ef sb = ef_mul(nm, " << iv << ");\n";
-                }
-                for (int e = 0; e < 4; e++)
-                    g.body << "        A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = sb.c[" << e << "];\n";
-                g.body << "        total = ef_add(total, sb);\n    }\n";
+        for (int b = 0; b < nb; b++) {
+            g.body << "    ef num" << b << ", den" << b << ";\n";
+            lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
+                         "den" + std::to_string(b));
+            // num_b -> LDS rows 4 b..; the prefix product before b -> rows 4(nb + b)..
+            g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * b << " + e) * 256 + threadIdx.x] = num" << b
+                   << ".c[e];\n";
+            if (b == 0) {
+                g.body << "    ef run = den" << b << ";\n";
+            } else {
+                g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * (nb + b)
+                       << " + e) * 256 + threadIdx.x] = run.c[e];\n"
+                       << "    run = ef_mul(run, den" << b << ");\n";
             }
         }
-        grp = 0;  // the groups below are done
-    }
-    for (int g0 = 0; grp && g0 < nb; g0 += grp) {
-        const int g1 = std::min(nb, g0 + grp);
-        for (int b = g0; b < g1; b++) {
+        g.body << "    ef iv = ef_inv(run);\n";
+        for (int b = nb - 1; b >= 0; b--) {
+            g.body << "    {\n        ef nm, pr;\n"
+                   << "        for (int e = 0; e < 4; e++) nm.c[e] = pl_lds[(" << 4 * b << " + e) * 256 + threadIdx.x];\n";
+            if (b > 0) {
+                g.body << "        for (int e = 0; e < 4; e++) pr.c[e] = pl_lds[(" << 4 * (nb + b)
+                       << " + e) * 256 + threadIdx.x];\n"
+                       << "        const ef sb = ef_mul(nm, ef_mul(iv, pr));\n"
+                       << "        iv = ef_mul(iv, den" << b << ");\n";
+            } else {
+                g.body << "        const ef sb = ef_mul(nm, iv);\n";
+            }
+            for (int e = 0; e < 4; e++)
+                g.body << "        A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = sb.c[" << e << "];\n";
+            g.body << "        total = ef_add(total, sb);\n    }\n";
+        }
+    } else {  // one batch, or more than kPermLdsBatches: prefix products in registers
+        for (int b = 0; b < nb; b++) {
             g.body << "    ef num" << b << ", den" << b << ";\n";
             lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
                          "den" + std::to_string(b));
         }
-        const std::string iv = "iv" + std::to_string(g0);
-        g.body << "    const ef pre" << g0 << " = den" << g0 << ";\n";
-        for (int b = g0 + 1; b < g1; b++)
+        g.body << "    const ef pre0 = den0;\n";
+        for (int b = 1; b < nb; b++)
             g.body << "    const ef pre" << b << " = ef_mul(pre" << b - 1 << ", den" << b << ");\n";
-        g.body << "    ef " << iv << " = ef_inv(pre" << g1 - 1 << ");\n";
-        for (int b = g1 - 1; b > g0; b--) {
-            g.body << "    const ef s" << b << " = ef_mul(num" << b << ", ef_mul(" << iv << ", pre" << b - 1 << "));\n";
-            g.body << "    " << iv << " = ef_mul(" << iv << ", den" << b << ");\n";
+        g.body << "    ef iv0 = ef_inv(pre" << nb - 1 << ");\n";
+        for (int b = nb - 1; b > 0; b--) {
+            g.body << "    const ef s" << b << " = ef_mul(num" << b << ", ef_mul(iv0, pre" << b - 1 << "));\n";
+            g.body << "    iv0 = ef_mul(iv0, den" << b << ");\n";
         }
-        g.body << "    const ef s" << g0 << " = ef_mul(num" << g0 << ", " << iv << ");\n";
-        for (int b = g0; b < g1; b++) {
+        g.body << "    const ef s0 = ef_mul(num0, iv0);\n";
+        for (int b = 0; b < nb; b++) {
             for (int e = 0; e < 4; e++)
                 g.body << "    A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = s" << b << ".c[" << e << "];\n";
             g.body << "    total = ef_add(total, s" << b << ");\n";
@@ -597,10 +576,10 @@ std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
     }
     std::ostringstream o;
     o << "extern \"C\" __global__ void " << perm_bounds() << " " << fname << "(const ZkmPermJitArgs A) {\n"
-      << (lds ? "    __shared__ uint32_t pl_lds[" + std::to_string(8 * gsz) + " * 256];\n" : std::string())
+      << (lds ? "    __shared__ uint32_t pl_lds[" + std::to_string(8 * nb) + " * 256];\n" : std::string())
       << "    const uint64_t rl = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n"
       << "    if (rl >= A.ld) return;\n"
-      << g.head.str() << g.pipelined(48, "ZKM_JIT_LOOKAHEAD_P")  // 48 -> 0.99 ms, 8 -> 1.37
+      << g.head.str() << g.pipelined(48)  // 48 -> 0.99 ms, 8 -> 1.37
       << "    A.rowsum[4 * rl + 0] = total.c[0];\n"
       << "    A.rowsum[4 * rl + 1] = total.c[1];\n"
       << "    A.rowsum[4 * rl + 2] = total.c[2];\n"

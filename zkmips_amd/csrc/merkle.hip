@@ -110,10 +110,8 @@ void launch_poseidon2_batch(uint32_t *d, uint64_t n, hipStream_t s) {
 static constexpr uint64_t SMALL16 = 8192;  // levels with <= SMALL16 nodes use the 16-lane form
 static constexpr int NT_TOP = 1024;
 static constexpr uint64_t TOP_MAX = NT_TOP / 16;  // levels with <= TOP_MAX nodes: one workgroup
-static uint64_t sub16_max() {  // levels with <= this many nodes: k_subtree16 (ZKM_SUB16 overrides)
-    static const uint64_t v = getenv("ZKM_SUB16") ? strtoull(getenv("ZKM_SUB16"), nullptr, 10) : 16384;
-    return v;
-}
+// levels with <= this many nodes: k_subtree16 (the threshold sweep, profiles/r03_sub16.txt)
+static uint64_t sub16_max() { return 16384; }
 
 __global__ __launch_bounds__(NT) void k_compress16(const uint32_t *__restrict__ prev, uint32_t *__restrict__ out,
                                                    uint64_t h) {
@@ -204,8 +202,7 @@ static bool build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
         bool later_inj = false;
         for (int k = L; k <= t.log_max; k++) later_inj |= inj[k].second != 0;
         const int ninj = inj[L].second;
-        static const bool subtree = !getenv("ZKM_NO_SUBTREE");  // A/B knob: per-level launches
-        if (subtree && h <= sub16_max() && ninj == 0) {
+        if (h <= sub16_max() && ninj == 0) {
             // subtree launches: one node per workgroup at the top of each (up to 7 levels), never across
             // a level with injected matrices
             const uint64_t m = h < TOP_MAX ? h : TOP_MAX;

@@ -282,7 +282,7 @@ struct ColMap {
 
 struct Twist {
     const uint32_t *lo0, *hi0, *lo1, *hi1;
-    // 8192-tile form (k_lde_fused13): f_e(rev_L(b 2^13 + i)) = g_e[b] * u_e[t][j] for element j of
+    // 8192-tile form (k_lde_fused13s): f_e(rev_L(b 2^13 + i)) = g_e[b] * u_e[t][j] for element j of
     // thread t in layout L2 (i = lay_idx<2>(t, j)); u_e: 512 x 16, g_e: 2^(L-13) entries
     const uint32_t *u0, *g0, *u1, *g1;
     __device__ __forceinline__ uint32_t f(int e, uint32_t k) const {
@@ -509,7 +509,7 @@ __device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint
 // 64 w + 63: L32 rows t >> 5 in {2w, 2w + 1}, L2 groups t >> 1 in [32 w, 32 w + 32)), so the L32 <-> L2
 // exchanges only touch the wave's own LDS words: a DS instruction stream of one wave executes in
 // order, and the compiler only has to keep the accesses in program order -- no workgroup barrier.
-// WL = false keeps the barriers (A/B, ZKM_T13_BARRIERS=1).
+// WL = false keeps workgroup barriers there instead.
 template <bool WL>
 __device__ __forceinline__ void own_sync() {
     if constexpr (WL) {
@@ -540,72 +540,6 @@ __device__ __forceinline__ void dif13(uint32_t v[16], uint32_t *x, uint32_t t, c
 
 }  // namespace t13
 
-// Fused middle of the natural-input LDE for transforms larger than one tile: the iNTT's last 13
-// (DIF) stages, both coset twists and the forward transforms' first 13 (DIT) stages.  Both cosets
-// run at once: the coefficients never leave registers, the two forward transforms share their
-// twiddle loads and barriers.  VALU-bound: 343 issue slots per input element (19.5 butterflies
-// + 4 twist products), measured at 0.86 of the VALU issue rate.
-namespace t13 {
-template <bool DIT, int SE>
-__device__ __forceinline__ void net16x2(uint32_t v0[16], uint32_t v1[16], uint32_t off,
-                                        const uint32_t *__restrict__ tt) {
-    uint32_t w16[16];
-    const uint4 *row = (const uint4 *)(tt + (tt_row(SE) + off) * 16);
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint4 r = row[q];
-        w16[4 * q] = r.x; w16[4 * q + 1] = r.y; w16[4 * q + 2] = r.z; w16[4 * q + 3] = r.w;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int st = DIT ? q : 3 - q;
-        const int span = 1 << st;
-#pragma unroll
-        for (int m = 0; m < span; m++) {
-            const uint32_t w = w16[span - 1 + m];
-#pragma unroll
-            for (int j = m; j < 16; j += 2 * span) {
-#pragma unroll
-                for (int e = 0; e < 2; e++) {
-                    uint32_t *v = e ? v1 : v0;
-                    const uint32_t x = v[j], y = v[j + span];
-                    const uint32_t tt = mul(y, w);
-                    if (q < 3 && ((j >> (st + 1)) & 1)) {
-                        v[j] = x + tt;
-                        v[j + span] = x + (P - tt);
-                    } else {
-                        v[j] = add(x, tt);
-                        v[j + span] = sub(x, tt);
-                    }
-                }
-            }
-        }
-    }
-}
-
-template <bool WL>
-__device__ __forceinline__ void dit13x2(uint32_t v0[16], uint32_t v1[16], uint32_t *x, uint32_t t,
-                                        const uint32_t *__restrict__ tw) {
-    uint32_t *x1 = x + LDS13;
-    stage_h1(v0, t & 1);
-    stage_h1(v1, t & 1);
-    net16x2<true, 2>(v0, v1, lay_off<2>(t), tw);
-    to_lds<2>(x, v0, t);
-    to_lds<2>(x1, v1, t);
-    own_sync<WL>();
-    from_lds<32>(x, v0, t);
-    from_lds<32>(x1, v1, t);
-    net16x2<true, 32>(v0, v1, lay_off<32>(t), tw);
-    own_sync<WL>();
-    to_lds<32>(x, v0, t);
-    to_lds<32>(x1, v1, t);
-    __syncthreads();
-    from_lds<512>(x, v0, t);
-    from_lds<512>(x1, v1, t);
-    net16x2<true, 512>(v0, v1, lay_off<512>(t), tw);
-}
-}  // namespace t13
-
 // TILED: source and destination tile-major (k_ntt_s9b TILE): element e of 8192-run b (b < 512) at
 // (e / 32) * 16384 + b * 32 + e % 32 -- the strided passes on either side then move contiguous 64 KB tiles,
 // and this VALU-bound kernel takes the 128-B segments instead
@@ -613,57 +547,12 @@ __device__ __forceinline__ uint32_t tiled13(uint32_t b, uint32_t t, uint32_t j) 
     return ((t >> 5) + 16 * j) * 16384u + b * 32u + (t & 31);
 }
 
-template <bool TILED, bool WL>
-__global__ __launch_bounds__(t13::NTH, 4) void k_lde_fused13(const uint32_t *src, uint32_t *dst, ColMap ms,
-                                                            ColMap md, int L, const uint32_t *__restrict__ tt_inv,
-                                                            const uint32_t *__restrict__ tt_fwd, Twist tws,
-                                                            uint64_t dst_half) {
-    using namespace t13;
-    __shared__ uint32_t x[2 * LDS13];
-    const uint32_t t = threadIdx.x;
-    const uint32_t base = TILED ? 0u : blockIdx.x * 8192u;
-    const uint32_t *sp = src + ms.off(blockIdx.y) + base;
-    uint32_t v0[16], v1[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) v0[j] = sp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)];
-    dif13<WL>(v0, x, t, tt_inv);
-    {
-        const uint32_t g0 = tws.g0[blockIdx.x], g1 = tws.g1[blockIdx.x];
-        const uint4 *u0 = (const uint4 *)(tws.u0 + t * 16), *u1 = (const uint4 *)(tws.u1 + t * 16);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint4 a = u0[q], b = u1[q];
-            const uint32_t au[4] = {a.x, a.y, a.z, a.w}, bu[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const uint32_t c = v0[4 * q + r];
-                v1[4 * q + r] = mul(mul_lazy(c, g1), bu[r]);
-                v0[4 * q + r] = mul(mul_lazy(c, g0), au[r]);
-            }
-        }
-    }
-    dit13x2<WL>(v0, v1, x, t, tt_fwd);
-    uint32_t *dp = dst + md.off(blockIdx.y) + base;
-    // an intermediate: default policy (ZKM_LDE_MID_AUX above; non-temporal measured -0.6 % with 16-column batches,
-    // profiles/r05_ntt_nt_store_ab.txt)
-#if ZKM_LDE_MID_AUX
-#define ZKM_ST13(v, p) __builtin_nontemporal_store(v, p)
-#else
-#define ZKM_ST13(v, p) (*(p) = (v))
-#endif
-#pragma unroll
-    for (int j = 0; j < 16; j++) ZKM_ST13(v0[j], &dp[TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j)]);
-#pragma unroll
-    for (int j = 0; j < 16; j++) ZKM_ST13(v1[j], &dp[dst_half + (TILED ? tiled13(blockIdx.x, t, j) : lay_idx<512>(t, j))]);
-#undef ZKM_ST13
-}
-
-// Sequential-coset form (the default; ZKM_T13_SEQ=0 selects k_lde_fused13): the coefficients stay in registers
-// while each coset is twisted, transformed and stored in turn through ONE 34.8 KB LDS tile, so a workgroup needs
-// half the LDS and fewer registers than k_lde_fused13 (no second 16-element state, no twiddle set held across
-// two transforms): 64 VGPRs, four workgroups (32 waves) per CU instead of two, for one more workgroup barrier and
-// the twiddle loads done twice.  Per 8-column batch of a 2^22 LDE 202 vs 208 us, LDE 2^22 x 67 -0.8 %
-// (profiles/r05_t13_seq_ab.txt): doubling the waves barely moves it, the tile is at ~0.74 of the VALU issue rate.
+// Fused middle of the natural-input LDE for transforms larger than one tile (k_lde_fused13s): the iNTT's last 13
+// (DIF) stages, both coset twists and the forward transforms' first 13 (DIT) stages.  The coefficients stay in
+// registers while each coset is twisted, transformed and stored in turn through ONE 34.8 KB LDS tile: 64 VGPRs,
+// four workgroups (32 waves) per CU.  Against round 5's two-coset form (both cosets in registers at once, twice
+// the LDS; deleted after its A/B, git history keeps it): per 8-column batch of a 2^22 LDE 202 vs 208 us, LDE
+// 2^22 x 67 -0.8 % (profiles/r05_t13_seq_ab.txt); the tile is at ~0.74 of the VALU issue rate.
 namespace t13 {
 // net16 with each stage's twiddles loaded just before the stage (at most 8 live instead of 15)
 template <bool DIT, int SE>
@@ -1079,39 +968,6 @@ __device__ __forceinline__ uint32_t atb(uint32_t r, uint32_t t) {
     else return r * 32 + t;
 }
 
-// three stages of one network; twiddle w_{2h}^{(off + rs m) S + ct} read at voff = (off S + ct) * 4
-// plus the uniform soff0 + (h + rs m S) * 4
-template <bool DIT, int LAY>
-__device__ __forceinline__ void net8b(uint32_t *v, __amdgpu_buffer_rsrc_t rtw, uint32_t voff, uint32_t soff0,
-                                      uint32_t S4) {
-    constexpr uint32_t rs = RS<LAY>;
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-        const int st = DIT ? q : 2 - q;
-        const int span = 1 << st;
-#pragma unroll
-        for (int m = 0; m < span; m++) {
-            const uint32_t w = bld(rtw, voff, soff0 + (rs * (uint32_t)(span + m)) * S4);
-#pragma unroll
-            for (int k = m; k < 8; k += 2 * span) {
-                const uint32_t a = v[k], b = v[k + span];
-                if (DIT) {
-                    const uint32_t tt = mul(b, w);
-                    if (q < 2 && ((k >> (st + 1)) & 1)) {
-                        v[k] = a + tt;
-                        v[k + span] = a + (P - tt);
-                    } else {
-                        v[k] = add(a, tt);
-                        v[k + span] = sub(a, tt);
-                    }
-                } else {
-                    v[k] = add(a, b);
-                    v[k + span] = mul(a + (P - b), w);
-                }
-            }
-        }
-    }
-}
 // The same network with its twiddles generated in registers from ONE loaded value.  Stage st of the network
 // (half-size h = rs 2^st S rows) uses w_{st,m} = w_{2h}^{(off + rs m) S + ct} = w_{st,0} * w_{2^(st+1)}^m, and
 // w_{st,0} = w_{st+1,0}^2 (the same exponent, a root of half the order); so only w_{2,0} is read and the other
@@ -1166,13 +1022,12 @@ __device__ __forceinline__ void net8r(uint32_t *v, const Tw8 &W) {
         }
     }
 }
-// one network's stages: twiddles loaded (net8b) or generated from w_{2,0} (net8r); the top twiddle sits at
-// voff + soff0 + 4 rs S words
-template <bool DIT, int LAY, bool TWG>
+// one network's stages, twiddles generated from w_{2,0}, which sits at voff + soff0 + 4 rs S words (the form that
+// loaded all seven per network lost its A/B: 3.94 vs 3.93 ms for the 2^22 x 67 LDE, round 5)
+template <bool DIT, int LAY>
 __device__ __forceinline__ void net8x(uint32_t *v, __amdgpu_buffer_rsrc_t rtw, uint32_t voff, uint32_t soff0,
                                       uint32_t S4, const TwC &c) {
-    if constexpr (TWG) net8r<DIT>(v, tw8(bld(rtw, voff, soff0 + 4 * RS<LAY> * S4), c));
-    else net8b<DIT, LAY>(v, rtw, voff, soff0, S4);
+    net8r<DIT>(v, tw8(bld(rtw, voff, soff0 + 4 * RS<LAY> * S4), c));
 }
 
 template <int LAY, bool SWZ>
@@ -1193,8 +1048,8 @@ __device__ __forceinline__ void from_ldsb(const uint32_t *x, uint32_t v[16], uin
 
 // TILE (bit 0: source, bit 1: destination; only for the one-pass case 512 x S = the column): that side is
 // tile-major -- the tile's 512 rows x 32 columns contiguous (64 KB, row pitch 32 words) at tile index
-// c0 / 32 -- instead of row-major with pitch S (the LDE's intermediates, lde_natural ZKM_LDE_TILED).
-template <bool DIT, int MODE, int TILE = 0, bool TWG = true>
+// c0 / 32 -- instead of row-major with pitch S (the LDE's intermediates at 2^22, lde_natural).
+template <bool DIT, int MODE, int TILE = 0>
 __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                         int logS, const uint32_t *__restrict__ tw,
                                                         uint32_t tw_words, uint32_t nv, int remap) {
@@ -1218,7 +1073,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
     const uint64_t tbase = (uint64_t)(c0 >> 5) * (512u * 32u);  // tile-major: the tile's 64 KB
     const auto rsrc = TS ? mkrs(src + ms.off(col) + tbase, 512u * 128u) : mkrs(src + ms.off(col) + base, 512u * S4);
     const auto rtw = mkrs(tw, tw_words * 4);
-    const TwC twk = TWG ? twc(tw) : TwC{};
+    const TwC twk = twc(tw);
     const uint32_t vLL = ct * 4;                    // twiddle offsets per layout / network
     const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4, vLM1 = (((2 * u + 1) & 7) * S + ct) * 4;
     const uint32_t vLH = (u * S + ct) * 4;          // also rows u + 32 n + 64 k of the tile
@@ -1233,25 +1088,22 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
         for (int n = 0; n < 2; n++)
 #pragma unroll
             for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, sL16, (uint32_t)(8 * n + k) * sP4);
-        if constexpr (TWG) {  // both networks of LL share their twiddles (off = 0)
+        {  // both networks of LL share their twiddles (off = 0)
             const Tw8 W = tw8(bld(rtw, vLL, 4 * S4), twk);
             net8r<true>(v, W);
             net8r<true>(v + 8, W);
-        } else {
-            net8b<true, LL>(v, rtw, vLL, 0, S4);
-            net8b<true, LL>(v + 8, rtw, vLL, 0, S4);
         }
         to_ldsb<LL, false>(x, v, u, t);
         __syncthreads();
         from_ldsb<LM, false>(x, v, u, t);
-        net8x<true, LM, TWG>(v, rtw, vLM0, 0, S4, twk);
-        net8x<true, LM, TWG>(v + 8, rtw, vLM1, 0, S4, twk);
+        net8x<true, LM>(v, rtw, vLM0, 0, S4, twk);
+        net8x<true, LM>(v + 8, rtw, vLM1, 0, S4, twk);
         __syncthreads();
         to_ldsb<LM, false>(x, v, u, t);
         __syncthreads();
         from_ldsb<LH, false>(x, v, u, t);
-        net8x<true, LH, TWG>(v, rtw, vLH, 0, S4, twk);
-        net8x<true, LH, TWG>(v + 8, rtw, vLH, 32 * S4, S4, twk);
+        net8x<true, LH>(v, rtw, vLH, 0, S4, twk);
+        net8x<true, LH>(v + 8, rtw, vLH, 32 * S4, S4, twk);
         if (MODE == MODE_PLAIN) {
             const auto rdst = TD ? mkrs(dst + md.off(col) + tbase, 512u * 128u) : mkrs(dst + md.off(col) + base, 512u * S4);
 #pragma unroll
@@ -1277,24 +1129,21 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
         for (int n = 0; n < 2; n++)
 #pragma unroll
             for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, sLH, (uint32_t)(32 * n + 64 * k) * sP4);
-        net8x<false, LH, TWG>(v, rtw, vLH, 0, S4, twk);
-        net8x<false, LH, TWG>(v + 8, rtw, vLH, 32 * S4, S4, twk);
+        net8x<false, LH>(v, rtw, vLH, 0, S4, twk);
+        net8x<false, LH>(v + 8, rtw, vLH, 32 * S4, S4, twk);
         to_ldsb<LH, false>(x, v, u, t);
         __syncthreads();
         from_ldsb<LM, false>(x, v, u, t);
-        net8x<false, LM, TWG>(v, rtw, vLM0, 0, S4, twk);
-        net8x<false, LM, TWG>(v + 8, rtw, vLM1, 0, S4, twk);
+        net8x<false, LM>(v, rtw, vLM0, 0, S4, twk);
+        net8x<false, LM>(v + 8, rtw, vLM1, 0, S4, twk);
         __syncthreads();
         to_ldsb<LM, false>(x, v, u, t);
         __syncthreads();
         from_ldsb<LL, false>(x, v, u, t);
-        if constexpr (TWG) {  // both networks of LL share their twiddles (off = 0)
+        {  // both networks of LL share their twiddles (off = 0)
             const Tw8 W = tw8(bld(rtw, vLL, 4 * S4), twk);
             net8r<false>(v, W);
             net8r<false>(v + 8, W);
-        } else {
-            net8b<false, LL>(v, rtw, vLL, 0, S4);
-            net8b<false, LL>(v + 8, rtw, vLL, 0, S4);
         }
         const auto rdst = TD ? mkrs(dst + md.off(col) + tbase, 512u * 128u) : mkrs(dst + md.off(col) + base, 512u * S4);
 #pragma unroll
@@ -1304,369 +1153,6 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
     }
 }
 
-// Two-column form of k_ntt_s9b: the same 512-row x 32-column tile and nine stages, but each thread holds
-// 8 rows of TWO adjacent columns (lane t' = tid & 15 -> columns c0 + 2t', c0 + 2t' + 1; u = tid >> 4 ->
-// one radix-8 network per column in the layouts LL / LM / LH with g = u), so every data and twiddle access
-// is one 8-byte buffer op (the twiddles of adjacent columns are adjacent in the table) and the LDS exchanges
-// are 8-byte: half the vector-memory and LDS instructions of k_ntt_s9b for the same bytes.  LDS rows are
-// stored at row ^ bit3(row) (a permutation of the tile's rows), so the two rows a 32-lane half touches in
-// every layout fall in different halves of the 64 banks.
-namespace s9 {
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u32x2 bld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
-}
-__device__ __forceinline__ void bst2(u32x2 v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, 0);
-}
-__device__ __forceinline__ uint32_t atc(uint32_t r, uint32_t c) { return (r ^ ((r >> 3) & 1)) * 32 + c; }
-template <int LAY>
-__device__ __forceinline__ uint32_t row0c(uint32_t u) {
-    if constexpr (LAY == LH) return u;
-    else if constexpr (LAY == LM) return (u >> 3) * 64 + (u & 7);
-    else return 8 * u;
-}
-// three stages of the radix-8 networks of both columns; twiddle pair at voff + soff0 + (rs (span + m)) S4
-template <bool DIT, int LAY>
-__device__ __forceinline__ void net8c(uint32_t *v0, uint32_t *v1, __amdgpu_buffer_rsrc_t rtw, uint32_t voff,
-                                      uint32_t S4) {
-    constexpr uint32_t rs = RS<LAY>;
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-        const int st = DIT ? q : 2 - q;
-        const int span = 1 << st;
-#pragma unroll
-        for (int m = 0; m < span; m++) {
-            const u32x2 w = bld2(rtw, voff, (rs * (uint32_t)(span + m)) * S4);
-#pragma unroll
-            for (int k = m; k < 8; k += 2 * span) {
-#pragma unroll
-                for (int c = 0; c < 2; c++) {
-                    uint32_t *v = c ? v1 : v0;
-                    const uint32_t wc = c ? w.y : w.x;
-                    const uint32_t a = v[k], b = v[k + span];
-                    if (DIT) {
-                        const uint32_t tt = mul(b, wc);
-                        if (q < 2 && ((k >> (st + 1)) & 1)) {
-                            v[k] = a + tt;
-                            v[k + span] = a + (P - tt);
-                        } else {
-                            v[k] = add(a, tt);
-                            v[k + span] = sub(a, tt);
-                        }
-                    } else {
-                        v[k] = add(a, b);
-                        v[k + span] = mul(a + (P - b), wc);
-                    }
-                }
-            }
-        }
-    }
-}
-template <int LAY>
-__device__ __forceinline__ void to_ldsc(uint32_t *x, const uint32_t *v0, const uint32_t *v1, uint32_t u, uint32_t c) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        u32x2 p;
-        p.x = v0[k];
-        p.y = v1[k];
-        *(u32x2 *)&x[atc(row0c<LAY>(u) + RS<LAY> * k, c)] = p;
-    }
-}
-template <int LAY>
-__device__ __forceinline__ void from_ldsc(const uint32_t *x, uint32_t *v0, uint32_t *v1, uint32_t u, uint32_t c) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const u32x2 p = *(const u32x2 *)&x[atc(row0c<LAY>(u) + RS<LAY> * k, c)];
-        v0[k] = p.x;
-        v1[k] = p.y;
-    }
-}
-}  // namespace s9
-
-template <bool DIT, int MODE>
-__global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9c(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
-                                                        int logS, const uint32_t *__restrict__ tw,
-                                                        uint32_t tw_words, uint32_t nv, int remap) {
-    using namespace s9;
-    __shared__ uint32_t x[512 * 32];
-    const uint32_t S = 1u << logS, S4 = S * 4;
-    const uint32_t total = gridDim.x, lin = blockIdx.x;
-    const uint32_t vid = (total & 7) ? lin : (lin & 7) * (total >> 3) + (lin >> 3);
-    const uint32_t ntile = total / nv;
-    const uint32_t col = remap ? vid % nv : lin / ntile, tile = remap ? vid / nv : lin % ntile;
-    const uint32_t outer = tile >> (logS - 5);
-    const uint32_t c0 = (tile & ((S >> 5) - 1)) * 32;
-    const uint32_t base = outer * 512u * S;
-    const uint32_t c = 2 * (threadIdx.x & 15), u = threadIdx.x >> 4;
-    const uint32_t ct = c0 + c;
-    const auto rsrc = mkrs(src + ms.off(col) + base, 512u * S4);
-    const auto rtw = mkrs(tw, tw_words * 4);
-    const uint32_t vLL = ct * 4, vLM = ((u & 7) * S + ct) * 4, vLH = (u * S + ct) * 4;
-    const uint32_t vL8 = (8 * u * S + ct) * 4;  // rows 8u + k
-    uint32_t v0[8], v1[8];
-    if (DIT) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const u32x2 p = bld2(rsrc, vL8, (uint32_t)k * S4);
-            v0[k] = p.x;
-            v1[k] = p.y;
-        }
-        net8c<true, LL>(v0, v1, rtw, vLL, S4);
-        to_ldsc<LL>(x, v0, v1, u, c);
-        __syncthreads();
-        from_ldsc<LM>(x, v0, v1, u, c);
-        net8c<true, LM>(v0, v1, rtw, vLM, S4);
-        __syncthreads();
-        to_ldsc<LM>(x, v0, v1, u, c);
-        __syncthreads();
-        from_ldsc<LH>(x, v0, v1, u, c);
-        net8c<true, LH>(v0, v1, rtw, vLH, S4);
-        if (MODE == MODE_PLAIN) {
-            const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                u32x2 p;
-                p.x = v0[k];
-                p.y = v1[k];
-                bst2(p, rdst, vLH, (uint32_t)(64 * k) * S4);
-            }
-        } else {  // BITREV_OUT through the swizzled tile of k_ntt_s9b
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t r = row0c<LH>(u) + 64 * k;
-                x[atb<true>(r, c)] = v0[k];
-                x[atb<true>(r, c + 1)] = v1[k];
-            }
-            __syncthreads();
-            const auto rdst = mkrs(dst + md.off(col), 512u * S4);
-            const uint32_t q = threadIdx.x & 511, hb = threadIdx.x >> 9, rq = rev_bits(q, 9);
-            const uint32_t vo = (((rev_bits(c0, logS) + (hb << (logS - 1))) << 9) + q) * 4;
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t tc = 2 * i + hb;
-                const uint32_t so = (rev_bits((uint32_t)(2 * i), 5) << (logS - 5)) << 11;
-                bst(x[atb<true>(rq, tc)], rdst, vo, so);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const u32x2 p = bld2(rsrc, vLH, (uint32_t)(64 * k) * S4);
-            v0[k] = p.x;
-            v1[k] = p.y;
-        }
-        net8c<false, LH>(v0, v1, rtw, vLH, S4);
-        to_ldsc<LH>(x, v0, v1, u, c);
-        __syncthreads();
-        from_ldsc<LM>(x, v0, v1, u, c);
-        net8c<false, LM>(v0, v1, rtw, vLM, S4);
-        __syncthreads();
-        to_ldsc<LM>(x, v0, v1, u, c);
-        __syncthreads();
-        from_ldsc<LL>(x, v0, v1, u, c);
-        net8c<false, LL>(v0, v1, rtw, vLL, S4);
-        const auto rdst = mkrs(dst + md.off(col) + base, 512u * S4);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            u32x2 p;
-            p.x = v0[k];
-            p.y = v1[k];
-            bst2(p, rdst, vL8, (uint32_t)k * S4);
-        }
-    }
-}
-
-// Persistent prefetching form of k_ntt_s9b (same tiles, TILE sides, register-generated twiddles; opt-in
-// ZKM_NTT_PF = workgroups per CU): each workgroup walks the work items lin = blockIdx.x, + gridDim.x, ...
-// (gridDim.x a multiple of 8, so every item stays on XCD lin mod 8 under k_ntt_s9b's remap) and keeps the NEXT
-// item's 16 loads in flight while it computes the current one.  vmcnt retires in issue order, so the item's
-// twiddle loads go out before the prefetch (a scheduling barrier keeps them there) and the barriers fence LDS
-// only ("local"), so the prefetch is not drained at them; 57-61 VGPRs, no spills, two workgroups per CU.  The
-// waits in the ISA are the intended ones, and still the LDE runs 2-3 % slower with PF=2 and 12 % with PF=1
-// (profiles/r05_ntt_prefetch_ab.txt): like round 3's k_ntt_s9p (which drained its prefetch at every wait), the
-// one-item-per-workgroup kernel with two resident workgroups already keeps HBM as busy as this layout allows.
-namespace s9 {
-__device__ __forceinline__ void lds_bar() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// a * b with b wave-uniform, read from an SGPR (the "v" operands of prod64 would pin a VGPR copy of every such
-// constant for the whole kernel -- six of them in k_ntt_s9q, which runs at the 64-VGPR limit)
-__device__ __forceinline__ uint32_t mul_s(uint32_t a, uint32_t b) {
-    uint64_t p, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(cc) : "v"(a), "s"(b));
-    return redc(p);
-}
-__device__ __forceinline__ Tw8 tw8s(uint32_t wtop, const TwC &c) {
-    Tw8 r;
-    r.w[2][0] = wtop;
-    r.w[1][0] = mul(wtop, wtop);
-    r.w[0][0] = mul(r.w[1][0], r.w[1][0]);
-    r.w[1][1] = mul_s(r.w[1][0], c.w4);
-#pragma unroll
-    for (int m = 1; m < 4; m++) r.w[2][m] = mul_s(wtop, c.w8[m - 1]);
-    return r;
-}
-
-template <bool DIT, int MODE, int TILE>
-struct S9Q {
-    static constexpr bool SWZ = DIT && MODE == MODE_BITREV_OUT;
-    static constexpr bool TS = TILE & 1, TD = (TILE & 2) != 0;
-    const uint32_t *src;
-    uint32_t *dst;
-    ColMap ms, md;
-    int logS;
-    uint32_t S, S4, nv, total, t, u;
-    __amdgpu_buffer_rsrc_t rtw;
-    TwC twk;
-    uint32_t w64, w16;
-
-    struct Item {
-        uint32_t col, c0, base, ct;
-        uint64_t tbase;
-    };
-    __device__ __forceinline__ Item item(uint32_t lin, uint32_t t) const {
-        const uint32_t vid = (lin & 7) * (total >> 3) + (lin >> 3);
-        Item it;
-        it.col = vid % nv;
-        const uint32_t tile = vid / nv;
-        it.c0 = (tile & ((S >> 5) - 1)) * 32;
-        it.base = (tile >> (logS - 5)) * 512u * S;
-        it.ct = it.c0 + t;
-        it.tbase = (uint64_t)(it.c0 >> 5) * (512u * 32u);
-        return it;
-    }
-    // live = false (past the last item): 16 loads of one cached word, so that every step has the same loads in
-    // flight and the waits can count them (a conditional prefetch makes the waits assume the worst path)
-    __device__ __forceinline__ void load(uint32_t lin, uint32_t (&v)[16], bool live = true) const {
-        const Item it = item(lin, t);
-        const auto rsrc = TS ? mkrs(src + ms.off(it.col) + it.tbase, 512u * 128u)
-                             : mkrs(src + ms.off(it.col) + it.base, 512u * S4);
-        const uint32_t sP4 = !live ? 0u : TS ? 128u : S4;
-        if (DIT) {
-            const uint32_t sL16 = TS ? (16 * u * 32 + t) * 4 : (16 * u * S + it.ct) * 4;
-#pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = bld(rsrc, sL16, (uint32_t)k * sP4);
-        } else {
-            const uint32_t sLH = TS ? (u * 32 + t) * 4 : (u * S + it.ct) * 4;
-#pragma unroll
-            for (int n = 0; n < 2; n++)
-#pragma unroll
-                for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, sLH, (uint32_t)(32 * n + 64 * k) * sP4);
-        }
-    }
-    // one work item on v, with the next item's loads into vn in flight
-    __device__ __forceinline__ void step(uint32_t *x, uint32_t lin, uint32_t (&v)[16], uint32_t (&vn)[16]) const {
-        // per-item copies of the lane coordinates, opaque to the compiler: the LDS and global addresses derived from
-        // them are recomputed in every item instead of being hoisted out of the item loop into ~16 live registers
-        uint32_t t = this->t, u = this->u;
-        asm volatile("" : "+v"(t), "+v"(u));
-        const Item it = item(lin, t);
-        const uint32_t ct = it.ct;
-        const uint32_t vLL = ct * 4;
-        const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4;
-        const uint32_t vLH = (u * S + ct) * 4;
-        // the top twiddles (net8x's TWG form) before the prefetch; each layout's second network is one row
-        // offset further (LM: +1 row of h = 32 S, LH: +32 rows of h = 256 S), i.e. its top twiddle is the first's
-        // times w_64 = tw[33] or w_16 = tw[9]
-        const uint32_t wLL = bld(rtw, vLL, 4 * S4), wLM0 = bld(rtw, vLM0, 32 * S4), wLH0 = bld(rtw, vLH, 256 * S4);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t nxt = lin + gridDim.x;
-        load(nxt < total ? nxt : lin, vn, nxt < total);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t wLM1 = mul_s(wLM0, w64), wLH1 = mul_s(wLH0, w16);
-        lds_bar();  // the previous item's last LDS reads are done
-        if (DIT) {
-            const Tw8 W = tw8s(wLL, twk);
-            net8r<true>(v, W);
-            net8r<true>(v + 8, W);
-            to_ldsb<LL, false>(x, v, u, t);
-            lds_bar();
-            from_ldsb<LM, false>(x, v, u, t);
-            net8r<true>(v, tw8s(wLM0, twk));
-            net8r<true>(v + 8, tw8s(wLM1, twk));
-            lds_bar();
-            to_ldsb<LM, false>(x, v, u, t);
-            lds_bar();
-            from_ldsb<LH, false>(x, v, u, t);
-            net8r<true>(v, tw8s(wLH0, twk));
-            net8r<true>(v + 8, tw8s(wLH1, twk));
-            if (MODE == MODE_PLAIN) {
-                const auto rdst = TD ? mkrs(dst + md.off(it.col) + it.tbase, 512u * 128u)
-                                     : mkrs(dst + md.off(it.col) + it.base, 512u * S4);
-                const uint32_t dP4 = TD ? 128u : S4, dLH = TD ? (u * 32 + t) * 4 : vLH;
-#pragma unroll
-                for (int n = 0; n < 2; n++)
-#pragma unroll
-                    for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, dLH, (uint32_t)(32 * n + 64 * k) * dP4);
-            } else {  // BITREV_OUT (as k_ntt_s9b)
-                lds_bar();
-                to_ldsb<LH, SWZ>(x, v, u, t);
-                lds_bar();
-                const auto rdst = mkrs(dst + md.off(it.col), 512u * S4);
-                const uint32_t q = (u << 5 | t) & 511, hb = u >> 4, rq = rev_bits(q, 9);
-                const uint32_t vo = (((rev_bits(it.c0, logS) + (hb << (logS - 1))) << 9) + q) * 4;
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const uint32_t tc = 2 * i + hb;
-                    const uint32_t so = (rev_bits((uint32_t)(2 * i), 5) << (logS - 5)) << 11;
-                    bst(x[atb<SWZ>(rq, tc)], rdst, vo, so);
-                }
-            }
-        } else {
-            net8r<false>(v, tw8s(wLH0, twk));
-            net8r<false>(v + 8, tw8s(wLH1, twk));
-            to_ldsb<LH, false>(x, v, u, t);
-            lds_bar();
-            from_ldsb<LM, false>(x, v, u, t);
-            net8r<false>(v, tw8s(wLM0, twk));
-            net8r<false>(v + 8, tw8s(wLM1, twk));
-            lds_bar();
-            to_ldsb<LM, false>(x, v, u, t);
-            lds_bar();
-            from_ldsb<LL, false>(x, v, u, t);
-            const Tw8 W = tw8s(wLL, twk);
-            net8r<false>(v, W);
-            net8r<false>(v + 8, W);
-            const auto rdst = TD ? mkrs(dst + md.off(it.col) + it.tbase, 512u * 128u)
-                                 : mkrs(dst + md.off(it.col) + it.base, 512u * S4);
-            const uint32_t dP4 = TD ? 128u : S4, dL16 = TD ? (16 * u * 32 + t) * 4 : (16 * u * S + ct) * 4;
-#pragma unroll
-            for (int n = 0; n < 2; n++)
-#pragma unroll
-                for (int k = 0; k < 8; k++) bst(v[8 * n + k], rdst, dL16, (uint32_t)(8 * n + k) * dP4);
-        }
-    }
-};
-}  // namespace s9
-
-template <bool DIT, int MODE, int TILE, int MINW>
-__global__ __launch_bounds__(s9::NTH, MINW) void k_ntt_s9q(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
-                                                        int logS, const uint32_t *__restrict__ tw, uint32_t tw_words,
-                                                        uint32_t nv, uint32_t total) {
-    using namespace s9;
-    __shared__ uint32_t x[512 * 32];
-    S9Q<DIT, MODE, TILE> q{src, dst, ms, md, logS, 1u << logS, 4u << logS, nv, total, threadIdx.x & 31u,
-                           threadIdx.x >> 5, mkrs(tw, tw_words * 4), twc(tw), tw[33], tw[9]};
-    uint32_t va[16], vb[16];
-    uint32_t lin = blockIdx.x;  // gridDim.x <= total: every workgroup has an item
-    q.load(lin, va);
-    // (the copy waits on the prefetch just where the next item needs it; an unrolled ping-pong of va / vb, tried
-    // first, doubled the code and spilled more at the 64-VGPR limit)
-#pragma unroll 1
-    for (; lin < total; lin += gridDim.x) {
-        q.step(x, lin, va, vb);
-#pragma unroll
-        for (int k = 0; k < 16; k++) va[k] = vb[k];
-    }
-}
-
-// (k_lde_fused13s: global accesses through buffer descriptors -- a per-thread voffset and a uniform soffset per
-// element -- so the 16 element addresses of the tile-major layout, 1 MB apart, are not 16 live 64-bit pointers)
 template <bool TILED>
 __global__ __launch_bounds__(t13::NTH, 6) void k_lde_fused13s(const uint32_t *src, uint32_t *dst, ColMap ms,
                                                              ColMap md, int L, const uint32_t *__restrict__ tt_inv,
@@ -1713,37 +1199,6 @@ static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 column
 
 static int strided_T(int logR) { return logR >= 5 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
 
-// k_ntt_s9b with its twiddles generated in registers (default) or loaded per butterfly group
-// (ZKM_NTT_TWLOAD=1, the round-4 form: A/B knob)
-template <bool DIT, int MODE, int TL>
-static void launch_s9b(dim3 g1, hipStream_t s, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, int logS,
-                       const uint32_t *tw, uint32_t tw_words, uint32_t nv, int remap) {
-    static const bool twload = getenv("ZKM_NTT_TWLOAD") != nullptr;
-    // persistent prefetching form (A/B): ZKM_NTT_PF = workgroups per CU (0: one item per workgroup)
-    static const int pf = [] {
-        const char *e = getenv("ZKM_NTT_PF");
-        return e ? atoi(e) : 0;
-    }();
-    const uint32_t total = g1.x;
-    if (pf > 0 && !twload && remap && (total & 7) == 0) {
-        const uint32_t grid = std::min<uint32_t>(total, 256u * (uint32_t)pf) & ~7u;
-        // two workgroups per CU: 8 waves per SIMD, at most 64 VGPRs; one: 128
-        if (pf >= 2)
-            hipLaunchKernelGGL((k_ntt_s9q<DIT, MODE, TL, 8>), dim3(grid), dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
-                               tw, tw_words, nv, total);
-        else
-            hipLaunchKernelGGL((k_ntt_s9q<DIT, MODE, TL, 4>), dim3(grid), dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
-                               tw, tw_words, nv, total);
-        return;
-    }
-    if (twload)
-        hipLaunchKernelGGL((k_ntt_s9b<DIT, MODE, TL, false>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                           tw_words, nv, remap);
-    else
-        hipLaunchKernelGGL((k_ntt_s9b<DIT, MODE, TL, true>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                           tw_words, nv, remap);
-}
-
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
                         int logS, const uint32_t *tw, int mode, hipStream_t s, Twist tws = Twist{},
@@ -1753,47 +1208,22 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     ARG_CHECK(!tile || (logR == 9 && logS + 9 == L && tw_words && mode != MODE_TWIST_OUT),
               "tile-major sides need the one-pass 512-row strided kernel");
     dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
-    if (tile) {  // k_ntt_s9b with a tile-major source (bit 0) and / or destination (bit 1)
+    if (logR == 9 && tw_words && mode != MODE_TWIST_OUT) {
+        // buffer-addressed register tiles (k_ntt_s9b), one grid dimension: (tile, column) remapped in the
+        // kernel; tile-major source (bit 0) and / or destination (bit 1)
         const dim3 g1(g.x * nv);
-#define S9T(TL)                                                                                 \
-    if (!DIT)                                                                                   \
-        launch_s9b<false, MODE_PLAIN, TL>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, 1);  \
-    else if (mode == MODE_PLAIN)                                                                \
-        launch_s9b<true, MODE_PLAIN, TL>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, 1);   \
-    else                                                                                        \
-        launch_s9b<true, MODE_BITREV_OUT, TL>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, 1);
-        if (tile == 1) { S9T(1) } else if (tile == 2) { S9T(2) } else { S9T(3) }
-#undef S9T
-        HIP_CHECK(hipGetLastError());
-        return;
-    }
-    if (logR == 9 && tw_words && mode != MODE_TWIST_OUT) {  // buffer-addressed register tiles
-        const dim3 g1(g.x * nv);  // one dimension: (tile, column) remapped in the kernel
-        static const int remap = getenv("ZKM_NTT_NOREMAP") ? 0 : 1;  // A/B knob
-        // two-column tiles (8-byte accesses): ZKM_NTT_S9C=0 selects the one-column k_ntt_s9b (A/B knob)
-        static const int s9c = [] {
-            const char *e = getenv("ZKM_NTT_S9C");
-            return e ? atoi(e) : 0;
-        }();
-        if (s9c) {
-            if (!DIT)
-                hipLaunchKernelGGL((k_ntt_s9c<false, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                                   tw_words, nv, remap);
-            else if (mode == MODE_PLAIN)
-                hipLaunchKernelGGL((k_ntt_s9c<true, MODE_PLAIN>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,
-                                   tw_words, nv, remap);
-            else
-                hipLaunchKernelGGL((k_ntt_s9c<true, MODE_BITREV_OUT>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS,
-                                   tw, tw_words, nv, remap);
-            HIP_CHECK(hipGetLastError());
-            return;
-        }
-        if (!DIT)
-            launch_s9b<false, MODE_PLAIN, 0>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, remap);
-        else if (mode == MODE_PLAIN)
-            launch_s9b<true, MODE_PLAIN, 0>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, remap);
-        else
-            launch_s9b<true, MODE_BITREV_OUT, 0>(g1, s, src, dst, ms, md, logS, tw, tw_words, nv, remap);
+#define S9B(TL)                                                                                                   \
+    if (!DIT)                                                                                                     \
+        hipLaunchKernelGGL((k_ntt_s9b<false, MODE_PLAIN, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw, \
+                           tw_words, nv, 1);                                                                      \
+    else if (mode == MODE_PLAIN)                                                                                  \
+        hipLaunchKernelGGL((k_ntt_s9b<true, MODE_PLAIN, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, tw,  \
+                           tw_words, nv, 1);                                                                      \
+    else                                                                                                          \
+        hipLaunchKernelGGL((k_ntt_s9b<true, MODE_BITREV_OUT, TL>), g1, dim3(s9::NTH), 0, s, src, dst, ms, md, logS, \
+                           tw, tw_words, nv, 1);
+        if (tile == 1) { S9B(1) } else if (tile == 2) { S9B(2) } else if (tile == 3) { S9B(3) } else { S9B(0) }
+#undef S9B
         HIP_CHECK(hipGetLastError());
         return;
     }
@@ -1814,8 +1244,6 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
         return;
     }
     if (logR >= 5 && logR <= 8) {  // register tiles of 2^logR rows x 32 columns (k_ntt_sr)
-        static const bool generic = getenv("ZKM_NTT_GENERIC8") && atoi(getenv("ZKM_NTT_GENERIC8"));  // A/B knob
-        if (!generic) {
 #define SRL(LR)                                                                                                   \
     if (!DIT)                                                                                                     \
         hipLaunchKernelGGL((k_ntt_sr<LR, false, MODE_PLAIN>), g, dim3(2 << LR), 0, s, src, dst, ms, md, logS, tw, tws, \
@@ -1829,13 +1257,10 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     else                                                                                                          \
         hipLaunchKernelGGL((k_ntt_sr<LR, true, MODE_BITREV_OUT>), g, dim3(2 << LR), 0, s, src, dst, ms, md, logS, tw,  \
                            tws, dst_half);
-            if (logR == 8) { SRL(8) } else if (logR == 7) { SRL(7) } else if (logR == 6) { SRL(6) } else { SRL(5) }
+        if (logR == 8) { SRL(8) } else if (logR == 7) { SRL(7) } else if (logR == 6) { SRL(6) } else { SRL(5) }
 #undef SRL
-            HIP_CHECK(hipGetLastError());
-            return;
-        }
-        ARG_CHECK((1 << logS) >= 64, "strided pass narrower than its tile");
-        g.x = (unsigned)(((1ull << L) >> logR) / 64);  // the generic kernel's 64-column tiles
+        HIP_CHECK(hipGetLastError());
+        return;
     }
 #define SCASE(k, t)                                                                                             \
     case k:                                                                                                     \
@@ -1843,8 +1268,7 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
                            dst_half);                                                                           \
         break;
     switch (logR) {
-        SCASE(1, 64) SCASE(2, 64) SCASE(3, 64) SCASE(4, 64) SCASE(5, 64) SCASE(6, 64) SCASE(7, 64) SCASE(8, 64)
-        SCASE(9, 32)
+        SCASE(1, 64) SCASE(2, 64) SCASE(3, 64) SCASE(4, 64)
         default: throw ArgError("bad strided radix");
     }
 #undef SCASE
@@ -1887,20 +1311,9 @@ static void run_fused(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, C
 }
 
 // strided pass radices for the bits above the contiguous tile (top to bottom, i.e. DIF order): the 13-stage tile and
-// the rest in passes of at most 9 stages.  ZKM_LDE_PLAN=1 (A/B): a 9-stage pass first and the tile taking the rest
-// -- faster only at 2^20 while that height's 7-stage pass was the LDS-staged kernel; with the register-tiled
-// k_ntt_sr the balanced plan wins there too (profiles/r05_lde_plan_ab.txt, r05_lde_s8_ab.txt)
+// the rest in balanced passes of at most 9 stages (a 9-stage pass first with an 11-stage tile was the faster 2^20
+// plan only while that height's 7-stage pass was LDS-staged: profiles/r05_lde_plan_ab.txt, r05_lde_s8_ab.txt)
 static std::vector<int> strided_plan(int L, int &logC) {
-    static const int plan = [] {
-        const char *e = getenv("ZKM_LDE_PLAN");
-        return e ? atoi(e) : 0;
-    }();
-    if (plan == 1 && L >= 14 && L != 22) {  // (the 9-stage pass needs L - 9 >= 5)
-        logC = L - 9 < LOGC ? L - 9 : LOGC;
-        std::vector<int> p{9};
-        if (L - 9 - logC > 0) p.push_back(L - 9 - logC);
-        return p;
-    }
     logC = L < LOGC ? L : LOGC;
     int rem = L - logC;
     std::vector<int> p;
@@ -2078,12 +1491,8 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
     DBuf winv(nsh > 1 ? N * cb : 0, s);
     // the intermediates tile-major (the one-strided-pass size, 2^22): the strided passes read / write whole
     // 64 KB tiles, the VALU-bound fused pass takes the 128-B segments: LDE 4.05-4.13 -> 3.92-3.94 ms for 2^22 x 67
-    // (profiles/r04_lde_tiled_plain_ab.txt; the pattern alone: profiles/r04_tile_probe.txt); ZKM_LDE_TILED=0 row-major
-    static const int tiled_env = [] {
-        const char *e = getenv("ZKM_LDE_TILED");
-        return e ? atoi(e) : 1;
-    }();
-    const bool tiled = tiled_env && nsh == 1 && logC == 13 && sp.size() == 1 && sp[0] == 9;  // (the tested case)
+    // (profiles/r04_lde_tiled_plain_ab.txt; the pattern alone: profiles/r04_tile_probe.txt)
+    const bool tiled = nsh == 1 && logC == 13 && sp.size() == 1 && sp[0] == 9;
     for (uint32_t c0 = 0; c0 < nv; c0 += cb) {
         const uint32_t nb = std::min(cb, nv - c0);
         const uint32_t *in = src.d + (uint64_t)c0 * N;
@@ -2103,17 +1512,7 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
             const Twist tws = get_twist(c, N, L, shifts[e], s);
             uint32_t *out = dst_d + (uint64_t)c0 * dst_stride + e * half_off;
             if (logC == 13) {
-                static const bool barriers = [] {
-                    const char *e = getenv("ZKM_T13_BARRIERS");
-                    return e && atoi(e) != 0;
-                }();
-                static const bool seq = [] {  // sequential cosets (default) or both at once (ZKM_T13_SEQ=0)
-                    const char *e = getenv("ZKM_T13_SEQ");
-                    return !e || atoi(e) != 0;
-                }();
-                auto k = seq ? (tiled ? k_lde_fused13s<true> : k_lde_fused13s<false>)
-                         : tiled ? (barriers ? k_lde_fused13<true, false> : k_lde_fused13<true, true>)
-                                 : (barriers ? k_lde_fused13<false, false> : k_lde_fused13<false, true>);
+                auto k = tiled ? k_lde_fused13s<true> : k_lde_fused13s<false>;
                 hipLaunchKernelGGL(k, dim3((unsigned)(N >> 13), nb), dim3(t13::NTH), 0, s, ibuf, work.p, m_i, m_w1, L,
                                    c.tt_inv, c.tt_fwd, tws, N);
                 HIP_CHECK(hipGetLastError());

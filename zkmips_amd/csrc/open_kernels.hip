@@ -511,12 +511,6 @@ __device__ __forceinline__ void open_dot_lds(const uint64_t *__restrict__ cols, 
         __syncthreads();  // red is reused by the next column block
     }
 }
-__global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
-                                                 OpenWeights pw, int with_next, int nseg, uint32_t slab,
-                                                 uint32_t *partial) {
-    open_dot_lds(cols, ncols, n, pw, with_next, nseg, slab, partial, blockIdx.x, blockIdx.y);
-}
-
 // Full segments (n a multiple of OPEN_SEG): thread t owns rows 4t..4t+3 and 4(NT + t)..+3 of its segment
 // for every column, so it computes those eight weights once (Montgomery's trick over the eight, one EF
 // inversion) and keeps them in registers: no LDS weight table, two 16-byte loads per column and thread
@@ -524,90 +518,7 @@ __global__ __launch_bounds__(NT) void k_open_dot(const uint64_t *__restrict__ co
 // lane (the wave's last lane loads it).  The per-thread sums of a column block are reduced through LDS
 // (eight threads per output word, 32 partial sums each) instead of a 6-step shuffle tree per word.
 static constexpr int OPEN_RED_LD = NT + 8;  // padded row: the eight outputs a wave sums sit on distinct banks
-__device__ __forceinline__ void open_dot_regs(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
-                                                      OpenWeights pw, int with_next, int nseg, uint32_t slab,
-                                                      uint32_t *partial, uint32_t bx, uint32_t by) {
-    __shared__ uint32_t red[OPEN_CB * 8][OPEN_RED_LD];
-    const uint64_t j0 = (uint64_t)bx * OPEN_SEG;
-    const uint32_t t = threadIdx.x, lane = t & 63;
-    const uint32_t ra = 4 * t, rb = 4 * NT + 4 * t;
-    ef w[8];
-    {
-        uint32_t om[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint64_t i = j0 + (k < 4 ? ra + k : rb + k - 4);
-            om[k] = root_pow(pw.tw, n, pw.bitrev ? rev_bits((uint32_t)i, pw.log_n) : i);
-        }
-        ef d[8];
-        ef run = ef_one();
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            d[k] = ef_sub(pw.z, ef_base(mul(pw.s, om[k])));
-            w[k] = run;
-            run = ef_mul(run, d[k]);
-        }
-        ef iv = ef_inv(run);
-#pragma unroll
-        for (int k = 7; k >= 0; k--) {
-            ef v = ef_mul(iv, w[k]);
-            iv = ef_mul(iv, d[k]);
-            w[k] = pw.mul_omega ? ef_mul_base(v, om[k]) : v;
-        }
-    }
-    const uint32_t c_begin = by * slab;
-    const uint32_t c_end = c_begin + slab < ncols ? c_begin + slab : ncols;
-    for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += OPEN_CB) {
-        const int nc = (int)(c_end - cb0 < (uint32_t)OPEN_CB ? c_end - cb0 : OPEN_CB);
-#pragma unroll
-        for (int k = 0; k < OPEN_CB; k++) {
-            const uint32_t *y = (const uint32_t *)cols[cb0 + (k < nc ? k : 0)];
-            const uint4 va = *(const uint4 *)(y + j0 + ra), vb = *(const uint4 *)(y + j0 + rb);
-            const uint32_t v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
-            uint64_t a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int e = 0; e < 4; e++)
-#pragma unroll
-                for (int m = 0; m < 4; m++) a0[e] = pair_acc(a0[e], v[m], w[m].c[e], v[m + 4], w[m + 4].c[e]);
-            if (with_next) {  // the next row wraps to row 0 at the end of the column
-                uint32_t xa = __shfl_down(va.x, 1, 64), xb = __shfl_down(vb.x, 1, 64);
-                if (lane == 63) {
-                    xa = y[(j0 + ra + 4) & (n - 1)];
-                    xb = y[(j0 + rb + 4) & (n - 1)];
-                }
-                const uint32_t u[8] = {va.y, va.z, va.w, xa, vb.y, vb.z, vb.w, xb};
-#pragma unroll
-                for (int e = 0; e < 4; e++)
-#pragma unroll
-                    for (int m = 0; m < 4; m++) a1[e] = pair_acc(a1[e], u[m], w[m].c[e], u[m + 4], w[m + 4].c[e]);
-            }
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                red[k * 8 + e][t] = acc_mod(a0[e]);
-                red[k * 8 + 4 + e][t] = with_next ? acc_mod(a1[e]) : 0u;
-            }
-        }
-        __syncthreads();
-        {
-            const uint32_t o = t >> 3, q = t & 7;  // output word o (column o / 8), partial sums q, q + 8, ...
-            uint64_t acc = 0;
-#pragma unroll
-            for (int i = 0; i < NT / 8; i++) acc += red[o][q + 8 * i];  // < 32 P
-            uint32_t r = acc_mod(acc);
-            r = add(r, __shfl_xor(r, 1, 64));
-            r = add(r, __shfl_xor(r, 2, 64));
-            r = add(r, __shfl_xor(r, 4, 64));
-            if (q == 0 && (int)(o >> 3) < nc) partial[((uint64_t)(cb0 + (o >> 3)) * nseg + bx) * 8 + (o & 7)] = r;
-        }
-        __syncthreads();  // red is reused by the next column block
-    }
-}
-__global__ __launch_bounds__(NT) void k_open_dot_regs(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
-                                                      OpenWeights pw, int with_next, int nseg, uint32_t slab,
-                                                      uint32_t *partial) {
-    open_dot_regs(cols, ncols, n, pw, with_next, nseg, slab, partial, blockIdx.x, blockIdx.y);
-}
-static_assert(OPEN_CB * 8 * 8 == NT, "one reduction thread group per output word");
+
 
 // 32-bit representative of a lazy dot-product sum v < 2^34 (four pair_acc terms, each < 2P): v mod 2^31 plus
 // (v >> 31)(2^24 - 1), since 2^31 = 2^24 - 1 mod p; < 2^31 + 2^27.  Congruent, not canonical: three VALU
@@ -617,8 +528,10 @@ __device__ __forceinline__ uint32_t fold_acc(uint64_t v) {
     return lo + (hi << 24) - hi;
 }
 
-// k_open_dot_regs with the next column block's loads issued before the current block's products (two
-// register sets used alternately): 152 VGPRs, 3 waves per SIMD
+// The full-segment kernel (round 4's register-weight form, above) with the next column block's loads issued
+// before the current block's products (two register sets used alternately), two columns per block: 116 VGPRs,
+// 4 waves per SIMD (0.600-0.606 vs 0.608-0.614 ms per shard with four columns, profiles/r05_open_cb_ab.txt; the
+// round-4 kernel without the prefetch and the LDS-weight form for full segments lost their A/Bs and are gone)
 template <int CB>
 __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                       OpenWeights pw, int with_next, int nseg, uint32_t slab,
@@ -746,12 +659,6 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
         process(cb1, b1);
     }
 }
-__global__ __launch_bounds__(NT) void k_open_dot_pf(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
-                                                      OpenWeights pw, int with_next, int nseg, uint32_t slab,
-                                                      uint32_t *partial) {
-    open_dot_pf<OPEN_CB>(cols, ncols, n, pw, with_next, nseg, slab, partial, blockIdx.x, blockIdx.y);
-}
-
 // out[col * 8 + e] = sum over the nseg segments of partial[(col * nseg + seg) * 8 + e]: one wave per
 // (column, e) pair group, lanes striding over the segments
 __device__ __forceinline__ void open_sum(const uint32_t *__restrict__ partial, int nseg, uint32_t *out, uint32_t col) {
@@ -772,11 +679,6 @@ __device__ __forceinline__ void open_sum(const uint32_t *__restrict__ partial, i
     }
     if (lane < 8) out[(uint64_t)col * 8 + lane] = r[lane];
 }
-__global__ __launch_bounds__(64) void k_open_sum(const uint32_t *__restrict__ partial, uint32_t ncols, int nseg,
-                                                 uint32_t *out) {
-    open_sum(partial, nseg, out, blockIdx.x);
-}
-
 // Every group of an opening in one grid per kernel kind (blockIdx.z = group; a group's workgroups beyond its
 // own segments / slabs, or of another kind, return at once): one launch instead of one per (height,
 // domain, points) group, so the small groups (short chips, quotient chunks) run beside each other
@@ -784,12 +686,8 @@ template <int KIND>
 __global__ __launch_bounds__(NT) void k_open_dot_groups(const OpenGroup *__restrict__ gs) {
     const OpenGroup g = gs[blockIdx.z];
     if (g.kind != KIND || blockIdx.x >= (uint32_t)g.nseg || blockIdx.y >= g.nslab) return;
-    if constexpr (KIND == 0)
+    if constexpr (KIND == 0)  // a partial last segment: the LDS weight table
         open_dot_lds(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
-    else if constexpr (KIND == 1)
-        open_dot_regs(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
-    else if constexpr (KIND == 2)
-        open_dot_pf<OPEN_CB>(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
     else
         open_dot_pf<2>(g.cols, g.ncols, g.n, g.w, g.with_next, g.nseg, g.slab, g.partial, blockIdx.x, blockIdx.y);
 }
@@ -807,30 +705,7 @@ static void open_group_shape(OpenGroup &g) {
     uint32_t nslab = (uint32_t)std::min<uint64_t>(blocks_c, std::max<uint64_t>(1, 1024 / (uint64_t)g.nseg));
     g.slab = ((blocks_c + nslab - 1) / nslab) * OPEN_CB;
     g.nslab = (g.ncols + g.slab - 1) / g.slab;
-    static const bool lds_weights = getenv("ZKM_OPEN_LDS_WEIGHTS") && atoi(getenv("ZKM_OPEN_LDS_WEIGHTS"));
-    static const bool prefetch = !getenv("ZKM_OPEN_PREFETCH") || atoi(getenv("ZKM_OPEN_PREFETCH"));
-    // the prefetching kernel walks its columns two at a time (kind 3: 116 VGPRs, 4 waves per SIMD; openings
-    // 0.600-0.606 vs 0.608-0.614 ms per shard with 4, profiles/r05_open_cb_ab.txt); ZKM_OPEN_CB=4 selects kind 2
-    static const int ocb = getenv("ZKM_OPEN_CB") ? atoi(getenv("ZKM_OPEN_CB")) : 2;
-    g.kind = (g.n % OPEN_SEG == 0 && !lds_weights) ? (prefetch ? (ocb == 2 ? 3 : 2) : 1) : 0;
-}
-
-void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const OpenWeights &w, bool with_next,
-                     uint32_t *out, hipStream_t s) {
-    if (!ncols) return;
-    OpenGroup g{d_cols, n, w, ncols, 0, 0, 0, (int)with_next, 0, nullptr, out};
-    open_group_shape(g);
-    DBuf part((size_t)ncols * g.nseg * 8, s);
-    const dim3 grid(g.nseg, g.nslab);
-    if (g.kind >= 2)
-        hipLaunchKernelGGL(k_open_dot_pf, grid, dim3(NT), 0, s, d_cols, ncols, n, w, g.with_next, g.nseg, g.slab, part.p);
-    else if (g.kind == 1)
-        hipLaunchKernelGGL(k_open_dot_regs, grid, dim3(NT), 0, s, d_cols, ncols, n, w, g.with_next, g.nseg, g.slab, part.p);
-    else
-        hipLaunchKernelGGL(k_open_dot, grid, dim3(NT), 0, s, d_cols, ncols, n, w, g.with_next, g.nseg, g.slab, part.p);
-    HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(k_open_sum, dim3(ncols), dim3(64), 0, s, part.p, ncols, g.nseg, out);
-    HIP_CHECK(hipGetLastError());
+    g.kind = g.n % OPEN_SEG == 0 ? 1 : 0;
 }
 
 void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s) {
@@ -841,7 +716,7 @@ void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s) {
     if (gs.empty()) return;
     size_t tot = 0;
     uint32_t gx = 1, gy = 1, maxc = 1;
-    bool kinds[4] = {false, false, false, false};
+    bool kinds[2] = {false, false};
     for (OpenGroup &g : gs) {
         open_group_shape(g);
         tot += (size_t)g.ncols * g.nseg * 8;
@@ -862,8 +737,6 @@ void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s) {
     const dim3 grid(gx, gy, (unsigned)gs.size());
     if (kinds[0]) hipLaunchKernelGGL(k_open_dot_groups<0>, grid, dim3(NT), 0, s, d);
     if (kinds[1]) hipLaunchKernelGGL(k_open_dot_groups<1>, grid, dim3(NT), 0, s, d);
-    if (kinds[2]) hipLaunchKernelGGL(k_open_dot_groups<2>, grid, dim3(NT), 0, s, d);
-    if (kinds[3]) hipLaunchKernelGGL(k_open_dot_groups<3>, grid, dim3(NT), 0, s, d);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_open_sum_groups, dim3(maxc, 1, (unsigned)gs.size()), dim3(64), 0, s, d);
     HIP_CHECK(hipGetLastError());
@@ -878,7 +751,7 @@ void launch_open_dot_groups(std::vector<OpenGroup> &gs, hipStream_t s) {
 // so no table of inverses crosses HBM.  One row per thread: ~50 VGPRs, 8 waves per SIMD; four rows took
 // 177 VGPRs and ran 2.2x slower (the kernel is bound by the loads in flight, not the inversions).
 static constexpr int RED_ROWS = 1;
-// LB column loads in flight per thread: 4 (ZKM_RED_LOADS = 1 / 2 / 8 / 16 for A/B): per shard 0.93-0.96 ms against
+// LB column loads in flight per thread: 4 (per shard 0.93-0.96 ms against
 // 1.12 (8), 1.08 (2), 1.41 (1), 1.34 (16): each load instruction of a wave reads 256 B of one column, and fewer
 // columns per thread at a time keep more of the concurrent waves on the same columns (profiles/r05_fri_reduce_ab.txt)
 template <int LB>
@@ -964,20 +837,7 @@ __global__ __launch_bounds__(NT) void k_fri_reduce(ReduceArgs a) {
 
 void launch_fri_reduce(const ReduceArgs &a, hipStream_t s) {
     const uint64_t threads = (a.h + RED_ROWS - 1) / RED_ROWS;
-    static const int lb = [] {
-        const char *e = getenv("ZKM_RED_LOADS");
-        return e ? atoi(e) : 4;
-    }();
-    if (lb >= 16)
-        hipLaunchKernelGGL(k_fri_reduce<16>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
-    else if (lb <= 1)
-        hipLaunchKernelGGL(k_fri_reduce<1>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
-    else if (lb <= 2)
-        hipLaunchKernelGGL(k_fri_reduce<2>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
-    else if (lb >= 8)
-        hipLaunchKernelGGL(k_fri_reduce<8>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_fri_reduce<4>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL(k_fri_reduce<4>, dim3((unsigned)((threads + NT - 1) / NT)), dim3(NT), 0, s, a);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -53,9 +53,6 @@ struct OpenWeights {
     const uint32_t *tw;  // forward twiddles
     int log_n, bitrev, mul_omega;
 };
-// out[col * 8 .. +8] = the (local, next-row) dot products of column col with the weights w (EF)
-void launch_open_dot(const uint64_t *d_cols, uint32_t ncols, uint64_t n, const OpenWeights &w, bool with_next,
-                     uint32_t *out, hipStream_t s);
 // One opening group: the columns of one (height, evaluation domain, point set), whose weights are shared.
 // The caller fills cols (device column pointer table), n, w, ncols, with_next and out; the launcher sets
 // the grid shape, kernel kind and partial-sum buffer.
