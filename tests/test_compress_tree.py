@@ -496,3 +496,58 @@ def test_dummy_vk_tree():
         path = path.copy()
         path[3, 0] ^= 1
         assert not VT.MerkleTree.verify(i, v, path, t.root)
+
+
+@pytest.fixture(scope="module")
+def deferred_setup(mips_execution):
+    """Execution A's complete compress root (the deferred proof) and execution B, whose guest commits the
+    deferred digest of A's root, oracle-proven: B's shard leaves and A's root."""
+    from zkmips_amd import mips_core as MC
+    from zkmips_amd import node_pv as NP
+    prove = _oracle_prove_factory(4)
+    vk, proofs = mips_execution
+    root_a = prove(CT.node_witness([(vk, p) for p in proofs], fix=False, is_first=True, is_complete=True))
+    pv_a = RV.parse_shard_proof(root_a[1]).pv
+    assert int(pv_a[NP.R_IS_COMPLETE]) == 1
+    d = NP.hash_deferred_proofs(np.zeros(8, np.int64), [pv_a])
+    run = MC.program_shards(MC.deferred_commit_program(d), seed=9, shard_size=1 << 10)
+    m, prep = run[0][0], run[0][1]
+    pr = O.OracleProver(m, prep, num_queries=NQ)
+    leaves = []
+    vk_b = RV.ChildVk.of(m, prep, pr.commit, num_queries=NQ)
+    for _, _, tr, pv in run:
+        rc, p = pr.prove(tr, pv)
+        assert rc == 0
+        leaves.append((vk_b, p))
+    assert [int(x) for x in run[-1][3][NP.C_DEFERRED:NP.C_DEFERRED + 8]] == [int(x) for x in d]
+    return leaves, root_a, d, prove
+
+
+def test_deferred_proof_chains_into_a_complete_root(deferred_setup):
+    """A Compress request with one deferred proof (prover/src/lib.rs:551-612, machine/deferred.rs): execution B's
+    shards reduce to a root that is not complete, A's complete root goes through a deferred node (its vk in the
+    vk tree, its digest valid, is_complete 1) that extends the reconstruct-deferred chain from zero, and the two
+    reduce to a complete root whose end digest is B's committed deferred_proofs_digest.  Without the deferred
+    proof B cannot complete; a deferred node over an incomplete proof, or one starting its chain elsewhere, is
+    refused."""
+    from zkmips_amd import node_pv as NP
+    leaves, root_a, d, prove = deferred_setup
+    submit = lambda ch, fl: _done_future(CT.node_witness(ch, fix=False, **fl))
+    root = CT.reduce_with_deferred(leaves, [root_a], submit, prove, inflight=1)
+    pv = RV.parse_shard_proof(root[1]).pv
+    assert int(pv[NP.R_IS_COMPLETE]) == 1 and int(pv[NP.R_CONTAINS_EXEC]) == 1
+    assert [int(x) for x in pv[NP.R_END_RECON:NP.R_END_RECON + 8]] == [int(x) for x in d]
+    assert not np.any(pv[NP.R_START_RECON:NP.R_START_RECON + 8])
+    with pytest.raises(ValueError, match="deferred"):
+        CT.node_witness(leaves, fix=False, is_first=True, is_complete=True)
+    last = RV.parse_shard_proof(leaves[-1][1]).pv
+    h = NP.DeferredHints.of(leaves[0][0], last, np.zeros(8, np.int64))
+    w = CT.node_witness([root_a], fix=False, deferred=h)
+    assert int(w[2][NP.R_CONTAINS_EXEC]) == 0 and int(w[2][NP.R_START_SHARD]) == int(last[NP.C_SHARD]) + 1
+    core = prove(CT.node_witness(leaves, fix=False, is_first=True))
+    with pytest.raises(ValueError, match="complete"):
+        CT.node_witness([core], fix=False, deferred=h)  # not a complete proof
+    bad = NP.DeferredHints.of(leaves[0][0], last, np.ones(8, np.int64))  # a chain that does not start at zero
+    dn = prove(CT.node_witness([root_a], fix=False, deferred=bad))
+    with pytest.raises(ValueError, match="deferred digest"):
+        CT.node_witness([core, dn], fix=False, is_complete=True)

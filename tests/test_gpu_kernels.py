@@ -51,7 +51,7 @@ def test_coset_lde_vs_oracle(dev, logn):
     assert np.array_equal(got, exp)
 
 
-@pytest.mark.parametrize("logn,w", [(20, 2), (21, 2), (22, 1), (22, 3), (23, 1)])
+@pytest.mark.parametrize("logn,w", [(20, 2), (21, 2), (22, 1), (22, 3), (23, 1), (23, 2)])
 def test_coset_lde_large_vs_oracle(dev, logn, w):
     m = W.random_matrix(1 << logn, w, seed=logn)
     assert np.array_equal(dev.coset_lde(m, 3), O.lde(m, 1, 3))

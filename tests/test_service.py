@@ -238,3 +238,63 @@ def test_compress_two_mips_shards_through_service(server):
     assert O.OracleProver(cm, cprep, **kw).verify(rproof) == 0
     assert rvk.commit == [int(x) for x in direct.vk_commit]
     assert {c[0]: c[1] for c in rvk.chips} == {k: shape[k] for k in rvk.ordering}
+
+
+@pytest.mark.gpu
+def test_compress_with_a_deferred_proof_through_service(server):
+    """Compress with `deferred_proofs` (crates/cuda/src/lib.rs:98-106, prover/src/lib.rs:551-612): execution A
+    compressed through the service is the deferred proof of execution B, whose guest committed A's deferred
+    digest.  The request comes back as a complete root whose end reconstruct-deferred digest is that digest; the
+    deferred node (machine/deferred.rs) at its RecursionShapeConfig shape proves to the oracle's bytes on the GPU
+    and the oracle verifies it; a request whose deferred proof is not the committed one is refused."""
+    from tests import _oracle as O
+    from zkmips_amd import bincode as B
+    from zkmips_amd import compress_tree as CT
+    from zkmips_amd import mips_core as MC
+    from zkmips_amd import node_pv as NP
+    from zkmips_amd import recursion as R
+    from zkmips_amd import recursion_verifier as RV
+    from zkmips_amd import shapes as SH
+    from zkmips_amd._lib import Device
+    from zkmips_amd.prover import HipProver
+    from zkmips_amd.septic import CURVE_CUMULATIVE_SUM_START as GCS
+    dev = Device(0)
+    port = server()
+    sh = SH.shape_execution(SH.MAXIMAL_22, 1, down=6)
+    m, prep = sh[0][0], sh[0][1]
+    hp = HipProver(dev, m, prep, num_queries=84)
+    proofs = [hp.prove_shard(s[2], s[3]) for s in sh]
+    st, _, body = post(port, "Compress", SV.encode_bytes_field(1, B.write_compress_request(
+        B.StarkVk.of_program(m, prep, hp.vk_commit, MC.PC_BASE, GCS), proofs)))
+    assert st == 200, body
+    a_vk, a_proof = B.read_reduce_proof(SV.decode_fields(body)[1])
+    pv_a = RV.parse_shard_proof(a_proof).pv
+    d = NP.hash_deferred_proofs(np.zeros(8, np.int64), [pv_a])
+    run = MC.program_shards(MC.deferred_commit_program(d), seed=9, shard_size=1 << 10)
+    mb, prepb = run[0][0], run[0][1]
+    hb = HipProver(dev, mb, prepb, num_queries=84)
+    proofs_b = [hb.prove_shard(s[2], s[3]) for s in run]
+    svk_b = B.StarkVk.of_program(mb, prepb, hb.vk_commit, MC.PC_BASE, GCS)
+    req = B.write_compress_request(svk_b, proofs_b, deferred=[(a_vk, a_proof)])
+    assert B.read_compress_request(req, with_deferred=True)[2] == [(a_vk, a_proof)]
+    st, _, body = post(port, "Compress", SV.encode_bytes_field(1, req))
+    assert st == 200, body
+    rvk, rproof = B.read_reduce_proof(SV.decode_fields(body)[1])
+    pv = RV.parse_shard_proof(rproof).pv
+    assert int(pv[NP.R_IS_COMPLETE]) == 1 and int(pv[NP.R_CONTAINS_EXEC]) == 1
+    assert [int(x) for x in pv[NP.R_END_RECON:NP.R_END_RECON + 8]] == [int(x) for x in d]
+    # the deferred node at its reference shape: GPU bytes == oracle bytes, verified
+    vk_b = SV.core_child_vk(svk_b)
+    h = NP.DeferredHints.of(vk_b, RV.parse_shard_proof(proofs_b[-1]).pv, np.zeros(8, np.int64))
+    cprep, tr, dpv, shape, _ = CT.node_witness([(SV.deferred_child_vk(a_vk), a_proof)], deferred=h)
+    assert shape in R.RECURSION_SHAPES and int(dpv[NP.R_CONTAINS_EXEC]) == 0
+    cm = R.compress_machine()
+    kw = dict(num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    got = HipProver(dev, cm, cprep, **kw).prove_shard(tr, dpv)
+    ov = O.OracleProver(cm, cprep, **kw)
+    rc, ref = ov.prove(tr, dpv)
+    assert rc == 0 and got == ref and ov.verify(got) == 0
+    # B's guest committed A's digest: another deferred proof (B's own root would be incomplete; use A twice)
+    bad = B.write_compress_request(svk_b, proofs_b, deferred=[(a_vk, a_proof), (a_vk, a_proof)])
+    st, _, body = post(port, "Compress", SV.encode_bytes_field(1, bad))
+    assert st == 400 and json.loads(body)["code"] == "invalid_argument"

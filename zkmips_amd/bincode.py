@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import struct
 from dataclasses import dataclass, field
-from typing import Dict, List, Tuple
+from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
 
@@ -135,9 +135,11 @@ def shard_proof_end(b: bytes, pos: int) -> int:
     return parse_shard_proof_at(b, pos)[1]
 
 
-def read_compress_request(b: bytes):
-    """CompressRequestPayload -> (StarkVk of the core program, [ShardProof bytes], number of deferred
-    proofs).  The stdin and public values that follow the shard proofs are skipped (length-delimited)."""
+def read_compress_request(b: bytes, with_deferred: bool = False):
+    """CompressRequestPayload (crates/cuda/src/lib.rs:98-106) -> (StarkVk of the core program, [ShardProof
+    bytes], number of deferred proofs), or with_deferred: (StarkVk, [ShardProof bytes], [(StarkVk, ShardProof
+    bytes)] of `deferred_proofs`).  The stdin (its buffers and the proofs the guest verifies, which the core
+    proof already accounts for) and the public values that follow the shard proofs are skipped."""
     r = Reader(b)
     vk = StarkVk.read(r)
     shards = []
@@ -159,11 +161,21 @@ def read_compress_request(b: bytes):
     r.raw(r.u64())
     r.u64()
     n_deferred = r.u64()
-    return vk, shards, n_deferred + n_stdin_proofs
+    if not with_deferred:
+        return vk, shards, n_deferred + n_stdin_proofs
+    deferred = []
+    for _ in range(n_deferred):  # ZKMReduceProof { vk: StarkVerifyingKey, proof: ShardProof }
+        dvk = StarkVk.read(r)
+        start = r.pos
+        r.pos = shard_proof_end(b, start)
+        deferred.append((dvk, bytes(b[start:r.pos])))
+    if r.pos != len(b):
+        raise ValueError("trailing bytes after the deferred proofs")
+    return vk, shards, deferred
 
 
 def write_compress_request(vk: StarkVk, shards: List[bytes], stdin: List[bytes] = (), public_values: bytes = b"",
-                           cycles: int = 0) -> bytes:
+                           cycles: int = 0, deferred: Sequence[Tuple[StarkVk, bytes]] = ()) -> bytes:
     """The client side (crates/cuda/src/lib.rs:92-102), for tests and for a caller holding this
     repository's shard proofs."""
     w = Writer()
@@ -180,7 +192,10 @@ def write_compress_request(vk: StarkVk, shards: List[bytes], stdin: List[bytes] 
     w.u64(len(public_values))
     w.raw(public_values)  # Buffer.ptr is not serialized
     w.u64(cycles)
-    w.u64(0)
+    w.u64(len(deferred))
+    for dvk, dproof in deferred:  # ZKMReduceProof: vk then proof
+        dvk.write(w)
+        w.raw(dproof)
     return w.bytes()
 
 

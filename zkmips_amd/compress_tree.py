@@ -331,7 +331,7 @@ def compact_traces(rec, shape) -> dict:
 
 
 def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool = False, compact: bool = False,
-                 dedup: bool = True, session=None, is_first: bool = False, is_complete: bool = False):
+                 dedup: bool = True, session=None, is_first: bool = False, is_complete: bool = False, deferred=None):
     """Worker body (no GPU): the compress node's program from its (ChildVk, proof) children, executed,
     padded to the first allowed recursion shape (fix=False: natural power-of-two heights, for small
     tests), as a compress-machine shard.  Returns (prep traces, main traces, public values, shape,
@@ -340,13 +340,14 @@ def node_witness(children: Sequence[tuple], fix: bool = True, p2_on_device: bool
     program structure, worker process and `session` (dedup; a consumer must pass the witnesses of one worker
     through register_prep in the order they were made, as Reducer does; one session per tree) -- a fraction
     of the bytes through the pool's pipe.  is_first / is_complete: the node covers the execution's first
-    shard / is the root of the whole tree (node_flags)."""
+    shard / is the root of the whole tree (node_flags).  deferred (node_pv.DeferredHints): the children are the
+    request's deferred proofs and the node is their deferred program (machine/deferred.rs)."""
     from . import recursion as R
     from . import recursion_verifier as RV
     t0 = time.perf_counter()
     children = [(resolve_vk(vk), proof) for vk, proof in children]
     # a FlatProgram: built once per program structure, then hints only
-    prog = RV.node_flat(children, is_first=is_first, is_complete=is_complete)
+    prog = RV.node_flat(children, is_first=is_first, is_complete=is_complete, deferred=deferred)
     t1 = time.perf_counter()
     shape = R.fix_shape(prog) if fix else {k: max(4, (h - 1).bit_length()) for k, h in R.program_heights(prog).items()}
     if compact:
@@ -734,6 +735,35 @@ def reduce_serial(leaves: Sequence[tuple], reducer: Reducer) -> tuple:
     mine = [n for l in layers for n in l]
     reducer.run(done, mine, widths)
     return done[layers[-1][0]]
+
+
+def reduce_with_deferred(leaves: Sequence[tuple], deferred: Sequence[tuple], submit_witness: Callable,
+                         prove: Callable, inflight: int = 3) -> tuple:
+    """A Compress request with deferred proofs (prover/src/lib.rs:614-954 over get_first_layer_inputs, :599-612):
+    the execution's shard leaves reduce to a root that is not complete; every deferred proof (ChildVk, complete
+    compress proof) gets its own deferred node (first_layer_batch_size 1) whose reconstruct-deferred chain starts
+    where the previous one ended (hash_deferred_proofs) and whose other values come from the last shard
+    (get_recursion_deferred_inputs, :551-593); then [execution root, deferred nodes...] in that order reduce to
+    the complete root, whose end digest must be the execution's committed deferred_proofs_digest
+    (assert_complete).  submit_witness / prove as for Reducer; returns the root's (vk, proof)."""
+    from . import node_pv as NP
+    from . import recursion_verifier as RV
+    if not leaves or not deferred:
+        raise ValueError("reduce_with_deferred: shard leaves and deferred proofs")
+    if len(leaves) == 1:
+        core = prove(register_prep(submit_witness(list(leaves), {"is_first": True, "is_complete": False}).result()))
+    else:
+        core = reduce_serial(leaves, Reducer(submit_witness, prove, inflight, complete=False))
+    core_vk = resolve_vk(leaves[0][0])
+    last_pv = RV.parse_shard_proof(leaves[-1][1]).pv
+    digest = np.zeros(8, np.int64)
+    futs = []
+    for vk, p in deferred:
+        h = NP.DeferredHints.of(core_vk, last_pv, digest)
+        futs.append(submit_witness([(vk, p)], {"is_first": False, "is_complete": False, "deferred": h}))
+        digest = NP.hash_deferred_proofs(digest, [RV.parse_shard_proof(p).pv])
+    nodes = [prove(register_prep(f.result())) for f in futs]
+    return reduce_serial([core] + nodes, Reducer(submit_witness, prove, inflight, complete=True))
 
 
 MSG_BYTES = 8 << 20  # fixed point-to-point message: a pickled (vk, proof) of a node (KB-MB)

@@ -1153,6 +1153,200 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9b(const uint32_t *src, uin
     }
 }
 
+// 10 strided stages (the 2^23 LDE = 2^13 tile x 2^10 strided: three HBM passes instead of five with two 5-stage
+// passes each way).  One workgroup of 1024 threads: 1024 rows (stride S) x 16 consecutive columns, 16 elements
+// per thread, 64 KB of LDS (two workgroups per CU, as k_ntt_s9b).  Lane -> column (t = tid & 15: 64-B row
+// segments), u = tid >> 4 < 64.  Layouts (network n in {0,1}, g = 2u + n < 128):
+//   LH: one 16-point network, rows u + 64k (k < 16)           stages h_r = 64, 128, 256, 512 rows
+//   LM: two 8-point networks, rows (g >> 3) 64 + (g & 7) + 8k  h_r = 8, 16, 32
+//   LL: two 8-point networks, rows 8g + k                      h_r = 1, 2, 4
+// Twiddles as k_ntt_s9b: one load per network (its top twiddle), the rest generated (squarings and products by
+// w_4, w_8^m, w_16^m).  LDS: row r at physical row r ^ (r1 ^ r4 ^ r9) (bit i of r: ri), so the two rows a
+// 32-lane half touches (in LH rows differing in bit 0, LM in bit 1, LL in bit 4, the bit-reversed output walk in
+// bit 9) sit in opposite 16-bank halves; the output walk also XORs the column with row bits 5..8.
+namespace s10 {
+constexpr int NTH = 1024;
+template <bool SWZ>
+__device__ __forceinline__ uint32_t at(uint32_t r, uint32_t t) {
+    const uint32_t p = r ^ (((r >> 1) ^ (r >> 4) ^ (r >> 9)) & 1u);
+    if constexpr (SWZ) return p * 16 + (t ^ ((r >> 5) & 15));
+    else return p * 16 + t;
+}
+struct Tw16 {
+    uint32_t w[4][8];  // w[st][m], m < 2^st
+};
+struct TwC16 {
+    uint32_t w4, w8[3], w16[7];
+};
+__device__ __forceinline__ TwC16 twc16(const uint32_t *__restrict__ tw) {
+    TwC16 c;
+    c.w4 = tw[3];
+#pragma unroll
+    for (int m = 1; m < 4; m++) c.w8[m - 1] = tw[4 + m];
+#pragma unroll
+    for (int m = 1; m < 8; m++) c.w16[m - 1] = tw[8 + m];
+    return c;
+}
+// w_{st,0} = w_{st+1,0}^2 and w_{st,m} = w_{st,0} w_{2^(st+1)}^m (the top twiddle w_{3,0} loaded)
+__device__ __forceinline__ Tw16 tw16(uint32_t wtop, const TwC16 &c) {
+    Tw16 r;
+    r.w[3][0] = wtop;
+    r.w[2][0] = mul(wtop, wtop);
+    r.w[1][0] = mul(r.w[2][0], r.w[2][0]);
+    r.w[0][0] = mul(r.w[1][0], r.w[1][0]);
+    r.w[1][1] = mul(r.w[1][0], c.w4);
+#pragma unroll
+    for (int m = 1; m < 4; m++) r.w[2][m] = mul(r.w[2][0], c.w8[m - 1]);
+#pragma unroll
+    for (int m = 1; m < 8; m++) r.w[3][m] = mul(wtop, c.w16[m - 1]);
+    return r;
+}
+template <bool DIT>
+__device__ __forceinline__ void net16r(uint32_t *v, const Tw16 &W) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int st = DIT ? q : 3 - q;
+        const int span = 1 << st;
+#pragma unroll
+        for (int m = 0; m < span; m++) {
+            const uint32_t w = W.w[st][m];
+#pragma unroll
+            for (int k = m; k < 16; k += 2 * span) {
+                const uint32_t a = v[k], b = v[k + span];
+                if (DIT) {
+                    const uint32_t tt = mul(b, w);
+                    if (q < 3 && ((k >> (st + 1)) & 1)) {  // next stage multiplies both: lazy [0, 2P)
+                        v[k] = a + tt;
+                        v[k + span] = a + (P - tt);
+                    } else {
+                        v[k] = add(a, tt);
+                        v[k + span] = sub(a, tt);
+                    }
+                } else {
+                    v[k] = add(a, b);
+                    v[k + span] = mul(a + (P - b), w);
+                }
+            }
+        }
+    }
+}
+// element k of network n of a layout: its tile row
+enum { LH = 0, LM = 1, LL = 2 };
+template <int LAY>
+__device__ __forceinline__ uint32_t row(uint32_t u, int n, int k) {
+    const uint32_t g = 2 * u + n;
+    if constexpr (LAY == LH) return u + 64 * (8 * n + k);  // (n, k) = element 8n + k of the 16-point network
+    else if constexpr (LAY == LM) return (g >> 3) * 64 + (g & 7) + 8 * k;
+    else return 8 * g + k;
+}
+template <int LAY, bool SWZ>
+__device__ __forceinline__ void to_lds(uint32_t *x, const uint32_t v[16], uint32_t u, uint32_t t) {
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[at<SWZ>(row<LAY>(u, n, k), t)] = v[8 * n + k];
+}
+template <int LAY>
+__device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint32_t u, uint32_t t) {
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[8 * n + k] = x[at<false>(row<LAY>(u, n, k), t)];
+}
+}  // namespace s10
+
+template <bool DIT, int MODE>
+__global__ __launch_bounds__(s10::NTH, 4) void k_ntt_s10(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
+                                                         int logS, const uint32_t *__restrict__ tw, uint32_t tw_words,
+                                                         uint32_t nv) {
+    using namespace s10;
+    using s9::bld;
+    using s9::mkrs;
+    using s9::TwC;
+    using s9::Tw8;
+    __shared__ uint32_t x[1024 * 16];
+    const uint32_t S = 1u << logS, S4 = S * 4;
+    // XCD-aware order (k_ntt_s9b): the columns of one tile back to back on one XCD
+    const uint32_t total = gridDim.x, lin = blockIdx.x;
+    const uint32_t vid = (total & 7) ? lin : (lin & 7) * (total >> 3) + (lin >> 3);
+    const uint32_t col = vid % nv, tile = vid / nv;
+    const uint32_t outer = tile >> (logS - 4);
+    const uint32_t c0 = (tile & ((S >> 4) - 1)) * 16;
+    const uint32_t base = outer * 1024u * S;
+    const uint32_t t = threadIdx.x & 15, u = threadIdx.x >> 4;
+    const uint32_t ct = c0 + t;
+    const auto rsrc = mkrs(src + ms.off(col) + base, 1024u * S4);
+    const auto rtw = mkrs(tw, tw_words * 4);
+    const TwC twk = s9::twc(tw);
+    const TwC16 tw16c = twc16(tw);
+    // top-twiddle offsets: LH w_{1024 S}^{u S + ct} (index 512 S + u S + ct), LM w_{64 S}^{(g & 7) S + ct}, LL
+    // w_{8 S}^{ct}; data: LH rows u + 64 k, LL rows 16 u + 8 n + k
+    const uint32_t vLH = (u * S + ct) * 4, vL16 = (16 * u * S + ct) * 4, vLL = ct * 4;
+    const uint32_t vLM0 = (((2 * u) & 7) * S + ct) * 4, vLM1 = (((2 * u + 1) & 7) * S + ct) * 4;
+    uint32_t v[16];
+    if (DIT) {
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[8 * n + k] = bld(rsrc, vL16, (uint32_t)(8 * n + k) * S4);
+        {  // both networks of LL share their twiddles (off = 0)
+            const Tw8 W = s9::tw8(bld(rtw, vLL, 4 * S4), twk);
+            s9::net8r<true>(v, W);
+            s9::net8r<true>(v + 8, W);
+        }
+        to_lds<LL, false>(x, v, u, t);
+        __syncthreads();
+        from_lds<LM>(x, v, u, t);
+        s9::net8r<true>(v, s9::tw8(bld(rtw, vLM0, 32 * S4), twk));
+        s9::net8r<true>(v + 8, s9::tw8(bld(rtw, vLM1, 32 * S4), twk));
+        __syncthreads();
+        to_lds<LM, false>(x, v, u, t);
+        __syncthreads();
+        from_lds<LH>(x, v, u, t);
+        net16r<true>(v, tw16(bld(rtw, vLH, 512 * S4), tw16c));
+        if (MODE == MODE_PLAIN) {
+            const auto rdst = mkrs(dst + md.off(col) + base, 1024u * S4);
+#pragma unroll
+            for (int k = 0; k < 16; k++) s9::bst_mid(v[k], rdst, vLH, (uint32_t)(64 * k) * S4);
+        } else {  // BITREV_OUT: natural n = r S + c -> row rev_L(n) = rev_logS(c) * 1024 + rev_10(r)
+            __syncthreads();
+            to_lds<LH, true>(x, v, u, t);
+            __syncthreads();
+            const auto rdst = mkrs(dst + md.off(col), 1024u * S4);
+            const uint32_t q = threadIdx.x, rq = rev_bits(q, 10);
+            const uint32_t vo = ((rev_bits(c0, logS) << 10) + q) * 4;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t so = (rev_bits((uint32_t)i, 4) << (logS - 4)) << 12;  // rows x 1024 words x 4 B
+                s9::bst(x[at<true>(rq, (uint32_t)i)], rdst, vo, so);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = bld(rsrc, vLH, (uint32_t)(64 * k) * S4);
+        net16r<false>(v, tw16(bld(rtw, vLH, 512 * S4), tw16c));
+        to_lds<LH, false>(x, v, u, t);
+        __syncthreads();
+        from_lds<LM>(x, v, u, t);
+        s9::net8r<false>(v, s9::tw8(bld(rtw, vLM0, 32 * S4), twk));
+        s9::net8r<false>(v + 8, s9::tw8(bld(rtw, vLM1, 32 * S4), twk));
+        __syncthreads();
+        to_lds<LM, false>(x, v, u, t);
+        __syncthreads();
+        from_lds<LL>(x, v, u, t);
+        {
+            const Tw8 W = s9::tw8(bld(rtw, vLL, 4 * S4), twk);
+            s9::net8r<false>(v, W);
+            s9::net8r<false>(v + 8, W);
+        }
+        const auto rdst = mkrs(dst + md.off(col) + base, 1024u * S4);
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) s9::bst_mid(v[8 * n + k], rdst, vL16, (uint32_t)(8 * n + k) * S4);
+    }
+}
+
 template <bool TILED>
 __global__ __launch_bounds__(t13::NTH, 6) void k_lde_fused13s(const uint32_t *src, uint32_t *dst, ColMap ms,
                                                              ColMap md, int L, const uint32_t *__restrict__ tt_inv,
@@ -1197,7 +1391,7 @@ __global__ __launch_bounds__(t13::NTH, 6) void k_lde_fused13s(const uint32_t *sr
 static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
 static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
 
-static int strided_T(int logR) { return logR >= 5 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
+static int strided_T(int logR) { return logR == 10 ? 16 : logR >= 5 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
 
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
@@ -1208,6 +1402,21 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     ARG_CHECK(!tile || (logR == 9 && logS + 9 == L && tw_words && mode != MODE_TWIST_OUT),
               "tile-major sides need the one-pass 512-row strided kernel");
     dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
+    if (logR == 10) {  // 1024-row x 16-column register tiles (k_ntt_s10), natural-input LDE of 2^23
+        ARG_CHECK(tw_words && mode != MODE_TWIST_OUT && !tile, "the 10-stage pass: plain or bit-reversed output");
+        const dim3 g1(g.x * nv);
+        if (!DIT)
+            hipLaunchKernelGGL((k_ntt_s10<false, MODE_PLAIN>), g1, dim3(s10::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tw_words, nv);
+        else if (mode == MODE_PLAIN)
+            hipLaunchKernelGGL((k_ntt_s10<true, MODE_PLAIN>), g1, dim3(s10::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tw_words, nv);
+        else
+            hipLaunchKernelGGL((k_ntt_s10<true, MODE_BITREV_OUT>), g1, dim3(s10::NTH), 0, s, src, dst, ms, md, logS,
+                               tw, tw_words, nv);
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
     if (logR == 9 && tw_words && mode != MODE_TWIST_OUT) {
         // buffer-addressed register tiles (k_ntt_s9b), one grid dimension: (tile, column) remapped in the
         // kernel; tile-major source (bit 0) and / or destination (bit 1)
@@ -1312,10 +1521,12 @@ static void run_fused(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, C
 
 // strided pass radices for the bits above the contiguous tile (top to bottom, i.e. DIF order): the 13-stage tile and
 // the rest in balanced passes of at most 9 stages (a 9-stage pass first with an 11-stage tile was the faster 2^20
-// plan only while that height's 7-stage pass was LDS-staged: profiles/r05_lde_plan_ab.txt, r05_lde_s8_ab.txt)
-static std::vector<int> strided_plan(int L, int &logC) {
+// plan only while that height's 7-stage pass was LDS-staged: profiles/r05_lde_plan_ab.txt, r05_lde_s8_ab.txt).
+// allow10: 10 remaining stages as one k_ntt_s10 pass (the natural-input LDE of 2^23: three HBM passes, not five)
+static std::vector<int> strided_plan(int L, int &logC, bool allow10 = false) {
     logC = L < LOGC ? L : LOGC;
     int rem = L - logC;
+    if (allow10 && rem == 10) return {10};
     std::vector<int> p;
     int np = (rem + LOGS - 1) / LOGS;
     for (int i = 0; i < np; i++) {
@@ -1474,7 +1685,7 @@ static void lde_natural(Ctx &c, const DMat &src, const uint32_t *shifts, int nsh
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
     int logC;
-    std::vector<int> sp = strided_plan(L, logC);
+    std::vector<int> sp = strided_plan(L, logC, true);
     const uint32_t nv = (uint32_t)W;
     ColMap m_src{N, 0, 1}, m_w1{2 * N, 0, 1}, m_w2{2 * N, N, 2}, m_out{dst_stride, N, 2};
     if (sp.empty()) {

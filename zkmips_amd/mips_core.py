@@ -2020,6 +2020,19 @@ def sha_program(calls: int, seed: int = 1, loads: int = 4, commit: bool = True, 
     return prog
 
 
+def deferred_commit_program(words, body: int = 8, iters: int = 30, seed: int = 9):
+    """A guest that runs a counted loop (loop_program), commits `words` as its deferred_proofs_digest
+    (COMMIT_DEFERRED_PROOFS word by word, syscalls/commit.rs) and halts: the public values of a guest that
+    verified deferred proofs, whose Compress request then carries those proofs (node_pv.deferred_node)."""
+    prog = list(loop_program(body, iters, seed))  # its END is the instruction after it
+    for i, w in enumerate(words):
+        prog += [(A.OP_ADD, SY.REG_V0, 0, SY.COMMIT_DEFERRED_PROOFS, 0, 1), (A.OP_ADD, SY.REG_A0, 0, i, 0, 1),
+                 (A.OP_ADD, SY.REG_A1, 0, int(w) % P, 0, 1), (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
+    prog += [(A.OP_ADD, SY.REG_V0, 0, SY.HALT, 0, 1), (A.OP_ADD, SY.REG_A0, 0, 0, 0, 1),
+             (SY.OP_SYSCALL, SY.REG_V0, SY.REG_A0, SY.REG_A1, 0, 0)]
+    return prog
+
+
 def shard_global_digest(traces) -> np.ndarray:
     """ShardProof::global_cumulative_sum of a shard: the Global chip's last-row cumulative sum."""
     return traces["Global"][-1, MM.G_CUM_X:MM.G_CUM_X + 14].copy()

@@ -19,6 +19,11 @@ The reference reduces an execution's shard proofs in two kinds of recursion prog
 
 Both end with `assert_complete` (machine/complete.rs) when the node is the root of the whole execution.
 
+A third program takes the request's deferred proofs (`ZKMDeferredVerifier::verify`, machine/deferred.rs:113-251):
+complete compress proofs of other executions, verified like compress children, whose (vk digest, committed value
+digest) pairs extend the reconstruct-deferred digest chain; its other public values are witnessed from the core
+proof's last shard, so it chains after the execution's nodes (`deferred_node`, `DeferredHints`).
+
 Children that are neither MIPS shards nor recursion proofs (this repository's synthetic FibCpu machine) get the
 structural part only: the node commits a RecursionPublicValues with the vk digest, the Global-scope sum and zero
 chaining fields, so that the compress layers above it apply the same checks to every tree.
@@ -473,6 +478,69 @@ def compress_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars], i
     return _finish(o, out, o.hint(1 if is_complete else 0))
 
 
+@dataclass
+class DeferredHints:
+    """The witnessed values of a deferred node (ZKMDeferredWitnessValues, machine/deferred.rs:53-72), as
+    `get_recursion_deferred_inputs` (prover/src/lib.rs:551-593) fills them: the chain's start digest, the core
+    program's vk digest, and the last core shard's digests, shard + 1, execution shard and final address bits;
+    end_pc 0 (the execution halted)."""
+    start_digest: np.ndarray
+    zkm_vk_digest: np.ndarray
+    committed_value_digest: np.ndarray
+    deferred_proofs_digest: np.ndarray
+    end_pc: int
+    end_shard: int
+    end_execution_shard: int
+    init_addr_bits: np.ndarray
+    finalize_addr_bits: np.ndarray
+
+    @staticmethod
+    def of(core_vk, last_core_pv, start_digest) -> "DeferredHints":
+        pv = np.asarray(last_core_pv, np.int64)
+        return DeferredHints(np.asarray(start_digest, np.int64), VT.vk_digest(core_vk).astype(np.int64),
+                             pv[C_COMMITTED:C_COMMITTED + 32].copy(), pv[C_DEFERRED:C_DEFERRED + 8].copy(), 0,
+                             int(pv[C_SHARD]) + 1, int(pv[C_EXEC]), pv[C_LAST_INIT:C_LAST_INIT + 32].copy(),
+                             pv[C_LAST_FIN:C_LAST_FIN + 32].copy())
+
+
+def hash_deferred_proofs(prev_digest, recursion_pvs: Sequence) -> np.ndarray:
+    """ZKMProver::hash_deferred_proofs (prover/src/lib.rs:1131-1147, primitives hash_deferred_proof): for each
+    deferred proof, digest = poseidon2_hash(digest || zkm_vk_digest || committed_value_digest (32 byte words))."""
+    d = np.asarray(prev_digest, np.int64)
+    for pv in recursion_pvs:
+        pv = np.asarray(pv, np.int64)
+        d = VT.hash_slice(np.concatenate([d, pv[R_VK_DIGEST:R_VK_DIGEST + 8], pv[R_COMMITTED:R_COMMITTED + 32]]))
+        d = np.asarray(d, np.int64)
+    return d
+
+
+def deferred_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars], h: DeferredHints) -> V:
+    """ZKMDeferredVerifier::verify (machine/deferred.rs:113-251) over complete recursion proofs: each child's vk
+    in the vk tree, its vk_root the witnessed one, its public-value digest valid, is_complete = 1, and the
+    reconstruct-deferred digest extended by poseidon2(digest || zkm_vk_digest || committed_value_digest); the
+    node's other public values are the witnessed ones (no execution shard, exit code 0, the zero global sum)."""
+    root = vk_root_const(o)
+    for (vk, _), cv in zip(children, cvs):
+        verify_vk_membership(o, vk, cv.vk_commit, root)
+    start = o.hint(h.start_digest)
+    recon = start
+    for cv in cvs:
+        pv = cv.pv
+        o.assert_eq(pv[R_VK_ROOT:R_VK_ROOT + 8], root, "deferred proof vk_root")
+        o.assert_eq(o.hash(pv[:NUM_PV_ELMS_TO_HASH]), pv[R_DIGEST:R_DIGEST + 8], "deferred proof public-value digest")
+        o.assert_eq(pv[R_IS_COMPLETE], o.const(1), "a deferred proof is complete")
+        recon = o.hash(cat(recon, pv[R_VK_DIGEST:R_VK_DIGEST + 8], pv[R_COMMITTED:R_COMMITTED + 32]))
+    end_pc, end_shard, end_exec = o.hint(h.end_pc), o.hint(h.end_shard), o.hint(h.end_execution_shard)
+    init, fin = o.hint(h.init_addr_bits), o.hint(h.finalize_addr_bits)
+    out = {R_COMMITTED: o.hint(h.committed_value_digest), R_DEFERRED: o.hint(h.deferred_proofs_digest),
+           R_START_PC: end_pc, R_NEXT_PC: end_pc, R_START_SHARD: end_shard, R_NEXT_SHARD: end_shard,
+           R_START_EXEC: end_exec, R_NEXT_EXEC: end_exec, R_PREV_INIT: init, R_LAST_INIT: init, R_PREV_FIN: fin,
+           R_LAST_FIN: fin, R_VK_DIGEST: o.hint(h.zkm_vk_digest), R_GCS: o.const(SP.CURVE_CUMULATIVE_SUM_START),
+           R_START_RECON: start, R_END_RECON: recon, R_EXIT: o.const(0), R_CONTAINS_EXEC: o.const(0),
+           R_VK_ROOT: root}
+    return _finish(o, out, o.hint(0))
+
+
 def synthetic_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars]) -> V:
     """Children of a machine with no MIPS public values: the vk digest and the Global-scope sum, zero chaining
     fields (so the compress layers above apply their checks uniformly)."""
@@ -484,13 +552,20 @@ def synthetic_node(o: Ops, children: Sequence[tuple], cvs: Sequence[ChildVars]) 
 
 
 def node_public_values(b, children: Sequence[tuple], cvs: Sequence[ChildVars], is_first: bool = False,
-                       is_complete: bool = False) -> V:
-    """The node's RecursionPublicValues after its kind's checks (module docstring)."""
+                       is_complete: bool = False, deferred: Optional[DeferredHints] = None) -> V:
+    """The node's RecursionPublicValues after its kind's checks (module docstring); `deferred`: a deferred node
+    over complete recursion proofs with these witnessed values."""
     kinds = {child_kind(vk) for vk, _ in children}
     if len(kinds) != 1:
         raise ValueError(f"compress node: children of different kinds {sorted(kinds)}")
     kind = kinds.pop()
     o = Ops(b)
+    if deferred is not None:
+        if kind != "recursion":
+            raise ValueError("deferred node: deferred proofs are compress (recursion) proofs")
+        if is_complete:
+            raise ValueError("deferred node: never the root (get_recursion_deferred_inputs: is_complete false)")
+        return deferred_node(o, children, cvs, deferred)
     if kind == "core":
         return core_node(o, children, cvs, is_first, is_complete)
     if kind == "recursion":

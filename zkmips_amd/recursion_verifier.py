@@ -1206,25 +1206,26 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
     return pairs
 
 
-def _build_node(prog, b, children: Sequence[tuple], ood: bool, is_first: bool, is_complete: bool):
+def _build_node(prog, b, children: Sequence[tuple], ood: bool, is_first: bool, is_complete: bool, deferred=None):
     from .node_pv import node_public_values
     if not children:
         raise ValueError("a compress node needs at least one child")
     cvs = [verify_shard(prog, vk, proof, b, ood=ood) for vk, proof in children]
-    pv = node_public_values(b, children, cvs, is_first=is_first, is_complete=is_complete)
+    pv = node_public_values(b, children, cvs, is_first=is_first, is_complete=is_complete, deferred=deferred)
     prog.commit_public_values(np.asarray(pv.a, np.int64))
     return pv
 
 
 def compress_node_program(children: Sequence[tuple], ood: bool = True, is_first: bool = False,
-                          is_complete: bool = False) -> R.RecursionProgram:
+                          is_complete: bool = False, deferred=None) -> R.RecursionProgram:
     """A compress node (prover/src/lib.rs:614-954): verify every child (ChildVk, proof bytes), check their
     public values the way the reference's core / compress recursion programs do, and commit the node's
     RecursionPublicValues (zkmips_amd/node_pv.py).  is_first: the node's first child is the execution's first
-    batch (core.rs `is_first_shard`); is_complete: the node is the root of the whole execution."""
+    batch (core.rs `is_first_shard`); is_complete: the node is the root of the whole execution; deferred
+    (node_pv.DeferredHints): the deferred program over complete compress proofs (machine/deferred.rs)."""
     prog = R.RecursionProgram()
     b = Builder(prog)
-    _build_node(prog, b, children, ood, is_first, is_complete)
+    _build_node(prog, b, children, ood, is_first, is_complete, deferred)
     return prog
 
 
@@ -1268,7 +1269,7 @@ _TEMPLATES: Dict[tuple, tuple] = {}  # per process: structure key -> (FlatProgra
 
 
 def node_flat(children: Sequence[tuple], ood: bool = True, is_first: bool = False,
-              is_complete: bool = False) -> "R.FlatProgram":
+              is_complete: bool = False, deferred=None) -> "R.FlatProgram":
     """compress_node_program(children) flattened, built once per program structure.  The verifier program
     depends on the children's vks and proof shapes only; the proofs themselves enter as hints.  So the
     first node of a structure is built in full and its FlatProgram kept; a later node with the same vks and
@@ -1277,13 +1278,13 @@ def node_flat(children: Sequence[tuple], ood: bool = True, is_first: bool = Fals
     the FlatProgram of compress_node_program(children) (tests/test_compress_verify.py)."""
     tape = _HintTape()
     b = Builder(tape)
-    _build_node(tape, b, children, ood, is_first, is_complete)
+    _build_node(tape, b, children, ood, is_first, is_complete, deferred)
     sizes = tuple(len(v) for v in tape.vals)
-    key = (tuple(_vk_key(vk) for vk, _ in children), tuple(tape.shapes), bool(ood), sizes,
+    key = (deferred is not None, tuple(_vk_key(vk) for vk, _ in children), tuple(tape.shapes), bool(ood), sizes,
            tuple(len(v) for v in tape.fresh))
     hit = _TEMPLATES.get(key)
     if hit is None:
-        prog = compress_node_program(children, ood=ood, is_first=is_first, is_complete=is_complete)
+        prog = compress_node_program(children, ood=ood, is_first=is_first, is_complete=is_complete, deferred=deferred)
         tpl = R.flatten(prog)
         hint_rows = tuple(int(n) for kc, _, n, _, _ in tpl.table if R.KINDS[kc] == "hint")
         fresh = [(int(tpl.table[bi][1]), int(tpl.table[bi][2])) for bi in prog.__dict__.get("fresh_blocks", [])]

@@ -185,6 +185,29 @@ def core_child_vk(vk):
                       order, heights, int(vk.pc_start), np.asarray(vk.gcs, np.int64))
 
 
+def deferred_child_vk(vk):
+    """The ChildVk of a deferred proof (ZKMReduceProof<InnerSC>.vk, a compress program's StarkVerifyingKey): the
+    compress machine's chips, the key's commitment and preprocessed heights, compress FRI parameters.  A chip the
+    compress machine does not preprocess, or a dimension that is not the chip's, is a ValueError."""
+    from . import compress_tree as CT
+    from . import recursion as R
+    from .septic import CURVE_CUMULATIVE_SUM_START
+    chips = {c.name: c for c in R.compress_machine().chips}
+    shape = {}
+    for name, log_n, shift, width, height in vk.chips:
+        c = chips.get(name)
+        if c is None or not c.prep_width:
+            raise ValueError(f"deferred proof: chip {name!r} has no preprocessed trace in the compress machine")
+        if width != c.prep_width or height != 1 << log_n or shift != 1:
+            raise ValueError(f"deferred proof: chip {name!r} preprocessed dimensions are not the machine's")
+        shape[name] = int(log_n)
+    if sorted(shape) != sorted(k for k, c in chips.items() if c.prep_width):
+        raise ValueError("deferred proof: not a compress program's verifying key")
+    if int(vk.pc_start) != 0 or [int(x) for x in vk.gcs] != [int(x) for x in CURVE_CUMULATIVE_SUM_START]:
+        raise ValueError("deferred proof: a compress vk has pc_start 0 and the zero initial global sum")
+    return CT.compress_child_vk(vk.commit, shape)
+
+
 def reduce_vk(cvk):
     """StarkVerifyingKey<InnerSC> of a compress proof's program (the vk field of ZKMReduceProof)."""
     from . import bincode as B
@@ -305,21 +328,21 @@ class ProverService:
         (zkmips_amd/node_pv.py: consecutive shard numbers and pcs, address bits, digests, exit code, the
         first-shard conditions, the child vks' membership in the dummy vk tree) and the root asserts the
         proof complete (start shard 1, next_pc 0, global sum zero); a request that fails them answers
-        invalid_argument before any GPU work.  Not supported: deferred proofs (unimplemented), the real vk
-        map (`vk_map.bin` is absent from the reference snapshot; the dummy map's tree is used, as
-        VERIFY_VK=false does)."""
+        invalid_argument before any GPU work.  Deferred proofs (complete compress proofs of other executions) are
+        verified by deferred nodes chained after the execution's (CT.reduce_with_deferred, lib.rs:551-604).  Not
+        supported: the real vk map (`vk_map.bin` is absent from the reference snapshot; the dummy map's tree is
+        used, as VERIFY_VK=false does)."""
         from . import bincode as B
         from . import compress_tree as CT
         try:
-            vk, shards, n_deferred = B.read_compress_request(data)
+            vk, shards, deferred = B.read_compress_request(data, with_deferred=True)
         except Exception as e:
-            raise TwirpError("invalid_argument", f"Compress payload: {e}")
-        if n_deferred:
-            raise TwirpError("unimplemented", "Compress: deferred proofs are not supported")
+            raise TwirpError("invalid_argument", f"Compress: payload: {e}")
         if not shards:
             raise TwirpError("invalid_argument", "Compress: the core proof has no shards")
         try:
             cvk = core_child_vk(vk)
+            dleaves = [(deferred_child_vk(dvk), dp) for dvk, dp in deferred]
         except ValueError as e:
             raise TwirpError("invalid_argument", f"Compress: {e}")
         leaves = [(cvk, s) for s in shards]
@@ -346,12 +369,13 @@ class ProverService:
             tp = ThreadPoolExecutor(2)
             # threads of this process: no once-per-program prep (arrival order is not completion order)
             submit = lambda ch, fl: tp.submit(CT.node_witness, ch, True, True, True, False, **fl)
-        reducer = CT.Reducer(submit, prove, self.compress_inflight)
         try:
-            if len(leaves) == 1:  # one shard is still wrapped by a compress node
+            if dleaves:
+                rvk, rproof = CT.reduce_with_deferred(leaves, dleaves, submit, prove, self.compress_inflight)
+            elif len(leaves) == 1:  # one shard is still wrapped by a compress node
                 rvk, rproof = prove(CT.register_prep(submit(leaves, {"is_first": True, "is_complete": True}).result()))
             else:
-                rvk, rproof = CT.reduce_serial(leaves, reducer)
+                rvk, rproof = CT.reduce_serial(leaves, CT.Reducer(submit, prove, self.compress_inflight))
         except ValueError as e:  # a child proof of the wrong shape for its verifying key
             raise TwirpError("invalid_argument", f"Compress: {e}")
         except RuntimeError as e:
