@@ -121,10 +121,44 @@ def test_compress_route_errors():
     with pytest.raises(SV.TwirpError) as e:
         svc.call("Compress", {1: bytes(req)})
     assert e.value.code == "invalid_argument"  # no shards
-    req[-8:] = struct.pack("<Q", 1)  # one deferred proof (its bytes are never read: refused first)
+    req[-8:] = struct.pack("<Q", 1)  # one deferred proof announced, its bytes missing: a malformed payload
     with pytest.raises(SV.TwirpError) as e:
         svc.call("Compress", {1: bytes(req)})
-    assert e.value.code == "unimplemented"
+    assert e.value.code == "invalid_argument"
+
+
+def test_deferred_proofs_in_the_compress_request():
+    """CompressRequestPayload.deferred_proofs (crates/cuda/src/lib.rs:98-106): ZKMReduceProof = StarkVerifyingKey
+    then ShardProof, written and read back; a deferred proof's vk must be a compress program's (its preprocessed
+    chips, pc_start 0, the zero initial global sum), so a core program's vk is refused."""
+    from zkmips_amd import recursion as R
+    from zkmips_amd import recursion_verifier as RV
+    from zkmips_amd import shapes as SH
+    from zkmips_amd import workloads as W
+    from tests import _oracle as O
+    from zkmips_amd.septic import CURVE_CUMULATIVE_SUM_START as GCS
+    m, prep, tr, pv = SH.shape_shards(SH.MAXIMAL_22, [1], down=8)[0]
+    core_vk = B.StarkVk.of_program(m, prep, np.arange(8) + 1, 0x00400000, GCS)
+    fm, fprep, ftr, fpv = W.fib_shard(64, seed=1)
+    rc, proof = O.OracleProver(fm, fprep, num_queries=2).prove(ftr, fpv)
+    assert rc == 0
+    cm = R.compress_machine()
+    shape = R.RECURSION_SHAPES[0]
+    cvk = B.StarkVk([3] * 8, 0, [int(x) for x in GCS],
+                    [(c.name, shape[c.name], 1, c.prep_width, 1 << shape[c.name])
+                     for c in sorted((c for c in cm.chips if c.prep_width), key=lambda c: (-shape[c.name], c.name))])
+    cvk.ordering = {c[0]: i for i, c in enumerate(cvk.chips)}
+    req = B.write_compress_request(core_vk, [proof], deferred=[(cvk, proof), (cvk, proof)])
+    vk, shards, deferred = B.read_compress_request(req, with_deferred=True)
+    assert shards == [proof] and deferred == [(cvk, proof), (cvk, proof)]
+    assert B.read_compress_request(req)[2] == 2
+    got = SV.deferred_child_vk(cvk)
+    assert got.prep_heights == {c[0]: c[4] for c in cvk.chips} and list(got.commit) == [3] * 8
+    assert got.num_queries == R.COMPRESS_NUM_QUERIES and got.log_blowup == R.COMPRESS_LOG_BLOWUP
+    with pytest.raises(ValueError):
+        SV.deferred_child_vk(core_vk)
+    with pytest.raises(ValueError):
+        SV.deferred_child_vk(B.StarkVk(cvk.commit, 4, cvk.gcs, cvk.chips, cvk.ordering))
 
 
 def test_compress_route_rejects_a_tampered_shard():
