@@ -1056,11 +1056,26 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
     finally:
         shutil.rmtree(d, ignore_errors=True)
     leaves, info = mips_leaves(dev, args.queries, run, dict(info, leaf_generation_s=round(gen_s, 1)))
-    # warm-up (untimed): one node's witness and proof (JIT modules, allocator pools); its key is dropped
-    wit = CT.node_witness(leaves[:2], True, True, True, False, is_first=True)
-    warm = CT.GpuProvers(dev)
-    warm.get(wit[0], CT.TreeStats()).prove_shard(CT.materialize(wit[1]), wit[2])
-    del warm
+    # warm-up (untimed): node witnesses and proofs of the first leaves (JIT modules, allocator pools; the keys are
+    # dropped), and in every witness worker the program templates of the tree's first layers, built from real
+    # chaining children (CT.prebuild_template) -- the reference holds its recursion programs ready per shape
+    # (prover/src/lib.rs:366-410: join programs precomputed, core programs in an LRU by shape)
+    warm, wst = CT.GpuProvers(dev), CT.TreeStats()
+
+    def wprove(children, **fl):
+        w = CT.node_witness(children, True, True, True, False, **fl)
+        pr = warm.get(w[0], wst)
+        return CT.compress_child_vk(pr.vk_commit, w[3]), pr.prove_shard(CT.materialize(w[1]), w[2])
+    cur = list(leaves[:8])
+    for depth in range(3):
+        if len(cur) < 2:
+            break
+        if hasattr(pool, "run_all"):
+            pool.run_all(CT.prebuild_template, CT.by_ref(cur[:2]), is_first=depth == 0)
+        if depth == 2 or len(cur) < 4:
+            break
+        cur = [wprove(cur[i:i + 2], is_first=depth == 0 and i == 0) for i in range(0, len(cur) - 1, 2)]
+    del warm, cur
     (rvk, rproof), r = compress_tree_run(pool, dev, leaves, inflight, distributed=world > 1)
     n = r["proofs"]
     nodes = len(leaves) - 1  # a binary tree over the leaves (odd nodes carried up) has leaves - 1 nodes

@@ -551,3 +551,16 @@ def test_deferred_proof_chains_into_a_complete_root(deferred_setup):
     dn = prove(CT.node_witness([root_a], fix=False, deferred=bad))
     with pytest.raises(ValueError, match="deferred digest"):
         CT.node_witness([core, dn], fix=False, is_complete=True)
+
+
+def test_prebuilt_template_serves_later_nodes(fib_leaves):
+    """prebuild_template keeps a node structure's program template in the process (as the reference holds its
+    recursion programs per shape); a later node of that structure is a template hit whose program executes to
+    the full build's public values."""
+    RV._TEMPLATES.clear()
+    n = CT.prebuild_template(fib_leaves[:2])
+    assert n == 1
+    flat = RV.node_flat(fib_leaves[2:])
+    assert len(RV._TEMPLATES) == 1
+    full = R.flatten(RV.compress_node_program(fib_leaves[2:]))
+    assert np.array_equal(R.execute(flat).public_values, R.execute(full).public_values)

@@ -384,6 +384,18 @@ def warm_worker() -> int:
     return os.getpid()
 
 
+def prebuild_template(children: Sequence[tuple], is_first: bool = False) -> int:
+    """Build (and keep, in this process) the node program template of `children`'s structure
+    (recursion_verifier.node_flat) without executing it: later nodes of the same structure -- any children with the
+    same vks up to their commitment and the same proof shapes -- only replace hint values.  The reference keeps
+    its programs ready the same way: the compress (join) programs precomputed per shape when the prover is built
+    (prover/src/lib.rs:398-410 `join_programs_map`), the core programs in an LRU cache by shape (:366-396).  The
+    children are real proofs that chain (every check applies); returns the number of templates held."""
+    from . import recursion_verifier as RV
+    RV.node_flat([(resolve_vk(vk), p) for vk, p in children], is_first=is_first)
+    return len(RV._TEMPLATES)
+
+
 def node_witness_shm(*args, **kwargs):
     """node_witness through shared memory (shm_pack): the pool's job for a consumer whose Reducer unpacks
     (register_prep)."""
@@ -578,9 +590,12 @@ class AffinityPool:
 
     def warm(self):
         """warm_worker on every worker (each its own executor), waited for."""
-        for f in [e.submit(warm_worker) for e in self._ex]:
-            f.result()
+        self.run_all(warm_worker)
         return self
+
+    def run_all(self, fn, *args, **kwargs) -> list:
+        """fn(*args, **kwargs) on every worker, waited for: their results in worker order."""
+        return [f.result() for f in [e.submit(fn, *args, **kwargs) for e in self._ex]]
 
     def _release(self, k: int):
         with self._lock:

@@ -65,10 +65,12 @@ __global__ void k_from_col_major(const uint32_t *__restrict__ in, uint64_t h, ui
 // Narrow matrices (w <= 128): a block takes 64 whole rows, so its read is one contiguous span of
 // 64 w words (the 64x64-tile kernel reads 4 w-byte rows in 256-byte pieces and, for w = 67, spends
 // a second tile column on 3 words per row); each column then leaves as one 256-byte segment.
+// The tile is sized to the matrix (w x 65 words of dynamic LDS, 17.4 KB for w = 67): a fixed 128-column tile
+// (33 KB) held a CU to four blocks' loads in flight.
 static constexpr int TW_ROWS = 64, TW_MAXW = 128;
 __global__ __launch_bounds__(NT) void k_to_col_major_rows(const uint32_t *__restrict__ in, uint64_t h, uint32_t w,
                                                           int mont_in, uint32_t *__restrict__ out) {
-    __shared__ uint32_t tile[TW_MAXW * (TW_ROWS + 1)];  // [c][r], pitch 65: conflict-free both ways
+    extern __shared__ uint32_t tile[];  // [c][r], pitch 65: conflict-free both ways
     const uint64_t nblk = (h + TW_ROWS - 1) / TW_ROWS;
     for (uint64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {  // grid-stride: a capped grid for host sources
     if (blk != blockIdx.x) __syncthreads();  // the previous block's tile has been written out
@@ -110,8 +112,8 @@ void launch_to_col_major(const uint32_t *d_in, uint64_t h, uint64_t w, bool mont
     if (w <= TW_MAXW) {
         uint64_t g = (h + TW_ROWS - 1) / TW_ROWS;
         if (max_grid && g > max_grid) g = max_grid;
-        hipLaunchKernelGGL(k_to_col_major_rows, dim3((unsigned)g), dim3(NT), 0, s, d_in, h,
-                           (uint32_t)w, (int)mont_in, d_out);
+        hipLaunchKernelGGL(k_to_col_major_rows, dim3((unsigned)g), dim3(NT), (unsigned)(w * (TW_ROWS + 1) * 4), s,
+                           d_in, h, (uint32_t)w, (int)mont_in, d_out);
         HIP_CHECK(hipGetLastError());
         return;
     }
