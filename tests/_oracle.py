@@ -153,7 +153,7 @@ class OracleProver:
     """CPU restatement of CpuProver (setup + commit/open) and the shard verifier."""
 
     def __init__(self, machine, prep_traces, num_queries=84, pow_bits=16, montgomery=False,
-                 pc_start=0x00400000, gcs=None, log_blowup=1):
+                 pc_start=None, gcs=None, log_blowup=1):
         from zkmips_amd.machine import P  # noqa
         self.machine = machine
         self.blob = machine.blob()
@@ -172,6 +172,8 @@ class OracleProver:
             gcs = np.asarray([637514027, 1595065213, 1998064738, 72333738, 1211544370, 822986770, 1518535784,
                               1604177449, 90440090, 259343427, 140470264, 1162099742, 941559812, 1064053343], np.uint32)
         self.commit = np.zeros(8, np.uint32)
+        if pc_start is None:  # the machine's programs' entry (MachineDesc.pc_start)
+            pc_start = getattr(machine, "pc_start", 0x00400000)
         self.pk = lib().orc_api_setup(self.mh, num_queries, pow_bits, int(montgomery), ptrs, hs, pc_start, _u32(gcs),
                                       self.commit, log_blowup)
         assert self.pk, "setup failed"

@@ -78,8 +78,8 @@ def test_not_ready_without_device(server):
 def test_shard_payload_roundtrip():
     m, prep, tr, pv = W.fib_shard(1 << 6, 3)
     data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=16)
-    blob, p2, t2, pv2, nq, lb = SV.unpack_shard(data)
-    assert np.array_equal(blob, m.blob()) and np.array_equal(pv2, pv) and nq == 16 and lb == 1
+    blob, p2, t2, pv2, nq, lb, pc = SV.unpack_shard(data)
+    assert np.array_equal(blob, m.blob()) and np.array_equal(pv2, pv) and nq == 16 and lb == 1 and pc == m.pc_start
     assert set(t2) == set(tr) and all(np.array_equal(t2[k], tr[k]) for k in tr)
     assert set(p2) == {k for k, v in prep.items() if v is not None}
 
@@ -109,7 +109,8 @@ def test_prove_compress_shard_through_service(server):
     from zkmips_amd import recursion as R
     port = server()
     m, prep, tr, pv = R.shard(R.program_merkle_openings(6, 21, 8)[0])
-    data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP)
+    data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP,
+                         pc_start=m.pc_start)
     st, ct, body = post(port, "ProveShard", SV.encode_bytes_field(1, data))
     assert st == 200
     rc, ref = O.OracleProver(m, prep, num_queries=R.COMPRESS_NUM_QUERIES, log_blowup=R.COMPRESS_LOG_BLOWUP).prove(tr, pv)
@@ -191,7 +192,7 @@ def test_two_compress_programs_through_one_server(server):
         m, prep, tr, pv = R.shard(R.program_merkle_openings(6, 21, 8, seed=seed)[0])
         blobs.append(m.blob().tobytes())
         data = SV.pack_shard(m.blob(), prep, tr, pv, num_queries=R.COMPRESS_NUM_QUERIES,
-                             log_blowup=R.COMPRESS_LOG_BLOWUP)
+                             log_blowup=R.COMPRESS_LOG_BLOWUP, pc_start=m.pc_start)
         st, _, body = post(port, "ProveShard", SV.encode_bytes_field(1, data))
         assert st == 200, body
         direct = HipProver(Device(0), m, prep, num_queries=R.COMPRESS_NUM_QUERIES,

@@ -446,7 +446,7 @@ def compress_child_vk(commit, shape: Dict[str, int], num_queries: int = None):
         if chips is None:
             m = R.compress_machine()
             chips = {"shapes": {c.name: RV.ChipShape.of(c) for c in m.chips}, "num_pv": m.num_pv,
-                     "prep": [c.name for c in m.chips if c.prep_width]}
+                     "prep": [c.name for c in m.chips if c.prep_width], "pc_start": m.pc_start}
             _CVK_CHIPS[0] = chips
         # one object per (program, shape): parents pass it by reference (vk_ref) without re-pickling it
         key = (tuple(int(x) for x in commit), tuple(sorted(shape.items())), num_queries)
@@ -457,8 +457,8 @@ def compress_child_vk(commit, shape: Dict[str, int], num_queries: int = None):
     order = sorted(heights, key=lambda k: (-heights[k], k))
     from .septic import CURVE_CUMULATIVE_SUM_START
     vk = RV.ChildVk(chips["shapes"], chips["num_pv"], np.asarray(commit, np.int64), order, heights,
-                    gcs=np.asarray(CURVE_CUMULATIVE_SUM_START, np.int64), log_blowup=R.COMPRESS_LOG_BLOWUP,
-                    num_queries=num_queries or R.COMPRESS_NUM_QUERIES)
+                    pc_start=chips["pc_start"], gcs=np.asarray(CURVE_CUMULATIVE_SUM_START, np.int64),
+                    log_blowup=R.COMPRESS_LOG_BLOWUP, num_queries=num_queries or R.COMPRESS_NUM_QUERIES)
     with _CVK_LOCK:
         got = _CVK_CHIPS.get(key)
         if got is not None:

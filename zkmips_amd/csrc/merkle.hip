@@ -40,8 +40,10 @@ __global__ __launch_bounds__(NT) void k_hash_leaves(const uint64_t *__restrict__
     o[1] = make_uint4(s[4], s[5], s[6], s[7]);
 }
 
+// One node per thread: compress(left, right).  (Levels with injected matrices: k_compress_inject; keeping a
+// sponge path in this kernel held it to 82 VGPRs, five waves per SIMD, instead of eight.)
 __global__ __launch_bounds__(NT) void k_compress_level(const uint32_t *__restrict__ prev, uint32_t *__restrict__ out,
-                                                       uint64_t h, const uint64_t *__restrict__ inj, int ninj) {
+                                                       uint64_t h) {
     uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (i >= h) return;
     uint32_t s[16];
@@ -50,13 +52,6 @@ __global__ __launch_bounds__(NT) void k_compress_level(const uint32_t *__restric
     s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
     s[8] = c.x; s[9] = c.y; s[10] = c.z; s[11] = c.w; s[12] = d.x; s[13] = d.y; s[14] = d.z; s[15] = d.w;
     p2::permute(s);
-    if (ninj) {
-        uint32_t r[8];
-        sponge_row(inj, ninj, i, r);
-#pragma unroll
-        for (int k = 0; k < 8; k++) s[8 + k] = r[k];
-        p2::permute(s);
-    }
     uint4 *o = (uint4 *)(out + i * 8);
     o[0] = make_uint4(s[0], s[1], s[2], s[3]);
     o[1] = make_uint4(s[4], s[5], s[6], s[7]);
@@ -256,8 +251,7 @@ static bool build_levels(DTree &t, uint64_t maxh, const std::vector<std::pair<co
             continue;
         }
         hipLaunchKernelGGL(k_compress_level, dim3((unsigned)((h + NT - 1) / NT)), dim3(NT), 0, s,
-                           (const uint32_t *)t.layers[L - 1], t.layers[L], h,
-                           inj[L].first ? (const uint64_t *)inj[L].first->p : (const uint64_t *)nullptr, ninj);
+                           (const uint32_t *)t.layers[L - 1], t.layers[L], h);
         HIP_CHECK(hipGetLastError());
     }
     return chal_done;

@@ -262,6 +262,10 @@ class ChipDesc:
 class MachineDesc:
     chips: List[ChipDesc]
     num_pv: int
+    # MachineProgram::pc_start of the programs it proves, observed by every shard's transcript and hashed into the
+    # vk: the MIPS program's entry (crates/core/executor/src/program.rs:329), 0 for recursion programs
+    # (crates/recursion/core/src/runtime/program.rs:20-22)
+    pc_start: int = 0x00400000
 
     def blob(self):
         import numpy as np

@@ -124,7 +124,7 @@ class HipProver:
 
     def __init__(self, device: Device, machine: MachineDesc, prep_traces: Dict[str, np.ndarray],
                  num_queries: int = 84, pow_bits: int = 16, proof_montgomery: bool = False,
-                 pc_start: int = 0x00400000, initial_global_cumulative_sum: Optional[np.ndarray] = None,
+                 pc_start: Optional[int] = None, initial_global_cumulative_sum: Optional[np.ndarray] = None,
                  log_blowup: int = 1):
         self.dev = device
         self.machine = machine
@@ -139,6 +139,8 @@ class HipProver:
             else:
                 mats[i] = Matrix(c.name.encode(), None, 0, 0, 0)
         gcs = as_u32(ZERO_DIGEST if initial_global_cumulative_sum is None else initial_global_cumulative_sum)
+        if pc_start is None:  # the machine's programs' entry (MachineDesc.pc_start)
+            pc_start = getattr(machine, "pc_start", 0x00400000)
         self.pk = C.c_void_p()
         self.vk_commit = np.zeros(8, np.uint32)
         check(lib().zkm_setup(device.h, self.blob.ctypes.data, self.blob.size, C.byref(self.cfg), mats,

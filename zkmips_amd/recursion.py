@@ -1081,14 +1081,14 @@ def compress_machine() -> MachineDesc:
     """RecursionAir::<F, 3>::compress_machine (machine.rs:112-128), observing all 231 public values."""
     return MachineDesc([mem_const_chip(), mem_var_chip(), _alu_chip("BaseAlu", False), _alu_chip("ExtAlu", True),
                         poseidon2_wide_chip(), batch_fri_chip(), select_chip(), exp_reverse_bits_chip(),
-                        public_values_chip()], PROOF_MAX_NUM_PVS)
+                        public_values_chip()], PROOF_MAX_NUM_PVS, pc_start=0)
 
 
 def wide_machine() -> MachineDesc:
     """RecursionAir::<F, 3>::machine_wide_with_all_chips (machine.rs:68-87): the compress chips plus FriFold."""
     return MachineDesc([mem_const_chip(), mem_var_chip(), _alu_chip("BaseAlu", False), _alu_chip("ExtAlu", True),
                         poseidon2_wide_chip(), fri_fold_chip(), batch_fri_chip(), select_chip(), exp_reverse_bits_chip(),
-                        public_values_chip()], PROOF_MAX_NUM_PVS)
+                        public_values_chip()], PROOF_MAX_NUM_PVS, pc_start=0)
 
 
 # ------------------------------------------------------------------ traces

@@ -292,13 +292,14 @@ class ChildVk:
 
     @staticmethod
     def of(machine, prep_traces: Dict[str, np.ndarray], commit, log_blowup=1, num_queries=84, pow_bits=16,
-           pc_start=0x00400000, gcs=None):
+           pc_start=None, gcs=None):
         from . import septic as S
         prep = {k: v for k, v in prep_traces.items() if v is not None}
         order = sorted(prep, key=lambda k: (-prep[k].shape[0], k))
         shapes = {c.name: ChipShape.of(c) for c in machine.chips}
         return ChildVk(shapes, machine.num_pv, np.asarray(commit, np.int64), order,
-                       {k: prep[k].shape[0] for k in prep}, pc_start,
+                       {k: prep[k].shape[0] for k in prep},
+                       getattr(machine, "pc_start", 0x00400000) if pc_start is None else pc_start,
                        np.asarray(S.CURVE_CUMULATIVE_SUM_START if gcs is None else gcs, np.int64), log_blowup,
                        num_queries, pow_bits)
 

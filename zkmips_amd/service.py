@@ -110,9 +110,12 @@ def encode_bool_field(field: int, v: bool) -> bytes:
 
 # ---------------------------------------------------------------- shard payloads (ProveShard)
 def pack_shard(machine_blob, prep: dict, traces: dict, public_values, num_queries: int = 84,
-               log_blowup: int = 1) -> bytes:
+               log_blowup: int = 1, pc_start: int = 0x00400000) -> bytes:
+    """A ProveShard payload (npz): the machine blob, FRI parameters, the programs' pc_start (MachineDesc.pc_start:
+    0 for recursion programs), preprocessed and main traces, public values."""
     arrs = {"machine_blob": np.asarray(machine_blob, np.uint32), "public_values": np.asarray(public_values, np.uint32),
-            "num_queries": np.asarray([num_queries], np.uint32), "log_blowup": np.asarray([log_blowup], np.uint32)}
+            "num_queries": np.asarray([num_queries], np.uint32), "log_blowup": np.asarray([log_blowup], np.uint32),
+            "pc_start": np.asarray([pc_start], np.uint32)}
     for k, v in prep.items():
         if v is not None:
             arrs[f"prep/{k}"] = np.asarray(v, np.uint32)
@@ -130,9 +133,10 @@ def unpack_shard(data: bytes):
     pv = files.pop("public_values")
     nq = int(files.pop("num_queries")[0])
     lb = int(files.pop("log_blowup", np.asarray([1]))[0])
+    pc = int(files.pop("pc_start", np.asarray([0x00400000]))[0])
     prep = {k[5:]: v for k, v in files.items() if k.startswith("prep/")}
     traces = {k[6:]: v for k, v in files.items() if k.startswith("trace/")}
-    return blob, prep, traces, pv, nq, lb
+    return blob, prep, traces, pv, nq, lb, pc
 
 
 class TwirpError(Exception):
@@ -144,14 +148,15 @@ class TwirpError(Exception):
         self.code, self.msg = code, msg
 
 
-def prover_key(blob, prep: dict, num_queries: int, log_blowup: int) -> bytes:
+def prover_key(blob, prep: dict, num_queries: int, log_blowup: int, pc_start: int = 0x00400000) -> bytes:
     """Identity of a proving key: the machine blob, the FRI parameters AND the preprocessed traces.
     A recursion (compress) program lives in its chips' preprocessed columns, so two programs of one
     machine need two keys (the reference sets each compress program up anew, prover/src/lib.rs:807)."""
     import hashlib
     h = hashlib.sha256()
     h.update(np.asarray(blob, np.uint32).tobytes())
-    h.update(np.asarray([num_queries, log_blowup], np.uint64).tobytes())
+    h.update(np.asarray([num_queries, log_blowup] + ([pc_start] if pc_start != 0x00400000 else []),
+                        np.uint64).tobytes())
     for name in sorted(k for k, v in prep.items() if v is not None):
         a = np.ascontiguousarray(np.asarray(prep[name], np.uint32))
         h.update(name.encode() + b"\0" + np.asarray(a.shape, np.uint64).tobytes())
@@ -203,7 +208,8 @@ def deferred_child_vk(vk):
         shape[name] = int(log_n)
     if sorted(shape) != sorted(k for k, c in chips.items() if c.prep_width):
         raise ValueError("deferred proof: not a compress program's verifying key")
-    if int(vk.pc_start) != 0 or [int(x) for x in vk.gcs] != [int(x) for x in CURVE_CUMULATIVE_SUM_START]:
+    if int(vk.pc_start) != R.compress_machine().pc_start or \
+            [int(x) for x in vk.gcs] != [int(x) for x in CURVE_CUMULATIVE_SUM_START]:
         raise ValueError("deferred proof: a compress vk has pc_start 0 and the zero initial global sum")
     return CT.compress_child_vk(vk.commit, shape)
 
@@ -268,15 +274,15 @@ class ProverService:
                     self._dev = Device(self.device_index)
             return self._dev
 
-    def _build(self, dev, blob, prep, nq, lb):
+    def _build(self, dev, blob, prep, nq, lb, pc_start=0x00400000):
         if self._prover_factory is not None:
             return self._prover_factory(dev, blob, prep, nq, lb)
         from .prover import HipProver
-        return HipProver.from_blob(dev, blob, prep, num_queries=nq, log_blowup=lb)
+        return HipProver.from_blob(dev, blob, prep, num_queries=nq, log_blowup=lb, pc_start=pc_start)
 
-    def get_prover(self, blob, prep: dict, nq: int, lb: int):
-        """The cached prover of (blob, prep, nq, lb), set up on first use."""
-        key = prover_key(blob, prep, nq, lb)
+    def get_prover(self, blob, prep: dict, nq: int, lb: int, pc_start: int = 0x00400000):
+        """The cached prover of (blob, prep, nq, lb, pc_start), set up on first use."""
+        key = prover_key(blob, prep, nq, lb, pc_start)
         dev = self._device()
         with self._lock:
             p = self._provers.get(key)
@@ -293,7 +299,7 @@ class ProverService:
                 raise pend.error
             return pend.prover
         try:
-            pend.prover = self._build(dev, blob, prep, nq, lb)
+            pend.prover = self._build(dev, blob, prep, nq, lb, pc_start)
         except BaseException as e:
             pend.error = e
             raise
@@ -317,10 +323,10 @@ class ProverService:
 
     def prove_shard(self, data: bytes) -> bytes:
         try:
-            blob, prep, traces, pv, nq, lb = unpack_shard(data)
+            blob, prep, traces, pv, nq, lb, pc = unpack_shard(data)
         except Exception as e:
             raise TwirpError("invalid_argument", f"ProveShard payload: {e}")
-        return self.get_prover(blob, prep, nq, lb).prove_shard(traces, pv)
+        return self.get_prover(blob, prep, nq, lb, pc).prove_shard(traces, pv)
 
     def compress(self, data: bytes) -> bytes:
         """CompressRequestPayload -> ZKMReduceProof (prover/src/lib.rs:614-954 on the GPU).  The shards must be
