@@ -57,7 +57,7 @@ def test_coset_lde_large_vs_oracle(dev, logn, w):
     assert np.array_equal(dev.coset_lde(m, 3), O.lde(m, 1, 3))
 
 
-@pytest.mark.parametrize("logn", [3, 12, 13, 14, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("logn", [3, 12, 13, 14, 17, 18, 19, 20, 21, 23])
 def test_coset_lde_bitrev_input(dev, logn):
     """The quotient-chunk pipeline: evaluations handed over in bit-reversed row order."""
     n = 1 << logn

@@ -1260,7 +1260,7 @@ __device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint
 template <bool DIT, int MODE>
 __global__ __launch_bounds__(s10::NTH, 4) void k_ntt_s10(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                          int logS, const uint32_t *__restrict__ tw, uint32_t tw_words,
-                                                         uint32_t nv) {
+                                                         uint32_t nv, Twist tws, uint64_t dst_half) {
     using namespace s10;
     using s9::bld;
     using s9::mkrs;
@@ -1310,6 +1310,14 @@ __global__ __launch_bounds__(s10::NTH, 4) void k_ntt_s10(const uint32_t *src, ui
             const auto rdst = mkrs(dst + md.off(col) + base, 1024u * S4);
 #pragma unroll
             for (int k = 0; k < 16; k++) s9::bst_mid(v[k], rdst, vLH, (uint32_t)(64 * k) * S4);
+        } else if (MODE == MODE_TWIST_OUT) {  // the inverse's last pass: coefficient n to both LDE halves, twisted
+            uint32_t *dp = dst + md.off(col);
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint32_t i = base + (u + 64 * (uint32_t)k) * S + ct;
+                dp[i] = mul(v[k], tws.f(0, i));
+                dp[dst_half + i] = mul(v[k], tws.f(1, i));
+            }
         } else {  // BITREV_OUT: natural n = r S + c -> row rev_L(n) = rev_logS(c) * 1024 + rev_10(r)
             __syncthreads();
             to_lds<LH, true>(x, v, u, t);
@@ -1404,18 +1412,21 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     ARG_CHECK(!tile || (logR == 9 && logS + 9 == L && tw_words && mode != MODE_TWIST_OUT),
               "tile-major sides need the one-pass 512-row strided kernel");
     dim3 g((unsigned)(((1ull << L) >> logR) / T), nv);
-    if (logR == 10) {  // 1024-row x 16-column register tiles (k_ntt_s10), natural-input LDE of 2^23
-        ARG_CHECK(tw_words && mode != MODE_TWIST_OUT && !tile, "the 10-stage pass: plain or bit-reversed output");
+    if (logR == 10) {  // 1024-row x 16-column register tiles (k_ntt_s10): the LDEs of 2^23
+        ARG_CHECK(tw_words && !tile, "the 10-stage pass: row-major sides");
         const dim3 g1(g.x * nv);
         if (!DIT)
             hipLaunchKernelGGL((k_ntt_s10<false, MODE_PLAIN>), g1, dim3(s10::NTH), 0, s, src, dst, ms, md, logS, tw,
-                               tw_words, nv);
+                               tw_words, nv, tws, dst_half);
         else if (mode == MODE_PLAIN)
             hipLaunchKernelGGL((k_ntt_s10<true, MODE_PLAIN>), g1, dim3(s10::NTH), 0, s, src, dst, ms, md, logS, tw,
-                               tw_words, nv);
+                               tw_words, nv, tws, dst_half);
+        else if (mode == MODE_TWIST_OUT)
+            hipLaunchKernelGGL((k_ntt_s10<true, MODE_TWIST_OUT>), g1, dim3(s10::NTH), 0, s, src, dst, ms, md, logS, tw,
+                               tw_words, nv, tws, dst_half);
         else
             hipLaunchKernelGGL((k_ntt_s10<true, MODE_BITREV_OUT>), g1, dim3(s10::NTH), 0, s, src, dst, ms, md, logS,
-                               tw, tw_words, nv);
+                               tw, tw_words, nv, tws, dst_half);
         HIP_CHECK(hipGetLastError());
         return;
     }
@@ -1524,7 +1535,7 @@ static void run_fused(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, C
 // strided pass radices for the bits above the contiguous tile (top to bottom, i.e. DIF order): the 13-stage tile and
 // the rest in balanced passes of at most 9 stages (a 9-stage pass first with an 11-stage tile was the faster 2^20
 // plan only while that height's 7-stage pass was LDS-staged: profiles/r05_lde_plan_ab.txt, r05_lde_s8_ab.txt).
-// allow10: 10 remaining stages as one k_ntt_s10 pass (the natural-input LDE of 2^23: three HBM passes, not five)
+// allow10: 10 remaining stages as one k_ntt_s10 pass (the LDEs of 2^23: three HBM passes, not five)
 static std::vector<int> strided_plan(int L, int &logC, bool allow10 = false) {
     logC = L < LOGC ? L : LOGC;
     int rem = L - logC;
@@ -1624,7 +1635,7 @@ void lde_batch_bitrev_in_strided(Ctx &c, const DMat &src, uint32_t shift, uint32
     ARG_CHECK((1ull << L) == N && L >= 1, "LDE height must be a power of two >= 2");
     ARG_CHECK(L + 1 <= c.tw_log, "LDE larger than the twiddle tables");
     int logC;
-    std::vector<int> sp = strided_plan(L, logC);
+    std::vector<int> sp = strided_plan(L, logC, true);
     const Twist tws = get_twist(c, N, L, shift, s);
     const uint32_t nv = (uint32_t)W;
     ColMap m_src{N, 0, 1}, m_dst1{dst_stride, 0, 1}, m_dst2{dst_stride, N, 2};
