@@ -96,7 +96,7 @@ struct Gen {
 // linearly with the unrolled lookups (ShaCompress, 116 lookups: minutes; EdAddAssign has 881), while
 // the table walk is wave-uniform (scalar loads of the descriptors, one column read per term).
 constexpr int kJitLookupUnroll = 64;
-constexpr int kPermLdsBatches = 10;  // LogUp batches staged in LDS (8 words x 256 threads each)
+constexpr int kPermLdsBatches = 10;  // LogUp batches staged in LDS (4 words x 256 threads each)
 
 // device helpers of the loop form: a VirtualPairCol at a row from the flattened table (advances off)
 const char *kLoopHelpers = R"(
@@ -514,41 +514,35 @@ std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
     const int batch = 1 << c.log_qd, nb = c.perm_w - 1;
     g.body << "    const ef alpha = ef{{A.alpha[0], A.alpha[1], A.alpha[2], A.alpha[3]}};\n";
     g.body << "    ef total = ef_zero();\n";
-    // One inversion per row with each batch's numerator and the running prefix product parked in LDS
-    // (each thread its own column of a [2 nb x 4][256] word array: no barriers, consecutive threads on
-    // consecutive banks) while the denominators stay in registers: the 256-register cap no longer
-    // spills to scratch (HBM).  Up to kPermLdsBatches batches (80 KB per workgroup, two per CU).  Splitting
-    // the batches into groups with one inversion each (less LDS, more waves) measured slower, 0.97-1.03 vs
-    // 0.79 ms (profiles/r04_logup_open_ab.txt), as did smaller register-only groups (r03_perm_group_sweep.txt).
+    // One inversion per row (Montgomery's trick): s_b = num_b / den_b = (num_b prefix_{b-1}) / prefix_b, so the
+    // forward pass parks r_b = num_b prefix_{b-1} in LDS (each thread its own column of a [4 nb][256] word array:
+    // no barriers, consecutive threads on consecutive banks) and the backward pass takes s_b = r_b iv, iv <- iv den_b
+    // with the denominators in registers: the same EF products as parking num_b and prefix_{b-1} separately, half
+    // the LDS (40 KB per workgroup at 10 batches: four workgroups per CU instead of two, and room beside the other
+    // slots' kernels).  The register-only form needs 170 VGPRs (two waves); splitting the batches into several
+    // inversions measured slower (profiles/r04_logup_open_ab.txt, r03_perm_group_sweep.txt).
     const bool lds = nb >= 2 && nb <= kPermLdsBatches;
     if (lds) {
         for (int b = 0; b < nb; b++) {
             g.body << "    ef num" << b << ", den" << b << ";\n";
             lookup_batch(g, c, b * batch, std::min(nloc, (b + 1) * batch), "alpha", "num" + std::to_string(b),
                          "den" + std::to_string(b));
-            // num_b -> LDS rows 4 b..; the prefix product before b -> rows 4(nb + b)..
-            g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * b << " + e) * 256 + threadIdx.x] = num" << b
-                   << ".c[e];\n";
             if (b == 0) {
-                g.body << "    ef run = den" << b << ";\n";
+                g.body << "    for (int e = 0; e < 4; e++) pl_lds[(0 + e) * 256 + threadIdx.x] = num0.c[e];\n"
+                       << "    ef run = den0;\n";
             } else {
-                g.body << "    for (int e = 0; e < 4; e++) pl_lds[(" << 4 * (nb + b)
-                       << " + e) * 256 + threadIdx.x] = run.c[e];\n"
+                g.body << "    {\n        const ef rb = ef_mul(num" << b << ", run);\n"
+                       << "        for (int e = 0; e < 4; e++) pl_lds[(" << 4 * b
+                       << " + e) * 256 + threadIdx.x] = rb.c[e];\n    }\n"
                        << "    run = ef_mul(run, den" << b << ");\n";
             }
         }
         g.body << "    ef iv = ef_inv(run);\n";
         for (int b = nb - 1; b >= 0; b--) {
-            g.body << "    {\n        ef nm, pr;\n"
-                   << "        for (int e = 0; e < 4; e++) nm.c[e] = pl_lds[(" << 4 * b << " + e) * 256 + threadIdx.x];\n";
-            if (b > 0) {
-                g.body << "        for (int e = 0; e < 4; e++) pr.c[e] = pl_lds[(" << 4 * (nb + b)
-                       << " + e) * 256 + threadIdx.x];\n"
-                       << "        const ef sb = ef_mul(nm, ef_mul(iv, pr));\n"
-                       << "        iv = ef_mul(iv, den" << b << ");\n";
-            } else {
-                g.body << "        const ef sb = ef_mul(nm, iv);\n";
-            }
+            g.body << "    {\n        ef rr;\n"
+                   << "        for (int e = 0; e < 4; e++) rr.c[e] = pl_lds[(" << 4 * b << " + e) * 256 + threadIdx.x];\n"
+                   << "        const ef sb = ef_mul(rr, iv);\n";
+            if (b > 0) g.body << "        iv = ef_mul(iv, den" << b << ");\n";
             for (int e = 0; e < 4; e++)
                 g.body << "        A.out[(uint64_t)" << 4 * b + e << " * A.ld + rl] = sb.c[" << e << "];\n";
             g.body << "        total = ef_add(total, sb);\n    }\n";
@@ -576,7 +570,7 @@ std::string gen_perm_source(const ChipDesc &c, const std::string &fname) {
     }
     std::ostringstream o;
     o << "extern \"C\" __global__ void " << perm_bounds() << " " << fname << "(const ZkmPermJitArgs A) {\n"
-      << (lds ? "    __shared__ uint32_t pl_lds[" + std::to_string(8 * nb) + " * 256];\n" : std::string())
+      << (lds ? "    __shared__ uint32_t pl_lds[" + std::to_string(4 * nb) + " * 256];\n" : std::string())
       << "    const uint64_t rl = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n"
       << "    if (rl >= A.ld) return;\n"
       << g.head.str() << g.pipelined(48)  // 48 -> 0.99 ms, 8 -> 1.37
