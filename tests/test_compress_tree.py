@@ -564,3 +564,29 @@ def test_prebuilt_template_serves_later_nodes(fib_leaves):
     assert len(RV._TEMPLATES) == 1
     full = R.flatten(RV.compress_node_program(fib_leaves[2:]))
     assert np.array_equal(R.execute(flat).public_values, R.execute(full).public_values)
+
+
+def test_two_deferred_proofs_chain_in_order(deferred_setup, mips_execution):
+    """Two deferred proofs: the second deferred node's chain starts where the first ended (hash_deferred_proofs
+    over both), [execution root, deferred 1, deferred 2] reduce to a complete root whose end digest is the
+    guest's committed digest of both."""
+    from zkmips_amd import mips_core as MC
+    from zkmips_amd import node_pv as NP
+    _, root_a, d1, prove = deferred_setup
+    pv_a = RV.parse_shard_proof(root_a[1]).pv
+    d2 = NP.hash_deferred_proofs(np.zeros(8, np.int64), [pv_a, pv_a])
+    assert [int(x) for x in NP.hash_deferred_proofs(d1, [pv_a])] == [int(x) for x in d2]
+    run = MC.program_shards(MC.deferred_commit_program(d2), seed=9, shard_size=1 << 10)
+    m, prep = run[0][0], run[0][1]
+    pr = O.OracleProver(m, prep, num_queries=NQ)
+    vk_b = RV.ChildVk.of(m, prep, pr.commit, num_queries=NQ)
+    leaves = []
+    for _, _, tr, pv in run:
+        rc, p = pr.prove(tr, pv)
+        assert rc == 0
+        leaves.append((vk_b, p))
+    submit = lambda ch, fl: _done_future(CT.node_witness(ch, fix=False, **fl))
+    root = CT.reduce_with_deferred(leaves, [root_a, root_a], submit, prove, inflight=1)
+    pv = RV.parse_shard_proof(root[1]).pv
+    assert int(pv[NP.R_IS_COMPLETE]) == 1
+    assert [int(x) for x in pv[NP.R_END_RECON:NP.R_END_RECON + 8]] == [int(x) for x in d2]
