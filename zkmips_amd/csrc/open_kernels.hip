@@ -536,10 +536,7 @@ template <int CB>
 __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, uint32_t ncols, uint64_t n,
                                                       OpenWeights pw, int with_next, int nseg, uint32_t slab,
                                                       uint32_t *partial, uint32_t bx, uint32_t by) {
-    // two reduction buffers, one per register set (block parity): a block's partial sums go to its buffer and
-    // one barrier later are summed, and the buffer is next written two blocks on, after the other block's
-    // barrier -- one barrier per column block instead of two
-    __shared__ uint32_t red[2][CB * 8][OPEN_RED_LD];
+    __shared__ uint32_t red[CB * 8][OPEN_RED_LD];
     constexpr int TPW = NT / (CB * 8);  // reduction threads per output word
     const uint64_t j0 = (uint64_t)bx * OPEN_SEG;
     const uint32_t t = threadIdx.x, lane = t & 63;
@@ -613,7 +610,7 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
             d.xb[k] = *(g1)(y + 4 * ((j0 + rb + 4) & (n - 1)));
         }
     };
-    auto process = [&](uint32_t cb0, const Blk &c, int pb) {
+    auto process = [&](uint32_t cb0, const Blk &c) {
         const int nc = (int)(c_end - cb0 < (uint32_t)CB ? c_end - cb0 : CB);
 #pragma unroll
         for (int k = 0; k < CB; k++) {
@@ -634,8 +631,8 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 // a 32-bit representative, not the canonical value: the sum over the block is reduced once
-                red[pb][k * 8 + e][t] = fold_acc(a0[e]);
-                red[pb][k * 8 + 4 + e][t] = with_next ? fold_acc(a1[e]) : 0u;
+                red[k * 8 + e][t] = fold_acc(a0[e]);
+                red[k * 8 + 4 + e][t] = with_next ? fold_acc(a1[e]) : 0u;
             }
         }
         __syncthreads();
@@ -643,22 +640,23 @@ __device__ __forceinline__ void open_dot_pf(const uint64_t *__restrict__ cols, u
             const uint32_t o = t / TPW, q = t % TPW;  // output word o (column o / 8), partial sums q, q + TPW, ...
             uint64_t acc = 0;
 #pragma unroll
-            for (int i = 0; i < NT / TPW; i++) acc += red[pb][o][q + TPW * i];  // < 32 * 2^32
+            for (int i = 0; i < NT / TPW; i++) acc += red[o][q + TPW * i];  // < 32 * 2^32
             uint32_t r = acc_mod(acc);
 #pragma unroll
             for (int sh = 1; sh < TPW; sh <<= 1) r = add(r, __shfl_xor(r, sh, 64));
             if (q == 0 && (int)(o >> 3) < nc) partial[((uint64_t)(cb0 + (o >> 3)) * nseg + bx) * 8 + (o & 7)] = r;
         }
+        __syncthreads();  // red is reused by the next column block
     };
     Blk b0, b1;
     if (c_begin < c_end) load_block(c_begin, b0);
     for (uint32_t cb0 = c_begin; cb0 < c_end; cb0 += 2 * CB) {
         const uint32_t cb1 = cb0 + CB;
         if (cb1 < c_end) load_block(cb1, b1);
-        process(cb0, b0, 0);
+        process(cb0, b0);
         if (cb1 >= c_end) break;
         if (cb1 + CB < c_end) load_block(cb1 + CB, b0);
-        process(cb1, b1, 1);
+        process(cb1, b1);
     }
 }
 // out[col * 8 + e] = sum over the nseg segments of partial[(col * nseg + seg) * 8 + e]: one wave per
