@@ -1664,7 +1664,8 @@ void lde_batch_bitrev_in_strided(Ctx &c, const DMat &src, uint32_t shift, uint32
 // Columns per pass batch of the natural-input LDE: 16 (measured 4.62 ms vs 4.67 ms for all 67 columns of a
 // 2^22 trace at once), 8 at 2^22 rows (with default-policy intermediate stores part of a batch's
 // intermediates stay in the Infinity Cache: 2^22 x 64 3.49 -> 3.43 ms against 16, 3.47 at 4, 3.75 at 2;
-// profiles/r05_lde_mall_ab.txt), and up to a 256 MB work buffer for short traces (compress shapes,
+// profiles/r05_lde_mall_ab.txt), 2 at 2^23 rows (k_ntt_s10's row-major intermediates: 2^23 x 64 7.24 ms against 7.38
+// at 4, 7.78 at 8, 7.83 at 16; profiles/r06_cb23.txt), and up to a 256 MB work buffer for short traces (compress shapes,
 // 2^14..2^18 rows: fewer launches; profiles/r03_lde_cb_ab.txt); ZKM_LDE_CB overrides (0 = all).
 static uint32_t lde_col_batch(uint64_t N, uint32_t nv) {
     static const long env = [] {
@@ -1673,7 +1674,7 @@ static uint32_t lde_col_batch(uint64_t N, uint32_t nv) {
     }();
     uint64_t cb;
     if (env >= 0) cb = env ? (uint64_t)env : nv;
-    else cb = N == (1ull << 22) ? 8 : std::max<uint64_t>(16, (1ull << 25) / N);
+    else cb = N == (1ull << 22) ? 8 : N == (1ull << 23) ? 2 : std::max<uint64_t>(16, (1ull << 25) / N);
     return (uint32_t)std::min<uint64_t>(cb, nv);
 }
 
