@@ -108,3 +108,35 @@ def test_product_poseidon2_host_matches_oracle(tmp_path):
     out = subprocess.run([str(exe), "40000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 mismatches" in out.stdout
+
+
+def test_host_poseidon2_batch_matches_oracle():
+    """libzkm_trace.so's batch permutation (sixteen states per AVX-512 pass, csrc/host/p2_simd.cpp, and the
+    one-state code for short tails) against the oracle's permutation, state by state: random states, all-zero
+    and all-(P-1) states, counts that are not multiples of 16, and in place."""
+    import ctypes
+    import numpy as np
+    from tests import _oracle as O
+    lib = ctypes.CDLL(os.path.join(ROOT, "zkmips_amd", "libzkm_trace.so"))
+    f = lib.zkm_host_poseidon2_permute
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    orc = O.lib()
+    P = 0x7f000001
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, P, size=(16 * 64 + 7, 16), dtype=np.uint32)
+    a[0] = 0
+    a[1] = P - 1
+    a[17] = np.arange(16)
+    out = np.empty_like(a)
+    f(a.ctypes.data, out.ctypes.data, len(a))
+    for i in range(len(a)):
+        st = (ctypes.c_uint32 * 16)(*[int(x) for x in a[i]])
+        orc.orc_p2_permute(st)
+        assert list(st) == [int(x) for x in out[i]], i
+    for n in (50, 3):  # a short tail (one-state code after the batches), and no full batch at all
+        o2 = np.empty((n, 16), np.uint32)
+        f(np.ascontiguousarray(a[:n]).ctypes.data, o2.ctypes.data, n)
+        assert np.array_equal(o2, out[:n]), n
+    b = a.copy()
+    f(b.ctypes.data, b.ctypes.data, len(b))
+    assert np.array_equal(b, out)

@@ -10,12 +10,18 @@
 // batch_fri.hpp / fri_fold.hpp / exp_reverse_bits.hpp event_to_row; Poseidon2 as (input, output) pairs),
 // canonical words, concatenated per kind in program order.  Single-threaded: the callers are
 // witness-generation worker processes, one per core.
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "../p2.cuh"
+
+namespace zkm_host {
+uint64_t p2_simd_permute(const uint32_t *in, size_t in_stride, uint32_t *out, size_t out_stride, uint64_t n);
+}
 
 namespace {
 constexpr uint64_t P = 0x7f000001u;
@@ -36,8 +42,11 @@ enum Slot {
 constexpr int NUM_PVS = 231;
 constexpr uint64_t OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_DIV = 3;
 
-inline uint64_t fadd(uint64_t a, uint64_t b) { return (a + b) % P; }
-inline uint64_t fsub(uint64_t a, uint64_t b) { return (a + P - b) % P; }
+inline uint64_t fadd(uint64_t a, uint64_t b) {  // a, b < P
+    const uint64_t s = a + b;
+    return s >= P ? s - P : s;
+}
+inline uint64_t fsub(uint64_t a, uint64_t b) { return a >= b ? a - b : a + P - b; }  // a, b < P
 inline uint64_t fmul(uint64_t a, uint64_t b) { return a * b % P; }
 inline uint64_t fpow(uint64_t a, uint64_t e) {
     uint64_t r = 1;
@@ -50,12 +59,12 @@ inline uint64_t finv(uint64_t a) { return fpow(a, P - 2); }  // 0 -> 0, as the n
 struct Ef {
     uint64_t c[4];
 };
-inline Ef ef_mul(const Ef &a, const Ef &b) {
+inline Ef ef_mul(const Ef &a, const Ef &b) {  // X^4 = 3; coefficients < P: four products < 4 P^2 < 2^64
     uint64_t t[7] = {0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++) t[i + j] = (t[i + j] + a.c[i] * b.c[j]) % P;
+        for (int j = 0; j < 4; j++) t[i + j] += a.c[i] * b.c[j];
     Ef r;
-    for (int k = 0; k < 4; k++) r.c[k] = (t[k] + (k < 3 ? 3 * t[k + 4] : 0)) % P;
+    for (int k = 0; k < 4; k++) r.c[k] = (t[k] % P + (k < 3 ? 3 * (t[k + 4] % P) : 0)) % P;
     return r;
 }
 inline Ef ef_add(const Ef &a, const Ef &b) {
@@ -82,7 +91,7 @@ inline Ef ef_inv(const Ef &a) {
 
 struct Vm {
     uint64_t n_addrs;
-    std::vector<uint32_t> mem;
+    std::unique_ptr<uint32_t[]> mem;  // not zeroed: a word is read only after its address was written
     std::vector<uint8_t> written;
     char *err;
     uint64_t err_len;
@@ -123,7 +132,8 @@ inline T *mp(void *const *s, int i) { return static_cast<T *>(s[i]); }
 // (inputs const, outputs written; unused kinds may be null).  Returns 0, or 1 with a message in err.
 extern "C" int zkm_host_recursion_execute(uint64_t num_addrs, uint64_t nblocks, const int64_t *table,
                                           void *const *slots, char *err, uint64_t err_len) {
-    Vm vm{num_addrs, std::vector<uint32_t>(4 * num_addrs, 0), std::vector<uint8_t>(num_addrs, 0), err, err_len};
+    Vm vm{num_addrs, std::unique_ptr<uint32_t[]>(new uint32_t[4 * num_addrs]), std::vector<uint8_t>(num_addrs, 0), err,
+          err_len};
     const void *const *in = const_cast<const void *const *>(slots);
     uint64_t n_commit = 0;
     for (uint64_t bi = 0; bi < nblocks; bi++) {
@@ -210,12 +220,11 @@ extern "C" int zkm_host_recursion_execute(uint64_t num_addrs, uint64_t nblocks, 
                 const int64_t *out = cp<int64_t>(in, P2_OUT) + 16 * s;
                 if (vm.check_reads(inp, 16 * n)) return 1;
                 uint32_t *ev = mp<uint32_t>(slots, P2_EV) + 32 * s;
-                for (uint64_t i = 0; i < n; i++) {
+                for (uint64_t i = 0; i < 16 * n; i++) ev[32 * (i / 16) + i % 16] = (uint32_t)vm.rd(inp[i]);
+                // sixteen permutations at a time where the CPU has AVX-512 (p2_simd.cpp), else one by one
+                for (uint64_t i = zkm_host::p2_simd_permute(ev, 32, ev + 16, 32, n); i < n; i++) {
                     uint32_t st[16];
-                    for (int j = 0; j < 16; j++) {
-                        ev[32 * i + j] = (uint32_t)vm.rd(inp[16 * i + j]);
-                        st[j] = kb::to_mont(ev[32 * i + j]);
-                    }
+                    for (int j = 0; j < 16; j++) st[j] = kb::to_mont(ev[32 * i + j]);
                     p2::permute(st);
                     for (int j = 0; j < 16; j++) ev[32 * i + 16 + j] = kb::from_mont(st[j]);
                 }
@@ -231,10 +240,15 @@ extern "C" int zkm_host_recursion_execute(uint64_t num_addrs, uint64_t nblocks, 
                 uint32_t *ev = mp<uint32_t>(slots, SEL_EV) + 5 * s;
                 for (uint64_t i = 0; i < n; i++) {
                     const uint64_t b = vm.rd(bit[i]), x = vm.rd(i1[i]), y = vm.rd(i2[i]);
-                    const uint64_t nb = (P + 1 - b) % P;
                     ev[5 * i] = (uint32_t)b;
-                    ev[5 * i + 1] = (uint32_t)fadd(fmul(b, y), fmul(nb, x));
-                    ev[5 * i + 2] = (uint32_t)fadd(fmul(b, x), fmul(nb, y));
+                    if (b <= 1) {  // a bit: the products pick
+                        ev[5 * i + 1] = (uint32_t)(b ? y : x);
+                        ev[5 * i + 2] = (uint32_t)(b ? x : y);
+                    } else {
+                        const uint64_t nb = (P + 1 - b) % P;
+                        ev[5 * i + 1] = (uint32_t)fadd(fmul(b, y), fmul(nb, x));
+                        ev[5 * i + 2] = (uint32_t)fadd(fmul(b, x), fmul(nb, y));
+                    }
                     ev[5 * i + 3] = (uint32_t)x;
                     ev[5 * i + 4] = (uint32_t)y;
                 }
@@ -356,7 +370,11 @@ extern "C" int zkm_host_recursion_execute(uint64_t num_addrs, uint64_t nblocks, 
                 return vm.fail("unknown instruction kind");
         }
     }
-    if (slots[MEM_IMAGE]) memcpy(slots[MEM_IMAGE], vm.mem.data(), vm.mem.size() * 4);
+    if (slots[MEM_IMAGE]) {  // (the image has zeros at unwritten addresses)
+        uint32_t *img = static_cast<uint32_t *>(slots[MEM_IMAGE]);
+        for (uint64_t a = 0; a < num_addrs; a++)
+            for (int k = 0; k < 4; k++) img[4 * a + k] = vm.written[a] ? vm.mem[4 * a + k] : 0u;
+    }
     (void)n_commit;
     return 0;
 }
