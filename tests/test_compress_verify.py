@@ -116,6 +116,12 @@ def test_node_proof_and_second_layer(leaves):
     cvk = RV.compress_vk(m, prep, commit, num_queries=nq2)
     prog2 = RV.compress_node_program([(cvk, layer1[0][3]), (cvk, layer1[1][3])])
     R.execute(prog2)
+    # the hint-tape path (node_flat on a template hit) over compress children equals their full build
+    RV._TEMPLATES.clear()
+    RV.node_flat([(cvk, layer1[0][3]), (cvk, layer1[1][3])])
+    rev = [(cvk, layer1[1][3]), (cvk, layer1[0][3])]
+    _flat_equal(RV.node_flat(rev), R.flatten(RV.compress_node_program(rev)))
+    assert len(RV._TEMPLATES) == 1
 
 
 @pytest.mark.gpu

@@ -105,6 +105,10 @@ class Ops:
         return V(np.asarray(self.b.hint_base(v), np.int64).reshape(v.shape), v)
 
     def _op(self, op, x: V, y: V, f) -> V:
+        if self.b._tape:
+            xv, yv = np.asarray(x.v, np.int64), np.asarray(y.v, np.int64)
+            v = f(xv, yv) % P
+            return V(self.b.base(op, np.asarray(x.a), np.asarray(y.a)).reshape(v.shape), v)
         xa, ya = np.broadcast_arrays(np.asarray(x.a, np.int64), np.asarray(y.a, np.int64))
         xv, yv = np.broadcast_arrays(np.asarray(x.v, np.int64), np.asarray(y.v, np.int64))
         return V(np.asarray(self.b.base(op, xa, ya), np.int64).reshape(xa.shape), f(xv, yv) % P)

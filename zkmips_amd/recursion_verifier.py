@@ -433,7 +433,8 @@ class Builder:
         return a
 
     def _out(self, x, y) -> np.ndarray:
-        shp = np.broadcast_shapes(np.shape(x), np.shape(y))
+        sx, sy = np.shape(x), np.shape(y)
+        shp = sx if sx == sy or not sy else sy if not sx else np.broadcast_shapes(sx, sy)
         return self.p.alloc(math.prod(shp)).reshape(shp)
 
     def base(self, op, x, y) -> np.ndarray:
@@ -470,6 +471,8 @@ class Builder:
 
     def p2(self, inp: np.ndarray) -> np.ndarray:
         """Poseidon2 permutations of (n, 16) input address rows -> (n, 16) output addresses."""
+        if self._tape:
+            return self.p.alloc(np.size(inp)).reshape(-1, R.WIDTH)
         inp = np.asarray(inp, np.int64).reshape(-1, R.WIDTH)
         out = self.p.alloc(inp.size).reshape(inp.shape)
         self.p.poseidon2(out, inp)
@@ -492,6 +495,9 @@ class Builder:
 
     def select(self, bits, x, y):
         """(bit ? y : x, bit ? x : y) per element: Select (select.rs)."""
+        if self._tape:
+            shp = np.broadcast_shapes(np.shape(bits), np.shape(x), np.shape(y))
+            return self.p.alloc(math.prod(shp)).reshape(shp), self.p.alloc(math.prod(shp)).reshape(shp)
         bits, x, y = np.broadcast_arrays(*(np.asarray(v, np.int64) for v in (bits, x, y)))
         o1, o2 = self.p.alloc(x.size).reshape(x.shape), self.p.alloc(x.size).reshape(x.shape)
         if x.size:
