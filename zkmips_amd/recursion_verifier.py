@@ -1247,6 +1247,9 @@ class _HintTape(R.RecursionProgram):
         self.fresh: List[np.ndarray] = []  # const_fresh blocks
         self.shapes: List[tuple] = []
 
+    def hint(self, addr, vals, mult=None):  # (RecursionProgram.hint's values, no block)
+        self.vals.append((np.asarray(vals, dtype=U).reshape(-1, D) % PU).astype(np.uint32))
+
     def _add(self, kind, **arrays):
         if kind == "hint":
             self.vals.append(np.asarray(arrays["vals"], np.uint32))
