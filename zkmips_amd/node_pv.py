@@ -95,9 +95,16 @@ class Ops:
 
     def __init__(self, b):
         self.b = b
+        self._consts = {}  # array constants by value (the builder caches each word's block the same way)
 
     def const(self, vals) -> V:
         v = np.asarray(vals, np.int64) % P
+        if v.ndim:
+            k = (v.shape, v.tobytes())
+            c = self._consts.get(k)
+            if c is None:
+                c = self._consts[k] = V(np.vectorize(self.b.const, otypes=[np.int64])(v), v)
+            return V(c.a.copy(), c.v.copy())
         return V(np.vectorize(self.b.const, otypes=[np.int64])(v) if v.ndim else np.int64(self.b.const(int(v))), v)
 
     def hint(self, vals) -> V:

@@ -509,6 +509,8 @@ class Builder:
         sample, and canonical (not the bits of x + p): returns (n, 31) bit addresses."""
         v = np.asarray(values, np.int64)
         bits = self.hint_base(((v[:, None] >> np.arange(31)[None, :]) & 1))
+        if self._tape:  # (the checks below add no hints)
+            return bits
         sq = self.base(R.OP_MUL, bits, bits)
         self.assert_eq_base(sq, bits, "bits boolean")
         acc = bits[:, 0]
@@ -992,13 +994,16 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
     rounds.append((quot_c, mats))
     # host mirror of the rounds (z values as ints) for the FRI leaf words
     zeta_h = rp.zeta
+    zn_h: Dict[int, list] = {}  # per height: zeta times the subgroup generator
     rounds_host = []
     for _, ms in rounds:
         hm = []
         for m in ms:
             pts = []
             for z, vals in m["pts"]:
-                zh = zeta_h if z == zeta else ef_mul(zeta_h, ef_base(two_adic_gen(m["log_n"])))
+                if z != zeta and m["log_n"] not in zn_h:
+                    zn_h[m["log_n"]] = ef_mul(zeta_h, ef_base(two_adic_gen(m["log_n"])))
+                zh = zeta_h if z == zeta else zn_h[m["log_n"]]
                 pts.append((zh, np.asarray(vals, np.int64).reshape(-1, 4)))
             hm.append((m["log_n"], m["width"], pts))
         rounds_host.append(hm)
@@ -1007,7 +1012,19 @@ def verify_shard(prog: R.RecursionProgram, vk: ChildVk, proof: bytes, b: Optiona
     for _, ms in rounds:
         for m in ms:
             m["pts"] = [(z, b.hint_ext(np.asarray(vals, np.int64).reshape(-1, 4))) for z, vals in m["pts"]]
-    if ood and not isinstance(prog, _HintTape):  # (no hints in the constraint check)
+    tape = isinstance(prog, _HintTape)
+    if tape:  # the rest adds hints only for the query rows, Merkle paths and the FRI steps: those alone
+        for t, (_, ms) in enumerate(rounds):
+            for k, m in enumerate(ms):
+                if m["width"]:
+                    b.hint_base(_q_rows(p, t, k))
+            b.hint_base(p.q_paths[t] if p.q_paths is not None else np.stack([qq[0][t][1] for qq in p.queries]))
+        for off in range(len(p.fri_commits)):
+            b.hint_ext(p.q_sib[off] if p.q_sib is not None else np.stack([qq[1][off][0] for qq in p.queries]))
+            b.hint_base(fri_pairs[off].astype(np.int64))
+            b.hint_base(p.q_fpath[off] if p.q_fpath is not None else np.stack([qq[1][off][1] for qq in p.queries]))
+        return cvars
+    if ood:  # (no hints in the constraint check)
         none = np.zeros(0, np.int64)
         opened = {c.name: {"prep_l": none, "prep_n": none, "quot": []} for c in chips}
         for name, m in zip(vk.prep_order, rounds[0][1]):
@@ -1146,11 +1163,11 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
         for log_n, width, pts in ms:
             total[log_n + lb] = total.get(log_n + lb, 0) + width * len(pts)
     npow = max(total.values()) if total else 0
-    pw_list = [[1, 0, 0, 0]]
-    fa_i = [int(v) for v in fa]
-    for _ in range(1, npow):  # Python-int EF products: a (4,) numpy product costs 16 array ops
-        pw_list.append(ef_mul(pw_list[-1], fa_i))
-    apow = np.asarray(pw_list, U)
+    apow, step = np.asarray([[1, 0, 0, 0]], U), fa[None, :]
+    while len(apow) < npow:  # doubling: [a^0..a^(k-1)] then a^k times them, one native EF product per step
+        apow = np.concatenate([apow, R.ext_mul(apow, np.broadcast_to(step, apow.shape))])
+        step = R.ext_mul(step, step)
+    apow = apow[:max(npow, 1)]
     ro: Dict[int, np.ndarray] = {}
     lhp: Dict[int, int] = {}
     xs: Dict[int, np.ndarray] = {}        # per LDE height: the queries' points x_q (one per height)
