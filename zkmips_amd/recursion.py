@@ -93,9 +93,12 @@ def _host(name: str):
         from . import septic
         f = getattr(septic.lib(), name)
         u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
-        f.argtypes = {"zkm_host_ef_mul": [u32p, u32p, u32p, C.c_uint64],
+        # (the per-call helpers take raw pointers: callers pass C-contiguous uint32 arrays' .ctypes.data, which
+        # costs a fraction of ndpointer's checks on the replay's thousands of small calls)
+        vp = C.c_void_p
+        f.argtypes = {"zkm_host_ef_mul": [vp, vp, vp, C.c_uint64],
                       "zkm_host_batch_fri": [u32p, u32p, u32p, C.c_uint64, C.c_uint64, u32p],
-                      "zkm_host_poseidon2_permute": [u32p, u32p, C.c_uint64],
+                      "zkm_host_poseidon2_permute": [vp, vp, C.c_uint64],
                       "zkm_host_recursion_execute": [C.c_uint64, C.c_uint64,
                                                      np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS"),
                                                      C.c_void_p, C.c_char_p, C.c_uint64]}[name]
@@ -111,7 +114,7 @@ def ext_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(a, dtype=np.uint32)
         y = np.ascontiguousarray(b, dtype=np.uint32)
         out = np.empty_like(x)
-        _host("zkm_host_ef_mul")(x, y, out, len(x))
+        _host("zkm_host_ef_mul")(x.ctypes.data, y.ctypes.data, out.ctypes.data, len(x))
         return out.astype(U)
     r = np.zeros(np.broadcast(a, b).shape, dtype=U)
     for i in range(D):
@@ -259,7 +262,7 @@ def poseidon2_permute_host(inputs: np.ndarray) -> np.ndarray:
     x = np.ascontiguousarray(inputs, dtype=np.uint32).reshape(-1, WIDTH)
     out = np.empty_like(x)
     if len(x):
-        _host("zkm_host_poseidon2_permute")(x, out, len(x))
+        _host("zkm_host_poseidon2_permute")(x.ctypes.data, out.ctypes.data, len(x))
     return out.astype(U)
 
 
