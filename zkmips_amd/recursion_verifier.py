@@ -422,14 +422,22 @@ class Builder:
         v = np.asarray(vals, np.int64)
         a = self.p.alloc(v.size).reshape(v.shape)
         if v.size:
-            self.p.hint(a.ravel(), _blk(v.ravel()))
+            if self._tape:  # the tape's value blocks directly (_blk, as uint32)
+                blk = np.zeros((v.size, D), np.uint32)
+                blk[:, 0] = np.asarray(v, U).reshape(-1) % PU
+                self.p.vals.append(blk)
+            else:
+                self.p.hint(a.ravel(), _blk(v.ravel()))
         return a
 
     def hint_ext(self, vals) -> np.ndarray:
         v = np.asarray(vals, np.int64).reshape(-1, 4)
         a = self.p.alloc(len(v))
         if len(v):
-            self.p.hint(a, v.astype(U) % PU)
+            if self._tape:
+                self.p.vals.append((v.astype(U) % PU).astype(np.uint32))
+            else:
+                self.p.hint(a, v.astype(U) % PU)
         return a
 
     def _out(self, x, y) -> np.ndarray:
@@ -1171,37 +1179,42 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
     ro: Dict[int, np.ndarray] = {}
     lhp: Dict[int, int] = {}
     xs: Dict[int, np.ndarray] = {}        # per LDE height: the queries' points x_q (one per height)
-    inv_zx: Dict[tuple, np.ndarray] = {}  # per (opening point, height): 1 / (z - x_q)
+    # every (matrix, point) term is (A - B[q]) / (z - x_q), and the divisor depends on (z, height) only: the
+    # matrices sharing one are summed first -- their columns side by side, one dot product and one division
+    groups: Dict[tuple, list] = {}  # (z, height) -> [alpha powers, opened values at z, query rows] per matrix
     for t, ms in enumerate(rounds_host):
         for k, (log_n, width, pts) in enumerate(ms):
             lh = log_n + lb
-            x = xs.get(lh)
-            if x is None:
-                row = (idx >> (log_max - lh)) & ((1 << lh) - 1)
-                g = np.full(nq, two_adic_gen(lh), U)
-                x = _m_u(R._pow_vec(g, _bitrev_arr(row, lh)), U(GENERATOR)) if lh else np.full(nq, GENERATOR, U)
-                xs[lh] = x
             rows = _q_rows(p, t, k) if width else None
             for z, vals in pts:
                 pw = lhp.get(lh, 0)
                 lhp[lh] = pw + width
+                g = groups.setdefault((tuple(int(v) for v in z), lh), [[], [], []])
                 if width:
-                    al = apow[pw:pw + width]
-                    A = R.ext_mul(al, np.asarray(vals, U) % PU).sum(axis=0) % PU
-                    B = _base_dot_ef(rows, al)
-                    acc = (A[None, :] + PU - B) % PU
-                else:
-                    acc = np.zeros((nq, 4), U)
-                key = (tuple(int(v) for v in z), lh)
-                iz = inv_zx.get(key)
-                if iz is None:
-                    zx = np.broadcast_to(np.asarray(z, U) % PU, (nq, 4)).copy()
-                    zx[:, 0] = (zx[:, 0] + PU - x) % PU
-                    iz = inv_zx[key] = R.ext_inv(zx)
-                term = R.ext_mul(acc, iz)
-                ro[lh] = term if lh not in ro else (ro[lh] + term) % PU
+                    g[0].append(apow[pw:pw + width])
+                    g[1].append(np.asarray(vals, U) % PU)
+                    g[2].append(np.asarray(rows, U))
+    for (z, lh), (als, vals, rows) in groups.items():
+        x = xs.get(lh)
+        if x is None:
+            row = (idx >> (log_max - lh)) & ((1 << lh) - 1)
+            g = np.full(nq, two_adic_gen(lh), U)
+            x = _m_u(R._pow_vec(g, _bitrev_arr(row, lh)), U(GENERATOR)) if lh else np.full(nq, GENERATOR, U)
+            xs[lh] = x
+        if als:
+            al = np.concatenate(als)
+            A = R.ext_mul(al, np.concatenate(vals)).sum(axis=0) % PU
+            acc = (A[None, :] + PU - _base_dot_ef(np.concatenate(rows, 1), al)) % PU
+        else:
+            acc = np.zeros((nq, 4), U)
+        zx = np.broadcast_to(np.asarray(z, U) % PU, (nq, 4)).copy()
+        zx[:, 0] = (zx[:, 0] + PU - x) % PU
+        term = R.ext_mul(acc, R.ext_inv(zx))
+        ro[lh] = term if lh not in ro else (ro[lh] + term) % PU
     folded = ro[log_max]
     x = R._pow_vec(np.full(nq, two_adic_gen(log_max), U), _bitrev_arr(idx, log_max))
+    # 1 / (x1 - x0) = +-1 / (2 x), and the next round's x is x^2: one inversion for all rounds
+    half_inv_x = _m_u(R._pow(x, P - 2), U(pow(2, P - 2, P)))
     pairs = []
     for off, _ in enumerate(p.queries[0][1]):
         bit = ((idx >> off) & 1).astype(bool)
@@ -1210,8 +1223,8 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
         e1 = np.where(bit[:, None], folded, sib)
         pairs.append(np.concatenate([e0, e1], 1))
         xn = (PU - x) % PU
-        x0, x1 = np.where(bit, xn, x), np.where(bit, x, xn)
-        inv = R._pow(((x1 + PU - x0) % PU).astype(U), P - 2)
+        x0 = np.where(bit, xn, x)
+        inv = np.where(bit, half_inv_x, (PU - half_inv_x) % PU)  # bit: x1 - x0 = 2x, else -2x
         beta = np.asarray(rp.betas[off], U)
         bx = np.broadcast_to(beta, (nq, 4)).copy()
         bx[:, 0] = (bx[:, 0] + PU - x0) % PU
@@ -1223,6 +1236,7 @@ def host_fri_pairs(vk: ChildVk, p: ShardProofData, rp: Replay, rounds_host) -> L
             b2 = R.ext_mul(beta[None, :], beta[None, :])
             folded = (folded + R.ext_mul(np.broadcast_to(b2, (nq, 4)), ro[lfh])) % PU
         x = _m_u(x, x)
+        half_inv_x = _m_u(_m_u(half_inv_x, half_inv_x), U(2))  # 1 / (2 x^2) = 2 (1 / (2x))^2
     fp = np.asarray(p.final_poly, U)
     bad = np.nonzero((folded != fp[None, :]).any(axis=1))[0]
     if len(bad):
