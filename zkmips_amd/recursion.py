@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import os
 import re
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -1257,8 +1258,29 @@ def prep_key(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None) -> by
         for nm in _PREP_INPUTS[k]:
             v = np.ascontiguousarray(rec.flat.a[k][nm])
             h.update(f"{k}.{nm}{v.shape}{v.dtype}".encode())
-            h.update(v.view(np.uint8).data)
+            h.update(_array_digest(v))
     return h.digest()
+
+
+_DIGESTS: "OrderedDict[int, tuple]" = OrderedDict()  # id -> (array, xxh3-128 of its bytes): large arrays
+
+
+def _array_digest(v: np.ndarray) -> bytes:
+    """xxh3-128 of an array's bytes, memoised for large arrays by identity (a node on a program template shares
+    the template's instruction arrays, recursion_verifier.node_flat, which nothing writes to; the entry holds
+    the array, so its id is not reused while the entry lives)."""
+    import xxhash
+    if v.size < (1 << 15):
+        return xxhash.xxh3_128(v.view(np.uint8).data).digest()
+    e = _DIGESTS.get(id(v))
+    if e is not None and e[0] is v:
+        _DIGESTS.move_to_end(id(v))
+        return e[1]
+    d = xxhash.xxh3_128(v.view(np.uint8).data).digest()
+    _DIGESTS[id(v)] = (v, d)
+    while len(_DIGESTS) > 256:
+        _DIGESTS.popitem(last=False)
+    return d
 
 
 def prep_records(rec: ExecutionRecord, shape: Optional[Dict[str, int]] = None) -> Dict[str, tuple]:
