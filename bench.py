@@ -975,6 +975,15 @@ def _union_s(intervals) -> float:
     return tot + (cur_e - cur_s if cur_e is not None else 0.0)
 
 
+def _by_layer(times: dict) -> dict:
+    """Reducer.times (node -> submit / witness / proved) grouped by the node's layer (complete entries only)."""
+    out = {}
+    for (layer, _), v in times.items():
+        if len(v) == 3:
+            out.setdefault(layer, []).append(v)
+    return out
+
+
 def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = False):
     """One 64-leaf compress tree, dependency-driven (zkmips_amd/compress_tree.py): witness generation in
     the pool overlapping GPU proving.  Returns (root (vk, proof), result dict)."""
@@ -1020,7 +1029,14 @@ def compress_tree_run(pool, dev, leaves, inflight: int, distributed: bool = Fals
         timeline = {"witness_latency_s_mean": round(float(np.mean([v["witness"] - v["submit"] for v in tl])), 3),
                     "prove_latency_s_mean": round(float(np.mean([v["proved"] - v["witness"] for v in tl])), 3),
                     "first_witness_back_s": round(min(v["witness"] for v in tl) - t0, 3),
-                    "last_layer_submit_s": round(max(v["submit"] for v in tl) - t0, 3)}
+                    "last_layer_submit_s": round(max(v["submit"] for v in tl) - t0, 3),
+                    # per layer, seconds from the tree's start: the first node ready to build (children proven),
+                    # the last witness back, the last proof done
+                    "layers": [{"layer": L, "nodes": len(vs),
+                                "first_ready_s": round(min(v["submit"] for v in vs) - t0, 3),
+                                "last_witness_s": round(max(v["witness"] for v in vs) - t0, 3),
+                                "last_proved_s": round(max(v["proved"] for v in vs) - t0, 3)}
+                               for L, vs in sorted(_by_layer(reducer.times).items())]}
     rows = shapes.pop("_rows")
     from zkmips_amd import recursion as R
     names = {",".join(f"{c}:{sh[c]}" for c in sorted(sh)): i for i, sh in enumerate(R.RECURSION_SHAPES)}
