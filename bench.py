@@ -1073,9 +1073,9 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
         shutil.rmtree(d, ignore_errors=True)
     leaves, info = mips_leaves(dev, args.queries, run, dict(info, leaf_generation_s=round(gen_s, 1)))
     # warm-up (untimed): node witnesses and proofs of the first leaves (JIT modules, allocator pools; the keys are
-    # dropped), and in every witness worker the program templates of the tree's first layers, built from real
-    # chaining children (CT.prebuild_template) -- the reference holds its recursion programs ready per shape
-    # (prover/src/lib.rs:366-410: join programs precomputed, core programs in an LRU by shape)
+    # dropped), and in every witness worker the program templates of the tree's first layers and of its right
+    # spine, built from real chaining children (CT.prebuild_template) -- the reference holds its recursion programs
+    # ready per shape (prover/src/lib.rs:366-410: join programs precomputed, core programs in an LRU by shape)
     warm, wst = CT.GpuProvers(dev), CT.TreeStats()
 
     def wprove(children, **fl):
@@ -1091,6 +1091,12 @@ def compress_leg(args, pool, dev, world: int = 1, rank: int = 0, inflight: int =
         if depth == 2 or len(cur) < 4:
             break
         cur = [wprove(cur[i:i + 2], is_first=depth == 0 and i == 0) for i in range(0, len(cur) - 1, 2)]
+    # the execution's last leaf is its memory shard, another proof shape: the programs of the tree's right spine
+    # (its layer-1 node, and the layer-2 node over it) are other structures, known from the shard shapes as well
+    if len(leaves) >= 4 and hasattr(pool, "run_all"):
+        pool.run_all(CT.prebuild_template, CT.by_ref(leaves[-2:]))
+        if len(leaves) >= 8:
+            pool.run_all(CT.prebuild_template, CT.by_ref([wprove(leaves[-4:-2]), wprove(leaves[-2:])]))
     del warm, cur
     (rvk, rproof), r = compress_tree_run(pool, dev, leaves, inflight, distributed=world > 1)
     n = r["proofs"]
