@@ -17,10 +17,11 @@ import csv, json, sys
 d = sys.argv[1]
 rows = [r for r in csv.DictReader(open(d + ".trace.csv")) if "k_hash_leaves" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-last = rows[-9:]  # the serial profiled region: 3 proofs x (main, perm, quotient) commits
+big = max(int(r["Grid_Size_X"]) for r in rows)  # the 2^23-row launches (one thread per LDE row)
+last = [r for r in rows if int(r["Grid_Size_X"]) == big][-9:]  # the serial profiled region: 3 proofs x 3 commits
 ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in last]
 line = json.loads(open(d + ".json").read().strip().splitlines()[-1])
-out = (f"# k_hash_leaves, the last 9 launches of the traced run (the serial profiled region): "
+out = (f"# k_hash_leaves, the last 9 2^23-row launches of the traced run (the serial profiled region): "
        + " ".join(f"{x:.3f}" for x in ms) + f" ms\n# their mean {sum(ms) / len(ms):.4f} ms; the line's roofline.avg_ms "
        f"in the same run {line['roofline']['avg_ms']} ms ({line['roofline']['kernel']}, {line['roofline']['launches']} launches)\n")
 open(d + ".check.txt", "w").write(out)
