@@ -199,7 +199,6 @@ def shm_pack(obj, min_bytes: int = 1 << 20):
     this worker's parent), or obj itself when its arrays are smaller than min_bytes.  A process pool's pipe
     moves a 90 MB witness in ~0.35 s (pickle, pipe, unpickle in the consumer under its GIL); this is one
     copy here and none there (shm_unpack maps the file)."""
-    import mmap
     import os
     bufs = []
     head = pickle.dumps(obj, protocol=5, buffer_callback=bufs.append)
@@ -211,13 +210,15 @@ def shm_pack(obj, min_bytes: int = 1 << 20):
     path = f"{_SHM_DIR}/{_SHM_PREFIX}{os.getppid()}_{os.getpid()}_{_shm_count[0]}"
     fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
     try:
-        os.ftruncate(fd, total)
+        # write(2) into the tmpfs file: ~2x faster than stores through a fresh mapping, which fault page by page
         spans, off = [], 0
-        with mmap.mmap(fd, total) as mm:
-            for r in raws:
-                mm[off:off + r.nbytes] = r
-                spans.append((off, r.nbytes))
-                off += r.nbytes
+        for r in raws:
+            mv = memoryview(r).cast("B")
+            done = 0
+            while done < mv.nbytes:
+                done += os.write(fd, mv[done:])
+            spans.append((off, mv.nbytes))
+            off += mv.nbytes
     except BaseException:
         os.unlink(path)
         raise
