@@ -41,7 +41,7 @@ def test_poseidon2_batch_vs_oracle(dev):
         assert np.array_equal(out[i], O.permute(st[i]))
 
 
-@pytest.mark.parametrize("logn", [1, 2, 4, 7, 11, 12, 13, 14, 16, 18, 19])
+@pytest.mark.parametrize("logn", [1, 2, 4, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19])
 def test_coset_lde_vs_oracle(dev, logn):
     n = 1 << logn
     w = 3 if logn < 16 else 2
@@ -57,7 +57,7 @@ def test_coset_lde_large_vs_oracle(dev, logn, w):
     assert np.array_equal(dev.coset_lde(m, 3), O.lde(m, 1, 3))
 
 
-@pytest.mark.parametrize("logn", [3, 12, 13, 14, 17, 18, 19, 20, 21, 23])
+@pytest.mark.parametrize("logn", [3, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 23])
 def test_coset_lde_bitrev_input(dev, logn):
     """The quotient-chunk pipeline: evaluations handed over in bit-reversed row order."""
     n = 1 << logn

@@ -939,6 +939,57 @@ __global__ __launch_bounds__(2 << LOGR) void k_ntt_sr(const uint32_t *src, uint3
     }
 }
 
+// LOGR = 1..4 strided stages (the short passes of the recursion shards' LDEs: 2^14..2^17 = the 13-stage tile + 1..4)
+// with one column per thread and all R = 2^LOGR rows in its registers: no LDS and no barrier; every load and store
+// instruction of a wave moves 256 consecutive bytes of one row, and the stage twiddles w_{2h}^{m S + c} are as
+// coalesced.  The bit-reversed-output pass keeps k_ntt_strided (its LDS transpose makes those writes coalesced).
+template <int LOGR, bool DIT, int MODE>
+__global__ __launch_bounds__(256) void k_ntt_rg(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, int logS,
+                                                const uint32_t *__restrict__ tw, Twist tws, uint64_t dst_half) {
+    constexpr uint32_t R = 1u << LOGR;
+    const uint32_t S = 1u << logS;
+    const uint32_t groups = S >> 8;  // 256-column groups per block of R S rows
+    const uint32_t outer = blockIdx.x / groups;
+    const uint32_t c = (blockIdx.x % groups) * 256 + threadIdx.x;
+    const uint32_t base = outer * R * S;
+    const uint32_t *sp = src + ms.off(blockIdx.y) + base + c;
+    uint32_t *dp = dst + md.off(blockIdx.y);
+    uint32_t v[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; r++) v[r] = sp[r * S];
+#pragma unroll
+    for (int q = 0; q < LOGR; q++) {
+        const int st = DIT ? q : LOGR - 1 - q;  // DIT: h = S, 2S, ...; DIF: reverse
+        const uint32_t span = 1u << st;
+#pragma unroll
+        for (uint32_t m = 0; m < span; m++) {
+            const uint32_t w = tw[(span + m) * S + c];  // w_{2h}^{m S + c}, h = span S
+#pragma unroll
+            for (uint32_t k = m; k < R; k += 2 * span) {
+                const uint32_t a = v[k], b = v[k + span];
+                if (DIT) {
+                    const uint32_t tt = mul(b, w);
+                    v[k] = add(a, tt);
+                    v[k + span] = sub(a, tt);
+                } else {
+                    v[k] = add(a, b);
+                    v[k + span] = mul(a + (P - b), w);  // (0, 2P) operand: no reduction before the product
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < R; r++) {
+        const uint32_t i = base + r * S + c;
+        if (MODE == MODE_TWIST_OUT) {
+            dp[i] = mul(v[r], tws.f(0, i));
+            dp[dst_half + i] = mul(v[r], tws.f(1, i));
+        } else {
+            dp[i] = v[r];
+        }
+    }
+}
+
 // Same tiles and networks as k_ntt_s9, addressed through buffer descriptors: every global access
 // (data, twiddles, stores) is one per-thread 32-bit voffset fixed for the kernel plus a
 // wave-uniform soffset (k S words, twiddle stage bases) computed on the scalar unit, so the
@@ -1481,6 +1532,23 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
                            tws, dst_half);
         if (logR == 8) { SRL(8) } else if (logR == 7) { SRL(7) } else if (logR == 6) { SRL(6) } else { SRL(5) }
 #undef SRL
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
+    if (logR <= 4 && mode != MODE_BITREV_OUT && logS >= 8) {  // one column per thread (k_ntt_rg)
+        const dim3 gr((unsigned)(((1ull << L) >> logR) >> 8), nv);
+#define RGL(LR)                                                                                                   \
+    if (!DIT)                                                                                                     \
+        hipLaunchKernelGGL((k_ntt_rg<LR, false, MODE_PLAIN>), gr, dim3(256), 0, s, src, dst, ms, md, logS, tw, tws, \
+                           dst_half);                                                                             \
+    else if (mode == MODE_PLAIN)                                                                                  \
+        hipLaunchKernelGGL((k_ntt_rg<LR, true, MODE_PLAIN>), gr, dim3(256), 0, s, src, dst, ms, md, logS, tw, tws,  \
+                           dst_half);                                                                             \
+    else                                                                                                          \
+        hipLaunchKernelGGL((k_ntt_rg<LR, true, MODE_TWIST_OUT>), gr, dim3(256), 0, s, src, dst, ms, md, logS, tw,   \
+                           tws, dst_half);
+        if (logR == 4) { RGL(4) } else if (logR == 3) { RGL(3) } else if (logR == 2) { RGL(2) } else { RGL(1) }
+#undef RGL
         HIP_CHECK(hipGetLastError());
         return;
     }
