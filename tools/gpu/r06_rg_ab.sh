@@ -1,4 +1,4 @@
-# Round 6 A/B of the one-column-per-thread short strided passes (k_ntt_rg; B = in-tree build) against k_ntt_strided
+# Round 6 A/B of the one-column-per-thread short strided passes (k_ntt_rg; B = in-tree build) against the previous build
 # (A = zkmips_amd/libzkm_hip_a.so): LDE parity tests first, then the LDE microbench at 2^15..2^17 and the compress
 # workload (prove-only rate), alternated twice, fresh process each.  gpurun_out/r06_rg_*
 set -e

@@ -942,7 +942,7 @@ __global__ __launch_bounds__(2 << LOGR) void k_ntt_sr(const uint32_t *src, uint3
 // LOGR = 1..4 strided stages (the short passes of the recursion shards' LDEs: 2^14..2^17 = the 13-stage tile + 1..4)
 // with one column per thread and all R = 2^LOGR rows in its registers: no LDS and no barrier; every load and store
 // instruction of a wave moves 256 consecutive bytes of one row, and the stage twiddles w_{2h}^{m S + c} are as
-// coalesced.  The bit-reversed-output pass keeps k_ntt_strided (its LDS transpose makes those writes coalesced).
+// coalesced.  The bit-reversed-output pass writes each thread's R outputs as one contiguous run (16-byte stores).
 template <int LOGR, bool DIT, int MODE>
 __global__ __launch_bounds__(256) void k_ntt_rg(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, int logS,
                                                 const uint32_t *__restrict__ tw, Twist tws, uint64_t dst_half) {
@@ -977,6 +977,19 @@ __global__ __launch_bounds__(256) void k_ntt_rg(const uint32_t *src, uint32_t *d
                 }
             }
         }
+    }
+    if (MODE == MODE_BITREV_OUT) {  // R S == N: natural n = r S + c -> row rev_logS(c) R + rev_LOGR(r), R words per thread
+        uint32_t *o = dp + (uint64_t)rev_bits(c, logS) * R;
+        if constexpr (R >= 4) {
+#pragma unroll
+            for (uint32_t j = 0; j < R; j += 4)
+                reinterpret_cast<uint4 *>(o)[j / 4] = make_uint4(v[rev_bits(j, LOGR)], v[rev_bits(j + 1, LOGR)],
+                                                                 v[rev_bits(j + 2, LOGR)], v[rev_bits(j + 3, LOGR)]);
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < R; j++) o[j] = v[rev_bits(j, LOGR)];
+        }
+        return;
     }
 #pragma unroll
     for (uint32_t r = 0; r < R; r++) {
@@ -1535,7 +1548,7 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
         HIP_CHECK(hipGetLastError());
         return;
     }
-    if (logR <= 4 && mode != MODE_BITREV_OUT && logS >= 8) {  // one column per thread (k_ntt_rg)
+    if (logR <= 4 && logS >= 8) {  // one column per thread (k_ntt_rg)
         const dim3 gr((unsigned)(((1ull << L) >> logR) >> 8), nv);
 #define RGL(LR)                                                                                                   \
     if (!DIT)                                                                                                     \
@@ -1544,8 +1557,11 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
     else if (mode == MODE_PLAIN)                                                                                  \
         hipLaunchKernelGGL((k_ntt_rg<LR, true, MODE_PLAIN>), gr, dim3(256), 0, s, src, dst, ms, md, logS, tw, tws,  \
                            dst_half);                                                                             \
-    else                                                                                                          \
+    else if (mode == MODE_TWIST_OUT)                                                                              \
         hipLaunchKernelGGL((k_ntt_rg<LR, true, MODE_TWIST_OUT>), gr, dim3(256), 0, s, src, dst, ms, md, logS, tw,   \
+                           tws, dst_half);                                                                        \
+    else                                                                                                          \
+        hipLaunchKernelGGL((k_ntt_rg<LR, true, MODE_BITREV_OUT>), gr, dim3(256), 0, s, src, dst, ms, md, logS, tw,  \
                            tws, dst_half);
         if (logR == 4) { RGL(4) } else if (logR == 3) { RGL(3) } else if (logR == 2) { RGL(2) } else { RGL(1) }
 #undef RGL
