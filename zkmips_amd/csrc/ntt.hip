@@ -292,54 +292,10 @@ struct Twist {
     }
 };
 
+// Strided-pass output modes: MODE_BITREV_OUT (last DIT pass, R*S == N): natural n = r*S + c goes to row rev_L(n);
+// MODE_TWIST_OUT (last DIT pass of an inverse transform): natural coefficient n goes to both LDE halves multiplied by
+// the coset twists f_0(n), f_1(n).
 enum PassMode { MODE_PLAIN = 0, MODE_BITREV_OUT = 1, MODE_TWIST_OUT = 2 };
-
-// Strided pass: rows at stride S = 2^logS inside outer blocks of R*S, tiles of T columns.
-//   MODE_BITREV_OUT (last DIT pass, R*S == N): natural n = r*S + c goes to row rev_L(n).
-//   MODE_TWIST_OUT  (last DIT pass of an inverse transform): natural coefficient n goes to both
-//                   LDE halves multiplied by the coset twists f_0(n), f_1(n).
-template <int LOGR, int T, bool DIT, int NTH>
-__global__ __launch_bounds__(NTH) void k_ntt_strided(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
-                                                    int logS, const uint32_t *__restrict__ tw, int mode, Twist tws,
-                                                    uint64_t dst_half) {
-    constexpr int R = 1 << LOGR;
-    constexpr int LD = T;                             // rows unpadded, columns XOR-swizzled
-    constexpr int SWS = LOGR >= 5 ? LOGR - 5 : 0;    // see tile_at
-    __shared__ uint32_t x[R * LD];
-    const uint32_t S = 1u << logS;
-    const uint32_t groups = S / T;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t outer = tile / groups;
-    const uint32_t c0 = (tile % groups) * T;
-    const uint32_t base = outer * (uint32_t)R * S;
-    const uint32_t *sp = src + ms.off(blockIdx.y);
-    uint32_t *dp = dst + md.off(blockIdx.y);
-    for (int i = threadIdx.x; i < R * T; i += NTH) {
-        const int r = i / T, t = i & (T - 1);
-        x[tile_at<LD, SWS>(r, t)] = sp[base + (uint32_t)r * S + c0 + t];
-    }
-    __syncthreads();
-    tile_stages<LOGR, T, LD, DIT, SWS, NTH>(x, tw, S, c0);
-    if (mode == MODE_PLAIN) {
-        for (int i = threadIdx.x; i < R * T; i += NTH) {
-            const int r = i / T, t = i & (T - 1);
-            dp[base + (uint32_t)r * S + c0 + t] = x[tile_at<LD, SWS>(r, t)];
-        }
-    } else if (mode == MODE_TWIST_OUT) {
-        for (int i = threadIdx.x; i < R * T; i += NTH) {
-            const int r = i / T, t = i & (T - 1);
-            const uint32_t n = base + (uint32_t)r * S + c0 + t;
-            const uint32_t v = x[tile_at<LD, SWS>(r, t)];
-            dp[n] = mul(v, tws.f(0, n));
-            dp[dst_half + n] = mul(v, tws.f(1, n));
-        }
-    } else {
-        for (int i = threadIdx.x; i < R * T; i += NTH) {
-            const int t = i / R, q = i & (R - 1);
-            dp[(uint64_t)rev_bits(c0 + t, logS) * R + q] = x[tile_at<LD, SWS>((int)rev_bits((uint32_t)q, LOGR), t)];
-        }
-    }
-}
 
 // Contiguous pass over blocks of R consecutive elements (bit-reversed-input pipeline):
 //   MODE_PLAIN: stages only; MODE_TWIST_OUT: DIT (inverse) then twisted writes to both halves.
@@ -689,7 +645,7 @@ __device__ __forceinline__ void from_lds(const uint32_t *x, uint32_t v[16], uint
 }  // namespace s9
 
 // 9 strided stages (rows at stride S = 2^logS) of a transform, natural order in and out, or (DIT)
-// with the MODE_BITREV_OUT / MODE_TWIST_OUT writes of k_ntt_strided.
+// with the MODE_BITREV_OUT / MODE_TWIST_OUT writes (natural n = r S + c to row rev_L(n); twisted into both halves).
 template <bool DIT, int MODE>
 __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9(const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md,
                                                        int logS, const uint32_t *__restrict__ tw, Twist tws,
@@ -770,7 +726,7 @@ __global__ __launch_bounds__(s9::NTH, 4) void k_ntt_s9(const uint32_t *src, uint
 
 // LOGR = 6..8 strided stages as register tiles of R = 2^LOGR rows x 32 columns, 2R threads x two 8-element
 // networks: the k_ntt_s9 design for the passes of the 2^19 and 2^21 LDEs (13-stage tile + 6 / 8) and of the
-// recursion shards' heights.  The LDS-staged k_ntt_strided these replace ran at about half the bytes per second
+// recursion shards' heights.  The LDS-staged strided kernel these replaced (deleted in round 6 with k_ntt_rg) ran at about half the bytes per second
 // of the 9-stage kernels (2^21 x 67 LDE 2.55 -> 2.01 ms, profiles/r05_lde_s8_ab.txt).  Layouts (u = tid >> 5,
 // network n in {0,1}, g = 2u + n < R/8, element k < 8), three stages per layout except where noted:
 //   LOGR 8: LH row g + 32k (h_r 32..128) | LM row (g>>2)*32 + (g&3) + 4k (4..16) | LL row 8g + k (1, 2)
@@ -1465,7 +1421,8 @@ __global__ __launch_bounds__(t13::NTH, 6) void k_lde_fused13s(const uint32_t *sr
 static constexpr int LOGC = 13;  // contiguous tile: 8192 elements
 static constexpr int LOGS = 9;   // strided radix per pass (512 rows x 32 columns)
 
-static int strided_T(int logR) { return logR == 10 ? 16 : logR >= 5 ? 32 : 64; }  // >= 32: the swizzle spans 32 columns
+// columns per tile: k_ntt_s10 16, k_ntt_s9* / k_ntt_sr 32 (their swizzle spans 32 columns), k_ntt_rg 256 (a column per thread)
+static int strided_T(int logR) { return logR == 10 ? 16 : logR >= 5 ? 32 : 256; }
 
 template <bool DIT>
 static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms, ColMap md, uint32_t nv, int L,
@@ -1548,7 +1505,7 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
         HIP_CHECK(hipGetLastError());
         return;
     }
-    if (logR <= 4 && logS >= 8) {  // one column per thread (k_ntt_rg)
+    if (logR >= 1 && logR <= 4) {  // one column per thread (k_ntt_rg)
         const dim3 gr((unsigned)(((1ull << L) >> logR) >> 8), nv);
 #define RGL(LR)                                                                                                   \
     if (!DIT)                                                                                                     \
@@ -1568,17 +1525,7 @@ static void run_strided(int logR, const uint32_t *src, uint32_t *dst, ColMap ms,
         HIP_CHECK(hipGetLastError());
         return;
     }
-#define SCASE(k, t)                                                                                             \
-    case k:                                                                                                     \
-        hipLaunchKernelGGL((k_ntt_strided<k, t, DIT, NT>), g, dim3(NT), 0, s, src, dst, ms, md, logS, tw, mode, tws, \
-                           dst_half);                                                                           \
-        break;
-    switch (logR) {
-        SCASE(1, 64) SCASE(2, 64) SCASE(3, 64) SCASE(4, 64)
-        default: throw ArgError("bad strided radix");
-    }
-#undef SCASE
-    HIP_CHECK(hipGetLastError());
+throw ArgError("bad strided radix");
 }
 
 template <bool DIT>
